@@ -1,0 +1,102 @@
+// Partial-gradient slab reduction + fused multi-tensor Adam over one flat fp32
+// parameter buffer (K13 of SURVEY §2.6; reference uses torch.optim.Adam with default
+// betas (0.9, 0.999), eps 1e-8 over the policy and value nets, REINFORCE.py:47-50).
+//
+// The step counter lives on the device so that an optimisation loop (e.g. the 80
+// value iterations, REINFORCE.py:110-115) can be captured into one hipGraph: every
+// block reads t from `step`, and the last block to finish (arrival ticket) bumps it.
+#include "common.h"
+
+namespace rrl {
+
+struct AdamArgs {
+  float* param;
+  float* m;
+  float* v;
+  const float* grad;  // [P] flat gradient, or null when reducing slabs
+  const float* slab;  // [nslab][P] partial gradients
+  int nslab;
+  float* grad_out;    // optional: write the reduced gradient here
+  int* step;          // device step counter
+  unsigned* ticket;   // device arrival counter (zeroed by the last block)
+  int P;
+  float lr, beta1, beta2, eps, grad_scale, weight_decay;
+};
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+  const int t = *a.step + 1;
+  const float bc1 = 1.f - __powf(a.beta1, (float)t);
+  const float bc2 = 1.f - __powf(a.beta2, (float)t);
+  const float step_size = a.lr / bc1;
+  const float rbc2 = rsqrtf(bc2);
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < a.P; p += gridDim.x * blockDim.x) {
+    float g;
+    if (a.grad) {
+      g = a.grad[p];
+    } else {
+      g = 0.f;
+      const float* s = a.slab + p;
+      int k = 0;
+      for (; k + 4 <= a.nslab; k += 4) {
+        const float g0 = s[(size_t)(k + 0) * a.P], g1 = s[(size_t)(k + 1) * a.P];
+        const float g2 = s[(size_t)(k + 2) * a.P], g3 = s[(size_t)(k + 3) * a.P];
+        g += (g0 + g1) + (g2 + g3);
+      }
+      for (; k < a.nslab; ++k) g += s[(size_t)k * a.P];
+    }
+    g *= a.grad_scale;
+    if (a.grad_out) a.grad_out[p] = g;
+    float w = a.param[p];
+    if (a.weight_decay != 0.f) g += a.weight_decay * w;
+    const float m = a.beta1 * a.m[p] + (1.f - a.beta1) * g;
+    const float v = a.beta2 * a.v[p] + (1.f - a.beta2) * g * g;
+    a.m[p] = m;
+    a.v[p] = v;
+    // torch.optim.Adam: p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
+    w -= step_size * m / (sqrtf(v) * rbc2 + a.eps);
+    a.param[p] = w;
+  }
+  // arrival ticket: the last block bumps the step counter
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = atomicAdd(a.ticket, 1u);
+    if (prev == gridDim.x - 1) {
+      *a.ticket = 0u;
+      *a.step = t;
+    }
+  }
+}
+
+// Plain slab reduction (used before a data-parallel all-reduce).
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* slab, int nslab, int P, float scale,
+                                                           float* out) {
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+    float g = 0.f;
+    for (int k = 0; k < nslab; ++k) g += slab[(size_t)k * P + p];
+    out[p] = g * scale;
+  }
+}
+
+}  // namespace rrl
+
+using namespace rrl;
+
+static int adam_grid(int P) {
+  int g = (P + 255) / 256;
+  return g > 1024 ? 1024 : (g < 1 ? 1 : g);
+}
+
+extern "C" int rrl_adam(float* param, float* m, float* v, const float* grad, const float* slab, int nslab,
+                        float* grad_out, int* step, unsigned* ticket, int P, float lr, float beta1,
+                        float beta2, float eps, float grad_scale, float weight_decay, void* stream) {
+  AdamArgs a{param, m, v, grad, slab, nslab, grad_out, step, ticket, P, lr, beta1, beta2, eps, grad_scale,
+             weight_decay};
+  hipLaunchKernelGGL(adam_kernel, dim3(adam_grid(P)), dim3(256), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int rrl_reduce_slabs(const float* slab, int nslab, int P, float scale, float* out, void* stream) {
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(adam_grid(P)), dim3(256), 0, (hipStream_t)stream, slab, nslab,
+                     P, scale, out);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,234 @@
+// Fused on-device actor: T steps of {policy MLP forward -> masked softmax -> Philox
+// categorical sample -> log-prob -> env physics -> auto-reset} for N vectorised envs
+// in ONE launch, writing a time-major SoA rollout into HBM.
+//
+// This replaces the reference's per-step agent path (request_for_action ->
+// TorchScript step() at batch 1 -> safetensors encode -> ZMQ push; SURVEY §3.3,
+// agent_zmq.rs:458-571) for the on-GPU actor.  Each wave owns 16 envs; every lane
+// of an env column keeps a replica of that env's state in registers, so the whole
+// step needs no cross-lane traffic except the two head reductions.
+#include "common.h"
+#include "heads.h"
+#include "envs.h"
+
+namespace rrl {
+
+struct RolloutArgs {
+  const float* params;
+  int N, T, H;
+  float* state;     // [N][NS]
+  int* ep_len;      // [N]
+  float* ep_ret;    // [N]
+  float* obs_buf;   // [T+1][N][D]
+  int* act_buf;     // [T][N]
+  float* logp_buf;  // [T][N]
+  float* rew_buf;   // [T][N]
+  float* done_buf;  // [T][N]
+  float* ep_stats;  // [grid][8]: n_done, sum_ret, sumsq_ret, max_ret, min_ret, sum_len
+  uint32_t seed_lo, seed_hi;
+  uint32_t step_lo, step_hi;  // global step of t = 0 (RNG counter)
+  int reset_all;
+  int max_steps;
+};
+
+template <class Env, int HT>
+__global__ __launch_bounds__(256, 2) void rollout_kernel(RolloutArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int DT = 1;
+  using L = LdsNet<DT, HT>;
+  constexpr int H = L::H;
+  constexpr int D = Env::D, A = Env::A, NS = Env::NS;
+  static_assert(D <= 16, "device envs use one input tile");
+  stage_net<DT, HT>(lds, p.params, D, A, false);
+  __syncthreads();
+
+  const int l = lane_id();
+  const int j = l & 15, g = l >> 4;
+  const int wave_in_block = threadIdx.x >> 6;
+  const int waves_per_block = blockDim.x >> 6;
+  const int wave = wave_in_block + blockIdx.x * waves_per_block;
+  const int total_waves = gridDim.x * waves_per_block;
+  const int ntiles = (p.N + kTileB - 1) / kTileB;
+  const uint2 key = make_uint2(p.seed_lo, p.seed_hi);
+  const uint64_t step0 = ((uint64_t)p.step_hi << 32) | p.step_lo;
+
+  float st_n = 0.f, st_sum = 0.f, st_sq = 0.f, st_max = -INFINITY, st_min = INFINITY, st_len = 0.f;
+
+  for (int tile = wave; tile < ntiles; tile += total_waves) {
+    const int env = tile * kTileB + j;
+    const bool valid = env < p.N;
+    const int envc = valid ? env : p.N - 1;
+    float s[NS];
+    int len;
+    float ret;
+    if (p.reset_all) {
+      const uint4 r = philox4x32(make_uint4((uint32_t)envc, (uint32_t)step0, (uint32_t)(step0 >> 32), 1u), key);
+      Env::reset(s, r);
+      len = 0;
+      ret = 0.f;
+    } else {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) s[k] = p.state[(size_t)envc * NS + k];
+      len = p.ep_len[envc];
+      ret = p.ep_ret[envc];
+    }
+
+    for (int t = 0; t < p.T; ++t) {
+      const uint64_t gstep = step0 + (uint64_t)t;
+      const size_t base = (size_t)t * p.N + env;
+      // observation tile (feature f of env j lives in lane group f>>2, reg f&3)
+      floatx4 x[1];
+      x[0] = zero4();
+#pragma unroll
+      for (int f = 0; f < D; ++f) {
+        const float o = Env::obs(s, f);
+        if ((f >> 2) == g) x[0][f & 3] = o;
+      }
+      if (valid) {
+#pragma unroll
+        for (int f = 0; f < D; ++f)
+          if ((f >> 2) == g) p.obs_buf[base * D + f] = x[0][f & 3];
+      }
+      floatx4 h1[HT], h2[HT];
+      dense_fwd<DT, HT, true>(lds + L::W1, L::S1, lds + L::B1, x, h1);
+      dense_fwd<HT, HT, true>(lds + L::W2, L::S2, lds + L::B2, h1, h2);
+      float logits[kMaxAct];
+      policy_logits<HT>(lds + L::W3, lds + L::B3, A, H, h2, logits);
+      const CatStats cs = cat_stats(A, logits);
+      const uint4 rnd = philox4x32(make_uint4((uint32_t)envc, (uint32_t)gstep, (uint32_t)(gstep >> 32), 0u), key);
+      const int a = cat_sample(A, logits, cs.lse, u01(rnd.x));
+      const float logp = pick_logit(A, logits, a) - cs.lse;
+
+      bool term;
+      const float r = Env::step(s, a, term);
+      len += 1;
+      ret += r;
+      const bool trunc = len >= p.max_steps;
+      const bool done = term || trunc;
+      if (valid && g == 0) {
+        p.act_buf[base] = a;
+        p.logp_buf[base] = logp;
+        p.rew_buf[base] = r;
+        p.done_buf[base] = done ? 1.f : 0.f;
+      }
+      if (done) {
+        if (valid && g == 0) {
+          st_n += 1.f;
+          st_sum += ret;
+          st_sq += ret * ret;
+          st_max = fmaxf(st_max, ret);
+          st_min = fminf(st_min, ret);
+          st_len += (float)len;
+        }
+        const uint4 rr = philox4x32(make_uint4((uint32_t)envc, (uint32_t)gstep, (uint32_t)(gstep >> 32), 1u), key);
+        Env::reset(s, rr);
+        len = 0;
+        ret = 0.f;
+      }
+    }
+    // final observation (bootstrap row T) and persistent env state
+    if (valid) {
+      const size_t base = (size_t)p.T * p.N + env;
+#pragma unroll
+      for (int f = 0; f < D; ++f)
+        if ((f >> 2) == g) p.obs_buf[base * D + f] = Env::obs(s, f);
+      if (g == 0) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) p.state[(size_t)env * NS + k] = s[k];
+        p.ep_len[env] = len;
+        p.ep_ret[env] = ret;
+      }
+    }
+  }
+
+  // workgroup reduction of episode statistics
+  __syncthreads();
+  float* red = lds;  // weights no longer needed
+  float v0 = wave_sum(st_n), v1 = wave_sum(st_sum), v2 = wave_sum(st_sq), v5 = wave_sum(st_len);
+  float v3 = st_max, v4 = st_min;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    v3 = fmaxf(v3, __shfl_xor(v3, o, 64));
+    v4 = fminf(v4, __shfl_xor(v4, o, 64));
+  }
+  if (l == 0) {
+    red[wave_in_block * 8 + 0] = v0;
+    red[wave_in_block * 8 + 1] = v1;
+    red[wave_in_block * 8 + 2] = v2;
+    red[wave_in_block * 8 + 3] = v3;
+    red[wave_in_block * 8 + 4] = v4;
+    red[wave_in_block * 8 + 5] = v5;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int q = threadIdx.x;
+    float v = red[q];
+    for (int w = 1; w < waves_per_block; ++w) {
+      const float u = red[w * 8 + q];
+      v = (q == 3) ? fmaxf(v, u) : (q == 4) ? fminf(v, u) : v + u;
+    }
+    p.ep_stats[blockIdx.x * 8 + q] = v;
+  }
+}
+
+}  // namespace rrl
+
+using namespace rrl;
+
+enum EnvId : int { ENV_CARTPOLE = 0, ENV_MOUNTAINCAR = 1, ENV_ACROBOT = 2 };
+
+extern "C" int rrl_env_dims(int env, int* D, int* A, int* NS, int* max_steps) {
+  switch (env) {
+    case ENV_CARTPOLE: *D = CartPoleEnv::D; *A = CartPoleEnv::A; *NS = CartPoleEnv::NS; *max_steps = CartPoleEnv::kMaxSteps; return 0;
+    case ENV_MOUNTAINCAR: *D = MountainCarEnv::D; *A = MountainCarEnv::A; *NS = MountainCarEnv::NS; *max_steps = MountainCarEnv::kMaxSteps; return 0;
+    case ENV_ACROBOT: *D = AcrobotEnv::D; *A = AcrobotEnv::A; *NS = AcrobotEnv::NS; *max_steps = AcrobotEnv::kMaxSteps; return 0;
+  }
+  return -1;
+}
+
+extern "C" int rrl_rollout_grid(int N, int num_cu) {
+  const int tiles = (N + kTileB - 1) / kTileB;
+  int grid = (tiles + 3) / 4;
+  const int cap = 2 * (num_cu > 0 ? num_cu : 256);
+  if (grid > cap) grid = cap;
+  return grid < 1 ? 1 : grid;
+}
+
+template <class Env, int HT>
+static int launch_rollout(const RolloutArgs& a, int grid, hipStream_t s) {
+  using L = LdsNet<1, HT>;
+  const size_t bytes = (size_t)L::floats(Env::A) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)rollout_kernel<Env, HT>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    attr = true;
+  }
+  hipLaunchKernelGGL((rollout_kernel<Env, HT>), dim3(grid), dim3(256), bytes, s, a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int rrl_rollout(int env, const float* params, int N, int T, int H, float* state, int* ep_len,
+                           float* ep_ret, float* obs_buf, int* act_buf, float* logp_buf, float* rew_buf,
+                           float* done_buf, float* ep_stats, uint64_t seed, uint64_t step0, int reset_all,
+                           int max_steps, int num_cu, void* stream) {
+  if (N <= 0 || T <= 0) return -2;
+  RolloutArgs a{params, N, T, H, state, ep_len, ep_ret, obs_buf, act_buf, logp_buf, rew_buf, done_buf, ep_stats,
+                (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step0, (uint32_t)(step0 >> 32), reset_all,
+                max_steps};
+  const int grid = rrl_rollout_grid(N, num_cu);
+  hipStream_t s = (hipStream_t)stream;
+  if (H == 128) {
+    switch (env) {
+      case ENV_CARTPOLE: return launch_rollout<CartPoleEnv, 8>(a, grid, s);
+      case ENV_MOUNTAINCAR: return launch_rollout<MountainCarEnv, 8>(a, grid, s);
+      case ENV_ACROBOT: return launch_rollout<AcrobotEnv, 8>(a, grid, s);
+    }
+  } else if (H == 64) {
+    switch (env) {
+      case ENV_CARTPOLE: return launch_rollout<CartPoleEnv, 4>(a, grid, s);
+      case ENV_MOUNTAINCAR: return launch_rollout<MountainCarEnv, 4>(a, grid, s);
+      case ENV_ACROBOT: return launch_rollout<AcrobotEnv, 4>(a, grid, s);
+    }
+  }
+  return -3;
+}

@@ -1,0 +1,167 @@
+"""In-tree build of the native extensions (no hipify, no JIT cache).
+
+Two shared objects are produced next to this file:
+
+* ``_hip_ops<EXT>``  -- the gfx950 HIP kernels (``csrc/kernels/*.hip``, compiled by
+  ``hipcc --offload-arch=gfx950`` with a C ABI) linked with the PyTorch binding
+  ``csrc/bindings/hip_ops.cpp`` (host compiler, PyTorch-ROCm headers).
+* ``_native<EXT>``   -- the host runtime in C++ (``csrc/host/*.cpp``): safetensors /
+  trajectory codec, ZMTP transport, vectorised CPU environments; pybind11 only.
+
+The reference builds its native core with cargo + PyO3 (relayrl_framework/Cargo.toml,
+build.rs); this is the MI355X-native equivalent.  Usage::
+
+    python -m relayrl_prototype_amd._build            # build both
+    python -m relayrl_prototype_amd._build --target native
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import subprocess
+import sys
+import sysconfig
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(REPO, "csrc")
+BUILD = os.path.join(REPO, "build")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+ARCH = os.environ.get("RRL_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", "g++")
+
+HIP_OPS = os.path.join(PKG_DIR, "_hip_ops" + EXT)
+NATIVE = os.path.join(PKG_DIR, "_native" + EXT)
+
+
+def _jobs() -> int:
+    env = os.environ.get("MAX_JOBS")
+    if env and env.isdigit():
+        return max(1, int(env))
+    return max(1, min(8, os.cpu_count() or 1))
+
+
+def _newer(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print("[build]", " ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build step failed:\n" + " ".join(cmd) + "\n" + r.stdout)
+    return r.stdout
+
+
+def _py_includes():
+    inc = [sysconfig.get_paths()["include"]]
+    try:
+        import pybind11
+
+        inc.append(pybind11.get_include())
+    except ImportError:  # pragma: no cover
+        pass
+    return inc
+
+
+def _torch_flags():
+    import torch
+
+    tdir = os.path.dirname(torch.__file__)
+    inc = [
+        os.path.join(tdir, "include"),
+        os.path.join(tdir, "include", "torch", "csrc", "api", "include"),
+    ]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cflags = [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-D__HIP_PLATFORM_AMD__", "-DUSE_ROCM"]
+    libdir = os.path.join(tdir, "lib")
+    ldflags = [f"-L{libdir}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+               "-ltorch_python", f"-Wl,-rpath,{libdir}"]
+    return inc, cflags, ldflags
+
+
+def build_hip(verbose=False, force=False) -> str:
+    kdir = os.path.join(CSRC, "kernels")
+    srcs = sorted(glob.glob(os.path.join(kdir, "*.hip")))
+    headers = sorted(glob.glob(os.path.join(kdir, "*.h")))
+    binding = os.path.join(CSRC, "bindings", "hip_ops.cpp")
+    odir = os.path.join(BUILD, "hip")
+    os.makedirs(odir, exist_ok=True)
+    objs, jobs = [], []
+    for s in srcs:
+        o = os.path.join(odir, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(o, [s] + headers):
+            jobs.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+                         "-munsafe-fp-atomics", "-I", kdir, "-c", s, "-o", o])
+    tinc, tcf, tld = _torch_flags()
+    bo = os.path.join(odir, "hip_ops.cpp.o")
+    objs.append(bo)
+    if force or _newer(bo, [binding]):
+        cmd = [CXX, "-O2", "-std=c++17", "-fPIC", "-DTORCH_EXTENSION_NAME=_hip_ops",
+               "-DTORCH_API_INCLUDE_EXTENSION_H", "-I/opt/rocm/include"] + tcf
+        for i in tinc + _py_includes():
+            cmd += ["-I", i]
+        cmd += ["-c", binding, "-o", bo]
+        jobs.append(cmd)
+    with cf.ThreadPoolExecutor(_jobs()) as ex:
+        list(ex.map(lambda c: _run(c, verbose), jobs))
+    if force or _newer(HIP_OPS, objs):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", HIP_OPS] + tld, verbose)
+    return HIP_OPS
+
+
+def build_native(verbose=False, force=False) -> str:
+    hdir = os.path.join(CSRC, "host")
+    srcs = sorted(glob.glob(os.path.join(hdir, "*.cpp"))) + [os.path.join(CSRC, "bindings", "native.cpp")]
+    headers = sorted(glob.glob(os.path.join(hdir, "*.h")))
+    odir = os.path.join(BUILD, "native")
+    os.makedirs(odir, exist_ok=True)
+    objs, jobs = [], []
+    for s in srcs:
+        if not os.path.exists(s):
+            continue
+        o = os.path.join(odir, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(o, [s] + headers):
+            cmd = [CXX, "-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-pthread", "-I", hdir]
+            for i in _py_includes():
+                cmd += ["-I", i]
+            cmd += ["-c", s, "-o", o]
+            jobs.append(cmd)
+    with cf.ThreadPoolExecutor(_jobs()) as ex:
+        list(ex.map(lambda c: _run(c, verbose), jobs))
+    if objs and (force or _newer(NATIVE, objs)):
+        _run([CXX, "-shared", "-fPIC", "-pthread"] + objs + ["-o", NATIVE], verbose)
+    return NATIVE
+
+
+def build(targets=("native", "hip"), verbose=False, force=False):
+    out = []
+    if "native" in targets:
+        out.append(build_native(verbose, force))
+    if "hip" in targets:
+        out.append(build_hip(verbose, force))
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--target", choices=["all", "hip", "native"], default="all")
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    t = ("native", "hip") if a.target == "all" else (a.target,)
+    for p in build(t, verbose=a.verbose, force=a.force):
+        print(p)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

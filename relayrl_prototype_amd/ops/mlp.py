@@ -1,0 +1,237 @@
+"""Flat-parameter MLP spec and device/oracle dispatch for every learner/actor op.
+
+All networks are stored as ONE flat fp32 vector per net (``MLPSpec.P`` floats, same
+order as ``nn.Sequential(Linear, ReLU, Linear, ReLU, Linear).parameters()``), so the
+optimiser is a single fused launch, weight broadcast is a single collective, and the
+kernels stage the whole net into LDS with one sweep.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from enum import IntEnum
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+
+class FwdMode(IntEnum):
+    VALUE = 0
+    CAT_SAMPLE = 1
+    CAT_EVAL = 2
+    LOGITS = 3
+    GAUSS_SAMPLE = 4
+    GAUSS_EVAL = 5
+
+
+class GradHead(IntEnum):
+    PG_CAT = 0
+    VALUE_MSE = 1
+    PPO_CAT = 2
+    PPO_GAUSS = 3
+    PG_GAUSS = 4
+
+
+@dataclass(frozen=True)
+class MLPSpec:
+    """Linear(D,H)-ReLU-Linear(H,H)-ReLU-Linear(H,A) [+ log_std(A)]."""
+
+    D: int
+    H: int
+    A: int
+    gaussian: bool = False
+
+    @property
+    def P(self) -> int:
+        D, H, A = self.D, self.H, self.A
+        return H * D + H + H * H + H + A * H + A + (A if self.gaussian else 0)
+
+    def offsets(self):
+        D, H, A = self.D, self.H, self.A
+        o = {}
+        o["w1"] = 0
+        o["b1"] = H * D
+        o["w2"] = o["b1"] + H
+        o["b2"] = o["w2"] + H * H
+        o["w3"] = o["b2"] + H
+        o["b3"] = o["w3"] + A * H
+        o["log_std"] = o["b3"] + A
+        return o
+
+    def init(self, generator: Optional[torch.Generator] = None, device="cpu", log_std_init: float = -0.5,
+             out_gain: Optional[float] = None) -> torch.Tensor:
+        """nn.Linear default init (kaiming_uniform(a=sqrt(5)) == U(+-1/sqrt(fan_in)))."""
+        D, H, A = self.D, self.H, self.A
+        parts = []
+        for fan_in, fan_out in ((D, H), (H, H), (H, A)):
+            bound = 1.0 / math.sqrt(fan_in)
+            w = (torch.rand(fan_out * fan_in, generator=generator) * 2 - 1) * bound
+            b = (torch.rand(fan_out, generator=generator) * 2 - 1) * bound
+            if out_gain is not None and fan_out == A:
+                w = w * out_gain
+                b = b * 0
+            parts += [w, b]
+        if self.gaussian:
+            parts.append(torch.full((A,), float(log_std_init)))
+        return torch.cat(parts).float().to(device)
+
+    def unflatten(self, params):
+        return ref.unflatten(params, self.D, self.H, self.A, self.gaussian)
+
+
+def _hip_for(t):
+    from . import use_hip, hip
+
+    return hip() if use_hip(t) else None
+
+
+def _f32(t):
+    return None if t is None else t.contiguous().float()
+
+
+def _i32(t):
+    return None if t is None else t.contiguous().to(torch.int32)
+
+
+def mlp_forward(mode: int, params: torch.Tensor, X: torch.Tensor, A: int, H: int, mask=None, act_in=None,
+                actc_in=None, seed: int = 0, step: int = 0, row_offset: int = 0, out: Optional[dict] = None):
+    """Batched fused forward.  Returns a dict with keys among v / act / logp / entropy / logits / mean."""
+    X = X.contiguous().float()
+    B = X.shape[0]
+    h = _hip_for(X)
+    if h is None:
+        return ref.mlp_forward_ref(int(mode), params, X, A, H, mask, act_in, actc_in, seed, step, row_offset)
+    dev = X.device
+    out = {} if out is None else out
+    mode = int(mode)
+    if mode == FwdMode.VALUE:
+        v = out.get("v")
+        if v is None:
+            v = out["v"] = torch.empty(B, device=dev)
+        h.mlp_forward(mode, params, X, A, H, None, None, None, None, None, v, None, None, seed, step, row_offset)
+        return out
+    o0 = out.setdefault("logp", torch.empty(B, device=dev))
+    o1 = out.setdefault("entropy", torch.empty(B, device=dev))
+    act_out = actc_out = logits = None
+    if mode == FwdMode.CAT_SAMPLE:
+        act_out = out.setdefault("act", torch.empty(B, dtype=torch.int32, device=dev))
+    elif mode == FwdMode.LOGITS:
+        logits = out.setdefault("logits", torch.empty(B, A, device=dev))
+    elif mode == FwdMode.GAUSS_SAMPLE:
+        actc_out = out.setdefault("act", torch.empty(B, A, device=dev))
+        logits = out.setdefault("mean", torch.empty(B, A, device=dev))
+    elif mode == FwdMode.GAUSS_EVAL:
+        logits = out.setdefault("mean", torch.empty(B, A, device=dev))
+    h.mlp_forward(mode, params, X, A, H, _f32(mask), _i32(act_in), _f32(actc_in), act_out, actc_out, o0, o1,
+                  logits, seed, step, row_offset)
+    return out
+
+
+def grad_slabs(B: int, device) -> int:
+    if torch.device(device).type != "cuda":
+        return 1
+    from . import hip
+
+    return int(hip().mlp_grad_slabs(B))
+
+
+def mlp_grad(head: int, params, X, A: int, H: int, mask=None, act=None, actc=None, adv=None, ret=None,
+             logp_old=None, adv_stats=None, inv_B: Optional[float] = None, clip_eps: float = 0.2,
+             ent_coef: float = 0.0, grad_slab=None, loss_slab=None):
+    """Fused forward+backward.  GPU: fills grad_slab [nslab, P] and loss_slab [nslab, 8] and
+    returns them; CPU: returns (grad [1, P], loss stats [1, 8]) computed with autograd."""
+    X = X.contiguous().float()
+    B = X.shape[0]
+    if inv_B is None:
+        inv_B = 1.0 / max(B, 1)
+    h = _hip_for(X)
+    if h is None:
+        g, st = ref.mlp_grad_ref(int(head), params, X, A, H, mask, act, actc, adv, ret, logp_old, adv_stats,
+                                 inv_B, clip_eps, ent_coef)
+        ls = torch.zeros(1, 8)
+        ls[0, 0] = st.get("loss", 0.0)
+        ls[0, 1] = st.get("entropy", 0.0)
+        ls[0, 2] = st.get("kl", 0.0)
+        ls[0, 3] = st.get("clipfrac", 0.0)
+        ls[0, 4] = st.get("v", 0.0)
+        ls[0, 5] = st.get("count", B)
+        return g.view(1, -1), ls
+    gaussian = int(head) in (GradHead.PPO_GAUSS, GradHead.PG_GAUSS)
+    Aeff = 1 if int(head) == GradHead.VALUE_MSE else A
+    P = MLPSpec(X.shape[1], H, Aeff, gaussian).P
+    ns = int(h.mlp_grad_slabs(B))
+    if grad_slab is None:
+        grad_slab = torch.empty(ns, P, device=X.device)
+    if loss_slab is None:
+        loss_slab = torch.empty(ns, 8, device=X.device)
+    h.mlp_grad(int(head), params, X, A, H, _f32(mask), _i32(act), _f32(actc), _f32(adv), _f32(ret), _f32(logp_old),
+               adv_stats, float(inv_B), float(clip_eps), float(ent_coef), grad_slab, loss_slab)
+    return grad_slab[:ns], loss_slab[:ns]
+
+
+def reduce_slabs(slab: torch.Tensor, scale: float = 1.0, out=None):
+    if out is None:
+        out = torch.empty(slab.shape[1], device=slab.device)
+    h = _hip_for(slab)
+    if h is None:
+        out.copy_(slab.sum(0) * scale)
+        return out
+    h.reduce_slabs(slab.contiguous(), float(scale), out)
+    return out
+
+
+def adam_step(param, m, v, step_t, ticket_t, lr, grad=None, slab=None, beta1=0.9, beta2=0.999, eps=1e-8,
+              grad_scale=1.0, weight_decay=0.0, grad_out=None):
+    """One fused Adam update of a flat parameter vector; `step_t` is a 1-elem int32 tensor
+    holding the number of completed steps (incremented on the device)."""
+    h = _hip_for(param)
+    if h is None:
+        g = grad if grad is not None else slab.sum(0)
+        g = g * grad_scale
+        if grad_out is not None:
+            grad_out.copy_(g)
+        step = int(step_t.item()) + 1
+        ref.adam_ref(param, m, v, g, step, lr, beta1, beta2, eps, weight_decay)
+        step_t.fill_(step)
+        return
+    h.adam(param, m, v, grad, slab, grad_out, step_t, ticket_t, float(lr), float(beta1), float(beta2), float(eps),
+           float(grad_scale), float(weight_decay))
+
+
+def gae_scan_tm(rew, done, val, gamma, lam, adv=None, ret=None, stats_part=None, stats_out=None):
+    """Time-major [T, N] GAE / discounted-return scan -> (adv, ret, stats[3])."""
+    h = _hip_for(rew)
+    if h is None:
+        a, r, s = ref.gae_scan_tm_ref(rew, done, val, gamma, lam)
+        if stats_out is not None:
+            stats_out.copy_(s)
+        return a, r, s
+    T, N = rew.shape
+    dev = rew.device
+    adv = torch.empty(T, N, device=dev) if adv is None else adv
+    ret = torch.empty(T, N, device=dev) if ret is None else ret
+    if stats_part is None:
+        stats_part = torch.empty(int(h.scan_tm_parts(N)), 3, device=dev)
+    if stats_out is None:
+        stats_out = torch.empty(3, device=dev)
+    h.gae_scan_tm(rew.contiguous(), done.contiguous(), None if val is None else val.contiguous(), adv, ret,
+                  stats_part, stats_out, float(gamma), float(lam))
+    return adv, ret, stats_out
+
+
+def scan_flat(rew, done, val, boot, gamma, lam):
+    """Flat concatenated-paths scan (finish_path semantics) -> (adv, ret, stats[3])."""
+    h = _hip_for(rew)
+    if h is None:
+        return ref.scan_flat_ref(rew, done, val, boot, gamma, lam)
+    L = rew.numel()
+    dev = rew.device
+    adv = torch.empty(L, device=dev)
+    ret = torch.empty(L, device=dev)
+    work = torch.empty(max(1, int(h.scan_flat_blocks(L))) * 9, device=dev)
+    stats = torch.empty(3, device=dev)
+    h.scan_flat(rew.contiguous().float(), done.contiguous().float(), _f32(val), _f32(boot), adv, ret, work, stats,
+                float(gamma), float(lam))
+    return adv, ret, stats
