@@ -1,0 +1,139 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: CartPole-v1 REINFORCE (+ value baseline), env steps/sec (whole node).
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is
+launched under ``torch.distributed.run`` with one rank per GPU (RCCL).  One "step" is
+one full training epoch of the on-device actor+learner (runtime/vec_trainer.py):
+rollout of num_envs x rollout_len env steps per GPU (policy forward + sampling + env
+physics in one fused kernel) + GAE scan + 1 policy Adam step + 80 value Adam steps
+(the reference REINFORCE.train_model, REINFORCE.py:97-125).  Nothing is skipped inside
+the timed region.  Weak scaling: per-GPU envs are fixed as N grows; gradients are
+all-reduced over RCCL every optimiser step.
+
+BASELINE.md: the reference publishes no numbers, so ``vs_baseline`` is null.
+``--ttt`` additionally measures wall-clock to the CartPole-v1 return threshold (475).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+METRIC = "env steps/sec (whole node) + wall-clock to return threshold, CartPole REINFORCE"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--num-envs", type=int, default=32768, help="envs per GPU")
+    ap.add_argument("--rollout-len", type=int, default=64)
+    ap.add_argument("--no-baseline", action="store_true", help="REINFORCE without the value baseline")
+    ap.add_argument("--vf-iters", type=int, default=80)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--ttt", action="store_true", help="also measure wall-clock to AverageEpRet >= 475")
+    ap.add_argument("--ttt-envs", type=int, default=4096)
+    ap.add_argument("--ttt-max-s", type=float, default=120.0)
+    return ap.parse_args(argv)
+
+
+def time_to_threshold(args, comm, threshold=475.0):
+    import torch
+    from relayrl_prototype_amd.runtime.vec_trainer import VecTrainer, VecTrainerConfig
+
+    cfg = VecTrainerConfig(num_envs=args.ttt_envs, rollout_len=128, with_baseline=True, pi_lr=1e-2, vf_lr=3e-3,
+                           train_vf_iters=20, gamma=0.99, lam=0.95, seed=7)
+    tr = VecTrainer(cfg, comm)
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while True:
+        tr.train_epoch()
+        m = tr.metrics()
+        el = time.perf_counter() - t0
+        if m["AverageEpRet"] == m["AverageEpRet"] and m["AverageEpRet"] >= threshold:
+            return el, tr.epoch, m["EnvSteps"]
+        if el > args.ttt_max_s:
+            return None, tr.epoch, m["EnvSteps"]
+
+
+def main(argv=None):
+    args = parse(argv)
+    import torch
+
+    from relayrl_prototype_amd.parallel.comm import init_distributed
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    comm = init_distributed()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    from relayrl_prototype_amd.runtime.vec_trainer import VecTrainer, VecTrainerConfig
+
+    cfg = VecTrainerConfig(num_envs=args.num_envs, rollout_len=args.rollout_len, with_baseline=not args.no_baseline,
+                           train_vf_iters=args.vf_iters, use_graphs=not args.no_graphs)
+    tr = VecTrainer(cfg, comm)
+    for _ in range(args.warmup):
+        tr.train_epoch()
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.train_epoch()
+    comm.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    comm.all_reduce_max_(t)
+    dt = float(t.item())
+    m = tr.metrics()
+    world = comm.world
+    steps_per_epoch = cfg.num_envs * cfg.rollout_len * world
+    value = steps_per_epoch * args.steps / dt
+    ttt = None
+    if args.ttt:
+        ttt = time_to_threshold(args, comm)
+    if comm.rank == 0:
+        algo = "REINFORCE" if args.no_baseline else "REINFORCE-with-baseline"
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "env_steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (on-device CartPole-v1 physics, random-init weights)",
+            "config": {
+                "model": f"{algo} MLP[128,128] CartPole-v1 (policy+value, fp32 MFMA)",
+                "global_batch": steps_per_epoch,
+                "seq_len": cfg.rollout_len,
+                "parallelism": f"dp{world}",
+                "envs_per_gpu": cfg.num_envs,
+                "train_vf_iters": cfg.train_vf_iters if cfg.with_baseline else 0,
+                "hyperparams": "reference defaults (gamma .98, lam .97, pi_lr 3e-4, vf_lr 1e-3)",
+            },
+            "final_avg_ep_ret": None if m["AverageEpRet"] != m["AverageEpRet"] else round(m["AverageEpRet"], 2),
+        }
+        if args.ttt:
+            rec["time_to_threshold_s"] = None if ttt[0] is None else round(ttt[0], 3)
+            rec["time_to_threshold_epochs"] = ttt[1]
+            rec["time_to_threshold_env_steps"] = ttt[2]
+        print(json.dumps(rec), flush=True)
+    if comm.world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,132 @@
+"""Device learner building blocks shared by REINFORCE / A2C / PPO.
+
+``FlatNet`` = one MLP as a single flat fp32 parameter vector + fused-Adam state (m, v,
+device step counter).  Gradients come out of the fused fwd+bwd kernel as per-workgroup
+slabs; with one rank the slabs feed the fused reduce+Adam kernel directly, with several
+ranks they are reduced to one flat vector, all-reduced over RCCL, then Adam runs on it.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..ops import MLPSpec, GradHead, adam_step, mlp_grad, reduce_slabs, grad_slabs
+from ..parallel.comm import Comm
+
+
+class FlatNet:
+    def __init__(self, spec: MLPSpec, lr: float, device, generator: Optional[torch.Generator] = None,
+                 betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, params: Optional[torch.Tensor] = None,
+                 log_std_init: float = -0.5):
+        self.spec = spec
+        self.device = torch.device(device)
+        self.lr = float(lr)
+        self.betas = betas
+        self.eps = float(eps)
+        self.weight_decay = float(weight_decay)
+        if params is None:
+            params = spec.init(generator, log_std_init=log_std_init)
+        assert params.numel() == spec.P, (params.numel(), spec.P)
+        self.params = params.detach().float().contiguous().to(self.device).clone()
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.step = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.grad = torch.zeros_like(self.params)
+        self.version = 0
+
+    @property
+    def P(self) -> int:
+        return self.spec.P
+
+    def apply(self, slab: torch.Tensor, comm: Optional[Comm] = None):
+        """Reduce the gradient slabs (and all-reduce across ranks) then take one Adam step."""
+        b1, b2 = self.betas
+        if comm is None or comm.world == 1:
+            adam_step(self.params, self.m, self.v, self.step, self.ticket, self.lr, slab=slab, beta1=b1, beta2=b2,
+                      eps=self.eps, weight_decay=self.weight_decay)
+        else:
+            reduce_slabs(slab, 1.0, out=self.grad)
+            comm.all_reduce_sum_(self.grad)
+            adam_step(self.params, self.m, self.v, self.step, self.ticket, self.lr, grad=self.grad, beta1=b1,
+                      beta2=b2, eps=self.eps, weight_decay=self.weight_decay)
+        self.version += 1
+
+    def state_dict(self) -> dict:
+        return {"params": self.params.detach().cpu(), "m": self.m.cpu(), "v": self.v.cpu(),
+                "step": self.step.cpu(), "lr": torch.tensor(self.lr)}
+
+    def load_state_dict(self, sd: dict):
+        self.params.copy_(sd["params"].to(self.device))
+        self.m.copy_(sd["m"].to(self.device))
+        self.v.copy_(sd["v"].to(self.device))
+        self.step.copy_(sd["step"].to(self.device))
+        if "lr" in sd:
+            self.lr = float(sd["lr"])
+
+
+class ValueLoop:
+    """``iters`` x (fused value fwd+bwd -> fused reduce+Adam), optionally captured into one
+    hipGraph (REINFORCE.py:110-115 runs this loop 80 times per epoch)."""
+
+    def __init__(self, net: FlatNet, comm: Optional[Comm], use_graph: bool = True):
+        self.net = net
+        self.comm = comm
+        self.use_graph = use_graph and net.device.type == "cuda" and (comm is None or comm.world == 1)
+        self._graph = None
+        self._key = None
+        self.loss_first = None
+        self.loss_last = None
+
+    def _body(self, obs, ret, iters, inv_B, slab, ls_first, ls_last):
+        H = self.net.spec.H
+        for k in range(iters):
+            ls = ls_first if k == 0 else ls_last
+            mlp_grad(GradHead.VALUE_MSE, self.net.params, obs, 1, H, ret=ret, inv_B=inv_B, grad_slab=slab,
+                     loss_slab=ls)
+            self.net.apply(slab, self.comm)
+
+    def run(self, obs: torch.Tensor, ret: torch.Tensor, iters: int, inv_B: float):
+        B = obs.shape[0]
+        dev = obs.device
+        if iters <= 0:
+            return
+        if dev.type != "cuda":
+            # CPU oracle path: autograd + torch Adam math
+            for k in range(iters):
+                g, ls = mlp_grad(GradHead.VALUE_MSE, self.net.params, obs, 1, self.net.spec.H, ret=ret, inv_B=inv_B)
+                if k == 0:
+                    self.loss_first = ls
+                self.loss_last = ls
+                self.net.apply(g, self.comm)
+            return
+        ns = grad_slabs(B, dev)
+        key = (obs.data_ptr(), ret.data_ptr(), B, iters, float(inv_B))
+        if self._key != key:
+            self._slab = torch.empty(ns, self.net.P, device=dev)
+            self.loss_first = torch.zeros(ns, 8, device=dev)
+            self.loss_last = torch.zeros(ns, 8, device=dev)
+            self._graph = None
+            self._key = key
+        if not self.use_graph:
+            self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last)
+            return
+        v0 = self.net.version
+        if self._graph is None:
+            # Warm up once eagerly (kernel attributes, allocator) on the real buffers,
+            # then restore the optimiser state so the warm-up step leaves no trace.
+            saved = [t.clone() for t in (self.net.params, self.net.m, self.net.v, self.net.step)]
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._body(obs, ret, 1, inv_B, self._slab, self.loss_first, self.loss_last)
+            torch.cuda.current_stream().wait_stream(s)
+            for dst, src in zip((self.net.params, self.net.m, self.net.v, self.net.step), saved):
+                dst.copy_(src)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last)
+            self._graph = g
+        self._graph.replay()
+        self.net.version = v0 + iters

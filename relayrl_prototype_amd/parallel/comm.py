@@ -1,0 +1,120 @@
+"""Process-group communicator: one process per GPU, RCCL over xGMI ("nccl" backend on
+ROCm), gloo for CPU tests.
+
+The reference has no collectives at all: trajectories fan in over
+ZMQ/gRPC and TorchScript files fan out.  Here every data-plane exchange is a
+collective on ONE flat buffer:
+
+* C8 gradient sync     -> ``all_reduce_sum_`` of the flat fp32 gradient (one call per update)
+* C2 weight fan-out    -> ``broadcast_`` of the flat fp32 parameter vector from the learner
+* C1 rollout fan-in    -> ``gather_to`` (paired send/recv so each actor uses its own link)
+* advantage statistics -> ``all_reduce_sum_`` of a 3-float vector
+
+xGMI is point-to-point (7 links per GPU); the flat gradient of a 128x128 MLP is ~70 KB,
+so these are latency-bound: keep them fused, one call per optimiser step.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def dist_env() -> tuple:
+    """(rank, local_rank, world) from torchrun-style environment variables."""
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    return rank, local, world
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) -> "Comm":
+    """Initialise the default process group from the environment (torchrun) if world > 1."""
+    rank, local, world = dist_env()
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s))
+    return Comm()
+
+
+class Comm:
+    """Thin wrapper so single-process code paths need no branches."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.enabled = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.enabled else 1
+        self.rank = dist.get_rank(group) if self.enabled else 0
+        self.backend = dist.get_backend(group) if self.enabled else "none"
+
+    @property
+    def is_master(self) -> bool:
+        return self.rank == 0
+
+    def all_reduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
+
+    def all_reduce_max_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t
+
+    def all_reduce_min_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return t
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.world > 1:
+            dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def barrier(self):
+        if self.world > 1:
+            if self.backend == "nccl" and torch.cuda.is_available():
+                dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
+            else:
+                dist.barrier(group=self.group)
+
+    def gather_to(self, t: torch.Tensor, dst: int, out: Optional[List[torch.Tensor]] = None):
+        """Rollout fan-in: every rank's ``t`` lands in ``out[rank]`` on ``dst``.
+
+        Implemented as grouped point-to-point send/recv (each actor->learner transfer
+        rides its own xGMI link) rather than a ring gather.
+        """
+        if self.world == 1:
+            if out is not None:
+                out[0].copy_(t)
+            return out
+        ops = []
+        if self.rank == dst:
+            assert out is not None and len(out) == self.world
+            for r in range(self.world):
+                if r == dst:
+                    out[r].copy_(t)
+                else:
+                    ops.append(dist.P2POp(dist.irecv, out[r], r, self.group))
+        else:
+            ops.append(dist.P2POp(dist.isend, t, dst, self.group))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        return out
+
+    def all_gather_object(self, obj):
+        if self.world == 1:
+            return [obj]
+        res = [None] * self.world
+        dist.all_gather_object(res, obj, group=self.group)
+        return res
