@@ -1,0 +1,129 @@
+"""Policy-gradient learner over flat device batches (REINFORCE, A2C, PPO).
+
+Shared by the trajectory-fed plugin algorithms (reinforce.py / ppo.py / a2c.py) and by
+the vectorised on-device trainer.  Every optimisation step is one fused fwd+bwd HIP
+launch + one fused reduce+Adam launch (+ one RCCL all-reduce with several ranks):
+
+  REINFORCE (REINFORCE.py:97-125): 1 policy step on -mean(logp * adv) then
+            ``train_vf_iters`` value steps (separate optimisers -- the reference's
+            pi_optimizer also covered the baseline parameters, defect A15);
+  A2C      : 1 policy step with an entropy bonus + value steps;
+  PPO      : ``train_pi_iters`` clipped-surrogate steps with approximate-KL early
+            stopping, then value steps.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..ops import GradHead, MLPSpec, mlp_grad, grad_slabs
+from ..parallel.comm import Comm
+from .core import FlatNet, ValueLoop
+
+
+class PGLearner:
+    def __init__(self, algo: str, obs_dim: int, act_dim: int, hidden: int = 128, discrete: bool = True,
+                 with_baseline: bool = True, pi_lr: float = 3e-4, vf_lr: float = 1e-3, train_vf_iters: int = 80,
+                 train_pi_iters: int = 1, clip_ratio: float = 0.2, target_kl: Optional[float] = None,
+                 ent_coef: float = 0.0, device="cpu", seed: int = 0, comm: Optional[Comm] = None,
+                 use_graphs: bool = True, log_std_init: float = -0.5, pi_params=None, vf_params=None):
+        algo = algo.lower()
+        assert algo in ("reinforce", "a2c", "ppo"), algo
+        self.algo = algo
+        self.obs_dim, self.act_dim, self.hidden = obs_dim, act_dim, hidden
+        self.discrete = discrete
+        self.with_baseline = with_baseline or algo in ("a2c", "ppo")
+        self.train_vf_iters = int(train_vf_iters)
+        self.train_pi_iters = int(train_pi_iters) if algo == "ppo" else 1
+        self.clip_ratio = float(clip_ratio)
+        self.target_kl = target_kl
+        self.ent_coef = float(ent_coef)
+        self.device = torch.device(device)
+        self.comm = comm or Comm()
+        g = torch.Generator().manual_seed(int(seed))
+        self.pi = FlatNet(MLPSpec(obs_dim, hidden, act_dim, not discrete), pi_lr, self.device, g, params=pi_params,
+                          log_std_init=log_std_init)
+        self.vf = FlatNet(MLPSpec(obs_dim, hidden, 1), vf_lr, self.device, g, params=vf_params) \
+            if self.with_baseline else None
+        self.vloop = ValueLoop(self.vf, self.comm, use_graph=use_graphs) if self.vf is not None else None
+        self._pi_slab = None
+        self._pi_loss = None
+        self.last = {}
+
+    @property
+    def head(self) -> int:
+        if self.algo == "ppo":
+            return int(GradHead.PPO_CAT if self.discrete else GradHead.PPO_GAUSS)
+        return int(GradHead.PG_CAT if self.discrete else GradHead.PG_GAUSS)
+
+    def _slabs(self, B):
+        if self.device.type != "cuda":
+            return None, None
+        ns = grad_slabs(B, self.device)
+        if self._pi_slab is None or self._pi_slab.shape[0] < ns:
+            self._pi_slab = torch.empty(ns, self.pi.P, device=self.device)
+            self._pi_loss = torch.empty(ns, 8, device=self.device)
+        return self._pi_slab[:ns], self._pi_loss[:ns]
+
+    def optimize(self, obs, act=None, actc=None, mask=None, adv=None, ret=None, adv_stats=None, logp_old=None,
+                 inv_B: Optional[float] = None):
+        """One epoch of updates on a prepared batch (adv/ret already computed).
+
+        Returns a dict of *device* tensors (loss slabs) -- call ``summarize`` to sync.
+        """
+        B = obs.shape[0]
+        if inv_B is None:
+            inv_B = 1.0 / max(B * self.comm.world, 1)
+        H, A = self.hidden, self.act_dim
+        slab, ls = self._slabs(B)
+        kl_stop = None
+        pi_loss = None
+        for it in range(self.train_pi_iters):
+            out = mlp_grad(self.head, self.pi.params, obs, A, H, mask=mask, act=act, actc=actc, adv=adv,
+                           logp_old=logp_old, adv_stats=adv_stats, inv_B=inv_B, clip_eps=self.clip_ratio,
+                           ent_coef=self.ent_coef, grad_slab=slab, loss_slab=ls)
+            if it == 0:
+                pi_loss = out[1].sum(0).clone()
+            if self.algo == "ppo" and self.target_kl is not None and it > 0:
+                # approx KL of the current policy (measured in this iteration's forward)
+                st = out[1].sum(0)
+                st = self.comm.all_reduce_sum_(st.clone())
+                kl = (st[2] / torch.clamp(st[5], min=1.0)).item()
+                if kl > 1.5 * self.target_kl:
+                    kl_stop = it
+                    break
+            self.pi.apply(out[0], self.comm)
+        if self.vloop is not None and self.train_vf_iters > 0:
+            self.vloop.run(obs, ret, self.train_vf_iters, inv_B)
+        self.last = {"pi_loss": pi_loss, "kl_stop": kl_stop}
+        return self.last
+
+    def summarize(self) -> dict:
+        """Synchronising read of the last optimize() statistics (global over ranks)."""
+        out = {}
+        pl = self.last.get("pi_loss")
+        if pl is not None:
+            v = self.comm.all_reduce_sum_(pl.clone().to(self.device)).tolist()
+            n = max(v[5], 1.0)
+            out.update(LossPi=v[0] / n, Entropy=v[1] / n, KL=v[2] / n, ClipFrac=v[3] / n, DeltaLossPi=0.0)
+        if self.vloop is not None and self.vloop.loss_last is not None:
+            l1 = self.vloop.loss_last.sum(0)
+            l0 = self.vloop.loss_first.sum(0)
+            v = self.comm.all_reduce_sum_(torch.stack([l1[0], l1[4], l1[5], l0[0]]).to(self.device)).tolist()
+            n = max(v[2], 1.0)
+            out.update(LossV=v[0] / n, VVals=v[1] / n, DeltaLossV=(v[0] - v[3]) / n)
+        if self.last.get("kl_stop") is not None:
+            out["StopIter"] = self.last["kl_stop"]
+        return out
+
+    def state_dict(self) -> dict:
+        sd = {"pi": self.pi.state_dict()}
+        if self.vf is not None:
+            sd["vf"] = self.vf.state_dict()
+        return sd
+
+    def load_state_dict(self, sd: dict):
+        self.pi.load_state_dict(sd["pi"])
+        if self.vf is not None and "vf" in sd:
+            self.vf.load_state_dict(sd["vf"])

@@ -1,0 +1,207 @@
+"""RelayRLAgent -- Python API of the reference's PyRelayRLAgent (o3_agent.rs:49-329;
+agent_wrapper.rs, agent_zmq.rs, agent_grpc.rs).
+
+Per step the agent evaluates its policy locally (CPU numpy MLP from the learner's flat
+weights -- no TorchScript interpreter, no per-step safetensors encodes) and appends an
+action to the current episode.  Semantics (docs/COMPAT.md):
+  * ``request_for_action(obs, mask, reward)``: ``reward`` is the reward of the PREVIOUS
+    step (the reference notebooks' calling convention); it is attributed to the previous
+    action, fixing the off-by-one alignment of the reference;
+  * ``flag_last_action(reward, done=True)`` ends the episode, attaches the final reward to
+    the last action and ships the episode (one RRLT frame); ``truncated=True`` ships it
+    as a time-limit cut so the learner bootstraps from V(s_T);
+  * model updates arrive asynchronously (ZMQ push / gRPC poll after each episode /
+    in-process subscription) and are swapped atomically between steps.
+"""
+from __future__ import annotations
+
+import threading
+from typing import Optional
+
+import numpy as np
+
+from ..config import ConfigLoader, address, resolve_config_json_path
+from ..models.cpu_policy import CPUPolicy
+from ..runtime.model_store import ModelBlob
+from ..types import RelayRLAction, RelayRLTrajectory
+
+
+class RelayRLAgent:
+    def __init__(self, model_path: Optional[str] = None, config_path: Optional[str] = "./config.json",
+                 server_type: str = "zmq", training_port: Optional[str] = None,
+                 training_prefix: Optional[str] = None, training_host: Optional[str] = None,
+                 agent_id: Optional[str] = None, seed: Optional[int] = None, handshake_timeout_s: float = 60.0):
+        from ..transport.zmq_transport import make_agent_id
+
+        self.config_path = resolve_config_json_path(config_path)
+        self.cfg = ConfigLoader(None, self.config_path)
+        self.server_type = (server_type or "zmq").lower()
+        self.agent_id = agent_id or make_agent_id()
+        ts = dict(self.cfg.get_train_server())
+        # NOTE: the reference bound these with port/prefix swapped (o3_agent.rs:89-96, A3)
+        if training_prefix is not None:
+            ts["prefix"] = training_prefix
+        if training_host is not None:
+            ts["host"] = training_host
+        if training_port is not None:
+            ts["port"] = str(training_port)
+        self.train_server = ts
+        self.max_traj_length = self.cfg.get_max_traj_length()
+        self._seed = seed
+        self.policy: Optional[CPUPolicy] = None
+        self._policy_lock = threading.Lock()
+        self.model_path = model_path
+        self.enabled = True
+        self.transport = None
+        self._handshake_timeout = handshake_timeout_s
+        self.traj = RelayRLTrajectory(self.max_traj_length, None, agent_id=self.agent_id)
+        if model_path is not None:
+            self._load_model_file(model_path)
+        self._connect()
+        self.episodes_sent = 0
+
+    # ------------------------------------------------------------------ models
+    def _load_model_file(self, path: str):
+        """Initial model from a TorchScript file WE exported (flat weights recovered)."""
+        import torch
+
+        from ..models.policies import flat_from_module, module_dims
+
+        m = torch.jit.load(path, map_location="cpu")
+        obs_dim, act_dim, hidden, discrete = module_dims(m)
+        pi, vf = flat_from_module(m, discrete)
+        self._set_policy(ModelBlob(0, {"obs_dim": obs_dim, "act_dim": act_dim, "hidden": int(hidden),
+                                       "discrete": discrete}, pi.numpy(), None if vf is None else vf.numpy()))
+
+    def _set_policy(self, blob: ModelBlob):
+        m = blob.meta
+        with self._policy_lock:
+            if self.policy is None or (self.policy.obs_dim, self.policy.act_dim, self.policy.hidden) != (
+                    m["obs_dim"], m["act_dim"], m["hidden"]):
+                seed = self._seed if self._seed is not None else (hash(self.agent_id) & 0x7FFFFFFF)
+                self.policy = CPUPolicy(m["obs_dim"], m["act_dim"], m["hidden"], m.get("discrete", True), blob.pi,
+                                        blob.vf, seed)
+            else:
+                self.policy.load(blob.pi, blob.vf)
+            self.policy.version = blob.version
+            self._validate()
+
+    def _validate(self):
+        """agent_wrapper.rs:88-168: dims known and a dummy step returns (act, non-empty dict)."""
+        p = self.policy
+        act, data = p.step(np.zeros(p.obs_dim, np.float32), np.ones(p.act_dim, np.float32))
+        if act is None or not data:
+            raise RuntimeError("model validation failed")
+
+    @property
+    def model_version(self) -> int:
+        return -1 if self.policy is None else self.policy.version
+
+    # ------------------------------------------------------------------ transport
+    def _connect(self, training_server_address: Optional[str] = None):
+        if training_server_address:
+            s = training_server_address
+            prefix = ""
+            if "://" in s:
+                prefix, s = s.split("://", 1)
+                prefix += "://"
+            host, port = s.rsplit(":", 1)
+            self.train_server = {"prefix": prefix or self.train_server.get("prefix", ""), "host": host, "port": port}
+        if self.server_type == "zmq":
+            from ..transport.zmq_transport import ZmqAgentTransport
+
+            al = dict(self.cfg.get_agent_listener())
+            tr = dict(self.cfg.get_traj_server())
+            for d in (al, tr):
+                if d["host"] in ("*", "0.0.0.0"):
+                    d["host"] = "127.0.0.1"
+            self.transport = ZmqAgentTransport(self.agent_id, address(al), address(tr), self._set_policy,
+                                               self._handshake_timeout)
+        elif self.server_type == "grpc":
+            from ..transport.grpc_transport import GrpcAgentTransport
+
+            host = self.train_server["host"]
+            if host in ("*", "0.0.0.0"):
+                host = "127.0.0.1"
+            self.transport = GrpcAgentTransport(f"{host}:{self.train_server['port']}", self._set_policy,
+                                                handshake_timeout_s=self._handshake_timeout)
+        elif self.server_type == "local":
+            from ..transport.local import LocalAgentTransport
+
+            self.transport = LocalAgentTransport(address(self.train_server), self._set_policy, self.agent_id)
+        else:
+            raise ValueError(f"server_type must be zmq, grpc or local, not {self.server_type!r}")
+
+    def _ship(self, traj: RelayRLTrajectory):
+        if self.server_type == "zmq":
+            self.transport.send_trajectory(traj.encode())
+        elif self.server_type == "grpc":
+            if self.transport.send_trajectory_pb(traj):
+                self.transport.poll(timeout_s=5.0)
+        else:
+            self.transport.send_trajectory_obj(traj)
+        self.episodes_sent += 1
+
+    # ------------------------------------------------------------------ API
+    def request_for_action(self, obs, mask=None, reward: float = 0.0) -> RelayRLAction:
+        if not self.enabled:
+            raise RuntimeError("agent is disabled")
+        if self.policy is None:
+            raise RuntimeError("no model loaded")
+        if len(self.traj) > 0:
+            self.traj.actions[-1].update_reward(float(reward))
+        with self._policy_lock:
+            p = self.policy
+            obs_a = np.asarray(obs, np.float32)
+            mask_a = np.ones(p.act_dim, np.float32) if mask is None else np.asarray(mask, np.float32)
+            act, data = p.step(obs_a, mask_a)
+        a0 = act[0] if act.ndim >= 1 else act
+        aux = {k: np.asarray(v[0], np.float32) for k, v in data.items()}
+        action = RelayRLAction(obs_a, np.asarray(a0), mask_a, 0.0, aux, False, False)
+        self.traj.add_action(action, send_if_done=False)
+        if len(self.traj) >= self.max_traj_length:
+            # very long episode: ship the segment (learner bootstraps it) and continue
+            self._ship(self.traj)
+            self.traj = RelayRLTrajectory(self.max_traj_length, None, agent_id=self.agent_id)
+            self.traj.seq = self.episodes_sent
+        return action
+
+    def flag_last_action(self, reward: float = 0.0, done: bool = True, truncated: bool = False) -> None:
+        if len(self.traj) == 0:
+            return
+        last = self.traj.actions[-1]
+        last.update_reward(float(reward))
+        if done and not truncated:
+            last._done = True
+        self.traj.seq = self.episodes_sent
+        self._ship(self.traj)
+        self.traj = RelayRLTrajectory(self.max_traj_length, None, agent_id=self.agent_id)
+
+    def restart_agent(self, training_server_address: Optional[str] = None) -> bool:
+        self.disable_agent()
+        try:
+            self.enable_agent(training_server_address)
+            return True
+        except Exception as e:
+            print(f"[RelayRLAgent] restart failed: {e!r}", flush=True)
+            return False
+
+    def disable_agent(self) -> None:
+        self.enabled = False
+        if self.transport is not None:
+            self.transport.close()
+            self.transport = None
+
+    def enable_agent(self, training_server_address: Optional[str] = None) -> None:
+        if self.transport is None:
+            self._connect(training_server_address)
+        self.enabled = True
+
+    def close(self):
+        self.disable_agent()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -1,0 +1,205 @@
+"""ZMTP (ZeroMQ wire protocol) endpoints over the native C++ sockets.
+
+Server side (reference training_zmq.rs:669-1058):
+  * ROUTER bound at ``agent_listener``: ``["", "GET_MODEL"(, fmt)]`` -> ``["", model]``;
+    ``["", "MODEL_SET"]`` -> register + ``["", "ID_LOGGED"]``; ``["", "HEARTBEAT"]``;
+    ``["", "BYE"]``.  Model updates are pushed to every registered agent over the same
+    ROUTER socket as ``["", "MODEL", version, blob]`` -- the reference instead connected
+    a PUSH to a PULL each agent had to *bind* on one fixed port, which limited it to one
+    agent per host (defect A6) and never stopped listening only when multiactor was set.
+  * PULL bound at ``trajectory_server``: one RRLT frame per trajectory (fan-in).
+Agent side (agent_zmq.rs:163-698): DEALER (identity = agent id) + PUSH.
+No busy polling anywhere (A7): receives block in C++ with timeouts.
+"""
+from __future__ import annotations
+
+import os
+import random
+import threading
+import time
+from typing import Callable, Optional
+
+from .. import _native
+from ..runtime.model_store import ModelBlob
+from ..types import RelayRLTrajectory
+
+FMT_TORCHSCRIPT = b"TORCHSCRIPT"
+FMT_RRLM = b"RRLM"
+
+
+def make_agent_id() -> str:
+    """``AGENT_ID-{pid}{rand}`` like agent_zmq.rs:171-174 (plus more entropy)."""
+    return f"AGENT_ID-{os.getpid()}{random.randint(0, 99)}-{random.getrandbits(32):08x}"
+
+
+class ZmqTrainingEndpoint:
+    def __init__(self, service, agent_listener: str, trajectory_server: str, multiactor: bool = True,
+                 verbose: bool = False):
+        self.service = service
+        self.multiactor = multiactor
+        self.verbose = verbose
+        self.router = _native.ZmtpSocket(_native.SockType.ROUTER)
+        self.pull = _native.ZmtpSocket(_native.SockType.PULL)
+        self.listener_port = self.router.bind(agent_listener)
+        self.traj_port = self.pull.bind(trajectory_server)
+        self.agents = {}  # identity -> wants format
+        self._lock = threading.Lock()
+        self._stop = threading.Event()
+        self._threads = [threading.Thread(target=self._listen_agents, daemon=True, name="rrl-zmq-listener"),
+                         threading.Thread(target=self._listen_traj, daemon=True, name="rrl-zmq-traj")]
+        for t in self._threads:
+            t.start()
+        service.store.subscribe(self._on_model)
+
+    def _log(self, *a):
+        if self.verbose:
+            print("[ZmqTrainingEndpoint]", *a, flush=True)
+
+    def _model_payload(self, fmt: bytes) -> bytes:
+        blob = self.service.store.latest()
+        if blob is None:
+            return b"ERROR: no model"
+        return blob.encode() if fmt == FMT_RRLM else blob.torchscript()
+
+    def _listen_agents(self):
+        while not self._stop.is_set():
+            msg = self.router.recv(100)
+            if msg is None:
+                continue
+            peer, frames = msg
+            body = [f for f in frames if f != b""]
+            if not body:
+                continue
+            cmd = body[0]
+            try:
+                if cmd == b"GET_MODEL":
+                    fmt = body[1] if len(body) > 1 else FMT_TORCHSCRIPT
+                    with self._lock:
+                        self.agents.setdefault(peer, fmt)
+                        self.agents[peer] = fmt
+                    self.router.send([peer, b"", self._model_payload(fmt)], 5000)
+                elif cmd == b"MODEL_SET":
+                    self.service.register_agent(peer.decode(errors="replace"))
+                    self.router.send([peer, b"", b"ID_LOGGED"], 5000)
+                    self._log("registered", peer)
+                elif cmd == b"HEARTBEAT":
+                    self.service.register_agent(peer.decode(errors="replace"))
+                elif cmd == b"BYE":
+                    with self._lock:
+                        self.agents.pop(peer, None)
+                else:
+                    self.router.send([peer, b"", b"ERROR: unknown command"], 1000)
+            except Exception as e:
+                self._log("listener error", e)
+
+    def _listen_traj(self):
+        while not self._stop.is_set():
+            msg = self.pull.recv(100)
+            if msg is None:
+                continue
+            _, frames = msg
+            for f in frames:
+                try:
+                    traj = RelayRLTrajectory.decode(f)
+                except Exception as e:
+                    self._log("bad trajectory frame", e)
+                    continue
+                self.service.submit(traj)
+
+    def _on_model(self, blob: ModelBlob):
+        with self._lock:
+            agents = list(self.agents.items())
+        if not agents:
+            return
+        enc = {}
+        for peer, fmt in agents:
+            if fmt not in enc:
+                enc[fmt] = blob.encode() if fmt == FMT_RRLM else blob.torchscript()
+            self.router.send([peer, b"", b"MODEL", str(blob.version).encode(), enc[fmt]], 1000)
+
+    def close(self):
+        self._stop.set()
+        self.service.store.unsubscribe(self._on_model)
+        for t in self._threads:
+            t.join(timeout=5)
+        self.router.close()
+        self.pull.close()
+
+
+class ZmqAgentTransport:
+    """DEALER handshake + model-update listener + PUSH trajectory sender."""
+
+    def __init__(self, agent_id: str, agent_listener: str, trajectory_server: str,
+                 on_model: Callable[[ModelBlob], None], handshake_timeout_s: float = 60.0):
+        self.agent_id = agent_id
+        self.on_model = on_model
+        self.dealer = _native.ZmtpSocket(_native.SockType.DEALER, agent_id.encode())
+        self.dealer.connect(agent_listener)
+        self.push = _native.ZmtpSocket(_native.SockType.PUSH)
+        self.push.connect(trajectory_server)
+        self._replies = []
+        self._cv = threading.Condition()
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._recv_loop, daemon=True, name="rrl-agent-dealer")
+        self._thread.start()
+        self.model: Optional[ModelBlob] = None
+        self._handshake(handshake_timeout_s)
+
+    def _recv_loop(self):
+        while not self._stop.is_set():
+            msg = self.dealer.recv(100)
+            if msg is None:
+                continue
+            _, frames = msg
+            body = [f for f in frames if f != b""] if frames and frames[0] == b"" else frames
+            if len(body) >= 3 and body[0] == b"MODEL":
+                try:
+                    blob = ModelBlob.decode(body[2])
+                    self.model = blob
+                    self.on_model(blob)
+                except Exception as e:
+                    print(f"[ZmqAgentTransport] bad model update: {e!r}", flush=True)
+                continue
+            with self._cv:
+                self._replies.append(body)
+                self._cv.notify_all()
+
+    def _request(self, frames, timeout_s: float):
+        with self._cv:
+            self._replies.clear()
+        if not self.dealer.send([b""] + frames, int(timeout_s * 1000)):
+            return None
+        with self._cv:
+            self._cv.wait_for(lambda: bool(self._replies), timeout=timeout_s)
+            return self._replies.pop(0) if self._replies else None
+
+    def _handshake(self, timeout_s: float):
+        """GET_MODEL -> MODEL_SET -> ID_LOGGED, retried every second (agent_zmq.rs:316-442)."""
+        t0 = time.time()
+        while time.time() - t0 < timeout_s:
+            rep = self._request([b"GET_MODEL", FMT_RRLM], 1.0)
+            if rep and rep[0][:4] == b"RRLM":
+                blob = ModelBlob.decode(rep[0])
+                self.model = blob
+                self.on_model(blob)
+                ack = self._request([b"MODEL_SET"], 5.0)
+                if ack and ack[0] == b"ID_LOGGED":
+                    return
+            time.sleep(0.05)
+        raise TimeoutError("ZMQ handshake with the training server timed out")
+
+    def send_trajectory(self, payload: bytes) -> bool:
+        return self.push.send([payload], 10000)
+
+    def heartbeat(self):
+        self.dealer.send([b"", b"HEARTBEAT"], 1000)
+
+    def close(self):
+        try:
+            self.dealer.send([b"", b"BYE"], 200)
+        except Exception:
+            pass
+        self._stop.set()
+        self._thread.join(timeout=5)
+        self.dealer.close()
+        self.push.close()

@@ -1,0 +1,303 @@
+"""RelayRLAction / RelayRLTrajectory (reference: rf/src/types/{action,trajectory}.rs and
+their PyO3 classes o3_action.rs:48-235, o3_trajectory.rs:34-166).
+
+Host-side record types of the agent API.  Tensors are kept as numpy arrays with their
+dtype and shape (the reference flattened everything to f64 via tolist(), defect A12);
+the wire encodings are native C++ (``_native``):
+
+* ``TensorData`` JSON form = {"shape", "dtype", "data": bytes of a one-tensor
+  safetensors file} -- byte-compatible with the reference (action.rs:342-352);
+* trajectories travel as RRLT binary frames (``RelayRLTrajectory.encode``).
+
+The on-GPU actor never builds these objects: it writes SoA rollout buffers in HBM.
+"""
+from __future__ import annotations
+
+import json
+import threading
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+from . import _native
+
+_NP2DT = {
+    np.dtype(np.uint8): "Byte",
+    np.dtype(np.int16): "Short",
+    np.dtype(np.int32): "Int",
+    np.dtype(np.int64): "Long",
+    np.dtype(np.float32): "Float",
+    np.dtype(np.float64): "Double",
+    np.dtype(np.bool_): "Bool",
+}
+_DT2NP = {v: k for k, v in _NP2DT.items()}
+_SCALAR_KINDS = ("Byte", "Short", "Int", "Long", "Float", "Double", "String", "Bool")
+
+
+def to_numpy(x) -> Optional[np.ndarray]:
+    """numpy / torch / list / scalar -> contiguous numpy array with a supported dtype."""
+    if x is None:
+        return None
+    if hasattr(x, "detach") and hasattr(x, "cpu"):  # torch.Tensor
+        x = x.detach().cpu().numpy()
+    a = np.asarray(x)
+    if a.dtype not in _NP2DT:
+        if np.issubdtype(a.dtype, np.floating):
+            a = a.astype(np.float32)
+        elif np.issubdtype(a.dtype, np.integer):
+            a = a.astype(np.int64)
+        else:
+            raise TypeError(f"unsupported tensor dtype {a.dtype}")
+    return np.ascontiguousarray(a)
+
+
+def tensor_to_wire(a: np.ndarray):
+    return (_NP2DT[a.dtype], list(a.shape), a.tobytes())
+
+
+def tensor_from_wire(t) -> np.ndarray:
+    dt, shape, raw = t
+    return np.frombuffer(raw, dtype=_DT2NP[dt]).reshape(shape).copy()
+
+
+def tensordata_json(a: np.ndarray) -> dict:
+    """Reference TensorData serde form: data = one-tensor safetensors file as u8 list."""
+    dt, shape, raw = tensor_to_wire(a)
+    st = _native.st_encode(dt, shape, raw)
+    return {"shape": shape, "dtype": dt, "data": list(st)}
+
+
+def tensordata_from_json(d: dict) -> np.ndarray:
+    dt, shape, raw = _native.st_decode(bytes(d["data"]))
+    a = np.frombuffer(raw, dtype=_DT2NP[dt]).reshape(shape).copy()
+    if d.get("dtype") == "Bool":
+        a = a.astype(np.bool_)
+    return a
+
+
+def _aux_to_wire(v):
+    if isinstance(v, (bool, np.bool_)):
+        return ("Bool", bool(v))
+    if isinstance(v, (int, np.integer)) and not isinstance(v, bool):
+        return ("Long", int(v))
+    if isinstance(v, (float, np.floating)):
+        return ("Double", float(v))
+    if isinstance(v, str):
+        return ("String", v)
+    return ("Tensor", tensor_to_wire(to_numpy(v)))
+
+
+def _aux_from_wire(kv):
+    kind, val = kv
+    if kind == "Tensor":
+        return tensor_from_wire(val)
+    return val
+
+
+class RelayRLAction:
+    """One (obs, act, mask, reward, aux data, done) record (action.rs:421-689)."""
+
+    __slots__ = ("_obs", "_act", "_mask", "_rew", "_data", "_done", "_reward_updated")
+
+    def __init__(self, obs=None, act=None, mask=None, rew: float = 0.0, data: Optional[Dict[str, Any]] = None,
+                 done: bool = False, reward_updated: bool = False):
+        self._obs = to_numpy(obs)
+        self._act = to_numpy(act)
+        self._mask = to_numpy(mask)
+        self._rew = float(rew)
+        self._data = None if data is None else {str(k): v for k, v in data.items()}
+        self._done = bool(done)
+        self._reward_updated = bool(reward_updated)
+
+    # getters (o3_action.rs:96-160)
+    def get_obs(self) -> Optional[np.ndarray]:
+        return self._obs
+
+    def get_act(self) -> Optional[np.ndarray]:
+        return self._act
+
+    def get_mask(self) -> Optional[np.ndarray]:
+        return self._mask
+
+    def get_rew(self) -> float:
+        return self._rew
+
+    def get_data(self) -> Dict[str, Any]:
+        if self._data is None:
+            return {}
+        out = {}
+        for k, v in self._data.items():
+            out[k] = to_numpy(v) if not isinstance(v, (bool, int, float, str, np.number, np.bool_)) else v
+        return out
+
+    def get_done(self) -> bool:
+        return self._done
+
+    def get_reward_updated(self) -> bool:
+        return self._reward_updated
+
+    def update_reward(self, reward: float) -> None:
+        self._rew = float(reward)
+        self._reward_updated = True
+
+    # wire forms ---------------------------------------------------------
+    def to_wire(self) -> dict:
+        return {
+            "obs": None if self._obs is None else tensor_to_wire(self._obs),
+            "act": None if self._act is None else tensor_to_wire(self._act),
+            "mask": None if self._mask is None else tensor_to_wire(self._mask),
+            "rew": self._rew,
+            "data": None if self._data is None else {k: _aux_to_wire(v) for k, v in self._data.items()},
+            "done": self._done,
+            "reward_updated": self._reward_updated,
+        }
+
+    @classmethod
+    def from_wire(cls, d: dict) -> "RelayRLAction":
+        a = cls.__new__(cls)
+        a._obs = None if d["obs"] is None else tensor_from_wire(d["obs"])
+        a._act = None if d["act"] is None else tensor_from_wire(d["act"])
+        a._mask = None if d["mask"] is None else tensor_from_wire(d["mask"])
+        a._rew = float(d["rew"])
+        a._data = None if d["data"] is None else {k: _aux_from_wire(v) for k, v in d["data"].items()}
+        a._done = bool(d["done"])
+        a._reward_updated = bool(d["reward_updated"])
+        return a
+
+    def to_json_dict(self) -> dict:
+        def td(x):
+            return None if x is None else tensordata_json(x)
+
+        data = None
+        if self._data is not None:
+            data = {}
+            for k, v in self._data.items():
+                kind, val = _aux_to_wire(v)
+                data[k] = {"Tensor": tensordata_json(tensor_from_wire(val))} if kind == "Tensor" else {kind: val}
+        return {"obs": td(self._obs), "act": td(self._act), "mask": td(self._mask), "rew": self._rew, "data": data,
+                "done": self._done, "reward_updated": self._reward_updated}
+
+    def to_json(self) -> str:
+        """Reference serde JSON (o3_action.rs:162-175)."""
+        return json.dumps(self.to_json_dict())
+
+    @staticmethod
+    def action_from_json(d) -> "RelayRLAction":
+        if isinstance(d, str):
+            d = json.loads(d)
+
+        def td(x):
+            return None if x is None else tensordata_from_json(x)
+
+        data = None
+        if d.get("data") is not None:
+            data = {}
+            for k, v in d["data"].items():
+                (kind, val), = v.items()
+                data[k] = tensordata_from_json(val) if kind == "Tensor" else val
+        return RelayRLAction(td(d.get("obs")), td(d.get("act")), td(d.get("mask")), d.get("rew", 0.0), data,
+                             d.get("done", False), d.get("reward_updated", False))
+
+    def __repr__(self):
+        return (f"RelayRLAction(obs={None if self._obs is None else self._obs.shape}, act={self._act}, "
+                f"rew={self._rew}, done={self._done})")
+
+
+class _PushPool:
+    """One long-lived PUSH socket per trajectory-server address (the reference opened a
+    new zmq Context + socket for every send, trajectory.rs:69-90)."""
+
+    _lock = threading.Lock()
+    _socks: Dict[str, Any] = {}
+
+    @classmethod
+    def get(cls, addr: str):
+        with cls._lock:
+            s = cls._socks.get(addr)
+            if s is None or s.closed():
+                s = _native.ZmtpSocket(_native.SockType.PUSH)
+                s.connect(addr)
+                cls._socks[addr] = s
+            return s
+
+
+class RelayRLTrajectory:
+    """Ordered list of actions for one agent (trajectory.rs:96-204).
+
+    ``add_action`` sends the trajectory to ``trajectory_server`` when a ``done`` action
+    arrives (if ``send_if_done``) and then CLEARS it -- the reference only cleared at
+    ``len >= max_length`` which made every upload cumulative (defect A1).
+    """
+
+    def __init__(self, max_length: int = 1000, trajectory_server: Optional[str] = "tcp://127.0.0.1:5556",
+                 agent_id: str = "", sender=None, send_if_done: bool = False):
+        self.max_length = int(max_length)
+        self.trajectory_server = trajectory_server
+        self.agent_id = agent_id
+        self.seq = 0
+        self.actions: List[RelayRLAction] = []
+        self._sender = sender
+        self._send_if_done = send_if_done
+
+    def get_actions(self) -> List[RelayRLAction]:
+        return list(self.actions)
+
+    def __len__(self):
+        return len(self.actions)
+
+    def add_action(self, action: RelayRLAction, send_if_done: Optional[bool] = None) -> bool:
+        """Append; on a done action optionally ship the episode.  Returns True if sent."""
+        self.actions.append(action)
+        send = self._send_if_done if send_if_done is None else send_if_done
+        sent = False
+        if action.get_done():
+            if send:
+                self.send()
+                sent = True
+            if sent or len(self.actions) >= self.max_length:
+                self.actions.clear()
+        elif len(self.actions) >= self.max_length and send:
+            # truncated episode: ship what we have (not done) and start a new segment
+            self.send()
+            self.actions.clear()
+            sent = True
+        return sent
+
+    def send(self):
+        payload = self.encode()
+        self.seq += 1
+        if self._sender is not None:
+            self._sender(payload)
+        elif self.trajectory_server:
+            _PushPool.get(self.trajectory_server).send([payload], 10000)
+
+    def clear(self):
+        self.actions.clear()
+
+    # encodings --------------------------------------------------------
+    def encode(self) -> bytes:
+        return _native.traj_encode({"server": self.trajectory_server or "", "max_length": self.max_length,
+                                    "agent_id": self.agent_id, "seq": self.seq,
+                                    "actions": [a.to_wire() for a in self.actions]})
+
+    @staticmethod
+    def decode(buf: bytes) -> "RelayRLTrajectory":
+        d = _native.traj_decode(buf)
+        t = RelayRLTrajectory(d["max_length"], d["server"] or None, d["agent_id"])
+        t.seq = d["seq"]
+        t.actions = [RelayRLAction.from_wire(a) for a in d["actions"]]
+        return t
+
+    def to_json(self) -> str:
+        """{"inner": {trajectory_server, max_length, actions}} (o3_trajectory.rs:75-78)."""
+        return json.dumps({"inner": {"trajectory_server": self.trajectory_server, "max_length": self.max_length,
+                                     "actions": [a.to_json_dict() for a in self.actions]}})
+
+    @staticmethod
+    def traj_from_json(d) -> "RelayRLTrajectory":
+        if isinstance(d, str):
+            d = json.loads(d)
+        inner = d["inner"] if "inner" in d else d
+        t = RelayRLTrajectory(inner.get("max_length", 1000), inner.get("trajectory_server"))
+        t.actions = [RelayRLAction.action_from_json(a) for a in inner.get("actions", [])]
+        return t

@@ -1,0 +1,172 @@
+"""End-to-end agent <-> training server over the local, ZMTP and gRPC transports (CPU).
+
+This is the reference's notebook flow (cartpole_zmq.ipynb:37-97) as a test: a server
+and an agent in one process, episodes of a CartPole env, the learner updating every
+``traj_per_epoch`` episodes and the agent receiving the new model.
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from relayrl_prototype_amd import _native
+from relayrl_prototype_amd.api.agent import RelayRLAgent
+from relayrl_prototype_amd.api.server import TrainingServer
+from relayrl_prototype_amd.config import DEFAULT_CONFIG_CONTENT
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture
+def cfgdir(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("RRL_QUIET_CONFIG", "1")
+    cfg = json.loads(DEFAULT_CONFIG_CONTENT)
+    cfg["algorithms"]["REINFORCE"]["traj_per_epoch"] = 4
+    cfg["algorithms"]["REINFORCE"]["train_vf_iters"] = 3
+    cfg["server"]["training_server"]["port"] = str(free_port())
+    cfg["server"]["trajectory_server"]["port"] = str(free_port())
+    cfg["server"]["agent_listener"]["port"] = str(free_port())
+    p = tmp_path / "relayrl_config.json"
+    p.write_text(json.dumps(cfg))
+    return tmp_path, str(p)
+
+
+def run_episodes(agent, n, max_steps=200):
+    env = _native.VecEnv("CartPole-v1", 1, 3, 1)
+    obs = np.zeros((1, 4), np.float32)
+    rew = np.zeros(1, np.float32)
+    done = np.zeros(1, np.float32)
+    act = np.zeros(1, np.int32)
+    env.reset_ptr(obs.ctypes.data)
+    lens = []
+    for _ in range(n):
+        r, steps = 0.0, 0
+        while True:
+            a = agent.request_for_action(obs[0].copy(), np.ones(2, np.float32), r)
+            act[0] = int(np.asarray(a.get_act()).reshape(-1)[0])
+            env.step_ptr(act.ctypes.data, obs.ctypes.data, rew.ctypes.data, done.ctypes.data)
+            r = float(rew[0])
+            steps += 1
+            if done[0] > 0 or steps >= max_steps:
+                agent.flag_last_action(r, done=bool(done[0] > 0), truncated=not bool(done[0] > 0))
+                break
+        lens.append(steps)
+    return lens
+
+
+@pytest.mark.parametrize("server_type", ["local", "zmq", "grpc"])
+def test_agent_server_roundtrip(cfgdir, server_type):
+    tmp, cfgp = cfgdir
+    srv = TrainingServer("REINFORCE", 4, 2, 100000, env_dir=str(tmp / "env"), config_path=cfgp,
+                         server_type=server_type, device="cpu", hyperparams={"with_vf_baseline": "true"})
+    try:
+        agent = RelayRLAgent(config_path=cfgp, server_type=server_type, handshake_timeout_s=30)
+        assert agent.model_version == 0
+        run_episodes(agent, 8)
+        import time
+
+        t0 = time.time()
+        while srv.service.received < 8 and time.time() - t0 < 20:
+            time.sleep(0.02)
+        assert srv.wait_idle(60)
+        assert srv.service.updates == 2 and srv.service.errors == 0, srv.service.last_error
+        # the agent picks the update up (push / poll / subscription)
+        import time
+
+        t0 = time.time()
+        while agent.model_version < 2 and time.time() - t0 < 10:
+            if server_type == "grpc":
+                agent.transport.poll(1.0)
+            time.sleep(0.05)
+        assert agent.model_version == 2
+        np.testing.assert_allclose(agent.policy.pi[0].T.ravel()[:10],
+                                   srv.algorithm.learner.pi.params[:10].numpy(), rtol=1e-6)
+        # progress.txt written with the reference columns
+        logs = list((tmp / "env" / "logs").rglob("progress.txt"))
+        assert logs
+        header = logs[0].read_text().splitlines()[0].split("\t")
+        for col in ("Epoch", "AverageEpRet", "StdEpRet", "MaxEpRet", "MinEpRet", "EpLen", "LossPi",
+                    "DeltaLossPi", "AverageVVals", "LossV", "KL", "Entropy"):
+            assert col in header, col
+        assert srv.restart_server()  # lifecycle keeps learner state
+        assert srv.service.updates == 2
+        agent.close()
+    finally:
+        srv.close(save=False)
+
+
+def test_two_agents_zmq(cfgdir):
+    tmp, cfgp = cfgdir
+    srv = TrainingServer("REINFORCE", 4, 2, 100000, env_dir=str(tmp / "env"), config_path=cfgp, server_type="zmq",
+                         device="cpu", multiactor=True)
+    try:
+        a1 = RelayRLAgent(config_path=cfgp, server_type="zmq")
+        a2 = RelayRLAgent(config_path=cfgp, server_type="zmq")
+        run_episodes(a1, 2)
+        run_episodes(a2, 2)
+        import time
+
+        t0 = time.time()
+        while srv.service.received < 4 and time.time() - t0 < 20:
+            time.sleep(0.02)
+        assert srv.wait_idle(60)
+        assert srv.service.updates == 1
+        import time
+
+        t0 = time.time()
+        while (a1.model_version < 1 or a2.model_version < 1) and time.time() - t0 < 10:
+            time.sleep(0.05)
+        assert a1.model_version == 1 and a2.model_version == 1  # both got the push (A6 fixed)
+        assert len(srv.service.agents) == 2
+        a1.close()
+        a2.close()
+    finally:
+        srv.close(save=False)
+
+
+def test_server_model_file_is_torchscript(cfgdir):
+    import torch
+
+    tmp, cfgp = cfgdir
+    srv = TrainingServer("REINFORCE", 4, 2, 1000, env_dir=str(tmp / "env"), config_path=cfgp, server_type="local",
+                         device="cpu")
+    try:
+        path = srv.cfg.get_server_model_path()
+        assert os.path.exists(path)
+        m = torch.jit.load(path)
+        act, data = m.step(torch.zeros(1, 4), torch.ones(1, 2))
+        assert m.get_input_dim() == 4 and m.get_output_dim() == 2 and "logp_a" in data
+        # an agent can start from that file
+        a = RelayRLAgent(model_path=path, config_path=cfgp, server_type="local")
+        assert a.policy.obs_dim == 4
+        a.close()
+    finally:
+        srv.close(save=False)
+
+
+def test_custom_algorithm_plugin(cfgdir):
+    tmp, cfgp = cfgdir
+    plug = tmp / "algos" / "MYALGO"
+    plug.mkdir(parents=True)
+    (plug / "MYALGO.py").write_text(
+        "from relayrl_prototype_amd.algorithms.reinforce import REINFORCE\n"
+        "class MYALGO(REINFORCE):\n"
+        "    CONFIG_NAME = 'REINFORCE'\n"
+        "    def exp_name(self):\n"
+        "        return 'my-algo'\n")
+    srv = TrainingServer("MYALGO", 4, 2, 1000, env_dir=str(tmp / "env"), config_path=cfgp, server_type="local",
+                         algorithm_dir=str(tmp / "algos"), device="cpu", hyperparams=["pi_lr=0.01", "bogus 3"])
+    try:
+        assert type(srv.algorithm).__name__ == "MYALGO"
+        assert srv.algorithm.params["pi_lr"] == 0.01
+    finally:
+        srv.close(save=False)
