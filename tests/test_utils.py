@@ -1,0 +1,113 @@
+"""Logger format, checkpoint round trip, reference-weight import, TB events, algorithms on CPU."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from relayrl_prototype_amd.utils.checkpoint import import_reference_weights, load_checkpoint, save_checkpoint
+from relayrl_prototype_amd.utils.logger import EpochLogger, read_progress, setup_logger_kwargs
+from relayrl_prototype_amd.utils.tensorboard import EventWriter, ProgressTensorboard, crc32c, read_events
+
+REF_CKPT = "/root/reference/examples/REINFORCE_without_baseline/classic_control/cartpole/zmq/client_model.pt"
+
+
+def test_crc32c_known_vector():
+    assert crc32c(b"123456789") == 0xE3069283
+
+
+def test_epoch_logger_progress_format(tmp_path):
+    kw = setup_logger_kwargs("relayrl-reinforce-info", seed=3, data_dir=str(tmp_path))
+    assert kw["output_dir"].endswith(os.path.join("relayrl-reinforce-info", "relayrl-reinforce-info_s3"))
+    lg = EpochLogger(**kw, quiet=True)
+    lg.save_config({"a": 1, "b": [1, 2]})
+    for ep in range(3):
+        lg.store(EpRet=[1.0 + ep, 3.0 + ep], EpLen=5)
+        lg.log_tabular("Epoch", ep + 1)
+        lg.log_tabular("EpRet", with_min_and_max=True)
+        lg.log_tabular("EpLen", average_only=True)
+        lg.dump_tabular()
+    cols = read_progress(os.path.join(kw["output_dir"], "progress.txt"))
+    assert list(cols) == ["Epoch", "AverageEpRet", "StdEpRet", "MaxEpRet", "MinEpRet", "EpLen"]
+    assert cols["AverageEpRet"] == [2.0, 3.0, 4.0] and cols["StdEpRet"][0] == 1.0
+    assert json.load(open(os.path.join(kw["output_dir"], "config.json")))["exp_name"] == "relayrl-reinforce-info"
+
+
+def test_reference_progress_parses():
+    p = ("/root/reference/examples/REINFORCE_without_baseline/box2d/lunar_lander/grpc/logs/relayrl-reinforce-info/"
+         "relayrl-reinforce-info_s298690001/progress.txt")
+    if not os.path.exists(p):
+        pytest.skip("reference not mounted")
+    cols = read_progress(p)
+    assert len(cols["Epoch"]) == 118 and "DeltaLossPi" in cols
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    st = {"pi": {"params": torch.randn(10), "step": torch.tensor([3], dtype=torch.int32)}, "epoch": 7,
+          "cfg": {"lr": 0.1, "name": "x"}}
+    save_checkpoint(str(tmp_path / "c"), st)
+    back = load_checkpoint(str(tmp_path / "c"))
+    assert torch.equal(back["pi"]["params"], st["pi"]["params"]) and back["epoch"] == 7
+    assert back["cfg"]["name"] == "x"
+
+
+def test_import_reference_weights_without_unpickling():
+    if not os.path.exists(REF_CKPT):
+        pytest.skip("reference not mounted")
+    pi, vf = import_reference_weights(REF_CKPT, 4, 2, 128)
+    assert pi.size == 17410 and vf is None and np.isfinite(pi).all()
+    from relayrl_prototype_amd.models.cpu_policy import CPUPolicy
+
+    p = CPUPolicy(4, 2, 128, True, pi)
+    act, data = p.step(np.zeros(4, np.float32), np.ones(2, np.float32))
+    assert act.shape == (1,) and np.isfinite(data["logp_a"]).all()
+
+
+def test_event_writer_and_progress_tail(tmp_path):
+    w = EventWriter(str(tmp_path / "tb"))
+    w.add_scalar("loss", 1.5, 3)
+    w.close()
+    assert read_events(w.path) == [("loss", 1.5, 3)]
+    logs = tmp_path / "logs" / "exp" / "exp_s0"
+    logs.mkdir(parents=True)
+    (logs / "progress.txt").write_text("Epoch\tAverageEpRet\tLossPi\n1\t10.0\t0.5\n2\t20.0\t0.25\n")
+    tb = ProgressTensorboard(str(tmp_path / "logs"), ["AverageEpRet", "LossPi"])
+    assert tb.poll_once() == 4
+    ev = glob_events(logs / "tb")
+    assert ("AverageEpRet", 20.0, 2) in read_events(ev)
+
+
+def glob_events(d):
+    import glob
+
+    return glob.glob(os.path.join(str(d), "events.out.tfevents.*"))[0]
+
+
+@pytest.mark.parametrize("algo,discrete", [("REINFORCE", True), ("PPO", True), ("PPO", False), ("A2C", True)])
+def test_trajectory_algorithms_cpu(tmp_path, monkeypatch, algo, discrete):
+    """Each algorithm ingests synthetic episodes and produces finite updates (oracle path)."""
+    monkeypatch.setenv("RRL_QUIET_CONFIG", "1")
+    from relayrl_prototype_amd.algorithms.registry import make_algorithm
+    from relayrl_prototype_amd.types import RelayRLAction, RelayRLTrajectory
+
+    D, A = 3, 2
+    alg = make_algorithm(algo, env_dir=str(tmp_path), config_path=str(tmp_path / "c.json"), obs_dim=D, act_dim=A,
+                         buf_size=10000, device="cpu", traj_per_epoch=2, train_vf_iters=2, discrete=discrete,
+                         train_pi_iters=3, hidden=64)
+    p0 = alg.learner.pi.params.clone()
+    rng = np.random.default_rng(0)
+    updated = False
+    for ep in range(2):
+        t = RelayRLTrajectory(100, None)
+        for s in range(7):
+            act = np.array([rng.integers(0, A)]) if discrete else rng.standard_normal(A).astype(np.float32)
+            t.add_action(RelayRLAction(obs=rng.standard_normal(D), act=act, mask=np.ones(A), rew=1.0,
+                                       data={"logp_a": np.float32(-0.7 if discrete else -2.0)}, done=(s == 6)))
+        updated = alg.receive_trajectory(t)
+    assert updated and alg.epoch == 1
+    assert torch.isfinite(alg.learner.pi.params).all() and not torch.equal(p0, alg.learner.pi.params)
+    m = alg.last_metrics
+    assert np.isfinite(m["LossPi"]) and np.isfinite(m["LossV"])
+    alg.save(str(tmp_path / "m.pt"))
+    assert os.path.getsize(tmp_path / "m.pt") > 1000
