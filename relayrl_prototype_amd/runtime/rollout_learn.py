@@ -1,0 +1,74 @@
+"""Shared "rollout -> returns -> optimise" step for the vectorised trainers."""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from ..algorithms.learner import PGLearner
+from ..ops import FwdMode, gae_scan_tm, mlp_forward
+from ..parallel.comm import Comm
+
+
+class RolloutLearner:
+    """Owns the HBM-resident scan buffers and drives a PGLearner on time-major rollouts."""
+
+    def __init__(self, learner: PGLearner, T: int, N: int, gamma: float, lam: float, comm: Optional[Comm] = None):
+        self.learner = learner
+        self.T, self.N = T, N
+        self.gamma, self.lam = gamma, lam
+        self.comm = comm or Comm()
+        dev = learner.device
+        self.val = torch.zeros(T + 1, N, device=dev) if learner.vf is not None else None
+        self.adv = torch.zeros(T, N, device=dev)
+        self.ret = torch.zeros(T, N, device=dev)
+        self.adv_stats = torch.zeros(3, device=dev)
+        self.stats_part = None
+        if dev.type == "cuda":
+            from ..ops import hip
+
+            self.stats_part = torch.zeros(hip().scan_tm_parts(N), 3, device=dev)
+
+    def learn(self, obs, act, rew, done, logp, mask=None):
+        """obs [T+1, N, D]; act [T, N] int32 or [T, N, A]; rew / done / logp [T, N]."""
+        T, N = self.T, self.N
+        lr = self.learner
+        D = obs.shape[-1]
+        obs_all = obs.reshape((T + 1) * N, D)
+        obs_b = obs_all[: T * N]
+        if lr.vf is not None:
+            mlp_forward(FwdMode.VALUE, lr.vf.params, obs_all, 1, lr.hidden, out={"v": self.val.view(-1)}) \
+                if obs_all.is_cuda else self.val.view(-1).copy_(
+                    mlp_forward(FwdMode.VALUE, lr.vf.params, obs_all, 1, lr.hidden)["v"])
+        adv, ret, stats = gae_scan_tm(rew, done, self.val, self.gamma, self.lam, adv=self.adv, ret=self.ret,
+                                      stats_part=self.stats_part, stats_out=self.adv_stats)
+        if not rew.is_cuda:
+            self.adv.copy_(adv)
+            self.ret.copy_(ret)
+            self.adv_stats.copy_(stats)
+        self.comm.all_reduce_sum_(self.adv_stats)
+        inv_B = 1.0 / (T * N * self.comm.world)
+        discrete = lr.discrete
+        a = act.reshape(T * N) if discrete else None
+        ac = None if discrete else act.reshape(T * N, -1)
+        m = None if mask is None else mask.reshape(T * N, -1)
+        lr.optimize(obs_b, act=a, actc=ac, mask=m, adv=self.adv.view(-1), ret=self.ret.view(-1),
+                    adv_stats=self.adv_stats, logp_old=logp.reshape(-1), inv_B=inv_B)
+
+
+def episode_metrics(comm: Comm, n, s, sq, mx, mn, sum_len) -> dict:
+    dev = "cuda" if comm.backend == "nccl" else "cpu"
+    vec = torch.tensor([n, s, sq, sum_len], dtype=torch.float64, device=dev)
+    comm.all_reduce_sum_(vec)
+    mxt = torch.tensor([mx], dtype=torch.float64, device=dev)
+    mnt = torch.tensor([mn], dtype=torch.float64, device=dev)
+    comm.all_reduce_max_(mxt)
+    comm.all_reduce_min_(mnt)
+    n, s, sq, sl = vec.tolist()
+    if n <= 0:
+        nan = float("nan")
+        return {"AverageEpRet": nan, "StdEpRet": nan, "MaxEpRet": nan, "MinEpRet": nan, "EpLen": nan, "Episodes": 0}
+    mean = s / n
+    return {"AverageEpRet": mean, "StdEpRet": math.sqrt(max(sq / n - mean * mean, 0.0)), "MaxEpRet": mxt.item(),
+            "MinEpRet": mnt.item(), "EpLen": sl / n, "Episodes": int(n)}
