@@ -23,41 +23,55 @@ struct AdamArgs {
   float lr, beta1, beta2, eps, grad_scale, weight_decay;
 };
 
-__global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
+// Block = 64 parameters x 16 slab groups (1024 threads): the slab sum is split over
+// 16 waves (coalesced 256-B rows per wave-load) and combined through LDS, so reducing
+// ~256 slabs of a 17k-parameter net is bandwidth- not latency-bound (was 23 us).
+constexpr int kAdamCols = 64;
+constexpr int kAdamGroups = 16;
+
+__global__ __launch_bounds__(1024) void adam_kernel(AdamArgs a) {
+  __shared__ float part[kAdamGroups][kAdamCols];
   const int t = *a.step + 1;
-  const float bc1 = 1.f - __powf(a.beta1, (float)t);
-  const float bc2 = 1.f - __powf(a.beta2, (float)t);
-  const float step_size = a.lr / bc1;
-  const float rbc2 = rsqrtf(bc2);
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < a.P; p += gridDim.x * blockDim.x) {
-    float g;
+  const int col = threadIdx.x & (kAdamCols - 1);
+  const int grp = threadIdx.x / kAdamCols;
+  const int p = blockIdx.x * kAdamCols + col;
+  float g = 0.f;
+  if (p < a.P) {
     if (a.grad) {
-      g = a.grad[p];
+      if (grp == 0) g = a.grad[p];
     } else {
-      g = 0.f;
       const float* s = a.slab + p;
-      int k = 0;
-      for (; k + 4 <= a.nslab; k += 4) {
-        const float g0 = s[(size_t)(k + 0) * a.P], g1 = s[(size_t)(k + 1) * a.P];
-        const float g2 = s[(size_t)(k + 2) * a.P], g3 = s[(size_t)(k + 3) * a.P];
+      int k = grp;
+      for (; k + 3 * kAdamGroups < a.nslab; k += 4 * kAdamGroups) {
+        const float g0 = s[(size_t)k * a.P], g1 = s[(size_t)(k + kAdamGroups) * a.P];
+        const float g2 = s[(size_t)(k + 2 * kAdamGroups) * a.P], g3 = s[(size_t)(k + 3 * kAdamGroups) * a.P];
         g += (g0 + g1) + (g2 + g3);
       }
-      for (; k < a.nslab; ++k) g += s[(size_t)k * a.P];
+      for (; k < a.nslab; k += kAdamGroups) g += s[(size_t)k * a.P];
     }
-    g *= a.grad_scale;
-    if (a.grad_out) a.grad_out[p] = g;
+  }
+  part[grp][col] = g;
+  __syncthreads();
+  if (grp == 0 && p < a.P) {
+    float gs = 0.f;
+#pragma unroll
+    for (int q = 0; q < kAdamGroups; ++q) gs += part[q][col];
+    gs *= a.grad_scale;
+    if (a.grad_out) a.grad_out[p] = gs;
+    const float bc1 = 1.f - __powf(a.beta1, (float)t);
+    const float bc2 = 1.f - __powf(a.beta2, (float)t);
     float w = a.param[p];
-    if (a.weight_decay != 0.f) g += a.weight_decay * w;
-    const float m = a.beta1 * a.m[p] + (1.f - a.beta1) * g;
-    const float v = a.beta2 * a.v[p] + (1.f - a.beta2) * g * g;
+    if (a.weight_decay != 0.f) gs += a.weight_decay * w;
+    const float m = a.beta1 * a.m[p] + (1.f - a.beta1) * gs;
+    const float v = a.beta2 * a.v[p] + (1.f - a.beta2) * gs * gs;
     a.m[p] = m;
     a.v[p] = v;
     // torch.optim.Adam: p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
-    w -= step_size * m / (sqrtf(v) * rbc2 + a.eps);
+    w -= (a.lr / bc1) * m / (sqrtf(v) * rsqrtf(bc2) + a.eps);
     a.param[p] = w;
   }
-  // arrival ticket: the last block bumps the step counter
-  __syncthreads();
+  // arrival ticket: the last block bumps the step counter (every block read `step`
+  // above, before its __syncthreads / ticket)
   if (threadIdx.x == 0) {
     const unsigned prev = atomicAdd(a.ticket, 1u);
     if (prev == gridDim.x - 1) {
@@ -91,7 +105,8 @@ extern "C" int rrl_adam(float* param, float* m, float* v, const float* grad, con
                         float beta2, float eps, float grad_scale, float weight_decay, void* stream) {
   AdamArgs a{param, m, v, grad, slab, nslab, grad_out, step, ticket, P, lr, beta1, beta2, eps, grad_scale,
              weight_decay};
-  hipLaunchKernelGGL(adam_kernel, dim3(adam_grid(P)), dim3(256), 0, (hipStream_t)stream, a);
+  const int grid = (P + kAdamCols - 1) / kAdamCols;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid < 1 ? 1 : grid), dim3(kAdamCols * kAdamGroups), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

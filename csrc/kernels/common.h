@@ -124,9 +124,13 @@ RRL_DEV void stage_net(float* __restrict__ lds, const float* __restrict__ flat, 
   constexpr int H = L::H;
   const FlatOffsets o = flat_offsets(D, H, A);
   const int tid = threadIdx.x, nt = blockDim.x;
+  // W1 columns are stored in the interleaved-input order (see load_x_tile): LDS column
+  // c = 16t + 4g + r holds input feature f = 16t + 4r + g.
   for (int idx = tid; idx < H * L::S1; idx += nt) {
-    const int r = idx / L::S1, c = idx - r * L::S1;
-    lds[L::W1 + idx] = (c < D) ? flat[o.w1 + r * D + c] : 0.f;
+    const int row = idx / L::S1, c = idx - row * L::S1;
+    const int t = c >> 4, rem = c & 15;
+    const int f = 16 * t + 4 * (rem & 3) + (rem >> 2);
+    lds[L::W1 + idx] = (c < 16 * DT && f < D) ? flat[o.w1 + row * D + f] : 0.f;
   }
   // W2: float4 copies (row length H is a multiple of 16)
   for (int idx = tid; idx < H * (H / 4); idx += nt) {
@@ -148,27 +152,41 @@ RRL_DEV void stage_net(float* __restrict__ lds, const float* __restrict__ flat, 
 // out = W * in + b  (transposed-activation tiles), optional ReLU.
 //   in : NI tiles, rows = input features (16*ti + 4g + r), col = batch (lane & 15)
 //   out: NO tiles, rows = output features
-// W is row-major [NO*16][S] in LDS, b is [NO*16] in LDS.
+// W is row-major [NO*16][S] in LDS, b is [NO*16] in LDS.  The A-operand loads of input
+// tile ti+1 are issued before the MFMAs of tile ti (register double buffer), and a
+// sched_barrier per tile stops the compiler from hoisting every load (register blow-up).
+// KR_LAST < 4 skips the k-steps of the last input tile that only see zero padding
+// (interleaved input layer: feature 4r+g lives in k-step r).
 template <int NI, int NO, bool RELU>
 RRL_DEV void dense_fwd(const float* __restrict__ W, int S, const float* __restrict__ b,
-                       const floatx4 (&in)[NI], floatx4 (&out)[NO]) {
+                       const floatx4 (&in)[NI], floatx4 (&out)[NO], int kr_last = 4) {
   const int l = lane_id();
   const int i = l & 15, g = l >> 4;
 #pragma unroll
   for (int to = 0; to < NO; ++to) out[to] = *reinterpret_cast<const floatx4*>(b + 16 * to + 4 * g);
+  floatx4 wc[NO], wn[NO];
+#pragma unroll
+  for (int to = 0; to < NO; ++to) wc[to] = *reinterpret_cast<const floatx4*>(W + (16 * to + i) * S + 4 * g);
 #pragma unroll
   for (int ti = 0; ti < NI; ++ti) {
-    floatx4 w[NO];
+    if (ti + 1 < NI) {
 #pragma unroll
-    for (int to = 0; to < NO; ++to)
-      w[to] = *reinterpret_cast<const floatx4*>(W + (16 * to + i) * S + 16 * ti + 4 * g);
+      for (int to = 0; to < NO; ++to)
+        wn[to] = *reinterpret_cast<const floatx4*>(W + (16 * to + i) * S + 16 * (ti + 1) + 4 * g);
+    }
+    const int kr = (ti == NI - 1) ? kr_last : 4;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+      if (r < kr) {
 #pragma unroll
-      for (int to = 0; to < NO; ++to) out[to] = mfma4(w[to][r], in[ti][r], out[to]);
+        for (int to = 0; to < NO; ++to) out[to] = mfma4(wc[to][r], in[ti][r], out[to]);
+      }
     }
-    // keep the next input tile's weight loads from being hoisted (register blow-up)
     __builtin_amdgcn_sched_barrier(0);
+    if (ti + 1 < NI) {
+#pragma unroll
+      for (int to = 0; to < NO; ++to) wc[to] = wn[to];
+    }
   }
   if (RELU) {
 #pragma unroll
@@ -177,6 +195,12 @@ RRL_DEV void dense_fwd(const float* __restrict__ W, int S, const float* __restri
       for (int r = 0; r < 4; ++r) out[to][r] = fmaxf(out[to][r], 0.f);
     }
   }
+}
+
+// k-steps of the last interleaved input tile that carry real features.
+RRL_DEV int input_kr_last(int D, int DT) {
+  const int rem = D - 16 * (DT - 1);
+  return rem >= 16 ? 4 : (rem + 3) >> 2;
 }
 
 // dIn = W^T * dOut  (sum over output features), no bias.  Optionally masked by
@@ -188,15 +212,34 @@ RRL_DEV void dense_bwd_data(const float* __restrict__ W, int S, const floatx4 (&
   const int i = l & 15, g = l >> 4;
 #pragma unroll
   for (int ti = 0; ti < NI; ++ti) din[ti] = zero4();
+  float wc[4][NI], wn[4][NI];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int ti = 0; ti < NI; ++ti) wc[r][ti] = W[(4 * g + r) * S + i + 16 * ti];
+  }
 #pragma unroll
   for (int to = 0; to < NO; ++to) {
+    if (to + 1 < NO) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int ti = 0; ti < NI; ++ti) wn[r][ti] = W[(16 * (to + 1) + 4 * g + r) * S + i + 16 * ti];
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float* wrow = W + (16 * to + 4 * g + r) * S + i;
 #pragma unroll
-      for (int ti = 0; ti < NI; ++ti) din[ti] = mfma4(wrow[16 * ti], dout[to][r], din[ti]);
+      for (int ti = 0; ti < NI; ++ti) din[ti] = mfma4(wc[r][ti], dout[to][r], din[ti]);
     }
     __builtin_amdgcn_sched_barrier(0);
+    if (to + 1 < NO) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int ti = 0; ti < NI; ++ti) wc[r][ti] = wn[r][ti];
+      }
+    }
   }
   if (MASK) {
 #pragma unroll
@@ -224,8 +267,9 @@ RRL_DEV float head_dot(const float* __restrict__ W3row, float b, const floatx4 (
   return group_sum(acc) + b;
 }
 
-// Load a [16 batch x D] observation tile into transposed tiles: lane (j, g) reg r holds
-// feature 16*t + 4g + r of row j.  Rows >= nrows are zero.
+// Load a [16 batch x D] observation tile in the INTERLEAVED input layout: lane (j, g)
+// reg r of tile t holds feature 16t + 4r + g of row j, so features 0..3 form k-step 0
+// of the first layer's MFMA (D = 4 needs 1 k-step instead of 4).  Rows >= nrows are 0.
 template <int DT>
 RRL_DEV void load_x_tile(const float* __restrict__ X, int ldx, int D, int row0, int nrows,
                          floatx4 (&x)[DT]) {
@@ -237,7 +281,7 @@ RRL_DEV void load_x_tile(const float* __restrict__ X, int ldx, int D, int row0, 
   for (int t = 0; t < DT; ++t) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int f = 16 * t + 4 * g + r;
+      const int f = 16 * t + 4 * r + g;
       x[t][r] = (ok && f < D) ? row[f] : 0.f;
     }
   }

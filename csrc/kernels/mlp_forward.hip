@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256, 2) void mlp_forward_kernel(FwdArgs p) {
 
     floatx4 x[DT], h1[HT], h2[HT];
     load_x_tile<DT>(p.X, p.D, p.D, row0, nrows, x);
-    dense_fwd<DT, HT, true>(lds + L::W1, L::S1, lds + L::B1, x, h1);
+    dense_fwd<DT, HT, true>(lds + L::W1, L::S1, lds + L::B1, x, h1, input_kr_last(p.D, DT));
     dense_fwd<HT, HT, true>(lds + L::W2, L::S2, lds + L::B2, h1, h2);
 
     if (MODE == MODE_VALUE) {

@@ -52,21 +52,30 @@ struct GradArgs {
 
 constexpr int kStageLd = 68;  // [feature][64 batch + 4 pad]
 
-// acc[to][ti] += sum_b At[16*(to0+to)+i][b] * Bt[16*(ti0+ti)+i][b], b over the 64-row slab
+// acc[to][ti] += sum_b At[16*(to0+to)+i][b] * Bt[16*(ti0+ti)+i][b], b over the 64-row slab.
+// Operands of batch block bb+1 are loaded while block bb's MFMAs issue.
 template <int NTO, int NTI>
 RRL_DEV void wgrad(const float* __restrict__ At, const float* __restrict__ Bt, int to0, int ti0,
                    floatx4 (&acc)[NTO][NTI], float (&bacc)[NTO]) {
   const int l = lane_id();
   const int i = l & 15, g = l >> 4;
+  floatx4 a[NTO], b[NTI], an[NTO], bn[NTI];
+#pragma unroll
+  for (int to = 0; to < NTO; ++to)
+    a[to] = *reinterpret_cast<const floatx4*>(At + (16 * (to0 + to) + i) * kStageLd + 4 * g);
+#pragma unroll
+  for (int ti = 0; ti < NTI; ++ti)
+    b[ti] = *reinterpret_cast<const floatx4*>(Bt + (16 * (ti0 + ti) + i) * kStageLd + 4 * g);
 #pragma unroll
   for (int bb = 0; bb < 4; ++bb) {
-    floatx4 a[NTO], b[NTI];
+    if (bb < 3) {
 #pragma unroll
-    for (int to = 0; to < NTO; ++to)
-      a[to] = *reinterpret_cast<const floatx4*>(At + (16 * (to0 + to) + i) * kStageLd + 16 * bb + 4 * g);
+      for (int to = 0; to < NTO; ++to)
+        an[to] = *reinterpret_cast<const floatx4*>(At + (16 * (to0 + to) + i) * kStageLd + 16 * (bb + 1) + 4 * g);
 #pragma unroll
-    for (int ti = 0; ti < NTI; ++ti)
-      b[ti] = *reinterpret_cast<const floatx4*>(Bt + (16 * (ti0 + ti) + i) * kStageLd + 16 * bb + 4 * g);
+      for (int ti = 0; ti < NTI; ++ti)
+        bn[ti] = *reinterpret_cast<const floatx4*>(Bt + (16 * (ti0 + ti) + i) * kStageLd + 16 * (bb + 1) + 4 * g);
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -78,6 +87,12 @@ RRL_DEV void wgrad(const float* __restrict__ At, const float* __restrict__ Bt, i
 #pragma unroll
     for (int to = 0; to < NTO; ++to) bacc[to] += (a[to][0] + a[to][1]) + (a[to][2] + a[to][3]);
     __builtin_amdgcn_sched_barrier(0);
+    if (bb < 3) {
+#pragma unroll
+      for (int to = 0; to < NTO; ++to) a[to] = an[to];
+#pragma unroll
+      for (int ti = 0; ti < NTI; ++ti) b[ti] = bn[ti];
+    }
   }
 }
 
@@ -93,7 +108,24 @@ RRL_DEV void stage_tiles(float* __restrict__ St, int wave, const floatx4 (&v)[NT
   }
 }
 
-template <int DT, int HT, int HEAD>
+// Interleaved input tile (load_x_tile layout: reg r of group g = feature 16t + 4r + g)
+// written into the staging image in natural feature order.
+template <int NT>
+RRL_DEV void stage_x_tiles(float* __restrict__ St, int wave, const floatx4 (&v)[NT]) {
+  const int l = lane_id();
+  const int j = l & 15, g = l >> 4;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) St[(16 * t + 4 * r + g) * kStageLd + 16 * wave + j] = v[t][r];
+  }
+}
+
+// A3 > 0: the last layer has A3 (<= 2) outputs and its weight gradient is accumulated on
+// the VALU in registers (dout x h2 outer products, reduced once at the end) instead of
+// a 16-row MFMA tile that would be 1/16 (value) or 1/8 (CartPole policy) useful; this
+// also removes one staging phase and two workgroup barriers per 64-row slab.
+template <int DT, int HT, int HEAD, int A3>
 __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   using L = LdsNet<DT, HT>;
@@ -139,6 +171,16 @@ __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
 #pragma unroll
   for (int a = 0; a < kMaxAct; ++a) dls_acc[a] = 0.f;
   float s_loss = 0.f, s_ent = 0.f, s_kl = 0.f, s_clip = 0.f, s_val = 0.f, s_cnt = 0.f;
+  constexpr int A3N = A3 > 0 ? A3 : 1;
+  floatx4 acc3v[A3N][HT];  // VALU dW3 partials (A3 > 0)
+  float bacc3v[A3N];
+#pragma unroll
+  for (int a = 0; a < A3N; ++a) {
+    bacc3v[a] = 0.f;
+#pragma unroll
+    for (int t = 0; t < HT; ++t) acc3v[a][t] = zero4();
+  }
+  const int kr1 = input_kr_last(p.D, DT);
 
   __syncthreads();
 
@@ -150,7 +192,7 @@ __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
 
     floatx4 x[DT], h1[HT], h2[HT];
     load_x_tile<DT>(p.X, p.D, p.D, row0, nrows, x);
-    dense_fwd<DT, HT, true>(lds + L::W1, L::S1, lds + L::B1, x, h1);
+    dense_fwd<DT, HT, true>(lds + L::W1, L::S1, lds + L::B1, x, h1, kr1);
     dense_fwd<HT, HT, true>(lds + L::W2, L::S2, lds + L::B2, h1, h2);
 
     // ------------------------------------------------------------ head + dLoss/dout
@@ -283,13 +325,25 @@ __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
     }
 
     // ------------------------------------------------------------ phase A: dW3, db3
-    __syncthreads();  // previous slab's phase-C readers are done with st0/st1
-    stage_tiles<HT>(st0, wave, h2);
+    if (A3 > 0) {
 #pragma unroll
-    for (int a = 0; a < kMaxAct; ++a)
-      if ((a >> 2) == g) st1[a * kStageLd + 16 * wave + j] = (a < A) ? dout[a] : 0.f;
-    __syncthreads();
-    wgrad<1, TI3>(st1, st0, 0, wave * TI3, acc3, bacc3);
+      for (int a = 0; a < A3N; ++a) {
+        bacc3v[a] += dout[a];
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc3v[a][t][r] = fmaf(dout[a], h2[t][r], acc3v[a][t][r]);
+        }
+      }
+    } else {
+      __syncthreads();  // previous slab's phase-C readers are done with st0/st1
+      stage_tiles<HT>(st0, wave, h2);
+#pragma unroll
+      for (int a = 0; a < kMaxAct; ++a)
+        if ((a >> 2) == g) st1[a * kStageLd + 16 * wave + j] = (a < A) ? dout[a] : 0.f;
+      __syncthreads();
+      wgrad<1, TI3>(st1, st0, 0, wave * TI3, acc3, bacc3);
+    }
 
     // ------------------------------------------------------------ phase B: dW2, db2
     __syncthreads();
@@ -303,7 +357,7 @@ __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
 
     // ------------------------------------------------------------ phase C: dW1, db1
     __syncthreads();
-    stage_tiles<DT>(st0, wave, x);
+    stage_x_tiles<DT>(st0, wave, x);
     stage_tiles<HT>(st1, wave, dh1);
     __syncthreads();
     wgrad<TO, DT>(st1, st0, wave * TO, 0, acc1, bacc1);
@@ -336,16 +390,45 @@ __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
     if (g == 0) slab[o.b1 + 16 * ot + j] = b1;
   }
   // dW3 / db3
+  if (A3 > 0) {
+    // reduce the per-lane partials over the 16 batch columns, then over the 4 waves
+    __syncthreads();
+    float* red3 = st1;  // [4 waves][A3 * H + A3]
 #pragma unroll
-  for (int ti = 0; ti < TI3; ++ti) {
+    for (int a = 0; a < A3N; ++a) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int a = 4 * g + r;
-      if (a < A) slab[o.w3 + a * H + 16 * (wave * TI3 + ti) + j] = acc3[0][ti][r];
+      for (int t = 0; t < HT; ++t) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = col_sum(acc3v[a][t][r]);
+          if (j == 0) red3[wave * (A3N * H + A3N) + a * H + 16 * t + 4 * g + r] = v;
+        }
+      }
+      const float bv = col_sum(bacc3v[a]);
+      if (l == 0) red3[wave * (A3N * H + A3N) + A3N * H + a] = bv;
     }
+    __syncthreads();
+    for (int q = threadIdx.x; q < A3N * H + A3N; q += blockDim.x) {
+      const int stride = A3N * H + A3N;
+      const float v = red3[q] + red3[stride + q] + red3[2 * stride + q] + red3[3 * stride + q];
+      if (q < A3N * H) {
+        if (q / H < A) slab[o.w3 + q] = v;
+      } else if (q - A3N * H < A) {
+        slab[o.b3 + (q - A3N * H)] = v;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int ti = 0; ti < TI3; ++ti) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int a = 4 * g + r;
+        if (a < A) slab[o.w3 + a * H + 16 * (wave * TI3 + ti) + j] = acc3[0][ti][r];
+      }
+    }
+    const float b3 = group_sum(bacc3[0]);
+    if (wave == 0 && g == 0 && j < A) slab[o.b3 + j] = b3;
   }
-  const float b3 = group_sum(bacc3[0]);
-  if (wave == 0 && g == 0 && j < A) slab[o.b3 + j] = b3;
 
   // Gaussian log_std grads and loss statistics: reduce over the workgroup via LDS
   __syncthreads();
@@ -376,7 +459,7 @@ __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
 
 using namespace rrl;
 
-template <int DT, int HT, int HEAD>
+template <int DT, int HT, int HEAD, int A3>
 static int launch_grad(const GradArgs& a, int grid, hipStream_t s) {
   using L = LdsNet<DT, HT>;
   const int A = (HEAD == HEAD_VALUE_MSE) ? 1 : a.A;
@@ -385,21 +468,28 @@ static int launch_grad(const GradArgs& a, int grid, hipStream_t s) {
   if (bytes > 163840) return -4;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)mlp_grad_kernel<DT, HT, HEAD>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    hipFuncSetAttribute((const void*)mlp_grad_kernel<DT, HT, HEAD, A3>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
     attr_set = true;
   }
-  hipLaunchKernelGGL((mlp_grad_kernel<DT, HT, HEAD>), dim3(grid), dim3(256), bytes, s, a);
+  hipLaunchKernelGGL((mlp_grad_kernel<DT, HT, HEAD, A3>), dim3(grid), dim3(256), bytes, s, a);
   return (int)hipGetLastError();
+}
+
+template <int DT, int HT, int HEAD>
+static int dispatch_a3(const GradArgs& a, int grid, hipStream_t s) {
+  if (HEAD == HEAD_VALUE_MSE || a.A == 1) return launch_grad<DT, HT, HEAD, 1>(a, grid, s);
+  if (a.A == 2) return launch_grad<DT, HT, HEAD, 2>(a, grid, s);
+  return launch_grad<DT, HT, HEAD, 0>(a, grid, s);
 }
 
 template <int DT, int HT>
 static int dispatch_head(int head, const GradArgs& a, int grid, hipStream_t s) {
   switch (head) {
-    case HEAD_PG_CAT: return launch_grad<DT, HT, HEAD_PG_CAT>(a, grid, s);
-    case HEAD_VALUE_MSE: return launch_grad<DT, HT, HEAD_VALUE_MSE>(a, grid, s);
-    case HEAD_PPO_CAT: return launch_grad<DT, HT, HEAD_PPO_CAT>(a, grid, s);
-    case HEAD_PPO_GAUSS: return launch_grad<DT, HT, HEAD_PPO_GAUSS>(a, grid, s);
-    case HEAD_PG_GAUSS: return launch_grad<DT, HT, HEAD_PG_GAUSS>(a, grid, s);
+    case HEAD_PG_CAT: return dispatch_a3<DT, HT, HEAD_PG_CAT>(a, grid, s);
+    case HEAD_VALUE_MSE: return launch_grad<DT, HT, HEAD_VALUE_MSE, 1>(a, grid, s);
+    case HEAD_PPO_CAT: return dispatch_a3<DT, HT, HEAD_PPO_CAT>(a, grid, s);
+    case HEAD_PPO_GAUSS: return dispatch_a3<DT, HT, HEAD_PPO_GAUSS>(a, grid, s);
+    case HEAD_PG_GAUSS: return dispatch_a3<DT, HT, HEAD_PG_GAUSS>(a, grid, s);
   }
   return -1;
 }

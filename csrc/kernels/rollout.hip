@@ -76,21 +76,22 @@ __global__ __launch_bounds__(256, 2) void rollout_kernel(RolloutArgs p) {
     for (int t = 0; t < p.T; ++t) {
       const uint64_t gstep = step0 + (uint64_t)t;
       const size_t base = (size_t)t * p.N + env;
-      // observation tile (feature f of env j lives in lane group f>>2, reg f&3)
+      // observation tile, interleaved layout: feature f of env j lives in lane group
+      // f&3, register f>>2 (so the 4 CartPole features are ONE MFMA k-step)
       floatx4 x[1];
       x[0] = zero4();
 #pragma unroll
       for (int f = 0; f < D; ++f) {
         const float o = Env::obs(s, f);
-        if ((f >> 2) == g) x[0][f & 3] = o;
+        if ((f & 3) == g) x[0][f >> 2] = o;
       }
       if (valid) {
 #pragma unroll
         for (int f = 0; f < D; ++f)
-          if ((f >> 2) == g) p.obs_buf[base * D + f] = x[0][f & 3];
+          if ((f & 3) == g) p.obs_buf[base * D + f] = x[0][f >> 2];
       }
       floatx4 h1[HT], h2[HT];
-      dense_fwd<DT, HT, true>(lds + L::W1, L::S1, lds + L::B1, x, h1);
+      dense_fwd<DT, HT, true>(lds + L::W1, L::S1, lds + L::B1, x, h1, (D + 3) >> 2);
       dense_fwd<HT, HT, true>(lds + L::W2, L::S2, lds + L::B2, h1, h2);
       float logits[kMaxAct];
       policy_logits<HT>(lds + L::W3, lds + L::B3, A, H, h2, logits);
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(256, 2) void rollout_kernel(RolloutArgs p) {
       const size_t base = (size_t)p.T * p.N + env;
 #pragma unroll
       for (int f = 0; f < D; ++f)
-        if ((f >> 2) == g) p.obs_buf[base * D + f] = Env::obs(s, f);
+        if ((f & 3) == g) p.obs_buf[base * D + f] = Env::obs(s, f);
       if (g == 0) {
 #pragma unroll
         for (int k = 0; k < NS; ++k) p.state[(size_t)env * NS + k] = s[k];
