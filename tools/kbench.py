@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmarks (timed with HIP events, interleaved rounds in one process).
+
+  python tools/kbench.py grad --B 2097152 --iters 20      # fused value fwd+bwd kernel
+  python tools/kbench.py all                               # every hot kernel
+
+Usable under rocprofv3 (--kernel-trace / --pmc) to attribute counters to one kernel.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+from relayrl_prototype_amd.ops import FwdMode, GradHead, MLPSpec, hip, mlp_forward, mlp_grad, adam_step, gae_scan_tm
+
+
+def timeit(fn, iters, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("which", choices=["grad", "pgrad", "fwd", "rollout", "adam", "scan", "all"])
+    ap.add_argument("--B", type=int, default=2097152)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--H", type=int, default=128)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    B, H, D = a.B, a.H, 4
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(B, D, generator=g).to(dev)
+    ret = torch.randn(B, generator=g).to(dev)
+    adv = torch.randn(B, generator=g).to(dev)
+    act = torch.randint(0, 2, (B,), generator=g, dtype=torch.int32).to(dev)
+    pv = MLPSpec(D, H, 1).init(g).to(dev)
+    pp = MLPSpec(D, H, 2).init(g).to(dev)
+    res = {}
+    flop_row = 2 * (D * H + H * H + H) * 3  # fwd + bwd-data + wgrad (nominal)
+    if a.which in ("grad", "all"):
+        ns = hip().mlp_grad_slabs(B)
+        slab = torch.empty(ns, pv.numel(), device=dev)
+        ls = torch.empty(ns, 8, device=dev)
+        us = timeit(lambda: mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret, grad_slab=slab, loss_slab=ls), a.iters)
+        res["value_grad_us"] = us
+        res["value_grad_TFLOPs_nominal"] = flop_row * B / us / 1e6
+    if a.which in ("pgrad", "all"):
+        ns = hip().mlp_grad_slabs(B)
+        slab = torch.empty(ns, pp.numel(), device=dev)
+        ls = torch.empty(ns, 8, device=dev)
+        st = torch.tensor([0.0, float(B), float(B)], device=dev)
+        us = timeit(lambda: mlp_grad(GradHead.PG_CAT, pp, X, 2, H, act=act, adv=adv, adv_stats=st, grad_slab=slab,
+                                     loss_slab=ls), a.iters)
+        res["policy_grad_us"] = us
+    if a.which in ("fwd", "all"):
+        out = {"v": torch.empty(B, device=dev)}
+        us = timeit(lambda: mlp_forward(FwdMode.VALUE, pv, X, 1, H, out=out), a.iters)
+        res["value_fwd_us"] = us
+        res["value_fwd_TFLOPs"] = 2 * (D * H + H * H + H) * B / us / 1e6
+    if a.which in ("adam", "all"):
+        ns = hip().mlp_grad_slabs(B)
+        slab = torch.randn(ns, pv.numel(), device=dev) * 1e-3
+        m = torch.zeros_like(pv)
+        v = torch.zeros_like(pv)
+        step = torch.zeros(1, dtype=torch.int32, device=dev)
+        tk = torch.zeros(1, dtype=torch.int32, device=dev)
+        p2 = pv.clone()
+        res["adam_us"] = timeit(lambda: adam_step(p2, m, v, step, tk, 1e-3, slab=slab), a.iters)
+    if a.which in ("scan", "all"):
+        T, N = 64, B // 64
+        rew = torch.rand(T, N, device=dev)
+        done = (torch.rand(T, N, device=dev) < 0.05).float()
+        val = torch.rand(T + 1, N, device=dev)
+        advb = torch.empty(T, N, device=dev)
+        retb = torch.empty(T, N, device=dev)
+        res["scan_us"] = timeit(lambda: gae_scan_tm(rew, done, val, 0.99, 0.95, adv=advb, ret=retb), a.iters)
+    if a.which in ("rollout", "all"):
+        h = hip()
+        T, N = 64, B // 64
+        st = torch.zeros(N, 4, device=dev)
+        el = torch.zeros(N, dtype=torch.int32, device=dev)
+        er = torch.zeros(N, device=dev)
+        obs = torch.empty(T + 1, N, 4, device=dev)
+        ac = torch.empty(T, N, dtype=torch.int32, device=dev)
+        lp = torch.empty(T, N, device=dev)
+        rw = torch.empty(T, N, device=dev)
+        dn = torch.empty(T, N, device=dev)
+        es = torch.empty(h.rollout_grid(N), 8, device=dev)
+        us = timeit(lambda: h.rollout(0, pp, H, st, el, er, obs, ac, lp, rw, dn, es, 1, 0, False, 500), a.iters)
+        res["rollout_us"] = us
+        res["rollout_Msteps_per_s"] = T * N / us
+    print(json.dumps({k: round(v, 3) for k, v in res.items()}))
+
+
+if __name__ == "__main__":
+    main()
