@@ -108,3 +108,40 @@ def test_dp_host_trainer_ranks_stay_in_sync():
     for rank, ok, steps in res:
         assert ok is True, (rank, ok)
         assert steps == 2 * 16 * 16 * 2
+
+
+def _worker_actor_learner(rank, world, port, q, lag=0):
+    try:
+        comm = _init(rank, world, port)
+        from relayrl_prototype_amd.runtime.actor_learner import ActorLearner, ActorLearnerConfig
+
+        cfg = ActorLearnerConfig(env="CartPole-v1", num_envs=8, rollout_len=16, algo="reinforce", hidden=64,
+                                 train_vf_iters=2, num_threads=1, seed=5, max_lag=lag)
+        al = ActorLearner(cfg, comm, device="cpu")
+        for _ in range(3):
+            al.step()
+        al.finish()
+        m = al.metrics()
+        w = al.wbuf.clone()
+        gathered = [torch.zeros_like(w) for _ in range(world)]
+        dist.all_gather(gathered, w)
+        same = all(torch.equal(gathered[0], x) for x in gathered)
+        q.put((rank, same, m.get("EnvSteps"), m.get("ActorSeqs")))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+
+        q.put((rank, traceback.format_exc(), None, None))
+
+
+def _worker_actor_learner_lag(rank, world, port, q):
+    _worker_actor_learner(rank, world, port, q, lag=1)
+
+
+@pytest.mark.parametrize("fn", [_worker_actor_learner, _worker_actor_learner_lag])
+def test_actor_learner_gloo(fn):
+    res = _run(fn, world=3)
+    for rank, same, steps, seqs in res:
+        assert same is True, (rank, same)
+    assert res[0][2] == 3 * 16 * 8 * 2  # two actors x 3 rollouts
+    assert res[0][3] == [3.0, 3.0]       # per-actor heartbeat sequence numbers
