@@ -28,6 +28,7 @@ from .. import _native
 from ..algorithms.learner import PGLearner
 from ..ops import FwdMode, mlp_forward
 from ..parallel.comm import Comm
+from ..utils.tracing import PhaseTimer
 from .rollout_learn import RolloutLearner, episode_metrics
 
 
@@ -53,6 +54,7 @@ class HostTrainerConfig:
     pipeline: bool = True
     use_graphs: bool = True
     log_std_init: float = -0.5
+    phase_timing: bool = False
 
     def to_dict(self):
         return asdict(self)
@@ -80,7 +82,8 @@ class HostVecTrainer:
                                  cfg.pi_lr, cfg.vf_lr, cfg.train_vf_iters, cfg.train_pi_iters, cfg.clip_ratio,
                                  cfg.target_kl, cfg.ent_coef, self.device, cfg.seed, self.comm, cfg.use_graphs,
                                  cfg.log_std_init)
-        self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.comm)
+        self.timer = PhaseTimer(self.device, enabled=cfg.phase_timing)
+        self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.comm, self.timer)
         pin = cuda
         D, A = self.D, self.A
         # pinned host staging (env side) and HBM rollout buffers (learner side)
@@ -168,7 +171,8 @@ class HostVecTrainer:
         self.timings["rollout_s"] += time.perf_counter() - t0
 
     def train_epoch(self):
-        self.rollout()
+        with self.timer.phase("Rollout"):
+            self.rollout()
         t0 = time.perf_counter()
         self.rl.learn(self.d_obs, self.d_act, self.d_rew, self.d_done, self.d_logp)
         # next rollout starts from the last observation
@@ -192,4 +196,9 @@ class HostVecTrainer:
         out.update(self.learner.summarize())
         out["EnvSteps"] = self.env_steps * self.comm.world
         out["WorldSize"] = self.comm.world
+        out["RolloutS"] = self.timings["rollout_s"]
+        out["LearnS"] = self.timings["learn_s"]
+        if self.timer.enabled:
+            out.update(self.timer.columns())
+            self.timer.reset()
         return out

@@ -9,13 +9,16 @@ import torch
 from ..algorithms.learner import PGLearner
 from ..ops import FwdMode, gae_scan_tm, mlp_forward
 from ..parallel.comm import Comm
+from ..utils.tracing import PhaseTimer
 
 
 class RolloutLearner:
     """Owns the HBM-resident scan buffers and drives a PGLearner on time-major rollouts."""
 
-    def __init__(self, learner: PGLearner, T: int, N: int, gamma: float, lam: float, comm: Optional[Comm] = None):
+    def __init__(self, learner: PGLearner, T: int, N: int, gamma: float, lam: float, comm: Optional[Comm] = None,
+                 timer: Optional[PhaseTimer] = None):
         self.learner = learner
+        self.timer = timer or PhaseTimer(learner.device, enabled=False)
         self.T, self.N = T, N
         self.gamma, self.lam = gamma, lam
         self.comm = comm or Comm()
@@ -37,24 +40,29 @@ class RolloutLearner:
         D = obs.shape[-1]
         obs_all = obs.reshape((T + 1) * N, D)
         obs_b = obs_all[: T * N]
-        if lr.vf is not None:
-            mlp_forward(FwdMode.VALUE, lr.vf.params, obs_all, 1, lr.hidden, out={"v": self.val.view(-1)}) \
-                if obs_all.is_cuda else self.val.view(-1).copy_(
-                    mlp_forward(FwdMode.VALUE, lr.vf.params, obs_all, 1, lr.hidden)["v"])
-        adv, ret, stats = gae_scan_tm(rew, done, self.val, self.gamma, self.lam, adv=self.adv, ret=self.ret,
-                                      stats_part=self.stats_part, stats_out=self.adv_stats)
-        if not rew.is_cuda:
-            self.adv.copy_(adv)
-            self.ret.copy_(ret)
-            self.adv_stats.copy_(stats)
-        self.comm.all_reduce_sum_(self.adv_stats)
+        tm = self.timer
+        with tm.phase("ValueFwd"):
+            if lr.vf is not None:
+                if obs_all.is_cuda:
+                    mlp_forward(FwdMode.VALUE, lr.vf.params, obs_all, 1, lr.hidden, out={"v": self.val.view(-1)})
+                else:
+                    self.val.view(-1).copy_(mlp_forward(FwdMode.VALUE, lr.vf.params, obs_all, 1, lr.hidden)["v"])
+        with tm.phase("Scan"):
+            adv, ret, stats = gae_scan_tm(rew, done, self.val, self.gamma, self.lam, adv=self.adv, ret=self.ret,
+                                          stats_part=self.stats_part, stats_out=self.adv_stats)
+            if not rew.is_cuda:
+                self.adv.copy_(adv)
+                self.ret.copy_(ret)
+                self.adv_stats.copy_(stats)
+            self.comm.all_reduce_sum_(self.adv_stats)
         inv_B = 1.0 / (T * N * self.comm.world)
         discrete = lr.discrete
         a = act.reshape(T * N) if discrete else None
         ac = None if discrete else act.reshape(T * N, -1)
         m = None if mask is None else mask.reshape(T * N, -1)
-        lr.optimize(obs_b, act=a, actc=ac, mask=m, adv=self.adv.view(-1), ret=self.ret.view(-1),
-                    adv_stats=self.adv_stats, logp_old=logp.reshape(-1), inv_B=inv_B)
+        with tm.phase("Optimize"):
+            lr.optimize(obs_b, act=a, actc=ac, mask=m, adv=self.adv.view(-1), ret=self.ret.view(-1),
+                        adv_stats=self.adv_stats, logp_old=logp.reshape(-1), inv_B=inv_B)
 
 
 def episode_metrics(comm: Comm, n, s, sq, mx, mn, sum_len) -> dict:

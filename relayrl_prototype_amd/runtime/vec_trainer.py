@@ -26,6 +26,7 @@ import torch
 from ..algorithms.learner import PGLearner
 from ..ops import hip
 from ..parallel.comm import Comm
+from ..utils.tracing import PhaseTimer
 from .rollout_learn import RolloutLearner, episode_metrics
 
 DEVICE_ENVS = {"CartPole-v1": 0, "MountainCar-v0": 1, "Acrobot-v1": 2}
@@ -51,6 +52,7 @@ class VecTrainerConfig:
     use_graphs: bool = True
     ent_coef: float = 0.0
     max_episode_steps: Optional[int] = None
+    phase_timing: bool = False     # per-phase HIP-event timing + roctx ranges
 
     def to_dict(self):
         return asdict(self)
@@ -79,7 +81,8 @@ class VecTrainer:
                                  cfg.train_pi_iters, cfg.clip_ratio, cfg.target_kl, cfg.ent_coef, dev, cfg.seed,
                                  self.comm, cfg.use_graphs)
         self.pi, self.vf = self.learner.pi, self.learner.vf
-        self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.comm)
+        self.timer = PhaseTimer(dev, enabled=cfg.phase_timing)
+        self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.comm, self.timer)
         self.env_seed = (cfg.seed * 0x9E3779B97F4A7C15 + rank * 0x632BE59BD9B4E019) & 0x7FFFFFFFFFFFFFFF
         # time-major SoA rollout buffers (HBM resident)
         self.obs = torch.zeros(T + 1, N, D, device=dev)
@@ -106,7 +109,8 @@ class VecTrainer:
         self._first = False
 
     def train_epoch(self):
-        self.rollout()
+        with self.timer.phase("Rollout"):
+            self.rollout()
         self.rl.learn(self.obs, self.act, self.rew, self.done, self.logp)
         self.epoch += 1
         self.env_steps += self.B
@@ -122,6 +126,9 @@ class VecTrainer:
         out.update(self.learner.summarize())
         out["EnvSteps"] = self.env_steps * self.comm.world
         out["WorldSize"] = self.comm.world
+        if self.timer.enabled:
+            out.update(self.timer.columns())
+            self.timer.reset()
         return out
 
     def state_dict(self) -> dict:

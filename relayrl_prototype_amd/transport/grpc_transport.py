@@ -241,6 +241,11 @@ class GrpcAgentTransport:
         self.on_model(blob)
 
     def send_trajectory_pb(self, traj: RelayRLTrajectory) -> bool:
+        from ..utils.faults import injector
+
+        inj = injector()
+        if inj.enabled and inj.filter_upload(b"x" * 32) is None:
+            return True  # injected loss
         try:
             r = self._send(trajectory_to_pb(traj), timeout=30)
             return r.code == 1

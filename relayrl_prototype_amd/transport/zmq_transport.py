@@ -43,6 +43,7 @@ class ZmqTrainingEndpoint:
         self.listener_port = self.router.bind(agent_listener)
         self.traj_port = self.pull.bind(trajectory_server)
         self.agents = {}  # identity -> wants format
+        self.bad_frames = 0
         self._lock = threading.Lock()
         self._stop = threading.Event()
         self._threads = [threading.Thread(target=self._listen_agents, daemon=True, name="rrl-zmq-listener"),
@@ -102,6 +103,7 @@ class ZmqTrainingEndpoint:
                 try:
                     traj = RelayRLTrajectory.decode(f)
                 except Exception as e:
+                    self.bad_frames += 1
                     self._log("bad trajectory frame", e)
                     continue
                 self.service.submit(traj)
@@ -189,6 +191,11 @@ class ZmqAgentTransport:
         raise TimeoutError("ZMQ handshake with the training server timed out")
 
     def send_trajectory(self, payload: bytes) -> bool:
+        from ..utils.faults import injector
+
+        payload = injector().filter_upload(payload)
+        if payload is None:
+            return True  # injected loss: the learner detects the sequence gap
         return self.push.send([payload], 10000)
 
     def heartbeat(self):

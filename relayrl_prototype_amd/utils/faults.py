@@ -1,0 +1,76 @@
+"""Fault injection for transport / runtime robustness tests.
+
+Configured by the ``RRL_FAULTS`` environment variable (or ``FaultInjector.configure``):
+
+    RRL_FAULTS="drop=0.1,corrupt=0.05,delay_ms=20,seed=3"
+
+* ``drop``     -- probability that an outgoing trajectory upload is silently dropped
+                  (the learner sees the per-agent sequence gap: LearnerService.dropped_seq);
+* ``corrupt``  -- probability that an upload has bytes flipped (the server must reject
+                  the frame and keep serving);
+* ``delay_ms`` -- fixed delay added before each upload (slow agent).
+
+Off by default; every hook is a no-op unless configured.
+"""
+from __future__ import annotations
+
+import os
+import random
+import threading
+import time
+from typing import Dict, Optional
+
+
+class FaultInjector:
+    def __init__(self, spec: Optional[str] = None):
+        self._lock = threading.Lock()
+        self.configure(spec if spec is not None else os.environ.get("RRL_FAULTS", ""))
+
+    def configure(self, spec: str):
+        cfg: Dict[str, float] = {}
+        for part in (spec or "").split(","):
+            if "=" in part:
+                k, v = part.split("=", 1)
+                cfg[k.strip()] = float(v)
+        self.drop = cfg.get("drop", 0.0)
+        self.corrupt = cfg.get("corrupt", 0.0)
+        self.delay_ms = cfg.get("delay_ms", 0.0)
+        self.rng = random.Random(int(cfg.get("seed", 0)))
+        self.enabled = bool(self.drop or self.corrupt or self.delay_ms)
+        self.stats = {"dropped": 0, "corrupted": 0, "delayed": 0}
+
+    def filter_upload(self, payload: bytes) -> Optional[bytes]:
+        """Returns the (possibly corrupted) payload, or None to drop it."""
+        if not self.enabled:
+            return payload
+        with self._lock:
+            if self.delay_ms:
+                self.stats["delayed"] += 1
+                time.sleep(self.delay_ms / 1000.0)
+            if self.drop and self.rng.random() < self.drop:
+                self.stats["dropped"] += 1
+                return None
+            if self.corrupt and self.rng.random() < self.corrupt and len(payload) > 16:
+                self.stats["corrupted"] += 1
+                b = bytearray(payload)
+                for _ in range(4):
+                    b[self.rng.randrange(len(b))] ^= 0xFF
+                b[0] ^= 0xFF  # always break the magic so decoding must reject it
+                return bytes(b)
+        return payload
+
+
+_GLOBAL: Optional[FaultInjector] = None
+
+
+def injector() -> FaultInjector:
+    global _GLOBAL
+    if _GLOBAL is None:
+        _GLOBAL = FaultInjector()
+    return _GLOBAL
+
+
+def reset(spec: str = "") -> FaultInjector:
+    global _GLOBAL
+    _GLOBAL = FaultInjector(spec)
+    return _GLOBAL

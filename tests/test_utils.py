@@ -111,3 +111,71 @@ def test_trajectory_algorithms_cpu(tmp_path, monkeypatch, algo, discrete):
     assert np.isfinite(m["LossPi"]) and np.isfinite(m["LossV"])
     alg.save(str(tmp_path / "m.pt"))
     assert os.path.getsize(tmp_path / "m.pt") > 1000
+
+
+def test_phase_timer_and_roctx():
+    from relayrl_prototype_amd.utils.tracing import PhaseTimer, roctx_available, roctx_range
+
+    t = PhaseTimer(None)
+    with t.phase("A"):
+        with roctx_range("inner"):
+            sum(range(1000))
+    cols = t.columns()
+    assert "AWallMs" in cols and cols["AWallMs"] >= 0
+    assert isinstance(roctx_available(), bool)
+
+
+def test_fault_injection_drop_and_corrupt(tmp_path, monkeypatch):
+    """Corrupted uploads are rejected by the server, dropped ones show up as sequence gaps."""
+    import time
+
+    from relayrl_prototype_amd import _native
+    from relayrl_prototype_amd.runtime.learner_service import LearnerService
+    from relayrl_prototype_amd.transport.zmq_transport import ZmqTrainingEndpoint
+    from relayrl_prototype_amd.types import RelayRLAction, RelayRLTrajectory
+    from relayrl_prototype_amd.utils import faults
+
+    class Alg:
+        def __init__(self):
+            self.got = []
+
+        def get_weights(self):
+            return {"pi": torch.zeros(3), "vf": None, "version": 0, "obs_dim": 1, "act_dim": 1, "hidden": 1,
+                    "discrete": True}
+
+        def model_bytes(self):
+            return b""
+
+        def receive_trajectory(self, t):
+            self.got.append(t.seq)
+            return False
+
+    svc = LearnerService(Alg())
+    svc.start()
+    ep = ZmqTrainingEndpoint(svc, "tcp://127.0.0.1:0", "tcp://127.0.0.1:0")
+    push = _native.ZmtpSocket(_native.SockType.PUSH)
+    push.connect(f"tcp://127.0.0.1:{ep.traj_port}")
+    inj = faults.reset("corrupt=1.0,seed=1")
+    t = RelayRLTrajectory(10, None, agent_id="a")
+    t.add_action(RelayRLAction(obs=np.zeros(2), rew=1.0, done=True))
+    push.send([inj.filter_upload(t.encode())], 2000)
+    inj = faults.reset("drop=1.0")
+    t.seq = 1
+    assert inj.filter_upload(t.encode()) is None
+    faults.reset("")
+    t.seq = 2
+    push.send([t.encode()], 2000)
+    t0 = time.time()
+    while svc.received < 1 and time.time() - t0 < 10:
+        time.sleep(0.01)
+    assert ep.bad_frames == 1
+    assert svc.algorithm.got == [2]
+    t.seq = 5
+    push.send([t.encode()], 2000)
+    t0 = time.time()
+    while svc.received < 2 and time.time() - t0 < 10:
+        time.sleep(0.01)
+    assert svc.dropped_seq == 2  # seq 3 and 4 never arrived
+    push.close()
+    ep.close()
+    svc.stop()
