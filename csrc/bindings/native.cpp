@@ -1,9 +1,12 @@
-// pybind11 bindings of the C++ host runtime (csrc/host): codec, ZMTP transport, VecEnv.
+// pybind11 bindings of the C++ host runtime (csrc/host): codec, ZMTP transport, VecEnv,
+// NativePolicy (agent-side CPU inference).
 // Replaces the reference's PyO3 layer for the host-side types (rf/src/bindings/python/*).
 #include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 
 #include "codec.h"
+#include "policy.h"
 #include "vecenv.h"
 #include "zmtp.h"
 
@@ -216,5 +219,59 @@ PYBIND11_MODULE(_native, m) {
         d["min"] = s.n > 0 ? s.min : 0.0;
         d["sum_len"] = s.sum_len;
         return d;
+      });
+
+  using farr = py::array_t<float, py::array::c_style | py::array::forcecast>;
+  py::class_<rrl::NativePolicy>(m, "NativePolicy")
+      .def(py::init<int, int, int, bool, uint64_t>(), py::arg("obs_dim"), py::arg("hidden"), py::arg("act_dim"),
+           py::arg("discrete"), py::arg("seed") = 0)
+      .def("load", [](rrl::NativePolicy& p, farr pi, py::object vf) {
+        if (vf.is_none()) {
+          p.load(pi.data(), pi.size(), nullptr, 0);
+        } else {
+          farr v = vf.cast<farr>();
+          p.load(pi.data(), pi.size(), v.data(), v.size());
+        }
+      }, py::arg("pi"), py::arg("vf") = py::none())
+      .def_property_readonly("has_value", &rrl::NativePolicy::has_value)
+      // -> (act [N] int32 | [N, A] float32, logp [N], v [N] | None)
+      .def("step", [](rrl::NativePolicy& p, farr obs, py::object mask) -> py::tuple {
+        if (obs.size() % p.D != 0) throw std::invalid_argument("obs size is not a multiple of obs_dim");
+        const int N = static_cast<int>(obs.size() / p.D);
+        farr m;
+        const float* mp = nullptr;
+        if (!mask.is_none()) {
+          m = mask.cast<farr>();
+          if (m.size() != static_cast<py::ssize_t>(N) * p.A) throw std::invalid_argument("mask size != N*act_dim");
+          mp = m.data();
+        }
+        py::array_t<float> logp(N);
+        py::object v = py::none();
+        float* vp = nullptr;
+        if (p.has_value()) {
+          py::array_t<float> va(N);
+          vp = va.mutable_data();
+          v = va;
+        }
+        if (p.discrete) {
+          py::array_t<int32_t> act(N);
+          p.step(obs.data(), mp, N, act.mutable_data(), nullptr, logp.mutable_data(), vp);
+          return py::make_tuple(act, logp, v);
+        }
+        py::array_t<float> act({N, p.A});
+        p.step(obs.data(), mp, N, nullptr, act.mutable_data(), logp.mutable_data(), vp);
+        return py::make_tuple(act, logp, v);
+      }, py::arg("obs"), py::arg("mask") = py::none())
+      .def("logits", [](const rrl::NativePolicy& p, farr obs) {
+        const int N = static_cast<int>(obs.size() / p.D);
+        py::array_t<float> out({N, p.A});
+        p.logits(obs.data(), N, out.mutable_data());
+        return out;
+      })
+      .def("value", [](const rrl::NativePolicy& p, farr obs) {
+        const int N = static_cast<int>(obs.size() / p.D);
+        py::array_t<float> out(N);
+        p.value(obs.data(), N, out.mutable_data());
+        return out;
       });
 }

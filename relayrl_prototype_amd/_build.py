@@ -131,7 +131,7 @@ def build_native(verbose=False, force=False) -> str:
         o = os.path.join(odir, os.path.basename(s) + ".o")
         objs.append(o)
         if force or _newer(o, [s] + headers):
-            cmd = [CXX, "-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-pthread", "-I", hdir]
+            cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-pthread", "-I", hdir]
             for i in _py_includes():
                 cmd += ["-I", i]
             cmd += ["-c", s, "-o", o]

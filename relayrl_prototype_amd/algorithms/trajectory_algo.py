@@ -21,6 +21,7 @@ from ..ops import FwdMode, mlp_forward, scan_flat
 from ..utils.logger import EpochLogger, setup_logger_kwargs
 from .base import AlgorithmAbstract
 from .learner import PGLearner
+from ..types import TrajectoryColumns
 
 
 class FlatBuffer:
@@ -60,6 +61,27 @@ class FlatBuffer:
             self.has_logp[i] = False
         self.done[i] = 0.0
         self.ptr += 1
+
+    def store_block(self, obs, act, mask, rew, logp=None) -> int:
+        """Append up to ``len(rew)`` rows at once (columnar RRLC uploads); returns rows stored."""
+        i = self.ptr
+        n = min(int(rew.shape[0]), self.size - i)
+        if n <= 0:
+            return 0
+        sl = slice(i, i + n)
+        self.obs[sl] = obs[:n].reshape(n, -1)[:, : self.obs_dim]
+        if self.discrete:
+            self.act[sl] = act[:n].reshape(n, -1)[:, 0]
+        else:
+            self.act[sl] = act[:n].reshape(n, -1)[:, : self.act_dim]
+        self.mask[sl] = 1.0 if mask is None else mask[:n].reshape(n, -1)[:, : self.act_dim]
+        self.rew[sl] = rew[:n]
+        if logp is not None:
+            self.logp[sl] = logp[:n]
+        self.has_logp[sl] = logp is not None
+        self.done[sl] = 0.0
+        self.ptr += n
+        return n
 
     def finish_path(self, terminal: bool = True):
         if self.ptr > self.path_start:
@@ -152,6 +174,40 @@ class TrajectoryAlgorithm(AlgorithmAbstract):
         """REINFORCE.receive_trajectory (REINFORCE.py:70-95) with per-episode semantics."""
         self.traj += 1
         buf = self.buffer
+        if isinstance(trajectory, TrajectoryColumns):
+            self._receive_columns(trajectory)
+        else:
+            self._receive_actions(trajectory)
+        if (self.traj % self.traj_per_epoch == 0) or buf.full():
+            self.epoch += 1
+            self.train_model()
+            self.log_epoch()
+            return True
+        return False
+
+    def _receive_columns(self, c) -> None:
+        buf = self.buffer
+        n = len(c)
+        ends = np.flatnonzero(c.done[:n]) + 1
+        start = 0
+        for stop in list(ends) + ([n] if (len(ends) == 0 or ends[-1] != n) else []):
+            k = buf.store_block(c.obs[start:stop], c.act[start:stop], None if c.mask is None else c.mask[start:stop],
+                                c.rew[start:stop], None if c.logp is None else c.logp[start:stop])
+            self._steps_epoch += k
+            self._ep_ret += float(c.rew[start:start + k].sum())
+            self._ep_len += k
+            if k < stop - start:  # buffer full: cut the path here
+                if buf.ptr > buf.path_start:
+                    buf.finish_path(terminal=False)
+                return
+            if c.done[stop - 1]:
+                self._end_episode(terminal=True)
+            elif buf.ptr > buf.path_start:
+                buf.finish_path(terminal=False)  # truncated segment: bootstrap from V(s_last)
+            start = stop
+
+    def _receive_actions(self, trajectory) -> None:
+        buf = self.buffer
         last = None
         for a in trajectory.get_actions():
             obs = a.get_obs()
@@ -175,12 +231,6 @@ class TrajectoryAlgorithm(AlgorithmAbstract):
                 break
         if last is not None and not last.get_done() and buf.ptr > buf.path_start:
             buf.finish_path(terminal=False)  # truncated segment: bootstrap from V(s_last)
-        if (self.traj % self.traj_per_epoch == 0) or buf.full():
-            self.epoch += 1
-            self.train_model()
-            self.log_epoch()
-            return True
-        return False
 
     def _end_episode(self, terminal: bool):
         self.buffer.finish_path(terminal)

@@ -23,14 +23,15 @@ import numpy as np
 from ..config import ConfigLoader, address, resolve_config_json_path
 from ..models.cpu_policy import CPUPolicy
 from ..runtime.model_store import ModelBlob
-from ..types import RelayRLAction, RelayRLTrajectory
+from ..types import EpisodeRecorder, RelayRLAction, RelayRLTrajectory, TrajectoryColumns
 
 
 class RelayRLAgent:
     def __init__(self, model_path: Optional[str] = None, config_path: Optional[str] = "./config.json",
                  server_type: str = "zmq", training_port: Optional[str] = None,
                  training_prefix: Optional[str] = None, training_host: Optional[str] = None,
-                 agent_id: Optional[str] = None, seed: Optional[int] = None, handshake_timeout_s: float = 60.0):
+                 agent_id: Optional[str] = None, seed: Optional[int] = None, handshake_timeout_s: float = 60.0,
+                 wire_format: str = "columns"):
         from ..transport.zmq_transport import make_agent_id
 
         self.config_path = resolve_config_json_path(config_path)
@@ -54,7 +55,10 @@ class RelayRLAgent:
         self.enabled = True
         self.transport = None
         self._handshake_timeout = handshake_timeout_s
-        self.traj = RelayRLTrajectory(self.max_traj_length, None, agent_id=self.agent_id)
+        if wire_format not in ("columns", "actions"):
+            raise ValueError("wire_format must be 'columns' (RRLC frames) or 'actions' (per-action RRLT / protobuf)")
+        self.wire_format = wire_format
+        self._rec = EpisodeRecorder(self.max_traj_length)
         if model_path is not None:
             self._load_model_file(model_path)
         self._connect()
@@ -132,15 +136,34 @@ class RelayRLAgent:
         else:
             raise ValueError(f"server_type must be zmq, grpc or local, not {self.server_type!r}")
 
-    def _ship(self, traj: RelayRLTrajectory):
+    def _ship(self, done: bool):
+        cols = self._rec.take(self.agent_id, self.episodes_sent, done)
+        cols.max_length = self.max_traj_length
         if self.server_type == "zmq":
-            self.transport.send_trajectory(traj.encode())
+            self.transport.send_trajectory(cols.encode() if self.wire_format == "columns"
+                                           else cols.to_trajectory().encode())
         elif self.server_type == "grpc":
-            if self.transport.send_trajectory_pb(traj):
-                self.transport.poll(timeout_s=5.0)
+            if self.wire_format == "columns":
+                self.transport.send_frame(cols.encode())
+            else:
+                self.transport.send_trajectory_pb(cols.to_trajectory())
         else:
-            self.transport.send_trajectory_obj(traj)
+            self.transport.send_trajectory_obj(cols)
         self.episodes_sent += 1
+
+    @property
+    def traj(self) -> RelayRLTrajectory:
+        """The current (unshipped) episode as reference-style actions (a copy)."""
+        r = self._rec
+        if r.n == 0:
+            return RelayRLTrajectory(self.max_traj_length, None, agent_id=self.agent_id)
+        n = r.n
+        cols = TrajectoryColumns(r.obs[:n], r.act[:n], r.rew[:n], r.done[:n], None if r.mask is None else r.mask[:n],
+                                 r.logp[:n], self.agent_id, self.episodes_sent, self.max_traj_length)
+        return cols.to_trajectory()
+
+    def clear_episode(self) -> None:
+        self._rec.n = 0
 
     # ------------------------------------------------------------------ API
     def request_for_action(self, obs, mask=None, reward: float = 0.0) -> RelayRLAction:
@@ -148,34 +171,28 @@ class RelayRLAgent:
             raise RuntimeError("agent is disabled")
         if self.policy is None:
             raise RuntimeError("no model loaded")
-        if len(self.traj) > 0:
-            self.traj.actions[-1].update_reward(float(reward))
+        rec = self._rec
+        rec.set_last_reward(float(reward))
         with self._policy_lock:
             p = self.policy
             obs_a = np.asarray(obs, np.float32)
             mask_a = np.ones(p.act_dim, np.float32) if mask is None else np.asarray(mask, np.float32)
             act, data = p.step(obs_a, mask_a)
-        a0 = act[0] if act.ndim >= 1 else act
+        a0 = np.asarray(act[0] if act.ndim >= 1 else act)
+        logp = data.get("logp_a")
+        rec.record(obs_a, a0, mask_a, None if logp is None else logp[0])
         aux = {k: np.asarray(v[0], np.float32) for k, v in data.items()}
-        action = RelayRLAction(obs_a, np.asarray(a0), mask_a, 0.0, aux, False, False)
-        self.traj.add_action(action, send_if_done=False)
-        if len(self.traj) >= self.max_traj_length:
+        action = RelayRLAction(obs_a, a0, mask_a, 0.0, aux, False, False)
+        if rec.full():
             # very long episode: ship the segment (learner bootstraps it) and continue
-            self._ship(self.traj)
-            self.traj = RelayRLTrajectory(self.max_traj_length, None, agent_id=self.agent_id)
-            self.traj.seq = self.episodes_sent
+            self._ship(done=False)
         return action
 
     def flag_last_action(self, reward: float = 0.0, done: bool = True, truncated: bool = False) -> None:
-        if len(self.traj) == 0:
+        if self._rec.n == 0:
             return
-        last = self.traj.actions[-1]
-        last.update_reward(float(reward))
-        if done and not truncated:
-            last._done = True
-        self.traj.seq = self.episodes_sent
-        self._ship(self.traj)
-        self.traj = RelayRLTrajectory(self.max_traj_length, None, agent_id=self.agent_id)
+        self._rec.set_last_reward(float(reward))
+        self._ship(done=done and not truncated)
 
     def restart_agent(self, training_server_address: Optional[str] = None) -> bool:
         self.disable_agent()

@@ -17,8 +17,12 @@ Tensor fields carry one-tensor safetensors files, ``data`` values carry the JSON
 RelayRLData enum (grpc_utils.rs:31-129).  Fixes vs the reference: real model versions
 (A5), no tempfile round trip for models (grpc_utils.rs:171-205), no process::exit on an
 RPC error (agent_grpc.rs:528-531), bounded connect retries (A4).
-``first_time & 2`` is an extension: the client asks for RRLM flat-weight frames
-instead of a TorchScript archive.
+Extensions (reference tonic clients never call them, so wire compatibility holds):
+``first_time & 2`` asks for RRLM flat-weight frames instead of a TorchScript archive, and
+``SendFrame(TrajectoryFrame{bytes frame=1})`` uploads one columnar RRLC / RRLT episode
+frame instead of a per-action protobuf (one memcpy-sized message per episode).  The
+agent keeps a background long-poll thread for model updates, so an upload never waits
+on ``ClientPoll`` (the reference polled synchronously after every send, agent_grpc.rs).
 """
 from __future__ import annotations
 
@@ -69,15 +73,18 @@ def _build_messages():
     msg("RelayRLModel", [("code", 1, F.TYPE_INT32, OPT, None), ("model", 2, F.TYPE_BYTES, OPT, None),
                          ("version", 3, F.TYPE_INT64, OPT, None), ("error", 4, F.TYPE_STRING, OPT, None)])
     msg("RequestModel", [("first_time", 1, F.TYPE_INT32, OPT, None), ("version", 2, F.TYPE_INT64, OPT, None)])
+    msg("TrajectoryFrame", [("frame", 1, F.TYPE_BYTES, OPT, None)])
     msg("ActionResponse", [("code", 1, F.TYPE_INT32, OPT, None), ("message", 2, F.TYPE_STRING, OPT, None)])
     svc = fdp.service.add(name="RelayRLRoute")
     svc.method.add(name="SendActions", input_type=f".{_PKG}.Trajectory", output_type=f".{_PKG}.ActionResponse")
+    svc.method.add(name="SendFrame", input_type=f".{_PKG}.TrajectoryFrame", output_type=f".{_PKG}.ActionResponse")
     svc.method.add(name="ClientPoll", input_type=f".{_PKG}.RequestModel", output_type=f".{_PKG}.RelayRLModel")
     pool = descriptor_pool.DescriptorPool()
     fd = pool.Add(fdp)
     get = message_factory.GetMessageClass
     return {n: get(pool.FindMessageTypeByName(f"{_PKG}.{n}"))
-            for n in ("RelayRLAction", "Trajectory", "RelayRLModel", "RequestModel", "ActionResponse")}, fdp
+            for n in ("RelayRLAction", "Trajectory", "RelayRLModel", "RequestModel", "ActionResponse",
+                      "TrajectoryFrame")}, fdp
 
 
 MESSAGES, FILE_DESCRIPTOR = _build_messages()
@@ -86,6 +93,7 @@ PbTrajectory = MESSAGES["Trajectory"]
 PbModel = MESSAGES["RelayRLModel"]
 PbRequest = MESSAGES["RequestModel"]
 PbResponse = MESSAGES["ActionResponse"]
+PbFrame = MESSAGES["TrajectoryFrame"]
 SERVICE = f"{_PKG}.RelayRLRoute"
 
 
@@ -156,6 +164,9 @@ class GrpcTrainingEndpoint:
             "SendActions": grpc.unary_unary_rpc_method_handler(
                 self._send_actions, request_deserializer=PbTrajectory.FromString,
                 response_serializer=PbResponse.SerializeToString),
+            "SendFrame": grpc.unary_unary_rpc_method_handler(
+                self._send_frame, request_deserializer=PbFrame.FromString,
+                response_serializer=PbResponse.SerializeToString),
             "ClientPoll": grpc.unary_unary_rpc_method_handler(
                 self._client_poll, request_deserializer=PbRequest.FromString,
                 response_serializer=PbModel.SerializeToString),
@@ -164,6 +175,7 @@ class GrpcTrainingEndpoint:
         addr = address.replace("tcp://", "")
         if addr.startswith("*:"):
             addr = "0.0.0.0:" + addr[2:]
+        self.bad_frames = 0
         self.port = self.server.add_insecure_port(addr)
         if self.port == 0:
             raise RuntimeError(f"gRPC server could not bind {address}")
@@ -178,6 +190,18 @@ class GrpcTrainingEndpoint:
             return PbResponse(code=1, message=f"received {len(req.actions)} actions from {peer}")
         except Exception as e:
             return PbResponse(code=0, message=f"error: {e!r}")
+
+    def _send_frame(self, req, ctx):
+        from ..types import TrajectoryColumns
+
+        try:
+            f = req.frame
+            traj = TrajectoryColumns.decode(f) if TrajectoryColumns.is_frame(f) else RelayRLTrajectory.decode(f)
+        except Exception as e:
+            self.bad_frames += 1
+            return PbResponse(code=0, message=f"bad frame: {e!r}")
+        self.service.submit(traj)
+        return PbResponse(code=1, message=f"received {len(traj)} actions")
 
     def _client_poll(self, req, ctx):
         rrlm = bool(req.first_time & 2)
@@ -200,7 +224,7 @@ class GrpcTrainingEndpoint:
 # ---------------------------------------------------------------------- client
 class GrpcAgentTransport:
     def __init__(self, address: str, on_model: Callable[[ModelBlob], None], connect_retries: int = 60,
-                 retry_interval_s: float = 0.5, handshake_timeout_s: float = 60.0):
+                 retry_interval_s: float = 0.5, handshake_timeout_s: float = 60.0, background_poll: bool = True):
         import grpc
 
         self.on_model = on_model
@@ -234,6 +258,19 @@ class GrpcAgentTransport:
             if time.time() - t0 > handshake_timeout_s:
                 raise TimeoutError("gRPC model handshake timed out")
             time.sleep(retry_interval_s)
+        self._sendf = self.channel.unary_unary(f"/{SERVICE}/SendFrame", request_serializer=PbFrame.SerializeToString,
+                                               response_deserializer=PbResponse.FromString)
+        self._stop = threading.Event()
+        self._poller = None
+        if background_poll:
+            self._poller = threading.Thread(target=self._poll_loop, daemon=True, name="rrl-grpc-poll")
+            self._poller.start()
+
+    def _poll_loop(self):
+        """Long-poll for newer models; the server parks each call up to its idle timeout."""
+        while not self._stop.is_set():
+            if not self.poll(timeout_s=5.0, quiet=True):
+                self._stop.wait(0.005)
 
     def _apply(self, r):
         blob = ModelBlob.decode(r.model)
@@ -253,11 +290,26 @@ class GrpcAgentTransport:
             print(f"[GrpcAgentTransport] SendActions failed: {e!r}", flush=True)
             return False
 
-    def poll(self, timeout_s: float = 5.0) -> bool:
+    def send_frame(self, frame: bytes) -> bool:
+        from ..utils.faults import injector
+
+        frame = injector().filter_upload(frame)
+        if frame is None:
+            return True  # injected loss
+        try:
+            return self._sendf(PbFrame(frame=frame), timeout=30).code == 1
+        except Exception as e:
+            print(f"[GrpcAgentTransport] SendFrame failed: {e!r}", flush=True)
+            return False
+
+    def poll(self, timeout_s: float = 5.0, quiet: bool = False) -> bool:
         try:
             r = self._poll(PbRequest(first_time=2, version=self.version), timeout=timeout_s)
         except Exception as e:
-            print(f"[GrpcAgentTransport] ClientPoll failed: {e!r}", flush=True)
+            if not quiet and not self._stop.is_set():
+                print(f"[GrpcAgentTransport] ClientPoll failed: {e!r}", flush=True)
+            if quiet:
+                self._stop.wait(0.2)
             return False
         if r.code == 1 and r.version > self.version:
             self._apply(r)
@@ -265,4 +317,7 @@ class GrpcAgentTransport:
         return False
 
     def close(self):
+        self._stop.set()
+        if self._poller is not None:
+            self._poller.join(timeout=6)
         self.channel.close()

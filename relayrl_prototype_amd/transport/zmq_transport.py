@@ -7,7 +7,8 @@ Server side (reference training_zmq.rs:669-1058):
     ROUTER socket as ``["", "MODEL", version, blob]`` -- the reference instead connected
     a PUSH to a PULL each agent had to *bind* on one fixed port, which limited it to one
     agent per host (defect A6) and never stopped listening only when multiactor was set.
-  * PULL bound at ``trajectory_server``: one RRLT frame per trajectory (fan-in).
+  * PULL bound at ``trajectory_server``: one frame per episode (fan-in) -- a columnar RRLC
+    frame (agent default) or a per-action RRLT frame.
 Agent side (agent_zmq.rs:163-698): DEALER (identity = agent id) + PUSH.
 No busy polling anywhere (A7): receives block in C++ with timeouts.
 """
@@ -21,7 +22,7 @@ from typing import Callable, Optional
 
 from .. import _native
 from ..runtime.model_store import ModelBlob
-from ..types import RelayRLTrajectory
+from ..types import RelayRLTrajectory, TrajectoryColumns
 
 FMT_TORCHSCRIPT = b"TORCHSCRIPT"
 FMT_RRLM = b"RRLM"
@@ -101,7 +102,7 @@ class ZmqTrainingEndpoint:
             _, frames = msg
             for f in frames:
                 try:
-                    traj = RelayRLTrajectory.decode(f)
+                    traj = TrajectoryColumns.decode(f) if TrajectoryColumns.is_frame(f) else RelayRLTrajectory.decode(f)
                 except Exception as e:
                     self.bad_frames += 1
                     self._log("bad trajectory frame", e)

@@ -14,6 +14,7 @@ The on-GPU actor never builds these objects: it writes SoA rollout buffers in HB
 from __future__ import annotations
 
 import json
+import struct
 import threading
 from typing import Any, Dict, List, Optional
 
@@ -301,3 +302,163 @@ class RelayRLTrajectory:
         t = RelayRLTrajectory(inner.get("max_length", 1000), inner.get("trajectory_server"))
         t.actions = [RelayRLAction.action_from_json(a) for a in inner.get("actions", [])]
         return t
+
+
+# ---------------------------------------------------------------------- columnar episodes
+_RRLC_MAGIC = b"RRLC"
+_RRLC_HDR = "<4sIIIIIBBBBq"  # magic, version, n, D, K, A, act_kind, has_mask, has_logp, flags, seq
+_ACT_KINDS = {0: np.float32, 1: np.int32}
+
+
+class TrajectoryColumns:
+    """One episode (or truncated segment) as columns -- the agent's fast upload format.
+
+    The reference pickles a ``Vec<RelayRLAction>`` with one safetensors file per tensor
+    (trajectory.rs:50-55, action.rs:40-90), i.e. O(actions x tensors) encode work on the
+    agent and the learner.  An RRLC frame is a fixed header + agent id + contiguous
+    little-endian arrays (obs [n,D] f32, act [n,K] f32|i32, mask [n,A] f32, rew [n] f32,
+    logp [n] f32, done [n] u8), so encode is a handful of memcpys and decode is zero-copy
+    ``np.frombuffer`` views that the learner appends to its flat buffer in one slice
+    assignment.  ``get_actions()`` materialises RelayRLAction objects for code that wants
+    the reference's per-action view.
+    """
+
+    __slots__ = ("obs", "act", "mask", "rew", "logp", "done", "agent_id", "seq", "max_length", "trajectory_server")
+
+    def __init__(self, obs, act, rew, done, mask=None, logp=None, agent_id: str = "", seq: int = 0,
+                 max_length: int = 1000):
+        self.obs = obs
+        self.act = act
+        self.rew = rew
+        self.done = done
+        self.mask = mask
+        self.logp = logp
+        self.agent_id = agent_id
+        self.seq = seq
+        self.max_length = max_length
+        self.trajectory_server = None
+
+    def __len__(self):
+        return int(self.rew.shape[0])
+
+    def encode(self) -> bytes:
+        n = len(self)
+        obs = np.ascontiguousarray(self.obs, np.float32).reshape(n, -1)
+        act = self.act.reshape(n, -1)
+        kind = 1 if np.issubdtype(act.dtype, np.integer) else 0
+        act = np.ascontiguousarray(act, _ACT_KINDS[kind])
+        A = 0 if self.mask is None else self.mask.reshape(n, -1).shape[1]
+        aid = self.agent_id.encode()
+        hdr = struct.pack(_RRLC_HDR, _RRLC_MAGIC, 1, n, obs.shape[1], act.shape[1], A, kind,
+                          self.mask is not None, self.logp is not None, 0, int(self.seq))
+        parts = [hdr, struct.pack("<H", len(aid)), aid, obs.tobytes(), act.tobytes()]
+        if self.mask is not None:
+            parts.append(np.ascontiguousarray(self.mask, np.float32).tobytes())
+        parts.append(np.ascontiguousarray(self.rew, np.float32).tobytes())
+        if self.logp is not None:
+            parts.append(np.ascontiguousarray(self.logp, np.float32).tobytes())
+        parts.append(np.ascontiguousarray(self.done, np.uint8).tobytes())
+        return b"".join(parts)
+
+    @staticmethod
+    def is_frame(buf) -> bool:
+        return bytes(buf[:4]) == _RRLC_MAGIC
+
+    @staticmethod
+    def decode(buf) -> "TrajectoryColumns":
+        mv = memoryview(buf)
+        hs = struct.calcsize(_RRLC_HDR)
+        if len(mv) < hs + 2:
+            raise ValueError("RRLC frame too short")
+        magic, ver, n, D, K, A, kind, has_mask, has_logp, _flags, seq = struct.unpack_from(_RRLC_HDR, mv, 0)
+        if magic != _RRLC_MAGIC or ver != 1 or kind not in _ACT_KINDS:
+            raise ValueError("not an RRLC v1 frame")
+        (alen,) = struct.unpack_from("<H", mv, hs)
+        off = hs + 2
+        aid = bytes(mv[off:off + alen]).decode()
+        off += alen
+        need = off + 4 * n * (D + K + (A if has_mask else 0) + 1 + (1 if has_logp else 0)) + n
+        if len(mv) != need:
+            raise ValueError(f"RRLC frame size {len(mv)} != expected {need}")
+
+        def take(count, dt, shape):
+            nonlocal off
+            a = np.frombuffer(mv, dt, count, off).reshape(shape)
+            off += count * np.dtype(dt).itemsize
+            return a
+
+        obs = take(n * D, np.float32, (n, D))
+        act = take(n * K, _ACT_KINDS[kind], (n, K))
+        mask = take(n * A, np.float32, (n, A)) if has_mask else None
+        rew = take(n, np.float32, (n,))
+        logp = take(n, np.float32, (n,)) if has_logp else None
+        done = take(n, np.uint8, (n,))
+        return TrajectoryColumns(obs, act, rew, done, mask, logp, aid, seq)
+
+    def get_actions(self) -> List[RelayRLAction]:
+        out = []
+        for i in range(len(self)):
+            data = None if self.logp is None else {"logp_a": np.float32(self.logp[i])}
+            out.append(RelayRLAction(self.obs[i].copy(), self.act[i].copy(),
+                                     None if self.mask is None else self.mask[i].copy(), float(self.rew[i]), data,
+                                     bool(self.done[i]), True))
+        return out
+
+    def to_trajectory(self) -> RelayRLTrajectory:
+        t = RelayRLTrajectory(self.max_length, None, agent_id=self.agent_id)
+        t.seq = self.seq
+        t.actions = self.get_actions()
+        return t
+
+
+class EpisodeRecorder:
+    """Preallocated per-agent episode columns; one row written per ``request_for_action``."""
+
+    def __init__(self, capacity: int):
+        self.capacity = int(capacity)
+        self.n = 0
+        self._shapes = None
+
+    def _alloc(self, obs, act, mask):
+        c = self.capacity
+        self.obs = np.zeros((c, obs.size), np.float32)
+        self.act = np.zeros((c, max(1, act.size)), np.int32 if np.issubdtype(act.dtype, np.integer) else np.float32)
+        self.mask = None if mask is None else np.zeros((c, mask.size), np.float32)
+        self.rew = np.zeros(c, np.float32)
+        self.logp = np.zeros(c, np.float32)
+        self.done = np.zeros(c, np.uint8)
+        self._shapes = (obs.size, act.size, act.dtype.kind, None if mask is None else mask.size)
+
+    def record(self, obs: np.ndarray, act: np.ndarray, mask, logp) -> None:
+        key = (obs.size, act.size, act.dtype.kind, None if mask is None else mask.size)
+        if self._shapes != key:
+            if self.n:
+                raise ValueError("observation/action shapes changed within an episode")
+            self._alloc(obs, act, mask)
+        i = self.n
+        self.obs[i] = obs.reshape(-1)
+        self.act[i] = act.reshape(-1)
+        if self.mask is not None:
+            self.mask[i] = mask.reshape(-1)
+        self.rew[i] = 0.0
+        self.logp[i] = 0.0 if logp is None else float(logp)
+        self.done[i] = 0
+        self.n = i + 1
+
+    def set_last_reward(self, r: float) -> None:
+        if self.n:
+            self.rew[self.n - 1] = r
+
+    def full(self) -> bool:
+        return self.n >= self.capacity
+
+    def take(self, agent_id: str, seq: int, done: bool) -> TrajectoryColumns:
+        n = self.n
+        d = self.done[:n].copy()
+        if n and done:
+            d[n - 1] = 1
+        cols = TrajectoryColumns(self.obs[:n].copy(), self.act[:n].copy(), self.rew[:n].copy(), d,
+                                 None if self.mask is None else self.mask[:n].copy(), self.logp[:n].copy(),
+                                 agent_id, seq)
+        self.n = 0
+        return cols

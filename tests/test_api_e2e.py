@@ -63,13 +63,14 @@ def run_episodes(agent, n, max_steps=200):
     return lens
 
 
-@pytest.mark.parametrize("server_type", ["local", "zmq", "grpc"])
-def test_agent_server_roundtrip(cfgdir, server_type):
+@pytest.mark.parametrize("server_type,wire", [("local", "columns"), ("zmq", "columns"), ("grpc", "columns"),
+                                              ("zmq", "actions"), ("grpc", "actions")])
+def test_agent_server_roundtrip(cfgdir, server_type, wire):
     tmp, cfgp = cfgdir
     srv = TrainingServer("REINFORCE", 4, 2, 100000, env_dir=str(tmp / "env"), config_path=cfgp,
                          server_type=server_type, device="cpu", hyperparams={"with_vf_baseline": "true"})
     try:
-        agent = RelayRLAgent(config_path=cfgp, server_type=server_type, handshake_timeout_s=30)
+        agent = RelayRLAgent(config_path=cfgp, server_type=server_type, handshake_timeout_s=30, wire_format=wire)
         assert agent.model_version == 0
         run_episodes(agent, 8)
         import time

@@ -179,3 +179,30 @@ def test_fault_injection_drop_and_corrupt(tmp_path, monkeypatch):
     push.close()
     ep.close()
     svc.stop()
+
+
+def test_plot_utils(tmp_path):
+    from relayrl_prototype_amd.utils.plot import get_datasets, get_newest_dataset, make_plots
+
+    for s in range(2):
+        d = tmp_path / "exp" / f"exp_s{s}"
+        d.mkdir(parents=True)
+        (d / "progress.txt").write_text("Epoch\tAverageEpRet\n" + "".join(f"{i}\t{i * (s + 1)}.0\n" for i in range(5)))
+    runs = get_datasets(str(tmp_path))
+    assert len(runs) == 2 and runs[0]["data"]["AverageEpRet"][4] == 4.0
+    assert get_newest_dataset(str(tmp_path)).endswith("progress.txt")
+    out = tmp_path / "curve.png"
+    make_plots([str(tmp_path)], values=["AverageEpRet"], smooth_k=2, out=str(out))
+    assert out.exists() and out.stat().st_size > 1000
+
+
+def test_server_config_manager(tmp_path, monkeypatch):
+    monkeypatch.setenv("RRL_QUIET_CONFIG", "1")
+    from relayrl_prototype_amd.utils.addresses import ServerConfigManager
+
+    m = ServerConfigManager(str(tmp_path / "cfg.json"), {"training_server": {"host": "*", "port": 7000}})
+    ts = m.get("training_server")
+    assert ts.bind_address().endswith("0.0.0.0:7000") and ts.connect_address().endswith("127.0.0.1:7000")
+    m.assign_free_ports()
+    ports = {e["port"] for e in m.as_dict().values()}
+    assert len(ports) == 3 and all(int(p) > 0 for p in ports)
