@@ -1,0 +1,246 @@
+// PyTorch bindings for the pixel-model kernels (csrc/kernels/cnn.hip, pong.hip).
+// Same contract as hip_ops.cpp: every tensor is validated (device, dtype, contiguity,
+// size) before a launch, launches go to the current HIP stream.
+#include <ATen/hip/HIPContext.h>
+#include <torch/extension.h>
+
+#include <cstdint>
+#include <optional>
+
+extern "C" {
+int rrl_conv_fwd(const void* x, int x_u8, const uint16_t* w, const float* b, uint16_t* y, int N, int H, int W,
+                 int C, int KH, int KW, int S, int Cout, int relu, void* stream);
+int rrl_gemm_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* mask, uint16_t* out, int M, int Cout,
+                   int K, void* stream);
+int rrl_col2im_mask(const uint16_t* dcol, const uint16_t* xact, uint16_t* dx, int N, int H, int W, int C, int KH,
+                    int KW, int S, void* stream);
+int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, int splits, int N, int H, int W, int C,
+                   int KH, int KW, int S, int Cout, void* stream);
+int rrl_gemm_splits(int R, int splits);
+int rrl_sum_splits(const float* part, int splits, long long n, float* out, void* stream);
+int rrl_colsum(const uint16_t* y, int M, int C, float* part, int splits, void* stream);
+int rrl_sumsq(const float* x, long long n, float* work, int work_n, float* out, void* stream);
+int rrl_adam_clip(float* p, float* m, float* v, const float* g, uint16_t* shadow, long long n, const float* norm_sq,
+                  float max_norm, float lr, float b1, float b2, float eps, int step, void* stream);
+int rrl_to_bf16(const float* x, uint16_t* y, long long n, void* stream);
+int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, int A, int32_t* act, float* logp,
+                 float* value, float* logits_out, unsigned long long seed, unsigned long long step, int row_offset,
+                 const int32_t* act_in, const float* adv, const float* ret, float inv_B, float vf_coef,
+                 float ent_coef, uint16_t* dh, float* dhead, float* stats, int grid, void* stream);
+int rrl_head_wgrad(const uint16_t* h, const float* dhead, int B, int A, float* part, int nblk, void* stream);
+int rrl_pong_state_size();
+int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len, int N,
+                  unsigned long long seed, unsigned long long step, int max_steps, int reset_all, void* stream);
+int rrl_pong_render(const float* state, uint8_t* obs, int N, void* stream);
+}
+
+namespace {
+
+using at::Tensor;
+using OptT = std::optional<Tensor>;
+
+void* stream() { return (void*)at::hip::getCurrentHIPStream().stream(); }
+
+void check(const Tensor& t, const char* name, at::ScalarType dt, int64_t min_numel) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.numel() >= min_numel, name, " has ", t.numel(), " elements, need >= ", min_numel);
+}
+template <class T>
+T* opt_ptr(const OptT& t, const char* name, at::ScalarType dt, int64_t n) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check(*t, name, dt, n);
+  return reinterpret_cast<T*>(t->data_ptr());
+}
+void rc_check(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, what, " failed with code ", rc,
+              " (", (rc > 0 ? hipGetErrorString((hipError_t)rc) : "unsupported shape"), ")");
+}
+uint16_t* bf(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+struct Geo {
+  int64_t N, H, W, C, KH, KW, S;
+  int64_t OH() const { return (H - KH) / S + 1; }
+  int64_t OW() const { return (W - KW) / S + 1; }
+};
+void check_geo(const Geo& g) {
+  TORCH_CHECK(g.N > 0 && g.H >= g.KH && g.W >= g.KW && g.S > 0 && g.C > 0, "bad conv geometry");
+}
+
+void conv_fwd(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& y, int64_t N, int64_t H, int64_t W,
+              int64_t C, int64_t KH, int64_t KW, int64_t S, int64_t Cout, bool relu) {
+  Geo g{N, H, W, C, KH, KW, S};
+  check_geo(g);
+  const bool u8 = x.scalar_type() == at::kByte;
+  check(x, "x", u8 ? at::kByte : at::kBFloat16, N * H * W * C);
+  TORCH_CHECK(u8 ? (C == 4 && KW % 2 == 0) : (C % 8 == 0), "conv_fwd: unsupported channel layout");
+  check(w, "w", at::kBFloat16, Cout * KH * KW * C);
+  check(b, "b", at::kFloat, Cout);
+  check(y, "y", at::kBFloat16, N * g.OH() * g.OW() * Cout);
+  rc_check(rrl_conv_fwd(x.data_ptr(), u8, bf(w), b.data_ptr<float>(), bf(y), N, H, W, C, KH, KW, S, Cout, relu,
+                        stream()),
+           "conv_fwd");
+}
+
+void gemm_dgrad(const Tensor& dy, const Tensor& w, const OptT& mask, const Tensor& out, int64_t M, int64_t Cout,
+                int64_t K) {
+  TORCH_CHECK(Cout % 8 == 0 && K % 8 == 0, "gemm_dgrad: Cout and K must be multiples of 8");
+  check(dy, "dy", at::kBFloat16, M * Cout);
+  check(w, "w", at::kBFloat16, Cout * K);
+  check(out, "out", at::kBFloat16, M * K);
+  const uint16_t* mp = opt_ptr<uint16_t>(mask, "mask", at::kBFloat16, M * K);
+  rc_check(rrl_gemm_dgrad(bf(dy), bf(w), mp, bf(out), M, Cout, K, stream()), "gemm_dgrad");
+}
+
+void col2im_mask(const Tensor& dcol, const Tensor& xact, const Tensor& dx, int64_t N, int64_t H, int64_t W,
+                 int64_t C, int64_t KH, int64_t KW, int64_t S) {
+  Geo g{N, H, W, C, KH, KW, S};
+  check_geo(g);
+  TORCH_CHECK(C % 8 == 0, "col2im_mask: C must be a multiple of 8");
+  check(dcol, "dcol", at::kBFloat16, N * g.OH() * g.OW() * KH * KW * C);
+  check(xact, "xact", at::kBFloat16, N * H * W * C);
+  check(dx, "dx", at::kBFloat16, N * H * W * C);
+  rc_check(rrl_col2im_mask(bf(dcol), bf(xact), bf(dx), N, H, W, C, KH, KW, S, stream()), "col2im_mask");
+}
+
+int64_t gemm_splits(int64_t R, int64_t splits) { return rrl_gemm_splits((int)R, (int)splits); }
+
+int64_t conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& part, int64_t splits, int64_t N, int64_t H,
+                   int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t S, int64_t Cout) {
+  Geo g{N, H, W, C, KH, KW, S};
+  check_geo(g);
+  const bool u8 = x.scalar_type() == at::kByte;
+  const int64_t M = N * g.OH() * g.OW(), K = KH * KW * C;
+  TORCH_CHECK(u8 ? (C == 4 && KW % 2 == 0) : (C % 8 == 0), "conv_wgrad: unsupported channel layout");
+  check(dy, "dy", at::kBFloat16, M * Cout);
+  check(x, "x", u8 ? at::kByte : at::kBFloat16, N * H * W * C);
+  const int64_t s = gemm_splits(M, splits);
+  check(part, "part", at::kFloat, s * Cout * K);
+  rc_check(rrl_conv_wgrad(bf(dy), x.data_ptr(), u8, part.data_ptr<float>(), (int)splits, N, H, W, C, KH, KW, S, Cout,
+                          stream()),
+           "conv_wgrad");
+  return s;
+}
+
+void sum_splits(const Tensor& part, int64_t splits, int64_t n, const Tensor& out) {
+  check(part, "part", at::kFloat, splits * n);
+  check(out, "out", at::kFloat, n);
+  rc_check(rrl_sum_splits(part.data_ptr<float>(), (int)splits, n, out.data_ptr<float>(), stream()), "sum_splits");
+}
+
+void colsum(const Tensor& y, int64_t M, int64_t C, const Tensor& part, int64_t splits) {
+  check(y, "y", at::kBFloat16, M * C);
+  check(part, "part", at::kFloat, splits * C);
+  rc_check(rrl_colsum(bf(y), M, C, part.data_ptr<float>(), (int)splits, stream()), "colsum");
+}
+
+void sumsq(const Tensor& x, const Tensor& work, const Tensor& out) {
+  check(x, "x", at::kFloat, 0);
+  check(work, "work", at::kFloat, 1);
+  check(out, "out", at::kFloat, 1);
+  rc_check(rrl_sumsq(x.data_ptr<float>(), x.numel(), work.data_ptr<float>(), (int)work.numel(),
+                     out.data_ptr<float>(), stream()),
+           "sumsq");
+}
+
+void adam_clip(const Tensor& p, const Tensor& m, const Tensor& v, const Tensor& g, const OptT& shadow,
+               const OptT& norm_sq, double max_norm, double lr, double b1, double b2, double eps, int64_t step) {
+  const int64_t n = p.numel();
+  check(p, "p", at::kFloat, n);
+  check(m, "m", at::kFloat, n);
+  check(v, "v", at::kFloat, n);
+  check(g, "g", at::kFloat, n);
+  TORCH_CHECK(step >= 1, "adam step must be >= 1");
+  uint16_t* sh = opt_ptr<uint16_t>(shadow, "shadow", at::kBFloat16, n);
+  const float* ns = opt_ptr<const float>(norm_sq, "norm_sq", at::kFloat, 1);
+  rc_check(rrl_adam_clip(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr<float>(), sh, n,
+                         ns, (float)max_norm, (float)lr, (float)b1, (float)b2, (float)eps, (int)step, stream()),
+           "adam_clip");
+}
+
+void to_bf16(const Tensor& x, const Tensor& y) {
+  check(x, "x", at::kFloat, 0);
+  check(y, "y", at::kBFloat16, x.numel());
+  rc_check(rrl_to_bf16(x.data_ptr<float>(), bf(y), x.numel(), stream()), "to_bf16");
+}
+
+void a2c_head(int64_t mode, const Tensor& h, const Tensor& head_params, int64_t B, int64_t A, const OptT& act,
+              const OptT& logp, const OptT& value, const OptT& logits, int64_t seed, int64_t step,
+              int64_t row_offset, const OptT& act_in, const OptT& adv, const OptT& ret, double inv_B, double vf_coef,
+              double ent_coef, const OptT& dh, const OptT& dhead, const OptT& stats, int64_t grid) {
+  constexpr int64_t F = 512;
+  TORCH_CHECK(A >= 1 && A <= 16, "a2c_head: 1 <= A <= 16");
+  TORCH_CHECK(mode == 0 || mode == 1, "a2c_head: mode must be 0 (rollout) or 1 (train)");
+  TORCH_CHECK(grid >= 1, "a2c_head: grid >= 1");
+  check(h, "h", at::kBFloat16, B * F);
+  check(head_params, "head_params", at::kFloat, (A + 1) * F + A + 1);
+  int32_t* ap = opt_ptr<int32_t>(act, "act", at::kInt, B);
+  float* lp = opt_ptr<float>(logp, "logp", at::kFloat, B);
+  float* vp = opt_ptr<float>(value, "value", at::kFloat, B);
+  float* lo = opt_ptr<float>(logits, "logits", at::kFloat, B * A);
+  const int32_t* ai = opt_ptr<const int32_t>(act_in, "act_in", at::kInt, mode == 1 ? B : 0);
+  const float* ad = opt_ptr<const float>(adv, "adv", at::kFloat, mode == 1 ? B : 0);
+  const float* re = opt_ptr<const float>(ret, "ret", at::kFloat, mode == 1 ? B : 0);
+  uint16_t* dhp = opt_ptr<uint16_t>(dh, "dh", at::kBFloat16, mode == 1 ? B * F : 0);
+  float* dhd = opt_ptr<float>(dhead, "dhead", at::kFloat, mode == 1 ? B * (A + 1) : 0);
+  float* st = opt_ptr<float>(stats, "stats", at::kFloat, mode == 1 ? grid * 4 : 0);
+  if (mode == 1)
+    TORCH_CHECK(ai && ad && re && dhp && dhd && st, "a2c_head train mode needs act_in, adv, ret, dh, dhead, stats");
+  rc_check(rrl_a2c_head((int)mode, bf(h), head_params.data_ptr<float>(), B, A, ap, lp, vp, lo, (uint64_t)seed,
+                        (uint64_t)step, (int)row_offset, ai, ad, re, (float)inv_B, (float)vf_coef, (float)ent_coef,
+                        dhp, dhd, st, (int)grid, stream()),
+           "a2c_head");
+}
+
+void head_wgrad(const Tensor& h, const Tensor& dhead, int64_t B, int64_t A, const Tensor& part, int64_t nblk) {
+  constexpr int64_t F = 512;
+  TORCH_CHECK(A >= 1 && A <= 16 && nblk >= 1, "head_wgrad: bad arguments");
+  check(h, "h", at::kBFloat16, B * F);
+  check(dhead, "dhead", at::kFloat, B * (A + 1));
+  check(part, "part", at::kFloat, nblk * ((A + 1) * F + A + 1));
+  rc_check(rrl_head_wgrad(bf(h), dhead.data_ptr<float>(), B, A, part.data_ptr<float>(), nblk, stream()),
+           "head_wgrad");
+}
+
+int64_t pong_state_size() { return rrl_pong_state_size(); }
+
+void pong_step(const Tensor& state, const Tensor& act, const Tensor& rew, const Tensor& done, const Tensor& fin_ret,
+               const Tensor& fin_len, int64_t N, int64_t seed, int64_t step, int64_t max_steps, bool reset_all) {
+  check(state, "state", at::kFloat, N * pong_state_size());
+  check(act, "act", at::kInt, reset_all ? 0 : N);
+  check(rew, "rew", at::kFloat, N);
+  check(done, "done", at::kFloat, N);
+  check(fin_ret, "fin_ret", at::kFloat, N);
+  check(fin_len, "fin_len", at::kFloat, N);
+  rc_check(rrl_pong_step(state.data_ptr<float>(), act.data_ptr<int32_t>(), rew.data_ptr<float>(),
+                         done.data_ptr<float>(), fin_ret.data_ptr<float>(), fin_len.data_ptr<float>(), (int)N,
+                         (uint64_t)seed, (uint64_t)step, (int)max_steps, reset_all ? 1 : 0, stream()),
+           "pong_step");
+}
+
+void pong_render(const Tensor& state, const Tensor& obs, int64_t N) {
+  check(state, "state", at::kFloat, N * pong_state_size());
+  check(obs, "obs", at::kByte, N * 84 * 84 * 4);
+  rc_check(rrl_pong_render(state.data_ptr<float>(), obs.data_ptr<uint8_t>(), (int)N, stream()), "pong_render");
+}
+
+}  // namespace
+
+void register_cnn_ops(pybind11::module_& m) {
+  m.def("conv_fwd", &conv_fwd);
+  m.def("gemm_dgrad", &gemm_dgrad);
+  m.def("col2im_mask", &col2im_mask);
+  m.def("gemm_splits", &gemm_splits);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("sum_splits", &sum_splits);
+  m.def("colsum", &colsum);
+  m.def("sumsq", &sumsq);
+  m.def("adam_clip", &adam_clip);
+  m.def("to_bf16", &to_bf16);
+  m.def("a2c_head", &a2c_head);
+  m.def("head_wgrad", &head_wgrad);
+  m.def("pong_state_size", &pong_state_size);
+  m.def("pong_step", &pong_step);
+  m.def("pong_render", &pong_render);
+}

@@ -301,6 +301,8 @@ void rollout(int64_t env, const Tensor& params, int64_t H, const Tensor& state, 
 
 }  // namespace
 
+void register_cnn_ops(pybind11::module_& m);  // cnn_ops.cpp
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "relayrl_prototype_amd gfx950 HIP kernels";
   m.def("num_cus", &num_cus);
@@ -317,4 +319,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("env_dims", &env_dims);
   m.def("rollout_grid", &rollout_grid);
   m.def("rollout", &rollout);
+  register_cnn_ops(m);
 }

@@ -1,0 +1,572 @@
+// Pixel-policy (Nature-CNN actor-critic) kernels for the A2C / Pong configuration
+// (BASELINE.json config 4; SURVEY §2.6 "New: CNN encoder (Pong) -- implicit-GEMM conv on
+// MFMA").  The reference has no pixel model; this family is new.
+//
+// Compute dtype: bf16 operands on v_mfma_f32_16x16x32_bf16 with fp32 accumulation,
+// fp32 master weights / Adam state, bf16 shadow weights written by the optimizer.
+// Activations are NHWC bf16 (post-ReLU), weights [Cout][KH][KW][Cin] so that a conv's
+// reduction index k = (kh, kw, c) is contiguous in both operands.
+//
+//   forward   Y  = relu(im2col(X) . W^T + b)        A = ConvLoader/FrameLoader, B = W   [NT]
+//   dgrad     dXc = dY . W                          A = dY, B = W (transposed LDS read) [NN]
+//             dX = col2im(dXc) * (X > 0)            gather form, no atomics
+//   wgrad     dW = dY^T . im2col(X)                 both operands via transposed reads,
+//                                                   split over batch x spatial -> fp32 partials
+#include "gemm_bf16.h"
+#include "heads.h"
+
+namespace rrl {
+
+struct ConvGeom {
+  int N, H, W, C, KH, KW, S, OH, OW, Cout;
+  __host__ __device__ int M() const { return N * OH * OW; }
+  __host__ __device__ int K() const { return KH * KW * C; }
+};
+
+// ----------------------------------------------------------------------------- epilogues
+struct BiasReluStore {  // bf16 [M][N] = act(acc + b[n])
+  uint16_t* y;
+  const float* b;
+  int M, N;
+  bool relu;
+  __device__ __forceinline__ void operator()(int m, int n, f32x4_t acc, int) const {
+    if (n >= N) return;
+    const float bb = b ? b[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (m + r < M) {
+        float v = acc[r] + bb;
+        if (relu) v = fmaxf(v, 0.f);
+        y[(size_t)(m + r) * N + n] = f2bf(v);
+      }
+    }
+  }
+};
+
+struct MaskStore {  // bf16 [M][N] = acc * (mask[m][n] > 0)   (mask == null: plain store)
+  uint16_t* y;
+  const uint16_t* mask;
+  int M, N;
+  __device__ __forceinline__ void operator()(int m, int n, f32x4_t acc, int) const {
+    if (n >= N) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (m + r < M) {
+        const size_t i = (size_t)(m + r) * N + n;
+        float v = acc[r];
+        if (mask && !(bf2f(mask[i]) > 0.f)) v = 0.f;
+        y[i] = f2bf(v);
+      }
+    }
+  }
+};
+
+struct PartialStore {  // fp32 [split][M][N]
+  float* out;
+  int M, N;
+  __device__ __forceinline__ void operator()(int m, int n, f32x4_t acc, int z) const {
+    if (n >= N) return;
+    float* o = out + (size_t)z * M * N;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (m + r < M) o[(size_t)(m + r) * N + n] = acc[r];
+  }
+};
+
+template <int BM, int BN, bool A_TR, bool B_TR, class LA, class LB, class Epi>
+static int launch_gemm(LA la, LB lb, Epi epi, int M, int N, int K, int splits, hipStream_t st) {
+  using S = GemmShape<BM, BN, A_TR, B_TR>;
+  auto kern = gemm_bf16_kernel<BM, BN, A_TR, B_TR, LA, LB, Epi>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS_BYTES);
+    attr = true;
+  }
+  splits = splits < 1 ? 1 : splits;
+  int kps = (K + splits - 1) / splits;
+  kps = (kps + kGemmBK - 1) / kGemmBK * kGemmBK;
+  splits = (K + kps - 1) / kps;
+  dim3 grid((M + BM - 1) / BM, (N + BN - 1) / BN, splits);
+  hipLaunchKernelGGL(kern, grid, dim3(256), S::LDS_BYTES, st, la, lb, epi, M, N, K, kps);
+  return (int)hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- col2im
+// dX[n][ih][iw][c] = sum over (kh, kw) with ih = oh*S + kh, iw = ow*S + kw of
+// dXc[(n, oh, ow)][(kh, kw, c)], then * (X > 0).  One thread per 8 channels.
+__global__ void col2im_mask_kernel(const uint16_t* __restrict__ dcol, const uint16_t* __restrict__ xact,
+                                   uint16_t* __restrict__ dx, ConvGeom g) {
+  const int C8 = g.C / 8;
+  const size_t total = (size_t)g.N * g.H * g.W * C8;
+  const int K = g.K();
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < total; t += (size_t)gridDim.x * blockDim.x) {
+    const int c8 = (int)(t % C8);
+    size_t r = t / C8;
+    const int iw = (int)(r % g.W);
+    r /= g.W;
+    const int ih = (int)(r % g.H);
+    const int n = (int)(r / g.H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int kh = 0; kh < g.KH; ++kh) {
+      const int th = ih - kh;
+      if (th < 0 || th % g.S) continue;
+      const int oh = th / g.S;
+      if (oh >= g.OH) continue;
+      for (int kw = 0; kw < g.KW; ++kw) {
+        const int tw = iw - kw;
+        if (tw < 0 || tw % g.S) continue;
+        const int ow = tw / g.S;
+        if (ow >= g.OW) continue;
+        const size_t m = ((size_t)n * g.OH + oh) * g.OW + ow;
+        const uint4 v = *reinterpret_cast<const uint4*>(dcol + m * K + (kh * g.KW + kw) * g.C + c8 * 8);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[2 * i] += bf2f((uint16_t)(w[i] & 0xffff));
+          acc[2 * i + 1] += bf2f((uint16_t)(w[i] >> 16));
+        }
+      }
+    }
+    const size_t o = t * 8;
+    const uint4 xm = *reinterpret_cast<const uint4*>(xact + o);
+    const uint32_t xw[4] = {xm.x, xm.y, xm.z, xm.w};
+    uint32_t ow4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float a = bf2f((uint16_t)(xw[i] & 0xffff)) > 0.f ? acc[2 * i] : 0.f;
+      const float b = bf2f((uint16_t)(xw[i] >> 16)) > 0.f ? acc[2 * i + 1] : 0.f;
+      ow4[i] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+    }
+    *reinterpret_cast<uint4*>(dx + o) = make_uint4(ow4[0], ow4[1], ow4[2], ow4[3]);
+  }
+}
+
+// ----------------------------------------------------------------------------- reductions
+// part [splits][n] fp32 -> out[n] (+= when accumulate)
+__global__ void sum_splits_kernel(const float* __restrict__ part, int splits, size_t n, float* __restrict__ out) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += part[(size_t)z * n + i];
+    out[i] = s;
+  }
+}
+
+// Column sums of a bf16 [M][C] matrix: partial [gridDim.y][C].  Block = 256 threads =
+// 64 columns x 4 row phases.
+__global__ void colsum_kernel(const uint16_t* __restrict__ y, int M, int C, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int ph = threadIdx.x >> 6;
+  const int rows = (M + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rows, r1 = min(M, r0 + rows);
+  float s = 0.f;
+  if (c < C)
+    for (int r = r0 + ph; r < r1; r += 4) s += bf2f(y[(size_t)r * C + c]);
+  red[ph][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ph == 0 && c < C) part[(size_t)blockIdx.y * C + c] = red[0][threadIdx.x] + red[1][threadIdx.x] +
+                                                           red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+// Sum of squares of an fp32 vector: two-pass, deterministic.
+__global__ void sumsq_partial_kernel(const float* __restrict__ x, size_t n, float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    s += v * v;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+__global__ void sum_small_kernel(const float* __restrict__ part, int n, float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += part[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = red[0] + red[1] + red[2] + red[3];
+}
+
+// Adam with global-norm clipping (scale = min(1, max_norm / ||g||), norm from the device)
+// and a bf16 shadow copy of the updated parameters for the next forward.
+__global__ void adam_clip_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
+                                 const float* __restrict__ g, uint16_t* __restrict__ shadow, size_t n,
+                                 const float* __restrict__ norm_sq, float max_norm, float lr, float b1, float b2,
+                                 float eps, float bc1, float bc2) {
+  float scale = 1.f;
+  if (norm_sq != nullptr && max_norm > 0.f) {
+    const float nrm = sqrtf(norm_sq[0]);
+    scale = nrm > max_norm ? max_norm / (nrm + 1e-6f) : 1.f;
+  }
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float gi = g[i] * scale;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi / bc2) + eps;
+    const float pi = p[i] - lr * (mi / bc1) / denom;
+    p[i] = pi;
+    if (shadow) shadow[i] = f2bf(pi);
+  }
+}
+
+__global__ void to_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    y[i] = f2bf(x[i]);
+}
+
+// ----------------------------------------------------------------------------- A2C head
+// One wave per row: lane owns features 8*lane .. 8*lane+7 of h (F = 512 -> 64 lanes x 8).
+// Head weights (A + 1 rows of F fp32: policy rows then the value row, and A + 1 biases)
+// are staged in LDS per block.
+constexpr int kHeadF = 512;
+
+struct HeadArgs {
+  const uint16_t* h;      // [B][F] post-ReLU fc output
+  const float* w;         // [A][F] policy rows; value row at w_v
+  const float* bias;      // [A]
+  const float* w_v;       // [F]
+  const float* b_v;       // [1]
+  int B, A;
+  // rollout outputs
+  int32_t* act;
+  float* logp;
+  float* value;
+  float* logits_out;      // optional [B][A]
+  uint32_t seed_lo, seed_hi, step_lo, step_hi;
+  int row_offset;
+  // training inputs / outputs
+  const int32_t* act_in;
+  const float* adv;
+  const float* ret;
+  float inv_B, vf_coef, ent_coef;
+  uint16_t* dh;           // [B][F] grad wrt fc pre-activation (masked), bf16
+  float* dhead;           // [B][A+1] fp32: dlogits, dv
+  float* stats;           // [gridDim.x][4]: pg loss, vf loss, entropy, count
+};
+
+template <bool TRAIN>
+__global__ void __launch_bounds__(256) a2c_head_kernel(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float hs[];  // [(A+1)][F] + [A+1]
+  const int A = a.A, F = kHeadF;
+  for (int i = threadIdx.x; i < A * F; i += 256) hs[i] = a.w[i];
+  for (int i = threadIdx.x; i < F; i += 256) hs[A * F + i] = a.w_v[i];
+  if (threadIdx.x < A) hs[(A + 1) * F + threadIdx.x] = a.bias[threadIdx.x];
+  if (threadIdx.x == 0) hs[(A + 1) * F + A] = a.b_v[0];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float st_pg = 0.f, st_vf = 0.f, st_ent = 0.f, st_n = 0.f;
+  for (int row = blockIdx.x * 4 + wave; row < a.B; row += gridDim.x * 4) {
+    const uint4 hv = *reinterpret_cast<const uint4*>(a.h + (size_t)row * F + 8 * lane);
+    const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w};
+    float x[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x[2 * i] = bf2f((uint16_t)(hw[i] & 0xffff));
+      x[2 * i + 1] = bf2f((uint16_t)(hw[i] >> 16));
+    }
+    float logits[kMaxAct];
+#pragma unroll
+    for (int o = 0; o < kMaxAct; ++o) logits[o] = -INFINITY;
+    float vsum = 0.f;
+    {
+      const float* wr = hs + A * F + 8 * lane;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) vsum += wr[i] * x[i];
+    }
+    const float value = wave_sum(vsum) + hs[(A + 1) * F + A];
+#pragma unroll
+    for (int o = 0; o < kMaxAct; ++o) {
+      if (o < A) {
+        const float* wr = hs + o * F + 8 * lane;
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += wr[i] * x[i];
+        logits[o] = wave_sum(s) + hs[(A + 1) * F + o];
+      }
+    }
+    const CatStats cs = cat_stats(A, logits);
+    if (!TRAIN) {
+      if (lane == 0) {
+        const uint4 r = philox4x32(make_uint4((uint32_t)(row + a.row_offset), a.step_lo, a.step_hi, 0x50u),
+                                   make_uint2(a.seed_lo, a.seed_hi));
+        const int pick = cat_sample(A, logits, cs.lse, u01(r.x));
+        if (a.act) a.act[row] = pick;
+        if (a.logp) a.logp[row] = pick_logit(A, logits, pick) - cs.lse;
+        if (a.value) a.value[row] = value;
+        if (a.logits_out)
+          for (int o = 0; o < A; ++o) a.logits_out[(size_t)row * A + o] = logits[o];
+      }
+    } else {
+      const int act = a.act_in[row];
+      const float adv = a.adv[row], ret = a.ret[row];
+      const float lp = pick_logit(A, logits, act) - cs.lse;
+      // d/dz of  -adv*logp(a) - ent_coef*H  (mean over B), d/dv of vf_coef*(v-ret)^2
+      float dz[kMaxAct];
+#pragma unroll
+      for (int o = 0; o < kMaxAct; ++o) {
+        dz[o] = 0.f;
+        if (o < A) {
+          const float lpo = logits[o] - cs.lse;
+          const float p = __expf(lpo);
+          dz[o] = a.inv_B * (-adv * ((o == act ? 1.f : 0.f) - p) + a.ent_coef * p * (lpo + cs.entropy));
+        }
+      }
+      const float dv = a.inv_B * 2.f * a.vf_coef * (value - ret);
+      float g[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) g[i] = dv * hs[A * F + 8 * lane + i];
+#pragma unroll
+      for (int o = 0; o < kMaxAct; ++o)
+        if (o < A) {
+          const float* wr = hs + o * F + 8 * lane;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) g[i] += dz[o] * wr[i];
+        }
+      uint32_t ow[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float lo = x[2 * i] > 0.f ? g[2 * i] : 0.f, hi = x[2 * i + 1] > 0.f ? g[2 * i + 1] : 0.f;
+        ow[i] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+      }
+      *reinterpret_cast<uint4*>(a.dh + (size_t)row * F + 8 * lane) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+      float mine = dv;
+#pragma unroll
+      for (int o = 0; o < kMaxAct; ++o)
+        if (o < A && lane == o) mine = dz[o];
+      if (lane <= A) a.dhead[(size_t)row * (A + 1) + lane] = mine;
+      if (lane == 0) {
+        st_pg += -adv * lp;
+        st_vf += (value - ret) * (value - ret);
+        st_ent += cs.entropy;
+        st_n += 1.f;
+      }
+    }
+  }
+  if (TRAIN) {
+    __syncthreads();
+    float* red = hs;  // reuse
+    if (lane == 0) {
+      red[wave * 4 + 0] = st_pg;
+      red[wave * 4 + 1] = st_vf;
+      red[wave * 4 + 2] = st_ent;
+      red[wave * 4 + 3] = st_n;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4)
+      a.stats[blockIdx.x * 4 + threadIdx.x] = red[threadIdx.x] + red[4 + threadIdx.x] + red[8 + threadIdx.x] +
+                                              red[12 + threadIdx.x];
+  }
+}
+
+// Head weight gradients: part[blk][ (A+1)*F + (A+1) ] = sum over the block's rows of
+// dhead[r][o] * h[r][f] (and dhead[r][o] for the biases).  Thread t owns f = 2t, 2t+1.
+__global__ void __launch_bounds__(256) head_wgrad_kernel(const uint16_t* __restrict__ h,
+                                                         const float* __restrict__ dhead, int B, int A,
+                                                         float* __restrict__ part) {
+  const int F = kHeadF, O = A + 1;
+  const int rows = (B + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * rows, r1 = min(B, r0 + rows);
+  const int f = 2 * threadIdx.x;
+  float acc[kMaxAct + 1][2];
+  float bacc[kMaxAct + 1];
+#pragma unroll
+  for (int o = 0; o <= kMaxAct; ++o) acc[o][0] = acc[o][1] = bacc[o] = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const uint32_t hv = *reinterpret_cast<const uint32_t*>(h + (size_t)r * F + f);
+    const float x0 = bf2f((uint16_t)(hv & 0xffff)), x1 = bf2f((uint16_t)(hv >> 16));
+#pragma unroll
+    for (int o = 0; o <= kMaxAct; ++o)
+      if (o < O) {
+        const float d = dhead[(size_t)r * O + o];
+        acc[o][0] += d * x0;
+        acc[o][1] += d * x1;
+        bacc[o] += d;
+      }
+  }
+  float* out = part + (size_t)blockIdx.x * (O * F + O);
+  // layout = flat param order: policy W [A][F], policy b [A], value W [F], value b [1]
+#pragma unroll
+  for (int o = 0; o <= kMaxAct; ++o)
+    if (o < O) {
+      float* wdst = o < A ? out + o * F : out + A * F + A;
+      wdst[f] = acc[o][0];
+      wdst[f + 1] = acc[o][1];
+    }
+  if (threadIdx.x == 0) {
+    for (int o = 0; o < A; ++o) out[A * F + o] = bacc[o];
+    out[A * F + A + F] = bacc[A];
+  }
+}
+
+}  // namespace rrl
+
+using namespace rrl;
+
+static int grid_for(size_t n, int per_block = 256, int cap = 4096) {
+  size_t g = (n + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > (size_t)cap) g = cap;
+  return (int)g;
+}
+
+extern "C" {
+
+// Forward conv (or fc as a 1x1 conv on H = W = 1): y bf16 [N*OH*OW][Cout].
+int rrl_conv_fwd(const void* x, int x_u8, const uint16_t* w, const float* b, uint16_t* y, int N, int H, int W,
+                 int C, int KH, int KW, int S, int Cout, int relu, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  ConvGeom g{N, H, W, C, KH, KW, S, (H - KH) / S + 1, (W - KW) / S + 1, Cout};
+  const int M = g.M(), K = g.K();
+  RowLoader lw{w, Cout, K};
+  BiasReluStore epi{y, b, M, Cout, relu != 0};
+  if (x_u8) {
+    if (C != 4 || (KW & 1)) return -1;
+    FrameLoader lx{(const uint8_t*)x, H, W, KW, S, g.OH, g.OW, M, K};
+    return Cout >= 64 ? launch_gemm<128, 64, false, false>(lx, lw, epi, M, Cout, K, 1, st)
+                      : launch_gemm<128, 32, false, false>(lx, lw, epi, M, Cout, K, 1, st);
+  }
+  if (C % 8) return -1;
+  ConvLoader lx{(const uint16_t*)x, H, W, C, KW, S, g.OH, g.OW, M, K};
+  return Cout >= 64 ? launch_gemm<128, 64, false, false>(lx, lw, epi, M, Cout, K, 1, st)
+                    : launch_gemm<128, 32, false, false>(lx, lw, epi, M, Cout, K, 1, st);
+}
+
+// dY [M][Cout] . W [Cout][K] -> bf16 [M][K] (masked by mask[M][K] > 0 when given).
+int rrl_gemm_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* mask, uint16_t* out, int M, int Cout,
+                   int K, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  if (Cout % 8 || K % 8) return -1;
+  RowLoader la{dy, M, Cout};
+  RowLoader lb{w, Cout, K};
+  MaskStore epi{out, mask, M, K};
+  return launch_gemm<128, 64, false, true>(la, lb, epi, M, K, Cout, 1, st);
+}
+
+int rrl_col2im_mask(const uint16_t* dcol, const uint16_t* xact, uint16_t* dx, int N, int H, int W, int C, int KH,
+                    int KW, int S, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  ConvGeom g{N, H, W, C, KH, KW, S, (H - KH) / S + 1, (W - KW) / S + 1, 0};
+  if (C % 8) return -1;
+  const size_t total = (size_t)N * H * W * (C / 8);
+  hipLaunchKernelGGL(col2im_mask_kernel, dim3(grid_for(total, 256, 16384)), dim3(256), 0, st, dcol, xact, dx, g);
+  return (int)hipGetLastError();
+}
+
+// dW partials: part [splits][Cout][K] = dY^T . im2col(X) over each split's rows.
+int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, int splits, int N, int H, int W,
+                   int C, int KH, int KW, int S, int Cout, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  ConvGeom g{N, H, W, C, KH, KW, S, (H - KH) / S + 1, (W - KW) / S + 1, Cout};
+  const int M = g.M(), K = g.K();
+  RowLoader la{dy, M, Cout};
+  PartialStore epi{part, Cout, K};
+  // rows of the output = Cout, cols = K, reduction = M (batch x spatial)
+  if (x_u8) {
+    if (C != 4 || (KW & 1)) return -1;
+    FrameLoader lx{(const uint8_t*)x, H, W, KW, S, g.OH, g.OW, M, K};
+    return Cout >= 64 ? launch_gemm<64, 64, true, true>(la, lx, epi, Cout, K, M, splits, st)
+                      : launch_gemm<32, 64, true, true>(la, lx, epi, Cout, K, M, splits, st);
+  }
+  if (C % 8) return -1;
+  ConvLoader lx{(const uint16_t*)x, H, W, C, KW, S, g.OH, g.OW, M, K};
+  return Cout >= 64 ? launch_gemm<64, 64, true, true>(la, lx, epi, Cout, K, M, splits, st)
+                    : launch_gemm<32, 64, true, true>(la, lx, epi, Cout, K, M, splits, st);
+}
+
+// Actual number of splits launch_gemm uses for a reduction of length R.
+int rrl_gemm_splits(int R, int splits) {
+  splits = splits < 1 ? 1 : splits;
+  int kps = (R + splits - 1) / splits;
+  kps = (kps + kGemmBK - 1) / kGemmBK * kGemmBK;
+  return (R + kps - 1) / kps;
+}
+
+int rrl_sum_splits(const float* part, int splits, long long n, float* out, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  hipLaunchKernelGGL(sum_splits_kernel, dim3(grid_for((size_t)n)), dim3(256), 0, st, part, splits, (size_t)n, out);
+  return (int)hipGetLastError();
+}
+
+int rrl_colsum(const uint16_t* y, int M, int C, float* part, int splits, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64, splits), dim3(256), 0, st, y, M, C, part);
+  return (int)hipGetLastError();
+}
+
+int rrl_sumsq(const float* x, long long n, float* work, int work_n, float* out, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  const int g = work_n < 1 ? 1 : (work_n > 1024 ? 1024 : work_n);
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(g), dim3(256), 0, st, x, (size_t)n, work);
+  hipLaunchKernelGGL(sum_small_kernel, dim3(1), dim3(256), 0, st, work, g, out);
+  return (int)hipGetLastError();
+}
+
+int rrl_adam_clip(float* p, float* m, float* v, const float* g, uint16_t* shadow, long long n, const float* norm_sq,
+                  float max_norm, float lr, float b1, float b2, float eps, int step, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
+  hipLaunchKernelGGL(adam_clip_kernel, dim3(grid_for((size_t)n, 256, 8192)), dim3(256), 0, st, p, m, v, g, shadow,
+                     (size_t)n, norm_sq, max_norm, lr, b1, b2, eps, bc1, bc2);
+  return (int)hipGetLastError();
+}
+
+int rrl_to_bf16(const float* x, uint16_t* y, long long n, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  hipLaunchKernelGGL(to_bf16_kernel, dim3(grid_for((size_t)n, 256, 8192)), dim3(256), 0, st, x, y, (size_t)n);
+  return (int)hipGetLastError();
+}
+
+// mode 0: rollout (sample act / logp / value), 1: training (dh, dhead, stats).
+int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, int A, int32_t* act, float* logp,
+                 float* value, float* logits_out, unsigned long long seed, unsigned long long step, int row_offset,
+                 const int32_t* act_in, const float* adv, const float* ret, float inv_B, float vf_coef,
+                 float ent_coef, uint16_t* dh, float* dhead, float* stats, int grid, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  if (A < 1 || A > kMaxAct) return -1;
+  HeadArgs a;
+  a.h = h;
+  a.w = head_params;
+  a.bias = head_params + A * kHeadF;
+  a.w_v = a.bias + A;
+  a.b_v = a.w_v + kHeadF;
+  a.B = B;
+  a.A = A;
+  a.act = act;
+  a.logp = logp;
+  a.value = value;
+  a.logits_out = logits_out;
+  a.seed_lo = (uint32_t)seed;
+  a.seed_hi = (uint32_t)(seed >> 32);
+  a.step_lo = (uint32_t)step;
+  a.step_hi = (uint32_t)(step >> 32);
+  a.row_offset = row_offset;
+  a.act_in = act_in;
+  a.adv = adv;
+  a.ret = ret;
+  a.inv_B = inv_B;
+  a.vf_coef = vf_coef;
+  a.ent_coef = ent_coef;
+  a.dh = dh;
+  a.dhead = dhead;
+  a.stats = stats;
+  const size_t lds = ((size_t)(A + 1) * kHeadF + A + 1) * sizeof(float);
+  if (mode == 0)
+    hipLaunchKernelGGL(a2c_head_kernel<false>, dim3(grid), dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL(a2c_head_kernel<true>, dim3(grid), dim3(256), lds, st, a);
+  return (int)hipGetLastError();
+}
+
+int rrl_head_wgrad(const uint16_t* h, const float* dhead, int B, int A, float* part, int nblk, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  hipLaunchKernelGGL(head_wgrad_kernel, dim3(nblk), dim3(256), 0, st, h, dhead, B, A, part);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,181 @@
+// PongSynth-v0: a device-resident Pong with Atari-style pixel observations, the env of
+// the A2C pixel configuration (BASELINE.json config 4; gymnasium/ALE are absent, so the
+// env is synthetic but keeps the Atari interface: 6 actions, frame-skip 4, 84x84
+// grayscale, 4 stacked frames, +-1 per point, episode ends at 21 points).
+//
+// One thread per env steps the physics (pong_step_kernel); a second kernel renders the
+// 4-frame stack straight into the uint8 NHWC observation tensor the conv stack reads
+// (channel f = frame f, oldest first), so observations never touch the host.
+#include "common.h"
+
+namespace rrl {
+
+constexpr int kPongState = 32;  // floats per env
+constexpr int kPongHW = 84;
+// state layout
+enum : int {
+  P_BX = 0, P_BY, P_VX, P_VY, P_PA, P_PO, P_SA, P_SO, P_T, P_RET,
+  P_HIST = 16  // 4 frames x (bx, by, pa, po)
+};
+constexpr float kTop = 2.f, kBot = 82.f, kPadHalf = 5.f, kBall = 2.f;
+constexpr float kAgentX = 76.f, kOppX = 6.f, kPadW = 2.f;
+constexpr float kPadSpeed = 2.5f, kOppSpeed = 1.6f, kMaxVy = 3.0f, kMaxVx = 3.0f;
+
+RRL_DEV void serve(float* s, uint4 r) {
+  s[P_BX] = 41.f;
+  s[P_BY] = 30.f + 24.f * u01(r.x);
+  s[P_VX] = (r.y & 1) ? 1.5f : -1.5f;
+  s[P_VY] = (u01(r.z) - 0.5f) * 3.0f;
+}
+
+RRL_DEV void push_hist(float* s) {
+#pragma unroll
+  for (int f = 0; f < 3; ++f)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[P_HIST + 4 * f + j] = s[P_HIST + 4 * (f + 1) + j];
+  s[P_HIST + 12] = s[P_BX];
+  s[P_HIST + 13] = s[P_BY];
+  s[P_HIST + 14] = s[P_PA];
+  s[P_HIST + 15] = s[P_PO];
+}
+
+RRL_DEV void reset_env(float* s, uint4 r) {
+  for (int i = 0; i < kPongState; ++i) s[i] = 0.f;
+  s[P_PA] = 42.f;
+  s[P_PO] = 42.f;
+  serve(s, r);
+  for (int f = 0; f < 4; ++f) push_hist(s);
+}
+
+__global__ void pong_step_kernel(float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew,
+                                 float* __restrict__ done, float* __restrict__ fin_ret, float* __restrict__ fin_len,
+                                 int N, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
+                                 int reset_all) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N) return;
+  float s[kPongState];
+#pragma unroll
+  for (int i = 0; i < kPongState; ++i) s[i] = state[(size_t)e * kPongState + i];
+  const uint4 r0 = philox4x32(make_uint4((uint32_t)e, step_lo, step_hi, 0x51u), key);
+  if (reset_all) {
+    reset_env(s, r0);
+  } else {
+    const int a = act[e];
+    const float dir = (a == 2 || a == 4) ? -1.f : ((a == 3 || a == 5) ? 1.f : 0.f);  // RIGHT = up, LEFT = down
+    float reward = 0.f;
+    bool point = false;
+    for (int sub = 0; sub < 4 && !point; ++sub) {
+      s[P_PA] = fminf(fmaxf(s[P_PA] + dir * kPadSpeed, kTop + kPadHalf), kBot - kPadHalf);
+      // opponent tracks the ball when it approaches, drifts to centre otherwise
+      const float target = s[P_VX] < 0.f ? s[P_BY] + 1.f : 42.f;
+      const float d = fminf(fmaxf(target - s[P_PO], -kOppSpeed), kOppSpeed);
+      s[P_PO] = fminf(fmaxf(s[P_PO] + d, kTop + kPadHalf), kBot - kPadHalf);
+      float bx = s[P_BX] + s[P_VX], by = s[P_BY] + s[P_VY];
+      if (by < kTop) { by = 2.f * kTop - by; s[P_VY] = -s[P_VY]; }
+      if (by + kBall > kBot) { by = 2.f * (kBot - kBall) - by; s[P_VY] = -s[P_VY]; }
+      const float cy = by + 0.5f * kBall;
+      if (s[P_VX] > 0.f && bx + kBall >= kAgentX && s[P_BX] + kBall <= kAgentX + kPadW &&
+          fabsf(cy - s[P_PA]) <= kPadHalf + 1.f) {
+        bx = kAgentX - kBall;
+        s[P_VX] = -fminf(fabsf(s[P_VX]) * 1.05f, kMaxVx);
+        s[P_VY] = fminf(fmaxf(s[P_VY] + 0.35f * (cy - s[P_PA]), -kMaxVy), kMaxVy);
+      } else if (s[P_VX] < 0.f && bx <= kOppX + kPadW && s[P_BX] >= kOppX && fabsf(cy - s[P_PO]) <= kPadHalf + 1.f) {
+        bx = kOppX + kPadW;
+        s[P_VX] = fminf(fabsf(s[P_VX]) * 1.05f, kMaxVx);
+        s[P_VY] = fminf(fmaxf(s[P_VY] + 0.35f * (cy - s[P_PO]), -kMaxVy), kMaxVy);
+      }
+      s[P_BX] = bx;
+      s[P_BY] = by;
+      if (bx > (float)kPongHW) {  // opponent scores
+        reward -= 1.f;
+        s[P_SO] += 1.f;
+        point = true;
+      } else if (bx + kBall < 0.f) {  // agent scores
+        reward += 1.f;
+        s[P_SA] += 1.f;
+        point = true;
+      }
+    }
+    if (point) serve(s, r0);
+    s[P_T] += 1.f;
+    s[P_RET] += reward;
+    push_hist(s);
+    const bool over = s[P_SA] >= 21.f || s[P_SO] >= 21.f || (max_steps > 0 && s[P_T] >= (float)max_steps);
+    rew[e] = reward;
+    done[e] = over ? 1.f : 0.f;
+    fin_ret[e] = over ? s[P_RET] : 0.f;
+    fin_len[e] = over ? s[P_T] : 0.f;
+    if (over) {
+      const uint4 r1 = philox4x32(make_uint4((uint32_t)e, step_lo, step_hi, 0x52u), key);
+      reset_env(s, r1);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kPongState; ++i) state[(size_t)e * kPongState + i] = s[i];
+}
+
+// One thread per (env, row): 84 pixels x 4 frames = 21 x 16 B.
+__global__ void pong_render_kernel(const float* __restrict__ state, uint8_t* __restrict__ obs, int N) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= (size_t)N * kPongHW) return;
+  const int e = (int)(t / kPongHW), y = (int)(t % kPongHW);
+  const float* h = state + (size_t)e * kPongState + P_HIST;
+  const float fy = (float)y + 0.5f;
+  const bool wall = fy < kTop || fy >= kBot;
+  uint8_t* row = obs + ((size_t)e * kPongHW + y) * kPongHW * 4;
+  // per-frame horizontal spans on this row
+  float bx0[4], pa_on[4], po_on[4], b_on[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const float bx = h[4 * f], by = h[4 * f + 1], pa = h[4 * f + 2], po = h[4 * f + 3];
+    bx0[f] = bx;
+    b_on[f] = (fy >= by && fy < by + kBall) ? 1.f : 0.f;
+    pa_on[f] = fabsf(fy - pa) < kPadHalf ? 1.f : 0.f;
+    po_on[f] = fabsf(fy - po) < kPadHalf ? 1.f : 0.f;
+  }
+  for (int c = 0; c < 21; ++c) {
+    uint32_t w[4];
+#pragma unroll
+    for (int px = 0; px < 4; ++px) {
+      const int x = 4 * c + px;
+      const float fx = (float)x + 0.5f;
+      uint32_t v = 0;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        uint32_t p = wall ? 100u : 0u;
+        if (pa_on[f] > 0.f && fx >= kAgentX && fx < kAgentX + kPadW) p = 255u;
+        if (po_on[f] > 0.f && fx >= kOppX && fx < kOppX + kPadW) p = 255u;
+        if (b_on[f] > 0.f && fx >= bx0[f] && fx < bx0[f] + kBall) p = 255u;
+        v |= p << (8 * f);
+      }
+      w[px] = v;
+    }
+    *reinterpret_cast<uint4*>(row + 16 * c) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+}  // namespace rrl
+
+using namespace rrl;
+
+extern "C" {
+
+int rrl_pong_state_size() { return kPongState; }
+
+int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len, int N,
+                  unsigned long long seed, unsigned long long step, int max_steps, int reset_all, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  hipLaunchKernelGGL(pong_step_kernel, dim3((N + 255) / 256), dim3(256), 0, st, state, act, rew, done, fin_ret,
+                     fin_len, N, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, reset_all);
+  return (int)hipGetLastError();
+}
+
+int rrl_pong_render(const float* state, uint8_t* obs, int N, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  const size_t t = (size_t)N * kPongHW;
+  hipLaunchKernelGGL(pong_render_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, state, obs, N);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -102,15 +102,17 @@ def build_hip(verbose=False, force=False) -> str:
             jobs.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                          "-munsafe-fp-atomics", "-I", kdir, "-c", s, "-o", o])
     tinc, tcf, tld = _torch_flags()
-    bo = os.path.join(odir, "hip_ops.cpp.o")
-    objs.append(bo)
-    if force or _newer(bo, [binding]):
-        cmd = [CXX, "-O2", "-std=c++17", "-fPIC", "-DTORCH_EXTENSION_NAME=_hip_ops",
-               "-DTORCH_API_INCLUDE_EXTENSION_H", "-I/opt/rocm/include"] + tcf
-        for i in tinc + _py_includes():
-            cmd += ["-I", i]
-        cmd += ["-c", binding, "-o", bo]
-        jobs.append(cmd)
+    bindings = [binding] + sorted(b for b in glob.glob(os.path.join(CSRC, "bindings", "*_ops.cpp")) if b != binding)
+    for bsrc in bindings:
+        bo = os.path.join(odir, os.path.basename(bsrc) + ".o")
+        objs.append(bo)
+        if force or _newer(bo, [bsrc]):
+            cmd = [CXX, "-O2", "-std=c++17", "-fPIC", "-DTORCH_EXTENSION_NAME=_hip_ops",
+                   "-DTORCH_API_INCLUDE_EXTENSION_H", "-I/opt/rocm/include"] + tcf
+            for i in tinc + _py_includes():
+                cmd += ["-I", i]
+            cmd += ["-c", bsrc, "-o", bo]
+            jobs.append(cmd)
     with cf.ThreadPoolExecutor(_jobs()) as ex:
         list(ex.map(lambda c: _run(c, verbose), jobs))
     if force or _newer(HIP_OPS, objs):

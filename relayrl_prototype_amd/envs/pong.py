@@ -1,0 +1,192 @@
+"""PongSynth-v0 -- device Pong with Atari-style observations (csrc/kernels/pong.hip).
+
+``PongRef`` is the vectorised numpy oracle of the kernel (same state layout, same
+float32 arithmetic order, same Philox draws), used by the CPU trainer path and by the
+GPU numerics tests; ``DevicePong`` drives the kernels on a torch device.
+
+Interface (Atari Pong): 6 actions (0 NOOP, 1 FIRE, 2 RIGHT = up, 3 LEFT = down,
+4 RIGHTFIRE, 5 LEFTFIRE), frame-skip 4, observation uint8 [84, 84, 4] NHWC with the 4
+most recent frames (oldest first), reward +1 / -1 per point, episode over at 21 points
+(or ``max_steps`` agent steps).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..ops.philox import philox4x32, u01
+
+NUM_ACTIONS = 6
+OBS_SHAPE = (84, 84, 4)
+STATE = 32
+HW = 84
+BX, BY, VX, VY, PA, PO, SA, SO, T, RET = range(10)
+HIST = 16
+TOP, BOT, PAD_HALF, BALL = 2.0, 82.0, 5.0, 2.0
+AGENT_X, OPP_X, PAD_W = 76.0, 6.0, 2.0
+PAD_SPEED, OPP_SPEED, MAX_VY, MAX_VX = 2.5, 1.6, 3.0, 3.0
+
+f32 = np.float32
+
+
+def _rand(seed, step, rows, tag):
+    k0, k1 = np.uint32(seed & 0xFFFFFFFF), np.uint32((seed >> 32) & 0xFFFFFFFF)
+    return philox4x32(rows.astype(np.uint32), np.full_like(rows, step & 0xFFFFFFFF, dtype=np.uint32),
+                      np.full_like(rows, (step >> 32) & 0xFFFFFFFF, dtype=np.uint32),
+                      np.full_like(rows, tag, dtype=np.uint32), k0, k1)
+
+
+class PongRef:
+    def __init__(self, num_envs: int, seed: int = 0, max_steps: int = 27000 // 4):
+        self.N = int(num_envs)
+        self.seed = int(seed)
+        self.max_steps = int(max_steps)
+        self.s = np.zeros((self.N, STATE), f32)
+        self.step_count = 0
+
+    # --- pieces shared with the kernel
+    def _serve(self, s, idx, r):
+        s[idx, BX] = f32(41.0)
+        s[idx, BY] = f32(30.0) + f32(24.0) * u01(r[0][idx])
+        s[idx, VX] = np.where(r[1][idx] & 1, f32(1.5), f32(-1.5))
+        s[idx, VY] = (u01(r[2][idx]) - f32(0.5)) * f32(3.0)
+
+    @staticmethod
+    def _push_hist(s, idx):
+        h = s[idx, HIST:HIST + 16].reshape(-1, 4, 4)
+        h[:, :3] = h[:, 1:].copy()
+        h[:, 3] = s[idx][:, [BX, BY, PA, PO]]
+        s[idx, HIST:HIST + 16] = h.reshape(-1, 16)
+
+    def _reset(self, s, idx, r):
+        s[idx] = 0
+        s[idx, PA] = 42.0
+        s[idx, PO] = 42.0
+        self._serve(s, idx, r)
+        for _ in range(4):
+            self._push_hist(s, idx)
+
+    def reset(self):
+        rows = np.arange(self.N, dtype=np.uint32)
+        r = _rand(self.seed, self.step_count, rows, 0x51)
+        self._reset(self.s, np.arange(self.N), r)
+        self.step_count += 1
+        return self.render()
+
+    def step(self, act):
+        s = self.s
+        N = self.N
+        rows = np.arange(N, dtype=np.uint32)
+        r0 = _rand(self.seed, self.step_count, rows, 0x51)
+        a = np.asarray(act).reshape(N)
+        d = np.where((a == 2) | (a == 4), f32(-1), np.where((a == 3) | (a == 5), f32(1), f32(0))).astype(f32)
+        reward = np.zeros(N, f32)
+        point = np.zeros(N, bool)
+        for _ in range(4):
+            live = ~point
+            pa = np.clip(s[:, PA] + d * f32(PAD_SPEED), f32(TOP + PAD_HALF), f32(BOT - PAD_HALF))
+            s[:, PA] = np.where(live, pa, s[:, PA])
+            target = np.where(s[:, VX] < 0, s[:, BY] + f32(1), f32(42))
+            dd = np.clip(target - s[:, PO], f32(-OPP_SPEED), f32(OPP_SPEED))
+            po = np.clip(s[:, PO] + dd, f32(TOP + PAD_HALF), f32(BOT - PAD_HALF))
+            s[:, PO] = np.where(live, po, s[:, PO])
+            bx = s[:, BX] + s[:, VX]
+            by = s[:, BY] + s[:, VY]
+            vy = s[:, VY].copy()
+            lo = by < f32(TOP)
+            by = np.where(lo, f32(2 * TOP) - by, by)
+            vy = np.where(lo, -vy, vy)
+            hi = by + f32(BALL) > f32(BOT)
+            by = np.where(hi, f32(2 * (BOT - BALL)) - by, by)
+            vy = np.where(hi, -vy, vy)
+            cy = by + f32(0.5 * BALL)
+            vx = s[:, VX].copy()
+            hit_a = (vx > 0) & (bx + f32(BALL) >= f32(AGENT_X)) & (s[:, BX] + f32(BALL) <= f32(AGENT_X + PAD_W)) & \
+                (np.abs(cy - s[:, PA]) <= f32(PAD_HALF + 1))
+            hit_o = ~hit_a & (vx < 0) & (bx <= f32(OPP_X + PAD_W)) & (s[:, BX] >= f32(OPP_X)) & \
+                (np.abs(cy - s[:, PO]) <= f32(PAD_HALF + 1))
+            bx = np.where(hit_a, f32(AGENT_X - BALL), np.where(hit_o, f32(OPP_X + PAD_W), bx))
+            spd = np.minimum(np.abs(vx) * f32(1.05), f32(MAX_VX))
+            vy_a = np.clip(vy + f32(0.35) * (cy - s[:, PA]), f32(-MAX_VY), f32(MAX_VY))
+            vy_o = np.clip(vy + f32(0.35) * (cy - s[:, PO]), f32(-MAX_VY), f32(MAX_VY))
+            new_vx = np.where(hit_a, -spd, np.where(hit_o, spd, vx))
+            new_vy = np.where(hit_a, vy_a, np.where(hit_o, vy_o, vy))
+            s[:, BX] = np.where(live, bx, s[:, BX])
+            s[:, BY] = np.where(live, by, s[:, BY])
+            s[:, VX] = np.where(live, new_vx, s[:, VX])
+            s[:, VY] = np.where(live, new_vy, s[:, VY])
+            opp = live & (bx > f32(HW))
+            ag = live & ~opp & (bx + f32(BALL) < f32(0))
+            reward = reward - opp.astype(f32) + ag.astype(f32)
+            s[:, SO] += opp
+            s[:, SA] += ag
+            point |= opp | ag
+        if point.any():
+            self._serve(s, np.flatnonzero(point), r0)
+        s[:, T] += 1
+        s[:, RET] += reward
+        self._push_hist(s, np.arange(N))
+        over = (s[:, SA] >= 21) | (s[:, SO] >= 21) | ((self.max_steps > 0) & (s[:, T] >= self.max_steps))
+        fin_ret = np.where(over, s[:, RET], 0).astype(f32)
+        fin_len = np.where(over, s[:, T], 0).astype(f32)
+        if over.any():
+            r1 = _rand(self.seed, self.step_count, rows, 0x52)
+            self._reset(s, np.flatnonzero(over), r1)
+        self.step_count += 1
+        return reward, over.astype(f32), fin_ret, fin_len
+
+    def render(self) -> np.ndarray:
+        N = self.N
+        h = self.s[:, HIST:HIST + 16].reshape(N, 4, 4)
+        fy = np.arange(HW, dtype=f32) + f32(0.5)
+        fx = fy
+        wall = (fy < TOP) | (fy >= BOT)
+        obs = np.where(wall[None, :, None, None], np.uint8(100), np.uint8(0)).astype(np.uint8)
+        obs = np.broadcast_to(obs, (N, HW, HW, 4)).copy()
+        for f in range(4):
+            bx, by, pa, po = h[:, f, 0], h[:, f, 1], h[:, f, 2], h[:, f, 3]
+            rows_pa = np.abs(fy[None] - pa[:, None]) < PAD_HALF
+            rows_po = np.abs(fy[None] - po[:, None]) < PAD_HALF
+            rows_b = (fy[None] >= by[:, None]) & (fy[None] < by[:, None] + BALL)
+            cols_a = (fx >= AGENT_X) & (fx < AGENT_X + PAD_W)
+            cols_o = (fx >= OPP_X) & (fx < OPP_X + PAD_W)
+            cols_b = (fx[None] >= bx[:, None]) & (fx[None] < bx[:, None] + BALL)
+            m = (rows_pa[:, :, None] & cols_a[None, None, :]) | (rows_po[:, :, None] & cols_o[None, None, :]) | \
+                (rows_b[:, :, None] & cols_b[:, None, :])
+            obs[..., f] = np.where(m, np.uint8(255), obs[..., f])
+        return obs
+
+
+class DevicePong:
+    """Kernel-driven batch of PongSynth envs on one device."""
+
+    def __init__(self, num_envs: int, device, seed: int = 0, max_steps: int = 27000 // 4):
+        from ..ops import hip
+
+        self.h = hip()
+        self.N = int(num_envs)
+        self.seed = int(seed) & 0x7FFFFFFFFFFFFFFF
+        self.max_steps = int(max_steps)
+        dev = torch.device(device)
+        self.state = torch.zeros(self.N * int(self.h.pong_state_size()), device=dev)
+        self.rew = torch.zeros(self.N, device=dev)
+        self.done = torch.zeros(self.N, device=dev)
+        self.fin_ret = torch.zeros(self.N, device=dev)
+        self.fin_len = torch.zeros(self.N, device=dev)
+        self._dummy_act = torch.zeros(self.N, dtype=torch.int32, device=dev)
+        self.step_count = 0
+
+    def reset(self, obs_out: torch.Tensor):
+        self.h.pong_step(self.state, self._dummy_act, self.rew, self.done, self.fin_ret, self.fin_len, self.N,
+                         self.seed, self.step_count, self.max_steps, True)
+        self.step_count += 1
+        self.h.pong_render(self.state, obs_out, self.N)
+
+    def step(self, act: torch.Tensor, obs_out: torch.Tensor, rew_out=None, done_out=None):
+        rew = self.rew if rew_out is None else rew_out
+        done = self.done if done_out is None else done_out
+        self.h.pong_step(self.state, act, rew, done, self.fin_ret, self.fin_len, self.N, self.seed, self.step_count,
+                         self.max_steps, False)
+        self.step_count += 1
+        self.h.pong_render(self.state, obs_out, self.N)
+        return rew, done

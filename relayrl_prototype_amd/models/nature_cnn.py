@@ -1,0 +1,337 @@
+"""Nature-CNN actor-critic for pixel observations (A2C / Pong configuration, BASELINE.json
+config 4 -- a model family the reference does not have; SURVEY §2.6 "New: CNN encoder").
+
+    obs uint8 [B, 84, 84, 4] (NHWC, 4 stacked frames)
+    conv 8x8/4  4 -> 32, ReLU      (84 -> 20)
+    conv 4x4/2 32 -> 64, ReLU      (20 -> 9)
+    conv 3x3/1 64 -> 64, ReLU      (9 -> 7)
+    fc 3136 -> 512, ReLU           (NHWC flatten)
+    policy 512 -> A, value 512 -> 1
+
+Parameters are ONE flat fp32 vector (master copy for Adam and the RCCL all-reduce) with
+conv weights stored [Cout][KH][KW][Cin] so that the implicit-GEMM reduction index
+(kh, kw, c) is contiguous in both operands; the device path keeps a bf16 shadow copy
+of the same vector for the MFMA GEMMs (written by the fused Adam).
+
+``DeviceNatureCNN`` runs everything through the gfx950 kernels (csrc/kernels/cnn.hip);
+``reference_forward`` is the fp32 (optionally bf16-emulating) PyTorch oracle the kernels
+are tested against and the CPU path of the trainer.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+import torch.nn.functional as F
+
+FRAME_HW = 84
+FRAMES = 4
+HIDDEN = 512
+
+
+@dataclass(frozen=True)
+class ConvLayer:
+    cin: int
+    cout: int
+    k: int
+    s: int
+    hin: int
+
+    @property
+    def hout(self) -> int:
+        return (self.hin - self.k) // self.s + 1
+
+    @property
+    def K(self) -> int:
+        return self.k * self.k * self.cin
+
+
+CONVS = (ConvLayer(FRAMES, 32, 8, 4, FRAME_HW), ConvLayer(32, 64, 4, 2, 20), ConvLayer(64, 64, 3, 1, 9))
+FC_IN = CONVS[-1].hout ** 2 * CONVS[-1].cout  # 3136
+
+
+@dataclass(frozen=True)
+class CNNSpec:
+    act_dim: int = 6
+
+    def offsets(self) -> Dict[str, int]:
+        o, off = {}, 0
+        for i, L in enumerate(CONVS, 1):
+            o[f"w{i}"] = off
+            off += L.cout * L.K
+            o[f"b{i}"] = off
+            off += L.cout
+        o["wfc"] = off
+        off += HIDDEN * FC_IN
+        o["bfc"] = off
+        off += HIDDEN
+        o["head"] = o["wpi"] = off
+        off += self.act_dim * HIDDEN
+        o["bpi"] = off
+        off += self.act_dim
+        o["wv"] = off
+        off += HIDDEN
+        o["bv"] = off
+        off += 1
+        o["P"] = off
+        return o
+
+    @property
+    def P(self) -> int:
+        return self.offsets()["P"]
+
+    @property
+    def head_size(self) -> int:
+        return (self.act_dim + 1) * HIDDEN + self.act_dim + 1
+
+    def init(self, seed: int = 0, device="cpu") -> torch.Tensor:
+        """Orthogonal init (gain sqrt(2) trunk, 0.01 policy, 1 value), zero biases -- the
+        usual A2C/Atari recipe."""
+        g = torch.Generator().manual_seed(int(seed))
+        o = self.offsets()
+        p = torch.zeros(o["P"])
+
+        def orth(rows, cols, gain):
+            w = torch.empty(rows, cols)
+            torch.nn.init.orthogonal_(w, gain=gain, generator=g)
+            return w.reshape(-1)
+
+        for i, L in enumerate(CONVS, 1):
+            p[o[f"w{i}"]:o[f"b{i}"]] = orth(L.cout, L.K, 2 ** 0.5)
+        p[o["wfc"]:o["bfc"]] = orth(HIDDEN, FC_IN, 2 ** 0.5)
+        p[o["wpi"]:o["bpi"]] = orth(self.act_dim, HIDDEN, 0.01)
+        p[o["wv"]:o["bv"]] = orth(1, HIDDEN, 1.0)
+        return p.to(device)
+
+    def views(self, params: torch.Tensor):
+        o = self.offsets()
+        v = {}
+        for i, L in enumerate(CONVS, 1):
+            v[f"w{i}"] = params[o[f"w{i}"]:o[f"b{i}"]].view(L.cout, L.k, L.k, L.cin)
+            v[f"b{i}"] = params[o[f"b{i}"]:o[f"b{i}"] + L.cout]
+        v["wfc"] = params[o["wfc"]:o["bfc"]].view(HIDDEN, FC_IN)
+        v["bfc"] = params[o["bfc"]:o["bfc"] + HIDDEN]
+        v["wpi"] = params[o["wpi"]:o["bpi"]].view(self.act_dim, HIDDEN)
+        v["bpi"] = params[o["bpi"]:o["bpi"] + self.act_dim]
+        v["wv"] = params[o["wv"]:o["bv"]]
+        v["bv"] = params[o["bv"]:o["bv"] + 1]
+        v["head"] = params[o["head"]:o["P"]]
+        return v
+
+
+def _bf(x, emulate: bool):
+    return x.to(torch.bfloat16).float() if emulate else x
+
+
+def reference_forward(spec: CNNSpec, params: torch.Tensor, obs_u8: torch.Tensor, emulate_bf16: bool = False):
+    """fp32 oracle.  ``emulate_bf16`` rounds weights, the scaled input and every stored
+    activation to bf16 exactly where the device path does.  Returns (logits, value, acts)."""
+    v = spec.views(params)
+    x = _bf(obs_u8.float() / 255.0, emulate_bf16).permute(0, 3, 1, 2)
+    acts = []
+    for i, L in enumerate(CONVS, 1):
+        w = _bf(v[f"w{i}"], emulate_bf16).permute(0, 3, 1, 2)
+        x = _bf(F.relu(F.conv2d(x, w, v[f"b{i}"], stride=L.s)), emulate_bf16)
+        acts.append(x)
+    flat = x.permute(0, 2, 3, 1).reshape(x.shape[0], FC_IN)
+    h = _bf(F.relu(flat @ _bf(v["wfc"], emulate_bf16).t() + v["bfc"]), emulate_bf16)
+    logits = h @ v["wpi"].t() + v["bpi"]
+    value = h @ v["wv"] + v["bv"]
+    return logits, value, acts + [h]
+
+
+def a2c_loss(logits, value, act, adv, ret, vf_coef: float, ent_coef: float):
+    logp_all = torch.log_softmax(logits, -1)
+    logp = logp_all.gather(1, act.long()[:, None])[:, 0]
+    ent = -(logp_all.exp() * logp_all).sum(-1)
+    pg = -(adv * logp).mean()
+    vf = ((value - ret) ** 2).mean()
+    return pg + vf_coef * vf - ent_coef * ent.mean(), pg, vf, ent.mean()
+
+
+class DeviceNatureCNN:
+    """Kernel-backed model: forward (rollout + stored activations), A2C backward, Adam."""
+
+    def __init__(self, spec: CNNSpec, device, max_batch: int, seed: int = 0, params: Optional[torch.Tensor] = None):
+        from ..ops import hip, use_hip
+
+        self.spec = spec
+        self.device = torch.device(device)
+        self.A = spec.act_dim
+        self.max_batch = int(max_batch)
+        self.params = (spec.init(seed) if params is None else params.detach().float().cpu()).to(self.device)
+        if not use_hip(self.params):
+            raise RuntimeError("DeviceNatureCNN needs a GPU tensor (CPU runs use reference_forward)")
+        self.h = hip()
+        self.o = spec.offsets()
+        self.P = self.o["P"]
+        dev = self.device
+        self.shadow = torch.empty(self.P, dtype=torch.bfloat16, device=dev)
+        self.h.to_bf16(self.params, self.shadow)
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.grad = torch.zeros_like(self.params)
+        self.step_count = 0
+        B = self.max_batch
+        bf = torch.bfloat16
+        L1, L2, L3 = CONVS
+        self.a1 = torch.empty(B * L1.hout ** 2 * L1.cout, dtype=bf, device=dev)
+        self.a2 = torch.empty(B * L2.hout ** 2 * L2.cout, dtype=bf, device=dev)
+        self.a3 = torch.empty(B * FC_IN, dtype=bf, device=dev)
+        self.hid = torch.empty(B * HIDDEN, dtype=bf, device=dev)
+        # backward buffers
+        self.dh = torch.empty(B * HIDDEN, dtype=bf, device=dev)
+        self.da3 = torch.empty(B * FC_IN, dtype=bf, device=dev)
+        self.dcol3 = torch.empty(B * L3.hout ** 2 * L3.K, dtype=bf, device=dev)
+        self.da2 = torch.empty(B * L2.hout ** 2 * L2.cout, dtype=bf, device=dev)
+        self.dcol2 = torch.empty(B * L2.hout ** 2 * L2.K, dtype=bf, device=dev)
+        self.da1 = torch.empty(B * L1.hout ** 2 * L1.cout, dtype=bf, device=dev)
+        self.dhead = torch.empty(B * (self.A + 1), dtype=torch.float32, device=dev)
+        self.head_grid = max(1, min(1024, (B + 3) // 4))
+        self.stats = torch.empty(self.head_grid * 4, device=dev)
+        self.head_blocks = max(1, min(256, (B + 31) // 32))
+        self.head_part = torch.empty(self.head_blocks * spec.head_size, device=dev)
+        # split-K plan for the weight gradients (enough workgroups to fill 256 CUs)
+        self._wplan = {}
+        need = self.head_blocks * spec.head_size
+        for name, cout, K, M in self._wgrad_layers(B):
+            tiles = -(-cout // 64) * -(-K // 64)
+            s = int(self.h.gemm_splits(M, max(1, min(512 // max(tiles, 1), -(-M // 64)))))
+            self._wplan[name] = s
+            need = max(need, s * cout * K)
+        self.part = torch.empty(need, device=dev)
+        self.bias_splits = 64
+        self.bias_part = torch.empty(self.bias_splits * HIDDEN, device=dev)
+        self.sq_work = torch.empty(1024, device=dev)
+        self.norm_sq = torch.empty(1, device=dev)
+
+    @staticmethod
+    def _wgrad_layers(B):
+        L1, L2, L3 = CONVS
+        return [("fc", HIDDEN, FC_IN, B), ("c3", L3.cout, L3.K, B * L3.hout ** 2),
+                ("c2", L2.cout, L2.K, B * L2.hout ** 2), ("c1", L1.cout, L1.K, B * L1.hout ** 2)]
+
+    # ------------------------------------------------------------------ forward
+    def _rows(self, buf, row0, rows, per_row):
+        return buf[row0 * per_row:(row0 + rows) * per_row]
+
+    def forward(self, obs_u8: torch.Tensor, row0: int = 0):
+        """Conv stack + fc on obs [n, 84, 84, 4]; activations land in rows row0.. of the
+        stored buffers.  Returns the hidden [n * 512] view."""
+        n = obs_u8.shape[0]
+        assert row0 + n <= self.max_batch, "batch exceeds the model's activation buffers"
+        h, o, sh, p = self.h, self.o, self.shadow, self.params
+        L1, L2, L3 = CONVS
+        a1 = self._rows(self.a1, row0, n, L1.hout ** 2 * L1.cout)
+        a2 = self._rows(self.a2, row0, n, L2.hout ** 2 * L2.cout)
+        a3 = self._rows(self.a3, row0, n, FC_IN)
+        hid = self._rows(self.hid, row0, n, HIDDEN)
+        x = obs_u8.contiguous()
+        for i, (L, y) in enumerate(zip(CONVS, (a1, a2, a3)), 1):
+            h.conv_fwd(x, sh[o[f"w{i}"]:o[f"b{i}"]], p[o[f"b{i}"]:o[f"b{i}"] + L.cout], y, n, L.hin, L.hin, L.cin,
+                       L.k, L.k, L.s, L.cout, True)
+            x = y
+        h.conv_fwd(a3, sh[o["wfc"]:o["bfc"]], p[o["bfc"]:o["bfc"] + HIDDEN], hid, n, 1, 1, FC_IN, 1, 1, 1, HIDDEN,
+                   True)
+        return hid
+
+    def act(self, obs_u8, row0, act_out, logp_out, value_out, seed: int, step: int, row_offset: int = 0):
+        hid = self.forward(obs_u8, row0)
+        n = obs_u8.shape[0]
+        self.h.a2c_head(0, hid, self.params[self.o["head"]:], n, self.A, act_out, logp_out, value_out, None,
+                        int(seed), int(step), int(row_offset), None, None, None, 0.0, 0.0, 0.0, None, None, None,
+                        max(1, min(1024, (n + 3) // 4)))
+
+    def value(self, obs_u8, row0, value_out):
+        hid = self.forward(obs_u8, row0)
+        n = obs_u8.shape[0]
+        self.h.a2c_head(0, hid, self.params[self.o["head"]:], n, self.A, None, None, value_out, None, 0, 0, 0, None,
+                        None, None, 0.0, 0.0, 0.0, None, None, None, max(1, min(1024, (n + 3) // 4)))
+
+    def logits(self, obs_u8):
+        n = obs_u8.shape[0]
+        hid = self.forward(obs_u8, 0)
+        lg = torch.empty(n, self.A, device=self.device)
+        val = torch.empty(n, device=self.device)
+        self.h.a2c_head(0, hid, self.params[self.o["head"]:], n, self.A, None, None, val, lg, 0, 0, 0, None, None,
+                        None, 0.0, 0.0, 0.0, None, None, None, max(1, min(1024, (n + 3) // 4)))
+        return lg, val
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, obs_u8: torch.Tensor, act: torch.Tensor, adv: torch.Tensor, ret: torch.Tensor,
+                 vf_coef: float, ent_coef: float) -> torch.Tensor:
+        """A2C gradients into ``self.grad`` from the activations stored by ``forward`` for
+        rows 0..B-1.  Returns the per-block loss stats [grid, 4] (pg, vf, ent, count)."""
+        h, o, sh, g = self.h, self.o, self.shadow, self.grad
+        B = obs_u8.shape[0]
+        L1, L2, L3 = CONVS
+        a1 = self.a1[:B * L1.hout ** 2 * L1.cout]
+        a2 = self.a2[:B * L2.hout ** 2 * L2.cout]
+        a3 = self.a3[:B * FC_IN]
+        hid = self.hid[:B * HIDDEN]
+        dh = self.dh[:B * HIDDEN]
+        dhead = self.dhead[:B * (self.A + 1)]
+        grid = max(1, min(self.head_grid, (B + 3) // 4))
+        stats = self.stats[:grid * 4]
+        h.a2c_head(1, hid, self.params[o["head"]:], B, self.A, None, None, None, None, 0, 0, 0, act, adv, ret,
+                   1.0 / B, float(vf_coef), float(ent_coef), dh, dhead, stats, grid)
+        nb = max(1, min(self.head_blocks, B))
+        hp = self.head_part[:nb * self.spec.head_size]
+        h.head_wgrad(hid, dhead, B, self.A, hp, nb)
+        h.sum_splits(hp, nb, self.spec.head_size, g[o["head"]:o["P"]])
+        # fc
+        self._wgrad("fc", dh, a3, B, 1, FC_IN, 1, 1, HIDDEN, o["wfc"])
+        self._bias(dh, B, HIDDEN, o["bfc"])
+        da3 = self.da3[:B * FC_IN]
+        h.gemm_dgrad(dh, sh[o["wfc"]:o["bfc"]], a3, da3, B, HIDDEN, FC_IN)
+        # conv3
+        self._wgrad("c3", da3, a2, B, L3.hin, L3.cin, L3.k, L3.s, L3.cout, o["w3"])
+        self._bias(da3, B * L3.hout ** 2, L3.cout, o["b3"])
+        dcol3 = self.dcol3[:B * L3.hout ** 2 * L3.K]
+        h.gemm_dgrad(da3, sh[o["w3"]:o["b3"]], None, dcol3, B * L3.hout ** 2, L3.cout, L3.K)
+        da2 = self.da2[:B * L2.hout ** 2 * L2.cout]
+        h.col2im_mask(dcol3, a2, da2, B, L3.hin, L3.hin, L3.cin, L3.k, L3.k, L3.s)
+        # conv2
+        self._wgrad("c2", da2, a1, B, L2.hin, L2.cin, L2.k, L2.s, L2.cout, o["w2"])
+        self._bias(da2, B * L2.hout ** 2, L2.cout, o["b2"])
+        dcol2 = self.dcol2[:B * L2.hout ** 2 * L2.K]
+        h.gemm_dgrad(da2, sh[o["w2"]:o["b2"]], None, dcol2, B * L2.hout ** 2, L2.cout, L2.K)
+        da1 = self.da1[:B * L1.hout ** 2 * L1.cout]
+        h.col2im_mask(dcol2, a1, da1, B, L2.hin, L2.hin, L2.cin, L2.k, L2.k, L2.s)
+        # conv1 (input = frames, no data gradient)
+        self._wgrad("c1", da1, obs_u8.contiguous(), B, L1.hin, L1.cin, L1.k, L1.s, L1.cout, o["w1"])
+        self._bias(da1, B * L1.hout ** 2, L1.cout, o["b1"])
+        return stats.view(grid, 4)
+
+    def _wgrad(self, name, dy, x, N, H, C, k, s, cout, off):
+        K = k * k * C
+        splits = int(self.h.conv_wgrad(dy, x, self.part, self._wplan[name], N, H, H, C, k, k, s, cout))
+        self.h.sum_splits(self.part, splits, cout * K, self.grad[off:off + cout * K])
+
+    def _bias(self, dy, M, C, off):
+        s = self.bias_splits
+        self.h.colsum(dy, M, C, self.bias_part, s)
+        self.h.sum_splits(self.bias_part, s, C, self.grad[off:off + C])
+
+    # ------------------------------------------------------------------ optimizer
+    def apply(self, lr: float, max_grad_norm: float = 0.5, comm=None, betas=(0.9, 0.999), eps: float = 1e-5):
+        """(DP all-reduce) -> global-norm clip -> Adam -> bf16 shadow, all on device."""
+        if comm is not None and comm.world > 1:
+            comm.all_reduce_sum_(self.grad)
+            self.grad.mul_(1.0 / comm.world)
+        self.h.sumsq(self.grad, self.sq_work, self.norm_sq)
+        self.step_count += 1
+        self.h.adam_clip(self.params, self.m, self.v, self.grad, self.shadow,
+                         self.norm_sq if max_grad_norm > 0 else None, float(max_grad_norm), float(lr),
+                         float(betas[0]), float(betas[1]), float(eps), self.step_count)
+
+    def state_dict(self):
+        return {"params": self.params, "m": self.m, "v": self.v, "step": torch.tensor([self.step_count])}
+
+    def load_state_dict(self, st):
+        self.params.copy_(st["params"])
+        self.m.copy_(st["m"])
+        self.v.copy_(st["v"])
+        self.step_count = int(st["step"][0])
+        self.h.to_bf16(self.params, self.shadow)

@@ -1,0 +1,193 @@
+"""A2C on pixels: PongSynth-v0 + Nature-CNN actor-critic (BASELINE.json config 4:
+"Actor-critic (A2C) Atari Pong pixels -- CNN encoder on MFMA, 8-GPU DP grad all-reduce").
+
+One update on each rank (one process per GPU), everything device resident:
+
+  1. rollout: T steps x N envs -- conv stack + fc on MFMA, fused policy/value head with
+     Philox sampling, Pong physics + 4-frame render straight into the uint8 obs ring;
+     the forward activations are KEPT (params do not change inside a rollout), so the
+     update needs no second forward pass
+  2. bootstrap value of obs[T], n-step returns via the GAE scan with lambda = 1
+  3. fused A2C head backward -> fc / conv weight gradients (transposed-LDS MFMA GEMMs,
+     split-K partials), data gradients + col2im with the ReLU mask fused
+  4. DP: one RCCL all-reduce of the flat fp32 gradient (world > 1)
+  5. global-norm clip + Adam + bf16 shadow weights in one kernel
+
+The CPU path (tests, no GPU) runs the same algorithm through the PyTorch oracle model
+and the numpy Pong reference.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import asdict, dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..models.nature_cnn import CNNSpec, DeviceNatureCNN, a2c_loss, reference_forward
+from ..parallel.comm import Comm
+from ..utils.tracing import PhaseTimer
+
+
+@dataclass
+class PixelA2CConfig:
+    env: str = "PongSynth-v0"
+    num_envs: int = 512            # envs per rank
+    rollout_len: int = 5           # A2C n-step
+    gamma: float = 0.99
+    lr: float = 2.5e-4
+    vf_coef: float = 0.5
+    ent_coef: float = 0.01
+    max_grad_norm: float = 0.5
+    seed: int = 0
+    max_episode_steps: int = 27000 // 4
+    phase_timing: bool = False
+
+    def to_dict(self):
+        return asdict(self)
+
+
+class PixelA2CTrainer:
+    def __init__(self, cfg: PixelA2CConfig, comm: Optional[Comm] = None, device=None):
+        if cfg.env != "PongSynth-v0":
+            raise ValueError(f"pixel trainer supports PongSynth-v0, not {cfg.env!r}")
+        self.cfg = cfg
+        self.comm = comm or Comm()
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+        self.on_gpu = self.device.type == "cuda"
+        self.spec = CNNSpec(act_dim=6)
+        N, T = cfg.num_envs, cfg.rollout_len
+        rank = self.comm.rank
+        env_seed = (cfg.seed * 1000003 + rank * 7919 + 17) & 0x7FFFFFFFFFFFFFFF
+        self.sample_seed = (cfg.seed * 2654435761 + rank * 97 + 5) & 0x7FFFFFFFFFFFFFFF
+        dev = self.device
+        self.obs = torch.zeros((T + 1, N, 84, 84, 4), dtype=torch.uint8, device=dev)
+        self.act = torch.zeros((T, N), dtype=torch.int32, device=dev)
+        self.logp = torch.zeros((T, N), device=dev)
+        self.val = torch.zeros((T + 1, N), device=dev)
+        self.rew = torch.zeros((T, N), device=dev)
+        self.done = torch.zeros((T, N), device=dev)
+        self.ep_sum = torch.zeros(4, dtype=torch.float64, device=dev)  # n, sum ret, sum len, sum ret^2
+        self.total_steps = 0
+        self.updates = 0
+        self.timer = PhaseTimer(dev if cfg.phase_timing and self.on_gpu else None)
+        if self.on_gpu:
+            from ..envs.pong import DevicePong
+
+            self.model = DeviceNatureCNN(self.spec, dev, max_batch=N * (T + 1), seed=cfg.seed)
+            self.env = DevicePong(N, dev, env_seed, cfg.max_episode_steps)
+            self.env.reset(self.obs[0])
+        else:
+            from ..envs.pong import PongRef
+
+            self.params = self.spec.init(cfg.seed).requires_grad_(True)
+            self.opt = torch.optim.Adam([self.params], lr=cfg.lr, eps=1e-5)
+            self.env = PongRef(N, env_seed, cfg.max_episode_steps)
+            self.obs[0] = torch.from_numpy(self.env.reset())
+            self.gen = torch.Generator().manual_seed(self.sample_seed)
+        self.comm.barrier() if self.comm.world > 1 else None
+
+    # ------------------------------------------------------------------ GPU
+    def _rollout_gpu(self):
+        cfg, m, N = self.cfg, self.model, self.cfg.num_envs
+        for t in range(cfg.rollout_len):
+            m.act(self.obs[t], t * N, self.act[t], self.logp[t], self.val[t], self.sample_seed,
+                  self.total_steps // N + t)
+            self.env.step(self.act[t], self.obs[t + 1], self.rew[t], self.done[t])
+            d = self.done[t]
+            self.ep_sum[0] += d.sum()
+            self.ep_sum[1] += (self.env.fin_ret * d).sum()
+            self.ep_sum[2] += (self.env.fin_len * d).sum()
+            self.ep_sum[3] += (self.env.fin_ret * self.env.fin_ret * d).sum()
+        # bootstrap V(obs[T]) with the pre-update weights; its activations go to the
+        # scratch rows [T*N, (T+1)*N) so the stored rollout activations stay intact
+        m.value(self.obs[cfg.rollout_len], cfg.rollout_len * N, self.val[cfg.rollout_len])
+
+    def _update_gpu(self):
+        from ..ops import gae_scan_tm
+
+        cfg, m = self.cfg, self.model
+        N, T = cfg.num_envs, cfg.rollout_len
+        B = N * T
+        with self.timer.phase("Returns"):
+            adv, ret, _ = gae_scan_tm(self.rew, self.done, self.val, cfg.gamma, 1.0)
+        with self.timer.phase("Backward"):
+            stats = m.backward(self.obs[:T].reshape(B, 84, 84, 4), self.act.reshape(B), adv.reshape(B),
+                               ret.reshape(B), cfg.vf_coef, cfg.ent_coef)
+        with self.timer.phase("Optimize"):
+            m.apply(cfg.lr, cfg.max_grad_norm, self.comm)
+        return stats
+
+    # ------------------------------------------------------------------ CPU
+    def _rollout_cpu(self):
+        cfg, N = self.cfg, self.cfg.num_envs
+        with torch.no_grad():
+            for t in range(cfg.rollout_len):
+                logits, value, _ = reference_forward(self.spec, self.params, self.obs[t])
+                a = torch.multinomial(torch.softmax(logits, -1), 1, generator=self.gen)[:, 0]
+                self.act[t] = a.int()
+                self.val[t] = value
+                r, d, fr, fl = self.env.step(a.numpy())
+                self.rew[t] = torch.from_numpy(r)
+                self.done[t] = torch.from_numpy(d)
+                self.obs[t + 1] = torch.from_numpy(self.env.render())
+                self.ep_sum += torch.tensor([d.sum(), (fr * d).sum(), (fl * d).sum(), (fr * fr * d).sum()],
+                                            dtype=torch.float64)
+
+    def _update_cpu(self):
+        from ..ops import gae_scan_tm
+
+        cfg = self.cfg
+        N, T = cfg.num_envs, cfg.rollout_len
+        B = N * T
+        adv, ret, _ = gae_scan_tm(self.rew, self.done, self.val, cfg.gamma, 1.0)
+        logits, value, _ = reference_forward(self.spec, self.params, self.obs[:T].reshape(B, 84, 84, 4))
+        loss, pg, vf, ent = a2c_loss(logits, value, self.act.reshape(B), adv.reshape(B), ret.reshape(B), cfg.vf_coef,
+                                     cfg.ent_coef)
+        self.opt.zero_grad()
+        loss.backward()
+        if self.comm.world > 1:
+            self.comm.all_reduce_sum_(self.params.grad)
+            self.params.grad.mul_(1.0 / self.comm.world)
+        torch.nn.utils.clip_grad_norm_([self.params], cfg.max_grad_norm)
+        self.opt.step()
+        return torch.tensor([[pg.item() * B, vf.item() * B, ent.item() * B, float(B)]])
+
+    # ------------------------------------------------------------------ API
+    def train_epoch(self):
+        cfg = self.cfg
+        N, T = cfg.num_envs, cfg.rollout_len
+        with self.timer.phase("Rollout"):
+            if self.on_gpu:
+                self._rollout_gpu()
+            else:
+                self._rollout_cpu()
+        if not self.on_gpu:
+            with torch.no_grad():
+                _, v, _ = reference_forward(self.spec, self.params, self.obs[T])
+            self.val[T] = v
+        if self.on_gpu:
+            stats = self._update_gpu()
+        else:
+            stats = self._update_cpu()
+        self.total_steps += N * T
+        self.updates += 1
+        self.obs[0].copy_(self.obs[T])
+        self._last_stats = stats
+        return stats
+
+    def metrics(self):
+        s = self.ep_sum.tolist()
+        st = self._last_stats.sum(0).tolist() if hasattr(self, "_last_stats") else [0, 0, 0, 1]
+        cnt = max(st[3], 1.0)
+        n = s[0]
+        out = {"Updates": self.updates, "EnvSteps": self.total_steps * self.comm.world,
+               "Episodes": n, "AverageEpRet": s[1] / n if n else float("nan"),
+               "EpLen": s[2] / n if n else float("nan"), "LossPi": st[0] / cnt, "LossV": st[1] / cnt,
+               "Entropy": st[2] / cnt}
+        return out
+
+    def reset_episode_stats(self):
+        self.ep_sum.zero_()
