@@ -9,7 +9,7 @@
 
 extern "C" {
 int rrl_conv_fwd(const void* x, int x_u8, const uint16_t* w, const float* b, uint16_t* y, int N, int H, int W,
-                 int C, int KH, int KW, int S, int Cout, int relu, void* stream);
+                 int C, int KH, int KW, int S, int Cout, int relu, float* work, long long work_elems, void* stream);
 int rrl_gemm_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* mask, uint16_t* out, int M, int Cout,
                    int K, void* stream);
 int rrl_col2im_mask(const uint16_t* dcol, const uint16_t* xact, uint16_t* dx, int N, int H, int W, int C, int KH,
@@ -29,7 +29,8 @@ int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, i
                  float ent_coef, uint16_t* dh, float* dhead, float* stats, int grid, void* stream);
 int rrl_head_wgrad(const uint16_t* h, const float* dhead, int B, int A, float* part, int nblk, void* stream);
 int rrl_pong_state_size();
-int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len, int N,
+int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
+                  float* ep_acc, int N,
                   unsigned long long seed, unsigned long long step, int max_steps, int reset_all, void* stream);
 int rrl_pong_render(const float* state, uint8_t* obs, int N, void* stream);
 }
@@ -69,7 +70,7 @@ void check_geo(const Geo& g) {
 }
 
 void conv_fwd(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& y, int64_t N, int64_t H, int64_t W,
-              int64_t C, int64_t KH, int64_t KW, int64_t S, int64_t Cout, bool relu) {
+              int64_t C, int64_t KH, int64_t KW, int64_t S, int64_t Cout, bool relu, const OptT& work) {
   Geo g{N, H, W, C, KH, KW, S};
   check_geo(g);
   const bool u8 = x.scalar_type() == at::kByte;
@@ -78,8 +79,10 @@ void conv_fwd(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& y
   check(w, "w", at::kBFloat16, Cout * KH * KW * C);
   check(b, "b", at::kFloat, Cout);
   check(y, "y", at::kBFloat16, N * g.OH() * g.OW() * Cout);
-  rc_check(rrl_conv_fwd(x.data_ptr(), u8, bf(w), b.data_ptr<float>(), bf(y), N, H, W, C, KH, KW, S, Cout, relu,
-                        stream()),
+  float* wk = opt_ptr<float>(work, "work", at::kFloat, 0);
+  const long long wn = wk ? work->numel() : 0;
+  rc_check(rrl_conv_fwd(x.data_ptr(), u8, bf(w), b.data_ptr<float>(), bf(y), N, H, W, C, KH, KW, S, Cout, relu, wk,
+                        wn, stream()),
            "conv_fwd");
 }
 
@@ -206,15 +209,17 @@ void head_wgrad(const Tensor& h, const Tensor& dhead, int64_t B, int64_t A, cons
 int64_t pong_state_size() { return rrl_pong_state_size(); }
 
 void pong_step(const Tensor& state, const Tensor& act, const Tensor& rew, const Tensor& done, const Tensor& fin_ret,
-               const Tensor& fin_len, int64_t N, int64_t seed, int64_t step, int64_t max_steps, bool reset_all) {
+               const Tensor& fin_len, const OptT& ep_acc, int64_t N, int64_t seed, int64_t step, int64_t max_steps,
+               bool reset_all) {
   check(state, "state", at::kFloat, N * pong_state_size());
   check(act, "act", at::kInt, reset_all ? 0 : N);
   check(rew, "rew", at::kFloat, N);
   check(done, "done", at::kFloat, N);
   check(fin_ret, "fin_ret", at::kFloat, N);
   check(fin_len, "fin_len", at::kFloat, N);
+  float* acc = opt_ptr<float>(ep_acc, "ep_acc", at::kFloat, 4 * N);
   rc_check(rrl_pong_step(state.data_ptr<float>(), act.data_ptr<int32_t>(), rew.data_ptr<float>(),
-                         done.data_ptr<float>(), fin_ret.data_ptr<float>(), fin_len.data_ptr<float>(), (int)N,
+                         done.data_ptr<float>(), fin_ret.data_ptr<float>(), fin_len.data_ptr<float>(), acc, (int)N,
                          (uint64_t)seed, (uint64_t)step, (int)max_steps, reset_all ? 1 : 0, stream()),
            "pong_step");
 }
@@ -228,7 +233,10 @@ void pong_render(const Tensor& state, const Tensor& obs, int64_t N) {
 }  // namespace
 
 void register_cnn_ops(pybind11::module_& m) {
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("y"),
+        pybind11::arg("N"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("C"), pybind11::arg("KH"),
+        pybind11::arg("KW"), pybind11::arg("S"), pybind11::arg("Cout"), pybind11::arg("relu"),
+        pybind11::arg("work") = pybind11::none());
   m.def("gemm_dgrad", &gemm_dgrad);
   m.def("col2im_mask", &col2im_mask);
   m.def("gemm_splits", &gemm_splits);

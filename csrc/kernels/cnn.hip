@@ -73,6 +73,22 @@ struct PartialStore {  // fp32 [split][M][N]
   }
 };
 
+struct PartialStoreT {  // fp32 [split][N][M]: the GEMM computed the transpose (rows = k, cols = cout)
+  float* out;
+  int M, N;  // GEMM dims: M = K of the conv (rows), N = Cout
+  __device__ __forceinline__ void operator()(int m, int n, f32x4_t acc, int z) const {
+    if (n >= N) return;
+    float* o = out + (size_t)z * M * N + (size_t)n * M;
+    if (m + 3 < M) {
+      *reinterpret_cast<float4*>(o + m) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (m + r < M) o[m + r] = acc[r];
+    }
+  }
+};
+
 template <int BM, int BN, bool A_TR, bool B_TR, class LA, class LB, class Epi>
 static int launch_gemm(LA la, LB lb, Epi epi, int M, int N, int K, int splits, hipStream_t st) {
   using S = GemmShape<BM, BN, A_TR, B_TR>;
@@ -141,6 +157,18 @@ __global__ void col2im_mask_kernel(const uint16_t* __restrict__ dcol, const uint
   }
 }
 
+// Split-K forward epilogue: y[m][n] = act(sum_z part[z][m][n] + b[n]) -> bf16.
+__global__ void bias_act_kernel(const float* __restrict__ part, int splits, int M, int N, const float* __restrict__ b,
+                                uint16_t* __restrict__ y, int relu) {
+  const size_t total = (size_t)M * N;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    float v = b ? b[i % N] : 0.f;
+    for (int z = 0; z < splits; ++z) v += part[(size_t)z * total + i];
+    if (relu) v = fmaxf(v, 0.f);
+    y[i] = f2bf(v);
+  }
+}
+
 // ----------------------------------------------------------------------------- reductions
 // part [splits][n] fp32 -> out[n] (+= when accumulate)
 __global__ void sum_splits_kernel(const float* __restrict__ part, int splits, size_t n, float* __restrict__ out) {
@@ -151,21 +179,41 @@ __global__ void sum_splits_kernel(const float* __restrict__ part, int splits, si
   }
 }
 
-// Column sums of a bf16 [M][C] matrix: partial [gridDim.y][C].  Block = 256 threads =
-// 64 columns x 4 row phases.
-__global__ void colsum_kernel(const uint16_t* __restrict__ y, int M, int C, float* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int ph = threadIdx.x >> 6;
-  const int rows = (M + gridDim.y - 1) / gridDim.y;
-  const int r0 = blockIdx.y * rows, r1 = min(M, r0 + rows);
-  float s = 0.f;
-  if (c < C)
-    for (int r = r0 + ph; r < r1; r += 4) s += bf2f(y[(size_t)r * C + c]);
-  red[ph][threadIdx.x & 63] = s;
+// Column sums of a bf16 [M][C] matrix (C % 8 == 0, C <= 2048): partial [gridDim.x][C].
+// A thread owns 8 consecutive columns of one row per pass (one 16-byte load); the
+// 256 / (C/8) row lanes of a block are folded through LDS at the end.
+__global__ void __launch_bounds__(256) colsum_kernel(const uint16_t* __restrict__ y, int M, int C,
+                                                     float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float cred[];  // [256][8]
+  const int cg = C / 8;
+  const int lanes_per_row = cg < 256 ? cg : 256;
+  const int row_lanes = 256 / lanes_per_row;
+  const int tid = threadIdx.x;
+  const int c8 = tid % lanes_per_row, rl = tid / lanes_per_row;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rl < row_lanes) {
+    for (int cc = c8; cc < cg; cc += lanes_per_row) {
+      for (int r = blockIdx.x * row_lanes + rl; r < M; r += gridDim.x * row_lanes) {
+        const uint4 v = *reinterpret_cast<const uint4*>(y + (size_t)r * C + 8 * cc);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[2 * i] += bf2f((uint16_t)(w[i] & 0xffff));
+          acc[2 * i + 1] += bf2f((uint16_t)(w[i] >> 16));
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) cred[tid * 8 + i] = acc[i];
   __syncthreads();
-  if (ph == 0 && c < C) part[(size_t)blockIdx.y * C + c] = red[0][threadIdx.x] + red[1][threadIdx.x] +
-                                                           red[2][threadIdx.x] + red[3][threadIdx.x];
+  if (rl == 0) {
+    for (int k = 1; k < row_lanes; ++k)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += cred[(k * lanes_per_row + c8) * 8 + i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) part[(size_t)blockIdx.x * C + 8 * c8 + i] = acc[i];
+  }
 }
 
 // Sum of squares of an fp32 vector: two-pass, deterministic.
@@ -408,6 +456,13 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(const uint16_t* __restr
 
 using namespace rrl;
 
+static int rrl_gemm_splits_impl(int R, int splits) {
+  splits = splits < 1 ? 1 : splits;
+  int kps = (R + splits - 1) / splits;
+  kps = (kps + kGemmBK - 1) / kGemmBK * kGemmBK;
+  return (R + kps - 1) / kps;
+}
+
 static int grid_for(size_t n, int per_block = 256, int cap = 4096) {
   size_t g = (n + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -417,9 +472,13 @@ static int grid_for(size_t n, int per_block = 256, int cap = 4096) {
 
 extern "C" {
 
-// Forward conv (or fc as a 1x1 conv on H = W = 1): y bf16 [N*OH*OW][Cout].
+// Forward conv (or fc as a 1x1 conv on H = W = 1): y bf16 [N*OH*OW][Cout].  When the
+// output has too few tiles to fill the chip (the fc layer at rollout batch sizes) and a
+// workspace is given, the reduction is split over workgroups into fp32 partials and a
+// second kernel applies bias + ReLU.
 int rrl_conv_fwd(const void* x, int x_u8, const uint16_t* w, const float* b, uint16_t* y, int N, int H, int W,
-                 int C, int KH, int KW, int S, int Cout, int relu, void* stream_) {
+                 int C, int KH, int KW, int S, int Cout, int relu, float* work, long long work_elems,
+                 void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   ConvGeom g{N, H, W, C, KH, KW, S, (H - KH) / S + 1, (W - KW) / S + 1, Cout};
   const int M = g.M(), K = g.K();
@@ -433,6 +492,22 @@ int rrl_conv_fwd(const void* x, int x_u8, const uint16_t* w, const float* b, uin
   }
   if (C % 8) return -1;
   ConvLoader lx{(const uint16_t*)x, H, W, C, KW, S, g.OH, g.OW, M, K};
+  const int tiles = ((M + 127) / 128) * ((Cout + 63) / 64);
+  if (work != nullptr && Cout >= 64 && tiles < 160 && K >= 1024) {
+    int splits = (320 + tiles - 1) / tiles;
+    if (splits > K / 256) splits = K / 256;
+    while (splits > 1 && (long long)splits * M * Cout > work_elems) --splits;
+    splits = rrl_gemm_splits_impl(K, splits);
+    if (splits > 1) {
+      PartialStore pe{work, M, Cout};
+      int rc = launch_gemm<128, 64, false, false>(lx, lw, pe, M, Cout, K, splits, st);
+      if (rc) return rc;
+      const size_t total = (size_t)M * Cout;
+      hipLaunchKernelGGL(bias_act_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0, st, work, splits, M,
+                         Cout, b, y, relu);
+      return (int)hipGetLastError();
+    }
+  }
   return Cout >= 64 ? launch_gemm<128, 64, false, false>(lx, lw, epi, M, Cout, K, 1, st)
                     : launch_gemm<128, 32, false, false>(lx, lw, epi, M, Cout, K, 1, st);
 }
@@ -459,33 +534,30 @@ int rrl_col2im_mask(const uint16_t* dcol, const uint16_t* xact, uint16_t* dx, in
 }
 
 // dW partials: part [splits][Cout][K] = dY^T . im2col(X) over each split's rows.
+// The GEMM is computed transposed -- rows = the conv's K (long), cols = Cout (32 / 64 /
+// 512) -- so the wide im2col operand gets the 128-row tile and the epilogue stores 4
+// consecutive k of one output channel as one 16-byte write.
 int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, int splits, int N, int H, int W,
                    int C, int KH, int KW, int S, int Cout, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   ConvGeom g{N, H, W, C, KH, KW, S, (H - KH) / S + 1, (W - KW) / S + 1, Cout};
   const int M = g.M(), K = g.K();
-  RowLoader la{dy, M, Cout};
-  PartialStore epi{part, Cout, K};
-  // rows of the output = Cout, cols = K, reduction = M (batch x spatial)
+  RowLoader ly{dy, M, Cout};
+  PartialStoreT epi{part, K, Cout};
   if (x_u8) {
     if (C != 4 || (KW & 1)) return -1;
     FrameLoader lx{(const uint8_t*)x, H, W, KW, S, g.OH, g.OW, M, K};
-    return Cout >= 64 ? launch_gemm<64, 64, true, true>(la, lx, epi, Cout, K, M, splits, st)
-                      : launch_gemm<32, 64, true, true>(la, lx, epi, Cout, K, M, splits, st);
+    return Cout >= 64 ? launch_gemm<128, 64, true, true>(lx, ly, epi, K, Cout, M, splits, st)
+                      : launch_gemm<128, 32, true, true>(lx, ly, epi, K, Cout, M, splits, st);
   }
   if (C % 8) return -1;
   ConvLoader lx{(const uint16_t*)x, H, W, C, KW, S, g.OH, g.OW, M, K};
-  return Cout >= 64 ? launch_gemm<64, 64, true, true>(la, lx, epi, Cout, K, M, splits, st)
-                    : launch_gemm<32, 64, true, true>(la, lx, epi, Cout, K, M, splits, st);
+  return Cout >= 64 ? launch_gemm<128, 64, true, true>(lx, ly, epi, K, Cout, M, splits, st)
+                    : launch_gemm<128, 32, true, true>(lx, ly, epi, K, Cout, M, splits, st);
 }
 
 // Actual number of splits launch_gemm uses for a reduction of length R.
-int rrl_gemm_splits(int R, int splits) {
-  splits = splits < 1 ? 1 : splits;
-  int kps = (R + splits - 1) / splits;
-  kps = (kps + kGemmBK - 1) / kGemmBK * kGemmBK;
-  return (R + kps - 1) / kps;
-}
+int rrl_gemm_splits(int R, int splits) { return rrl_gemm_splits_impl(R, splits); }
 
 int rrl_sum_splits(const float* part, int splits, long long n, float* out, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
@@ -495,7 +567,8 @@ int rrl_sum_splits(const float* part, int splits, long long n, float* out, void*
 
 int rrl_colsum(const uint16_t* y, int M, int C, float* part, int splits, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
-  hipLaunchKernelGGL(colsum_kernel, dim3((C + 63) / 64, splits), dim3(256), 0, st, y, M, C, part);
+  if (C % 8 || C > 2048 || splits < 1) return -1;
+  hipLaunchKernelGGL(colsum_kernel, dim3(splits), dim3(256), 256 * 8 * sizeof(float), st, y, M, C, part);
   return (int)hipGetLastError();
 }
 

@@ -49,7 +49,7 @@ RRL_DEV void reset_env(float* s, uint4 r) {
 
 __global__ void pong_step_kernel(float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew,
                                  float* __restrict__ done, float* __restrict__ fin_ret, float* __restrict__ fin_len,
-                                 int N, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
+                                 float* __restrict__ ep_acc, int N, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
                                  int reset_all) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= N) return;
@@ -105,6 +105,13 @@ __global__ void pong_step_kernel(float* __restrict__ state, const int32_t* __res
     done[e] = over ? 1.f : 0.f;
     fin_ret[e] = over ? s[P_RET] : 0.f;
     fin_len[e] = over ? s[P_T] : 0.f;
+    if (over && ep_acc) {  // per-env running episode statistics: count, sum ret, sum len, sum ret^2
+      float* acc = ep_acc + 4 * (size_t)e;
+      acc[0] += 1.f;
+      acc[1] += s[P_RET];
+      acc[2] += s[P_T];
+      acc[3] += s[P_RET] * s[P_RET];
+    }
     if (over) {
       const uint4 r1 = philox4x32(make_uint4((uint32_t)e, step_lo, step_hi, 0x52u), key);
       reset_env(s, r1);
@@ -162,12 +169,13 @@ extern "C" {
 
 int rrl_pong_state_size() { return kPongState; }
 
-int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len, int N,
+int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
+                  float* ep_acc, int N,
                   unsigned long long seed, unsigned long long step, int max_steps, int reset_all, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
   hipLaunchKernelGGL(pong_step_kernel, dim3((N + 255) / 256), dim3(256), 0, st, state, act, rew, done, fin_ret,
-                     fin_len, N, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, reset_all);
+                     fin_len, ep_acc, N, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, reset_all);
   return (int)hipGetLastError();
 }
 

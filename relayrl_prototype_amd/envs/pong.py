@@ -173,20 +173,25 @@ class DevicePong:
         self.done = torch.zeros(self.N, device=dev)
         self.fin_ret = torch.zeros(self.N, device=dev)
         self.fin_len = torch.zeros(self.N, device=dev)
+        self.ep_acc = torch.zeros(self.N, 4, device=dev)  # per env: episodes, sum ret, sum len, sum ret^2
         self._dummy_act = torch.zeros(self.N, dtype=torch.int32, device=dev)
         self.step_count = 0
 
     def reset(self, obs_out: torch.Tensor):
-        self.h.pong_step(self.state, self._dummy_act, self.rew, self.done, self.fin_ret, self.fin_len, self.N,
+        self.h.pong_step(self.state, self._dummy_act, self.rew, self.done, self.fin_ret, self.fin_len, None, self.N,
                          self.seed, self.step_count, self.max_steps, True)
         self.step_count += 1
         self.h.pong_render(self.state, obs_out, self.N)
 
+    def episode_stats(self):
+        """(episodes, sum return, sum length, sum return^2) over all envs since the last reset."""
+        return self.ep_acc.double().sum(0)
+
     def step(self, act: torch.Tensor, obs_out: torch.Tensor, rew_out=None, done_out=None):
         rew = self.rew if rew_out is None else rew_out
         done = self.done if done_out is None else done_out
-        self.h.pong_step(self.state, act, rew, done, self.fin_ret, self.fin_len, self.N, self.seed, self.step_count,
-                         self.max_steps, False)
+        self.h.pong_step(self.state, act, rew, done, self.fin_ret, self.fin_len, self.ep_acc, self.N, self.seed,
+                         self.step_count, self.max_steps, False)
         self.step_count += 1
         self.h.pong_render(self.state, obs_out, self.N)
         return rew, done

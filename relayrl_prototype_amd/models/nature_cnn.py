@@ -196,12 +196,12 @@ class DeviceNatureCNN:
         self._wplan = {}
         need = self.head_blocks * spec.head_size
         for name, cout, K, M in self._wgrad_layers(B):
-            tiles = -(-cout // 64) * -(-K // 64)
+            tiles = -(-K // 128) * -(-cout // (64 if cout >= 64 else 32))
             s = int(self.h.gemm_splits(M, max(1, min(512 // max(tiles, 1), -(-M // 64)))))
             self._wplan[name] = s
             need = max(need, s * cout * K)
         self.part = torch.empty(need, device=dev)
-        self.bias_splits = 64
+        self.bias_splits = 512
         self.bias_part = torch.empty(self.bias_splits * HIDDEN, device=dev)
         self.sq_work = torch.empty(1024, device=dev)
         self.norm_sq = torch.empty(1, device=dev)
@@ -233,7 +233,7 @@ class DeviceNatureCNN:
                        L.k, L.k, L.s, L.cout, True)
             x = y
         h.conv_fwd(a3, sh[o["wfc"]:o["bfc"]], p[o["bfc"]:o["bfc"] + HIDDEN], hid, n, 1, 1, FC_IN, 1, 1, 1, HIDDEN,
-                   True)
+                   True, self.part)  # split-K when the batch is too small to fill the chip
         return hid
 
     def act(self, obs_u8, row0, act_out, logp_out, value_out, seed: int, step: int, row_offset: int = 0):

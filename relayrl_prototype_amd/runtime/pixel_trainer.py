@@ -18,11 +18,9 @@ and the numpy Pong reference.
 """
 from __future__ import annotations
 
-import time
 from dataclasses import asdict, dataclass
 from typing import Optional
 
-import numpy as np
 import torch
 
 from ..models.nature_cnn import CNNSpec, DeviceNatureCNN, a2c_loss, reference_forward
@@ -96,11 +94,6 @@ class PixelA2CTrainer:
             m.act(self.obs[t], t * N, self.act[t], self.logp[t], self.val[t], self.sample_seed,
                   self.total_steps // N + t)
             self.env.step(self.act[t], self.obs[t + 1], self.rew[t], self.done[t])
-            d = self.done[t]
-            self.ep_sum[0] += d.sum()
-            self.ep_sum[1] += (self.env.fin_ret * d).sum()
-            self.ep_sum[2] += (self.env.fin_len * d).sum()
-            self.ep_sum[3] += (self.env.fin_ret * self.env.fin_ret * d).sum()
         # bootstrap V(obs[T]) with the pre-update weights; its activations go to the
         # scratch rows [T*N, (T+1)*N) so the stored rollout activations stay intact
         m.value(self.obs[cfg.rollout_len], cfg.rollout_len * N, self.val[cfg.rollout_len])
@@ -179,7 +172,7 @@ class PixelA2CTrainer:
         return stats
 
     def metrics(self):
-        s = self.ep_sum.tolist()
+        s = (self.env.episode_stats() if self.on_gpu else self.ep_sum).tolist()
         st = self._last_stats.sum(0).tolist() if hasattr(self, "_last_stats") else [0, 0, 0, 1]
         cnt = max(st[3], 1.0)
         n = s[0]
@@ -191,3 +184,5 @@ class PixelA2CTrainer:
 
     def reset_episode_stats(self):
         self.ep_sum.zero_()
+        if self.on_gpu:
+            self.env.ep_acc.zero_()

@@ -251,3 +251,22 @@ def test_pixel_trainer_gpu_runs(cuda):
     assert torch.isfinite(tr.model.params).all()
     assert np.isfinite(m["LossPi"]) and np.isfinite(m["LossV"]) and abs(m["Entropy"] - np.log(6)) < 0.1
     assert m["EnvSteps"] == 3 * 64 * 5
+
+
+@pytest.mark.parametrize("B", [37, 512])
+def test_fc_forward_splitk_matches_direct(cuda, B):
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    g = torch.Generator().manual_seed(B)
+    x = _bf(F.relu(torch.randn(B, FC_IN, generator=g)))
+    w = _bf(torch.randn(HIDDEN, FC_IN, generator=g) * 0.02)
+    b = torch.randn(HIDDEN, generator=g) * 0.1
+    xd, wd, bd = x.to(cuda).bfloat16().reshape(-1), w.to(cuda).bfloat16().reshape(-1), b.to(cuda)
+    y1 = torch.empty(B * HIDDEN, dtype=torch.bfloat16, device=cuda)
+    y2 = torch.empty_like(y1)
+    h.conv_fwd(xd, wd, bd, y1, B, 1, 1, FC_IN, 1, 1, 1, HIDDEN, True)
+    work = torch.empty(16 * B * HIDDEN, device=cuda)
+    h.conv_fwd(xd, wd, bd, y2, B, 1, 1, FC_IN, 1, 1, 1, HIDDEN, True, work)
+    ref = F.relu(x @ w.t() + b).reshape(-1)
+    assert relerr(y1, ref) < 1e-2 and relerr(y2, ref) < 1e-2
