@@ -17,6 +17,8 @@ int rrl_col2im_mask(const uint16_t* dcol, const uint16_t* xact, uint16_t* dx, in
 int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, int splits, int N, int H, int W, int C,
                    int KH, int KW, int S, int Cout, void* stream);
 int rrl_gemm_splits(int R, int splits);
+int rrl_conv_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, int N, int H, int W,
+                   int C, int KH, int KW, int S, int Cout, void* stream);
 int rrl_sum_splits(const float* part, int splits, long long n, float* out, void* stream);
 int rrl_colsum(const uint16_t* y, int M, int C, float* part, int splits, void* stream);
 int rrl_sumsq(const float* x, long long n, float* work, int work_n, float* out, void* stream);
@@ -105,6 +107,21 @@ void col2im_mask(const Tensor& dcol, const Tensor& xact, const Tensor& dx, int64
   check(xact, "xact", at::kBFloat16, N * H * W * C);
   check(dx, "dx", at::kBFloat16, N * H * W * C);
   rc_check(rrl_col2im_mask(bf(dcol), bf(xact), bf(dx), N, H, W, C, KH, KW, S, stream()), "col2im_mask");
+}
+
+// Returns false (nothing launched) for geometries without an implicit-dgrad kernel.
+bool conv_dgrad(const Tensor& dy, const Tensor& w, const Tensor& xact, const Tensor& dx, int64_t N, int64_t H,
+                int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t S, int64_t Cout) {
+  Geo g{N, H, W, C, KH, KW, S};
+  check_geo(g);
+  check(dy, "dy", at::kBFloat16, N * g.OH() * g.OW() * Cout);
+  check(w, "w", at::kBFloat16, Cout * KH * KW * C);
+  check(xact, "xact", at::kBFloat16, N * H * W * C);
+  check(dx, "dx", at::kBFloat16, N * H * W * C);
+  const int rc = rrl_conv_dgrad(bf(dy), bf(w), bf(xact), bf(dx), N, H, W, C, KH, KW, S, Cout, stream());
+  if (rc == -1) return false;
+  rc_check(rc, "conv_dgrad");
+  return true;
 }
 
 int64_t gemm_splits(int64_t R, int64_t splits) { return rrl_gemm_splits((int)R, (int)splits); }
@@ -239,6 +256,7 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("work") = pybind11::none());
   m.def("gemm_dgrad", &gemm_dgrad);
   m.def("col2im_mask", &col2im_mask);
+  m.def("conv_dgrad", &conv_dgrad);
   m.def("gemm_splits", &gemm_splits);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("sum_splits", &sum_splits);

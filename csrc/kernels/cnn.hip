@@ -107,6 +107,110 @@ static int launch_gemm(LA la, LB lb, Epi epi, int M, int N, int K, int splits, h
   return (int)hipGetLastError();
 }
 
+// Calls f(loader) with the fastest im2col loader for the geometry: compile-time
+// variants for the Nature-CNN layers, plain row loader for 1x1 (fc), runtime otherwise.
+template <class F>
+static int with_im2col(const ConvGeom& g, const void* x, bool u8, F&& f) {
+  const int M = g.M(), K = g.K();
+  if (u8) {
+    if (g.C != 4 || (g.KW & 1)) return -1;
+    if (g.H == 84 && g.W == 84 && g.KH == 8 && g.KW == 8 && g.S == 4)
+      return f(FrameLoaderT<84, 84, 8, 4, 20, 20>{(const uint8_t*)x, M, K});
+    return f(FrameLoader{(const uint8_t*)x, g.H, g.W, g.KW, g.S, g.OH, g.OW, M, K});
+  }
+  if (g.C % 8) return -1;
+  const uint16_t* xb = (const uint16_t*)x;
+  if (g.H == 1 && g.W == 1 && g.KH == 1 && g.KW == 1) return f(RowLoader{xb, M, K});
+  if (g.H == 20 && g.W == 20 && g.C == 32 && g.KH == 4 && g.KW == 4 && g.S == 2)
+    return f(ConvLoaderT<20, 20, 32, 4, 2, 9, 9>{xb, M, K});
+  if (g.H == 9 && g.W == 9 && g.C == 64 && g.KH == 3 && g.KW == 3 && g.S == 1)
+    return f(ConvLoaderT<9, 9, 64, 3, 1, 7, 7>{xb, M, K});
+  return f(ConvLoader{xb, g.H, g.W, g.C, g.KW, g.S, g.OH, g.OW, M, K});
+}
+
+// ----------------------------------------------------------------------------- implicit dgrad
+// dX = conv^T(dY, W) * (X > 0) without a column buffer.  Input pixels are split into
+// S x S phase classes (ih = ph + S*a, iw = pw + S*b); inside a class every pixel sees
+// the same taps kh = ph + S*i, kw = pw + S*j, so the class is one GEMM with
+//   rows = (n, a, b),  cols = c,  reduction = (i, j, co):
+//   A[(n,a,b)][(i,j,co)] = dY[n][a-i][b-j][co]   (0 outside the output)
+//   B[(i,j,co)][c]       = W[co][ph+S*i][pw+S*j][c]   (transposed LDS read)
+// Requires H % S == 0, W % S == 0, KH % S == 0, KW % S == 0 (true for the Nature CNN).
+template <int H, int W, int C, int KH, int KW, int S, int OH, int OW, int CO>
+struct DgradGeo {
+  static constexpr int HA = H / S, WB = W / S, TH = KH / S, TW = KW / S;
+  static constexpr int RED = TH * TW * CO;
+  static_assert(H % S == 0 && W % S == 0 && KH % S == 0 && KW % S == 0, "phase-class dgrad geometry");
+};
+
+template <class G, int H, int W, int C, int KH, int KW, int S, int OH, int OW, int CO>
+struct DgradALoader {
+  const uint16_t* dy;
+  int M;
+  __device__ __forceinline__ uint4 operator()(int m, int r) const {
+    if (m >= M) return make_uint4(0, 0, 0, 0);
+    const unsigned um = (unsigned)m, ur = (unsigned)r;
+    const unsigned n = um / (G::HA * G::WB), p = um - n * (G::HA * G::WB);
+    const int a = (int)(p / G::WB), b = (int)(p - (p / G::WB) * G::WB);
+    const unsigned tap = ur / CO, co = ur - tap * CO;
+    const int i = (int)(tap / G::TW), j = (int)(tap - (tap / G::TW) * G::TW);
+    const int oh = a - i, ow = b - j;
+    if (oh < 0 || oh >= OH || ow < 0 || ow >= OW) return make_uint4(0, 0, 0, 0);
+    return *reinterpret_cast<const uint4*>(dy + (((size_t)n * OH + oh) * OW + ow) * CO + co);
+  }
+};
+
+template <class G, int H, int W, int C, int KH, int KW, int S, int OH, int OW, int CO>
+struct DgradBLoader {
+  const uint16_t* w;
+  int ph, pw;
+  __device__ __forceinline__ uint4 operator()(int r, int c) const {
+    const unsigned ur = (unsigned)r;
+    const unsigned tap = ur / CO, co = ur - tap * CO;
+    const int i = (int)(tap / G::TW), j = (int)(tap - (tap / G::TW) * G::TW);
+    const int kh = ph + S * i, kw = pw + S * j;
+    return *reinterpret_cast<const uint4*>(w + (((size_t)co * KH + kh) * KW + kw) * C + c);
+  }
+};
+
+template <class G, int H, int W, int C>
+struct DgradStore {
+  uint16_t* dx;
+  const uint16_t* xact;
+  int M, ph, pw, S;
+  __device__ __forceinline__ void operator()(int m, int c, f32x4_t acc, int) const {
+    if (c >= C) return;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int mm = m + r;
+      if (mm < M) {
+        const unsigned um = (unsigned)mm;
+        const unsigned n = um / (G::HA * G::WB), p = um - n * (G::HA * G::WB);
+        const unsigned a = p / G::WB, b = p - a * G::WB;
+        const size_t idx = (((size_t)n * H + ph + S * a) * W + pw + S * b) * C + c;
+        dx[idx] = bf2f(xact[idx]) > 0.f ? f2bf(acc[r]) : (uint16_t)0;
+      }
+    }
+  }
+};
+
+template <int H, int W, int C, int KH, int KW, int S, int OH, int OW, int CO>
+static int launch_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, int N,
+                        hipStream_t st) {
+  using G = DgradGeo<H, W, C, KH, KW, S, OH, OW, CO>;
+  const int M = N * G::HA * G::WB;
+  for (int ph = 0; ph < S; ++ph)
+    for (int pw = 0; pw < S; ++pw) {
+      DgradALoader<G, H, W, C, KH, KW, S, OH, OW, CO> la{dy, M};
+      DgradBLoader<G, H, W, C, KH, KW, S, OH, OW, CO> lb{w, ph, pw};
+      DgradStore<G, H, W, C> epi{dx, xact, M, ph, pw, S};
+      const int rc = C >= 64 ? launch_gemm<128, 64, false, true>(la, lb, epi, M, C, G::RED, 1, st)
+                             : launch_gemm<128, 32, false, true>(la, lb, epi, M, C, G::RED, 1, st);
+      if (rc) return rc;
+    }
+  return 0;
+}
+
 // ----------------------------------------------------------------------------- col2im
 // dX[n][ih][iw][c] = sum over (kh, kw) with ih = oh*S + kh, iw = ow*S + kw of
 // dXc[(n, oh, ow)][(kh, kw, c)], then * (X > 0).  One thread per 8 channels.
@@ -170,12 +274,50 @@ __global__ void bias_act_kernel(const float* __restrict__ part, int splits, int 
 }
 
 // ----------------------------------------------------------------------------- reductions
-// part [splits][n] fp32 -> out[n] (+= when accumulate)
-__global__ void sum_splits_kernel(const float* __restrict__ part, int splits, size_t n, float* __restrict__ out) {
+// part [splits][n] fp32 -> out[n].  Block = 16 float4 columns x 16 split phases (LDS
+// fold), so a few thousand outputs with hundreds of splits still spread over the chip.
+__global__ void __launch_bounds__(256) sum_splits_kernel(const float* __restrict__ part, int splits, size_t n,
+                                                         float* __restrict__ out) {
+  __shared__ float4 red[16][16];
+  const int col = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const size_t i4 = (size_t)blockIdx.x * 16 + col;  // float4 index
+  const size_t n4 = n / 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < n4) {
+    for (int z = ph; z < splits; z += 16) {
+      const float4 v = reinterpret_cast<const float4*>(part + (size_t)z * n)[i4];
+      a.x += v.x;
+      a.y += v.y;
+      a.z += v.z;
+      a.w += v.w;
+    }
+  }
+  red[ph][col] = a;
+  __syncthreads();
+  if (ph == 0 && i4 < n4) {
+    for (int k = 1; k < 16; ++k) {
+      a.x += red[k][col].x;
+      a.y += red[k][col].y;
+      a.z += red[k][col].z;
+      a.w += red[k][col].w;
+    }
+    reinterpret_cast<float4*>(out)[i4] = a;
+  }
+  // tail (n % 4) handled by block 0
+  if (blockIdx.x == 0 && threadIdx.x < (int)(n & 3)) {
+    const size_t i = n4 * 4 + threadIdx.x;
+    float t = 0.f;
+    for (int z = 0; z < splits; ++z) t += part[(size_t)z * n + i];
+    out[i] = t;
+  }
+}
+
+__global__ void sum_splits_scalar_kernel(const float* __restrict__ part, int splits, size_t n,
+                                         float* __restrict__ out) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += part[(size_t)z * n + i];
-    out[i] = s;
+    float t = 0.f;
+    for (int z = 0; z < splits; ++z) t += part[(size_t)z * n + i];
+    out[i] = t;
   }
 }
 
@@ -484,20 +626,15 @@ int rrl_conv_fwd(const void* x, int x_u8, const uint16_t* w, const float* b, uin
   const int M = g.M(), K = g.K();
   RowLoader lw{w, Cout, K};
   BiasReluStore epi{y, b, M, Cout, relu != 0};
-  if (x_u8) {
-    if (C != 4 || (KW & 1)) return -1;
-    FrameLoader lx{(const uint8_t*)x, H, W, KW, S, g.OH, g.OW, M, K};
-    return Cout >= 64 ? launch_gemm<128, 64, false, false>(lx, lw, epi, M, Cout, K, 1, st)
-                      : launch_gemm<128, 32, false, false>(lx, lw, epi, M, Cout, K, 1, st);
-  }
-  if (C % 8) return -1;
-  ConvLoader lx{(const uint16_t*)x, H, W, C, KW, S, g.OH, g.OW, M, K};
   const int tiles = ((M + 127) / 128) * ((Cout + 63) / 64);
-  if (work != nullptr && Cout >= 64 && tiles < 160 && K >= 1024) {
-    int splits = (320 + tiles - 1) / tiles;
+  int splits = 1;
+  if (!x_u8 && work != nullptr && Cout >= 64 && tiles < 160 && K >= 1024) {
+    splits = (320 + tiles - 1) / tiles;
     if (splits > K / 256) splits = K / 256;
     while (splits > 1 && (long long)splits * M * Cout > work_elems) --splits;
     splits = rrl_gemm_splits_impl(K, splits);
+  }
+  return with_im2col(g, x, x_u8 != 0, [&](auto lx) -> int {
     if (splits > 1) {
       PartialStore pe{work, M, Cout};
       int rc = launch_gemm<128, 64, false, false>(lx, lw, pe, M, Cout, K, splits, st);
@@ -507,9 +644,9 @@ int rrl_conv_fwd(const void* x, int x_u8, const uint16_t* w, const float* b, uin
                          Cout, b, y, relu);
       return (int)hipGetLastError();
     }
-  }
-  return Cout >= 64 ? launch_gemm<128, 64, false, false>(lx, lw, epi, M, Cout, K, 1, st)
-                    : launch_gemm<128, 32, false, false>(lx, lw, epi, M, Cout, K, 1, st);
+    return Cout >= 64 ? launch_gemm<128, 64, false, false>(lx, lw, epi, M, Cout, K, 1, st)
+                      : launch_gemm<128, 32, false, false>(lx, lw, epi, M, Cout, K, 1, st);
+  });
 }
 
 // dY [M][Cout] . W [Cout][K] -> bf16 [M][K] (masked by mask[M][K] > 0 when given).
@@ -521,6 +658,18 @@ int rrl_gemm_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* mask, 
   RowLoader lb{w, Cout, K};
   MaskStore epi{out, mask, M, K};
   return launch_gemm<128, 64, false, true>(la, lb, epi, M, K, Cout, 1, st);
+}
+
+// Implicit dgrad + ReLU mask for the supported geometries (-1 otherwise: callers fall
+// back to gemm_dgrad + col2im_mask).
+int rrl_conv_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, int N, int H, int W,
+                   int C, int KH, int KW, int S, int Cout, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  if (H == 20 && W == 20 && C == 32 && KH == 4 && KW == 4 && S == 2 && Cout == 64)
+    return launch_dgrad<20, 20, 32, 4, 4, 2, 9, 9, 64>(dy, w, xact, dx, N, st);
+  if (H == 9 && W == 9 && C == 64 && KH == 3 && KW == 3 && S == 1 && Cout == 64)
+    return launch_dgrad<9, 9, 64, 3, 3, 1, 7, 7, 64>(dy, w, xact, dx, N, st);
+  return -1;
 }
 
 int rrl_col2im_mask(const uint16_t* dcol, const uint16_t* xact, uint16_t* dx, int N, int H, int W, int C, int KH,
@@ -544,16 +693,10 @@ int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, int
   const int M = g.M(), K = g.K();
   RowLoader ly{dy, M, Cout};
   PartialStoreT epi{part, K, Cout};
-  if (x_u8) {
-    if (C != 4 || (KW & 1)) return -1;
-    FrameLoader lx{(const uint8_t*)x, H, W, KW, S, g.OH, g.OW, M, K};
+  return with_im2col(g, x, x_u8 != 0, [&](auto lx) -> int {
     return Cout >= 64 ? launch_gemm<128, 64, true, true>(lx, ly, epi, K, Cout, M, splits, st)
                       : launch_gemm<128, 32, true, true>(lx, ly, epi, K, Cout, M, splits, st);
-  }
-  if (C % 8) return -1;
-  ConvLoader lx{(const uint16_t*)x, H, W, C, KW, S, g.OH, g.OW, M, K};
-  return Cout >= 64 ? launch_gemm<128, 64, true, true>(lx, ly, epi, K, Cout, M, splits, st)
-                    : launch_gemm<128, 32, true, true>(lx, ly, epi, K, Cout, M, splits, st);
+  });
 }
 
 // Actual number of splits launch_gemm uses for a reduction of length R.
@@ -561,7 +704,14 @@ int rrl_gemm_splits(int R, int splits) { return rrl_gemm_splits_impl(R, splits);
 
 int rrl_sum_splits(const float* part, int splits, long long n, float* out, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
-  hipLaunchKernelGGL(sum_splits_kernel, dim3(grid_for((size_t)n)), dim3(256), 0, st, part, splits, (size_t)n, out);
+  if (((uintptr_t)part & 15) || ((uintptr_t)out & 15) || (n & 3)) {  // float4 path needs aligned rows
+    hipLaunchKernelGGL(sum_splits_scalar_kernel, dim3(grid_for((size_t)n)), dim3(256), 0, st, part, splits,
+                       (size_t)n, out);
+    return (int)hipGetLastError();
+  }
+  const size_t blocks = ((size_t)n / 4 + 15) / 16;
+  hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)(blocks < 1 ? 1 : blocks)), dim3(256), 0, st, part, splits,
+                     (size_t)n, out);
   return (int)hipGetLastError();
 }
 

@@ -93,6 +93,50 @@ struct FrameLoader {
   }
 };
 
+// Compile-time-geometry variants: every index division becomes a multiply-shift, which
+// matters because the loader runs once per 16-byte chunk (the Nature-CNN layers use
+// these; other shapes fall back to the runtime-geometry loaders above).
+template <int H, int W, int C, int KW, int S, int OH, int OW>
+struct ConvLoaderT {
+  const uint16_t* x;
+  int M, K;
+  __device__ __forceinline__ uint4 operator()(int m, int k) const {
+    if (m >= M || k >= K) return make_uint4(0, 0, 0, 0);
+    const unsigned um = (unsigned)m, uk = (unsigned)k;
+    const unsigned n = um / (OH * OW), p = um - n * (OH * OW);
+    const unsigned oh = p / OW, ow = p - oh * OW;
+    const unsigned kh = uk / (KW * C), r = uk - kh * (KW * C);
+    const unsigned kw = r / C, c = r - kw * C;
+    const size_t off = (((size_t)n * H + (oh * S + kh)) * W + (ow * S + kw)) * C + c;
+    return *reinterpret_cast<const uint4*>(x + off);
+  }
+};
+
+template <int H, int W, int KW, int S, int OH, int OW>
+struct FrameLoaderT {
+  const uint8_t* x;
+  int M, K;
+  __device__ __forceinline__ uint4 operator()(int m, int k) const {
+    if (m >= M || k >= K) return make_uint4(0, 0, 0, 0);
+    const unsigned um = (unsigned)m, uk = (unsigned)k;
+    const unsigned n = um / (OH * OW), p = um - n * (OH * OW);
+    const unsigned oh = p / OW, ow = p - oh * OW;
+    const unsigned kh = uk / (KW * 4), kw = (uk - kh * (KW * 4)) >> 2;
+    const size_t off = (((size_t)n * H + (oh * S + kh)) * W + (ow * S + kw)) * 4;
+    const uint2 b = *reinterpret_cast<const uint2*>(x + off);
+    const float s = 1.0f / 255.0f;
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t src = i < 2 ? b.x : b.y;
+      const int sh = (i & 1) * 16;
+      const float lo = (float)((src >> sh) & 0xff) * s, hi = (float)((src >> (sh + 8)) & 0xff) * s;
+      w[i] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+
 // ----------------------------------------------------------------------------- kernel
 constexpr int kGemmBK = 64;
 constexpr int kGemmPad = 8;  // bf16 elements of row padding (16 B)

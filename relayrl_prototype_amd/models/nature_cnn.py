@@ -183,9 +183,7 @@ class DeviceNatureCNN:
         # backward buffers
         self.dh = torch.empty(B * HIDDEN, dtype=bf, device=dev)
         self.da3 = torch.empty(B * FC_IN, dtype=bf, device=dev)
-        self.dcol3 = torch.empty(B * L3.hout ** 2 * L3.K, dtype=bf, device=dev)
         self.da2 = torch.empty(B * L2.hout ** 2 * L2.cout, dtype=bf, device=dev)
-        self.dcol2 = torch.empty(B * L2.hout ** 2 * L2.K, dtype=bf, device=dev)
         self.da1 = torch.empty(B * L1.hout ** 2 * L1.cout, dtype=bf, device=dev)
         self.dhead = torch.empty(B * (self.A + 1), dtype=torch.float32, device=dev)
         self.head_grid = max(1, min(1024, (B + 3) // 4))
@@ -288,21 +286,29 @@ class DeviceNatureCNN:
         # conv3
         self._wgrad("c3", da3, a2, B, L3.hin, L3.cin, L3.k, L3.s, L3.cout, o["w3"])
         self._bias(da3, B * L3.hout ** 2, L3.cout, o["b3"])
-        dcol3 = self.dcol3[:B * L3.hout ** 2 * L3.K]
-        h.gemm_dgrad(da3, sh[o["w3"]:o["b3"]], None, dcol3, B * L3.hout ** 2, L3.cout, L3.K)
         da2 = self.da2[:B * L2.hout ** 2 * L2.cout]
-        h.col2im_mask(dcol3, a2, da2, B, L3.hin, L3.hin, L3.cin, L3.k, L3.k, L3.s)
+        self._dgrad(da3, sh[o["w3"]:o["b3"]], a2, da2, B, L3)
         # conv2
         self._wgrad("c2", da2, a1, B, L2.hin, L2.cin, L2.k, L2.s, L2.cout, o["w2"])
         self._bias(da2, B * L2.hout ** 2, L2.cout, o["b2"])
-        dcol2 = self.dcol2[:B * L2.hout ** 2 * L2.K]
-        h.gemm_dgrad(da2, sh[o["w2"]:o["b2"]], None, dcol2, B * L2.hout ** 2, L2.cout, L2.K)
         da1 = self.da1[:B * L1.hout ** 2 * L1.cout]
-        h.col2im_mask(dcol2, a1, da1, B, L2.hin, L2.hin, L2.cin, L2.k, L2.k, L2.s)
+        self._dgrad(da2, sh[o["w2"]:o["b2"]], a1, da1, B, L2)
         # conv1 (input = frames, no data gradient)
         self._wgrad("c1", da1, obs_u8.contiguous(), B, L1.hin, L1.cin, L1.k, L1.s, L1.cout, o["w1"])
         self._bias(da1, B * L1.hout ** 2, L1.cout, o["b1"])
         return stats.view(grid, 4)
+
+    def _dgrad(self, dy, w, xact, dx, B, L):
+        """dX * (X > 0): implicit phase-class GEMM when the geometry has one, else an
+        explicit column buffer + col2im (allocated on first use)."""
+        if self.h.conv_dgrad(dy, w, xact, dx, B, L.hin, L.hin, L.cin, L.k, L.k, L.s, L.cout):
+            return
+        n = B * L.hout ** 2 * L.K
+        if getattr(self, "_dcol", None) is None or self._dcol.numel() < n:
+            self._dcol = torch.empty(self.max_batch * L.hout ** 2 * L.K, dtype=torch.bfloat16, device=self.device)
+        dcol = self._dcol[:n]
+        self.h.gemm_dgrad(dy, w, None, dcol, B * L.hout ** 2, L.cout, L.K)
+        self.h.col2im_mask(dcol, xact, dx, B, L.hin, L.hin, L.cin, L.k, L.k, L.s)
 
     def _wgrad(self, name, dy, x, N, H, C, k, s, cout, off):
         K = k * k * C

@@ -83,6 +83,9 @@ def test_conv_dgrad_col2im_and_wgrad(cuda, li, N):
     dx = torch.empty(N * L.hin ** 2 * L.cin, dtype=torch.bfloat16, device=cuda)
     h.col2im_mask(dcol, xd, dx, N, L.hin, L.hin, L.cin, L.k, L.k, L.s)
     assert relerr(dx, dx_ref) < 2e-2
+    dx2 = torch.full_like(dx, float("nan"))
+    assert h.conv_dgrad(dyd, wd, xd, dx2, N, L.hin, L.hin, L.cin, L.k, L.k, L.s, L.cout)  # implicit path exists
+    assert relerr(dx2, dx_ref) < 1e-2
     for splits in (1, 7):
         s = int(h.gemm_splits(M, splits))
         part = torch.empty(s * L.cout * K, device=cuda)
