@@ -77,7 +77,7 @@ void conv_fwd(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& y
   check_geo(g);
   const bool u8 = x.scalar_type() == at::kByte;
   check(x, "x", u8 ? at::kByte : at::kBFloat16, N * H * W * C);
-  TORCH_CHECK(u8 ? (C == 4 && KW % 2 == 0) : (C % 8 == 0), "conv_fwd: unsupported channel layout");
+  TORCH_CHECK(u8 ? ((C == 4 && KW % 2 == 0) || C % 8 == 0) : (C % 8 == 0), "conv_fwd: unsupported channel layout");
   check(w, "w", at::kBFloat16, Cout * KH * KW * C);
   check(b, "b", at::kFloat, Cout);
   check(y, "y", at::kBFloat16, N * g.OH() * g.OW() * Cout);
@@ -132,7 +132,7 @@ int64_t conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& part, int64_
   check_geo(g);
   const bool u8 = x.scalar_type() == at::kByte;
   const int64_t M = N * g.OH() * g.OW(), K = KH * KW * C;
-  TORCH_CHECK(u8 ? (C == 4 && KW % 2 == 0) : (C % 8 == 0), "conv_wgrad: unsupported channel layout");
+  TORCH_CHECK(u8 ? ((C == 4 && KW % 2 == 0) || C % 8 == 0) : (C % 8 == 0), "conv_wgrad: unsupported channel layout");
   check(dy, "dy", at::kBFloat16, M * Cout);
   check(x, "x", u8 ? at::kByte : at::kBFloat16, N * H * W * C);
   const int64_t s = gemm_splits(M, splits);
@@ -243,7 +243,7 @@ void pong_step(const Tensor& state, const Tensor& act, const Tensor& rew, const 
 
 void pong_render(const Tensor& state, const Tensor& obs, int64_t N) {
   check(state, "state", at::kFloat, N * pong_state_size());
-  check(obs, "obs", at::kByte, N * 84 * 84 * 4);
+  check(obs, "obs", at::kByte, N * 84 * 84 * 4);  // [N][21][21][64] space-to-depth
   rc_check(rrl_pong_render(state.data_ptr<float>(), obs.data_ptr<uint8_t>(), (int)N, stream()), "pong_render");
 }
 

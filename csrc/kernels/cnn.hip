@@ -113,10 +113,16 @@ template <class F>
 static int with_im2col(const ConvGeom& g, const void* x, bool u8, F&& f) {
   const int M = g.M(), K = g.K();
   if (u8) {
-    if (g.C != 4 || (g.KW & 1)) return -1;
+    const uint8_t* xu = (const uint8_t*)x;
+    if (g.C % 8 == 0) {  // space-to-depth frames (the PongSynth layout: 21 x 21 x 64)
+      if (g.H == 21 && g.W == 21 && g.C == 64 && g.KH == 2 && g.KW == 2 && g.S == 1)
+        return f(U8ConvLoaderT<21, 21, 64, 2, 1, 20, 20>{xu, M, K});
+      return f(U8ConvLoader{xu, g.H, g.W, g.C, g.KW, g.S, g.OH, g.OW, M, K});
+    }
+    if (g.C != 4 || (g.KW & 1)) return -1;  // plain NHWC stacked frames
     if (g.H == 84 && g.W == 84 && g.KH == 8 && g.KW == 8 && g.S == 4)
-      return f(FrameLoaderT<84, 84, 8, 4, 20, 20>{(const uint8_t*)x, M, K});
-    return f(FrameLoader{(const uint8_t*)x, g.H, g.W, g.KW, g.S, g.OH, g.OW, M, K});
+      return f(FrameLoaderT<84, 84, 8, 4, 20, 20>{xu, M, K});
+    return f(FrameLoader{xu, g.H, g.W, g.KW, g.S, g.OH, g.OW, M, K});
   }
   if (g.C % 8) return -1;
   const uint16_t* xb = (const uint16_t*)x;

@@ -137,6 +137,53 @@ struct FrameLoaderT {
   }
 };
 
+// uint8 NHWC input with C % 8 == 0 (space-to-depth frames): 8 consecutive k are 8
+// consecutive channels of one pixel = 8 contiguous bytes, scaled by 1/255.
+__device__ __forceinline__ uint4 u8x8_to_bf16x8(uint2 b) {
+  const float s = 1.0f / 255.0f;
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t src = i < 2 ? b.x : b.y;
+    const int sh = (i & 1) * 16;
+    const float lo = (float)((src >> sh) & 0xff) * s, hi = (float)((src >> (sh + 8)) & 0xff) * s;
+    w[i] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <int H, int W, int C, int KW, int S, int OH, int OW>
+struct U8ConvLoaderT {
+  const uint8_t* x;
+  int M, K;
+  __device__ __forceinline__ uint4 operator()(int m, int k) const {
+    if (m >= M || k >= K) return make_uint4(0, 0, 0, 0);
+    const unsigned um = (unsigned)m, uk = (unsigned)k;
+    const unsigned n = um / (OH * OW), p = um - n * (OH * OW);
+    const unsigned oh = p / OW, ow = p - oh * OW;
+    const unsigned kh = uk / (KW * C), r = uk - kh * (KW * C);
+    const unsigned kw = r / C, c = r - kw * C;
+    const size_t off = (((size_t)n * H + (oh * S + kh)) * W + (ow * S + kw)) * C + c;
+    return u8x8_to_bf16x8(*reinterpret_cast<const uint2*>(x + off));
+  }
+};
+
+struct U8ConvLoader {
+  const uint8_t* x;
+  int H, W, C, KW, S, OH, OW, M, K;
+  __device__ __forceinline__ uint4 operator()(int m, int k) const {
+    if (m >= M || k >= K) return make_uint4(0, 0, 0, 0);
+    const int ohw = OH * OW;
+    const int n = m / ohw, p = m - n * ohw;
+    const int oh = p / OW, ow = p - oh * OW;
+    const int kc = KW * C;
+    const int kh = k / kc, r = k - kh * kc;
+    const int kw = r / C, c = r - kw * C;
+    const size_t off = (((size_t)n * H + (oh * S + kh)) * W + (ow * S + kw)) * C + c;
+    return u8x8_to_bf16x8(*reinterpret_cast<const uint2*>(x + off));
+  }
+};
+
 // ----------------------------------------------------------------------------- kernel
 constexpr int kGemmBK = 64;
 constexpr int kGemmPad = 8;  // bf16 elements of row padding (16 B)

@@ -121,7 +121,11 @@ __global__ void pong_step_kernel(float* __restrict__ state, const int32_t* __res
   for (int i = 0; i < kPongState; ++i) state[(size_t)e * kPongState + i] = s[i];
 }
 
-// One thread per (env, row): 84 pixels x 4 frames = 21 x 16 B.
+// One thread per (env, row): 84 pixels x 4 frames = 21 x 16 B.  The observation is
+// written space-to-depth: obs[n][a][b][dy][dx][f] with y = 4a + dy, x = 4b + dx (i.e.
+// [N][21][21][64]), so the first 8x8/4 conv becomes a 2x2/1 conv over 64 contiguous
+// channels and its im2col reads 8-byte runs; a 16-byte chunk of 4 pixels x 4 frames of
+// one row lands contiguously at (a, b, dy).
 __global__ void pong_render_kernel(const float* __restrict__ state, uint8_t* __restrict__ obs, int N) {
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (t >= (size_t)N * kPongHW) return;
@@ -129,7 +133,8 @@ __global__ void pong_render_kernel(const float* __restrict__ state, uint8_t* __r
   const float* h = state + (size_t)e * kPongState + P_HIST;
   const float fy = (float)y + 0.5f;
   const bool wall = fy < kTop || fy >= kBot;
-  uint8_t* row = obs + ((size_t)e * kPongHW + y) * kPongHW * 4;
+  const int a = y >> 2, dy = y & 3;
+  uint8_t* base = obs + (size_t)e * kPongHW * kPongHW * 4 + (size_t)a * 21 * 64 + dy * 16;
   // per-frame horizontal spans on this row
   float bx0[4], pa_on[4], po_on[4], b_on[4];
 #pragma unroll
@@ -157,7 +162,7 @@ __global__ void pong_render_kernel(const float* __restrict__ state, uint8_t* __r
       }
       w[px] = v;
     }
-    *reinterpret_cast<uint4*>(row + 16 * c) = make_uint4(w[0], w[1], w[2], w[3]);
+    *reinterpret_cast<uint4*>(base + c * 64) = make_uint4(w[0], w[1], w[2], w[3]);
   }
 }
 

@@ -5,9 +5,14 @@ float32 arithmetic order, same Philox draws), used by the CPU trainer path and b
 GPU numerics tests; ``DevicePong`` drives the kernels on a torch device.
 
 Interface (Atari Pong): 6 actions (0 NOOP, 1 FIRE, 2 RIGHT = up, 3 LEFT = down,
-4 RIGHTFIRE, 5 LEFTFIRE), frame-skip 4, observation uint8 [84, 84, 4] NHWC with the 4
-most recent frames (oldest first), reward +1 / -1 per point, episode over at 21 points
-(or ``max_steps`` agent steps).
+4 RIGHTFIRE, 5 LEFTFIRE), frame-skip 4, 84x84 grayscale frames, the 4 most recent
+frames stacked (oldest first), reward +1 / -1 per point, episode over at 21 points (or
+``max_steps`` agent steps).
+
+Observation layout: uint8 [21, 21, 64] = space-to-depth(4) of the NHWC [84, 84, 4]
+stack, obs[a][b][dy*16 + dx*4 + f] = frame f at pixel (4a + dy, 4b + dx); convert with
+``s2d_to_nhwc`` / ``nhwc_to_s2d``.  The layout is what the first conv layer streams
+(an 8x8/4 conv == a 2x2/1 conv over 64 contiguous channels).
 """
 from __future__ import annotations
 
@@ -17,7 +22,8 @@ import torch
 from ..ops.philox import philox4x32, u01
 
 NUM_ACTIONS = 6
-OBS_SHAPE = (84, 84, 4)
+OBS_SHAPE = (21, 21, 64)
+NHWC_SHAPE = (84, 84, 4)
 STATE = 32
 HW = 84
 BX, BY, VX, VY, PA, PO, SA, SO, T, RET = range(10)
@@ -34,6 +40,26 @@ def _rand(seed, step, rows, tag):
     return philox4x32(rows.astype(np.uint32), np.full_like(rows, step & 0xFFFFFFFF, dtype=np.uint32),
                       np.full_like(rows, (step >> 32) & 0xFFFFFFFF, dtype=np.uint32),
                       np.full_like(rows, tag, dtype=np.uint32), k0, k1)
+
+
+def nhwc_to_s2d(x):
+    """[..., 84, 84, 4] -> [..., 21, 21, 64] (numpy or torch)."""
+    lead = x.shape[:-3]
+    y = x.reshape(*lead, 21, 4, 21, 4, 4)
+    n = len(lead)
+    perm = tuple(range(n)) + (n, n + 2, n + 1, n + 3, n + 4)
+    y = y.transpose(perm) if isinstance(y, np.ndarray) else y.permute(perm)
+    return y.reshape(*lead, 21, 21, 64)
+
+
+def s2d_to_nhwc(x):
+    """[..., 21, 21, 64] -> [..., 84, 84, 4] (numpy or torch)."""
+    lead = x.shape[:-3]
+    y = x.reshape(*lead, 21, 21, 4, 4, 4)
+    n = len(lead)
+    perm = tuple(range(n)) + (n, n + 2, n + 1, n + 3, n + 4)
+    y = y.transpose(perm) if isinstance(y, np.ndarray) else y.permute(perm)
+    return y.reshape(*lead, 84, 84, 4)
 
 
 class PongRef:
@@ -136,6 +162,10 @@ class PongRef:
         return reward, over.astype(f32), fin_ret, fin_len
 
     def render(self) -> np.ndarray:
+        """Observation in the device layout (space-to-depth, [N, 21, 21, 64])."""
+        return np.ascontiguousarray(nhwc_to_s2d(self.render_nhwc()))
+
+    def render_nhwc(self) -> np.ndarray:
         N = self.N
         h = self.s[:, HIST:HIST + 16].reshape(N, 4, 4)
         fy = np.arange(HW, dtype=f32) + f32(0.5)

@@ -1,8 +1,8 @@
 """Nature-CNN actor-critic for pixel observations (A2C / Pong configuration, BASELINE.json
 config 4 -- a model family the reference does not have; SURVEY §2.6 "New: CNN encoder").
 
-    obs uint8 [B, 84, 84, 4] (NHWC, 4 stacked frames)
-    conv 8x8/4  4 -> 32, ReLU      (84 -> 20)
+    obs uint8 [B, 21, 21, 64]  (space-to-depth(4) of the [84, 84, 4] NHWC frame stack)
+    conv 8x8/4  4 -> 32, ReLU      (84 -> 20; run as a 2x2/1 conv over the 64 s2d channels)
     conv 4x4/2 32 -> 64, ReLU      (20 -> 9)
     conv 3x3/1 64 -> 64, ReLU      (9 -> 7)
     fc 3136 -> 512, ReLU           (NHWC flatten)
@@ -10,7 +10,8 @@ config 4 -- a model family the reference does not have; SURVEY §2.6 "New: CNN e
 
 Parameters are ONE flat fp32 vector (master copy for Adam and the RCCL all-reduce) with
 conv weights stored [Cout][KH][KW][Cin] so that the implicit-GEMM reduction index
-(kh, kw, c) is contiguous in both operands; the device path keeps a bf16 shadow copy
+(kh, kw, c) is contiguous in both operands (conv1 in its space-to-depth order
+[32][kh2][kw2][dy][dx][c] with kh = 4*kh2 + dy, kw = 4*kw2 + dx); the device path keeps a bf16 shadow copy
 of the same vector for the MFMA GEMMs (written by the fused Adam).
 
 ``DeviceNatureCNN`` runs everything through the gfx950 kernels (csrc/kernels/cnn.hip);
@@ -48,6 +49,25 @@ class ConvLayer:
 
 
 CONVS = (ConvLayer(FRAMES, 32, 8, 4, FRAME_HW), ConvLayer(32, 64, 4, 2, 20), ConvLayer(64, 64, 3, 1, 9))
+# the geometry conv1 actually runs with on the space-to-depth input
+S2D = ConvLayer(64, 32, 2, 1, 21)
+OBS_S2D = (21, 21, 64)
+
+
+def conv1_s2d_to_khkwc(w):
+    """conv1 weights [32, 2, 2, 64] (s2d order) -> [32, 8, 8, 4] ([Cout][kh][kw][c])."""
+    return w.reshape(32, 2, 2, 4, 4, 4).permute(0, 1, 3, 2, 4, 5).reshape(32, 8, 8, 4)
+
+
+def conv1_khkwc_to_s2d(w):
+    return w.reshape(32, 2, 4, 2, 4, 4).permute(0, 1, 3, 2, 4, 5).reshape(32, 2, 2, 64)
+
+
+def obs_to_nchw(obs_u8):
+    """uint8 observations (s2d [B, 21, 21, 64] or NHWC [B, 84, 84, 4]) -> float NCHW / 255."""
+    if tuple(obs_u8.shape[1:]) == OBS_S2D:
+        obs_u8 = obs_u8.reshape(-1, 21, 21, 4, 4, 4).permute(0, 1, 3, 2, 4, 5).reshape(-1, 84, 84, 4)
+    return (obs_u8.float() / 255.0).permute(0, 3, 1, 2)
 FC_IN = CONVS[-1].hout ** 2 * CONVS[-1].cout  # 3136
 
 
@@ -108,7 +128,8 @@ class CNNSpec:
         o = self.offsets()
         v = {}
         for i, L in enumerate(CONVS, 1):
-            v[f"w{i}"] = params[o[f"w{i}"]:o[f"b{i}"]].view(L.cout, L.k, L.k, L.cin)
+            w = params[o[f"w{i}"]:o[f"b{i}"]]
+            v[f"w{i}"] = conv1_s2d_to_khkwc(w) if i == 1 else w.view(L.cout, L.k, L.k, L.cin)
             v[f"b{i}"] = params[o[f"b{i}"]:o[f"b{i}"] + L.cout]
         v["wfc"] = params[o["wfc"]:o["bfc"]].view(HIDDEN, FC_IN)
         v["bfc"] = params[o["bfc"]:o["bfc"] + HIDDEN]
@@ -128,7 +149,7 @@ def reference_forward(spec: CNNSpec, params: torch.Tensor, obs_u8: torch.Tensor,
     """fp32 oracle.  ``emulate_bf16`` rounds weights, the scaled input and every stored
     activation to bf16 exactly where the device path does.  Returns (logits, value, acts)."""
     v = spec.views(params)
-    x = _bf(obs_u8.float() / 255.0, emulate_bf16).permute(0, 3, 1, 2)
+    x = _bf(obs_to_nchw(obs_u8), emulate_bf16)
     acts = []
     for i, L in enumerate(CONVS, 1):
         w = _bf(v[f"w{i}"], emulate_bf16).permute(0, 3, 1, 2)
@@ -226,7 +247,8 @@ class DeviceNatureCNN:
         a3 = self._rows(self.a3, row0, n, FC_IN)
         hid = self._rows(self.hid, row0, n, HIDDEN)
         x = obs_u8.contiguous()
-        for i, (L, y) in enumerate(zip(CONVS, (a1, a2, a3)), 1):
+        assert tuple(x.shape[1:]) == OBS_S2D, "device CNN takes space-to-depth observations [n, 21, 21, 64]"
+        for i, (L, y) in enumerate(zip((S2D,) + CONVS[1:], (a1, a2, a3)), 1):
             h.conv_fwd(x, sh[o[f"w{i}"]:o[f"b{i}"]], p[o[f"b{i}"]:o[f"b{i}"] + L.cout], y, n, L.hin, L.hin, L.cin,
                        L.k, L.k, L.s, L.cout, True)
             x = y
@@ -294,7 +316,7 @@ class DeviceNatureCNN:
         da1 = self.da1[:B * L1.hout ** 2 * L1.cout]
         self._dgrad(da2, sh[o["w2"]:o["b2"]], a1, da1, B, L2)
         # conv1 (input = frames, no data gradient)
-        self._wgrad("c1", da1, obs_u8.contiguous(), B, L1.hin, L1.cin, L1.k, L1.s, L1.cout, o["w1"])
+        self._wgrad("c1", da1, obs_u8.contiguous(), B, S2D.hin, S2D.cin, S2D.k, S2D.s, S2D.cout, o["w1"])
         self._bias(da1, B * L1.hout ** 2, L1.cout, o["b1"])
         return stats.view(grid, 4)
 

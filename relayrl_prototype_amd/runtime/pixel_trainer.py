@@ -61,7 +61,7 @@ class PixelA2CTrainer:
         env_seed = (cfg.seed * 1000003 + rank * 7919 + 17) & 0x7FFFFFFFFFFFFFFF
         self.sample_seed = (cfg.seed * 2654435761 + rank * 97 + 5) & 0x7FFFFFFFFFFFFFFF
         dev = self.device
-        self.obs = torch.zeros((T + 1, N, 84, 84, 4), dtype=torch.uint8, device=dev)
+        self.obs = torch.zeros((T + 1, N, 21, 21, 64), dtype=torch.uint8, device=dev)  # space-to-depth frames
         self.act = torch.zeros((T, N), dtype=torch.int32, device=dev)
         self.logp = torch.zeros((T, N), device=dev)
         self.val = torch.zeros((T + 1, N), device=dev)
@@ -107,7 +107,7 @@ class PixelA2CTrainer:
         with self.timer.phase("Returns"):
             adv, ret, _ = gae_scan_tm(self.rew, self.done, self.val, cfg.gamma, 1.0)
         with self.timer.phase("Backward"):
-            stats = m.backward(self.obs[:T].reshape(B, 84, 84, 4), self.act.reshape(B), adv.reshape(B),
+            stats = m.backward(self.obs[:T].reshape(B, 21, 21, 64), self.act.reshape(B), adv.reshape(B),
                                ret.reshape(B), cfg.vf_coef, cfg.ent_coef)
         with self.timer.phase("Optimize"):
             m.apply(cfg.lr, cfg.max_grad_norm, self.comm)
@@ -136,7 +136,7 @@ class PixelA2CTrainer:
         N, T = cfg.num_envs, cfg.rollout_len
         B = N * T
         adv, ret, _ = gae_scan_tm(self.rew, self.done, self.val, cfg.gamma, 1.0)
-        logits, value, _ = reference_forward(self.spec, self.params, self.obs[:T].reshape(B, 84, 84, 4))
+        logits, value, _ = reference_forward(self.spec, self.params, self.obs[:T].reshape(B, 21, 21, 64))
         loss, pg, vf, ent = a2c_loss(logits, value, self.act.reshape(B), adv.reshape(B), ret.reshape(B), cfg.vf_coef,
                                      cfg.ent_coef)
         self.opt.zero_grad()

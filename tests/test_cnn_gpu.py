@@ -9,6 +9,7 @@ import torch
 import torch.nn.functional as F
 
 from relayrl_prototype_amd.models.nature_cnn import (CONVS, FC_IN, HIDDEN, CNNSpec, DeviceNatureCNN, a2c_loss,
+                                                    conv1_khkwc_to_s2d, conv1_s2d_to_khkwc, obs_to_nchw,
                                                     reference_forward)
 
 pytestmark = pytest.mark.gpu
@@ -21,6 +22,22 @@ def relerr(a, b):
 
 def _bf(x):
     return x.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("N", [1, 7, 64])
+def test_conv1_forward_s2d(cuda, N):
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    g = torch.Generator().manual_seed(N)
+    x = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g)
+    w = torch.randn(32, 8, 8, 4, generator=g) * 0.05
+    b = torch.randn(32, generator=g) * 0.1
+    y = torch.empty(N * 400 * 32, dtype=torch.bfloat16, device=cuda)
+    h.conv_fwd(x.to(cuda), conv1_khkwc_to_s2d(w).contiguous().to(cuda).bfloat16().reshape(-1), b.to(cuda), y, N, 21,
+               21, 64, 2, 2, 1, 32, True)
+    ref = F.relu(F.conv2d(_bf(obs_to_nchw(x)), _bf(w).permute(0, 3, 1, 2), b, stride=4))
+    assert relerr(y, ref.permute(0, 2, 3, 1).reshape(-1)) < 1e-2
 
 
 @pytest.mark.parametrize("N", [1, 7, 64])
@@ -101,6 +118,26 @@ def test_conv_dgrad_col2im_and_wgrad(cuda, li, N):
     assert relerr(db, dy.reshape(-1, L.cout).sum(0)) < 1e-4
 
 
+def test_conv1_wgrad_from_s2d_frames(cuda):
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    N = 9
+    g = torch.Generator().manual_seed(12)
+    x = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g)
+    dy = _bf(torch.randn(N, 20, 20, 32, generator=g))
+    wt = torch.zeros(32, 4, 8, 8, requires_grad=True)
+    F.conv2d(_bf(obs_to_nchw(x)), wt, stride=4).backward(dy.permute(0, 3, 1, 2))
+    dw_ref = conv1_khkwc_to_s2d(wt.grad.permute(0, 2, 3, 1)).reshape(-1)
+    M = N * 400
+    s = int(h.gemm_splits(M, 16))
+    part = torch.empty(s * 32 * 256, device=cuda)
+    h.conv_wgrad(dy.to(cuda).bfloat16().reshape(-1), x.to(cuda), part, 16, N, 21, 21, 64, 2, 2, 1, 32)
+    dw = torch.empty(32 * 256, device=cuda)
+    h.sum_splits(part, s, 32 * 256, dw)
+    assert relerr(dw, dw_ref) < 1e-2
+
+
 def test_conv1_wgrad_from_frames(cuda):
     from relayrl_prototype_amd.ops import hip
 
@@ -147,7 +184,7 @@ def test_full_model_forward_backward_matches_autograd(cuda):
     params[o["wpi"]:o["bpi"]] *= 50.0
     m = DeviceNatureCNN(spec, cuda, max_batch=B, params=params)
     g = torch.Generator().manual_seed(5)
-    obs = torch.randint(0, 256, (B, 84, 84, 4), dtype=torch.uint8, generator=g)
+    obs = torch.randint(0, 256, (B, 21, 21, 64), dtype=torch.uint8, generator=g)
     act = torch.randint(0, 6, (B,), dtype=torch.int32, generator=g)
     adv = torch.randn(B, generator=g)
     ret = torch.randn(B, generator=g)
@@ -204,7 +241,7 @@ def test_head_sampling_distribution(cuda):
     o = spec.offsets()
     params[o["wpi"]:o["bpi"]] *= 80.0
     m = DeviceNatureCNN(spec, cuda, max_batch=B, params=params)
-    obs = torch.randint(0, 256, (1, 84, 84, 4), dtype=torch.uint8).expand(B, 84, 84, 4).contiguous().to(cuda)
+    obs = torch.randint(0, 256, (1, 21, 21, 64), dtype=torch.uint8).expand(B, 21, 21, 64).contiguous().to(cuda)
     act = torch.empty(B, dtype=torch.int32, device=cuda)
     logp = torch.empty(B, device=cuda)
     val = torch.empty(B, device=cuda)
@@ -222,7 +259,7 @@ def test_device_pong_matches_reference(cuda):
     N, steps = 64, 60
     ref = PongRef(N, seed=21, max_steps=50)
     dev = DevicePong(N, cuda, seed=21, max_steps=50)
-    obs = torch.empty(N, 84, 84, 4, dtype=torch.uint8, device=cuda)
+    obs = torch.empty(N, 21, 21, 64, dtype=torch.uint8, device=cuda)
     o_ref = ref.reset()
     dev.reset(obs)
     assert (obs.cpu().numpy() != o_ref).mean() < 1e-3

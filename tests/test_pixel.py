@@ -5,7 +5,7 @@ import pytest
 import torch
 import torch.distributed as dist
 
-from relayrl_prototype_amd.envs.pong import PongRef
+from relayrl_prototype_amd.envs.pong import PongRef, nhwc_to_s2d, s2d_to_nhwc
 from relayrl_prototype_amd.models.nature_cnn import CNNSpec, a2c_loss, reference_forward
 
 
@@ -16,8 +16,11 @@ def test_cnn_spec_layout_and_forward():
     assert spec.P == 8192 + 32 + 32768 + 64 + 36864 + 64 + 3136 * 512 + 512 + 6 * 512 + 6 + 512 + 1
     p = spec.init(0)
     assert torch.equal(p, spec.init(0)) and not torch.equal(p, spec.init(1))
-    obs = torch.randint(0, 256, (3, 84, 84, 4), dtype=torch.uint8)
+    obs = torch.randint(0, 256, (3, 21, 21, 64), dtype=torch.uint8)
     logits, value, acts = reference_forward(spec, p, obs)
+    # the NHWC form of the same frames gives the same outputs
+    l_n, v_n, _ = reference_forward(spec, p, s2d_to_nhwc(obs).contiguous())
+    assert torch.allclose(l_n, logits) and torch.allclose(v_n, value)
     assert logits.shape == (3, 6) and value.shape == (3,)
     assert [a.shape[1:] for a in acts[:3]] == [(32, 20, 20), (64, 9, 9), (64, 7, 7)] and acts[3].shape == (3, 512)
     # bf16 emulation stays close to fp32
@@ -25,10 +28,23 @@ def test_cnn_spec_layout_and_forward():
     assert torch.allclose(l2, logits, atol=5e-3) and torch.allclose(v2, value, rtol=5e-2, atol=5e-2)
 
 
+def test_conv1_s2d_weight_order_roundtrip():
+    from relayrl_prototype_amd.models.nature_cnn import conv1_khkwc_to_s2d, conv1_s2d_to_khkwc
+
+    w = torch.randn(32, 8, 8, 4)
+    assert torch.equal(conv1_s2d_to_khkwc(conv1_khkwc_to_s2d(w)), w)
+    # 8x8/4 conv on NHWC == 2x2/1 conv on the s2d input with s2d-ordered weights
+    x = torch.rand(2, 84, 84, 4)
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), stride=4)
+    xs = nhwc_to_s2d(x).permute(0, 3, 1, 2)
+    ws = conv1_khkwc_to_s2d(w).permute(0, 3, 1, 2)
+    assert torch.allclose(torch.nn.functional.conv2d(xs, ws, stride=1), ref, atol=1e-4)
+
+
 def test_a2c_loss_gradients_finite():
     spec = CNNSpec(6)
     p = spec.init(0).requires_grad_(True)
-    obs = torch.randint(0, 256, (4, 84, 84, 4), dtype=torch.uint8)
+    obs = torch.randint(0, 256, (4, 21, 21, 64), dtype=torch.uint8)
     lg, v, _ = reference_forward(spec, p, obs)
     loss, pg, vf, ent = a2c_loss(lg, v, torch.tensor([0, 1, 2, 5]), torch.randn(4), torch.randn(4), 0.5, 0.01)
     loss.backward()
@@ -39,7 +55,9 @@ def test_a2c_loss_gradients_finite():
 def test_pong_reference_dynamics():
     env = PongRef(16, seed=3, max_steps=400)
     obs = env.reset()
-    assert obs.shape == (16, 84, 84, 4) and obs.dtype == np.uint8
+    assert obs.shape == (16, 21, 21, 64) and obs.dtype == np.uint8
+    assert np.array_equal(nhwc_to_s2d(s2d_to_nhwc(obs)), obs)
+    obs = s2d_to_nhwc(obs)
     assert (obs[:, 0] == 100).all() and (obs[:, 83] == 100).all()  # walls
     assert (obs == 255).any()  # paddles / ball drawn
     rng = np.random.default_rng(0)
@@ -52,7 +70,7 @@ def test_pong_reference_dynamics():
         assert set(np.unique(r)).issubset({-1.0, 0.0, 1.0})
     assert (total < 0).sum() >= 8  # a random paddle loses points to the tracking opponent
     assert dones >= 16  # max_steps truncation (or 21 points) ended every env at least once
-    o = env.render()
+    o = env.render_nhwc()
     # the newest frame's ball is drawn where the state says
     bx, by = env.s[0, 16 + 12], env.s[0, 16 + 13]
     if 0 <= bx < 83 and 2 <= by < 81:
