@@ -24,18 +24,19 @@ struct ConvGeom {
 };
 
 // ----------------------------------------------------------------------------- epilogues
-struct BiasReluStore {  // bf16 [M][N] = act(acc + b[n])
+struct BiasReluStore {  // bf16 [M][N] = act(scale * acc + b[n])
   uint16_t* y;
   const float* b;
   int M, N;
   bool relu;
+  float scale;
   __device__ __forceinline__ void operator()(int m, int n, f32x4_t acc, int) const {
     if (n >= N) return;
     const float bb = b ? b[n] : 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (m + r < M) {
-        float v = acc[r] + bb;
+        float v = scale * acc[r] + bb;
         if (relu) v = fmaxf(v, 0.f);
         y[(size_t)(m + r) * N + n] = f2bf(v);
       }
@@ -73,18 +74,20 @@ struct PartialStore {  // fp32 [split][M][N]
   }
 };
 
-struct PartialStoreT {  // fp32 [split][N][M]: the GEMM computed the transpose (rows = k, cols = cout)
+struct PartialStoreT {  // fp32 [split][N][M] = scale * acc: the GEMM computed the transpose (rows = k, cols = cout)
   float* out;
   int M, N;  // GEMM dims: M = K of the conv (rows), N = Cout
+  float scale;
   __device__ __forceinline__ void operator()(int m, int n, f32x4_t acc, int z) const {
     if (n >= N) return;
     float* o = out + (size_t)z * M * N + (size_t)n * M;
     if (m + 3 < M) {
-      *reinterpret_cast<float4*>(o + m) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      *reinterpret_cast<float4*>(o + m) =
+          make_float4(scale * acc[0], scale * acc[1], scale * acc[2], scale * acc[3]);
     } else {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (m + r < M) o[m + r] = acc[r];
+        if (m + r < M) o[m + r] = scale * acc[r];
     }
   }
 };
@@ -631,7 +634,7 @@ int rrl_conv_fwd(const void* x, int x_u8, const uint16_t* w, const float* b, uin
   ConvGeom g{N, H, W, C, KH, KW, S, (H - KH) / S + 1, (W - KW) / S + 1, Cout};
   const int M = g.M(), K = g.K();
   RowLoader lw{w, Cout, K};
-  BiasReluStore epi{y, b, M, Cout, relu != 0};
+  BiasReluStore epi{y, b, M, Cout, relu != 0, x_u8 ? kU8Scale : 1.0f};
   const int tiles = ((M + 127) / 128) * ((Cout + 63) / 64);
   int splits = 1;
   if (!x_u8 && work != nullptr && Cout >= 64 && tiles < 160 && K >= 1024) {
@@ -698,7 +701,7 @@ int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, int
   ConvGeom g{N, H, W, C, KH, KW, S, (H - KH) / S + 1, (W - KW) / S + 1, Cout};
   const int M = g.M(), K = g.K();
   RowLoader ly{dy, M, Cout};
-  PartialStoreT epi{part, K, Cout};
+  PartialStoreT epi{part, K, Cout, x_u8 ? kU8Scale : 1.0f};
   return with_im2col(g, x, x_u8 != 0, [&](auto lx) -> int {
     return Cout >= 64 ? launch_gemm<128, 64, true, true>(lx, ly, epi, K, Cout, M, splits, st)
                       : launch_gemm<128, 32, true, true>(lx, ly, epi, K, Cout, M, splits, st);

@@ -36,6 +36,23 @@ __device__ __forceinline__ uint16_t f2bf(float f) {  // round-to-nearest-even
 }
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
+// uint8 inputs are fed to the MFMA as exact integers 0..255 in bf16 (8 significant bits
+// fit the bf16 mantissa, so the conversion is a byte->f32 convert plus taking the high
+// half -- no rounding); the 1/255 input scale is applied to the fp32 accumulator in the
+// epilogue instead (kU8Scale).  uint8 NHWC input with C % 8 == 0 (space-to-depth
+// frames): 8 consecutive k = 8 consecutive channels of one pixel = 8 contiguous bytes.
+constexpr float kU8Scale = 1.0f / 255.0f;
+__device__ __forceinline__ uint32_t pack_hi16(float lo, float hi) {
+  return (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+}
+__device__ __forceinline__ uint4 u8x8_to_bf16x8(uint2 b) {
+  return make_uint4(pack_hi16((float)(b.x & 0xff), (float)((b.x >> 8) & 0xff)),
+                    pack_hi16((float)((b.x >> 16) & 0xff), (float)(b.x >> 24)),
+                    pack_hi16((float)(b.y & 0xff), (float)((b.y >> 8) & 0xff)),
+                    pack_hi16((float)((b.y >> 16) & 0xff), (float)(b.y >> 24)));
+}
+
+
 // ----------------------------------------------------------------------------- loaders
 // Plain row-major bf16 matrix [rows][cols] (cols % 8 == 0).
 struct RowLoader {
@@ -67,7 +84,7 @@ struct ConvLoader {
 };
 
 // Implicit im2col over uint8 NHWC frames with C == 4 (stacked grayscale frames): 8
-// consecutive k are 2 adjacent pixels x 4 channels = 8 contiguous bytes, scaled by 1/255.
+// consecutive k are 2 adjacent pixels x 4 channels = 8 contiguous bytes (raw 0..255, see kU8Scale).
 struct FrameLoader {
   const uint8_t* x;
   int H, W, KW, S, OH, OW, M, K;
@@ -79,17 +96,7 @@ struct FrameLoader {
     const int kc = KW * 4;
     const int kh = k / kc, kw = (k - kh * kc) >> 2;
     const size_t off = (((size_t)n * H + (oh * S + kh)) * W + (ow * S + kw)) * 4;
-    const uint2 b = *reinterpret_cast<const uint2*>(x + off);
-    const float s = 1.0f / 255.0f;
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t src = i < 2 ? b.x : b.y;
-      const int sh = (i & 1) * 16;
-      const float lo = (float)((src >> sh) & 0xff) * s, hi = (float)((src >> (sh + 8)) & 0xff) * s;
-      w[i] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
-    }
-    return make_uint4(w[0], w[1], w[2], w[3]);
+    return u8x8_to_bf16x8(*reinterpret_cast<const uint2*>(x + off));
   }
 };
 
@@ -123,34 +130,9 @@ struct FrameLoaderT {
     const unsigned oh = p / OW, ow = p - oh * OW;
     const unsigned kh = uk / (KW * 4), kw = (uk - kh * (KW * 4)) >> 2;
     const size_t off = (((size_t)n * H + (oh * S + kh)) * W + (ow * S + kw)) * 4;
-    const uint2 b = *reinterpret_cast<const uint2*>(x + off);
-    const float s = 1.0f / 255.0f;
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t src = i < 2 ? b.x : b.y;
-      const int sh = (i & 1) * 16;
-      const float lo = (float)((src >> sh) & 0xff) * s, hi = (float)((src >> (sh + 8)) & 0xff) * s;
-      w[i] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
-    }
-    return make_uint4(w[0], w[1], w[2], w[3]);
+    return u8x8_to_bf16x8(*reinterpret_cast<const uint2*>(x + off));
   }
 };
-
-// uint8 NHWC input with C % 8 == 0 (space-to-depth frames): 8 consecutive k are 8
-// consecutive channels of one pixel = 8 contiguous bytes, scaled by 1/255.
-__device__ __forceinline__ uint4 u8x8_to_bf16x8(uint2 b) {
-  const float s = 1.0f / 255.0f;
-  uint32_t w[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t src = i < 2 ? b.x : b.y;
-    const int sh = (i & 1) * 16;
-    const float lo = (float)((src >> sh) & 0xff) * s, hi = (float)((src >> (sh + 8)) & 0xff) * s;
-    w[i] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
-}
 
 template <int H, int W, int C, int KW, int S, int OH, int OW>
 struct U8ConvLoaderT {
