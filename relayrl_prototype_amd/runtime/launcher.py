@@ -1,0 +1,267 @@
+"""Launcher: one process per GPU, named presets for the five BASELINE.json configurations.
+
+    python -m relayrl_prototype_amd train --preset cartpole-reinforce-baseline --gpus 1 --epochs 50
+    python -m relayrl_prototype_amd train --preset pong-a2c --gpus 8 --epochs 2000
+
+``--gpus N > 1`` outside torchrun starts ``torch.distributed.run`` as a CHILD process
+(never an exec, nothing touches the GPU before it) with a 127.0.0.1 rendezvous, and
+returns its exit code; each rank then runs ``run_preset``.  The reference has no
+launcher (one Python process per TrainingServer, training_server_wrapper.rs); its only
+multi-process story was N agents over TCP (config 1 here).
+
+Every preset logs the reference's progress.txt columns plus throughput columns through
+``EpochLogger`` (rank 0) and can checkpoint / resume (utils/checkpoint.py).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+from dataclasses import dataclass
+from typing import Callable, Dict, Optional
+
+
+@dataclass
+class Preset:
+    name: str
+    baseline_config: str
+    kind: str  # vec | host | actor_learner | pixel | agent_server
+    overrides: Dict
+
+
+PRESETS: Dict[str, Preset] = {
+    "cartpole-reinforce-zmq": Preset(
+        "cartpole-reinforce-zmq", "REINFORCE (no baseline) CartPole-v1, 1 agent <-> 1 trainer over ZMQ on CPU",
+        "agent_server", {"env": "CartPole-v1", "server_type": "zmq", "episodes_per_epoch": 8}),
+    "cartpole-reinforce-baseline": Preset(
+        "cartpole-reinforce-baseline", "REINFORCE-with-baseline CartPole-v1, 1 actor+learner per MI355X",
+        "vec", {"env": "CartPole-v1", "num_envs": 32768, "rollout_len": 64, "with_baseline": True}),
+    "lunarlander-reinforce-baseline": Preset(
+        "lunarlander-reinforce-baseline", "REINFORCE-with-baseline LunarLander, actor GPUs -> learner via RCCL gather",
+        "actor_learner", {"env": "LunarLanderSynth-v0", "num_envs": 2048, "rollout_len": 128, "with_baseline": True,
+                          "learner_acts": True, "num_threads": 8}),
+    "pong-a2c": Preset(
+        "pong-a2c", "A2C Pong pixels, Nature-CNN on MFMA, DP gradient all-reduce",
+        "pixel", {"num_envs": 1024, "rollout_len": 5}),
+    "halfcheetah-ppo": Preset(
+        "halfcheetah-ppo", "PPO HalfCheetah continuous Gaussian policy, large-batch GAE",
+        "host", {"env": "HalfCheetahSynth-v0", "algo": "ppo", "num_envs": 4096, "rollout_len": 256,
+                 "train_pi_iters": 10, "train_vf_iters": 10, "num_threads": 8, "with_baseline": True}),
+}
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _make_trainer(preset: Preset, comm, device, overrides: Dict):
+    kw = dict(preset.overrides)
+    kw.update(overrides)
+    if preset.kind == "vec":
+        from .vec_trainer import VecTrainer, VecTrainerConfig
+
+        return VecTrainer(VecTrainerConfig(**_filter(VecTrainerConfig, kw)), comm, device)
+    if preset.kind == "host":
+        from .host_trainer import HostTrainerConfig, HostVecTrainer
+
+        return HostVecTrainer(HostTrainerConfig(**_filter(HostTrainerConfig, kw)), comm, device)
+    if preset.kind == "actor_learner":
+        from .actor_learner import ActorLearner, ActorLearnerConfig
+
+        return ActorLearner(ActorLearnerConfig(**_filter(ActorLearnerConfig, kw)), comm, device)
+    if preset.kind == "pixel":
+        from .pixel_trainer import PixelA2CConfig, PixelA2CTrainer
+
+        return PixelA2CTrainer(PixelA2CConfig(**_filter(PixelA2CConfig, kw)), comm, device)
+    raise ValueError(preset.kind)
+
+
+def _filter(cls, kw: Dict) -> Dict:
+    import dataclasses
+
+    names = {f.name for f in dataclasses.fields(cls)}
+    return {k: v for k, v in kw.items() if k in names}
+
+
+def _epoch(tr):
+    if hasattr(tr, "train_epoch"):
+        return tr.train_epoch()
+    return tr.step()
+
+
+def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optional[Dict] = None,
+               checkpoint_every: int = 0, resume: Optional[str] = None, log_every: int = 1,
+               on_metrics: Optional[Callable[[Dict], None]] = None) -> Dict:
+    """Run one rank of a preset for ``epochs`` epochs; returns the last metrics (rank 0)."""
+    import torch
+
+    from ..parallel.comm import Comm, dist_env, init_distributed
+    from ..utils.logger import EpochLogger, setup_logger_kwargs
+
+    preset = PRESETS[name]
+    overrides = dict(overrides or {})
+    if preset.kind == "agent_server":
+        return _run_agent_server(preset, epochs, out_dir, overrides)
+    _, local_rank, world = dist_env()
+    comm = init_distributed() if world > 1 else Comm()
+    if torch.cuda.is_available():
+        dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    tr = _make_trainer(preset, comm, dev, overrides)
+    if resume:
+        from ..utils.checkpoint import load_checkpoint
+
+        st = load_checkpoint(resume)
+        tr.load_state_dict(st["trainer"])
+    logger = None
+    if comm.rank == 0:
+        kw = setup_logger_kwargs(f"relayrl-{name}", seed=int(overrides.get("seed", 0)), data_dir=out_dir)
+        logger = EpochLogger(**kw, quiet=True)
+        logger.save_config({"preset": name, "overrides": overrides, "world_size": comm.world,
+                            "baseline_config": preset.baseline_config})
+    t0 = time.perf_counter()
+    last: Dict = {}
+    for ep in range(1, epochs + 1):
+        _epoch(tr)
+        if ep % log_every == 0 or ep == epochs:
+            m = tr.metrics()
+            el = time.perf_counter() - t0
+            if comm.rank == 0 and m:
+                m = dict(m)
+                m["Time"] = el
+                if "EnvSteps" in m and el > 0:
+                    m["EnvStepsPerSec"] = m["EnvSteps"] / el
+                for k, v in m.items():
+                    if isinstance(v, (int, float)):
+                        logger.log_tabular(k, v)
+                logger.dump_tabular()
+                last = m
+                if on_metrics:
+                    on_metrics(m)
+        if checkpoint_every and ep % checkpoint_every == 0 and comm.rank == 0 and hasattr(tr, "state_dict"):
+            from ..utils.checkpoint import save_checkpoint
+
+            save_checkpoint(os.path.join(out_dir, f"{name}_ckpt"), {"trainer": tr.state_dict(), "epoch": ep})
+    if hasattr(tr, "finish"):
+        tr.finish()
+    return last
+
+
+def _run_agent_server(preset: Preset, epochs: int, out_dir: str, overrides: Dict) -> Dict:
+    """Config 1: TrainingServer + RelayRLAgent over ZMQ (or gRPC) in one process, CPU only."""
+    import numpy as np
+
+    from .. import _native
+    from ..api.agent import RelayRLAgent
+    from ..api.server import TrainingServer
+    from ..config import DEFAULT_CONFIG_CONTENT
+
+    os.makedirs(out_dir, exist_ok=True)
+    cfg = json.loads(DEFAULT_CONFIG_CONTENT)
+    for k in ("training_server", "trajectory_server", "agent_listener"):
+        cfg["server"][k]["port"] = str(_free_port())
+    per = int(overrides.get("episodes_per_epoch", preset.overrides["episodes_per_epoch"]))
+    cfg["algorithms"]["REINFORCE"]["traj_per_epoch"] = per
+    cfg_path = os.path.join(out_dir, "relayrl_config.json")
+    with open(cfg_path, "w") as f:
+        json.dump(cfg, f, indent=2)
+    st = overrides.get("server_type", preset.overrides["server_type"])
+    srv = TrainingServer("REINFORCE", 4, 2, 1_000_000, env_dir=out_dir, config_path=cfg_path, server_type=st,
+                         device="cpu")
+    agent = RelayRLAgent(config_path=cfg_path, server_type=st)
+    env = _native.VecEnv(overrides.get("env", "CartPole-v1"), 1, int(overrides.get("seed", 0)), 1)
+    obs = np.zeros((1, env.obs_dim), np.float32)
+    rew = np.zeros(1, np.float32)
+    done = np.zeros(1, np.float32)
+    act = np.zeros(1, np.int32)
+    env.reset_ptr(obs.ctypes.data)
+    steps, t0 = 0, time.perf_counter()
+    try:
+        for _ in range(epochs * per):
+            r = 0.0
+            while True:
+                a = agent.request_for_action(obs[0], None, r)
+                act[0] = int(np.asarray(a.get_act()).reshape(-1)[0])
+                env.step_ptr(act.ctypes.data, obs.ctypes.data, rew.ctypes.data, done.ctypes.data)
+                r = float(rew[0])
+                steps += 1
+                if done[0] > 0:
+                    agent.flag_last_action(r)
+                    break
+        srv.wait_idle(60)
+        el = time.perf_counter() - t0
+        return {"EnvSteps": steps, "EnvStepsPerSec": steps / el, "Updates": srv.service.updates,
+                "ModelVersion": agent.model_version}
+    finally:
+        agent.close()
+        srv.close(save=True)
+
+
+def spawn_ranks(argv, gpus: int) -> int:
+    """Start torch.distributed.run as a child with one rank per GPU; returns its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m", "relayrl_prototype_amd"] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    return subprocess.call(cmd, env=env)
+
+
+def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    ap = argparse.ArgumentParser(prog="python -m relayrl_prototype_amd")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    t = sub.add_parser("train", help="run a training preset (one process per GPU)")
+    t.add_argument("--preset", choices=sorted(PRESETS), default="cartpole-reinforce-baseline")
+    t.add_argument("--gpus", type=int, default=1)
+    t.add_argument("--epochs", type=int, default=20)
+    t.add_argument("--out", default="runs")
+    t.add_argument("--set", nargs="*", default=[], help="overrides key=value (e.g. num_envs=8192)")
+    t.add_argument("--checkpoint-every", type=int, default=0)
+    t.add_argument("--resume", default=None)
+    sub.add_parser("presets", help="list the presets")
+    b = sub.add_parser("build", help="compile the HIP and C++ extensions in-tree")
+    b.add_argument("--force", action="store_true")
+    p = sub.add_parser("plot", help="plot progress.txt runs")
+    p.add_argument("rest", nargs=argparse.REMAINDER)
+    a = ap.parse_args(argv)
+    if a.cmd == "presets":
+        for k, v in PRESETS.items():
+            print(f"{k:34s} [{v.kind}] {v.baseline_config}")
+        return 0
+    if a.cmd == "build":
+        from .._build import build
+
+        build(force=a.force)
+        return 0
+    if a.cmd == "plot":
+        from ..utils.plot import main as plot_main
+
+        plot_main(a.rest)
+        return 0
+    in_torchrun = "LOCAL_RANK" in os.environ and "WORLD_SIZE" in os.environ
+    if a.gpus > 1 and not in_torchrun:
+        return spawn_ranks(argv, a.gpus)
+    ov = {}
+    for kv in a.set:
+        k, v = kv.split("=", 1)
+        try:
+            v = json.loads(v)
+        except ValueError:
+            pass
+        ov[k] = v
+    m = run_preset(a.preset, a.epochs, a.out, ov, a.checkpoint_every, a.resume)
+    if m:
+        print(json.dumps({k: v for k, v in m.items() if isinstance(v, (int, float, str))}), flush=True)
+    return 0

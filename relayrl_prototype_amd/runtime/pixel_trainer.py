@@ -182,6 +182,31 @@ class PixelA2CTrainer:
                "Entropy": st[2] / cnt}
         return out
 
+    def state_dict(self) -> dict:
+        st = {"updates": self.updates, "total_steps": self.total_steps, "obs0": self.obs[0].cpu(),
+              "cfg": self.cfg.to_dict()}
+        if self.on_gpu:
+            st["model"] = {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
+            st["env_state"] = self.env.state.cpu()
+            st["env_step"] = self.env.step_count
+        else:
+            st["params"] = self.params.detach().cpu()
+            st["opt"] = self.opt.state_dict()
+        return st
+
+    def load_state_dict(self, st: dict):
+        self.updates = int(st["updates"])
+        self.total_steps = int(st["total_steps"])
+        self.obs[0].copy_(st["obs0"].to(self.device))
+        if self.on_gpu:
+            self.model.load_state_dict({k: v.to(self.device) for k, v in st["model"].items()})
+            self.env.state.copy_(st["env_state"].to(self.device))
+            self.env.step_count = int(st["env_step"])
+        else:
+            with torch.no_grad():
+                self.params.copy_(st["params"])
+            self.opt.load_state_dict(st["opt"])
+
     def reset_episode_stats(self):
         self.ep_sum.zero_()
         if self.on_gpu:

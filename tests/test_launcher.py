@@ -1,0 +1,43 @@
+"""Launcher / CLI: presets for the BASELINE configs, per-rank logging, checkpoint-resume,
+and the multi-rank spawn (torch.distributed.run child, gloo on CPU)."""
+import glob
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from relayrl_prototype_amd.runtime.launcher import PRESETS, run_preset
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_presets_cover_baseline_configs():
+    base = json.load(open(os.path.join(REPO, "BASELINE.json")))["configs"]
+    assert len(PRESETS) == len(base) == 5
+    kinds = {p.kind for p in PRESETS.values()}
+    assert kinds == {"agent_server", "vec", "actor_learner", "pixel", "host"}
+
+
+def test_pixel_preset_cpu_logs_and_resumes(tmp_path, monkeypatch):
+    monkeypatch.setenv("RRL_QUIET_CONFIG", "1")
+    ov = {"num_envs": 2, "rollout_len": 2, "seed": 3}
+    m = run_preset("pong-a2c", 2, str(tmp_path), ov, checkpoint_every=2)
+    assert m["Updates"] == 2 and m["EnvSteps"] == 8
+    prog = glob.glob(str(tmp_path / "**" / "progress.txt"), recursive=True)
+    assert prog and "EnvStepsPerSec" in open(prog[0]).readline()
+    ck = str(tmp_path / "pong-a2c_ckpt")
+    assert os.path.exists(ck) or glob.glob(ck + "*")
+    m2 = run_preset("pong-a2c", 1, str(tmp_path / "r"), ov, resume=ck)
+    assert m2["Updates"] == 3  # resumed counters
+
+
+def test_cli_spawns_ranks_gloo(tmp_path):
+    env = dict(os.environ, PYTHONPATH=REPO, RRL_QUIET_CONFIG="1", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, "-m", "relayrl_prototype_amd", "train", "--preset", "pong-a2c", "--gpus", "2",
+                        "--epochs", "1", "--out", str(tmp_path), "--set", "num_envs=2", "rollout_len=2"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    assert json.loads(line)["EnvSteps"] == 2 * 2 * 2  # whole job over 2 ranks
