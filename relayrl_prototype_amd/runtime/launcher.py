@@ -97,10 +97,17 @@ def _epoch(tr):
     return tr.step()
 
 
+def ckpt_dir(out_dir: str, name: str, rank: int) -> str:
+    return os.path.join(out_dir, f"{name}_ckpt_r{rank}")
+
+
 def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optional[Dict] = None,
                checkpoint_every: int = 0, resume: Optional[str] = None, log_every: int = 1,
-               on_metrics: Optional[Callable[[Dict], None]] = None) -> Dict:
-    """Run one rank of a preset for ``epochs`` epochs; returns the last metrics (rank 0)."""
+               on_metrics: Optional[Callable[[Dict], None]] = None, auto_resume: bool = False) -> Dict:
+    """Run one rank of a preset until ``epochs`` epochs are done; returns the last metrics
+    (rank 0).  Checkpoints are per rank (each rank owns its env streams); with
+    ``auto_resume`` a (re)started rank continues from its own latest checkpoint, which is
+    how a torchrun group restart after a rank failure recovers (--max-restarts)."""
     import torch
 
     from ..parallel.comm import Comm, dist_env, init_distributed
@@ -118,11 +125,16 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
     else:
         dev = torch.device("cpu")
     tr = _make_trainer(preset, comm, dev, overrides)
+    start = 0
+    if auto_resume and resume is None and os.path.exists(os.path.join(ckpt_dir(out_dir, name, comm.rank),
+                                                                      "state.json")):
+        resume = ckpt_dir(out_dir, name, comm.rank)
     if resume:
         from ..utils.checkpoint import load_checkpoint
 
         st = load_checkpoint(resume)
         tr.load_state_dict(st["trainer"])
+        start = int(st.get("epoch", 0)) if auto_resume else 0
     logger = None
     if comm.rank == 0:
         kw = setup_logger_kwargs(f"relayrl-{name}", seed=int(overrides.get("seed", 0)), data_dir=out_dir)
@@ -131,7 +143,9 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
                             "baseline_config": preset.baseline_config})
     t0 = time.perf_counter()
     last: Dict = {}
-    for ep in range(1, epochs + 1):
+    from ..utils.faults import maybe_kill_rank
+
+    for ep in range(start + 1, epochs + 1):
         _epoch(tr)
         if ep % log_every == 0 or ep == epochs:
             m = tr.metrics()
@@ -148,10 +162,11 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
                 last = m
                 if on_metrics:
                     on_metrics(m)
-        if checkpoint_every and ep % checkpoint_every == 0 and comm.rank == 0 and hasattr(tr, "state_dict"):
+        if checkpoint_every and ep % checkpoint_every == 0 and hasattr(tr, "state_dict"):
             from ..utils.checkpoint import save_checkpoint
 
-            save_checkpoint(os.path.join(out_dir, f"{name}_ckpt"), {"trainer": tr.state_dict(), "epoch": ep})
+            save_checkpoint(ckpt_dir(out_dir, name, comm.rank), {"trainer": tr.state_dict(), "epoch": ep})
+        maybe_kill_rank(comm.rank, ep, out_dir)
     if hasattr(tr, "finish"):
         tr.finish()
     return last
@@ -207,10 +222,11 @@ def _run_agent_server(preset: Preset, epochs: int, out_dir: str, overrides: Dict
         srv.close(save=True)
 
 
-def spawn_ranks(argv, gpus: int) -> int:
+def spawn_ranks(argv, gpus: int, max_restarts: int = 0) -> int:
     """Start torch.distributed.run as a child with one rank per GPU; returns its exit code."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m", "relayrl_prototype_amd"] + argv
+           f"--max-restarts={max_restarts}", "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "relayrl_prototype_amd"] + argv
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -230,6 +246,8 @@ def main(argv=None) -> int:
     t.add_argument("--set", nargs="*", default=[], help="overrides key=value (e.g. num_envs=8192)")
     t.add_argument("--checkpoint-every", type=int, default=0)
     t.add_argument("--resume", default=None)
+    t.add_argument("--auto-resume", action="store_true", help="continue from this rank's last checkpoint if any")
+    t.add_argument("--max-restarts", type=int, default=0, help="torchrun group restarts after a rank failure")
     sub.add_parser("presets", help="list the presets")
     b = sub.add_parser("build", help="compile the HIP and C++ extensions in-tree")
     b.add_argument("--force", action="store_true")
@@ -252,7 +270,7 @@ def main(argv=None) -> int:
         return 0
     in_torchrun = "LOCAL_RANK" in os.environ and "WORLD_SIZE" in os.environ
     if a.gpus > 1 and not in_torchrun:
-        return spawn_ranks(argv, a.gpus)
+        return spawn_ranks(argv, a.gpus, a.max_restarts)
     ov = {}
     for kv in a.set:
         k, v = kv.split("=", 1)
@@ -261,7 +279,7 @@ def main(argv=None) -> int:
         except ValueError:
             pass
         ov[k] = v
-    m = run_preset(a.preset, a.epochs, a.out, ov, a.checkpoint_every, a.resume)
+    m = run_preset(a.preset, a.epochs, a.out, ov, a.checkpoint_every, a.resume, auto_resume=a.auto_resume)
     if m:
         print(json.dumps({k: v for k, v in m.items() if isinstance(v, (int, float, str))}), flush=True)
     return 0

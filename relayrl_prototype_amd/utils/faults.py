@@ -11,6 +11,12 @@ Configured by the ``RRL_FAULTS`` environment variable (or ``FaultInjector.config
 * ``delay_ms`` -- fixed delay added before each upload (slow agent).
 
 Off by default; every hook is a no-op unless configured.
+
+Process-level faults for the elastic-restart path (runtime/launcher.py):
+
+    RRL_FAULT_KILL="1:3"   -- rank 1 dies (exit 17) after epoch 3, once per run directory;
+                              torchrun (--max-restarts) restarts the group and every rank
+                              resumes from its last checkpoint.
 """
 from __future__ import annotations
 
@@ -74,3 +80,20 @@ def reset(spec: str = "") -> FaultInjector:
     global _GLOBAL
     _GLOBAL = FaultInjector(spec)
     return _GLOBAL
+
+
+def maybe_kill_rank(rank: int, epoch: int, run_dir: str) -> None:
+    """Crash this process once if RRL_FAULT_KILL names (rank, epoch)."""
+    spec = os.environ.get("RRL_FAULT_KILL", "")
+    if not spec:
+        return
+    r, e = (int(x) for x in spec.split(":"))
+    if r != rank or e != epoch:
+        return
+    marker = os.path.join(run_dir, f".fault_fired_r{rank}_e{epoch}")
+    if os.path.exists(marker):
+        return
+    os.makedirs(run_dir, exist_ok=True)
+    open(marker, "w").close()
+    print(f"[faults] injected crash of rank {rank} after epoch {epoch}", flush=True)
+    os._exit(17)

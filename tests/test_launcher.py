@@ -27,8 +27,8 @@ def test_pixel_preset_cpu_logs_and_resumes(tmp_path, monkeypatch):
     assert m["Updates"] == 2 and m["EnvSteps"] == 8
     prog = glob.glob(str(tmp_path / "**" / "progress.txt"), recursive=True)
     assert prog and "EnvStepsPerSec" in open(prog[0]).readline()
-    ck = str(tmp_path / "pong-a2c_ckpt")
-    assert os.path.exists(ck) or glob.glob(ck + "*")
+    ck = str(tmp_path / "pong-a2c_ckpt_r0")
+    assert os.path.exists(os.path.join(ck, "state.json"))
     m2 = run_preset("pong-a2c", 1, str(tmp_path / "r"), ov, resume=ck)
     assert m2["Updates"] == 3  # resumed counters
 
@@ -41,3 +41,18 @@ def test_cli_spawns_ranks_gloo(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     assert json.loads(line)["EnvSteps"] == 2 * 2 * 2  # whole job over 2 ranks
+
+
+def test_rank_failure_group_restart_resumes(tmp_path):
+    """Rank 1 crashes after epoch 2; torchrun restarts the group, every rank resumes from
+    its own checkpoint and the run completes all epochs (SURVEY §5.3 elastic recovery)."""
+    env = dict(os.environ, PYTHONPATH=REPO, RRL_QUIET_CONFIG="1", OMP_NUM_THREADS="1", RRL_FAULT_KILL="1:2")
+    r = subprocess.run([sys.executable, "-m", "relayrl_prototype_amd", "train", "--preset", "pong-a2c", "--gpus", "2",
+                        "--epochs", "4", "--out", str(tmp_path), "--checkpoint-every", "1", "--auto-resume",
+                        "--max-restarts", "1", "--set", "num_envs=2", "rollout_len=2"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert os.path.exists(tmp_path / ".fault_fired_r1_e2")
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    m = json.loads(line)
+    assert m["Updates"] == 4 and m["EnvSteps"] == 4 * 2 * 2 * 2
