@@ -4,6 +4,14 @@
 #include <cmath>
 #include <stdexcept>
 
+// target_clones dispatches through IFUNC resolvers, which run during relocation --
+// before the ThreadSanitizer runtime is up -- so TSan builds use the default clone.
+#if defined(__SANITIZE_THREAD__)
+#define RRL_TARGET_CLONES
+#else
+#define RRL_TARGET_CLONES __attribute__((target_clones("avx512f", "avx2", "default")))
+#endif
+
 namespace rrl {
 
 namespace {
@@ -17,7 +25,7 @@ uint64_t splitmix(uint64_t& s) {
 
 // y[O] = act(b + x[I] @ Wt[I][O]).  The inner loop runs over contiguous outputs so the
 // compiler vectorises it; target_clones picks AVX-512 / AVX2 at load time.
-__attribute__((target_clones("avx512f", "avx2", "default"))) void dense(const float* __restrict x, int I,
+RRL_TARGET_CLONES void dense(const float* __restrict x, int I,
                                                                          const float* __restrict wt,
                                                                          const float* __restrict b, int O,
                                                                          float* __restrict y, bool relu) {

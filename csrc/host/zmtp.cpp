@@ -364,6 +364,19 @@ void Socket::drop(const std::shared_ptr<Conn>& c) {
   }
 }
 
+// Timed condition waits go through system_clock: libstdc++ implements steady_clock waits
+// with pthread_cond_clockwait, which the GCC 11 ThreadSanitizer runtime does not
+// intercept (it would report every timed wait as a double lock).  A wall-clock jump can
+// only lengthen or shorten one bounded wait.
+template <class Pred>
+static bool timed_wait(std::condition_variable& cv, std::unique_lock<std::mutex>& g,
+                       std::chrono::steady_clock::time_point deadline, Pred pred) {
+  const auto left = deadline - std::chrono::steady_clock::now();
+  return cv.wait_until(g, std::chrono::system_clock::now() +
+                              std::chrono::duration_cast<std::chrono::system_clock::duration>(left),
+                       pred);
+}
+
 bool Socket::send(const std::vector<std::string>& frames, int timeout_ms) {
   if (frames.empty()) return false;
   if (type_ == SockType::PULL) throw std::runtime_error("PULL sockets cannot send");
@@ -383,7 +396,7 @@ bool Socket::send(const std::vector<std::string>& frames, int timeout_ms) {
       } else {
         auto pred = [&] { return !conns_.empty() || closed_.load(); };
         if (timeout_ms < 0) conn_cv_.wait(g, pred);
-        else if (!conn_cv_.wait_until(g, deadline, pred)) return false;
+        else if (!timed_wait(conn_cv_, g, deadline, pred)) return false;
         continue;
       }
     }
@@ -398,7 +411,8 @@ bool Socket::recv(Message& out, int timeout_ms) {
   std::unique_lock<std::mutex> g(qmu_);
   auto pred = [&] { return !inbox_.empty() || closed_.load(); };
   if (timeout_ms < 0) qcv_.wait(g, pred);
-  else if (!qcv_.wait_for(g, std::chrono::milliseconds(timeout_ms), pred)) return false;
+  else if (!timed_wait(qcv_, g, std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms), pred))
+    return false;
   if (inbox_.empty()) return false;
   out = std::move(inbox_.front());
   inbox_.pop_front();

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Sanitizer builds of the C++ host runtime (SURVEY §5.2 -- the reference has none).
+#   tools/sanitize_host.sh           # ASan+UBSan and TSan builds, then run both
+# Host code only: GPU sanitizers (xnack+) are not available on the MI355X pool.
+set -euo pipefail
+ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+OUT="${ROOT}/build/sanitize"
+mkdir -p "$OUT"
+SRCS="$ROOT/csrc/host/selftest/host_selftest.cpp $ROOT/csrc/host/codec.cpp $ROOT/csrc/host/zmtp.cpp $ROOT/csrc/host/vecenv.cpp $ROOT/csrc/host/policy.cpp"
+CXX="${CXX:-g++}"
+$CXX -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined \
+  -pthread -I "$ROOT/csrc/host" $SRCS -o "$OUT/host_selftest_asan"
+$CXX -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=thread -pthread -I "$ROOT/csrc/host" $SRCS \
+  -o "$OUT/host_selftest_tsan"
+echo "== ASan + UBSan"
+ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 "$OUT/host_selftest_asan"
+echo "== TSan"
+TSAN_OPTIONS=halt_on_error=1:second_deadlock_stack=1 "$OUT/host_selftest_tsan"
