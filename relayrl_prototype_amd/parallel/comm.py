@@ -41,8 +41,17 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
         os.environ.setdefault("MASTER_PORT", "29500")
         if backend == "nccl":
             torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend, rank=rank, world_size=world,
-                                timeout=datetime.timedelta(seconds=timeout_s))
+        tmo = datetime.timedelta(seconds=timeout_s)
+        restart = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+        if restart > 0:
+            # after a torchrun group restart the rendezvous store still holds the dead
+            # group's keys (peer addresses); namespace this attempt's keys
+            base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world, False,
+                                 timeout=tmo)
+            store = dist.PrefixStore(f"rrl_attempt_{restart}", base)
+            dist.init_process_group(backend=backend, store=store, rank=rank, world_size=world, timeout=tmo)
+        else:
+            dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=tmo)
     return Comm()
 
 
