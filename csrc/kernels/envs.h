@@ -22,7 +22,7 @@ struct CartPoleEnv {
     return f == 0 ? s[0] : f == 1 ? s[1] : f == 2 ? s[2] : s[3];
   }
   // Euler integration exactly as gymnasium CartPoleEnv.step (kinematics_integrator="euler").
-  RRL_DEV static float step(float (&s)[NS], int a, bool& terminated) {
+  RRL_DEV static float step(float (&s)[NS], int a, bool& terminated, float /*noise01*/) {
     const float gravity = 9.8f, masspole = 0.1f, total_mass = 1.1f, length = 0.5f;
     const float polemass_length = masspole * length, force_mag = 10.f, tau = 0.02f;
     const float force = a == 1 ? force_mag : -force_mag;
@@ -49,7 +49,7 @@ struct MountainCarEnv {
     s[1] = 0.f;
   }
   RRL_DEV static float obs(const float (&s)[NS], int f) { return f == 0 ? s[0] : s[1]; }
-  RRL_DEV static float step(float (&s)[NS], int a, bool& terminated) {
+  RRL_DEV static float step(float (&s)[NS], int a, bool& terminated, float /*noise01*/) {
     float pos = s[0], vel = s[1];
     vel += (float)(a - 1) * 0.001f + cosf(3.f * pos) * (-0.0025f);
     vel = fminf(fmaxf(vel, -0.07f), 0.07f);
@@ -104,7 +104,7 @@ struct AcrobotEnv {
     while (x < -pi) x += 2.f * pi;
     return x;
   }
-  RRL_DEV static float step(float (&s)[NS], int a, bool& terminated) {
+  RRL_DEV static float step(float (&s)[NS], int a, bool& terminated, float /*noise01*/) {
     const float torque = (float)(a - 1);
     const float dt = 0.2f;
     float y0[5] = {s[0], s[1], s[2], s[3], torque}, k1[4], k2[4], k3[4], k4[4], y[5];
@@ -124,6 +124,68 @@ struct AcrobotEnv {
     s[3] = fminf(fmaxf(ns[3], -9.f * pi), 9.f * pi);
     terminated = (-cosf(s[0]) - cosf(s[1] + s[0])) > 1.f;
     return terminated ? 0.f : -1.f;
+  }
+};
+
+// LunarLanderSynth-v0: the same point-mass lander as the host VecEnv (csrc/host/vecenv.cpp
+// LunarLanderSynth) -- 8 obs (x, y, vx, vy, angle, angular velocity, leg1, leg2), 4 actions
+// (noop, left, main, right), gymnasium-style potential shaping and +-100 terminal bonus.
+// The lateral noise draw comes from the kernel's Philox stream instead of the host Rng.
+struct LunarLanderSynthEnv {
+  static constexpr int D = 8, A = 4, NS = 7;  // x y vx vy ang angv prev_shaping
+  static constexpr int kMaxSteps = 1000;
+  RRL_DEV static float shaping(const float (&s)[NS]) {
+    const float legs = s[1] < 0.05f ? 20.f : 0.f;
+    return -100.f * sqrtf(s[0] * s[0] + s[1] * s[1]) - 100.f * sqrtf(s[2] * s[2] + s[3] * s[3]) -
+           100.f * fabsf(s[4]) + legs;
+  }
+  RRL_DEV static void reset(float (&s)[NS], uint4 r) {
+    s[0] = -0.3f + 0.6f * u01(r.x);
+    s[1] = 1.4f;
+    s[2] = -0.5f + 1.0f * u01(r.y);
+    s[3] = -0.3f + 0.3f * u01(r.z);
+    s[4] = -0.1f + 0.2f * u01(r.w);
+    s[5] = 0.f;
+    s[6] = shaping(s);
+  }
+  RRL_DEV static float obs(const float (&s)[NS], int f) {
+    if (f < 6) return f == 0 ? s[0] : f == 1 ? s[1] : f == 2 ? s[2] : f == 3 ? s[3] : f == 4 ? s[4] : s[5];
+    return s[1] < 0.05f ? 1.f : 0.f;
+  }
+  RRL_DEV static float step(float (&s)[NS], int a, bool& terminated, float noise01) {
+    const float dt = 1.f / 50.f;
+    float ax = 0.f, ay = -10.f / 6.f, aa = 0.f, fuel = 0.f;
+    if (a == 2) {
+      ax += -sinf(s[4]) * 13.f / 6.f;
+      ay += cosf(s[4]) * 13.f / 6.f;
+      fuel += 0.3f;
+    } else if (a == 1 || a == 3) {
+      const float dir = a == 1 ? -1.f : 1.f;
+      ax += dir * cosf(s[4]) * 0.6f / 6.f;
+      aa += -dir * 1.5f;
+      fuel += 0.03f;
+    }
+    ax += -0.05f + 0.1f * noise01;
+    s[2] += ax * dt * 6.f;
+    s[3] += ay * dt * 6.f;
+    s[5] += aa * dt;
+    s[0] += s[2] * dt;
+    s[1] += s[3] * dt;
+    s[4] += s[5] * dt;
+    const float sh = shaping(s);
+    float rew = sh - s[6] - fuel;
+    s[6] = sh;
+    terminated = false;
+    if (s[1] <= 0.f) {
+      s[1] = 0.f;
+      terminated = true;
+      const bool soft = fabsf(s[3]) < 0.5f && fabsf(s[2]) < 0.5f && fabsf(s[4]) < 0.3f && fabsf(s[0]) < 0.5f;
+      rew += soft ? 100.f : -100.f;
+    } else if (fabsf(s[0]) >= 1.f) {
+      terminated = true;
+      rew -= 100.f;
+    }
+    return rew;
   }
 };
 

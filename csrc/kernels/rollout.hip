@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256, 2) void rollout_kernel(RolloutArgs p) {
       const float logp = pick_logit(A, logits, a) - cs.lse;
 
       bool term;
-      const float r = Env::step(s, a, term);
+      const float r = Env::step(s, a, term, u01(rnd.y));
       len += 1;
       ret += r;
       const bool trunc = len >= p.max_steps;
@@ -176,13 +176,19 @@ __global__ __launch_bounds__(256, 2) void rollout_kernel(RolloutArgs p) {
 
 using namespace rrl;
 
-enum EnvId : int { ENV_CARTPOLE = 0, ENV_MOUNTAINCAR = 1, ENV_ACROBOT = 2 };
+enum EnvId : int { ENV_CARTPOLE = 0, ENV_MOUNTAINCAR = 1, ENV_ACROBOT = 2, ENV_LUNARLANDER = 3 };
 
 extern "C" int rrl_env_dims(int env, int* D, int* A, int* NS, int* max_steps) {
   switch (env) {
     case ENV_CARTPOLE: *D = CartPoleEnv::D; *A = CartPoleEnv::A; *NS = CartPoleEnv::NS; *max_steps = CartPoleEnv::kMaxSteps; return 0;
     case ENV_MOUNTAINCAR: *D = MountainCarEnv::D; *A = MountainCarEnv::A; *NS = MountainCarEnv::NS; *max_steps = MountainCarEnv::kMaxSteps; return 0;
     case ENV_ACROBOT: *D = AcrobotEnv::D; *A = AcrobotEnv::A; *NS = AcrobotEnv::NS; *max_steps = AcrobotEnv::kMaxSteps; return 0;
+    case ENV_LUNARLANDER:
+      *D = LunarLanderSynthEnv::D;
+      *A = LunarLanderSynthEnv::A;
+      *NS = LunarLanderSynthEnv::NS;
+      *max_steps = LunarLanderSynthEnv::kMaxSteps;
+      return 0;
   }
   return -1;
 }
@@ -223,12 +229,14 @@ extern "C" int rrl_rollout(int env, const float* params, int N, int T, int H, fl
       case ENV_CARTPOLE: return launch_rollout<CartPoleEnv, 8>(a, grid, s);
       case ENV_MOUNTAINCAR: return launch_rollout<MountainCarEnv, 8>(a, grid, s);
       case ENV_ACROBOT: return launch_rollout<AcrobotEnv, 8>(a, grid, s);
+      case ENV_LUNARLANDER: return launch_rollout<LunarLanderSynthEnv, 8>(a, grid, s);
     }
   } else if (H == 64) {
     switch (env) {
       case ENV_CARTPOLE: return launch_rollout<CartPoleEnv, 4>(a, grid, s);
       case ENV_MOUNTAINCAR: return launch_rollout<MountainCarEnv, 4>(a, grid, s);
       case ENV_ACROBOT: return launch_rollout<AcrobotEnv, 4>(a, grid, s);
+      case ENV_LUNARLANDER: return launch_rollout<LunarLanderSynthEnv, 4>(a, grid, s);
     }
   }
   return -3;

@@ -29,7 +29,7 @@ from ..parallel.comm import Comm
 from ..utils.tracing import PhaseTimer
 from .rollout_learn import RolloutLearner, episode_metrics
 
-DEVICE_ENVS = {"CartPole-v1": 0, "MountainCar-v0": 1, "Acrobot-v1": 2}
+DEVICE_ENVS = {"CartPole-v1": 0, "MountainCar-v0": 1, "Acrobot-v1": 2, "LunarLanderSynth-v0": 3}
 
 
 @dataclass

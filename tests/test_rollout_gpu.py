@@ -90,3 +90,62 @@ def test_rollout_other_envs(cuda):
         torch.cuda.synchronize()
         assert torch.isfinite(obs).all()
         assert int(act.max().item()) < A and int(act.min().item()) >= 0
+
+
+def _lander_step_np(o, a, noise01):
+    """numpy float32 oracle of LunarLanderSynthEnv.step (csrc/kernels/envs.h) from the obs."""
+    f = np.float32
+    x, y, vx, vy, ang, angv = (o[:, i].astype(f) for i in range(6))
+
+    def shaping(x, y, vx, vy, ang):
+        return (-100 * np.sqrt(x * x + y * y) - 100 * np.sqrt(vx * vx + vy * vy) - 100 * np.abs(ang)
+                + np.where(y < 0.05, f(20), f(0))).astype(f)
+
+    prev = shaping(x, y, vx, vy, ang)
+    dt = f(1 / 50)
+    main = a == 2
+    side = (a == 1) | (a == 3)
+    d = np.where(a == 1, f(-1), f(1))
+    ax = np.where(main, -np.sin(ang) * f(13 / 6), np.where(side, d * np.cos(ang) * f(0.6 / 6), f(0)))
+    ay = f(-10 / 6) + np.where(main, np.cos(ang) * f(13 / 6), f(0))
+    aa = np.where(side, -d * f(1.5), f(0))
+    fuel = np.where(main, f(0.3), np.where(side, f(0.03), f(0)))
+    ax = ax + f(-0.05) + f(0.1) * noise01
+    vx = vx + ax * dt * f(6)
+    vy = vy + ay * dt * f(6)
+    angv = angv + aa * dt
+    x = x + vx * dt
+    y = y + vy * dt
+    ang = ang + angv * dt
+    sh = shaping(x, y, vx, vy, ang)
+    rew = sh - prev - fuel
+    return np.stack([x, y, vx, vy, ang, angv], 1), rew
+
+
+def test_lunarlander_device_rollout_matches_oracle(cuda):
+    h = hip()
+    env = 3
+    D, A, NS, ms = h.env_dims(env)
+    assert (D, A, ms) == (8, 4, 1000)
+    N, T, H, seed = 256, 40, 128, 5
+    params = MLPSpec(D, H, A).init(torch.Generator().manual_seed(3)).to(cuda)
+    state = torch.zeros(N, NS, device=cuda)
+    ep_len = torch.zeros(N, dtype=torch.int32, device=cuda)
+    ep_ret = torch.zeros(N, device=cuda)
+    obs = torch.zeros(T + 1, N, D, device=cuda)
+    act = torch.zeros(T, N, dtype=torch.int32, device=cuda)
+    logp, rew, done = (torch.zeros(T, N, device=cuda) for _ in range(3))
+    stats = torch.zeros(h.rollout_grid(N), 8, device=cuda)
+    h.rollout(env, params, H, state, ep_len, ep_ret, obs, act, logp, rew, done, stats, seed, 0, True, ms)
+    torch.cuda.synchronize()
+    o, a, r, d = obs.cpu().numpy(), act.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
+    checked = 0
+    for t in range(T):
+        u = philox.uniforms(seed, t, np.arange(N), 0)
+        ns, rr = _lander_step_np(o[t], a[t], u[1])
+        live = d[t] == 0
+        np.testing.assert_allclose(o[t + 1][live, :6], ns[live], rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(r[t][live], rr[live], rtol=1e-3, atol=1e-3)
+        checked += live.sum()
+    assert checked > N * T // 2
+    assert np.isin(np.unique(a), np.arange(4)).all()
