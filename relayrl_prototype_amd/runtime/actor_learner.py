@@ -129,8 +129,9 @@ class ActorLearner:
     def __init__(self, cfg: ActorLearnerConfig, comm: Optional[Comm] = None, device=None):
         self.cfg = cfg
         self.comm = comm or Comm()
-        if self.comm.world < 2:
-            raise ValueError("actor-learner mode needs world_size >= 2 (rank 0 learns, others act)")
+        if self.comm.world < 2 and not cfg.learner_acts:
+            raise ValueError("actor-learner mode needs world_size >= 2 (rank 0 learns, others act) "
+                             "unless the learner also acts (learner_acts=True)")
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
@@ -200,6 +201,8 @@ class ActorLearner:
                 w.wait()
 
     def _bcast_weights(self, async_op: bool):
+        if self.comm.world == 1:  # colocated single-GPU actor+learner: weights are shared
+            return None
         return dist.broadcast(self.wbuf, src=0, async_op=async_op)
 
     # ------------------------------------------------------------------ one step
@@ -216,7 +219,7 @@ class ActorLearner:
         if cfg.max_lag >= 1:
             if self._pending is not None:
                 self._pending.wait()
-            self._pending = self._bcast_weights(async_op=True)
+            self._pending = self._bcast_weights(async_op=True)  # None on a single rank
         else:
             self._bcast_weights(async_op=False)
         self.version += 1

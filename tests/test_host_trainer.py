@@ -39,3 +39,17 @@ def test_cartpole_reinforce_learns_cpu():
         if best > 100:
             break
     assert best > 100, best
+
+
+def test_actor_learner_single_rank_colocated():
+    """One rank that both acts and learns (the 1-GPU form of BASELINE config 3)."""
+    from relayrl_prototype_amd.runtime.actor_learner import ActorLearner, ActorLearnerConfig
+
+    al = ActorLearner(ActorLearnerConfig(env="LunarLanderSynth-v0", num_envs=8, rollout_len=16, learner_acts=True,
+                                         hidden=64, train_vf_iters=2, num_threads=1), device="cpu")
+    p0 = al.learner.pi.params.clone()
+    for _ in range(2):
+        al.step()
+    al.finish()
+    m = al.metrics()
+    assert m["EnvSteps"] == 2 * 16 * 8 and not torch.equal(p0, al.learner.pi.params)
