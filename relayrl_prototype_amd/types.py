@@ -341,13 +341,20 @@ class TrajectoryColumns:
     def __len__(self):
         return int(self.rew.shape[0])
 
+    @staticmethod
+    def _rows(a, n):
+        a = np.asarray(a)
+        if n:
+            return a.reshape(n, -1)
+        return a.reshape(0, a.shape[-1] if a.ndim > 1 else 0)
+
     def encode(self) -> bytes:
         n = len(self)
-        obs = np.ascontiguousarray(self.obs, np.float32).reshape(n, -1)
-        act = self.act.reshape(n, -1)
+        obs = self._rows(np.ascontiguousarray(self.obs, np.float32), n)
+        act = self._rows(self.act, n)
         kind = 1 if np.issubdtype(act.dtype, np.integer) else 0
         act = np.ascontiguousarray(act, _ACT_KINDS[kind])
-        A = 0 if self.mask is None else self.mask.reshape(n, -1).shape[1]
+        A = 0 if self.mask is None else self._rows(self.mask, n).shape[1]
         aid = self.agent_id.encode()
         hdr = struct.pack(_RRLC_HDR, _RRLC_MAGIC, 1, n, obs.shape[1], act.shape[1], A, kind,
                           self.mask is not None, self.logp is not None, 0, int(self.seq))
