@@ -70,7 +70,9 @@ def main(argv=None):
     if world_env > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     comm = init_distributed()
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from relayrl_prototype_amd.parallel.comm import local_device_index
+
+    local = local_device_index()
     torch.cuda.set_device(local)
     from relayrl_prototype_amd.runtime.vec_trainer import VecTrainer, VecTrainerConfig
 
@@ -123,6 +125,15 @@ def main(argv=None):
             },
             "final_avg_ep_ret": None if m["AverageEpRet"] != m["AverageEpRet"] else round(m["AverageEpRet"], 2),
         }
+        ref_eq = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1_reference_equivalent_cpu.json")
+        if os.path.exists(ref_eq):  # measured here, labelled: the reference itself publishes no numbers
+            try:
+                r = json.load(open(ref_eq))
+                rec["reference_equivalent_cpu"] = {"env_steps_per_s": round(r["value"], 1),
+                                                   "time_to_threshold_s": r.get("time_to_threshold_s"),
+                                                   "source": "benchmarks/reference_equivalent_cpu.py"}
+            except (ValueError, KeyError):
+                pass
         if args.ttt:
             rec["time_to_threshold_s"] = None if ttt[0] is None else round(ttt[0], 3)
             rec["time_to_threshold_epochs"] = ttt[1]

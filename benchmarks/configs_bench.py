@@ -28,9 +28,11 @@ def main():
     from relayrl_prototype_amd.parallel.comm import Comm, dist_env, init_distributed
     from relayrl_prototype_amd.runtime.launcher import PRESETS, _epoch, _make_trainer
 
-    _, local, world = dist_env()
+    from relayrl_prototype_amd.parallel.comm import local_device_index
+
+    _, _, world = dist_env()
     comm = init_distributed() if world > 1 else Comm()
-    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    dev = torch.device("cuda", local_device_index()) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     ov = {}

@@ -29,7 +29,9 @@ def main():
     from relayrl_prototype_amd.runtime.pixel_trainer import PixelA2CConfig, PixelA2CTrainer
 
     comm = init_distributed() if int(os.environ.get("WORLD_SIZE", "1")) > 1 else Comm()
-    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    from relayrl_prototype_amd.parallel.comm import local_device_index
+
+    dev = torch.device("cuda", local_device_index())
     torch.cuda.set_device(dev)
     cfg = PixelA2CConfig(num_envs=a.num_envs, rollout_len=a.rollout_len, phase_timing=a.phase_timing)
     tr = PixelA2CTrainer(cfg, comm, device=dev)

@@ -31,10 +31,21 @@ def dist_env() -> tuple:
     return rank, local, world
 
 
+def local_device_index() -> int:
+    """GPU of this rank: LOCAL_RANK, unless RRL_FORCE_DEVICE pins every rank to one GPU
+    (rehearsing the multi-rank path on a one-GPU box, together with RRL_DIST_BACKEND=gloo)."""
+    forced = os.environ.get("RRL_FORCE_DEVICE")
+    return int(forced) if forced not in (None, "") else dist_env()[1]
+
+
 def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) -> "Comm":
-    """Initialise the default process group from the environment (torchrun) if world > 1."""
+    """Initialise the default process group from the environment (torchrun) if world > 1.
+    Backend: ``nccl`` (= RCCL over xGMI on ROCm) with GPUs, ``gloo`` on CPU; override with
+    RRL_DIST_BACKEND."""
     rank, local, world = dist_env()
+    local = local_device_index()
     if world > 1 and not dist.is_initialized():
+        backend = backend or os.environ.get("RRL_DIST_BACKEND") or None
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -117,10 +117,12 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
     overrides = dict(overrides or {})
     if preset.kind == "agent_server":
         return _run_agent_server(preset, epochs, out_dir, overrides)
-    _, local_rank, world = dist_env()
+    from ..parallel.comm import local_device_index
+
+    _, _, world = dist_env()
     comm = init_distributed() if world > 1 else Comm()
     if torch.cuda.is_available():
-        dev = torch.device("cuda", local_rank)
+        dev = torch.device("cuda", local_device_index())
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
