@@ -125,7 +125,7 @@ RRL_DEV void stage_x_tiles(float* __restrict__ St, int wave, const floatx4 (&v)[
 // the VALU in registers (dout x h2 outer products, reduced once at the end) instead of
 // a 16-row MFMA tile that would be 1/16 (value) or 1/8 (CartPole policy) useful; this
 // also removes one staging phase and two workgroup barriers per 64-row slab.
-template <int DT, int HT, int HEAD, int A3>
+template <int DT, int HT, int HEAD, int A3, int EARLY>
 __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   using L = LdsNet<DT, HT>;
@@ -349,11 +349,15 @@ __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
     __syncthreads();
     stage_tiles<HT>(st0, wave, h1);
     stage_tiles<HT>(st1, wave, dh2);
+    floatx4 dh1[HT];
+    if (EARLY) {
+      // dh1 needs only registers + W2: issuing its 256 MFMAs before the barrier hides the
+      // staging-write latency and the wave skew at the barrier
+      dense_bwd_data<HT, HT, true>(lds + L::W2, L::S2, dh2, h1, dh1);
+    }
     __syncthreads();
     wgrad<TO, HT>(st1, st0, wave * TO, 0, acc2, bacc2);
-
-    floatx4 dh1[HT];
-    dense_bwd_data<HT, HT, true>(lds + L::W2, L::S2, dh2, h1, dh1);
+    if (!EARLY) dense_bwd_data<HT, HT, true>(lds + L::W2, L::S2, dh2, h1, dh1);
 
     // ------------------------------------------------------------ phase C: dW1, db1
     __syncthreads();
@@ -459,8 +463,8 @@ __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
 
 using namespace rrl;
 
-template <int DT, int HT, int HEAD, int A3>
-static int launch_grad(const GradArgs& a, int grid, hipStream_t s) {
+template <int DT, int HT, int HEAD, int A3, int EARLY>
+static int launch_grad_v(const GradArgs& a, int grid, hipStream_t s) {
   using L = LdsNet<DT, HT>;
   const int A = (HEAD == HEAD_VALUE_MSE) ? 1 : a.A;
   const size_t floats = (size_t)((L::floats(A) + 3) & ~3) + 2 * (size_t)L::H * kStageLd;
@@ -468,11 +472,17 @@ static int launch_grad(const GradArgs& a, int grid, hipStream_t s) {
   if (bytes > 163840) return -4;
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)mlp_grad_kernel<DT, HT, HEAD, A3>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    (void)hipFuncSetAttribute((const void*)mlp_grad_kernel<DT, HT, HEAD, A3, EARLY>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
     attr_set = true;
   }
-  hipLaunchKernelGGL((mlp_grad_kernel<DT, HT, HEAD, A3>), dim3(grid), dim3(256), bytes, s, a);
+  hipLaunchKernelGGL((mlp_grad_kernel<DT, HT, HEAD, A3, EARLY>), dim3(grid), dim3(256), bytes, s, a);
   return (int)hipGetLastError();
+}
+
+template <int DT, int HT, int HEAD, int A3>
+static int launch_grad(const GradArgs& a, int grid, hipStream_t s) {
+  return launch_grad_v<DT, HT, HEAD, A3, 1>(a, grid, s);
 }
 
 template <int DT, int HT, int HEAD>
