@@ -280,9 +280,16 @@ class DeviceNatureCNN:
 
     # ------------------------------------------------------------------ backward
     def backward(self, obs_u8: torch.Tensor, act: torch.Tensor, adv: torch.Tensor, ret: torch.Tensor,
-                 vf_coef: float, ent_coef: float) -> torch.Tensor:
+                 vf_coef: float, ent_coef: float, comm=None) -> torch.Tensor:
         """A2C gradients into ``self.grad`` from the activations stored by ``forward`` for
-        rows 0..B-1.  Returns the per-block loss stats [grid, 4] (pg, vf, ent, count)."""
+        rows 0..B-1.  Returns the per-block loss stats [grid, 4] (pg, vf, ent, count).
+
+        With ``comm`` (world > 1) the data-parallel all-reduce is bucketed and overlapped
+        with the backward: the fc + head bucket (96 % of the 1.7 M gradient floats) is
+        all-reduced asynchronously on RCCL's stream as soon as it is final, while the conv
+        gradients are still being computed; the conv bucket follows at the end."""
+        self._reduced = False
+        pending = None
         h, o, sh, g = self.h, self.o, self.shadow, self.grad
         B = obs_u8.shape[0]
         L1, L2, L3 = CONVS
@@ -305,6 +312,10 @@ class DeviceNatureCNN:
         self._bias(dh, B, HIDDEN, o["bfc"])
         da3 = self.da3[:B * FC_IN]
         h.gemm_dgrad(dh, sh[o["wfc"]:o["bfc"]], a3, da3, B, HIDDEN, FC_IN)
+        if comm is not None and comm.world > 1:
+            import torch.distributed as dist
+
+            pending = dist.all_reduce(g[o["wfc"]:o["P"]], group=comm.group, async_op=True)
         # conv3
         self._wgrad("c3", da3, a2, B, L3.hin, L3.cin, L3.k, L3.s, L3.cout, o["w3"])
         self._bias(da3, B * L3.hout ** 2, L3.cout, o["b3"])
@@ -318,6 +329,11 @@ class DeviceNatureCNN:
         # conv1 (input = frames, no data gradient)
         self._wgrad("c1", da1, obs_u8.contiguous(), B, S2D.hin, S2D.cin, S2D.k, S2D.s, S2D.cout, o["w1"])
         self._bias(da1, B * L1.hout ** 2, L1.cout, o["b1"])
+        if pending is not None:
+            comm.all_reduce_sum_(g[:o["wfc"]])
+            pending.wait()
+            g.mul_(1.0 / comm.world)
+            self._reduced = True
         return stats.view(grid, 4)
 
     def _dgrad(self, dy, w, xact, dx, B, L):
@@ -345,9 +361,10 @@ class DeviceNatureCNN:
     # ------------------------------------------------------------------ optimizer
     def apply(self, lr: float, max_grad_norm: float = 0.5, comm=None, betas=(0.9, 0.999), eps: float = 1e-5):
         """(DP all-reduce) -> global-norm clip -> Adam -> bf16 shadow, all on device."""
-        if comm is not None and comm.world > 1:
+        if comm is not None and comm.world > 1 and not getattr(self, "_reduced", False):
             comm.all_reduce_sum_(self.grad)
             self.grad.mul_(1.0 / comm.world)
+        self._reduced = False
         self.h.sumsq(self.grad, self.sq_work, self.norm_sq)
         self.step_count += 1
         self.h.adam_clip(self.params, self.m, self.v, self.grad, self.shadow,

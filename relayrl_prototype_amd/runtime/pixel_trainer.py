@@ -10,7 +10,8 @@ One update on each rank (one process per GPU), everything device resident:
   2. bootstrap value of obs[T], n-step returns via the GAE scan with lambda = 1
   3. fused A2C head backward -> fc / conv weight gradients (transposed-LDS MFMA GEMMs,
      split-K partials), data gradients + col2im with the ReLU mask fused
-  4. DP: one RCCL all-reduce of the flat fp32 gradient (world > 1)
+  4. DP: RCCL all-reduce of the flat fp32 gradient in two buckets, the fc+head bucket
+     overlapped with the conv backward (world > 1)
   5. global-norm clip + Adam + bf16 shadow weights in one kernel
 
 The CPU path (tests, no GPU) runs the same algorithm through the PyTorch oracle model
@@ -108,7 +109,7 @@ class PixelA2CTrainer:
             adv, ret, _ = gae_scan_tm(self.rew, self.done, self.val, cfg.gamma, 1.0)
         with self.timer.phase("Backward"):
             stats = m.backward(self.obs[:T].reshape(B, 21, 21, 64), self.act.reshape(B), adv.reshape(B),
-                               ret.reshape(B), cfg.vf_coef, cfg.ent_coef)
+                               ret.reshape(B), cfg.vf_coef, cfg.ent_coef, comm=self.comm)
         with self.timer.phase("Optimize"):
             m.apply(cfg.lr, cfg.max_grad_norm, self.comm)
         return stats

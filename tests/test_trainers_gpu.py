@@ -90,3 +90,65 @@ def test_trajectory_reinforce_on_gpu(cuda, tmp_path, monkeypatch):
         up = alg.receive_trajectory(t)
     assert up and alg.learner.pi.params.is_cuda
     assert math.isfinite(alg.last_metrics["LossPi"]) and math.isfinite(alg.last_metrics["LossV"])
+
+
+def test_agent_server_zmq_with_gpu_learner(cuda, tmp_path, monkeypatch):
+    """Notebook flow with the learner on the MI355X: columnar uploads over ZMTP feed the
+    HIP learner; the new weights reach the agent's C++ policy."""
+    import json
+    import socket
+    import time
+
+    from relayrl_prototype_amd import _native
+    from relayrl_prototype_amd.api.agent import RelayRLAgent
+    from relayrl_prototype_amd.api.server import TrainingServer
+    from relayrl_prototype_amd.config import DEFAULT_CONFIG_CONTENT
+
+    def port():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        return p
+
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("RRL_QUIET_CONFIG", "1")
+    cfg = json.loads(DEFAULT_CONFIG_CONTENT)
+    cfg["algorithms"]["REINFORCE"]["traj_per_epoch"] = 4
+    for k in ("training_server", "trajectory_server", "agent_listener"):
+        cfg["server"][k]["port"] = str(port())
+    (tmp_path / "c.json").write_text(json.dumps(cfg))
+    srv = TrainingServer("REINFORCE", 4, 2, 100000, env_dir=str(tmp_path), config_path=str(tmp_path / "c.json"),
+                         server_type="zmq", device="cuda", hyperparams={"with_vf_baseline": "true"})
+    try:
+        assert srv.algorithm.learner.pi.params.is_cuda
+        agent = RelayRLAgent(config_path=str(tmp_path / "c.json"), server_type="zmq")
+        env = _native.VecEnv("CartPole-v1", 1, 0, 1)
+        obs = np.zeros((1, 4), np.float32)
+        rew = np.zeros(1, np.float32)
+        done = np.zeros(1, np.float32)
+        act = np.zeros(1, np.int32)
+        env.reset_ptr(obs.ctypes.data)
+        for _ in range(8):
+            r = 0.0
+            while True:
+                a = agent.request_for_action(obs[0], None, r)
+                act[0] = int(np.asarray(a.get_act()).reshape(-1)[0])
+                env.step_ptr(act.ctypes.data, obs.ctypes.data, rew.ctypes.data, done.ctypes.data)
+                r = float(rew[0])
+                if done[0] > 0:
+                    agent.flag_last_action(r)
+                    break
+        t0 = time.time()
+        while srv.service.received < 8 and time.time() - t0 < 30:
+            time.sleep(0.02)
+        assert srv.wait_idle(60) and srv.service.updates == 2, srv.service.last_error
+        t0 = time.time()
+        while agent.model_version < 2 and time.time() - t0 < 10:
+            time.sleep(0.05)
+        assert agent.model_version == 2
+        np.testing.assert_allclose(agent.policy.pi[0].T.ravel()[:10],
+                                   srv.algorithm.learner.pi.params[:10].cpu().numpy(), rtol=1e-6)
+        agent.close()
+    finally:
+        srv.close(save=False)
