@@ -310,3 +310,64 @@ def test_fc_forward_splitk_matches_direct(cuda, B):
     h.conv_fwd(xd, wd, bd, y2, B, 1, 1, FC_IN, 1, 1, 1, HIDDEN, True, work)
     ref = F.relu(x @ w.t() + b).reshape(-1)
     assert relerr(y1, ref) < 1e-2 and relerr(y2, ref) < 1e-2
+
+
+def _dp_worker(rank, world, port, q):
+    import os
+
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank), RRL_DIST_BACKEND="gloo", RRL_FORCE_DEVICE="0")
+        import torch.distributed as dist
+
+        from relayrl_prototype_amd.parallel.comm import init_distributed
+
+        comm = init_distributed()
+        dev = torch.device("cuda", 0)
+        spec = CNNSpec(6)
+        B = 16
+        m = DeviceNatureCNN(spec, dev, max_batch=B, params=spec.init(3))
+        grads = []
+        for r in range(world):  # every rank computes every rank's local gradient (oracle)
+            g = torch.Generator().manual_seed(100 + r)
+            obs = torch.randint(0, 256, (B, 21, 21, 64), dtype=torch.uint8, generator=g).to(dev)
+            act = torch.randint(0, 6, (B,), dtype=torch.int32, generator=g).to(dev)
+            adv, ret = torch.randn(B, generator=g).to(dev), torch.randn(B, generator=g).to(dev)
+            m.forward(obs, 0)
+            m.backward(obs, act, adv, ret, 0.5, 0.01)
+            grads.append(m.grad.clone())
+            if r == rank:
+                mine = (obs, act, adv, ret)
+        m.forward(mine[0], 0)
+        m.backward(*mine, 0.5, 0.01, comm=comm)  # bucketed, overlapped all-reduce
+        expect = sum(grads) / world
+        err = ((m.grad - expect).norm() / expect.norm()).item()
+        q.put((rank, err))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+
+
+def test_cnn_dp_overlapped_allreduce_matches_mean_gradient(cuda):
+    """Two ranks (gloo, sharing the one GPU): the overlapped two-bucket all-reduce equals the
+    mean of the per-rank gradients."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, err in res:
+        assert isinstance(err, float) and err < 1e-5, (rank, err)
