@@ -33,6 +33,10 @@ int rrl_adam(float* param, float* m, float* v, const float* grad, const float* s
              float eps, float grad_scale, float weight_decay, void* stream);
 int rrl_reduce_slabs(const float* slab, int nslab, int P, float scale, float* out, void* stream);
 int rrl_env_dims(int env, int* D, int* A, int* NS, int* max_steps);
+int rrl_rollout_cont(int env, const float* params, const float* env_consts, int N, int T, int H, float* state,
+                     int* ep_len, float* ep_ret, float* obs_buf, float* act_buf, float* logp_buf, float* rew_buf,
+                     float* done_buf, float* ep_stats, uint64_t seed, uint64_t step0, int reset_all, int max_steps,
+                     int num_cu, void* stream);
 int rrl_rollout_grid(int N, int num_cu);
 int rrl_rollout(int env, const float* params, int N, int T, int H, float* state, int* ep_len, float* ep_ret,
                 float* obs_buf, int* act_buf, float* logp_buf, float* rew_buf, float* done_buf,
@@ -299,6 +303,47 @@ void rollout(int64_t env, const Tensor& params, int64_t H, const Tensor& state, 
   check_rc(rc, "rollout");
 }
 
+// Continuous-action fused rollout (diagonal Gaussian policy; env id 4 = HalfCheetahSynth).
+void rollout_cont(int64_t env, const Tensor& params, const Tensor& env_consts, int64_t H, const Tensor& state,
+                  const Tensor& ep_len, const Tensor& ep_ret, const Tensor& obs_buf, const Tensor& act_buf,
+                  const Tensor& logp_buf, const Tensor& rew_buf, const Tensor& done_buf, const Tensor& ep_stats,
+                  int64_t seed, int64_t step0, bool reset_all, int64_t max_steps) {
+  auto [D, A, NS, ms] = env_dims(env);
+  (void)ms;
+  TORCH_CHECK(env == 4, "rollout_cont supports the continuous device env 4 (HalfCheetahSynth)");
+  TORCH_CHECK(H == 64 || H == 128, "hidden size must be 64 or 128");
+  check_dev(params, "params", at::kFloat);
+  check_numel(params, "params", flat_size(D, H, A, true));
+  check_dev(env_consts, "env_consts", at::kFloat);
+  check_numel(env_consts, "env_consts", 17 * 17 + 17 * 6);
+  check_dev(act_buf, "act_buf", at::kFloat);
+  TORCH_CHECK(act_buf.dim() == 3 && act_buf.size(2) == A, "act_buf must be [T, N, A]");
+  const int64_t T = act_buf.size(0), N = act_buf.size(1);
+  check_dev(state, "state", at::kFloat);
+  check_numel(state, "state", N * NS);
+  check_dev(ep_len, "ep_len", at::kInt);
+  check_numel(ep_len, "ep_len", N);
+  check_dev(ep_ret, "ep_ret", at::kFloat);
+  check_numel(ep_ret, "ep_ret", N);
+  check_dev(obs_buf, "obs_buf", at::kFloat);
+  check_numel(obs_buf, "obs_buf", (T + 1) * N * D);
+  check_dev(logp_buf, "logp_buf", at::kFloat);
+  check_numel(logp_buf, "logp_buf", T * N);
+  check_dev(rew_buf, "rew_buf", at::kFloat);
+  check_numel(rew_buf, "rew_buf", T * N);
+  check_dev(done_buf, "done_buf", at::kFloat);
+  check_numel(done_buf, "done_buf", T * N);
+  check_dev(ep_stats, "ep_stats", at::kFloat);
+  check_numel(ep_stats, "ep_stats", rollout_grid(N) * 8);
+  check_rc(rrl_rollout_cont((int)env, params.data_ptr<float>(), env_consts.data_ptr<float>(), (int)N, (int)T, (int)H,
+                            state.data_ptr<float>(), ep_len.data_ptr<int>(), ep_ret.data_ptr<float>(),
+                            obs_buf.data_ptr<float>(), act_buf.data_ptr<float>(), logp_buf.data_ptr<float>(),
+                            rew_buf.data_ptr<float>(), done_buf.data_ptr<float>(), ep_stats.data_ptr<float>(),
+                            (uint64_t)seed, (uint64_t)step0, reset_all ? 1 : 0, (int)max_steps, num_cus(),
+                            cur_stream()),
+           "rollout_cont");
+}
+
 }  // namespace
 
 void register_cnn_ops(pybind11::module_& m);  // cnn_ops.cpp
@@ -319,5 +364,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("env_dims", &env_dims);
   m.def("rollout_grid", &rollout_grid);
   m.def("rollout", &rollout);
+  m.def("rollout_cont", &rollout_cont);
   register_cnn_ops(m);
 }

@@ -192,6 +192,7 @@ PYBIND11_MODULE(_native, m) {
       .def("num_connections", &zmtp::Socket::num_connections);
 
   m.def("env_names", &env_names);
+  m.def("env_constants", &env_constants);
   py::class_<VecEnv>(m, "VecEnv")
       .def(py::init<const std::string&, int, uint64_t, int>(), py::arg("name"), py::arg("num_envs"),
            py::arg("seed") = 0, py::arg("num_threads") = 1)

@@ -247,15 +247,19 @@ class LunarLanderSynth : public Env {
 // ------------------------------------------------------------------ HalfCheetah-shaped (synthetic)
 // 17 obs / 6 continuous actions in [-1, 1]; a fixed, stable, weakly non-linear
 // dynamical system with reward = forward velocity (obs[8]) - 0.1 |a|^2, 1000 steps.
+// The system matrices are part of the env definition (also exported to the device env
+// through env_constants("HalfCheetahSynth-v0")).
+void halfcheetah_matrices(float (&A)[17][17], float (&B)[17][6]) {
+  Rng r(12345);
+  for (int i = 0; i < 17; ++i)
+    for (int j = 0; j < 17; ++j) A[i][j] = (i == j ? 0.9f : 0.f) + r.uniform(-0.03f, 0.03f);
+  for (int i = 0; i < 17; ++i)
+    for (int j = 0; j < 6; ++j) B[i][j] = r.uniform(-0.2f, 0.2f);
+}
+
 class HalfCheetahSynth : public Env {
  public:
-  HalfCheetahSynth() {
-    Rng r(12345);  // the system matrices are part of the env definition
-    for (int i = 0; i < 17; ++i)
-      for (int j = 0; j < 17; ++j) A_[i][j] = (i == j ? 0.9f : 0.f) + r.uniform(-0.03f, 0.03f);
-    for (int i = 0; i < 17; ++i)
-      for (int j = 0; j < 6; ++j) B_[i][j] = r.uniform(-0.2f, 0.2f);
-  }
+  HalfCheetahSynth() { halfcheetah_matrices(A_, B_); }
   int obs_dim() const override { return 17; }
   int act_dim() const override { return 6; }
   bool continuous() const override { return true; }
@@ -288,6 +292,17 @@ class HalfCheetahSynth : public Env {
 };
 
 }  // namespace
+
+std::vector<float> env_constants(const std::string& name) {
+  if (name == "HalfCheetahSynth-v0" || name == "HalfCheetah-v4") {
+    float A[17][17], B[17][6];
+    halfcheetah_matrices(A, B);
+    std::vector<float> out(&A[0][0], &A[0][0] + 17 * 17);
+    out.insert(out.end(), &B[0][0], &B[0][0] + 17 * 6);
+    return out;
+  }
+  return {};
+}
 
 std::vector<std::string> env_names() {
   return {"CartPole-v1", "MountainCar-v0", "Acrobot-v1", "Pendulum-v1", "LunarLanderSynth-v0", "HalfCheetahSynth-v0"};

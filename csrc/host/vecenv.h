@@ -59,6 +59,8 @@ class Env {
 
 std::unique_ptr<Env> make_env(const std::string& name);
 std::vector<std::string> env_names();
+// Constant tables that define an env (HalfCheetahSynth: A[17x17] then B[17x6]); empty if none.
+std::vector<float> env_constants(const std::string& name);
 
 struct EpisodeStats {
   double n = 0, sum = 0, sumsq = 0, max = -1e300, min = 1e300, sum_len = 0;

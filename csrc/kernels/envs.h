@@ -189,4 +189,52 @@ struct LunarLanderSynthEnv {
   }
 };
 
+// HalfCheetahSynth-v0: the host env's stable weakly non-linear system (csrc/host/vecenv.cpp)
+// s' = tanh(A s + B clip(u, -1, 1)) + U(-0.01, 0.01), reward = s'[8] - 0.1 |clip(u)|^2,
+// 17 obs, 6 continuous actions, 1000 steps.  A and B come from env_constants() and are
+// staged in LDS; the noise comes from the kernel's Philox stream.
+struct HalfCheetahSynthEnv {
+  static constexpr int D = 17, A = 6, NS = 17;
+  static constexpr int kMaxSteps = 1000;
+  static constexpr int kConsts = 17 * 17 + 17 * 6;
+  RRL_DEV static void reset(float (&s)[NS], uint2 key, uint32_t env, uint64_t step) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const uint4 r = philox4x32(make_uint4(env, (uint32_t)step, (uint32_t)(step >> 32), 16u + q), key);
+      const float u[4] = {u01(r.x), u01(r.y), u01(r.z), u01(r.w)};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (4 * q + k < NS) s[4 * q + k] = -0.1f + 0.2f * u[k];
+    }
+  }
+  RRL_DEV static float step(float (&s)[NS], const float (&a)[kMaxAct], const float* __restrict__ cst, uint2 key,
+                            uint32_t env, uint64_t step) {
+    float u[A], ctrl = 0.f;
+#pragma unroll
+    for (int j = 0; j < A; ++j) {
+      u[j] = fminf(fmaxf(a[j], -1.f), 1.f);
+      ctrl += u[j] * u[j];
+    }
+    float ns[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      float v = 0.f;
+#pragma unroll
+      for (int j = 0; j < NS; ++j) v += cst[i * 17 + j] * s[j];
+#pragma unroll
+      for (int j = 0; j < A; ++j) v += cst[17 * 17 + i * 6 + j] * u[j];
+      ns[i] = tanhf(v);
+    }
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const uint4 r = philox4x32(make_uint4(env, (uint32_t)step, (uint32_t)(step >> 32), 8u + q), key);
+      const float n[4] = {u01(r.x), u01(r.y), u01(r.z), u01(r.w)};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (4 * q + k < NS) s[4 * q + k] = ns[4 * q + k] + (-0.01f + 0.02f * n[k]);
+    }
+    return s[8] - 0.1f * ctrl;
+  }
+};
+
 }  // namespace rrl

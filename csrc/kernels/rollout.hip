@@ -172,11 +172,189 @@ __global__ __launch_bounds__(256, 2) void rollout_kernel(RolloutArgs p) {
   }
 }
 
+// ------------------------------------------------------------------ continuous envs
+// Same structure for a diagonal-Gaussian policy (PPO / REINFORCE on HalfCheetahSynth):
+// mu = MLP(obs), a = mu + exp(log_std) * n with n from Box-Muller over Philox draws
+// (tags 0 and 2), logp = sum(-n^2/2 - log_std - log(2 pi)/2) -- the learner's GAUSS_EVAL
+// formula.  Env constant tables (system matrices) are staged in LDS after the net.
+struct RolloutContArgs {
+  const float* params;
+  const float* env_consts;
+  int N, T;
+  float* state;     // [N][NS]
+  int* ep_len;      // [N]
+  float* ep_ret;    // [N]
+  float* obs_buf;   // [T+1][N][D]
+  float* act_buf;   // [T][N][A]
+  float* logp_buf;  // [T][N]
+  float* rew_buf;   // [T][N]
+  float* done_buf;  // [T][N]
+  float* ep_stats;  // [grid][8]
+  uint32_t seed_lo, seed_hi;
+  uint32_t step_lo, step_hi;
+  int reset_all;
+  int max_steps;
+};
+
+template <class Env, int HT>
+__global__ __launch_bounds__(256, 2) void rollout_cont_kernel(RolloutContArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int DT = (Env::D + 15) / 16;
+  using L = LdsNet<DT, HT>;
+  constexpr int H = L::H;
+  constexpr int D = Env::D, A = Env::A, NS = Env::NS;
+  static_assert(NS == D, "continuous device envs observe their full state");
+  const int net_floats = (L::floats(A) + 3) & ~3;
+  float* cst = lds + net_floats;
+  stage_net<DT, HT>(lds, p.params, D, A, true);
+  for (int i = threadIdx.x; i < Env::kConsts; i += blockDim.x) cst[i] = p.env_consts[i];
+  __syncthreads();
+
+  const int l = lane_id();
+  const int j = l & 15, g = l >> 4;
+  const int wave_in_block = threadIdx.x >> 6;
+  const int waves_per_block = blockDim.x >> 6;
+  const int wave = wave_in_block + blockIdx.x * waves_per_block;
+  const int total_waves = gridDim.x * waves_per_block;
+  const int ntiles = (p.N + kTileB - 1) / kTileB;
+  const uint2 key = make_uint2(p.seed_lo, p.seed_hi);
+  const uint64_t step0 = ((uint64_t)p.step_hi << 32) | p.step_lo;
+  const int kr1 = input_kr_last(D, DT);
+
+  float st_n = 0.f, st_sum = 0.f, st_sq = 0.f, st_max = -INFINITY, st_min = INFINITY, st_len = 0.f;
+
+  for (int tile = wave; tile < ntiles; tile += total_waves) {
+    const int env = tile * kTileB + j;
+    const bool valid = env < p.N;
+    const int envc = valid ? env : p.N - 1;
+    float s[NS];
+    int len;
+    float ret;
+    if (p.reset_all) {
+      Env::reset(s, key, (uint32_t)envc, step0);
+      len = 0;
+      ret = 0.f;
+    } else {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) s[k] = p.state[(size_t)envc * NS + k];
+      len = p.ep_len[envc];
+      ret = p.ep_ret[envc];
+    }
+    for (int t = 0; t < p.T; ++t) {
+      const uint64_t gstep = step0 + (uint64_t)t;
+      const size_t base = (size_t)t * p.N + env;
+      floatx4 x[DT];
+#pragma unroll
+      for (int q = 0; q < DT; ++q) x[q] = zero4();
+#pragma unroll
+      for (int f = 0; f < D; ++f)
+        if ((f & 3) == g) x[f >> 4][(f >> 2) & 3] = s[f];
+      if (valid) {
+#pragma unroll
+        for (int f = 0; f < D; ++f)
+          if ((f & 3) == g) p.obs_buf[base * D + f] = s[f];
+      }
+      floatx4 h1[HT], h2[HT];
+      dense_fwd<DT, HT, true>(lds + L::W1, L::S1, lds + L::B1, x, h1, kr1);
+      dense_fwd<HT, HT, true>(lds + L::W2, L::S2, lds + L::B2, h1, h2);
+      float mu[kMaxAct];
+      policy_logits<HT>(lds + L::W3, lds + L::B3, A, H, h2, mu);
+      const uint4 r0 = philox4x32(make_uint4((uint32_t)envc, (uint32_t)gstep, (uint32_t)(gstep >> 32), 0u), key);
+      const uint4 r1 = philox4x32(make_uint4((uint32_t)envc, (uint32_t)gstep, (uint32_t)(gstep >> 32), 2u), key);
+      const float uu[8] = {u01(r0.x), u01(r0.y), u01(r0.z), u01(r0.w), u01(r1.x), u01(r1.y), u01(r1.z), u01(r1.w)};
+      float nrm[8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float rad = sqrtf(-2.f * __logf(1.f - uu[2 * q]));
+        float sn, cs;
+        __sincosf(6.283185307179586f * uu[2 * q + 1], &sn, &cs);
+        nrm[2 * q] = rad * cs;
+        nrm[2 * q + 1] = rad * sn;
+      }
+      float act[kMaxAct];
+      float logp = 0.f;
+#pragma unroll
+      for (int a = 0; a < kMaxAct; ++a) {
+        act[a] = 0.f;
+        if (a < A) {
+          const float ls = lds[L::LOGSTD + a];
+          const float n = nrm[a < 8 ? a : 0];
+          act[a] = mu[a] + __expf(ls) * n;
+          logp += -0.5f * n * n - ls - kHalfLog2Pi;
+        }
+      }
+      const float r = Env::step(s, act, cst, key, (uint32_t)envc, gstep);
+      len += 1;
+      ret += r;
+      const bool done = len >= p.max_steps;  // this env only truncates (time limit)
+      if (valid && g == 0) {
+#pragma unroll
+        for (int a = 0; a < A; ++a) p.act_buf[base * A + a] = act[a];
+        p.logp_buf[base] = logp;
+        p.rew_buf[base] = r;
+        p.done_buf[base] = done ? 1.f : 0.f;
+      }
+      if (done) {
+        if (valid && g == 0) {
+          st_n += 1.f;
+          st_sum += ret;
+          st_sq += ret * ret;
+          st_max = fmaxf(st_max, ret);
+          st_min = fminf(st_min, ret);
+          st_len += (float)len;
+        }
+        Env::reset(s, key, (uint32_t)envc, gstep + 0x100000000ull);
+        len = 0;
+        ret = 0.f;
+      }
+    }
+    if (valid) {
+      const size_t base = (size_t)p.T * p.N + env;
+#pragma unroll
+      for (int f = 0; f < D; ++f)
+        if ((f & 3) == g) p.obs_buf[base * D + f] = s[f];
+      if (g == 0) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) p.state[(size_t)env * NS + k] = s[k];
+        p.ep_len[env] = len;
+        p.ep_ret[env] = ret;
+      }
+    }
+  }
+  __syncthreads();
+  float* red = lds;
+  float v0 = wave_sum(st_n), v1 = wave_sum(st_sum), v2 = wave_sum(st_sq), v5 = wave_sum(st_len);
+  float v3 = st_max, v4 = st_min;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    v3 = fmaxf(v3, __shfl_xor(v3, o, 64));
+    v4 = fminf(v4, __shfl_xor(v4, o, 64));
+  }
+  if (l == 0) {
+    red[wave_in_block * 8 + 0] = v0;
+    red[wave_in_block * 8 + 1] = v1;
+    red[wave_in_block * 8 + 2] = v2;
+    red[wave_in_block * 8 + 3] = v3;
+    red[wave_in_block * 8 + 4] = v4;
+    red[wave_in_block * 8 + 5] = v5;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int q = threadIdx.x;
+    float v = red[q];
+    for (int w = 1; w < waves_per_block; ++w) {
+      const float u = red[w * 8 + q];
+      v = (q == 3) ? fmaxf(v, u) : (q == 4) ? fminf(v, u) : v + u;
+    }
+    p.ep_stats[blockIdx.x * 8 + q] = v;
+  }
+}
+
 }  // namespace rrl
 
 using namespace rrl;
 
-enum EnvId : int { ENV_CARTPOLE = 0, ENV_MOUNTAINCAR = 1, ENV_ACROBOT = 2, ENV_LUNARLANDER = 3 };
+enum EnvId : int { ENV_CARTPOLE = 0, ENV_MOUNTAINCAR = 1, ENV_ACROBOT = 2, ENV_LUNARLANDER = 3, ENV_HALFCHEETAH = 4 };
 
 extern "C" int rrl_env_dims(int env, int* D, int* A, int* NS, int* max_steps) {
   switch (env) {
@@ -188,6 +366,12 @@ extern "C" int rrl_env_dims(int env, int* D, int* A, int* NS, int* max_steps) {
       *A = LunarLanderSynthEnv::A;
       *NS = LunarLanderSynthEnv::NS;
       *max_steps = LunarLanderSynthEnv::kMaxSteps;
+      return 0;
+    case ENV_HALFCHEETAH:
+      *D = HalfCheetahSynthEnv::D;
+      *A = HalfCheetahSynthEnv::A;
+      *NS = HalfCheetahSynthEnv::NS;
+      *max_steps = HalfCheetahSynthEnv::kMaxSteps;
       return 0;
   }
   return -1;
@@ -239,5 +423,36 @@ extern "C" int rrl_rollout(int env, const float* params, int N, int T, int H, fl
       case ENV_LUNARLANDER: return launch_rollout<LunarLanderSynthEnv, 4>(a, grid, s);
     }
   }
+  return -3;
+}
+
+template <class Env, int HT>
+static int launch_rollout_cont(const RolloutContArgs& a, int grid, hipStream_t s) {
+  constexpr int DT = (Env::D + 15) / 16;
+  using L = LdsNet<DT, HT>;
+  const size_t bytes = ((size_t)((L::floats(Env::A) + 3) & ~3) + Env::kConsts) * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)rollout_cont_kernel<Env, HT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    attr = true;
+  }
+  hipLaunchKernelGGL((rollout_cont_kernel<Env, HT>), dim3(grid), dim3(256), bytes, s, a);
+  return (int)hipGetLastError();
+}
+
+// Continuous-action device envs (env id ENV_HALFCHEETAH); env_consts = env_constants(name).
+extern "C" int rrl_rollout_cont(int env, const float* params, const float* env_consts, int N, int T, int H,
+                                float* state, int* ep_len, float* ep_ret, float* obs_buf, float* act_buf,
+                                float* logp_buf, float* rew_buf, float* done_buf, float* ep_stats, uint64_t seed,
+                                uint64_t step0, int reset_all, int max_steps, int num_cu, void* stream) {
+  if (N <= 0 || T <= 0 || env != ENV_HALFCHEETAH || env_consts == nullptr) return -2;
+  RolloutContArgs a{params, env_consts, N, T, state, ep_len, ep_ret, obs_buf, act_buf, logp_buf, rew_buf, done_buf,
+                    ep_stats, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step0, (uint32_t)(step0 >> 32),
+                    reset_all, max_steps};
+  const int grid = rrl_rollout_grid(N, num_cu);
+  hipStream_t s = (hipStream_t)stream;
+  if (H == 128) return launch_rollout_cont<HalfCheetahSynthEnv, 8>(a, grid, s);
+  if (H == 64) return launch_rollout_cont<HalfCheetahSynthEnv, 4>(a, grid, s);
   return -3;
 }

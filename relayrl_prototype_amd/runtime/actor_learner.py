@@ -68,9 +68,10 @@ class _Actor:
 
     def __init__(self, cfg: ActorLearnerConfig, comm: Comm, device):
         self.device = torch.device(device)
-        from .vec_trainer import DEVICE_ENVS
+        from .vec_trainer import CONTINUOUS_DEVICE_ENVS, DEVICE_ENVS
 
-        self.kind = "device" if (self.device.type == "cuda" and cfg.env in DEVICE_ENVS) else "host"
+        self.kind = "device" if (self.device.type == "cuda" and cfg.env in DEVICE_ENVS
+                                 and cfg.env not in CONTINUOUS_DEVICE_ENVS) else "host"
         if self.kind == "device":
             from .vec_trainer import VecTrainer, VecTrainerConfig
 

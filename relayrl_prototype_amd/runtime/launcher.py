@@ -48,7 +48,11 @@ PRESETS: Dict[str, Preset] = {
         "pong-a2c", "A2C Pong pixels, Nature-CNN on MFMA, DP gradient all-reduce",
         "pixel", {"num_envs": 1024, "rollout_len": 5}),
     "halfcheetah-ppo": Preset(
-        "halfcheetah-ppo", "PPO HalfCheetah continuous Gaussian policy, large-batch GAE",
+        "halfcheetah-ppo", "PPO HalfCheetah continuous Gaussian policy, large-batch GAE, HBM rollout buffer",
+        "vec", {"env": "HalfCheetahSynth-v0", "algo": "ppo", "num_envs": 16384, "rollout_len": 256,
+                "train_pi_iters": 10, "train_vf_iters": 10, "with_baseline": True, "gamma": 0.99, "lam": 0.95}),
+    "halfcheetah-ppo-host": Preset(
+        "halfcheetah-ppo-host", "PPO HalfCheetah with C++ host env threads (pinned H2D/D2H pipeline)",
         "host", {"env": "HalfCheetahSynth-v0", "algo": "ppo", "num_envs": 4096, "rollout_len": 256,
                  "train_pi_iters": 10, "train_vf_iters": 10, "num_threads": 8, "with_baseline": True}),
 }

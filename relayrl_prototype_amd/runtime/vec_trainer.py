@@ -29,7 +29,9 @@ from ..parallel.comm import Comm
 from ..utils.tracing import PhaseTimer
 from .rollout_learn import RolloutLearner, episode_metrics
 
-DEVICE_ENVS = {"CartPole-v1": 0, "MountainCar-v0": 1, "Acrobot-v1": 2, "LunarLanderSynth-v0": 3}
+DEVICE_ENVS = {"CartPole-v1": 0, "MountainCar-v0": 1, "Acrobot-v1": 2, "LunarLanderSynth-v0": 3,
+               "HalfCheetahSynth-v0": 4}
+CONTINUOUS_DEVICE_ENVS = {"HalfCheetahSynth-v0"}
 
 
 @dataclass
@@ -77,7 +79,9 @@ class VecTrainer:
         dev = self.device
         rank = self.comm.rank
         # identical initial weights on every rank (seeded), per-rank env RNG streams
-        self.learner = PGLearner(cfg.algo, D, A, H, True, cfg.with_baseline, cfg.pi_lr, cfg.vf_lr, cfg.train_vf_iters,
+        self.continuous = cfg.env in CONTINUOUS_DEVICE_ENVS
+        self.learner = PGLearner(cfg.algo, D, A, H, not self.continuous, cfg.with_baseline, cfg.pi_lr, cfg.vf_lr,
+                                 cfg.train_vf_iters,
                                  cfg.train_pi_iters, cfg.clip_ratio, cfg.target_kl, cfg.ent_coef, dev, cfg.seed,
                                  self.comm, cfg.use_graphs)
         self.pi, self.vf = self.learner.pi, self.learner.vf
@@ -86,7 +90,13 @@ class VecTrainer:
         self.env_seed = (cfg.seed * 0x9E3779B97F4A7C15 + rank * 0x632BE59BD9B4E019) & 0x7FFFFFFFFFFFFFFF
         # time-major SoA rollout buffers (HBM resident)
         self.obs = torch.zeros(T + 1, N, D, device=dev)
-        self.act = torch.zeros(T, N, dtype=torch.int32, device=dev)
+        if self.continuous:
+            from .. import _native
+
+            self.act = torch.zeros(T, N, A, device=dev)
+            self.env_consts = torch.tensor(_native.env_constants(cfg.env), dtype=torch.float32, device=dev)
+        else:
+            self.act = torch.zeros(T, N, dtype=torch.int32, device=dev)
         self.logp = torch.zeros(T, N, device=dev)
         self.rew = torch.zeros(T, N, device=dev)
         self.done = torch.zeros(T, N, device=dev)
@@ -104,8 +114,14 @@ class VecTrainer:
     def rollout(self):
         cfg, h = self.cfg, hip()
         step0 = self.epoch * cfg.rollout_len
-        h.rollout(self.env_id, self.pi.params, cfg.hidden, self.state, self.ep_len, self.ep_ret, self.obs, self.act,
-                  self.logp, self.rew, self.done, self.ep_stats, self.env_seed, step0, self._first, self.max_steps)
+        if self.continuous:
+            h.rollout_cont(self.env_id, self.pi.params, self.env_consts, cfg.hidden, self.state, self.ep_len,
+                           self.ep_ret, self.obs, self.act, self.logp, self.rew, self.done, self.ep_stats,
+                           self.env_seed, step0, self._first, self.max_steps)
+        else:
+            h.rollout(self.env_id, self.pi.params, cfg.hidden, self.state, self.ep_len, self.ep_ret, self.obs,
+                      self.act, self.logp, self.rew, self.done, self.ep_stats, self.env_seed, step0, self._first,
+                      self.max_steps)
         self._first = False
 
     def train_epoch(self):

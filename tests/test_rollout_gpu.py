@@ -149,3 +149,46 @@ def test_lunarlander_device_rollout_matches_oracle(cuda):
         checked += live.sum()
     assert checked > N * T // 2
     assert np.isin(np.unique(a), np.arange(4)).all()
+
+
+def test_halfcheetah_gaussian_device_rollout_matches_oracle(cuda):
+    """Continuous fused rollout: Gaussian actions / log-probs vs the fp32 MLP oracle and the
+    env transition vs a numpy oracle of HalfCheetahSynth with the kernel's Philox noise."""
+    from relayrl_prototype_amd import _native
+
+    h = hip()
+    env = 4
+    D, A, NS, ms = h.env_dims(env)
+    assert (D, A) == (17, 6)
+    N, T, H, seed = 128, 6, 128, 11
+    spec = MLPSpec(D, H, A, gaussian=True)
+    params = spec.init(torch.Generator().manual_seed(2))
+    cst = np.asarray(_native.env_constants("HalfCheetahSynth-v0"), np.float32)
+    Am, Bm = cst[:289].reshape(17, 17), cst[289:].reshape(17, 6)
+    state = torch.zeros(N, NS, device=cuda)
+    ep_len = torch.zeros(N, dtype=torch.int32, device=cuda)
+    ep_ret = torch.zeros(N, device=cuda)
+    obs = torch.zeros(T + 1, N, D, device=cuda)
+    act = torch.zeros(T, N, A, device=cuda)
+    logp, rew, done = (torch.zeros(T, N, device=cuda) for _ in range(3))
+    stats = torch.zeros(h.rollout_grid(N), 8, device=cuda)
+    h.rollout_cont(env, params.to(cuda), torch.from_numpy(cst).to(cuda), H, state, ep_len, ep_ret, obs, act, logp,
+                   rew, done, stats, seed, 0, True, ms)
+    torch.cuda.synchronize()
+    o, a, lp, r = obs.cpu(), act.cpu(), logp.cpu(), rew.cpu()
+    ls = params[spec.offsets()["log_std"]:spec.offsets()["log_std"] + A]
+    for t in range(T):
+        mu = ref.mlp_forward_ref(3, params, o[t], A, H)["logits"]
+        z = (a[t] - mu) / torch.exp(ls)
+        lp_ref = (-0.5 * z * z - ls - 0.9189385332046727).sum(-1)
+        torch.testing.assert_close(lp[t], lp_ref, rtol=1e-3, atol=2e-3)
+        u = np.clip(a[t].numpy(), -1, 1)
+        pre = o[t].numpy() @ Am.T + u @ Bm.T
+        noise = np.concatenate([np.stack(philox.uniforms(seed, t, np.arange(N), 8 + q), 1) for q in range(5)], 1)
+        ns = np.tanh(pre) + (-0.01 + 0.02 * noise[:, :17])
+        np.testing.assert_allclose(o[t + 1].numpy(), ns, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(r[t].numpy(), ns[:, 8] - 0.1 * (u * u).sum(1), rtol=1e-4, atol=1e-4)
+    # sampled actions are mu + std * N(0, 1)
+    zs = ((a - torch.stack([ref.mlp_forward_ref(3, params, o[t], A, H)["logits"] for t in range(T)]))
+          / torch.exp(ls)).reshape(-1)
+    assert abs(zs.mean().item()) < 0.05 and abs(zs.std().item() - 1.0) < 0.05
