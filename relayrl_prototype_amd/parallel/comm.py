@@ -38,12 +38,16 @@ def local_device_index() -> int:
     return int(forced) if forced not in (None, "") else dist_env()[1]
 
 
-def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) -> "Comm":
+def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> "Comm":
     """Initialise the default process group from the environment (torchrun) if world > 1.
     Backend: ``nccl`` (= RCCL over xGMI on ROCm) with GPUs, ``gloo`` on CPU; override with
     RRL_DIST_BACKEND."""
     rank, local, world = dist_env()
     local = local_device_index()
+    if timeout_s is None:
+        # a stalled rank turns into a collective timeout -> the rank exits -> torchrun restarts
+        # the group (--max-restarts) and ranks auto-resume from their checkpoints
+        timeout_s = float(os.environ.get("RRL_COLLECTIVE_TIMEOUT_S", "600"))
     if world > 1 and not dist.is_initialized():
         backend = backend or os.environ.get("RRL_DIST_BACKEND") or None
         if backend is None:

@@ -161,6 +161,9 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
                 m["Time"] = el
                 if "EnvSteps" in m and el > 0:
                     m["EnvStepsPerSec"] = m["EnvSteps"] / el
+                m["UpdatesPerSec"] = (ep - start) / el if el > 0 else 0.0
+                if dev.type == "cuda":
+                    m["HBMUsedGB"] = torch.cuda.max_memory_allocated(dev) / 2 ** 30
                 for k, v in m.items():
                     if isinstance(v, (int, float)):
                         logger.log_tabular(k, v)
