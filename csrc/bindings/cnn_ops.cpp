@@ -23,17 +23,20 @@ int rrl_sum_splits(const float* part, int splits, long long n, float* out, void*
 int rrl_colsum(const uint16_t* y, int M, int C, float* part, int splits, void* stream);
 int rrl_sumsq(const float* x, long long n, float* work, int work_n, float* out, void* stream);
 int rrl_adam_clip(float* p, float* m, float* v, const float* g, uint16_t* shadow, long long n, const float* norm_sq,
-                  float max_norm, float lr, float b1, float b2, float eps, int step, void* stream);
+                  float max_norm, float lr, float b1, float b2, float eps, int step, const long long* step_dev,
+                  void* stream);
+int rrl_counter_add(long long* c, long long inc, void* stream);
 int rrl_to_bf16(const float* x, uint16_t* y, long long n, void* stream);
 int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, int A, int32_t* act, float* logp,
-                 float* value, float* logits_out, unsigned long long seed, unsigned long long step, int row_offset,
+                 float* value, float* logits_out, unsigned long long seed, unsigned long long step,
+                 const unsigned long long* step_base, int row_offset,
                  const int32_t* act_in, const float* adv, const float* ret, float inv_B, float vf_coef,
                  float ent_coef, uint16_t* dh, float* dhead, float* stats, int grid, void* stream);
 int rrl_head_wgrad(const uint16_t* h, const float* dhead, int B, int A, float* part, int nblk, void* stream);
 int rrl_pong_state_size();
 int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
-                  float* ep_acc, int N,
-                  unsigned long long seed, unsigned long long step, int max_steps, int reset_all, void* stream);
+                  float* ep_acc, int N, unsigned long long seed, unsigned long long step,
+                  const unsigned long long* step_base, int max_steps, int reset_all, void* stream);
 int rrl_pong_render(const float* state, uint8_t* obs, int N, void* stream);
 }
 
@@ -165,18 +168,26 @@ void sumsq(const Tensor& x, const Tensor& work, const Tensor& out) {
 }
 
 void adam_clip(const Tensor& p, const Tensor& m, const Tensor& v, const Tensor& g, const OptT& shadow,
-               const OptT& norm_sq, double max_norm, double lr, double b1, double b2, double eps, int64_t step) {
+               const OptT& norm_sq, double max_norm, double lr, double b1, double b2, double eps, int64_t step,
+               const OptT& step_dev) {
   const int64_t n = p.numel();
   check(p, "p", at::kFloat, n);
   check(m, "m", at::kFloat, n);
   check(v, "v", at::kFloat, n);
   check(g, "g", at::kFloat, n);
-  TORCH_CHECK(step >= 1, "adam step must be >= 1");
+  const long long* sd = opt_ptr<const long long>(step_dev, "step_dev", at::kLong, 1);
+  TORCH_CHECK(sd != nullptr || step >= 1, "adam step must be >= 1");
   uint16_t* sh = opt_ptr<uint16_t>(shadow, "shadow", at::kBFloat16, n);
   const float* ns = opt_ptr<const float>(norm_sq, "norm_sq", at::kFloat, 1);
   rc_check(rrl_adam_clip(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr<float>(), sh, n,
-                         ns, (float)max_norm, (float)lr, (float)b1, (float)b2, (float)eps, (int)step, stream()),
+                         ns, (float)max_norm, (float)lr, (float)b1, (float)b2, (float)eps, (int)step, sd, stream()),
            "adam_clip");
+}
+
+void counter_add(const Tensor& c, int64_t inc) {
+  check(c, "counter", at::kLong, 1);
+  rc_check(rrl_counter_add((long long*)c.data_ptr(), inc, stream()),
+           "counter_add");
 }
 
 void to_bf16(const Tensor& x, const Tensor& y) {
@@ -188,7 +199,8 @@ void to_bf16(const Tensor& x, const Tensor& y) {
 void a2c_head(int64_t mode, const Tensor& h, const Tensor& head_params, int64_t B, int64_t A, const OptT& act,
               const OptT& logp, const OptT& value, const OptT& logits, int64_t seed, int64_t step,
               int64_t row_offset, const OptT& act_in, const OptT& adv, const OptT& ret, double inv_B, double vf_coef,
-              double ent_coef, const OptT& dh, const OptT& dhead, const OptT& stats, int64_t grid) {
+              double ent_coef, const OptT& dh, const OptT& dhead, const OptT& stats, int64_t grid,
+              const OptT& step_base) {
   constexpr int64_t F = 512;
   TORCH_CHECK(A >= 1 && A <= 16, "a2c_head: 1 <= A <= 16");
   TORCH_CHECK(mode == 0 || mode == 1, "a2c_head: mode must be 0 (rollout) or 1 (train)");
@@ -207,8 +219,9 @@ void a2c_head(int64_t mode, const Tensor& h, const Tensor& head_params, int64_t 
   float* st = opt_ptr<float>(stats, "stats", at::kFloat, mode == 1 ? grid * 4 : 0);
   if (mode == 1)
     TORCH_CHECK(ai && ad && re && dhp && dhd && st, "a2c_head train mode needs act_in, adv, ret, dh, dhead, stats");
+  const unsigned long long* sb = opt_ptr<const unsigned long long>(step_base, "step_base", at::kLong, 1);
   rc_check(rrl_a2c_head((int)mode, bf(h), head_params.data_ptr<float>(), B, A, ap, lp, vp, lo, (uint64_t)seed,
-                        (uint64_t)step, (int)row_offset, ai, ad, re, (float)inv_B, (float)vf_coef, (float)ent_coef,
+                        (uint64_t)step, sb, (int)row_offset, ai, ad, re, (float)inv_B, (float)vf_coef, (float)ent_coef,
                         dhp, dhd, st, (int)grid, stream()),
            "a2c_head");
 }
@@ -227,7 +240,7 @@ int64_t pong_state_size() { return rrl_pong_state_size(); }
 
 void pong_step(const Tensor& state, const Tensor& act, const Tensor& rew, const Tensor& done, const Tensor& fin_ret,
                const Tensor& fin_len, const OptT& ep_acc, int64_t N, int64_t seed, int64_t step, int64_t max_steps,
-               bool reset_all) {
+               bool reset_all, const OptT& step_base) {
   check(state, "state", at::kFloat, N * pong_state_size());
   check(act, "act", at::kInt, reset_all ? 0 : N);
   check(rew, "rew", at::kFloat, N);
@@ -235,9 +248,10 @@ void pong_step(const Tensor& state, const Tensor& act, const Tensor& rew, const 
   check(fin_ret, "fin_ret", at::kFloat, N);
   check(fin_len, "fin_len", at::kFloat, N);
   float* acc = opt_ptr<float>(ep_acc, "ep_acc", at::kFloat, 4 * N);
+  const unsigned long long* sb = opt_ptr<const unsigned long long>(step_base, "step_base", at::kLong, 1);
   rc_check(rrl_pong_step(state.data_ptr<float>(), act.data_ptr<int32_t>(), rew.data_ptr<float>(),
                          done.data_ptr<float>(), fin_ret.data_ptr<float>(), fin_len.data_ptr<float>(), acc, (int)N,
-                         (uint64_t)seed, (uint64_t)step, (int)max_steps, reset_all ? 1 : 0, stream()),
+                         (uint64_t)seed, (uint64_t)step, sb, (int)max_steps, reset_all ? 1 : 0, stream()),
            "pong_step");
 }
 
@@ -262,11 +276,23 @@ void register_cnn_ops(pybind11::module_& m) {
   m.def("sum_splits", &sum_splits);
   m.def("colsum", &colsum);
   m.def("sumsq", &sumsq);
-  m.def("adam_clip", &adam_clip);
+  m.def("adam_clip", &adam_clip, pybind11::arg("p"), pybind11::arg("m"), pybind11::arg("v"), pybind11::arg("g"),
+        pybind11::arg("shadow"), pybind11::arg("norm_sq"), pybind11::arg("max_norm"), pybind11::arg("lr"),
+        pybind11::arg("b1"), pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("step"),
+        pybind11::arg("step_dev") = pybind11::none());
+  m.def("counter_add", &counter_add);
   m.def("to_bf16", &to_bf16);
-  m.def("a2c_head", &a2c_head);
+  m.def("a2c_head", &a2c_head, pybind11::arg("mode"), pybind11::arg("h"), pybind11::arg("head_params"),
+        pybind11::arg("B"), pybind11::arg("A"), pybind11::arg("act"), pybind11::arg("logp"), pybind11::arg("value"),
+        pybind11::arg("logits"), pybind11::arg("seed"), pybind11::arg("step"), pybind11::arg("row_offset"),
+        pybind11::arg("act_in"), pybind11::arg("adv"), pybind11::arg("ret"), pybind11::arg("inv_B"),
+        pybind11::arg("vf_coef"), pybind11::arg("ent_coef"), pybind11::arg("dh"), pybind11::arg("dhead"),
+        pybind11::arg("stats"), pybind11::arg("grid"), pybind11::arg("step_base") = pybind11::none());
   m.def("head_wgrad", &head_wgrad);
   m.def("pong_state_size", &pong_state_size);
-  m.def("pong_step", &pong_step);
+  m.def("pong_step", &pong_step, pybind11::arg("state"), pybind11::arg("act"), pybind11::arg("rew"),
+        pybind11::arg("done"), pybind11::arg("fin_ret"), pybind11::arg("fin_len"), pybind11::arg("ep_acc"),
+        pybind11::arg("N"), pybind11::arg("seed"), pybind11::arg("step"), pybind11::arg("max_steps"),
+        pybind11::arg("reset_all"), pybind11::arg("step_base") = pybind11::none());
   m.def("pong_render", &pong_render);
 }

@@ -395,7 +395,12 @@ __global__ void sum_small_kernel(const float* __restrict__ part, int n, float* _
 __global__ void adam_clip_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                  const float* __restrict__ g, uint16_t* __restrict__ shadow, size_t n,
                                  const float* __restrict__ norm_sq, float max_norm, float lr, float b1, float b2,
-                                 float eps, float bc1, float bc2) {
+                                 float eps, float bc1, float bc2, const long long* __restrict__ step_dev) {
+  if (step_dev) {  // bias corrections from the device step counter (capturable in a hipGraph)
+    const float t = (float)(*step_dev);
+    bc1 = 1.f - powf(b1, t);
+    bc2 = 1.f - powf(b2, t);
+  }
   float scale = 1.f;
   if (norm_sq != nullptr && max_norm > 0.f) {
     const float nrm = sqrtf(norm_sq[0]);
@@ -438,6 +443,7 @@ struct HeadArgs {
   float* value;
   float* logits_out;      // optional [B][A]
   uint32_t seed_lo, seed_hi, step_lo, step_hi;
+  const unsigned long long* step_base;  // optional device counter added to the step (graph replays)
   int row_offset;
   // training inputs / outputs
   const int32_t* act_in;
@@ -492,7 +498,9 @@ __global__ void __launch_bounds__(256) a2c_head_kernel(HeadArgs a) {
     const CatStats cs = cat_stats(A, logits);
     if (!TRAIN) {
       if (lane == 0) {
-        const uint4 r = philox4x32(make_uint4((uint32_t)(row + a.row_offset), a.step_lo, a.step_hi, 0x50u),
+        unsigned long long st = ((unsigned long long)a.step_hi << 32) | a.step_lo;
+        if (a.step_base) st += *a.step_base;
+        const uint4 r = philox4x32(make_uint4((uint32_t)(row + a.row_offset), (uint32_t)st, (uint32_t)(st >> 32), 0x50u),
                                    make_uint2(a.seed_lo, a.seed_hi));
         const int pick = cat_sample(A, logits, cs.lse, u01(r.x));
         if (a.act) a.act[row] = pick;
@@ -740,11 +748,21 @@ int rrl_sumsq(const float* x, long long n, float* work, int work_n, float* out, 
 }
 
 int rrl_adam_clip(float* p, float* m, float* v, const float* g, uint16_t* shadow, long long n, const float* norm_sq,
-                  float max_norm, float lr, float b1, float b2, float eps, int step, void* stream_) {
+                  float max_norm, float lr, float b1, float b2, float eps, int step, const long long* step_dev,
+                  void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
   hipLaunchKernelGGL(adam_clip_kernel, dim3(grid_for((size_t)n, 256, 8192)), dim3(256), 0, st, p, m, v, g, shadow,
-                     (size_t)n, norm_sq, max_norm, lr, b1, b2, eps, bc1, bc2);
+                     (size_t)n, norm_sq, max_norm, lr, b1, b2, eps, bc1, bc2, step_dev);
+  return (int)hipGetLastError();
+}
+
+__global__ void counter_add_kernel(long long* c, long long inc) { c[0] += inc; }
+
+// Device-side step counters advanced inside captured graphs.
+int rrl_counter_add(long long* c, long long inc, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, st, c, inc);
   return (int)hipGetLastError();
 }
 
@@ -756,7 +774,8 @@ int rrl_to_bf16(const float* x, uint16_t* y, long long n, void* stream_) {
 
 // mode 0: rollout (sample act / logp / value), 1: training (dh, dhead, stats).
 int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, int A, int32_t* act, float* logp,
-                 float* value, float* logits_out, unsigned long long seed, unsigned long long step, int row_offset,
+                 float* value, float* logits_out, unsigned long long seed, unsigned long long step,
+                 const unsigned long long* step_base, int row_offset,
                  const int32_t* act_in, const float* adv, const float* ret, float inv_B, float vf_coef,
                  float ent_coef, uint16_t* dh, float* dhead, float* stats, int grid, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
@@ -777,6 +796,7 @@ int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, i
   a.seed_hi = (uint32_t)(seed >> 32);
   a.step_lo = (uint32_t)step;
   a.step_hi = (uint32_t)(step >> 32);
+  a.step_base = step_base;
   a.row_offset = row_offset;
   a.act_in = act_in;
   a.adv = adv;

@@ -50,9 +50,14 @@ RRL_DEV void reset_env(float* s, uint4 r) {
 __global__ void pong_step_kernel(float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew,
                                  float* __restrict__ done, float* __restrict__ fin_ret, float* __restrict__ fin_len,
                                  float* __restrict__ ep_acc, int N, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
-                                 int reset_all) {
+                                 int reset_all, const unsigned long long* __restrict__ step_base) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= N) return;
+  if (step_base) {  // device step counter (graph replays): the host value is an offset
+    const unsigned long long st = (((unsigned long long)step_hi << 32) | step_lo) + *step_base;
+    step_lo = (uint32_t)st;
+    step_hi = (uint32_t)(st >> 32);
+  }
   float s[kPongState];
 #pragma unroll
   for (int i = 0; i < kPongState; ++i) s[i] = state[(size_t)e * kPongState + i];
@@ -175,12 +180,13 @@ extern "C" {
 int rrl_pong_state_size() { return kPongState; }
 
 int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
-                  float* ep_acc, int N,
-                  unsigned long long seed, unsigned long long step, int max_steps, int reset_all, void* stream_) {
+                  float* ep_acc, int N, unsigned long long seed, unsigned long long step,
+                  const unsigned long long* step_base, int max_steps, int reset_all, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
   hipLaunchKernelGGL(pong_step_kernel, dim3((N + 255) / 256), dim3(256), 0, st, state, act, rew, done, fin_ret,
-                     fin_len, ep_acc, N, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, reset_all);
+                     fin_len, ep_acc, N, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, reset_all,
+                     step_base);
   return (int)hipGetLastError();
 }
 

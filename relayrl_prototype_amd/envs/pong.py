@@ -205,23 +205,39 @@ class DevicePong:
         self.fin_len = torch.zeros(self.N, device=dev)
         self.ep_acc = torch.zeros(self.N, 4, device=dev)  # per env: episodes, sum ret, sum len, sum ret^2
         self._dummy_act = torch.zeros(self.N, dtype=torch.int32, device=dev)
-        self.step_count = 0
+        self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    # The RNG step counter lives on the device (``step_t``) so that a rollout captured in
+    # a hipGraph draws fresh numbers on every replay; kernels add their host ``offset``.
+    @property
+    def step_count(self) -> int:
+        return int(self.step_t.item())
+
+    @step_count.setter
+    def step_count(self, v: int):
+        self.step_t.fill_(int(v))
+
+    def advance(self, k: int):
+        self.h.counter_add(self.step_t, int(k))
 
     def reset(self, obs_out: torch.Tensor):
         self.h.pong_step(self.state, self._dummy_act, self.rew, self.done, self.fin_ret, self.fin_len, None, self.N,
-                         self.seed, self.step_count, self.max_steps, True)
-        self.step_count += 1
+                         self.seed, 0, self.max_steps, True, self.step_t)
+        self.advance(1)
         self.h.pong_render(self.state, obs_out, self.N)
 
     def episode_stats(self):
         """(episodes, sum return, sum length, sum return^2) over all envs since the last reset."""
         return self.ep_acc.double().sum(0)
 
-    def step(self, act: torch.Tensor, obs_out: torch.Tensor, rew_out=None, done_out=None):
+    def step(self, act: torch.Tensor, obs_out: torch.Tensor, rew_out=None, done_out=None, offset: int = None):
+        """One env step.  Without ``offset`` the device counter is advanced after the step;
+        with it (graph-captured rollouts) the caller advances once per rollout."""
         rew = self.rew if rew_out is None else rew_out
         done = self.done if done_out is None else done_out
         self.h.pong_step(self.state, act, rew, done, self.fin_ret, self.fin_len, self.ep_acc, self.N, self.seed,
-                         self.step_count, self.max_steps, False)
-        self.step_count += 1
+                         0 if offset is None else int(offset), self.max_steps, False, self.step_t)
+        if offset is None:
+            self.advance(1)
         self.h.pong_render(self.state, obs_out, self.N)
         return rew, done

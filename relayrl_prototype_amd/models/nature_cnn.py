@@ -193,7 +193,7 @@ class DeviceNatureCNN:
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params)
         self.grad = torch.zeros_like(self.params)
-        self.step_count = 0
+        self.step_t = torch.zeros(1, dtype=torch.int64, device=dev)  # Adam step (device: graph replays)
         B = self.max_batch
         bf = torch.bfloat16
         L1, L2, L3 = CONVS
@@ -256,12 +256,14 @@ class DeviceNatureCNN:
                    True, self.part)  # split-K when the batch is too small to fill the chip
         return hid
 
-    def act(self, obs_u8, row0, act_out, logp_out, value_out, seed: int, step: int, row_offset: int = 0):
+    def act(self, obs_u8, row0, act_out, logp_out, value_out, seed: int, step: int, row_offset: int = 0,
+            step_base=None):
+        """Sample actions; the Philox step is ``step`` (+ the device counter ``step_base``)."""
         hid = self.forward(obs_u8, row0)
         n = obs_u8.shape[0]
         self.h.a2c_head(0, hid, self.params[self.o["head"]:], n, self.A, act_out, logp_out, value_out, None,
                         int(seed), int(step), int(row_offset), None, None, None, 0.0, 0.0, 0.0, None, None, None,
-                        max(1, min(1024, (n + 3) // 4)))
+                        max(1, min(1024, (n + 3) // 4)), step_base)
 
     def value(self, obs_u8, row0, value_out):
         hid = self.forward(obs_u8, row0)
@@ -366,17 +368,17 @@ class DeviceNatureCNN:
             self.grad.mul_(1.0 / comm.world)
         self._reduced = False
         self.h.sumsq(self.grad, self.sq_work, self.norm_sq)
-        self.step_count += 1
+        self.h.counter_add(self.step_t, 1)
         self.h.adam_clip(self.params, self.m, self.v, self.grad, self.shadow,
                          self.norm_sq if max_grad_norm > 0 else None, float(max_grad_norm), float(lr),
-                         float(betas[0]), float(betas[1]), float(eps), self.step_count)
+                         float(betas[0]), float(betas[1]), float(eps), 0, self.step_t)
 
     def state_dict(self):
-        return {"params": self.params, "m": self.m, "v": self.v, "step": torch.tensor([self.step_count])}
+        return {"params": self.params, "m": self.m, "v": self.v, "step": self.step_t.cpu()}
 
     def load_state_dict(self, st):
         self.params.copy_(st["params"])
         self.m.copy_(st["m"])
         self.v.copy_(st["v"])
-        self.step_count = int(st["step"][0])
+        self.step_t.fill_(int(st["step"][0]))
         self.h.to_bf16(self.params, self.shadow)

@@ -14,6 +14,10 @@ One update on each rank (one process per GPU), everything device resident:
      overlapped with the conv backward (world > 1)
   5. global-norm clip + Adam + bf16 shadow weights in one kernel
 
+On one rank the whole update (~80 launches) is captured into a hipGraph after one eager
+warm-up update and replayed: RNG step counters and the Adam step live on the device, so
+replays draw fresh samples and bias corrections without host involvement.
+
 The CPU path (tests, no GPU) runs the same algorithm through the PyTorch oracle model
 and the numpy Pong reference.
 """
@@ -42,6 +46,7 @@ class PixelA2CConfig:
     seed: int = 0
     max_episode_steps: int = 27000 // 4
     phase_timing: bool = False
+    use_graphs: bool = True        # capture the whole update as one hipGraph (world == 1)
 
     def to_dict(self):
         return asdict(self)
@@ -71,13 +76,22 @@ class PixelA2CTrainer:
         self.ep_sum = torch.zeros(4, dtype=torch.float64, device=dev)  # n, sum ret, sum len, sum ret^2
         self.total_steps = 0
         self.updates = 0
-        self.timer = PhaseTimer(dev if cfg.phase_timing and self.on_gpu else None)
+        self.timer = PhaseTimer(dev if cfg.phase_timing and self.on_gpu else None, enabled=cfg.phase_timing)
         if self.on_gpu:
             from ..envs.pong import DevicePong
 
             self.model = DeviceNatureCNN(self.spec, dev, max_batch=N * (T + 1), seed=cfg.seed)
             self.env = DevicePong(N, dev, env_seed, cfg.max_episode_steps)
             self.env.reset(self.obs[0])
+            self.sample_t = torch.zeros(1, dtype=torch.int64, device=dev)  # Philox step of the action sampler
+            self.adv = torch.zeros(T, N, device=dev)
+            self.ret = torch.zeros(T, N, device=dev)
+            from ..ops import hip
+
+            self._stats_part = torch.zeros(int(hip().scan_tm_parts(N)), 3, device=dev)
+            self._stats_out = torch.zeros(3, device=dev)
+            self._graph = None
+            self._warm = False
         else:
             from ..envs.pong import PongRef
 
@@ -92,9 +106,11 @@ class PixelA2CTrainer:
     def _rollout_gpu(self):
         cfg, m, N = self.cfg, self.model, self.cfg.num_envs
         for t in range(cfg.rollout_len):
-            m.act(self.obs[t], t * N, self.act[t], self.logp[t], self.val[t], self.sample_seed,
-                  self.total_steps // N + t)
-            self.env.step(self.act[t], self.obs[t + 1], self.rew[t], self.done[t])
+            m.act(self.obs[t], t * N, self.act[t], self.logp[t], self.val[t], self.sample_seed, t,
+                  step_base=self.sample_t)
+            self.env.step(self.act[t], self.obs[t + 1], self.rew[t], self.done[t], offset=t)
+        self.model.h.counter_add(self.sample_t, cfg.rollout_len)
+        self.env.advance(cfg.rollout_len)
         # bootstrap V(obs[T]) with the pre-update weights; its activations go to the
         # scratch rows [T*N, (T+1)*N) so the stored rollout activations stay intact
         m.value(self.obs[cfg.rollout_len], cfg.rollout_len * N, self.val[cfg.rollout_len])
@@ -106,7 +122,8 @@ class PixelA2CTrainer:
         N, T = cfg.num_envs, cfg.rollout_len
         B = N * T
         with self.timer.phase("Returns"):
-            adv, ret, _ = gae_scan_tm(self.rew, self.done, self.val, cfg.gamma, 1.0)
+            adv, ret, _ = gae_scan_tm(self.rew, self.done, self.val, cfg.gamma, 1.0, self.adv, self.ret,
+                                      self._stats_part, self._stats_out)
         with self.timer.phase("Backward"):
             stats = m.backward(self.obs[:T].reshape(B, 21, 21, 64), self.act.reshape(B), adv.reshape(B),
                                ret.reshape(B), cfg.vf_coef, cfg.ent_coef, comm=self.comm)
@@ -150,25 +167,48 @@ class PixelA2CTrainer:
         return torch.tensor([[pg.item() * B, vf.item() * B, ent.item() * B, float(B)]])
 
     # ------------------------------------------------------------------ API
+    def _gpu_update_body(self):
+        with self.timer.phase("Rollout"):
+            self._rollout_gpu()
+        stats = self._update_gpu()
+        self.obs[0].copy_(self.obs[self.cfg.rollout_len])
+        return stats
+
+    def _graphable(self) -> bool:
+        return self.on_gpu and self.cfg.use_graphs and self.comm.world == 1 and not self.timer.enabled
+
     def train_epoch(self):
         cfg = self.cfg
         N, T = cfg.num_envs, cfg.rollout_len
-        with self.timer.phase("Rollout"):
-            if self.on_gpu:
-                self._rollout_gpu()
+        if self.on_gpu:
+            if self._graphable() and self._graph is not None:
+                self._graph.replay()
+                stats = self._graph_stats
+            elif self._graphable() and self._warm:
+                # capture once (kernel attributes / workspaces were set up by the eager warm-up)
+                g = torch.cuda.CUDAGraph()
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    with torch.cuda.graph(g, stream=s):
+                        self._graph_stats = self._gpu_update_body()
+                torch.cuda.current_stream().wait_stream(s)
+                self._graph = g
+                g.replay()  # the capture itself does not execute
+                stats = self._graph_stats
             else:
+                stats = self._gpu_update_body()
+                self._warm = True
+        else:
+            with self.timer.phase("Rollout"):
                 self._rollout_cpu()
-        if not self.on_gpu:
             with torch.no_grad():
                 _, v, _ = reference_forward(self.spec, self.params, self.obs[T])
             self.val[T] = v
-        if self.on_gpu:
-            stats = self._update_gpu()
-        else:
             stats = self._update_cpu()
+            self.obs[0].copy_(self.obs[T])
         self.total_steps += N * T
         self.updates += 1
-        self.obs[0].copy_(self.obs[T])
         self._last_stats = stats
         return stats
 
@@ -190,6 +230,7 @@ class PixelA2CTrainer:
             st["model"] = {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
             st["env_state"] = self.env.state.cpu()
             st["env_step"] = self.env.step_count
+            st["sample_step"] = int(self.sample_t.item())
         else:
             st["params"] = self.params.detach().cpu()
             st["opt"] = self.opt.state_dict()
@@ -203,6 +244,7 @@ class PixelA2CTrainer:
             self.model.load_state_dict({k: v.to(self.device) for k, v in st["model"].items()})
             self.env.state.copy_(st["env_state"].to(self.device))
             self.env.step_count = int(st["env_step"])
+            self.sample_t.fill_(int(st.get("sample_step", self.updates * self.cfg.rollout_len)))
         else:
             with torch.no_grad():
                 self.params.copy_(st["params"])

@@ -371,3 +371,20 @@ def test_cnn_dp_overlapped_allreduce_matches_mean_gradient(cuda):
         p.join(timeout=60)
     for rank, err in res:
         assert isinstance(err, float) and err < 1e-5, (rank, err)
+
+
+def test_pixel_trainer_graph_replay_matches_eager(cuda):
+    """The captured update (device RNG / Adam counters) reproduces the eager updates exactly."""
+    from relayrl_prototype_amd.runtime.pixel_trainer import PixelA2CConfig, PixelA2CTrainer
+
+    cfg = dict(num_envs=32, rollout_len=4, seed=9)
+    a = PixelA2CTrainer(PixelA2CConfig(use_graphs=True, **cfg), device=cuda)
+    b = PixelA2CTrainer(PixelA2CConfig(use_graphs=False, **cfg), device=cuda)
+    for _ in range(4):  # eager warm-up, capture+replay, 2 replays
+        a.train_epoch()
+        b.train_epoch()
+    torch.cuda.synchronize()
+    assert a._graph is not None and b._graph is None
+    assert torch.equal(a.act, b.act) and torch.equal(a.obs, b.obs)
+    torch.testing.assert_close(a.model.params, b.model.params, rtol=0, atol=0)
+    assert int(a.model.step_t.item()) == 4 and a.env.step_count == b.env.step_count
