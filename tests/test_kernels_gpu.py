@@ -93,6 +93,9 @@ GRAD_CASES = [
     (GradHead.PPO_CAT, 4, 128, 2, 2000),
     (GradHead.PPO_GAUSS, 17, 128, 6, 1500),
     (GradHead.PG_GAUSS, 5, 64, 3, 129),
+    (GradHead.PG_GAUSS, 3, 128, 2, 700),
+    (GradHead.VALUE_MSE, 4, 128, 1, 40000),   # several 64-row slabs per workgroup
+    (GradHead.PG_CAT, 4, 128, 2, 40000),
 ]
 
 
