@@ -95,6 +95,8 @@ GRAD_CASES = [
     (GradHead.PG_GAUSS, 5, 64, 3, 129),
     (GradHead.PG_GAUSS, 3, 128, 2, 700),
     (GradHead.VALUE_MSE, 4, 128, 1, 40000),   # several 64-row slabs per workgroup
+    (GradHead.VALUE_MSE, 2, 128, 1, 777),     # D < 4, ragged tail
+    (GradHead.VALUE_MSE, 3, 128, 1, 16),
     (GradHead.PG_CAT, 4, 128, 2, 40000),
 ]
 
