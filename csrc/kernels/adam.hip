@@ -29,6 +29,20 @@ struct AdamArgs {
 constexpr int kAdamCols = 64;
 constexpr int kAdamGroups = 16;
 
+// Partial sum of column p over the slabs k = grp, grp + 16, ... (one of 16 groups).
+RRL_DEV float slab_group_sum(const float* __restrict__ slab, int nslab, int P, int p, int grp) {
+  const float* s = slab + p;
+  float g = 0.f;
+  int k = grp;
+  for (; k + 3 * kAdamGroups < nslab; k += 4 * kAdamGroups) {
+    const float g0 = s[(size_t)k * P], g1 = s[(size_t)(k + kAdamGroups) * P];
+    const float g2 = s[(size_t)(k + 2 * kAdamGroups) * P], g3 = s[(size_t)(k + 3 * kAdamGroups) * P];
+    g += (g0 + g1) + (g2 + g3);
+  }
+  for (; k < nslab; k += kAdamGroups) g += s[(size_t)k * P];
+  return g;
+}
+
 __global__ __launch_bounds__(1024) void adam_kernel(AdamArgs a) {
   __shared__ float part[kAdamGroups][kAdamCols];
   const int t = *a.step + 1;
@@ -40,14 +54,7 @@ __global__ __launch_bounds__(1024) void adam_kernel(AdamArgs a) {
     if (a.grad) {
       if (grp == 0) g = a.grad[p];
     } else {
-      const float* s = a.slab + p;
-      int k = grp;
-      for (; k + 3 * kAdamGroups < a.nslab; k += 4 * kAdamGroups) {
-        const float g0 = s[(size_t)k * a.P], g1 = s[(size_t)(k + kAdamGroups) * a.P];
-        const float g2 = s[(size_t)(k + 2 * kAdamGroups) * a.P], g3 = s[(size_t)(k + 3 * kAdamGroups) * a.P];
-        g += (g0 + g1) + (g2 + g3);
-      }
-      for (; k < a.nslab; k += kAdamGroups) g += s[(size_t)k * a.P];
+      g = slab_group_sum(a.slab, a.nslab, a.P, p, grp);
     }
   }
   part[grp][col] = g;
@@ -81,24 +88,28 @@ __global__ __launch_bounds__(1024) void adam_kernel(AdamArgs a) {
   }
 }
 
-// Plain slab reduction (used before a data-parallel all-reduce).
-__global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* slab, int nslab, int P, float scale,
-                                                           float* out) {
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
-    float g = 0.f;
-    for (int k = 0; k < nslab; ++k) g += slab[(size_t)k * P + p];
-    out[p] = g * scale;
+// Plain slab reduction (used before a data-parallel all-reduce): the same 64-column x
+// 16-group layout as the Adam kernel (the per-thread serial loop over ~256 slabs it
+// replaces was latency-bound, and runs once per optimiser step when world > 1).
+__global__ __launch_bounds__(1024) void reduce_slabs_kernel(const float* slab, int nslab, int P, float scale,
+                                                            float* out) {
+  __shared__ float part[kAdamGroups][kAdamCols];
+  const int col = threadIdx.x & (kAdamCols - 1);
+  const int grp = threadIdx.x / kAdamCols;
+  const int p = blockIdx.x * kAdamCols + col;
+  part[grp][col] = p < P ? slab_group_sum(slab, nslab, P, p, grp) : 0.f;
+  __syncthreads();
+  if (grp == 0 && p < P) {
+    float gs = 0.f;
+#pragma unroll
+    for (int q = 0; q < kAdamGroups; ++q) gs += part[q][col];
+    out[p] = gs * scale;
   }
 }
 
 }  // namespace rrl
 
 using namespace rrl;
-
-static int adam_grid(int P) {
-  int g = (P + 255) / 256;
-  return g > 1024 ? 1024 : (g < 1 ? 1 : g);
-}
 
 extern "C" int rrl_adam(float* param, float* m, float* v, const float* grad, const float* slab, int nslab,
                         float* grad_out, int* step, unsigned* ticket, int P, float lr, float beta1,
@@ -111,7 +122,8 @@ extern "C" int rrl_adam(float* param, float* m, float* v, const float* grad, con
 }
 
 extern "C" int rrl_reduce_slabs(const float* slab, int nslab, int P, float scale, float* out, void* stream) {
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(adam_grid(P)), dim3(256), 0, (hipStream_t)stream, slab, nslab,
-                     P, scale, out);
+  const int grid = (P + kAdamCols - 1) / kAdamCols;
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(grid < 1 ? 1 : grid), dim3(kAdamCols * kAdamGroups), 0,
+                     (hipStream_t)stream, slab, nslab, P, scale, out);
   return (int)hipGetLastError();
 }

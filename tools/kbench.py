@@ -16,6 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 from relayrl_prototype_amd.ops import FwdMode, GradHead, MLPSpec, hip, mlp_forward, mlp_grad, adam_step, gae_scan_tm
+from relayrl_prototype_amd.ops import reduce_slabs
 
 
 def timeit(fn, iters, warmup=3):
@@ -33,7 +34,7 @@ def timeit(fn, iters, warmup=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["grad", "pgrad", "fwd", "rollout", "adam", "scan", "all"])
+    ap.add_argument("which", choices=["grad", "pgrad", "fwd", "rollout", "adam", "rslab", "scan", "all"])
     ap.add_argument("--B", type=int, default=2097152)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--H", type=int, default=128)
@@ -78,6 +79,11 @@ def main():
         tk = torch.zeros(1, dtype=torch.int32, device=dev)
         p2 = pv.clone()
         res["adam_us"] = timeit(lambda: adam_step(p2, m, v, step, tk, 1e-3, slab=slab), a.iters)
+    if a.which in ("rslab", "all"):
+        ns = hip().mlp_grad_slabs(B)
+        slab = torch.randn(ns, pv.numel(), device=dev)
+        out = torch.empty(pv.numel(), device=dev)
+        res["reduce_slabs_us"] = timeit(lambda: reduce_slabs(slab, 1.0, out=out), a.iters)
     if a.which in ("scan", "all"):
         T, N = 64, B // 64
         rew = torch.rand(T, N, device=dev)
