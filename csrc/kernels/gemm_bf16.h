@@ -15,9 +15,9 @@
 // read.  Implicit im2col lives in the loader (ConvLoader), so convolutions never write
 // a column buffer in the forward or weight-gradient pass.
 //
-// Block = 256 threads (4 waves), tile BM x BN x 64, double-buffered LDS with register
-// staging of the next tile; split-K over gridDim.z for reductions that dwarf the output
-// (weight gradients over batch x spatial).
+// Block = 256 threads (4 waves), tile BM x BN x 64, one LDS buffer with register staging
+// of the next tile (kGemmStages); split-K over gridDim.z for reductions that dwarf the
+// output (weight gradients over batch x spatial).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -169,6 +169,15 @@ struct U8ConvLoader {
 // ----------------------------------------------------------------------------- kernel
 constexpr int kGemmBK = 64;
 constexpr int kGemmPad = 8;  // bf16 elements of row padding (16 B)
+// LDS buffers per workgroup.  The next k-tile is always staged in registers while the
+// current one is consumed, so one LDS buffer (two barriers per k-tile) suffices, and it
+// halves the LDS footprint: 3 -> 6 resident 128x32 workgroups per CU and 2 -> 4 for
+// 128x64, which hides the global-load latency of the short-K conv GEMMs better
+// (PongSynth A2C, 2048 envs: 2.66 -> 3.21 M env-steps/s; docs/PERF_NOTES.md).
+#ifndef RRL_GEMM_STAGES
+#define RRL_GEMM_STAGES 1
+#endif
+constexpr int kGemmStages = RRL_GEMM_STAGES;
 
 template <int BM, int BN, bool A_TR, bool B_TR>
 struct GemmShape {
@@ -179,7 +188,7 @@ struct GemmShape {
   static constexpr int A_LD = A_COLS + kGemmPad, B_LD = B_COLS + kGemmPad;
   static constexpr int A_ELEMS = A_ROWS * A_LD, B_ELEMS = B_ROWS * B_LD;
   static constexpr int STAGE = A_ELEMS + B_ELEMS;                 // bf16 elements per stage
-  static constexpr int LDS_BYTES = 2 * STAGE * 2;                 // double buffered
+  static constexpr int LDS_BYTES = kGemmStages * STAGE * 2;
   static constexpr int A_CHUNKS = A_ROWS * A_COLS / 8, B_CHUNKS = B_ROWS * B_COLS / 8;
   static constexpr int A_PER_T = (A_CHUNKS + 255) / 256, B_PER_T = (B_CHUNKS + 255) / 256;
   // wave grid: 2x2 when both dims >= 32 per wave, else 4x1
@@ -313,9 +322,15 @@ gemm_bf16_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_per_split) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (more) {
-      lstore(buf ^ 1);
-      __syncthreads();
-      buf ^= 1;
+      if (kGemmStages == 1) {
+        __syncthreads();  // every wave is done reading the tile
+        lstore(0);
+        __syncthreads();
+      } else {
+        lstore(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+      }
     }
   }
 #pragma unroll
