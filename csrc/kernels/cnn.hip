@@ -611,6 +611,126 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(const uint16_t* __restr
   }
 }
 
+
+// ----------------------------------------------------------------------------- conv1 wgrad
+// dW1[cout][kh][kw][c] = sum over images and 20x20 output pixels p of
+//   dY[p][cout] * X[p + (kh, kw)][c]
+// for the space-to-depth first layer (21x21x64 uint8 frames, 2x2 stride-1 taps, 32
+// outputs).  The implicit-GEMM path re-reads and re-converts every input byte once per
+// tap and dY once per 128-row tile (~1.7 GB for a 2048-env update).  Here a workgroup
+// streams whole images: the frame (converted to bf16 once) and dY go into LDS, and wave
+// w computes tap (kh, kw) = (w >> 1, w & 1) as a 32 x 64 GEMM over the image's 400 pixels
+// whose B operand is the SHIFTED frame, read by row offset from the same LDS image
+// (~550 MB of traffic, one pass).  The next image is prefetched into registers.
+//
+// MFMA k-order: lane group g of a 32-pixel chunk takes pixels 4g..4g+3 and 16+4g..16+4g+3
+// (a 4-pixel run never crosses an output row, so its frame rows are consecutive); with
+// rows of 80 bf16 the 8 rows one transposed read touches land in distinct bank octets.
+constexpr int kW1Ld = 80;
+constexpr int kW1XRows = 448;  // 441 frame pixels (+ pad)
+constexpr int kW1YRows = 416;  // 400 output pixels + 16 zero rows (13 chunks of 32)
+constexpr int kW1Lds = (kW1XRows + kW1YRows) * kW1Ld * 2;
+
+__device__ __forceinline__ bf16x8_t tr8(const uint16_t* a0, const uint16_t* a1) {
+  typedef __attribute__((address_space(3))) s16x4_t lds_v4;
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a1));
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+__global__ __launch_bounds__(256, 1) void conv1_wgrad_s2d_kernel(const uint8_t* __restrict__ x,
+                                                                 const uint16_t* __restrict__ dy,
+                                                                 float* __restrict__ part, int N) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Xi = smem;                   // [kW1XRows][kW1Ld] frame, bf16 integers 0..255
+  uint16_t* Yi = smem + kW1XRows * kW1Ld;  // [kW1YRows][kW1Ld] dY
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int kh = w >> 1, kw = w & 1;
+  const int n0 = (int)(((long long)N * blockIdx.x) / gridDim.x);
+  const int n1 = (int)(((long long)N * (blockIdx.x + 1)) / gridDim.x);
+  for (int q = tid; q < 16 * (kW1Ld / 8); q += 256)
+    *reinterpret_cast<uint4*>(Yi + (400 + q / (kW1Ld / 8)) * kW1Ld + 8 * (q % (kW1Ld / 8))) = make_uint4(0, 0, 0, 0);
+
+  f32x4_t acc[2][4];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int XC = 441 * 4, YC = 400 * 4;  // 16-byte chunks per image
+  constexpr int XPT = (XC + 255) / 256, YPT = (YC + 255) / 256;
+  uint4 rx[XPT], ry[YPT];
+  auto gload = [&](int n) {
+    const uint4* xs = reinterpret_cast<const uint4*>(x + (size_t)n * 441 * 64);
+    const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 400 * 32);
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int q = tid + 256 * i;
+      rx[i] = q < XC ? xs[q] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int q = tid + 256 * i;
+      ry[i] = q < YC ? ys[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int q = tid + 256 * i;
+      if (q < XC) {
+        uint16_t* d = Xi + (q >> 2) * kW1Ld + (q & 3) * 16;
+        *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(rx[i].x, rx[i].y));
+        *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(rx[i].z, rx[i].w));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < YPT; ++i) {
+      const int q = tid + 256 * i;
+      if (q < YC) *reinterpret_cast<uint4*>(Yi + (q >> 2) * kW1Ld + (q & 3) * 8) = ry[i];
+    }
+  };
+
+  const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  if (n0 < n1) gload(n0);
+  for (int n = n0; n < n1; ++n) {
+    __syncthreads();  // the previous image's fragment reads are done
+    lstore();
+    if (n + 1 < n1) gload(n + 1);
+    __syncthreads();
+#pragma unroll 1
+    for (int kc = 0; kc < kW1YRows / 32; ++kc) {
+      const int pa = 32 * kc + 4 * g, pb = pa + 16;
+      // frame row of output pixel p under this wave's tap (0 past the last pixel: dY is 0 there)
+      const int ra = (pa < 400 ? (pa / 20 + kh) * 21 + pa % 20 + kw : 0) + qq;
+      const int rb = (pb < 400 ? (pb / 20 + kh) * 21 + pb % 20 + kw : 0) + qq;
+      bf16x8_t af[2], bfr[4];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        af[mt] = tr8(Yi + (pa + qq) * kW1Ld + 16 * mt + 4 * pp, Yi + (pb + qq) * kW1Ld + 16 * mt + 4 * pp);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        bfr[nt] = tr8(Xi + ra * kW1Ld + 16 * nt + 4 * pp, Xi + rb * kW1Ld + 16 * nt + 4 * pp);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
+    }
+  }
+  // part[split][cout][kh][kw][c], raw-byte products scaled by 1/255
+  float* o = part + (size_t)blockIdx.x * 32 * 256 + kh * 128 + kw * 64;
+  const int j = lane & 15;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[(16 * mt + 4 * g + r) * 256 + 16 * nt + j] = acc[mt][nt][r] * kU8Scale;
+}
+
 }  // namespace rrl
 
 using namespace rrl;
@@ -708,6 +828,19 @@ int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, int
   hipStream_t st = (hipStream_t)stream_;
   ConvGeom g{N, H, W, C, KH, KW, S, (H - KH) / S + 1, (W - KW) / S + 1, Cout};
   const int M = g.M(), K = g.K();
+  if (x_u8 && H == 21 && W == 21 && C == 64 && KH == 2 && KW == 2 && S == 1 && Cout == 32) {
+    // PongSynth's space-to-depth first layer: one streaming pass (conv1_wgrad_s2d_kernel);
+    // same number of partial slabs as the GEMM path would use
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)conv1_wgrad_s2d_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kW1Lds);
+      attr = true;
+    }
+    const int grid = rrl_gemm_splits_impl(M, splits);
+    hipLaunchKernelGGL(conv1_wgrad_s2d_kernel, dim3(grid), dim3(256), kW1Lds, st, (const uint8_t*)x, dy, part, N);
+    return (int)hipGetLastError();
+  }
   RowLoader ly{dy, M, Cout};
   PartialStoreT epi{part, K, Cout, x_u8 ? kU8Scale : 1.0f};
   return with_im2col(g, x, x_u8 != 0, [&](auto lx) -> int {

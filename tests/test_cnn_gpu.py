@@ -118,11 +118,13 @@ def test_conv_dgrad_col2im_and_wgrad(cuda, li, N):
     assert relerr(db, dy.reshape(-1, L.cout).sum(0)) < 1e-4
 
 
-def test_conv1_wgrad_from_s2d_frames(cuda):
+@pytest.mark.parametrize("N,splits", [(9, 16), (300, 64), (5, 256)])
+def test_conv1_wgrad_from_s2d_frames(cuda, N, splits):
+    """Streaming conv1 weight-gradient kernel (one pass over frames + dY) vs autograd;
+    (5, 256): more partial slabs than images, the idle workgroups must write zeros."""
     from relayrl_prototype_amd.ops import hip
 
     h = hip()
-    N = 9
     g = torch.Generator().manual_seed(12)
     x = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g)
     dy = _bf(torch.randn(N, 20, 20, 32, generator=g))
@@ -130,9 +132,9 @@ def test_conv1_wgrad_from_s2d_frames(cuda):
     F.conv2d(_bf(obs_to_nchw(x)), wt, stride=4).backward(dy.permute(0, 3, 1, 2))
     dw_ref = conv1_khkwc_to_s2d(wt.grad.permute(0, 2, 3, 1)).reshape(-1)
     M = N * 400
-    s = int(h.gemm_splits(M, 16))
-    part = torch.empty(s * 32 * 256, device=cuda)
-    h.conv_wgrad(dy.to(cuda).bfloat16().reshape(-1), x.to(cuda), part, 16, N, 21, 21, 64, 2, 2, 1, 32)
+    s = int(h.gemm_splits(M, splits))
+    part = torch.full((s * 32 * 256,), float("nan"), device=cuda)
+    h.conv_wgrad(dy.to(cuda).bfloat16().reshape(-1), x.to(cuda), part, splits, N, 21, 21, 64, 2, 2, 1, 32)
     dw = torch.empty(32 * 256, device=cuda)
     h.sum_splits(part, s, 32 * 256, dw)
     assert relerr(dw, dw_ref) < 1e-2
