@@ -81,6 +81,7 @@ void conv_fwd(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& y
   const bool u8 = x.scalar_type() == at::kByte;
   check(x, "x", u8 ? at::kByte : at::kBFloat16, N * H * W * C);
   TORCH_CHECK(u8 ? ((C == 4 && KW % 2 == 0) || C % 8 == 0) : (C % 8 == 0), "conv_fwd: unsupported channel layout");
+  TORCH_CHECK(Cout % 8 == 0, "conv_fwd: Cout must be a multiple of 8 (16-byte epilogue stores)");
   check(w, "w", at::kBFloat16, Cout * KH * KW * C);
   check(b, "b", at::kFloat, Cout);
   check(y, "y", at::kBFloat16, N * g.OH() * g.OW() * Cout);

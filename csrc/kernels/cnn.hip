@@ -30,6 +30,16 @@ struct BiasReluStore {  // bf16 [M][N] = act(scale * acc + b[n])
   int M, N;
   bool relu;
   float scale;
+  static constexpr bool kVec8 = true;
+  __device__ __forceinline__ void store8(int m, int n, const float (&v)[8], int) const {
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float t = scale * v[e] + (b ? b[n + e] : 0.f);
+      o[e] = relu ? fmaxf(t, 0.f) : t;
+    }
+    *reinterpret_cast<uint4*>(y + (size_t)m * N + n) = pack_bf16x8(o);
+  }
   __device__ __forceinline__ void operator()(int m, int n, f32x4_t acc, int) const {
     if (n >= N) return;
     const float bb = b ? b[n] : 0.f;
@@ -48,6 +58,15 @@ struct MaskStore {  // bf16 [M][N] = acc * (mask[m][n] > 0)   (mask == null: pla
   uint16_t* y;
   const uint16_t* mask;
   int M, N;
+  static constexpr bool kVec8 = true;
+  __device__ __forceinline__ void store8(int m, int n, const float (&v)[8], int) const {
+    const size_t i = (size_t)m * N + n;
+    float o[8];
+    const uint4 mk = mask ? *reinterpret_cast<const uint4*>(mask + i) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (!mask || bf16x8_at(mk, e) > 0.f) ? v[e] : 0.f;
+    *reinterpret_cast<uint4*>(y + i) = pack_bf16x8(o);
+  }
   __device__ __forceinline__ void operator()(int m, int n, f32x4_t acc, int) const {
     if (n >= N) return;
 #pragma unroll
@@ -65,6 +84,12 @@ struct MaskStore {  // bf16 [M][N] = acc * (mask[m][n] > 0)   (mask == null: pla
 struct PartialStore {  // fp32 [split][M][N]
   float* out;
   int M, N;
+  static constexpr bool kVec8 = true;
+  __device__ __forceinline__ void store8(int m, int n, const float (&v)[8], int z) const {
+    float* o = out + (size_t)z * M * N + (size_t)m * N + n;
+    *reinterpret_cast<f32x4_t*>(o) = f32x4_t{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4_t*>(o + 4) = f32x4_t{v[4], v[5], v[6], v[7]};
+  }
   __device__ __forceinline__ void operator()(int m, int n, f32x4_t acc, int z) const {
     if (n >= N) return;
     float* o = out + (size_t)z * M * N;
@@ -187,6 +212,18 @@ struct DgradStore {
   uint16_t* dx;
   const uint16_t* xact;
   int M, ph, pw, S;
+  static constexpr bool kVec8 = (C % 8 == 0);
+  __device__ __forceinline__ void store8(int m, int c, const float (&v)[8], int) const {
+    const unsigned um = (unsigned)m;
+    const unsigned n = um / (G::HA * G::WB), p = um - n * (G::HA * G::WB);
+    const unsigned a = p / G::WB, b = p - a * G::WB;
+    const size_t idx = (((size_t)n * H + ph + S * a) * W + pw + S * b) * C + c;
+    const uint4 xa = *reinterpret_cast<const uint4*>(xact + idx);
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = bf16x8_at(xa, e) > 0.f ? v[e] : 0.f;
+    *reinterpret_cast<uint4*>(dx + idx) = pack_bf16x8(o);
+  }
   __device__ __forceinline__ void operator()(int m, int c, f32x4_t acc, int) const {
     if (c >= C) return;
 #pragma unroll

@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace rrl {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -35,6 +37,15 @@ __device__ __forceinline__ uint16_t f2bf(float f) {  // round-to-nearest-even
   return (uint16_t)(u >> 16);
 }
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+__device__ __forceinline__ uint4 pack_bf16x8(const float (&v)[8]) {
+  return make_uint4(f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16),
+                    f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16), f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16));
+}
+// element e (0..7) of 8 bf16 packed in a uint4, as float
+__device__ __forceinline__ float bf16x8_at(uint4 u, int e) {
+  const uint32_t w = e < 2 ? u.x : (e < 4 ? u.y : (e < 6 ? u.z : u.w));
+  return __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
+}
 
 // uint8 inputs are fed to the MFMA as exact integers 0..255 in bf16 (8 significant bits
 // fit the bf16 mantissa, so the conversion is a byte->f32 convert plus taking the high
@@ -188,7 +199,9 @@ struct GemmShape {
   static constexpr int A_LD = A_COLS + kGemmPad, B_LD = B_COLS + kGemmPad;
   static constexpr int A_ELEMS = A_ROWS * A_LD, B_ELEMS = B_ROWS * B_LD;
   static constexpr int STAGE = A_ELEMS + B_ELEMS;                 // bf16 elements per stage
-  static constexpr int LDS_BYTES = kGemmStages * STAGE * 2;
+  static constexpr int OUT_LD = BN + 4;                           // fp32 output tile row (vec8 epilogues)
+  static constexpr int OUT_BYTES = BM * OUT_LD * 4;
+  static constexpr int LDS_BYTES = (kGemmStages * STAGE * 2 > OUT_BYTES) ? kGemmStages * STAGE * 2 : OUT_BYTES;
   static constexpr int A_CHUNKS = A_ROWS * A_COLS / 8, B_CHUNKS = B_ROWS * B_COLS / 8;
   static constexpr int A_PER_T = (A_CHUNKS + 255) / 256, B_PER_T = (B_CHUNKS + 255) / 256;
   // wave grid: 2x2 when both dims >= 32 per wave, else 4x1
@@ -215,6 +228,16 @@ __device__ __forceinline__ bf16x8_t frag_tr(const uint16_t* img, int ld, int k0,
   s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8_t, v);
 }
+
+// Epilogues that define `static constexpr bool kVec8 = true` and
+//   store8(m, n, const float (&v)[8], split)      (columns n .. n+7 of row m, n % 8 == 0)
+// get the output tile through LDS: the MFMA C layout (4 rows x 1 column per lane) is
+// re-read as 8 consecutive columns of one row per thread, so NHWC bf16 outputs (and the
+// masks / skip inputs they read) move as 16-byte accesses instead of 2-byte ones.
+template <class Epi, class = void>
+struct EpiVec8 : std::false_type {};
+template <class Epi>
+struct EpiVec8<Epi, std::void_t<decltype(Epi::kVec8)>> : std::integral_constant<bool, Epi::kVec8> {};
 
 // Loaders are called with global IMAGE coordinates (row, contiguous col):
 //   A !TR: (m, k)   A TR: (k, m)   B !TR: (n, k)   B TR: (k, n)
@@ -333,14 +356,34 @@ gemm_bf16_kernel(LA la, LB lb, Epi epi, int M, int N, int K, int k_per_split) {
       }
     }
   }
+  if constexpr (EpiVec8<Epi>::value) {
+    float* T = reinterpret_cast<float*>(smem);  // [BM][OUT_LD] fp32 tile
+    __syncthreads();                            // every wave is done reading the operand tiles
 #pragma unroll
-  for (int i = 0; i < S::TM; ++i)
+    for (int i = 0; i < S::TM; ++i)
 #pragma unroll
-    for (int j = 0; j < S::TN; ++j) {
-      const int m = m0 + wm0 + 16 * i + 4 * g;
-      const int n = n0 + wn0 + 16 * j + li;
-      epi(m, n, acc[i][j], blockIdx.z);
+      for (int j = 0; j < S::TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) T[(wm0 + 16 * i + 4 * g + r) * S::OUT_LD + wn0 + 16 * j + li] = acc[i][j][r];
+    __syncthreads();
+    for (int q = tid; q < BM * (BN / 8); q += 256) {
+      const int row = q / (BN / 8), c = (q % (BN / 8)) * 8;
+      if (m0 + row >= M || n0 + c >= N) continue;
+      const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(T + row * S::OUT_LD + c);
+      const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(T + row * S::OUT_LD + c + 4);
+      const float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      epi.store8(m0 + row, n0 + c, v, blockIdx.z);
     }
+  } else {
+#pragma unroll
+    for (int i = 0; i < S::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < S::TN; ++j) {
+        const int m = m0 + wm0 + 16 * i + 4 * g;
+        const int n = n0 + wn0 + 16 * j + li;
+        epi(m, n, acc[i][j], blockIdx.z);
+      }
+  }
 }
 
 }  // namespace rrl
