@@ -768,6 +768,101 @@ __global__ __launch_bounds__(256, 1) void conv1_wgrad_s2d_kernel(const uint8_t* 
       for (int r = 0; r < 4; ++r) o[(16 * mt + 4 * g + r) * 256 + 16 * nt + j] = acc[mt][nt][r] * kU8Scale;
 }
 
+
+// ----------------------------------------------------------------------------- conv1 forward
+// y[n][p][co] = act(scale * sum_{kh,kw,c} X[n][p + (kh, kw)][c] W[co][kh][kw][c] + b[co]) for the
+// space-to-depth first layer (21x21x64 uint8 frame -> 20x20x32).  Persistent workgroups
+// walk the frames with the next frame prefetched into registers; each frame is converted
+// to bf16 ONCE into LDS (the implicit-GEMM loader converted every byte once per tap),
+// each tap reads its shifted rows from that image, W stays in registers, and the 400 x 32
+// output goes back through LDS as one contiguous 25.6 KB block.
+constexpr int kF1Lds = kW1XRows * kW1Ld * 2;
+
+__global__ __launch_bounds__(256, 2) void conv1_fwd_s2d_kernel(const uint8_t* __restrict__ x,
+                                                               const uint16_t* __restrict__ w,
+                                                               const float* __restrict__ b, uint16_t* __restrict__ y,
+                                                               int N, float scale, int relu) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Xi = smem;  // [441][kW1Ld] frame (bf16 integers 0..255); later [400][40] output
+  uint16_t* O = smem;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  // weights -> registers: B fragment (k-step ks, cout tile nt) = W[16nt + i][32ks + 8g .. +7]
+  bf16x8_t wf[8][2];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) wf[ks][nt] = *reinterpret_cast<const bf16x8_t*>(w + (16 * nt + i) * 256 + 32 * ks + 8 * g);
+  const float b0 = b[i], b1 = b[16 + i];
+  constexpr int XC = 441 * 4, XPT = (XC + 255) / 256;
+  uint4 rx[XPT];
+  auto gload = [&](size_t n) {
+    const uint4* xs = reinterpret_cast<const uint4*>(x + n * 441 * 64);
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int q = tid + 256 * k;
+      rx[k] = q < XC ? xs[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  // persistent over frames; the next frame is prefetched into registers
+  if ((int)blockIdx.x < N) gload(blockIdx.x);
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    __syncthreads();  // the previous frame's output tile has been copied out
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int q = tid + 256 * k;
+      if (q < XC) {
+        uint16_t* d = Xi + (q >> 2) * kW1Ld + (q & 3) * 16;
+        *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(rx[k].x, rx[k].y));
+        *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(rx[k].z, rx[k].w));
+      }
+    }
+    if (n + (int)gridDim.x < N) gload((size_t)n + gridDim.x);
+    __syncthreads();
+    // 25 pixel tiles of 16; wave w takes tiles w, w + 4, ...
+    constexpr int MT = 7;
+    f32x4_t acc[MT][2];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      acc[t][0] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      acc[t][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int mt = wave + 4 * t;
+      if (mt < 25) {
+        const int p = 16 * mt + i;
+        const int r0 = (p / 20) * 21 + p % 20;  // frame row of tap (0, 0)
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          const int tap = ks >> 1;  // (kh, kw) = (tap >> 1, tap & 1); 2 k-steps of 32 channels each
+          const int row = r0 + (tap >> 1) * 21 + (tap & 1);
+          const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(Xi + row * kW1Ld + 32 * (ks & 1) + 8 * g);
+          acc[t][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[ks][0], acc[t][0], 0, 0, 0);
+          acc[t][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[ks][1], acc[t][1], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // the frame image is dead: reuse the LDS for the output tile [400][40]
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      const int mt = wave + 4 * t;
+      if (mt < 25) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = 16 * mt + 4 * g + r;
+          float v0 = scale * acc[t][0][r] + b0, v1 = scale * acc[t][1][r] + b1;
+          if (relu) {
+            v0 = fmaxf(v0, 0.f);
+            v1 = fmaxf(v1, 0.f);
+          }
+          O[p * 40 + i] = f2bf(v0);
+          O[p * 40 + 16 + i] = f2bf(v1);
+        }
+      }
+    }
+    __syncthreads();
+    uint4* yd = reinterpret_cast<uint4*>(y + (size_t)n * 400 * 32);
+    for (int q = tid; q < 400 * 4; q += 256) yd[q] = *reinterpret_cast<const uint4*>(O + (q >> 2) * 40 + (q & 3) * 8);
+  }
+}
 }  // namespace rrl
 
 using namespace rrl;
@@ -798,6 +893,20 @@ int rrl_conv_fwd(const void* x, int x_u8, const uint16_t* w, const float* b, uin
   hipStream_t st = (hipStream_t)stream_;
   ConvGeom g{N, H, W, C, KH, KW, S, (H - KH) / S + 1, (W - KW) / S + 1, Cout};
   const int M = g.M(), K = g.K();
+  if (x_u8 && H == 21 && W == 21 && C == 64 && KH == 2 && KW == 2 && S == 1 && Cout == 32) {
+    // PongSynth's space-to-depth first layer: one workgroup per frame (conv1_fwd_s2d_kernel)
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)conv1_fwd_s2d_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kF1Lds);
+      attr = true;
+    }
+    if (N < 1) return 0;
+    const int grid = N < 512 ? N : 512;  // 2 resident workgroups per CU
+    hipLaunchKernelGGL(conv1_fwd_s2d_kernel, dim3(grid), dim3(256), kF1Lds, st, (const uint8_t*)x, w, b, y, N,
+                       kU8Scale, relu);
+    return (int)hipGetLastError();
+  }
   RowLoader lw{w, Cout, K};
   BiasReluStore epi{y, b, M, Cout, relu != 0, x_u8 ? kU8Scale : 1.0f};
   const int tiles = ((M + 127) / 128) * ((Cout + 63) / 64);
