@@ -358,12 +358,26 @@ __global__ void __launch_bounds__(256) sum_splits_kernel(const float* __restrict
   }
 }
 
-__global__ void sum_splits_scalar_kernel(const float* __restrict__ part, int splits, size_t n,
-                                         float* __restrict__ out) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    float t = 0.f;
-    for (int z = 0; z < splits; ++z) t += part[(size_t)z * n + i];
-    out[i] = t;
+// Unaligned / odd-length split sums (e.g. the A2C head, n = 512 (A+1) + A+1): a block
+// owns 64 consecutive columns and splits the slab sum over 16 row groups (coalesced 256-B
+// rows per wave), folded through LDS -- the one-thread-per-column serial loop it replaces
+// was latency-bound (61 us for 256 slabs of 3.6 K floats).
+__global__ void __launch_bounds__(1024) sum_splits_scalar_kernel(const float* __restrict__ part, int splits, size_t n,
+                                                                 float* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int col = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const size_t i = (size_t)blockIdx.x * 64 + col;
+  float t = 0.f;
+  if (i < n) {
+    for (int z = grp; z < splits; z += 16) t += part[(size_t)z * n + i];
+  }
+  red[grp][col] = t;
+  __syncthreads();
+  if (grp == 0 && i < n) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += red[q][col];
+    out[i] = s;
   }
 }
 
@@ -1001,7 +1015,7 @@ int rrl_gemm_splits(int R, int splits) { return rrl_gemm_splits_impl(R, splits);
 int rrl_sum_splits(const float* part, int splits, long long n, float* out, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   if (((uintptr_t)part & 15) || ((uintptr_t)out & 15) || (n & 3)) {  // float4 path needs aligned rows
-    hipLaunchKernelGGL(sum_splits_scalar_kernel, dim3(grid_for((size_t)n)), dim3(256), 0, st, part, splits,
+    hipLaunchKernelGGL(sum_splits_scalar_kernel, dim3((unsigned)((n + 63) / 64)), dim3(1024), 0, st, part, splits,
                        (size_t)n, out);
     return (int)hipGetLastError();
   }

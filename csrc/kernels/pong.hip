@@ -131,44 +131,37 @@ __global__ void pong_step_kernel(float* __restrict__ state, const int32_t* __res
 // [N][21][21][64]), so the first 8x8/4 conv becomes a 2x2/1 conv over 64 contiguous
 // channels and its im2col reads 8-byte runs; a 16-byte chunk of 4 pixels x 4 frames of
 // one row lands contiguously at (a, b, dy).
+// One thread per 16-byte output chunk (4 pixels x 4 frames of one row), chunks in memory
+// order, so every wave stores 1 KB contiguously.  Chunk q of an env's [21][21][64] s2d
+// frame: a = q / 84 (block row), c = (q % 84) / 4 (block column), dy = q % 4 (row in the
+// 4x4 block) -> image row y = 4a + dy, pixels x = 4c .. 4c+3.
 __global__ void pong_render_kernel(const float* __restrict__ state, uint8_t* __restrict__ obs, int N) {
+  constexpr int kChunks = kPongHW * kPongHW * 4 / 16;  // 1764 per env
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (t >= (size_t)N * kPongHW) return;
-  const int e = (int)(t / kPongHW), y = (int)(t % kPongHW);
+  if (t >= (size_t)N * kChunks) return;
+  const int e = (int)(t / kChunks), q = (int)(t % kChunks);
+  const int a = q / 84, rem = q - a * 84, c = rem >> 2, dy = rem & 3;
   const float* h = state + (size_t)e * kPongState + P_HIST;
-  const float fy = (float)y + 0.5f;
+  const float fy = (float)(4 * a + dy) + 0.5f;
   const bool wall = fy < kTop || fy >= kBot;
-  const int a = y >> 2, dy = y & 3;
-  uint8_t* base = obs + (size_t)e * kPongHW * kPongHW * 4 + (size_t)a * 21 * 64 + dy * 16;
-  // per-frame horizontal spans on this row
-  float bx0[4], pa_on[4], po_on[4], b_on[4];
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
     const float bx = h[4 * f], by = h[4 * f + 1], pa = h[4 * f + 2], po = h[4 * f + 3];
-    bx0[f] = bx;
-    b_on[f] = (fy >= by && fy < by + kBall) ? 1.f : 0.f;
-    pa_on[f] = fabsf(fy - pa) < kPadHalf ? 1.f : 0.f;
-    po_on[f] = fabsf(fy - po) < kPadHalf ? 1.f : 0.f;
-  }
-  for (int c = 0; c < 21; ++c) {
-    uint32_t w[4];
+    const bool b_on = fy >= by && fy < by + kBall;
+    const bool pa_on = fabsf(fy - pa) < kPadHalf;
+    const bool po_on = fabsf(fy - po) < kPadHalf;
 #pragma unroll
     for (int px = 0; px < 4; ++px) {
-      const int x = 4 * c + px;
-      const float fx = (float)x + 0.5f;
-      uint32_t v = 0;
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        uint32_t p = wall ? 100u : 0u;
-        if (pa_on[f] > 0.f && fx >= kAgentX && fx < kAgentX + kPadW) p = 255u;
-        if (po_on[f] > 0.f && fx >= kOppX && fx < kOppX + kPadW) p = 255u;
-        if (b_on[f] > 0.f && fx >= bx0[f] && fx < bx0[f] + kBall) p = 255u;
-        v |= p << (8 * f);
-      }
-      w[px] = v;
+      const float fx = (float)(4 * c + px) + 0.5f;
+      uint32_t v = wall ? 100u : 0u;
+      if (pa_on && fx >= kAgentX && fx < kAgentX + kPadW) v = 255u;
+      if (po_on && fx >= kOppX && fx < kOppX + kPadW) v = 255u;
+      if (b_on && fx >= bx && fx < bx + kBall) v = 255u;
+      w[px] |= v << (8 * f);
     }
-    *reinterpret_cast<uint4*>(base + c * 64) = make_uint4(w[0], w[1], w[2], w[3]);
   }
+  *reinterpret_cast<uint4*>(obs + t * 16) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 }  // namespace rrl
@@ -192,7 +185,7 @@ int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, flo
 
 int rrl_pong_render(const float* state, uint8_t* obs, int N, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
-  const size_t t = (size_t)N * kPongHW;
+  const size_t t = (size_t)N * (kPongHW * kPongHW * 4 / 16);
   hipLaunchKernelGGL(pong_render_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, state, obs, N);
   return (int)hipGetLastError();
 }

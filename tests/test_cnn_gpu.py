@@ -243,7 +243,8 @@ def test_head_sampling_distribution(cuda):
     o = spec.offsets()
     params[o["wpi"]:o["bpi"]] *= 80.0
     m = DeviceNatureCNN(spec, cuda, max_batch=B, params=params)
-    obs = torch.randint(0, 256, (1, 21, 21, 64), dtype=torch.uint8).expand(B, 21, 21, 64).contiguous().to(cuda)
+    obs = torch.randint(0, 256, (1, 21, 21, 64), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
+    obs = obs.expand(B, 21, 21, 64).contiguous().to(cuda)
     act = torch.empty(B, dtype=torch.int32, device=cuda)
     logp = torch.empty(B, device=cuda)
     val = torch.empty(B, device=cuda)
@@ -252,7 +253,9 @@ def test_head_sampling_distribution(cuda):
     p = torch.softmax(lg[0].cpu(), -1)
     freq = torch.bincount(act.cpu().long(), minlength=6).float() / B
     assert (freq - p).abs().max() < 0.03
-    assert torch.allclose(logp.cpu(), torch.log(p)[act.cpu().long()], atol=1e-4)
+    # the batch-4096 and batch-1 forwards take different fc schedules (split-K for tiny
+    # batches), so the bf16-rounded hidden units can differ in the last bit: ~1e-4 in logp
+    assert torch.allclose(logp.cpu(), torch.log(p)[act.cpu().long()], atol=1e-3)
 
 
 def test_device_pong_matches_reference(cuda):
@@ -390,3 +393,15 @@ def test_pixel_trainer_graph_replay_matches_eager(cuda):
     assert torch.equal(a.act, b.act) and torch.equal(a.obs, b.obs)
     torch.testing.assert_close(a.model.params, b.model.params, rtol=0, atol=0)
     assert int(a.model.step_t.item()) == 4 and a.env.step_count == b.env.step_count
+
+
+@pytest.mark.parametrize("splits,n", [(256, 3591), (3, 7), (17, 4096)])
+def test_sum_splits_matches_torch(cuda, splits, n):
+    """Split-slab reduction, including the unaligned / odd-length path (A2C head: n = 3591)."""
+    from relayrl_prototype_amd.ops import hip
+
+    g = torch.Generator().manual_seed(splits + n)
+    part = torch.randn(splits, n, generator=g)
+    out = torch.empty(n, device=cuda)
+    hip().sum_splits(part.to(cuda).reshape(-1), splits, n, out)
+    torch.testing.assert_close(out.cpu(), part.sum(0), rtol=1e-5, atol=1e-4)
