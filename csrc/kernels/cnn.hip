@@ -877,6 +877,115 @@ __global__ __launch_bounds__(256, 2) void conv1_fwd_s2d_kernel(const uint8_t* __
     for (int q = tid; q < 400 * 4; q += 256) yd[q] = *reinterpret_cast<const uint4*>(O + (q >> 2) * 40 + (q & 3) * 8);
   }
 }
+
+// ----------------------------------------------------------------------------- conv2 dgrad
+// da1 = conv^T(da2, W2) * (a1 > 0) for the Nature CNN's second layer (20x20x32 input, 4x4
+// stride-2 taps, 9x9x64 output).  Persistent workgroups walk the images; wave w owns the
+// phase class (ph, pw) = (w >> 1, w & 1) of input pixels (ih, iw) = (ph + 2a, pw + 2b), a
+// 100 x 32 GEMM over (tap (i, j), co) whose A operand reads da2[a - i][b - j] straight out
+// of a zero-bordered 11x11 LDS image of the output gradient (no per-tap global re-reads:
+// the implicit-GEMM path fetched every da2 element 16 times), B = this class's W2 taps held
+// in registers.  The 400 x 32 result goes through LDS and leaves as contiguous 16-byte
+// chunks, masked by a1 on the way out.
+constexpr int kD2Ld = 72;                  // da2 image row: 64 co + 8 pad (bf16)
+constexpr int kD2Rows = 121;               // (oh + 1) * 11 + (ow + 1), oh, ow in -1 .. 9
+constexpr int kD2OutLd = 40;               // staging row: 32 c + 8 pad
+constexpr int kD2Lds = (kD2Rows * kD2Ld + 400 * kD2OutLd) * 2;
+
+__global__ __launch_bounds__(256, 2) void conv2_dgrad_kernel(const uint16_t* __restrict__ dy,
+                                                             const uint16_t* __restrict__ w,
+                                                             const uint16_t* __restrict__ xact,
+                                                             uint16_t* __restrict__ dx, int N) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Yi = smem;                      // [121][72] da2, zero border
+  uint16_t* O = smem + kD2Rows * kD2Ld;      // [400][40] unmasked da1
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i16 = lane & 15, g = lane >> 4;
+  const int ph = wave >> 1, pw = wave & 1;
+  // B fragments: k-step ks = (tap t = ks >> 1, co block (ks & 1) * 32), n tile nt:
+  // W2[co0 + 8g + e][ph + 2 (t >> 1)][pw + 2 (t & 1)][16 nt + i16], e = 0..7
+  bf16x8_t wf[8][2];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    const int t = ks >> 1, kh = ph + 2 * (t >> 1), kw = pw + 2 * (t & 1), co0 = (ks & 1) * 32 + 8 * g;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      typedef short s16x8_t __attribute__((ext_vector_type(8)));
+      s16x8_t v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (short)w[(((co0 + e) * 4 + kh) * 4 + kw) * 32 + 16 * nt + i16];
+      wf[ks][nt] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  }
+  // zero the border rows of the da2 image once (the interior is rewritten per image)
+  for (int q = tid; q < kD2Rows * (kD2Ld / 8); q += 256) {
+    const int r = q / (kD2Ld / 8), oh = r / 11 - 1, ow = r % 11 - 1;
+    if (oh < 0 || oh > 8 || ow < 0 || ow > 8)
+      *reinterpret_cast<uint4*>(Yi + r * kD2Ld + 8 * (q % (kD2Ld / 8))) = make_uint4(0, 0, 0, 0);
+  }
+  constexpr int YC = 81 * 8, YPT = (YC + 255) / 256;  // 16-byte chunks of one da2 image
+  uint4 ry[YPT];
+  auto gload = [&](int n) {
+    const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 81 * 64);
+#pragma unroll
+    for (int k = 0; k < YPT; ++k) {
+      const int q = tid + 256 * k;
+      ry[k] = q < YC ? ys[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if ((int)blockIdx.x < N) gload(blockIdx.x);
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    __syncthreads();  // the previous image's staging tile has been copied out
+#pragma unroll
+    for (int k = 0; k < YPT; ++k) {
+      const int q = tid + 256 * k;
+      if (q < YC) {
+        const int pix = q >> 3, oh = pix / 9, ow = pix - oh * 9;
+        *reinterpret_cast<uint4*>(Yi + ((oh + 1) * 11 + ow + 1) * kD2Ld + (q & 7) * 8) = ry[k];
+      }
+    }
+    if (n + (int)gridDim.x < N) gload(n + gridDim.x);
+    __syncthreads();
+    // class GEMM: 7 tiles of 16 pixels (a, b) = (p / 10, p % 10), p < 100
+#pragma unroll
+    for (int mt = 0; mt < 7; ++mt) {
+      f32x4_t acc0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, acc1 = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int p = 16 * mt + i16;
+      const int pc = p < 100 ? p : 0;  // rows past the class are computed and discarded
+      const int a = pc / 10, b = pc - a * 10;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int t = ks >> 1, ti = t >> 1, tj = t & 1;
+        const int row = (a - ti + 1) * 11 + (b - tj + 1);
+        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(Yi + row * kD2Ld + (ks & 1) * 32 + 8 * g);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[ks][0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[ks][1], acc1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = 16 * mt + 4 * g + r;
+        if (q < 100) {
+          const int aa = q / 10, bb = q - aa * 10;
+          const int pix = (ph + 2 * aa) * 20 + pw + 2 * bb;
+          O[pix * kD2OutLd + i16] = f2bf(acc0[r]);
+          O[pix * kD2OutLd + 16 + i16] = f2bf(acc1[r]);
+        }
+      }
+    }
+    __syncthreads();
+    const uint4* xa = reinterpret_cast<const uint4*>(xact + (size_t)n * 400 * 32);
+    uint4* xd = reinterpret_cast<uint4*>(dx + (size_t)n * 400 * 32);
+    for (int q = tid; q < 400 * 4; q += 256) {
+      const uint4 m = xa[q];
+      const uint4 v = *reinterpret_cast<const uint4*>(O + (q >> 2) * kD2OutLd + (q & 3) * 8);
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = bf16x8_at(m, e) > 0.f ? bf16x8_at(v, e) : 0.f;
+      xd[q] = pack_bf16x8(o);
+    }
+  }
+}
+
 }  // namespace rrl
 
 using namespace rrl;
@@ -962,8 +1071,17 @@ int rrl_gemm_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* mask, 
 int rrl_conv_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, int N, int H, int W,
                    int C, int KH, int KW, int S, int Cout, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
-  if (H == 20 && W == 20 && C == 32 && KH == 4 && KW == 4 && S == 2 && Cout == 64)
-    return launch_dgrad<20, 20, 32, 4, 4, 2, 9, 9, 64>(dy, w, xact, dx, N, st);
+  if (H == 20 && W == 20 && C == 32 && KH == 4 && KW == 4 && S == 2 && Cout == 64) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)conv2_dgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kD2Lds);
+      attr = true;
+    }
+    if (N < 1) return 0;
+    const int grid = N < 512 ? N : 512;  // 2 resident workgroups per CU (190 VGPRs)
+    hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(grid), dim3(256), kD2Lds, st, dy, w, xact, dx, N);
+    return (int)hipGetLastError();
+  }
   if (H == 9 && W == 9 && C == 64 && KH == 3 && KW == 3 && S == 1 && Cout == 64)
     return launch_dgrad<9, 9, 64, 3, 3, 1, 7, 7, 64>(dy, w, xact, dx, N, st);
   return -1;

@@ -74,7 +74,7 @@ def test_conv_forward_bf16(cuda, li, N):
     assert relerr(y, ref.permute(0, 2, 3, 1).reshape(-1)) < 1e-2
 
 
-@pytest.mark.parametrize("li,N", [(1, 6), (2, 19)])
+@pytest.mark.parametrize("li,N", [(1, 6), (2, 19), (1, 900)])
 def test_conv_dgrad_col2im_and_wgrad(cuda, li, N):
     """dX (masked by the input activation) and dW / db of a conv vs autograd."""
     from relayrl_prototype_amd.ops import hip
