@@ -14,7 +14,8 @@ int rrl_gemm_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* mask, 
                    int K, void* stream);
 int rrl_col2im_mask(const uint16_t* dcol, const uint16_t* xact, uint16_t* dx, int N, int H, int W, int C, int KH,
                     int KW, int S, void* stream);
-int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, int splits, int N, int H, int W, int C,
+int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, float* bias_part, int splits, int N,
+                   int H, int W, int C,
                    int KH, int KW, int S, int Cout, void* stream);
 int rrl_gemm_splits(int R, int splits);
 int rrl_conv_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, int N, int H, int W,
@@ -131,7 +132,7 @@ bool conv_dgrad(const Tensor& dy, const Tensor& w, const Tensor& xact, const Ten
 int64_t gemm_splits(int64_t R, int64_t splits) { return rrl_gemm_splits((int)R, (int)splits); }
 
 int64_t conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& part, int64_t splits, int64_t N, int64_t H,
-                   int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t S, int64_t Cout) {
+                   int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t S, int64_t Cout, const OptT& bias_part) {
   Geo g{N, H, W, C, KH, KW, S};
   check_geo(g);
   const bool u8 = x.scalar_type() == at::kByte;
@@ -141,8 +142,13 @@ int64_t conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& part, int64_
   check(x, "x", u8 ? at::kByte : at::kBFloat16, N * H * W * C);
   const int64_t s = gemm_splits(M, splits);
   check(part, "part", at::kFloat, s * Cout * K);
-  rc_check(rrl_conv_wgrad(bf(dy), x.data_ptr(), u8, part.data_ptr<float>(), (int)splits, N, H, W, C, KH, KW, S, Cout,
-                          stream()),
+  float* bp = nullptr;
+  if (bias_part.has_value()) {  // also the bias gradient: partials [s][Cout]
+    check(*bias_part, "bias_part", at::kFloat, s * Cout);
+    bp = bias_part->data_ptr<float>();
+  }
+  rc_check(rrl_conv_wgrad(bf(dy), x.data_ptr(), u8, part.data_ptr<float>(), bp, (int)splits, N, H, W, C, KH, KW, S,
+                          Cout, stream()),
            "conv_wgrad");
   return s;
 }
@@ -273,7 +279,10 @@ void register_cnn_ops(pybind11::module_& m) {
   m.def("col2im_mask", &col2im_mask);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("gemm_splits", &gemm_splits);
-  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad", &conv_wgrad, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("part"),
+        pybind11::arg("splits"), pybind11::arg("N"), pybind11::arg("H"), pybind11::arg("W"), pybind11::arg("C"),
+        pybind11::arg("KH"), pybind11::arg("KW"), pybind11::arg("S"), pybind11::arg("Cout"),
+        pybind11::arg("bias_part") = pybind11::none());
   m.def("sum_splits", &sum_splits);
   m.def("colsum", &colsum);
   m.def("sumsq", &sumsq);

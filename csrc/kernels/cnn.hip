@@ -693,7 +693,8 @@ __device__ __forceinline__ bf16x8_t tr8(const uint16_t* a0, const uint16_t* a1) 
 
 __global__ __launch_bounds__(256, 1) void conv1_wgrad_s2d_kernel(const uint8_t* __restrict__ x,
                                                                  const uint16_t* __restrict__ dy,
-                                                                 float* __restrict__ part, int N) {
+                                                                 float* __restrict__ part,
+                                                                 float* __restrict__ bias_part, int N) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Xi = smem;                   // [kW1XRows][kW1Ld] frame, bf16 integers 0..255
   uint16_t* Yi = smem + kW1XRows * kW1Ld;  // [kW1YRows][kW1Ld] dY
@@ -704,11 +705,23 @@ __global__ __launch_bounds__(256, 1) void conv1_wgrad_s2d_kernel(const uint8_t* 
   for (int q = tid; q < 16 * (kW1Ld / 8); q += 256)
     *reinterpret_cast<uint4*>(Yi + (400 + q / (kW1Ld / 8)) * kW1Ld + 8 * (q % (kW1Ld / 8))) = make_uint4(0, 0, 0, 0);
 
-  f32x4_t acc[2][4];
+  f32x4_t acc[2][4], accb[2];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+  for (int mt = 0; mt < 2; ++mt) {
+    accb[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  // bias gradient db[co] = sum_p dY[p][co] rides along on wave 0 as one more MFMA column
+  // block whose B operand is 1 in column 0 (the separate column-sum pass re-read dY)
+  const bool do_bias = bias_part != nullptr && w == 0;
+  bf16x8_t ones;
+  {
+    typedef short s16x8_t __attribute__((ext_vector_type(8)));
+    const short one = (lane & 15) == 0 ? (short)0x3f80 : (short)0;  // bf16 1.0 in column 0
+    s16x8_t v = {one, one, one, one, one, one, one, one};
+    ones = __builtin_bit_cast(bf16x8_t, v);
+  }
 
   constexpr int XC = 441 * 4, YC = 400 * 4;  // 16-byte chunks per image
   constexpr int XPT = (XC + 255) / 256, YPT = (YC + 255) / 256;
@@ -769,7 +782,17 @@ __global__ __launch_bounds__(256, 1) void conv1_wgrad_s2d_kernel(const uint8_t* 
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) accb[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], ones, accb[mt], 0, 0, 0);
+      }
     }
+  }
+  if (do_bias && (lane & 15) == 0) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias_part[(size_t)blockIdx.x * 32 + 16 * mt + 4 * g + r] = accb[mt][r];
   }
   // part[split][cout][kh][kw][c], raw-byte products scaled by 1/255
   float* o = part + (size_t)blockIdx.x * 32 * 256 + kh * 128 + kw * 64;
@@ -1101,8 +1124,8 @@ int rrl_col2im_mask(const uint16_t* dcol, const uint16_t* xact, uint16_t* dx, in
 // The GEMM is computed transposed -- rows = the conv's K (long), cols = Cout (32 / 64 /
 // 512) -- so the wide im2col operand gets the 128-row tile and the epilogue stores 4
 // consecutive k of one output channel as one 16-byte write.
-int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, int splits, int N, int H, int W,
-                   int C, int KH, int KW, int S, int Cout, void* stream_) {
+int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, float* bias_part, int splits, int N,
+                   int H, int W, int C, int KH, int KW, int S, int Cout, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   ConvGeom g{N, H, W, C, KH, KW, S, (H - KH) / S + 1, (W - KW) / S + 1, Cout};
   const int M = g.M(), K = g.K();
@@ -1116,8 +1139,16 @@ int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, int
       attr = true;
     }
     const int grid = rrl_gemm_splits_impl(M, splits);
-    hipLaunchKernelGGL(conv1_wgrad_s2d_kernel, dim3(grid), dim3(256), kW1Lds, st, (const uint8_t*)x, dy, part, N);
+    hipLaunchKernelGGL(conv1_wgrad_s2d_kernel, dim3(grid), dim3(256), kW1Lds, st, (const uint8_t*)x, dy, part,
+                       bias_part, N);
     return (int)hipGetLastError();
+  }
+  if (bias_part != nullptr) {  // bias partials [splits][Cout] from the column-sum kernel
+    if (Cout % 8 || Cout > 2048) return -1;
+    hipLaunchKernelGGL(colsum_kernel, dim3(rrl_gemm_splits_impl(M, splits)), dim3(256), 256 * 8 * sizeof(float), st,
+                       dy, M, Cout, bias_part);
+    const int rc = (int)hipGetLastError();
+    if (rc) return rc;
   }
   RowLoader ly{dy, M, Cout};
   PartialStoreT epi{part, K, Cout, x_u8 ? kU8Scale : 1.0f};

@@ -329,8 +329,9 @@ class DeviceNatureCNN:
         da1 = self.da1[:B * L1.hout ** 2 * L1.cout]
         self._dgrad(da2, sh[o["w2"]:o["b2"]], a1, da1, B, L2)
         # conv1 (input = frames, no data gradient)
-        self._wgrad("c1", da1, obs_u8.contiguous(), B, S2D.hin, S2D.cin, S2D.k, S2D.s, S2D.cout, o["w1"])
-        self._bias(da1, B * L1.hout ** 2, L1.cout, o["b1"])
+        # (its bias gradient comes out of the same pass over da1)
+        self._wgrad("c1", da1, obs_u8.contiguous(), B, S2D.hin, S2D.cin, S2D.k, S2D.s, S2D.cout, o["w1"],
+                    bias_off=o["b1"])
         if pending is not None:
             comm.all_reduce_sum_(g[:o["wfc"]])
             pending.wait()
@@ -350,10 +351,13 @@ class DeviceNatureCNN:
         self.h.gemm_dgrad(dy, w, None, dcol, B * L.hout ** 2, L.cout, L.K)
         self.h.col2im_mask(dcol, xact, dx, B, L.hin, L.hin, L.cin, L.k, L.k, L.s)
 
-    def _wgrad(self, name, dy, x, N, H, C, k, s, cout, off):
+    def _wgrad(self, name, dy, x, N, H, C, k, s, cout, off, bias_off=None):
         K = k * k * C
-        splits = int(self.h.conv_wgrad(dy, x, self.part, self._wplan[name], N, H, H, C, k, k, s, cout))
+        bp = self.bias_part if bias_off is not None else None
+        splits = int(self.h.conv_wgrad(dy, x, self.part, self._wplan[name], N, H, H, C, k, k, s, cout, bp))
         self.h.sum_splits(self.part, splits, cout * K, self.grad[off:off + cout * K])
+        if bias_off is not None:
+            self.h.sum_splits(self.bias_part, splits, cout, self.grad[bias_off:bias_off + cout])
 
     def _bias(self, dy, M, C, off):
         s = self.bias_splits

@@ -106,11 +106,15 @@ def test_conv_dgrad_col2im_and_wgrad(cuda, li, N):
     for splits in (1, 7):
         s = int(h.gemm_splits(M, splits))
         part = torch.empty(s * L.cout * K, device=cuda)
-        s2 = int(h.conv_wgrad(dyd, xd, part, splits, N, L.hin, L.hin, L.cin, L.k, L.k, L.s, L.cout))
+        bsp = torch.empty(s * L.cout, device=cuda)
+        s2 = int(h.conv_wgrad(dyd, xd, part, splits, N, L.hin, L.hin, L.cin, L.k, L.k, L.s, L.cout, bsp))
         assert s2 == s
         dw = torch.empty(L.cout * K, device=cuda)
         h.sum_splits(part, s, L.cout * K, dw)
         assert relerr(dw, dw_ref) < 1e-2, splits
+        dbs = torch.empty(L.cout, device=cuda)
+        h.sum_splits(bsp, s, L.cout, dbs)  # bias partials requested from the generic path (column sums)
+        assert relerr(dbs, dy.reshape(-1, L.cout).sum(0)) < 1e-4
     bp = torch.empty(3 * L.cout, device=cuda)
     h.colsum(dyd, M, L.cout, bp, 3)
     db = torch.empty(L.cout, device=cuda)
@@ -134,10 +138,14 @@ def test_conv1_wgrad_from_s2d_frames(cuda, N, splits):
     M = N * 400
     s = int(h.gemm_splits(M, splits))
     part = torch.full((s * 32 * 256,), float("nan"), device=cuda)
-    h.conv_wgrad(dy.to(cuda).bfloat16().reshape(-1), x.to(cuda), part, splits, N, 21, 21, 64, 2, 2, 1, 32)
+    bpart = torch.full((s * 32,), float("nan"), device=cuda)
+    h.conv_wgrad(dy.to(cuda).bfloat16().reshape(-1), x.to(cuda), part, splits, N, 21, 21, 64, 2, 2, 1, 32, bpart)
     dw = torch.empty(32 * 256, device=cuda)
     h.sum_splits(part, s, 32 * 256, dw)
     assert relerr(dw, dw_ref) < 1e-2
+    db = torch.empty(32, device=cuda)
+    h.sum_splits(bpart, s, 32, db)  # fused bias gradient
+    assert relerr(db, dy.reshape(-1, 32).sum(0)) < 1e-4
 
 
 def test_conv1_wgrad_from_frames(cuda):
