@@ -1009,6 +1009,103 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_kernel(const uint16_t* __r
   }
 }
 
+
+// ----------------------------------------------------------------------------- conv2/3 forward
+// y = relu(conv(x, W) + b) for the Nature CNN's bf16 layers (20x20x32 -> 9x9x64, 4x4 s2;
+// 9x9x64 -> 7x7x64, 3x3 s1).  Persistent workgroups walk the images with the next image
+// prefetched into registers: the input image goes into LDS once (the implicit-GEMM loader
+// fetched each input element once per overlapping tap), wave w computes output channels
+// 16w..16w+15 with its W slice in registers (K / 32 fragments), and the OHxOWx64 result
+// leaves through LDS as one contiguous block.
+template <int H, int W, int C, int KH, int KW, int S, int OH, int OW>
+__global__ __launch_bounds__(256, 2) void conv_fwd_img_kernel(const uint16_t* __restrict__ x,
+                                                              const uint16_t* __restrict__ w,
+                                                              const float* __restrict__ b, uint16_t* __restrict__ y,
+                                                              int N, int relu) {
+  constexpr int CO = 64, K = KH * KW * C, KS = K / 32, CB = C / 32;
+  constexpr int P = OH * OW, MT = (P + 15) / 16;
+  constexpr int XLD = C + 8, OLD = CO + 8;
+  constexpr int XC = H * W * C / 8, XPT = (XC + 255) / 256;  // 16-byte chunks of one input image
+  static_assert(C % 32 == 0, "k-steps of 32 channels");
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Xi = smem;  // [H*W][XLD]
+  uint16_t* O = smem;   // [P][OLD] after the MFMAs (aliases the input image)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  bf16x8_t wf[KS];  // B operand: W[16 wave + i][8g .. 8g+7 of k-step ks]
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) wf[ks] = *reinterpret_cast<const bf16x8_t*>(w + (size_t)(16 * wave + i) * K + 32 * ks + 8 * g);
+  const float bias = b[16 * wave + i];
+  uint4 rx[XPT];
+  auto gload = [&](int n) {
+    const uint4* xs = reinterpret_cast<const uint4*>(x + (size_t)n * H * W * C);
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int q = tid + 256 * k;
+      rx[k] = q < XC ? xs[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if ((int)blockIdx.x < N) gload(blockIdx.x);
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    __syncthreads();  // the previous image's output has been copied out
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int q = tid + 256 * k;
+      if (q < XC) *reinterpret_cast<uint4*>(Xi + (q / (C / 8)) * XLD + (q % (C / 8)) * 8) = rx[k];
+    }
+    if (n + (int)gridDim.x < N) gload(n + gridDim.x);
+    __syncthreads();
+    f32x4_t acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      acc[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int p = 16 * mt + i;
+      const int pc = p < P ? p : 0;  // rows past the image are computed and discarded
+      const int oh = pc / OW, ow = pc - oh * OW;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int tap = ks / CB, kh = tap / KW, kw = tap - kh * KW;
+        const int row = (oh * S + kh) * W + ow * S + kw;
+        const bf16x8_t a = *reinterpret_cast<const bf16x8_t*>(Xi + row * XLD + 32 * (ks % CB) + 8 * g);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[ks], acc[mt], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // the input image is dead: reuse the LDS for the output tile
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = 16 * mt + 4 * g + r;
+        if (p < P) {
+          float v = acc[mt][r] + bias;
+          if (relu) v = fmaxf(v, 0.f);
+          O[p * OLD + 16 * wave + i] = f2bf(v);
+        }
+      }
+    }
+    __syncthreads();
+    uint4* yd = reinterpret_cast<uint4*>(y + (size_t)n * P * CO);
+    for (int q = tid; q < P * CO / 8; q += 256)
+      yd[q] = *reinterpret_cast<const uint4*>(O + (q / (CO / 8)) * OLD + (q % (CO / 8)) * 8);
+  }
+}
+
+template <int H, int W, int C, int KH, int KW, int S, int OH, int OW>
+static int launch_conv_fwd_img(const uint16_t* x, const uint16_t* w, const float* b, uint16_t* y, int N, int relu,
+                               hipStream_t st) {
+  constexpr int lds = (H * W * (C + 8) > OH * OW * 72 ? H * W * (C + 8) : OH * OW * 72) * 2;
+  auto kern = conv_fwd_img_kernel<H, W, C, KH, KW, S, OH, OW>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  if (N < 1) return 0;
+  const int grid = N < 512 ? N : 512;  // 2 resident workgroups per CU
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, w, b, y, N, relu);
+  return (int)hipGetLastError();
+}
+
 }  // namespace rrl
 
 using namespace rrl;
@@ -1053,6 +1150,10 @@ int rrl_conv_fwd(const void* x, int x_u8, const uint16_t* w, const float* b, uin
                        kU8Scale, relu);
     return (int)hipGetLastError();
   }
+  if (!x_u8 && H == 20 && W == 20 && C == 32 && KH == 4 && KW == 4 && S == 2 && Cout == 64)
+    return launch_conv_fwd_img<20, 20, 32, 4, 4, 2, 9, 9>((const uint16_t*)x, w, b, y, N, relu, st);
+  if (!x_u8 && H == 9 && W == 9 && C == 64 && KH == 3 && KW == 3 && S == 1 && Cout == 64)
+    return launch_conv_fwd_img<9, 9, 64, 3, 3, 1, 7, 7>((const uint16_t*)x, w, b, y, N, relu, st);
   RowLoader lw{w, Cout, K};
   BiasReluStore epi{y, b, M, Cout, relu != 0, x_u8 ? kU8Scale : 1.0f};
   const int tiles = ((M + 127) / 128) * ((Cout + 63) / 64);

@@ -57,7 +57,7 @@ def test_conv1_forward_u8(cuda, N):
     assert relerr(y, ref) < 1e-2
 
 
-@pytest.mark.parametrize("li,N", [(1, 5), (2, 33), (1, 130)])
+@pytest.mark.parametrize("li,N", [(1, 5), (2, 33), (1, 130), (1, 1100), (2, 700)])
 def test_conv_forward_bf16(cuda, li, N):
     from relayrl_prototype_amd.ops import hip
 
