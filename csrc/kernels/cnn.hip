@@ -162,101 +162,6 @@ static int with_im2col(const ConvGeom& g, const void* x, bool u8, F&& f) {
   return f(ConvLoader{xb, g.H, g.W, g.C, g.KW, g.S, g.OH, g.OW, M, K});
 }
 
-// ----------------------------------------------------------------------------- implicit dgrad
-// dX = conv^T(dY, W) * (X > 0) without a column buffer.  Input pixels are split into
-// S x S phase classes (ih = ph + S*a, iw = pw + S*b); inside a class every pixel sees
-// the same taps kh = ph + S*i, kw = pw + S*j, so the class is one GEMM with
-//   rows = (n, a, b),  cols = c,  reduction = (i, j, co):
-//   A[(n,a,b)][(i,j,co)] = dY[n][a-i][b-j][co]   (0 outside the output)
-//   B[(i,j,co)][c]       = W[co][ph+S*i][pw+S*j][c]   (transposed LDS read)
-// Requires H % S == 0, W % S == 0, KH % S == 0, KW % S == 0 (true for the Nature CNN).
-template <int H, int W, int C, int KH, int KW, int S, int OH, int OW, int CO>
-struct DgradGeo {
-  static constexpr int HA = H / S, WB = W / S, TH = KH / S, TW = KW / S;
-  static constexpr int RED = TH * TW * CO;
-  static_assert(H % S == 0 && W % S == 0 && KH % S == 0 && KW % S == 0, "phase-class dgrad geometry");
-};
-
-template <class G, int H, int W, int C, int KH, int KW, int S, int OH, int OW, int CO>
-struct DgradALoader {
-  const uint16_t* dy;
-  int M;
-  __device__ __forceinline__ uint4 operator()(int m, int r) const {
-    if (m >= M) return make_uint4(0, 0, 0, 0);
-    const unsigned um = (unsigned)m, ur = (unsigned)r;
-    const unsigned n = um / (G::HA * G::WB), p = um - n * (G::HA * G::WB);
-    const int a = (int)(p / G::WB), b = (int)(p - (p / G::WB) * G::WB);
-    const unsigned tap = ur / CO, co = ur - tap * CO;
-    const int i = (int)(tap / G::TW), j = (int)(tap - (tap / G::TW) * G::TW);
-    const int oh = a - i, ow = b - j;
-    if (oh < 0 || oh >= OH || ow < 0 || ow >= OW) return make_uint4(0, 0, 0, 0);
-    return *reinterpret_cast<const uint4*>(dy + (((size_t)n * OH + oh) * OW + ow) * CO + co);
-  }
-};
-
-template <class G, int H, int W, int C, int KH, int KW, int S, int OH, int OW, int CO>
-struct DgradBLoader {
-  const uint16_t* w;
-  int ph, pw;
-  __device__ __forceinline__ uint4 operator()(int r, int c) const {
-    const unsigned ur = (unsigned)r;
-    const unsigned tap = ur / CO, co = ur - tap * CO;
-    const int i = (int)(tap / G::TW), j = (int)(tap - (tap / G::TW) * G::TW);
-    const int kh = ph + S * i, kw = pw + S * j;
-    return *reinterpret_cast<const uint4*>(w + (((size_t)co * KH + kh) * KW + kw) * C + c);
-  }
-};
-
-template <class G, int H, int W, int C>
-struct DgradStore {
-  uint16_t* dx;
-  const uint16_t* xact;
-  int M, ph, pw, S;
-  static constexpr bool kVec8 = (C % 8 == 0);
-  __device__ __forceinline__ void store8(int m, int c, const float (&v)[8], int) const {
-    const unsigned um = (unsigned)m;
-    const unsigned n = um / (G::HA * G::WB), p = um - n * (G::HA * G::WB);
-    const unsigned a = p / G::WB, b = p - a * G::WB;
-    const size_t idx = (((size_t)n * H + ph + S * a) * W + pw + S * b) * C + c;
-    const uint4 xa = *reinterpret_cast<const uint4*>(xact + idx);
-    float o[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = bf16x8_at(xa, e) > 0.f ? v[e] : 0.f;
-    *reinterpret_cast<uint4*>(dx + idx) = pack_bf16x8(o);
-  }
-  __device__ __forceinline__ void operator()(int m, int c, f32x4_t acc, int) const {
-    if (c >= C) return;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int mm = m + r;
-      if (mm < M) {
-        const unsigned um = (unsigned)mm;
-        const unsigned n = um / (G::HA * G::WB), p = um - n * (G::HA * G::WB);
-        const unsigned a = p / G::WB, b = p - a * G::WB;
-        const size_t idx = (((size_t)n * H + ph + S * a) * W + pw + S * b) * C + c;
-        dx[idx] = bf2f(xact[idx]) > 0.f ? f2bf(acc[r]) : (uint16_t)0;
-      }
-    }
-  }
-};
-
-template <int H, int W, int C, int KH, int KW, int S, int OH, int OW, int CO>
-static int launch_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, int N,
-                        hipStream_t st) {
-  using G = DgradGeo<H, W, C, KH, KW, S, OH, OW, CO>;
-  const int M = N * G::HA * G::WB;
-  for (int ph = 0; ph < S; ++ph)
-    for (int pw = 0; pw < S; ++pw) {
-      DgradALoader<G, H, W, C, KH, KW, S, OH, OW, CO> la{dy, M};
-      DgradBLoader<G, H, W, C, KH, KW, S, OH, OW, CO> lb{w, ph, pw};
-      DgradStore<G, H, W, C> epi{dx, xact, M, ph, pw, S};
-      const int rc = C >= 64 ? launch_gemm<128, 64, false, true>(la, lb, epi, M, C, G::RED, 1, st)
-                             : launch_gemm<128, 32, false, true>(la, lb, epi, M, C, G::RED, 1, st);
-      if (rc) return rc;
-    }
-  return 0;
-}
-
 // ----------------------------------------------------------------------------- col2im
 // dX[n][ih][iw][c] = sum over (kh, kw) with ih = oh*S + kh, iw = ow*S + kw of
 // dXc[(n, oh, ow)][(kh, kw, c)], then * (X > 0).  One thread per 8 channels.
@@ -968,6 +873,15 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_kernel(const uint16_t* __r
       }
     }
     if (n + (int)gridDim.x < N) gload(n + gridDim.x);
+    // this image's activation mask, fetched now so its latency hides behind the MFMAs
+    constexpr int XC = 400 * 4, XPT = (XC + 255) / 256;
+    uint4 rm[XPT];
+    const uint4* xa = reinterpret_cast<const uint4*>(xact + (size_t)n * 400 * 32);
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int q = tid + 256 * k;
+      rm[k] = q < XC ? xa[q] : make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
     // class GEMM: 7 tiles of 16 pixels (a, b) = (p / 10, p % 10), p < 100
 #pragma unroll
@@ -996,15 +910,17 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_kernel(const uint16_t* __r
       }
     }
     __syncthreads();
-    const uint4* xa = reinterpret_cast<const uint4*>(xact + (size_t)n * 400 * 32);
     uint4* xd = reinterpret_cast<uint4*>(dx + (size_t)n * 400 * 32);
-    for (int q = tid; q < 400 * 4; q += 256) {
-      const uint4 m = xa[q];
-      const uint4 v = *reinterpret_cast<const uint4*>(O + (q >> 2) * kD2OutLd + (q & 3) * 8);
-      float o[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = bf16x8_at(m, e) > 0.f ? bf16x8_at(v, e) : 0.f;
-      xd[q] = pack_bf16x8(o);
+    for (int k = 0; k < XPT; ++k) {
+      const int q = tid + 256 * k;
+      if (q < XC) {
+        const uint4 v = *reinterpret_cast<const uint4*>(O + (q >> 2) * kD2OutLd + (q & 3) * 8);
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = bf16x8_at(rm[k], e) > 0.f ? bf16x8_at(v, e) : 0.f;
+        xd[q] = pack_bf16x8(o);
+      }
     }
   }
 }
@@ -1104,6 +1020,107 @@ static int launch_conv_fwd_img(const uint16_t* x, const uint16_t* w, const float
   const int grid = N < 512 ? N : 512;  // 2 resident workgroups per CU
   hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, st, x, w, b, y, N, relu);
   return (int)hipGetLastError();
+}
+
+
+// ----------------------------------------------------------------------------- conv3 dgrad
+// da2 = conv^T(da3, W3) * (a2 > 0) for the third layer (9x9x64 input, 3x3 stride-1 taps,
+// 7x7x64 output): per image an 81 x 64 GEMM over (tap, co) whose A operand reads da3 from
+// an LDS image with a 2-pixel zero border; wave w owns input channels 16w..16w+15 with its
+// W3 taps in registers; the mask is prefetched and the result leaves as 16-byte chunks.
+constexpr int kD3Ld = 72;    // [121 bordered da3 pixels][64 co + 8]
+constexpr int kD3OutLd = 72;  // [81][64 c + 8]
+constexpr int kD3Lds = (121 * kD3Ld + 81 * kD3OutLd) * 2;
+
+__global__ __launch_bounds__(256, 2) void conv3_dgrad_kernel(const uint16_t* __restrict__ dy,
+                                                             const uint16_t* __restrict__ w,
+                                                             const uint16_t* __restrict__ xact,
+                                                             uint16_t* __restrict__ dx, int N) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Yi = smem;                 // (oh + 2) * 11 + (ow + 2), oh, ow in -2 .. 8
+  uint16_t* O = smem + 121 * kD3Ld;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i16 = lane & 15, g = lane >> 4;
+  // B fragments: k-step ks = (tap t = ks >> 1, co block (ks & 1) * 32):
+  // W3[co0 + 8g + e][t / 3][t % 3][16 wave + i16]
+  bf16x8_t wf[18];
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks) {
+    const int t = ks >> 1, co0 = (ks & 1) * 32 + 8 * g;
+    typedef short s16x8_t __attribute__((ext_vector_type(8)));
+    s16x8_t v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (short)w[((co0 + e) * 9 + t) * 64 + 16 * wave + i16];
+    wf[ks] = __builtin_bit_cast(bf16x8_t, v);
+  }
+  for (int q = tid; q < 121 * (kD3Ld / 8); q += 256) {
+    const int r = q / (kD3Ld / 8), oh = r / 11 - 2, ow = r % 11 - 2;
+    if (oh < 0 || oh > 6 || ow < 0 || ow > 6)
+      *reinterpret_cast<uint4*>(Yi + r * kD3Ld + 8 * (q % (kD3Ld / 8))) = make_uint4(0, 0, 0, 0);
+  }
+  constexpr int YC = 49 * 8, YPT = (YC + 255) / 256, XC = 81 * 8, XPT = (XC + 255) / 256;
+  uint4 ry[YPT];
+  auto gload = [&](int n) {
+    const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 49 * 64);
+#pragma unroll
+    for (int k = 0; k < YPT; ++k) {
+      const int q = tid + 256 * k;
+      ry[k] = q < YC ? ys[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if ((int)blockIdx.x < N) gload(blockIdx.x);
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < YPT; ++k) {
+      const int q = tid + 256 * k;
+      if (q < YC) {
+        const int pix = q >> 3, oh = pix / 7, ow = pix - oh * 7;
+        *reinterpret_cast<uint4*>(Yi + ((oh + 2) * 11 + ow + 2) * kD3Ld + (q & 7) * 8) = ry[k];
+      }
+    }
+    if (n + (int)gridDim.x < N) gload(n + gridDim.x);
+    uint4 rm[XPT];
+    const uint4* xa = reinterpret_cast<const uint4*>(xact + (size_t)n * 81 * 64);
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int q = tid + 256 * k;
+      rm[k] = q < XC ? xa[q] : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int mt = 0; mt < 6; ++mt) {
+      f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int p = 16 * mt + i16;
+      const int pc = p < 81 ? p : 0;
+      const int ih = pc / 9, iw = pc - ih * 9;
+#pragma unroll
+      for (int ks = 0; ks < 18; ++ks) {
+        const int t = ks >> 1, kh = t / 3, kw = t - kh * 3;
+        const int row = (ih - kh + 2) * 11 + (iw - kw + 2);
+        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(Yi + row * kD3Ld + (ks & 1) * 32 + 8 * g);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[ks], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = 16 * mt + 4 * g + r;
+        if (q < 81) O[q * kD3OutLd + 16 * wave + i16] = f2bf(acc[r]);
+      }
+    }
+    __syncthreads();
+    uint4* xd = reinterpret_cast<uint4*>(dx + (size_t)n * 81 * 64);
+#pragma unroll
+    for (int k = 0; k < XPT; ++k) {
+      const int q = tid + 256 * k;
+      if (q < XC) {
+        const uint4 v = *reinterpret_cast<const uint4*>(O + (q >> 3) * kD3OutLd + (q & 7) * 8);
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = bf16x8_at(rm[k], e) > 0.f ? bf16x8_at(v, e) : 0.f;
+        xd[q] = pack_bf16x8(o);
+      }
+    }
+  }
 }
 
 }  // namespace rrl
@@ -1206,8 +1223,17 @@ int rrl_conv_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, 
     hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(grid), dim3(256), kD2Lds, st, dy, w, xact, dx, N);
     return (int)hipGetLastError();
   }
-  if (H == 9 && W == 9 && C == 64 && KH == 3 && KW == 3 && S == 1 && Cout == 64)
-    return launch_dgrad<9, 9, 64, 3, 3, 1, 7, 7, 64>(dy, w, xact, dx, N, st);
+  if (H == 9 && W == 9 && C == 64 && KH == 3 && KW == 3 && S == 1 && Cout == 64) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)conv3_dgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kD3Lds);
+      attr = true;
+    }
+    if (N < 1) return 0;
+    const int grid = N < 512 ? N : 512;
+    hipLaunchKernelGGL(conv3_dgrad_kernel, dim3(grid), dim3(256), kD3Lds, st, dy, w, xact, dx, N);
+    return (int)hipGetLastError();
+  }
   return -1;
 }
 
