@@ -1,0 +1,38 @@
+// Arguments of the fused learner-gradient kernels (mlp_grad.hip, value_grad.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace rrl {
+
+enum GradHead : int {
+  HEAD_PG_CAT = 0,     // REINFORCE: loss = -mean(logp(a) * adv)
+  HEAD_VALUE_MSE = 1,  // baseline: loss = mean((v - ret)^2)
+  HEAD_PPO_CAT = 2,    // PPO clipped surrogate, categorical
+  HEAD_PPO_GAUSS = 3,  // PPO clipped surrogate, diagonal Gaussian
+  HEAD_PG_GAUSS = 4,   // REINFORCE / A2C with a Gaussian policy
+};
+
+struct GradArgs {
+  const float* params;
+  const float* X;  // [B][D]
+  int B, D, A;
+  const float* mask;       // [B][A] or null
+  const int* act;          // [B]
+  const float* actc;       // [B][A]
+  const float* adv;        // [B]
+  const float* ret;        // [B]
+  const float* logp_old;   // [B] or null
+  const float* adv_stats;  // [3] = {sum, sumsq, count} -> normalise adv, or null
+  float inv_B;             // 1 / (global batch)
+  float clip_eps;
+  float ent_coef;
+  float* grad_slab;  // [grid][P]
+  float* loss_slab;  // [grid][8]
+  int P;
+};
+
+// Weight-stationary bf16x6 value-gradient kernel (value_grad.hip): H = 128, D <= 8.
+bool value_grad_split_supported(int D, int H);
+int launch_value_grad_split(const GradArgs& a, int grid, hipStream_t s);
+
+}  // namespace rrl

@@ -20,35 +20,9 @@
 // reduce+Adam kernel (adam.hip) sums the slabs, so the result is deterministic.
 #include "common.h"
 #include "heads.h"
+#include "grad_args.h"
 
 namespace rrl {
-
-enum GradHead : int {
-  HEAD_PG_CAT = 0,     // REINFORCE: loss = -mean(logp(a) * adv)
-  HEAD_VALUE_MSE = 1,  // baseline: loss = mean((v - ret)^2)
-  HEAD_PPO_CAT = 2,    // PPO clipped surrogate, categorical
-  HEAD_PPO_GAUSS = 3,  // PPO clipped surrogate, diagonal Gaussian
-  HEAD_PG_GAUSS = 4,   // REINFORCE / A2C with a Gaussian policy
-};
-
-struct GradArgs {
-  const float* params;
-  const float* X;  // [B][D]
-  int B, D, A;
-  const float* mask;       // [B][A] or null
-  const int* act;          // [B]
-  const float* actc;       // [B][A]
-  const float* adv;        // [B]
-  const float* ret;        // [B]
-  const float* logp_old;   // [B] or null
-  const float* adv_stats;  // [3] = {sum, sumsq, count} -> normalise adv, or null
-  float inv_B;             // 1 / (global batch)
-  float clip_eps;
-  float ent_coef;
-  float* grad_slab;  // [grid][P]
-  float* loss_slab;  // [grid][8]
-  int P;
-};
 
 constexpr int kStageLd = 68;  // [feature][64 batch + 4 pad]
 
@@ -504,6 +478,15 @@ static int dispatch_head(int head, const GradArgs& a, int grid, hipStream_t s) {
   return -1;
 }
 
+// Value-MSE gradient path: 1 = weight-stationary bf16x6 kernel (value_grad.hip) where it
+// applies (H = 128, D <= 8), 0 = the fp32-MFMA kernel above for every shape.
+static int g_value_grad_mode = 1;
+extern "C" int rrl_set_value_grad_mode(int mode) {
+  const int old = g_value_grad_mode;
+  if (mode == 0 || mode == 1) g_value_grad_mode = mode;
+  return old;
+}
+
 // Number of partial-gradient slabs (== grid size) the launcher will use.
 extern "C" int rrl_mlp_grad_slabs(int B, int num_cu) {
   int grid = (B + 63) / 64;
@@ -523,6 +506,8 @@ extern "C" int rrl_mlp_grad(int head, const float* params, const float* X, int B
              ent_coef, grad_slab, loss_slab, P};
   const int grid = rrl_mlp_grad_slabs(B, num_cu);
   hipStream_t s = (hipStream_t)stream;
+  if (head == HEAD_VALUE_MSE && g_value_grad_mode == 1 && value_grad_split_supported(D, H))
+    return launch_value_grad_split(a, grid, s);
   const int DT = (D <= 16) ? 1 : 2;
   if (H == 128) return DT == 1 ? dispatch_head<1, 8>(head, a, grid, s) : dispatch_head<2, 8>(head, a, grid, s);
   if (H == 64) return DT == 1 ? dispatch_head<1, 4>(head, a, grid, s) : dispatch_head<2, 4>(head, a, grid, s);

@@ -1,0 +1,409 @@
+// Weight-stationary value-function gradient on bf16 matrix cores with fp32 accuracy
+// (K12 of SURVEY §2.6: compute_loss_vf + backward, REINFORCE.py:110-115,158-160).
+//
+// The value step runs train_vf_iters = 80 times per epoch (REINFORCE.py:110-115), so on the
+// CartPole flagship it is ~96 % of the learner's GPU time.  mlp_grad.hip runs it on the
+// fp32 MFMA (v_mfma_f32_16x16x4_f32: 1,024 MAC per 32 cycles); this kernel runs the three
+// 128x128 products on v_mfma_f32_16x16x32_bf16 (8,192 MAC per 16 cycles) with every fp32
+// operand split into three bf16 pieces, x = hi + mid + lo (each rounded to nearest, so
+// |x - hi - mid - lo| <= 2^-24 |x|), and the six products whose weight is >= 2^-16 summed
+// in the fp32 accumulator (small terms first):
+//     a b ~ al bh + ah bl + am bm + am bh + ah bm + ah bh      (dropped: am bl, al bm, al bl <= 2^-23)
+// i.e. fp32-level products (the bf16 x bf16 products are exact in fp32) at 6 x 16 = 96
+// cycles per 16x16x32 step instead of 8 x 32 = 256.  tests/test_value_grad_gpu.py checks
+// it against float64 and against the fp32-MFMA kernel.
+//
+// Work split (one persistent 4-wave workgroup per CU, 64-row batch slabs): wave w OWNS
+// hidden features [32w, 32w + 32) of both layers and computes them for all 64 rows, so its
+// slices of W2 stay in registers for the whole launch, pre-split:
+//     wA = W2[own rows][all 128]     (forward  h2 = W2 h1)
+//     wB = W2[all 128][own cols]^T   (backward dh1 = W2^T dh2)
+// Activations cross waves through LDS as pre-split bf16 images [64 batch][128 feature]
+// (row stride 144 elements: conflict-free b128 reads and transposed reads):
+//     h1 image  -> B operand of the forward (b128) and of dW2 (ds_read_b64_tr_b16)
+//     dh2 image -> B operand of dh1 (b128) and A operand of dW2 (transposed)
+// dW2 for the wave's 32 rows accumulates in registers across all slabs; layer 1 (K = D <= 8)
+// is one fp32 MFMA k-step, dW1 / dW3 / biases are VALU outer products.  The value head's
+// dot product is reduced over the 4 waves through LDS.
+#include "common.h"
+#include "grad_args.h"
+
+namespace rrl {
+
+typedef __bf16 vbf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 vbf16x4 __attribute__((ext_vector_type(4)));
+typedef short vs16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kVgH = 128;
+constexpr int kVgLd = 144;          // bf16 row stride of the activation images
+constexpr int kVgImg = 64 * kVgLd;  // elements per image piece
+constexpr int kVgLds = 6 * kVgImg * 2 + 8 * 64 * 4 + 2 * 64 * 8 * 4 + 3 * 128 * 4;
+
+struct Split8 {
+  vbf16x8 h, m, l;
+};
+
+RRL_DEV void split4(const floatx4 v, vbf16x4& h, vbf16x4& m, vbf16x4& lo) {
+  h = __builtin_convertvector(v, vbf16x4);
+  const floatx4 r1 = v - __builtin_convertvector(h, floatx4);
+  m = __builtin_convertvector(r1, vbf16x4);
+  const floatx4 r2 = r1 - __builtin_convertvector(m, floatx4);
+  lo = __builtin_convertvector(r2, vbf16x4);
+}
+
+RRL_DEV Split8 split8(const floatx4 v0, const floatx4 v1) {
+  vbf16x4 h0, m0, l0, h1, m1, l1;
+  split4(v0, h0, m0, l0);
+  split4(v1, h1, m1, l1);
+  Split8 s;
+  s.h = __builtin_shufflevector(h0, h1, 0, 1, 2, 3, 4, 5, 6, 7);
+  s.m = __builtin_shufflevector(m0, m1, 0, 1, 2, 3, 4, 5, 6, 7);
+  s.l = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return s;
+}
+
+RRL_DEV floatx4 mfma_bf16(vbf16x8 a, vbf16x8 b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// fp32-accurate 16x16x32 step from split operands
+RRL_DEV floatx4 mma6(const Split8& a, const Split8& b, floatx4 c) {
+  c = mfma_bf16(a.l, b.h, c);
+  c = mfma_bf16(a.h, b.l, c);
+  c = mfma_bf16(a.m, b.m, c);
+  c = mfma_bf16(a.m, b.h, c);
+  c = mfma_bf16(a.h, b.m, c);
+  return mfma_bf16(a.h, b.h, c);
+}
+
+// 8 consecutive features of batch row `row` (b128 read of each piece).
+RRL_DEV Split8 frag_row(const uint16_t* img, int row, int col) {
+  Split8 s;
+  const uint16_t* a = img + row * kVgLd + col;
+  s.h = *reinterpret_cast<const vbf16x8*>(a);
+  s.m = *reinterpret_cast<const vbf16x8*>(a + kVgImg);
+  s.l = *reinterpret_cast<const vbf16x8*>(a + 2 * kVgImg);
+  return s;
+}
+
+// Batch-contracted fragment of column col0 + (lane & 15) from a [batch][feature] image:
+// lane group g gets batch rows k0 + 4g + {0..3} and k0 + 16 + 4g + {0..3} (two transposed
+// reads; rows 4 apart in one 32-lane half fall in disjoint bank halves at stride 144).
+RRL_DEV vbf16x8 frag_tr1(const uint16_t* img, int k0, int col0, int lane) {
+  typedef __attribute__((address_space(3))) vs16x4 lds_v4;
+  const int q = (lane >> 2) & 3, pp = lane & 3, g = lane >> 4;
+  const uint16_t* a0 = img + (k0 + 4 * g + q) * kVgLd + col0 + 4 * pp;
+  const vs16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0));
+  const vs16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0 + 16 * kVgLd));
+  typedef short vs16x8 __attribute__((ext_vector_type(8)));
+  const vs16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(vbf16x8, v);
+}
+RRL_DEV Split8 frag_tr(const uint16_t* img, int k0, int col0, int lane) {
+  Split8 s;
+  s.h = frag_tr1(img, k0, col0, lane);
+  s.m = frag_tr1(img + kVgImg, k0, col0, lane);
+  s.l = frag_tr1(img + 2 * kVgImg, k0, col0, lane);
+  return s;
+}
+
+// Store a wave's C-layout tile (rows = 4 consecutive features of this lane, col = batch
+// row) into the three pieces of a [batch][feature] image.
+RRL_DEV void store_split(uint16_t* img, int row, int col, const floatx4 v) {
+  vbf16x4 h, m, lo;
+  split4(v, h, m, lo);
+  uint16_t* a = img + row * kVgLd + col;
+  *reinterpret_cast<vbf16x4*>(a) = h;
+  *reinterpret_cast<vbf16x4*>(a + kVgImg) = m;
+  *reinterpret_cast<vbf16x4*>(a + 2 * kVgImg) = lo;
+}
+
+// Sum of v[q] over the 16 lanes of this lane's row, for q = j only (4 butterfly steps).
+RRL_DEV float reduce_scatter16(const float (&v)[16], int j) {
+  float u[8], w4[4], w2[2];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool hi = j & 8;
+    const float send = hi ? v[k] : v[k + 8], keep = hi ? v[k + 8] : v[k];
+    u[k] = keep + __shfl_xor(send, 8, 64);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const bool hi = j & 4;
+    const float send = hi ? u[k] : u[k + 4], keep = hi ? u[k + 4] : u[k];
+    w4[k] = keep + __shfl_xor(send, 4, 64);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const bool hi = j & 2;
+    const float send = hi ? w4[k] : w4[k + 2], keep = hi ? w4[k + 2] : w4[k];
+    w2[k] = keep + __shfl_xor(send, 2, 64);
+  }
+  const bool hi = j & 1;
+  const float send = hi ? w2[0] : w2[1], keep = hi ? w2[1] : w2[0];
+  return keep + __shfl_xor(send, 1, 64);
+}
+
+template <int DP>
+__global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t vg_lds[];
+  uint16_t* h1img = vg_lds;
+  uint16_t* dhimg = vg_lds + 3 * kVgImg;
+  float* red = reinterpret_cast<float*>(vg_lds + 6 * kVgImg);  // [8 waves][64 rows]
+  float* xsb = red + 8 * 64;                                     // [2][64 rows][DP]
+  float* vecs = xsb + 2 * 64 * 8;                                // b1[128] b2[128] w3[128]
+  int parity = 0;
+  constexpr int KS1 = DP / 4;
+  const int l = lane_id();
+  const int j = l & 15, g = l >> 4, w = threadIdx.x >> 6;
+  const int D = p.D;
+  const FlatOffsets o = flat_offsets(D, kVgH, 1);
+  const float* __restrict__ P = p.params;
+  const int own = 16 * w;  // this wave's 16 hidden features
+
+  // ---------------------------------------------------------------- stationary weights
+  Split8 wA[4], wB[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    floatx4 a0, a1, b0, b1;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      // wA: A[m = own + j][k = 32c + 8g + e] = W2[m][k]      (forward)
+      a0[e] = P[o.w2 + (own + j) * kVgH + 32 * c + 8 * g + e];
+      a1[e] = P[o.w2 + (own + j) * kVgH + 32 * c + 8 * g + 4 + e];
+      // wB: A[m = own + j][k = 32c + 8g + e] = W2[k][m]      (backward data)
+      b0[e] = P[o.w2 + (32 * c + 8 * g + e) * kVgH + own + j];
+      b1[e] = P[o.w2 + (32 * c + 8 * g + 4 + e) * kVgH + own + j];
+    }
+    wA[c] = split8(a0, a1);
+    wB[c] = split8(b0, b1);
+  }
+  float w1a[KS1];  // layer-1 A operand: W1[own + j][4s + g]
+#pragma unroll
+  for (int s = 0; s < KS1; ++s) {
+    const int k = 4 * s + g;
+    w1a[s] = (k < D) ? P[o.w1 + (own + j) * D + k] : 0.f;
+  }
+  for (int q = threadIdx.x; q < 3 * kVgH; q += blockDim.x) {
+    const int k = q >> 7, f = q & (kVgH - 1);
+    vecs[q] = P[(k == 0 ? o.b1 : k == 1 ? o.b2 : o.w3) + f];
+  }
+  const float b3 = P[o.b3];
+  // per C-layout row own + 4g + r (re-read from LDS where used: registers are the limit)
+  const float* b1p = vecs + own + 4 * g;
+  const float* b2p = vecs + kVgH + own + 4 * g;
+  const float* w3p = vecs + 2 * kVgH + own + 4 * g;
+
+  floatx4 acc2[8];
+  float accv = 0.f;  // entry j of [db2 | dW3 | db1 | -] (4 rows each), summed over the batch lanes
+  float acc1[DP / 4];  // dW1[own + 4g + (j & 3)][4 d4 + (j >> 2)], summed over the batch lanes
+#pragma unroll
+  for (int it = 0; it < 8; ++it) acc2[it] = zero4();
+#pragma unroll
+  for (int d4 = 0; d4 < DP / 4; ++d4) acc1[d4] = 0.f;
+  float bacc3 = 0.f, s_loss = 0.f, s_val = 0.f, s_cnt = 0.f;
+
+  for (int base = blockIdx.x * 64; base < p.B; base += gridDim.x * 64) {
+    // ------------------------------------------------------------ x slab -> LDS
+    // (double-buffered by slab parity: the buffer written here was last read two slabs ago)
+    float* xs = xsb + (parity & 1) * 64 * DP;
+    parity ^= 1;
+    if (threadIdx.x < 64 * DP) {
+      const int rl = threadIdx.x / DP, d = threadIdx.x % DP, b = base + rl;
+      const float v = p.X[(size_t)min(b, p.B - 1) * D + min(d, D - 1)];
+      xs[threadIdx.x] = (b < p.B && d < D) ? v : 0.f;
+    }
+    __syncthreads();  // x visible; the previous slab's readers of both images are done
+
+    // ------------------------------------------------------------ layer 1 (fp32 MFMA)
+    uint32_t m1 = 0;  // relu'(h1) bits: 4 bt + r
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) {
+      floatx4 acc = *reinterpret_cast<const floatx4*>(b1p);
+#pragma unroll
+      for (int s = 0; s < KS1; ++s) acc = mfma4(w1a[s], xs[(16 * bt + j) * DP + 4 * s + g], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        acc[r] = fmaxf(acc[r], 0.f);
+        if (acc[r] > 0.f) m1 |= 1u << (4 * bt + r);
+      }
+      store_split(h1img, 16 * bt + j, own + 4 * g, acc);
+    }
+    __syncthreads();
+
+    // ------------------------------------------------------------ layer 2 (bf16x6 MFMA)
+    floatx4 h2[4];
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) h2[bt] = *reinterpret_cast<const floatx4*>(b2p);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+        const Split8 hb = frag_row(h1img, 16 * bt + j, 32 * c + 8 * g);
+        h2[bt] = mma6(wA[c], hb, h2[bt]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h2[bt][r] = fmaxf(h2[bt][r], 0.f);
+    }
+
+    // ------------------------------------------------------------ value head
+    floatx4 w3v = *reinterpret_cast<const floatx4*>(w3p);
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) {
+      float pv = w3v[0] * h2[bt][0];
+      pv = fmaf(w3v[1], h2[bt][1], pv);
+      pv = fmaf(w3v[2], h2[bt][2], pv);
+      pv = fmaf(w3v[3], h2[bt][3], pv);
+      pv = group_sum(pv);
+      if (g == bt) red[w * 64 + 16 * bt + j] = pv;
+    }
+    __syncthreads();
+    float dout[4];
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) {
+      const int rl = 16 * bt + j, b = base + rl;
+      const float v = (((red[rl] + red[64 + rl]) + (red[128 + rl] + red[192 + rl])) +
+                       ((red[256 + rl] + red[320 + rl]) + (red[384 + rl] + red[448 + rl]))) + b3;
+      const bool ok = b < p.B;
+      const float diff = v - (ok ? p.ret[min(b, p.B - 1)] : 0.f);
+      dout[bt] = ok ? 2.f * diff * p.inv_B : 0.f;
+      if (w == 0 && g == 0) {
+        bacc3 += dout[bt];
+        if (ok) {
+          s_loss += diff * diff;
+          s_val += v;
+          s_cnt += 1.f;
+        }
+      }
+    }
+
+    // ------------------------------------------------------------ dh2, dW3, db2
+    float tv[16];  // this slab's [db2 | dW3 | db1 | -] partials of rows own + 4g + r
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tv[q] = 0.f;
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) {
+      floatx4 d;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        d[r] = h2[bt][r] > 0.f ? w3v[r] * dout[bt] : 0.f;
+        tv[r] += d[r];
+        tv[4 + r] = fmaf(dout[bt], h2[bt][r], tv[4 + r]);
+      }
+      store_split(dhimg, 16 * bt + j, own + 4 * g, d);
+    }
+    accv += reduce_scatter16(tv, j);
+    __syncthreads();
+
+    // ------------------------------------------------------------ dh1 (own), dW1, db1
+    floatx4 dh1[4];
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) dh1[bt] = zero4();
+    float tb[16];  // db1 partials in entries 8..11 (the rest stay zero)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tb[q] = 0.f;
+    float t1[DP / 4][16];  // this slab's dW1 partials, entry 4 e + r of input column 4 d4 + e
+#pragma unroll
+    for (int d4 = 0; d4 < DP / 4; ++d4) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) t1[d4][q] = 0.f;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+        const Split8 db = frag_row(dhimg, 16 * bt + j, 32 * c + 8 * g);
+        dh1[bt] = mma6(wB[c], db, dh1[bt]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) {
+      floatx4 d = dh1[bt];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) d[r] = ((m1 >> (4 * bt + r)) & 1u) ? d[r] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tb[8 + r] += d[r];
+#pragma unroll
+      for (int d4 = 0; d4 < DP / 4; ++d4) {
+        const floatx4 x = *reinterpret_cast<const floatx4*>(xs + (16 * bt + j) * DP + 4 * d4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t1[d4][4 * e + r] = fmaf(d[r], x[e], t1[d4][4 * e + r]);
+        }
+      }
+    }
+    // fold the slab's dW1 partials over the 16 batch lanes: lane j keeps entry j
+#pragma unroll
+    for (int d4 = 0; d4 < DP / 4; ++d4) acc1[d4] += reduce_scatter16(t1[d4], j);
+    accv += reduce_scatter16(tb, j);
+
+    // ------------------------------------------------------------ dW2 += dh2 h1^T
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+      const Split8 a = frag_tr(dhimg, 32 * kc, own, l);
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const Split8 bb = frag_tr(h1img, 32 * kc, 16 * it, l);
+        acc2[it] = mma6(a, bb, acc2[it]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------ epilogue
+  float* slab = p.grad_slab + (size_t)blockIdx.x * p.P;
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) slab[o.w2 + (own + 4 * g + r) * kVgH + 16 * it + j] = acc2[it][r];
+  }
+  {
+    const int f = own + 4 * g + (j & 3), k = j >> 2;
+    if (k < 3) slab[(k == 0 ? o.b2 : k == 1 ? o.w3 : o.b1) + f] = accv;
+  }
+#pragma unroll
+  for (int d4 = 0; d4 < DP / 4; ++d4) {
+    const int f = own + 4 * g + (j & 3), dd = 4 * d4 + (j >> 2);
+    if (dd < D) slab[o.w1 + f * D + dd] = acc1[d4];
+  }
+  if (w == 0) {
+    const float vb3 = wave_sum(bacc3);
+    const float sl = wave_sum(s_loss), sv = wave_sum(s_val), sc = wave_sum(s_cnt);
+    if (l == 0) {
+      slab[o.b3] = vb3;
+      float* ls = p.loss_slab + blockIdx.x * 8;
+      ls[0] = sl;
+      ls[1] = 0.f;
+      ls[2] = 0.f;
+      ls[3] = 0.f;
+      ls[4] = sv;
+      ls[5] = sc;
+    }
+  }
+}
+
+bool value_grad_split_supported(int D, int H) { return H == kVgH && D >= 1 && D <= 8; }
+
+template <int DP>
+static int launch_vg(const GradArgs& a, int grid, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kVgLds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(value_grad_split_kernel<DP>, dim3(grid), dim3(512), kVgLds, s, a);
+  return (int)hipGetLastError();
+}
+
+int launch_value_grad_split(const GradArgs& a, int grid, hipStream_t s) {
+  return a.D <= 4 ? launch_vg<4>(a, grid, s) : launch_vg<8>(a, grid, s);
+}
+
+}  // namespace rrl

@@ -62,6 +62,7 @@ from .mlp import (  # noqa: E402
     GradHead,
     mlp_forward,
     mlp_grad,
+    set_value_grad_mode,
     grad_slabs,
     adam_step,
     reduce_slabs,
@@ -79,6 +80,7 @@ __all__ = [
     "GradHead",
     "mlp_forward",
     "mlp_grad",
+    "set_value_grad_mode",
     "grad_slabs",
     "adam_step",
     "reduce_slabs",

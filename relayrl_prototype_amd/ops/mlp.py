@@ -137,6 +137,15 @@ def grad_slabs(B: int, device) -> int:
     return int(hip().mlp_grad_slabs(B))
 
 
+def set_value_grad_mode(mode: int) -> int:
+    """Select the GPU value-MSE gradient kernel: 1 = weight-stationary bf16x6 (fp32-accurate
+    split-bf16 MFMA, csrc/kernels/value_grad.hip; H = 128, D <= 8), 0 = fp32 MFMA
+    (mlp_grad.hip).  -1 only queries.  Returns the previous mode."""
+    from . import hip
+
+    return int(hip().set_value_grad_mode(int(mode)))
+
+
 def mlp_grad(head: int, params, X, A: int, H: int, mask=None, act=None, actc=None, adv=None, ret=None,
              logp_old=None, adv_stats=None, inv_B: Optional[float] = None, clip_eps: float = 0.2,
              ent_coef: float = 0.0, grad_slab=None, loss_slab=None):

@@ -1,0 +1,98 @@
+"""The weight-stationary bf16x6 value-gradient kernel (csrc/kernels/value_grad.hip).
+
+It replaces the fp32-MFMA kernel for the value step (train_vf_iters = 80 per epoch,
+REINFORCE.py:110-115) when H = 128 and D <= 8.  Its products run on bf16 matrix cores with
+every fp32 operand split three ways, so it must be as accurate as fp32 math: both kernels
+are compared against a float64 autograd oracle of the same loss, and the split kernel's
+error may not exceed the fp32 kernel's by more than a small factor.
+"""
+import pytest
+import torch
+
+from relayrl_prototype_amd.ops import GradHead, MLPSpec, mlp_grad, set_value_grad_mode
+
+pytestmark = pytest.mark.gpu
+
+
+def _grad64(params, X, ret, D, H, inv_B):
+    p = params.double().clone().requires_grad_(True)
+    o = 0
+    W1 = p[o:o + H * D].view(H, D); o += H * D
+    b1 = p[o:o + H]; o += H
+    W2 = p[o:o + H * H].view(H, H); o += H * H
+    b2 = p[o:o + H]; o += H
+    W3 = p[o:o + H].view(1, H); o += H
+    b3 = p[o:o + 1]
+    h1 = torch.relu(X.double() @ W1.T + b1)
+    h2 = torch.relu(h1 @ W2.T + b2)
+    v = (h2 @ W3.T + b3)[:, 0]
+    loss = ((v - ret.double()) ** 2).sum() * inv_B
+    loss.backward()
+    return p.grad, ((v - ret.double()) ** 2).sum().item()
+
+
+def _away_from_relu_kinks(params, X, D, H, tau=1e-5):
+    """Rows whose hidden pre-activations are all at least tau away from 0 in float64.
+
+    Any two fp32-accurate evaluations of the same net differ by ~1e-7 in a pre-activation,
+    so where one lies within that of the ReLU kink the two can take opposite sides of it and
+    their gradients then legitimately differ by a whole row's contribution.  Dropping the
+    ~0.1 % of rows with a pre-activation inside +-1e-5 makes the comparison a test of the
+    arithmetic only."""
+    p = params.double()
+    o = 0
+    W1 = p[o:o + H * D].view(H, D); o += H * D
+    b1 = p[o:o + H]; o += H
+    W2 = p[o:o + H * H].view(H, H); o += H * H
+    b2 = p[o:o + H]
+    z1 = X.double() @ W1.T + b1
+    z2 = torch.relu(z1) @ W2.T + b2
+    m = torch.minimum(z1.abs().min(1).values, z2.abs().min(1).values)
+    return m > tau
+
+
+def _run(mode, pp, X, ret, H):
+    old = set_value_grad_mode(mode)
+    try:
+        slab, loss = mlp_grad(GradHead.VALUE_MSE, pp, X, 1, H, ret=ret)
+        torch.cuda.synchronize()
+    finally:
+        set_value_grad_mode(old)
+    return slab.sum(0, dtype=torch.float64).cpu(), loss.sum(0).cpu()
+
+
+@pytest.mark.parametrize("D,B", [(4, 1), (4, 63), (4, 5000), (4, 70000), (8, 33000), (2, 777), (6, 4097), (3, 16)])
+def test_split_kernel_matches_float64(cuda, D, B):
+    H = 128
+    g = torch.Generator().manual_seed(D * 1000 + B)
+    spec = MLPSpec(D, H, 1, False)
+    pp = spec.init(g)
+    pp = pp + 0.05 * torch.randn(pp.shape, generator=g)  # non-zero biases, generic weights
+    X = torch.randn(B, D, generator=g) * 1.5
+    ret = torch.randn(B, generator=g) * 20 + 5
+    keep = _away_from_relu_kinks(pp, X, D, H)
+    X, ret = X[keep], ret[keep]
+    B = X.shape[0]
+    g64, loss64 = _grad64(pp, X, ret, D, H, 1.0 / B)
+    gs, ls = _run(1, pp.to(cuda), X.to(cuda), ret.to(cuda), H)
+    gf, lf = _run(0, pp.to(cuda), X.to(cuda), ret.to(cuda), H)
+    scale = g64.abs().max().item()
+    err_split = (gs - g64).abs().max().item() / scale
+    err_fp32 = (gf - g64).abs().max().item() / scale
+    # fp32-level: both within a few fp32 ulps of the largest gradient entry, and the split
+    # kernel no worse than twice the fp32 kernel's error
+    assert err_fp32 < 1e-5, err_fp32
+    assert err_split < 1e-5, (err_split, err_fp32)
+    assert err_split <= 2.0 * err_fp32 + 2e-7, (err_split, err_fp32)
+    assert abs(ls[0].item() - loss64) <= 1e-5 * abs(loss64) + 1e-6
+    assert int(ls[5].item()) == B
+    assert ls[1:4].abs().sum().item() == 0.0
+
+
+def test_mode_switch_roundtrip(cuda):
+    old = set_value_grad_mode(-1)
+    assert old in (0, 1)
+    assert set_value_grad_mode(0) == old
+    assert set_value_grad_mode(-1) == 0
+    assert set_value_grad_mode(old) == 0
+    assert set_value_grad_mode(-1) == old

@@ -57,6 +57,10 @@ def main():
         us = timeit(lambda: mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret, grad_slab=slab, loss_slab=ls), a.iters)
         res["value_grad_us"] = us
         res["value_grad_TFLOPs_nominal"] = flop_row * B / us / 1e6
+        old = hip().set_value_grad_mode(0)  # the fp32-MFMA kernel, for comparison
+        us0 = timeit(lambda: mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret, grad_slab=slab, loss_slab=ls), a.iters)
+        hip().set_value_grad_mode(old)
+        res["value_grad_fp32mfma_us"] = us0
     if a.which in ("pgrad", "all"):
         ns = hip().mlp_grad_slabs(B)
         slab = torch.empty(ns, pp.numel(), device=dev)
