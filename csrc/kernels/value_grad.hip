@@ -13,18 +13,28 @@
 // cycles per 16x16x32 step instead of 8 x 32 = 256.  tests/test_value_grad_gpu.py checks
 // it against float64 and against the fp32-MFMA kernel.
 //
-// Work split (one persistent 4-wave workgroup per CU, 64-row batch slabs): wave w OWNS
-// hidden features [32w, 32w + 32) of both layers and computes them for all 64 rows, so its
-// slices of W2 stay in registers for the whole launch, pre-split:
+// Work split (one persistent 8-wave workgroup per CU, 64-row batch slabs, 2 waves per
+// SIMD): wave w OWNS hidden features [16w, 16w + 16) of both layers and computes them for all
+// 64 rows, so its slices of W2 stay in registers for the whole launch, pre-split:
 //     wA = W2[own rows][all 128]     (forward  h2 = W2 h1)
 //     wB = W2[all 128][own cols]^T   (backward dh1 = W2^T dh2)
-// Activations cross waves through LDS as pre-split bf16 images [64 batch][128 feature]
-// (row stride 144 elements: conflict-free b128 reads and transposed reads):
+// (hi + mid pieces in registers; the lo pieces of W2 sit in one LDS image [o][i] that
+// both fragment kinds read once per 32-wide k-chunk).  Activations cross waves through LDS
+// as pre-split bf16 images [64 batch][128 feature] (row stride 144 elements: conflict-free
+// b128 reads and transposed reads):
 //     h1 image  -> B operand of the forward (b128) and of dW2 (ds_read_b64_tr_b16)
 //     dh2 image -> B operand of dh1 (b128) and A operand of dW2 (transposed)
-// dW2 for the wave's 32 rows accumulates in registers across all slabs; layer 1 (K = D <= 8)
-// is one fp32 MFMA k-step, dW1 / dW3 / biases are VALU outer products.  The value head's
-// dot product is reduced over the 4 waves through LDS.
+// Each MFMA loop loads the next step's fragment before issuing the current step's six
+// MFMAs.  dW2 for the wave's 16 rows accumulates in registers across all slabs; layer 1
+// (K = D <= 8) is one or two fp32 MFMA k-steps; dW1 / dW3 / biases are VALU outer products
+// folded over the 16 batch lanes once per slab by a DPP reduce-scatter (lane j keeps entry
+// j), which keeps their accumulators at one register each.  The value head's dot product
+// is reduced over the 8 waves through LDS.  4 workgroup barriers per slab.
+//
+// Measured (tools/kbench.py grad, B = 2,097,152 rows, CartPole D = 4): 1.06 ms vs 1.91 ms for
+// the fp32-MFMA kernel.  A ds_bpermute-based reduce-scatter gave run-to-run different dW1
+// entries in one lane at D = 4 (tests/test_value_grad_gpu.py::test_deterministic); the DPP
+// form is bitwise reproducible.
 #include "common.h"
 #include "grad_args.h"
 
@@ -37,18 +47,44 @@ typedef short vs16x4 __attribute__((ext_vector_type(4)));
 constexpr int kVgH = 128;
 constexpr int kVgLd = 144;          // bf16 row stride of the activation images
 constexpr int kVgImg = 64 * kVgLd;  // elements per image piece
-constexpr int kVgLds = 6 * kVgImg * 2 + 8 * 64 * 4 + 2 * 64 * 8 * 4 + 3 * 128 * 4;
+constexpr int kVgWLo = 6 * kVgImg * 2 + 8 * 64 * 4 + 2 * 64 * 8 * 4 + 3 * 128 * 4;  // byte offset of the W2 lo image
+constexpr int kVgLds = kVgWLo + kVgH * kVgLd * 2;
 
 struct Split8 {
   vbf16x8 h, m, l;
 };
 
+typedef float vf32x2 __attribute__((ext_vector_type(2)));
+
+// Two fp32 -> packed bf16 pair (round to nearest even), a in the low half.
+RRL_DEV uint32_t cvt_pk_bf16(float a, float b) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// The packed pair back as two fp32 (exact).
+RRL_DEV vf32x2 unpack_bf16(uint32_t p) {
+  vf32x2 f;
+  f.x = __uint_as_float(p << 16);
+  f.y = __uint_as_float(p & 0xffff0000u);
+  return f;
+}
+// x = hi + mid + lo, each piece rounded to nearest: 3 converts, 2 unpacks and 2 packed
+// subtracts per pair of values.
+RRL_DEV void split2(vf32x2 v, uint32_t& h, uint32_t& m, uint32_t& lo) {
+  h = cvt_pk_bf16(v.x, v.y);
+  const vf32x2 r1 = v - unpack_bf16(h);
+  m = cvt_pk_bf16(r1.x, r1.y);
+  const vf32x2 r2 = r1 - unpack_bf16(m);
+  lo = cvt_pk_bf16(r2.x, r2.y);
+}
 RRL_DEV void split4(const floatx4 v, vbf16x4& h, vbf16x4& m, vbf16x4& lo) {
-  h = __builtin_convertvector(v, vbf16x4);
-  const floatx4 r1 = v - __builtin_convertvector(h, floatx4);
-  m = __builtin_convertvector(r1, vbf16x4);
-  const floatx4 r2 = r1 - __builtin_convertvector(m, floatx4);
-  lo = __builtin_convertvector(r2, vbf16x4);
+  uint32_t h0, m0, l0, h1, m1, l1;
+  split2(vf32x2{v[0], v[1]}, h0, m0, l0);
+  split2(vf32x2{v[2], v[3]}, h1, m1, l1);
+  h = __builtin_bit_cast(vbf16x4, make_uint2(h0, h1));
+  m = __builtin_bit_cast(vbf16x4, make_uint2(m0, m1));
+  lo = __builtin_bit_cast(vbf16x4, make_uint2(l0, l1));
 }
 
 RRL_DEV Split8 split8(const floatx4 v0, const floatx4 v1) {
@@ -61,6 +97,10 @@ RRL_DEV Split8 split8(const floatx4 v0, const floatx4 v1) {
   s.l = __builtin_shufflevector(l0, l1, 0, 1, 2, 3, 4, 5, 6, 7);
   return s;
 }
+
+struct Split8HM {  // hi + mid pieces (the lo piece of a stationary weight fragment lives in LDS)
+  vbf16x8 h, m;
+};
 
 RRL_DEV floatx4 mfma_bf16(vbf16x8 a, vbf16x8 b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -99,6 +139,17 @@ RRL_DEV vbf16x8 frag_tr1(const uint16_t* img, int k0, int col0, int lane) {
   const vs16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(vbf16x8, v);
 }
+// Rows k0 .. k0 + 7 of column col0 + (lane & 15) of a [k][col] image (k0 includes 8g).
+RRL_DEV vbf16x8 frag_tr8(const uint16_t* img, int k0, int col0, int lane) {
+  typedef __attribute__((address_space(3))) vs16x4 lds_v4;
+  const int q = (lane >> 2) & 3, pp = lane & 3;
+  const uint16_t* a0 = img + (k0 + q) * kVgLd + col0 + 4 * pp;
+  const vs16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0));
+  const vs16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0 + 4 * kVgLd));
+  typedef short vs16x8 __attribute__((ext_vector_type(8)));
+  const vs16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(vbf16x8, v);
+}
 RRL_DEV Split8 frag_tr(const uint16_t* img, int k0, int col0, int lane) {
   Split8 s;
   s.h = frag_tr1(img, k0, col0, lane);
@@ -118,30 +169,42 @@ RRL_DEV void store_split(uint16_t* img, int row, int col, const floatx4 v) {
   *reinterpret_cast<vbf16x4*>(a + 2 * kVgImg) = lo;
 }
 
-// Sum of v[q] over the 16 lanes of this lane's row, for q = j only (4 butterfly steps).
+// Value of v from the partner lane selected by a DPP control (VALU cross-lane move, no LDS).
+template <int CTRL>
+RRL_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, true));
+}
+constexpr int kDppXor8 = 0x128;     // row_ror:8 (16-lane rows: lane ^ 8)
+constexpr int kDppMirror8 = 0x141;  // row_half_mirror (lane ^ 7 within 8: flips bit 2)
+constexpr int kDppXor2 = 0x4e;      // quad_perm [2,3,0,1]
+constexpr int kDppXor1 = 0xb1;      // quad_perm [1,0,3,2]
+
+// Sum of v[q] over the 16 lanes of this lane's row, for q = j only: recursive halving with
+// DPP partner moves; at each step the partner differs in the bit that decides which half of
+// the remaining entries a lane keeps, so lane j ends with entry j.
 RRL_DEV float reduce_scatter16(const float (&v)[16], int j) {
   float u[8], w4[4], w2[2];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const bool hi = j & 8;
     const float send = hi ? v[k] : v[k + 8], keep = hi ? v[k + 8] : v[k];
-    u[k] = keep + __shfl_xor(send, 8, 64);
+    u[k] = keep + dpp_f<kDppXor8>(send);
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const bool hi = j & 4;
     const float send = hi ? u[k] : u[k + 4], keep = hi ? u[k + 4] : u[k];
-    w4[k] = keep + __shfl_xor(send, 4, 64);
+    w4[k] = keep + dpp_f<kDppMirror8>(send);
   }
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const bool hi = j & 2;
     const float send = hi ? w4[k] : w4[k + 2], keep = hi ? w4[k + 2] : w4[k];
-    w2[k] = keep + __shfl_xor(send, 2, 64);
+    w2[k] = keep + dpp_f<kDppXor2>(send);
   }
   const bool hi = j & 1;
   const float send = hi ? w2[0] : w2[1], keep = hi ? w2[1] : w2[0];
-  return keep + __shfl_xor(send, 1, 64);
+  return keep + dpp_f<kDppXor1>(send);
 }
 
 template <int DP>
@@ -162,7 +225,9 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   const int own = 16 * w;  // this wave's 16 hidden features
 
   // ---------------------------------------------------------------- stationary weights
-  Split8 wA[4], wB[4];
+  // hi + mid pieces in registers; the lo pieces of W2 go to an LDS image [o][i] that both
+  // fragment kinds read once per 32-wide k-chunk (b128 for wA, transposed for wB)
+  Split8HM wA[4], wB[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     floatx4 a0, a1, b0, b1;
@@ -175,8 +240,20 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       b0[e] = P[o.w2 + (32 * c + 8 * g + e) * kVgH + own + j];
       b1[e] = P[o.w2 + (32 * c + 8 * g + 4 + e) * kVgH + own + j];
     }
-    wA[c] = split8(a0, a1);
-    wB[c] = split8(b0, b1);
+    const Split8 sa = split8(a0, a1), sb = split8(b0, b1);
+    wA[c].h = sa.h;
+    wA[c].m = sa.m;
+    wB[c].h = sb.h;
+    wB[c].m = sb.m;
+  }
+  uint16_t* w2lo = vg_lds + kVgWLo / 2;
+  for (int q = threadIdx.x; q < kVgH * kVgH / 4; q += blockDim.x) {
+    floatx4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = P[o.w2 + 4 * q + e];
+    vbf16x4 h, m, lo;
+    split4(v, h, m, lo);
+    *reinterpret_cast<vbf16x4*>(w2lo + (q >> 5) * kVgLd + 4 * (q & 31)) = lo;
   }
   float w1a[KS1];  // layer-1 A operand: W1[own + j][4s + g]
 #pragma unroll
@@ -224,8 +301,9 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       for (int s = 0; s < KS1; ++s) acc = mfma4(w1a[s], xs[(16 * bt + j) * DP + 4 * s + g], acc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        acc[r] = fmaxf(acc[r], 0.f);
-        if (acc[r] > 0.f) m1 |= 1u << (4 * bt + r);
+        const bool pos = acc[r] > 0.f;  // (fmaxf would add a NaN-canonicalising max per value)
+        acc[r] = pos ? acc[r] : 0.f;
+        m1 |= (uint32_t)pos << (4 * bt + r);
       }
       store_split(h1img, 16 * bt + j, own + 4 * g, acc);
     }
@@ -235,19 +313,29 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     floatx4 h2[4];
 #pragma unroll
     for (int bt = 0; bt < 4; ++bt) h2[bt] = *reinterpret_cast<const floatx4*>(b2p);
+    {
+      // 16 steps (c, bt); the next step's B fragment (and W2-lo piece) load before this one's MFMAs
+      Split8 cur = frag_row(h1img, j, 8 * g);
+      vbf16x8 al = *reinterpret_cast<const vbf16x8*>(w2lo + (own + j) * kVgLd + 8 * g);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-#pragma unroll
-      for (int bt = 0; bt < 4; ++bt) {
-        const Split8 hb = frag_row(h1img, 16 * bt + j, 32 * c + 8 * g);
-        h2[bt] = mma6(wA[c], hb, h2[bt]);
+      for (int it = 0; it < 16; ++it) {
+        const int c = it >> 2, bt = it & 3;
+        Split8 nxt;
+        vbf16x8 aln;
+        if (it + 1 < 16) nxt = frag_row(h1img, 16 * ((it + 1) & 3) + j, 32 * ((it + 1) >> 2) + 8 * g);
+        if (bt == 3 && it + 1 < 16)
+          aln = *reinterpret_cast<const vbf16x8*>(w2lo + (own + j) * kVgLd + 32 * (c + 1) + 8 * g);
+        const Split8 a{wA[c].h, wA[c].m, al};
+        h2[bt] = mma6(a, cur, h2[bt]);
         __builtin_amdgcn_sched_barrier(0);
+        if (it + 1 < 16) cur = nxt;
+        if (bt == 3 && it + 1 < 16) al = aln;
       }
     }
 #pragma unroll
     for (int bt = 0; bt < 4; ++bt) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h2[bt][r] = fmaxf(h2[bt][r], 0.f);
+      for (int r = 0; r < 4; ++r) h2[bt][r] = h2[bt][r] > 0.f ? h2[bt][r] : 0.f;
     }
 
     // ------------------------------------------------------------ value head
@@ -312,13 +400,21 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) t1[d4][q] = 0.f;
     }
+    {
+      Split8 cur = frag_row(dhimg, j, 8 * g);
+      vbf16x8 bl = frag_tr8(w2lo, 8 * g, own, l);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-#pragma unroll
-      for (int bt = 0; bt < 4; ++bt) {
-        const Split8 db = frag_row(dhimg, 16 * bt + j, 32 * c + 8 * g);
-        dh1[bt] = mma6(wB[c], db, dh1[bt]);
+      for (int it = 0; it < 16; ++it) {
+        const int c = it >> 2, bt = it & 3;
+        Split8 nxt;
+        vbf16x8 bln;
+        if (it + 1 < 16) nxt = frag_row(dhimg, 16 * ((it + 1) & 3) + j, 32 * ((it + 1) >> 2) + 8 * g);
+        if (bt == 3 && it + 1 < 16) bln = frag_tr8(w2lo, 32 * (c + 1) + 8 * g, own, l);
+        const Split8 a{wB[c].h, wB[c].m, bl};
+        dh1[bt] = mma6(a, cur, dh1[bt]);
         __builtin_amdgcn_sched_barrier(0);
+        if (it + 1 < 16) cur = nxt;
+        if (bt == 3 && it + 1 < 16) bl = bln;
       }
     }
 #pragma unroll
@@ -344,14 +440,20 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     accv += reduce_scatter16(tb, j);
 
     // ------------------------------------------------------------ dW2 += dh2 h1^T
+    {
+      Split8 a = frag_tr(dhimg, 0, own, l);
+      Split8 cur = frag_tr(h1img, 0, 0, l);
 #pragma unroll
-    for (int kc = 0; kc < 2; ++kc) {
-      const Split8 a = frag_tr(dhimg, 32 * kc, own, l);
-#pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const Split8 bb = frag_tr(h1img, 32 * kc, 16 * it, l);
-        acc2[it] = mma6(a, bb, acc2[it]);
+      for (int it = 0; it < 16; ++it) {
+        const int kc = it >> 3, t = it & 7;
+        Split8 nxt, an;
+        if (it + 1 < 16) nxt = frag_tr(h1img, 32 * ((it + 1) >> 3), 16 * ((it + 1) & 7), l);
+        if (it == 7) an = frag_tr(dhimg, 32, own, l);
+        acc2[t] = mma6(a, cur, acc2[t]);
         __builtin_amdgcn_sched_barrier(0);
+        if (it + 1 < 16) cur = nxt;
+        if (it == 7) a = an;
+        (void)kc;
       }
     }
   }
@@ -398,7 +500,7 @@ static int launch_vg(const GradArgs& a, int grid, hipStream_t s) {
                               kVgLds);
     attr_set = true;
   }
-  hipLaunchKernelGGL(value_grad_split_kernel<DP>, dim3(grid), dim3(512), kVgLds, s, a);
+  hipLaunchKernelGGL((value_grad_split_kernel<DP>), dim3(grid), dim3(512), kVgLds, s, a);
   return (int)hipGetLastError();
 }
 
