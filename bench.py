@@ -132,10 +132,11 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp32",  # value step: 3-way bf16 split of every fp32 operand (bf16x6), fp32-accurate
             "data": "synthetic (on-device CartPole-v1 physics, random-init weights)",
             "config": {
-                "model": f"{algo} MLP[128,128] CartPole-v1 (policy+value, fp32 MFMA)",
+                "model": f"{algo} MLP[128,128] CartPole-v1 (policy: fp32 MFMA; value step: fp32-accurate "
+                         "bf16x6 split MFMA, csrc/kernels/value_grad.hip)",
                 "global_batch": steps_per_epoch,
                 "seq_len": cfg.rollout_len,
                 "parallelism": f"dp{world}",
