@@ -479,7 +479,7 @@ static int dispatch_head(int head, const GradArgs& a, int grid, hipStream_t s) {
 }
 
 // Value-MSE gradient path: 1 = weight-stationary bf16x6 kernel (value_grad.hip) where it
-// applies (H = 128, D <= 8), 0 = the fp32-MFMA kernel above for every shape.
+// applies (H = 128, D <= 24), 0 = the fp32-MFMA kernel above for every shape.
 static int g_value_grad_mode = 1;
 extern "C" int rrl_set_value_grad_mode(int mode) {
   const int old = g_value_grad_mode;

@@ -26,7 +26,7 @@
 //     dh2 image -> B operand of dh1 (b128) and A operand of dW2 (transposed)
 // Each MFMA loop loads the next step's fragment before issuing the current step's six
 // MFMAs.  dW2 for the wave's 16 rows accumulates in registers across all slabs; layer 1
-// (K = D <= 8) is one or two fp32 MFMA k-steps; dW1 / dW3 / biases are VALU outer products
+// (K = D <= 24) is DP / 4 fp32 MFMA k-steps; dW1 / dW3 / biases are VALU outer products
 // folded over the 16 batch lanes once per slab by a DPP reduce-scatter (lane j keeps entry
 // j), which keeps their accumulators at one register each.  The value head's dot product
 // is reduced over the 8 waves through LDS.  4 workgroup barriers per slab.
@@ -47,8 +47,11 @@ typedef short vs16x4 __attribute__((ext_vector_type(4)));
 constexpr int kVgH = 128;
 constexpr int kVgLd = 144;          // bf16 row stride of the activation images
 constexpr int kVgImg = 64 * kVgLd;  // elements per image piece
-constexpr int kVgWLo = 6 * kVgImg * 2 + 8 * 64 * 4 + 2 * 64 * 8 * 4 + 3 * 128 * 4;  // byte offset of the W2 lo image
-constexpr int kVgLds = kVgWLo + kVgH * kVgLd * 2;
+// LDS: h1 + dh2 images (3 pieces each), head partials [8][64], x slabs [2][64][DP], b1/b2/w3,
+// then the W2 lo image; DP = 24 (D <= 24) uses 163,328 of the 163,840 bytes.
+constexpr int vg_wlo_bytes(int DP) { return 6 * kVgImg * 2 + 8 * 64 * 4 + 2 * 64 * DP * 4 + 3 * 128 * 4; }
+constexpr int vg_lds_bytes(int DP) { return vg_wlo_bytes(DP) + kVgH * kVgLd * 2; }
+static_assert(vg_lds_bytes(24) <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
 
 struct Split8 {
   vbf16x8 h, m, l;
@@ -214,7 +217,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   uint16_t* dhimg = vg_lds + 3 * kVgImg;
   float* red = reinterpret_cast<float*>(vg_lds + 6 * kVgImg);  // [8 waves][64 rows]
   float* xsb = red + 8 * 64;                                     // [2][64 rows][DP]
-  float* vecs = xsb + 2 * 64 * 8;                                // b1[128] b2[128] w3[128]
+  float* vecs = xsb + 2 * 64 * DP;                               // b1[128] b2[128] w3[128]
   int parity = 0;
   constexpr int KS1 = DP / 4;
   const int l = lane_id();
@@ -246,7 +249,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     wB[c].h = sb.h;
     wB[c].m = sb.m;
   }
-  uint16_t* w2lo = vg_lds + kVgWLo / 2;
+  uint16_t* w2lo = vg_lds + vg_wlo_bytes(DP) / 2;
   for (int q = threadIdx.x; q < kVgH * kVgH / 4; q += blockDim.x) {
     floatx4 v;
 #pragma unroll
@@ -285,10 +288,10 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     // (double-buffered by slab parity: the buffer written here was last read two slabs ago)
     float* xs = xsb + (parity & 1) * 64 * DP;
     parity ^= 1;
-    if (threadIdx.x < 64 * DP) {
-      const int rl = threadIdx.x / DP, d = threadIdx.x % DP, b = base + rl;
+    for (int q = threadIdx.x; q < 64 * DP; q += blockDim.x) {
+      const int rl = q / DP, d = q % DP, b = base + rl;
       const float v = p.X[(size_t)min(b, p.B - 1) * D + min(d, D - 1)];
-      xs[threadIdx.x] = (b < p.B && d < D) ? v : 0.f;
+      xs[q] = (b < p.B && d < D) ? v : 0.f;
     }
     __syncthreads();  // x visible; the previous slab's readers of both images are done
 
@@ -394,12 +397,6 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     float tb[16];  // db1 partials in entries 8..11 (the rest stay zero)
 #pragma unroll
     for (int q = 0; q < 16; ++q) tb[q] = 0.f;
-    float t1[DP / 4][16];  // this slab's dW1 partials, entry 4 e + r of input column 4 d4 + e
-#pragma unroll
-    for (int d4 = 0; d4 < DP / 4; ++d4) {
-#pragma unroll
-      for (int q = 0; q < 16; ++q) t1[d4][q] = 0.f;
-    }
     {
       Split8 cur = frag_row(dhimg, j, 8 * g);
       vbf16x8 bl = frag_tr8(w2lo, 8 * g, own, l);
@@ -419,25 +416,31 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     }
 #pragma unroll
     for (int bt = 0; bt < 4; ++bt) {
-      floatx4 d = dh1[bt];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) d[r] = ((m1 >> (4 * bt + r)) & 1u) ? d[r] : 0.f;
+      for (int r = 0; r < 4; ++r) {
+        dh1[bt][r] = ((m1 >> (4 * bt + r)) & 1u) ? dh1[bt][r] : 0.f;
+        tb[8 + r] += dh1[bt][r];
+      }
+    }
+    accv += reduce_scatter16(tb, j);
+    // dW1 one group of 4 input columns at a time (16 partials live, whatever D is), each
+    // folded over the 16 batch lanes right away: lane j keeps entry j
 #pragma unroll
-      for (int r = 0; r < 4; ++r) tb[8 + r] += d[r];
+    for (int d4 = 0; d4 < DP / 4; ++d4) {
+      float t1[16];  // entry 4 e + r of input column 4 d4 + e
 #pragma unroll
-      for (int d4 = 0; d4 < DP / 4; ++d4) {
+      for (int q = 0; q < 16; ++q) t1[q] = 0.f;
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
         const floatx4 x = *reinterpret_cast<const floatx4*>(xs + (16 * bt + j) * DP + 4 * d4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) t1[d4][4 * e + r] = fmaf(d[r], x[e], t1[d4][4 * e + r]);
+          for (int r = 0; r < 4; ++r) t1[4 * e + r] = fmaf(dh1[bt][r], x[e], t1[4 * e + r]);
         }
       }
+      acc1[d4] += reduce_scatter16(t1, j);
     }
-    // fold the slab's dW1 partials over the 16 batch lanes: lane j keeps entry j
-#pragma unroll
-    for (int d4 = 0; d4 < DP / 4; ++d4) acc1[d4] += reduce_scatter16(t1[d4], j);
-    accv += reduce_scatter16(tb, j);
 
     // ------------------------------------------------------------ dW2 += dh2 h1^T
     {
@@ -490,22 +493,25 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   }
 }
 
-bool value_grad_split_supported(int D, int H) { return H == kVgH && D >= 1 && D <= 8; }
+bool value_grad_split_supported(int D, int H) { return H == kVgH && D >= 1 && D <= 24; }
 
 template <int DP>
 static int launch_vg(const GradArgs& a, int grid, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kVgLds);
+                              vg_lds_bytes(DP));
     attr_set = true;
   }
-  hipLaunchKernelGGL((value_grad_split_kernel<DP>), dim3(grid), dim3(512), kVgLds, s, a);
+  hipLaunchKernelGGL((value_grad_split_kernel<DP>), dim3(grid), dim3(512), vg_lds_bytes(DP), s, a);
   return (int)hipGetLastError();
 }
 
 int launch_value_grad_split(const GradArgs& a, int grid, hipStream_t s) {
-  return a.D <= 4 ? launch_vg<4>(a, grid, s) : launch_vg<8>(a, grid, s);
+  if (a.D <= 4) return launch_vg<4>(a, grid, s);
+  if (a.D <= 8) return launch_vg<8>(a, grid, s);
+  if (a.D <= 16) return launch_vg<16>(a, grid, s);
+  return launch_vg<24>(a, grid, s);  // HalfCheetahSynth (D = 17)
 }
 
 }  // namespace rrl
