@@ -64,16 +64,16 @@ def time_to_threshold(args, comm, threshold=475.0):
         t0 = time.perf_counter()
         while True:
             tr.train_epoch()
-            m = tr.metrics()
+            ret = tr.average_ep_return()  # one D2H read per epoch (== metrics()["AverageEpRet"])
             el = time.perf_counter() - t0
-            if m["AverageEpRet"] == m["AverageEpRet"] and m["AverageEpRet"] >= threshold:
+            if ret == ret and ret >= threshold:
                 times.append(el)
                 break
             if el > args.ttt_max_s:
                 times.append(float("inf"))
                 break
         epochs.append(tr.epoch)
-        steps.append(m["EnvSteps"])
+        steps.append(tr.env_steps * comm.world)
         del tr
     med = statistics.median(times)
     return (None if med == float("inf") else med), times, int(statistics.median(epochs)), int(statistics.median(steps))

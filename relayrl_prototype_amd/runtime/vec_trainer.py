@@ -147,6 +147,20 @@ class VecTrainer:
             self.timer.reset()
         return out
 
+    def average_ep_return(self) -> float:
+        """AverageEpRet of the last epoch (global over ranks) from ONE device->host read:
+        the per-epoch check of the time-to-threshold loop.  metrics() reads every column
+        and the learner's loss slabs (~7 synchronising reads, a sizeable share of a 1 ms
+        epoch); this returns the same value metrics()["AverageEpRet"] would."""
+        ns = self.ep_stats[:, :2].sum(0)
+        if self.comm.world > 1:
+            ns = ns.double()
+            if self.comm.backend != "nccl":
+                ns = ns.cpu()
+            self.comm.all_reduce_sum_(ns)
+        n, s = ns.tolist()
+        return s / n if n > 0 else float("nan")
+
     def state_dict(self) -> dict:
         return {"learner": self.learner.state_dict(), "epoch": self.epoch, "env_steps": self.env_steps,
                 "env_state": self.state.cpu(), "ep_len": self.ep_len.cpu(), "ep_ret": self.ep_ret.cpu(),

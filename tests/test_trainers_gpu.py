@@ -24,6 +24,25 @@ def test_vec_trainer_graph_equals_eager(cuda):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
+def test_average_ep_return_matches_metrics(cuda):
+    """The one-read threshold check of bench.py's time-to-threshold loop returns exactly
+    metrics()["AverageEpRet"] (NaN before the first finished episode)."""
+    from relayrl_prototype_amd.runtime.vec_trainer import VecTrainer, VecTrainerConfig
+
+    tr = VecTrainer(VecTrainerConfig(num_envs=1024, rollout_len=64, train_vf_iters=3, seed=2))
+    seen = 0
+    for _ in range(4):
+        tr.train_epoch()
+        fast = tr.average_ep_return()
+        full = tr.metrics()["AverageEpRet"]
+        if full != full:
+            assert fast != fast
+        else:
+            seen += 1
+            assert fast == full
+    assert seen > 0
+
+
 @pytest.mark.parametrize("algo", ["reinforce", "a2c", "ppo"])
 def test_vec_trainer_algos(cuda, algo):
     from relayrl_prototype_amd.runtime.vec_trainer import VecTrainer, VecTrainerConfig
