@@ -172,6 +172,161 @@ __global__ __launch_bounds__(256, 2) void rollout_kernel(RolloutArgs p) {
   }
 }
 
+// ------------------------------------------------------------------ small-N variant
+// rollout_kernel gives each wave 16 envs and a whole 128x128 layer per step, so a short
+// rollout over few envs (the time-to-threshold config: 1,024 envs = 64 tiles) runs 64 long
+// serial chains on 16 CUs.  Here a workgroup's 4 waves share ONE 16-env tile: every wave
+// keeps the env replica and the full layer 1 (8 MFMAs), computes a quarter of layer 2
+// (HT/4 output tiles) and its partial logits, and the partials meet in LDS (double-buffered
+// by step parity: one barrier per step).  All waves then sum the 4 partials in the same
+// order, so they draw the same action and step identical env replicas; wave 0 writes.
+template <class Env, int HT>
+__global__ __launch_bounds__(256, 2) void rollout_wide_kernel(RolloutArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int DT = 1;
+  using L = LdsNet<DT, HT>;
+  constexpr int H = L::H;
+  constexpr int D = Env::D, A = Env::A, NS = Env::NS;
+  constexpr int QT = HT / 4;  // layer-2 output tiles per wave
+  static_assert(D <= 16 && HT % 4 == 0, "one input tile, layer 2 split over 4 waves");
+  stage_net<DT, HT>(lds, p.params, D, A, false);
+  float* part = lds + ((L::floats(A) + 3) & ~3);  // [2 parity][4 waves][kMaxAct][16 envs]
+  __syncthreads();
+
+  const int l = lane_id();
+  const int j = l & 15, g = l >> 4;
+  const int w = threadIdx.x >> 6;
+  const int to0 = w * QT;
+  const int ntiles = (p.N + kTileB - 1) / kTileB;
+  const uint2 key = make_uint2(p.seed_lo, p.seed_hi);
+  const uint64_t step0 = ((uint64_t)p.step_hi << 32) | p.step_lo;
+  const bool writer = (w == 0) && (g == 0);
+  int parity = 0;
+
+  float st_n = 0.f, st_sum = 0.f, st_sq = 0.f, st_max = -INFINITY, st_min = INFINITY, st_len = 0.f;
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int env = tile * kTileB + j;
+    const bool valid = env < p.N;
+    const int envc = valid ? env : p.N - 1;
+    float s[NS];
+    int len;
+    float ret;
+    if (p.reset_all) {
+      const uint4 r = philox4x32(make_uint4((uint32_t)envc, (uint32_t)step0, (uint32_t)(step0 >> 32), 1u), key);
+      Env::reset(s, r);
+      len = 0;
+      ret = 0.f;
+    } else {
+#pragma unroll
+      for (int k = 0; k < NS; ++k) s[k] = p.state[(size_t)envc * NS + k];
+      len = p.ep_len[envc];
+      ret = p.ep_ret[envc];
+    }
+
+    for (int t = 0; t < p.T; ++t) {
+      const uint64_t gstep = step0 + (uint64_t)t;
+      const size_t base = (size_t)t * p.N + env;
+      floatx4 x[1];
+      x[0] = zero4();
+#pragma unroll
+      for (int f = 0; f < D; ++f) {
+        const float o = Env::obs(s, f);
+        if ((f & 3) == g) x[0][f >> 2] = o;
+      }
+      if (valid && w == 0) {
+#pragma unroll
+        for (int f = 0; f < D; ++f)
+          if ((f & 3) == g) p.obs_buf[base * D + f] = x[0][f >> 2];
+      }
+      floatx4 h1[HT], h2[QT];
+      dense_fwd<DT, HT, true>(lds + L::W1, L::S1, lds + L::B1, x, h1, (D + 3) >> 2);
+      dense_fwd<HT, QT, true>(lds + L::W2 + 16 * to0 * L::S2, L::S2, lds + L::B2 + 16 * to0, h1, h2);
+      float* pp = part + parity * (4 * kMaxAct * 16);
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        const float v = head_dot<QT>(lds + L::W3 + a * H + 16 * to0, 0.f, h2);
+        if (g == 0) pp[(w * kMaxAct + a) * 16 + j] = v;
+      }
+      __syncthreads();
+      float logits[kMaxAct];
+#pragma unroll
+      for (int a = 0; a < kMaxAct; ++a) {
+        if (a < A) {
+          const float* q = pp + a * 16 + j;
+          logits[a] = ((q[0] + q[kMaxAct * 16]) + (q[2 * kMaxAct * 16] + q[3 * kMaxAct * 16])) + lds[L::B3 + a];
+        } else {
+          logits[a] = -INFINITY;
+        }
+      }
+      parity ^= 1;
+      const CatStats cs = cat_stats(A, logits);
+      const uint4 rnd = philox4x32(make_uint4((uint32_t)envc, (uint32_t)gstep, (uint32_t)(gstep >> 32), 0u), key);
+      const int a = cat_sample(A, logits, cs.lse, u01(rnd.x));
+      const float logp = pick_logit(A, logits, a) - cs.lse;
+
+      bool term;
+      const float r = Env::step(s, a, term, u01(rnd.y));
+      len += 1;
+      ret += r;
+      const bool trunc = len >= p.max_steps;
+      const bool done = term || trunc;
+      if (valid && writer) {
+        p.act_buf[base] = a;
+        p.logp_buf[base] = logp;
+        p.rew_buf[base] = r;
+        p.done_buf[base] = done ? 1.f : 0.f;
+      }
+      if (done) {
+        if (valid && writer) {
+          st_n += 1.f;
+          st_sum += ret;
+          st_sq += ret * ret;
+          st_max = fmaxf(st_max, ret);
+          st_min = fminf(st_min, ret);
+          st_len += (float)len;
+        }
+        const uint4 rr = philox4x32(make_uint4((uint32_t)envc, (uint32_t)gstep, (uint32_t)(gstep >> 32), 1u), key);
+        Env::reset(s, rr);
+        len = 0;
+        ret = 0.f;
+      }
+    }
+    if (valid && w == 0) {
+      const size_t base = (size_t)p.T * p.N + env;
+#pragma unroll
+      for (int f = 0; f < D; ++f)
+        if ((f & 3) == g) p.obs_buf[base * D + f] = Env::obs(s, f);
+      if (g == 0) {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) p.state[(size_t)env * NS + k] = s[k];
+        p.ep_len[env] = len;
+        p.ep_ret[env] = ret;
+      }
+    }
+  }
+
+  // workgroup statistics: only wave 0 accumulated, so its wave reduction is the answer
+  if (w == 0) {
+    float v0 = wave_sum(st_n), v1 = wave_sum(st_sum), v2 = wave_sum(st_sq), v5 = wave_sum(st_len);
+    float v3 = st_max, v4 = st_min;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      v3 = fmaxf(v3, __shfl_xor(v3, o, 64));
+      v4 = fminf(v4, __shfl_xor(v4, o, 64));
+    }
+    if (l == 0) {
+      float* e = p.ep_stats + blockIdx.x * 8;
+      e[0] = v0;
+      e[1] = v1;
+      e[2] = v2;
+      e[3] = v3;
+      e[4] = v4;
+      e[5] = v5;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ continuous envs
 // Same structure for a diagonal-Gaussian policy (PPO / REINFORCE on HalfCheetahSynth):
 // mu = MLP(obs), a = mu + exp(log_std) * n with n from Box-Muller over Philox draws
@@ -377,8 +532,16 @@ extern "C" int rrl_env_dims(int env, int* D, int* A, int* NS, int* max_steps) {
   return -1;
 }
 
+// Few envs (at most two 16-env tiles per CU): one workgroup per tile, layer 2 split over
+// its 4 waves (rollout_wide_kernel); otherwise 4 tiles per workgroup, one per wave.
+static bool rollout_wide(int N, int num_cu) {
+  const int tiles = (N + kTileB - 1) / kTileB;
+  return tiles <= 2 * (num_cu > 0 ? num_cu : 256);
+}
+
 extern "C" int rrl_rollout_grid(int N, int num_cu) {
   const int tiles = (N + kTileB - 1) / kTileB;
+  if (rollout_wide(N, num_cu)) return tiles < 1 ? 1 : tiles;
   int grid = (tiles + 3) / 4;
   const int cap = 2 * (num_cu > 0 ? num_cu : 256);
   if (grid > cap) grid = cap;
@@ -386,15 +549,23 @@ extern "C" int rrl_rollout_grid(int N, int num_cu) {
 }
 
 template <class Env, int HT>
-static int launch_rollout(const RolloutArgs& a, int grid, hipStream_t s) {
+static int launch_rollout(const RolloutArgs& a, int grid, bool wide, hipStream_t s) {
   using L = LdsNet<1, HT>;
-  const size_t bytes = (size_t)L::floats(Env::A) * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)rollout_kernel<Env, HT>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    (void)hipFuncSetAttribute((const void*)rollout_kernel<Env, HT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              163840);
+    (void)hipFuncSetAttribute((const void*)rollout_wide_kernel<Env, HT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
     attr = true;
   }
-  hipLaunchKernelGGL((rollout_kernel<Env, HT>), dim3(grid), dim3(256), bytes, s, a);
+  if (wide) {
+    const size_t bytes = ((size_t)((L::floats(Env::A) + 3) & ~3) + 2 * 4 * kMaxAct * 16) * sizeof(float);
+    hipLaunchKernelGGL((rollout_wide_kernel<Env, HT>), dim3(grid), dim3(256), bytes, s, a);
+  } else {
+    const size_t bytes = (size_t)L::floats(Env::A) * sizeof(float);
+    hipLaunchKernelGGL((rollout_kernel<Env, HT>), dim3(grid), dim3(256), bytes, s, a);
+  }
   return (int)hipGetLastError();
 }
 
@@ -407,20 +578,21 @@ extern "C" int rrl_rollout(int env, const float* params, int N, int T, int H, fl
                 (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step0, (uint32_t)(step0 >> 32), reset_all,
                 max_steps};
   const int grid = rrl_rollout_grid(N, num_cu);
+  const bool wide = rollout_wide(N, num_cu);
   hipStream_t s = (hipStream_t)stream;
   if (H == 128) {
     switch (env) {
-      case ENV_CARTPOLE: return launch_rollout<CartPoleEnv, 8>(a, grid, s);
-      case ENV_MOUNTAINCAR: return launch_rollout<MountainCarEnv, 8>(a, grid, s);
-      case ENV_ACROBOT: return launch_rollout<AcrobotEnv, 8>(a, grid, s);
-      case ENV_LUNARLANDER: return launch_rollout<LunarLanderSynthEnv, 8>(a, grid, s);
+      case ENV_CARTPOLE: return launch_rollout<CartPoleEnv, 8>(a, grid, wide, s);
+      case ENV_MOUNTAINCAR: return launch_rollout<MountainCarEnv, 8>(a, grid, wide, s);
+      case ENV_ACROBOT: return launch_rollout<AcrobotEnv, 8>(a, grid, wide, s);
+      case ENV_LUNARLANDER: return launch_rollout<LunarLanderSynthEnv, 8>(a, grid, wide, s);
     }
   } else if (H == 64) {
     switch (env) {
-      case ENV_CARTPOLE: return launch_rollout<CartPoleEnv, 4>(a, grid, s);
-      case ENV_MOUNTAINCAR: return launch_rollout<MountainCarEnv, 4>(a, grid, s);
-      case ENV_ACROBOT: return launch_rollout<AcrobotEnv, 4>(a, grid, s);
-      case ENV_LUNARLANDER: return launch_rollout<LunarLanderSynthEnv, 4>(a, grid, s);
+      case ENV_CARTPOLE: return launch_rollout<CartPoleEnv, 4>(a, grid, wide, s);
+      case ENV_MOUNTAINCAR: return launch_rollout<MountainCarEnv, 4>(a, grid, wide, s);
+      case ENV_ACROBOT: return launch_rollout<AcrobotEnv, 4>(a, grid, wide, s);
+      case ENV_LUNARLANDER: return launch_rollout<LunarLanderSynthEnv, 4>(a, grid, wide, s);
     }
   }
   return -3;
