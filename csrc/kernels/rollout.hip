@@ -175,22 +175,24 @@ __global__ __launch_bounds__(256, 2) void rollout_kernel(RolloutArgs p) {
 // ------------------------------------------------------------------ small-N variant
 // rollout_kernel gives each wave 16 envs and a whole 128x128 layer per step, so a short
 // rollout over few envs (the time-to-threshold config: 1,024 envs = 64 tiles) runs 64 long
-// serial chains on 16 CUs.  Here a workgroup's 4 waves share ONE 16-env tile: every wave
-// keeps the env replica and the full layer 1 (8 MFMAs), computes a quarter of layer 2
-// (HT/4 output tiles) and its partial logits, and the partials meet in LDS (double-buffered
-// by step parity: one barrier per step).  All waves then sum the 4 partials in the same
-// order, so they draw the same action and step identical env replicas; wave 0 writes.
-template <class Env, int HT>
-__global__ __launch_bounds__(256, 2) void rollout_wide_kernel(RolloutArgs p) {
+// serial chains on 16 CUs.  Here a workgroup's WPT = 4 waves share ONE 16-env tile: every
+// wave keeps the env replica and the full layer 1 (HT MFMAs), computes HT/WPT output tiles of layer 2 and their partial logits, and the partials meet in LDS
+// (double-buffered by step parity: one barrier per step).  All waves then sum the WPT
+// partials in the same order, so they draw the same action and step identical env
+// replicas; wave 0 writes.  Measured at 1,024 envs x 64 steps: 340 us (rollout_kernel),
+// 166 us (4 waves per tile), 187 us (8 waves per tile: the per-step barrier and the
+// redundant layer 1 outweigh the shorter layer-2 slice).
+template <class Env, int HT, int WPT>
+__global__ __launch_bounds__(64 * WPT, 1) void rollout_wide_kernel(RolloutArgs p) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int DT = 1;
   using L = LdsNet<DT, HT>;
   constexpr int H = L::H;
   constexpr int D = Env::D, A = Env::A, NS = Env::NS;
-  constexpr int QT = HT / 4;  // layer-2 output tiles per wave
-  static_assert(D <= 16 && HT % 4 == 0, "one input tile, layer 2 split over 4 waves");
+  constexpr int QT = HT / WPT;  // layer-2 output tiles per wave
+  static_assert(D <= 16 && HT % WPT == 0, "one input tile, layer 2 split over the tile's waves");
   stage_net<DT, HT>(lds, p.params, D, A, false);
-  float* part = lds + ((L::floats(A) + 3) & ~3);  // [2 parity][4 waves][kMaxAct][16 envs]
+  float* part = lds + ((L::floats(A) + 3) & ~3);  // [2 parity][WPT waves][kMaxAct][16 envs]
   __syncthreads();
 
   const int l = lane_id();
@@ -242,7 +244,7 @@ __global__ __launch_bounds__(256, 2) void rollout_wide_kernel(RolloutArgs p) {
       floatx4 h1[HT], h2[QT];
       dense_fwd<DT, HT, true>(lds + L::W1, L::S1, lds + L::B1, x, h1, (D + 3) >> 2);
       dense_fwd<HT, QT, true>(lds + L::W2 + 16 * to0 * L::S2, L::S2, lds + L::B2 + 16 * to0, h1, h2);
-      float* pp = part + parity * (4 * kMaxAct * 16);
+      float* pp = part + parity * (WPT * kMaxAct * 16);
 #pragma unroll
       for (int a = 0; a < A; ++a) {
         const float v = head_dot<QT>(lds + L::W3 + a * H + 16 * to0, 0.f, h2);
@@ -254,7 +256,10 @@ __global__ __launch_bounds__(256, 2) void rollout_wide_kernel(RolloutArgs p) {
       for (int a = 0; a < kMaxAct; ++a) {
         if (a < A) {
           const float* q = pp + a * 16 + j;
-          logits[a] = ((q[0] + q[kMaxAct * 16]) + (q[2 * kMaxAct * 16] + q[3 * kMaxAct * 16])) + lds[L::B3 + a];
+          float z = q[0];
+#pragma unroll
+          for (int v = 1; v < WPT; ++v) z += q[v * kMaxAct * 16];  // same order in every wave
+          logits[a] = z + lds[L::B3 + a];
         } else {
           logits[a] = -INFINITY;
         }
@@ -533,7 +538,7 @@ extern "C" int rrl_env_dims(int env, int* D, int* A, int* NS, int* max_steps) {
 }
 
 // Few envs (at most two 16-env tiles per CU): one workgroup per tile, layer 2 split over
-// its 4 waves (rollout_wide_kernel); otherwise 4 tiles per workgroup, one per wave.
+// its waves (rollout_wide_kernel); otherwise 4 tiles per workgroup, one per wave.
 static bool rollout_wide(int N, int num_cu) {
   const int tiles = (N + kTileB - 1) / kTileB;
   return tiles <= 2 * (num_cu > 0 ? num_cu : 256);
@@ -555,13 +560,14 @@ static int launch_rollout(const RolloutArgs& a, int grid, bool wide, hipStream_t
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)rollout_kernel<Env, HT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               163840);
-    (void)hipFuncSetAttribute((const void*)rollout_wide_kernel<Env, HT>,
+    (void)hipFuncSetAttribute((const void*)rollout_wide_kernel<Env, HT, 4>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
     attr = true;
   }
   if (wide) {
-    const size_t bytes = ((size_t)((L::floats(Env::A) + 3) & ~3) + 2 * 4 * kMaxAct * 16) * sizeof(float);
-    hipLaunchKernelGGL((rollout_wide_kernel<Env, HT>), dim3(grid), dim3(256), bytes, s, a);
+    constexpr int WPT = 4;  // 8 waves per tile (one layer-2 output tile each) measured slower: 187 vs 166 us
+    const size_t bytes = ((size_t)((L::floats(Env::A) + 3) & ~3) + 2 * WPT * kMaxAct * 16) * sizeof(float);
+    hipLaunchKernelGGL((rollout_wide_kernel<Env, HT, WPT>), dim3(grid), dim3(64 * WPT), bytes, s, a);
   } else {
     const size_t bytes = (size_t)L::floats(Env::A) * sizeof(float);
     hipLaunchKernelGGL((rollout_kernel<Env, HT>), dim3(grid), dim3(256), bytes, s, a);
