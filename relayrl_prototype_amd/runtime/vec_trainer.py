@@ -34,6 +34,36 @@ DEVICE_ENVS = {"CartPole-v1": 0, "MountainCar-v0": 1, "Acrobot-v1": 2, "LunarLan
 CONTINUOUS_DEVICE_ENVS = {"HalfCheetahSynth-v0"}
 
 
+class SolvedCheck:
+    """Return-threshold test for the time-to-threshold metric: the mean return of the most
+    recent >= ``min_episodes`` finished episodes (gymnasium's CartPole-v1 criterion: mean
+    >= 475 over 100 consecutive episodes), at epoch granularity -- the newest epochs whose
+    episode counts add up to ``min_episodes``.  Feed it VecTrainer.episode_sums() once per
+    epoch; it keeps only the epochs the window can still need."""
+
+    def __init__(self, threshold: float = 475.0, min_episodes: int = 100):
+        self.threshold = threshold
+        self.min_episodes = min_episodes
+        self.hist = []  # (n, s) per epoch, oldest first
+
+    def update(self, n: float, s: float) -> float:
+        """Add one epoch; returns the window mean (NaN until min_episodes have finished)."""
+        self.hist.append((n, s))
+        tn = ts = 0.0
+        keep = 0
+        for en, es in reversed(self.hist):
+            tn += en
+            ts += es
+            keep += 1
+            if tn >= self.min_episodes:
+                break
+        del self.hist[:len(self.hist) - keep]
+        return ts / tn if tn >= self.min_episodes else float("nan")
+
+    def solved(self, mean: float) -> bool:
+        return mean == mean and mean >= self.threshold
+
+
 @dataclass
 class VecTrainerConfig:
     env: str = "CartPole-v1"
@@ -147,11 +177,11 @@ class VecTrainer:
             self.timer.reset()
         return out
 
-    def average_ep_return(self) -> float:
-        """AverageEpRet of the last epoch (global over ranks) from ONE device->host read:
-        the per-epoch check of the time-to-threshold loop.  metrics() reads every column
-        and the learner's loss slabs (~7 synchronising reads, a sizeable share of a 1 ms
-        epoch); this returns the same value metrics()["AverageEpRet"] would."""
+    def episode_sums(self) -> tuple:
+        """(finished episodes, sum of their returns) in the last epoch, global over ranks,
+        from ONE device->host read: the per-epoch check of the time-to-threshold loop.
+        metrics() reads every column and the learner's loss slabs (~7 synchronising reads,
+        a sizeable share of a 1 ms epoch)."""
         ns = self.ep_stats[:, :2].sum(0)
         if self.comm.world > 1:
             ns = ns.double()
@@ -159,6 +189,11 @@ class VecTrainer:
                 ns = ns.cpu()
             self.comm.all_reduce_sum_(ns)
         n, s = ns.tolist()
+        return n, s
+
+    def average_ep_return(self) -> float:
+        """The value metrics()["AverageEpRet"] would return, from one read."""
+        n, s = self.episode_sums()
         return s / n if n > 0 else float("nan")
 
     def state_dict(self) -> dict:

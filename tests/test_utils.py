@@ -206,3 +206,20 @@ def test_server_config_manager(tmp_path, monkeypatch):
     m.assign_free_ports()
     ports = {e["port"] for e in m.as_dict().values()}
     assert len(ports) == 3 and all(int(p) > 0 for p in ports)
+
+
+def test_solved_check_window_of_100_episodes():
+    """bench.py's time-to-threshold criterion: mean of the newest >= 100 finished episodes
+    (whole epochs), NaN until 100 have finished; older epochs are dropped."""
+    import math
+
+    from relayrl_prototype_amd.runtime.vec_trainer import SolvedCheck
+
+    c = SolvedCheck(475.0, min_episodes=100)
+    assert math.isnan(c.update(30, 30 * 480.0))
+    assert math.isnan(c.update(40, 40 * 470.0))
+    m = c.update(50, 50 * 490.0)  # 120 episodes: all three epochs
+    assert abs(m - (30 * 480 + 40 * 470 + 50 * 490) / 120) < 1e-9 and c.solved(m)
+    m = c.update(120, 120 * 400.0)  # the newest epoch alone fills the window
+    assert m == 400.0 and not c.solved(m) and len(c.hist) == 1
+    assert math.isnan(SolvedCheck().update(0, 0.0))

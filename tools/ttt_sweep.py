@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
 """Sweep the time-to-threshold configuration (CartPole-v1, mean return >= 475) of the
-device trainer; one JSON line per (config, seed).  Used to pick bench.py --ttt defaults."""
+device trainer; one JSON line per (config, seed).  Used to pick bench.py --ttt defaults.
+
+    python tools/ttt_sweep.py                       # the original grid (1024-8192 envs)
+    python tools/ttt_sweep.py --grid small --seeds 1 2 3 --max-s 2
+"""
+import argparse
 import itertools
 import json
 import os
@@ -11,34 +16,54 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 
+GRIDS = {
+    # num_envs, rollout_len, vf_iters, pi_lr, vf_lr, gamma, lam
+    "base": (itertools.product([1024, 2048, 4096, 8192], [64, 128], [5, 10, 20], [1e-2, 3e-2], [3e-3],
+                               [0.99], [0.95])),
+    # after the small-N rollout kernel: fewer envs / shorter rollouts got cheaper per step
+    "small": (itertools.product([256, 512, 1024, 2048], [32, 64], [5, 10], [1e-2, 2e-2], [3e-3, 1e-2],
+                                [0.99], [0.95])),
+    # the best of "small" re-run over more seeds
+    "refine": [row + (0.99, 0.95) for row in [
+        (256, 64, 5, 1e-2, 1e-2), (512, 64, 10, 2e-2, 1e-2), (256, 64, 10, 1e-2, 1e-2), (512, 64, 10, 1e-2, 1e-2),
+        (1024, 32, 5, 1e-2, 1e-2), (256, 32, 10, 2e-2, 1e-2), (512, 32, 5, 1e-2, 3e-3), (1024, 64, 5, 1e-2, 1e-2),
+        (1024, 64, 10, 1e-2, 3e-3), (512, 64, 5, 1e-2, 1e-2)]],
+}
+
 
 def ttt(cfg, max_s=20.0, threshold=475.0):
-    from relayrl_prototype_amd.runtime.vec_trainer import VecTrainer
+    from relayrl_prototype_amd.runtime.vec_trainer import SolvedCheck, VecTrainer
 
     tr = VecTrainer(cfg)
+    check = SolvedCheck(threshold, min_episodes=100)  # the same criterion as bench.py
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     while True:
         tr.train_epoch()
-        m = tr.metrics()
+        ret = check.update(*tr.episode_sums())
         el = time.perf_counter() - t0
-        if m["AverageEpRet"] == m["AverageEpRet"] and m["AverageEpRet"] >= threshold:
-            return el, tr.epoch, m["EnvSteps"]
+        if check.solved(ret):
+            return el, tr.epoch, tr.env_steps
         if el > max_s:
-            return None, tr.epoch, m["EnvSteps"]
+            return None, tr.epoch, tr.env_steps
 
 
 def main():
     from relayrl_prototype_amd.runtime.vec_trainer import VecTrainerConfig
 
-    grid = itertools.product([1024, 2048, 4096, 8192], [64, 128], [5, 10, 20], [1e-2, 3e-2])
-    for n, t, vfi, lr in grid:
-        for seed in (7, 8):
-            cfg = VecTrainerConfig(num_envs=n, rollout_len=t, with_baseline=True, pi_lr=lr, vf_lr=3e-3,
-                                   train_vf_iters=vfi, gamma=0.99, lam=0.95, seed=seed)
-            s, ep, steps = ttt(cfg)
-            print(json.dumps({"num_envs": n, "rollout_len": t, "vf_iters": vfi, "pi_lr": lr, "seed": seed,
-                              "ttt_s": s, "epochs": ep, "env_steps": steps}), flush=True)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--grid", choices=sorted(GRIDS), default="base")
+    ap.add_argument("--seeds", type=int, nargs="*", default=[7, 8])
+    ap.add_argument("--max-s", type=float, default=20.0)
+    a = ap.parse_args()
+    for n, t, vfi, lr, vlr, gamma, lam in GRIDS[a.grid]:
+        for seed in a.seeds:
+            cfg = VecTrainerConfig(num_envs=n, rollout_len=t, with_baseline=True, pi_lr=lr, vf_lr=vlr,
+                                   train_vf_iters=vfi, gamma=gamma, lam=lam, seed=seed)
+            s, ep, steps = ttt(cfg, a.max_s)
+            print(json.dumps({"num_envs": n, "rollout_len": t, "vf_iters": vfi, "pi_lr": lr, "vf_lr": vlr,
+                              "gamma": gamma, "lam": lam, "seed": seed, "ttt_s": s, "epochs": ep,
+                              "env_steps": steps}), flush=True)
 
 
 if __name__ == "__main__":
