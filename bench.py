@@ -143,8 +143,8 @@ def main(argv=None):
             "dtype": "fp32",  # value step: 3-way bf16 split of every fp32 operand (bf16x6), fp32-accurate
             "data": "synthetic (on-device CartPole-v1 physics, random-init weights)",
             "config": {
-                "model": f"{algo} MLP[128,128] CartPole-v1 (policy: fp32 MFMA; value step: fp32-accurate "
-                         "bf16x6 split MFMA, csrc/kernels/value_grad.hip)",
+                "model": f"{algo} MLP[128,128] CartPole-v1 (rollout: fp32 MFMA; policy and value steps: "
+                         "fp32-accurate bf16x6 split MFMA, csrc/kernels/value_grad.hip)",
                 "global_batch": steps_per_epoch,
                 "seq_len": cfg.rollout_len,
                 "parallelism": f"dp{world}",

@@ -31,8 +31,11 @@ struct GradArgs {
   int P;
 };
 
-// Weight-stationary bf16x6 value-gradient kernel (value_grad.hip): H = 128, D <= 8.
+// Weight-stationary bf16x6 gradient kernels (value_grad.hip): value head for H = 128,
+// D <= 24; 2-action categorical policy heads (PG / PPO) for H = 128, D <= 8.
 bool value_grad_split_supported(int D, int H);
 int launch_value_grad_split(const GradArgs& a, int grid, hipStream_t s);
+bool policy_grad_split_supported(int D, int H, int A);
+int launch_policy_grad_split(const GradArgs& a, int head, int grid, hipStream_t s);
 
 }  // namespace rrl

@@ -37,6 +37,7 @@
 // form is bitwise reproducible.
 #include "common.h"
 #include "grad_args.h"
+#include "heads.h"
 
 namespace rrl {
 
@@ -47,11 +48,15 @@ typedef short vs16x4 __attribute__((ext_vector_type(4)));
 constexpr int kVgH = 128;
 constexpr int kVgLd = 144;          // bf16 row stride of the activation images
 constexpr int kVgImg = 64 * kVgLd;  // elements per image piece
-// LDS: h1 + dh2 images (3 pieces each), head partials [8][64], x slabs [2][64][DP], b1/b2/w3,
-// then the W2 lo image; DP = 24 (D <= 24) uses 163,328 of the 163,840 bytes.
-constexpr int vg_wlo_bytes(int DP) { return 6 * kVgImg * 2 + 8 * 64 * 4 + 2 * 64 * DP * 4 + 3 * 128 * 4; }
-constexpr int vg_lds_bytes(int DP) { return vg_wlo_bytes(DP) + kVgH * kVgLd * 2; }
-static_assert(vg_lds_bytes(24) <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
+// LDS: h1 + dh2 images (3 pieces each), head partials [8 waves][NA][64], x slabs [2][64][DP],
+// b1 / b2 / w3[NA], then the W2 lo image; DP = 24 (D <= 24) with the value head (NA = 1) uses
+// 163,328 of the 163,840 bytes; the 2-action policy heads (NA = 2) take DP <= 8.
+constexpr int vg_wlo_bytes(int DP, int NA) {
+  return 6 * kVgImg * 2 + 8 * 64 * NA * 4 + 2 * 64 * DP * 4 + (2 + NA) * 128 * 4;
+}
+constexpr int vg_lds_bytes(int DP, int NA) { return vg_wlo_bytes(DP, NA) + kVgH * kVgLd * 2; }
+static_assert(vg_lds_bytes(24, 1) <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
+static_assert(vg_lds_bytes(8, 2) <= 160 * 1024, "policy-grad LDS plan exceeds 160 KB");
 
 struct Split8 {
   vbf16x8 h, m, l;
@@ -210,20 +215,32 @@ RRL_DEV float reduce_scatter16(const float (&v)[16], int j) {
   return keep + dpp_f<kDppXor1>(send);
 }
 
-template <int DP>
+// HEAD: HEAD_VALUE_MSE (one output) or a 2-action categorical policy head (HEAD_PG_CAT /
+// HEAD_PPO_CAT, the CartPole policy step): the same three 128x128 products, only the head
+// (NA outputs reduced over the 8 waves, loss gradient, dW3 / db3 rows) differs.
+template <int DP, int HEAD>
 __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   extern __shared__ __attribute__((aligned(16))) uint16_t vg_lds[];
+  constexpr bool kValue = HEAD == HEAD_VALUE_MSE;
+  constexpr int NA = kValue ? 1 : 2;
   uint16_t* h1img = vg_lds;
   uint16_t* dhimg = vg_lds + 3 * kVgImg;
-  float* red = reinterpret_cast<float*>(vg_lds + 6 * kVgImg);  // [8 waves][64 rows]
-  float* xsb = red + 8 * 64;                                     // [2][64 rows][DP]
-  float* vecs = xsb + 2 * 64 * DP;                               // b1[128] b2[128] w3[128]
+  float* red = reinterpret_cast<float*>(vg_lds + 6 * kVgImg);  // [8 waves][NA][64 rows]
+  float* xsb = red + 8 * NA * 64;                                // [2][64 rows][DP]
+  float* vecs = xsb + 2 * 64 * DP;                               // b1[128] b2[128] w3[NA][128]
   int parity = 0;
   constexpr int KS1 = DP / 4;
   const int l = lane_id();
   const int j = l & 15, g = l >> 4, w = threadIdx.x >> 6;
   const int D = p.D;
-  const FlatOffsets o = flat_offsets(D, kVgH, 1);
+  const FlatOffsets o = flat_offsets(D, kVgH, NA);
+  float adv_mean = 0.f, adv_rstd = 1.f;
+  if (!kValue && p.adv_stats != nullptr) {
+    const float n = fmaxf(p.adv_stats[2], 1.f);
+    adv_mean = p.adv_stats[0] / n;
+    const float var = fmaxf(p.adv_stats[1] / n - adv_mean * adv_mean, 0.f);
+    adv_rstd = 1.f / (sqrtf(var) + 1e-8f);
+  }
   const float* __restrict__ P = p.params;
   const int own = 16 * w;  // this wave's 16 hidden features
 
@@ -249,7 +266,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     wB[c].h = sb.h;
     wB[c].m = sb.m;
   }
-  uint16_t* w2lo = vg_lds + vg_wlo_bytes(DP) / 2;
+  uint16_t* w2lo = vg_lds + vg_wlo_bytes(DP, NA) / 2;
   for (int q = threadIdx.x; q < kVgH * kVgH / 4; q += blockDim.x) {
     floatx4 v;
 #pragma unroll
@@ -264,24 +281,29 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     const int k = 4 * s + g;
     w1a[s] = (k < D) ? P[o.w1 + (own + j) * D + k] : 0.f;
   }
-  for (int q = threadIdx.x; q < 3 * kVgH; q += blockDim.x) {
+  for (int q = threadIdx.x; q < (2 + NA) * kVgH; q += blockDim.x) {
     const int k = q >> 7, f = q & (kVgH - 1);
-    vecs[q] = P[(k == 0 ? o.b1 : k == 1 ? o.b2 : o.w3) + f];
+    vecs[q] = P[(k == 0 ? o.b1 : k == 1 ? o.b2 : o.w3 + (k - 2) * kVgH) + f];
   }
-  const float b3 = P[o.b3];
+  float b3[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) b3[a] = P[o.b3 + a];
   // per C-layout row own + 4g + r (re-read from LDS where used: registers are the limit)
   const float* b1p = vecs + own + 4 * g;
   const float* b2p = vecs + kVgH + own + 4 * g;
   const float* w3p = vecs + 2 * kVgH + own + 4 * g;
 
   floatx4 acc2[8];
-  float accv = 0.f;  // entry j of [db2 | dW3 | db1 | -] (4 rows each), summed over the batch lanes
+  float accv = 0.f;  // entry j of [db2 | dW3 row 0 | db1 | dW3 row 1 (NA = 2)] (4 features each), batch-summed
   float acc1[DP / 4];  // dW1[own + 4g + (j & 3)][4 d4 + (j >> 2)], summed over the batch lanes
 #pragma unroll
   for (int it = 0; it < 8; ++it) acc2[it] = zero4();
 #pragma unroll
   for (int d4 = 0; d4 < DP / 4; ++d4) acc1[d4] = 0.f;
-  float bacc3 = 0.f, s_loss = 0.f, s_val = 0.f, s_cnt = 0.f;
+  float bacc3[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) bacc3[a] = 0.f;
+  float s_loss = 0.f, s_val = 0.f, s_cnt = 0.f, s_ent = 0.f, s_kl = 0.f, s_clip = 0.f;
 
   for (int base = blockIdx.x * 64; base < p.B; base += gridDim.x * 64) {
     // ------------------------------------------------------------ x slab -> LDS
@@ -341,39 +363,91 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       for (int r = 0; r < 4; ++r) h2[bt][r] = h2[bt][r] > 0.f ? h2[bt][r] : 0.f;
     }
 
-    // ------------------------------------------------------------ value head
-    floatx4 w3v = *reinterpret_cast<const floatx4*>(w3p);
+    // ------------------------------------------------------------ head
+    floatx4 w3v[NA];
 #pragma unroll
-    for (int bt = 0; bt < 4; ++bt) {
-      float pv = w3v[0] * h2[bt][0];
-      pv = fmaf(w3v[1], h2[bt][1], pv);
-      pv = fmaf(w3v[2], h2[bt][2], pv);
-      pv = fmaf(w3v[3], h2[bt][3], pv);
-      pv = group_sum(pv);
-      if (g == bt) red[w * 64 + 16 * bt + j] = pv;
+    for (int a = 0; a < NA; ++a) {
+      w3v[a] = *reinterpret_cast<const floatx4*>(w3p + a * kVgH);
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+        float pv = w3v[a][0] * h2[bt][0];
+        pv = fmaf(w3v[a][1], h2[bt][1], pv);
+        pv = fmaf(w3v[a][2], h2[bt][2], pv);
+        pv = fmaf(w3v[a][3], h2[bt][3], pv);
+        pv = group_sum(pv);
+        if (g == bt) red[(w * NA + a) * 64 + 16 * bt + j] = pv;
+      }
     }
     __syncthreads();
-    float dout[4];
+    float dout[4][NA];
 #pragma unroll
     for (int bt = 0; bt < 4; ++bt) {
       const int rl = 16 * bt + j, b = base + rl;
-      const float v = (((red[rl] + red[64 + rl]) + (red[128 + rl] + red[192 + rl])) +
-                       ((red[256 + rl] + red[320 + rl]) + (red[384 + rl] + red[448 + rl]))) + b3;
       const bool ok = b < p.B;
-      const float diff = v - (ok ? p.ret[min(b, p.B - 1)] : 0.f);
-      dout[bt] = ok ? 2.f * diff * p.inv_B : 0.f;
-      if (w == 0 && g == 0) {
-        bacc3 += dout[bt];
-        if (ok) {
+      const int bc = min(b, p.B - 1);
+      float outv[NA];
+#pragma unroll
+      for (int a = 0; a < NA; ++a) {
+        const float* r = red + a * 64 + rl;
+        constexpr int S = NA * 64;  // wave stride
+        outv[a] = (((r[0] + r[S]) + (r[2 * S] + r[3 * S])) + ((r[4 * S] + r[5 * S]) + (r[6 * S] + r[7 * S]))) + b3[a];
+      }
+      if (kValue) {
+        const float v = outv[0];
+        const float diff = v - (ok ? p.ret[bc] : 0.f);
+        dout[bt][0] = ok ? 2.f * diff * p.inv_B : 0.f;
+        if (w == 0 && g == 0 && ok) {
           s_loss += diff * diff;
           s_val += v;
           s_cnt += 1.f;
         }
+      } else {
+        // categorical policy head (mlp_grad.hip HEAD_PG_CAT / HEAD_PPO_CAT, REINFORCE.py:141-152)
+        float logits[kMaxAct];
+#pragma unroll
+        for (int a = 0; a < kMaxAct; ++a) logits[a] = a < NA ? outv[a] : -INFINITY;
+        if (ok) apply_mask(p.mask ? p.mask + (size_t)bc * NA : nullptr, NA, logits);
+        const CatStats cs = cat_stats(NA, logits);
+        const int act = ok ? p.act[bc] : 0;
+        const float logp = pick_logit(NA, logits, act) - cs.lse;
+        const float adv = ((ok ? p.adv[bc] : 0.f) - adv_mean) * adv_rstd;
+        float dlogp, loss_i;
+        if (HEAD == HEAD_PG_CAT) {
+          dlogp = -adv;
+          loss_i = -logp * adv;
+        } else {
+          const float lpo = ok ? p.logp_old[bc] : logp;
+          const float ratio = __expf(logp - lpo);
+          const float s1 = ratio * adv;
+          const float s2 = fminf(fmaxf(ratio, 1.f - p.clip_eps), 1.f + p.clip_eps) * adv;
+          dlogp = (s1 <= s2) ? -adv * ratio : 0.f;
+          loss_i = -fminf(s1, s2);
+          if (w == 0 && g == 0 && ok) s_clip += (fabsf(ratio - 1.f) > p.clip_eps) ? 1.f : 0.f;
+        }
+        const float scale = ok ? p.inv_B : 0.f;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+          const float lpa = logits[a] - cs.lse;
+          const float pa = __expf(lpa);
+          const float dpg = dlogp * ((a == act ? 1.f : 0.f) - pa);
+          const float dent = pa > 0.f ? p.ent_coef * pa * (lpa + cs.entropy) : 0.f;
+          dout[bt][a] = scale * (dpg + dent);
+        }
+        if (w == 0 && g == 0 && ok) {
+          s_loss += loss_i;
+          s_ent += cs.entropy;
+          if (p.logp_old) s_kl += p.logp_old[bc] - logp;
+          s_cnt += 1.f;
+        }
+      }
+      if (w == 0 && g == 0) {
+#pragma unroll
+        for (int a = 0; a < NA; ++a) bacc3[a] += dout[bt][a];
       }
     }
 
     // ------------------------------------------------------------ dh2, dW3, db2
-    float tv[16];  // this slab's [db2 | dW3 | db1 | -] partials of rows own + 4g + r
+    float tv[16];  // this slab's [db2 | dW3 row 0 | db1 | dW3 row 1] partials of features own + 4g + r
 #pragma unroll
     for (int q = 0; q < 16; ++q) tv[q] = 0.f;
 #pragma unroll
@@ -381,9 +455,12 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       floatx4 d;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        d[r] = h2[bt][r] > 0.f ? w3v[r] * dout[bt] : 0.f;
+        float s3 = w3v[0][r] * dout[bt][0];
+        if (NA == 2) s3 = fmaf(w3v[NA - 1][r], dout[bt][NA - 1], s3);
+        d[r] = h2[bt][r] > 0.f ? s3 : 0.f;
         tv[r] += d[r];
-        tv[4 + r] = fmaf(dout[bt], h2[bt][r], tv[4 + r]);
+        tv[4 + r] = fmaf(dout[bt][0], h2[bt][r], tv[4 + r]);
+        if (NA == 2) tv[12 + r] = fmaf(dout[bt][NA - 1], h2[bt][r], tv[12 + r]);
       }
       store_split(dhimg, 16 * bt + j, own + 4 * g, d);
     }
@@ -471,6 +548,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   {
     const int f = own + 4 * g + (j & 3), k = j >> 2;
     if (k < 3) slab[(k == 0 ? o.b2 : k == 1 ? o.w3 : o.b1) + f] = accv;
+    if (NA == 2 && k == 3) slab[o.w3 + kVgH + f] = accv;
   }
 #pragma unroll
   for (int d4 = 0; d4 < DP / 4; ++d4) {
@@ -478,15 +556,19 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     if (dd < D) slab[o.w1 + f * D + dd] = acc1[d4];
   }
   if (w == 0) {
-    const float vb3 = wave_sum(bacc3);
+    float vb3[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) vb3[a] = wave_sum(bacc3[a]);
     const float sl = wave_sum(s_loss), sv = wave_sum(s_val), sc = wave_sum(s_cnt);
+    const float se = wave_sum(s_ent), sk = wave_sum(s_kl), scl = wave_sum(s_clip);
     if (l == 0) {
-      slab[o.b3] = vb3;
+#pragma unroll
+      for (int a = 0; a < NA; ++a) slab[o.b3 + a] = vb3[a];
       float* ls = p.loss_slab + blockIdx.x * 8;
       ls[0] = sl;
-      ls[1] = 0.f;
-      ls[2] = 0.f;
-      ls[3] = 0.f;
+      ls[1] = se;
+      ls[2] = sk;
+      ls[3] = scl;
       ls[4] = sv;
       ls[5] = sc;
     }
@@ -494,24 +576,34 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 }
 
 bool value_grad_split_supported(int D, int H) { return H == kVgH && D >= 1 && D <= 24; }
+bool policy_grad_split_supported(int D, int H, int A) { return H == kVgH && D >= 1 && D <= 8 && A == 2; }
 
-template <int DP>
+template <int DP, int HEAD>
 static int launch_vg(const GradArgs& a, int grid, hipStream_t s) {
+  constexpr int NA = HEAD == HEAD_VALUE_MSE ? 1 : 2;
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              vg_lds_bytes(DP));
+    (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP, HEAD>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, vg_lds_bytes(DP, NA));
     attr_set = true;
   }
-  hipLaunchKernelGGL((value_grad_split_kernel<DP>), dim3(grid), dim3(512), vg_lds_bytes(DP), s, a);
+  hipLaunchKernelGGL((value_grad_split_kernel<DP, HEAD>), dim3(grid), dim3(512), vg_lds_bytes(DP, NA), s, a);
   return (int)hipGetLastError();
 }
 
 int launch_value_grad_split(const GradArgs& a, int grid, hipStream_t s) {
-  if (a.D <= 4) return launch_vg<4>(a, grid, s);
-  if (a.D <= 8) return launch_vg<8>(a, grid, s);
-  if (a.D <= 16) return launch_vg<16>(a, grid, s);
-  return launch_vg<24>(a, grid, s);  // HalfCheetahSynth (D = 17)
+  if (a.D <= 4) return launch_vg<4, HEAD_VALUE_MSE>(a, grid, s);
+  if (a.D <= 8) return launch_vg<8, HEAD_VALUE_MSE>(a, grid, s);
+  if (a.D <= 16) return launch_vg<16, HEAD_VALUE_MSE>(a, grid, s);
+  return launch_vg<24, HEAD_VALUE_MSE>(a, grid, s);  // HalfCheetahSynth (D = 17)
+}
+
+// 2-action categorical policy step (CartPole: REINFORCE / A2C / PPO policy gradient).
+int launch_policy_grad_split(const GradArgs& a, int head, int grid, hipStream_t s) {
+  if (head == HEAD_PG_CAT) return a.D <= 4 ? launch_vg<4, HEAD_PG_CAT>(a, grid, s) : launch_vg<8, HEAD_PG_CAT>(a, grid, s);
+  if (head == HEAD_PPO_CAT)
+    return a.D <= 4 ? launch_vg<4, HEAD_PPO_CAT>(a, grid, s) : launch_vg<8, HEAD_PPO_CAT>(a, grid, s);
+  return -2;
 }
 
 }  // namespace rrl

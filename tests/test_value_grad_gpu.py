@@ -118,3 +118,79 @@ def test_deterministic(cuda, D, B):
             assert torch.equal(s, ref)
     finally:
         set_value_grad_mode(old)
+
+
+def _pg64(head, pp, X, A, H, mask, act, adv, logp_old, stats, inv_B, clip, ent_coef):
+    """float64 autograd gradient of the categorical PG / PPO loss (mlp_grad.hip semantics:
+    normalised advantages, masked logits, entropy bonus, true log_softmax log-probs)."""
+    D = X.shape[1]
+    p = pp.double().clone().requires_grad_(True)
+    o = 0
+    W1 = p[o:o + H * D].view(H, D); o += H * D
+    b1 = p[o:o + H]; o += H
+    W2 = p[o:o + H * H].view(H, H); o += H * H
+    b2 = p[o:o + H]; o += H
+    W3 = p[o:o + A * H].view(A, H); o += A * H
+    b3 = p[o:o + A]
+    h = torch.relu(torch.relu(X.double() @ W1.T + b1) @ W2.T + b2)
+    lsm = torch.log_softmax(h @ W3.T + b3 + (mask.double() - 1.0) * 1e8, -1)
+    logp = lsm.gather(1, act.long()[:, None])[:, 0]
+    n = float(stats[2])
+    mean = float(stats[0]) / n
+    var = max(float(stats[1]) / n - mean * mean, 0.0)
+    advn = (adv.double() - mean) / (var ** 0.5 + 1e-8)
+    if head == "PG_CAT":
+        li = -logp * advn
+    else:
+        ratio = torch.exp(logp - logp_old.double())
+        li = -torch.minimum(ratio * advn, torch.clamp(ratio, 1 - clip, 1 + clip) * advn)
+    ent = -(lsm.exp() * lsm).sum(-1)
+    ((li.sum() - ent_coef * ent.sum()) * inv_B).backward()
+    return p.grad.detach()
+
+
+@pytest.mark.parametrize("head", ["PG_CAT", "PPO_CAT"])
+@pytest.mark.parametrize("D,B", [(4, 5000), (4, 70000), (3, 777), (8, 33000)])
+def test_policy_split_kernel_matches_oracle(cuda, head, D, B):
+    """The 2-action categorical policy heads on the bf16x6 kernel (CartPole's policy step)
+    against the fp32-MFMA kernel and the autograd oracle: masks, advantage normalisation,
+    PPO ratio clipping, entropy bonus and the loss statistics."""
+    H, A = 128, 2
+    hd = getattr(GradHead, head)
+    g = torch.Generator().manual_seed(D * 31 + B)
+    spec = MLPSpec(D, H, A, False)
+    pp = spec.init(g)
+    pp = pp + 0.05 * torch.randn(pp.shape, generator=g)
+    X = torch.randn(B, D, generator=g) * 1.5
+    keep = _away_from_relu_kinks(pp, X, D, H)
+    X = X[keep]
+    B = X.shape[0]
+    act = torch.randint(0, A, (B,), generator=g, dtype=torch.int32)
+    adv = torch.randn(B, generator=g) * 3 + 0.5
+    mask = torch.ones(B, A)
+    mask[torch.arange(B) % 97 == 5, 1] = 0.0
+    act[torch.arange(B) % 97 == 5] = 0
+    logp_old = -torch.rand(B, generator=g) * 1.2 - 0.05
+    stats = torch.tensor([adv.sum().item(), (adv * adv).sum().item(), float(B)])
+    kw = dict(mask=mask, act=act, adv=adv, logp_old=logp_old, adv_stats=stats, inv_B=1.0 / B, clip_eps=0.2,
+              ent_coef=0.01)
+    g_ref = _pg64(head, pp, X, A, H, mask, act, adv, logp_old, stats, 1.0 / B, 0.2, 0.01)
+    out = {}
+    for mode in (1, 0):
+        old = set_value_grad_mode(mode)
+        try:
+            kwc = {k: (v.to(cuda) if torch.is_tensor(v) else v) for k, v in kw.items()}
+            slab, loss = mlp_grad(hd, pp.to(cuda), X.to(cuda), A, H, **kwc)
+            torch.cuda.synchronize()
+        finally:
+            set_value_grad_mode(old)
+        out[mode] = (slab.sum(0, dtype=torch.float64).cpu(), loss.sum(0).cpu())
+    scale = g_ref.abs().max().item()
+    err_split = (out[1][0] - g_ref).abs().max().item() / scale
+    err_fp32 = (out[0][0] - g_ref).abs().max().item() / scale
+    assert err_fp32 < 1e-5, err_fp32
+    assert err_split < 1e-5, (err_split, err_fp32)
+    ls, lf = out[1][1], out[0][1]
+    assert int(ls[5].item()) == B and int(lf[5].item()) == B
+    for k, name in ((0, "loss"), (1, "entropy"), (2, "kl"), (3, "clipfrac")):
+        assert abs(ls[k].item() - lf[k].item()) <= 1e-4 * max(1.0, abs(lf[k].item())), (name, ls[k], lf[k])
