@@ -595,7 +595,8 @@ int launch_value_grad_split(const GradArgs& a, int grid, hipStream_t s) {
   if (a.D <= 4) return launch_vg<4, HEAD_VALUE_MSE>(a, grid, s);
   if (a.D <= 8) return launch_vg<8, HEAD_VALUE_MSE>(a, grid, s);
   if (a.D <= 16) return launch_vg<16, HEAD_VALUE_MSE>(a, grid, s);
-  return launch_vg<24, HEAD_VALUE_MSE>(a, grid, s);  // HalfCheetahSynth (D = 17)
+  if (a.D <= 20) return launch_vg<20, HEAD_VALUE_MSE>(a, grid, s);  // HalfCheetahSynth (D = 17)
+  return launch_vg<24, HEAD_VALUE_MSE>(a, grid, s);
 }
 
 // 2-action categorical policy step (CartPole: REINFORCE / A2C / PPO policy gradient).
