@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 kernel-trace database (or kernel_stats.csv) per kernel."""
+import csv
 import sqlite3
 import sys
 import re
@@ -10,7 +11,19 @@ def short(n):
     return n[:90]
 
 
+def main_csv(path):
+    rows = list(csv.DictReader(open(path)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    print(f"{'total ms':>9s} {'calls':>6s} {'avg us':>9s} {'pct':>5s}  kernel")
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
+        t, n = float(r["TotalDurationNs"]), int(r["Calls"])
+        print(f"{t / 1e6:9.2f} {n:6d} {t / n / 1e3:9.1f} {100 * t / tot:5.1f}  {r['Name'][:100]}")
+    print(f"total GPU kernel time {tot / 1e6:.2f} ms")
+
+
 def main(path):
+    if path.endswith(".csv"):
+        return main_csv(path)
     c = sqlite3.connect(path)
     cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
     name_col = "kernel_name" if "kernel_name" in cols else ("name" if "name" in cols else None)
