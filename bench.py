@@ -1,29 +1,40 @@
 #!/usr/bin/env python3
-"""Flagship benchmark: CartPole-v1 REINFORCE (+ value baseline), env steps/sec (whole node).
+"""Flagship benchmark: CartPole-v1 REINFORCE (+ value baseline), env steps/sec (whole node)
++ wall-clock to the return threshold.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is
-launched under ``torch.distributed.run`` with one rank per GPU (RCCL).  One "step" is
-one full training epoch of the on-device actor+learner (runtime/vec_trainer.py):
-rollout of num_envs x rollout_len env steps per GPU (policy forward + sampling + env
-physics in one fused kernel) + GAE scan + 1 policy Adam step + 80 value Adam steps
-(the reference REINFORCE.train_model, REINFORCE.py:97-125).  Nothing is skipped inside
-the timed region.  Weak scaling: per-GPU envs are fixed as N grows; gradients are
-all-reduced over RCCL every optimiser step.
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``.  For N > 1 the driver
+launches it under ``torch.distributed.run`` (one rank per GPU, RCCL); run WITHOUT a launcher
+and ``--gpus N > 1``, this script starts ``torch.distributed.run`` itself as a CHILD process
+(nothing touches the GPU first; never an exec) and relays rank 0's JSON line.
 
-BASELINE.md: the reference publishes no numbers, so ``vs_baseline`` is null.
-The second half of the metric, wall-clock to the CartPole-v1 return threshold (475), is
-measured after the timed steps (median over ``--ttt-seeds`` seeds) on a single GPU by
-default (``--ttt`` forces it with several ranks, ``--no-ttt`` skips it).
+One "step" is one full training epoch of the on-device actor + learner
+(runtime/vec_trainer.py): a rollout of num_envs x rollout_len env steps per GPU (policy
+forward + sampling + env physics in one fused kernel) + value forward + GAE scan + 1 policy
+Adam step + 80 value Adam steps (the reference REINFORCE.train_model, REINFORCE.py:97-125),
+with one RCCL all-reduce of the flat gradient per optimiser step across ranks.  Nothing is
+skipped inside the timed region.  Weak scaling: per-GPU envs are fixed as N grows.
+
+BASELINE.md: the reference publishes no numbers, so ``vs_baseline`` is null.  The second
+half of the metric, wall-clock to CartPole-v1 solved (mean return of the newest >= 100
+episodes >= 475), is measured through the reference API -- the clock starts at
+``TrainingServer(..., engine="vec")`` construction and stops at the first epoch that meets
+the criterion -- with the tuned config AND the reference hyperparameters (gamma .98, lam .97,
+pi lr 3e-4, V lr 1e-3, 80 value iterations), median over seeds, after the timed steps.
+``benchmarks/reference_equivalent_cpu.py`` (the reference's per-step CPU pipeline, same
+criterion) runs concurrently in a child process and is reported next to them.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 METRIC = "env steps/sec (whole node) + wall-clock to return threshold, CartPole REINFORCE"
+REPO = os.path.dirname(os.path.abspath(__file__))
 
 
 def parse(argv=None):
@@ -36,8 +47,10 @@ def parse(argv=None):
     ap.add_argument("--no-baseline", action="store_true", help="REINFORCE without the value baseline")
     ap.add_argument("--vf-iters", type=int, default=80)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--device", choices=("gpu", "cpu"), default="gpu",
+                    help="cpu = plumbing check of the multi-rank path with the host engine (not a benchmark)")
     ap.add_argument("--ttt", action="store_true",
-                    help="also measure wall-clock to AverageEpRet >= 475 (default on a single GPU)")
+                    help="also measure wall-clock to the threshold with several ranks (default: one GPU only)")
     ap.add_argument("--no-ttt", action="store_true", help="skip the time-to-threshold measurement")
     ap.add_argument("--ttt-envs", type=int, default=1024)
     ap.add_argument("--ttt-rollout-len", type=int, default=64)
@@ -45,92 +58,185 @@ def parse(argv=None):
     ap.add_argument("--ttt-pi-lr", type=float, default=1e-2)
     ap.add_argument("--ttt-vf-lr", type=float, default=1e-2)
     ap.add_argument("--ttt-graphs", action="store_true",
-                    help="capture the 5-iteration value loop as a hipGraph in the TTT runs (eager is faster "
-                         "there: the capture costs ~0.45 ms in the first epoch, tools/ttt_graph_probe.py)")
+                    help="capture the value loop as a hipGraph in the tuned TTT runs (eager is faster there: "
+                         "the capture costs ~0.45 ms in the first epoch, tools/ttt_graph_probe.py)")
     ap.add_argument("--ttt-seeds", type=int, default=10, help="report the median over this many seeds")
+    ap.add_argument("--ttt-ref-seeds", type=int, default=5, help="seeds of the reference-hyperparameter TTT")
     ap.add_argument("--ttt-max-s", type=float, default=30.0, help="give up on a seed after this many seconds")
+    ap.add_argument("--ref-cpu-seconds", type=float, default=150.0,
+                    help="budget of the concurrent reference-equivalent CPU run (0 = skip)")
     return ap.parse_args(argv)
 
 
-def time_to_threshold(args, comm, threshold=475.0):
-    """Wall-clock (trainer construction starts -> first epoch at which the most recent >= 100
-    finished episodes average >= 475, the gymnasium CartPole-v1 criterion)
-    for ``--ttt-seeds`` seeds; returns (median_s, [per-seed s], median epochs, median env steps).
-    Configuration from tools/ttt_sweep.py --grid small / refine (10/10 seeds solved on MI355X,
-    profiles/r1_ttt_sweep_refine.jsonl)."""
+# ---------------------------------------------------------------------- launcher (no GPU here)
+def spawn_ranks(argv) -> int:
+    """torch.distributed.run as a CHILD (one rank per GPU, 127.0.0.1 rendezvous); its stdout is
+    inherited, so rank 0's JSON line is this process's output."""
+    import socket
+
+    a = parse(argv)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["PYTHONPATH"] = REPO + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------------- time to threshold
+def _ttt_config_file(tmp: str) -> str:
+    import socket
+
+    from relayrl_prototype_amd.config import DEFAULT_CONFIG_CONTENT
+
+    cfg = json.loads(DEFAULT_CONFIG_CONTENT)
+    for k in ("training_server", "trajectory_server", "agent_listener"):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        cfg["server"][k]["port"] = str(s.getsockname()[1])
+        s.close()
+    p = os.path.join(tmp, "relayrl_config.json")
+    with open(p, "w") as f:
+        json.dump(cfg, f)
+    return p
+
+
+def time_to_threshold(hp: dict, mi355x: dict, seeds: int, max_s: float, comm, threshold: float = 475.0):
+    """Per seed: the clock starts at TrainingServer(..., engine="vec") construction (BASELINE.md:
+    "from TrainingServer start") and stops after the first epoch whose newest >= 100 finished
+    episodes average >= threshold (gymnasium CartPole-v1).  Returns (median s, per-seed s,
+    median epochs, median env steps)."""
     import statistics
 
     import torch
-    from relayrl_prototype_amd.runtime.vec_trainer import SolvedCheck, VecTrainer, VecTrainerConfig
 
+    from relayrl_prototype_amd.api.server import TrainingServer
+
+    os.environ.setdefault("RRL_QUIET_CONFIG", "1")
     times, epochs, steps = [], [], []
-    for seed in range(1, args.ttt_seeds + 1):
-        cfg = VecTrainerConfig(num_envs=args.ttt_envs, rollout_len=args.ttt_rollout_len, with_baseline=True,
-                               pi_lr=args.ttt_pi_lr, vf_lr=args.ttt_vf_lr, train_vf_iters=args.ttt_vf_iters,
-                               gamma=0.99, lam=0.95, seed=seed, use_graphs=args.ttt_graphs)
-        comm.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()  # the clock includes building the trainer (BASELINE.md: from server start)
-        tr = VecTrainer(cfg, comm)
-        check = SolvedCheck(threshold, min_episodes=100)
-        while True:
-            tr.train_epoch()
-            ret = check.update(*tr.episode_sums())  # one D2H read per epoch
-            el = time.perf_counter() - t0
-            if check.solved(ret):
-                times.append(el)
-                break
-            if el > args.ttt_max_s:
-                times.append(float("inf"))
-                break
-        epochs.append(tr.epoch)
-        steps.append(tr.env_steps * comm.world)
-        del tr
+    with tempfile.TemporaryDirectory() as tmp:
+        cfgp = _ttt_config_file(tmp)
+        for seed in range(1, seeds + 1):
+            h = dict(hp, seed=seed)
+            h.update({k: v for k, v in mi355x.items()})
+            comm.barrier()
+            torch.cuda.synchronize()
+            srv = TrainingServer("REINFORCE", 4, 2, 1000, env_dir=os.path.join(tmp, f"env{seed}"), config_path=cfgp,
+                                 server_type="local", hyperparams=h, engine="vec")
+            try:
+                r = srv.train(target_return=threshold, window=100, max_seconds=max_s, log_every=0, publish_every=0)
+            finally:
+                srv.close(save=False)
+            times.append(r.time_to_threshold_s if r.solved else float("inf"))
+            epochs.append(r.epochs)
+            steps.append(r.env_steps)
     med = statistics.median(times)
     return (None if med == float("inf") else med), times, int(statistics.median(epochs)), int(statistics.median(steps))
 
 
+def start_reference_cpu(seconds: float):
+    if seconds <= 0:
+        return None
+    cmd = [sys.executable, os.path.join(REPO, "benchmarks", "reference_equivalent_cpu.py"), "--seconds",
+           str(seconds), "--window", "100"]
+    env = dict(os.environ)
+    env["PYTHONPATH"] = REPO + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    env["HIP_VISIBLE_DEVICES"] = ""  # CPU only: never touches the GPU
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    return subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+
+
+def collect_reference_cpu(proc, budget_s: float):
+    if proc is None:
+        return None
+    try:
+        out, _ = proc.communicate(timeout=budget_s + 60)
+    except subprocess.TimeoutExpired:
+        proc.kill()
+        return None
+    for line in reversed(out.strip().splitlines()):
+        try:
+            return json.loads(line)
+        except ValueError:
+            continue
+    return None
+
+
+# ---------------------------------------------------------------------- main
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        return spawn_ranks(argv)
+    if world_env is not None and int(world_env) != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world_env} but --gpus {args.gpus}; launch one rank per GPU")
     import torch
 
-    from relayrl_prototype_amd.parallel.comm import init_distributed
+    from relayrl_prototype_amd.parallel.comm import init_distributed, local_device_index
 
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if world_env > 1:
+    on_gpu = args.device == "gpu"
+    if int(world_env or 1) > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     comm = init_distributed()
-    from relayrl_prototype_amd.parallel.comm import local_device_index
+    world = comm.world
+    rank = comm.rank
+    ref_proc = start_reference_cpu(args.ref_cpu_seconds) if (rank == 0 and world == 1 and on_gpu) else None
+    if on_gpu:
+        torch.cuda.set_device(local_device_index())
+        from relayrl_prototype_amd.runtime.vec_trainer import VecTrainer, VecTrainerConfig
 
-    local = local_device_index()
-    torch.cuda.set_device(local)
-    from relayrl_prototype_amd.runtime.vec_trainer import VecTrainer, VecTrainerConfig
+        cfg = VecTrainerConfig(num_envs=args.num_envs, rollout_len=args.rollout_len,
+                               with_baseline=not args.no_baseline, train_vf_iters=args.vf_iters,
+                               use_graphs=not args.no_graphs)
+        tr = VecTrainer(cfg, comm)
+        sync = torch.cuda.synchronize
+        dev = "cuda"
+    else:
+        from relayrl_prototype_amd.runtime.host_trainer import HostTrainerConfig, HostVecTrainer
 
-    cfg = VecTrainerConfig(num_envs=args.num_envs, rollout_len=args.rollout_len, with_baseline=not args.no_baseline,
-                           train_vf_iters=args.vf_iters, use_graphs=not args.no_graphs)
-    tr = VecTrainer(cfg, comm)
+        cfg = HostTrainerConfig(num_envs=args.num_envs, rollout_len=args.rollout_len,
+                                with_baseline=not args.no_baseline, train_vf_iters=args.vf_iters, num_threads=1,
+                                gamma=0.98, lam=0.97)
+        tr = HostVecTrainer(cfg, comm, device="cpu")
+        sync = lambda: None  # noqa: E731
+        dev = "cpu"
     for _ in range(args.warmup):
         tr.train_epoch()
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tr.train_epoch()
     comm.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    sync()
+    dt_local = time.perf_counter() - t0
+    t = torch.tensor([dt_local], dtype=torch.float64, device=dev)
     comm.all_reduce_max_(t)
     dt = float(t.item())
     m = tr.metrics()
-    world = comm.world
     steps_per_epoch = cfg.num_envs * cfg.rollout_len * world
     value = steps_per_epoch * args.steps / dt
-    ttt = None
-    do_ttt = (args.ttt or comm.world == 1) and not args.no_ttt
+    per_rank = comm.all_gather_object(round(cfg.num_envs * cfg.rollout_len * args.steps / dt_local, 1))
+    ttt = ttt_ref = None
+    do_ttt = on_gpu and (args.ttt or world == 1) and not args.no_ttt
     if do_ttt:
-        ttt = time_to_threshold(args, comm)
-    if comm.rank == 0:
+        del tr
+        torch.cuda.empty_cache()
+        tuned = {"with_vf_baseline": True, "train_vf_iters": args.ttt_vf_iters, "pi_lr": args.ttt_pi_lr,
+                 "vf_lr": args.ttt_vf_lr, "gamma": 0.99, "lam": 0.95}
+        ref_hp = {"with_vf_baseline": True, "train_vf_iters": 80, "pi_lr": 3e-4, "vf_lr": 1e-3, "gamma": 0.98,
+                  "lam": 0.97}
+        shape = {"num_envs": args.ttt_envs, "rollout_len": args.ttt_rollout_len}
+        ttt = time_to_threshold(tuned, dict(shape, use_graphs=bool(args.ttt_graphs)), args.ttt_seeds,
+                                args.ttt_max_s, comm)
+        ttt_ref = time_to_threshold(ref_hp, dict(shape, use_graphs=True), args.ttt_ref_seeds, args.ttt_max_s, comm)
+    ref_cpu = collect_reference_cpu(ref_proc, args.ref_cpu_seconds)
+    if rank == 0:
         algo = "REINFORCE" if args.no_baseline else "REINFORCE-with-baseline"
         rec = {
             "metric": METRIC,
@@ -143,8 +249,9 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",  # value step: 3-way bf16 split of every fp32 operand (bf16x6), fp32-accurate
-            "data": "synthetic (on-device CartPole-v1 physics, random-init weights)",
+            "dtype": "fp32",  # value / policy steps: 3-way bf16 split of every fp32 operand (bf16x6), fp32-accurate
+            "data": ("synthetic (on-device CartPole-v1 physics, random-init weights)" if on_gpu else
+                     "CPU plumbing check of the multi-rank path (host engine, oracle ops) -- not a benchmark"),
             "config": {
                 "model": f"{algo} MLP[128,128] CartPole-v1 (rollout: fp32 MFMA; policy and value steps: "
                          "fp32-accurate bf16x6 split MFMA, csrc/kernels/value_grad.hip)",
@@ -155,30 +262,39 @@ def main(argv=None):
                 "train_vf_iters": cfg.train_vf_iters if cfg.with_baseline else 0,
                 "hyperparams": "reference defaults (gamma .98, lam .97, pi_lr 3e-4, vf_lr 1e-3)",
             },
+            "backend": comm.backend,
+            "rccl_world": world if comm.backend == "nccl" else 0,
+            "per_rank_env_steps_per_s": per_rank,
             "final_avg_ep_ret": None if m["AverageEpRet"] != m["AverageEpRet"] else round(m["AverageEpRet"], 2),
         }
-        ref_eq = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r1_reference_equivalent_cpu.json")
-        if os.path.exists(ref_eq):  # measured here, labelled: the reference itself publishes no numbers
-            try:
-                r = json.load(open(ref_eq))
-                rec["reference_equivalent_cpu"] = {"env_steps_per_s": round(r["value"], 1),
-                                                   "time_to_threshold_s": r.get("time_to_threshold_s"),
-                                                   "source": "benchmarks/reference_equivalent_cpu.py"}
-            except (ValueError, KeyError):
-                pass
         if do_ttt:
+            def pack(r, hp, shape_cfg, seeds):
+                return {"time_to_threshold_s": None if r[0] is None else round(r[0], 4),
+                        "per_seed_s": [round(x, 4) if x != float("inf") else None for x in r[1]],
+                        "epochs": r[2], "env_steps": r[3], "seeds": seeds, "hyperparams": hp, **shape_cfg}
+
+            shape_cfg = {"num_envs": args.ttt_envs, "rollout_len": args.ttt_rollout_len}
             rec["time_to_threshold_s"] = None if ttt[0] is None else round(ttt[0], 4)
-            rec["time_to_threshold_per_seed_s"] = [round(x, 4) if x != float("inf") else None for x in ttt[1]]
-            rec["time_to_threshold_epochs"] = ttt[2]
-            rec["time_to_threshold_env_steps"] = ttt[3]
-            rec["time_to_threshold_config"] = {"num_envs": args.ttt_envs, "rollout_len": args.ttt_rollout_len,
-                                               "train_vf_iters": args.ttt_vf_iters, "pi_lr": args.ttt_pi_lr,
-                                               "vf_lr": args.ttt_vf_lr, "gamma": 0.99, "lam": 0.95,
-                                               "threshold": 475,
-                                               "criterion": "mean return of the most recent >= 100 finished "
-                                                            "episodes >= 475 (gymnasium CartPole-v1), checked "
-                                                            "every epoch; clock starts before the trainer is built",
-                                               "value_loop_graph": bool(args.ttt_graphs)}
+            rec["time_to_threshold_reference_hparams_s"] = None if ttt_ref[0] is None else round(ttt_ref[0], 4)
+            rec["time_to_threshold"] = {
+                "criterion": "mean return of the newest >= 100 finished episodes >= 475 (gymnasium CartPole-v1), "
+                             "checked after every epoch",
+                "clock": "starts at TrainingServer(..., engine='vec') construction (api/server.py), stops after "
+                         "the first solved epoch; includes trainer/buffer allocation",
+                "tuned": pack(ttt, {"gamma": 0.99, "lam": 0.95, "pi_lr": args.ttt_pi_lr, "vf_lr": args.ttt_vf_lr,
+                                    "train_vf_iters": args.ttt_vf_iters}, shape_cfg, args.ttt_seeds),
+                "reference_hparams": pack(ttt_ref, {"gamma": 0.98, "lam": 0.97, "pi_lr": 3e-4, "vf_lr": 1e-3,
+                                                    "train_vf_iters": 80}, shape_cfg, args.ttt_ref_seeds),
+            }
+        if ref_cpu is not None:
+            rec["reference_equivalent_cpu"] = {
+                "env_steps_per_s": round(ref_cpu.get("value", 0.0), 1),
+                "time_to_threshold_s": ref_cpu.get("time_to_threshold_s"),
+                "best_window_return": ref_cpu.get("best_window_return"),
+                "budget_s": args.ref_cpu_seconds,
+                "criterion": "same (newest >= 100 episodes >= 475), reference hyperparameters, batch-1 per-step "
+                             "TorchScript pipeline on one CPU thread, measured concurrently in this run",
+                "source": "benchmarks/reference_equivalent_cpu.py"}
         print(json.dumps(rec), flush=True)
     if comm.world > 1:
         import torch.distributed as dist

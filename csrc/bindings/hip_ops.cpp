@@ -15,7 +15,7 @@ extern "C" {
 int rrl_mlp_forward(int mode, const float* params, const float* X, int B, int D, int A, int H,
                     const float* mask, const int* act_in, const float* actc_in, int* act_out,
                     float* actc_out, float* out0, float* out1, float* logits_out, uint64_t seed,
-                    uint64_t step, uint32_t row_offset, int num_cu, void* stream);
+                    uint64_t step, uint32_t row_offset, const float* gate, int num_cu, void* stream);
 int rrl_mlp_grad_slabs(int B, int num_cu);
 int rrl_set_value_grad_mode(int mode);
 int rrl_mlp_grad(int head, const float* params, const float* X, int B, int D, int A, int H,
@@ -23,8 +23,9 @@ int rrl_mlp_grad(int head, const float* params, const float* X, int B, int D, in
                  const float* logp_old, const float* adv_stats, float inv_B, float clip_eps, float ent_coef,
                  float* grad_slab, float* loss_slab, int P, int num_cu, void* stream);
 int rrl_scan_tm_parts(int N);
-int rrl_gae_scan_tm(const float* rew, const float* done, const float* val, float* adv, float* ret,
-                    float* stats_part, float* stats_out, int T, int N, float gamma, float lam, void* stream);
+int rrl_gae_scan_tm(const float* rew, const float* done, const float* val, const float* tval, float* adv,
+                    float* ret, float* stats_part, float* stats_out, int T, int N, float gamma, float lam,
+                    void* stream);
 int rrl_scan_flat_blocks(int L);
 int rrl_scan_flat(const float* rew, const float* done, const float* val, const float* boot, float* adv,
                   float* ret, float* work, float* stats_out, int L, float gamma, float lam, void* stream);
@@ -36,13 +37,13 @@ int rrl_reduce_slabs(const float* slab, int nslab, int P, float scale, float* ou
 int rrl_env_dims(int env, int* D, int* A, int* NS, int* max_steps);
 int rrl_rollout_cont(int env, const float* params, const float* env_consts, int N, int T, int H, float* state,
                      int* ep_len, float* ep_ret, float* obs_buf, float* act_buf, float* logp_buf, float* rew_buf,
-                     float* done_buf, float* ep_stats, uint64_t seed, uint64_t step0, int reset_all, int max_steps,
-                     int num_cu, void* stream);
+                     float* done_buf, float* tobs_buf, float* ep_stats, uint64_t seed, uint64_t step0,
+                     int reset_all, int max_steps, int num_cu, void* stream);
 int rrl_rollout_grid(int N, int num_cu);
 int rrl_rollout(int env, const float* params, int N, int T, int H, float* state, int* ep_len, float* ep_ret,
                 float* obs_buf, int* act_buf, float* logp_buf, float* rew_buf, float* done_buf,
-                float* ep_stats, uint64_t seed, uint64_t step0, int reset_all, int max_steps, int num_cu,
-                void* stream);
+                float* tobs_buf, float* ep_stats, uint64_t seed, uint64_t step0, int reset_all, int max_steps,
+                int num_cu, void* stream);
 }
 
 namespace {
@@ -91,7 +92,7 @@ void check_rc(int rc, const char* what) {
 void mlp_forward(int64_t mode, const Tensor& params, const Tensor& X, int64_t A, int64_t H, const OptT& mask,
                  const OptT& act_in, const OptT& actc_in, const OptT& act_out, const OptT& actc_out,
                  const Tensor& out0, const OptT& out1, const OptT& logits_out, int64_t seed, int64_t step,
-                 int64_t row_offset) {
+                 int64_t row_offset, const OptT& gate) {
   check_dev(params, "params", at::kFloat);
   check_dev(X, "X", at::kFloat);
   TORCH_CHECK(X.dim() == 2, "X must be [B, D]");
@@ -117,9 +118,11 @@ void mlp_forward(int64_t mode, const Tensor& params, const Tensor& X, int64_t A,
   float* o1 = fptr_mut(out1, "out1", B);
   float* lo = fptr_mut(logits_out, "logits_out", B * A);
   if (mode == 3) TORCH_CHECK(lo != nullptr, "logits_out required for LOGITS");
+  const float* gt = fptr(gate, "gate", B);
+  TORCH_CHECK(gt == nullptr || mode == 0, "gate applies to the VALUE mode only");
   const int rc = rrl_mlp_forward((int)mode, params.data_ptr<float>(), X.data_ptr<float>(), (int)B, (int)D, (int)A,
                                  (int)H, m, ai, ci, ao, co, out0.data_ptr<float>(), o1, lo, (uint64_t)seed,
-                                 (uint64_t)step, (uint32_t)row_offset, num_cus(), cur_stream());
+                                 (uint64_t)step, (uint32_t)row_offset, gt, num_cus(), cur_stream());
   check_rc(rc, "mlp_forward");
 }
 
@@ -168,14 +171,15 @@ void mlp_grad(int64_t head, const Tensor& params, const Tensor& X, int64_t A, in
 
 int64_t scan_tm_parts(int64_t N) { return rrl_scan_tm_parts((int)N); }
 
-void gae_scan_tm(const Tensor& rew, const Tensor& done, const OptT& val, const Tensor& adv, const Tensor& ret,
-                 const Tensor& stats_part, const OptT& stats_out, double gamma, double lam) {
+void gae_scan_tm(const Tensor& rew, const Tensor& done, const OptT& val, const OptT& tval, const Tensor& adv,
+                 const Tensor& ret, const Tensor& stats_part, const OptT& stats_out, double gamma, double lam) {
   check_dev(rew, "rew", at::kFloat);
   TORCH_CHECK(rew.dim() == 2, "rew must be [T, N]");
   const int64_t T = rew.size(0), N = rew.size(1);
   check_dev(done, "done", at::kFloat);
   check_numel(done, "done", T * N);
   const float* v = fptr(val, "val", (T + 1) * N);
+  const float* tv = fptr(tval, "tval", T * N);
   check_dev(adv, "adv", at::kFloat);
   check_numel(adv, "adv", T * N);
   check_dev(ret, "ret", at::kFloat);
@@ -183,7 +187,7 @@ void gae_scan_tm(const Tensor& rew, const Tensor& done, const OptT& val, const T
   check_dev(stats_part, "stats_part", at::kFloat);
   check_numel(stats_part, "stats_part", scan_tm_parts(N) * 3);
   float* so = fptr_mut(stats_out, "stats_out", 3);
-  const int rc = rrl_gae_scan_tm(rew.data_ptr<float>(), done.data_ptr<float>(), v, adv.data_ptr<float>(),
+  const int rc = rrl_gae_scan_tm(rew.data_ptr<float>(), done.data_ptr<float>(), v, tv, adv.data_ptr<float>(),
                                  ret.data_ptr<float>(), stats_part.data_ptr<float>(), so, (int)T, (int)N,
                                  (float)gamma, (float)lam, cur_stream());
   check_rc(rc, "gae_scan_tm");
@@ -270,8 +274,8 @@ int64_t rollout_grid(int64_t N) { return rrl_rollout_grid((int)N, num_cus()); }
 
 void rollout(int64_t env, const Tensor& params, int64_t H, const Tensor& state, const Tensor& ep_len,
              const Tensor& ep_ret, const Tensor& obs_buf, const Tensor& act_buf, const Tensor& logp_buf,
-             const Tensor& rew_buf, const Tensor& done_buf, const Tensor& ep_stats, int64_t seed, int64_t step0,
-             bool reset_all, int64_t max_steps) {
+             const Tensor& rew_buf, const Tensor& done_buf, const OptT& tobs_buf, const Tensor& ep_stats,
+             int64_t seed, int64_t step0, bool reset_all, int64_t max_steps) {
   auto [D, A, NS, ms] = env_dims(env);
   (void)ms;
   TORCH_CHECK(H == 64 || H == 128, "hidden size must be 64 or 128");
@@ -296,10 +300,11 @@ void rollout(int64_t env, const Tensor& params, int64_t H, const Tensor& state, 
   check_numel(done_buf, "done_buf", T * N);
   check_dev(ep_stats, "ep_stats", at::kFloat);
   check_numel(ep_stats, "ep_stats", rollout_grid(N) * 8);
+  float* tob = fptr_mut(tobs_buf, "tobs_buf", T * N * D);
   const int rc = rrl_rollout((int)env, params.data_ptr<float>(), (int)N, (int)T, (int)H, state.data_ptr<float>(),
                              ep_len.data_ptr<int>(), ep_ret.data_ptr<float>(), obs_buf.data_ptr<float>(),
                              act_buf.data_ptr<int>(), logp_buf.data_ptr<float>(), rew_buf.data_ptr<float>(),
-                             done_buf.data_ptr<float>(), ep_stats.data_ptr<float>(), (uint64_t)seed, (uint64_t)step0,
+                             done_buf.data_ptr<float>(), tob, ep_stats.data_ptr<float>(), (uint64_t)seed, (uint64_t)step0,
                              reset_all ? 1 : 0, (int)max_steps, num_cus(), cur_stream());
   check_rc(rc, "rollout");
 }
@@ -307,8 +312,8 @@ void rollout(int64_t env, const Tensor& params, int64_t H, const Tensor& state, 
 // Continuous-action fused rollout (diagonal Gaussian policy; env id 4 = HalfCheetahSynth).
 void rollout_cont(int64_t env, const Tensor& params, const Tensor& env_consts, int64_t H, const Tensor& state,
                   const Tensor& ep_len, const Tensor& ep_ret, const Tensor& obs_buf, const Tensor& act_buf,
-                  const Tensor& logp_buf, const Tensor& rew_buf, const Tensor& done_buf, const Tensor& ep_stats,
-                  int64_t seed, int64_t step0, bool reset_all, int64_t max_steps) {
+                  const Tensor& logp_buf, const Tensor& rew_buf, const Tensor& done_buf, const OptT& tobs_buf,
+                  const Tensor& ep_stats, int64_t seed, int64_t step0, bool reset_all, int64_t max_steps) {
   auto [D, A, NS, ms] = env_dims(env);
   (void)ms;
   TORCH_CHECK(env == 4, "rollout_cont supports the continuous device env 4 (HalfCheetahSynth)");
@@ -336,10 +341,11 @@ void rollout_cont(int64_t env, const Tensor& params, const Tensor& env_consts, i
   check_numel(done_buf, "done_buf", T * N);
   check_dev(ep_stats, "ep_stats", at::kFloat);
   check_numel(ep_stats, "ep_stats", rollout_grid(N) * 8);
+  float* tob = fptr_mut(tobs_buf, "tobs_buf", T * N * D);
   check_rc(rrl_rollout_cont((int)env, params.data_ptr<float>(), env_consts.data_ptr<float>(), (int)N, (int)T, (int)H,
                             state.data_ptr<float>(), ep_len.data_ptr<int>(), ep_ret.data_ptr<float>(),
                             obs_buf.data_ptr<float>(), act_buf.data_ptr<float>(), logp_buf.data_ptr<float>(),
-                            rew_buf.data_ptr<float>(), done_buf.data_ptr<float>(), ep_stats.data_ptr<float>(),
+                            rew_buf.data_ptr<float>(), done_buf.data_ptr<float>(), tob, ep_stats.data_ptr<float>(),
                             (uint64_t)seed, (uint64_t)step0, reset_all ? 1 : 0, (int)max_steps, num_cus(),
                             cur_stream()),
            "rollout_cont");

@@ -206,10 +206,13 @@ PYBIND11_MODULE(_native, m) {
         py::gil_scoped_release nogil;
         e.reset((float*)obs);
       })
-      .def("step_ptr", [](VecEnv& e, uintptr_t act, uintptr_t obs, uintptr_t rew, uintptr_t done) {
-        py::gil_scoped_release nogil;
-        e.step((const void*)act, (float*)obs, (float*)rew, (float*)done);
-      })
+      .def(
+          "step_ptr",
+          [](VecEnv& e, uintptr_t act, uintptr_t obs, uintptr_t rew, uintptr_t done, uintptr_t tobs) {
+            py::gil_scoped_release nogil;
+            e.step((const void*)act, (float*)obs, (float*)rew, (float*)done, (float*)tobs);
+          },
+          py::arg("act"), py::arg("obs"), py::arg("rew"), py::arg("done"), py::arg("tobs") = 0)
       .def("take_stats", [](VecEnv& e) {
         EpisodeStats s = e.take_stats();
         py::dict d;

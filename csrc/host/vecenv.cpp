@@ -393,7 +393,7 @@ void VecEnv::reset(float* obs) {
   });
 }
 
-void VecEnv::step(const void* actions, float* obs, float* rew, float* done) {
+void VecEnv::step(const void* actions, float* obs, float* rew, float* done, float* tobs) {
   run_parallel([&](int tid, int nt) {
     const int lo = (int)((int64_t)n_ * tid / nt), hi = (int)((int64_t)n_ * (tid + 1) / nt);
     EpisodeStats& st = tstats_[tid];
@@ -412,8 +412,10 @@ void VecEnv::step(const void* actions, float* obs, float* rew, float* done) {
       len_[i] += 1;
       ret_[i] += r;
       const bool d = term || len_[i] >= max_steps_;
+      const bool boot = d && !term && tobs != nullptr;
       rew[i] = r;
-      done[i] = d ? 1.f : 0.f;
+      done[i] = boot ? 2.f : (d ? 1.f : 0.f);
+      if (boot) std::copy(o, o + obs_dim_, tobs + (size_t)i * obs_dim_);
       if (d) {
         st.n += 1;
         st.sum += ret_[i];

@@ -78,7 +78,10 @@ class VecEnv {
   void reset(float* obs);
   // actions: int32[N] (discrete) or float[N*act_dim] (continuous).  Finished envs are
   // auto-reset; obs then holds the first observation of the next episode.
-  void step(const void* actions, float* obs, float* rew, float* done);
+  // done codes: 0 running, 1 terminal, 2 time-limit truncation; with ``tobs`` non-null a
+  // truncated env's pre-reset observation goes to tobs[i] (its value bootstraps the cut
+  // episode), without it truncations are reported as 1.
+  void step(const void* actions, float* obs, float* rew, float* done, float* tobs = nullptr);
   EpisodeStats take_stats();
 
  private:

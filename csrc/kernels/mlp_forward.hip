@@ -38,6 +38,8 @@ struct FwdArgs {
   uint32_t seed_lo, seed_hi;
   uint32_t step_lo, step_hi;
   uint32_t row_offset;   // stream id of row 0 (global env index)
+  const float* gate;     // MODE_VALUE: [B] done codes; only 16-row tiles holding a code 2
+                         // (time-limit truncation) are evaluated, or null = every row
 };
 
 template <int DT, int HT, int MODE>
@@ -62,6 +64,10 @@ __global__ __launch_bounds__(256, 2) void mlp_forward_kernel(FwdArgs p) {
     const int nrows = min(kTileB, p.B - row0);
     const int row = row0 + j;
     const bool valid = j < nrows;
+    if (MODE == MODE_VALUE && p.gate != nullptr) {
+      // truncation bootstraps are rare (CartPole: one per 500 steps): skip tiles without one
+      if (__ballot(valid && p.gate[row] > 1.5f) == 0) continue;
+    }
 
     floatx4 x[DT], h1[HT], h2[HT];
     load_x_tile<DT>(p.X, p.D, p.D, row0, nrows, x);
@@ -171,11 +177,11 @@ extern "C" int rrl_mlp_forward(int mode, const float* params, const float* X, in
                                int H, const float* mask, const int* act_in, const float* actc_in,
                                int* act_out, float* actc_out, float* out0, float* out1,
                                float* logits_out, uint64_t seed, uint64_t step, uint32_t row_offset,
-                               int num_cu, void* stream) {
+                               const float* gate, int num_cu, void* stream) {
   if (B <= 0) return 0;
   if (A < 1 || A > kMaxAct || D < 1 || D > 32) return -2;
   FwdArgs a{params, X, B, D, A, H, mask, act_in, actc_in, act_out, actc_out, out0, out1, logits_out,
-            (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step, (uint32_t)(step >> 32), row_offset};
+            (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step, (uint32_t)(step >> 32), row_offset, gate};
   const int tiles = (B + kTileB - 1) / kTileB;
   const int waves_needed = tiles;
   int grid = (waves_needed + 3) / 4;

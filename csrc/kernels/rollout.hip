@@ -23,7 +23,8 @@ struct RolloutArgs {
   int* act_buf;     // [T][N]
   float* logp_buf;  // [T][N]
   float* rew_buf;   // [T][N]
-  float* done_buf;  // [T][N]
+  float* done_buf;  // [T][N]: 0 running, 1 terminal, 2 time-limit truncation (needs tobs_buf)
+  float* tobs_buf;  // [T][N][D] pre-reset observation where done == 2, or null (truncation -> 1)
   float* ep_stats;  // [grid][8]: n_done, sum_ret, sumsq_ret, max_ret, min_ret, sum_len
   uint32_t seed_lo, seed_hi;
   uint32_t step_lo, step_hi;  // global step of t = 0 (RNG counter)
@@ -106,11 +107,17 @@ __global__ __launch_bounds__(256, 2) void rollout_kernel(RolloutArgs p) {
       ret += r;
       const bool trunc = len >= p.max_steps;
       const bool done = term || trunc;
+      const bool boot = trunc && !term && p.tobs_buf != nullptr;  // cut path: bootstrap V(s_t+1)
       if (valid && g == 0) {
         p.act_buf[base] = a;
         p.logp_buf[base] = logp;
         p.rew_buf[base] = r;
-        p.done_buf[base] = done ? 1.f : 0.f;
+        p.done_buf[base] = boot ? 2.f : (done ? 1.f : 0.f);
+      }
+      if (boot && valid) {
+#pragma unroll
+        for (int f = 0; f < D; ++f)
+          if ((f & 3) == g) p.tobs_buf[base * D + f] = Env::obs(s, f);
       }
       if (done) {
         if (valid && g == 0) {
@@ -276,11 +283,17 @@ __global__ __launch_bounds__(64 * WPT, 1) void rollout_wide_kernel(RolloutArgs p
       ret += r;
       const bool trunc = len >= p.max_steps;
       const bool done = term || trunc;
+      const bool boot = trunc && !term && p.tobs_buf != nullptr;
       if (valid && writer) {
         p.act_buf[base] = a;
         p.logp_buf[base] = logp;
         p.rew_buf[base] = r;
-        p.done_buf[base] = done ? 1.f : 0.f;
+        p.done_buf[base] = boot ? 2.f : (done ? 1.f : 0.f);
+      }
+      if (boot && valid && w == 0) {
+#pragma unroll
+        for (int f = 0; f < D; ++f)
+          if ((f & 3) == g) p.tobs_buf[base * D + f] = Env::obs(s, f);
       }
       if (done) {
         if (valid && writer) {
@@ -348,7 +361,8 @@ struct RolloutContArgs {
   float* act_buf;   // [T][N][A]
   float* logp_buf;  // [T][N]
   float* rew_buf;   // [T][N]
-  float* done_buf;  // [T][N]
+  float* done_buf;  // [T][N]: 0 running, 2 time-limit truncation (1 without tobs_buf)
+  float* tobs_buf;  // [T][N][D] pre-reset observation where done == 2, or null
   float* ep_stats;  // [grid][8]
   uint32_t seed_lo, seed_hi;
   uint32_t step_lo, step_hi;
@@ -447,12 +461,18 @@ __global__ __launch_bounds__(256, 2) void rollout_cont_kernel(RolloutContArgs p)
       len += 1;
       ret += r;
       const bool done = len >= p.max_steps;  // this env only truncates (time limit)
+      const bool boot = done && p.tobs_buf != nullptr;
       if (valid && g == 0) {
 #pragma unroll
         for (int a = 0; a < A; ++a) p.act_buf[base * A + a] = act[a];
         p.logp_buf[base] = logp;
         p.rew_buf[base] = r;
-        p.done_buf[base] = done ? 1.f : 0.f;
+        p.done_buf[base] = boot ? 2.f : (done ? 1.f : 0.f);
+      }
+      if (boot && valid) {
+#pragma unroll
+        for (int f = 0; f < D; ++f)
+          if ((f & 3) == g) p.tobs_buf[base * D + f] = s[f];
       }
       if (done) {
         if (valid && g == 0) {
@@ -577,10 +597,10 @@ static int launch_rollout(const RolloutArgs& a, int grid, bool wide, hipStream_t
 
 extern "C" int rrl_rollout(int env, const float* params, int N, int T, int H, float* state, int* ep_len,
                            float* ep_ret, float* obs_buf, int* act_buf, float* logp_buf, float* rew_buf,
-                           float* done_buf, float* ep_stats, uint64_t seed, uint64_t step0, int reset_all,
-                           int max_steps, int num_cu, void* stream) {
+                           float* done_buf, float* tobs_buf, float* ep_stats, uint64_t seed, uint64_t step0,
+                           int reset_all, int max_steps, int num_cu, void* stream) {
   if (N <= 0 || T <= 0) return -2;
-  RolloutArgs a{params, N, T, H, state, ep_len, ep_ret, obs_buf, act_buf, logp_buf, rew_buf, done_buf, ep_stats,
+  RolloutArgs a{params, N, T, H, state, ep_len, ep_ret, obs_buf, act_buf, logp_buf, rew_buf, done_buf, tobs_buf, ep_stats,
                 (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step0, (uint32_t)(step0 >> 32), reset_all,
                 max_steps};
   const int grid = rrl_rollout_grid(N, num_cu);
@@ -622,11 +642,11 @@ static int launch_rollout_cont(const RolloutContArgs& a, int grid, hipStream_t s
 // Continuous-action device envs (env id ENV_HALFCHEETAH); env_consts = env_constants(name).
 extern "C" int rrl_rollout_cont(int env, const float* params, const float* env_consts, int N, int T, int H,
                                 float* state, int* ep_len, float* ep_ret, float* obs_buf, float* act_buf,
-                                float* logp_buf, float* rew_buf, float* done_buf, float* ep_stats, uint64_t seed,
-                                uint64_t step0, int reset_all, int max_steps, int num_cu, void* stream) {
+                                float* logp_buf, float* rew_buf, float* done_buf, float* tobs_buf, float* ep_stats,
+                                uint64_t seed, uint64_t step0, int reset_all, int max_steps, int num_cu, void* stream) {
   if (N <= 0 || T <= 0 || env != ENV_HALFCHEETAH || env_consts == nullptr) return -2;
   RolloutContArgs a{params, env_consts, N, T, state, ep_len, ep_ret, obs_buf, act_buf, logp_buf, rew_buf, done_buf,
-                    ep_stats, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step0, (uint32_t)(step0 >> 32),
+                    tobs_buf, ep_stats, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step0, (uint32_t)(step0 >> 32),
                     reset_all, max_steps};
   const int grid = rrl_rollout_grid(N, num_cu);
   hipStream_t s = (hipStream_t)stream;

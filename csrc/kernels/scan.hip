@@ -5,7 +5,10 @@
 //   with baseline   : adv = disc(r + g*V' - V, g*lam), ret = disc(r ++ [last_val], g)[:-1]
 //   without baseline: adv = disc(r, g*lam),           ret = disc(r, g)
 // Both are reverse linear recurrences y_t = b_t + a_t * y_{t+1} with a_t = 0 at a
-// path end.  Two layouts are supported:
+// path end.  done codes: 0 = running, 1 = terminal (bootstrap 0), 2 = time-limit
+// truncation (bootstrap with V of the pre-reset observation, tval[t]) -- the reference
+// bootstraps its cut paths with last_val (replay_buffer.py:48-79, REINFORCE.py:86).
+// Two layouts are supported:
 //   * time-major [T][N] rollouts from the vectorised actors: one thread per env column,
 //     sequential in t (coalesced across envs) -- T is short, N is huge;
 //   * flat [L] buffers of concatenated variable-length paths (the agent/trajectory API):
@@ -18,6 +21,7 @@ struct ScanTM {
   const float* rew;    // [T][N]
   const float* done;   // [T][N]  (1 if the episode ended at this step)
   const float* val;    // [T+1][N] or null (row T = bootstrap value V(s_T))
+  const float* tval;   // [T][N] V(pre-reset obs), read where done == 2, or null
   float* adv;          // [T][N]
   float* ret;          // [T][N]
   float* stats_part;   // [nblocks][3] adv sum / sumsq / count
@@ -37,10 +41,11 @@ __global__ __launch_bounds__(256) void gae_scan_tm_kernel(ScanTM p) {
       for (int t = p.T - 1; t >= 0; --t) {
         const size_t idx = (size_t)t * N + n;
         const float r = p.rew[idx], d = p.done[idx], v = p.val[idx];
-        const float nd = 1.f - d;
-        const float delta = r + p.gamma * v_next * nd - v;
+        const float nd = d == 0.f ? 1.f : 0.f;
+        const float vb = (d > 1.5f && p.tval != nullptr) ? p.tval[idx] : 0.f;  // truncation bootstrap
+        const float delta = r + p.gamma * (v_next * nd + vb) - v;
         const float a = delta + gl * nd * adv_next;
-        const float rt = r + p.gamma * nd * ret_next;
+        const float rt = r + p.gamma * (nd * ret_next + vb);
         p.adv[idx] = a;
         p.ret[idx] = rt;
         s += a;
@@ -54,7 +59,7 @@ __global__ __launch_bounds__(256) void gae_scan_tm_kernel(ScanTM p) {
       for (int t = p.T - 1; t >= 0; --t) {
         const size_t idx = (size_t)t * N + n;
         const float r = p.rew[idx], d = p.done[idx];
-        const float nd = 1.f - d;
+        const float nd = d == 0.f ? 1.f : 0.f;  // no value function: truncation cuts like a terminal
         const float a = r + gl * nd * adv_next;
         const float rt = r + p.gamma * nd * ret_next;
         p.adv[idx] = a;
@@ -136,7 +141,7 @@ constexpr int kFlatChunk = kFlatPer * kFlatBlock;
 
 RRL_DEV void flat_coeffs(const ScanFlat& p, int t, float& a_adv, float& b_adv, float& a_ret, float& b_ret) {
   const float r = p.rew[t];
-  const float d = p.done[t];
+  const float d = p.done[t] > 0.f ? 1.f : 0.f;  // flat paths: any nonzero code ends the path
   const float nd = 1.f - d;
   const float boot = (p.boot != nullptr && d > 0.f) ? p.boot[t] : 0.f;
   if (p.val != nullptr) {
@@ -257,12 +262,12 @@ using namespace rrl;
 
 extern "C" int rrl_scan_tm_parts(int N) { return (N + 255) / 256; }
 
-extern "C" int rrl_gae_scan_tm(const float* rew, const float* done, const float* val, float* adv,
-                               float* ret, float* stats_part, float* stats_out, int T, int N,
+extern "C" int rrl_gae_scan_tm(const float* rew, const float* done, const float* val, const float* tval,
+                               float* adv, float* ret, float* stats_part, float* stats_out, int T, int N,
                                float gamma, float lam, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   const int nb = rrl_scan_tm_parts(N);
-  ScanTM p{rew, done, val, adv, ret, stats_part, T, N, gamma, lam};
+  ScanTM p{rew, done, val, tval, adv, ret, stats_part, T, N, gamma, lam};
   hipLaunchKernelGGL(gae_scan_tm_kernel, dim3(nb), dim3(256), 0, s, p);
   if (stats_out) hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(256), 0, s, stats_part, nb, stats_out);
   return (int)hipGetLastError();

@@ -37,6 +37,9 @@ class FlatBuffer:
         self.has_logp = np.zeros(self.size, bool)
         self.done = np.zeros(self.size, np.float32)
         self.boot = np.zeros(self.size, np.float32)
+        # s_T of a cut path (shipped by the agent): its value bootstraps the path end
+        self.boot_obs = np.zeros((self.size, obs_dim), np.float32)
+        self.has_boot_obs = np.zeros(self.size, bool)
         self.ptr = 0
         self.path_start = 0
 
@@ -80,13 +83,20 @@ class FlatBuffer:
             self.logp[sl] = logp[:n]
         self.has_logp[sl] = logp is not None
         self.done[sl] = 0.0
+        self.has_boot_obs[sl] = False
         self.ptr += n
         return n
 
-    def finish_path(self, terminal: bool = True):
+    def finish_path(self, terminal: bool = True, boot_obs=None):
+        """Close the current path.  A cut (non-terminal) path bootstraps with V(boot_obs) when
+        the agent shipped its next observation, else with V of its last state (nan marker)."""
         if self.ptr > self.path_start:
-            self.done[self.ptr - 1] = 1.0
-            self.boot[self.ptr - 1] = np.nan if not terminal else 0.0  # nan = bootstrap with V(s_last)
+            i = self.ptr - 1
+            self.done[i] = 1.0
+            self.boot[i] = np.nan if not terminal else 0.0  # nan = bootstrap with a value
+            if not terminal and boot_obs is not None:
+                self.boot_obs[i] = np.asarray(boot_obs, np.float32).reshape(-1)[: self.obs_dim]
+                self.has_boot_obs[i] = True
         self.path_start = self.ptr
 
     def take(self, device) -> Dict[str, torch.Tensor]:
@@ -102,6 +112,10 @@ class FlatBuffer:
             "done": torch.from_numpy(self.done[sl].copy()),
             "boot": torch.from_numpy(self.boot[sl].copy()),
         }
+        idx = np.flatnonzero(self.has_boot_obs[sl])
+        out["boot_idx"] = torch.from_numpy(idx.astype(np.int64))
+        out["boot_obs"] = torch.from_numpy(self.boot_obs[idx].copy())
+        self.has_boot_obs[sl] = False
         self.ptr = 0
         self.path_start = 0
         if torch.device(device).type == "cuda":
@@ -203,7 +217,8 @@ class TrajectoryAlgorithm(AlgorithmAbstract):
             if c.done[stop - 1]:
                 self._end_episode(terminal=True)
             elif buf.ptr > buf.path_start:
-                buf.finish_path(terminal=False)  # truncated segment: bootstrap from V(s_last)
+                # cut segment: bootstrap with V(s_T) when the agent shipped s_T, else V(s_last)
+                buf.finish_path(terminal=False, boot_obs=getattr(c, "next_obs", None))
             start = stop
 
     def _receive_actions(self, trajectory) -> None:
@@ -249,8 +264,12 @@ class TrajectoryAlgorithm(AlgorithmAbstract):
         if self.learner.vf is not None:
             val = mlp_forward(FwdMode.VALUE, self.learner.vf.params, obs, 1, H)["v"]
             self.logger.store(VVals=val.detach().cpu().numpy())
-            # nan boot = truncated path: bootstrap with the value of its last state
+            # nan boot = cut path: V(s_T) where the agent shipped s_T, else V(last state)
             boot = torch.where(torch.isnan(boot), val, boot)
+            bi = d["boot_idx"]
+            if bi.numel():
+                vb = mlp_forward(FwdMode.VALUE, self.learner.vf.params, d["boot_obs"], 1, H)["v"]
+                boot = boot.index_copy(0, bi.to(boot.device), vb.to(boot.dtype))
         else:
             boot = torch.nan_to_num(boot, nan=0.0)
         adv, ret, stats = scan_flat(d["rew"], d["done"], val, boot, self.gamma, self.lam)

@@ -136,8 +136,8 @@ class RelayRLAgent:
         else:
             raise ValueError(f"server_type must be zmq, grpc or local, not {self.server_type!r}")
 
-    def _ship(self, done: bool):
-        cols = self._rec.take(self.agent_id, self.episodes_sent, done)
+    def _ship(self, done: bool, next_obs=None):
+        cols = self._rec.take(self.agent_id, self.episodes_sent, done, next_obs)
         cols.max_length = self.max_traj_length
         if self.server_type == "zmq":
             self.transport.send_trajectory(cols.encode() if self.wire_format == "columns"
@@ -173,9 +173,13 @@ class RelayRLAgent:
             raise RuntimeError("no model loaded")
         rec = self._rec
         rec.set_last_reward(float(reward))
+        obs_a = np.asarray(obs, np.float32)
+        if rec.full():
+            # very long episode: every recorded action now has its reward; ship the segment
+            # (not done) with s_T = this observation so the learner bootstraps it with V(s_T)
+            self._ship(done=False, next_obs=obs_a)
         with self._policy_lock:
             p = self.policy
-            obs_a = np.asarray(obs, np.float32)
             mask_a = np.ones(p.act_dim, np.float32) if mask is None else np.asarray(mask, np.float32)
             act, data = p.step(obs_a, mask_a)
         a0 = np.asarray(act[0] if act.ndim >= 1 else act)
@@ -183,16 +187,18 @@ class RelayRLAgent:
         rec.record(obs_a, a0, mask_a, None if logp is None else logp[0])
         aux = {k: np.asarray(v[0], np.float32) for k, v in data.items()}
         action = RelayRLAction(obs_a, a0, mask_a, 0.0, aux, False, False)
-        if rec.full():
-            # very long episode: ship the segment (learner bootstraps it) and continue
-            self._ship(done=False)
         return action
 
-    def flag_last_action(self, reward: float = 0.0, done: bool = True, truncated: bool = False) -> None:
+    def flag_last_action(self, reward: float = 0.0, done: bool = True, truncated: bool = False,
+                         next_obs=None) -> None:
+        """Close the episode with the final reward (agent_zmq.rs:605-610).  ``truncated=True``
+        marks a time-limit cut: pass the final observation as ``next_obs`` and the learner
+        bootstraps the cut path with V(next_obs) (without it, V of the last acted state)."""
         if self._rec.n == 0:
             return
         self._rec.set_last_reward(float(reward))
-        self._ship(done=done and not truncated)
+        cut = truncated or not done
+        self._ship(done=not cut, next_obs=next_obs if cut else None)
 
     def restart_agent(self, training_server_address: Optional[str] = None) -> bool:
         self.disable_agent()

@@ -8,12 +8,17 @@ Differences by design (docs/COMPAT.md):
   * ``hyperparams`` override the JSON config instead of crashing the algorithm (A9);
   * the ZMQ server pushes model updates over the agent's DEALER connection, so any
     number of agents can attach (A6); ``multiactor`` is accepted for compatibility;
-  * ``server_type="local"`` runs agent and learner in one process without sockets.
+  * ``server_type="local"`` runs agent and learner in one process without sockets;
+  * ``engine="vec" | "host" | "actor_learner" | "pixel"`` (or the config's ``"mi355x"``
+    block / ``hyperparams={"engine": ...}``) puts a GPU device engine behind the server
+    (runtime/engine.py): ``train(...)`` runs it, logs the reference progress.txt columns and
+    publishes every update to attached agents; ``world_size > 1`` launches one rank per GPU.
 """
 from __future__ import annotations
 
 import os
 import threading
+import time
 from typing import Dict, List, Optional, Union
 
 from ..algorithms.registry import make_algorithm, parse_hyperparams
@@ -29,7 +34,8 @@ class TrainingServer:
                  hyperparams: Optional[Union[Dict[str, str], List[str]]] = None, server_type: str = "zmq",
                  training_prefix: Optional[str] = None, training_host: Optional[str] = None,
                  training_port: Optional[str] = None, device=None, checkpoint_dir: Optional[str] = None,
-                 checkpoint_every: int = 0, verbose: bool = False):
+                 checkpoint_every: int = 0, verbose: bool = False, engine: Optional[str] = None):
+        self._t_start = time.perf_counter()  # the time-to-threshold clock starts here
         os.makedirs(env_dir, exist_ok=True)
         self.config_path = resolve_config_json_path(config_path)
         self.cfg = ConfigLoader(algorithm_name, self.config_path)
@@ -41,8 +47,22 @@ class TrainingServer:
         self.multiactor = multiactor
         self.verbose = verbose
         hp = parse_hyperparams(hyperparams)
-        self.algorithm = make_algorithm(algorithm_name, algorithm_dir, env_dir=env_dir, config_path=self.config_path,
-                                        obs_dim=obs_dim, act_dim=act_dim, buf_size=buf_size, device=device, **hp)
+        from ..runtime import engine as eng
+
+        ap = (self.cfg.get_algorithm_params() or {}).get(algorithm_name.upper(), {})
+        self.engine_spec = eng.resolve_engine(algorithm_name, obs_dim, act_dim, ap, self.cfg.get_mi355x_params(), hp,
+                                              engine)
+        self.engine = None
+        if self.engine_spec is None:
+            self.algorithm = make_algorithm(algorithm_name, algorithm_dir, env_dir=env_dir,
+                                            config_path=self.config_path, obs_dim=obs_dim, act_dim=act_dim,
+                                            buf_size=buf_size, device=device, **hp)
+        elif self.engine_spec.world_size > 1:
+            self.algorithm = eng.RemoteEngineAlgorithm(self.engine_spec, obs_dim, act_dim,
+                                                       os.path.join(env_dir, "engine"), self.cfg.get_server_model_path())
+        else:
+            self.algorithm = eng.EngineAlgorithm(self.engine_spec, env_dir, self.cfg.get_server_model_path(),
+                                                 device=device)
         self._ckpt = None
         if checkpoint_dir and checkpoint_every > 0:
             from ..utils.checkpoint import periodic_checkpointer
@@ -50,6 +70,11 @@ class TrainingServer:
             self._ckpt = periodic_checkpointer(checkpoint_dir, checkpoint_every)
         self.service = LearnerService(self.algorithm, checkpoint_fn=self._ckpt)
         self.service.start()
+        if self.engine_spec is not None:
+            if self.engine_spec.world_size > 1:
+                self.engine = eng.MultiRankEngineRunner(self.algorithm, self.service, env_dir, self._t_start)
+            else:
+                self.engine = eng.EngineRunner(self.algorithm, self.service, self._t_start)
         ts = dict(self.cfg.get_train_server())
         if training_prefix is not None:
             ts["prefix"] = training_prefix
@@ -68,11 +93,14 @@ class TrainingServer:
             self.tb = ProgressTensorboard(os.path.join(env_dir, "logs"), tb["scalar_tags"], tb["global_step_tag"])
             self.tb.start()
         self.enable_server()
-        try:
-            self.algorithm.save()  # initial server model file, like the first GET_MODEL did
-        except Exception as e:  # model export must not take the server down
-            if verbose:
-                print(f"[TrainingServer] initial model export failed: {e!r}", flush=True)
+        if self.engine is None:
+            try:
+                self.algorithm.save()  # initial server model file, like the first GET_MODEL did
+            except Exception as e:  # model export must not take the server down
+                if verbose:
+                    print(f"[TrainingServer] initial model export failed: {e!r}", flush=True)
+        # engine mode: the TorchScript archive is produced lazily (GET_MODEL / close), not on
+        # the time-to-threshold clock
 
     # ------------------------------------------------------------------ addresses
     def addresses(self) -> List[str]:
@@ -142,6 +170,9 @@ class TrainingServer:
         self.train_server = {"prefix": prefix or self.train_server.get("prefix", ""), "host": host, "port": port}
 
     def close(self, save: bool = True):
+        if self.engine is not None and hasattr(self.engine, "stop"):
+            self.engine.stop()
+            self.engine.join(60)
         self.disable_server()
         self.service.stop(drain=True)
         if self.tb is not None:
@@ -151,6 +182,26 @@ class TrainingServer:
                 self.algorithm.save()
             except Exception:
                 pass
+
+    # ------------------------------------------------------------------ device engine
+    def train(self, epochs: Optional[int] = None, target_return: Optional[float] = None, window: int = 100,
+              max_seconds: Optional[float] = None, log_every: int = 1, publish_every: int = 1,
+              background: bool = False):
+        """Run the device engine (see runtime/engine.py) until ``epochs`` epochs, the mean return of
+        the newest >= ``window`` episodes reaching ``target_return``, or ``max_seconds``.  Returns a
+        TrainResult (``time_to_threshold_s`` is measured from this server's construction);
+        ``background=True`` returns at once (``engine.join()`` for the result)."""
+        if self.engine is None:
+            raise RuntimeError("this server learns from agent uploads; construct it with engine=... "
+                               "(or an \"engine\" entry in the config's \"mi355x\" block) to train on device envs")
+        kw = dict(epochs=epochs, target_return=target_return, window=window, max_seconds=max_seconds,
+                  log_every=log_every, publish_every=publish_every)
+        if background:
+            if not hasattr(self.engine, "start"):
+                raise RuntimeError("background training needs the in-process (world_size 1) engine")
+            self.engine.start(**kw)
+            return None
+        return self.engine.train(**kw)
 
     # ------------------------------------------------------------------ extras
     def wait_idle(self, timeout: float = 60.0) -> bool:

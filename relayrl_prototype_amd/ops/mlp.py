@@ -96,13 +96,25 @@ def _i32(t):
 
 
 def mlp_forward(mode: int, params: torch.Tensor, X: torch.Tensor, A: int, H: int, mask=None, act_in=None,
-                actc_in=None, seed: int = 0, step: int = 0, row_offset: int = 0, out: Optional[dict] = None):
-    """Batched fused forward.  Returns a dict with keys among v / act / logp / entropy / logits / mean."""
+                actc_in=None, seed: int = 0, step: int = 0, row_offset: int = 0, out: Optional[dict] = None,
+                gate=None):
+    """Batched fused forward.  Returns a dict with keys among v / act / logp / entropy / logits / mean.
+
+    ``gate`` (VALUE mode): [B] done codes; the kernel evaluates only the 16-row tiles that
+    contain a time-limit truncation (code 2) -- the bootstrap values of cut episodes."""
     X = X.contiguous().float()
     B = X.shape[0]
     h = _hip_for(X)
     if h is None:
-        return ref.mlp_forward_ref(int(mode), params, X, A, H, mask, act_in, actc_in, seed, step, row_offset)
+        r = ref.mlp_forward_ref(int(mode), params, X, A, H, mask, act_in, actc_in, seed, step, row_offset)
+        if out is not None:
+            for k, v in r.items():
+                if k in out:
+                    out[k].copy_(v)
+                else:
+                    out[k] = v
+            return out
+        return r
     dev = X.device
     out = {} if out is None else out
     mode = int(mode)
@@ -110,7 +122,8 @@ def mlp_forward(mode: int, params: torch.Tensor, X: torch.Tensor, A: int, H: int
         v = out.get("v")
         if v is None:
             v = out["v"] = torch.empty(B, device=dev)
-        h.mlp_forward(mode, params, X, A, H, None, None, None, None, None, v, None, None, seed, step, row_offset)
+        h.mlp_forward(mode, params, X, A, H, None, None, None, None, None, v, None, None, seed, step, row_offset,
+                      _f32(gate))
         return out
     o0 = out.setdefault("logp", torch.empty(B, device=dev))
     o1 = out.setdefault("entropy", torch.empty(B, device=dev))
@@ -125,7 +138,7 @@ def mlp_forward(mode: int, params: torch.Tensor, X: torch.Tensor, A: int, H: int
     elif mode == FwdMode.GAUSS_EVAL:
         logits = out.setdefault("mean", torch.empty(B, A, device=dev))
     h.mlp_forward(mode, params, X, A, H, _f32(mask), _i32(act_in), _f32(actc_in), act_out, actc_out, o0, o1,
-                  logits, seed, step, row_offset)
+                  logits, seed, step, row_offset, None)
     return out
 
 
@@ -209,11 +222,14 @@ def adam_step(param, m, v, step_t, ticket_t, lr, grad=None, slab=None, beta1=0.9
            float(grad_scale), float(weight_decay))
 
 
-def gae_scan_tm(rew, done, val, gamma, lam, adv=None, ret=None, stats_part=None, stats_out=None):
-    """Time-major [T, N] GAE / discounted-return scan -> (adv, ret, stats[3])."""
+def gae_scan_tm(rew, done, val, gamma, lam, adv=None, ret=None, stats_part=None, stats_out=None, tval=None):
+    """Time-major [T, N] GAE / discounted-return scan -> (adv, ret, stats[3]).
+
+    done codes: 0 running, 1 terminal, 2 time-limit truncation -- bootstrapped with
+    ``tval`` [T, N] = V(pre-reset observation) (replay_buffer.py:48-79 last_val)."""
     h = _hip_for(rew)
     if h is None:
-        a, r, s = ref.gae_scan_tm_ref(rew, done, val, gamma, lam)
+        a, r, s = ref.gae_scan_tm_ref(rew, done, val, gamma, lam, tval)
         if stats_out is not None:
             stats_out.copy_(s)
         return a, r, s
@@ -225,7 +241,7 @@ def gae_scan_tm(rew, done, val, gamma, lam, adv=None, ret=None, stats_part=None,
         stats_part = torch.empty(int(h.scan_tm_parts(N)), 3, device=dev)
     if stats_out is None:
         stats_out = torch.empty(3, device=dev)
-    h.gae_scan_tm(rew.contiguous(), done.contiguous(), None if val is None else val.contiguous(), adv, ret,
+    h.gae_scan_tm(rew.contiguous(), done.contiguous(), None if val is None else val.contiguous(), _f32(tval), adv, ret,
                   stats_part, stats_out, float(gamma), float(lam))
     return adv, ret, stats_out
 

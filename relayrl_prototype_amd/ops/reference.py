@@ -178,7 +178,8 @@ def discount_cumsum(x: np.ndarray, discount: float) -> np.ndarray:
 
 
 @torch.no_grad()
-def gae_scan_tm_ref(rew, done, val, gamma, lam):
+def gae_scan_tm_ref(rew, done, val, gamma, lam, tval=None):
+    """done codes: 0 running, 1 terminal, 2 time-limit truncation (bootstrap tval[t])."""
     T, N = rew.shape
     adv = torch.zeros_like(rew)
     ret = torch.zeros_like(rew)
@@ -187,16 +188,18 @@ def gae_scan_tm_ref(rew, done, val, gamma, lam):
         adv_next = torch.zeros(N, dtype=rew.dtype, device=rew.device)
         ret_next = v_next.clone()
         for t in range(T - 1, -1, -1):
-            nd = 1.0 - done[t]
-            delta = rew[t] + gamma * v_next * nd - val[t]
+            nd = (done[t] == 0).to(rew.dtype)
+            vb = torch.where(done[t] > 1.5, tval[t], torch.zeros_like(rew[t])) if tval is not None \
+                else torch.zeros_like(rew[t])
+            delta = rew[t] + gamma * (v_next * nd + vb) - val[t]
             adv[t] = delta + gamma * lam * nd * adv_next
-            ret[t] = rew[t] + gamma * nd * ret_next
+            ret[t] = rew[t] + gamma * (nd * ret_next + vb)
             adv_next, ret_next, v_next = adv[t], ret[t], val[t]
     else:
         adv_next = torch.zeros(N, dtype=rew.dtype, device=rew.device)
         ret_next = torch.zeros(N, dtype=rew.dtype, device=rew.device)
         for t in range(T - 1, -1, -1):
-            nd = 1.0 - done[t]
+            nd = (done[t] == 0).to(rew.dtype)
             adv[t] = rew[t] + gamma * lam * nd * adv_next
             ret[t] = rew[t] + gamma * nd * ret_next
             adv_next, ret_next = adv[t], ret[t]

@@ -1,0 +1,553 @@
+"""The GPU engines behind the reference API.
+
+The reference's ``TrainingServer`` always spawns one Python learner that trains on the
+trajectories agents upload (o3_training_server.rs:78-151 -> training_server_wrapper.rs:235-380
+-> training_zmq.rs / training_grpc.rs).  Here ``TrainingServer(..., engine=...)`` -- or the
+config's ``"mi355x": {"engine": ...}`` block, or ``hyperparams={"engine": ...}`` -- puts one of
+the device engines behind the same object instead:
+
+  vec            runtime/vec_trainer.py     fused on-device actor + HIP learner per GPU
+  host           runtime/host_trainer.py    C++ host env threads + HIP learner
+  actor_learner  runtime/actor_learner.py   actor ranks -> learner group over RCCL
+  pixel          runtime/pixel_trainer.py   Pong pixels, Nature-CNN A2C
+
+The engine trains on its own vectorised envs; ``TrainingServer.train(...)`` drives epochs,
+writes the reference's ``progress.txt`` columns (REINFORCE.py:127-139) through the
+EpochLogger and publishes each new policy to the server's ModelStore, so agents attached
+over ZMQ / gRPC / local keep receiving models exactly as with the trajectory learner.
+With ``world_size > 1`` the ranks run as a ``torch.distributed.run`` CHILD process (one
+rank per GPU, RCCL); rank 0 drops versioned weight files that the API process publishes.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, Optional
+
+import torch
+
+from ..algorithms.base import AlgorithmAbstract
+
+ENGINE_KINDS = ("vec", "host", "actor_learner", "pixel")
+# (obs_dim, act_dim) of the built-in envs -> env name (the reference passes only the dims)
+ENV_BY_DIMS = {(4, 2): "CartPole-v1", (2, 3): "MountainCar-v0", (6, 3): "Acrobot-v1",
+               (8, 4): "LunarLanderSynth-v0", (17, 6): "HalfCheetahSynth-v0"}
+# reference hyperparameter name -> trainer config field
+_PARAM_MAP = {"gamma": "gamma", "lam": "lam", "pi_lr": "pi_lr", "vf_lr": "vf_lr", "train_vf_iters": "train_vf_iters",
+              "train_pi_iters": "train_pi_iters", "clip_ratio": "clip_ratio", "target_kl": "target_kl",
+              "ent_coef": "ent_coef", "seed": "seed", "with_vf_baseline": "with_baseline"}
+# "mi355x" block name -> trainer config field
+_MI355X_MAP = {"envs_per_actor": "num_envs", "num_envs": "num_envs", "rollout_len": "rollout_len",
+               "hidden": "hidden", "use_graphs": "use_graphs", "max_episode_steps": "max_episode_steps",
+               "num_threads": "num_threads", "learner_acts": "learner_acts", "max_lag": "max_lag",
+               "learner_ranks": "learner_ranks"}
+
+
+@dataclass
+class EngineSpec:
+    kind: str
+    env: str
+    algo: str                     # reinforce | ppo | a2c
+    world_size: int = 1
+    trainer: Dict[str, Any] = field(default_factory=dict)
+
+    def to_json(self) -> str:
+        return json.dumps(dataclasses.asdict(self))
+
+    @staticmethod
+    def from_json(s: str) -> "EngineSpec":
+        return EngineSpec(**json.loads(s))
+
+
+def resolve_engine(algorithm_name: str, obs_dim: int, act_dim: int, algo_params: Dict[str, Any],
+                   mi355x: Dict[str, Any], hyperparams: Dict[str, Any], engine: Optional[str] = None
+                   ) -> Optional[EngineSpec]:
+    """EngineSpec from (explicit engine > hyperparams > config "mi355x" block), or None for the
+    trajectory learner.  Hyperparameters override the config like everywhere else (A9)."""
+    hp = dict(hyperparams or {})
+    kind = engine or hp.pop("engine", None) or mi355x.get("engine")
+    hp.pop("engine", None)
+    if not kind:
+        return None
+    kind = str(kind).lower()
+    if kind not in ENGINE_KINDS:
+        raise ValueError(f"engine must be one of {ENGINE_KINDS}, not {kind!r}")
+    env = hp.pop("env", None) or mi355x.get("env") or ("PongSynth-v0" if kind == "pixel" else
+                                                        ENV_BY_DIMS.get((int(obs_dim), int(act_dim))))
+    if env is None:
+        raise ValueError(f"no built-in env with obs_dim={obs_dim}, act_dim={act_dim}; name one in the "
+                         "'mi355x' config block (\"env\": ...) or hyperparams")
+    world = int(hp.pop("world_size", mi355x.get("world_size", 1)) or 1)
+    algo = {"REINFORCE": "reinforce", "PPO": "ppo", "A2C": "a2c"}.get(algorithm_name.upper(), "reinforce")
+    tr: Dict[str, Any] = {}
+    for k, v in (algo_params or {}).items():
+        if k in _PARAM_MAP and v is not None:
+            tr[_PARAM_MAP[k]] = v
+    for k, v in mi355x.items():
+        if k in _MI355X_MAP:
+            tr[_MI355X_MAP[k]] = v
+    for k, v in hp.items():  # explicit overrides win (any trainer field by its own name too)
+        tr[_PARAM_MAP.get(k, _MI355X_MAP.get(k, k))] = v
+    if kind != "pixel":
+        tr["env"] = env
+        tr["algo"] = algo
+    if kind == "pixel":
+        # A2C on pixels: one lr for the shared CNN
+        if "pi_lr" in tr and "lr" not in tr:
+            tr["lr"] = tr["pi_lr"]
+    return EngineSpec(kind, env, algo, world, tr)
+
+
+def _filter(cls, kw: Dict[str, Any]) -> Dict[str, Any]:
+    names = {f.name for f in dataclasses.fields(cls)}
+    return {k: v for k, v in kw.items() if k in names}
+
+
+def make_trainer(spec: EngineSpec, comm=None, device=None):
+    kw = dict(spec.trainer)
+    if spec.kind == "vec":
+        from .vec_trainer import VecTrainer, VecTrainerConfig
+
+        return VecTrainer(VecTrainerConfig(**_filter(VecTrainerConfig, kw)), comm, device)
+    if spec.kind == "host":
+        from .host_trainer import HostTrainerConfig, HostVecTrainer
+
+        return HostVecTrainer(HostTrainerConfig(**_filter(HostTrainerConfig, kw)), comm, device)
+    if spec.kind == "actor_learner":
+        from .actor_learner import ActorLearner, ActorLearnerConfig
+
+        return ActorLearner(ActorLearnerConfig(**_filter(ActorLearnerConfig, kw)), comm, device)
+    from .pixel_trainer import PixelA2CConfig, PixelA2CTrainer
+
+    return PixelA2CTrainer(PixelA2CConfig(**_filter(PixelA2CConfig, kw)), comm, device)
+
+
+def _epoch(tr):
+    return tr.train_epoch() if hasattr(tr, "train_epoch") else tr.step()
+
+
+# reference progress.txt columns (REINFORCE.py:127-139, progress.txt:1 of the shipped gRPC run)
+_REF_COLS = ("AverageEpRet", "StdEpRet", "MaxEpRet", "MinEpRet", "EpLen", "LossPi", "DeltaLossPi")
+_VF_COLS = ("AverageVVals", "StdVVals", "MaxVVals", "MinVVals", "LossV", "DeltaLossV")
+
+
+class EngineAlgorithm(AlgorithmAbstract):
+    """A device engine behind the plugin contract (AlgorithmAbstract, BaseAlgorithm.py:4-39):
+    ``train_model`` = one engine epoch, ``log_epoch`` = one reference progress.txt row,
+    ``save`` / ``model_bytes`` = the TorchScript policy (kernel.py:87-143 interface)."""
+
+    def __init__(self, spec: EngineSpec, env_dir: str = ".", save_model_path: Optional[str] = None, comm=None,
+                 device=None, log: bool = True):
+        self.spec = spec
+        if device is None and torch.cuda.is_available():
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.trainer = make_trainer(spec, comm, device)
+        self.comm = getattr(self.trainer, "comm", None)
+        self.rank = 0 if self.comm is None else self.comm.rank
+        self.save_model_path = save_model_path or os.path.join(os.getcwd(), "server_model.pt")
+        self.version = 0
+        self.epoch = 0
+        self.ignored_trajectories = 0
+        self.seed = int(spec.trainer.get("seed", 0))
+        self.logger = None
+        if log and self.rank == 0:
+            from ..utils.logger import EpochLogger, setup_logger_kwargs
+
+            exp = f"relayrl-{spec.algo}-{spec.kind}-info"
+            self.logger = EpochLogger(**setup_logger_kwargs(exp, self.seed, data_dir=os.path.join(env_dir, "logs")),
+                                      quiet=True)
+            self.logger.save_config({"engine": dataclasses.asdict(spec),
+                                     "world_size": 1 if self.comm is None else self.comm.world})
+        self.last_metrics: Dict[str, Any] = {}
+
+    # ------------------------------------------------------------------ model access
+    @property
+    def learner(self):
+        return getattr(self.trainer, "learner", None)
+
+    @property
+    def publishes_policy(self) -> bool:
+        """MLP policies can be served to agents (NativePolicy / TorchScript); the CNN cannot."""
+        return self.learner is not None and self.spec.kind != "pixel"
+
+    def get_weights(self) -> Dict[str, Any]:
+        lr = self.learner
+        if lr is None:
+            return {"pi": torch.zeros(1), "version": self.version, "obs_dim": 0, "act_dim": 0, "hidden": 0,
+                    "discrete": True}
+        w = {"pi": lr.pi.params.detach().cpu().clone(), "version": self.version, "obs_dim": lr.obs_dim,
+             "act_dim": lr.act_dim, "hidden": lr.hidden, "discrete": lr.discrete}
+        if lr.vf is not None:
+            w["vf"] = lr.vf.params.detach().cpu().clone()
+        return w
+
+    def policy_module(self):
+        from ..models.policies import build_policy_module
+
+        lr = self.learner
+        if lr is None:
+            raise RuntimeError(f"the {self.spec.kind} engine has no MLP policy to export")
+        return build_policy_module(lr.obs_dim, lr.act_dim, lr.hidden, lr.pi.params,
+                                   None if lr.vf is None else lr.vf.params, lr.discrete)
+
+    def model_bytes(self) -> bytes:
+        from ..models.policies import torchscript_bytes
+
+        return torchscript_bytes(self.policy_module())
+
+    def save(self, path: Optional[str] = None) -> None:
+        from ..models.policies import export_torchscript
+
+        export_torchscript(self.policy_module(), path or self.save_model_path)
+
+    # ------------------------------------------------------------------ plugin contract
+    def receive_trajectory(self, trajectory) -> bool:
+        # the engine learns from its own device envs; agent uploads are counted, not trained on
+        self.ignored_trajectories += 1
+        return False
+
+    def train_model(self) -> None:
+        _epoch(self.trainer)
+        self.epoch += 1
+        self.version += 1
+
+    def epoch_metrics(self) -> Dict[str, Any]:
+        m = self.trainer.metrics() or {}
+        self.last_metrics = m
+        return m
+
+    def log_epoch(self, m: Optional[Dict[str, Any]] = None, extra: Optional[Dict[str, float]] = None) -> None:
+        if self.logger is None:
+            return
+        m = self.epoch_metrics() if m is None else m
+        lg = self.logger
+        nan = float("nan")
+        lg.log_tabular("Epoch", self.epoch)
+        for k in _REF_COLS:
+            lg.log_tabular(k, float(m.get(k, 0.0 if k == "DeltaLossPi" else nan)))
+        if self.learner is not None and self.learner.vf is not None:
+            vv = {"AverageVVals": m.get("VVals", nan), "LossV": m.get("LossV", nan),
+                  "DeltaLossV": m.get("DeltaLossV", nan)}
+            for k in _VF_COLS:
+                lg.log_tabular(k, float(vv.get(k, nan)))
+        lg.log_tabular("KL", float(m.get("KL", nan)))
+        lg.log_tabular("Entropy", float(m.get("Entropy", nan)))
+        for k, v in (extra or {}).items():
+            lg.log_tabular(k, float(v))
+        lg.dump_tabular()
+
+    def episode_sums(self, m: Optional[Dict[str, Any]] = None):
+        """(finished episodes, their return sum) of the last epoch, global over ranks."""
+        if m is None and hasattr(self.trainer, "episode_sums"):
+            return self.trainer.episode_sums()
+        m = self.epoch_metrics() if m is None else m
+        n = float(m.get("Episodes", 0) or 0)
+        r = m.get("AverageEpRet", float("nan"))
+        return n, (n * r if n > 0 and r == r else 0.0)
+
+    def state_dict(self) -> Dict[str, Any]:
+        return {"trainer": self.trainer.state_dict(), "epoch": self.epoch, "version": self.version}
+
+    def load_state_dict(self, sd: Dict[str, Any]):
+        self.trainer.load_state_dict(sd["trainer"])
+        self.epoch, self.version = int(sd["epoch"]), int(sd["version"])
+
+
+@dataclass
+class TrainResult:
+    epochs: int
+    seconds: float
+    env_steps: int
+    solved: bool
+    time_to_threshold_s: Optional[float]   # from TrainingServer construction
+    last_window_return: float
+    metrics: Dict[str, Any]
+
+    def to_dict(self):
+        return dataclasses.asdict(self)
+
+
+class EngineRunner:
+    """Drives an in-process EngineAlgorithm: epochs, the return-threshold check, logging and
+    model publishing to the server's LearnerService store."""
+
+    def __init__(self, algo: EngineAlgorithm, service, t_start: float):
+        self.algo = algo
+        self.service = service
+        self.t_start = t_start
+        self._thread: Optional[threading.Thread] = None
+        self._stop = threading.Event()
+        self.result: Optional[TrainResult] = None
+        self._lock = threading.Lock()
+
+    def _publish(self):
+        if self.algo.publishes_policy:
+            self.service.updates += 1
+            self.service.publish_model()
+
+    def train(self, epochs: Optional[int] = None, target_return: Optional[float] = None, window: int = 100,
+              max_seconds: Optional[float] = None, log_every: int = 1, publish_every: int = 1) -> TrainResult:
+        """Run until ``epochs`` epochs, the mean return of the newest >= ``window`` finished
+        episodes reaching ``target_return`` (checked once per epoch), or ``max_seconds``."""
+        from .vec_trainer import SolvedCheck
+
+        if epochs is None and target_return is None and max_seconds is None:
+            raise ValueError("give epochs, target_return or max_seconds")
+        with self._lock:
+            algo = self.algo
+            comm = algo.comm
+            world = 1 if comm is None else comm.world
+            check = SolvedCheck(target_return, window) if target_return is not None else None
+            t0 = time.perf_counter()
+            e0 = algo.epoch
+            steps0 = int(getattr(algo.trainer, "env_steps", 0)) * world
+            solved, ttt, win = False, None, float("nan")
+            m: Dict[str, Any] = {}
+            while not self._stop.is_set():
+                algo.train_model()
+                k = algo.epoch - e0
+                # every rank takes the same branches: metrics() / episode_sums() are collectives
+                log_now = bool(log_every) and k % log_every == 0
+                m = algo.epoch_metrics() if log_now else {}
+                if check is not None:
+                    win = check.update(*algo.episode_sums(m if log_now else None))
+                    if check.solved(win):
+                        solved = True
+                        ttt = time.perf_counter() - self.t_start
+                if log_now:
+                    el = time.perf_counter() - t0
+                    extra = {"Time": el}
+                    if "EnvSteps" in m and el > 0:
+                        extra["EnvStepsPerSec"] = (m["EnvSteps"] - steps0) / el
+                    algo.log_epoch(m, extra)
+                if publish_every and k % publish_every == 0:
+                    self._publish()
+                if solved:
+                    break
+                if epochs is not None and k >= epochs:
+                    break
+                if max_seconds is not None and _agree(comm, time.perf_counter() - t0 >= max_seconds):
+                    break
+            if not publish_every or (algo.epoch - e0) % publish_every:
+                self._publish()
+            el = time.perf_counter() - t0
+            steps = int(getattr(algo.trainer, "env_steps", 0)) * world - steps0
+            self.result = TrainResult(algo.epoch - e0, el, steps, solved, ttt, win,
+                                      {k: v for k, v in m.items() if isinstance(v, (int, float))})
+            return self.result
+
+    def start(self, **kw):
+        """Train in a background thread (``join()`` for the result)."""
+        self._stop.clear()
+        self._thread = threading.Thread(target=lambda: self.train(**kw), name="relayrl-engine", daemon=True)
+        self._thread.start()
+
+    def stop(self):
+        self._stop.set()
+
+    def join(self, timeout: Optional[float] = None) -> Optional[TrainResult]:
+        if self._thread is not None:
+            self._thread.join(timeout)
+        return self.result
+
+
+def _agree(comm, flag: bool) -> bool:
+    """True on every rank if it is true on any (wall-clock stops must not split the ranks)."""
+    if comm is None or comm.world == 1:
+        return flag
+    dev = "cuda" if comm.backend == "nccl" else "cpu"
+    t = torch.tensor([1.0 if flag else 0.0], device=dev)
+    comm.all_reduce_max_(t)
+    return bool(t.item() > 0)
+
+
+# ---------------------------------------------------------------------- multi-rank (child ranks)
+class RemoteEngineAlgorithm(AlgorithmAbstract):
+    """API-side view of an engine whose ranks run in a child ``torch.distributed.run``: holds
+    the newest policy rank 0 published (``publish_dir``) so the server can serve it."""
+
+    def __init__(self, spec: EngineSpec, obs_dim: int, act_dim: int, publish_dir: str,
+                 save_model_path: Optional[str] = None):
+        from ..ops.mlp import MLPSpec
+
+        self.spec = spec
+        self.publish_dir = publish_dir
+        os.makedirs(publish_dir, exist_ok=True)
+        self.save_model_path = save_model_path or os.path.join(os.getcwd(), "server_model.pt")
+        self.obs_dim, self.act_dim = int(obs_dim), int(act_dim)
+        self.hidden = int(spec.trainer.get("hidden", 128))
+        self.discrete = spec.env != "HalfCheetahSynth-v0"
+        g = torch.Generator().manual_seed(int(spec.trainer.get("seed", 0)))
+        self.pi = MLPSpec(self.obs_dim, self.hidden, self.act_dim, not self.discrete).init(g)
+        with_vf = bool(spec.trainer.get("with_baseline", True)) or spec.algo in ("a2c", "ppo")
+        self.vf = MLPSpec(self.obs_dim, self.hidden, 1).init(g) if with_vf else None
+        self.version = 0
+        self.epoch = 0
+
+    def poll(self) -> bool:
+        """Load a newer published policy if rank 0 wrote one; True when it did."""
+        p = os.path.join(self.publish_dir, "latest.json")
+        try:
+            meta = json.load(open(p))
+        except (OSError, ValueError):
+            return False
+        if int(meta["version"]) <= self.version:
+            return False
+        from safetensors.torch import load_file
+
+        t = load_file(os.path.join(self.publish_dir, meta["file"]))
+        self.pi = t["pi"]
+        if "vf" in t:
+            self.vf = t["vf"]
+        self.version = int(meta["version"])
+        self.epoch = int(meta.get("epoch", self.version))
+        return True
+
+    def get_weights(self) -> Dict[str, Any]:
+        w = {"pi": self.pi.clone(), "version": self.version, "obs_dim": self.obs_dim, "act_dim": self.act_dim,
+             "hidden": self.hidden, "discrete": self.discrete}
+        if self.vf is not None:
+            w["vf"] = self.vf.clone()
+        return w
+
+    def policy_module(self):
+        from ..models.policies import build_policy_module
+
+        return build_policy_module(self.obs_dim, self.act_dim, self.hidden, self.pi, self.vf, self.discrete)
+
+    def model_bytes(self) -> bytes:
+        from ..models.policies import torchscript_bytes
+
+        return torchscript_bytes(self.policy_module())
+
+    def save(self, path: Optional[str] = None) -> None:
+        from ..models.policies import export_torchscript
+
+        export_torchscript(self.policy_module(), path or self.save_model_path)
+
+    def receive_trajectory(self, trajectory) -> bool:
+        return False
+
+    def train_model(self) -> None:
+        raise RuntimeError("the ranks train in the child process; use TrainingServer.train()")
+
+    def log_epoch(self) -> None:
+        pass
+
+
+def publish_weights(algo: EngineAlgorithm, publish_dir: str) -> None:
+    """Rank 0: write the current policy as ``model_<version>.safetensors`` + ``latest.json``."""
+    from safetensors.torch import save_file
+
+    w = algo.get_weights()
+    os.makedirs(publish_dir, exist_ok=True)
+    name = f"model_{algo.version:08d}.safetensors"
+    t = {"pi": w["pi"].contiguous()}
+    if w.get("vf") is not None:
+        t["vf"] = w["vf"].contiguous()
+    save_file(t, os.path.join(publish_dir, name))
+    tmp = os.path.join(publish_dir, f"latest.json.tmp{os.getpid()}")
+    with open(tmp, "w") as f:
+        json.dump({"version": algo.version, "epoch": algo.epoch, "file": name}, f)
+    os.replace(tmp, os.path.join(publish_dir, "latest.json"))
+    old = os.path.join(publish_dir, f"model_{algo.version - 2:08d}.safetensors")
+    if algo.version >= 2 and os.path.exists(old):
+        os.remove(old)
+
+
+class MultiRankEngineRunner:
+    """Runs the engine's ranks as a ``torch.distributed.run`` child (one rank per GPU over
+    RCCL) and republishes rank 0's policy files to the server's store."""
+
+    def __init__(self, algo: RemoteEngineAlgorithm, service, env_dir: str, t_start: float):
+        self.algo = algo
+        self.service = service
+        self.env_dir = env_dir
+        self.t_start = t_start
+        self.result: Optional[TrainResult] = None
+
+    def _watch(self, stop: threading.Event):
+        while not stop.is_set():
+            if self.algo.poll():
+                self.service.updates += 1
+                self.service.publish_model()
+            stop.wait(0.05)
+
+    def train(self, epochs: Optional[int] = None, target_return: Optional[float] = None, window: int = 100,
+              max_seconds: Optional[float] = None, log_every: int = 1, publish_every: int = 1) -> TrainResult:
+        from .launcher import spawn_ranks
+
+        spec_path = os.path.join(self.algo.publish_dir, "spec.json")
+        with open(spec_path, "w") as f:
+            f.write(self.algo.spec.to_json())
+        res_path = os.path.join(self.algo.publish_dir, "result.json")
+        if os.path.exists(res_path):
+            os.remove(res_path)
+        argv = ["engine", "--spec", spec_path, "--env-dir", self.env_dir, "--publish-dir", self.algo.publish_dir,
+                "--log-every", str(log_every), "--publish-every", str(publish_every), "--window", str(window),
+                "--t-start-wall", repr(time.time() - (time.perf_counter() - self.t_start)), "--result", res_path]
+        if epochs is not None:
+            argv += ["--epochs", str(epochs)]
+        if target_return is not None:
+            argv += ["--target-return", str(target_return)]
+        if max_seconds is not None:
+            argv += ["--max-seconds", str(max_seconds)]
+        stop = threading.Event()
+        w = threading.Thread(target=self._watch, args=(stop,), daemon=True)
+        w.start()
+        try:
+            rc = spawn_ranks(argv, self.algo.spec.world_size)
+        finally:
+            stop.set()
+            w.join()
+        if self.algo.poll():
+            self.service.updates += 1
+            self.service.publish_model()
+        if rc != 0:
+            raise RuntimeError(f"engine ranks exited with code {rc}")
+        d = json.load(open(res_path))
+        self.result = TrainResult(**d)
+        return self.result
+
+
+def run_engine_rank(spec: EngineSpec, env_dir: str, publish_dir: Optional[str], epochs: Optional[int],
+                    target_return: Optional[float], window: int, max_seconds: Optional[float], log_every: int,
+                    publish_every: int, t_start_wall: Optional[float], result_path: Optional[str]) -> int:
+    """One rank of a multi-GPU engine (``python -m relayrl_prototype_amd engine ...``)."""
+    from ..parallel.comm import Comm, dist_env, init_distributed, local_device_index
+
+    _, _, world = dist_env()
+    comm = init_distributed() if world > 1 else Comm()
+    dev = None
+    if torch.cuda.is_available():
+        dev = torch.device("cuda", local_device_index())
+        torch.cuda.set_device(dev)
+    algo = EngineAlgorithm(spec, env_dir, comm=comm, device=dev)
+
+    class _Pub:  # rank 0 publishes through files instead of a ModelStore
+        updates = 0
+
+        def publish_model(self):
+            if algo.rank == 0 and publish_dir and algo.publishes_policy:
+                publish_weights(algo, publish_dir)
+
+    # the clock of the threshold metric starts where the API object was built (parent process)
+    t_start = time.perf_counter() - (time.time() - t_start_wall) if t_start_wall else time.perf_counter()
+    r = EngineRunner(algo, _Pub(), t_start)
+    res = r.train(epochs, target_return, window, max_seconds, log_every, publish_every)
+    if algo.rank == 0 and result_path:
+        tmp = result_path + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(res.to_dict(), f)
+        os.replace(tmp, result_path)
+    if hasattr(algo.trainer, "finish"):
+        algo.trainer.finish()
+    if comm.world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+    return 0

@@ -89,7 +89,10 @@ class HostVecTrainer:
         # pinned host staging (env side) and HBM rollout buffers (learner side)
         self.h_obs = torch.zeros(T + 1, N, D, pin_memory=pin)
         self.h_rew = torch.zeros(T, N, pin_memory=pin)
-        self.h_done = torch.zeros(T, N, pin_memory=pin)
+        self.h_done = torch.zeros(T, N, pin_memory=pin)  # 0 / 1 terminal / 2 time-limit truncation
+        # pre-reset observations of truncated steps (bootstrap V(s_T) of cut episodes)
+        self.h_tobs = torch.zeros(T, N, D, pin_memory=pin) if self.learner.vf is not None else None
+        self.d_tobs = torch.zeros(T, N, D, device=self.device) if self.learner.vf is not None else None
         if self.continuous:
             self.h_act = torch.zeros(T, N, A, pin_memory=pin)
             self.d_act = torch.zeros(T, N, A, device=self.device)
@@ -145,7 +148,8 @@ class HostVecTrainer:
     def _step_env(self, t, h):
         lo = self.bounds[h]
         self.envs[h].step_ptr(self.h_act[t, lo].data_ptr(), self.h_obs[t + 1, lo].data_ptr(),
-                              self.h_rew[t, lo].data_ptr(), self.h_done[t, lo].data_ptr())
+                              self.h_rew[t, lo].data_ptr(), self.h_done[t, lo].data_ptr(),
+                              self.h_tobs[t, lo].data_ptr() if self.h_tobs is not None else 0)
 
     def rollout(self):
         T = self.cfg.rollout_len
@@ -162,11 +166,15 @@ class HostVecTrainer:
                 self.d_obs[T].copy_(self.h_obs[T], non_blocking=True)
                 self.d_rew.copy_(self.h_rew, non_blocking=True)
                 self.d_done.copy_(self.h_done, non_blocking=True)
+                if self.d_tobs is not None:
+                    self.d_tobs.copy_(self.h_tobs, non_blocking=True)
             torch.cuda.current_stream(self.device).wait_stream(self.copy_stream)
         else:
             self.d_obs[T].copy_(self.h_obs[T])
             self.d_rew.copy_(self.h_rew)
             self.d_done.copy_(self.h_done)
+            if self.d_tobs is not None:
+                self.d_tobs.copy_(self.h_tobs)
         self.global_step += T
         self.timings["rollout_s"] += time.perf_counter() - t0
 
@@ -174,7 +182,7 @@ class HostVecTrainer:
         with self.timer.phase("Rollout"):
             self.rollout()
         t0 = time.perf_counter()
-        self.rl.learn(self.d_obs, self.d_act, self.d_rew, self.d_done, self.d_logp)
+        self.rl.learn(self.d_obs, self.d_act, self.d_rew, self.d_done, self.d_logp, tobs=self.d_tobs)
         # next rollout starts from the last observation
         self.h_obs[0].copy_(self.h_obs[self.cfg.rollout_len])
         self.timings["learn_s"] += time.perf_counter() - t0

@@ -257,6 +257,18 @@ def main(argv=None) -> int:
     t.add_argument("--resume", default=None)
     t.add_argument("--auto-resume", action="store_true", help="continue from this rank's last checkpoint if any")
     t.add_argument("--max-restarts", type=int, default=0, help="torchrun group restarts after a rank failure")
+    e = sub.add_parser("engine", help="one rank of a TrainingServer device engine (runtime/engine.py)")
+    e.add_argument("--spec", required=True)
+    e.add_argument("--env-dir", default=".")
+    e.add_argument("--publish-dir", default=None)
+    e.add_argument("--epochs", type=int, default=None)
+    e.add_argument("--target-return", type=float, default=None)
+    e.add_argument("--window", type=int, default=100)
+    e.add_argument("--max-seconds", type=float, default=None)
+    e.add_argument("--log-every", type=int, default=1)
+    e.add_argument("--publish-every", type=int, default=1)
+    e.add_argument("--t-start-wall", type=float, default=None)
+    e.add_argument("--result", default=None)
     sub.add_parser("presets", help="list the presets")
     b = sub.add_parser("build", help="compile the HIP and C++ extensions in-tree")
     b.add_argument("--force", action="store_true")
@@ -272,6 +284,12 @@ def main(argv=None) -> int:
 
         build(force=a.force)
         return 0
+    if a.cmd == "engine":
+        from .engine import EngineSpec, run_engine_rank
+
+        spec = EngineSpec.from_json(open(a.spec).read())
+        return run_engine_rank(spec, a.env_dir, a.publish_dir, a.epochs, a.target_return, a.window, a.max_seconds,
+                               a.log_every, a.publish_every, a.t_start_wall, a.result)
     if a.cmd == "plot":
         from ..utils.plot import main as plot_main
 

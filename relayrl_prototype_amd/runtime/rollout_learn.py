@@ -24,6 +24,7 @@ class RolloutLearner:
         self.comm = comm or Comm()
         dev = learner.device
         self.val = torch.zeros(T + 1, N, device=dev) if learner.vf is not None else None
+        self.tval = torch.zeros(T, N, device=dev) if learner.vf is not None else None  # V(pre-reset obs)
         self.adv = torch.zeros(T, N, device=dev)
         self.ret = torch.zeros(T, N, device=dev)
         self.adv_stats = torch.zeros(3, device=dev)
@@ -33,8 +34,12 @@ class RolloutLearner:
 
             self.stats_part = torch.zeros(hip().scan_tm_parts(N), 3, device=dev)
 
-    def learn(self, obs, act, rew, done, logp, mask=None):
-        """obs [T+1, N, D]; act [T, N] int32 or [T, N, A]; rew / done / logp [T, N]."""
+    def learn(self, obs, act, rew, done, logp, mask=None, tobs=None):
+        """obs [T+1, N, D]; act [T, N] int32 or [T, N, A]; rew / done / logp [T, N].
+
+        done codes 0 / 1 / 2 = running / terminal / time-limit truncation; ``tobs`` [T, N, D]
+        holds the pre-reset observation of truncated steps, whose value bootstraps the cut
+        episode (replay_buffer.py:48-79 finish_path(last_val))."""
         T, N = self.T, self.N
         lr = self.learner
         D = obs.shape[-1]
@@ -47,9 +52,14 @@ class RolloutLearner:
                     mlp_forward(FwdMode.VALUE, lr.vf.params, obs_all, 1, lr.hidden, out={"v": self.val.view(-1)})
                 else:
                     self.val.view(-1).copy_(mlp_forward(FwdMode.VALUE, lr.vf.params, obs_all, 1, lr.hidden)["v"])
+                if tobs is not None:
+                    # only the 16-row tiles holding a truncation are evaluated (gate = done codes)
+                    mlp_forward(FwdMode.VALUE, lr.vf.params, tobs.reshape(T * N, D), 1, lr.hidden,
+                                out={"v": self.tval.view(-1)}, gate=done.reshape(-1))
         with tm.phase("Scan"):
             adv, ret, stats = gae_scan_tm(rew, done, self.val, self.gamma, self.lam, adv=self.adv, ret=self.ret,
-                                          stats_part=self.stats_part, stats_out=self.adv_stats)
+                                          stats_part=self.stats_part, stats_out=self.adv_stats,
+                                          tval=self.tval if tobs is not None else None)
             if not rew.is_cuda:
                 self.adv.copy_(adv)
                 self.ret.copy_(ret)

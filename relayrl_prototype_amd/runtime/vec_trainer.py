@@ -129,7 +129,10 @@ class VecTrainer:
             self.act = torch.zeros(T, N, dtype=torch.int32, device=dev)
         self.logp = torch.zeros(T, N, device=dev)
         self.rew = torch.zeros(T, N, device=dev)
-        self.done = torch.zeros(T, N, device=dev)
+        self.done = torch.zeros(T, N, device=dev)  # 0 running / 1 terminal / 2 time-limit truncation
+        # pre-reset observation of truncated steps (read only where done == 2): the scan
+        # bootstraps a cut episode with V(s_T) like the reference's last_val
+        self.tobs = torch.zeros(T, N, D, device=dev) if cfg.with_baseline or cfg.algo != "reinforce" else None
         self.state = torch.zeros(N, NS, device=dev)
         self.ep_len = torch.zeros(N, dtype=torch.int32, device=dev)
         self.ep_ret = torch.zeros(N, device=dev)
@@ -146,18 +149,18 @@ class VecTrainer:
         step0 = self.epoch * cfg.rollout_len
         if self.continuous:
             h.rollout_cont(self.env_id, self.pi.params, self.env_consts, cfg.hidden, self.state, self.ep_len,
-                           self.ep_ret, self.obs, self.act, self.logp, self.rew, self.done, self.ep_stats,
+                           self.ep_ret, self.obs, self.act, self.logp, self.rew, self.done, self.tobs, self.ep_stats,
                            self.env_seed, step0, self._first, self.max_steps)
         else:
             h.rollout(self.env_id, self.pi.params, cfg.hidden, self.state, self.ep_len, self.ep_ret, self.obs,
-                      self.act, self.logp, self.rew, self.done, self.ep_stats, self.env_seed, step0, self._first,
-                      self.max_steps)
+                      self.act, self.logp, self.rew, self.done, self.tobs, self.ep_stats, self.env_seed, step0,
+                      self._first, self.max_steps)
         self._first = False
 
     def train_epoch(self):
         with self.timer.phase("Rollout"):
             self.rollout()
-        self.rl.learn(self.obs, self.act, self.rew, self.done, self.logp)
+        self.rl.learn(self.obs, self.act, self.rew, self.done, self.logp, tobs=self.tobs)
         self.epoch += 1
         self.env_steps += self.B
 

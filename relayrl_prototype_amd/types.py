@@ -317,16 +317,19 @@ class TrajectoryColumns:
     (trajectory.rs:50-55, action.rs:40-90), i.e. O(actions x tensors) encode work on the
     agent and the learner.  An RRLC frame is a fixed header + agent id + contiguous
     little-endian arrays (obs [n,D] f32, act [n,K] f32|i32, mask [n,A] f32, rew [n] f32,
-    logp [n] f32, done [n] u8), so encode is a handful of memcpys and decode is zero-copy
+    logp [n] f32, done [n] u8, then -- flags bit 0 -- next_obs [D] f32: the observation that
+    follows the last action of a cut segment, whose value bootstraps it, like the
+    reference's finish_path(last_val), replay_buffer.py:48-79), so encode is a handful of memcpys and decode is zero-copy
     ``np.frombuffer`` views that the learner appends to its flat buffer in one slice
     assignment.  ``get_actions()`` materialises RelayRLAction objects for code that wants
     the reference's per-action view.
     """
 
-    __slots__ = ("obs", "act", "mask", "rew", "logp", "done", "agent_id", "seq", "max_length", "trajectory_server")
+    __slots__ = ("obs", "act", "mask", "rew", "logp", "done", "agent_id", "seq", "max_length", "trajectory_server",
+                 "next_obs")
 
     def __init__(self, obs, act, rew, done, mask=None, logp=None, agent_id: str = "", seq: int = 0,
-                 max_length: int = 1000):
+                 max_length: int = 1000, next_obs=None):
         self.obs = obs
         self.act = act
         self.rew = rew
@@ -337,6 +340,7 @@ class TrajectoryColumns:
         self.seq = seq
         self.max_length = max_length
         self.trajectory_server = None
+        self.next_obs = next_obs  # [D] or None: s_T of a cut (not done) segment
 
     def __len__(self):
         return int(self.rew.shape[0])
@@ -356,8 +360,11 @@ class TrajectoryColumns:
         act = np.ascontiguousarray(act, _ACT_KINDS[kind])
         A = 0 if self.mask is None else self._rows(self.mask, n).shape[1]
         aid = self.agent_id.encode()
+        nxt = None if self.next_obs is None else np.ascontiguousarray(self.next_obs, np.float32).reshape(-1)
+        if nxt is not None and nxt.size != obs.shape[1]:
+            raise ValueError(f"next_obs has {nxt.size} values, observations have {obs.shape[1]}")
         hdr = struct.pack(_RRLC_HDR, _RRLC_MAGIC, 1, n, obs.shape[1], act.shape[1], A, kind,
-                          self.mask is not None, self.logp is not None, 0, int(self.seq))
+                          self.mask is not None, self.logp is not None, 1 if nxt is not None else 0, int(self.seq))
         parts = [hdr, struct.pack("<H", len(aid)), aid, obs.tobytes(), act.tobytes()]
         if self.mask is not None:
             parts.append(np.ascontiguousarray(self.mask, np.float32).tobytes())
@@ -365,6 +372,8 @@ class TrajectoryColumns:
         if self.logp is not None:
             parts.append(np.ascontiguousarray(self.logp, np.float32).tobytes())
         parts.append(np.ascontiguousarray(self.done, np.uint8).tobytes())
+        if nxt is not None:
+            parts.append(nxt.tobytes())
         return b"".join(parts)
 
     @staticmethod
@@ -377,14 +386,16 @@ class TrajectoryColumns:
         hs = struct.calcsize(_RRLC_HDR)
         if len(mv) < hs + 2:
             raise ValueError("RRLC frame too short")
-        magic, ver, n, D, K, A, kind, has_mask, has_logp, _flags, seq = struct.unpack_from(_RRLC_HDR, mv, 0)
-        if magic != _RRLC_MAGIC or ver != 1 or kind not in _ACT_KINDS:
+        magic, ver, n, D, K, A, kind, has_mask, has_logp, flags, seq = struct.unpack_from(_RRLC_HDR, mv, 0)
+        if magic != _RRLC_MAGIC or ver != 1 or kind not in _ACT_KINDS or flags & ~1:
             raise ValueError("not an RRLC v1 frame")
+        has_next = bool(flags & 1)
         (alen,) = struct.unpack_from("<H", mv, hs)
         off = hs + 2
         aid = bytes(mv[off:off + alen]).decode()
         off += alen
-        need = off + 4 * n * (D + K + (A if has_mask else 0) + 1 + (1 if has_logp else 0)) + n
+        need = off + 4 * n * (D + K + (A if has_mask else 0) + 1 + (1 if has_logp else 0)) + n + \
+            (4 * D if has_next else 0)
         if len(mv) != need:
             raise ValueError(f"RRLC frame size {len(mv)} != expected {need}")
 
@@ -400,7 +411,8 @@ class TrajectoryColumns:
         rew = take(n, np.float32, (n,))
         logp = take(n, np.float32, (n,)) if has_logp else None
         done = take(n, np.uint8, (n,))
-        return TrajectoryColumns(obs, act, rew, done, mask, logp, aid, seq)
+        nxt = take(D, np.float32, (D,)) if has_next else None
+        return TrajectoryColumns(obs, act, rew, done, mask, logp, aid, seq, next_obs=nxt)
 
     def get_actions(self) -> List[RelayRLAction]:
         out = []
@@ -459,13 +471,14 @@ class EpisodeRecorder:
     def full(self) -> bool:
         return self.n >= self.capacity
 
-    def take(self, agent_id: str, seq: int, done: bool) -> TrajectoryColumns:
+    def take(self, agent_id: str, seq: int, done: bool, next_obs=None) -> TrajectoryColumns:
         n = self.n
         d = self.done[:n].copy()
         if n and done:
             d[n - 1] = 1
+        nxt = None if (done or next_obs is None) else np.asarray(next_obs, np.float32).reshape(-1).copy()
         cols = TrajectoryColumns(self.obs[:n].copy(), self.act[:n].copy(), self.rew[:n].copy(), d,
                                  None if self.mask is None else self.mask[:n].copy(), self.logp[:n].copy(),
-                                 agent_id, seq)
+                                 agent_id, seq, next_obs=nxt)
         self.n = 0
         return cols

@@ -1,0 +1,39 @@
+"""bench.py's multi-rank contract on CPU: ``python bench.py --gpus 2`` without an external
+launcher starts torch.distributed.run as a child (gloo here, RCCL on MI355X) and prints ONE
+JSON line for the whole job."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, timeout=300):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, cwd=REPO, env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
+    return r
+
+
+def test_bench_spawns_ranks_without_torchrun():
+    r = _run(["--gpus", "2", "--steps", "2", "--warmup", "1", "--device", "cpu", "--num-envs", "16",
+              "--rollout-len", "8", "--vf-iters", "2"], {"RRL_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["steps"] == 2 and rec["warmup"] == 1 and rec["backend"] == "gloo"
+    assert rec["config"]["global_batch"] == 2 * 16 * 8
+    assert len(rec["per_rank_env_steps_per_s"]) == 2
+    assert rec["value"] > 0 and rec["ms_per_step"] > 0
+    for k in ("metric", "unit", "higher_is_better", "scaling", "vs_baseline", "dtype", "data"):
+        assert k in rec
+
+
+def test_bench_rejects_world_size_mismatch():
+    r = _run(["--gpus", "2", "--device", "cpu"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr

@@ -1,0 +1,133 @@
+"""Device engines behind the reference API: TrainingServer(..., engine=...).
+
+CPU: the host engine (C++ env threads + oracle learner) trained through the API object, with
+progress.txt in the reference's columns and every update reaching an attached agent; the
+multi-rank path runs its ranks as a torch.distributed.run child over gloo.  The GPU twin
+(tests/test_engine_gpu.py) trains CartPole to the 475 threshold through the same call.
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from relayrl_prototype_amd.api.agent import RelayRLAgent
+from relayrl_prototype_amd.api.server import TrainingServer
+from relayrl_prototype_amd.config import DEFAULT_CONFIG_CONTENT
+from relayrl_prototype_amd.runtime.engine import resolve_engine
+from relayrl_prototype_amd.utils.logger import read_progress
+
+REF_COLS = ("Epoch", "AverageEpRet", "StdEpRet", "MaxEpRet", "MinEpRet", "EpLen", "LossPi", "DeltaLossPi",
+            "AverageVVals", "StdVVals", "MaxVVals", "MinVVals", "LossV", "DeltaLossV", "KL", "Entropy")
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture
+def cfgdir(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("RRL_QUIET_CONFIG", "1")
+    cfg = json.loads(DEFAULT_CONFIG_CONTENT)
+    cfg["algorithms"]["REINFORCE"]["with_vf_baseline"] = True
+    for k in ("training_server", "trajectory_server", "agent_listener"):
+        cfg["server"][k]["port"] = str(free_port())
+    p = tmp_path / "relayrl_config.json"
+    p.write_text(json.dumps(cfg))
+    return tmp_path, str(p)
+
+
+def test_resolve_engine_precedence():
+    ap = {"gamma": 0.98, "lam": 0.97, "pi_lr": 3e-4, "vf_lr": 1e-3, "train_vf_iters": 80, "with_vf_baseline": True,
+          "seed": 1, "traj_per_epoch": 8, "discrete": True}
+    mi = {"engine": "vec", "envs_per_actor": 2048, "rollout_len": 32, "world_size": 4}
+    spec = resolve_engine("REINFORCE", 4, 2, ap, mi, {"vf_lr": 1e-2, "num_envs": 512})
+    assert spec.kind == "vec" and spec.env == "CartPole-v1" and spec.world_size == 4 and spec.algo == "reinforce"
+    t = spec.trainer
+    assert t["gamma"] == 0.98 and t["lam"] == 0.97 and t["train_vf_iters"] == 80 and t["with_baseline"] is True
+    assert t["vf_lr"] == 1e-2 and t["num_envs"] == 512 and t["rollout_len"] == 32  # hyperparams beat the config
+    assert resolve_engine("REINFORCE", 4, 2, ap, {}, {}) is None  # no engine -> trajectory learner
+    assert resolve_engine("PPO", 17, 6, ap, {}, {}, engine="vec").env == "HalfCheetahSynth-v0"
+    with pytest.raises(ValueError):
+        resolve_engine("REINFORCE", 5, 5, ap, {}, {}, engine="vec")  # no env with those dims
+    with pytest.raises(ValueError):
+        resolve_engine("REINFORCE", 4, 2, ap, {}, {}, engine="warp")
+
+
+def test_training_server_host_engine_cpu(cfgdir):
+    tmp, cfgp = cfgdir
+    hp = {"num_envs": 16, "rollout_len": 16, "train_vf_iters": 2, "num_threads": 1}
+    srv = TrainingServer("REINFORCE", 4, 2, 1000, env_dir=str(tmp / "env"), config_path=cfgp, server_type="local",
+                         device="cpu", hyperparams=hp, engine="host")
+    try:
+        agent = RelayRLAgent(config_path=cfgp, server_type="local", handshake_timeout_s=30)
+        assert agent.model_version == 0
+        res = srv.train(epochs=3)
+        assert res.epochs == 3 and res.env_steps == 3 * 16 * 16
+        assert srv.model_version == 3 and agent.model_version == 3
+        # the agent acts with the engine's current policy
+        np.testing.assert_allclose(agent.policy.pi[0].T.ravel()[:8],
+                                   srv.algorithm.learner.pi.params[:8].numpy(), rtol=1e-6)
+        a = agent.request_for_action(np.zeros(4, np.float32), None, 0.0)
+        assert int(np.asarray(a.get_act()).reshape(-1)[0]) in (0, 1)
+        prog = list((tmp / "env" / "logs").rglob("progress.txt"))
+        assert len(prog) == 1
+        header = prog[0].read_text().splitlines()[0].split("\t")
+        for c in REF_COLS:
+            assert c in header, c
+        cols = read_progress(str(prog[0]))
+        assert cols["Epoch"] == [1.0, 2.0, 3.0]
+        # agent uploads are accepted but the engine trains on its own envs
+        agent.flag_last_action(1.0)
+        assert srv.wait_idle(10)
+        assert srv.algorithm.ignored_trajectories == 1
+        with pytest.raises(RuntimeError):
+            TrainingServer("REINFORCE", 4, 2, 1000, env_dir=str(tmp / "env2"), config_path=cfgp,
+                           server_type="local", training_port=str(free_port()), device="cpu").train(epochs=1)
+        agent.close()
+    finally:
+        srv.close(save=True)
+    assert os.path.exists(srv.cfg.get_server_model_path())  # TorchScript export on close
+
+
+def test_training_server_engine_from_config_block(cfgdir):
+    tmp, cfgp = cfgdir
+    cfg = json.loads(open(cfgp).read())
+    cfg["mi355x"] = {"engine": "host", "envs_per_actor": 8, "rollout_len": 8, "num_threads": 1}
+    cfg["algorithms"]["REINFORCE"]["train_vf_iters"] = 1
+    open(cfgp, "w").write(json.dumps(cfg))
+    srv = TrainingServer("REINFORCE", 4, 2, 1000, env_dir=str(tmp / "env"), config_path=cfgp, server_type="local",
+                         device="cpu")
+    try:
+        assert srv.engine_spec.kind == "host" and srv.engine_spec.trainer["num_envs"] == 8
+        res = srv.train(epochs=2, log_every=2, publish_every=2)
+        assert res.epochs == 2 and srv.model_version == 2
+    finally:
+        srv.close(save=False)
+
+
+def test_training_server_multi_rank_engine_gloo(cfgdir, monkeypatch):
+    """world_size 2: the ranks run in a torch.distributed.run child; rank 0's policy files are
+    republished by the API process."""
+    tmp, cfgp = cfgdir
+    monkeypatch.setenv("RRL_DIST_BACKEND", "gloo")
+    hp = {"num_envs": 8, "rollout_len": 8, "train_vf_iters": 1, "num_threads": 1, "world_size": 2}
+    srv = TrainingServer("REINFORCE", 4, 2, 1000, env_dir=str(tmp / "env"), config_path=cfgp, server_type="local",
+                         device="cpu", hyperparams=hp, engine="host")
+    try:
+        agent = RelayRLAgent(config_path=cfgp, server_type="local", handshake_timeout_s=30)
+        res = srv.train(epochs=2)
+        assert res.epochs == 2 and res.env_steps == 2 * 8 * 8 * 2  # both ranks' envs
+        assert srv.model_version == 2 and agent.model_version == 2
+        prog = list((tmp / "env" / "logs").rglob("progress.txt"))
+        assert len(prog) == 1  # rank 0 logs
+        assert read_progress(str(prog[0]))["Epoch"] == [1.0, 2.0]
+        agent.close()
+    finally:
+        srv.close(save=False)

@@ -16,7 +16,21 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_presets_cover_baseline_configs():
     base = json.load(open(os.path.join(REPO, "BASELINE.json")))["configs"]
     assert len(base) == 5 and len(PRESETS) >= 5
-    assert all(any(b.split()[0].lower().startswith(p.split("-")[-1][:3]) or True for p in PRESETS) for b in base)
+    # each BASELINE config -> the preset that runs it, checked on the config's own words
+    cover = {0: ("cartpole-reinforce-zmq", ("CartPole", "ZMQ")),
+             1: ("cartpole-reinforce-baseline", ("REINFORCE-with-baseline", "CartPole")),
+             2: ("lunarlander-reinforce-baseline", ("LunarLander", "RCCL")),
+             3: ("pong-a2c", ("A2C", "Pong")),
+             4: ("halfcheetah-ppo", ("PPO", "HalfCheetah"))}
+    for i, (name, words) in cover.items():
+        assert name in PRESETS, name
+        for w in words:
+            assert w in base[i], (i, w)
+    assert PRESETS["cartpole-reinforce-zmq"].overrides["server_type"] == "zmq"
+    assert PRESETS["cartpole-reinforce-baseline"].overrides["with_baseline"] is True
+    assert PRESETS["lunarlander-reinforce-baseline"].overrides["env"].startswith("LunarLander")
+    assert PRESETS["halfcheetah-ppo"].overrides["algo"] == "ppo"
+    assert PRESETS["pong-a2c"].kind == "pixel"
     kinds = {p.kind for p in PRESETS.values()}
     assert kinds == {"agent_server", "vec", "actor_learner", "pixel", "host"}
 

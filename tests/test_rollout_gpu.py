@@ -43,7 +43,7 @@ def test_cartpole_rollout(cuda, N, T, H):
     done = torch.zeros(T, N, device=dev)
     stats = torch.zeros(h.rollout_grid(N), 8, device=dev)
     seed, step0 = 777, 1000
-    h.rollout(0, params, H, state, ep_len, ep_ret, obs, act, logp, rew, done, stats, seed, step0, True, max_steps)
+    h.rollout(0, params, H, state, ep_len, ep_ret, obs, act, logp, rew, done, None, stats, seed, step0, True, max_steps)
     torch.cuda.synchronize()
     obs_c, act_c, logp_c, done_c = obs.cpu(), act.cpu(), logp.cpu(), done.cpu()
     # initial reset state from Philox tag 1
@@ -85,8 +85,8 @@ def test_rollout_other_envs(cuda):
         act = torch.zeros(T, N, dtype=torch.int32, device=cuda)
         f = [torch.zeros(T, N, device=cuda) for _ in range(3)]
         stats = torch.zeros(h.rollout_grid(N), 8, device=cuda)
-        h.rollout(env, params, H, bufs["state"], bufs["ep_len"], bufs["ep_ret"], obs, act, f[0], f[1], f[2], stats,
-                  1, 0, True, ms)
+        h.rollout(env, params, H, bufs["state"], bufs["ep_len"], bufs["ep_ret"], obs, act, f[0], f[1], f[2], None,
+                  stats, 1, 0, True, ms)
         torch.cuda.synchronize()
         assert torch.isfinite(obs).all()
         assert int(act.max().item()) < A and int(act.min().item()) >= 0
@@ -136,7 +136,7 @@ def test_lunarlander_device_rollout_matches_oracle(cuda):
     act = torch.zeros(T, N, dtype=torch.int32, device=cuda)
     logp, rew, done = (torch.zeros(T, N, device=cuda) for _ in range(3))
     stats = torch.zeros(h.rollout_grid(N), 8, device=cuda)
-    h.rollout(env, params, H, state, ep_len, ep_ret, obs, act, logp, rew, done, stats, seed, 0, True, ms)
+    h.rollout(env, params, H, state, ep_len, ep_ret, obs, act, logp, rew, done, None, stats, seed, 0, True, ms)
     torch.cuda.synchronize()
     o, a, r, d = obs.cpu().numpy(), act.cpu().numpy(), rew.cpu().numpy(), done.cpu().numpy()
     checked = 0
@@ -173,7 +173,7 @@ def test_halfcheetah_gaussian_device_rollout_matches_oracle(cuda):
     logp, rew, done = (torch.zeros(T, N, device=cuda) for _ in range(3))
     stats = torch.zeros(h.rollout_grid(N), 8, device=cuda)
     h.rollout_cont(env, params.to(cuda), torch.from_numpy(cst).to(cuda), H, state, ep_len, ep_ret, obs, act, logp,
-                   rew, done, stats, seed, 0, True, ms)
+                   rew, done, None, stats, seed, 0, True, ms)
     torch.cuda.synchronize()
     o, a, lp, r = obs.cpu(), act.cpu(), logp.cpu(), rew.cpu()
     ls = params[spec.offsets()["log_std"]:spec.offsets()["log_std"] + A]

@@ -1,0 +1,173 @@
+"""Time-limit truncation: cut episodes bootstrap with V(pre-reset observation).
+
+The reference's finish_path bootstraps a cut path with ``last_val`` (replay_buffer.py:48-79,
+REINFORCE.py:86).  The vectorised trainers mark a time-limit truncation with done code 2
+and keep the pre-reset observation (``tobs``); the GAE / return scan then uses V(tobs)
+instead of 0.  Every check here is against a float64 per-episode oracle that walks each
+env column, splits it into episodes and applies finish_path literally.
+"""
+import numpy as np
+import pytest
+import torch
+
+from relayrl_prototype_amd import _native
+from relayrl_prototype_amd.ops import reference as ref
+
+
+def disc(x, g):
+    out = np.zeros(len(x))
+    run = 0.0
+    for t in range(len(x) - 1, -1, -1):
+        run = x[t] + g * run
+        out[t] = run
+    return out
+
+
+def oracle_tm(rew, done, val, tval, gamma, lam):
+    """float64 per-episode finish_path over a time-major [T, N] rollout.
+    val [T+1, N] (row T bootstraps the open episode), tval [T, N] read where done == 2."""
+    rew, done, val, tval = (np.asarray(x, dtype=np.float64) for x in (rew, done, val, tval))
+    T, N = rew.shape
+    adv = np.zeros((T, N))
+    ret = np.zeros((T, N))
+    for n in range(N):
+        start = 0
+        for t in range(T):
+            end_here = done[t, n] > 0 or t == T - 1
+            if not end_here:
+                continue
+            if done[t, n] == 1:
+                last = 0.0
+            elif done[t, n] == 2:
+                last = tval[t, n]
+            else:
+                last = val[T, n]
+            sl = slice(start, t + 1)
+            rr = np.append(rew[sl, n], last)
+            vv = np.append(val[sl, n], last)
+            deltas = rr[:-1] + gamma * vv[1:] - vv[:-1]
+            adv[sl, n] = disc(deltas, gamma * lam)
+            ret[sl, n] = disc(rr, gamma)[:-1]
+            start = t + 1
+    return adv, ret
+
+
+def values64(params, X, D, H):
+    out, _ = ref.trunk(params.double().cpu(), X.double().cpu(), D, H, 1)
+    return out[..., 0].numpy()
+
+
+def test_scan_ref_matches_per_episode_oracle():
+    g = torch.Generator().manual_seed(0)
+    T, N = 37, 19
+    rew = torch.randn(T, N, generator=g)
+    u = torch.rand(T, N, generator=g)
+    done = torch.where(u < 0.08, torch.ones(T, N), torch.where(u < 0.16, 2 * torch.ones(T, N), torch.zeros(T, N)))
+    val = torch.randn(T + 1, N, generator=g)
+    tval = torch.randn(T, N, generator=g)
+    adv, ret, _ = ref.gae_scan_tm_ref(rew, done, val, 0.98, 0.97, tval)
+    a64, r64 = oracle_tm(rew, done, val, tval, 0.98, 0.97)
+    np.testing.assert_allclose(adv.numpy(), a64, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(ret.numpy(), r64, rtol=1e-5, atol=1e-5)
+    # without tval a truncation is a terminal (the previous behaviour)
+    adv0, _, _ = ref.gae_scan_tm_ref(rew, torch.clamp(done, max=1.0), val, 0.98, 0.97)
+    a0, _ = oracle_tm(rew, torch.clamp(done, max=1.0), val, tval, 0.98, 0.97)
+    np.testing.assert_allclose(adv0.numpy(), a0, rtol=1e-5, atol=1e-5)
+
+
+def test_host_env_marks_truncation_and_keeps_pre_reset_obs():
+    # MountainCar-v0 under random actions never reaches the flag: every episode is cut at 200
+    N, D = 6, 2
+    env = _native.VecEnv("MountainCar-v0", N, 3, 2)
+    assert env.max_steps == 200
+    obs = np.zeros((N, D), np.float32)
+    env.reset_ptr(obs.ctypes.data)
+    act = np.zeros(N, np.int32)
+    rew = np.zeros(N, np.float32)
+    done = np.zeros(N, np.float32)
+    tobs = np.full((N, D), np.nan, np.float32)
+    rng = np.random.default_rng(0)
+    for t in range(200):
+        prev = obs.copy()
+        act[:] = rng.integers(0, 3, N)
+        env.step_ptr(act.ctypes.data, obs.ctypes.data, rew.ctypes.data, done.ctypes.data, tobs.ctypes.data)
+        if t < 199:
+            assert (done == 0).all()
+    assert (done == 2).all(), done
+    # the kept observation continues the trajectory (|dx| <= max speed), the new one is a reset
+    assert np.all(np.abs(tobs[:, 0] - prev[:, 0]) <= 0.07 + 1e-6)
+    assert np.all(obs[:, 1] == 0) and np.all((obs[:, 0] >= -0.6) & (obs[:, 0] <= -0.4))
+    # without a tobs buffer truncations are reported as terminal (code 1)
+    env2 = _native.VecEnv("MountainCar-v0", N, 3, 1)
+    env2.reset_ptr(obs.ctypes.data)
+    for t in range(200):
+        env2.step_ptr(act.ctypes.data, obs.ctypes.data, rew.ctypes.data, done.ctypes.data)
+    assert (done == 1).all()
+
+
+def test_host_trainer_bootstraps_truncated_episodes_cpu():
+    from relayrl_prototype_amd.runtime.host_trainer import HostTrainerConfig, HostVecTrainer
+
+    cfg = HostTrainerConfig(env="MountainCar-v0", num_envs=4, rollout_len=230, num_threads=1, train_vf_iters=1,
+                            gamma=0.99, lam=0.95, seed=5)
+    tr = HostVecTrainer(cfg, device="cpu")
+    tr.rollout()
+    vf = tr.learner.vf.params.detach().clone()
+    done = tr.d_done.clone()
+    assert (done == 2).sum().item() == cfg.num_envs  # one cut per env at step 200
+    tr.rl.learn(tr.d_obs, tr.d_act, tr.d_rew, tr.d_done, tr.d_logp, tobs=tr.d_tobs)
+    T, N, D, H = cfg.rollout_len, cfg.num_envs, tr.D, cfg.hidden
+    val = values64(vf, tr.d_obs, D, H)
+    tval = values64(vf, tr.d_tobs, D, H)
+    a64, r64 = oracle_tm(tr.d_rew.numpy(), done.numpy(), val, tval, cfg.gamma, cfg.lam)
+    np.testing.assert_allclose(tr.rl.adv.numpy(), a64, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(tr.rl.ret.numpy(), r64, rtol=1e-4, atol=1e-4)
+
+
+def _device_trainer_check(cuda, env, T, N, algo="reinforce", max_steps=None):
+    from relayrl_prototype_amd.runtime.vec_trainer import VecTrainer, VecTrainerConfig
+
+    cfg = VecTrainerConfig(env=env, num_envs=N, rollout_len=T, algo=algo, with_baseline=True, train_vf_iters=1,
+                           train_pi_iters=1, gamma=0.99, lam=0.95, seed=11, use_graphs=False,
+                           max_episode_steps=max_steps)
+    tr = VecTrainer(cfg, device=cuda)
+    tr.rollout()
+    vf = tr.vf.params.detach().clone()
+    done = tr.done.clone()
+    n_cut = int((done == 2).sum().item())
+    assert n_cut > 0, "the rollout must cross the time limit"
+    tr.rl.learn(tr.obs, tr.act, tr.rew, tr.done, tr.logp, tobs=tr.tobs)
+    torch.cuda.synchronize()
+    D, H = tr.D, cfg.hidden
+    val = values64(vf, tr.obs, D, H)
+    tval = values64(vf, tr.tobs, D, H)
+    cut = (done == 2).cpu().numpy()
+    a64, r64 = oracle_tm(tr.rew.cpu().numpy(), done.cpu().numpy(), val, np.where(cut, tval, 0.0), cfg.gamma,
+                         cfg.lam)
+    adv, ret = tr.rl.adv.cpu().numpy(), tr.rl.ret.cpu().numpy()
+    scale = max(1.0, float(np.abs(r64).max()))
+    np.testing.assert_allclose(adv, a64, rtol=1e-4, atol=1e-4 * scale)
+    np.testing.assert_allclose(ret, r64, rtol=1e-4, atol=1e-4 * scale)
+    # the truncation bootstrap matters: treating the cut as terminal gives different returns
+    a_term, r_term = oracle_tm(tr.rew.cpu().numpy(), np.minimum(done.cpu().numpy(), 1), val, tval, cfg.gamma,
+                               cfg.lam)
+    assert np.abs(r_term - r64).max() > 1e-3
+    return n_cut
+
+
+@pytest.mark.gpu
+def test_device_cartpole_cut_at_limit(cuda):
+    # CartPole's 500-step limit, scaled down so a random-init policy reaches it
+    _device_trainer_check(cuda, "CartPole-v1", T=64, N=256, max_steps=12)
+
+
+@pytest.mark.gpu
+def test_device_mountaincar_cut_at_200(cuda):
+    n = _device_trainer_check(cuda, "MountainCar-v0", T=230, N=64)
+    assert n >= 64
+
+
+@pytest.mark.gpu
+def test_device_halfcheetah_cut_at_1000(cuda):
+    n = _device_trainer_check(cuda, "HalfCheetahSynth-v0", T=1010, N=32, algo="ppo")
+    assert n == 32  # HalfCheetah only truncates: exactly one cut per env at step 1000

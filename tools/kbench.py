@@ -108,7 +108,7 @@ def main():
         rw = torch.empty(T, N, device=dev)
         dn = torch.empty(T, N, device=dev)
         es = torch.empty(h.rollout_grid(N), 8, device=dev)
-        us = timeit(lambda: h.rollout(0, pp, H, st, el, er, obs, ac, lp, rw, dn, es, 1, 0, False, 500), a.iters)
+        us = timeit(lambda: h.rollout(0, pp, H, st, el, er, obs, ac, lp, rw, dn, None, es, 1, 0, False, 500), a.iters)
         res["rollout_us"] = us
         res["rollout_Msteps_per_s"] = T * N / us
     print(json.dumps({k: round(v, 3) for k, v in res.items()}))
