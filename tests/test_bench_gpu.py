@@ -33,7 +33,8 @@ def _json_lines(out):
 
 def test_bench_single_gpu_contract(cuda):
     r = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--num-envs", "2048",
-                        "--vf-iters", "4", "--ttt-seeds", "1"], cwd=REPO, capture_output=True, text=True, timeout=240)
+                        "--vf-iters", "4", "--ttt-seeds", "1", "--ttt-ref-seeds", "1", "--ref-cpu-seconds", "0"],
+                       cwd=REPO, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     recs = _json_lines(r.stdout)
     assert len(recs) == 1
@@ -51,7 +52,7 @@ def test_bench_two_ranks_gloo_shared_gpu(cuda):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus", "2", "--steps", "2",
            "--warmup", "1", "--num-envs", "1024", "--vf-iters", "4"]
-    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     recs = _json_lines(r.stdout)
     assert len(recs) == 1, r.stdout  # rank 0 only
