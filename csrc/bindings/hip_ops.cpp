@@ -24,8 +24,8 @@ int rrl_mlp_grad(int head, const float* params, const float* X, int B, int D, in
                  float* grad_slab, float* loss_slab, int P, int num_cu, void* stream);
 int rrl_scan_tm_parts(int N);
 int rrl_gae_scan_tm(const float* rew, const float* done, const float* val, const float* tval, float* adv,
-                    float* ret, float* stats_part, float* stats_out, int T, int N, float gamma, float lam,
-                    void* stream);
+                    float* ret, float* stats_part, float* stats_out, int K, int T, int N, float gamma,
+                    float lam, void* stream);
 int rrl_scan_flat_blocks(int L);
 int rrl_scan_flat(const float* rew, const float* done, const float* val, const float* boot, float* adv,
                   float* ret, float* work, float* stats_out, int L, float gamma, float lam, void* stream);
@@ -173,22 +173,24 @@ int64_t scan_tm_parts(int64_t N) { return rrl_scan_tm_parts((int)N); }
 
 void gae_scan_tm(const Tensor& rew, const Tensor& done, const OptT& val, const OptT& tval, const Tensor& adv,
                  const Tensor& ret, const Tensor& stats_part, const OptT& stats_out, double gamma, double lam) {
+  // rew [T, N] or [K, T, N] (K actor blocks of one learner shard); val [K*T*N + K*N]
   check_dev(rew, "rew", at::kFloat);
-  TORCH_CHECK(rew.dim() == 2, "rew must be [T, N]");
-  const int64_t T = rew.size(0), N = rew.size(1);
+  TORCH_CHECK(rew.dim() == 2 || rew.dim() == 3, "rew must be [T, N] or [K, T, N]");
+  const int64_t K = rew.dim() == 3 ? rew.size(0) : 1;
+  const int64_t T = rew.size(rew.dim() - 2), N = rew.size(rew.dim() - 1);
   check_dev(done, "done", at::kFloat);
-  check_numel(done, "done", T * N);
-  const float* v = fptr(val, "val", (T + 1) * N);
-  const float* tv = fptr(tval, "tval", T * N);
+  check_numel(done, "done", K * T * N);
+  const float* v = fptr(val, "val", K * (T + 1) * N);
+  const float* tv = fptr(tval, "tval", K * T * N);
   check_dev(adv, "adv", at::kFloat);
-  check_numel(adv, "adv", T * N);
+  check_numel(adv, "adv", K * T * N);
   check_dev(ret, "ret", at::kFloat);
-  check_numel(ret, "ret", T * N);
+  check_numel(ret, "ret", K * T * N);
   check_dev(stats_part, "stats_part", at::kFloat);
-  check_numel(stats_part, "stats_part", scan_tm_parts(N) * 3);
+  check_numel(stats_part, "stats_part", scan_tm_parts(K * N) * 3);
   float* so = fptr_mut(stats_out, "stats_out", 3);
   const int rc = rrl_gae_scan_tm(rew.data_ptr<float>(), done.data_ptr<float>(), v, tv, adv.data_ptr<float>(),
-                                 ret.data_ptr<float>(), stats_part.data_ptr<float>(), so, (int)T, (int)N,
+                                 ret.data_ptr<float>(), stats_part.data_ptr<float>(), so, (int)K, (int)T, (int)N,
                                  (float)gamma, (float)lam, cur_stream());
   check_rc(rc, "gae_scan_tm");
 }

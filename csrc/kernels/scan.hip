@@ -10,7 +10,9 @@
 // bootstraps its cut paths with last_val (replay_buffer.py:48-79, REINFORCE.py:86).
 // Two layouts are supported:
 //   * time-major [T][N] rollouts from the vectorised actors: one thread per env column,
-//     sequential in t (coalesced across envs) -- T is short, N is huge;
+//     sequential in t (coalesced across envs) -- T is short, N is huge.  A learner shard
+//     fed by K actors holds K such blocks back to back ([K][T][N], each received whole
+//     over its own link), with the K x N bootstrap values after all of them;
 //   * flat [L] buffers of concatenated variable-length paths (the agent/trajectory API):
 //     a 3-phase parallel affine scan (thread chunk -> block scan -> block carries).
 #include "common.h"
@@ -18,28 +20,30 @@
 namespace rrl {
 
 struct ScanTM {
-  const float* rew;    // [T][N]
-  const float* done;   // [T][N]  (1 if the episode ended at this step)
-  const float* val;    // [T+1][N] or null (row T = bootstrap value V(s_T))
-  const float* tval;   // [T][N] V(pre-reset obs), read where done == 2, or null
-  float* adv;          // [T][N]
-  float* ret;          // [T][N]
+  const float* rew;    // [K][T][N]
+  const float* done;   // [K][T][N]  (0 running / 1 terminal / 2 truncated)
+  const float* val;    // [K*T*N + K*N] or null: V of every step, then V(s_T) of each column
+  const float* tval;   // [K][T][N] V(pre-reset obs), read where done == 2, or null
+  float* adv;          // [K][T][N]
+  float* ret;          // [K][T][N]
   float* stats_part;   // [nblocks][3] adv sum / sumsq / count
-  int T, N;
+  int T, N, K;
   float gamma, lam;
 };
 
 __global__ __launch_bounds__(256) void gae_scan_tm_kernel(ScanTM p) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;  // column = block k, env n
   float s = 0.f, ss = 0.f, c = 0.f;
-  if (n < p.N) {
+  if (col < p.K * p.N) {
     const float gl = p.gamma * p.lam;
     const size_t N = (size_t)p.N;
+    const int k = col / p.N;
+    const size_t base = (size_t)k * p.T * N + (col - k * p.N);
     if (p.val != nullptr) {
-      float v_next = p.val[(size_t)p.T * N + n];
+      float v_next = p.val[(size_t)p.K * p.T * N + col];
       float adv_next = 0.f, ret_next = v_next;
       for (int t = p.T - 1; t >= 0; --t) {
-        const size_t idx = (size_t)t * N + n;
+        const size_t idx = base + (size_t)t * N;
         const float r = p.rew[idx], d = p.done[idx], v = p.val[idx];
         const float nd = d == 0.f ? 1.f : 0.f;
         const float vb = (d > 1.5f && p.tval != nullptr) ? p.tval[idx] : 0.f;  // truncation bootstrap
@@ -57,7 +61,7 @@ __global__ __launch_bounds__(256) void gae_scan_tm_kernel(ScanTM p) {
     } else {
       float adv_next = 0.f, ret_next = 0.f;
       for (int t = p.T - 1; t >= 0; --t) {
-        const size_t idx = (size_t)t * N + n;
+        const size_t idx = base + (size_t)t * N;
         const float r = p.rew[idx], d = p.done[idx];
         const float nd = d == 0.f ? 1.f : 0.f;  // no value function: truncation cuts like a terminal
         const float a = r + gl * nd * adv_next;
@@ -262,12 +266,13 @@ using namespace rrl;
 
 extern "C" int rrl_scan_tm_parts(int N) { return (N + 255) / 256; }
 
+// nparts of rrl_scan_tm_parts(K * N)
 extern "C" int rrl_gae_scan_tm(const float* rew, const float* done, const float* val, const float* tval,
-                               float* adv, float* ret, float* stats_part, float* stats_out, int T, int N,
+                               float* adv, float* ret, float* stats_part, float* stats_out, int K, int T, int N,
                                float gamma, float lam, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  const int nb = rrl_scan_tm_parts(N);
-  ScanTM p{rew, done, val, tval, adv, ret, stats_part, T, N, gamma, lam};
+  const int nb = rrl_scan_tm_parts(K * N);
+  ScanTM p{rew, done, val, tval, adv, ret, stats_part, T, N, K, gamma, lam};
   hipLaunchKernelGGL(gae_scan_tm_kernel, dim3(nb), dim3(256), 0, s, p);
   if (stats_out) hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(256), 0, s, stats_part, nb, stats_out);
   return (int)hipGetLastError();

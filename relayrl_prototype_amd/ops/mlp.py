@@ -223,22 +223,26 @@ def adam_step(param, m, v, step_t, ticket_t, lr, grad=None, slab=None, beta1=0.9
 
 
 def gae_scan_tm(rew, done, val, gamma, lam, adv=None, ret=None, stats_part=None, stats_out=None, tval=None):
-    """Time-major [T, N] GAE / discounted-return scan -> (adv, ret, stats[3]).
+    """Time-major GAE / discounted-return scan -> (adv, ret, stats[3]).
 
+    ``rew`` / ``done`` / ``tval`` are [T, N], or [K, T, N] for a learner shard holding K
+    actor blocks; ``val`` is flat [K*T*N + K*N]: V of every step, then the bootstrap value
+    V(s_T) of each of the K*N columns (for K = 1 exactly a [T+1, N] buffer).
     done codes: 0 running, 1 terminal, 2 time-limit truncation -- bootstrapped with
-    ``tval`` [T, N] = V(pre-reset observation) (replay_buffer.py:48-79 last_val)."""
+    ``tval`` = V(pre-reset observation) (replay_buffer.py:48-79 last_val)."""
     h = _hip_for(rew)
     if h is None:
         a, r, s = ref.gae_scan_tm_ref(rew, done, val, gamma, lam, tval)
         if stats_out is not None:
             stats_out.copy_(s)
         return a, r, s
-    T, N = rew.shape
+    K = rew.shape[0] if rew.dim() == 3 else 1
+    T, N = rew.shape[-2], rew.shape[-1]
     dev = rew.device
-    adv = torch.empty(T, N, device=dev) if adv is None else adv
-    ret = torch.empty(T, N, device=dev) if ret is None else ret
+    adv = torch.empty(rew.shape, device=dev) if adv is None else adv
+    ret = torch.empty(rew.shape, device=dev) if ret is None else ret
     if stats_part is None:
-        stats_part = torch.empty(int(h.scan_tm_parts(N)), 3, device=dev)
+        stats_part = torch.empty(int(h.scan_tm_parts(K * N)), 3, device=dev)
     if stats_out is None:
         stats_out = torch.empty(3, device=dev)
     h.gae_scan_tm(rew.contiguous(), done.contiguous(), None if val is None else val.contiguous(), _f32(tval), adv, ret,

@@ -179,8 +179,23 @@ def discount_cumsum(x: np.ndarray, discount: float) -> np.ndarray:
 
 @torch.no_grad()
 def gae_scan_tm_ref(rew, done, val, gamma, lam, tval=None):
-    """done codes: 0 running, 1 terminal, 2 time-limit truncation (bootstrap tval[t])."""
+    """done codes: 0 running, 1 terminal, 2 time-limit truncation (bootstrap tval[t]).
+
+    [K, T, N] inputs (K actor blocks) with flat ``val`` [K*T*N + K*N] are scanned as one
+    [T, K*N] problem (column k*N + n)."""
+    if rew.dim() == 3:
+        K, T, N = rew.shape
+        tm = lambda x: x.reshape(K, T, N).permute(1, 0, 2).reshape(T, K * N)  # noqa: E731
+        v = None
+        if val is not None:
+            vf = val.reshape(-1)
+            v = torch.cat([tm(vf[:K * T * N]), vf[K * T * N:K * T * N + K * N].reshape(1, K * N)])
+        a, r, s = gae_scan_tm_ref(tm(rew), tm(done), v, gamma, lam, None if tval is None else tm(tval))
+        back = lambda x: x.reshape(T, K, N).permute(1, 0, 2).contiguous()  # noqa: E731
+        return back(a), back(r), s
     T, N = rew.shape
+    if val is not None:
+        val = val.reshape(T + 1, N)
     adv = torch.zeros_like(rew)
     ret = torch.zeros_like(rew)
     if val is not None:

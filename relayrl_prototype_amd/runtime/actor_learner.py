@@ -1,39 +1,50 @@
-"""Actor-learner decoupling over collectives (SURVEY §2.7 C1/C2/C3, §2.8 row 1).
+"""Actor-learner decoupling over collectives (SURVEY §2.7 C1/C2/C3/C8, §2.8 row 1).
 
 The reference decouples agents and the training server with ZeroMQ / gRPC over TCP:
-trajectories fan in to one learner (trajectory.rs:69-90 -> training_zmq.rs:948-1058),
-TorchScript models fan out through files + sockets.  Here every rank is one process
-per GPU:
+every trajectory fans in to ONE learner (trajectory.rs:69-90 -> training_zmq.rs:948-1058)
+and TorchScript models fan out through files + sockets.  One learner GPU cannot keep up
+with many actor GPUs (the learner does ~96 % of the FLOPs of an epoch), so here the
+learner is a process GROUP:
 
-  rank 0          : learner -- receives every actor's rollout straight into HBM,
-                    runs the fused HIP learner, broadcasts the flat weight vector;
-  ranks 1 .. W-1  : actors -- fused on-device rollout kernel (or host C++ envs),
-                    ship [T, N] SoA rollouts to rank 0 with point-to-point sends
-                    (each actor -> learner transfer rides its own xGMI link).
+  W ranks, one per GPU.  Ranks 0 .. L-1 form the learner group (``learner_ranks`` = L,
+  default W).  Every rank acts by default (``learner_acts``); actor a feeds learner
+  shard ``a mod L``.  A shard receives its K = actors / L rollouts with point-to-point
+  receives straight into ONE contiguous HBM batch (K time-major [T, N] blocks back to
+  back, then the K x N final observations -- rollout_learn.py ``blocks``), so every
+  actor -> learner transfer is a single message per tensor on its own xGMI link and
+  nothing is re-stacked.  The shards then run the fused HIP learner data-parallel:
+  one RCCL all-reduce of the flat gradient per optimiser step inside the learner group
+  (core.FlatNet.apply), which keeps every learner's weights identical.  Each learner
+  sends the new flat weight vector back to its own actors (P2P, again one link each).
 
 Handshake (GET_MODEL / MODEL_SET / ID_LOGGED, agent_zmq.rs:316-442) becomes the
 process-group rendezvous + an initial weight broadcast; the agent registry is the rank
-table.  Each rollout carries a header (sequence number, episode statistics) that is the
-actor heartbeat; the learner detects stalled actors through the collective timeout.
+table.  Every rollout carries a header: sequence number (heartbeat), episode statistics,
+and the version + checksum of the weights it was rolled out with.
 
-``max_lag = 1`` overlaps the weight broadcast with the next rollout: actors act with a
-policy at most one update old (asynchronous actor-learner, like IMPALA/A3C-style
-pipelines); ``max_lag = 0`` is fully synchronous.
+``max_lag = 1`` overlaps an actor's rollout of epoch k+1 with the learners' update on
+epoch k (IMPALA-style lag-1 pipelining).  Weights arrive in a BACK buffer; the actor
+copies back -> front on its compute stream only after the receive completed and only
+after the previous rollout kernel was queued, and posts the next receive after that
+copy, so a rollout never reads a half-written policy.  Learners send from a snapshot of
+the parameters, never from the live vector the next Adam step updates in place.  With
+``verify_versions`` the learner checks every received header: version in
+[k - max_lag, k] and checksum equal to the one recorded when that version was produced.
 """
 from __future__ import annotations
 
-import time
 from dataclasses import asdict, dataclass
-from typing import Optional
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
 
 from ..algorithms.learner import PGLearner
 from ..parallel.comm import Comm
-from .rollout_learn import RolloutLearner, episode_metrics
+from .rollout_learn import RolloutLearner
 
-HDR = 8  # header floats: seq, n_episodes, sum_ret, sumsq_ret, max_ret, min_ret, sum_len, version
+# header (float64): seq, n_episodes, sum_ret, sumsq_ret, max_ret, min_ret, sum_len, version, checksum, wsum
+HDR = 10
 
 
 @dataclass
@@ -54,19 +65,53 @@ class ActorLearnerConfig:
     target_kl: Optional[float] = None
     ent_coef: float = 0.0
     seed: int = 0
-    max_lag: int = 0
-    learner_acts: bool = False     # rank 0 also rolls out (colocated actor)
+    max_lag: int = 0               # 0 synchronous, 1 = actors roll out on weights one update old
+    learner_ranks: int = 0         # L: ranks 0 .. L-1 learn (0 = every rank)
+    learner_acts: bool = True      # learner ranks also roll out (colocated actor)
     num_threads: int = 4
     use_graphs: bool = True
+    verify_versions: bool = False  # check header version/checksum on the learners (syncs)
 
     def to_dict(self):
         return asdict(self)
 
 
+def weight_checksum(p: torch.Tensor) -> torch.Tensor:
+    """(sum, index-weighted sum) in fp64 on the device: a torn or stale weight vector
+    changes at least one of them."""
+    d = p.detach().double()
+    w = torch.arange(1, d.numel() + 1, dtype=torch.float64, device=d.device) / d.numel()
+    return torch.stack([d.sum(), (d * w).sum()])
+
+
+class Topology:
+    """Rank roles: who learns, who acts, which learner shard every actor feeds."""
+
+    def __init__(self, world: int, learner_ranks: int, learner_acts: bool):
+        L = learner_ranks or world
+        if not 1 <= L <= world:
+            raise ValueError(f"learner_ranks={learner_ranks} with world_size={world}")
+        self.world, self.L = world, L
+        self.actors = list(range(world)) if learner_acts else list(range(L, world))
+        if not self.actors:
+            raise ValueError("no actor ranks: use world_size > learner_ranks or learner_acts=True")
+        if len(self.actors) % L:
+            raise ValueError(f"{len(self.actors)} actors do not split evenly over {L} learner shards")
+        self.K = len(self.actors) // L  # actor blocks per learner shard
+        self.learner_acts = learner_acts
+
+    def learner_of(self, actor: int) -> int:
+        return self.actors.index(actor) % self.L
+
+    def shard(self, learner: int) -> List[int]:
+        """Actors feeding ``learner``, its own (colocated) actor first."""
+        return [a for a in self.actors if self.learner_of(a) == learner]
+
+
 class _Actor:
     """Rollout engine for one rank: device envs when possible, host C++ envs otherwise."""
 
-    def __init__(self, cfg: ActorLearnerConfig, comm: Comm, device):
+    def __init__(self, cfg: ActorLearnerConfig, comm: Comm, device, need_tobs: bool):
         self.device = torch.device(device)
         from .vec_trainer import CONTINUOUS_DEVICE_ENVS, DEVICE_ENVS
 
@@ -88,58 +133,77 @@ class _Actor:
                                      seed=cfg.seed, num_threads=cfg.num_threads, train_vf_iters=0)
             self.eng = HostVecTrainer(hcfg, comm, device=self.device)
             self.params = self.eng.learner.pi.params
+        self.need_tobs = need_tobs
         self.seq = 0
+        self.header = torch.zeros(HDR, dtype=torch.float64, device=self.device)
 
     @property
     def dims(self):
         e = self.eng
         return e.D, e.A, (getattr(e, "continuous", False))
 
-    def rollout(self):
-        """-> (obs [T+1,N,D], act, logp, rew, done, header[HDR])"""
+    def rollout(self, version: int):
+        """-> (obs_train [T,N,D], obs_last [N,D], act, logp, rew, done, tobs|None, header[HDR])"""
         e = self.eng
+        T = e.cfg.rollout_len
+        ck = weight_checksum(self.params)  # queued before the rollout: same weights it reads
         if self.kind == "device":
             e.rollout()
             e.epoch += 1
             st = e.ep_stats
             ep = st.sum(0)
-            hdr = torch.stack([ep[0], ep[1], ep[2], st[:, 3].max(), st[:, 4].min(), ep[5]])
-            out = (e.obs, e.act, e.logp, e.rew, e.done)
+            stats = torch.stack([ep[0], ep[1], ep[2], st[:, 3].max(), st[:, 4].min(), ep[5]]).double()
+            obs, act, logp, rew, done, tobs = e.obs, e.act, e.logp, e.rew, e.done, e.tobs
         else:
             e.rollout()
             s = {"n": 0.0, "sum": 0.0, "sumsq": 0.0, "max": -1e30, "min": 1e30, "sum_len": 0.0}
             for env in e.envs:
                 x = env.take_stats()
-                s["n"] += x["n"]
-                s["sum"] += x["sum"]
-                s["sumsq"] += x["sumsq"]
-                s["sum_len"] += x["sum_len"]
+                for k in ("n", "sum", "sumsq", "sum_len"):
+                    s[k] += x[k]
                 if x["n"] > 0:
                     s["max"] = max(s["max"], x["max"])
                     s["min"] = min(s["min"], x["min"])
-            hdr = torch.tensor([s["n"], s["sum"], s["sumsq"], s["max"], s["min"], s["sum_len"]], device=self.device)
-            out = (e.d_obs, e.d_act, e.d_logp, e.d_rew, e.d_done)
-            e.h_obs[0].copy_(e.h_obs[e.cfg.rollout_len])
+            stats = torch.tensor([s["n"], s["sum"], s["sumsq"], s["max"], s["min"], s["sum_len"]],
+                                 dtype=torch.float64, device=self.device)
+            obs, act, logp, rew, done, tobs = e.d_obs, e.d_act, e.d_logp, e.d_rew, e.d_done, e.d_tobs
+            e.h_obs[0].copy_(e.h_obs[T])
         self.seq += 1
-        header = torch.cat([torch.tensor([float(self.seq)], device=self.device), hdr.float(),
-                            torch.zeros(HDR - 7, device=self.device)])
-        return out + (header,)
+        h = self.header
+        h[0] = float(self.seq)
+        h[1:7].copy_(stats)
+        h[7] = float(version)
+        h[8:10].copy_(ck)
+        if self.need_tobs and tobs is None:
+            tobs = torch.zeros_like(obs[:T])
+        return (obs[:T], obs[T], act, logp, rew, done, tobs if self.need_tobs else None, h)
 
 
 class ActorLearner:
     def __init__(self, cfg: ActorLearnerConfig, comm: Optional[Comm] = None, device=None):
         self.cfg = cfg
         self.comm = comm or Comm()
-        if self.comm.world < 2 and not cfg.learner_acts:
-            raise ValueError("actor-learner mode needs world_size >= 2 (rank 0 learns, others act) "
-                             "unless the learner also acts (learner_acts=True)")
+        W = self.comm.world
+        if W < 2 and not cfg.learner_acts:
+            raise ValueError("actor-learner mode needs world_size >= 2 (learners + actors) "
+                             "unless the learners also act (learner_acts=True)")
+        if cfg.max_lag not in (0, 1):
+            raise ValueError("max_lag must be 0 or 1")
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
         self.rank = self.comm.rank
-        self.is_learner = self.rank == 0
-        self.actor = _Actor(cfg, self.comm, self.device) if (not self.is_learner or cfg.learner_acts) else None
-        # every rank needs the dims; derive them from a throw-away env on the learner
+        self.topo = topo = Topology(W, cfg.learner_ranks, cfg.learner_acts)
+        self.is_learner = self.rank < topo.L
+        self.acts = self.rank in topo.actors
+        # the learner group (a collective over the default group: every rank calls new_group)
+        if topo.L == W:
+            self.lcomm = self.comm
+        else:
+            grp = dist.new_group(list(range(topo.L))) if W > 1 else None
+            self.lcomm = Comm(grp) if self.is_learner else None
+        need_tobs = cfg.with_baseline or cfg.algo != "reinforce"
+        self.actor = _Actor(cfg, self.comm, self.device, need_tobs) if self.acts else None
         if self.actor is not None:
             D, A, cont = self.actor.dims
         else:
@@ -148,126 +212,227 @@ class ActorLearner:
             e = _native.VecEnv(cfg.env, 1, 0, 1)
             D, A, cont = e.obs_dim, e.act_dim, e.continuous
         self.D, self.A, self.continuous = D, A, cont
-        T, N = cfg.rollout_len, cfg.num_envs
-        self.n_actors = self.comm.world - (0 if cfg.learner_acts else 1)
+        T, N, K = cfg.rollout_len, cfg.num_envs, topo.K
+        self.n_actors = len(topo.actors)
         self.version = 0
         self.received = 0
         self.epoch = 0
+        self.last_hdr = None
+        self._send_works = []
+        self._recv_work = None
+        self._ck = {}  # version -> checksum (learners, verify_versions)
         if self.is_learner:
-            # identical init to the actors' policies (same seed)
             self.learner = PGLearner(cfg.algo, D, A, cfg.hidden, not cont, cfg.with_baseline, cfg.pi_lr, cfg.vf_lr,
                                      cfg.train_vf_iters, cfg.train_pi_iters, cfg.clip_ratio, cfg.target_kl,
-                                     cfg.ent_coef, self.device, cfg.seed, _SoloComm(),
-                                     cfg.use_graphs)
-            if self.actor is not None:
-                self.actor.params.copy_(self.learner.pi.params)
-            W = self.comm.world
-            adt = torch.float32 if cont else torch.int32
-            ash = (T, N, A) if cont else (T, N)
-            self.g_obs = [torch.zeros(T + 1, N, D, device=self.device) for _ in range(W)]
-            self.g_act = [torch.zeros(*ash, dtype=adt, device=self.device) for _ in range(W)]
-            self.g_logp = [torch.zeros(T, N, device=self.device) for _ in range(W)]
-            self.g_rew = [torch.zeros(T, N, device=self.device) for _ in range(W)]
-            self.g_done = [torch.zeros(T, N, device=self.device) for _ in range(W)]
-            self.g_hdr = [torch.zeros(HDR, device=self.device) for _ in range(W)]
-            self.rl = RolloutLearner(self.learner, T, N * self.n_actors, cfg.gamma, cfg.lam, _SoloComm())
-            self.wbuf = self.learner.pi.params
+                                     cfg.ent_coef, self.device, cfg.seed, self.lcomm, cfg.use_graphs)
+            self.shard = topo.shard(self.rank)
+            dev = self.device
+            # ONE contiguous shard batch: K [T, N] blocks, then the K x N final observations
+            self.b_obs = torch.zeros(K * T * N + K * N, D, device=dev)
+            self.b_act = torch.zeros((K, T, N, A) if cont else (K, T, N), dtype=torch.float32 if cont else torch.int32,
+                                     device=dev)
+            self.b_logp = torch.zeros(K, T, N, device=dev)
+            self.b_rew = torch.zeros(K, T, N, device=dev)
+            self.b_done = torch.zeros(K, T, N, device=dev)
+            self.b_tobs = torch.zeros(K, T, N, D, device=dev) if need_tobs else None
+            self.b_hdr = torch.zeros(K, HDR, dtype=torch.float64, device=dev)
+            self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.lcomm, blocks=K)
+            self.wsend = torch.zeros_like(self.learner.pi.params)  # snapshot the P2P sends read
+            self.front = self.learner.pi.params
         else:
-            self.wbuf = self.actor.params
-        self._pending = None
-        self.last_hdr = None
-        # initial weight broadcast (the handshake's GET_MODEL)
-        self.comm.broadcast_(self.wbuf, 0)
+            self.learner = None
+            self.front = self.actor.params
+        self.back = torch.zeros_like(self.front) if (self.acts and not self.is_learner) else None
+        # initial weight broadcast from rank 0 (the handshake's GET_MODEL)
+        self.comm.broadcast_(self.front, 0)
+        if self.is_learner and self.actor is not None:
+            self.actor.params.copy_(self.front)
+        if self.is_learner and cfg.verify_versions:
+            self._ck[0] = weight_checksum(self.front).cpu()
 
-    # ------------------------------------------------------------------ collectives
-    def _exchange_rollout(self, parts):
-        """P2P fan-in of the six rollout tensors from every actor to rank 0."""
-        names = ("g_obs", "g_act", "g_logp", "g_rew", "g_done", "g_hdr")
-        W = self.comm.world
-        ops = []
-        if self.is_learner:
-            for k, name in enumerate(names):
-                bufs = getattr(self, name)
-                for r in range(W):
-                    if r == 0:
-                        if self.cfg.learner_acts:
-                            bufs[0].copy_(parts[k])
-                        continue
-                    ops.append(dist.P2POp(dist.irecv, bufs[r], r))
-        else:
-            for k in range(len(names)):
-                ops.append(dist.P2POp(dist.isend, parts[k].contiguous(), 0))
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
-
-    def _bcast_weights(self, async_op: bool):
-        if self.comm.world == 1:  # colocated single-GPU actor+learner: weights are shared
-            return None
-        return dist.broadcast(self.wbuf, src=0, async_op=async_op)
+    # ------------------------------------------------------------------ buffers
+    def _slot(self, k: int):
+        """Contiguous views of slot k of the shard batch (one P2P message per tensor)."""
+        T, N, K = self.cfg.rollout_len, self.cfg.num_envs, self.topo.K
+        obs_tr = self.b_obs[k * T * N:(k + 1) * T * N]
+        obs_last = self.b_obs[K * T * N + k * N:K * T * N + (k + 1) * N]
+        tobs = self.b_tobs[k] if self.b_tobs is not None else None
+        return (obs_tr, obs_last, self.b_act[k], self.b_logp[k], self.b_rew[k], self.b_done[k], tobs, self.b_hdr[k])
 
     # ------------------------------------------------------------------ one step
     def step(self):
         cfg = self.cfg
-        parts = None
-        if self.actor is not None:
-            parts = self.actor.rollout()
-        if not self.is_learner and cfg.max_lag >= 1 and self._pending is not None:
-            pass  # rollout above used the stale params; the new ones land below
-        self._exchange_rollout(parts)
+        parts = self.actor.rollout(self.version_in_use) if self.actor is not None else None
         if self.is_learner:
+            self._gather(parts)
             self._learn()
-        if cfg.max_lag >= 1:
-            if self._pending is not None:
-                self._pending.wait()
-            self._pending = self._bcast_weights(async_op=True)  # None on a single rank
+            self._send_weights()
         else:
-            self._bcast_weights(async_op=False)
+            self._send_rollout(parts)
+            self._recv_weights()
         self.version += 1
         self.epoch += 1
 
-    def finish(self):
-        if self._pending is not None:
-            self._pending.wait()
-            self._pending = None
+    @property
+    def version_in_use(self) -> int:
+        """Version of the weights the next rollout reads (actors lag by up to max_lag)."""
+        if self.is_learner:
+            return self.version
+        return getattr(self, "_front_version", 0)
 
-    def _learn(self):
-        W = self.comm.world
-        ranks = [r for r in range(W) if r != 0 or self.cfg.learner_acts]
-        T, N = self.cfg.rollout_len, self.cfg.num_envs
-        A = len(ranks)
-        cat = lambda bufs: torch.stack([bufs[r] for r in ranks], 1)  # [T(+1), A, N, ...]
-        obs = cat(self.g_obs).reshape(T + 1, A * N, self.D)
-        act = cat(self.g_act).reshape((T, A * N, self.A) if self.continuous else (T, A * N))
-        logp = cat(self.g_logp).reshape(T, A * N)
-        rew = cat(self.g_rew).reshape(T, A * N)
-        done = cat(self.g_done).reshape(T, A * N)
-        self.rl.learn(obs, act, rew, done, logp)
-        hdr = torch.stack([self.g_hdr[r] for r in ranks])
-        self.last_hdr = hdr
-        self.received += A
-        if self.actor is not None:
+    def _gather(self, parts):
+        """Fan-in: own rollout -> slot 0 (device copy), remote actors -> their slots (P2P)."""
+        ops = []
+        for k, a in enumerate(self.shard):
+            dst = self._slot(k)
+            if a == self.rank:
+                for d, s in zip(dst, parts):
+                    if d is not None:
+                        d.copy_(s.reshape(d.shape))
+                continue
+            for d in dst:
+                if d is not None:
+                    ops.append(dist.P2POp(dist.irecv, d, a))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+
+    def _send_rollout(self, parts):
+        dst = self.topo.learner_of(self.rank)
+        ops = [dist.P2POp(dist.isend, p.contiguous(), dst) for p in parts if p is not None]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()  # NCCL: stream order only; the next rollout kernel is queued after the send
+
+    def _send_weights(self):
+        remote = [a for a in self.shard if a != self.rank]
+        for w in self._send_works:  # the snapshot is free again once its sends completed
+            w.wait()
+        self._send_works = []
+        if self.cfg.verify_versions:
+            self._ck[self.version + 1] = weight_checksum(self.learner.pi.params).cpu()
+        if self.actor is not None:  # colocated actor: next rollout on the newest weights
             self.actor.params.copy_(self.learner.pi.params)
+        if not remote:
+            return
+        self.wsend.copy_(self.learner.pi.params)
+        self._send_works = dist.batch_isend_irecv([dist.P2POp(dist.isend, self.wsend, a) for a in remote])
+
+    def _recv_weights(self):
+        """Actor: the learner sends v_{k+1} after learning rollout k.  max_lag 0 waits for it;
+        max_lag 1 keeps rolling out on v_k and picks v_{k+1} up one step later."""
+        src = self.topo.learner_of(self.rank)
+        if self._recv_work is not None:  # (lag 1) v_k, posted last step
+            self._finish_recv()
+        self._recv_work = (self.version + 1, dist.batch_isend_irecv([dist.P2POp(dist.irecv, self.back, src)]))
+        if self.cfg.max_lag == 0:
+            self._finish_recv()
+
+    def _finish_recv(self):
+        ver, works = self._recv_work
+        for w in works:
+            w.wait()
+        self.front.copy_(self.back)  # compute stream, after the receive and after the last rollout
+        self._front_version = ver
+        self._recv_work = None
+
+    def finish(self):
+        """Drain in-flight weight transfers (every rank then holds the newest weights)."""
+        if self._recv_work is not None:
+            self._finish_recv()
+        for w in self._send_works:
+            w.wait()
+        self._send_works = []
+
+    @property
+    def wbuf(self) -> torch.Tensor:
+        return self.front
+
+    # ------------------------------------------------------------------ learner
+    def _learn(self):
+        cfg = self.cfg
+        K = self.topo.K
+        self.rl.learn(self.b_obs, self.b_act, self.b_rew, self.b_done, self.b_logp, tobs=self.b_tobs)
+        self.last_hdr = self.b_hdr
+        self.received += K
+        if cfg.verify_versions:
+            self._verify(self.b_hdr.cpu())
+
+    def _verify(self, hdr):
+        k, lag = self.version, self.cfg.max_lag
+        for j, a in enumerate(self.shard):
+            ver = int(hdr[j, 7].item())
+            if not (k - lag <= ver <= k):
+                raise RuntimeError(f"actor {a}: rollout {k} used weights v{ver}, allowed v{k - lag}..v{k}")
+            ref = self._ck.get(ver)
+            if ref is None or not torch.allclose(hdr[j, 8:10], ref, rtol=0, atol=0):
+                raise RuntimeError(f"actor {a}: rollout {k} weights do not match v{ver} (torn or stale copy)")
+        for v in [v for v in self._ck if v < k - lag]:
+            del self._ck[v]
+
+    # ------------------------------------------------------------------ metrics
+    @property
+    def env_steps(self) -> int:
+        """Per-rank share of the job's env steps (x world = total, like the other engines)."""
+        return self.epoch * self.cfg.rollout_len * self.cfg.num_envs * self.n_actors // self.comm.world
+
+    def _episode_vec(self):
+        """Global (n, sum, sumsq, sum_len, max, min) of the newest rollout, over every actor."""
+        dev = "cuda" if self.comm.backend == "nccl" else ("cpu" if self.comm.world > 1 else self.device)
+        if self.actor is not None:
+            h = self.actor.header.to(dev)
+            vec = torch.stack([h[1], h[2], h[3], h[6]])
+            mx, mn = h[4:5].clone(), h[5:6].clone()
+        else:
+            vec = torch.zeros(4, dtype=torch.float64, device=dev)
+            mx = torch.full((1,), -1e300, dtype=torch.float64, device=dev)
+            mn = torch.full((1,), 1e300, dtype=torch.float64, device=dev)
+        self.comm.all_reduce_sum_(vec)
+        self.comm.all_reduce_max_(mx)
+        self.comm.all_reduce_min_(mn)
+        return vec.tolist(), mx.item(), mn.item()
+
+    def episode_sums(self) -> tuple:
+        (n, s, _, _), _, _ = self._episode_vec()
+        return n, s
 
     def metrics(self) -> dict:
-        if not self.is_learner or self.last_hdr is None:
-            return {}
-        h = self.last_hdr.double().cpu()
-        n, s, sq, mx, mn, sl = h[:, 1].sum().item(), h[:, 2].sum().item(), h[:, 3].sum().item(), \
-            h[:, 4].max().item(), h[:, 5].min().item(), h[:, 6].sum().item()
-        out = {"Epoch": self.epoch, "Version": self.version, "ActorSeqs": h[:, 0].tolist()}
-        out.update(episode_metrics(_SoloComm(), n, s, sq, mx, mn, sl))
-        out.update(self.learner.summarize())
+        """Collective over every rank (episode statistics) and the learner group (losses);
+        the episode columns are identical on every rank."""
+        import math
+
+        (n, s, sq, sl), mx, mn = self._episode_vec()
+        out = {"Epoch": self.epoch, "Version": self.version, "WorldSize": self.comm.world,
+               "LearnerRanks": self.topo.L}
+        if n > 0:
+            mean = s / n
+            out.update(AverageEpRet=mean, StdEpRet=math.sqrt(max(sq / n - mean * mean, 0.0)), MaxEpRet=mx,
+                       MinEpRet=mn, EpLen=sl / n, Episodes=int(n))
+        else:
+            nan = float("nan")
+            out.update(AverageEpRet=nan, StdEpRet=nan, MaxEpRet=nan, MinEpRet=nan, EpLen=nan, Episodes=0)
+        if self.is_learner and self.last_hdr is not None:
+            h = self.last_hdr.cpu()
+            out["ActorSeqs"] = h[:, 0].tolist()
+            out["ActorVersions"] = [int(x) for x in h[:, 7].tolist()]
+            out.update(self.learner.summarize())
         out["EnvSteps"] = self.epoch * self.cfg.rollout_len * self.cfg.num_envs * self.n_actors
         return out
 
+    # ------------------------------------------------------------------ checkpoint
+    def state_dict(self) -> dict:
+        sd = {"epoch": self.epoch, "version": self.version, "cfg": self.cfg.to_dict()}
+        if self.learner is not None:
+            sd["learner"] = self.learner.state_dict()
+        else:
+            sd["front"] = self.front.cpu()
+        return sd
 
-class _SoloComm(Comm):
-    """The learner's optimiser runs on one rank: no gradient all-reduce."""
-
-    def __init__(self):
-        self.group = None
-        self.enabled = False
-        self.world = 1
-        self.rank = 0
-        self.backend = "none"
+    def load_state_dict(self, sd: dict):
+        self.epoch, self.version = int(sd["epoch"]), int(sd["version"])
+        if self.learner is not None and "learner" in sd:
+            self.learner.load_state_dict(sd["learner"])
+            if self.actor is not None:
+                self.actor.params.copy_(self.learner.pi.params)
+        elif "front" in sd:
+            self.front.copy_(sd["front"].to(self.device))
+            self._front_version = self.version

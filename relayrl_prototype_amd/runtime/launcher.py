@@ -41,9 +41,10 @@ PRESETS: Dict[str, Preset] = {
         "cartpole-reinforce-baseline", "REINFORCE-with-baseline CartPole-v1, 1 actor+learner per MI355X",
         "vec", {"env": "CartPole-v1", "num_envs": 32768, "rollout_len": 64, "with_baseline": True}),
     "lunarlander-reinforce-baseline": Preset(
-        "lunarlander-reinforce-baseline", "REINFORCE-with-baseline LunarLander, actor GPUs -> learner via RCCL gather",
+        "lunarlander-reinforce-baseline", "REINFORCE-with-baseline LunarLander, actor GPUs -> learner group "
+        "(P2P rollout fan-in to learner shards, gradient all-reduce inside the group)",
         "actor_learner", {"env": "LunarLanderSynth-v0", "num_envs": 2048, "rollout_len": 128, "with_baseline": True,
-                          "learner_acts": True, "num_threads": 8}),
+                          "learner_acts": True, "learner_ranks": 0, "num_threads": 8}),
     "pong-a2c": Preset(
         "pong-a2c", "A2C Pong pixels, Nature-CNN on MFMA, DP gradient all-reduce",
         "pixel", {"num_envs": 1024, "rollout_len": 5}),

@@ -110,38 +110,86 @@ def test_dp_host_trainer_ranks_stay_in_sync():
         assert steps == 2 * 16 * 16 * 2
 
 
-def _worker_actor_learner(rank, world, port, q, lag=0):
+def _al_worker(rank, world, port, q, lag=0, learners=0, learner_acts=True, steps=3, verify=True, algo="reinforce"):
     try:
         comm = _init(rank, world, port)
         from relayrl_prototype_amd.runtime.actor_learner import ActorLearner, ActorLearnerConfig
 
-        cfg = ActorLearnerConfig(env="CartPole-v1", num_envs=8, rollout_len=16, algo="reinforce", hidden=64,
-                                 train_vf_iters=2, num_threads=1, seed=5, max_lag=lag)
+        cfg = ActorLearnerConfig(env="CartPole-v1", num_envs=8, rollout_len=16, algo=algo, hidden=64,
+                                 train_vf_iters=2, train_pi_iters=2, num_threads=1, seed=5, max_lag=lag,
+                                 learner_ranks=learners, learner_acts=learner_acts, verify_versions=verify)
         al = ActorLearner(cfg, comm, device="cpu")
-        for _ in range(3):
+        versions = []
+        for _ in range(steps):
             al.step()
+            if al.is_learner:
+                versions.append([int(x) for x in al.b_hdr[:, 7].tolist()])
         al.finish()
         m = al.metrics()
         w = al.wbuf.clone()
         gathered = [torch.zeros_like(w) for _ in range(world)]
         dist.all_gather(gathered, w)
         same = all(torch.equal(gathered[0], x) for x in gathered)
-        q.put((rank, same, m.get("EnvSteps"), m.get("ActorSeqs")))
+        q.put((rank, same, m.get("EnvSteps"), m.get("ActorSeqs"), versions, w, m.get("Episodes")))
         dist.destroy_process_group()
     except Exception:
         import traceback
 
-        q.put((rank, traceback.format_exc(), None, None))
+        q.put((rank, traceback.format_exc(), None, None, None, None, None))
+
+
+def _worker_actor_learner(rank, world, port, q):
+    # classic topology: rank 0 learns only, ranks 1, 2 act
+    _al_worker(rank, world, port, q, lag=0, learners=1, learner_acts=False)
 
 
 def _worker_actor_learner_lag(rank, world, port, q):
-    _worker_actor_learner(rank, world, port, q, lag=1)
+    _al_worker(rank, world, port, q, lag=1, learners=1, learner_acts=False)
 
 
 @pytest.mark.parametrize("fn", [_worker_actor_learner, _worker_actor_learner_lag])
 def test_actor_learner_gloo(fn):
     res = _run(fn, world=3)
-    for rank, same, steps, seqs in res:
-        assert same is True, (rank, same)
+    for r in res:
+        assert r[1] is True, (r[0], r[1])
     assert res[0][2] == 3 * 16 * 8 * 2  # two actors x 3 rollouts
     assert res[0][3] == [3.0, 3.0]       # per-actor heartbeat sequence numbers
+    lag = 1 if fn is _worker_actor_learner_lag else 0
+    # version of the weights each rollout used: exactly k (sync) or max(k-1, 0) (lag 1);
+    # verify_versions also matched every rollout's weight checksum against that version
+    for k, vs in enumerate(res[0][4]):
+        assert vs == [max(k - lag, 0)] * 2, (k, vs)
+
+
+def _worker_group_l2(rank, world, port, q):
+    # W = 4, L = 2: every rank acts, ranks 0 and 1 learn on two actor blocks each
+    _al_worker(rank, world, port, q, lag=0, learners=2, learner_acts=True, steps=2, algo="ppo")
+
+
+def _worker_group_dp(rank, world, port, q):
+    # oracle: plain data parallel (every rank learns its own rollout)
+    _al_worker(rank, world, port, q, lag=0, learners=4, learner_acts=True, steps=2, algo="ppo")
+
+
+def test_learner_group_matches_data_parallel_oracle():
+    g = _run(_worker_group_l2, world=4)
+    o = _run(_worker_group_dp, world=4)
+    for r in g + o:
+        assert r[1] is True, (r[0], r[1])
+    assert g[0][2] == o[0][2] == 2 * 16 * 8 * 4
+    assert g[0][6] == o[0][6]  # identical episode statistics (same rollouts)
+    # same weights up to the summation order of the gradient (2 shards x 2 blocks vs 4 x 1)
+    torch.testing.assert_close(g[0][5], o[0][5], rtol=1e-5, atol=1e-6)
+
+
+def _worker_group_lag(rank, world, port, q):
+    # W = 4, L = 2, learners only learn: actors 2, 3 feed shards 0, 1 with lag-1 weights
+    _al_worker(rank, world, port, q, lag=1, learners=2, learner_acts=False, steps=4)
+
+
+def test_learner_group_lag1_versions_never_torn():
+    res = _run(_worker_group_lag, world=4)
+    for r in res:
+        assert r[1] is True, (r[0], r[1])
+    for lr in (0, 1):
+        assert [v[0] for v in res[lr][4]] == [0, 0, 1, 2]

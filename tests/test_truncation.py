@@ -171,3 +171,21 @@ def test_device_mountaincar_cut_at_200(cuda):
 def test_device_halfcheetah_cut_at_1000(cuda):
     n = _device_trainer_check(cuda, "HalfCheetahSynth-v0", T=1010, N=32, algo="ppo")
     assert n == 32  # HalfCheetah only truncates: exactly one cut per env at step 1000
+
+
+def test_blocked_scan_oracle_equals_per_block_scans():
+    """[K, T, N] blocks with flat val [K*T*N + K*N] == K independent [T+1, N] scans."""
+    K, T, N = 3, 12, 7
+    g = torch.Generator().manual_seed(3)
+    rew = torch.randn(K, T, N, generator=g)
+    u = torch.rand(K, T, N, generator=g)
+    done = torch.where(u < 0.1, torch.ones_like(u), torch.where(u < 0.15, torch.full_like(u, 2.0), torch.zeros_like(u)))
+    val = torch.randn(K * T * N + K * N, generator=g)
+    tval = torch.randn(K, T, N, generator=g)
+    adv, ret, st = ref.gae_scan_tm_ref(rew, done, val, 0.98, 0.97, tval)
+    for k in range(K):
+        vk = torch.cat([val[k * T * N:(k + 1) * T * N].reshape(T, N), val[K * T * N + k * N:K * T * N + (k + 1) * N][None]])
+        a, r, _ = ref.gae_scan_tm_ref(rew[k], done[k], vk, 0.98, 0.97, tval[k])
+        torch.testing.assert_close(adv[k], a)
+        torch.testing.assert_close(ret[k], r)
+    torch.testing.assert_close(st[0], adv.sum())
