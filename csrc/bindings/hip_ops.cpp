@@ -18,6 +18,8 @@ int rrl_mlp_forward(int mode, const float* params, const float* X, int B, int D,
                     uint64_t step, uint32_t row_offset, const float* gate, int num_cu, void* stream);
 int rrl_mlp_grad_slabs(int B, int num_cu);
 int rrl_set_value_grad_mode(int mode);
+int rrl_set_value_grad_tune(int tune);
+void rrl_set_value_grad_stamps(void* buf);
 int rrl_mlp_grad(int head, const float* params, const float* X, int B, int D, int A, int H,
                  const float* mask, const int* act, const float* actc, const float* adv, const float* ret,
                  const float* logp_old, const float* adv_stats, float inv_B, float clip_eps, float ent_coef,
@@ -363,6 +365,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mlp_forward", &mlp_forward);
   m.def("mlp_grad_slabs", &mlp_grad_slabs);
   m.def("mlp_grad", &mlp_grad);
+  m.def("set_value_grad_stamps", [](const Tensor& t) { rrl_set_value_grad_stamps(t.numel() ? t.data_ptr() : nullptr); });
+  m.def("set_value_grad_tune", [](int64_t t) { return (int64_t)rrl_set_value_grad_tune((int)t); });
   m.def("set_value_grad_mode", [](int64_t mode) { return (int64_t)rrl_set_value_grad_mode((int)mode); },
         "value-MSE gradient kernel: 1 = bf16x6 weight-stationary (H 128, D <= 8), 0 = fp32 MFMA; returns the "
         "previous mode (-1 queries without changing)");

@@ -29,6 +29,8 @@ struct GradArgs {
   float* grad_slab;  // [grid][P]
   float* loss_slab;  // [grid][8]
   int P;
+  int tune = 0;      // value_grad.hip scheduling variant (set by its launcher)
+  unsigned long long* stamps = nullptr;  // diagnostic stamp sums (value_grad.hip STAMP build)
 };
 
 // Weight-stationary bf16x6 gradient kernels (value_grad.hip): value head for H = 128,

@@ -124,10 +124,26 @@ RRL_DEV floatx4 mma6(const Split8& a, const Split8& b, floatx4 c) {
   return mfma_bf16(a.h, b.h, c);
 }
 
+// Element (row, col) of an activation image.  The 16-byte chunk index (col / 8) is XORed with
+// (row / 4) mod 4: the C-layout stores (16 lanes = 16 consecutive rows, one 8-byte half chunk
+// each) then fall 2-way on the 32 store banks instead of 4-way at the plain 72-dword row
+// stride, while the b128 row reads stay conflict-free and the transposed reads (rows 4g + q,
+// two half chunks per row) stay conflict-free too (bank maps in docs/KERNELS.md).
+RRL_DEV int img_off(int row, int col) { return row * kVgLd + (((col >> 3) ^ ((row >> 2) & 3)) << 3) + (col & 7); }
+
+// Sum over the 4 lane groups (lanes j, j+16, j+32, j+48) with VALU lane swaps (no LDS
+// round trip, unlike __shfl_xor): a wave-uniform call site only (EXEC all ones).
+RRL_DEV float group_sum_swap(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float s = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 // 8 consecutive features of batch row `row` (b128 read of each piece).
 RRL_DEV Split8 frag_row(const uint16_t* img, int row, int col) {
   Split8 s;
-  const uint16_t* a = img + row * kVgLd + col;
+  const uint16_t* a = img + img_off(row, col);
   s.h = *reinterpret_cast<const vbf16x8*>(a);
   s.m = *reinterpret_cast<const vbf16x8*>(a + kVgImg);
   s.l = *reinterpret_cast<const vbf16x8*>(a + 2 * kVgImg);
@@ -140,7 +156,7 @@ RRL_DEV Split8 frag_row(const uint16_t* img, int row, int col) {
 RRL_DEV vbf16x8 frag_tr1(const uint16_t* img, int k0, int col0, int lane) {
   typedef __attribute__((address_space(3))) vs16x4 lds_v4;
   const int q = (lane >> 2) & 3, pp = lane & 3, g = lane >> 4;
-  const uint16_t* a0 = img + (k0 + 4 * g + q) * kVgLd + col0 + 4 * pp;
+  const uint16_t* a0 = img + img_off(k0 + 4 * g + q, col0 + 4 * pp);  // row + 16: same swizzle
   const vs16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0));
   const vs16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0 + 16 * kVgLd));
   typedef short vs16x8 __attribute__((ext_vector_type(8)));
@@ -171,7 +187,7 @@ RRL_DEV Split8 frag_tr(const uint16_t* img, int k0, int col0, int lane) {
 RRL_DEV void store_split(uint16_t* img, int row, int col, const floatx4 v) {
   vbf16x4 h, m, lo;
   split4(v, h, m, lo);
-  uint16_t* a = img + row * kVgLd + col;
+  uint16_t* a = img + img_off(row, col);
   *reinterpret_cast<vbf16x4*>(a) = h;
   *reinterpret_cast<vbf16x4*>(a + kVgImg) = m;
   *reinterpret_cast<vbf16x4*>(a + 2 * kVgImg) = lo;
@@ -218,8 +234,21 @@ RRL_DEV float reduce_scatter16(const float (&v)[16], int j) {
 // HEAD: HEAD_VALUE_MSE (one output) or a 2-action categorical policy head (HEAD_PG_CAT /
 // HEAD_PPO_CAT, the CartPole policy step): the same three 128x128 products, only the head
 // (NA outputs reduced over the 8 waves, loss gradient, dW3 / db3 rows) differs.
-template <int DP, int HEAD>
+// Diagnostic in-kernel stamps (STAMP = true builds only, tools/kbench.py --stamps): per-wave
+// cycle sums of the slab's segments, written to p.stamps; never part of a timed run.
+#define VG_STAMP(k)                                                                     \
+  if (STAMP) {                                                                          \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    unsigned long long t_;                                                              \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    if ((k) > 0) st_sum[(k)-1] += t_ - st_prev;                                         \
+    st_prev = t_;                                                                       \
+  }
+
+template <int DP, int HEAD, bool STAMP = false>
 __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
+  unsigned long long st_prev = 0, st_sum[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   extern __shared__ __attribute__((aligned(16))) uint16_t vg_lds[];
   constexpr bool kValue = HEAD == HEAD_VALUE_MSE;
   constexpr int NA = kValue ? 1 : 2;
@@ -305,17 +334,60 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   for (int a = 0; a < NA; ++a) bacc3[a] = 0.f;
   float s_loss = 0.f, s_val = 0.f, s_cnt = 0.f, s_ent = 0.f, s_kl = 0.f, s_clip = 0.f;
 
+  // Per-slab global inputs are prefetched ONE SLAB AHEAD into registers (issue early, write
+  // late): the x slab (XQ values per thread) and this lane's head inputs for its 4 batch rows
+  // 16 bt + j (ret, or adv / act / logp_old).  Their HBM latency hides under a whole slab of
+  // MFMA work instead of stalling the slab's first barrier and the head.
+  constexpr int XQ = (64 * DP + 511) / 512;
+  float xr[XQ];
+  float hin[4], hlp[4];  // ret (value) or adv (policy); logp_old
+  int hact[4];
+  auto prefetch = [&](int b0) {
+#pragma unroll
+    for (int i = 0; i < XQ; ++i) {
+      const int q = min((int)threadIdx.x + 512 * i, 64 * DP - 1);
+      const int rl = q / DP, d = q % DP, b = b0 + rl;
+      const float v = p.X[(size_t)min(b, p.B - 1) * D + min(d, D - 1)];
+      xr[i] = (b < p.B && d < D) ? v : 0.f;
+    }
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) {
+      const int bc = min(b0 + 16 * bt + j, p.B - 1);
+      if (kValue) {
+        hin[bt] = p.ret[bc];
+      } else {
+        hin[bt] = p.adv[bc];
+        hact[bt] = p.act[bc];
+        hlp[bt] = p.logp_old ? p.logp_old[bc] : 0.f;
+      }
+    }
+  };
+  prefetch(blockIdx.x * 64);
+  if ((p.tune & 1) && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  if ((p.tune & 2) && __builtin_amdgcn_readfirstlane(threadIdx.x) < 256) __builtin_amdgcn_s_setprio(1);
+
   for (int base = blockIdx.x * 64; base < p.B; base += gridDim.x * 64) {
+    VG_STAMP(0);
     // ------------------------------------------------------------ x slab -> LDS
     // (double-buffered by slab parity: the buffer written here was last read two slabs ago)
     float* xs = xsb + (parity & 1) * 64 * DP;
     parity ^= 1;
-    for (int q = threadIdx.x; q < 64 * DP; q += blockDim.x) {
-      const int rl = q / DP, d = q % DP, b = base + rl;
-      const float v = p.X[(size_t)min(b, p.B - 1) * D + min(d, D - 1)];
-      xs[q] = (b < p.B && d < D) ? v : 0.f;
+#pragma unroll
+    for (int i = 0; i < XQ; ++i) {
+      const int q = (int)threadIdx.x + 512 * i;
+      if (q < 64 * DP) xs[q] = xr[i];
     }
+    float cin[4], clp[4];
+    int cact[4];
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) {
+      cin[bt] = hin[bt];
+      clp[bt] = hlp[bt];
+      cact[bt] = hact[bt];
+    }
+    if (base + (int)gridDim.x * 64 < p.B) prefetch(base + gridDim.x * 64);
     __syncthreads();  // x visible; the previous slab's readers of both images are done
+    VG_STAMP(1);
 
     // ------------------------------------------------------------ layer 1 (fp32 MFMA)
     uint32_t m1 = 0;  // relu'(h1) bits: 4 bt + r
@@ -334,6 +406,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     }
     __syncthreads();
 
+    VG_STAMP(2);
     // ------------------------------------------------------------ layer 2 (bf16x6 MFMA)
     floatx4 h2[4];
 #pragma unroll
@@ -363,6 +436,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       for (int r = 0; r < 4; ++r) h2[bt][r] = h2[bt][r] > 0.f ? h2[bt][r] : 0.f;
     }
 
+    VG_STAMP(3);
     // ------------------------------------------------------------ head
     floatx4 w3v[NA];
 #pragma unroll
@@ -374,7 +448,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         pv = fmaf(w3v[a][1], h2[bt][1], pv);
         pv = fmaf(w3v[a][2], h2[bt][2], pv);
         pv = fmaf(w3v[a][3], h2[bt][3], pv);
-        pv = group_sum(pv);
+        pv = group_sum_swap(pv);
         if (g == bt) red[(w * NA + a) * 64 + 16 * bt + j] = pv;
       }
     }
@@ -394,7 +468,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       }
       if (kValue) {
         const float v = outv[0];
-        const float diff = v - (ok ? p.ret[bc] : 0.f);
+        const float diff = v - (ok ? cin[bt] : 0.f);
         dout[bt][0] = ok ? 2.f * diff * p.inv_B : 0.f;
         if (w == 0 && g == 0 && ok) {
           s_loss += diff * diff;
@@ -408,15 +482,15 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         for (int a = 0; a < kMaxAct; ++a) logits[a] = a < NA ? outv[a] : -INFINITY;
         if (ok) apply_mask(p.mask ? p.mask + (size_t)bc * NA : nullptr, NA, logits);
         const CatStats cs = cat_stats(NA, logits);
-        const int act = ok ? p.act[bc] : 0;
+        const int act = ok ? cact[bt] : 0;
         const float logp = pick_logit(NA, logits, act) - cs.lse;
-        const float adv = ((ok ? p.adv[bc] : 0.f) - adv_mean) * adv_rstd;
+        const float adv = ((ok ? cin[bt] : 0.f) - adv_mean) * adv_rstd;
         float dlogp, loss_i;
         if (HEAD == HEAD_PG_CAT) {
           dlogp = -adv;
           loss_i = -logp * adv;
         } else {
-          const float lpo = ok ? p.logp_old[bc] : logp;
+          const float lpo = (ok && p.logp_old) ? clp[bt] : logp;
           const float ratio = __expf(logp - lpo);
           const float s1 = ratio * adv;
           const float s2 = fminf(fmaxf(ratio, 1.f - p.clip_eps), 1.f + p.clip_eps) * adv;
@@ -436,7 +510,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         if (w == 0 && g == 0 && ok) {
           s_loss += loss_i;
           s_ent += cs.entropy;
-          if (p.logp_old) s_kl += p.logp_old[bc] - logp;
+          if (p.logp_old) s_kl += clp[bt] - logp;
           s_cnt += 1.f;
         }
       }
@@ -446,6 +520,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       }
     }
 
+    VG_STAMP(4);
     // ------------------------------------------------------------ dh2, dW3, db2
     float tv[16];  // this slab's [db2 | dW3 row 0 | db1 | dW3 row 1] partials of features own + 4g + r
 #pragma unroll
@@ -467,6 +542,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     accv += reduce_scatter16(tv, j);
     __syncthreads();
 
+    VG_STAMP(5);
     // ------------------------------------------------------------ dh1 (own), dW1, db1
     floatx4 dh1[4];
 #pragma unroll
@@ -499,6 +575,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         tb[8 + r] += dh1[bt][r];
       }
     }
+    VG_STAMP(6);
     accv += reduce_scatter16(tb, j);
     // dW1 one group of 4 input columns at a time (16 partials live, whatever D is), each
     // folded over the 16 batch lanes right away: lane j keeps entry j
@@ -519,6 +596,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       acc1[d4] += reduce_scatter16(t1, j);
     }
 
+    VG_STAMP(7);
     // ------------------------------------------------------------ dW2 += dh2 h1^T
     {
       Split8 a = frag_tr(dhimg, 0, own, l);
@@ -536,6 +614,12 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         (void)kc;
       }
     }
+    VG_STAMP(8);
+    if (STAMP) st_sum[8] += 0;
+  }
+  if (STAMP && p.stamps != nullptr && l == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p.stamps[(blockIdx.x * 8 + w) * 8 + k] = st_sum[k];
   }
 
   // ------------------------------------------------------------------ epilogue
@@ -578,14 +662,30 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 bool value_grad_split_supported(int D, int H) { return H == kVgH && D >= 1 && D <= 24; }
 bool policy_grad_split_supported(int D, int H, int A) { return H == kVgH && D >= 1 && D <= 8 && A == 2; }
 
+static int g_vg_tune = 0;  // scheduling experiments (bit 0: waves 4-7 at prio 1, bit 1: waves 0-3, bit 3: stamps)
+static unsigned long long* g_vg_stamps = nullptr;
+
 template <int DP, int HEAD>
-static int launch_vg(const GradArgs& a, int grid, hipStream_t s) {
+static int launch_vg(const GradArgs& a0, int grid, hipStream_t s) {
+  GradArgs a = a0;
+  a.tune = g_vg_tune;
+  a.stamps = g_vg_stamps;
   constexpr int NA = HEAD == HEAD_VALUE_MSE ? 1 : 2;
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP, HEAD>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, vg_lds_bytes(DP, NA));
     attr_set = true;
+  }
+  if (a.tune & 8) {  // diagnostic stamps build
+    static bool attr_st = false;
+    if (!attr_st) {
+      (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP, HEAD, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, vg_lds_bytes(DP, NA));
+      attr_st = true;
+    }
+    hipLaunchKernelGGL((value_grad_split_kernel<DP, HEAD, true>), dim3(grid), dim3(512), vg_lds_bytes(DP, NA), s, a);
+    return (int)hipGetLastError();
   }
   hipLaunchKernelGGL((value_grad_split_kernel<DP, HEAD>), dim3(grid), dim3(512), vg_lds_bytes(DP, NA), s, a);
   return (int)hipGetLastError();
@@ -608,3 +708,11 @@ int launch_policy_grad_split(const GradArgs& a, int head, int grid, hipStream_t 
 }
 
 }  // namespace rrl
+
+extern "C" void rrl_set_value_grad_stamps(void* buf) { rrl::g_vg_stamps = (unsigned long long*)buf; }
+
+extern "C" int rrl_set_value_grad_tune(int t) {
+  const int old = rrl::g_vg_tune;
+  rrl::g_vg_tune = t;
+  return old;
+}

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--B", type=int, default=2097152)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--H", type=int, default=128)
+    ap.add_argument("--stamps", action="store_true", help="diagnostic per-segment cycle stamps of the value-grad kernel")
+    ap.add_argument("--tunes", default="", help="comma list of value_grad scheduling variants to time too")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, H, D = a.B, a.H, 4
@@ -57,6 +59,24 @@ def main():
         us = timeit(lambda: mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret, grad_slab=slab, loss_slab=ls), a.iters)
         res["value_grad_us"] = us
         res["value_grad_TFLOPs_nominal"] = flop_row * B / us / 1e6
+        if a.stamps:
+            st = torch.zeros(ns * 8 * 8, dtype=torch.int64, device=dev)
+            hip().set_value_grad_stamps(st)
+            old_t = hip().set_value_grad_tune(8)
+            mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret, grad_slab=slab, loss_slab=ls)
+            torch.cuda.synchronize()
+            hip().set_value_grad_tune(old_t)
+            hip().set_value_grad_stamps(torch.empty(0, device=dev))
+            seg = st.view(ns, 8, 8).double().mean(0) / (B / 64 / ns)  # cycles per slab, per wave x segment
+            names = ["xstore+bar", "layer1+bar", "layer2 mfma", "head+bar", "dout/dh2+bar", "dh1 mfma", "dW1", "dW2 mfma"]
+            res_st = {names[k]: [round(x, 1) for x in seg[:, k].tolist()] for k in range(8)}
+            print(json.dumps({"stamps_cycles_per_slab_per_wave": res_st}))
+        if a.tunes:
+            for t in [int(x) for x in a.tunes.split(",")]:
+                old_t = hip().set_value_grad_tune(t)
+                res[f"value_grad_tune{t}_us"] = timeit(
+                    lambda: mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret, grad_slab=slab, loss_slab=ls), a.iters)
+                hip().set_value_grad_tune(old_t)
         old = hip().set_value_grad_mode(0)  # the fp32-MFMA kernel, for comparison
         us0 = timeit(lambda: mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret, grad_slab=slab, loss_slab=ls), a.iters)
         hip().set_value_grad_mode(old)
