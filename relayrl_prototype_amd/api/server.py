@@ -134,7 +134,8 @@ class TrainingServer:
                 from ..transport.zmq_transport import ZmqTrainingEndpoint
 
                 al, tr = self._zmq_endpoints()
-                self._endpoints.append(ZmqTrainingEndpoint(self.service, al, tr, self.multiactor, self.verbose))
+                self._endpoints.append(ZmqTrainingEndpoint(self.service, al, tr, self.multiactor, self.verbose,
+                                                           model_push_addr=address(self.train_server)))
             elif self.server_type == "grpc":
                 from ..transport.grpc_transport import GrpcTrainingEndpoint
 

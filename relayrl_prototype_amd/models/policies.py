@@ -177,19 +177,60 @@ def module_dims(m: nn.Module):
     return int(w1.shape[1]), int(w3.shape[0]), int(w1.shape[0]), "policy.log_std" not in sd
 
 
+# TorchScript qualified names of the reference model file: the archive holds
+# code/__torch__/REINFORCE/kernel.py with class PolicyWithoutBaseline / PolicyWithBaseline
+# (examples/.../cartpole/zmq/client_model.pt; REINFORCE.py:64-68 scripts kernel.py's classes).
+# Export-only subclasses carry that module path; the exported copy's submodules are re-classed
+# to them just before scripting (TorchScript caches compiled types per Python class, so the
+# working classes keep their own names).
+REFERENCE_MODULE = "REINFORCE.kernel"
+_REF_CLASSES = {base: type(base.__name__, (base,), {"__module__": REFERENCE_MODULE, "__qualname__": base.__name__})
+                for base in (DiscretePolicyNetwork, ContinuousPolicyNetwork, BaselineValueNetwork,
+                             PolicyWithoutBaseline, PolicyWithBaseline)}
+
+
+def reference_named(module: nn.Module) -> nn.Module:
+    """A copy of ``module`` whose policy classes script as ``__torch__.REINFORCE.kernel.*``."""
+    import copy
+
+    m = copy.deepcopy(module)
+    for sub in m.modules():
+        cls = _REF_CLASSES.get(type(sub))
+        if cls is not None:
+            sub.__class__ = cls
+    return m
+
+
+def _save_scripted(module: nn.Module, path: str) -> None:
+    torch.jit.save(torch.jit.script(reference_named(module)), path)
+
+
 def export_torchscript(module: nn.Module, path: str) -> None:
-    """torch.jit.script + save (REINFORCE.py:64-68); written atomically (tmp + rename)."""
+    """torch.jit.script + save (REINFORCE.py:64-68), written atomically.  The archive root is
+    the file's stem (``server_model/`` for server_model.pt, like the reference), so the file is
+    written under its final name inside a private temp directory and then moved."""
     import os
+    import tempfile
 
-    scripted = torch.jit.script(module)
-    tmp = f"{path}.tmp.{os.getpid()}"
-    torch.jit.save(scripted, tmp)
-    os.replace(tmp, path)
+    d = tempfile.mkdtemp(prefix=".rrl_export_", dir=os.path.dirname(os.path.abspath(path)))
+    try:
+        tmp = os.path.join(d, os.path.basename(path))
+        _save_scripted(module, tmp)
+        os.replace(tmp, path)
+    finally:
+        try:
+            os.rmdir(d)
+        except OSError:
+            pass
 
 
-def torchscript_bytes(module: nn.Module) -> bytes:
-    import io
+def torchscript_bytes(module: nn.Module, archive: str = "server_model") -> bytes:
+    """The TorchScript archive as bytes, rooted at ``{archive}/`` (reference: server_model/)."""
+    import os
+    import tempfile
 
-    buf = io.BytesIO()
-    torch.jit.save(torch.jit.script(module), buf)
-    return buf.getvalue()
+    with tempfile.TemporaryDirectory(prefix="rrl_ts_") as d:
+        path = os.path.join(d, f"{archive}.pt")
+        _save_scripted(module, path)
+        with open(path, "rb") as f:
+            return f.read()

@@ -1,0 +1,359 @@
+"""Reference ZMQ trajectory frames: the ``serde_pickle`` encoding of ``Vec<RelayRLAction>``.
+
+A reference agent uploads every finished episode as ``serde_pickle::to_writer(&actions)``
+(trajectory.rs:50-55, decoded by training_zmq.rs:994-1012 with ``pickle::from_slice``).
+serde_pickle writes a pickle protocol-3 stream of plain containers: a struct is a dict keyed
+by field names, ``Option::None`` is ``None``, ``Vec<u8>`` a list of ints, a newtype enum
+variant ``{name: value}`` (or ``(name, value)`` with its compat representation) and a unit
+variant its name.
+
+``loads`` here is NOT Python's unpickler: it is a small interpreter of the data-only opcode
+subset (containers, scalars, strings, bytes, memo).  Every opcode that can import a name or
+call one -- GLOBAL, STACK_GLOBAL, REDUCE, BUILD, INST, OBJ, NEWOBJ, EXT*, PERSID -- is an
+error, so a frame can never execute anything.  ``dumps`` writes the same subset the way
+serde_pickle does (protocol 3, no memo); tests use it to build reference-shaped fixtures.
+
+``actions_from_reference`` maps the decoded list onto :class:`RelayRLAction`s (TensorData =
+{shape, dtype, data: bytes of a one-tensor safetensors file}, action.rs:193-352), and
+:class:`CumulativeDeduper` strips the prefix a reference agent re-sends with every upload
+(it never clears its trajectory below max_length: defect A1).
+"""
+from __future__ import annotations
+
+import hashlib
+import struct
+from collections import OrderedDict
+from typing import Any, List, Optional, Tuple
+
+MAX_DEPTH = 64
+
+
+class PickleFrameError(ValueError):
+    pass
+
+
+_MARK = object()
+
+
+def is_pickle_frame(buf: bytes) -> bool:
+    return len(buf) >= 2 and buf[0] == 0x80 and buf[1] <= 5
+
+
+def loads(buf: bytes) -> Any:
+    """Decode a data-only pickle (protocols 2-5 opcode subset); raises PickleFrameError on
+    any opcode outside the subset."""
+    mv = memoryview(buf)
+    n = len(mv)
+    pos = 0
+    stack: List[Any] = []
+    memo = {}
+
+    def take(k: int) -> memoryview:
+        nonlocal pos
+        if pos + k > n:
+            raise PickleFrameError("truncated frame")
+        out = mv[pos:pos + k]
+        pos += k
+        return out
+
+    def pop_mark() -> List[Any]:
+        for i in range(len(stack) - 1, -1, -1):
+            if stack[i] is _MARK:
+                items = stack[i + 1:]
+                del stack[i:]
+                return items
+        raise PickleFrameError("MARK not found")
+
+    def top_container(kind):
+        if not stack or not isinstance(stack[-1], kind):
+            raise PickleFrameError(f"expected a {kind.__name__} on the stack")
+        return stack[-1]
+
+    while True:
+        op = take(1)[0]
+        if op == 0x80:  # PROTO
+            take(1)
+        elif op == 0x95:  # FRAME
+            take(8)
+        elif op == 0x2E:  # STOP
+            if len(stack) != 1:
+                raise PickleFrameError("bad stack at STOP")
+            return stack[0]
+        elif op == 0x4E:  # NONE
+            stack.append(None)
+        elif op == 0x88:
+            stack.append(True)
+        elif op == 0x89:
+            stack.append(False)
+        elif op == 0x4B:  # BININT1
+            stack.append(take(1)[0])
+        elif op == 0x4D:  # BININT2
+            stack.append(struct.unpack("<H", take(2))[0])
+        elif op == 0x4A:  # BININT
+            stack.append(struct.unpack("<i", take(4))[0])
+        elif op == 0x8A:  # LONG1
+            k = take(1)[0]
+            stack.append(int.from_bytes(take(k), "little", signed=True) if k else 0)
+        elif op == 0x8B:  # LONG4
+            k = struct.unpack("<i", take(4))[0]
+            if k < 0 or k > 64:
+                raise PickleFrameError("LONG4 too large")
+            stack.append(int.from_bytes(take(k), "little", signed=True) if k else 0)
+        elif op == 0x47:  # BINFLOAT (big-endian double)
+            stack.append(struct.unpack(">d", take(8))[0])
+        elif op == 0x58:  # BINUNICODE
+            k = struct.unpack("<I", take(4))[0]
+            stack.append(str(take(k), "utf-8"))
+        elif op == 0x8C:  # SHORT_BINUNICODE
+            k = take(1)[0]
+            stack.append(str(take(k), "utf-8"))
+        elif op == 0x8D:  # BINUNICODE8
+            k = struct.unpack("<Q", take(8))[0]
+            stack.append(str(take(k), "utf-8"))
+        elif op == 0x42:  # BINBYTES
+            k = struct.unpack("<I", take(4))[0]
+            stack.append(bytes(take(k)))
+        elif op == 0x43:  # SHORT_BINBYTES
+            k = take(1)[0]
+            stack.append(bytes(take(k)))
+        elif op == 0x8E:  # BINBYTES8
+            k = struct.unpack("<Q", take(8))[0]
+            stack.append(bytes(take(k)))
+        elif op == 0x28:  # MARK
+            if sum(1 for s in stack if s is _MARK) >= MAX_DEPTH:
+                raise PickleFrameError("nesting too deep")
+            stack.append(_MARK)
+        elif op == 0x5D:  # EMPTY_LIST
+            stack.append([])
+        elif op == 0x7D:  # EMPTY_DICT
+            stack.append({})
+        elif op == 0x29:  # EMPTY_TUPLE
+            stack.append(())
+        elif op == 0x8F:  # EMPTY_SET
+            stack.append(set())
+        elif op == 0x61:  # APPEND
+            v = stack.pop()
+            top_container(list).append(v)
+        elif op == 0x65:  # APPENDS
+            items = pop_mark()
+            top_container(list).extend(items)
+        elif op == 0x73:  # SETITEM
+            v = stack.pop()
+            k = stack.pop()
+            top_container(dict)[_key(k)] = v
+        elif op == 0x75:  # SETITEMS
+            items = pop_mark()
+            if len(items) % 2:
+                raise PickleFrameError("odd SETITEMS")
+            d = top_container(dict)
+            for i in range(0, len(items), 2):
+                d[_key(items[i])] = items[i + 1]
+        elif op == 0x90:  # ADDITEMS
+            items = pop_mark()
+            top_container(set).update(_key(x) for x in items)
+        elif op == 0x91:  # FROZENSET
+            stack.append(frozenset(_key(x) for x in pop_mark()))
+        elif op == 0x74:  # TUPLE
+            stack.append(tuple(pop_mark()))
+        elif op in (0x85, 0x86, 0x87):  # TUPLE1..3
+            k = op - 0x84
+            if len(stack) < k:
+                raise PickleFrameError("stack underflow")
+            items = stack[-k:]
+            del stack[-k:]
+            stack.append(tuple(items))
+        elif op == 0x71:  # BINPUT
+            memo[take(1)[0]] = stack[-1]
+        elif op == 0x72:  # LONG_BINPUT
+            memo[struct.unpack("<I", take(4))[0]] = stack[-1]
+        elif op == 0x94:  # MEMOIZE
+            memo[len(memo)] = stack[-1]
+        elif op == 0x68:  # BINGET
+            stack.append(memo[take(1)[0]])
+        elif op == 0x6A:  # LONG_BINGET
+            stack.append(memo[struct.unpack("<I", take(4))[0]])
+        elif op == 0x30:  # POP
+            stack.pop()
+        elif op == 0x31:  # POP_MARK
+            pop_mark()
+        else:
+            raise PickleFrameError(f"opcode 0x{op:02x} is not allowed in a trajectory frame")
+
+
+def _key(k):
+    if isinstance(k, (list, dict, set)):
+        raise PickleFrameError("unhashable key")
+    return k
+
+
+# ---------------------------------------------------------------------- writer (serde_pickle style)
+def dumps(obj: Any) -> bytes:
+    out = bytearray(b"\x80\x03")
+    _dump(obj, out, 0)
+    out += b"."
+    return bytes(out)
+
+
+def _dump(o: Any, out: bytearray, depth: int):
+    if depth > MAX_DEPTH:
+        raise ValueError("nesting too deep")
+    if o is None:
+        out += b"N"
+    elif o is True:
+        out += b"\x88"
+    elif o is False:
+        out += b"\x89"
+    elif isinstance(o, int):
+        if 0 <= o < 256:
+            out += b"K" + bytes([o])
+        elif 0 <= o < 65536:
+            out += b"M" + struct.pack("<H", o)
+        elif -2**31 <= o < 2**31:
+            out += b"J" + struct.pack("<i", o)
+        else:
+            raw = o.to_bytes((o.bit_length() + 8) // 8, "little", signed=True)
+            out += b"\x8a" + bytes([len(raw)]) + raw
+    elif isinstance(o, float):
+        out += b"G" + struct.pack(">d", o)
+    elif isinstance(o, str):
+        raw = o.encode("utf-8")
+        out += b"X" + struct.pack("<I", len(raw)) + raw
+    elif isinstance(o, (bytes, bytearray)):
+        out += (b"C" + bytes([len(o)]) if len(o) < 256 else b"B" + struct.pack("<I", len(o))) + bytes(o)
+    elif isinstance(o, tuple):
+        if len(o) == 0:
+            out += b")"
+        else:
+            out += b"("
+            for x in o:
+                _dump(x, out, depth + 1)
+            out += b"t"
+    elif isinstance(o, list):
+        out += b"]"
+        for i in range(0, len(o), 1000):
+            out += b"("
+            for x in o[i:i + 1000]:
+                _dump(x, out, depth + 1)
+            out += b"e"
+    elif isinstance(o, dict):
+        out += b"}"
+        if o:
+            out += b"("
+            for k, v in o.items():
+                _dump(k, out, depth + 1)
+                _dump(v, out, depth + 1)
+            out += b"u"
+    else:
+        raise TypeError(f"cannot serialise {type(o).__name__}")
+
+
+# ---------------------------------------------------------------------- reference actions
+def enum_variant(v: Any) -> Tuple[str, Any]:
+    """serde enum in any serde_pickle representation -> (variant, payload)."""
+    if isinstance(v, str):
+        return v, None
+    if isinstance(v, dict) and len(v) == 1:
+        (k, val), = v.items()
+        return str(k), val
+    if isinstance(v, (tuple, list)) and 1 <= len(v) <= 2 and isinstance(v[0], str):
+        return v[0], (v[1] if len(v) == 2 else None)
+    raise PickleFrameError(f"not an enum value: {type(v).__name__}")
+
+
+def _tensordata(d: Any):
+    from ..types import tensordata_from_json
+
+    if d is None:
+        return None
+    if not isinstance(d, dict) or "data" not in d:
+        raise PickleFrameError("TensorData must be a dict with shape / dtype / data")
+    dt, _ = enum_variant(d.get("dtype", "Float"))
+    data = d["data"]
+    raw = bytes(data) if isinstance(data, (bytes, bytearray, list, tuple)) else None
+    if raw is None:
+        raise PickleFrameError("TensorData.data must be bytes or a list of u8")
+    return tensordata_from_json({"shape": list(d.get("shape", [])), "dtype": dt, "data": raw})
+
+
+def actions_from_reference(obj: Any):
+    """Decoded ``Vec<RelayRLAction>`` (or a RelayRLTrajectory struct) -> [RelayRLAction]."""
+    from ..types import RelayRLAction
+
+    if isinstance(obj, dict) and "actions" in obj:  # a whole RelayRLTrajectory struct
+        obj = obj["actions"]
+    if not isinstance(obj, (list, tuple)):
+        raise PickleFrameError("expected a list of actions")
+    out = []
+    for a in obj:
+        if not isinstance(a, dict):
+            raise PickleFrameError("an action must be a dict")
+        data = None
+        if a.get("data") is not None:
+            data = {}
+            for k, v in a["data"].items():
+                kind, val = enum_variant(v)
+                data[str(k)] = _tensordata(val) if kind == "Tensor" else val
+        out.append(RelayRLAction(_tensordata(a.get("obs")), _tensordata(a.get("act")), _tensordata(a.get("mask")),
+                                 float(a.get("rew", 0.0)), data, bool(a.get("done", False)),
+                                 bool(a.get("reward_updated", False))))
+    return out
+
+
+def reference_frame(actions) -> bytes:
+    """[RelayRLAction] -> the frame a reference agent would send (serde_pickle of the
+    actions' serde form; enums in serde_pickle's default ``{variant: value}`` / name form)."""
+    out = []
+    for a in actions:
+        d = a.to_json_dict()
+        for key in ("obs", "act", "mask"):
+            if d[key] is not None:
+                d[key] = dict(d[key], data=list(d[key]["data"]))
+        if d["data"] is not None:
+            for k, v in d["data"].items():
+                (kind, val), = v.items()
+                if kind == "Tensor":
+                    d["data"][k] = {"Tensor": dict(val, data=list(val["data"]))}
+        out.append(d)
+    return dumps(out)
+
+
+class CumulativeDeduper:
+    """Reference agents re-send every earlier episode with each upload (the trajectory is
+    only cleared at max_length, trajectory.rs:160-204), each over a NEW connection, so the
+    learner would train on the same actions again and again.  Uploads are matched by a
+    digest of their first action; an upload that extends the previous one from the same
+    agent keeps only its new actions."""
+
+    def __init__(self, capacity: int = 4096):
+        self.capacity = capacity
+        self._seen: "OrderedDict[bytes, Tuple[int, bytes]]" = OrderedDict()
+        self.stripped = 0
+
+    @staticmethod
+    def _digest(actions) -> bytes:
+        h = hashlib.blake2b(digest_size=16)
+        for a in actions:
+            for t in (a.get_obs(), a.get_act()):
+                h.update(b"-" if t is None else t.tobytes())
+            h.update(struct.pack("<f?", a.get_rew(), a.get_done()))
+        return h.digest()
+
+    def new_actions(self, actions) -> list:
+        if not actions:
+            return actions
+        head = self._digest(actions[:1])
+        prev = self._seen.get(head)
+        keep = actions
+        if prev is not None:
+            n_prev, dig = prev
+            if len(actions) > n_prev and self._digest(actions[:n_prev]) == dig:
+                keep = actions[n_prev:]
+                self.stripped += n_prev
+            elif len(actions) == n_prev and self._digest(actions) == dig:
+                keep = []  # an exact re-send
+                self.stripped += n_prev
+        self._seen[head] = (len(actions), self._digest(actions))
+        self._seen.move_to_end(head)
+        while len(self._seen) > self.capacity:
+            self._seen.popitem(last=False)
+        return keep

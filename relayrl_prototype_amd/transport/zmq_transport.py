@@ -8,7 +8,13 @@ Server side (reference training_zmq.rs:669-1058):
     a PUSH to a PULL each agent had to *bind* on one fixed port, which limited it to one
     agent per host (defect A6) and never stopped listening only when multiactor was set.
   * PULL bound at ``trajectory_server``: one frame per episode (fan-in) -- a columnar RRLC
-    frame (agent default) or a per-action RRLT frame.
+    frame (agent default), a per-action RRLT frame, or a reference agent's
+    ``serde_pickle(Vec<RelayRLAction>)`` frame (trajectory.rs:50-90), decoded by the
+    data-only opcode interpreter of ``serde_pickle.py`` with the re-sent prefix stripped.
+  * Reference agents (GET_MODEL without a format frame, agent_zmq.rs:316-442) get their
+    model updates the reference way: a PUSH connected to the ``training_server`` address the
+    agent BINDS a PULL on (training_zmq.rs:876-934, agent_zmq.rs:625-698), one TorchScript
+    frame per update.
 Agent side (agent_zmq.rs:163-698): DEALER (identity = agent id) + PUSH.
 No busy polling anywhere (A7): receives block in C++ with timeouts.
 """
@@ -35,8 +41,15 @@ def make_agent_id() -> str:
 
 class ZmqTrainingEndpoint:
     def __init__(self, service, agent_listener: str, trajectory_server: str, multiactor: bool = True,
-                 verbose: bool = False):
+                 verbose: bool = False, model_push_addr: Optional[str] = None):
+        from .serde_pickle import CumulativeDeduper
+
         self.service = service
+        self.model_push_addr = model_push_addr
+        self.ref_agents = set()   # identities that did the reference handshake
+        self._model_push = None   # PUSH -> reference agents' bound PULL (lazy)
+        self.dedupe = CumulativeDeduper()
+        self.reference_frames = 0
         self.multiactor = multiactor
         self.verbose = verbose
         self.router = _native.ZmtpSocket(_native.SockType.ROUTER)
@@ -77,8 +90,10 @@ class ZmqTrainingEndpoint:
                 if cmd == b"GET_MODEL":
                     fmt = body[1] if len(body) > 1 else FMT_TORCHSCRIPT
                     with self._lock:
-                        self.agents.setdefault(peer, fmt)
-                        self.agents[peer] = fmt
+                        if len(body) > 1:
+                            self.agents[peer] = fmt
+                        else:  # reference agent: updates go to its bound PULL, not the ROUTER
+                            self.ref_agents.add(peer)
                     self.router.send([peer, b"", self._model_payload(fmt)], 5000)
                 elif cmd == b"MODEL_SET":
                     self.service.register_agent(peer.decode(errors="replace"))
@@ -102,16 +117,39 @@ class ZmqTrainingEndpoint:
             _, frames = msg
             for f in frames:
                 try:
-                    traj = TrajectoryColumns.decode(f) if TrajectoryColumns.is_frame(f) else RelayRLTrajectory.decode(f)
+                    traj = self._decode_traj(f)
                 except Exception as e:
                     self.bad_frames += 1
                     self._log("bad trajectory frame", e)
                     continue
-                self.service.submit(traj)
+                if traj is not None:
+                    self.service.submit(traj)
+
+    def _decode_traj(self, f: bytes):
+        from . import serde_pickle
+
+        if TrajectoryColumns.is_frame(f):
+            return TrajectoryColumns.decode(f)
+        if serde_pickle.is_pickle_frame(f):
+            acts = self.dedupe.new_actions(serde_pickle.actions_from_reference(serde_pickle.loads(f)))
+            self.reference_frames += 1
+            if not acts:
+                return None
+            t = RelayRLTrajectory(max(len(acts), 1), None, "reference-agent")
+            t.actions = acts
+            return t
+        return RelayRLTrajectory.decode(f)
 
     def _on_model(self, blob: ModelBlob):
         with self._lock:
             agents = list(self.agents.items())
+            push_ref = bool(self.ref_agents) and self.model_push_addr is not None
+        if push_ref:
+            if self._model_push is None:
+                self._model_push = _native.ZmtpSocket(_native.SockType.PUSH)
+                self._model_push.connect(self.model_push_addr)
+            if not self._model_push.send([blob.torchscript()], 1000):
+                self._log("model push to", self.model_push_addr, "timed out")
         if not agents:
             return
         enc = {}
@@ -127,6 +165,8 @@ class ZmqTrainingEndpoint:
             t.join(timeout=5)
         self.router.close()
         self.pull.close()
+        if self._model_push is not None:
+            self._model_push.close()
 
 
 class ZmqAgentTransport:
