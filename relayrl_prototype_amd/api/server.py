@@ -146,9 +146,13 @@ class TrainingServer:
                 local_transport.register(self._local_addr, self.service)
                 self._endpoints.append("local")
             self.service.start()
+            mi = self.cfg.get_mi355x_params()
+            self.service.start_sweeper(float(mi.get("agent_timeout_s", 120.0) or 0.0),
+                                       float(mi.get("agent_sweep_period_s", 5.0)))
 
     def disable_server(self) -> None:
         with self._lock:
+            self.service.stop_sweeper()
             for e in self._endpoints:
                 if e == "local":
                     local_transport.unregister(self._local_addr, self.service)

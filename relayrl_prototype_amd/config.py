@@ -124,6 +124,8 @@ MI355X_DEFAULTS = {
     "use_graphs": True,
     "transport": "rccl",
     "mode": "dp",  # dp | actor_learner
+    "agent_timeout_s": 120.0,  # evict agents silent this long (0 = never); agents heartbeat every 10 s
+    "agent_sweep_period_s": 5.0,
 }
 
 _REINFORCE_TYPES = {

@@ -71,6 +71,8 @@ class ActorLearnerConfig:
     num_threads: int = 4
     use_graphs: bool = True
     verify_versions: bool = False  # check header version/checksum on the learners (syncs)
+    stall_timeout_s: float = 120.0  # per-step watchdog floor (0 = off); budget = max(floor, factor x avg step)
+    stall_factor: float = 20.0
 
     def to_dict(self):
         return asdict(self)
@@ -180,7 +182,7 @@ class _Actor:
 
 
 class ActorLearner:
-    def __init__(self, cfg: ActorLearnerConfig, comm: Optional[Comm] = None, device=None):
+    def __init__(self, cfg: ActorLearnerConfig, comm: Optional[Comm] = None, device=None, on_stall=None):
         self.cfg = cfg
         self.comm = comm or Comm()
         W = self.comm.world
@@ -243,6 +245,13 @@ class ActorLearner:
             self.learner = None
             self.front = self.actor.params
         self.back = torch.zeros_like(self.front) if (self.acts and not self.is_learner) else None
+        self._pending_peers = []  # (peer rank, work) of the step's in-flight P2P transfers
+        self._seen_seq = {}       # actor rank -> last heartbeat sequence number received
+        from ..utils.watchdog import StepWatchdog
+
+        self.watchdog = StepWatchdog(f"rank {self.rank} ({'learner' if self.is_learner else 'actor'})",
+                                     cfg.stall_timeout_s if W > 1 else 0.0, cfg.stall_factor, self._diagnose,
+                                     on_stall)
         # initial weight broadcast from rank 0 (the handshake's GET_MODEL)
         self.comm.broadcast_(self.front, 0)
         if self.is_learner and self.actor is not None:
@@ -261,7 +270,7 @@ class ActorLearner:
 
     # ------------------------------------------------------------------ one step
     def step(self):
-        cfg = self.cfg
+        self.watchdog.begin(self.epoch)
         parts = self.actor.rollout(self.version_in_use) if self.actor is not None else None
         if self.is_learner:
             self._gather(parts)
@@ -272,6 +281,26 @@ class ActorLearner:
             self._recv_weights()
         self.version += 1
         self.epoch += 1
+        self.watchdog.end()
+
+    def _diagnose(self) -> str:
+        """What this rank is blocked on (called by the watchdog thread)."""
+        waiting = []
+        for peer, w in list(self._pending_peers):
+            try:
+                done = w.is_completed()
+            except Exception:
+                done = False
+            if not done:
+                waiting.append(peer)
+        waiting = sorted(set(waiting))
+        if self.is_learner:
+            lost = waiting or [a for a in self.shard if a != self.rank]
+            seqs = {a: self._seen_seq.get(a) for a in lost}
+            return (f"learner {self.rank} is missing rollout {self.epoch} from actor(s) {lost} "
+                    f"(last heartbeat seq {seqs}); the learner group all-reduce may be waiting on a peer shard")
+        return (f"actor {self.rank} is waiting on learner {self.topo.learner_of(self.rank)} "
+                f"(weights v{self.version + 1 - self.cfg.max_lag})")
 
     @property
     def version_in_use(self) -> int:
@@ -294,8 +323,12 @@ class ActorLearner:
                 if d is not None:
                     ops.append(dist.P2POp(dist.irecv, d, a))
         if ops:
-            for w in dist.batch_isend_irecv(ops):
+            works = dist.batch_isend_irecv(ops)
+            peers = [op.peer for op in ops] if len(works) == len(ops) else [op.peer for op in ops][:len(works)]
+            self._pending_peers = list(zip(peers, works))
+            for w in works:
                 w.wait()
+            self._pending_peers = []
 
     def _send_rollout(self, parts):
         dst = self.topo.learner_of(self.rank)
@@ -323,7 +356,9 @@ class ActorLearner:
         src = self.topo.learner_of(self.rank)
         if self._recv_work is not None:  # (lag 1) v_k, posted last step
             self._finish_recv()
-        self._recv_work = (self.version + 1, dist.batch_isend_irecv([dist.P2POp(dist.irecv, self.back, src)]))
+        works = dist.batch_isend_irecv([dist.P2POp(dist.irecv, self.back, src)])
+        self._recv_work = (self.version + 1, works)
+        self._pending_peers = [(src, w) for w in works]
         if self.cfg.max_lag == 0:
             self._finish_recv()
 
@@ -342,6 +377,7 @@ class ActorLearner:
         for w in self._send_works:
             w.wait()
         self._send_works = []
+        self.watchdog.close()
 
     @property
     def wbuf(self) -> torch.Tensor:
@@ -354,6 +390,7 @@ class ActorLearner:
         self.rl.learn(self.b_obs, self.b_act, self.b_rew, self.b_done, self.b_logp, tobs=self.b_tobs)
         self.last_hdr = self.b_hdr
         self.received += K
+        self._seen_seq = {a: self.epoch + 1 for a in self.shard}  # headers carry seq = epoch + 1
         if cfg.verify_versions:
             self._verify(self.b_hdr.cpu())
 

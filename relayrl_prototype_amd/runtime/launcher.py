@@ -150,9 +150,10 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
                             "baseline_config": preset.baseline_config})
     t0 = time.perf_counter()
     last: Dict = {}
-    from ..utils.faults import maybe_kill_rank
+    from ..utils.faults import maybe_kill_rank, maybe_stall_rank
 
     for ep in range(start + 1, epochs + 1):
+        maybe_stall_rank(comm.rank, ep, out_dir)
         _epoch(tr)
         if ep % log_every == 0 or ep == epochs:
             m = tr.metrics()

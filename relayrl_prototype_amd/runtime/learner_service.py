@@ -32,6 +32,10 @@ class LearnerService:
         self.errors = 0
         self.last_error: Optional[str] = None
         self.checkpoint_fn = checkpoint_fn
+        self.evicted: Dict[str, Dict[str, Any]] = {}
+        self._evict_cbs = []
+        self._sweeper: Optional[threading.Thread] = None
+        self._stop_sweep = threading.Event()
         self.publish_model()
 
     # ------------------------------------------------------------------ models
@@ -55,6 +59,46 @@ class LearnerService:
         now = time.time()
         with self._agents_lock:
             return [a for a, r in self.agents.items() if now - r["last_seen"] > timeout_s]
+
+    def on_evict(self, fn) -> None:
+        """``fn(agent_ids)`` runs after each eviction (transports drop their routing state)."""
+        self._evict_cbs.append(fn)
+
+    def evict_stale(self, timeout_s: float) -> list:
+        """Drop agents silent for ``timeout_s`` (no upload, heartbeat or handshake): they stop
+        receiving model pushes; an evicted agent that comes back simply re-registers."""
+        now = time.time()
+        with self._agents_lock:
+            gone = [a for a, r in self.agents.items() if now - r["last_seen"] > timeout_s]
+            for a in gone:
+                self.evicted[a] = self.agents.pop(a)
+        if gone:
+            print(f"[LearnerService] evicted {len(gone)} silent agent(s) (> {timeout_s:.0f} s): {gone}", flush=True)
+            for fn in list(self._evict_cbs):
+                try:
+                    fn(gone)
+                except Exception as e:
+                    print(f"[LearnerService] eviction hook failed: {e!r}", flush=True)
+        return gone
+
+    def start_sweeper(self, timeout_s: float, period_s: float = 5.0) -> None:
+        """Periodic ``evict_stale`` in a daemon thread."""
+        if timeout_s <= 0 or (self._sweeper is not None and self._sweeper.is_alive()):
+            return
+
+        def loop():
+            while not self._stop_sweep.wait(period_s):
+                self.evict_stale(timeout_s)
+
+        self._stop_sweep.clear()
+        self._sweeper = threading.Thread(target=loop, name="relayrl-agent-sweeper", daemon=True)
+        self._sweeper.start()
+
+    def stop_sweeper(self) -> None:
+        self._stop_sweep.set()
+        if self._sweeper is not None:
+            self._sweeper.join(timeout=5)
+        self._sweeper = None
 
     # ------------------------------------------------------------------ ingest
     def submit(self, traj, block: bool = True, timeout: Optional[float] = None) -> bool:

@@ -65,6 +65,15 @@ class ZmqTrainingEndpoint:
         for t in self._threads:
             t.start()
         service.store.subscribe(self._on_model)
+        if hasattr(service, "on_evict"):
+            service.on_evict(self._on_evict)
+
+    def _on_evict(self, agent_ids):
+        ids = {a.encode() if isinstance(a, str) else a for a in agent_ids}
+        with self._lock:
+            for peer in [p for p in self.agents if p in ids]:
+                del self.agents[peer]
+            self.ref_agents -= ids
 
     def _log(self, *a):
         if self.verbose:
@@ -94,6 +103,7 @@ class ZmqTrainingEndpoint:
                             self.agents[peer] = fmt
                         else:  # reference agent: updates go to its bound PULL, not the ROUTER
                             self.ref_agents.add(peer)
+                    self.service.register_agent(peer.decode(errors="replace"))
                     self.router.send([peer, b"", self._model_payload(fmt)], 5000)
                 elif cmd == b"MODEL_SET":
                     self.service.register_agent(peer.decode(errors="replace"))
@@ -101,6 +111,9 @@ class ZmqTrainingEndpoint:
                     self._log("registered", peer)
                 elif cmd == b"HEARTBEAT":
                     self.service.register_agent(peer.decode(errors="replace"))
+                    with self._lock:  # an evicted agent that is alive again gets pushes again
+                        if len(body) > 1 and peer not in self.agents:
+                            self.agents[peer] = body[1]
                 elif cmd == b"BYE":
                     with self._lock:
                         self.agents.pop(peer, None)
@@ -173,7 +186,8 @@ class ZmqAgentTransport:
     """DEALER handshake + model-update listener + PUSH trajectory sender."""
 
     def __init__(self, agent_id: str, agent_listener: str, trajectory_server: str,
-                 on_model: Callable[[ModelBlob], None], handshake_timeout_s: float = 60.0):
+                 on_model: Callable[[ModelBlob], None], handshake_timeout_s: float = 60.0,
+                 heartbeat_s: float = 10.0):
         self.agent_id = agent_id
         self.on_model = on_model
         self.dealer = _native.ZmtpSocket(_native.SockType.DEALER, agent_id.encode())
@@ -187,6 +201,15 @@ class ZmqAgentTransport:
         self._thread.start()
         self.model: Optional[ModelBlob] = None
         self._handshake(handshake_timeout_s)
+        self._hb = None
+        if heartbeat_s > 0:  # keeps an idle agent registered (LearnerService.start_sweeper)
+            self._hb = threading.Thread(target=self._heartbeat_loop, args=(heartbeat_s,), daemon=True,
+                                        name="rrl-agent-heartbeat")
+            self._hb.start()
+
+    def _heartbeat_loop(self, period_s: float):
+        while not self._stop.wait(period_s):
+            self.heartbeat()
 
     def _recv_loop(self):
         while not self._stop.is_set():
@@ -240,7 +263,7 @@ class ZmqAgentTransport:
         return self.push.send([payload], 10000)
 
     def heartbeat(self):
-        self.dealer.send([b"", b"HEARTBEAT"], 1000)
+        self.dealer.send([b"", b"HEARTBEAT", FMT_RRLM], 1000)
 
     def close(self):
         try:
@@ -249,5 +272,7 @@ class ZmqAgentTransport:
             pass
         self._stop.set()
         self._thread.join(timeout=5)
+        if self._hb is not None:
+            self._hb.join(timeout=5)
         self.dealer.close()
         self.push.close()

@@ -17,6 +17,9 @@ Process-level faults for the elastic-restart path (runtime/launcher.py):
     RRL_FAULT_KILL="1:3"   -- rank 1 dies (exit 17) after epoch 3, once per run directory;
                               torchrun (--max-restarts) restarts the group and every rank
                               resumes from its last checkpoint.
+    RRL_FAULT_STALL="2:2:60" -- rank 2 hangs for 60 s before epoch 2 (a stuck actor), once
+                              per run directory: its peers' step watchdogs
+                              (utils/watchdog.py) exit them, torchrun restarts the group.
 """
 from __future__ import annotations
 
@@ -97,3 +100,20 @@ def maybe_kill_rank(rank: int, epoch: int, run_dir: str) -> None:
     open(marker, "w").close()
     print(f"[faults] injected crash of rank {rank} after epoch {epoch}", flush=True)
     os._exit(17)
+
+
+def maybe_stall_rank(rank: int, epoch: int, run_dir: str) -> None:
+    """Hang this rank once if RRL_FAULT_STALL names (rank, epoch, seconds)."""
+    spec = os.environ.get("RRL_FAULT_STALL", "")
+    if not spec:
+        return
+    r, e, sec = spec.split(":")
+    if int(r) != rank or int(e) != epoch:
+        return
+    marker = os.path.join(run_dir, f".stall_fired_r{rank}_e{epoch}")
+    if os.path.exists(marker):
+        return
+    os.makedirs(run_dir, exist_ok=True)
+    open(marker, "w").close()
+    print(f"[faults] injected stall of rank {rank} before epoch {epoch} ({sec} s)", flush=True)
+    time.sleep(float(sec))

@@ -130,7 +130,7 @@ def _al_worker(rank, world, port, q, lag=0, learners=0, learner_acts=True, steps
         gathered = [torch.zeros_like(w) for _ in range(world)]
         dist.all_gather(gathered, w)
         same = all(torch.equal(gathered[0], x) for x in gathered)
-        q.put((rank, same, m.get("EnvSteps"), m.get("ActorSeqs"), versions, w, m.get("Episodes")))
+        q.put((rank, same, m.get("EnvSteps"), m.get("ActorSeqs"), versions, w.numpy().copy(), m.get("Episodes")))
         dist.destroy_process_group()
     except Exception:
         import traceback
@@ -179,7 +179,7 @@ def test_learner_group_matches_data_parallel_oracle():
     assert g[0][2] == o[0][2] == 2 * 16 * 8 * 4
     assert g[0][6] == o[0][6]  # identical episode statistics (same rollouts)
     # same weights up to the summation order of the gradient (2 shards x 2 blocks vs 4 x 1)
-    torch.testing.assert_close(g[0][5], o[0][5], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(torch.from_numpy(g[0][5]), torch.from_numpy(o[0][5]), rtol=1e-5, atol=1e-6)
 
 
 def _worker_group_lag(rank, world, port, q):
@@ -193,3 +193,64 @@ def test_learner_group_lag1_versions_never_torn():
         assert r[1] is True, (r[0], r[1])
     for lr in (0, 1):
         assert [v[0] for v in res[lr][4]] == [0, 0, 1, 2]
+
+
+def _worker_stall(rank, world, port, q):
+    import time
+
+    try:
+        comm = _init(rank, world, port)
+        from relayrl_prototype_amd.runtime.actor_learner import ActorLearner, ActorLearnerConfig
+
+        cfg = ActorLearnerConfig(env="CartPole-v1", num_envs=8, rollout_len=16, hidden=64, train_vf_iters=2,
+                                 num_threads=1, seed=5, learner_ranks=1, learner_acts=False, stall_timeout_s=3.0)
+        def report(msg):  # flush the queue's feeder thread: the watchdog exits right after
+            q.put((rank, "stall", msg))
+            q.close()
+            q.join_thread()
+
+        al = ActorLearner(cfg, comm, device="cpu", on_stall=report)
+        for k in range(4):
+            if rank == 2 and k == 2:
+                time.sleep(60)  # a hung actor: no rollout, no heartbeat
+            al.step()
+        q.put((rank, "done", None))
+    except Exception as e:
+        q.put((rank, "error", repr(e)))
+
+
+def test_stalled_actor_is_named_and_learner_exits_for_restart():
+    """Actor 2 hangs before its third rollout: the learner's step watchdog names it (with
+    its last heartbeat) within the per-epoch budget -- not the 10-minute collective timeout
+    -- and exits with EXIT_STALL so torchrun restarts the group."""
+    import time
+
+    from relayrl_prototype_amd.utils.watchdog import EXIT_STALL
+
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker_stall, args=(r, 3, port, q)) for r in range(3)]
+    t0 = time.time()
+    for p in ps:
+        p.start()
+    try:
+        msgs = []
+        while time.time() - t0 < 90:
+            try:
+                msgs.append(q.get(timeout=1))
+            except Exception:
+                pass
+            if any(m[0] == 0 and m[1] == "stall" for m in msgs):
+                break
+        stall = [m for m in msgs if m[0] == 0 and m[1] == "stall"]
+        assert stall, msgs
+        assert "actor(s) [2]" in stall[0][2] and "rollout 2" in stall[0][2], stall[0][2]
+        assert time.time() - t0 < 60
+        ps[0].join(timeout=20)
+        assert ps[0].exitcode == EXIT_STALL
+    finally:
+        for p in ps:
+            if p.is_alive():
+                p.kill()
+            p.join(timeout=10)

@@ -71,3 +71,20 @@ def test_rank_failure_group_restart_resumes(tmp_path):
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     m = json.loads(line)
     assert m["Updates"] == 4 and m["EnvSteps"] == 4 * 2 * 2 * 2
+
+
+def test_stalled_actor_group_restart_resumes(tmp_path):
+    """Actor-learner preset over 3 gloo ranks: rank 2 hangs before epoch 3; the other
+    ranks' step watchdogs exit them (EXIT_STALL) well inside the collective timeout,
+    torchrun restarts the group and every rank resumes from its checkpoint."""
+    env = dict(os.environ, PYTHONPATH=REPO, RRL_QUIET_CONFIG="1", OMP_NUM_THREADS="1", RRL_FAULT_STALL="2:3:120")
+    r = subprocess.run([sys.executable, "-m", "relayrl_prototype_amd", "train", "--preset",
+                        "lunarlander-reinforce-baseline", "--gpus", "3", "--epochs", "4", "--out", str(tmp_path),
+                        "--checkpoint-every", "1", "--auto-resume", "--max-restarts", "1", "--set", "num_envs=4",
+                        "rollout_len=8", "train_vf_iters=2", "num_threads=1", "stall_timeout_s=4"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert os.path.exists(tmp_path / ".stall_fired_r2_e3")
+    assert "[watchdog]" in r.stderr and "stalled" in r.stderr
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    assert json.loads(line)["EnvSteps"] == 4 * 8 * 4 * 3

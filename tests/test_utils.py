@@ -223,3 +223,39 @@ def test_solved_check_window_of_100_episodes():
     m = c.update(120, 120 * 400.0)  # the newest epoch alone fills the window
     assert m == 400.0 and not c.solved(m) and len(c.hist) == 1
     assert math.isnan(SolvedCheck().update(0, 0.0))
+
+
+def test_learner_service_evicts_silent_agents_and_endpoint_stops_pushing():
+    import time as _t
+
+    from relayrl_prototype_amd.runtime.learner_service import LearnerService
+
+    class _Algo:
+        def get_weights(self):
+            import torch
+
+            return {"pi": torch.zeros(4), "version": 0, "obs_dim": 1, "act_dim": 1, "hidden": 1, "discrete": True}
+
+        def model_bytes(self):
+            return b""
+
+        def receive_trajectory(self, t):
+            return False
+
+    svc = LearnerService(_Algo())
+    hooked = []
+    svc.on_evict(hooked.extend)
+    svc.register_agent("A")
+    svc.register_agent("B")
+    svc.agents["A"]["last_seen"] -= 100.0  # silent for 100 s
+    assert svc.evict_stale(30.0) == ["A"] and hooked == ["A"]
+    assert "A" in svc.evicted and list(svc.agents) == ["B"]
+    svc.register_agent("A")  # a returning agent re-registers
+    assert "A" in svc.agents
+    svc.agents["B"]["last_seen"] -= 100.0
+    svc.start_sweeper(30.0, period_s=0.05)
+    t0 = _t.time()
+    while "B" in svc.agents and _t.time() - t0 < 5:
+        _t.sleep(0.02)
+    svc.stop_sweeper()
+    assert "B" not in svc.agents and "B" in hooked
