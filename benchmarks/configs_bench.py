@@ -66,7 +66,11 @@ def main():
             print(json.dumps({"preset": name, "baseline_config": p.baseline_config, "n_gpus": comm.world,
                               "env_steps_per_sec": steps / el.item(), "ms_per_epoch": el.item() / a.steps * 1e3,
                               "env_steps_per_epoch": steps / a.steps,
-                              "avg_ep_ret": m1.get("AverageEpRet")}), flush=True)
+                              "avg_ep_ret": m1.get("AverageEpRet"),
+                              **({"rollout_s_per_epoch": (m1["RolloutS"] - m0["RolloutS"]) / a.steps,
+                                  "learn_s_per_epoch": (m1["LearnS"] - m0["LearnS"]) / a.steps,
+                                  "overlap": bool(getattr(tr, "overlap", False))} if "RolloutS" in m1 else {})}),
+                  flush=True)
         del tr
         if dev.type == "cuda":
             torch.cuda.empty_cache()

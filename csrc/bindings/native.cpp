@@ -213,6 +213,14 @@ PYBIND11_MODULE(_native, m) {
             e.step((const void*)act, (float*)obs, (float*)rew, (float*)done, (float*)tobs);
           },
           py::arg("act"), py::arg("obs"), py::arg("rew"), py::arg("done"), py::arg("tobs") = 0)
+      .def(
+          "step_async_ptr",
+          [](VecEnv& e, uintptr_t act, uintptr_t obs, uintptr_t rew, uintptr_t done, uintptr_t tobs) {
+            py::gil_scoped_release nogil;
+            e.step_async((const void*)act, (float*)obs, (float*)rew, (float*)done, (float*)tobs);
+          },
+          py::arg("act"), py::arg("obs"), py::arg("rew"), py::arg("done"), py::arg("tobs") = 0)
+      .def("wait", &VecEnv::wait, py::call_guard<py::gil_scoped_release>())
       .def("take_stats", [](VecEnv& e) {
         EpisodeStats s = e.take_stats();
         py::dict d;

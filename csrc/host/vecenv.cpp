@@ -334,10 +334,13 @@ VecEnv::VecEnv(const std::string& name, int num_envs, uint64_t seed, int num_thr
   ret_.assign(n_, 0.f);
   nthreads_ = std::max(1, std::min(num_threads, n_));
   tstats_.resize(nthreads_);
-  for (int t = 1; t < nthreads_; ++t) pool_.emplace_back(&VecEnv::worker, this, t);
+  // every slice runs on a pool thread (the caller only submits and waits), so a step can
+  // also be left running while the caller does other work (step_async)
+  for (int t = 0; t < nthreads_; ++t) pool_.emplace_back(&VecEnv::worker, this, t);
 }
 
 VecEnv::~VecEnv() {
+  wait();
   {
     std::lock_guard<std::mutex> g(mu_);
     stop_ = true;
@@ -349,15 +352,13 @@ VecEnv::~VecEnv() {
 void VecEnv::worker(int tid) {
   uint64_t seen = 0;
   while (true) {
-    const std::function<void(int, int)>* job;
     {
       std::unique_lock<std::mutex> g(mu_);
       cv_.wait(g, [&] { return stop_ || gen_ != seen; });
       if (stop_) return;
       seen = gen_;
-      job = job_;
     }
-    (*job)(tid, nthreads_);
+    job_(tid, nthreads_);  // job_ is only replaced after every worker finished (wait())
     {
       std::lock_guard<std::mutex> g(mu_);
       if (--pending_ == 0) done_cv_.notify_all();
@@ -365,21 +366,27 @@ void VecEnv::worker(int tid) {
   }
 }
 
-void VecEnv::run_parallel(const std::function<void(int, int)>& fn) {
-  if (nthreads_ == 1) {
-    fn(0, 1);
-    return;
-  }
+void VecEnv::submit(std::function<void(int, int)> fn) {
+  wait();
   {
     std::lock_guard<std::mutex> g(mu_);
-    job_ = &fn;
-    pending_ = nthreads_ - 1;
+    job_ = std::move(fn);
+    pending_ = nthreads_;
+    busy_ = true;
     ++gen_;
   }
   cv_.notify_all();
-  fn(0, nthreads_);
+}
+
+void VecEnv::wait() {
   std::unique_lock<std::mutex> g(mu_);
   done_cv_.wait(g, [&] { return pending_ == 0; });
+  busy_ = false;
+}
+
+void VecEnv::run_parallel(const std::function<void(int, int)>& fn) {
+  submit(fn);
+  wait();
 }
 
 void VecEnv::reset(float* obs) {
@@ -394,7 +401,16 @@ void VecEnv::reset(float* obs) {
 }
 
 void VecEnv::step(const void* actions, float* obs, float* rew, float* done, float* tobs) {
-  run_parallel([&](int tid, int nt) {
+  step_async(actions, obs, rew, done, tobs);
+  wait();
+}
+
+void VecEnv::step_async(const void* actions, float* obs, float* rew, float* done, float* tobs) {
+  submit([this, actions, obs, rew, done, tobs](int tid, int nt) { step_range(tid, nt, actions, obs, rew, done, tobs); });
+}
+
+void VecEnv::step_range(int tid, int nt, const void* actions, float* obs, float* rew, float* done, float* tobs) {
+  {
     const int lo = (int)((int64_t)n_ * tid / nt), hi = (int)((int64_t)n_ * (tid + 1) / nt);
     EpisodeStats& st = tstats_[tid];
     for (int i = lo; i < hi; ++i) {
@@ -428,10 +444,11 @@ void VecEnv::step(const void* actions, float* obs, float* rew, float* done, floa
         ret_[i] = 0.f;
       }
     }
-  });
+  }
 }
 
 EpisodeStats VecEnv::take_stats() {
+  wait();  // never read the per-thread sums while an async step is writing them
   EpisodeStats s;
   for (auto& t : tstats_) {
     s.n += t.n;

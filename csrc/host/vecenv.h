@@ -82,10 +82,17 @@ class VecEnv {
   // truncated env's pre-reset observation goes to tobs[i] (its value bootstraps the cut
   // episode), without it truncations are reported as 1.
   void step(const void* actions, float* obs, float* rew, float* done, float* tobs = nullptr);
+  // Asynchronous step: the pool starts stepping and the call returns at once; wait() blocks
+  // until it finished (the buffers must stay untouched until then).  Two VecEnvs stepped
+  // asynchronously keep both thread pools busy at the same time (host_trainer.py pipeline).
+  void step_async(const void* actions, float* obs, float* rew, float* done, float* tobs = nullptr);
+  void wait();
   EpisodeStats take_stats();
 
  private:
   void run_parallel(const std::function<void(int, int)>& fn);
+  void submit(std::function<void(int, int)> fn);
+  void step_range(int tid, int nt, const void* actions, float* obs, float* rew, float* done, float* tobs);
   void worker(int tid);
 
   std::string name_;
@@ -104,7 +111,8 @@ class VecEnv {
   uint64_t gen_ = 0;
   int pending_ = 0;
   bool stop_ = false;
-  const std::function<void(int, int)>* job_ = nullptr;
+  std::function<void(int, int)> job_;  // owned: an async job outlives the submitting call
+  bool busy_ = false;                   // a submitted job has not been waited for
 };
 
 }  // namespace rrl

@@ -74,7 +74,7 @@ class ValueLoop:
         self.net = net
         self.comm = comm
         self.use_graph = use_graph and net.device.type == "cuda" and (comm is None or comm.world == 1)
-        self._graph = None
+        self._graphs = {}
         self._key = None
         self.loss_first = None
         self.loss_last = None
@@ -102,18 +102,22 @@ class ValueLoop:
                 self.net.apply(g, self.comm)
             return
         ns = grad_slabs(B, dev)
-        key = (obs.data_ptr(), ret.data_ptr(), B, iters, float(inv_B))
-        if self._key != key:
+        shape_key = (B, iters, float(inv_B))
+        if self._key != shape_key:
             self._slab = torch.empty(ns, self.net.P, device=dev)
             self.loss_first = torch.zeros(ns, 8, device=dev)
             self.loss_last = torch.zeros(ns, 8, device=dev)
-            self._graph = None
-            self._key = key
+            self._graphs = {}
+            self._key = shape_key
         if not self.use_graph:
             self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last)
             return
         v0 = self.net.version
-        if self._graph is None:
+        gkey = (obs.data_ptr(), ret.data_ptr())  # one graph per input buffer set (double-buffered trainers)
+        g = self._graphs.get(gkey)
+        if g is None:
+            if len(self._graphs) >= 4:
+                self._graphs.clear()
             # Warm up once eagerly (kernel attributes, allocator) on the real buffers,
             # then restore the optimiser state so the warm-up step leaves no trace.
             saved = [t.clone() for t in (self.net.params, self.net.m, self.net.v, self.net.step)]
@@ -125,8 +129,9 @@ class ValueLoop:
             for dst, src in zip((self.net.params, self.net.m, self.net.v, self.net.step), saved):
                 dst.copy_(src)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # thread_local: a host rollout thread (host_trainer overlap) may issue HIP calls meanwhile
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last)
-            self._graph = g
-        self._graph.replay()
+            self._graphs[gkey] = g
+        g.replay()
         self.net.version = v0 + iters

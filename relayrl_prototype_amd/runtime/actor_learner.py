@@ -169,7 +169,6 @@ class _Actor:
             stats = torch.tensor([s["n"], s["sum"], s["sumsq"], s["max"], s["min"], s["sum_len"]],
                                  dtype=torch.float64, device=self.device)
             obs, act, logp, rew, done, tobs = e.d_obs, e.d_act, e.d_logp, e.d_rew, e.d_done, e.d_tobs
-            e.h_obs[0].copy_(e.h_obs[T])
         self.seq += 1
         h = self.header
         h[0] = float(self.seq)

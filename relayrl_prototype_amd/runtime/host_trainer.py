@@ -7,21 +7,31 @@ through pinned hipMemcpyAsync overlapped ..."):
    -> H2D copy on a side stream (non_blocking) -> fused sampling kernel (HIP)
    -> D2H actions into pinned memory -> env threads step ...
 
-The envs are split into two halves that run in a software pipeline: while the GPU
-samples actions for half B, the CPU threads step half A, so neither side idles.  The
-rollout (obs, actions, log-probs) never leaves HBM for the learner; only rewards /
-done flags go host -> device once per rollout.
+The envs are split into two halves, each with its own C++ thread pool, stepped
+ASYNCHRONOUSLY (``VecEnv.step_async``): while the GPU samples actions for one half, the
+other half's threads step, and both pools run at the same time -- every env thread is
+busy, not half of them.  The rollout (obs, actions, log-probs) never leaves HBM for the
+learner; only rewards / done flags go host -> device once per rollout.  Waiting for a
+half's actions is a spin on a non-blocking HIP event (no OS sleep in the loop).
+
+``overlap=True`` (lag-1 pipelining, like the reference's asynchronous agent / trainer
+split, training_zmq.rs:549-618): two buffer sets; while the compute stream runs epoch k's
+update, a rollout thread steps epoch k+1's envs on a SNAPSHOT of the policy one update
+old, on its own HIP streams, into the other buffer set.  Epoch time becomes
+max(rollout, learn) instead of their sum.  The learner never reads a buffer before the
+rollout that fills it has signalled its event, and the snapshot is copied on the
+compute stream after the previous update, so neither side sees a half-written tensor.
 
 On a CPU-only machine the same loop runs with the PyTorch oracle ops (used by the
 multi-process gloo tests).
 """
 from __future__ import annotations
 
+import threading
 import time
 from dataclasses import asdict, dataclass
 from typing import Optional
 
-import numpy as np
 import torch
 
 from .. import _native
@@ -55,9 +65,33 @@ class HostTrainerConfig:
     use_graphs: bool = True
     log_std_init: float = -0.5
     phase_timing: bool = False
+    overlap: bool = False          # lag-1: roll out epoch k+1 while epoch k's update runs (GPU only)
 
     def to_dict(self):
         return asdict(self)
+
+
+class _Buffers:
+    """One rollout's pinned host staging (env side) and HBM buffers (learner side)."""
+
+    def __init__(self, T, N, D, A, continuous, pin, device, with_tobs):
+        self.h_obs = torch.zeros(T + 1, N, D, pin_memory=pin)
+        self.h_rew = torch.zeros(T, N, pin_memory=pin)
+        self.h_done = torch.zeros(T, N, pin_memory=pin)  # 0 / 1 terminal / 2 time-limit truncation
+        # pre-reset observations of truncated steps (bootstrap V(s_T) of cut episodes)
+        self.h_tobs = torch.zeros(T, N, D, pin_memory=pin) if with_tobs else None
+        self.d_tobs = torch.zeros(T, N, D, device=device) if with_tobs else None
+        if continuous:
+            self.h_act = torch.zeros(T, N, A, pin_memory=pin)
+            self.d_act = torch.zeros(T, N, A, device=device)
+        else:
+            self.h_act = torch.zeros(T, N, dtype=torch.int32, pin_memory=pin)
+            self.d_act = torch.zeros(T, N, dtype=torch.int32, device=device)
+        self.d_obs = torch.zeros(T + 1, N, D, device=device)
+        self.d_logp = torch.zeros(T, N, device=device)
+        self.d_rew = torch.zeros(T, N, device=device)
+        self.d_done = torch.zeros(T, N, device=device)
+        self.ready = torch.cuda.Event() if device.type == "cuda" else None  # rollout landed in HBM
 
 
 class HostVecTrainer:
@@ -84,110 +118,213 @@ class HostVecTrainer:
                                  cfg.log_std_init)
         self.timer = PhaseTimer(self.device, enabled=cfg.phase_timing)
         self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.comm, self.timer)
-        pin = cuda
-        D, A = self.D, self.A
-        # pinned host staging (env side) and HBM rollout buffers (learner side)
-        self.h_obs = torch.zeros(T + 1, N, D, pin_memory=pin)
-        self.h_rew = torch.zeros(T, N, pin_memory=pin)
-        self.h_done = torch.zeros(T, N, pin_memory=pin)  # 0 / 1 terminal / 2 time-limit truncation
-        # pre-reset observations of truncated steps (bootstrap V(s_T) of cut episodes)
-        self.h_tobs = torch.zeros(T, N, D, pin_memory=pin) if self.learner.vf is not None else None
-        self.d_tobs = torch.zeros(T, N, D, device=self.device) if self.learner.vf is not None else None
-        if self.continuous:
-            self.h_act = torch.zeros(T, N, A, pin_memory=pin)
-            self.d_act = torch.zeros(T, N, A, device=self.device)
-        else:
-            self.h_act = torch.zeros(T, N, dtype=torch.int32, pin_memory=pin)
-            self.d_act = torch.zeros(T, N, dtype=torch.int32, device=self.device)
-        self.d_obs = torch.zeros(T + 1, N, D, device=self.device)
-        self.d_logp = torch.zeros(T, N, device=self.device)
-        self.d_rew = torch.zeros(T, N, device=self.device)
-        self.d_done = torch.zeros(T, N, device=self.device)
+        self.overlap = bool(cfg.overlap and cuda)
+        with_tobs = self.learner.vf is not None
+        self.bufs = [_Buffers(T, N, self.D, self.A, self.continuous, cuda, self.device, with_tobs)
+                     for _ in range(2 if self.overlap else 1)]
+        self.cur = 0  # buffer set of the newest completed rollout
         self.copy_stream = torch.cuda.Stream(self.device) if cuda else None
+        if self.overlap:
+            self.actor_stream = torch.cuda.Stream(self.device)
+            self.actor_copy_stream = torch.cuda.Stream(self.device)
+            self.actor_params = self.learner.pi.params.clone()  # lag-1 snapshot the rollout thread reads
+        self._pending = None  # (thread, buffer index) of the rollout running ahead
+        self.snapshot_versions = []  # policy version each overlapped rollout acted with
+        self._primed = False  # a completed rollout waits in self.bufs[self.cur]
+        self._rollout_error = None
         # first observation
         for h, env in enumerate(self.envs):
-            lo = bounds[h]
-            env.reset_ptr(self.h_obs[0, lo].data_ptr())
+            env.reset_ptr(self.bufs[0].h_obs[0, bounds[h]].data_ptr())
+        self._final_obs = None  # host view of the newest env observation (start of the next rollout)
         self.epoch = 0
         self.env_steps = 0
         self.global_step = 0
-        self.timings = {"rollout_s": 0.0, "learn_s": 0.0}
+        self.timings = {"rollout_s": 0.0, "learn_s": 0.0, "wait_rollout_s": 0.0}
 
-    def _sample(self, t, h):
+    # views of the newest completed rollout (actor_learner.py, tests)
+    @property
+    def h_obs(self):
+        return self.bufs[self.cur].h_obs
+
+    @property
+    def h_act(self):
+        return self.bufs[self.cur].h_act
+
+    @property
+    def d_obs(self):
+        return self.bufs[self.cur].d_obs
+
+    @property
+    def d_act(self):
+        return self.bufs[self.cur].d_act
+
+    @property
+    def d_logp(self):
+        return self.bufs[self.cur].d_logp
+
+    @property
+    def d_rew(self):
+        return self.bufs[self.cur].d_rew
+
+    @property
+    def d_done(self):
+        return self.bufs[self.cur].d_done
+
+    @property
+    def d_tobs(self):
+        return self.bufs[self.cur].d_tobs
+
+    # ------------------------------------------------------------------ rollout
+    def _sample(self, b: _Buffers, params, copy_stream, t, h, step):
         lo, hi = self.bounds[h], self.bounds[h + 1]
         cuda = self.device.type == "cuda"
         mode = FwdMode.GAUSS_SAMPLE if self.continuous else FwdMode.CAT_SAMPLE
         seed = (self.cfg.seed * 0x9E3779B9 + self.comm.rank * 0x85EBCA6B) & 0x7FFFFFFFFFFF
         if cuda:
             cs = torch.cuda.current_stream(self.device)
-            with torch.cuda.stream(self.copy_stream):
-                self.d_obs[t, lo:hi].copy_(self.h_obs[t, lo:hi], non_blocking=True)
+            with torch.cuda.stream(copy_stream):
+                b.d_obs[t, lo:hi].copy_(b.h_obs[t, lo:hi], non_blocking=True)
                 ev = torch.cuda.Event()
-                ev.record(self.copy_stream)
+                ev.record(copy_stream)
             cs.wait_event(ev)
-            out = {"logp": self.d_logp[t, lo:hi]}
+            out = {"logp": b.d_logp[t, lo:hi], "act": b.d_act[t, lo:hi]}
             if self.continuous:
-                out["act"] = self.d_act[t, lo:hi]
                 out["mean"] = torch.empty(hi - lo, self.A, device=self.device)
-            else:
-                out["act"] = self.d_act[t, lo:hi]
-            mlp_forward(mode, self.learner.pi.params, self.d_obs[t, lo:hi], self.A, self.cfg.hidden, seed=seed,
-                        step=self.global_step + t, row_offset=lo, out=out)
-            self.h_act[t, lo:hi].copy_(self.d_act[t, lo:hi], non_blocking=True)
-            done_ev = torch.cuda.Event()
+            mlp_forward(mode, params, b.d_obs[t, lo:hi], self.A, self.cfg.hidden, seed=seed, step=step + t,
+                        row_offset=lo, out=out)
+            b.h_act[t, lo:hi].copy_(b.d_act[t, lo:hi], non_blocking=True)
+            done_ev = torch.cuda.Event()  # non-blocking event: synchronize() spins, no OS sleep
             done_ev.record(cs)
             return done_ev
-        self.d_obs[t, lo:hi].copy_(self.h_obs[t, lo:hi])
-        r = mlp_forward(mode, self.learner.pi.params, self.d_obs[t, lo:hi], self.A, self.cfg.hidden, seed=seed,
-                        step=self.global_step + t, row_offset=lo)
-        self.d_act[t, lo:hi].copy_(r["act"])
-        self.d_logp[t, lo:hi].copy_(r["logp"])
-        self.h_act[t, lo:hi].copy_(r["act"])
+        b.d_obs[t, lo:hi].copy_(b.h_obs[t, lo:hi])
+        r = mlp_forward(mode, params, b.d_obs[t, lo:hi], self.A, self.cfg.hidden, seed=seed, step=step + t,
+                        row_offset=lo)
+        b.d_act[t, lo:hi].copy_(r["act"])
+        b.d_logp[t, lo:hi].copy_(r["logp"])
+        b.h_act[t, lo:hi].copy_(r["act"])
         return None
 
-    def _step_env(self, t, h):
+    def _step_async(self, b: _Buffers, t, h):
         lo = self.bounds[h]
-        self.envs[h].step_ptr(self.h_act[t, lo].data_ptr(), self.h_obs[t + 1, lo].data_ptr(),
-                              self.h_rew[t, lo].data_ptr(), self.h_done[t, lo].data_ptr(),
-                              self.h_tobs[t, lo].data_ptr() if self.h_tobs is not None else 0)
+        self.envs[h].step_async_ptr(b.h_act[t, lo].data_ptr(), b.h_obs[t + 1, lo].data_ptr(),
+                                    b.h_rew[t, lo].data_ptr(), b.h_done[t, lo].data_ptr(),
+                                    b.h_tobs[t, lo].data_ptr() if b.h_tobs is not None else 0)
 
-    def rollout(self):
+    def _rollout_into(self, idx: int, params, copy_stream, step0: int):
+        """T env steps into buffer set ``idx`` on the calling thread's current stream."""
         T = self.cfg.rollout_len
-        t0 = time.perf_counter()
+        b = self.bufs[idx]
+        if self._final_obs is not None and self._final_obs.data_ptr() != b.h_obs[0].data_ptr():
+            b.h_obs[0].copy_(self._final_obs)  # continue every env where the last rollout left it
         for t in range(T):
-            evs = [self._sample(t, h) for h in range(self.halves)]
+            evs = []
+            for h in range(self.halves):
+                if t > 0:
+                    self.envs[h].wait()  # obs_t of half h (its step t-1 ran on the pool)
+                evs.append(self._sample(b, params, copy_stream, t, h, step0))
             for h in range(self.halves):
                 if evs[h] is not None:
-                    evs[h].synchronize()  # actions of half h are on the host; half h+1 still sampling
-                self._step_env(t, h)
+                    evs[h].synchronize()  # actions of half h are on the host; the other half may still sample
+                self._step_async(b, t, h)
+        for env in self.envs:
+            env.wait()
         # last observation + rewards / dones to the device (async on the copy stream)
         if self.device.type == "cuda":
-            with torch.cuda.stream(self.copy_stream):
-                self.d_obs[T].copy_(self.h_obs[T], non_blocking=True)
-                self.d_rew.copy_(self.h_rew, non_blocking=True)
-                self.d_done.copy_(self.h_done, non_blocking=True)
-                if self.d_tobs is not None:
-                    self.d_tobs.copy_(self.h_tobs, non_blocking=True)
-            torch.cuda.current_stream(self.device).wait_stream(self.copy_stream)
+            with torch.cuda.stream(copy_stream):
+                b.d_obs[T].copy_(b.h_obs[T], non_blocking=True)
+                b.d_rew.copy_(b.h_rew, non_blocking=True)
+                b.d_done.copy_(b.h_done, non_blocking=True)
+                if b.d_tobs is not None:
+                    b.d_tobs.copy_(b.h_tobs, non_blocking=True)
+            cs = torch.cuda.current_stream(self.device)
+            cs.wait_stream(copy_stream)
+            b.ready.record(cs)
         else:
-            self.d_obs[T].copy_(self.h_obs[T])
-            self.d_rew.copy_(self.h_rew)
-            self.d_done.copy_(self.h_done)
-            if self.d_tobs is not None:
-                self.d_tobs.copy_(self.h_tobs)
-        self.global_step += T
+            b.d_obs[T].copy_(b.h_obs[T])
+            b.d_rew.copy_(b.h_rew)
+            b.d_done.copy_(b.h_done)
+            if b.d_tobs is not None:
+                b.d_tobs.copy_(b.h_tobs)
+        self._final_obs = b.h_obs[T]
+
+    def rollout(self):
+        """One synchronous rollout with the current weights into the current buffer set."""
+        t0 = time.perf_counter()
+        self._rollout_into(self.cur, self.learner.pi.params, self.copy_stream, self.global_step)
+        self.global_step += self.cfg.rollout_len
         self.timings["rollout_s"] += time.perf_counter() - t0
 
+    # ------------------------------------------------------------------ epoch
     def train_epoch(self):
-        with self.timer.phase("Rollout"):
-            self.rollout()
-        t0 = time.perf_counter()
-        self.rl.learn(self.d_obs, self.d_act, self.d_rew, self.d_done, self.d_logp, tobs=self.d_tobs)
-        # next rollout starts from the last observation
-        self.h_obs[0].copy_(self.h_obs[self.cfg.rollout_len])
-        self.timings["learn_s"] += time.perf_counter() - t0
+        if not self.overlap:
+            with self.timer.phase("Rollout"):
+                self.rollout()
+            t0 = time.perf_counter()
+            self._learn(self.cur)
+            self.timings["learn_s"] += time.perf_counter() - t0
+        else:
+            self._train_epoch_overlapped()
         self.epoch += 1
         self.env_steps += self.cfg.num_envs * self.cfg.rollout_len
+
+    def _learn(self, idx: int):
+        b = self.bufs[idx]
+        if b.ready is not None:
+            torch.cuda.current_stream(self.device).wait_event(b.ready)
+        self.rl.learn(b.d_obs, b.d_act, b.d_rew, b.d_done, b.d_logp, tobs=b.d_tobs)
+
+    def _launch_ahead(self, idx: int):
+        """Roll out into buffer set ``idx`` on a thread, with the weights as of now."""
+        self.actor_params.copy_(self.learner.pi.params)  # compute stream, after the previous update
+        self.snapshot_versions.append(self.learner.pi.version)
+        snap = torch.cuda.Event()
+        snap.record(torch.cuda.current_stream(self.device))
+        step0 = self.global_step
+        self.global_step += self.cfg.rollout_len
+
+        def run():
+            try:
+                torch.cuda.set_device(self.device)
+                with torch.cuda.stream(self.actor_stream):
+                    self.actor_stream.wait_event(snap)
+                    t0 = time.perf_counter()
+                    self._rollout_into(idx, self.actor_params, self.actor_copy_stream, step0)
+                    self.timings["rollout_s"] += time.perf_counter() - t0
+            except BaseException as e:  # surfaced on join
+                self._rollout_error = e
+
+        th = threading.Thread(target=run, name="relayrl-host-rollout", daemon=True)
+        th.start()
+        self._pending = (th, idx)
+
+    def _join_ahead(self) -> int:
+        th, idx = self._pending
+        t0 = time.perf_counter()
+        th.join()
+        self.timings["wait_rollout_s"] += time.perf_counter() - t0
+        self._pending = None
+        if self._rollout_error is not None:
+            e, self._rollout_error = self._rollout_error, None
+            raise RuntimeError("host rollout thread failed") from e
+        return idx
+
+    def _train_epoch_overlapped(self):
+        if not self._primed:  # first epoch: nothing rolled out ahead yet
+            self._launch_ahead(self.cur)
+            self._join_ahead()
+            self._primed = True
+        learn_idx = self.cur
+        nxt = 1 - learn_idx
+        self._launch_ahead(nxt)  # epoch k+1's envs step while epoch k's update runs
+        t0 = time.perf_counter()
+        with self.timer.phase("Optimize"):
+            self._learn(learn_idx)
+        self.timings["learn_s"] += time.perf_counter() - t0
+        self.cur = self._join_ahead()
+
+    def finish(self):
+        if self._pending is not None:
+            self._join_ahead()
 
     def metrics(self) -> dict:
         tot = {"n": 0.0, "sum": 0.0, "sumsq": 0.0, "max": -1e300, "min": 1e300, "sum_len": 0.0}
@@ -206,6 +343,7 @@ class HostVecTrainer:
         out["WorldSize"] = self.comm.world
         out["RolloutS"] = self.timings["rollout_s"]
         out["LearnS"] = self.timings["learn_s"]
+        out["WaitRolloutS"] = self.timings["wait_rollout_s"]
         if self.timer.enabled:
             out.update(self.timer.columns())
             self.timer.reset()

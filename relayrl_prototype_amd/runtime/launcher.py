@@ -53,9 +53,16 @@ PRESETS: Dict[str, Preset] = {
         "vec", {"env": "HalfCheetahSynth-v0", "algo": "ppo", "num_envs": 16384, "rollout_len": 256,
                 "train_pi_iters": 10, "train_vf_iters": 10, "with_baseline": True, "gamma": 0.99, "lam": 0.95}),
     "halfcheetah-ppo-host": Preset(
-        "halfcheetah-ppo-host", "PPO HalfCheetah with C++ host env threads (pinned H2D/D2H pipeline)",
+        "halfcheetah-ppo-host", "PPO HalfCheetah with C++ host env threads (pinned H2D/D2H pipeline, "
+        "lag-1 rollout/update overlap)",
         "host", {"env": "HalfCheetahSynth-v0", "algo": "ppo", "num_envs": 4096, "rollout_len": 256,
-                 "train_pi_iters": 10, "train_vf_iters": 10, "num_threads": 8, "with_baseline": True}),
+                 "train_pi_iters": 10, "train_vf_iters": 10, "num_threads": 16, "with_baseline": True,
+                 "overlap": True}),
+    "cartpole-reinforce-host": Preset(
+        "cartpole-reinforce-host", "REINFORCE-with-baseline CartPole-v1 with C++ host env threads (pinned "
+        "H2D/D2H pipeline, lag-1 rollout/update overlap)",
+        "host", {"env": "CartPole-v1", "num_envs": 8192, "rollout_len": 64, "with_baseline": True,
+                 "num_threads": 16, "gamma": 0.98, "lam": 0.97, "overlap": True}),
 }
 
 

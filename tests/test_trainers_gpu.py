@@ -171,3 +171,40 @@ def test_agent_server_zmq_with_gpu_learner(cuda, tmp_path, monkeypatch):
         agent.close()
     finally:
         srv.close(save=False)
+
+
+def test_host_trainer_overlap_lag1(cuda):
+    """Lag-1 host pipeline: rollout k+1 acts with the policy of update k-1 while update k runs,
+    every epoch learns exactly one rollout, and the buffers alternate."""
+    from relayrl_prototype_amd.runtime.host_trainer import HostTrainerConfig, HostVecTrainer
+
+    cfg = HostTrainerConfig(env="CartPole-v1", num_envs=512, rollout_len=32, train_vf_iters=4, num_threads=4,
+                            overlap=True, seed=2)
+    tr = HostVecTrainer(cfg, device=cuda)
+    assert tr.overlap and len(tr.bufs) == 2
+    for _ in range(4):
+        tr.train_epoch()
+    tr.finish()
+    torch.cuda.synchronize()
+    assert tr.snapshot_versions == [0, 0, 1, 2, 3]  # REINFORCE: one policy step per epoch
+    m = tr.metrics()
+    assert m["EnvSteps"] == 4 * 512 * 32
+    assert math.isfinite(m["LossPi"]) and torch.isfinite(tr.learner.pi.params).all()
+
+
+def test_host_trainer_overlap_learns(cuda):
+    from relayrl_prototype_amd.runtime.host_trainer import HostTrainerConfig, HostVecTrainer
+
+    cfg = HostTrainerConfig(env="CartPole-v1", num_envs=256, rollout_len=100, algo="ppo", pi_lr=3e-3, vf_lr=3e-3,
+                            train_vf_iters=10, train_pi_iters=10, num_threads=4, seed=0, overlap=True)
+    tr = HostVecTrainer(cfg, device=cuda)
+    best = 0.0
+    for _ in range(40):
+        tr.train_epoch()
+        m = tr.metrics()
+        if m["Episodes"]:
+            best = max(best, m["AverageEpRet"])
+        if best > 150:
+            break
+    tr.finish()
+    assert best > 150, best
