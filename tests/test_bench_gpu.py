@@ -61,3 +61,22 @@ def test_bench_two_ranks_gloo_shared_gpu(cuda):
     assert rec["config"]["parallelism"] == "dp2"
     assert rec["config"]["global_batch"] == 2 * 1024 * 64  # weak scaling: per-rank envs fixed
     assert "time_to_threshold_s" not in rec
+
+
+def test_bench_two_rccl_ranks(cuda):
+    """``bench.py --gpus 2`` without a launcher: it starts torch.distributed.run itself, one
+    rank per GPU over RCCL (the driver's scaling run).  Needs two visible GPUs."""
+    import torch
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs >= 2 GPUs (the 1-GPU box rehearses the rank logic over gloo above)")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("RRL_DIST_BACKEND", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--num-envs",
+                        "2048", "--vf-iters", "4"], cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = _json_lines(r.stdout)
+    assert len(recs) == 1
+    rec = recs[0]
+    assert rec["n_gpus"] == 2 and rec["backend"] == "nccl" and rec["rccl_world"] == 2
+    assert rec["config"]["parallelism"] == "dp2" and len(rec["per_rank_env_steps_per_s"]) == 2
