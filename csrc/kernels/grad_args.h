@@ -34,10 +34,11 @@ struct GradArgs {
 };
 
 // Weight-stationary bf16x6 gradient kernels (value_grad.hip): value head for H = 128,
-// D <= 24; 2-action categorical policy heads (PG / PPO) for H = 128, D <= 8.
+// D <= 24; categorical policy heads (PG / PPO) for H = 128, D <= 8, A = 2..4; Gaussian
+// policy heads for H = 128, D <= 20, A = 1 or 6.
 bool value_grad_split_supported(int D, int H);
 int launch_value_grad_split(const GradArgs& a, int grid, hipStream_t s);
-bool policy_grad_split_supported(int D, int H, int A);
+bool policy_grad_split_supported(int D, int H, int A, int head);
 int launch_policy_grad_split(const GradArgs& a, int head, int grid, hipStream_t s);
 
 }  // namespace rrl

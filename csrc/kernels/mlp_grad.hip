@@ -478,9 +478,9 @@ static int dispatch_head(int head, const GradArgs& a, int grid, hipStream_t s) {
   return -1;
 }
 
-// Value-MSE and 2-action categorical policy gradient path: 1 = weight-stationary bf16x6 kernels
-// (value_grad.hip) where they apply (value: H = 128, D <= 24; policy: H = 128, D <= 8, A = 2),
-// 0 = the fp32-MFMA kernel above for every shape.
+// Value-MSE and policy gradient path: 1 = weight-stationary bf16x6 kernels (value_grad.hip)
+// where they apply (value: H = 128, D <= 24; categorical: D <= 8, A = 2..4; Gaussian: D <= 24,
+// A = 1 or 6), 0 = the fp32-MFMA kernel above for every shape.
 static int g_value_grad_mode = 1;
 extern "C" int rrl_set_value_grad_mode(int mode) {
   const int old = g_value_grad_mode;
@@ -509,7 +509,7 @@ extern "C" int rrl_mlp_grad(int head, const float* params, const float* X, int B
   hipStream_t s = (hipStream_t)stream;
   if (head == HEAD_VALUE_MSE && g_value_grad_mode == 1 && value_grad_split_supported(D, H))
     return launch_value_grad_split(a, grid, s);
-  if ((head == HEAD_PG_CAT || head == HEAD_PPO_CAT) && g_value_grad_mode == 1 && policy_grad_split_supported(D, H, A))
+  if (head != HEAD_VALUE_MSE && g_value_grad_mode == 1 && policy_grad_split_supported(D, H, A, head))
     return launch_policy_grad_split(a, head, grid, s);
   const int DT = (D <= 16) ? 1 : 2;
   if (H == 128) return DT == 1 ? dispatch_head<1, 8>(head, a, grid, s) : dispatch_head<2, 8>(head, a, grid, s);

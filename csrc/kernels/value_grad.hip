@@ -20,16 +20,17 @@
 //     wB = W2[all 128][own cols]^T   (backward dh1 = W2^T dh2)
 // (hi + mid pieces in registers; the lo pieces of W2 sit in one LDS image [o][i] that
 // both fragment kinds read once per 32-wide k-chunk).  Activations cross waves through LDS
-// as pre-split bf16 images [64 batch][128 feature] (row stride 144 elements: conflict-free
-// b128 reads and transposed reads):
+// as pre-split bf16 images [64 batch][128 feature] (row stride 144 elements with an XOR
+// chunk swizzle: conflict-free b128 reads and transposed reads, 2-way stores):
 //     h1 image  -> B operand of the forward (b128) and of dW2 (ds_read_b64_tr_b16)
 //     dh2 image -> B operand of dh1 (b128) and A operand of dW2 (transposed)
 // Each MFMA loop loads the next step's fragment before issuing the current step's six
 // MFMAs.  dW2 for the wave's 16 rows accumulates in registers across all slabs; layer 1
 // (K = D <= 24) is DP / 4 fp32 MFMA k-steps; dW1 / dW3 / biases are VALU outer products
 // folded over the 16 batch lanes once per slab by a DPP reduce-scatter (lane j keeps entry
-// j), which keeps their accumulators at one register each.  The value head's dot product
-// is reduced over the 8 waves through LDS.  4 workgroup barriers per slab.
+// j), which keeps their accumulators at one register each.  The head's NA dot products are
+// reduced over the 8 waves through LDS.  4 workgroup barriers per slab.  The same body serves
+// the value step and the policy steps (categorical and Gaussian heads, PG and PPO).
 //
 // Measured (tools/kbench.py grad, B = 2,097,152 rows, CartPole D = 4): 1.06 ms vs 1.91 ms for
 // the fp32-MFMA kernel.  A ds_bpermute-based reduce-scatter gave run-to-run different dW1
@@ -49,17 +50,27 @@ constexpr int kVgH = 128;
 constexpr int kVgLd = 144;          // bf16 row stride of the activation images
 constexpr int kVgImg = 64 * kVgLd;  // elements per image piece
 // LDS: h1 + dh2 images (3 pieces each), head partials [8 waves][NA][64], x slabs [2][64][DP],
-// b1 / b2 / w3[NA], then the W2 lo image; DP = 24 (D <= 24) with the value head (NA = 1) uses
-// 163,328 of the 163,840 bytes; the 2-action policy heads (NA = 2) take DP <= 8.
-constexpr int vg_wlo_bytes(int DP, int NA) {
-  return 6 * kVgImg * 2 + 8 * 64 * NA * 4 + 2 * 64 * DP * 4 + (2 + NA) * 128 * 4;
+// b1 / b2 / w3[NA], then the W2 lo image.  When the head partials do not fit beside the rest
+// (Gaussian NA = 6 at DP >= 20) they live inside the dh2 image, which is free from the start
+// of a slab until its dh2 stores -- one extra barrier orders their last read before those.
+constexpr int vg_red_bytes(int NA) { return 8 * 64 * NA * 4; }
+constexpr int vg_base_bytes(int DP, int NA) {
+  return 6 * kVgImg * 2 + 2 * 64 * DP * 4 + (2 + NA) * 128 * 4 + 32 * 4 + kVgH * kVgLd * 2;
 }
-constexpr int vg_lds_bytes(int DP, int NA) { return vg_wlo_bytes(DP, NA) + kVgH * kVgLd * 2; }
-static_assert(vg_lds_bytes(24, 1) <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
-static_assert(vg_lds_bytes(8, 2) <= 160 * 1024, "policy-grad LDS plan exceeds 160 KB");
+constexpr bool vg_red_in_image(int DP, int NA) { return vg_base_bytes(DP, NA) + vg_red_bytes(NA) > 160 * 1024; }
+constexpr int vg_lds_bytes(int DP, int NA) {
+  return vg_base_bytes(DP, NA) + (vg_red_in_image(DP, NA) ? 0 : vg_red_bytes(NA));
+}
+static_assert(vg_lds_bytes(24, 1) <= 160 * 1024 && !vg_red_in_image(24, 1), "value-grad LDS plan");
+static_assert(vg_lds_bytes(20, 6) <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
+static_assert(vg_red_bytes(6) <= 3 * kVgImg * 2, "head partials must fit in the dh2 image");
 
 struct Split8 {
   vbf16x8 h, m, l;
+};
+
+struct Split8HM {  // hi + mid pieces (the lo piece of a stationary weight fragment lives in LDS)
+  vbf16x8 h, m;
 };
 
 typedef float vf32x2 __attribute__((ext_vector_type(2)));
@@ -106,9 +117,6 @@ RRL_DEV Split8 split8(const floatx4 v0, const floatx4 v1) {
   return s;
 }
 
-struct Split8HM {  // hi + mid pieces (the lo piece of a stationary weight fragment lives in LDS)
-  vbf16x8 h, m;
-};
 
 RRL_DEV floatx4 mfma_bf16(vbf16x8 a, vbf16x8 b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -140,6 +148,10 @@ RRL_DEV float group_sum_swap(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// Sum over the whole wave on the VALU (DPP within 16-lane rows, lane swaps across rows):
+// every lane gets the total; wave-uniform call sites only.
+RRL_DEV float wave_sum_vl(float v);
+
 // 8 consecutive features of batch row `row` (b128 read of each piece).
 RRL_DEV Split8 frag_row(const uint16_t* img, int row, int col) {
   Split8 s;
@@ -163,7 +175,7 @@ RRL_DEV vbf16x8 frag_tr1(const uint16_t* img, int k0, int col0, int lane) {
   const vs16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(vbf16x8, v);
 }
-// Rows k0 .. k0 + 7 of column col0 + (lane & 15) of a [k][col] image (k0 includes 8g).
+// Rows k0 .. k0 + 7 of column col0 + (lane & 15) of a plain [k][col] image (k0 includes 8g).
 RRL_DEV vbf16x8 frag_tr8(const uint16_t* img, int k0, int col0, int lane) {
   typedef __attribute__((address_space(3))) vs16x4 lds_v4;
   const int q = (lane >> 2) & 3, pp = lane & 3;
@@ -231,9 +243,18 @@ RRL_DEV float reduce_scatter16(const float (&v)[16], int j) {
   return keep + dpp_f<kDppXor1>(send);
 }
 
-// HEAD: HEAD_VALUE_MSE (one output) or a 2-action categorical policy head (HEAD_PG_CAT /
-// HEAD_PPO_CAT, the CartPole policy step): the same three 128x128 products, only the head
-// (NA outputs reduced over the 8 waves, loss gradient, dW3 / db3 rows) differs.
+RRL_DEV float wave_sum_vl(float v) {
+  v += dpp_f<kDppXor1>(v);
+  v += dpp_f<kDppXor2>(v);
+  v += dpp_f<kDppMirror8>(v);
+  v += dpp_f<kDppXor8>(v);
+  return group_sum_swap(v);
+}
+
+// HEAD: HEAD_VALUE_MSE (one output), a categorical policy head (HEAD_PG_CAT / HEAD_PPO_CAT,
+// NA = 2..4 actions) or a diagonal-Gaussian policy head (HEAD_PG_GAUSS / HEAD_PPO_GAUSS, NA
+// action dims, state-independent log_std): the same three 128x128 products, only the head
+// (NA outputs reduced over the 8 waves, loss gradient, dW3 / db3 / dlog_std) differs.
 // Diagnostic in-kernel stamps (STAMP = true builds only, tools/kbench.py --stamps): per-wave
 // cycle sums of the slab's segments, written to p.stamps; never part of a timed run.
 #define VG_STAMP(k)                                                                     \
@@ -242,21 +263,31 @@ RRL_DEV float reduce_scatter16(const float (&v)[16], int j) {
     unsigned long long t_;                                                              \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");          \
     __builtin_amdgcn_sched_barrier(0);                                                  \
-    if ((k) > 0) st_sum[(k)-1] += t_ - st_prev;                                         \
+    if ((k) > 0) st_sum[(k) > 0 ? (k)-1 : 0] += t_ - st_prev;                           \
     st_prev = t_;                                                                       \
   }
 
-template <int DP, int HEAD, bool STAMP = false>
+template <int DP, int HEAD, int NA, bool STAMP = false>
 __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   unsigned long long st_prev = 0, st_sum[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   extern __shared__ __attribute__((aligned(16))) uint16_t vg_lds[];
   constexpr bool kValue = HEAD == HEAD_VALUE_MSE;
-  constexpr int NA = kValue ? 1 : 2;
+  constexpr bool kGauss = HEAD == HEAD_PG_GAUSS || HEAD == HEAD_PPO_GAUSS;
+  constexpr bool kPPO = HEAD == HEAD_PPO_CAT || HEAD == HEAD_PPO_GAUSS;
+  static_assert(!kValue || NA == 1, "the value head has one output");
+  static_assert(NA >= 1 && NA <= 6, "NA <= 6 (LDS plan, two field groups)");
+  // batch-summed 4-feature fields of the head / bias gradients, folded over the 16 batch
+  // lanes by the DPP reduce-scatter: field 0 db2, 1 dW3 row 0, 2 db1, 3 dW3 row 1, 4.. rows 2..
+  constexpr int NF = NA + 2;
+  constexpr int NG = (NF + 3) / 4;  // 16-slot groups (one register each)
+  constexpr bool kRedImg = vg_red_in_image(DP, NA);
   uint16_t* h1img = vg_lds;
   uint16_t* dhimg = vg_lds + 3 * kVgImg;
-  float* red = reinterpret_cast<float*>(vg_lds + 6 * kVgImg);  // [8 waves][NA][64 rows]
-  float* xsb = red + 8 * NA * 64;                                // [2][64 rows][DP]
-  float* vecs = xsb + 2 * 64 * DP;                               // b1[128] b2[128] w3[NA][128]
+  float* tail = reinterpret_cast<float*>(vg_lds + 6 * kVgImg);
+  float* red = kRedImg ? reinterpret_cast<float*>(dhimg) : tail;  // [8 waves][NA][64 rows]
+  float* xsb = kRedImg ? tail : tail + 8 * NA * 64;                // [2][64 rows][DP]
+  float* vecs = xsb + 2 * 64 * DP;                                 // b1[128] b2[128] w3[NA][128]
+  uint16_t* w2lo = reinterpret_cast<uint16_t*>(vecs + (2 + NA) * kVgH + 32);  // [128][kVgLd]
   int parity = 0;
   constexpr int KS1 = DP / 4;
   const int l = lane_id();
@@ -295,7 +326,6 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     wB[c].h = sb.h;
     wB[c].m = sb.m;
   }
-  uint16_t* w2lo = vg_lds + vg_wlo_bytes(DP, NA) / 2;
   for (int q = threadIdx.x; q < kVgH * kVgH / 4; q += blockDim.x) {
     floatx4 v;
 #pragma unroll
@@ -314,34 +344,45 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     const int k = q >> 7, f = q & (kVgH - 1);
     vecs[q] = P[(k == 0 ? o.b1 : k == 1 ? o.b2 : o.w3 + (k - 2) * kVgH) + f];
   }
-  float b3[NA];
-#pragma unroll
-  for (int a = 0; a < NA; ++a) b3[a] = P[o.b3 + a];
-  // per C-layout row own + 4g + r (re-read from LDS where used: registers are the limit)
+  // head scalars b3[NA], log_std[NA], 1/std[NA] in LDS after w3 (read once per slab by the head)
+  float* hsc = vecs + (2 + NA) * kVgH;
+  if (threadIdx.x < NA) {
+    const int a = threadIdx.x;
+    const float lsa = kGauss ? P[o.log_std + a] : 0.f;
+    hsc[a] = P[o.b3 + a];
+    hsc[NA + a] = lsa;
+    hsc[2 * NA + a] = __expf(-lsa);
+  }
+  // per C-layout row own + 4g + r (re-read from LDS where used)
   const float* b1p = vecs + own + 4 * g;
   const float* b2p = vecs + kVgH + own + 4 * g;
   const float* w3p = vecs + 2 * kVgH + own + 4 * g;
 
   floatx4 acc2[8];
-  float accv = 0.f;  // entry j of [db2 | dW3 row 0 | db1 | dW3 row 1 (NA = 2)] (4 features each), batch-summed
+  float accv[NG];      // slot j of each 16-slot group of fields (4 features each), batch-summed
   float acc1[DP / 4];  // dW1[own + 4g + (j & 3)][4 d4 + (j >> 2)], summed over the batch lanes
 #pragma unroll
   for (int it = 0; it < 8; ++it) acc2[it] = zero4();
 #pragma unroll
-  for (int d4 = 0; d4 < DP / 4; ++d4) acc1[d4] = 0.f;
-  float bacc3[NA];
+  for (int q = 0; q < NG; ++q) accv[q] = 0.f;
 #pragma unroll
-  for (int a = 0; a < NA; ++a) bacc3[a] = 0.f;
+  for (int d4 = 0; d4 < DP / 4; ++d4) acc1[d4] = 0.f;
+  // db3 / dlog_std: wave w owns output a = w (NA <= 8 waves) and keeps its batch sum in one
+  // wave-uniform register, folded over the 64 rows of every slab on the VALU
+  float bacc3 = 0.f, dls = 0.f;
   float s_loss = 0.f, s_val = 0.f, s_cnt = 0.f, s_ent = 0.f, s_kl = 0.f, s_clip = 0.f;
 
-  // Per-slab global inputs are prefetched ONE SLAB AHEAD into registers (issue early, write
+  // Per-slab global inputs are prefetched one slab ahead into registers (issue early, write
   // late): the x slab (XQ values per thread) and this lane's head inputs for its 4 batch rows
-  // 16 bt + j (ret, or adv / act / logp_old).  Their HBM latency hides under a whole slab of
-  // MFMA work instead of stalling the slab's first barrier and the head.
+  // 16 bt + j (ret; or adv / act / logp_old, and the NA action values of a Gaussian head).
+  // The next slab's loads are issued right after this slab's head consumed the current
+  // ones, so their latency hides under the backward MFMA work.
   constexpr int XQ = (64 * DP + 511) / 512;
+  constexpr int NC = kGauss ? NA : 1;
   float xr[XQ];
-  float hin[4], hlp[4];  // ret (value) or adv (policy); logp_old
-  int hact[4];
+  float hin, hlp;  // this lane's row: ret (value) or adv (policy); logp_old
+  int hact;
+  float hac[NC];   // Gaussian action
   auto prefetch = [&](int b0) {
 #pragma unroll
     for (int i = 0; i < XQ; ++i) {
@@ -350,15 +391,17 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       const float v = p.X[(size_t)min(b, p.B - 1) * D + min(d, D - 1)];
       xr[i] = (b < p.B && d < D) ? v : 0.f;
     }
+    const int bc = min(b0 + l, p.B - 1);  // lane l handles batch row l of the slab in the head
+    if (kValue) {
+      hin = p.ret[bc];
+    } else {
+      hin = p.adv[bc];
+      hlp = p.logp_old ? p.logp_old[bc] : 0.f;
+      if (kGauss) {
 #pragma unroll
-    for (int bt = 0; bt < 4; ++bt) {
-      const int bc = min(b0 + 16 * bt + j, p.B - 1);
-      if (kValue) {
-        hin[bt] = p.ret[bc];
+        for (int a = 0; a < NC; ++a) hac[a] = p.actc[(size_t)bc * NA + a];
       } else {
-        hin[bt] = p.adv[bc];
-        hact[bt] = p.act[bc];
-        hlp[bt] = p.logp_old ? p.logp_old[bc] : 0.f;
+        hact = p.act[bc];
       }
     }
   };
@@ -377,15 +420,6 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       const int q = (int)threadIdx.x + 512 * i;
       if (q < 64 * DP) xs[q] = xr[i];
     }
-    float cin[4], clp[4];
-    int cact[4];
-#pragma unroll
-    for (int bt = 0; bt < 4; ++bt) {
-      cin[bt] = hin[bt];
-      clp[bt] = hlp[bt];
-      cact[bt] = hact[bt];
-    }
-    if (base + (int)gridDim.x * 64 < p.B) prefetch(base + gridDim.x * 64);
     __syncthreads();  // x visible; the previous slab's readers of both images are done
     VG_STAMP(1);
 
@@ -438,108 +472,178 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 
     VG_STAMP(3);
     // ------------------------------------------------------------ head
-    floatx4 w3v[NA];
+    // partial dot products over this wave's 16 features -> LDS, reduced over the 8 waves
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
-      w3v[a] = *reinterpret_cast<const floatx4*>(w3p + a * kVgH);
+      const floatx4 w3a = *reinterpret_cast<const floatx4*>(w3p + a * kVgH);
 #pragma unroll
       for (int bt = 0; bt < 4; ++bt) {
-        float pv = w3v[a][0] * h2[bt][0];
-        pv = fmaf(w3v[a][1], h2[bt][1], pv);
-        pv = fmaf(w3v[a][2], h2[bt][2], pv);
-        pv = fmaf(w3v[a][3], h2[bt][3], pv);
+        float pv = w3a[0] * h2[bt][0];
+        pv = fmaf(w3a[1], h2[bt][1], pv);
+        pv = fmaf(w3a[2], h2[bt][2], pv);
+        pv = fmaf(w3a[3], h2[bt][3], pv);
         pv = group_sum_swap(pv);
         if (g == bt) red[(w * NA + a) * 64 + 16 * bt + j] = pv;
       }
+      if (NA > 2) __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
-    float dout[4][NA];
-#pragma unroll
-    for (int bt = 0; bt < 4; ++bt) {
-      const int rl = 16 * bt + j, b = base + rl;
+    // loss head: lane l handles batch row l (every wave computes the same 64 rows; wave 0's
+    // lanes count each row once in the batch statistics and the head gradient sums)
+    const bool lead = w == 0;
+    float dout[NA];
+    float dls_row[kGauss ? NA : 1];  // this row's dLoss/dlog_std terms (Gaussian heads)
+    {
+      const int b = base + l;
       const bool ok = b < p.B;
       const int bc = min(b, p.B - 1);
       float outv[NA];
 #pragma unroll
       for (int a = 0; a < NA; ++a) {
-        const float* r = red + a * 64 + rl;
+        const float* r = red + a * 64 + l;
         constexpr int S = NA * 64;  // wave stride
-        outv[a] = (((r[0] + r[S]) + (r[2 * S] + r[3 * S])) + ((r[4 * S] + r[5 * S]) + (r[6 * S] + r[7 * S]))) + b3[a];
+        outv[a] = (((r[0] + r[S]) + (r[2 * S] + r[3 * S])) + ((r[4 * S] + r[5 * S]) + (r[6 * S] + r[7 * S]))) + hsc[a];
       }
       if (kValue) {
         const float v = outv[0];
-        const float diff = v - (ok ? cin[bt] : 0.f);
-        dout[bt][0] = ok ? 2.f * diff * p.inv_B : 0.f;
-        if (w == 0 && g == 0 && ok) {
+        const float diff = v - (ok ? hin : 0.f);
+        dout[0] = ok ? 2.f * diff * p.inv_B : 0.f;
+        if (lead && ok) {
           s_loss += diff * diff;
           s_val += v;
           s_cnt += 1.f;
         }
       } else {
-        // categorical policy head (mlp_grad.hip HEAD_PG_CAT / HEAD_PPO_CAT, REINFORCE.py:141-152)
+        // policy heads (mlp_grad.hip HEAD_PG_* / HEAD_PPO_*, REINFORCE.py:141-152)
+        const float adv = ((ok ? hin : 0.f) - adv_mean) * adv_rstd;
+        float logp = 0.f, ent = 0.f;
         float logits[kMaxAct];
+        CatStats cs{0.f, 0.f};
+        int act = 0;
+        if (kGauss) {
 #pragma unroll
-        for (int a = 0; a < kMaxAct; ++a) logits[a] = a < NA ? outv[a] : -INFINITY;
-        if (ok) apply_mask(p.mask ? p.mask + (size_t)bc * NA : nullptr, NA, logits);
-        const CatStats cs = cat_stats(NA, logits);
-        const int act = ok ? cact[bt] : 0;
-        const float logp = pick_logit(NA, logits, act) - cs.lse;
-        const float adv = ((ok ? cin[bt] : 0.f) - adv_mean) * adv_rstd;
+          for (int a = 0; a < NA; ++a) {
+            const float xa = ok ? hac[a % NC] : outv[a];
+            const float z = (xa - outv[a]) * hsc[2 * NA + a];
+            logp += -0.5f * z * z - hsc[NA + a] - kHalfLog2Pi;
+            ent += 0.5f + kHalfLog2Pi + hsc[NA + a];
+          }
+        } else {
+#pragma unroll
+          for (int a = 0; a < kMaxAct; ++a) logits[a] = a < NA ? outv[a] : -INFINITY;
+          if (ok) apply_mask(p.mask ? p.mask + (size_t)bc * NA : nullptr, NA, logits);
+          cs = cat_stats(NA, logits);
+          act = ok ? hact : 0;
+          logp = pick_logit(NA, logits, act) - cs.lse;
+          ent = cs.entropy;
+        }
         float dlogp, loss_i;
-        if (HEAD == HEAD_PG_CAT) {
+        if (!kPPO) {
           dlogp = -adv;
           loss_i = -logp * adv;
         } else {
-          const float lpo = (ok && p.logp_old) ? clp[bt] : logp;
+          const float lpo = (ok && p.logp_old) ? hlp : logp;
           const float ratio = __expf(logp - lpo);
           const float s1 = ratio * adv;
           const float s2 = fminf(fmaxf(ratio, 1.f - p.clip_eps), 1.f + p.clip_eps) * adv;
           dlogp = (s1 <= s2) ? -adv * ratio : 0.f;
           loss_i = -fminf(s1, s2);
-          if (w == 0 && g == 0 && ok) s_clip += (fabsf(ratio - 1.f) > p.clip_eps) ? 1.f : 0.f;
+          if (lead && ok) s_clip += (fabsf(ratio - 1.f) > p.clip_eps) ? 1.f : 0.f;
         }
         const float scale = ok ? p.inv_B : 0.f;
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
-          const float lpa = logits[a] - cs.lse;
-          const float pa = __expf(lpa);
-          const float dpg = dlogp * ((a == act ? 1.f : 0.f) - pa);
-          const float dent = pa > 0.f ? p.ent_coef * pa * (lpa + cs.entropy) : 0.f;
-          dout[bt][a] = scale * (dpg + dent);
+          if (kGauss) {
+            // dlogp/dmu = d / var ; dlogp/dlog_std = d^2 / var - 1 ; dH/dlog_std = 1
+            const float d = (ok ? hac[a % NC] : outv[a]) - outv[a];
+            const float iv = hsc[2 * NA + a] * hsc[2 * NA + a];
+            dout[a] = scale * dlogp * d * iv;
+            dls_row[a % NC] = scale * (dlogp * (d * d * iv - 1.f) - p.ent_coef);
+          } else {
+            const float lpa = logits[a] - cs.lse;
+            const float pa = __expf(lpa);
+            const float dpg = dlogp * ((a == act ? 1.f : 0.f) - pa);
+            const float dent = pa > 0.f ? p.ent_coef * pa * (lpa + cs.entropy) : 0.f;
+            dout[a] = scale * (dpg + dent);
+          }
         }
-        if (w == 0 && g == 0 && ok) {
+        if (lead && ok) {
           s_loss += loss_i;
-          s_ent += cs.entropy;
-          if (p.logp_old) s_kl += clp[bt] - logp;
+          s_ent += ent;
+          if (p.logp_old) s_kl += hlp - logp;
           s_cnt += 1.f;
         }
       }
-      if (w == 0 && g == 0) {
+      float mb = 0.f, ml = 0.f;  // this wave's output
 #pragma unroll
-        for (int a = 0; a < NA; ++a) bacc3[a] += dout[bt][a];
+      for (int a = 0; a < NA; ++a) {
+        if (a == w) {
+          mb = dout[a];
+          if (kGauss) ml = dls_row[a % NC];
+        }
+      }
+      if (w < NA) {  // wave-uniform
+        bacc3 += wave_sum_vl(mb);
+        if (kGauss) dls += wave_sum_vl(ml);
       }
     }
+    // the head consumed this slab's inputs: issue the next slab's loads now
+    if (base + (int)gridDim.x * 64 < p.B) prefetch(base + gridDim.x * 64);
+    if (kRedImg) __syncthreads();  // every wave read the partials before dh2 overwrites them
 
     VG_STAMP(4);
     // ------------------------------------------------------------ dh2, dW3, db2
-    float tv[16];  // this slab's [db2 | dW3 row 0 | db1 | dW3 row 1] partials of features own + 4g + r
+    // dout of batch row 16 bt + j comes from lane 16 bt + j (ds_bpermute, no barrier).  Field
+    // group 0 (db2, dW3 rows 0 / 1) is folded first; the rows of outputs 2.. (group 1) in a
+    // second pass, so only 16 partials are live at a time.
+    floatx4 dd[4];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) tv[q] = 0.f;
+    for (int bt = 0; bt < 4; ++bt) dd[bt] = zero4();
+    {
+      float tv[16];  // this slab's field partials of features own + 4g + r
 #pragma unroll
-    for (int bt = 0; bt < 4; ++bt) {
-      floatx4 d;
+      for (int e = 0; e < 16; ++e) tv[e] = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float s3 = w3v[0][r] * dout[bt][0];
-        if (NA == 2) s3 = fmaf(w3v[NA - 1][r], dout[bt][NA - 1], s3);
-        d[r] = h2[bt][r] > 0.f ? s3 : 0.f;
-        tv[r] += d[r];
-        tv[4 + r] = fmaf(dout[bt][0], h2[bt][r], tv[4 + r]);
-        if (NA == 2) tv[12 + r] = fmaf(dout[bt][NA - 1], h2[bt][r], tv[12 + r]);
+      for (int a = 0; a < NA; ++a) {
+        const floatx4 w3a = *reinterpret_cast<const floatx4*>(w3p + a * kVgH);
+        const int f = a == 0 ? 1 : 3;
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {
+          const float v = __shfl(dout[a], 16 * bt + j, 64);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dd[bt][r] = fmaf(w3a[r], v, dd[bt][r]);
+            if (a < 2) tv[4 * f + r] = fmaf(v, h2[bt][r], tv[4 * f + r]);
+          }
+        }
       }
-      store_split(dhimg, 16 * bt + j, own + 4 * g, d);
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dd[bt][r] = h2[bt][r] > 0.f ? dd[bt][r] : 0.f;
+          tv[r] += dd[bt][r];
+        }
+        store_split(dhimg, 16 * bt + j, own + 4 * g, dd[bt]);
+      }
+      accv[0] += reduce_scatter16(tv, j);
     }
-    accv += reduce_scatter16(tv, j);
+    if (NA > 2) {
+      float tv[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) tv[e] = 0.f;
+#pragma unroll
+      for (int a = 2; a < NA; ++a) {
+        const int f = a + 2;  // fields 4 .. NA + 1 -> group 1 (NA <= 6)
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {
+          const float v = __shfl(dout[a], 16 * bt + j, 64);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) tv[4 * (f & 3) + r] = fmaf(v, h2[bt][r], tv[4 * (f & 3) + r]);
+        }
+      }
+      accv[1] += reduce_scatter16(tv, j);
+    }
     __syncthreads();
 
     VG_STAMP(5);
@@ -547,7 +651,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     floatx4 dh1[4];
 #pragma unroll
     for (int bt = 0; bt < 4; ++bt) dh1[bt] = zero4();
-    float tb[16];  // db1 partials in entries 8..11 (the rest stay zero)
+    float tb[16];  // db1 partials in entries 8..11 (field 2; the rest stay zero)
 #pragma unroll
     for (int q = 0; q < 16; ++q) tb[q] = 0.f;
     {
@@ -576,7 +680,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       }
     }
     VG_STAMP(6);
-    accv += reduce_scatter16(tb, j);
+    accv[0] += reduce_scatter16(tb, j);
     // dW1 one group of 4 input columns at a time (16 partials live, whatever D is), each
     // folded over the 16 batch lanes right away: lane j keeps entry j
 #pragma unroll
@@ -603,7 +707,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       Split8 cur = frag_tr(h1img, 0, 0, l);
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
-        const int kc = it >> 3, t = it & 7;
+        const int t = it & 7;
         Split8 nxt, an;
         if (it + 1 < 16) nxt = frag_tr(h1img, 32 * ((it + 1) >> 3), 16 * ((it + 1) & 7), l);
         if (it == 7) an = frag_tr(dhimg, 32, own, l);
@@ -611,11 +715,9 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         __builtin_amdgcn_sched_barrier(0);
         if (it + 1 < 16) cur = nxt;
         if (it == 7) a = an;
-        (void)kc;
       }
     }
     VG_STAMP(8);
-    if (STAMP) st_sum[8] += 0;
   }
   if (STAMP && p.stamps != nullptr && l == 0) {
 #pragma unroll
@@ -629,82 +731,126 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) slab[o.w2 + (own + 4 * g + r) * kVgH + 16 * it + j] = acc2[it][r];
   }
-  {
-    const int f = own + 4 * g + (j & 3), k = j >> 2;
-    if (k < 3) slab[(k == 0 ? o.b2 : k == 1 ? o.w3 : o.b1) + f] = accv;
-    if (NA == 2 && k == 3) slab[o.w3 + kVgH + f] = accv;
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    const int f = 4 * q + (j >> 2), feat = own + 4 * g + (j & 3);
+    if (f < NF) {
+      const int off = f == 0 ? o.b2 : f == 1 ? o.w3 : f == 2 ? o.b1 : o.w3 + (f == 3 ? 1 : f - 2) * kVgH;
+      slab[off + feat] = accv[q];
+    }
   }
 #pragma unroll
   for (int d4 = 0; d4 < DP / 4; ++d4) {
     const int f = own + 4 * g + (j & 3), dd = 4 * d4 + (j >> 2);
     if (dd < D) slab[o.w1 + f * D + dd] = acc1[d4];
   }
+  if (w < NA && l == 0) {
+    slab[o.b3 + w] = bacc3;
+    if (kGauss) slab[o.log_std + w] = dls;
+  }
   if (w == 0) {
-    float vb3[NA];
-#pragma unroll
-    for (int a = 0; a < NA; ++a) vb3[a] = wave_sum(bacc3[a]);
     const float sl = wave_sum(s_loss), sv = wave_sum(s_val), sc = wave_sum(s_cnt);
     const float se = wave_sum(s_ent), sk = wave_sum(s_kl), scl = wave_sum(s_clip);
     if (l == 0) {
-#pragma unroll
-      for (int a = 0; a < NA; ++a) slab[o.b3 + a] = vb3[a];
-      float* ls = p.loss_slab + blockIdx.x * 8;
-      ls[0] = sl;
-      ls[1] = se;
-      ls[2] = sk;
-      ls[3] = scl;
-      ls[4] = sv;
-      ls[5] = sc;
+      float* lsl = p.loss_slab + blockIdx.x * 8;
+      lsl[0] = sl;
+      lsl[1] = se;
+      lsl[2] = sk;
+      lsl[3] = scl;
+      lsl[4] = sv;
+      lsl[5] = sc;
     }
   }
 }
 
 bool value_grad_split_supported(int D, int H) { return H == kVgH && D >= 1 && D <= 24; }
-bool policy_grad_split_supported(int D, int H, int A) { return H == kVgH && D >= 1 && D <= 8 && A == 2; }
+
+// (head, A, D) combinations with a bf16x6 instance (the rest run the fp32-MFMA mlp_grad kernel)
+bool policy_grad_split_supported(int D, int H, int A, int head) {
+  if (H != kVgH || D < 1) return false;
+  if (head == HEAD_PG_CAT || head == HEAD_PPO_CAT) return D <= 8 && A >= 2 && A <= 4;
+  if (head == HEAD_PG_GAUSS || head == HEAD_PPO_GAUSS) return D <= 20 && (A == 1 || A == 6);
+  return false;
+}
 
 static int g_vg_tune = 0;  // scheduling experiments (bit 0: waves 4-7 at prio 1, bit 1: waves 0-3, bit 3: stamps)
 static unsigned long long* g_vg_stamps = nullptr;
 
-template <int DP, int HEAD>
+template <int DP, int HEAD, int NA>
 static int launch_vg(const GradArgs& a0, int grid, hipStream_t s) {
   GradArgs a = a0;
   a.tune = g_vg_tune;
   a.stamps = g_vg_stamps;
-  constexpr int NA = HEAD == HEAD_VALUE_MSE ? 1 : 2;
+  constexpr int bytes = vg_lds_bytes(DP, NA);
+  static_assert(bytes <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP, HEAD>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, vg_lds_bytes(DP, NA));
+    (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP, HEAD, NA>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     attr_set = true;
   }
   if (a.tune & 8) {  // diagnostic stamps build
     static bool attr_st = false;
     if (!attr_st) {
-      (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP, HEAD, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, vg_lds_bytes(DP, NA));
+      (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP, HEAD, NA, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
       attr_st = true;
     }
-    hipLaunchKernelGGL((value_grad_split_kernel<DP, HEAD, true>), dim3(grid), dim3(512), vg_lds_bytes(DP, NA), s, a);
+    hipLaunchKernelGGL((value_grad_split_kernel<DP, HEAD, NA, true>), dim3(grid), dim3(512), bytes, s, a);
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL((value_grad_split_kernel<DP, HEAD>), dim3(grid), dim3(512), vg_lds_bytes(DP, NA), s, a);
+  hipLaunchKernelGGL((value_grad_split_kernel<DP, HEAD, NA>), dim3(grid), dim3(512), bytes, s, a);
   return (int)hipGetLastError();
 }
 
 int launch_value_grad_split(const GradArgs& a, int grid, hipStream_t s) {
-  if (a.D <= 4) return launch_vg<4, HEAD_VALUE_MSE>(a, grid, s);
-  if (a.D <= 8) return launch_vg<8, HEAD_VALUE_MSE>(a, grid, s);
-  if (a.D <= 16) return launch_vg<16, HEAD_VALUE_MSE>(a, grid, s);
-  if (a.D <= 20) return launch_vg<20, HEAD_VALUE_MSE>(a, grid, s);  // HalfCheetahSynth (D = 17)
-  return launch_vg<24, HEAD_VALUE_MSE>(a, grid, s);
+  if (a.D <= 4) return launch_vg<4, HEAD_VALUE_MSE, 1>(a, grid, s);
+  if (a.D <= 8) return launch_vg<8, HEAD_VALUE_MSE, 1>(a, grid, s);
+  if (a.D <= 16) return launch_vg<16, HEAD_VALUE_MSE, 1>(a, grid, s);
+  if (a.D <= 20) return launch_vg<20, HEAD_VALUE_MSE, 1>(a, grid, s);  // HalfCheetahSynth (D = 17)
+  return launch_vg<24, HEAD_VALUE_MSE, 1>(a, grid, s);
 }
 
-// 2-action categorical policy step (CartPole: REINFORCE / A2C / PPO policy gradient).
+template <int HEAD, int NA>
+static int launch_cat(const GradArgs& a, int grid, hipStream_t s) {
+  return a.D <= 4 ? launch_vg<4, HEAD, NA>(a, grid, s) : launch_vg<8, HEAD, NA>(a, grid, s);
+}
+
+template <int HEAD>
+static int launch_cat_a(const GradArgs& a, int grid, hipStream_t s) {
+  switch (a.A) {
+    case 2: return launch_cat<HEAD, 2>(a, grid, s);  // CartPole
+    case 3: return launch_cat<HEAD, 3>(a, grid, s);  // MountainCar, Acrobot
+    case 4: return launch_cat<HEAD, 4>(a, grid, s);  // LunarLander
+    default: return -2;
+  }
+}
+
+template <int HEAD, int NA>
+static int launch_gauss(const GradArgs& a, int grid, hipStream_t s) {
+  if (a.D <= 4) return launch_vg<4, HEAD, NA>(a, grid, s);  // Pendulum (D = 3, A = 1)
+  if (a.D <= 8) return launch_vg<8, HEAD, NA>(a, grid, s);
+  return launch_vg<20, HEAD, NA>(a, grid, s);  // HalfCheetahSynth (D = 17, A = 6)
+}
+
+template <int HEAD>
+static int launch_gauss_a(const GradArgs& a, int grid, hipStream_t s) {
+  switch (a.A) {
+    case 1: return launch_gauss<HEAD, 1>(a, grid, s);
+    case 6: return launch_gauss<HEAD, 6>(a, grid, s);
+    default: return -2;
+  }
+}
+
+// Policy-gradient step on the bf16x6 kernel (categorical A = 2..4, Gaussian A = 1 or 6).
 int launch_policy_grad_split(const GradArgs& a, int head, int grid, hipStream_t s) {
-  if (head == HEAD_PG_CAT) return a.D <= 4 ? launch_vg<4, HEAD_PG_CAT>(a, grid, s) : launch_vg<8, HEAD_PG_CAT>(a, grid, s);
-  if (head == HEAD_PPO_CAT)
-    return a.D <= 4 ? launch_vg<4, HEAD_PPO_CAT>(a, grid, s) : launch_vg<8, HEAD_PPO_CAT>(a, grid, s);
-  return -2;
+  switch (head) {
+    case HEAD_PG_CAT: return launch_cat_a<HEAD_PG_CAT>(a, grid, s);
+    case HEAD_PPO_CAT: return launch_cat_a<HEAD_PPO_CAT>(a, grid, s);
+    case HEAD_PG_GAUSS: return launch_gauss_a<HEAD_PG_GAUSS>(a, grid, s);
+    case HEAD_PPO_GAUSS: return launch_gauss_a<HEAD_PPO_GAUSS>(a, grid, s);
+    default: return -2;
+  }
 }
 
 }  // namespace rrl

@@ -150,12 +150,13 @@ def _pg64(head, pp, X, A, H, mask, act, adv, logp_old, stats, inv_B, clip, ent_c
 
 
 @pytest.mark.parametrize("head", ["PG_CAT", "PPO_CAT"])
-@pytest.mark.parametrize("D,B", [(4, 5000), (4, 70000), (3, 777), (8, 33000)])
-def test_policy_split_kernel_matches_oracle(cuda, head, D, B):
-    """The 2-action categorical policy heads on the bf16x6 kernel (CartPole's policy step)
-    against the fp32-MFMA kernel and the autograd oracle: masks, advantage normalisation,
-    PPO ratio clipping, entropy bonus and the loss statistics."""
-    H, A = 128, 2
+@pytest.mark.parametrize("D,B,A", [(4, 5000, 2), (4, 70000, 2), (3, 777, 2), (8, 33000, 2), (2, 4097, 3),
+                                   (6, 20000, 3), (8, 33000, 4), (4, 999, 4)])
+def test_policy_split_kernel_matches_oracle(cuda, head, D, B, A):
+    """Categorical policy heads (A = 2..4: CartPole, MountainCar / Acrobot, LunarLander) on the
+    bf16x6 kernel against the fp32-MFMA kernel and the autograd oracle: masks, advantage
+    normalisation, PPO ratio clipping, entropy bonus and the loss statistics."""
+    H = 128
     hd = getattr(GradHead, head)
     g = torch.Generator().manual_seed(D * 31 + B)
     spec = MLPSpec(D, H, A, False)
@@ -168,13 +169,97 @@ def test_policy_split_kernel_matches_oracle(cuda, head, D, B):
     act = torch.randint(0, A, (B,), generator=g, dtype=torch.int32)
     adv = torch.randn(B, generator=g) * 3 + 0.5
     mask = torch.ones(B, A)
-    mask[torch.arange(B) % 97 == 5, 1] = 0.0
+    mask[torch.arange(B) % 97 == 5, A - 1] = 0.0
     act[torch.arange(B) % 97 == 5] = 0
     logp_old = -torch.rand(B, generator=g) * 1.2 - 0.05
     stats = torch.tensor([adv.sum().item(), (adv * adv).sum().item(), float(B)])
     kw = dict(mask=mask, act=act, adv=adv, logp_old=logp_old, adv_stats=stats, inv_B=1.0 / B, clip_eps=0.2,
               ent_coef=0.01)
     g_ref = _pg64(head, pp, X, A, H, mask, act, adv, logp_old, stats, 1.0 / B, 0.2, 0.01)
+    out = {}
+    for mode in (1, 0):
+        old = set_value_grad_mode(mode)
+        try:
+            kwc = {k: (v.to(cuda) if torch.is_tensor(v) else v) for k, v in kw.items()}
+            slab, loss = mlp_grad(hd, pp.to(cuda), X.to(cuda), A, H, **kwc)
+            torch.cuda.synchronize()
+        finally:
+            set_value_grad_mode(old)
+        out[mode] = (slab.sum(0, dtype=torch.float64).cpu(), loss.sum(0).cpu())
+    scale = g_ref.abs().max().item()
+    err_split = (out[1][0] - g_ref).abs().max().item() / scale
+    err_fp32 = (out[0][0] - g_ref).abs().max().item() / scale
+    assert err_fp32 < 1e-5, err_fp32
+    assert err_split < 1e-5, (err_split, err_fp32)
+    ls, lf = out[1][1], out[0][1]
+    assert int(ls[5].item()) == B and int(lf[5].item()) == B
+    for k, name in ((0, "loss"), (1, "entropy"), (2, "kl"), (3, "clipfrac")):
+        assert abs(ls[k].item() - lf[k].item()) <= 1e-4 * max(1.0, abs(lf[k].item())), (name, ls[k], lf[k])
+
+
+def _gauss64(head, pp, X, A, H, actc, adv, logp_old, stats, inv_B, clip, ent_coef):
+    """float64 autograd gradient of the diagonal-Gaussian PG / PPO loss (mlp_grad.hip
+    HEAD_PG_GAUSS / HEAD_PPO_GAUSS: state-independent log_std, entropy bonus)."""
+    import math
+
+    D = X.shape[1]
+    p = pp.double().clone().requires_grad_(True)
+    o = 0
+    W1 = p[o:o + H * D].view(H, D); o += H * D
+    b1 = p[o:o + H]; o += H
+    W2 = p[o:o + H * H].view(H, H); o += H * H
+    b2 = p[o:o + H]; o += H
+    W3 = p[o:o + A * H].view(A, H); o += A * H
+    b3 = p[o:o + A]; o += A
+    ls = p[o:o + A]
+    mu = torch.relu(torch.relu(X.double() @ W1.T + b1) @ W2.T + b2) @ W3.T + b3
+    z = (actc.double() - mu) * torch.exp(-ls)
+    logp = (-0.5 * z * z - ls - 0.5 * math.log(2 * math.pi)).sum(-1)
+    n = float(stats[2])
+    mean = float(stats[0]) / n
+    var = max(float(stats[1]) / n - mean * mean, 0.0)
+    advn = (adv.double() - mean) / (var ** 0.5 + 1e-8)
+    if head == "PG_GAUSS":
+        li = -logp * advn
+    else:
+        ratio = torch.exp(logp - logp_old.double())
+        li = -torch.minimum(ratio * advn, torch.clamp(ratio, 1 - clip, 1 + clip) * advn)
+    ent = (0.5 + 0.5 * math.log(2 * math.pi) + ls).sum() * X.shape[0]
+    ((li.sum() - ent_coef * ent) * inv_B).backward()
+    return p.grad.detach(), logp.detach()
+
+
+@pytest.mark.parametrize("head", ["PG_GAUSS", "PPO_GAUSS"])
+@pytest.mark.parametrize("D,B,A", [(17, 33000, 6), (17, 777, 6), (3, 20000, 1), (8, 4097, 6)])
+def test_gaussian_split_kernel_matches_oracle(cuda, head, D, B, A):
+    """Diagonal-Gaussian policy heads (HalfCheetah A = 6, Pendulum A = 1) on the bf16x6 kernel
+    against the float64 oracle and the fp32-MFMA kernel, including the log_std gradient."""
+    H = 128
+    hd = getattr(GradHead, head)
+    g = torch.Generator().manual_seed(D * 17 + B + A)
+    spec = MLPSpec(D, H, A, True)
+    pp = spec.init(g, log_std_init=-0.5)
+    pp = pp + 0.05 * torch.randn(pp.shape, generator=g)
+    X = torch.randn(B, D, generator=g) * 1.5
+    keep = _away_from_relu_kinks(pp, X, D, H)
+    X = X[keep]
+    B = X.shape[0]
+    actc = torch.randn(B, A, generator=g) * 0.7
+    adv = torch.randn(B, generator=g) * 3 + 0.5
+    stats = torch.tensor([adv.sum().item(), (adv * adv).sum().item(), float(B)])
+    _, logp_now = _gauss64("PG_GAUSS", pp, X, A, H, actc, adv, None, stats, 1.0 / B, 0.2, 0.01)
+    logp_old = (logp_now + 0.3 * torch.randn(B, generator=g, dtype=torch.float64)).float()
+    # the clipped surrogate is discontinuous at ratio = 1 +- clip: rows whose float64 ratio lies
+    # within 1e-4 of it can fall on either side for any two fp32-accurate evaluations (and one
+    # such row moves a gradient entry by ~1e-4 of its scale), so they are left out, like the
+    # ReLU kinks above
+    ratio = torch.exp(logp_now - logp_old.double())
+    far = ((ratio - 1.2).abs() > 1e-4) & ((ratio - 0.8).abs() > 1e-4)
+    X, actc, adv, logp_old = X[far], actc[far], adv[far], logp_old[far]
+    B = X.shape[0]
+    stats = torch.tensor([adv.sum().item(), (adv * adv).sum().item(), float(B)])
+    kw = dict(actc=actc, adv=adv, logp_old=logp_old, adv_stats=stats, inv_B=1.0 / B, clip_eps=0.2, ent_coef=0.01)
+    g_ref, _ = _gauss64(head, pp, X, A, H, actc, adv, logp_old, stats, 1.0 / B, 0.2, 0.01)
     out = {}
     for mode in (1, 0):
         old = set_value_grad_mode(mode)

@@ -34,7 +34,7 @@ def timeit(fn, iters, warmup=3):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("which", choices=["grad", "pgrad", "fwd", "rollout", "adam", "rslab", "scan", "all"])
+    ap.add_argument("which", choices=["grad", "pgrad", "pgauss", "fwd", "rollout", "adam", "rslab", "scan", "all"])
     ap.add_argument("--B", type=int, default=2097152)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--H", type=int, default=128)
@@ -89,6 +89,32 @@ def main():
         us = timeit(lambda: mlp_grad(GradHead.PG_CAT, pp, X, 2, H, act=act, adv=adv, adv_stats=st, grad_slab=slab,
                                      loss_slab=ls), a.iters)
         res["policy_grad_us"] = us
+        old = hip().set_value_grad_mode(0)
+        res["policy_grad_fp32mfma_us"] = timeit(lambda: mlp_grad(GradHead.PG_CAT, pp, X, 2, H, act=act, adv=adv,
+                                                                 adv_stats=st, grad_slab=slab, loss_slab=ls), a.iters)
+        hip().set_value_grad_mode(old)
+    if a.which in ("pgauss", "all"):
+        # HalfCheetah PPO policy step: D = 17, A = 6 Gaussian head (bf16x6 kernel vs fp32 MFMA)
+        Dg, Ag = 17, 6
+        Xg = torch.randn(B, Dg, generator=g).to(dev)
+        pg = MLPSpec(Dg, H, Ag, True).init(g).to(dev)
+        actc = torch.randn(B, Ag, generator=g).to(dev)
+        lpo = -torch.rand(B, generator=g).to(dev) * 5
+        ns = hip().mlp_grad_slabs(B)
+        slab = torch.empty(ns, pg.numel(), device=dev)
+        ls = torch.empty(ns, 8, device=dev)
+        st = torch.tensor([0.0, float(B), float(B)], device=dev)
+        fn = lambda: mlp_grad(GradHead.PPO_GAUSS, pg, Xg, Ag, H, actc=actc, adv=adv, logp_old=lpo, adv_stats=st,  # noqa
+                              grad_slab=slab, loss_slab=ls)
+        res["ppo_gauss_split_us"] = timeit(fn, a.iters)
+        old = hip().set_value_grad_mode(0)
+        res["ppo_gauss_fp32mfma_us"] = timeit(fn, a.iters)
+        hip().set_value_grad_mode(old)
+        Xv = Xg
+        pv17 = MLPSpec(Dg, H, 1).init(g).to(dev)
+        slabv = torch.empty(ns, pv17.numel(), device=dev)
+        res["value_grad_d17_us"] = timeit(lambda: mlp_grad(GradHead.VALUE_MSE, pv17, Xv, 1, H, ret=ret,
+                                                           grad_slab=slabv, loss_slab=ls), a.iters)
     if a.which in ("fwd", "all"):
         out = {"v": torch.empty(B, device=dev)}
         us = timeit(lambda: mlp_forward(FwdMode.VALUE, pv, X, 1, H, out=out), a.iters)
