@@ -142,6 +142,7 @@ void mlp_grad(int64_t head, const Tensor& params, const Tensor& X, int64_t A, in
   TORCH_CHECK(D >= 1 && D <= 32, "obs dim must be in [1, 32]");
   TORCH_CHECK(A >= 1 && A <= 16, "act dim must be in [1, 16]");
   TORCH_CHECK(head >= 0 && head <= 4, "bad head");
+  TORCH_CHECK(B * std::max<int64_t>(D, A) < (int64_t)INT32_MAX, "batch too large for 32-bit row indexing");
   const bool gauss = head == 3 || head == 4;
   const bool cat = head == 0 || head == 2;
   const int64_t Aeff = head == 1 ? 1 : A;

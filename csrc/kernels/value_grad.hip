@@ -269,7 +269,7 @@ RRL_DEV float wave_sum_vl(float v) {
 
 template <int DP, int HEAD, int NA, bool STAMP = false>
 __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
-  unsigned long long st_prev = 0, st_sum[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_prev = 0, st_sum[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   extern __shared__ __attribute__((aligned(16))) uint16_t vg_lds[];
   constexpr bool kValue = HEAD == HEAD_VALUE_MSE;
   constexpr bool kGauss = HEAD == HEAD_PG_GAUSS || HEAD == HEAD_PPO_GAUSS;
@@ -384,19 +384,21 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   int hact;
   float hac[NC];   // Gaussian action
   auto prefetch = [&](int b0) {
+    // unconditional loads from clamped addresses: nothing here consumes a loaded value (a
+    // select on it would make the compiler wait for the load right away); padding columns /
+    // rows past B are zeroed where the values are used
 #pragma unroll
     for (int i = 0; i < XQ; ++i) {
       const int q = min((int)threadIdx.x + 512 * i, 64 * DP - 1);
       const int rl = q / DP, d = q % DP, b = b0 + rl;
-      const float v = p.X[(size_t)min(b, p.B - 1) * D + min(d, D - 1)];
-      xr[i] = (b < p.B && d < D) ? v : 0.f;
+      xr[i] = p.X[(size_t)min(b, p.B - 1) * D + min(d, D - 1)];
     }
     const int bc = min(b0 + l, p.B - 1);  // lane l handles batch row l of the slab in the head
     if (kValue) {
       hin = p.ret[bc];
     } else {
       hin = p.adv[bc];
-      hlp = p.logp_old ? p.logp_old[bc] : 0.f;
+      hlp = (p.logp_old ? p.logp_old : p.adv)[bc];
       if (kGauss) {
 #pragma unroll
         for (int a = 0; a < NC; ++a) hac[a] = p.actc[(size_t)bc * NA + a];
@@ -418,7 +420,8 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 #pragma unroll
     for (int i = 0; i < XQ; ++i) {
       const int q = (int)threadIdx.x + 512 * i;
-      if (q < 64 * DP) xs[q] = xr[i];
+      const int rl = q / DP, d = q % DP;
+      if (q < 64 * DP) xs[q] = (base + rl < p.B && d < D) ? xr[i] : 0.f;
     }
     __syncthreads();  // x visible; the previous slab's readers of both images are done
     VG_STAMP(1);
@@ -487,7 +490,9 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       }
       if (NA > 2) __builtin_amdgcn_sched_barrier(0);
     }
+    VG_STAMP(4);
     __syncthreads();
+    VG_STAMP(5);
     // loss head: lane l handles batch row l (every wave computes the same 64 rows; wave 0's
     // lanes count each row once in the batch statistics and the head gradient sums)
     const bool lead = w == 0;
@@ -591,7 +596,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     if (base + (int)gridDim.x * 64 < p.B) prefetch(base + gridDim.x * 64);
     if (kRedImg) __syncthreads();  // every wave read the partials before dh2 overwrites them
 
-    VG_STAMP(4);
+    VG_STAMP(6);
     // ------------------------------------------------------------ dh2, dW3, db2
     // dout of batch row 16 bt + j comes from lane 16 bt + j (ds_bpermute, no barrier).  Field
     // group 0 (db2, dW3 rows 0 / 1) is folded first; the rows of outputs 2.. (group 1) in a
@@ -646,7 +651,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     }
     __syncthreads();
 
-    VG_STAMP(5);
+    VG_STAMP(7);
     // ------------------------------------------------------------ dh1 (own), dW1, db1
     floatx4 dh1[4];
 #pragma unroll
@@ -683,7 +688,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     // waves 4-7 dW2 first, so the two waves sharing a SIMD pair matrix work with vector work
     // (MI355X_MICROARCH.md, two waves per SIMD) instead of both idling the matrix pipe at once
     auto do_dw1 = [&]() {
-      VG_STAMP(6);
+      VG_STAMP(8);
       accv[0] += reduce_scatter16(tb, j);
       // dW1 one group of 4 input columns at a time (16 partials live, whatever D is), each
       // folded over the 16 batch lanes right away: lane j keeps entry j
@@ -706,7 +711,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     };
     // ------------------------------------------------------------ dW2 += dh2 h1^T
     auto do_dw2 = [&]() {
-      VG_STAMP(7);
+      VG_STAMP(9);
       Split8 a = frag_tr(dhimg, 0, own, l);
       Split8 cur = frag_tr(h1img, 0, 0, l);
 #pragma unroll
@@ -725,11 +730,11 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     // measured 1 % slower and added register pressure: both orders kept the same)
     do_dw1();
     do_dw2();
-    VG_STAMP(8);
+    VG_STAMP(10);
   }
   if (STAMP && p.stamps != nullptr && l == 0) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) p.stamps[(blockIdx.x * 8 + w) * 8 + k] = st_sum[k];
+    for (int k = 0; k < 10; ++k) p.stamps[(blockIdx.x * 8 + w) * 16 + k] = st_sum[k];
   }
 
   // ------------------------------------------------------------------ epilogue

@@ -60,16 +60,17 @@ def main():
         res["value_grad_us"] = us
         res["value_grad_TFLOPs_nominal"] = flop_row * B / us / 1e6
         if a.stamps:
-            st = torch.zeros(ns * 8 * 8, dtype=torch.int64, device=dev)
+            st = torch.zeros(ns * 8 * 16, dtype=torch.int64, device=dev)
             hip().set_value_grad_stamps(st)
             old_t = hip().set_value_grad_tune(8)
             mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret, grad_slab=slab, loss_slab=ls)
             torch.cuda.synchronize()
             hip().set_value_grad_tune(old_t)
             hip().set_value_grad_stamps(torch.empty(0, device=dev))
-            seg = st.view(ns, 8, 8).double().mean(0) / (B / 64 / ns)  # cycles per slab, per wave x segment
-            names = ["xstore+bar", "layer1+bar", "layer2 mfma", "head+bar", "dout/dh2+bar", "dh1 mfma", "dW1", "dW2 mfma"]
-            res_st = {names[k]: [round(x, 1) for x in seg[:, k].tolist()] for k in range(8)}
+            seg = st.view(ns, 8, 16).double().mean(0) / (B / 64 / ns)  # cycles per slab, per wave x segment
+            names = ["xstore+bar", "layer1+bar", "layer2 mfma", "head partials", "bar3", "dout+prefetch",
+                     "dh2+bar", "dh1 mfma", "dW1", "dW2 mfma"]
+            res_st = {names[k]: [round(x, 1) for x in seg[:, k].tolist()] for k in range(10)}
             print(json.dumps({"stamps_cycles_per_slab_per_wave": res_st}))
         if a.tunes:
             for t in [int(x) for x in a.tunes.split(",")]:
