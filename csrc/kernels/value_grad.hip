@@ -205,6 +205,17 @@ RRL_DEV void store_split(uint16_t* img, int row, int col, const floatx4 v) {
   *reinterpret_cast<vbf16x4*>(a + 2 * kVgImg) = lo;
 }
 
+// A C-layout tile's three packed bf16 pieces, and their store into an image.
+struct Pieces {
+  vbf16x4 h, m, l;
+};
+RRL_DEV void store_pieces(uint16_t* img, int row, int col, const Pieces& pc) {
+  uint16_t* a = img + img_off(row, col);
+  *reinterpret_cast<vbf16x4*>(a) = pc.h;
+  *reinterpret_cast<vbf16x4*>(a + kVgImg) = pc.m;
+  *reinterpret_cast<vbf16x4*>(a + 2 * kVgImg) = pc.l;
+}
+
 // Value of v from the partner lane selected by a DPP control (VALU cross-lane move, no LDS).
 template <int CTRL>
 RRL_DEV float dpp_f(float v) {
@@ -278,6 +289,12 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   static_assert(NA >= 1 && NA <= 6, "NA <= 6 (LDS plan, two field groups)");
   // batch-summed 4-feature fields of the head / bias gradients, folded over the 16 batch
   // lanes by the DPP reduce-scatter: field 0 db2, 1 dW3 row 0, 2 db1, 3 dW3 row 1, 4.. rows 2..
+  // Value head, DP = 4 (the flagship): dh2 = w3 (x) (relu'(h2) * dout) is rank-1 per row, so the
+  // dh2 image holds dh2' = relu'(h2) * dout (each piece = mask * a piece of the ROW's dout: one
+  // split per row, not per element), w3 folds into a stationary A' = W2^T diag(w3) for dh1 and
+  // into the epilogue for dW2 / db2, and dh1 = r * (A' x hi(dh2')) with r = dout / hi(dout)
+  // per row: 3 MFMAs per step instead of 6 (hi(dh2') = mask * hi(dout) is exact in bf16).
+  constexpr bool kFactor = kValue && DP <= 8;
   constexpr int NF = NA + 2;
   constexpr int NG = (NF + 3) / 4;  // 16-slot groups (one register each)
   constexpr bool kRedImg = vg_red_in_image(DP, NA);
@@ -308,6 +325,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   // hi + mid pieces in registers; the lo pieces of W2 go to an LDS image [o][i] that both
   // fragment kinds read once per 32-wide k-chunk (b128 for wA, transposed for wB)
   Split8HM wA[4], wB[4];
+  vbf16x8 wBl[kFactor ? 4 : 1];  // lo pieces of A' (kFactor)
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     floatx4 a0, a1, b0, b1;
@@ -317,14 +335,20 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       a0[e] = P[o.w2 + (own + j) * kVgH + 32 * c + 8 * g + e];
       a1[e] = P[o.w2 + (own + j) * kVgH + 32 * c + 8 * g + 4 + e];
       // wB: A[m = own + j][k = 32c + 8g + e] = W2[k][m]      (backward data)
+      //     (kFactor: A'[m][k] = W2[k][m] * w3[k])
       b0[e] = P[o.w2 + (32 * c + 8 * g + e) * kVgH + own + j];
       b1[e] = P[o.w2 + (32 * c + 8 * g + 4 + e) * kVgH + own + j];
+      if (kFactor) {
+        b0[e] *= P[o.w3 + 32 * c + 8 * g + e];
+        b1[e] *= P[o.w3 + 32 * c + 8 * g + 4 + e];
+      }
     }
     const Split8 sa = split8(a0, a1), sb = split8(b0, b1);
     wA[c].h = sa.h;
     wA[c].m = sa.m;
     wB[c].h = sb.h;
     wB[c].m = sb.m;
+    if (kFactor) wBl[c % (kFactor ? 4 : 1)] = sb.l;
   }
   for (int q = threadIdx.x; q < kVgH * kVgH / 4; q += blockDim.x) {
     floatx4 v;
@@ -598,56 +622,89 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 
     VG_STAMP(6);
     // ------------------------------------------------------------ dh2, dW3, db2
-    // dout of batch row 16 bt + j comes from lane 16 bt + j (ds_bpermute, no barrier).  Field
-    // group 0 (db2, dW3 rows 0 / 1) is folded first; the rows of outputs 2.. (group 1) in a
-    // second pass, so only 16 partials are live at a time.
-    floatx4 dd[4];
-#pragma unroll
-    for (int bt = 0; bt < 4; ++bt) dd[bt] = zero4();
-    {
-      float tv[16];  // this slab's field partials of features own + 4g + r
+    float rr[4];  // kFactor: per batch tile, this lane's row correction dout / hi(dout)
+    if (kFactor) {
+      float tv[16];  // fields: db2' (x w3 in the epilogue), dW3 row 0
 #pragma unroll
       for (int e = 0; e < 16; ++e) tv[e] = 0.f;
-#pragma unroll
-      for (int a = 0; a < NA; ++a) {
-        const floatx4 w3a = *reinterpret_cast<const floatx4*>(w3p + a * kVgH);
-        const int f = a == 0 ? 1 : 3;
-#pragma unroll
-        for (int bt = 0; bt < 4; ++bt) {
-          const float v = __shfl(dout[a], 16 * bt + j, 64);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            dd[bt][r] = fmaf(w3a[r], v, dd[bt][r]);
-            if (a < 2) tv[4 * f + r] = fmaf(v, h2[bt][r], tv[4 * f + r]);
-          }
-        }
-      }
 #pragma unroll
       for (int bt = 0; bt < 4; ++bt) {
+        const float v = __shfl(dout[0], 16 * bt + j, 64);
+        // the row's dout split once: v = vh + vm + vl
+        uint32_t ph, pm, pl;
+        split2(vf32x2{v, v}, ph, pm, pl);
+        const float vh = __uint_as_float(ph << 16);
+        rr[bt] = vh != 0.f ? v * __builtin_amdgcn_rcpf(vh) : 0.f;  // 1 ulp: within fp32 accuracy
+        uint32_t mw[2];  // relu'(h2) of this lane's 4 features as bf16 lane masks
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const bool p0 = h2[bt][2 * q] > 0.f, p1 = h2[bt][2 * q + 1] > 0.f;
+          mw[q] = (p0 ? 0x0000ffffu : 0u) | (p1 ? 0xffff0000u : 0u);
+        }
+        Pieces pc;
+        pc.h = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & ph, mw[1] & ph));
+        pc.m = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & pm, mw[1] & pm));
+        pc.l = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & pl, mw[1] & pl));
+        store_pieces(dhimg, 16 * bt + j, own + 4 * g, pc);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          dd[bt][r] = h2[bt][r] > 0.f ? dd[bt][r] : 0.f;
-          tv[r] += dd[bt][r];
+          tv[r] += h2[bt][r] > 0.f ? v : 0.f;
+          tv[4 + r] = fmaf(v, h2[bt][r], tv[4 + r]);
         }
-        store_split(dhimg, 16 * bt + j, own + 4 * g, dd[bt]);
       }
       accv[0] += reduce_scatter16(tv, j);
-    }
-    if (NA > 2) {
-      float tv[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) tv[e] = 0.f;
-#pragma unroll
-      for (int a = 2; a < NA; ++a) {
-        const int f = a + 2;  // fields 4 .. NA + 1 -> group 1 (NA <= 6)
-#pragma unroll
-        for (int bt = 0; bt < 4; ++bt) {
-          const float v = __shfl(dout[a], 16 * bt + j, 64);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) tv[4 * (f & 3) + r] = fmaf(v, h2[bt][r], tv[4 * (f & 3) + r]);
+    } else {
+      // dout of batch row 16 bt + j comes from lane 16 bt + j (ds_bpermute, no barrier).  Field
+      // group 0 (db2, dW3 rows 0 / 1) is folded first; the rows of outputs 2.. (group 1) in a
+      // second pass, so only 16 partials are live at a time.
+      floatx4 dd[4];
+  #pragma unroll
+      for (int bt = 0; bt < 4; ++bt) dd[bt] = zero4();
+      {
+        float tv[16];  // this slab's field partials of features own + 4g + r
+  #pragma unroll
+        for (int e = 0; e < 16; ++e) tv[e] = 0.f;
+  #pragma unroll
+        for (int a = 0; a < NA; ++a) {
+          const floatx4 w3a = *reinterpret_cast<const floatx4*>(w3p + a * kVgH);
+          const int f = a == 0 ? 1 : 3;
+  #pragma unroll
+          for (int bt = 0; bt < 4; ++bt) {
+            const float v = __shfl(dout[a], 16 * bt + j, 64);
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              dd[bt][r] = fmaf(w3a[r], v, dd[bt][r]);
+              if (a < 2) tv[4 * f + r] = fmaf(v, h2[bt][r], tv[4 * f + r]);
+            }
+          }
         }
+  #pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dd[bt][r] = h2[bt][r] > 0.f ? dd[bt][r] : 0.f;
+            tv[r] += dd[bt][r];
+          }
+          store_split(dhimg, 16 * bt + j, own + 4 * g, dd[bt]);
+        }
+        accv[0] += reduce_scatter16(tv, j);
       }
-      accv[1] += reduce_scatter16(tv, j);
+      if (NA > 2) {
+        float tv[16];
+  #pragma unroll
+        for (int e = 0; e < 16; ++e) tv[e] = 0.f;
+  #pragma unroll
+        for (int a = 2; a < NA; ++a) {
+          const int f = a + 2;  // fields 4 .. NA + 1 -> group 1 (NA <= 6)
+  #pragma unroll
+          for (int bt = 0; bt < 4; ++bt) {
+            const float v = __shfl(dout[a], 16 * bt + j, 64);
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) tv[4 * (f & 3) + r] = fmaf(v, h2[bt][r], tv[4 * (f & 3) + r]);
+          }
+        }
+        accv[1] += reduce_scatter16(tv, j);
+      }
     }
     __syncthreads();
 
@@ -659,7 +716,28 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     float tb[16];  // db1 partials in entries 8..11 (field 2; the rest stay zero)
 #pragma unroll
     for (int q = 0; q < 16; ++q) tb[q] = 0.f;
-    {
+    if (kFactor) {
+      // dh1 = r * (A' x hi(dh2')): the hi piece alone is exact (mask * hi(dout))
+      vbf16x8 cur = *reinterpret_cast<const vbf16x8*>(dhimg + img_off(j, 8 * g));
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int c = it >> 2, bt = it & 3;
+        vbf16x8 nxt;
+        if (it + 1 < 16)
+          nxt = *reinterpret_cast<const vbf16x8*>(
+              dhimg + img_off(16 * ((it + 1) & 3) + j, 32 * ((it + 1) >> 2) + 8 * g));
+        dh1[bt] = mfma_bf16(wBl[c % (kFactor ? 4 : 1)], cur, dh1[bt]);
+        dh1[bt] = mfma_bf16(wB[c].m, cur, dh1[bt]);
+        dh1[bt] = mfma_bf16(wB[c].h, cur, dh1[bt]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (it + 1 < 16) cur = nxt;
+      }
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dh1[bt][r] *= rr[bt];
+      }
+    } else {
       Split8 cur = frag_row(dhimg, j, 8 * g);
       vbf16x8 bl = frag_tr8(w2lo, 8 * g, own, l);
 #pragma unroll
@@ -684,9 +762,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         tb[8 + r] += dh1[bt][r];
       }
     }
-    // dW1 (VALU outer products) and dW2 (MFMA) are independent: waves 0-3 run dW1 first,
-    // waves 4-7 dW2 first, so the two waves sharing a SIMD pair matrix work with vector work
-    // (MI355X_MICROARCH.md, two waves per SIMD) instead of both idling the matrix pipe at once
+    // dW1 (VALU outer products) and dW2 (MFMA) are independent of each other
     auto do_dw1 = [&]() {
       VG_STAMP(8);
       accv[0] += reduce_scatter16(tb, j);
@@ -739,17 +815,20 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 
   // ------------------------------------------------------------------ epilogue
   float* slab = p.grad_slab + (size_t)blockIdx.x * p.P;
+  floatx4 w3s;  // kFactor: dW2 rows / db2 are w3 x the accumulated dh2' sums
+#pragma unroll
+  for (int r = 0; r < 4; ++r) w3s[r] = kFactor ? P[o.w3 + own + 4 * g + r] : 1.f;
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) slab[o.w2 + (own + 4 * g + r) * kVgH + 16 * it + j] = acc2[it][r];
+    for (int r = 0; r < 4; ++r) slab[o.w2 + (own + 4 * g + r) * kVgH + 16 * it + j] = acc2[it][r] * w3s[r];
   }
 #pragma unroll
   for (int q = 0; q < NG; ++q) {
     const int f = 4 * q + (j >> 2), feat = own + 4 * g + (j & 3);
     if (f < NF) {
       const int off = f == 0 ? o.b2 : f == 1 ? o.w3 : f == 2 ? o.b1 : o.w3 + (f == 3 ? 1 : f - 2) * kVgH;
-      slab[off + feat] = accv[q];
+      slab[off + feat] = (kFactor && f == 0) ? accv[q] * P[o.w3 + feat] : accv[q];
     }
   }
 #pragma unroll
