@@ -87,6 +87,24 @@ class ValueLoop:
                      loss_slab=ls)
             self.net.apply(slab, self.comm)
 
+    def step(self, obs: torch.Tensor, ret: torch.Tensor, inv_B: float, first: bool = False):
+        """One eager value step on a (mini)batch; ``first`` marks the step whose loss is
+        reported as the epoch's starting loss (PPO minibatch schedule, learner.py)."""
+        dev = obs.device
+        slab = ls = None
+        if dev.type == "cuda":
+            ns = grad_slabs(obs.shape[0], dev)
+            if getattr(self, "_mb_slab", None) is None or self._mb_slab.shape[0] < ns:
+                self._mb_slab = torch.empty(ns, self.net.P, device=dev)
+                self._mb_loss = torch.empty(ns, 8, device=dev)
+            slab, ls = self._mb_slab, self._mb_loss
+        g, ls = mlp_grad(GradHead.VALUE_MSE, self.net.params, obs, 1, self.net.spec.H, ret=ret, inv_B=inv_B,
+                         grad_slab=slab, loss_slab=ls)
+        if first:
+            self.loss_first = ls.clone()
+        self.loss_last = ls
+        self.net.apply(g, self.comm)
+
     def run(self, obs: torch.Tensor, ret: torch.Tensor, iters: int, inv_B: float):
         B = obs.shape[0]
         dev = obs.device

@@ -8,8 +8,12 @@ launch + one fused reduce+Adam launch (+ one RCCL all-reduce with several ranks)
             ``train_vf_iters`` value steps (separate optimisers -- the reference's
             pi_optimizer also covered the baseline parameters, defect A15);
   A2C      : 1 policy step with an entropy bonus + value steps;
-  PPO      : ``train_pi_iters`` clipped-surrogate steps with approximate-KL early
-            stopping, then value steps.
+  PPO      : ``train_pi_iters`` clipped-surrogate epochs with approximate-KL early
+            stopping, then ``train_vf_iters`` value epochs.  With ``num_minibatches`` M > 1
+            every epoch reshuffles the batch (one device ``randperm`` per epoch) and takes M
+            steps on disjoint minibatches (the usual PPO schedule); advantages keep the
+            full-batch normalisation statistics.  M = 1 is the full-batch form, whose value
+            loop is one hipGraph replay.
 """
 from __future__ import annotations
 
@@ -27,7 +31,8 @@ class PGLearner:
                  with_baseline: bool = True, pi_lr: float = 3e-4, vf_lr: float = 1e-3, train_vf_iters: int = 80,
                  train_pi_iters: int = 1, clip_ratio: float = 0.2, target_kl: Optional[float] = None,
                  ent_coef: float = 0.0, device="cpu", seed: int = 0, comm: Optional[Comm] = None,
-                 use_graphs: bool = True, log_std_init: float = -0.5, pi_params=None, vf_params=None):
+                 use_graphs: bool = True, log_std_init: float = -0.5, pi_params=None, vf_params=None,
+                 num_minibatches: int = 1):
         algo = algo.lower()
         assert algo in ("reinforce", "a2c", "ppo"), algo
         self.algo = algo
@@ -47,6 +52,11 @@ class PGLearner:
         self.vf = FlatNet(MLPSpec(obs_dim, hidden, 1), vf_lr, self.device, g, params=vf_params) \
             if self.with_baseline else None
         self.vloop = ValueLoop(self.vf, self.comm, use_graph=use_graphs) if self.vf is not None else None
+        self.num_minibatches = max(1, int(num_minibatches)) if algo == "ppo" else 1
+        # minibatch shuffles: one stream per rank (different data shards), reproducible from the seed
+        self.mb_seed = int(seed) * 1000003 + 17 + self.comm.rank
+        self._mb_gen = torch.Generator(device=self.device).manual_seed(self.mb_seed) \
+            if self.num_minibatches > 1 else None
         self._pi_slab = None
         self._pi_loss = None
         self.last = {}
@@ -76,28 +86,54 @@ class PGLearner:
         if inv_B is None:
             inv_B = 1.0 / max(B * self.comm.world, 1)
         H, A = self.hidden, self.act_dim
+        M = self.num_minibatches
         slab, ls = self._slabs(B)
         kl_stop = None
         pi_loss = None
+        step = 0
         for it in range(self.train_pi_iters):
-            out = mlp_grad(self.head, self.pi.params, obs, A, H, mask=mask, act=act, actc=actc, adv=adv,
-                           logp_old=logp_old, adv_stats=adv_stats, inv_B=inv_B, clip_eps=self.clip_ratio,
-                           ent_coef=self.ent_coef, grad_slab=slab, loss_slab=ls)
-            if it == 0:
-                pi_loss = out[1].sum(0).clone()
-            if self.algo == "ppo" and self.target_kl is not None and it > 0:
-                # approx KL of the current policy (measured in this iteration's forward)
-                st = out[1].sum(0)
-                st = self.comm.all_reduce_sum_(st.clone())
-                kl = (st[2] / torch.clamp(st[5], min=1.0)).item()
-                if kl > 1.5 * self.target_kl:
-                    kl_stop = it
-                    break
-            self.pi.apply(out[0], self.comm)
+            if M == 1:
+                batches = [(None, inv_B)]
+            else:
+                batches = [(idx, inv_B * B / idx.numel()) for idx in self.minibatches(B)]
+            for idx, inv in batches:
+                def sel(t):
+                    return t if idx is None or t is None else t.index_select(0, idx)
+
+                out = mlp_grad(self.head, self.pi.params, sel(obs), A, H, mask=sel(mask), act=sel(act),
+                               actc=sel(actc), adv=sel(adv), logp_old=sel(logp_old), adv_stats=adv_stats, inv_B=inv,
+                               clip_eps=self.clip_ratio, ent_coef=self.ent_coef, grad_slab=slab, loss_slab=ls)
+                if step == 0:
+                    pi_loss = out[1].sum(0).clone()
+                if self.algo == "ppo" and self.target_kl is not None and step > 0:
+                    # approx KL of the current policy (measured in this step's forward)
+                    st = out[1].sum(0)
+                    st = self.comm.all_reduce_sum_(st.clone())
+                    kl = (st[2] / torch.clamp(st[5], min=1.0)).item()
+                    if kl > 1.5 * self.target_kl:
+                        kl_stop = it
+                        break
+                self.pi.apply(out[0], self.comm)
+                step += 1
+            if kl_stop is not None:
+                break
         if self.vloop is not None and self.train_vf_iters > 0:
-            self.vloop.run(obs, ret, self.train_vf_iters, inv_B)
+            if M == 1:
+                self.vloop.run(obs, ret, self.train_vf_iters, inv_B)
+            else:
+                for ep in range(self.train_vf_iters):
+                    for j, idx in enumerate(self.minibatches(B)):
+                        self.vloop.step(obs.index_select(0, idx), ret.index_select(0, idx), inv_B * B / idx.numel(),
+                                        first=(ep == 0 and j == 0))
         self.last = {"pi_loss": pi_loss, "kl_stop": kl_stop}
         return self.last
+
+    def minibatches(self, B: int):
+        """Row indices of one epoch's ``num_minibatches`` disjoint minibatches (a fresh
+        permutation of the B rows; sizes differ by at most one row)."""
+        M = self.num_minibatches
+        perm = torch.randperm(B, device=self.device, generator=self._mb_gen)
+        return [perm[i * B // M:(i + 1) * B // M] for i in range(M)]
 
     def summarize(self) -> dict:
         """Synchronising read of the last optimize() statistics (global over ranks)."""

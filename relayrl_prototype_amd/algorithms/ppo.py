@@ -10,7 +10,7 @@ from .trajectory_algo import TrajectoryAlgorithm
 class PPO(TrajectoryAlgorithm):
     ALGO = "ppo"
     CONFIG_NAME = "PPO"
-    EXTRA_KEYS = ("hidden", "with_vf_baseline")
+    EXTRA_KEYS = ("hidden", "with_vf_baseline", "num_minibatches")
 
     def exp_name(self) -> str:
         return "relayrl-ppo-info"

@@ -181,7 +181,7 @@ class TrajectoryAlgorithm(AlgorithmAbstract):
                          pi_lr=p["pi_lr"], vf_lr=p["vf_lr"], train_vf_iters=p.get("train_vf_iters", 80),
                          train_pi_iters=p.get("train_pi_iters", 1), clip_ratio=p.get("clip_ratio", 0.2),
                          target_kl=p.get("target_kl"), ent_coef=p.get("ent_coef", 0.0), device=self.device,
-                         seed=self.seed, use_graphs=False)
+                         seed=self.seed, use_graphs=False, num_minibatches=p.get("num_minibatches", 1))
 
     # ------------------------------------------------------------------ API
     def receive_trajectory(self, trajectory) -> bool:

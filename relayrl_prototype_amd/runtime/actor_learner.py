@@ -61,6 +61,7 @@ class ActorLearnerConfig:
     vf_lr: float = 1e-3
     train_vf_iters: int = 80
     train_pi_iters: int = 10
+    num_minibatches: int = 1       # PPO only
     clip_ratio: float = 0.2
     target_kl: Optional[float] = None
     ent_coef: float = 0.0
@@ -225,7 +226,8 @@ class ActorLearner:
         if self.is_learner:
             self.learner = PGLearner(cfg.algo, D, A, cfg.hidden, not cont, cfg.with_baseline, cfg.pi_lr, cfg.vf_lr,
                                      cfg.train_vf_iters, cfg.train_pi_iters, cfg.clip_ratio, cfg.target_kl,
-                                     cfg.ent_coef, self.device, cfg.seed, self.lcomm, cfg.use_graphs)
+                                     cfg.ent_coef, self.device, cfg.seed, self.lcomm, cfg.use_graphs,
+                                     num_minibatches=cfg.num_minibatches)
             self.shard = topo.shard(self.rank)
             dev = self.device
             # ONE contiguous shard batch: K [T, N] blocks, then the K x N final observations

@@ -39,7 +39,7 @@ ENV_BY_DIMS = {(4, 2): "CartPole-v1", (2, 3): "MountainCar-v0", (6, 3): "Acrobot
 # reference hyperparameter name -> trainer config field
 _PARAM_MAP = {"gamma": "gamma", "lam": "lam", "pi_lr": "pi_lr", "vf_lr": "vf_lr", "train_vf_iters": "train_vf_iters",
               "train_pi_iters": "train_pi_iters", "clip_ratio": "clip_ratio", "target_kl": "target_kl",
-              "ent_coef": "ent_coef", "seed": "seed", "with_vf_baseline": "with_baseline"}
+              "ent_coef": "ent_coef", "seed": "seed", "num_minibatches": "num_minibatches", "with_vf_baseline": "with_baseline"}
 # "mi355x" block name -> trainer config field
 _MI355X_MAP = {"envs_per_actor": "num_envs", "num_envs": "num_envs", "rollout_len": "rollout_len",
                "hidden": "hidden", "use_graphs": "use_graphs", "max_episode_steps": "max_episode_steps",

@@ -56,6 +56,7 @@ class HostTrainerConfig:
     vf_lr: float = 1e-3
     train_vf_iters: int = 80
     train_pi_iters: int = 10
+    num_minibatches: int = 1       # PPO only
     clip_ratio: float = 0.2
     target_kl: Optional[float] = None
     ent_coef: float = 0.0
@@ -115,7 +116,7 @@ class HostVecTrainer:
         self.learner = PGLearner(cfg.algo, self.D, self.A, cfg.hidden, not self.continuous, cfg.with_baseline,
                                  cfg.pi_lr, cfg.vf_lr, cfg.train_vf_iters, cfg.train_pi_iters, cfg.clip_ratio,
                                  cfg.target_kl, cfg.ent_coef, self.device, cfg.seed, self.comm, cfg.use_graphs,
-                                 cfg.log_std_init)
+                                 cfg.log_std_init, num_minibatches=cfg.num_minibatches)
         self.timer = PhaseTimer(self.device, enabled=cfg.phase_timing)
         self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.comm, self.timer)
         self.overlap = bool(cfg.overlap and cuda)

@@ -78,6 +78,7 @@ class VecTrainerConfig:
     vf_lr: float = 1e-3
     train_vf_iters: int = 80
     train_pi_iters: int = 10       # PPO only
+    num_minibatches: int = 1       # PPO only: shuffled minibatches per epoch
     clip_ratio: float = 0.2
     target_kl: Optional[float] = None
     seed: int = 1
@@ -113,7 +114,7 @@ class VecTrainer:
         self.learner = PGLearner(cfg.algo, D, A, H, not self.continuous, cfg.with_baseline, cfg.pi_lr, cfg.vf_lr,
                                  cfg.train_vf_iters,
                                  cfg.train_pi_iters, cfg.clip_ratio, cfg.target_kl, cfg.ent_coef, dev, cfg.seed,
-                                 self.comm, cfg.use_graphs)
+                                 self.comm, cfg.use_graphs, num_minibatches=cfg.num_minibatches)
         self.pi, self.vf = self.learner.pi, self.learner.vf
         self.timer = PhaseTimer(dev, enabled=cfg.phase_timing)
         self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.comm, self.timer)
