@@ -61,6 +61,12 @@ constexpr bool vg_red_in_image(int DP, int NA) { return vg_base_bytes(DP, NA) + 
 constexpr int vg_lds_bytes(int DP, int NA) {
   return vg_base_bytes(DP, NA) + (vg_red_in_image(DP, NA) ? 0 : vg_red_bytes(NA));
 }
+// Factored value head (DP <= 8, see the kernel): after the W2 lo image, the relu'(h2) mask of
+// the slab as bytes [64 rows][4 lane groups][4 k-chunks] (byte = 8 features) and the table
+// byte -> 8 bf16 {0, 1} [256][8] that turns a byte into a dh1 B fragment.
+constexpr bool vg_factor(int DP, int HEAD) { return HEAD == HEAD_VALUE_MSE && DP <= 8; }
+constexpr int vg_mask_bytes(int DP, int HEAD) { return vg_factor(DP, HEAD) ? 64 * 16 + 256 * 16 : 0; }
+static_assert(vg_lds_bytes(8, 1) + vg_mask_bytes(8, HEAD_VALUE_MSE) <= 160 * 1024, "factored LDS plan");
 static_assert(vg_lds_bytes(24, 1) <= 160 * 1024 && !vg_red_in_image(24, 1), "value-grad LDS plan");
 static_assert(vg_lds_bytes(20, 6) <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
 static_assert(vg_red_bytes(6) <= 3 * kVgImg * 2, "head partials must fit in the dh2 image");
@@ -118,6 +124,14 @@ RRL_DEV Split8 split8(const floatx4 v0, const floatx4 v1) {
 }
 
 
+// max(x, 0) as ONE v_max_i32 on the bit pattern (negative floats, -0 included, are negative
+// ints): fmaxf / fmed3 get a NaN-canonicalising max per value, a compare + select an SGPR pair.
+// (Not inline asm: the compiler inserts no MFMA -> VALU wait states in front of an asm block,
+// and these inputs come straight out of MFMAs.)
+RRL_DEV float relu1(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+// 1 if a relu1 output is non-zero, as an integer bit (no compare mask)
+RRL_DEV uint32_t nonzero_bit(float x) { return min(__float_as_uint(x), 1u); }
+
 RRL_DEV floatx4 mfma_bf16(vbf16x8 a, vbf16x8 b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -146,6 +160,14 @@ RRL_DEV float group_sum_swap(float v) {
   const float s = __uint_as_float(a[0]) + __uint_as_float(a[1]);
   const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
+// Bitwise OR over the 4 lane groups (same lane swaps as group_sum_swap; wave-uniform call site).
+RRL_DEV uint32_t group_or_swap(uint32_t v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  const uint32_t s = a[0] | a[1];
+  const auto b = __builtin_amdgcn_permlane32_swap(s, s, false, false);
+  return b[0] | b[1];
 }
 
 // Sum over the whole wave on the VALU (DPP within 16-lane rows, lane swaps across rows):
@@ -278,7 +300,15 @@ RRL_DEV float wave_sum_vl(float v) {
     st_prev = t_;                                                                       \
   }
 
-template <int DP, int HEAD, int NA, bool STAMP = false>
+// Structural variants of the factored value head (template V, A/B-selectable at run time with
+// tune bit 6, tools/kbench.py --tunes): bit 0 = dh1 from the mask table without the dh2 barrier
+// (else from the hi piece of dh2', rescaled by dout / hi(dout), after a barrier); bit 1 (with
+// bit 0) = the dh2 tiles' vector work runs between dh1's MFMAs and dW1's between dW2's, so each
+// wave's own matrix instructions cover it (otherwise the phases run one after the other).
+// production variant per input width (DP = 8 spills 4 VGPRs with the interleave)
+constexpr int vg_prod_v(int DP) { return DP <= 4 ? 3 : 1; }
+
+template <int DP, int HEAD, int NA, bool STAMP = false, int V = vg_prod_v(DP)>
 __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   unsigned long long st_prev = 0, st_sum[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   extern __shared__ __attribute__((aligned(16))) uint16_t vg_lds[];
@@ -289,12 +319,18 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   static_assert(NA >= 1 && NA <= 6, "NA <= 6 (LDS plan, two field groups)");
   // batch-summed 4-feature fields of the head / bias gradients, folded over the 16 batch
   // lanes by the DPP reduce-scatter: field 0 db2, 1 dW3 row 0, 2 db1, 3 dW3 row 1, 4.. rows 2..
-  // Value head, DP = 4 (the flagship): dh2 = w3 (x) (relu'(h2) * dout) is rank-1 per row, so the
-  // dh2 image holds dh2' = relu'(h2) * dout (each piece = mask * a piece of the ROW's dout: one
-  // split per row, not per element), w3 folds into a stationary A' = W2^T diag(w3) for dh1 and
-  // into the epilogue for dW2 / db2, and dh1 = r * (A' x hi(dh2')) with r = dout / hi(dout)
-  // per row: 3 MFMAs per step instead of 6 (hi(dh2') = mask * hi(dout) is exact in bf16).
-  constexpr bool kFactor = kValue && DP <= 8;
+  // Value head, DP <= 8 (the flagship): dh2 = w3 (x) (relu'(h2) * dout) is rank-1 per row.
+  // w3 folds into a stationary A' = W2^T diag(w3) and into the epilogue of dW2 / db2, so
+  //  * dh1 = dout * (A' x mask) with the exact 0/1 mask relu'(h2): 3 MFMAs per step instead of
+  //    6.  The mask goes to LDS as bits right after layer 2, so the head's barrier publishes it
+  //    and dh1 needs no barrier of its own; a byte of 8 mask bits becomes a B fragment through
+  //    a 256-entry table;
+  //  * dW2 needs dh2' = mask * dout of the wave's OWN 16 features only (A operand): its image
+  //    pieces are mask * the pieces of the row's dout (one split per row, not per element),
+  //    written and read back by the same wave.
+  constexpr bool kFactor = vg_factor(DP, HEAD);
+  constexpr bool kMaskB = kFactor && (V & 1);
+  constexpr bool kInterleave = kMaskB && (V & 2);
   constexpr int NF = NA + 2;
   constexpr int NG = (NF + 3) / 4;  // 16-slot groups (one register each)
   constexpr bool kRedImg = vg_red_in_image(DP, NA);
@@ -305,6 +341,15 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   float* xsb = kRedImg ? tail : tail + 8 * NA * 64;                // [2][64 rows][DP]
   float* vecs = xsb + 2 * 64 * DP;                                 // b1[128] b2[128] w3[NA][128]
   uint16_t* w2lo = reinterpret_cast<uint16_t*>(vecs + (2 + NA) * kVgH + 32);  // [128][kVgLd]
+  uint32_t* mk = reinterpret_cast<uint32_t*>(w2lo + kVgH * kVgLd);  // kFactor: mask bytes [64][4][4]
+  const vbf16x8* mtab = reinterpret_cast<const vbf16x8*>(mk + 64 * 4);  // kFactor: [256]
+  if (kMaskB) {
+    // entry i: element e (feature 8 g + e of a fragment) = 1.0 if bit e of i is set
+    for (int q = threadIdx.x; q < 256 * 4; q += blockDim.x) {
+      const int i = q >> 2, e = 2 * (q & 3);
+      mk[64 * 4 + q] = (((i >> e) & 1) ? 0x3F80u : 0u) | (((i >> (e + 1)) & 1) ? 0x3F800000u : 0u);
+    }
+  }
   int parity = 0;
   constexpr int KS1 = DP / 4;
   const int l = lane_id();
@@ -452,18 +497,32 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 
     // ------------------------------------------------------------ layer 1 (fp32 MFMA)
     uint32_t m1 = 0;  // relu'(h1) bits: 4 bt + r
+    {
+      // all x reads first, then the 4 tiles' MFMAs back to back, then relu + split + stores
+      // (a read placed after the previous tile's image stores would wait for them: LDS alias)
+      float xv[4][KS1];
 #pragma unroll
-    for (int bt = 0; bt < 4; ++bt) {
-      floatx4 acc = *reinterpret_cast<const floatx4*>(b1p);
+      for (int bt = 0; bt < 4; ++bt) {
 #pragma unroll
-      for (int s = 0; s < KS1; ++s) acc = mfma4(w1a[s], xs[(16 * bt + j) * DP + 4 * s + g], acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool pos = acc[r] > 0.f;  // (fmaxf would add a NaN-canonicalising max per value)
-        acc[r] = pos ? acc[r] : 0.f;
-        m1 |= (uint32_t)pos << (4 * bt + r);
+        for (int s = 0; s < KS1; ++s) xv[bt][s] = xs[(16 * bt + j) * DP + 4 * s + g];
       }
-      store_split(h1img, 16 * bt + j, own + 4 * g, acc);
+      const floatx4 b1v = *reinterpret_cast<const floatx4*>(b1p);
+      floatx4 a1[4];
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+        a1[bt] = b1v;
+#pragma unroll
+        for (int s = 0; s < KS1; ++s) a1[bt] = mfma4(w1a[s], xv[bt][s], a1[bt]);
+      }
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a1[bt][r] = relu1(a1[bt][r]);
+          m1 |= nonzero_bit(a1[bt][r]) << (4 * bt + r);
+        }
+        store_split(h1img, 16 * bt + j, own + 4 * g, a1[bt]);
+      }
     }
     __syncthreads();
 
@@ -494,7 +553,29 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 #pragma unroll
     for (int bt = 0; bt < 4; ++bt) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h2[bt][r] = h2[bt][r] > 0.f ? h2[bt][r] : 0.f;
+      for (int r = 0; r < 4; ++r) h2[bt][r] = relu1(h2[bt][r]);
+    }
+    if (kMaskB) {
+      // relu'(h2) bits for dh1's B fragments.  Byte (row, g', c') holds features 32 c' + 8 g' +
+      // {0..7}; this wave's features own + {0..7} / {8..15} are bytes (c' = w / 2, g' = 2 (w & 1)
+      // + 0 / 1).  The 4 lane groups' nibbles of rows 16 bt + j are OR-ed together, then lane
+      // group g writes the 16 bits of row 16 g + j.
+      uint32_t x01 = 0, x23 = 0;
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+        uint32_t nib = 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) nib |= (h2[bt][r] > 0.f ? 1u : 0u) << r;
+        const uint32_t sh = 4 * g + 16 * (bt & 1);
+        if (bt < 2) x01 |= nib << sh;
+        else x23 |= nib << sh;
+      }
+      x01 = group_or_swap(x01);
+      x23 = group_or_swap(x23);
+      const uint32_t u = ((g < 2 ? x01 : x23) >> (16 * (g & 1))) & 0xffffu;
+      uint8_t* mb = reinterpret_cast<uint8_t*>(mk) + (16 * g + j) * 16 + 8 * (w & 1) + (w >> 1);
+      mb[0] = (uint8_t)(u & 0xffu);
+      mb[4] = (uint8_t)(u >> 8);
     }
 
     VG_STAMP(3);
@@ -621,66 +702,157 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     if (kRedImg) __syncthreads();  // every wave read the partials before dh2 overwrites them
 
     VG_STAMP(6);
-    // ------------------------------------------------------------ dh2, dW3, db2
-    float rr[4];  // kFactor: per batch tile, this lane's row correction dout / hi(dout)
+    // ------------------------------------------------------------ dh2, dW3, db2 / dh1, db1
+    floatx4 dh1[4];
+#pragma unroll
+    for (int bt = 0; bt < 4; ++bt) dh1[bt] = zero4();
+    float tb[16];  // db1 partials in entries 8..11 (field 2; the rest stay zero)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) tb[q] = 0.f;
+    auto dh1_relu = [&]() {  // relu'(h1) and the db1 partials
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dh1[bt][r] = ((m1 >> (4 * bt + r)) & 1u) ? dh1[bt][r] : 0.f;
+          tb[8 + r] += dh1[bt][r];
+        }
+      }
+    };
     if (kFactor) {
+      float dv[4];  // dout of this lane's batch row 16 bt + j
+      float rr[4];  // hi-piece variant: dout / hi(dout)
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) dv[bt] = __shfl(dout[0], 16 * bt + j, 64);
       float tv[16];  // fields: db2' (x w3 in the epilogue), dW3 row 0
 #pragma unroll
       for (int e = 0; e < 16; ++e) tv[e] = 0.f;
+      // dh2' pieces of batch tile bt (stores) and its field partials
+      auto kf_tile = [&](const int bt) {
+        {
+          const float v = dv[bt];
+          // the row's dout split once: v = vh + vm + vl
+          uint32_t ph, pm, pl;
+          split2(vf32x2{v, v}, ph, pm, pl);
+          if (!kMaskB) {
+            const float vh = __uint_as_float(ph << 16);
+            rr[bt] = vh != 0.f ? v * __builtin_amdgcn_rcpf(vh) : 0.f;  // 1 ulp: within fp32 accuracy
+          }
+          uint32_t mw[2];  // relu'(h2) of this lane's 4 features as bf16 lane masks
 #pragma unroll
-      for (int bt = 0; bt < 4; ++bt) {
-        const float v = __shfl(dout[0], 16 * bt + j, 64);
-        // the row's dout split once: v = vh + vm + vl
-        uint32_t ph, pm, pl;
-        split2(vf32x2{v, v}, ph, pm, pl);
-        const float vh = __uint_as_float(ph << 16);
-        rr[bt] = vh != 0.f ? v * __builtin_amdgcn_rcpf(vh) : 0.f;  // 1 ulp: within fp32 accuracy
-        uint32_t mw[2];  // relu'(h2) of this lane's 4 features as bf16 lane masks
+          for (int q = 0; q < 2; ++q) {
+            const bool p0 = h2[bt][2 * q] > 0.f, p1 = h2[bt][2 * q + 1] > 0.f;
+            mw[q] = (p0 ? 0x0000ffffu : 0u) | (p1 ? 0xffff0000u : 0u);
+          }
+          Pieces pc;
+          pc.h = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & ph, mw[1] & ph));
+          pc.m = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & pm, mw[1] & pm));
+          pc.l = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & pl, mw[1] & pl));
+          store_pieces(dhimg, 16 * bt + j, own + 4 * g, pc);
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const bool p0 = h2[bt][2 * q] > 0.f, p1 = h2[bt][2 * q + 1] > 0.f;
-          mw[q] = (p0 ? 0x0000ffffu : 0u) | (p1 ? 0xffff0000u : 0u);
+          for (int r = 0; r < 4; ++r) {
+            tv[r] += h2[bt][r] > 0.f ? v : 0.f;
+            tv[4 + r] = fmaf(v, h2[bt][r], tv[4 + r]);
+          }
         }
-        Pieces pc;
-        pc.h = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & ph, mw[1] & ph));
-        pc.m = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & pm, mw[1] & pm));
-        pc.l = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & pl, mw[1] & pl));
-        store_pieces(dhimg, 16 * bt + j, own + 4 * g, pc);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          tv[r] += h2[bt][r] > 0.f ? v : 0.f;
-          tv[4 + r] = fmaf(v, h2[bt][r], tv[4 + r]);
+      };
+      auto kf_finish = [&]() {
+        accv[0] += reduce_scatter16(tv, j);
+        if (kMaskB) {
+          // the dh2' image is read back (dW2) only by the wave that wrote it: in-order LDS
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+          __builtin_amdgcn_wave_barrier();
         }
+      };
+      auto kf_dh2 = [&]() {
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) kf_tile(bt);
+        kf_finish();
+      };
+      auto kf_dh1 = [&]() {
+        if (kMaskB) {
+          // dh1 = dout * (A' x mask), exact: the B fragment of (k-chunk c, batch tile bt) is
+          // the table entry of mask byte (row 16 bt + j, g, c); a row's 4 bytes are one dword
+          uint32_t mrow[4];
+#pragma unroll
+          for (int bt = 0; bt < 4; ++bt) mrow[bt] = mk[(16 * bt + j) * 4 + g];
+          vbf16x8 cur = mtab[mrow[0] & 0xffu];
+#pragma unroll
+          for (int it = 0; it < 16; ++it) {
+            const int c = it >> 2, bt = it & 3;
+            vbf16x8 nxt;
+            if (it + 1 < 16) nxt = mtab[(mrow[(it + 1) & 3] >> (8 * ((it + 1) >> 2))) & 0xffu];
+            dh1[bt] = mfma_bf16(wBl[c % (kFactor ? 4 : 1)], cur, dh1[bt]);
+            dh1[bt] = mfma_bf16(wB[c].m, cur, dh1[bt]);
+            dh1[bt] = mfma_bf16(wB[c].h, cur, dh1[bt]);
+            if (kInterleave) {  // this wave's dh2 work beside its own MFMAs
+              if ((it & 3) == 1) kf_tile(it >> 2);
+              if (it == 15) kf_finish();
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (it + 1 < 16) cur = nxt;
+          }
+        } else {
+          // dh1 = rr * (A' x hi(dh2')): the hi piece alone is exact (mask * hi(dout))
+          vbf16x8 cur = *reinterpret_cast<const vbf16x8*>(dhimg + img_off(j, 8 * g));
+#pragma unroll
+          for (int it = 0; it < 16; ++it) {
+            const int c = it >> 2, bt = it & 3;
+            vbf16x8 nxt;
+            if (it + 1 < 16)
+              nxt = *reinterpret_cast<const vbf16x8*>(
+                  dhimg + img_off(16 * ((it + 1) & 3) + j, 32 * ((it + 1) >> 2) + 8 * g));
+            dh1[bt] = mfma_bf16(wBl[c % (kFactor ? 4 : 1)], cur, dh1[bt]);
+            dh1[bt] = mfma_bf16(wB[c].m, cur, dh1[bt]);
+            dh1[bt] = mfma_bf16(wB[c].h, cur, dh1[bt]);
+            __builtin_amdgcn_sched_barrier(0);
+            if (it + 1 < 16) cur = nxt;
+          }
+        }
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dh1[bt][r] *= kMaskB ? dv[bt] : rr[bt];
+        }
+        dh1_relu();
+      };
+      if (kInterleave) {
+        VG_STAMP(7);
+        kf_dh1();  // (with the dh2 tiles inside)
+      } else {
+        kf_dh2();
+        if (!kMaskB) __syncthreads();  // dh1 reads every wave's hi(dh2') features
+        VG_STAMP(7);
+        kf_dh1();
       }
-      accv[0] += reduce_scatter16(tv, j);
     } else {
       // dout of batch row 16 bt + j comes from lane 16 bt + j (ds_bpermute, no barrier).  Field
       // group 0 (db2, dW3 rows 0 / 1) is folded first; the rows of outputs 2.. (group 1) in a
       // second pass, so only 16 partials are live at a time.
       floatx4 dd[4];
-  #pragma unroll
+#pragma unroll
       for (int bt = 0; bt < 4; ++bt) dd[bt] = zero4();
       {
         float tv[16];  // this slab's field partials of features own + 4g + r
-  #pragma unroll
+#pragma unroll
         for (int e = 0; e < 16; ++e) tv[e] = 0.f;
-  #pragma unroll
+#pragma unroll
         for (int a = 0; a < NA; ++a) {
           const floatx4 w3a = *reinterpret_cast<const floatx4*>(w3p + a * kVgH);
           const int f = a == 0 ? 1 : 3;
-  #pragma unroll
+#pragma unroll
           for (int bt = 0; bt < 4; ++bt) {
             const float v = __shfl(dout[a], 16 * bt + j, 64);
-  #pragma unroll
+#pragma unroll
             for (int r = 0; r < 4; ++r) {
               dd[bt][r] = fmaf(w3a[r], v, dd[bt][r]);
               if (a < 2) tv[4 * f + r] = fmaf(v, h2[bt][r], tv[4 * f + r]);
             }
           }
         }
-  #pragma unroll
+#pragma unroll
         for (int bt = 0; bt < 4; ++bt) {
-  #pragma unroll
+#pragma unroll
           for (int r = 0; r < 4; ++r) {
             dd[bt][r] = h2[bt][r] > 0.f ? dd[bt][r] : 0.f;
             tv[r] += dd[bt][r];
@@ -691,53 +863,23 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       }
       if (NA > 2) {
         float tv[16];
-  #pragma unroll
+#pragma unroll
         for (int e = 0; e < 16; ++e) tv[e] = 0.f;
-  #pragma unroll
+#pragma unroll
         for (int a = 2; a < NA; ++a) {
           const int f = a + 2;  // fields 4 .. NA + 1 -> group 1 (NA <= 6)
-  #pragma unroll
+#pragma unroll
           for (int bt = 0; bt < 4; ++bt) {
             const float v = __shfl(dout[a], 16 * bt + j, 64);
-  #pragma unroll
+#pragma unroll
             for (int r = 0; r < 4; ++r) tv[4 * (f & 3) + r] = fmaf(v, h2[bt][r], tv[4 * (f & 3) + r]);
           }
         }
         accv[1] += reduce_scatter16(tv, j);
       }
-    }
-    __syncthreads();
-
-    VG_STAMP(7);
-    // ------------------------------------------------------------ dh1 (own), dW1, db1
-    floatx4 dh1[4];
-#pragma unroll
-    for (int bt = 0; bt < 4; ++bt) dh1[bt] = zero4();
-    float tb[16];  // db1 partials in entries 8..11 (field 2; the rest stay zero)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) tb[q] = 0.f;
-    if (kFactor) {
-      // dh1 = r * (A' x hi(dh2')): the hi piece alone is exact (mask * hi(dout))
-      vbf16x8 cur = *reinterpret_cast<const vbf16x8*>(dhimg + img_off(j, 8 * g));
-#pragma unroll
-      for (int it = 0; it < 16; ++it) {
-        const int c = it >> 2, bt = it & 3;
-        vbf16x8 nxt;
-        if (it + 1 < 16)
-          nxt = *reinterpret_cast<const vbf16x8*>(
-              dhimg + img_off(16 * ((it + 1) & 3) + j, 32 * ((it + 1) >> 2) + 8 * g));
-        dh1[bt] = mfma_bf16(wBl[c % (kFactor ? 4 : 1)], cur, dh1[bt]);
-        dh1[bt] = mfma_bf16(wB[c].m, cur, dh1[bt]);
-        dh1[bt] = mfma_bf16(wB[c].h, cur, dh1[bt]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (it + 1 < 16) cur = nxt;
-      }
-#pragma unroll
-      for (int bt = 0; bt < 4; ++bt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dh1[bt][r] *= rr[bt];
-      }
-    } else {
+      __syncthreads();
+      VG_STAMP(7);
+      // dh1 (own features) = W2^T dh2
       Split8 cur = frag_row(dhimg, j, 8 * g);
       vbf16x8 bl = frag_tr8(w2lo, 8 * g, own, l);
 #pragma unroll
@@ -753,14 +895,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         if (it + 1 < 16) cur = nxt;
         if (bt == 3 && it + 1 < 16) bl = bln;
       }
-    }
-#pragma unroll
-    for (int bt = 0; bt < 4; ++bt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        dh1[bt][r] = ((m1 >> (4 * bt + r)) & 1u) ? dh1[bt][r] : 0.f;
-        tb[8 + r] += dh1[bt][r];
-      }
+      dh1_relu();
     }
     // dW1 (VALU outer products) and dW2 (MFMA) are independent of each other
     auto do_dw1 = [&]() {
@@ -802,10 +937,56 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         if (it == 7) a = an;
       }
     };
-    // (running dW2 before dW1 on waves 4-7, to pair their MFMAs with waves 0-3's VALU work,
-    // measured 1 % slower and added register pressure: both orders kept the same)
-    do_dw1();
-    do_dw2();
+    // dW2 MFMAs with dW1's vector work between them (kInterleave): step 0 folds db1, then
+    // per 4-column group 4 steps of outer products (x read one step ahead) and one fold
+    auto do_dw2_dw1 = [&]() {
+      VG_STAMP(8);
+      VG_STAMP(9);
+      constexpr int NG1 = DP / 4;
+      static_assert(!kInterleave || 1 + 5 * NG1 <= 16, "dW1 steps must fit in the dW2 loop");
+      Split8 a = frag_tr(dhimg, 0, own, l);
+      Split8 cur = frag_tr(h1img, 0, 0, l);
+      float t1[16];
+      floatx4 xq = *reinterpret_cast<const floatx4*>(xs + j * DP);
+#pragma unroll
+      for (int it = 0; it < 16; ++it) {
+        const int t = it & 7;
+        Split8 nxt, an;
+        if (it + 1 < 16) nxt = frag_tr(h1img, 32 * ((it + 1) >> 3), 16 * ((it + 1) & 7), l);
+        if (it == 7) an = frag_tr(dhimg, 32, own, l);
+        acc2[t] = mma6(a, cur, acc2[t]);
+        if (it == 0) accv[0] += reduce_scatter16(tb, j);
+        if (it >= 1 && it < 1 + 5 * NG1) {
+          const int d4 = (it - 1) / 5, k = (it - 1) % 5;
+          if (k < 4) {
+            if (k == 0) {
+#pragma unroll
+              for (int q = 0; q < 16; ++q) t1[q] = 0.f;
+            }
+            const floatx4 x = xq;
+            // next step's x (tile k + 1 of this group, or tile 0 of the next group)
+            const int nk = k + 1 < 4 ? k + 1 : 0, nd = k + 1 < 4 ? d4 : d4 + 1;
+            if (nd < NG1) xq = *reinterpret_cast<const floatx4*>(xs + (16 * nk + j) * DP + 4 * nd);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) t1[4 * e + r] = fmaf(dh1[k][r], x[e], t1[4 * e + r]);
+            }
+          } else {
+            acc1[d4] += reduce_scatter16(t1, j);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (it + 1 < 16) cur = nxt;
+        if (it == 7) a = an;
+      }
+    };
+    if (kInterleave) {
+      do_dw2_dw1();
+    } else {
+      do_dw1();
+      do_dw2();
+    }
     VG_STAMP(10);
   }
   if (STAMP && p.stamps != nullptr && l == 0) {
@@ -865,34 +1046,46 @@ bool policy_grad_split_supported(int D, int H, int A, int head) {
   return false;
 }
 
-static int g_vg_tune = 0;  // scheduling experiments (bit 0: waves 4-7 at prio 1, bit 1: waves 0-3, bit 3: stamps)
+static int g_vg_tune = 0;  // experiments (bit 0: waves 4-7 at prio 1, bit 1: waves 0-3, bit 3: stamps,
+                           // bit 6: variant V = bits 4..5 of the DP = 4 value kernel)
 static unsigned long long* g_vg_stamps = nullptr;
+
+template <int DP, int HEAD, int NA, bool STAMP, int V>
+static int launch_inst(const GradArgs& a, int grid, hipStream_t s) {
+  constexpr int bytes = vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD);
+  static_assert(bytes <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP, HEAD, NA, STAMP, V>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((value_grad_split_kernel<DP, HEAD, NA, STAMP, V>), dim3(grid), dim3(512), bytes, s, a);
+  return (int)hipGetLastError();
+}
+
+template <int DP, int HEAD, int NA, bool STAMP>
+static int launch_var(const GradArgs& a, int grid, hipStream_t s) {
+  if constexpr (HEAD == HEAD_VALUE_MSE && DP == 4) {
+    if (a.tune & 64) {  // structural A/B (vg_prod_v): V = tune bits 4..5
+      switch ((a.tune >> 4) & 3) {
+        case 0: return launch_inst<DP, HEAD, NA, STAMP, 0>(a, grid, s);
+        case 1: return launch_inst<DP, HEAD, NA, STAMP, 1>(a, grid, s);
+        case 2: return launch_inst<DP, HEAD, NA, STAMP, 2>(a, grid, s);
+        default: return launch_inst<DP, HEAD, NA, STAMP, 3>(a, grid, s);
+      }
+    }
+  }
+  return launch_inst<DP, HEAD, NA, STAMP, vg_prod_v(DP)>(a, grid, s);
+}
 
 template <int DP, int HEAD, int NA>
 static int launch_vg(const GradArgs& a0, int grid, hipStream_t s) {
   GradArgs a = a0;
   a.tune = g_vg_tune;
   a.stamps = g_vg_stamps;
-  constexpr int bytes = vg_lds_bytes(DP, NA);
-  static_assert(bytes <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP, HEAD, NA>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    attr_set = true;
-  }
-  if (a.tune & 8) {  // diagnostic stamps build
-    static bool attr_st = false;
-    if (!attr_st) {
-      (void)hipFuncSetAttribute((const void*)value_grad_split_kernel<DP, HEAD, NA, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-      attr_st = true;
-    }
-    hipLaunchKernelGGL((value_grad_split_kernel<DP, HEAD, NA, true>), dim3(grid), dim3(512), bytes, s, a);
-    return (int)hipGetLastError();
-  }
-  hipLaunchKernelGGL((value_grad_split_kernel<DP, HEAD, NA>), dim3(grid), dim3(512), bytes, s, a);
-  return (int)hipGetLastError();
+  if (a.tune & 8) return launch_var<DP, HEAD, NA, true>(a, grid, s);  // diagnostic stamps build
+  return launch_var<DP, HEAD, NA, false>(a, grid, s);
 }
 
 int launch_value_grad_split(const GradArgs& a, int grid, hipStream_t s) {

@@ -90,6 +90,38 @@ def test_split_kernel_matches_float64(cuda, D, B):
     assert ls[1:4].abs().sum().item() == 0.0
 
 
+@pytest.mark.parametrize("tune", [64, 80, 112])  # V = 0 (hi-piece dh1), 1 (mask table), 3 (+ interleaved vector work)
+@pytest.mark.parametrize("B", [5000, 70000])
+def test_split_kernel_variants_match_float64(cuda, tune, B):
+    """Every structural variant of the factored value head (value_grad.hip vg_prod_v) is as
+    accurate as the fp32 kernel and bitwise deterministic."""
+    from relayrl_prototype_amd.ops import hip
+
+    D, H = 4, 128
+    g = torch.Generator().manual_seed(B + tune)
+    pp = MLPSpec(D, H, 1, False).init(g)
+    pp = pp + 0.05 * torch.randn(pp.shape, generator=g)
+    X = torch.randn(B, D, generator=g) * 1.5
+    ret = torch.randn(B, generator=g) * 20 + 5
+    keep = _away_from_relu_kinks(pp, X, D, H)
+    X, ret = X[keep], ret[keep]
+    B = X.shape[0]
+    g64, loss64 = _grad64(pp, X, ret, D, H, 1.0 / B)
+    old = hip().set_value_grad_tune(tune)
+    try:
+        gs, ls = _run(1, pp.to(cuda), X.to(cuda), ret.to(cuda), H)
+        gs2, _ = _run(1, pp.to(cuda), X.to(cuda), ret.to(cuda), H)
+    finally:
+        hip().set_value_grad_tune(old)
+    gf, _ = _run(0, pp.to(cuda), X.to(cuda), ret.to(cuda), H)
+    scale = g64.abs().max().item()
+    err_split = (gs - g64).abs().max().item() / scale
+    err_fp32 = (gf - g64).abs().max().item() / scale
+    assert err_split < 1e-5 and err_split <= 2.0 * err_fp32 + 2e-7, (err_split, err_fp32)
+    assert abs(ls[0].item() - loss64) <= 1e-5 * abs(loss64) + 1e-6
+    assert torch.equal(gs, gs2)
+
+
 def test_mode_switch_roundtrip(cuda):
     old = set_value_grad_mode(-1)
     assert old in (0, 1)

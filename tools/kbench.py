@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--H", type=int, default=128)
     ap.add_argument("--stamps", action="store_true", help="diagnostic per-segment cycle stamps of the value-grad kernel")
     ap.add_argument("--tunes", default="", help="comma list of value_grad scheduling variants to time too")
+    ap.add_argument("--stamp-tunes", default="", help="comma list of tunes to run the stamps build with")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, H, D = a.B, a.H, 4
@@ -59,10 +60,13 @@ def main():
         us = timeit(lambda: mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret, grad_slab=slab, loss_slab=ls), a.iters)
         res["value_grad_us"] = us
         res["value_grad_TFLOPs_nominal"] = flop_row * B / us / 1e6
-        if a.stamps:
+        stamp_tunes = [0] if a.stamps else []
+        if a.stamp_tunes:
+            stamp_tunes = [int(x) for x in a.stamp_tunes.split(",")]
+        for t in stamp_tunes:
             st = torch.zeros(ns * 8 * 16, dtype=torch.int64, device=dev)
             hip().set_value_grad_stamps(st)
-            old_t = hip().set_value_grad_tune(8)
+            old_t = hip().set_value_grad_tune(8 | t)
             mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret, grad_slab=slab, loss_slab=ls)
             torch.cuda.synchronize()
             hip().set_value_grad_tune(old_t)
@@ -71,7 +75,8 @@ def main():
             names = ["xstore+bar", "layer1+bar", "layer2 mfma", "head partials", "bar3", "dout+prefetch",
                      "dh2+bar", "dh1 mfma", "dW1", "dW2 mfma"]
             res_st = {names[k]: [round(x, 1) for x in seg[:, k].tolist()] for k in range(10)}
-            print(json.dumps({"stamps_cycles_per_slab_per_wave": res_st}))
+            res_st["total_w0_w4"] = [round(float(seg[0, :10].sum()), 1), round(float(seg[4, :10].sum()), 1)]
+            print(json.dumps({"stamps_cycles_per_slab_per_wave": res_st, "tune": t}))
         if a.tunes:
             for t in [int(x) for x in a.tunes.split(",")]:
                 old_t = hip().set_value_grad_tune(t)
