@@ -146,6 +146,17 @@ RRL_DEV floatx4 mma6(const Split8& a, const Split8& b, floatx4 c) {
   return mfma_bf16(a.h, b.h, c);
 }
 
+// The same six products with the roles of the operands exchanged: the transposed tile
+// (b supplies the A operand), e.g. dh1 with batch rows along the registers.
+RRL_DEV floatx4 mma6t(const Split8& a, const Split8& b, floatx4 c) {
+  c = mfma_bf16(b.h, a.l, c);
+  c = mfma_bf16(b.l, a.h, c);
+  c = mfma_bf16(b.m, a.m, c);
+  c = mfma_bf16(b.h, a.m, c);
+  c = mfma_bf16(b.m, a.h, c);
+  return mfma_bf16(b.h, a.h, c);
+}
+
 // Element (row, col) of an activation image.  The 16-byte chunk index (col / 8) is XORed with
 // (row / 4) mod 4: the C-layout stores (16 lanes = 16 consecutive rows, one 8-byte half chunk
 // each) then fall 2-way on the 32 store banks instead of 4-way at the plain 72-dword row
@@ -301,10 +312,11 @@ RRL_DEV float wave_sum_vl(float v) {
   }
 
 // Structural variants of the factored value head (template V, A/B-selectable at run time with
-// tune bit 6, tools/kbench.py --tunes): bit 0 = dh1 from the mask table without the dh2 barrier
+// tune bit 7, V = tune bits 4..6, tools/kbench.py --tunes): bit 0 = dh1 from the mask table without the dh2 barrier
 // (else from the hi piece of dh2', rescaled by dout / hi(dout), after a barrier); bit 1 (with
 // bit 0) = the dh2 tiles' vector work runs between dh1's MFMAs and dW1's between dW2's, so each
-// wave's own matrix instructions cover it (otherwise the phases run one after the other).
+// wave's own matrix instructions cover it (otherwise the phases run one after the other); bit 2 =
+// dW1 on fp32 MFMA tiles at DP = 4 too (12 of its 16 columns idle) instead of vector FMAs.
 // production variant per input width (DP = 8 spills 4 VGPRs with the interleave)
 constexpr int vg_prod_v(int DP) { return DP <= 4 ? 3 : 1; }
 
@@ -318,7 +330,8 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   static_assert(!kValue || NA == 1, "the value head has one output");
   static_assert(NA >= 1 && NA <= 6, "NA <= 6 (LDS plan, two field groups)");
   // batch-summed 4-feature fields of the head / bias gradients, folded over the 16 batch
-  // lanes by the DPP reduce-scatter: field 0 db2, 1 dW3 row 0, 2 db1, 3 dW3 row 1, 4.. rows 2..
+  // lanes by the DPP reduce-scatter: field 0 db2, 1 dW3 row 0, 2 (unused: db1 is summed in
+  // the lane), 3 dW3 row 1, 4.. rows 2..
   // Value head, DP <= 8 (the flagship): dh2 = w3 (x) (relu'(h2) * dout) is rank-1 per row.
   // w3 folds into a stationary A' = W2^T diag(w3) and into the epilogue of dW2 / db2, so
   //  * dh1 = dout * (A' x mask) with the exact 0/1 mask relu'(h2): 3 MFMAs per step instead of
@@ -429,13 +442,22 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 
   floatx4 acc2[8];
   float accv[NG];      // slot j of each 16-slot group of fields (4 features each), batch-summed
-  float acc1[DP / 4];  // dW1[own + 4g + (j & 3)][4 d4 + (j >> 2)], summed over the batch lanes
+  // dW1 / db1 from the TRANSPOSED dh1 tile (lane (j, g) holds rows 16 bt + 4 g + i of
+  // feature own + j): summed inside the lane over the slabs, over the 4 lane groups once in
+  // the epilogue.  DP = 4: vector FMAs on broadcast x rows; wider inputs: fp32 MFMA tiles.
+  constexpr bool kDw1Mfma = DP > 4 || (kFactor && (V & 4));
+  constexpr int NT1 = (DP + 15) / 16;
+  float acc1[kDw1Mfma ? 1 : DP];      // dW1[own + j][d], this lane's rows
+  floatx4 acc1m[kDw1Mfma ? NT1 : 1];  // dW1[own + 4 g + i][16 nt + j]
+  float db1acc = 0.f;                 // db1[own + j], this lane's rows
 #pragma unroll
   for (int it = 0; it < 8; ++it) acc2[it] = zero4();
 #pragma unroll
   for (int q = 0; q < NG; ++q) accv[q] = 0.f;
 #pragma unroll
-  for (int d4 = 0; d4 < DP / 4; ++d4) acc1[d4] = 0.f;
+  for (int d = 0; d < (kDw1Mfma ? 1 : DP); ++d) acc1[d] = 0.f;
+#pragma unroll
+  for (int nt = 0; nt < (kDw1Mfma ? NT1 : 1); ++nt) acc1m[nt] = zero4();
   // db3 / dlog_std: wave w owns output a = w (NA <= 8 waves) and keeps its batch sum in one
   // wave-uniform register, folded over the 64 rows of every slab on the VALU
   float bacc3 = 0.f, dls = 0.f;
@@ -496,7 +518,6 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     VG_STAMP(1);
 
     // ------------------------------------------------------------ layer 1 (fp32 MFMA)
-    uint32_t m1 = 0;  // relu'(h1) bits: 4 bt + r
     {
       // all x reads first, then the 4 tiles' MFMAs back to back, then relu + split + stores
       // (a read placed after the previous tile's image stores would wait for them: LDS alias)
@@ -517,10 +538,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 #pragma unroll
       for (int bt = 0; bt < 4; ++bt) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          a1[bt][r] = relu1(a1[bt][r]);
-          m1 |= nonzero_bit(a1[bt][r]) << (4 * bt + r);
-        }
+        for (int r = 0; r < 4; ++r) a1[bt][r] = relu1(a1[bt][r]);
         store_split(h1img, 16 * bt + j, own + 4 * g, a1[bt]);
       }
     }
@@ -703,25 +721,28 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 
     VG_STAMP(6);
     // ------------------------------------------------------------ dh2, dW3, db2 / dh1, db1
+    // dh1 comes out TRANSPOSED (its MFMAs take the batch-side fragment as the A operand): lane
+    // (j, g) holds dh1[row 16 bt + 4 g + i][feature own + j], i = 0..3.
     floatx4 dh1[4];
 #pragma unroll
     for (int bt = 0; bt < 4; ++bt) dh1[bt] = zero4();
-    float tb[16];  // db1 partials in entries 8..11 (field 2; the rest stay zero)
+    // relu'(h1) of the transposed tile from the h1 image's hi piece (h1 >= 0: hi != 0 iff
+    // h1 > 0), two transposed reads give this lane's 16 rows; then the db1 partial
+    auto dh1_relu = [&]() {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) tb[q] = 0.f;
-    auto dh1_relu = [&]() {  // relu'(h1) and the db1 partials
+      for (int cc = 0; cc < 2; ++cc) {
+        typedef unsigned short vu16x8 __attribute__((ext_vector_type(8)));
+        const vu16x8 hb = __builtin_bit_cast(vu16x8, frag_tr1(h1img, 32 * cc, own, l));
 #pragma unroll
-      for (int bt = 0; bt < 4; ++bt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          dh1[bt][r] = ((m1 >> (4 * bt + r)) & 1u) ? dh1[bt][r] : 0.f;
-          tb[8 + r] += dh1[bt][r];
+        for (int e = 0; e < 8; ++e) {
+          const int bt = 2 * cc + (e >> 2), i = e & 3;
+          dh1[bt][i] = hb[e] != 0 ? dh1[bt][i] : 0.f;
+          db1acc += dh1[bt][i];
         }
       }
     };
     if (kFactor) {
-      float dv[4];  // dout of this lane's batch row 16 bt + j
-      float rr[4];  // hi-piece variant: dout / hi(dout)
+      float dv[4];  // dout of C-layout row 16 bt + j (the dh2' tiles)
 #pragma unroll
       for (int bt = 0; bt < 4; ++bt) dv[bt] = __shfl(dout[0], 16 * bt + j, 64);
       float tv[16];  // fields: db2' (x w3 in the epilogue), dW3 row 0
@@ -729,31 +750,25 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       for (int e = 0; e < 16; ++e) tv[e] = 0.f;
       // dh2' pieces of batch tile bt (stores) and its field partials
       auto kf_tile = [&](const int bt) {
-        {
-          const float v = dv[bt];
-          // the row's dout split once: v = vh + vm + vl
-          uint32_t ph, pm, pl;
-          split2(vf32x2{v, v}, ph, pm, pl);
-          if (!kMaskB) {
-            const float vh = __uint_as_float(ph << 16);
-            rr[bt] = vh != 0.f ? v * __builtin_amdgcn_rcpf(vh) : 0.f;  // 1 ulp: within fp32 accuracy
-          }
-          uint32_t mw[2];  // relu'(h2) of this lane's 4 features as bf16 lane masks
+        const float v = dv[bt];
+        // the row's dout split once: v = vh + vm + vl
+        uint32_t ph, pm, pl;
+        split2(vf32x2{v, v}, ph, pm, pl);
+        uint32_t mw[2];  // relu'(h2) of this lane's 4 features as bf16 lane masks
 #pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const bool p0 = h2[bt][2 * q] > 0.f, p1 = h2[bt][2 * q + 1] > 0.f;
-            mw[q] = (p0 ? 0x0000ffffu : 0u) | (p1 ? 0xffff0000u : 0u);
-          }
-          Pieces pc;
-          pc.h = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & ph, mw[1] & ph));
-          pc.m = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & pm, mw[1] & pm));
-          pc.l = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & pl, mw[1] & pl));
-          store_pieces(dhimg, 16 * bt + j, own + 4 * g, pc);
+        for (int q = 0; q < 2; ++q) {
+          const bool p0 = h2[bt][2 * q] > 0.f, p1 = h2[bt][2 * q + 1] > 0.f;
+          mw[q] = (p0 ? 0x0000ffffu : 0u) | (p1 ? 0xffff0000u : 0u);
+        }
+        Pieces pc;
+        pc.h = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & ph, mw[1] & ph));
+        pc.m = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & pm, mw[1] & pm));
+        pc.l = __builtin_bit_cast(vbf16x4, make_uint2(mw[0] & pl, mw[1] & pl));
+        store_pieces(dhimg, 16 * bt + j, own + 4 * g, pc);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            tv[r] += h2[bt][r] > 0.f ? v : 0.f;
-            tv[4 + r] = fmaf(v, h2[bt][r], tv[4 + r]);
-          }
+        for (int r = 0; r < 4; ++r) {
+          tv[r] += h2[bt][r] > 0.f ? v : 0.f;
+          tv[4 + r] = fmaf(v, h2[bt][r], tv[4 + r]);
         }
       };
       auto kf_finish = [&]() {
@@ -771,8 +786,8 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       };
       auto kf_dh1 = [&]() {
         if (kMaskB) {
-          // dh1 = dout * (A' x mask), exact: the B fragment of (k-chunk c, batch tile bt) is
-          // the table entry of mask byte (row 16 bt + j, g, c); a row's 4 bytes are one dword
+          // dh1^T = dout * (mask x A'^T), exact: the mask fragment of (k-chunk c, batch tile
+          // bt) is the table entry of byte (row 16 bt + j, g, c); a row's 4 bytes are one dword
           uint32_t mrow[4];
 #pragma unroll
           for (int bt = 0; bt < 4; ++bt) mrow[bt] = mk[(16 * bt + j) * 4 + g];
@@ -782,9 +797,9 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
             const int c = it >> 2, bt = it & 3;
             vbf16x8 nxt;
             if (it + 1 < 16) nxt = mtab[(mrow[(it + 1) & 3] >> (8 * ((it + 1) >> 2))) & 0xffu];
-            dh1[bt] = mfma_bf16(wBl[c % (kFactor ? 4 : 1)], cur, dh1[bt]);
-            dh1[bt] = mfma_bf16(wB[c].m, cur, dh1[bt]);
-            dh1[bt] = mfma_bf16(wB[c].h, cur, dh1[bt]);
+            dh1[bt] = mfma_bf16(cur, wBl[c % (kFactor ? 4 : 1)], dh1[bt]);
+            dh1[bt] = mfma_bf16(cur, wB[c].m, dh1[bt]);
+            dh1[bt] = mfma_bf16(cur, wB[c].h, dh1[bt]);
             if (kInterleave) {  // this wave's dh2 work beside its own MFMAs
               if ((it & 3) == 1) kf_tile(it >> 2);
               if (it == 15) kf_finish();
@@ -793,7 +808,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
             if (it + 1 < 16) cur = nxt;
           }
         } else {
-          // dh1 = rr * (A' x hi(dh2')): the hi piece alone is exact (mask * hi(dout))
+          // dh1^T = rr * (hi(dh2') x A'^T): the hi piece alone is exact (mask * hi(dout))
           vbf16x8 cur = *reinterpret_cast<const vbf16x8*>(dhimg + img_off(j, 8 * g));
 #pragma unroll
           for (int it = 0; it < 16; ++it) {
@@ -802,17 +817,23 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
             if (it + 1 < 16)
               nxt = *reinterpret_cast<const vbf16x8*>(
                   dhimg + img_off(16 * ((it + 1) & 3) + j, 32 * ((it + 1) >> 2) + 8 * g));
-            dh1[bt] = mfma_bf16(wBl[c % (kFactor ? 4 : 1)], cur, dh1[bt]);
-            dh1[bt] = mfma_bf16(wB[c].m, cur, dh1[bt]);
-            dh1[bt] = mfma_bf16(wB[c].h, cur, dh1[bt]);
+            dh1[bt] = mfma_bf16(cur, wBl[c % (kFactor ? 4 : 1)], dh1[bt]);
+            dh1[bt] = mfma_bf16(cur, wB[c].m, dh1[bt]);
+            dh1[bt] = mfma_bf16(cur, wB[c].h, dh1[bt]);
             __builtin_amdgcn_sched_barrier(0);
             if (it + 1 < 16) cur = nxt;
           }
         }
+        // per-row scale of the transposed tile (rows 16 bt + 4 g + i): dout, or dout / hi(dout)
+        float sr = dout[0];  // lane l: row l
+        if (!kMaskB) {
+          const float vh = __uint_as_float(cvt_pk_bf16(sr, sr) << 16);
+          sr = vh != 0.f ? sr * __builtin_amdgcn_rcpf(vh) : 0.f;  // 1 ulp: within fp32 accuracy
+        }
 #pragma unroll
         for (int bt = 0; bt < 4; ++bt) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) dh1[bt][r] *= kMaskB ? dv[bt] : rr[bt];
+          for (int i = 0; i < 4; ++i) dh1[bt][i] *= __shfl(sr, 16 * bt + 4 * g + i, 64);
         }
         dh1_relu();
       };
@@ -879,7 +900,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       }
       __syncthreads();
       VG_STAMP(7);
-      // dh1 (own features) = W2^T dh2
+      // dh1^T (own features) = dh2 x W2
       Split8 cur = frag_row(dhimg, j, 8 * g);
       vbf16x8 bl = frag_tr8(w2lo, 8 * g, own, l);
 #pragma unroll
@@ -890,34 +911,54 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         if (it + 1 < 16) nxt = frag_row(dhimg, 16 * ((it + 1) & 3) + j, 32 * ((it + 1) >> 2) + 8 * g);
         if (bt == 3 && it + 1 < 16) bln = frag_tr8(w2lo, 32 * (c + 1) + 8 * g, own, l);
         const Split8 a{wB[c].h, wB[c].m, bl};
-        dh1[bt] = mma6(a, cur, dh1[bt]);
+        dh1[bt] = mma6t(a, cur, dh1[bt]);
         __builtin_amdgcn_sched_barrier(0);
         if (it + 1 < 16) cur = nxt;
         if (bt == 3 && it + 1 < 16) bl = bln;
       }
       dh1_relu();
     }
-    // dW1 (VALU outer products) and dW2 (MFMA) are independent of each other
-    auto do_dw1 = [&]() {
-      VG_STAMP(8);
-      accv[0] += reduce_scatter16(tb, j);
-      // dW1 one group of 4 input columns at a time (16 partials live, whatever D is), each
-      // folded over the 16 batch lanes right away: lane j keeps entry j
+    // dW1 row (16 bt + 4 g + i) of the transposed dh1 tile
+    auto dw1_rows_valu = [&](int bt, int i, const floatx4 (&x)[DP / 4]) {
 #pragma unroll
       for (int d4 = 0; d4 < DP / 4; ++d4) {
-        float t1[16];  // entry 4 e + r of input column 4 d4 + e
 #pragma unroll
-        for (int q = 0; q < 16; ++q) t1[q] = 0.f;
+        for (int e = 0; e < 4; ++e) acc1[(4 * d4 + e) % (kDw1Mfma ? 1 : DP)] =
+            fmaf(dh1[bt][i], x[d4][e], acc1[(4 * d4 + e) % (kDw1Mfma ? 1 : DP)]);
+      }
+    };
+    auto load_xrow = [&](int row, floatx4 (&x)[DP / 4]) {
+#pragma unroll
+      for (int d4 = 0; d4 < DP / 4; ++d4) x[d4] = *reinterpret_cast<const floatx4*>(xs + row * DP + 4 * d4);
+    };
+    auto do_dw1 = [&]() {
+      VG_STAMP(8);
+      if (kDw1Mfma) {
+        // dW1 tile [own features][16 inputs] += dh1^T row block x x: A = the transposed dh1
+        // value (feature own + j, row 16 bt + 4 g + i), B = x[that row][16 nt + j]
 #pragma unroll
         for (int bt = 0; bt < 4; ++bt) {
-          const floatx4 x = *reinterpret_cast<const floatx4*>(xs + (16 * bt + j) * DP + 4 * d4);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
+          for (int i = 0; i < 4; ++i) {
+            const int row = 16 * bt + 4 * g + i;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) t1[4 * e + r] = fmaf(dh1[bt][r], x[e], t1[4 * e + r]);
+            for (int nt = 0; nt < (kDw1Mfma ? NT1 : 1); ++nt) {
+              const int d = 16 * nt + j;
+              const float xb = d < DP ? xs[row * DP + d] : 0.f;
+              acc1m[nt] = mfma4(dh1[bt][i], xb, acc1m[nt]);
+            }
           }
         }
-        acc1[d4] += reduce_scatter16(t1, j);
+      } else {
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            floatx4 x[DP / 4];
+            load_xrow(16 * bt + 4 * g + i, x);
+            dw1_rows_valu(bt, i, x);
+          }
+        }
       }
     };
     // ------------------------------------------------------------ dW2 += dh2 h1^T
@@ -937,17 +978,15 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         if (it == 7) a = an;
       }
     };
-    // dW2 MFMAs with dW1's vector work between them (kInterleave): step 0 folds db1, then
-    // per 4-column group 4 steps of outer products (x read one step ahead) and one fold
+    // dW2 MFMAs with dW1 vector work between them (kInterleave, DP = 4): one dh1 row per
+    // step, its x row read one step ahead
     auto do_dw2_dw1 = [&]() {
       VG_STAMP(8);
       VG_STAMP(9);
-      constexpr int NG1 = DP / 4;
-      static_assert(!kInterleave || 1 + 5 * NG1 <= 16, "dW1 steps must fit in the dW2 loop");
       Split8 a = frag_tr(dhimg, 0, own, l);
       Split8 cur = frag_tr(h1img, 0, 0, l);
-      float t1[16];
-      floatx4 xq = *reinterpret_cast<const floatx4*>(xs + j * DP);
+      floatx4 xq[DP / 4];
+      load_xrow(4 * g, xq);
 #pragma unroll
       for (int it = 0; it < 16; ++it) {
         const int t = it & 7;
@@ -955,33 +994,19 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         if (it + 1 < 16) nxt = frag_tr(h1img, 32 * ((it + 1) >> 3), 16 * ((it + 1) & 7), l);
         if (it == 7) an = frag_tr(dhimg, 32, own, l);
         acc2[t] = mma6(a, cur, acc2[t]);
-        if (it == 0) accv[0] += reduce_scatter16(tb, j);
-        if (it >= 1 && it < 1 + 5 * NG1) {
-          const int d4 = (it - 1) / 5, k = (it - 1) % 5;
-          if (k < 4) {
-            if (k == 0) {
+        {
+          floatx4 xc[DP / 4];
 #pragma unroll
-              for (int q = 0; q < 16; ++q) t1[q] = 0.f;
-            }
-            const floatx4 x = xq;
-            // next step's x (tile k + 1 of this group, or tile 0 of the next group)
-            const int nk = k + 1 < 4 ? k + 1 : 0, nd = k + 1 < 4 ? d4 : d4 + 1;
-            if (nd < NG1) xq = *reinterpret_cast<const floatx4*>(xs + (16 * nk + j) * DP + 4 * nd);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) t1[4 * e + r] = fmaf(dh1[k][r], x[e], t1[4 * e + r]);
-            }
-          } else {
-            acc1[d4] += reduce_scatter16(t1, j);
-          }
+          for (int d4 = 0; d4 < DP / 4; ++d4) xc[d4] = xq[d4];
+          if (it + 1 < 16) load_xrow(16 * ((it + 1) >> 2) + 4 * g + ((it + 1) & 3), xq);
+          dw1_rows_valu(it >> 2, it & 3, xc);
         }
         __builtin_amdgcn_sched_barrier(0);
         if (it + 1 < 16) cur = nxt;
         if (it == 7) a = an;
       }
     };
-    if (kInterleave) {
+    if (kInterleave && !kDw1Mfma) {
       do_dw2_dw1();
     } else {
       do_dw1();
@@ -1009,13 +1034,28 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     const int f = 4 * q + (j >> 2), feat = own + 4 * g + (j & 3);
     if (f < NF) {
       const int off = f == 0 ? o.b2 : f == 1 ? o.w3 : f == 2 ? o.b1 : o.w3 + (f == 3 ? 1 : f - 2) * kVgH;
-      slab[off + feat] = (kFactor && f == 0) ? accv[q] * P[o.w3 + feat] : accv[q];
+      if (f != 2) slab[off + feat] = (kFactor && f == 0) ? accv[q] * P[o.w3 + feat] : accv[q];
     }
   }
+  if (kDw1Mfma) {
 #pragma unroll
-  for (int d4 = 0; d4 < DP / 4; ++d4) {
-    const int f = own + 4 * g + (j & 3), dd = 4 * d4 + (j >> 2);
-    if (dd < D) slab[o.w1 + f * D + dd] = acc1[d4];
+    for (int nt = 0; nt < (kDw1Mfma ? NT1 : 1); ++nt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int d = 16 * nt + j;
+        if (d < D) slab[o.w1 + (own + 4 * g + i) * D + d] = acc1m[nt][i];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int d = 0; d < (kDw1Mfma ? 1 : DP); ++d) {
+      const float sd = group_sum_swap(acc1[d]);  // over the 4 lane groups (all lanes call)
+      if (g == (d & 3) && d < D) slab[o.w1 + (own + j) * D + d] = sd;
+    }
+  }
+  {
+    const float sb = group_sum_swap(db1acc);
+    if (g == 0) slab[o.b1 + own + j] = sb;
   }
   if (w < NA && l == 0) {
     slab[o.b3 + w] = bacc3;
@@ -1047,7 +1087,7 @@ bool policy_grad_split_supported(int D, int H, int A, int head) {
 }
 
 static int g_vg_tune = 0;  // experiments (bit 0: waves 4-7 at prio 1, bit 1: waves 0-3, bit 3: stamps,
-                           // bit 6: variant V = bits 4..5 of the DP = 4 value kernel)
+                           // bit 7: variant V = bits 4..6 of the DP = 4 value kernel)
 static unsigned long long* g_vg_stamps = nullptr;
 
 template <int DP, int HEAD, int NA, bool STAMP, int V>
@@ -1067,12 +1107,14 @@ static int launch_inst(const GradArgs& a, int grid, hipStream_t s) {
 template <int DP, int HEAD, int NA, bool STAMP>
 static int launch_var(const GradArgs& a, int grid, hipStream_t s) {
   if constexpr (HEAD == HEAD_VALUE_MSE && DP == 4) {
-    if (a.tune & 64) {  // structural A/B (vg_prod_v): V = tune bits 4..5
-      switch ((a.tune >> 4) & 3) {
+    if (a.tune & 128) {  // structural A/B (vg_prod_v): V = tune bits 4..6
+      switch ((a.tune >> 4) & 7) {
         case 0: return launch_inst<DP, HEAD, NA, STAMP, 0>(a, grid, s);
         case 1: return launch_inst<DP, HEAD, NA, STAMP, 1>(a, grid, s);
-        case 2: return launch_inst<DP, HEAD, NA, STAMP, 2>(a, grid, s);
-        default: return launch_inst<DP, HEAD, NA, STAMP, 3>(a, grid, s);
+        case 3: return launch_inst<DP, HEAD, NA, STAMP, 3>(a, grid, s);
+        case 5: return launch_inst<DP, HEAD, NA, STAMP, 5>(a, grid, s);
+        case 7: return launch_inst<DP, HEAD, NA, STAMP, 7>(a, grid, s);
+        default: break;
       }
     }
   }
