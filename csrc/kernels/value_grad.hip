@@ -66,7 +66,24 @@ constexpr int vg_lds_bytes(int DP, int NA) {
 // byte -> 8 bf16 {0, 1} [256][8] that turns a byte into a dh1 B fragment.
 constexpr bool vg_factor(int DP, int HEAD) { return HEAD == HEAD_VALUE_MSE && DP <= 8; }
 constexpr int vg_mask_bytes(int DP, int HEAD) { return vg_factor(DP, HEAD) ? 64 * 16 + 256 * 16 : 0; }
-static_assert(vg_lds_bytes(8, 1) + vg_mask_bytes(8, HEAD_VALUE_MSE) <= 160 * 1024, "factored LDS plan");
+// The slab's head inputs, DMA'd from global memory: ret, or adv / logp_old / act (actc [64][NA]
+// for a Gaussian head).  Inside the dh2 image after the head partials when those live there.
+// (Policy heads only: the value head keeps its x slab and ret prefetched in registers, which
+// measured ~1-3 % faster there; the DMA path won 6 % on the register-starved Gaussian head.)
+constexpr int vg_hbuf_bytes(int HEAD, int NA) {
+  return HEAD == HEAD_VALUE_MSE ? 0 : 64 * 4 * (2 + ((HEAD == HEAD_PG_GAUSS || HEAD == HEAD_PPO_GAUSS) ? NA : 1));
+}
+// Outside the image the head inputs are double-buffered (DMA'd a slab ahead) when LDS allows.
+constexpr bool vg_hbuf2(int DP, int HEAD, int NA) {
+  return !vg_red_in_image(DP, NA) &&
+         vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD) + 2 * vg_hbuf_bytes(HEAD, NA) <= 160 * 1024;
+}
+constexpr int vg_total_bytes(int DP, int HEAD, int NA) {
+  return vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD) +
+         (vg_red_in_image(DP, NA) ? 0 : (vg_hbuf2(DP, HEAD, NA) ? 2 : 1) * vg_hbuf_bytes(HEAD, NA));
+}
+static_assert(vg_red_bytes(6) + vg_hbuf_bytes(HEAD_PPO_GAUSS, 6) <= 3 * kVgImg * 2, "head inputs in the dh2 image");
+static_assert(vg_total_bytes(8, HEAD_VALUE_MSE, 1) <= 160 * 1024, "factored LDS plan");
 static_assert(vg_lds_bytes(24, 1) <= 160 * 1024 && !vg_red_in_image(24, 1), "value-grad LDS plan");
 static_assert(vg_lds_bytes(20, 6) <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
 static_assert(vg_red_bytes(6) <= 3 * kVgImg * 2, "head partials must fit in the dh2 image");
@@ -356,6 +373,10 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   uint16_t* w2lo = reinterpret_cast<uint16_t*>(vecs + (2 + NA) * kVgH + 32);  // [128][kVgLd]
   uint32_t* mk = reinterpret_cast<uint32_t*>(w2lo + kVgH * kVgLd);  // kFactor: mask bytes [64][4][4]
   const vbf16x8* mtab = reinterpret_cast<const vbf16x8*>(mk + 64 * 4);  // kFactor: [256]
+  // head inputs of the current slab: [0, 64) ret or adv, [64, 128) logp_old, [128, ..) act
+  // (int bits) or actc [64][NA]
+  float* hbuf0 = kRedImg ? red + 8 * NA * 64
+                         : reinterpret_cast<float*>(reinterpret_cast<char*>(mk) + vg_mask_bytes(DP, HEAD));
   if (kMaskB) {
     // entry i: element e (feature 8 g + e of a fragment) = 1.0 if bit e of i is set
     for (int q = threadIdx.x; q < 256 * 4; q += blockDim.x) {
@@ -463,58 +484,93 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   float bacc3 = 0.f, dls = 0.f;
   float s_loss = 0.f, s_val = 0.f, s_cnt = 0.f, s_ent = 0.f, s_kl = 0.f, s_clip = 0.f;
 
-  // Per-slab global inputs are prefetched one slab ahead into registers (issue early, write
-  // late): the x slab (XQ values per thread) and this lane's head inputs for its 4 batch rows
-  // 16 bt + j (ret; or adv / act / logp_old, and the NA action values of a Gaussian head).
-  // The next slab's loads are issued right after this slab's head consumed the current
-  // ones, so their latency hides under the backward MFMA work.
-  constexpr int XQ = (64 * DP + 511) / 512;
+  // Global inputs go straight to LDS by DMA (global_load_lds_dword: lane l's dword lands at
+  // the wave-uniform destination + 4 l), so no register holds them across the slab (held in
+  // registers they were spilled under the Gaussian heads' pressure, and every spill store
+  // waited for its HBM load).  The x slab [64][D] (compact, row stride D) is issued one slab
+  // ahead into the other half of the double buffer; the head inputs at the top of their own
+  // slab, behind ~6,000 cycles of layer 1 + layer 2.  The issuing waves wait for their DMAs
+  // (vmcnt) before the barrier that publishes them.  Rows past B load clamped duplicates:
+  // finite, and their dout is 0.
   constexpr int NC = kGauss ? NA : 1;
-  float xr[XQ];
-  float hin, hlp;  // this lane's row: ret (value) or adv (policy); logp_old
-  int hact;
-  float hac[NC];   // Gaussian action
-  auto prefetch = [&](int b0) {
-    // unconditional loads from clamped addresses: nothing here consumes a loaded value (a
-    // select on it would make the compiler wait for the load right away); padding columns /
-    // rows past B are zeroed where the values are used
-#pragma unroll
-    for (int i = 0; i < XQ; ++i) {
-      const int q = min((int)threadIdx.x + 512 * i, 64 * DP - 1);
-      const int rl = q / DP, d = q % DP, b = b0 + rl;
-      xr[i] = p.X[(size_t)min(b, p.B - 1) * D + min(d, D - 1)];
-    }
-    const int bc = min(b0 + l, p.B - 1);  // lane l handles batch row l of the slab in the head
-    if (kValue) {
-      hin = p.ret[bc];
-    } else {
-      hin = p.adv[bc];
-      hlp = (p.logp_old ? p.logp_old : p.adv)[bc];
-      if (kGauss) {
-#pragma unroll
-        for (int a = 0; a < NC; ++a) hac[a] = p.actc[(size_t)bc * NA + a];
-      } else {
-        hact = p.act[bc];
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto dma = [&](const void* src, long n, long first, float* dst, int chunks, int w0) {
+    for (int k = 0; k < chunks; ++k) {
+      if (((k + w0) & 7) == wu) {
+        const long e = min(first + 64L * k + l, n - 1);
+        __builtin_amdgcn_global_load_lds(static_cast<const uint32_t*>(src) + e,
+                                         (__attribute__((address_space(3))) void*)(dst + 64 * k), 4, 0, 0);
       }
     }
   };
-  prefetch(blockIdx.x * 64);
+  // x slab by DMA in the [64][DP] layout: chunk k covers LDS floats 64 k .. 64 k + 63 and lane
+  // l loads element (row q / DP, column min(q % DP, D - 1)) of q = 64 k + l, so a padding
+  // column holds a finite duplicate -- layer 1 multiplies it by W1's zero padding and dW1's
+  // padding outputs are never written.  (A compact stride-D layout needed per-read address
+  // arithmetic and selects: +2,500 cycles per slab at D = 17.)
+  // Value heads instead prefetch the x slab (XQ values per thread) and ret into registers a
+  // slab ahead (issued right after the head, stored to LDS at the next slab's top).
+  constexpr bool kDmaIn = !kValue;
+  constexpr int XQ = (64 * DP + 511) / 512;
+  float xr[kDmaIn ? 1 : XQ];
+  float hin_r = 0.f;
+  auto prefetch_x = [&](int b0, float* dst) {
+    if (kDmaIn) {
+      // this wave's chunks k = w, w + 8, ..: a runtime loop, so no per-chunk address is
+      // hoisted out of the slab loop into a live register
+      for (int k = wu; k < DP; k += 8) {
+        const int q = 64 * k + l, row = q / DP, d = q % DP;
+        const long e = (long)min(b0 + row, p.B - 1) * D + min(d, D - 1);
+        __builtin_amdgcn_global_load_lds(static_cast<const uint32_t*>(static_cast<const void*>(p.X)) + e,
+                                         (__attribute__((address_space(3))) void*)(dst + 64 * k), 4, 0, 0);
+      }
+    } else {
+      // unconditional loads from clamped addresses: nothing here consumes a loaded value (a
+      // select on it would make the compiler wait for the load right away)
+#pragma unroll
+      for (int i = 0; i < (kDmaIn ? 1 : XQ); ++i) {
+        const int q = min((int)threadIdx.x + 512 * i, 64 * DP - 1);
+        const int rl = q / DP, d = q % DP, b = b0 + rl;
+        xr[i] = p.X[(size_t)min(b, p.B - 1) * D + min(d, D - 1)];
+      }
+      hin_r = p.ret[min(b0 + l, p.B - 1)];
+    }
+  };
+  constexpr bool kHb2 = kDmaIn && vg_hbuf2(DP, HEAD, NA);
+  constexpr int HBF = vg_hbuf_bytes(HEAD, NA) / 4;  // floats per head-input buffer
+  auto dma_head = [&](int b0, float* hbuf) {
+    if (kDmaIn) {
+      dma(p.adv, p.B, b0, hbuf, 1, 3);
+      if (p.logp_old) dma(p.logp_old, p.B, b0, hbuf + 64, 1, 4);
+      if (kGauss) dma(p.actc, (long)p.B * NA, (long)b0 * NA, hbuf + 128, NA, 5);
+      else dma(p.act, p.B, b0, hbuf + 128, 1, 5);
+    }
+  };
+  auto vm_wait0 = []() { __builtin_amdgcn_s_waitcnt(0x0F70); };  // vmcnt(0) only
+  prefetch_x(blockIdx.x * 64, xsb);
+  if (kHb2) dma_head(blockIdx.x * 64, hbuf0);
   if ((p.tune & 1) && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   if ((p.tune & 2) && __builtin_amdgcn_readfirstlane(threadIdx.x) < 256) __builtin_amdgcn_s_setprio(1);
 
   for (int base = blockIdx.x * 64; base < p.B; base += gridDim.x * 64) {
     VG_STAMP(0);
-    // ------------------------------------------------------------ x slab -> LDS
-    // (double-buffered by slab parity: the buffer written here was last read two slabs ago)
+    // ------------------------------------------------------------ x slab (DMA'd a slab ago)
+    // (double-buffered by slab parity: the next slab's DMA targets the other half)
     float* xs = xsb + (parity & 1) * 64 * DP;
+    float* hbuf = hbuf0 + (kHb2 ? (parity & 1) * HBF : 0);
     parity ^= 1;
+    if (kDmaIn) {
+      vm_wait0();
+    } else {
 #pragma unroll
-    for (int i = 0; i < XQ; ++i) {
-      const int q = (int)threadIdx.x + 512 * i;
-      const int rl = q / DP, d = q % DP;
-      if (q < 64 * DP) xs[q] = (base + rl < p.B && d < D) ? xr[i] : 0.f;
+      for (int i = 0; i < (kDmaIn ? 1 : XQ); ++i) {
+        const int q = (int)threadIdx.x + 512 * i;
+        const int rl = q / DP, d = q % DP;
+        if (q < 64 * DP) xs[q] = (base + rl < p.B && d < D) ? xr[i] : 0.f;
+      }
     }
-    __syncthreads();  // x visible; the previous slab's readers of both images are done
+    __syncthreads();  // x (and kHb2 head inputs) visible; the previous slab's readers are done
+    if (kDmaIn && !kHb2) dma_head(base, hbuf);
     VG_STAMP(1);
 
     // ------------------------------------------------------------ layer 1 (fp32 MFMA)
@@ -614,6 +670,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       if (NA > 2) __builtin_amdgcn_sched_barrier(0);
     }
     VG_STAMP(4);
+    if (kDmaIn && !kHb2) vm_wait0();  // this wave's head-input DMAs
     __syncthreads();
     VG_STAMP(5);
     // loss head: lane l handles batch row l (every wave computes the same 64 rows; wave 0's
@@ -625,6 +682,12 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       const int b = base + l;
       const bool ok = b < p.B;
       const int bc = min(b, p.B - 1);
+      const float hin = kDmaIn ? hbuf[l] : hin_r;
+      const float hlp = kValue ? 0.f : hbuf[64 + l];
+      const int hact = (kValue || kGauss) ? 0 : __float_as_int(hbuf[128 + l]);
+      float hac[NC];
+#pragma unroll
+      for (int a = 0; a < NC; ++a) hac[a] = kGauss ? hbuf[128 + l * NC + a] : 0.f;
       float outv[NA];
 #pragma unroll
       for (int a = 0; a < NA; ++a) {
@@ -715,8 +778,11 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         if (kGauss) dls += wave_sum_vl(ml);
       }
     }
-    // the head consumed this slab's inputs: issue the next slab's loads now
-    if (base + (int)gridDim.x * 64 < p.B) prefetch(base + gridDim.x * 64);
+    // the head consumed this slab's inputs: issue the next slab's x DMA now
+    if (base + (int)gridDim.x * 64 < p.B) {
+      prefetch_x(base + gridDim.x * 64, xsb + (parity & 1) * 64 * DP);
+      if (kHb2) dma_head(base + gridDim.x * 64, hbuf0 + (parity & 1) * HBF);
+    }
     if (kRedImg) __syncthreads();  // every wave read the partials before dh2 overwrites them
 
     VG_STAMP(6);
@@ -1092,7 +1158,7 @@ static unsigned long long* g_vg_stamps = nullptr;
 
 template <int DP, int HEAD, int NA, bool STAMP, int V>
 static int launch_inst(const GradArgs& a, int grid, hipStream_t s) {
-  constexpr int bytes = vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD);
+  constexpr int bytes = vg_total_bytes(DP, HEAD, NA);
   static_assert(bytes <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
   static bool attr_set = false;
   if (!attr_set) {

@@ -19,6 +19,27 @@ from relayrl_prototype_amd.ops import FwdMode, GradHead, MLPSpec, hip, mlp_forwa
 from relayrl_prototype_amd.ops import reduce_slabs
 
 
+STAMP_NAMES = ["xstore+bar", "layer1+bar", "layer2 mfma", "head partials", "bar3", "dout+prefetch",
+               "dh2+bar", "dh1 mfma", "dW1", "dW2 mfma"]
+
+
+def run_stamps(fn, ns, tune, label, rows):
+    """Per-segment cycles per 64-row slab of the value-grad kernel (diagnostic stamps build)."""
+    dev = torch.device("cuda")
+    st = torch.zeros(ns * 8 * 16, dtype=torch.int64, device=dev)
+    hip().set_value_grad_stamps(st)
+    old_t = hip().set_value_grad_tune(8 | tune)
+    fn()
+    torch.cuda.synchronize()
+    hip().set_value_grad_tune(old_t)
+    hip().set_value_grad_stamps(torch.empty(0, device=dev))
+    slabs_per_wg = rows / 64 / ns
+    seg = st.view(ns, 8, 16).double().mean(0) / slabs_per_wg
+    res = {STAMP_NAMES[k]: [round(x, 1) for x in seg[:, k].tolist()] for k in range(10)}
+    res["total_w0_w4"] = [round(float(seg[0, :10].sum()), 1), round(float(seg[4, :10].sum()), 1)]
+    print(json.dumps({"stamps_cycles_per_slab_per_wave": res, "tune": tune, "kernel": label}))
+
+
 def timeit(fn, iters, warmup=3):
     for _ in range(warmup):
         fn()
@@ -64,19 +85,8 @@ def main():
         if a.stamp_tunes:
             stamp_tunes = [int(x) for x in a.stamp_tunes.split(",")]
         for t in stamp_tunes:
-            st = torch.zeros(ns * 8 * 16, dtype=torch.int64, device=dev)
-            hip().set_value_grad_stamps(st)
-            old_t = hip().set_value_grad_tune(8 | t)
-            mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret, grad_slab=slab, loss_slab=ls)
-            torch.cuda.synchronize()
-            hip().set_value_grad_tune(old_t)
-            hip().set_value_grad_stamps(torch.empty(0, device=dev))
-            seg = st.view(ns, 8, 16).double().mean(0) / (B / 64 / ns)  # cycles per slab, per wave x segment
-            names = ["xstore+bar", "layer1+bar", "layer2 mfma", "head partials", "bar3", "dout+prefetch",
-                     "dh2+bar", "dh1 mfma", "dW1", "dW2 mfma"]
-            res_st = {names[k]: [round(x, 1) for x in seg[:, k].tolist()] for k in range(10)}
-            res_st["total_w0_w4"] = [round(float(seg[0, :10].sum()), 1), round(float(seg[4, :10].sum()), 1)]
-            print(json.dumps({"stamps_cycles_per_slab_per_wave": res_st, "tune": t}))
+            run_stamps(lambda: mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret, grad_slab=slab, loss_slab=ls),
+                       ns, t, "value", B)
         if a.tunes:
             for t in [int(x) for x in a.tunes.split(",")]:
                 old_t = hip().set_value_grad_tune(t)
@@ -113,14 +123,18 @@ def main():
         fn = lambda: mlp_grad(GradHead.PPO_GAUSS, pg, Xg, Ag, H, actc=actc, adv=adv, logp_old=lpo, adv_stats=st,  # noqa
                               grad_slab=slab, loss_slab=ls)
         res["ppo_gauss_split_us"] = timeit(fn, a.iters)
+        if a.stamps:
+            run_stamps(fn, ns, 0, "ppo_gauss", B)
         old = hip().set_value_grad_mode(0)
         res["ppo_gauss_fp32mfma_us"] = timeit(fn, a.iters)
         hip().set_value_grad_mode(old)
         Xv = Xg
         pv17 = MLPSpec(Dg, H, 1).init(g).to(dev)
         slabv = torch.empty(ns, pv17.numel(), device=dev)
-        res["value_grad_d17_us"] = timeit(lambda: mlp_grad(GradHead.VALUE_MSE, pv17, Xv, 1, H, ret=ret,
-                                                           grad_slab=slabv, loss_slab=ls), a.iters)
+        fv = lambda: mlp_grad(GradHead.VALUE_MSE, pv17, Xv, 1, H, ret=ret, grad_slab=slabv, loss_slab=ls)  # noqa
+        res["value_grad_d17_us"] = timeit(fv, a.iters)
+        if a.stamps:
+            run_stamps(fv, ns, 0, "value_d17", B)
     if a.which in ("fwd", "all"):
         out = {"v": torch.empty(B, device=dev)}
         us = timeit(lambda: mlp_forward(FwdMode.VALUE, pv, X, 1, H, out=out), a.iters)
