@@ -113,12 +113,13 @@ RRL_DEV vf32x2 unpack_bf16(uint32_t p) {
 }
 // x = hi + mid + lo, each piece rounded to nearest: 3 converts, 2 unpacks and 2 packed
 // subtracts per pair of values.
+// (Scalar subtracts, not a packed v_pk_add_f32: packed f32 VALU beside MFMAs costs more.)
 RRL_DEV void split2(vf32x2 v, uint32_t& h, uint32_t& m, uint32_t& lo) {
   h = cvt_pk_bf16(v.x, v.y);
-  const vf32x2 r1 = v - unpack_bf16(h);
-  m = cvt_pk_bf16(r1.x, r1.y);
-  const vf32x2 r2 = r1 - unpack_bf16(m);
-  lo = cvt_pk_bf16(r2.x, r2.y);
+  const float r1x = v.x - __uint_as_float(h << 16), r1y = v.y - __uint_as_float(h & 0xffff0000u);
+  m = cvt_pk_bf16(r1x, r1y);
+  const float r2x = r1x - __uint_as_float(m << 16), r2y = r1y - __uint_as_float(m & 0xffff0000u);
+  lo = cvt_pk_bf16(r2x, r2y);
 }
 RRL_DEV void split4(const floatx4 v, vbf16x4& h, vbf16x4& m, vbf16x4& lo) {
   uint32_t h0, m0, l0, h1, m1, l1;

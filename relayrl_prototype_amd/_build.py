@@ -87,6 +87,12 @@ def _torch_flags():
     return inc, cflags, ldflags
 
 
+# Per-kernel compiler flags.  value_grad.hip: no SLP vectorisation -- packed f32 VALU
+# (v_pk_fma_f32 / v_pk_mul_f32) beside MFMAs costs ~22 cycles more than two plain FMAs on
+# gfx950, and the packed temporaries raised register pressure (spills) in the policy heads.
+FILE_FLAGS = {"value_grad.hip": ["-fno-slp-vectorize"]}
+
+
 def build_hip(verbose=False, force=False) -> str:
     kdir = os.path.join(CSRC, "kernels")
     srcs = sorted(glob.glob(os.path.join(kdir, "*.hip")))
@@ -100,7 +106,8 @@ def build_hip(verbose=False, force=False) -> str:
         objs.append(o)
         if force or _newer(o, [s] + headers):
             jobs.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-                         "-munsafe-fp-atomics", "-I", kdir, "-c", s, "-o", o])
+                         "-munsafe-fp-atomics", *FILE_FLAGS.get(os.path.basename(s), []), "-I", kdir, "-c", s,
+                         "-o", o])
     tinc, tcf, tld = _torch_flags()
     bindings = [binding] + sorted(b for b in glob.glob(os.path.join(CSRC, "bindings", "*_ops.cpp")) if b != binding)
     for bsrc in bindings:

@@ -1,6 +1,6 @@
 #!/bin/bash
 # usage: tools_resusage.sh file.hip  -> one line per kernel: name VGPR AGPR spill occupancy LDS
-hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c "$1" -o /tmp/_ru.o -Rpass-analysis=kernel-resource-usage 2>&1 | \
+hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC ${RU_FLAGS} -c "$1" -o /tmp/_ru.o -Rpass-analysis=kernel-resource-usage 2>&1 | \
 python3 -c '
 import sys,re
 cur=None;rows=[]

@@ -13,7 +13,13 @@ import torch
 from relayrl_prototype_amd.runtime.vec_trainer import VecTrainer, VecTrainerConfig
 
 
+REF = "--ref" in sys.argv  # the reference hyperparameters (80 value iterations per epoch)
+
+
 def cfg(**kw):
+    if REF:
+        return VecTrainerConfig(num_envs=1024, rollout_len=64, with_baseline=True, pi_lr=3e-4, vf_lr=1e-3,
+                                train_vf_iters=80, gamma=0.98, lam=0.97, seed=1, **kw)
     return VecTrainerConfig(num_envs=1024, rollout_len=64, with_baseline=True, pi_lr=1e-2, vf_lr=3e-3,
                             train_vf_iters=10, gamma=0.99, lam=0.95, seed=1, **kw)
 
