@@ -87,10 +87,11 @@ def _torch_flags():
     return inc, cflags, ldflags
 
 
-# Per-kernel compiler flags.  value_grad.hip: no SLP vectorisation -- packed f32 VALU
-# (v_pk_fma_f32 / v_pk_mul_f32) beside MFMAs costs ~22 cycles more than two plain FMAs on
-# gfx950, and the packed temporaries raised register pressure (spills) in the policy heads.
-FILE_FLAGS = {"value_grad.hip": ["-fno-slp-vectorize"]}
+# Compiler flags for the HIP kernels: no SLP vectorisation -- packed f32 VALU (v_pk_fma_f32 /
+# v_pk_mul_f32) beside MFMAs costs ~22 cycles more than two plain FMAs on gfx950, and the
+# packed temporaries raised register pressure (spills in the value/policy-grad kernel).
+HIP_FLAGS = ["-fno-slp-vectorize"]
+FILE_FLAGS = {}
 
 
 def build_hip(verbose=False, force=False) -> str:
@@ -106,7 +107,8 @@ def build_hip(verbose=False, force=False) -> str:
         objs.append(o)
         if force or _newer(o, [s] + headers):
             jobs.append([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-                         "-munsafe-fp-atomics", *FILE_FLAGS.get(os.path.basename(s), []), "-I", kdir, "-c", s,
+                         "-munsafe-fp-atomics", *HIP_FLAGS, *FILE_FLAGS.get(os.path.basename(s), []), "-I", kdir,
+                         "-c", s,
                          "-o", o])
     tinc, tcf, tld = _torch_flags()
     bindings = [binding] + sorted(b for b in glob.glob(os.path.join(CSRC, "bindings", "*_ops.cpp")) if b != binding)
