@@ -1154,7 +1154,7 @@ bool policy_grad_split_supported(int D, int H, int A, int head) {
 }
 
 static int g_vg_tune = 0;  // experiments (bit 0: waves 4-7 at prio 1, bit 1: waves 0-3, bit 3: stamps,
-                           // bit 7: variant V = bits 4..6 of the DP = 4 value kernel)
+                           // bit 7: variant V = bits 4..6 of the DP = 4 / 8 value kernels)
 static unsigned long long* g_vg_stamps = nullptr;
 
 template <int DP, int HEAD, int NA, bool STAMP, int V>
@@ -1173,7 +1173,7 @@ static int launch_inst(const GradArgs& a, int grid, hipStream_t s) {
 
 template <int DP, int HEAD, int NA, bool STAMP>
 static int launch_var(const GradArgs& a, int grid, hipStream_t s) {
-  if constexpr (HEAD == HEAD_VALUE_MSE && DP == 4) {
+  if constexpr (HEAD == HEAD_VALUE_MSE && DP <= 8) {
     if (a.tune & 128) {  // structural A/B (vg_prod_v): V = tune bits 4..6
       switch ((a.tune >> 4) & 7) {
         case 0: return launch_inst<DP, HEAD, NA, STAMP, 0>(a, grid, s);

@@ -92,13 +92,14 @@ def test_split_kernel_matches_float64(cuda, D, B):
 
 @pytest.mark.parametrize("tune", [128, 144, 176, 208, 240])  # V = 0 (hi-piece dh1), 1 (mask table), 3 (+ interleaved), 5 / 7 (MFMA dW1)
 @pytest.mark.parametrize("B", [5000, 70000])
-def test_split_kernel_variants_match_float64(cuda, tune, B):
+@pytest.mark.parametrize("D", [4, 8])
+def test_split_kernel_variants_match_float64(cuda, tune, B, D):
     """Every structural variant of the factored value head (value_grad.hip vg_prod_v) is as
     accurate as the fp32 kernel and bitwise deterministic."""
     from relayrl_prototype_amd.ops import hip
 
-    D, H = 4, 128
-    g = torch.Generator().manual_seed(B + tune)
+    H = 128
+    g = torch.Generator().manual_seed(B + tune + D)
     pp = MLPSpec(D, H, 1, False).init(g)
     pp = pp + 0.05 * torch.randn(pp.shape, generator=g)
     X = torch.randn(B, D, generator=g) * 1.5

@@ -57,6 +57,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("which", choices=["grad", "pgrad", "pgauss", "fwd", "rollout", "adam", "rslab", "scan", "all"])
     ap.add_argument("--B", type=int, default=2097152)
+    ap.add_argument("--vd", type=int, default=4, help="input width of the value-grad bench (grad)")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--H", type=int, default=128)
     ap.add_argument("--stamps", action="store_true", help="diagnostic per-segment cycle stamps of the value-grad kernel")
@@ -64,7 +65,7 @@ def main():
     ap.add_argument("--stamp-tunes", default="", help="comma list of tunes to run the stamps build with")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    B, H, D = a.B, a.H, 4
+    B, H, D = a.B, a.H, a.vd
     g = torch.Generator().manual_seed(0)
     X = torch.randn(B, D, generator=g).to(dev)
     ret = torch.randn(B, generator=g).to(dev)
