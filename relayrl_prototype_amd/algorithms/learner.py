@@ -153,6 +153,15 @@ class PGLearner:
             out["StopIter"] = self.last["kl_stop"]
         return out
 
+    def broadcast_state_(self, comm: Comm, src: int = 0):
+        """Overwrite this learner's parameters and Adam state with rank ``src``'s (after an
+        elastic re-form a new learner may join without state)."""
+        for net in (self.pi, self.vf):
+            if net is None:
+                continue
+            for t in (net.params, net.m, net.v, net.step):
+                comm.broadcast_(t, src)
+
     def state_dict(self) -> dict:
         sd = {"pi": self.pi.state_dict()}
         if self.vf is not None:

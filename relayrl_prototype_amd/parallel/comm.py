@@ -38,6 +38,13 @@ def local_device_index() -> int:
     return int(forced) if forced not in (None, "") else dist_env()[1]
 
 
+def collective_timeout() -> datetime.timedelta:
+    """The bound on every collective / P2P wait (RRL_COLLECTIVE_TIMEOUT_S, default 600 s).
+    Subgroups must be given it explicitly: ``dist.new_group`` does not inherit the default
+    group's timeout."""
+    return datetime.timedelta(seconds=float(os.environ.get("RRL_COLLECTIVE_TIMEOUT_S", "600")))
+
+
 def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> "Comm":
     """Initialise the default process group from the environment (torchrun) if world > 1.
     Backend: ``nccl`` (= RCCL over xGMI on ROCm) with GPUs, ``gloo`` on CPU; override with

@@ -40,7 +40,7 @@ import torch
 import torch.distributed as dist
 
 from ..algorithms.learner import PGLearner
-from ..parallel.comm import Comm
+from ..parallel.comm import Comm, collective_timeout
 from .rollout_learn import RolloutLearner
 
 # header (float64): seq, n_episodes, sum_ret, sumsq_ret, max_ret, min_ret, sum_len, version, checksum, wsum
@@ -102,6 +102,18 @@ class Topology:
             raise ValueError(f"{len(self.actors)} actors do not split evenly over {L} learner shards")
         self.K = len(self.actors) // L  # actor blocks per learner shard
         self.learner_acts = learner_acts
+
+    @staticmethod
+    def fit_learners(world: int, learner_ranks: int, learner_acts: bool) -> int:
+        """The largest learner count <= ``learner_ranks`` whose shards split the actors evenly
+        on ``world`` ranks (after an elastic shrink the requested count may no longer fit)."""
+        L = min(learner_ranks or world, world)
+        while L > 1:
+            n_act = world if learner_acts else world - L
+            if n_act >= 1 and n_act % L == 0:
+                return L
+            L -= 1
+        return 1
 
     def learner_of(self, actor: int) -> int:
         return self.actors.index(actor) % self.L
@@ -202,7 +214,7 @@ class ActorLearner:
         if topo.L == W:
             self.lcomm = self.comm
         else:
-            grp = dist.new_group(list(range(topo.L))) if W > 1 else None
+            grp = dist.new_group(list(range(topo.L)), timeout=collective_timeout()) if W > 1 else None
             self.lcomm = Comm(grp) if self.is_learner else None
         need_tobs = cfg.with_baseline or cfg.algo != "reinforce"
         self.actor = _Actor(cfg, self.comm, self.device, need_tobs) if self.acts else None
@@ -455,6 +467,20 @@ class ActorLearner:
             out.update(self.learner.summarize())
         out["EnvSteps"] = self.epoch * self.cfg.rollout_len * self.cfg.num_envs * self.n_actors
         return out
+
+    def sync_from_rank0(self):
+        """Make every learner hold rank 0's learner state and every rank its policy weights
+        (after an elastic re-form, parallel/elastic.py)."""
+        if self.is_learner and self.lcomm is not None and self.lcomm.world > 1:
+            self.learner.broadcast_state_(self.lcomm, 0)
+        self.comm.broadcast_(self.front, 0)
+        if self.is_learner and self.actor is not None:
+            self.actor.params.copy_(self.front)
+        vec = torch.tensor([float(self.epoch), float(self.version)], dtype=torch.float64,
+                           device="cuda" if self.comm.backend == "nccl" else "cpu")
+        self.comm.broadcast_(vec, 0)
+        self.epoch, self.version = int(vec[0].item()), int(vec[1].item())
+        self._front_version = self.version
 
     # ------------------------------------------------------------------ checkpoint
     def state_dict(self) -> dict:

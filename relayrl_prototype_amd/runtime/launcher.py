@@ -115,11 +115,18 @@ def ckpt_dir(out_dir: str, name: str, rank: int) -> str:
 
 def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optional[Dict] = None,
                checkpoint_every: int = 0, resume: Optional[str] = None, log_every: int = 1,
-               on_metrics: Optional[Callable[[Dict], None]] = None, auto_resume: bool = False) -> Dict:
+               on_metrics: Optional[Callable[[Dict], None]] = None, auto_resume: bool = False,
+               elastic: bool = False) -> Dict:
     """Run one rank of a preset until ``epochs`` epochs are done; returns the last metrics
     (rank 0).  Checkpoints are per rank (each rank owns its env streams); with
     ``auto_resume`` a (re)started rank continues from its own latest checkpoint, which is
-    how a torchrun group restart after a rank failure recovers (--max-restarts)."""
+    how a torchrun group restart after a rank failure recovers (--max-restarts).
+
+    ``elastic``: a stalled rank does not stop the job -- the survivors' failed collective
+    leads to a re-form of the process group without it (parallel/elastic.py), the trainer is
+    rebuilt on the smaller group from its in-memory state (learner state broadcast from the
+    new rank 0) and the failed epoch is retried.  An evicted rank returns
+    ``{"Evicted": True}``."""
     import torch
 
     from ..parallel.comm import Comm, dist_env, init_distributed
@@ -131,8 +138,18 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
         return _run_agent_server(preset, epochs, out_dir, overrides)
     from ..parallel.comm import local_device_index
 
-    _, _, world = dist_env()
-    comm = init_distributed() if world > 1 else Comm()
+    orig_rank, _, world = dist_env()
+    eg = None
+    if elastic and world > 1:
+        from ..parallel.elastic import ElasticGroup
+
+        eg = ElasticGroup()
+        comm = eg.init_group()
+        # collective timeouts detect a stalled peer; the exiting step watchdog would end the
+        # survivors too
+        overrides.setdefault("stall_timeout_s", 0.0)
+    else:
+        comm = init_distributed() if world > 1 else Comm()
     if torch.cuda.is_available():
         dev = torch.device("cuda", local_device_index())
         torch.cuda.set_device(dev)
@@ -159,11 +176,48 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
     last: Dict = {}
     from ..utils.faults import maybe_kill_rank, maybe_stall_rank
 
-    for ep in range(start + 1, epochs + 1):
-        maybe_stall_rank(comm.rank, ep, out_dir)
-        _epoch(tr)
-        if ep % log_every == 0 or ep == epochs:
-            m = tr.metrics()
+    ep = start + 1
+    while ep <= epochs:
+        try:
+            maybe_stall_rank(orig_rank if eg is not None else comm.rank, ep, out_dir)
+            _epoch(tr)
+            m = tr.metrics() if (ep % log_every == 0 or ep == epochs) else None
+        except Exception as e:
+            if eg is None:
+                raise
+            from ..parallel.elastic import Evicted
+
+            sd = tr.state_dict()
+            if hasattr(tr, "watchdog"):
+                tr.watchdog.close()
+            try:
+                comm = eg.reform()
+            except Evicted as ev:
+                print(f"[elastic] {ev}", flush=True)
+                eg.close()
+                return {"Evicted": True, "Epoch": ep - 1}
+            if getattr(comm, "unchanged", False):
+                raise  # every rank is alive: not a lost peer
+            print(f"[elastic] rank {orig_rank}: re-formed without the lost rank(s) after {type(e).__name__}; "
+                  f"world {comm.world}, rank {comm.rank}, retrying epoch {ep}", flush=True)
+            ov = dict(overrides)
+            if preset.kind == "actor_learner":
+                from .actor_learner import Topology
+
+                req = dict(preset.overrides)
+                req.update(overrides)
+                if int(req.get("learner_ranks", 0)):
+                    ov["learner_ranks"] = Topology.fit_learners(comm.world, int(req["learner_ranks"]),
+                                                                bool(req.get("learner_acts", True)))
+            tr = _make_trainer(preset, comm, dev, ov)
+            tr.load_state_dict(sd)
+            if hasattr(tr, "sync_from_rank0"):
+                tr.sync_from_rank0()
+            if comm.rank == 0 and logger is None:
+                kw = setup_logger_kwargs(f"relayrl-{name}", seed=int(overrides.get("seed", 0)), data_dir=out_dir)
+                logger = EpochLogger(**kw, quiet=True)
+            continue
+        if m is not None:
             el = time.perf_counter() - t0
             if comm.rank == 0 and m:
                 m = dict(m)
@@ -185,8 +239,14 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
 
             save_checkpoint(ckpt_dir(out_dir, name, comm.rank), {"trainer": tr.state_dict(), "epoch": ep})
         maybe_kill_rank(comm.rank, ep, out_dir)
+        ep += 1
     if hasattr(tr, "finish"):
         tr.finish()
+    if eg is not None:
+        last = dict(last)
+        last["ElasticReforms"] = eg.reforms
+        last["FinalWorld"] = comm.world
+        eg.close()
     return last
 
 
@@ -266,6 +326,8 @@ def main(argv=None) -> int:
     t.add_argument("--resume", default=None)
     t.add_argument("--auto-resume", action="store_true", help="continue from this rank's last checkpoint if any")
     t.add_argument("--max-restarts", type=int, default=0, help="torchrun group restarts after a rank failure")
+    t.add_argument("--elastic", action="store_true",
+                   help="survivors of a stalled rank re-form the group without it and continue")
     e = sub.add_parser("engine", help="one rank of a TrainingServer device engine (runtime/engine.py)")
     e.add_argument("--spec", required=True)
     e.add_argument("--env-dir", default=".")
@@ -315,7 +377,8 @@ def main(argv=None) -> int:
         except ValueError:
             pass
         ov[k] = v
-    m = run_preset(a.preset, a.epochs, a.out, ov, a.checkpoint_every, a.resume, auto_resume=a.auto_resume)
+    m = run_preset(a.preset, a.epochs, a.out, ov, a.checkpoint_every, a.resume, auto_resume=a.auto_resume,
+                   elastic=a.elastic)
     if m:
         print(json.dumps({k: v for k, v in m.items() if isinstance(v, (int, float, str))}), flush=True)
     return 0

@@ -1,0 +1,91 @@
+"""Elastic shrink (parallel/elastic.py): the survivors of a stalled rank re-form
+the process group without it and keep training; the stalled rank is evicted (exit 0)."""
+import datetime
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cport, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    from relayrl_prototype_amd.parallel.elastic import ElasticGroup, Evicted
+
+    eg = ElasticGroup(backend="gloo", timeout_s=2.0, grace_s=5.0, control_port=cport)
+    comm = eg.init_group()
+    t = torch.ones(3)
+    comm.all_reduce_sum_(t)
+    assert t.tolist() == [3.0] * 3
+    if rank == 2:
+        time.sleep(15)  # stalled: the others re-form without it; the monitor ends this process
+    result = {"rank": rank}
+    try:
+        comm.all_reduce_sum_(torch.ones(3))
+        result["second"] = "ok"
+    except Exception as e:
+        try:
+            comm = eg.reform()
+        except Evicted:
+            result["evicted"] = True
+            json.dump(result, open(os.path.join(out_dir, f"r{rank}.json"), "w"))
+            return
+        t = torch.full((3,), float(rank + 1))
+        comm.all_reduce_sum_(t)
+        result.update(error=type(e).__name__, world=comm.world, new_rank=comm.rank, sum=t.tolist(),
+                      members=eg.members)
+    json.dump(result, open(os.path.join(out_dir, f"r{rank}.json"), "w"))
+    dist.destroy_process_group()
+    eg.close()  # rank 0 (the control store) waits for the evicted rank to have left
+
+
+def test_elastic_group_drops_stalled_rank(tmp_path):
+    mp.spawn(_worker, args=(3, _port(), _port(), str(tmp_path)), nprocs=3, join=True)
+    r0 = json.load(open(tmp_path / "r0.json"))
+    r1 = json.load(open(tmp_path / "r1.json"))
+    for r in (r0, r1):
+        assert r["world"] == 2 and r["members"] == [0, 1], r
+        assert r["sum"] == [3.0, 3.0, 3.0], r  # ranks 0 + 1 contribute 1 + 2
+    assert r0["new_rank"] == 0 and r1["new_rank"] == 1
+    # the stalled rank was ended by its monitor thread (exit 0) before it could write a result
+    assert not (tmp_path / "r2.json").exists()
+
+
+@pytest.mark.timeout(300)
+def test_elastic_actor_learner_continues_without_stalled_actor(tmp_path):
+    """4 gloo ranks, learners {0, 1}, every rank acting; actor-only rank 3 hangs before epoch
+    3.  The survivors re-form a 3-rank group, rebuild the actor-learner on it from their
+    in-memory state (Topology.fit_learners) and finish all 5 epochs; the evicted rank exits 0,
+    so torchrun reports success."""
+    env = dict(os.environ, PYTHONPATH=REPO, RRL_QUIET_CONFIG="1", OMP_NUM_THREADS="1", RRL_FAULT_STALL="3:3:40",
+               RRL_COLLECTIVE_TIMEOUT_S="3")
+    r = subprocess.run([sys.executable, "-m", "relayrl_prototype_amd", "train", "--preset",
+                        "lunarlander-reinforce-baseline", "--gpus", "4", "--epochs", "5", "--out", str(tmp_path),
+                        "--elastic", "--set", "num_envs=4", "rollout_len=8", "train_vf_iters=2", "num_threads=1",
+                        "learner_ranks=2"],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert os.path.exists(tmp_path / ".stall_fired_r3_e3")
+    assert "re-formed without the lost rank" in r.stdout and "evicted" in r.stdout
+    line = [l for l in r.stdout.splitlines() if l.startswith("{") and "FinalWorld" in l][-1]
+    m = json.loads(line)
+    assert m["FinalWorld"] == 3 and m["ElasticReforms"] == 1 and m["Epoch"] == 5, m
+    # 3 actors do not split over 2 learner shards: the rebuilt topology fits 1 learner
+    assert m["WorldSize"] == 3 and m["LearnerRanks"] == 1
