@@ -333,8 +333,8 @@ RRL_DEV float wave_sum_vl(float v) {
 // tune bit 7, V = tune bits 4..6, tools/kbench.py --tunes): bit 0 = dh1 from the mask table without the dh2 barrier
 // (else from the hi piece of dh2', rescaled by dout / hi(dout), after a barrier); bit 1 (with
 // bit 0) = the dh2 tiles' vector work runs between dh1's MFMAs and dW1's between dW2's, so each
-// wave's own matrix instructions cover it (otherwise the phases run one after the other); bit 2 =
-// dW1 on fp32 MFMA tiles at DP = 4 too (12 of its 16 columns idle) instead of vector FMAs.
+// wave's own matrix instructions cover it (otherwise the phases run one after the other).  (A
+// bit-2 variant with fp32-MFMA dW1 at DP = 4 measured 905 vs 839 us and was removed.)
 // production variant per input width (DP = 8 spills 4 VGPRs with the interleave)
 constexpr int vg_prod_v(int DP) { return DP <= 4 ? 3 : 1; }
 
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   // dW1 / db1 from the TRANSPOSED dh1 tile (lane (j, g) holds rows 16 bt + 4 g + i of
   // feature own + j): summed inside the lane over the slabs, over the 4 lane groups once in
   // the epilogue.  DP = 4: vector FMAs on broadcast x rows; wider inputs: fp32 MFMA tiles.
-  constexpr bool kDw1Mfma = DP > 4 || (kFactor && (V & 4));
+  constexpr bool kDw1Mfma = DP > 4;
   constexpr int NT1 = (DP + 15) / 16;
   float acc1[kDw1Mfma ? 1 : DP];      // dW1[own + j][d], this lane's rows
   floatx4 acc1m[kDw1Mfma ? NT1 : 1];  // dW1[own + 4 g + i][16 nt + j]
@@ -1179,8 +1179,6 @@ static int launch_var(const GradArgs& a, int grid, hipStream_t s) {
         case 0: return launch_inst<DP, HEAD, NA, STAMP, 0>(a, grid, s);
         case 1: return launch_inst<DP, HEAD, NA, STAMP, 1>(a, grid, s);
         case 3: return launch_inst<DP, HEAD, NA, STAMP, 3>(a, grid, s);
-        case 5: return launch_inst<DP, HEAD, NA, STAMP, 5>(a, grid, s);
-        case 7: return launch_inst<DP, HEAD, NA, STAMP, 7>(a, grid, s);
         default: break;
       }
     }
