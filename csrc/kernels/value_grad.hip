@@ -483,6 +483,21 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   // db3 / dlog_std: wave w owns output a = w (NA <= 8 waves) and keeps its batch sum in one
   // wave-uniform register, folded over the 64 rows of every slab on the VALU
   float bacc3 = 0.f, dls = 0.f;
+  // factored value head: this lane's partials of the fields db2' (x w3 in the epilogue) and
+  // dW3 row 0 for its 4 features, summed over all its slabs and folded over the 16 batch lanes
+  // once, after the loop (a DPP reduce-scatter per slab cost ~45 vector instructions)
+  // (DP = 4 only: at DP = 8 the kernel is at 253 VGPRs and the extra live partials measured
+  // 122 -> 133 us at 262 k rows, while DP = 4 gained 826 -> 810 us at 2.1 M rows)
+  constexpr bool kTvPersist = kFactor && DP == 4;
+  float tvs[kFactor ? 16 : 1];
+#pragma unroll
+  for (int e = 0; e < (kFactor ? 16 : 1); ++e) tvs[e] = 0.f;
+  auto fold_tvs = [&]() {
+    float tf[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) tf[e] = kFactor ? tvs[e % (kFactor ? 16 : 1)] : 0.f;
+    return reduce_scatter16(tf, j);
+  };
   float s_loss = 0.f, s_val = 0.f, s_cnt = 0.f, s_ent = 0.f, s_kl = 0.f, s_clip = 0.f;
 
   // Global inputs go straight to LDS by DMA (global_load_lds_dword: lane l's dword lands at
@@ -812,9 +827,11 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       float dv[4];  // dout of C-layout row 16 bt + j (the dh2' tiles)
 #pragma unroll
       for (int bt = 0; bt < 4; ++bt) dv[bt] = __shfl(dout[0], 16 * bt + j, 64);
-      float tv[16];  // fields: db2' (x w3 in the epilogue), dW3 row 0
+      float* tv = tvs;  // fields: db2' (x w3 in the epilogue), dW3 row 0 (kTvPersist: kept over slabs)
+      if (!kTvPersist) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) tv[e] = 0.f;
+        for (int e = 0; e < 16; ++e) tvs[e % (kFactor ? 16 : 1)] = 0.f;
+      }
       // dh2' pieces of batch tile bt (stores) and its field partials
       auto kf_tile = [&](const int bt) {
         const float v = dv[bt];
@@ -839,7 +856,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         }
       };
       auto kf_finish = [&]() {
-        accv[0] += reduce_scatter16(tv, j);
+        if (!kTvPersist) accv[0] += fold_tvs();
         if (kMaskB) {
           // the dh2' image is read back (dW2) only by the wave that wrote it: in-order LDS
           __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -1087,6 +1104,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   }
 
   // ------------------------------------------------------------------ epilogue
+  if (kTvPersist) accv[0] += fold_tvs();
   float* slab = p.grad_slab + (size_t)blockIdx.x * p.P;
   floatx4 w3s;  // kFactor: dW2 rows / db2 are w3 x the accumulated dh2' sums
 #pragma unroll
