@@ -73,14 +73,23 @@ constexpr int vg_mask_bytes(int DP, int HEAD) { return vg_factor(DP, HEAD) ? 64 
 constexpr int vg_hbuf_bytes(int HEAD, int NA) {
   return HEAD == HEAD_VALUE_MSE ? 0 : 64 * 4 * (2 + ((HEAD == HEAD_PG_GAUSS || HEAD == HEAD_PPO_GAUSS) ? NA : 1));
 }
+// Gaussian heads with NA > 1 compute the head once per row (lane = (row, output), spread over
+// the 8 waves) and hand dout to the dh2 phase through a [64][NA] table after the head inputs.
+constexpr bool vg_split_head(int HEAD, int NA) {
+  return (HEAD == HEAD_PG_GAUSS || HEAD == HEAD_PPO_GAUSS) && NA > 1;
+}
+// (+ the per-wave db3 / dlog_std sums [8][2 NA], accumulated in LDS across the slabs)
+constexpr int vg_dtab_bytes(int HEAD, int NA) { return vg_split_head(HEAD, NA) ? (64 + 16) * NA * 4 : 0; }
 // Outside the image the head inputs are double-buffered (DMA'd a slab ahead) when LDS allows.
 constexpr bool vg_hbuf2(int DP, int HEAD, int NA) {
-  return !vg_red_in_image(DP, NA) &&
-         vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD) + 2 * vg_hbuf_bytes(HEAD, NA) <= 160 * 1024;
+  return !vg_red_in_image(DP, NA) && vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD) +
+                                             2 * vg_hbuf_bytes(HEAD, NA) + vg_dtab_bytes(HEAD, NA) <=
+                                         160 * 1024;
 }
 constexpr int vg_total_bytes(int DP, int HEAD, int NA) {
   return vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD) +
-         (vg_red_in_image(DP, NA) ? 0 : (vg_hbuf2(DP, HEAD, NA) ? 2 : 1) * vg_hbuf_bytes(HEAD, NA));
+         (vg_red_in_image(DP, NA) ? 0 : (vg_hbuf2(DP, HEAD, NA) ? 2 : 1) * vg_hbuf_bytes(HEAD, NA)) +
+         vg_dtab_bytes(HEAD, NA);
 }
 static_assert(vg_red_bytes(6) + vg_hbuf_bytes(HEAD_PPO_GAUSS, 6) <= 3 * kVgImg * 2, "head inputs in the dh2 image");
 static_assert(vg_total_bytes(8, HEAD_VALUE_MSE, 1) <= 160 * 1024, "factored LDS plan");
@@ -347,6 +356,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   constexpr bool kPPO = HEAD == HEAD_PPO_CAT || HEAD == HEAD_PPO_GAUSS;
   static_assert(!kValue || NA == 1, "the value head has one output");
   static_assert(NA >= 1 && NA <= 6, "NA <= 6 (LDS plan, two field groups)");
+  static_assert(!vg_split_head(HEAD, NA) || NA % 2 == 0, "the dout table is read in output pairs");
   // batch-summed 4-feature fields of the head / bias gradients, folded over the 16 batch
   // lanes by the DPP reduce-scatter: field 0 db2, 1 dW3 row 0, 2 (unused: db1 is summed in
   // the lane), 3 dW3 row 1, 4.. rows 2..
@@ -365,10 +375,12 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   constexpr int NF = NA + 2;
   constexpr int NG = (NF + 3) / 4;  // 16-slot groups (one register each)
   constexpr bool kRedImg = vg_red_in_image(DP, NA);
+  constexpr bool kSplitHead = vg_split_head(HEAD, NA);
   uint16_t* h1img = vg_lds;
   uint16_t* dhimg = vg_lds + 3 * kVgImg;
   float* tail = reinterpret_cast<float*>(vg_lds + 6 * kVgImg);
-  float* red = kRedImg ? reinterpret_cast<float*>(dhimg) : tail;  // [8 waves][NA][64 rows]
+  // [8 waves][NA][64 rows], or [8 waves][64 rows][NA] under kSplitHead
+  float* red = kRedImg ? reinterpret_cast<float*>(dhimg) : tail;
   float* xsb = kRedImg ? tail : tail + 8 * NA * 64;                // [2][64 rows][DP]
   float* vecs = xsb + 2 * 64 * DP;                                 // b1[128] b2[128] w3[NA][128]
   uint16_t* w2lo = reinterpret_cast<uint16_t*>(vecs + (2 + NA) * kVgH + 32);  // [128][kVgLd]
@@ -378,6 +390,12 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   // (int bits) or actc [64][NA]
   float* hbuf0 = kRedImg ? red + 8 * NA * 64
                          : reinterpret_cast<float*>(reinterpret_cast<char*>(mk) + vg_mask_bytes(DP, HEAD));
+  // kSplitHead: the slab's dout [64 rows][NA] (outside both images: read while dh2 is stored)
+  float* dtab = reinterpret_cast<float*>(
+      reinterpret_cast<char*>(mk) + vg_mask_bytes(DP, HEAD) +
+      (kRedImg ? 0 : (vg_hbuf2(DP, HEAD, NA) ? 2 : 1) * vg_hbuf_bytes(HEAD, NA)));
+  float* hacc = dtab + 64 * NA;  // kSplitHead: [8 waves][db3[NA], dlog_std[NA]]
+  if (kSplitHead && lane_id() < 2 * NA) hacc[(threadIdx.x >> 6) * 2 * NA + lane_id()] = 0.f;
   if (kMaskB) {
     // entry i: element e (feature 8 g + e of a fragment) = 1.0 if bit e of i is set
     for (int q = threadIdx.x; q < 256 * 4; q += blockDim.x) {
@@ -481,7 +499,8 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 #pragma unroll
   for (int nt = 0; nt < (kDw1Mfma ? NT1 : 1); ++nt) acc1m[nt] = zero4();
   // db3 / dlog_std: wave w owns output a = w (NA <= 8 waves) and keeps its batch sum in one
-  // wave-uniform register, folded over the 64 rows of every slab on the VALU
+  // wave-uniform register, folded over the 64 rows of every slab on the VALU.  kSplitHead:
+  // the wave folds its lanes (r, a) per output a and adds the sums to its slots of hacc.
   float bacc3 = 0.f, dls = 0.f;
   // factored value head: this lane's partials of the fields db2' (x w3 in the epilogue) and
   // dW3 row 0 for its 4 features, summed over all its slabs and folded over the 16 batch lanes
@@ -681,7 +700,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         pv = fmaf(w3a[2], h2[bt][2], pv);
         pv = fmaf(w3a[3], h2[bt][3], pv);
         pv = group_sum_swap(pv);
-        if (g == bt) red[(w * NA + a) * 64 + 16 * bt + j] = pv;
+        if (g == bt) red[kSplitHead ? (w * 64 + 16 * bt + j) * NA + a : (w * NA + a) * 64 + 16 * bt + j] = pv;
       }
       if (NA > 2) __builtin_amdgcn_sched_barrier(0);
     }
@@ -694,7 +713,66 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     const bool lead = w == 0;
     float dout[NA];
     float dls_row[kGauss ? NA : 1];  // this row's dLoss/dlog_std terms (Gaussian heads)
-    {
+    if constexpr (kSplitHead) {
+      // Gaussian head, NA > 1: lane (r, a) = (l >> 3, l & 7) of wave w takes output a of row
+      // 8 w + r, so each of the 64 x NA terms is computed once instead of in every wave; a
+      // row's log-prob / entropy is summed over its 8 lanes by DPP, and dout goes to the
+      // table that the barrier below publishes to every wave's dh2 phase
+      const int a8 = l & 7, R = 8 * w + (l >> 3);
+      const bool va = a8 < NA;
+      const int ac = min(a8, NA - 1);
+      const bool ok = base + R < p.B;
+      const float* rr = red + R * NA + ac;
+      constexpr int S = 64 * NA;  // wave stride
+      const float outv = (((rr[0] + rr[S]) + (rr[2 * S] + rr[3 * S])) + ((rr[4 * S] + rr[5 * S]) + (rr[6 * S] + rr[7 * S]))) +
+                         hsc[ac];
+      const float hin = hbuf[R], hlp = hbuf[64 + R];
+      const float lsd = hsc[NA + ac], istd = hsc[2 * NA + ac];
+      // dlogp/dmu = d / var ; dlogp/dlog_std = d^2 / var - 1 ; dH/dlog_std = 1
+      const float d = (ok ? hbuf[128 + R * NA + ac] : outv) - outv;
+      const float z = d * istd;
+      float logp = va ? -0.5f * z * z - lsd - kHalfLog2Pi : 0.f;
+      float ent = va ? 0.5f + kHalfLog2Pi + lsd : 0.f;
+      logp += dpp_f<kDppXor1>(logp);
+      ent += dpp_f<kDppXor1>(ent);
+      logp += dpp_f<kDppXor2>(logp);
+      ent += dpp_f<kDppXor2>(ent);
+      logp += dpp_f<kDppMirror8>(logp);
+      ent += dpp_f<kDppMirror8>(ent);
+      const float adv = ((ok ? hin : 0.f) - adv_mean) * adv_rstd;
+      float dlogp, loss_i;
+      if (!kPPO) {
+        dlogp = -adv;
+        loss_i = -logp * adv;
+      } else {
+        const float lpo = (ok && p.logp_old) ? hlp : logp;
+        const float ratio = __expf(logp - lpo);
+        const float s1 = ratio * adv;
+        const float s2 = fminf(fmaxf(ratio, 1.f - p.clip_eps), 1.f + p.clip_eps) * adv;
+        dlogp = (s1 <= s2) ? -adv * ratio : 0.f;
+        loss_i = -fminf(s1, s2);
+        if (a8 == 0 && ok) s_clip += (fabsf(ratio - 1.f) > p.clip_eps) ? 1.f : 0.f;
+      }
+      const float scale = (ok && va) ? p.inv_B : 0.f;
+      const float iv = istd * istd;
+      const float da = scale * dlogp * d * iv;
+      const float dl = scale * (dlogp * (d * d * iv - 1.f) - p.ent_coef);
+      if (va) dtab[R * NA + a8] = da;
+      // this wave's sums of output a (lanes a + 8 r) into its LDS slots (a VGPR accumulator per
+      // lane would cost registers the DP = 20 kernel spills for; the wave-uniform ones did not)
+      const float hb = group_sum_swap(da + dpp_f<kDppXor8>(da));
+      const float hl = group_sum_swap(dl + dpp_f<kDppXor8>(dl));
+      if (l < NA) {
+        hacc[w * 2 * NA + l] += hb;
+        hacc[w * 2 * NA + NA + l] += hl;
+      }
+      if (a8 == 0 && ok) {
+        s_loss += loss_i;
+        s_ent += ent;
+        if (p.logp_old) s_kl += hlp - logp;
+        s_cnt += 1.f;
+      }
+    } else {
       const int b = base + l;
       const bool ok = b < p.B;
       const int bc = min(b, p.B - 1);
@@ -799,7 +877,8 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       prefetch_x(base + gridDim.x * 64, xsb + (parity & 1) * 64 * DP);
       if (kHb2) dma_head(base + gridDim.x * 64, hbuf0 + (parity & 1) * HBF);
     }
-    if (kRedImg) __syncthreads();  // every wave read the partials before dh2 overwrites them
+    // every wave read the partials before dh2 overwrites them (kSplitHead: the dout table is visible)
+    if (kRedImg || kSplitHead) __syncthreads();
 
     VG_STAMP(6);
     // ------------------------------------------------------------ dh2, dW3, db2 / dh1, db1
@@ -934,26 +1013,36 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       // dout of batch row 16 bt + j comes from lane 16 bt + j (ds_bpermute, no barrier).  Field
       // group 0 (db2, dW3 rows 0 / 1) is folded first; the rows of outputs 2.. (group 1) in a
       // second pass, so only 16 partials are live at a time.
+      // kSplitHead: dout comes from the table instead, as pairs (a, a + 1) of rows 16 bt + j (b64
+      // reads), one pair at a time (sched barrier: hoisted together the reads held 24 registers
+      // and the DP = 20 kernel spilled for them; a pair read ahead spilled too)
       floatx4 dd[4];
 #pragma unroll
       for (int bt = 0; bt < 4; ++bt) dd[bt] = zero4();
+      auto tab_pair = [&](int a2, vf32x2(&q)[4]) {
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) q[bt] = *reinterpret_cast<const vf32x2*>(dtab + (16 * bt + j) * NA + a2);
+      };
+      vf32x2 vq[4];
       {
         float tv[16];  // this slab's field partials of features own + 4g + r
 #pragma unroll
         for (int e = 0; e < 16; ++e) tv[e] = 0.f;
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
+          if (kSplitHead && (a & 1) == 0) tab_pair(a, vq);
           const floatx4 w3a = *reinterpret_cast<const floatx4*>(w3p + a * kVgH);
           const int f = a == 0 ? 1 : 3;
 #pragma unroll
           for (int bt = 0; bt < 4; ++bt) {
-            const float v = __shfl(dout[a], 16 * bt + j, 64);
+            const float v = kSplitHead ? vq[bt][a & 1] : __shfl(dout[a], 16 * bt + j, 64);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               dd[bt][r] = fmaf(w3a[r], v, dd[bt][r]);
               if (a < 2) tv[4 * f + r] = fmaf(v, h2[bt][r], tv[4 * f + r]);
             }
           }
+          if (kSplitHead && (a & 1)) __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
         for (int bt = 0; bt < 4; ++bt) {
@@ -972,13 +1061,15 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         for (int e = 0; e < 16; ++e) tv[e] = 0.f;
 #pragma unroll
         for (int a = 2; a < NA; ++a) {
+          if (kSplitHead && (a & 1) == 0) tab_pair(a, vq);
           const int f = a + 2;  // fields 4 .. NA + 1 -> group 1 (NA <= 6)
 #pragma unroll
           for (int bt = 0; bt < 4; ++bt) {
-            const float v = __shfl(dout[a], 16 * bt + j, 64);
+            const float v = kSplitHead ? vq[bt][a & 1] : __shfl(dout[a], 16 * bt + j, 64);
 #pragma unroll
             for (int r = 0; r < 4; ++r) tv[4 * (f & 3) + r] = fmaf(v, h2[bt][r], tv[4 * (f & 3) + r]);
           }
+          if (kSplitHead && (a & 1)) __builtin_amdgcn_sched_barrier(0);
         }
         accv[1] += reduce_scatter16(tv, j);
       }
@@ -1142,11 +1233,36 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     const float sb = group_sum_swap(db1acc);
     if (g == 0) slab[o.b1 + own + j] = sb;
   }
-  if (w < NA && l == 0) {
+  if constexpr (kSplitHead) {
+    // db3 / dlog_std: the waves' hacc slots; loss sums: lanes 8 r of every wave, folded in the
+    // wave and then over the 8 waves through LDS (fixed order)
+    const float st[6] = {wave_sum_vl(s_loss), wave_sum_vl(s_ent), wave_sum_vl(s_kl),
+                         wave_sum_vl(s_clip), wave_sum_vl(s_val), wave_sum_vl(s_cnt)};
+    __syncthreads();  // every wave is past its last dh2 phase: the dout table is free
+    float* ep = dtab;  // [8 waves][6]: loss sums
+    if (l == 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) ep[w * 6 + k] = st[k];
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < 2 * NA) {
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) v += hacc[ww * 2 * NA + t];
+      slab[(t < NA ? o.b3 : o.log_std - NA) + t] = v;
+    } else if (t >= 64 && t < 70) {
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) v += ep[ww * 6 + t - 64];
+      p.loss_slab[blockIdx.x * 8 + t - 64] = v;
+    }
+  }
+  if (!kSplitHead && w < NA && l == 0) {
     slab[o.b3 + w] = bacc3;
     if (kGauss) slab[o.log_std + w] = dls;
   }
-  if (w == 0) {
+  if (!kSplitHead && w == 0) {
     const float sl = wave_sum(s_loss), sv = wave_sum(s_val), sc = wave_sum(s_cnt);
     const float se = wave_sum(s_ent), sk = wave_sum(s_kl), scl = wave_sum(s_clip);
     if (l == 0) {
