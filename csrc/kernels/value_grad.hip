@@ -356,7 +356,8 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   constexpr bool kPPO = HEAD == HEAD_PPO_CAT || HEAD == HEAD_PPO_GAUSS;
   static_assert(!kValue || NA == 1, "the value head has one output");
   static_assert(NA >= 1 && NA <= 6, "NA <= 6 (LDS plan, two field groups)");
-  static_assert(!vg_split_head(HEAD, NA) || NA % 2 == 0, "the dout table is read in output pairs");
+  static_assert(!vg_split_head(HEAD, NA) || (NA % 2 == 0 && NA <= 6),
+                "the dout table is read in output pairs; head MFMA lanes g = 0, 1 hold outputs 0..7");
   // batch-summed 4-feature fields of the head / bias gradients, folded over the 16 batch
   // lanes by the DPP reduce-scatter: field 0 db2, 1 dW3 row 0, 2 (unused: db1 is summed in
   // the lane), 3 dW3 row 1, 4.. rows 2..
@@ -690,6 +691,28 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     VG_STAMP(3);
     // ------------------------------------------------------------ head
     // partial dot products over this wave's 16 features -> LDS, reduced over the 8 waves
+    if constexpr (kSplitHead) {
+      // on fp32 MFMA (exact fp32 products): C[a][row] = sum_k W3[a][k] h2[row][k] over the
+      // wave's features k, A = W3 row a = lane & 15 (zero past NA), B = the h2 tile as it sits
+      // in C layout (k = own + 4 g + r over the 4 steps r, n = row 16 bt + j).  Lane (j, g)
+      // gets outputs 4 g + i of row 16 bt + j: one sum over the lane groups per MFMA instead
+      // of NA dot products + lane-swap sums on the VALU
+      floatx4 w3m = zero4();
+      if (j < NA) w3m = *reinterpret_cast<const floatx4*>(w3p + j * kVgH);
+#pragma unroll
+      for (int bt = 0; bt < 4; ++bt) {
+        floatx4 c = zero4();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c = mfma4(w3m[r], h2[bt][r], c);
+        float* dst = red + (w * 64 + 16 * bt + j) * NA + 4 * g;
+        if (g == 0) {
+          *reinterpret_cast<vf32x2*>(dst) = vf32x2{c[0], c[1]};
+          *reinterpret_cast<vf32x2*>(dst + 2) = vf32x2{c[2], c[3]};
+        } else if (4 * g < NA) {
+          *reinterpret_cast<vf32x2*>(dst) = vf32x2{c[0], c[1]};
+        }
+      }
+    } else {
 #pragma unroll
     for (int a = 0; a < NA; ++a) {
       const floatx4 w3a = *reinterpret_cast<const floatx4*>(w3p + a * kVgH);
@@ -700,9 +723,10 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         pv = fmaf(w3a[2], h2[bt][2], pv);
         pv = fmaf(w3a[3], h2[bt][3], pv);
         pv = group_sum_swap(pv);
-        if (g == bt) red[kSplitHead ? (w * 64 + 16 * bt + j) * NA + a : (w * NA + a) * 64 + 16 * bt + j] = pv;
+        if (g == bt) red[(w * NA + a) * 64 + 16 * bt + j] = pv;
       }
       if (NA > 2) __builtin_amdgcn_sched_barrier(0);
+    }
     }
     VG_STAMP(4);
     if (kDmaIn && !kHb2) vm_wait0();  // this wave's head-input DMAs
