@@ -606,7 +606,6 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       }
     }
     __syncthreads();  // x (and kHb2 head inputs) visible; the previous slab's readers are done
-    if (kDmaIn && !kHb2) dma_head(base, hbuf);
     VG_STAMP(1);
 
     // ------------------------------------------------------------ layer 1 (fp32 MFMA)
@@ -635,6 +634,9 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       }
     }
     __syncthreads();
+    // this slab's head inputs (not double-buffered): issued after layer 1's barrier, which would
+    // otherwise wait for them (vmcnt 0), and landed behind layer 2 (vm_wait0 before the head's)
+    if (kDmaIn && !kHb2) dma_head(base, hbuf);
 
     VG_STAMP(2);
     // ------------------------------------------------------------ layer 2 (bf16x6 MFMA)
@@ -896,13 +898,22 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         if (kGauss) dls += wave_sum_vl(ml);
       }
     }
-    // the head consumed this slab's inputs: issue the next slab's x DMA now
-    if (base + (int)gridDim.x * 64 < p.B) {
-      prefetch_x(base + gridDim.x * 64, xsb + (parity & 1) * 64 * DP);
-      if (kHb2) dma_head(base + gridDim.x * 64, hbuf0 + (parity & 1) * HBF);
-    }
+    // the head consumed this slab's inputs: issue the next slab's x DMA now -- after the barrier
+    // below where there is one: __syncthreads waits for every outstanding vector memory op
+    // (vmcnt 0), so a DMA issued just before it would stall the slab for its HBM latency
+    auto prefetch_next = [&]() {
+      if (base + (int)gridDim.x * 64 < p.B) {
+        prefetch_x(base + gridDim.x * 64, xsb + (parity & 1) * 64 * DP);
+        if (kHb2) dma_head(base + gridDim.x * 64, hbuf0 + (parity & 1) * HBF);
+      }
+    };
+    constexpr bool kHeadBar = kRedImg || kSplitHead;
+    if (!kHeadBar && kFactor) prefetch_next();  // (V1 / V3: no barrier before the next slab's)
     // every wave read the partials before dh2 overwrites them (kSplitHead: the dout table is visible)
-    if (kRedImg || kSplitHead) __syncthreads();
+    if (kHeadBar) {
+      __syncthreads();
+      prefetch_next();
+    }
 
     VG_STAMP(6);
     // ------------------------------------------------------------ dh2, dW3, db2 / dh1, db1
@@ -1098,6 +1109,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         accv[1] += reduce_scatter16(tv, j);
       }
       __syncthreads();
+      if (!kHeadBar) prefetch_next();  // after the dh2 barrier, for the same reason
       VG_STAMP(7);
       // dh1^T (own features) = dh2 x W2
       Split8 cur = frag_row(dhimg, j, 8 * g);
