@@ -487,8 +487,12 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   // feature own + j): summed inside the lane over the slabs, over the 4 lane groups once in
   // the epilogue.  DP = 4: vector FMAs on broadcast x rows; wider inputs: fp32 MFMA tiles.
   constexpr bool kDw1Mfma = DP > 4;
-  constexpr int NT1 = (DP + 15) / 16;
-  float acc1[kDw1Mfma ? 1 : DP];      // dW1[own + j][d], this lane's rows
+  // DP = 20 (D = 17..20): inputs 16..19 on the VALU beside the first tile's MFMAs (a second
+  // 16-wide tile would be 3/4 padding and cost as much MFMA time as the first)
+  constexpr int kTail1 = (DP > 16 && DP % 16 == 4) ? 4 : 0;
+  constexpr int NT1 = kTail1 ? DP / 16 : (DP + 15) / 16;
+  constexpr int NA1 = kDw1Mfma ? (kTail1 ? kTail1 : 1) : DP;
+  float acc1[NA1];                    // dW1[own + j][d] (kTail1: d = 16 NT1 + e), this lane's rows
   floatx4 acc1m[kDw1Mfma ? NT1 : 1];  // dW1[own + 4 g + i][16 nt + j]
   float db1acc = 0.f;                 // db1[own + j], this lane's rows
 #pragma unroll
@@ -496,7 +500,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 #pragma unroll
   for (int q = 0; q < NG; ++q) accv[q] = 0.f;
 #pragma unroll
-  for (int d = 0; d < (kDw1Mfma ? 1 : DP); ++d) acc1[d] = 0.f;
+  for (int d = 0; d < NA1; ++d) acc1[d] = 0.f;
 #pragma unroll
   for (int nt = 0; nt < (kDw1Mfma ? NT1 : 1); ++nt) acc1m[nt] = zero4();
   // db3 / dlog_std: wave w owns output a = w (NA <= 8 waves) and keeps its batch sum in one
@@ -1134,8 +1138,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 #pragma unroll
       for (int d4 = 0; d4 < DP / 4; ++d4) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc1[(4 * d4 + e) % (kDw1Mfma ? 1 : DP)] =
-            fmaf(dh1[bt][i], x[d4][e], acc1[(4 * d4 + e) % (kDw1Mfma ? 1 : DP)]);
+        for (int e = 0; e < 4; ++e) acc1[(4 * d4 + e) % NA1] = fmaf(dh1[bt][i], x[d4][e], acc1[(4 * d4 + e) % NA1]);
       }
     };
     auto load_xrow = [&](int row, floatx4 (&x)[DP / 4]) {
@@ -1157,6 +1160,11 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
               const int d = 16 * nt + j;
               const float xb = d < DP ? xs[row * DP + d] : 0.f;
               acc1m[nt] = mfma4(dh1[bt][i], xb, acc1m[nt]);
+            }
+            if (kTail1) {
+              const floatx4 xt = *reinterpret_cast<const floatx4*>(xs + row * DP + 16 * NT1);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc1[e % NA1] = fmaf(dh1[bt][i], xt[e], acc1[e % NA1]);
             }
           }
         }
@@ -1258,9 +1266,15 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         if (d < D) slab[o.w1 + (own + 4 * g + i) * D + d] = acc1m[nt][i];
       }
     }
+#pragma unroll
+    for (int e = 0; e < kTail1; ++e) {
+      const float sd = group_sum_swap(acc1[e % NA1]);  // over the 4 lane groups (all lanes call)
+      const int d = 16 * NT1 + e;
+      if (g == e && d < D) slab[o.w1 + (own + j) * D + d] = sd;
+    }
   } else {
 #pragma unroll
-    for (int d = 0; d < (kDw1Mfma ? 1 : DP); ++d) {
+    for (int d = 0; d < NA1; ++d) {
       const float sd = group_sum_swap(acc1[d]);  // over the 4 lane groups (all lanes call)
       if (g == (d & 3) && d < D) slab[o.w1 + (own + j) * D + d] = sd;
     }

@@ -62,7 +62,7 @@ def _run(mode, pp, X, ret, H):
 
 
 @pytest.mark.parametrize("D,B", [(4, 1), (4, 63), (4, 5000), (4, 70000), (8, 33000), (2, 777), (6, 4097), (3, 16),
-                                 (11, 3000), (16, 4100), (17, 33000), (24, 777)])
+                                 (11, 3000), (16, 4100), (17, 33000), (19, 5000), (20, 3000), (24, 777)])
 def test_split_kernel_matches_float64(cuda, D, B):
     H = 128
     g = torch.Generator().manual_seed(D * 1000 + B)
@@ -263,7 +263,7 @@ def _gauss64(head, pp, X, A, H, actc, adv, logp_old, stats, inv_B, clip, ent_coe
 
 
 @pytest.mark.parametrize("head", ["PG_GAUSS", "PPO_GAUSS"])
-@pytest.mark.parametrize("D,B,A", [(17, 33000, 6), (17, 777, 6), (3, 20000, 1), (8, 4097, 6)])
+@pytest.mark.parametrize("D,B,A", [(17, 33000, 6), (17, 777, 6), (20, 5000, 6), (3, 20000, 1), (8, 4097, 6)])
 def test_gaussian_split_kernel_matches_oracle(cuda, head, D, B, A):
     """Diagonal-Gaussian policy heads (HalfCheetah A = 6, Pendulum A = 1) on the bf16x6 kernel
     against the float64 oracle and the fp32-MFMA kernel, including the log_std gradient."""
