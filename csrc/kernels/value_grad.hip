@@ -1056,8 +1056,24 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       // reads), one pair at a time (sched barrier: hoisted together the reads held 24 registers
       // and the DP = 20 kernel spilled for them; a pair read ahead spilled too)
       floatx4 dd[4];
+      if constexpr (kSplitHead) {
+        // dd = dout x W3 on fp32 MFMA over k = outputs 4 s + g: A = W3[4 s + g][own + j], B =
+        // dout[row 16 bt + j][4 s + g] from the table; C comes out in h2's layout (lane (j, g):
+        // features own + 4 g + i of row 16 bt + j)
+        const float* w3v = vecs + 2 * kVgH + own + j;
+        const float wk0 = g < NA ? w3v[g * kVgH] : 0.f;
+        const float wk1 = 4 + g < NA ? w3v[(4 + g) * kVgH] : 0.f;
 #pragma unroll
-      for (int bt = 0; bt < 4; ++bt) dd[bt] = zero4();
+        for (int bt = 0; bt < 4; ++bt) {
+          const float* dr = dtab + (16 * bt + j) * NA;
+          const float b0 = g < NA ? dr[g] : 0.f;
+          const float b1 = 4 + g < NA ? dr[4 + g] : 0.f;
+          dd[bt] = mfma4(wk1, b1, mfma4(wk0, b0, zero4()));
+        }
+      } else {
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) dd[bt] = zero4();
+      }
       auto tab_pair = [&](int a2, vf32x2(&q)[4]) {
 #pragma unroll
         for (int bt = 0; bt < 4; ++bt) q[bt] = *reinterpret_cast<const vf32x2*>(dtab + (16 * bt + j) * NA + a2);
@@ -1070,14 +1086,14 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
           if (kSplitHead && (a & 1) == 0) tab_pair(a, vq);
-          const floatx4 w3a = *reinterpret_cast<const floatx4*>(w3p + a * kVgH);
+          const floatx4 w3a = kSplitHead ? zero4() : *reinterpret_cast<const floatx4*>(w3p + a * kVgH);
           const int f = a == 0 ? 1 : 3;
 #pragma unroll
           for (int bt = 0; bt < 4; ++bt) {
             const float v = kSplitHead ? vq[bt][a & 1] : __shfl(dout[a], 16 * bt + j, 64);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              dd[bt][r] = fmaf(w3a[r], v, dd[bt][r]);
+              if (!kSplitHead) dd[bt][r] = fmaf(w3a[r], v, dd[bt][r]);
               if (a < 2) tv[4 * f + r] = fmaf(v, h2[bt][r], tv[4 * f + r]);
             }
           }
