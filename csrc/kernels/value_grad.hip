@@ -350,6 +350,8 @@ constexpr int vg_prod_v(int DP) { return DP <= 4 ? 3 : 1; }
 template <int DP, int HEAD, int NA, bool STAMP = false, int V = vg_prod_v(DP)>
 __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   unsigned long long st_prev = 0, st_sum[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_entry = 0;  // STAMP: slots 10 / 11 = prologue / epilogue cycles per workgroup
+  if (STAMP) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_entry)::"memory");
   extern __shared__ __attribute__((aligned(16))) uint16_t vg_lds[];
   constexpr bool kValue = HEAD == HEAD_VALUE_MSE;
   constexpr bool kGauss = HEAD == HEAD_PG_GAUSS || HEAD == HEAD_PPO_GAUSS;
@@ -420,6 +422,74 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   const float* __restrict__ P = p.params;
   const int own = 16 * w;  // this wave's 16 hidden features
 
+  // Global inputs go straight to LDS by DMA (global_load_lds_dword: lane l's dword lands at
+  // the wave-uniform destination + 4 l), so no register holds them across the slab (held in
+  // registers they were spilled under the Gaussian heads' pressure, and every spill store
+  // waited for its HBM load).  The x slab [64][D] (compact, row stride D) is issued one slab
+  // ahead into the other half of the double buffer; the head inputs at the top of their own
+  // slab, behind ~6,000 cycles of layer 1 + layer 2.  The issuing waves wait for their DMAs
+  // (vmcnt) before the barrier that publishes them.  Rows past B load clamped duplicates:
+  // finite, and their dout is 0.
+  constexpr int NC = kGauss ? NA : 1;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  auto dma = [&](const void* src, long n, long first, float* dst, int chunks, int w0) {
+    for (int k = 0; k < chunks; ++k) {
+      if (((k + w0) & 7) == wu) {
+        const long e = min(first + 64L * k + l, n - 1);
+        __builtin_amdgcn_global_load_lds(static_cast<const uint32_t*>(src) + e,
+                                         (__attribute__((address_space(3))) void*)(dst + 64 * k), 4, 0, 0);
+      }
+    }
+  };
+  // x slab by DMA in the [64][DP] layout: chunk k covers LDS floats 64 k .. 64 k + 63 and lane
+  // l loads element (row q / DP, column min(q % DP, D - 1)) of q = 64 k + l, so a padding
+  // column holds a finite duplicate -- layer 1 multiplies it by W1's zero padding and dW1's
+  // padding outputs are never written.  (A compact stride-D layout needed per-read address
+  // arithmetic and selects: +2,500 cycles per slab at D = 17.)
+  // Value heads instead prefetch the x slab (XQ values per thread) and ret into registers a
+  // slab ahead (issued right after the head, stored to LDS at the next slab's top).
+  constexpr bool kDmaIn = !kValue;
+  constexpr int XQ = (64 * DP + 511) / 512;
+  float xr[kDmaIn ? 1 : XQ];
+  float hin_r = 0.f;
+  auto prefetch_x = [&](int b0, float* dst) {
+    if (kDmaIn) {
+      // this wave's chunks k = w, w + 8, ..: a runtime loop, so no per-chunk address is
+      // hoisted out of the slab loop into a live register
+      for (int k = wu; k < DP; k += 8) {
+        const int q = 64 * k + l, row = q / DP, d = q % DP;
+        const long e = (long)min(b0 + row, p.B - 1) * D + min(d, D - 1);
+        __builtin_amdgcn_global_load_lds(static_cast<const uint32_t*>(static_cast<const void*>(p.X)) + e,
+                                         (__attribute__((address_space(3))) void*)(dst + 64 * k), 4, 0, 0);
+      }
+    } else {
+      // unconditional loads from clamped addresses: nothing here consumes a loaded value (a
+      // select on it would make the compiler wait for the load right away)
+#pragma unroll
+      for (int i = 0; i < (kDmaIn ? 1 : XQ); ++i) {
+        const int q = min((int)threadIdx.x + 512 * i, 64 * DP - 1);
+        const int rl = q / DP, d = q % DP, b = b0 + rl;
+        xr[i] = p.X[(size_t)min(b, p.B - 1) * D + min(d, D - 1)];
+      }
+      hin_r = p.ret[min(b0 + l, p.B - 1)];
+    }
+  };
+  constexpr bool kHb2 = kDmaIn && vg_hbuf2(DP, HEAD, NA);
+  constexpr int HBF = vg_hbuf_bytes(HEAD, NA) / 4;  // floats per head-input buffer
+  auto dma_head = [&](int b0, float* hbuf) {
+    if (kDmaIn) {
+      dma(p.adv, p.B, b0, hbuf, 1, 3);
+      if (p.logp_old) dma(p.logp_old, p.B, b0, hbuf + 64, 1, 4);
+      if (kGauss) dma(p.actc, (long)p.B * NA, (long)b0 * NA, hbuf + 128, NA, 5);
+      else dma(p.act, p.B, b0, hbuf + 128, 1, 5);
+    }
+  };
+  auto vm_wait0 = []() { __builtin_amdgcn_s_waitcnt(0x0F70); };  // vmcnt(0) only
+  // the first slab's inputs go out before the weight loads of the prologue (which then hide
+  // their latency) rather than after them
+  prefetch_x(blockIdx.x * 64, xsb);
+  if (kHb2) dma_head(blockIdx.x * 64, hbuf0);
+
   // ---------------------------------------------------------------- stationary weights
   // hi + mid pieces in registers; the lo pieces of W2 go to an LDS image [o][i] that both
   // fragment kinds read once per 32-wide k-chunk (b128 for wA, transposed for wB)
@@ -449,8 +519,12 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     wB[c].m = sb.m;
     if (kFactor) wBl[c % (kFactor ? 4 : 1)] = sb.l;
   }
-  for (int q = threadIdx.x; q < kVgH * kVgH / 4; q += blockDim.x) {
-    floatx4 v;
+  // (512 threads: 8 rows of 4 each, unrolled so the 8 loads are in flight together -- as a
+  // runtime loop each iteration waited for its own load: ~6,000 of a ~14,500-cycle prologue)
+#pragma unroll
+  for (int it = 0; it < kVgH * kVgH / 4 / 512; ++it) {
+    const int q = (int)threadIdx.x + 512 * it;
+    floatx4 v;  // (element loads: params may be a slice of a flat buffer, 4-byte aligned only)
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = P[o.w2 + 4 * q + e];
     vbf16x4 h, m, lo;
@@ -524,74 +598,11 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   };
   float s_loss = 0.f, s_val = 0.f, s_cnt = 0.f, s_ent = 0.f, s_kl = 0.f, s_clip = 0.f;
 
-  // Global inputs go straight to LDS by DMA (global_load_lds_dword: lane l's dword lands at
-  // the wave-uniform destination + 4 l), so no register holds them across the slab (held in
-  // registers they were spilled under the Gaussian heads' pressure, and every spill store
-  // waited for its HBM load).  The x slab [64][D] (compact, row stride D) is issued one slab
-  // ahead into the other half of the double buffer; the head inputs at the top of their own
-  // slab, behind ~6,000 cycles of layer 1 + layer 2.  The issuing waves wait for their DMAs
-  // (vmcnt) before the barrier that publishes them.  Rows past B load clamped duplicates:
-  // finite, and their dout is 0.
-  constexpr int NC = kGauss ? NA : 1;
-  const int wu = __builtin_amdgcn_readfirstlane(w);
-  auto dma = [&](const void* src, long n, long first, float* dst, int chunks, int w0) {
-    for (int k = 0; k < chunks; ++k) {
-      if (((k + w0) & 7) == wu) {
-        const long e = min(first + 64L * k + l, n - 1);
-        __builtin_amdgcn_global_load_lds(static_cast<const uint32_t*>(src) + e,
-                                         (__attribute__((address_space(3))) void*)(dst + 64 * k), 4, 0, 0);
-      }
-    }
-  };
-  // x slab by DMA in the [64][DP] layout: chunk k covers LDS floats 64 k .. 64 k + 63 and lane
-  // l loads element (row q / DP, column min(q % DP, D - 1)) of q = 64 k + l, so a padding
-  // column holds a finite duplicate -- layer 1 multiplies it by W1's zero padding and dW1's
-  // padding outputs are never written.  (A compact stride-D layout needed per-read address
-  // arithmetic and selects: +2,500 cycles per slab at D = 17.)
-  // Value heads instead prefetch the x slab (XQ values per thread) and ret into registers a
-  // slab ahead (issued right after the head, stored to LDS at the next slab's top).
-  constexpr bool kDmaIn = !kValue;
-  constexpr int XQ = (64 * DP + 511) / 512;
-  float xr[kDmaIn ? 1 : XQ];
-  float hin_r = 0.f;
-  auto prefetch_x = [&](int b0, float* dst) {
-    if (kDmaIn) {
-      // this wave's chunks k = w, w + 8, ..: a runtime loop, so no per-chunk address is
-      // hoisted out of the slab loop into a live register
-      for (int k = wu; k < DP; k += 8) {
-        const int q = 64 * k + l, row = q / DP, d = q % DP;
-        const long e = (long)min(b0 + row, p.B - 1) * D + min(d, D - 1);
-        __builtin_amdgcn_global_load_lds(static_cast<const uint32_t*>(static_cast<const void*>(p.X)) + e,
-                                         (__attribute__((address_space(3))) void*)(dst + 64 * k), 4, 0, 0);
-      }
-    } else {
-      // unconditional loads from clamped addresses: nothing here consumes a loaded value (a
-      // select on it would make the compiler wait for the load right away)
-#pragma unroll
-      for (int i = 0; i < (kDmaIn ? 1 : XQ); ++i) {
-        const int q = min((int)threadIdx.x + 512 * i, 64 * DP - 1);
-        const int rl = q / DP, d = q % DP, b = b0 + rl;
-        xr[i] = p.X[(size_t)min(b, p.B - 1) * D + min(d, D - 1)];
-      }
-      hin_r = p.ret[min(b0 + l, p.B - 1)];
-    }
-  };
-  constexpr bool kHb2 = kDmaIn && vg_hbuf2(DP, HEAD, NA);
-  constexpr int HBF = vg_hbuf_bytes(HEAD, NA) / 4;  // floats per head-input buffer
-  auto dma_head = [&](int b0, float* hbuf) {
-    if (kDmaIn) {
-      dma(p.adv, p.B, b0, hbuf, 1, 3);
-      if (p.logp_old) dma(p.logp_old, p.B, b0, hbuf + 64, 1, 4);
-      if (kGauss) dma(p.actc, (long)p.B * NA, (long)b0 * NA, hbuf + 128, NA, 5);
-      else dma(p.act, p.B, b0, hbuf + 128, 1, 5);
-    }
-  };
-  auto vm_wait0 = []() { __builtin_amdgcn_s_waitcnt(0x0F70); };  // vmcnt(0) only
-  prefetch_x(blockIdx.x * 64, xsb);
-  if (kHb2) dma_head(blockIdx.x * 64, hbuf0);
   if ((p.tune & 1) && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   if ((p.tune & 2) && __builtin_amdgcn_readfirstlane(threadIdx.x) < 256) __builtin_amdgcn_s_setprio(1);
 
+  VG_STAMP(0);
+  if (STAMP) st_sum[10] = st_prev - st_entry;
   for (int base = blockIdx.x * 64; base < p.B; base += gridDim.x * 64) {
     VG_STAMP(0);
     // ------------------------------------------------------------ x slab (DMA'd a slab ago)
@@ -1249,10 +1260,6 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     }
     VG_STAMP(10);
   }
-  if (STAMP && p.stamps != nullptr && l == 0) {
-#pragma unroll
-    for (int k = 0; k < 10; ++k) p.stamps[(blockIdx.x * 8 + w) * 16 + k] = st_sum[k];
-  }
 
   // ------------------------------------------------------------------ epilogue
   if (kTvPersist) accv[0] += fold_tvs();
@@ -1339,6 +1346,15 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       lsl[3] = scl;
       lsl[4] = sv;
       lsl[5] = sc;
+    }
+  }
+  if (STAMP && p.stamps != nullptr) {
+    unsigned long long t_end;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_end)::"memory");
+    st_sum[11] = t_end - st_prev;
+    if (l == 0) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) p.stamps[(blockIdx.x * 8 + w) * 16 + k] = st_sum[k];
     }
   }
 }

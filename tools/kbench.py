@@ -37,6 +37,11 @@ def run_stamps(fn, ns, tune, label, rows):
     seg = st.view(ns, 8, 16).double().mean(0) / slabs_per_wg
     res = {STAMP_NAMES[k]: [round(x, 1) for x in seg[:, k].tolist()] for k in range(10)}
     res["total_w0_w4"] = [round(float(seg[0, :10].sum()), 1), round(float(seg[4, :10].sum()), 1)]
+    # once per workgroup, not per slab: kernel entry -> loop, last slab -> kernel end
+    per_wg = st.view(ns, 8, 16).double().mean(0)
+    res["prologue_per_wg"] = [round(x, 1) for x in per_wg[:, 10].tolist()]
+    res["epilogue_per_wg"] = [round(x, 1) for x in per_wg[:, 11].tolist()]
+    res["slabs_per_wg"] = slabs_per_wg
     print(json.dumps({"stamps_cycles_per_slab_per_wave": res, "tune": tune, "kernel": label}))
 
 
