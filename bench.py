@@ -55,6 +55,10 @@ def parse(argv=None):
     ap.add_argument("--ttt-envs", type=int, default=1024)
     ap.add_argument("--ttt-rollout-len", type=int, default=64)
     ap.add_argument("--ttt-vf-iters", type=int, default=5)
+    ap.add_argument("--ttt-ref-envs", type=int, default=512,
+                    help="batch shape of the reference-hyperparameter TTT runs (tools/ttt_sweep.py --grid refhp: "
+                         "512 x 16 was the fastest of 256..4096 envs x 16..128 steps)")
+    ap.add_argument("--ttt-ref-rollout-len", type=int, default=16)
     ap.add_argument("--ttt-pi-lr", type=float, default=1e-2)
     ap.add_argument("--ttt-vf-lr", type=float, default=1e-2)
     ap.add_argument("--ttt-graphs", action="store_true",
@@ -234,7 +238,9 @@ def main(argv=None):
         shape = {"num_envs": args.ttt_envs, "rollout_len": args.ttt_rollout_len}
         ttt = time_to_threshold(tuned, dict(shape, use_graphs=bool(args.ttt_graphs)), args.ttt_seeds,
                                 args.ttt_max_s, comm)
-        ttt_ref = time_to_threshold(ref_hp, dict(shape, use_graphs=True), args.ttt_ref_seeds, args.ttt_max_s, comm)
+        ref_shape = {"num_envs": args.ttt_ref_envs, "rollout_len": args.ttt_ref_rollout_len}
+        ttt_ref = time_to_threshold(ref_hp, dict(ref_shape, use_graphs=True), args.ttt_ref_seeds, args.ttt_max_s,
+                                    comm)
     ref_cpu = collect_reference_cpu(ref_proc, args.ref_cpu_seconds)
     if rank == 0:
         algo = "REINFORCE" if args.no_baseline else "REINFORCE-with-baseline"
@@ -284,7 +290,9 @@ def main(argv=None):
                 "tuned": pack(ttt, {"gamma": 0.99, "lam": 0.95, "pi_lr": args.ttt_pi_lr, "vf_lr": args.ttt_vf_lr,
                                     "train_vf_iters": args.ttt_vf_iters}, shape_cfg, args.ttt_seeds),
                 "reference_hparams": pack(ttt_ref, {"gamma": 0.98, "lam": 0.97, "pi_lr": 3e-4, "vf_lr": 1e-3,
-                                                    "train_vf_iters": 80}, shape_cfg, args.ttt_ref_seeds),
+                                                    "train_vf_iters": 80},
+                                          {"num_envs": args.ttt_ref_envs, "rollout_len": args.ttt_ref_rollout_len},
+                                          args.ttt_ref_seeds),
             }
         if ref_cpu is not None:
             rec["reference_equivalent_cpu"] = {

@@ -14,13 +14,16 @@ from relayrl_prototype_amd.runtime.vec_trainer import VecTrainer, VecTrainerConf
 
 
 REF = "--ref" in sys.argv  # the reference hyperparameters (80 value iterations per epoch)
+# --shape N T: envs x rollout length (default 1024 x 64)
+SHAPE = (int(sys.argv[sys.argv.index("--shape") + 1]), int(sys.argv[sys.argv.index("--shape") + 2])) \
+    if "--shape" in sys.argv else (1024, 64)
 
 
 def cfg(**kw):
     if REF:
-        return VecTrainerConfig(num_envs=1024, rollout_len=64, with_baseline=True, pi_lr=3e-4, vf_lr=1e-3,
+        return VecTrainerConfig(num_envs=SHAPE[0], rollout_len=SHAPE[1], with_baseline=True, pi_lr=3e-4, vf_lr=1e-3,
                                 train_vf_iters=80, gamma=0.98, lam=0.97, seed=1, **kw)
-    return VecTrainerConfig(num_envs=1024, rollout_len=64, with_baseline=True, pi_lr=1e-2, vf_lr=3e-3,
+    return VecTrainerConfig(num_envs=SHAPE[0], rollout_len=SHAPE[1], with_baseline=True, pi_lr=1e-2, vf_lr=3e-3,
                             train_vf_iters=10, gamma=0.99, lam=0.95, seed=1, **kw)
 
 

@@ -28,6 +28,10 @@ GRIDS = {
         (256, 64, 5, 1e-2, 1e-2), (512, 64, 10, 2e-2, 1e-2), (256, 64, 10, 1e-2, 1e-2), (512, 64, 10, 1e-2, 1e-2),
         (1024, 32, 5, 1e-2, 1e-2), (256, 32, 10, 2e-2, 1e-2), (512, 32, 5, 1e-2, 3e-3), (1024, 64, 5, 1e-2, 1e-2),
         (1024, 64, 10, 1e-2, 3e-3), (512, 64, 5, 1e-2, 1e-2)]],
+    # the reference hyperparameters (REINFORCE.py / default_config.json: 80 value iterations,
+    # pi lr 3e-4, vf lr 1e-3, gamma .98, lam .97): only the batch shape is free
+    "refhp": (itertools.product([256, 512, 1024, 2048, 4096], [16, 32, 64, 128], [80], [3e-4], [1e-3],
+                                [0.98], [0.97])),
 }
 
 
