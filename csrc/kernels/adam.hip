@@ -29,15 +29,24 @@ struct AdamArgs {
 constexpr int kAdamCols = 64;
 constexpr int kAdamGroups = 16;
 
-// Partial sum of column p over the slabs k = grp, grp + 16, ... (one of 16 groups).
+// Partial sum of column p over the slabs k = grp, grp + 16, ... (one of 16 groups).  Up to 8
+// loads in flight per thread: at the small-batch value step (128 slabs, 8 per thread) the
+// whole sum is one HBM latency instead of two.
 RRL_DEV float slab_group_sum(const float* __restrict__ slab, int nslab, int P, int p, int grp) {
   const float* s = slab + p;
   float g = 0.f;
   int k = grp;
-  for (; k + 3 * kAdamGroups < nslab; k += 4 * kAdamGroups) {
+  for (; k + 7 * kAdamGroups < nslab; k += 8 * kAdamGroups) {
+    float q[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = s[(size_t)(k + i * kAdamGroups) * P];
+    g += ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+  }
+  if (k + 3 * kAdamGroups < nslab) {
     const float g0 = s[(size_t)k * P], g1 = s[(size_t)(k + kAdamGroups) * P];
     const float g2 = s[(size_t)(k + 2 * kAdamGroups) * P], g3 = s[(size_t)(k + 3 * kAdamGroups) * P];
     g += (g0 + g1) + (g2 + g3);
+    k += 4 * kAdamGroups;
   }
   for (; k < nslab; k += kAdamGroups) g += s[(size_t)k * P];
   return g;
@@ -49,6 +58,13 @@ __global__ __launch_bounds__(1024) void adam_kernel(AdamArgs a) {
   const int col = threadIdx.x & (kAdamCols - 1);
   const int grp = threadIdx.x / kAdamCols;
   const int p = blockIdx.x * kAdamCols + col;
+  // the update's own operands are loaded before the slab sum, so their latency hides under it
+  float w = 0.f, m0 = 0.f, v0 = 0.f;
+  if (grp == 0 && p < a.P) {
+    w = a.param[p];
+    m0 = a.m[p];
+    v0 = a.v[p];
+  }
   float g = 0.f;
   if (p < a.P) {
     if (a.grad) {
@@ -67,10 +83,9 @@ __global__ __launch_bounds__(1024) void adam_kernel(AdamArgs a) {
     if (a.grad_out) a.grad_out[p] = gs;
     const float bc1 = 1.f - __powf(a.beta1, (float)t);
     const float bc2 = 1.f - __powf(a.beta2, (float)t);
-    float w = a.param[p];
     if (a.weight_decay != 0.f) gs += a.weight_decay * w;
-    const float m = a.beta1 * a.m[p] + (1.f - a.beta1) * gs;
-    const float v = a.beta2 * a.v[p] + (1.f - a.beta2) * gs * gs;
+    const float m = a.beta1 * m0 + (1.f - a.beta1) * gs;
+    const float v = a.beta2 * v0 + (1.f - a.beta2) * gs * gs;
     a.m[p] = m;
     a.v[p] = v;
     // torch.optim.Adam: p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)

@@ -491,25 +491,77 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   if (kHb2) dma_head(blockIdx.x * 64, hbuf0);
 
   // ---------------------------------------------------------------- stationary weights
-  // hi + mid pieces in registers; the lo pieces of W2 go to an LDS image [o][i] that both
+  // W2 is staged once in fp32 through the activation images (free until the first slab's
+  // barrier): 8 b128 global loads per thread instead of ~130 element loads (the strided wB
+  // columns and the w3 scale were one 4-byte load per lane each), and its lo pieces go to the
+  // W2 lo image from the same registers.  Then each wave reads its fragments from LDS.
+  // (Element loads when the params slice is not 16-byte aligned.)
+  constexpr int kW2Ld = kVgH + 4;  // fp32 row stride of the staged W2 (16-byte rows, 2-way bank split)
+  static_assert(kVgH * kW2Ld * 4 <= 6 * kVgImg * 2, "staged W2 must fit in the activation images");
+  float* w2s = reinterpret_cast<float*>(vg_lds);
+  // head scalars b3[NA], log_std[NA], 1/std[NA] in LDS after w3 (read once per slab by the head)
+  float* hsc = vecs + (2 + NA) * kVgH;
+  // (the other weights' loads go out with W2's, ahead of the staging barrier)
+  float w1a[KS1];  // layer-1 A operand: W1[own + j][4s + g]
+#pragma unroll
+  for (int s = 0; s < KS1; ++s) {
+    const int k = 4 * s + g;
+    w1a[s] = (k < D) ? P[o.w1 + (own + j) * D + k] : 0.f;
+  }
+  {
+    const float* gw2 = P + o.w2;
+    const bool al16 = (reinterpret_cast<uintptr_t>(gw2) & 15) == 0;
+    floatx4 v[kVgH * kVgH / 4 / 512];
+#pragma unroll
+    for (int it = 0; it < kVgH * kVgH / 4 / 512; ++it) {
+      const int q = (int)threadIdx.x + 512 * it;  // float4 q: row q >> 5, columns 4 (q & 31) ..
+      if (al16) {
+        v[it] = *reinterpret_cast<const floatx4*>(gw2 + 4 * q);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[it][e] = gw2[4 * q + e];
+      }
+    }
+    for (int q = threadIdx.x; q < (2 + NA) * kVgH; q += blockDim.x) {
+      const int k = q >> 7, f = q & (kVgH - 1);
+      vecs[q] = P[(k == 0 ? o.b1 : k == 1 ? o.b2 : o.w3 + (k - 2) * kVgH) + f];
+    }
+    if (threadIdx.x < NA) {
+      const int a = threadIdx.x;
+      const float lsa = kGauss ? P[o.log_std + a] : 0.f;
+      hsc[a] = P[o.b3 + a];
+      hsc[NA + a] = lsa;
+      hsc[2 * NA + a] = __expf(-lsa);
+    }
+#pragma unroll
+    for (int it = 0; it < kVgH * kVgH / 4 / 512; ++it) {
+      const int q = (int)threadIdx.x + 512 * it;
+      *reinterpret_cast<floatx4*>(w2s + (q >> 5) * kW2Ld + 4 * (q & 31)) = v[it];
+      vbf16x4 h, m, lo;
+      split4(v[it], h, m, lo);
+      *reinterpret_cast<vbf16x4*>(w2lo + (q >> 5) * kVgLd + 4 * (q & 31)) = lo;
+    }
+  }
+  __syncthreads();  // staged W2 and b1 / b2 / w3 visible
+  // hi + mid pieces in registers; the lo pieces of W2 sit in the LDS image [o][i] that both
   // fragment kinds read once per 32-wide k-chunk (b128 for wA, transposed for wB)
   Split8HM wA[4], wB[4];
   vbf16x8 wBl[kFactor ? 4 : 1];  // lo pieces of A' (kFactor)
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    floatx4 a0, a1, b0, b1;
+    // wA: A[m = own + j][k = 32c + 8g + e] = W2[m][k]      (forward)
+    const floatx4 a0 = *reinterpret_cast<const floatx4*>(w2s + (own + j) * kW2Ld + 32 * c + 8 * g);
+    const floatx4 a1 = *reinterpret_cast<const floatx4*>(w2s + (own + j) * kW2Ld + 32 * c + 8 * g + 4);
+    floatx4 b0, b1;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      // wA: A[m = own + j][k = 32c + 8g + e] = W2[m][k]      (forward)
-      a0[e] = P[o.w2 + (own + j) * kVgH + 32 * c + 8 * g + e];
-      a1[e] = P[o.w2 + (own + j) * kVgH + 32 * c + 8 * g + 4 + e];
       // wB: A[m = own + j][k = 32c + 8g + e] = W2[k][m]      (backward data)
       //     (kFactor: A'[m][k] = W2[k][m] * w3[k])
-      b0[e] = P[o.w2 + (32 * c + 8 * g + e) * kVgH + own + j];
-      b1[e] = P[o.w2 + (32 * c + 8 * g + 4 + e) * kVgH + own + j];
+      b0[e] = w2s[(32 * c + 8 * g + e) * kW2Ld + own + j];
+      b1[e] = w2s[(32 * c + 8 * g + 4 + e) * kW2Ld + own + j];
       if (kFactor) {
-        b0[e] *= P[o.w3 + 32 * c + 8 * g + e];
-        b1[e] *= P[o.w3 + 32 * c + 8 * g + 4 + e];
+        b0[e] *= vecs[2 * kVgH + 32 * c + 8 * g + e];
+        b1[e] *= vecs[2 * kVgH + 32 * c + 8 * g + 4 + e];
       }
     }
     const Split8 sa = split8(a0, a1), sb = split8(b0, b1);
@@ -518,37 +570,6 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     wB[c].h = sb.h;
     wB[c].m = sb.m;
     if (kFactor) wBl[c % (kFactor ? 4 : 1)] = sb.l;
-  }
-  // (512 threads: 8 rows of 4 each, unrolled so the 8 loads are in flight together -- as a
-  // runtime loop each iteration waited for its own load: ~6,000 of a ~14,500-cycle prologue)
-#pragma unroll
-  for (int it = 0; it < kVgH * kVgH / 4 / 512; ++it) {
-    const int q = (int)threadIdx.x + 512 * it;
-    floatx4 v;  // (element loads: params may be a slice of a flat buffer, 4-byte aligned only)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = P[o.w2 + 4 * q + e];
-    vbf16x4 h, m, lo;
-    split4(v, h, m, lo);
-    *reinterpret_cast<vbf16x4*>(w2lo + (q >> 5) * kVgLd + 4 * (q & 31)) = lo;
-  }
-  float w1a[KS1];  // layer-1 A operand: W1[own + j][4s + g]
-#pragma unroll
-  for (int s = 0; s < KS1; ++s) {
-    const int k = 4 * s + g;
-    w1a[s] = (k < D) ? P[o.w1 + (own + j) * D + k] : 0.f;
-  }
-  for (int q = threadIdx.x; q < (2 + NA) * kVgH; q += blockDim.x) {
-    const int k = q >> 7, f = q & (kVgH - 1);
-    vecs[q] = P[(k == 0 ? o.b1 : k == 1 ? o.b2 : o.w3 + (k - 2) * kVgH) + f];
-  }
-  // head scalars b3[NA], log_std[NA], 1/std[NA] in LDS after w3 (read once per slab by the head)
-  float* hsc = vecs + (2 + NA) * kVgH;
-  if (threadIdx.x < NA) {
-    const int a = threadIdx.x;
-    const float lsa = kGauss ? P[o.log_std + a] : 0.f;
-    hsc[a] = P[o.b3 + a];
-    hsc[NA + a] = lsa;
-    hsc[2 * NA + a] = __expf(-lsa);
   }
   // per C-layout row own + 4g + r (re-read from LDS where used)
   const float* b1p = vecs + own + 4 * g;

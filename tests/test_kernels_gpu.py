@@ -158,6 +158,30 @@ def test_grad_reduce_and_adam_match_torch(cuda):
     torch.testing.assert_close(red.cpu(), slab.sum(0).cpu() * 0.5, rtol=1e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("nslab", [1, 5, 63, 64, 128, 129, 200, 256, 300])
+def test_slab_reduction_and_adam_all_batchings(cuda, nslab):
+    """The slab sum issues 8 loads, then 4, then single loads per thread: every path vs fp64."""
+    torch.manual_seed(nslab)
+    P = 17_000
+    slab = torch.randn(nslab, P)
+    ref_sum = slab.double().sum(0)
+    red = reduce_slabs(slab.to(cuda), 1.0)
+    torch.testing.assert_close(red.cpu().double(), ref_sum, rtol=1e-5, atol=1e-5)
+    p0 = torch.randn(P)
+    pg = p0.clone().to(cuda)
+    m = torch.zeros_like(pg)
+    v = torch.zeros_like(pg)
+    step = torch.zeros(1, dtype=torch.int32, device=cuda)
+    ticket = torch.zeros(1, dtype=torch.int32, device=cuda)
+    adam_step(pg, m, v, step, ticket, 1e-3, slab=slab.to(cuda))
+    pt = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pt], lr=1e-3)
+    pt.grad = ref_sum.float()
+    opt.step()
+    assert int(step.item()) == 1
+    torch.testing.assert_close(pg.cpu(), pt.detach(), rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("T,N,baseline", [(64, 1000, True), (128, 33, False), (7, 5000, True)])
 def test_gae_scan_tm(cuda, T, N, baseline):
     torch.manual_seed(T + N)
