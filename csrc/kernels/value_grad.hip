@@ -86,10 +86,13 @@ constexpr bool vg_hbuf2(int DP, int HEAD, int NA) {
                                              2 * vg_hbuf_bytes(HEAD, NA) + vg_dtab_bytes(HEAD, NA) <=
                                          160 * 1024;
 }
+// Factored value head: each wave's copy of the slab's dout [8 waves][64 rows] (the wave reads
+// its own rows back as b128 / b32 LDS reads instead of 20 ds_bpermutes per slab), last in LDS.
+constexpr int vg_dw_bytes(int DP, int HEAD) { return vg_factor(DP, HEAD) ? 8 * 64 * 4 : 0; }
 constexpr int vg_total_bytes(int DP, int HEAD, int NA) {
   return vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD) +
          (vg_red_in_image(DP, NA) ? 0 : (vg_hbuf2(DP, HEAD, NA) ? 2 : 1) * vg_hbuf_bytes(HEAD, NA)) +
-         vg_dtab_bytes(HEAD, NA);
+         vg_dtab_bytes(HEAD, NA) + vg_dw_bytes(DP, HEAD);
 }
 static_assert(vg_red_bytes(6) + vg_hbuf_bytes(HEAD_PPO_GAUSS, 6) <= 3 * kVgImg * 2, "head inputs in the dh2 image");
 static_assert(vg_total_bytes(8, HEAD_VALUE_MSE, 1) <= 160 * 1024, "factored LDS plan");
@@ -975,8 +978,19 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     };
     if (kFactor) {
       float dv[4];  // dout of C-layout row 16 bt + j (the dh2' tiles)
+      // kMaskB: the wave's dout table (lane l writes row l; only this wave reads it back)
+      float* dtw = reinterpret_cast<float*>(reinterpret_cast<char*>(vg_lds) + vg_total_bytes(DP, HEAD, NA) -
+                                            vg_dw_bytes(DP, HEAD)) + 64 * w;
+      if (kMaskB) {
+        dtw[l] = dout[0];
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int bt = 0; bt < 4; ++bt) dv[bt] = __shfl(dout[0], 16 * bt + j, 64);
+        for (int bt = 0; bt < 4; ++bt) dv[bt] = dtw[16 * bt + j];
+      } else {
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) dv[bt] = __shfl(dout[0], 16 * bt + j, 64);
+      }
       float* tv = tvs;  // fields: db2' (x w3 in the epilogue), dW3 row 0 (kTvPersist: kept over slabs)
       if (!kTvPersist) {
 #pragma unroll
@@ -1064,10 +1078,20 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
           const float vh = __uint_as_float(cvt_pk_bf16(sr, sr) << 16);
           sr = vh != 0.f ? sr * __builtin_amdgcn_rcpf(vh) : 0.f;  // 1 ulp: within fp32 accuracy
         }
+        if (kMaskB) {
+          // rows 16 bt + 4 g .. + 3 of the wave's dout table: one b128 read per batch tile
 #pragma unroll
-        for (int bt = 0; bt < 4; ++bt) {
+          for (int bt = 0; bt < 4; ++bt) {
+            const floatx4 d4 = *reinterpret_cast<const floatx4*>(dtw + 16 * bt + 4 * g);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) dh1[bt][i] *= __shfl(sr, 16 * bt + 4 * g + i, 64);
+            for (int i = 0; i < 4; ++i) dh1[bt][i] *= d4[i];
+          }
+        } else {
+#pragma unroll
+          for (int bt = 0; bt < 4; ++bt) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dh1[bt][i] *= __shfl(sr, 16 * bt + 4 * g + i, 64);
+          }
         }
         dh1_relu();
       };
