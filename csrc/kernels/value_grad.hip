@@ -88,7 +88,12 @@ constexpr bool vg_hbuf2(int DP, int HEAD, int NA) {
 }
 // Factored value head: each wave's copy of the slab's dout [8 waves][64 rows] (the wave reads
 // its own rows back as b128 / b32 LDS reads instead of 20 ds_bpermutes per slab), last in LDS.
-constexpr int vg_dw_bytes(int DP, int HEAD) { return vg_factor(DP, HEAD) ? 8 * 64 * 4 : 0; }
+// (Other value heads too, where LDS allows: 4 ds_bpermutes per slab there.)
+constexpr int vg_dw_bytes(int DP, int HEAD) {
+  return (vg_factor(DP, HEAD) || (HEAD == HEAD_VALUE_MSE && vg_lds_bytes(DP, 1) + 8 * 64 * 4 <= 160 * 1024))
+             ? 8 * 64 * 4
+             : 0;
+}
 constexpr int vg_total_bytes(int DP, int HEAD, int NA) {
   return vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD) +
          (vg_red_in_image(DP, NA) ? 0 : (vg_hbuf2(DP, HEAD, NA) ? 2 : 1) * vg_hbuf_bytes(HEAD, NA)) +
@@ -96,6 +101,8 @@ constexpr int vg_total_bytes(int DP, int HEAD, int NA) {
 }
 static_assert(vg_red_bytes(6) + vg_hbuf_bytes(HEAD_PPO_GAUSS, 6) <= 3 * kVgImg * 2, "head inputs in the dh2 image");
 static_assert(vg_total_bytes(8, HEAD_VALUE_MSE, 1) <= 160 * 1024, "factored LDS plan");
+static_assert(vg_dw_bytes(20, HEAD_VALUE_MSE) > 0 && vg_total_bytes(20, HEAD_VALUE_MSE, 1) <= 160 * 1024,
+              "dout table of the D = 17..20 value kernel");
 static_assert(vg_lds_bytes(24, 1) <= 160 * 1024 && !vg_red_in_image(24, 1), "value-grad LDS plan");
 static_assert(vg_lds_bytes(20, 6) <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
 static_assert(vg_red_bytes(6) <= 3 * kVgImg * 2, "head partials must fit in the dh2 image");
@@ -976,11 +983,13 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         }
       }
     };
+    // the wave's dout table (lane l writes row l; only this wave reads it back): kMaskB and the
+    // non-factored value heads
+    constexpr bool kDwTab = vg_dw_bytes(DP, HEAD) > 0 && (kMaskB || !kFactor);
+    float* dtw = reinterpret_cast<float*>(reinterpret_cast<char*>(vg_lds) + vg_total_bytes(DP, HEAD, NA) -
+                                          vg_dw_bytes(DP, HEAD)) + 64 * w;
     if (kFactor) {
       float dv[4];  // dout of C-layout row 16 bt + j (the dh2' tiles)
-      // kMaskB: the wave's dout table (lane l writes row l; only this wave reads it back)
-      float* dtw = reinterpret_cast<float*>(reinterpret_cast<char*>(vg_lds) + vg_total_bytes(DP, HEAD, NA) -
-                                            vg_dw_bytes(DP, HEAD)) + 64 * w;
       if (kMaskB) {
         dtw[l] = dout[0];
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -1135,6 +1144,11 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         for (int bt = 0; bt < 4; ++bt) q[bt] = *reinterpret_cast<const vf32x2*>(dtab + (16 * bt + j) * NA + a2);
       };
       vf32x2 vq[4];
+      if (kDwTab) {
+        dtw[l] = dout[0];
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
       {
         float tv[16];  // this slab's field partials of features own + 4g + r
 #pragma unroll
@@ -1146,7 +1160,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
           const int f = a == 0 ? 1 : 3;
 #pragma unroll
           for (int bt = 0; bt < 4; ++bt) {
-            const float v = kSplitHead ? vq[bt][a & 1] : __shfl(dout[a], 16 * bt + j, 64);
+            const float v = kSplitHead ? vq[bt][a & 1] : kDwTab ? dtw[16 * bt + j] : __shfl(dout[a], 16 * bt + j, 64);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               if (!kSplitHead) dd[bt][r] = fmaf(w3a[r], v, dd[bt][r]);
