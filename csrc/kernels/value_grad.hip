@@ -47,6 +47,9 @@ typedef __bf16 vbf16x4 __attribute__((ext_vector_type(4)));
 typedef short vs16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kVgH = 128;
+#ifndef VG_MT2
+#define VG_MT2 1
+#endif
 constexpr int kVgLd = 144;          // bf16 row stride of the activation images
 constexpr int kVgImg = 64 * kVgLd;  // elements per image piece
 // LDS: h1 + dh2 images (3 pieces each), head partials [8 waves][NA][64], x slabs [2][64][DP],
@@ -1048,21 +1051,31 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
           uint32_t mrow[4];
 #pragma unroll
           for (int bt = 0; bt < 4; ++bt) mrow[bt] = mk[(16 * bt + j) * 4 + g];
-          vbf16x8 cur = mtab[mrow[0] & 0xffu];
+          // table fragments read two steps ahead (VG_MT2): one step of 3 MFMAs did not cover
+          // the LDS latency (an lgkmcnt(0) wait before every step)
+          constexpr int kAhead = VG_MT2 ? 2 : 1;
+          auto mfrag = [&](int it) { return mtab[(mrow[it & 3] >> (8 * (it >> 2))) & 0xffu]; };
+          vbf16x8 q0 = mfrag(0), q1;
+          if (kAhead == 2) q1 = mfrag(1);
 #pragma unroll
           for (int it = 0; it < 16; ++it) {
             const int c = it >> 2, bt = it & 3;
             vbf16x8 nxt;
-            if (it + 1 < 16) nxt = mtab[(mrow[(it + 1) & 3] >> (8 * ((it + 1) >> 2))) & 0xffu];
-            dh1[bt] = mfma_bf16(cur, wBl[c % (kFactor ? 4 : 1)], dh1[bt]);
-            dh1[bt] = mfma_bf16(cur, wB[c].m, dh1[bt]);
-            dh1[bt] = mfma_bf16(cur, wB[c].h, dh1[bt]);
+            if (it + kAhead < 16) nxt = mfrag(it + kAhead);
+            dh1[bt] = mfma_bf16(q0, wBl[c % (kFactor ? 4 : 1)], dh1[bt]);
+            dh1[bt] = mfma_bf16(q0, wB[c].m, dh1[bt]);
+            dh1[bt] = mfma_bf16(q0, wB[c].h, dh1[bt]);
             if (kInterleave) {  // this wave's dh2 work beside its own MFMAs
               if ((it & 3) == 1) kf_tile(it >> 2);
               if (it == 15) kf_finish();
             }
             __builtin_amdgcn_sched_barrier(0);
-            if (it + 1 < 16) cur = nxt;
+            if (kAhead == 2) {
+              q0 = q1;
+              if (it + 2 < 16) q1 = nxt;
+            } else if (it + 1 < 16) {
+              q0 = nxt;
+            }
           }
         } else {
           // dh1^T = rr * (hi(dh2') x A'^T): the hi piece alone is exact (mask * hi(dout))
