@@ -30,6 +30,13 @@ GRIDS = {
         (1024, 64, 10, 1e-2, 3e-3), (512, 64, 5, 1e-2, 1e-2)]],
     # the reference hyperparameters (REINFORCE.py / default_config.json: 80 value iterations,
     # pi lr 3e-4, vf lr 1e-3, gamma .98, lam .97): only the batch shape is free
+    # round 2 (faster value kernel, small-batch fixed costs cut): tuned-config shapes incl. 16-step rollouts
+    "r2": (itertools.product([256, 512, 1024, 2048], [16, 32, 64], [5, 10], [1e-2, 2e-2], [1e-2],
+                             [0.99], [0.95])),
+    # the best of "r2" re-run over more seeds
+    "r2refine": [row + (1e-2, 0.99, 0.95) for row in [
+        (512, 64, 10, 1e-2), (256, 64, 10, 1e-2), (256, 64, 5, 1e-2), (256, 64, 10, 2e-2), (1024, 64, 5, 1e-2),
+        (512, 64, 5, 1e-2)]],
     "refhp": (itertools.product([256, 512, 1024, 2048, 4096], [16, 32, 64, 128], [80], [3e-4], [1e-3],
                                 [0.98], [0.97])),
 }
@@ -59,11 +66,12 @@ def main():
     ap.add_argument("--grid", choices=sorted(GRIDS), default="base")
     ap.add_argument("--seeds", type=int, nargs="*", default=[7, 8])
     ap.add_argument("--max-s", type=float, default=20.0)
+    ap.add_argument("--eager", action="store_true", help="value loop launched eagerly (bench.py's tuned TTT runs)")
     a = ap.parse_args()
     for n, t, vfi, lr, vlr, gamma, lam in GRIDS[a.grid]:
         for seed in a.seeds:
             cfg = VecTrainerConfig(num_envs=n, rollout_len=t, with_baseline=True, pi_lr=lr, vf_lr=vlr,
-                                   train_vf_iters=vfi, gamma=gamma, lam=lam, seed=seed)
+                                   train_vf_iters=vfi, gamma=gamma, lam=lam, seed=seed, use_graphs=not a.eager)
             s, ep, steps = ttt(cfg, a.max_s)
             print(json.dumps({"num_envs": n, "rollout_len": t, "vf_iters": vfi, "pi_lr": lr, "vf_lr": vlr,
                               "gamma": gamma, "lam": lam, "seed": seed, "ttt_s": s, "epochs": ep,
