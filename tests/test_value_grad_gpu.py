@@ -153,6 +153,31 @@ def test_deterministic(cuda, D, B):
         set_value_grad_mode(old)
 
 
+@pytest.mark.parametrize("D,B,shift", [(4, 20000, 1), (4, 20000, 2), (8, 9000, 3), (17, 9000, 1)])
+def test_unaligned_params_slice(cuda, D, B, shift):
+    """The prologue stages W2 with 16-byte loads when the params slice allows and with element
+    loads otherwise: a params view at a 4-byte (not 16-byte) offset gives bitwise the same slabs."""
+    H = 128
+    g = torch.Generator().manual_seed(11 * D + shift)
+    spec = MLPSpec(D, H, 1, False)
+    pp = (spec.init(g) + 0.05 * torch.randn(spec.P, generator=g)).to(cuda)
+    buf = torch.zeros(spec.P + 8, device=cuda)
+    buf[shift:shift + spec.P] = pp
+    pv = buf[shift:shift + spec.P]
+    assert pv.data_ptr() % 16 != 0
+    X = (torch.randn(B, D, generator=g) * 1.5).to(cuda)
+    ret = (torch.randn(B, generator=g) * 20 + 5).to(cuda)
+    old = set_value_grad_mode(1)
+    try:
+        ref, lref = mlp_grad(GradHead.VALUE_MSE, pp, X, 1, H, ret=ret)
+        ref, lref = ref.clone(), lref.clone()
+        s, ls = mlp_grad(GradHead.VALUE_MSE, pv, X, 1, H, ret=ret)
+        assert torch.equal(s, ref)
+        assert torch.equal(ls, lref)
+    finally:
+        set_value_grad_mode(old)
+
+
 def _pg64(head, pp, X, A, H, mask, act, adv, logp_old, stats, inv_B, clip, ent_coef):
     """float64 autograd gradient of the categorical PG / PPO loss (mlp_grad.hip semantics:
     normalised advantages, masked logits, entropy bonus, true log_softmax log-probs)."""
