@@ -468,17 +468,20 @@ class ActorLearner:
         out["EnvSteps"] = self.epoch * self.cfg.rollout_len * self.cfg.num_envs * self.n_actors
         return out
 
-    def sync_from_rank0(self):
-        """Make every learner hold rank 0's learner state and every rank its policy weights
-        (after an elastic re-form, parallel/elastic.py)."""
+    def sync_from_rank0(self, src: int = 0):
+        """Make every learner hold learner ``src``'s state and every rank its policy weights
+        (after an elastic re-form, parallel/elastic.py, or an auto-resume).  ``src`` must be a
+        learner rank (the learner group is ranks 0 .. L-1, so its group rank is ``src``)."""
+        if src >= self.topo.L:
+            raise ValueError(f"sync source {src} is not a learner rank (L = {self.topo.L})")
         if self.is_learner and self.lcomm is not None and self.lcomm.world > 1:
-            self.learner.broadcast_state_(self.lcomm, 0)
-        self.comm.broadcast_(self.front, 0)
+            self.learner.broadcast_state_(self.lcomm, src)
+        self.comm.broadcast_(self.front, src)
         if self.is_learner and self.actor is not None:
             self.actor.params.copy_(self.front)
         vec = torch.tensor([float(self.epoch), float(self.version)], dtype=torch.float64,
                            device="cuda" if self.comm.backend == "nccl" else "cpu")
-        self.comm.broadcast_(vec, 0)
+        self.comm.broadcast_(vec, src)
         self.epoch, self.version = int(vec[0].item()), int(vec[1].item())
         self._front_version = self.version
 

@@ -215,6 +215,11 @@ class HostVecTrainer:
         """T env steps into buffer set ``idx`` on the calling thread's current stream."""
         T = self.cfg.rollout_len
         b = self.bufs[idx]
+        if self.device.type == "cuda":
+            # write-after-read: the previous update (queued on the compute stream, or for the
+            # overlapped rollout the ``snap`` event this stream waited on) may still read this
+            # buffer set; the copy stream's first H2D into it must wait for that (ADVICE r2)
+            copy_stream.wait_stream(torch.cuda.current_stream(self.device))
         if self._final_obs is not None and self._final_obs.data_ptr() != b.h_obs[0].data_ptr():
             b.h_obs[0].copy_(self._final_obs)  # continue every env where the last rollout left it
         for t in range(T):
@@ -326,6 +331,28 @@ class HostVecTrainer:
     def finish(self):
         if self._pending is not None:
             self._join_ahead()
+
+    def state_dict(self) -> dict:
+        """Learner state + counters.  The C++ env threads' states are not exported: a resumed
+        host trainer starts fresh episodes (its env seeds advance with the epoch)."""
+        return {"learner": self.learner.state_dict(), "epoch": self.epoch, "env_steps": self.env_steps,
+                "global_step": self.global_step, "cfg": self.cfg.to_dict()}
+
+    def load_state_dict(self, sd: dict):
+        self.finish()
+        self.learner.load_state_dict(sd["learner"])
+        self.epoch = int(sd["epoch"])
+        self.env_steps = int(sd["env_steps"])
+        self.global_step = int(sd.get("global_step", self.epoch * self.cfg.rollout_len))
+        if self.overlap:
+            self.actor_params.copy_(self.learner.pi.params)
+
+    def sync_from_rank0(self, src: int = 0):
+        """Rank ``src``'s learner state everywhere; each rank keeps its own env streams."""
+        if self.comm.world > 1:
+            self.learner.broadcast_state_(self.comm, src)
+            if self.overlap:
+                self.actor_params.copy_(self.learner.pi.params)
 
     def metrics(self) -> dict:
         tot = {"n": 0.0, "sum": 0.0, "sumsq": 0.0, "max": -1e300, "min": 1e300, "sum_len": 0.0}

@@ -113,6 +113,47 @@ def ckpt_dir(out_dir: str, name: str, rank: int) -> str:
     return os.path.join(out_dir, f"{name}_ckpt_r{rank}")
 
 
+def _agree_resume(tr, comm, path: str) -> int:
+    """Auto-resume that every rank agrees on: the job restarts from the NEWEST checkpoint
+    epoch E any rank holds (all-reduce max).  Ranks whose own checkpoint is from epoch E load
+    it (learner state + their env streams); the lowest such rank that can serve as a source
+    (a learner for the actor-learner engine) then broadcasts the learner state, so ranks
+    with a stale or missing checkpoint (e.g. one evicted by an elastic shrink before the
+    restart) rejoin with fresh env streams but identical weights, and every rank runs the
+    same epochs -- no mismatched collectives."""
+    import torch
+
+    from ..utils.checkpoint import load_checkpoint
+
+    st = load_checkpoint(path) if os.path.exists(os.path.join(path, "state.json")) else None
+    mine = int(st.get("epoch", 0)) if st is not None else -1
+    if comm.world == 1:
+        if st is not None:
+            tr.load_state_dict(st["trainer"])
+        return max(mine, 0)
+    dev = torch.device("cuda", torch.cuda.current_device()) if comm.backend == "nccl" else torch.device("cpu")
+    e = torch.tensor([float(mine)], dtype=torch.float64, device=dev)
+    comm.all_reduce_max_(e)
+    E = int(e.item())
+    if E < 0:
+        return 0
+    can_src = getattr(tr, "is_learner", True)
+    cand = torch.tensor([float(comm.rank if (mine == E and can_src) else comm.world)], dtype=torch.float64,
+                        device=dev)
+    comm.all_reduce_min_(cand)
+    src = int(cand.item())
+    if src >= comm.world:
+        raise RuntimeError(f"auto-resume: no learner rank holds the newest checkpoint (epoch {E})")
+    if mine == E:
+        tr.load_state_dict(st["trainer"])
+    elif st is not None:
+        print(f"[resume] rank {comm.rank}: own checkpoint is from epoch {mine}, the job resumes at {E}; "
+              f"learner state from rank {src}", flush=True)
+    if hasattr(tr, "sync_from_rank0"):
+        tr.sync_from_rank0(src)
+    return E
+
+
 def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optional[Dict] = None,
                checkpoint_every: int = 0, resume: Optional[str] = None, log_every: int = 1,
                on_metrics: Optional[Callable[[Dict], None]] = None, auto_resume: bool = False,
@@ -157,15 +198,13 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
         dev = torch.device("cpu")
     tr = _make_trainer(preset, comm, dev, overrides)
     start = 0
-    if auto_resume and resume is None and os.path.exists(os.path.join(ckpt_dir(out_dir, name, comm.rank),
-                                                                      "state.json")):
-        resume = ckpt_dir(out_dir, name, comm.rank)
-    if resume:
+    if auto_resume and resume is None:
+        start = _agree_resume(tr, comm, ckpt_dir(out_dir, name, orig_rank))
+    elif resume:
         from ..utils.checkpoint import load_checkpoint
 
         st = load_checkpoint(resume)
         tr.load_state_dict(st["trainer"])
-        start = int(st.get("epoch", 0)) if auto_resume else 0
     logger = None
     if comm.rank == 0:
         kw = setup_logger_kwargs(f"relayrl-{name}", seed=int(overrides.get("seed", 0)), data_dir=out_dir)
@@ -237,8 +276,11 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
         if checkpoint_every and ep % checkpoint_every == 0 and hasattr(tr, "state_dict"):
             from ..utils.checkpoint import save_checkpoint
 
-            save_checkpoint(ckpt_dir(out_dir, name, comm.rank), {"trainer": tr.state_dict(), "epoch": ep})
-        maybe_kill_rank(comm.rank, ep, out_dir)
+            # keyed on the ORIGINAL (torchrun) rank: after an elastic shrink the survivors'
+            # new ranks would overwrite other ranks' directories
+            save_checkpoint(ckpt_dir(out_dir, name, orig_rank), {"trainer": tr.state_dict(), "epoch": ep,
+                                                                 "world": comm.world, "rank": comm.rank})
+        maybe_kill_rank(orig_rank, ep, out_dir)
         ep += 1
     if hasattr(tr, "finish"):
         tr.finish()

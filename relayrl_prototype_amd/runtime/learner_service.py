@@ -69,7 +69,8 @@ class LearnerService:
         receiving model pushes; an evicted agent that comes back simply re-registers."""
         now = time.time()
         with self._agents_lock:
-            gone = [a for a, r in self.agents.items() if now - r["last_seen"] > timeout_s]
+            # ``exempt`` = a peer without any liveness signal (reference agents, zmq_transport.py)
+            gone = [a for a, r in self.agents.items() if now - r["last_seen"] > timeout_s and not r.get("exempt")]
             for a in gone:
                 self.evicted[a] = self.agents.pop(a)
         if gone:

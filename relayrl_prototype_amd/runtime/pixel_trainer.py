@@ -250,6 +250,23 @@ class PixelA2CTrainer:
                 self.params.copy_(st["params"])
             self.opt.load_state_dict(st["opt"])
 
+    def sync_from_rank0(self, src: int = 0):
+        """Rank ``src``'s model and optimiser state everywhere (elastic re-form / auto-resume)."""
+        if self.comm.world <= 1:
+            return
+        if self.on_gpu:
+            m = self.model
+            for t in (m.params, m.m, m.v, m.step_t):
+                self.comm.broadcast_(t, src)
+            m.h.to_bf16(m.params, m.shadow)
+        else:
+            with torch.no_grad():
+                self.comm.broadcast_(self.params.data, src)
+            for st in self.opt.state.values():
+                for v in st.values():
+                    if torch.is_tensor(v):
+                        self.comm.broadcast_(v, src)
+
     def reset_episode_stats(self):
         self.ep_sum.zero_()
         if self.on_gpu:

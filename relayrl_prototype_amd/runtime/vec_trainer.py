@@ -200,11 +200,12 @@ class VecTrainer:
         n, s = self.episode_sums()
         return s / n if n > 0 else float("nan")
 
-    def sync_from_rank0(self):
-        """Rank 0's learner state everywhere (after an elastic re-form, parallel/elastic.py);
-        each rank keeps its own env streams."""
+    def sync_from_rank0(self, src: int = 0):
+        """Rank ``src``'s learner state everywhere (after an elastic re-form, parallel/elastic.py,
+        or an auto-resume where only some ranks hold the newest checkpoint); each rank keeps
+        its own env streams."""
         if self.comm.world > 1:
-            self.learner.broadcast_state_(self.comm, 0)
+            self.learner.broadcast_state_(self.comm, src)
 
     def state_dict(self) -> dict:
         return {"learner": self.learner.state_dict(), "epoch": self.epoch, "env_steps": self.env_steps,

@@ -26,6 +26,8 @@ from collections import OrderedDict
 from typing import Any, List, Optional, Tuple
 
 MAX_DEPTH = 64
+MAX_STACK = 1 << 20   # values on the interpreter stack (a frame holds ~10 per action)
+MAX_MEMO = 1 << 16
 
 
 class PickleFrameError(ValueError):
@@ -47,6 +49,7 @@ def loads(buf: bytes) -> Any:
     pos = 0
     stack: List[Any] = []
     memo = {}
+    marks = 0  # MARKs on the stack (a running count: O(1) per MARK / pop_mark)
 
     def take(k: int) -> memoryview:
         nonlocal pos
@@ -57,12 +60,21 @@ def loads(buf: bytes) -> Any:
         return out
 
     def pop_mark() -> List[Any]:
+        nonlocal marks
+        if marks == 0:
+            raise PickleFrameError("MARK not found")
         for i in range(len(stack) - 1, -1, -1):
             if stack[i] is _MARK:
                 items = stack[i + 1:]
                 del stack[i:]
+                marks -= 1
                 return items
         raise PickleFrameError("MARK not found")
+
+    def pop_value():
+        if not stack or stack[-1] is _MARK:
+            raise PickleFrameError("stack underflow")
+        return stack.pop()
 
     def top_container(kind):
         if not stack or not isinstance(stack[-1], kind):
@@ -70,6 +82,8 @@ def loads(buf: bytes) -> Any:
         return stack[-1]
 
     while True:
+        if len(stack) > MAX_STACK or len(memo) > MAX_MEMO:
+            raise PickleFrameError("frame too large")
         op = take(1)[0]
         if op == 0x80:  # PROTO
             take(1)
@@ -120,9 +134,10 @@ def loads(buf: bytes) -> Any:
             k = struct.unpack("<Q", take(8))[0]
             stack.append(bytes(take(k)))
         elif op == 0x28:  # MARK
-            if sum(1 for s in stack if s is _MARK) >= MAX_DEPTH:
+            if marks >= MAX_DEPTH:
                 raise PickleFrameError("nesting too deep")
             stack.append(_MARK)
+            marks += 1
         elif op == 0x5D:  # EMPTY_LIST
             stack.append([])
         elif op == 0x7D:  # EMPTY_DICT
@@ -132,14 +147,14 @@ def loads(buf: bytes) -> Any:
         elif op == 0x8F:  # EMPTY_SET
             stack.append(set())
         elif op == 0x61:  # APPEND
-            v = stack.pop()
+            v = pop_value()
             top_container(list).append(v)
         elif op == 0x65:  # APPENDS
             items = pop_mark()
             top_container(list).extend(items)
         elif op == 0x73:  # SETITEM
-            v = stack.pop()
-            k = stack.pop()
+            v = pop_value()
+            k = pop_value()
             top_container(dict)[_key(k)] = v
         elif op == 0x75:  # SETITEMS
             items = pop_mark()
@@ -173,7 +188,10 @@ def loads(buf: bytes) -> Any:
         elif op == 0x6A:  # LONG_BINGET
             stack.append(memo[struct.unpack("<I", take(4))[0]])
         elif op == 0x30:  # POP
-            stack.pop()
+            if not stack:
+                raise PickleFrameError("stack underflow")
+            if stack.pop() is _MARK:
+                marks -= 1
         elif op == 0x31:  # POP_MARK
             pop_mark()
         else:
@@ -321,8 +339,18 @@ class CumulativeDeduper:
     """Reference agents re-send every earlier episode with each upload (the trajectory is
     only cleared at max_length, trajectory.rs:160-204), each over a NEW connection, so the
     learner would train on the same actions again and again.  Uploads are matched by a
-    digest of their first action; an upload that extends the previous one from the same
-    agent keeps only its new actions."""
+    digest of their first action.  An upload keeps only its new actions when it strictly
+    extends a remembered upload AT AN EPISODE BOUNDARY: the remembered prefix must end in
+    a ``done`` action, which every cumulative re-send does (the agent sends right after
+    appending a done marker, trajectory.rs:172-203).
+
+    Residual ambiguity: the sender is not part of the key -- each reference upload comes
+    over a fresh PUSH connection with no identity, so two agents cannot be told apart.  An
+    upload of the same length as a remembered one is therefore never dropped: the
+    reference never re-sends an upload unchanged (every send follows a new done action),
+    while two identical independent episodes (deterministic policy, fixed start state) are
+    real data.  Only an independent episode that begins with another complete episode's
+    exact action sequence would still be trimmed."""
 
     def __init__(self, capacity: int = 4096):
         self.capacity = capacity
@@ -346,11 +374,8 @@ class CumulativeDeduper:
         keep = actions
         if prev is not None:
             n_prev, dig = prev
-            if len(actions) > n_prev and self._digest(actions[:n_prev]) == dig:
+            if len(actions) > n_prev and actions[n_prev - 1].get_done() and self._digest(actions[:n_prev]) == dig:
                 keep = actions[n_prev:]
-                self.stripped += n_prev
-            elif len(actions) == n_prev and self._digest(actions) == dig:
-                keep = []  # an exact re-send
                 self.stripped += n_prev
         self._seen[head] = (len(actions), self._digest(actions))
         self._seen.move_to_end(head)

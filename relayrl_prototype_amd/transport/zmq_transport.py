@@ -69,11 +69,23 @@ class ZmqTrainingEndpoint:
             service.on_evict(self._on_evict)
 
     def _on_evict(self, agent_ids):
+        """Our agents heartbeat, so silence means gone: drop their push routes.  Reference
+        agents have no liveness signal at all (agent_zmq.rs handshakes once at startup and
+        never again, and uploads over a fresh PUSH connection each time, so an upload cannot
+        be tied to a DEALER identity): they are registered ``exempt`` and never reach this
+        hook -- the PUSH to their bound PULL simply times out if one has really gone."""
         ids = {a.encode() if isinstance(a, str) else a for a in agent_ids}
         with self._lock:
             for peer in [p for p in self.agents if p in ids]:
                 del self.agents[peer]
-            self.ref_agents -= ids
+
+    def _touch_reference_agents(self):
+        """A reference upload arrived: refresh every reference agent's last_seen (the upload's
+        PUSH connection carries no identity, training_zmq.rs:971-1012)."""
+        with self._lock:
+            ref = list(self.ref_agents)
+        for peer in ref:
+            self.service.register_agent(peer.decode(errors="replace"))
 
     def _log(self, *a):
         if self.verbose:
@@ -103,7 +115,8 @@ class ZmqTrainingEndpoint:
                             self.agents[peer] = fmt
                         else:  # reference agent: updates go to its bound PULL, not the ROUTER
                             self.ref_agents.add(peer)
-                    self.service.register_agent(peer.decode(errors="replace"))
+                    self.service.register_agent(peer.decode(errors="replace"),
+                                                None if len(body) > 1 else {"exempt": True, "reference": True})
                     self.router.send([peer, b"", self._model_payload(fmt)], 5000)
                 elif cmd == b"MODEL_SET":
                     self.service.register_agent(peer.decode(errors="replace"))
@@ -146,6 +159,7 @@ class ZmqTrainingEndpoint:
         if serde_pickle.is_pickle_frame(f):
             acts = self.dedupe.new_actions(serde_pickle.actions_from_reference(serde_pickle.loads(f)))
             self.reference_frames += 1
+            self._touch_reference_agents()
             if not acts:
                 return None
             t = RelayRLTrajectory(max(len(acts), 1), None, "reference-agent")

@@ -88,3 +88,55 @@ def test_stalled_actor_group_restart_resumes(tmp_path):
     assert "[watchdog]" in r.stderr and "stalled" in r.stderr
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     assert json.loads(line)["EnvSteps"] == 4 * 8 * 4 * 3
+
+
+def _worker_agree_resume(rank, world, port, ckroot, q):
+    try:
+        import torch
+
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                          LOCAL_RANK=str(rank))
+        torch.set_num_threads(1)
+        from relayrl_prototype_amd.parallel.comm import init_distributed
+        from relayrl_prototype_amd.runtime.host_trainer import HostTrainerConfig, HostVecTrainer
+        from relayrl_prototype_amd.runtime.launcher import _agree_resume, ckpt_dir
+        from relayrl_prototype_amd.utils.checkpoint import save_checkpoint
+
+        comm = init_distributed(backend="gloo")
+        cfg = HostTrainerConfig(num_envs=8, rollout_len=8, hidden=32, train_vf_iters=1, num_threads=1, seed=rank)
+        # rank 0 trained to epoch 3, rank 1's checkpoint is a stale epoch-1 state (it was evicted)
+        tr = HostVecTrainer(cfg, comm, device="cpu")
+        with torch.no_grad():
+            tr.learner.pi.params.add_(float(rank + 1))
+        save_checkpoint(ckpt_dir(ckroot, "p", rank), {"trainer": tr.state_dict(), "epoch": 3 if rank == 0 else 1})
+        comm.barrier()
+        fresh = HostVecTrainer(cfg, comm, device="cpu")
+        start = _agree_resume(fresh, comm, ckpt_dir(ckroot, "p", rank))
+        g = [torch.zeros_like(fresh.learner.pi.params) for _ in range(world)]
+        torch.distributed.all_gather(g, fresh.learner.pi.params)
+        q.put((rank, start, bool(torch.equal(g[0], g[1]))))
+        torch.distributed.destroy_process_group()
+    except Exception as e:
+        q.put((rank, repr(e), False))
+
+
+def test_auto_resume_ranks_agree_on_one_epoch(tmp_path):
+    """ranks holding checkpoints of different epochs all resume at the newest one,
+    with the learner state of the rank that holds it (no mismatched collectives)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker_agree_resume, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert res == [(0, 3, True), (1, 3, True)], res

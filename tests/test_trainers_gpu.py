@@ -208,3 +208,28 @@ def test_host_trainer_overlap_learns(cuda):
             break
     tr.finish()
     assert best > 150, best
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+def test_host_trainer_no_sync_equals_synced(cuda, overlap):
+    """without a host sync between epochs (log_every > 1) the next rollout's first
+    H2D copy must still wait for the previous update's reads of that buffer set.  The run
+    with a synchronize() after every epoch is the race-free reference; both must agree
+    bit for bit (every kernel here is deterministic)."""
+    from relayrl_prototype_amd.runtime.host_trainer import HostTrainerConfig, HostVecTrainer
+
+    def run(sync_every_epoch):
+        cfg = HostTrainerConfig(env="CartPole-v1", num_envs=2048, rollout_len=16, train_vf_iters=20, num_threads=4,
+                                overlap=overlap, seed=5)
+        tr = HostVecTrainer(cfg, device=cuda)
+        for _ in range(6):
+            tr.train_epoch()
+            if sync_every_epoch:
+                torch.cuda.synchronize()
+        tr.finish()
+        torch.cuda.synchronize()
+        return tr.learner.pi.params.clone(), tr.learner.vf.params.clone()
+
+    p_sync, v_sync = run(True)
+    p_fast, v_fast = run(False)
+    assert torch.equal(p_sync, p_fast) and torch.equal(v_sync, v_fast)

@@ -109,6 +109,30 @@ def test_cumulative_uploads_are_deduplicated():
     assert dd.stripped == 3
 
 
+def test_deduper_keeps_identical_independent_episodes():
+    """a deterministic policy from a fixed start state uploads the same episode
+    twice -- both are data, not a re-send (the reference never re-sends an upload unchanged)."""
+    mk = lambda i, d=False: RelayRLAction(np.full(4, i, np.float32), np.array([i % 2]), None, 1.0, None, d)  # noqa
+    ep = [mk(0), mk(1), mk(2, True)]
+    dd = sp.CumulativeDeduper()
+    assert len(dd.new_actions(ep)) == 3
+    assert len(dd.new_actions(list(ep))) == 3
+    # a longer upload that merely starts like a remembered one, without an episode boundary there
+    part = [mk(0), mk(1)]
+    dd2 = sp.CumulativeDeduper()
+    dd2.new_actions(part)
+    assert len(dd2.new_actions(part + [mk(2, True)])) == 3
+
+
+def test_pickle_mark_heavy_frame_is_linear():
+    """MARK / POP_MARK pairs over a deep stack cost O(1) each (running counter)."""
+    body = b"K\x01" * 50000 + b"(1" * 50000
+    t0 = time.time()
+    with pytest.raises(sp.PickleFrameError):
+        sp.loads(b"\x80\x03" + body + b".")  # 50000 values left on the stack at STOP
+    assert time.time() - t0 < 2.0
+
+
 # ---------------------------------------------------------------------- ZMQ endpoint
 class _Store:
     def __init__(self):
@@ -135,7 +159,7 @@ class _Service:
         self.got.append(traj)
         return True
 
-    def register_agent(self, a):
+    def register_agent(self, a, info=None):
         self.agents.append(a)
 
 
@@ -194,6 +218,50 @@ def test_endpoint_trains_on_reference_frames_and_pushes_models():
         assert msg[1][0] == svc.store.blob.torchscript()
     finally:
         for s in (dealer, push, agent_pull):
+            s.close()
+        ep.close()
+
+
+def test_reference_agents_survive_the_eviction_sweep():
+    """a reference agent never heartbeats; after the sweeper's timeout it
+    must still receive model pushes (it is registered exempt and refreshed by its uploads)."""
+    from relayrl_prototype_amd.runtime.learner_service import LearnerService
+    from relayrl_prototype_amd.transport.zmq_transport import ZmqTrainingEndpoint
+
+    class _Algo:
+        def get_weights(self):
+            b = _blob()
+            return {"obs_dim": 4, "act_dim": 2, "hidden": 128, "discrete": True, "version": b.version,
+                    "pi": __import__("torch").from_numpy(b.pi), "vf": None}
+
+        def model_bytes(self):
+            return _blob().torchscript()
+
+        def receive_trajectory(self, traj):
+            return False
+
+    svc = LearnerService(_Algo())
+    al, tr, ts = _port(), _port(), _port()
+    ep = ZmqTrainingEndpoint(svc, f"tcp://127.0.0.1:{al}", f"tcp://127.0.0.1:{tr}",
+                             model_push_addr=f"tcp://127.0.0.1:{ts}")
+    agent_pull = _native.ZmtpSocket(_native.SockType.PULL)
+    agent_pull.bind(f"tcp://127.0.0.1:{ts}")
+    dealer = _native.ZmtpSocket(_native.SockType.DEALER, b"AGENT_ID-ref2")
+    try:
+        dealer.connect(f"tcp://127.0.0.1:{al}")
+        assert dealer.send([b"", b"GET_MODEL"], 5000)
+        assert dealer.recv(5000) is not None
+        assert dealer.send([b"", b"MODEL_SET"], 5000)
+        assert dealer.recv(5000)[1][-1] == b"ID_LOGGED"
+        # the agent stays silent far past the timeout: the sweep evicts nothing of it
+        svc.agents["AGENT_ID-ref2"]["last_seen"] -= 1000.0
+        assert svc.evict_stale(1.0) == []
+        assert b"AGENT_ID-ref2" in ep.ref_agents
+        ep._on_model(svc.store.latest())
+        msg = agent_pull.recv(10000)
+        assert msg is not None and msg[1][0][:2] == b"PK"
+    finally:
+        for s in (dealer, agent_pull):
             s.close()
         ep.close()
 
