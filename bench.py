@@ -72,6 +72,18 @@ def parse(argv=None):
     ap.add_argument("--ttt-max-s", type=float, default=30.0, help="give up on a seed after this many seconds")
     ap.add_argument("--ref-cpu-seconds", type=float, default=150.0,
                     help="budget of the concurrent reference-equivalent CPU run (0 = skip)")
+    ap.add_argument("--phase-steps", type=int, default=3,
+                    help="extra epochs AFTER the timed steps with HIP-event phase timing on (per-rank "
+                         "Rollout / ValueFwd / Scan / Optimize / AllReduce ms); 0 = skip")
+    ap.add_argument("--actor-learner", choices=("auto", "on", "off"), default="auto",
+                    help="secondary phase: the actor -> learner-group P2P data plane (BASELINE config #3 "
+                         "topology, K = 2 actor blocks per learner shard); auto = only with world > 1")
+    ap.add_argument("--al-steps", type=int, default=10)
+    ap.add_argument("--al-warmup", type=int, default=5)
+    ap.add_argument("--al-env", default="LunarLanderSynth-v0")
+    ap.add_argument("--al-num-envs", type=int, default=2048)
+    ap.add_argument("--al-rollout-len", type=int, default=128)
+    ap.add_argument("--al-vf-iters", type=int, default=80)
     return ap.parse_args(argv)
 
 
@@ -173,6 +185,104 @@ def collect_reference_cpu(proc, budget_s: float):
     return None
 
 
+# ---------------------------------------------------------------------- comm-phase observability
+def phase_probe(tr, comm, steps: int) -> dict:
+    """``steps`` more epochs with the trainer's HIP-event PhaseTimer on (after the timed
+    region, so the headline number carries no event overhead).  Returns per-rank lists of
+    per-epoch device ms per phase (AllReduce = every RCCL gradient / statistics all-reduce)."""
+    tm = tr.timer
+    tm.reset()
+    tm.enabled = True
+    if comm.world > 1:
+        comm.timer = tm
+    for _ in range(steps):
+        tr.train_epoch()
+    mine = tm.per_step(steps)
+    tm.enabled = False
+    comm.timer = None
+    tm.reset()
+    rows = comm.all_gather_object(mine)
+    keys = sorted({k for r in rows for k in r})
+    return {k: [r.get(k) for r in rows] for k in keys}
+
+
+def actor_learner_probe(args, comm, on_gpu: bool) -> dict:
+    """Secondary phase at world > 1: the actor -> learner data plane of BASELINE config #3.
+
+    Every rank acts; ranks 0 .. W/2-1 also learn (learner_ranks = W/2, so K = 2 actor
+    blocks per learner shard): each learner receives one remote rollout over P2P straight
+    into its contiguous shard batch (C1, reference trajectory.rs:69-90 ->
+    training_zmq.rs:948-1058), the shards all-reduce gradients inside the learner group,
+    and each learner P2P-sends the new weights back to its remote actor (C2,
+    training_zmq.rs:876-934 -> agent_zmq.rs:625-698) with a one-version lag (max_lag 1).
+    Every received rollout header is verified (version within the lag, weight checksum of
+    that version).  Errors and timeouts land in the record instead of failing the headline."""
+    import torch
+
+    from relayrl_prototype_amd.runtime.actor_learner import ActorLearner, ActorLearnerConfig
+
+    W = comm.world
+    L = max(1, W // 2)
+    rec = {"env": args.al_env, "K": (W // L), "L": L, "world": W, "max_lag": 1, "steps": args.al_steps,
+           "warmup": args.al_warmup}
+    try:
+        if on_gpu:
+            n, t, vi, thr = args.al_num_envs, args.al_rollout_len, args.al_vf_iters, 8
+        else:  # gloo plumbing check: tiny shapes, oracle ops
+            n, t, vi, thr = 16, 8, 2, 1
+        cfg = ActorLearnerConfig(env=args.al_env, num_envs=n, rollout_len=t, with_baseline=True, gamma=0.98,
+                                 lam=0.97, pi_lr=3e-4, vf_lr=1e-3, train_vf_iters=vi, learner_ranks=L,
+                                 learner_acts=True, max_lag=1, verify_versions=True, stall_timeout_s=0.0,
+                                 num_threads=thr, seed=1)
+        dev = torch.device("cuda", torch.cuda.current_device()) if on_gpu else torch.device("cpu")
+        al = ActorLearner(cfg, comm, dev)
+        rec.update(num_envs=n, rollout_len=t, train_vf_iters=vi, role="learner" if al.is_learner else "actor")
+        sync = torch.cuda.synchronize if on_gpu else (lambda: None)
+        for _ in range(args.al_warmup):
+            al.step()
+        comm.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.al_steps):
+            al.step()
+        comm.barrier()
+        sync()
+        dt_local = time.perf_counter() - t0
+        dt = torch.tensor([dt_local], dtype=torch.float64, device=dev)
+        comm.all_reduce_max_(dt)
+        dt = float(dt.item())
+        # phase timing in extra steps (events + the per-step syncs of verify_versions)
+        al.timer.enabled = True
+        ph_steps = max(2, args.al_steps // 2)
+        for _ in range(ph_steps):
+            al.step()
+        phases = al.timer.per_step(ph_steps)
+        al.timer.enabled = False
+        al.finish()
+        vers = al.last_hdr[:, 7].tolist() if al.is_learner and al.last_hdr is not None else []
+        ok = all(al.version - 1 - cfg.max_lag <= v <= al.version - 1 for v in vers)
+        per_rank = comm.all_gather_object({"rank": comm.rank, "role": rec["role"], "step_ms":
+                                           round(dt_local / args.al_steps * 1e3, 3), "versions": vers,
+                                           "versions_ok": ok, **phases})
+        rec.update(
+            env_steps_per_s=round(args.al_steps * t * n * len(al.topo.actors) / dt, 1),
+            ms_per_step=round(dt / args.al_steps * 1e3, 3),
+            versions_ok=all(r["versions_ok"] for r in per_rank),
+            gather_ms=[r.get("GatherMs") for r in per_rank],
+            allreduce_ms=[r.get("AllReduceMs") for r in per_rank],
+            allreduce_calls=[r.get("AllReduceCalls") for r in per_rank],
+            weight_send_ms=[r.get("WeightSendMs") for r in per_rank],
+            weight_recv_ms=[r.get("WeightRecvMs") for r in per_rank],
+            learn_ms=[r.get("LearnMs") for r in per_rank],
+            rollout_ms=[r.get("RolloutMs") for r in per_rank],
+            per_rank=per_rank,
+            backend=comm.backend)
+        al.watchdog.close()
+    except Exception as e:  # noqa: BLE001 -- recorded, the headline line still prints
+        rec["error"] = f"{type(e).__name__}: {e}"[:500]
+    return rec
+
+
 # ---------------------------------------------------------------------- main
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -189,6 +299,10 @@ def main(argv=None):
     on_gpu = args.device == "gpu"
     if int(world_env or 1) > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        # a hung peer becomes an exception inside 90 s (recorded in the JSON by the secondary
+        # actor-learner phase) instead of a 10-minute wait or a torn-down process
+        os.environ.setdefault("RRL_COLLECTIVE_TIMEOUT_S", "90")
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "2")
     comm = init_distributed()
     world = comm.world
     rank = comm.rank
@@ -229,6 +343,11 @@ def main(argv=None):
     steps_per_epoch = cfg.num_envs * cfg.rollout_len * world
     value = steps_per_epoch * args.steps / dt
     per_rank = comm.all_gather_object(round(cfg.num_envs * cfg.rollout_len * args.steps / dt_local, 1))
+    per_rank_ms = comm.all_gather_object(round(dt_local / args.steps * 1e3, 3))
+    phases = phase_probe(tr, comm, args.phase_steps) if args.phase_steps > 0 else None
+    al_rec = None
+    if args.actor_learner == "on" or (args.actor_learner == "auto" and world > 1):
+        al_rec = actor_learner_probe(args, comm, on_gpu)
     ttt = ttt_ref = None
     do_ttt = on_gpu and (args.ttt or world == 1) and not args.no_ttt
     if do_ttt:
@@ -274,6 +393,7 @@ def main(argv=None):
             "backend": comm.backend,
             "rccl_world": world if comm.backend == "nccl" else 0,
             "per_rank_env_steps_per_s": per_rank,
+            "per_rank_ms_per_step": per_rank_ms,
             "final_avg_ep_ret": None if m["AverageEpRet"] != m["AverageEpRet"] else round(m["AverageEpRet"], 2),
         }
         if do_ttt:
@@ -297,6 +417,12 @@ def main(argv=None):
                                           {"num_envs": args.ttt_ref_envs, "rollout_len": args.ttt_ref_rollout_len},
                                           args.ttt_ref_seeds),
             }
+        if phases is not None:
+            rec["phase_ms_per_step"] = dict(phases, steps=args.phase_steps,
+                                            note="per rank, device ms per epoch from HIP events, measured in "
+                                                 "extra epochs after the timed region")
+        if al_rec is not None:
+            rec["actor_learner"] = al_rec
         if ref_cpu is not None:
             rec["reference_equivalent_cpu"] = {
                 "env_steps_per_s": round(ref_cpu.get("value", 0.0), 1),
@@ -310,7 +436,10 @@ def main(argv=None):
     if comm.world > 1:
         import torch.distributed as dist
 
-        dist.destroy_process_group()
+        try:
+            dist.destroy_process_group()
+        except Exception:  # noqa: BLE001 -- after a recorded comm failure
+            pass
     return 0
 
 

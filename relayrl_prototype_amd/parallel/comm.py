@@ -86,6 +86,10 @@ class Comm:
         self.world = dist.get_world_size(group) if self.enabled else 1
         self.rank = dist.get_rank(group) if self.enabled else 0
         self.backend = dist.get_backend(group) if self.enabled else "none"
+        # optional utils.tracing.PhaseTimer: every gradient / statistics all-reduce is timed as
+        # the "AllReduce" phase (HIP events on the current stream bracket the RCCL call, which
+        # the stream waits on); skipped while a hipGraph is being captured
+        self.timer = None
 
     @property
     def is_master(self) -> bool:
@@ -93,7 +97,12 @@ class Comm:
 
     def all_reduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            tm = self.timer
+            if tm is not None and tm.enabled and not (t.is_cuda and torch.cuda.is_current_stream_capturing()):
+                with tm.phase("AllReduce"):
+                    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t
 
     def all_reduce_max_(self, t: torch.Tensor) -> torch.Tensor:

@@ -41,6 +41,7 @@ import torch.distributed as dist
 
 from ..algorithms.learner import PGLearner
 from ..parallel.comm import Comm, collective_timeout
+from ..utils.tracing import PhaseTimer
 from .rollout_learn import RolloutLearner
 
 # header (float64): seq, n_episodes, sum_ret, sumsq_ret, max_ret, min_ret, sum_len, version, checksum, wsum
@@ -74,6 +75,7 @@ class ActorLearnerConfig:
     verify_versions: bool = False  # check header version/checksum on the learners (syncs)
     stall_timeout_s: float = 120.0  # per-step watchdog floor (0 = off); budget = max(floor, factor x avg step)
     stall_factor: float = 20.0
+    phase_timing: bool = False     # HIP-event phases: Rollout, Gather, Learn, AllReduce, WeightSend, ...
 
     def to_dict(self):
         return asdict(self)
@@ -207,6 +209,10 @@ class ActorLearner:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"
         self.device = torch.device(device)
         self.rank = self.comm.rank
+        # comm-phase observability: Rollout / Gather / Learn / WeightSend on the
+        # learners, Rollout / SendRollout / WeightRecv on actor-only ranks, and every gradient
+        # all-reduce inside the learner group as AllReduce (Comm.timer)
+        self.timer = PhaseTimer(self.device, enabled=cfg.phase_timing)
         self.topo = topo = Topology(W, cfg.learner_ranks, cfg.learner_acts)
         self.is_learner = self.rank < topo.L
         self.acts = self.rank in topo.actors
@@ -216,6 +222,8 @@ class ActorLearner:
         else:
             grp = dist.new_group(list(range(topo.L)), timeout=collective_timeout()) if W > 1 else None
             self.lcomm = Comm(grp) if self.is_learner else None
+        if self.lcomm is not None:
+            self.lcomm.timer = self.timer
         need_tobs = cfg.with_baseline or cfg.algo != "reinforce"
         self.actor = _Actor(cfg, self.comm, self.device, need_tobs) if self.acts else None
         if self.actor is not None:
@@ -251,7 +259,7 @@ class ActorLearner:
             self.b_done = torch.zeros(K, T, N, device=dev)
             self.b_tobs = torch.zeros(K, T, N, D, device=dev) if need_tobs else None
             self.b_hdr = torch.zeros(K, HDR, dtype=torch.float64, device=dev)
-            self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.lcomm, blocks=K)
+            self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.lcomm, self.timer, blocks=K)
             self.wsend = torch.zeros_like(self.learner.pi.params)  # snapshot the P2P sends read
             self.front = self.learner.pi.params
         else:
@@ -284,14 +292,23 @@ class ActorLearner:
     # ------------------------------------------------------------------ one step
     def step(self):
         self.watchdog.begin(self.epoch)
-        parts = self.actor.rollout(self.version_in_use) if self.actor is not None else None
+        tm = self.timer
+        parts = None
+        if self.actor is not None:
+            with tm.phase("Rollout"):
+                parts = self.actor.rollout(self.version_in_use)
         if self.is_learner:
-            self._gather(parts)
-            self._learn()
-            self._send_weights()
+            with tm.phase("Gather"):
+                self._gather(parts)
+            with tm.phase("Learn"):
+                self._learn()
+            with tm.phase("WeightSend"):
+                self._send_weights()
         else:
-            self._send_rollout(parts)
-            self._recv_weights()
+            with tm.phase("SendRollout"):
+                self._send_rollout(parts)
+            with tm.phase("WeightRecv"):
+                self._recv_weights()
         self.version += 1
         self.epoch += 1
         self.watchdog.end()
@@ -466,6 +483,9 @@ class ActorLearner:
             out["ActorVersions"] = [int(x) for x in h[:, 7].tolist()]
             out.update(self.learner.summarize())
         out["EnvSteps"] = self.epoch * self.cfg.rollout_len * self.cfg.num_envs * self.n_actors
+        if self.timer.enabled:
+            out.update(self.timer.columns())
+            self.timer.reset()
         return out
 
     def sync_from_rank0(self, src: int = 0):

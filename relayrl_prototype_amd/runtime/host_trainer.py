@@ -118,6 +118,8 @@ class HostVecTrainer:
                                  cfg.target_kl, cfg.ent_coef, self.device, cfg.seed, self.comm, cfg.use_graphs,
                                  cfg.log_std_init, num_minibatches=cfg.num_minibatches)
         self.timer = PhaseTimer(self.device, enabled=cfg.phase_timing)
+        if self.comm.world > 1 and cfg.phase_timing:
+            self.comm.timer = self.timer
         self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.comm, self.timer)
         self.overlap = bool(cfg.overlap and cuda)
         with_tobs = self.learner.vf is not None

@@ -117,6 +117,8 @@ class VecTrainer:
                                  self.comm, cfg.use_graphs, num_minibatches=cfg.num_minibatches)
         self.pi, self.vf = self.learner.pi, self.learner.vf
         self.timer = PhaseTimer(dev, enabled=cfg.phase_timing)
+        if self.comm.world > 1 and cfg.phase_timing:
+            self.comm.timer = self.timer  # AllReduce phase (gradient + statistics all-reduces)
         self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.comm, self.timer)
         self.env_seed = (cfg.seed * 0x9E3779B97F4A7C15 + rank * 0x632BE59BD9B4E019) & 0x7FFFFFFFFFFFFFFF
         # time-major SoA rollout buffers (HBM resident)

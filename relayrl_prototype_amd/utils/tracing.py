@@ -133,6 +133,17 @@ class PhaseTimer:
             out[f"{prefix}{k}Ms"] = v
         return out
 
+    def per_step(self, steps: int) -> Dict[str, float]:
+        """Device ms per step of every phase (wall ms where no device time exists: CPU / gloo),
+        and the number of calls per step -- e.g. 81 AllReduce calls per learner epoch."""
+        dev = self.resolve()
+        out = {}
+        for k in self.wall:
+            v = dev.get(k, 1e3 * self.wall[k])
+            out[f"{k}Ms"] = round(v / max(steps, 1), 4)
+            out[f"{k}Calls"] = round(self.count[k] / max(steps, 1), 2)
+        return out
+
     def reset(self):
         self.resolve()
         self.wall.clear()

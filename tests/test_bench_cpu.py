@@ -32,6 +32,17 @@ def test_bench_spawns_ranks_without_torchrun():
     assert rec["value"] > 0 and rec["ms_per_step"] > 0
     for k in ("metric", "unit", "higher_is_better", "scaling", "vs_baseline", "dtype", "data"):
         assert k in rec
+    # comm-phase observability: per-rank phase lists, AllReduce included
+    ph = rec["phase_ms_per_step"]
+    assert len(ph["AllReduceMs"]) == 2 and all(x > 0 for x in ph["AllReduceMs"])
+    assert ph["AllReduceCalls"] == [4.0, 4.0]  # stats + policy + 2 value steps
+    # secondary phase: actor -> learner-group P2P fan-in / weight fan-out, lag 1, headers verified
+    al = rec["actor_learner"]
+    assert "error" not in al, al
+    assert al["K"] == 2 and al["L"] == 1 and al["versions_ok"] is True
+    assert al["env_steps_per_s"] > 0 and al["gather_ms"][0] > 0 and al["weight_recv_ms"][1] is not None
+    vers = al["per_rank"][0]["versions"]
+    assert len(vers) == 2 and vers[0] - vers[1] == 1  # own rollout on v_k, the remote actor's on v_{k-1}
 
 
 def test_bench_rejects_world_size_mismatch():
