@@ -69,8 +69,12 @@ def main():
                               "avg_ep_ret": m1.get("AverageEpRet"),
                               **({"rollout_s_per_epoch": (m1["RolloutS"] - m0["RolloutS"]) / a.steps,
                                   "learn_s_per_epoch": (m1["LearnS"] - m0["LearnS"]) / a.steps,
-                                  "overlap": bool(getattr(tr, "overlap", False))} if "RolloutS" in m1 else {})}),
+                                  "overlap": bool(getattr(tr, "overlap", False))} if "RolloutS" in m1 else {}),
+                              # C++ host rollout loop, per env step (driver thread wall time)
+                              **{k: round(v, 2) for k, v in m1.items() if k.startswith("Host") and k.endswith("Us")}}),
                   flush=True)
+        if hasattr(tr, "close"):
+            tr.close()
         del tr
         if dev.type == "cuda":
             torch.cuda.empty_cache()

@@ -8,14 +8,19 @@
 #include <ATen/hip/HIPContext.h>
 #include <torch/extension.h>
 
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
 #include <cstdint>
 #include <optional>
+#include <vector>
 
 extern "C" {
 int rrl_mlp_forward(int mode, const float* params, const float* X, int B, int D, int A, int H,
                     const float* mask, const int* act_in, const float* actc_in, int* act_out,
                     float* actc_out, float* out0, float* out1, float* logits_out, uint64_t seed,
-                    uint64_t step, uint32_t row_offset, const float* gate, int num_cu, void* stream);
+                    uint64_t step, uint32_t row_offset, const float* gate, float* x_copy, int* act_host,
+                    float* actc_host, int num_cu, void* stream);
 int rrl_mlp_grad_slabs(int B, int num_cu);
 int rrl_set_value_grad_mode(int mode);
 int rrl_set_value_grad_tune(int tune);
@@ -53,10 +58,42 @@ namespace {
 using at::Tensor;
 using OptT = std::optional<Tensor>;
 
-int num_cus() {
+int g_cu_limit = 0;  // > 0: size every grid for this many CUs (set_cu_limit)
+
+int device_cus() {
   static int n = -1;
   if (n < 0) n = at::cuda::getCurrentDeviceProperties()->multiProcessorCount;
   return n;
+}
+
+// CUs the grids of this process are sized for: all of them, or the learner's share when the
+// host-env trainer partitions the chip between its actor and learner streams.
+int num_cus() { return g_cu_limit > 0 ? std::min(g_cu_limit, device_cus()) : device_cus(); }
+
+int64_t set_cu_limit(int64_t n) {
+  const int64_t prev = g_cu_limit;
+  g_cu_limit = (int)std::max<int64_t>(n, 0);
+  return prev;
+}
+
+// A stream whose kernels run only on the listed CUs (hipExtStreamCreateWithCUMask): the
+// actor / learner partition of the overlapped host-env trainer, so the rollout's sampling
+// launches never queue behind the learner's persistent one-workgroup-per-CU kernels.
+int64_t cu_masked_stream(const std::vector<int64_t>& cus) {
+  const int n = device_cus();
+  std::vector<uint32_t> mask((n + 31) / 32, 0u);
+  for (int64_t c : cus) {
+    TORCH_CHECK(c >= 0 && c < n, "CU index ", c, " out of range [0, ", n, ")");
+    mask[c / 32] |= 1u << (c % 32);
+  }
+  hipStream_t st = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data());
+  TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
+  return (int64_t)(uintptr_t)st;
+}
+
+void destroy_stream(int64_t st) {
+  if (st) (void)hipStreamDestroy((hipStream_t)(uintptr_t)st);
 }
 
 void* cur_stream() { return (void*)at::hip::getCurrentHIPStream().stream(); }
@@ -124,7 +161,8 @@ void mlp_forward(int64_t mode, const Tensor& params, const Tensor& X, int64_t A,
   TORCH_CHECK(gt == nullptr || mode == 0, "gate applies to the VALUE mode only");
   const int rc = rrl_mlp_forward((int)mode, params.data_ptr<float>(), X.data_ptr<float>(), (int)B, (int)D, (int)A,
                                  (int)H, m, ai, ci, ao, co, out0.data_ptr<float>(), o1, lo, (uint64_t)seed,
-                                 (uint64_t)step, (uint32_t)row_offset, gt, num_cus(), cur_stream());
+                                 (uint64_t)step, (uint32_t)row_offset, gt, nullptr, nullptr, nullptr, num_cus(),
+                                 cur_stream());
   check_rc(rc, "mlp_forward");
 }
 
@@ -358,11 +396,16 @@ void rollout_cont(int64_t env, const Tensor& params, const Tensor& env_consts, i
 
 }  // namespace
 
-void register_cnn_ops(pybind11::module_& m);  // cnn_ops.cpp
+void register_cnn_ops(pybind11::module_& m);      // cnn_ops.cpp
+void register_rollout_ops(pybind11::module_& m);  // rollout_ops.cpp (host-env rollout driver)
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "relayrl_prototype_amd gfx950 HIP kernels";
   m.def("num_cus", &num_cus);
+  m.def("device_cus", &device_cus);
+  m.def("set_cu_limit", &set_cu_limit, "size grids for n CUs (0 = all); returns the previous limit");
+  m.def("cu_masked_stream", &cu_masked_stream);
+  m.def("destroy_stream", &destroy_stream);
   m.def("mlp_forward", &mlp_forward);
   m.def("mlp_grad_slabs", &mlp_grad_slabs);
   m.def("mlp_grad", &mlp_grad);
@@ -383,4 +426,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rollout", &rollout);
   m.def("rollout_cont", &rollout_cont);
   register_cnn_ops(m);
+  register_rollout_ops(m);
 }

@@ -40,6 +40,13 @@ struct FwdArgs {
   uint32_t row_offset;   // stream id of row 0 (global env index)
   const float* gate;     // MODE_VALUE: [B] done codes; only 16-row tiles holding a code 2
                          // (time-limit truncation) are evaluated, or null = every row
+  // host-env rollout (runtime/host_rollout.cpp): X may be PINNED HOST memory read over PCIe
+  // (zero-copy); x_copy gets the rows in HBM for the learner and act_host / actc_host the
+  // sampled actions in pinned host memory for the env threads -- one launch per half-step,
+  // no H2D / D2H copies.  All null on the ordinary path.
+  float* x_copy;         // [B][D] or null
+  int* act_host;         // [B] or null (CAT_SAMPLE)
+  float* actc_host;      // [B][A] or null (GAUSS_SAMPLE)
 };
 
 template <int DT, int HT, int MODE>
@@ -71,6 +78,16 @@ __global__ __launch_bounds__(256, 2) void mlp_forward_kernel(FwdArgs p) {
 
     floatx4 x[DT], h1[HT], h2[HT];
     load_x_tile<DT>(p.X, p.D, p.D, row0, nrows, x);
+    if (p.x_copy != nullptr && valid) {  // every (row, feature) is held by exactly one lane
+      float* xr = p.x_copy + (size_t)row * p.D;
+#pragma unroll
+      for (int t = 0; t < DT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 16 * t + 4 * r + g;
+          if (f < p.D) xr[f] = x[t][r];
+        }
+    }
     dense_fwd<DT, HT, true>(lds + L::W1, L::S1, lds + L::B1, x, h1, input_kr_last(p.D, DT));
     dense_fwd<HT, HT, true>(lds + L::W2, L::S2, lds + L::B2, h1, h2);
 
@@ -95,6 +112,7 @@ __global__ __launch_bounds__(256, 2) void mlp_forward_kernel(FwdArgs p) {
         const int a = cat_sample(A, logits, cs.lse, u01(rnd.x));
         if (valid && g == 0) {
           p.act_out[row] = a;
+          if (p.act_host != nullptr) p.act_host[row] = a;
           p.out0[row] = pick_logit(A, logits, a) - cs.lse;
           if (p.out1) p.out1[row] = cs.entropy;
         }
@@ -124,7 +142,10 @@ __global__ __launch_bounds__(256, 2) void mlp_forward_kernel(FwdArgs p) {
             const float u2 = u01((a & 1) ? rnd.w : rnd.y);
             const float z = sqrtf(-2.f * __logf(u1)) * __cosf(6.2831853071795864f * u2);
             xa = mu + sd * z;
-            if (valid && g == 0) p.actc_out[(size_t)row * A + a] = xa;
+            if (valid && g == 0) {
+              p.actc_out[(size_t)row * A + a] = xa;
+              if (p.actc_host != nullptr) p.actc_host[(size_t)row * A + a] = xa;
+            }
           } else {
             xa = valid ? p.actc_in[(size_t)row * A + a] : mu;
           }
@@ -177,11 +198,13 @@ extern "C" int rrl_mlp_forward(int mode, const float* params, const float* X, in
                                int H, const float* mask, const int* act_in, const float* actc_in,
                                int* act_out, float* actc_out, float* out0, float* out1,
                                float* logits_out, uint64_t seed, uint64_t step, uint32_t row_offset,
-                               const float* gate, int num_cu, void* stream) {
+                               const float* gate, float* x_copy, int* act_host, float* actc_host, int num_cu,
+                               void* stream) {
   if (B <= 0) return 0;
   if (A < 1 || A > kMaxAct || D < 1 || D > 32) return -2;
   FwdArgs a{params, X, B, D, A, H, mask, act_in, actc_in, act_out, actc_out, out0, out1, logits_out,
-            (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step, (uint32_t)(step >> 32), row_offset, gate};
+            (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step, (uint32_t)(step >> 32), row_offset, gate,
+            x_copy, act_host, actc_host};
   const int tiles = (B + kTileB - 1) / kTileB;
   const int waves_needed = tiles;
   int grid = (waves_needed + 3) / 4;

@@ -110,14 +110,24 @@ def build_hip(verbose=False, force=False) -> str:
                          "-munsafe-fp-atomics", *HIP_FLAGS, *FILE_FLAGS.get(os.path.basename(s), []), "-I", kdir,
                          "-c", s,
                          "-o", o])
+    # host runtime linked into this module: the host-env rollout driver (csrc/runtime) and the
+    # env pools it steps from C++ (csrc/host/vecenv.cpp, a private copy: hidden symbols)
+    hdir, rdir = os.path.join(CSRC, "host"), os.path.join(CSRC, "runtime")
+    rt_headers = sorted(glob.glob(os.path.join(hdir, "*.h"))) + sorted(glob.glob(os.path.join(rdir, "*.h")))
+    for s in sorted(glob.glob(os.path.join(rdir, "*.cpp"))) + [os.path.join(hdir, "vecenv.cpp")]:
+        o = os.path.join(odir, "rt_" + os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(o, [s] + rt_headers):
+            jobs.append([CXX, "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden", "-pthread",
+                         "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-I", hdir, "-I", rdir, "-c", s, "-o", o])
     tinc, tcf, tld = _torch_flags()
     bindings = [binding] + sorted(b for b in glob.glob(os.path.join(CSRC, "bindings", "*_ops.cpp")) if b != binding)
     for bsrc in bindings:
         bo = os.path.join(odir, os.path.basename(bsrc) + ".o")
         objs.append(bo)
-        if force or _newer(bo, [bsrc]):
+        if force or _newer(bo, [bsrc] + rt_headers):
             cmd = [CXX, "-O2", "-std=c++17", "-fPIC", "-DTORCH_EXTENSION_NAME=_hip_ops",
-                   "-DTORCH_API_INCLUDE_EXTENSION_H", "-I/opt/rocm/include"] + tcf
+                   "-DTORCH_API_INCLUDE_EXTENSION_H", "-I/opt/rocm/include", "-I", hdir, "-I", rdir] + tcf
             for i in tinc + _py_includes():
                 cmd += ["-I", i]
             cmd += ["-c", bsrc, "-o", bo]
@@ -125,7 +135,8 @@ def build_hip(verbose=False, force=False) -> str:
     with cf.ThreadPoolExecutor(_jobs()) as ex:
         list(ex.map(lambda c: _run(c, verbose), jobs))
     if force or _newer(HIP_OPS, objs):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + objs + ["-o", HIP_OPS] + tld, verbose)
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread"] + objs + ["-o", HIP_OPS] + tld,
+             verbose)
     return HIP_OPS
 
 

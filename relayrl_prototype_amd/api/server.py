@@ -178,6 +178,9 @@ class TrainingServer:
         if self.engine is not None and hasattr(self.engine, "stop"):
             self.engine.stop()
             self.engine.join(60)
+        tr = getattr(self.algorithm, "trainer", None)
+        if tr is not None and hasattr(tr, "close"):  # releases the host trainer's CU-masked streams
+            tr.close()
         self.disable_server()
         self.service.stop(drain=True)
         if self.tb is not None:

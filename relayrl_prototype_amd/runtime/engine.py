@@ -544,7 +544,9 @@ def run_engine_rank(spec: EngineSpec, env_dir: str, publish_dir: Optional[str], 
         with open(tmp, "w") as f:
             json.dump(res.to_dict(), f)
         os.replace(tmp, result_path)
-    if hasattr(algo.trainer, "finish"):
+    if hasattr(algo.trainer, "close"):
+        algo.trainer.close()
+    elif hasattr(algo.trainer, "finish"):
         algo.trainer.finish()
     if comm.world > 1:
         import torch.distributed as dist

@@ -67,6 +67,11 @@ class HostTrainerConfig:
     log_std_init: float = -0.5
     phase_timing: bool = False
     overlap: bool = False          # lag-1: roll out epoch k+1 while epoch k's update runs (GPU only)
+    native_rollout: bool = True    # GPU: the T-step loop in C++ (csrc/runtime/host_rollout.cpp); False = Python loop
+    driver_wait: int = 2           # C++ driver: 0 tight event poll, 1 hipEventSynchronize, 2 poll with back-off
+    actor_cus: int = 0             # overlap + native: CUs reserved for the rollout's sampling launches (CU-masked
+                                   # streams), the learner's grids sized for the rest.  0 = no partition (measured
+                                   # faster on the CartPole / HalfCheetah host presets, docs/PERF_NOTES.md)
 
     def to_dict(self):
         return asdict(self)
@@ -109,8 +114,19 @@ class HostVecTrainer:
         bounds = [0, N // 2, N] if halves == 2 else [0, N]
         self.bounds = bounds
         rank = self.comm.rank
-        self.envs = [_native.VecEnv(cfg.env, bounds[h + 1] - bounds[h], cfg.seed * 1000003 + rank * 7919 + h,
-                                    max(1, cfg.num_threads // halves)) for h in range(halves)]
+        # GPU + native_rollout: the env pools belong to the HIP extension, whose C++ rollout
+        # driver steps them (no Python per step); otherwise the host runtime's pools
+        envmod = _native
+        self.driver = None
+        if cuda and cfg.native_rollout:
+            from ..ops import hip
+
+            envmod = hip()
+        self.envs = [envmod.VecEnv(cfg.env, bounds[h + 1] - bounds[h], cfg.seed * 1000003 + rank * 7919 + h,
+                                   max(1, cfg.num_threads // halves)) for h in range(halves)]
+        if envmod is not _native:
+            self.driver = envmod.HostRollout(self.envs, bounds)
+            self.driver.set_wait_mode(cfg.driver_wait)
         e0 = self.envs[0]
         self.D, self.A, self.continuous = e0.obs_dim, e0.act_dim, e0.continuous
         self.learner = PGLearner(cfg.algo, self.D, self.A, cfg.hidden, not self.continuous, cfg.with_baseline,
@@ -127,10 +143,14 @@ class HostVecTrainer:
                      for _ in range(2 if self.overlap else 1)]
         self.cur = 0  # buffer set of the newest completed rollout
         self.copy_stream = torch.cuda.Stream(self.device) if cuda else None
+        self.learn_stream = None
+        self._masked = []
         if self.overlap:
             self.actor_stream = torch.cuda.Stream(self.device)
             self.actor_copy_stream = torch.cuda.Stream(self.device)
             self.actor_params = self.learner.pi.params.clone()  # lag-1 snapshot the rollout thread reads
+            if self.driver is not None and cfg.actor_cus > 0:
+                self._partition_cus(cfg.actor_cus, bounds)
         self._pending = None  # (thread, buffer index) of the rollout running ahead
         self.snapshot_versions = []  # policy version each overlapped rollout acted with
         self._primed = False  # a completed rollout waits in self.bufs[self.cur]
@@ -143,6 +163,50 @@ class HostVecTrainer:
         self.env_steps = 0
         self.global_step = 0
         self.timings = {"rollout_s": 0.0, "learn_s": 0.0, "wait_rollout_s": 0.0}
+
+    def _partition_cus(self, n_actor: int, bounds):
+        """Split the chip between the overlapped rollout and the learner: the value / policy
+        kernels are persistent, one 160 KB-LDS workgroup per CU, so a sampling launch on an
+        unpartitioned stream waits for a whole learner kernel to drain (measured: 236 us of
+        a 278 us CartPole env step).  The actor gets ``n_actor`` CUs spread over the chip
+        through a CU-masked stream, the learner a masked stream over the rest, and every
+        grid the learner launches is sized for its share (set_cu_limit)."""
+        from ..ops import hip
+
+        h = hip()
+        n = h.device_cus()
+        n_actor = max(8, min(n_actor, n // 4)) // 8 * 8
+        # CU-mask bit i lands on XCC i % 8 (the driver deals mask bits round-robin over the
+        # XCCs): bits 0 .. n_actor-1 take n_actor / 8 CUs from every XCD, so the learner's grid
+        # (dealt round-robin over the XCDs too) finds the same number of CUs on each.  A
+        # stride pick (0, 16, 32, ...) put every actor CU on one XCD and made the learner
+        # 1.5x slower there (tools/host_overlap_probe.py).
+        actor = list(range(n_actor))
+        learner = list(range(n_actor, n))
+        a_ptr, l_ptr = h.cu_masked_stream(actor), h.cu_masked_stream(learner)
+        self._masked = [a_ptr, l_ptr]
+        self.actor_stream = torch.cuda.ExternalStream(a_ptr, device=self.device)
+        self.learn_stream = torch.cuda.ExternalStream(l_ptr, device=self.device)
+        h.set_cu_limit(len(learner))
+        # the learner was built for the whole chip: re-size its gradient slabs for its share
+        self.learner._pi_slab = None
+        if self.learner.vloop is not None:
+            self.learner.vloop._key = None
+        self.driver = h.HostRollout(self.envs, bounds, len(actor))
+        self.driver.set_wait_mode(self.cfg.driver_wait)
+        self.cu_split = (len(actor), len(learner))
+
+    def close(self):
+        """Release the CU-masked streams and the grid-size limit (overlapped host trainer)."""
+        self.finish()
+        if self._masked:
+            from ..ops import hip
+
+            torch.cuda.synchronize(self.device)
+            hip().set_cu_limit(0)
+            for p in self._masked:
+                hip().destroy_stream(p)
+            self._masked = []
 
     # views of the newest completed rollout (actor_learner.py, tests)
     @property
@@ -178,11 +242,15 @@ class HostVecTrainer:
         return self.bufs[self.cur].d_tobs
 
     # ------------------------------------------------------------------ rollout
+    @property
+    def sample_seed(self) -> int:
+        return (self.cfg.seed * 0x9E3779B9 + self.comm.rank * 0x85EBCA6B) & 0x7FFFFFFFFFFF
+
     def _sample(self, b: _Buffers, params, copy_stream, t, h, step):
         lo, hi = self.bounds[h], self.bounds[h + 1]
         cuda = self.device.type == "cuda"
         mode = FwdMode.GAUSS_SAMPLE if self.continuous else FwdMode.CAT_SAMPLE
-        seed = (self.cfg.seed * 0x9E3779B9 + self.comm.rank * 0x85EBCA6B) & 0x7FFFFFFFFFFF
+        seed = self.sample_seed
         if cuda:
             cs = torch.cuda.current_stream(self.device)
             with torch.cuda.stream(copy_stream):
@@ -224,6 +292,14 @@ class HostVecTrainer:
             copy_stream.wait_stream(torch.cuda.current_stream(self.device))
         if self._final_obs is not None and self._final_obs.data_ptr() != b.h_obs[0].data_ptr():
             b.h_obs[0].copy_(self._final_obs)  # continue every env where the last rollout left it
+        if self.driver is not None:
+            # C++ loop: one zero-copy sampling launch per half-step on this thread's current
+            # stream (ordered after the previous update's reads of these buffers)
+            self.driver.run(params, self.cfg.hidden, b.h_obs, b.h_act, b.h_rew, b.h_done, b.h_tobs, b.d_obs,
+                            b.d_act, b.d_logp, b.d_rew, b.d_done, b.d_tobs, self.sample_seed, step0)
+            b.ready.record(torch.cuda.current_stream(self.device))
+            self._final_obs = b.h_obs[T]
+            return
         for t in range(T):
             evs = []
             for h in range(self.halves):
@@ -283,10 +359,12 @@ class HostVecTrainer:
 
     def _launch_ahead(self, idx: int):
         """Roll out into buffer set ``idx`` on a thread, with the weights as of now."""
-        self.actor_params.copy_(self.learner.pi.params)  # compute stream, after the previous update
+        ls = self.learn_stream or torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(ls):
+            self.actor_params.copy_(self.learner.pi.params)  # learner stream, after the previous update
         self.snapshot_versions.append(self.learner.pi.version)
         snap = torch.cuda.Event()
-        snap.record(torch.cuda.current_stream(self.device))
+        snap.record(ls)
         step0 = self.global_step
         self.global_step += self.cfg.rollout_len
 
@@ -325,8 +403,16 @@ class HostVecTrainer:
         nxt = 1 - learn_idx
         self._launch_ahead(nxt)  # epoch k+1's envs step while epoch k's update runs
         t0 = time.perf_counter()
-        with self.timer.phase("Optimize"):
-            self._learn(learn_idx)
+        if self.learn_stream is not None:
+            cs = torch.cuda.current_stream(self.device)
+            self.learn_stream.wait_stream(cs)
+            with torch.cuda.stream(self.learn_stream):
+                with self.timer.phase("Optimize"):
+                    self._learn(learn_idx)
+            cs.wait_stream(self.learn_stream)  # everything after the epoch sees the update
+        else:
+            with self.timer.phase("Optimize"):
+                self._learn(learn_idx)
         self.timings["learn_s"] += time.perf_counter() - t0
         self.cur = self._join_ahead()
 
@@ -374,6 +460,12 @@ class HostVecTrainer:
         out["RolloutS"] = self.timings["rollout_s"]
         out["LearnS"] = self.timings["learn_s"]
         out["WaitRolloutS"] = self.timings["wait_rollout_s"]
+        if self.driver is not None:  # per-env-step breakdown of the C++ rollout loop (driver thread)
+            st = self.driver.take_stats()
+            n = max(st["steps"], 1)
+            out.update(HostStepUs=st["total_us"] / n, HostEnvWaitUs=st["env_wait_us"] / n,
+                       HostGpuWaitUs=st["gpu_wait_us"] / n, HostLaunchUs=st["launch_us"] / n,
+                       HostTailUs=st["tail_us"] / n)
         if self.timer.enabled:
             out.update(self.timer.columns())
             self.timer.reset()

@@ -282,7 +282,9 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
                                                                  "world": comm.world, "rank": comm.rank})
         maybe_kill_rank(orig_rank, ep, out_dir)
         ep += 1
-    if hasattr(tr, "finish"):
+    if hasattr(tr, "close"):
+        tr.close()
+    elif hasattr(tr, "finish"):
         tr.finish()
     if eg is not None:
         last = dict(last)

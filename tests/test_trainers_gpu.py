@@ -173,13 +173,22 @@ def test_agent_server_zmq_with_gpu_learner(cuda, tmp_path, monkeypatch):
         srv.close(save=False)
 
 
+def hip_cus_limit() -> int:
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    prev = h.set_cu_limit(0)
+    h.set_cu_limit(prev)
+    return prev
+
+
 def test_host_trainer_overlap_lag1(cuda):
     """Lag-1 host pipeline: rollout k+1 acts with the policy of update k-1 while update k runs,
     every epoch learns exactly one rollout, and the buffers alternate."""
     from relayrl_prototype_amd.runtime.host_trainer import HostTrainerConfig, HostVecTrainer
 
     cfg = HostTrainerConfig(env="CartPole-v1", num_envs=512, rollout_len=32, train_vf_iters=4, num_threads=4,
-                            overlap=True, seed=2)
+                            overlap=True, seed=2, actor_cus=16)
     tr = HostVecTrainer(cfg, device=cuda)
     assert tr.overlap and len(tr.bufs) == 2
     for _ in range(4):
@@ -190,6 +199,9 @@ def test_host_trainer_overlap_lag1(cuda):
     m = tr.metrics()
     assert m["EnvSteps"] == 4 * 512 * 32
     assert math.isfinite(m["LossPi"]) and torch.isfinite(tr.learner.pi.params).all()
+    assert tr.cu_split[0] == 16 and hip_cus_limit() == tr.cu_split[1]
+    tr.close()
+    assert hip_cus_limit() == 0
 
 
 def test_host_trainer_overlap_learns(cuda):
@@ -206,7 +218,7 @@ def test_host_trainer_overlap_learns(cuda):
             best = max(best, m["AverageEpRet"])
         if best > 150:
             break
-    tr.finish()
+    tr.close()
     assert best > 150, best
 
 
@@ -226,10 +238,40 @@ def test_host_trainer_no_sync_equals_synced(cuda, overlap):
             tr.train_epoch()
             if sync_every_epoch:
                 torch.cuda.synchronize()
-        tr.finish()
+        tr.close()
         torch.cuda.synchronize()
         return tr.learner.pi.params.clone(), tr.learner.vf.params.clone()
 
     p_sync, v_sync = run(True)
     p_fast, v_fast = run(False)
     assert torch.equal(p_sync, p_fast) and torch.equal(v_sync, v_fast)
+
+
+@pytest.mark.parametrize("env", ["CartPole-v1", "HalfCheetahSynth-v0"])
+def test_native_host_rollout_matches_python_loop(cuda, env):
+    """The C++ rollout driver (csrc/runtime/host_rollout.cpp: zero-copy sampling launches,
+    env threads stepped from C++) produces bit for bit the rollout of the Python loop
+    (same Philox streams, same env seeds), and the learner then agrees exactly."""
+    from relayrl_prototype_amd.runtime.host_trainer import HostTrainerConfig, HostVecTrainer
+
+    def run(native):
+        cfg = HostTrainerConfig(env=env, num_envs=1000, rollout_len=24, train_vf_iters=3, num_threads=4, seed=3,
+                                algo="ppo" if env.startswith("Half") else "reinforce", train_pi_iters=2,
+                                native_rollout=native)
+        tr = HostVecTrainer(cfg, device=cuda)
+        assert (tr.driver is not None) == native
+        outs = []
+        for _ in range(3):
+            tr.train_epoch()
+            torch.cuda.synchronize()
+            outs.append([x.clone() for x in (tr.d_obs, tr.d_act, tr.d_logp, tr.d_rew, tr.d_done)])
+        m = tr.metrics()
+        return outs, tr.learner.pi.params.clone(), m
+
+    o_nat, p_nat, m_nat = run(True)
+    o_py, p_py, _ = run(False)
+    for a, b in zip(o_nat, o_py):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    assert torch.equal(p_nat, p_py)
+    assert m_nat["HostStepUs"] > 0 and m_nat["HostEnvWaitUs"] >= 0
