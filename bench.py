@@ -78,6 +78,9 @@ def parse(argv=None):
     ap.add_argument("--actor-learner", choices=("auto", "on", "off"), default="auto",
                     help="secondary phase: the actor -> learner-group P2P data plane (BASELINE config #3 "
                          "topology, K = 2 actor blocks per learner shard); auto = only with world > 1")
+    ap.add_argument("--host-steps", type=int, default=6,
+                    help="1 GPU: also time the host-env data path (C++ env threads + the C++ rollout driver, "
+                         "cartpole-reinforce-host preset, lag-1 overlap) for this many epochs; 0 = skip")
     ap.add_argument("--al-steps", type=int, default=10)
     ap.add_argument("--al-warmup", type=int, default=5)
     ap.add_argument("--al-env", default="LunarLanderSynth-v0")
@@ -183,6 +186,49 @@ def collect_reference_cpu(proc, budget_s: float):
         except ValueError:
             continue
     return None
+
+
+# ---------------------------------------------------------------------- host-env data path
+def host_path_probe(steps: int, comm) -> dict:
+    """The north-star data path on one GPU: CartPole envs stepped by C++ threads on the host,
+    the T-step loop in C++ (csrc/runtime/host_rollout.cpp: zero-copy sampling launches), the
+    same fused learner on the GPU, rollout k+1 overlapped with update k (lag 1).  Reported
+    next to the headline; 2 untimed warmup epochs, then ``steps`` timed ones."""
+    import torch
+
+    from relayrl_prototype_amd.runtime.launcher import PRESETS, _make_trainer
+
+    p = PRESETS["cartpole-reinforce-host"]
+    dev = torch.device("cuda", torch.cuda.current_device())
+    rec = {"preset": p.name, "steps": steps, "warmup": 2}
+    tr = None
+    try:
+        tr = _make_trainer(p, comm, dev, {})
+        for _ in range(2):
+            tr.train_epoch()
+        tr.finish()
+        m0 = tr.metrics()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            tr.train_epoch()
+        tr.finish()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        m1 = tr.metrics()
+        n = m1["EnvSteps"] - m0["EnvSteps"]
+        rec.update(env_steps_per_s=round(n / dt, 1), ms_per_epoch=round(dt / steps * 1e3, 3),
+                   num_envs=tr.cfg.num_envs, rollout_len=tr.cfg.rollout_len, env_threads=tr.cfg.num_threads,
+                   overlap=tr.overlap, per_env_step_us={k: round(v, 2) for k, v in m1.items()
+                                                        if k.startswith("Host") and k.endswith("Us")})
+    except Exception as e:  # noqa: BLE001 -- recorded; the headline still prints
+        rec["error"] = f"{type(e).__name__}: {e}"[:300]
+    finally:
+        if tr is not None:
+            tr.close()
+            del tr
+        torch.cuda.empty_cache()
+    return rec
 
 
 # ---------------------------------------------------------------------- comm-phase observability
@@ -345,6 +391,7 @@ def main(argv=None):
     per_rank = comm.all_gather_object(round(cfg.num_envs * cfg.rollout_len * args.steps / dt_local, 1))
     per_rank_ms = comm.all_gather_object(round(dt_local / args.steps * 1e3, 3))
     phases = phase_probe(tr, comm, args.phase_steps) if args.phase_steps > 0 else None
+    host_rec = host_path_probe(args.host_steps, comm) if (on_gpu and world == 1 and args.host_steps > 0) else None
     al_rec = None
     if args.actor_learner == "on" or (args.actor_learner == "auto" and world > 1):
         al_rec = actor_learner_probe(args, comm, on_gpu)
@@ -421,6 +468,8 @@ def main(argv=None):
             rec["phase_ms_per_step"] = dict(phases, steps=args.phase_steps,
                                             note="per rank, device ms per epoch from HIP events, measured in "
                                                  "extra epochs after the timed region")
+        if host_rec is not None:
+            rec["host_env_path"] = host_rec
         if al_rec is not None:
             rec["actor_learner"] = al_rec
         if ref_cpu is not None:

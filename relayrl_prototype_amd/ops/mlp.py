@@ -142,12 +142,25 @@ def mlp_forward(mode: int, params: torch.Tensor, X: torch.Tensor, A: int, H: int
     return out
 
 
+# Rows per fused fwd+bwd launch.  The grad kernels index rows x features in 32 bits (the binding
+# refuses B * max(D, A) >= 2^31), so a larger batch -- the 10^8-transition HBM rollout buffers of
+# BASELINE config #5 -- is launched in chunks whose gradient slabs sit back to back in one slab
+# array: the fused reduce + Adam sums them all, and inv_B stays 1 / (the whole batch).
+GRAD_CHUNK_ROWS = 1 << 25
+
+
+def grad_chunks(B: int):
+    """[(lo, hi)] row ranges of the launches for a B-row batch."""
+    return [(lo, min(B, lo + GRAD_CHUNK_ROWS)) for lo in range(0, max(B, 1), GRAD_CHUNK_ROWS)]
+
+
 def grad_slabs(B: int, device) -> int:
     if torch.device(device).type != "cuda":
         return 1
     from . import hip
 
-    return int(hip().mlp_grad_slabs(B))
+    h = hip()
+    return sum(int(h.mlp_grad_slabs(hi - lo)) for lo, hi in grad_chunks(B))
 
 
 def set_value_grad_mode(mode: int) -> int:
@@ -183,13 +196,24 @@ def mlp_grad(head: int, params, X, A: int, H: int, mask=None, act=None, actc=Non
     gaussian = int(head) in (GradHead.PPO_GAUSS, GradHead.PG_GAUSS)
     Aeff = 1 if int(head) == GradHead.VALUE_MSE else A
     P = MLPSpec(X.shape[1], H, Aeff, gaussian).P
-    ns = int(h.mlp_grad_slabs(B))
+    ns = grad_slabs(B, X.device)
     if grad_slab is None:
         grad_slab = torch.empty(ns, P, device=X.device)
     if loss_slab is None:
         loss_slab = torch.empty(ns, 8, device=X.device)
-    h.mlp_grad(int(head), params, X, A, H, _f32(mask), _i32(act), _f32(actc), _f32(adv), _f32(ret), _f32(logp_old),
-               adv_stats, float(inv_B), float(clip_eps), float(ent_coef), grad_slab, loss_slab)
+    mask, act, actc, adv, ret, logp_old = _f32(mask), _i32(act), _f32(actc), _f32(adv), _f32(ret), _f32(logp_old)
+    off = 0
+    for lo, hi in grad_chunks(B):
+        whole = lo == 0 and hi == B
+
+        def rows(t):
+            return t if (t is None or whole) else t[lo:hi]
+
+        n = int(h.mlp_grad_slabs(hi - lo))
+        h.mlp_grad(int(head), params, rows(X), A, H, rows(mask), rows(act), rows(actc), rows(adv), rows(ret),
+                   rows(logp_old), adv_stats, float(inv_B), float(clip_eps), float(ent_coef), grad_slab[off:off + n],
+                   loss_slab[off:off + n])
+        off += n
     return grad_slab[:ns], loss_slab[:ns]
 
 

@@ -130,10 +130,11 @@ class _Actor:
 
     def __init__(self, cfg: ActorLearnerConfig, comm: Comm, device, need_tobs: bool):
         self.device = torch.device(device)
-        from .vec_trainer import CONTINUOUS_DEVICE_ENVS, DEVICE_ENVS
+        from .vec_trainer import DEVICE_ENVS
 
-        self.kind = "device" if (self.device.type == "cuda" and cfg.env in DEVICE_ENVS
-                                 and cfg.env not in CONTINUOUS_DEVICE_ENVS) else "host"
+        # device envs (discrete: rollout_kernel; continuous HalfCheetahSynth: the Gaussian
+        # rollout_cont_kernel, the reference's ContinuousPolicyNetwork completed, kernel.py:49-75)
+        self.kind = "device" if (self.device.type == "cuda" and cfg.env in DEVICE_ENVS) else "host"
         if self.kind == "device":
             from .vec_trainer import VecTrainer, VecTrainerConfig
 

@@ -66,3 +66,43 @@ def test_actor_learner_colocated_gpu(cuda):
     assert m["EnvSteps"] == 3 * 32 * 512 and m["ActorVersions"] == [2]
     assert torch.isfinite(al.learner.pi.params).all() and not torch.equal(p0, al.learner.pi.params)
     assert torch.equal(al.actor.params, al.learner.pi.params)
+
+
+def test_actor_learner_colocated_continuous_device_env(cuda):
+    """HalfCheetahSynth under the actor-learner topology rolls out on the DEVICE (the
+    Gaussian rollout_cont kernel), not on host threads."""
+    from relayrl_prototype_amd.runtime.actor_learner import ActorLearner, ActorLearnerConfig
+
+    al = ActorLearner(ActorLearnerConfig(env="HalfCheetahSynth-v0", algo="ppo", num_envs=1024, rollout_len=32,
+                                         train_vf_iters=3, train_pi_iters=3, verify_versions=True,
+                                         phase_timing=True), device=cuda)
+    assert al.actor.kind == "device" and al.continuous and al.topo.K == 1
+    p0 = al.learner.pi.params.clone()
+    for _ in range(3):
+        al.step()
+    al.finish()
+    m = al.metrics()
+    assert m["EnvSteps"] == 3 * 32 * 1024 and m["ActorVersions"] == [2]
+    assert m["RolloutMs"] > 0 and m["LearnMs"] > 0  # phase columns
+    assert torch.isfinite(al.learner.pi.params).all() and not torch.equal(p0, al.learner.pi.params)
+    assert al.b_act.dtype == torch.float32 and al.b_act.shape[-1] == 6
+
+
+def test_grad_chunks_equal_one_launch(cuda, monkeypatch):
+    """Batches past GRAD_CHUNK_ROWS are launched in chunks whose slabs sit back to back; the
+    summed gradient equals the one-launch gradient (fp32 summation order aside)."""
+    from relayrl_prototype_amd.ops import GradHead, mlp, MLPSpec, mlp_grad, reduce_slabs
+
+    g = torch.Generator().manual_seed(3)
+    B, D = 70_000, 17
+    X = torch.randn(B, D, generator=g).to(cuda)
+    ret = torch.randn(B, generator=g).to(cuda)
+    vp = MLPSpec(D, 128, 1).init(g).to(cuda)
+    one = reduce_slabs(mlp_grad(GradHead.VALUE_MSE, vp, X, 1, 128, ret=ret, inv_B=1.0 / B)[0])
+    monkeypatch.setattr(mlp, "GRAD_CHUNK_ROWS", 16_384)
+    assert len(mlp.grad_chunks(B)) == 5
+    slab, ls = mlp_grad(GradHead.VALUE_MSE, vp, X, 1, 128, ret=ret, inv_B=1.0 / B)
+    assert slab.shape[0] == mlp.grad_slabs(B, cuda)
+    chunked = reduce_slabs(slab)
+    torch.testing.assert_close(chunked, one, rtol=1e-4, atol=1e-6)
+    assert int(ls[:, 5].sum().item()) == B  # every row counted once

@@ -275,3 +275,36 @@ def test_native_host_rollout_matches_python_loop(cuda, env):
             assert torch.equal(x, y)
     assert torch.equal(p_nat, p_py)
     assert m_nat["HostStepUs"] > 0 and m_nat["HostEnvWaitUs"] >= 0
+
+
+def test_halfcheetah_ppo_chunked_big_batch(cuda):
+    """A 39 M-transition PPO epoch (HalfCheetahSynth, 65,536 envs x 600 steps): the fused
+    fwd+bwd launches split at GRAD_CHUNK_ROWS (2 chunks), 64-bit buffer addressing in the
+    rollout / forward / scan kernels (obs buffer 2.7 GB, > 2^31 floats' byte offsets), and the
+    GAE scan of sampled columns against the float64 oracle."""
+    from relayrl_prototype_amd.ops import mlp as mlpops
+    from relayrl_prototype_amd.ops import reference as ref
+    from relayrl_prototype_amd.runtime.vec_trainer import VecTrainer, VecTrainerConfig
+
+    T, N = 600, 65536
+    assert len(mlpops.grad_chunks(T * N)) == 2
+    cfg = VecTrainerConfig(env="HalfCheetahSynth-v0", algo="ppo", num_envs=N, rollout_len=T, train_pi_iters=2,
+                           train_vf_iters=2, gamma=0.99, lam=0.95, use_graphs=False)
+    tr = VecTrainer(cfg, device=cuda)
+    p0 = tr.pi.params.clone()
+    tr.train_epoch()
+    torch.cuda.synchronize()
+    m = tr.metrics()
+    assert torch.isfinite(tr.pi.params).all() and not torch.equal(p0, tr.pi.params)
+    assert math.isfinite(m["LossPi"]) and math.isfinite(m["LossV"])
+    cols = torch.randperm(N, generator=torch.Generator().manual_seed(1))[:32].to(cuda)
+    rl = tr.rl
+    a_ref, r_ref, _ = ref.gae_scan_tm_ref(tr.rew[:, cols].double().cpu(), tr.done[:, cols].double().cpu(),
+                                          rl.val.view(T + 1, N)[:, cols].double().cpu().reshape(-1), 0.99, 0.95,
+                                          rl.tval[:, cols].double().cpu())
+    torch.testing.assert_close(rl.adv[:, cols].double().cpu(), a_ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rl.ret[:, cols].double().cpu(), r_ref, rtol=1e-4, atol=1e-4)
+    # the last env column's final observation sits past byte offset 2^31 of the obs buffer
+    assert tr.obs.numel() * 4 > 2 ** 31 and torch.isfinite(tr.obs[T, N - 1]).all()
+    del tr
+    torch.cuda.empty_cache()
