@@ -12,6 +12,17 @@ action to the current episode.  Semantics (docs/COMPAT.md):
     as a time-limit cut so the learner bootstraps from V(s_T);
   * model updates arrive asynchronously (ZMQ push / gRPC poll after each episode /
     in-process subscription) and are swapped atomically between steps.
+
+``wire_format``: "columns" (one RRLC frame per episode, the default), "actions" (per-action
+RRLT frames / protobuf actions), or "reference" (ZMQ only): the reference agent's own wire,
+to train against a reference Rust training server -- GET_MODEL without a format frame,
+``serde_pickle(Vec<RelayRLAction>)`` uploads (trajectory.rs:50-90) and TorchScript model
+pushes into a PULL this agent binds on ``training_server`` (agent_zmq.rs:316-442, 625-698).
+Uploads are per episode (the reference re-sent the whole history each time, defect A1); each
+action carries its OWN step's reward and ``data = {"logp_a", "v"}`` tensors, and the episode
+ends in the reference's terminal marker ``(None, None, None, rew, done=True)`` whose reward is
+the REINFORCE.py:86 ``finish_path(last_val)`` bootstrap: 0 after a terminal state, V(s_T)
+after a time-limit cut (docs/COMPAT.md).
 """
 from __future__ import annotations
 
@@ -55,9 +66,13 @@ class RelayRLAgent:
         self.enabled = True
         self.transport = None
         self._handshake_timeout = handshake_timeout_s
-        if wire_format not in ("columns", "actions"):
-            raise ValueError("wire_format must be 'columns' (RRLC frames) or 'actions' (per-action RRLT / protobuf)")
+        if wire_format not in ("columns", "actions", "reference"):
+            raise ValueError("wire_format must be 'columns' (RRLC frames), 'actions' (per-action RRLT / protobuf) "
+                             "or 'reference' (serde_pickle frames + TorchScript pushes, ZMQ only)")
+        if wire_format == "reference" and self.server_type != "zmq":
+            raise ValueError("wire_format='reference' is the reference's ZMQ wire; use server_type='zmq'")
         self.wire_format = wire_format
+        self._vals = []  # reference wire: V(s_t) of the recorded steps (the actions' data['v'])
         self._rec = EpisodeRecorder(self.max_traj_length)
         if model_path is not None:
             self._load_model_file(model_path)
@@ -119,6 +134,13 @@ class RelayRLAgent:
             for d in (al, tr):
                 if d["host"] in ("*", "0.0.0.0"):
                     d["host"] = "127.0.0.1"
+            if self.wire_format == "reference":
+                from ..transport.zmq_transport import ReferenceZmqAgentTransport
+
+                ts = dict(self.train_server)  # the PULL this agent binds (agent_zmq.rs:625-640)
+                self.transport = ReferenceZmqAgentTransport(self.agent_id, address(al), address(tr), address(ts),
+                                                            self._set_policy, self._handshake_timeout)
+                return
             self.transport = ZmqAgentTransport(self.agent_id, address(al), address(tr), self._set_policy,
                                                self._handshake_timeout)
         elif self.server_type == "grpc":
@@ -136,7 +158,33 @@ class RelayRLAgent:
         else:
             raise ValueError(f"server_type must be zmq, grpc or local, not {self.server_type!r}")
 
+    def _reference_frame(self, cols, done: bool, next_obs=None) -> bytes:
+        """One episode as the reference agent's upload: serde_pickle(Vec<RelayRLAction>)."""
+        from ..transport.serde_pickle import reference_frame
+
+        acts = []
+        vals = self._vals
+        for i in range(len(cols)):
+            data = {"logp_a": np.array([cols.logp[i]], np.float32)}
+            if i < len(vals) and vals[i] is not None:
+                data["v"] = np.array([vals[i]], np.float32)
+            acts.append(RelayRLAction(cols.obs[i], cols.act[i], None if cols.mask is None else cols.mask[i],
+                                      float(cols.rew[i]), data, False, True))
+        last = 0.0
+        if not done and next_obs is not None and self.policy is not None:
+            with self._policy_lock:
+                v = self.policy.value(np.asarray(next_obs, np.float32).reshape(1, -1))
+            last = 0.0 if v is None else float(np.asarray(v).reshape(-1)[0])
+        acts.append(RelayRLAction(None, None, None, last, None, True, False))  # agent_zmq.rs:605-610 marker
+        self._vals = []
+        return reference_frame(acts)
+
     def _ship(self, done: bool, next_obs=None):
+        if self.wire_format == "reference":
+            cols = self._rec.take(self.agent_id, self.episodes_sent, done, next_obs)
+            self.transport.send_trajectory(self._reference_frame(cols, done, next_obs))
+            self.episodes_sent += 1
+            return
         cols = self._rec.take(self.agent_id, self.episodes_sent, done, next_obs)
         cols.max_length = self.max_traj_length
         if self.server_type == "zmq":
@@ -185,6 +233,9 @@ class RelayRLAgent:
         a0 = np.asarray(act[0] if act.ndim >= 1 else act)
         logp = data.get("logp_a")
         rec.record(obs_a, a0, mask_a, None if logp is None else logp[0])
+        if self.wire_format == "reference":
+            v = data.get("v")
+            self._vals.append(None if v is None else float(np.asarray(v).reshape(-1)[0]))
         aux = {k: np.asarray(v[0], np.float32) for k, v in data.items()}
         action = RelayRLAction(obs_a, a0, mask_a, 0.0, aux, False, False)
         return action

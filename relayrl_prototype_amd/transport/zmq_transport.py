@@ -290,3 +290,109 @@ class ZmqAgentTransport:
             self._hb.join(timeout=5)
         self.dealer.close()
         self.push.close()
+
+
+class ReferenceZmqAgentTransport:
+    """The reference agent's own wire, for talking to a reference (Rust) training server
+    (or to ZmqTrainingEndpoint, which accepts both dialects):
+
+      * handshake (agent_zmq.rs:316-442): DEALER (identity = agent id) -> ``["", "GET_MODEL"]``
+        with NO format frame; the server answers ``["", <TorchScript archive>]`` (or
+        ``"ERROR: ..."``); the agent loads it, then ``["", "MODEL_SET"]`` -> ``["", "ID_LOGGED"]``;
+        retried every second until the timeout;
+      * uploads (trajectory.rs:50-90): ``serde_pickle(Vec<RelayRLAction>)`` frames on a PUSH to
+        ``trajectory_server`` (one connection for all uploads, not a new context per send);
+      * model updates (agent_zmq.rs:625-698): the agent BINDS a PULL on its ``training_server``
+        address and the server PUSH-connects to it, one TorchScript archive per update.  A
+        receive thread blocks with a timeout (no busy poll) and swaps the policy.
+    Archives are read by ``utils.checkpoint.reference_weights_from_bytes`` (raw zip storages;
+    nothing in them is unpickled or executed)."""
+
+    def __init__(self, agent_id: str, agent_listener: str, trajectory_server: str, training_server: str,
+                 on_model: Callable[[ModelBlob], None], handshake_timeout_s: float = 60.0):
+        self.agent_id = agent_id
+        self.on_model = on_model
+        self.version = 0
+        self.bad_models = 0
+        self.pull = _native.ZmtpSocket(_native.SockType.PULL)
+        self.pull.bind(training_server)  # before the handshake: the server may push at once
+        self.dealer = _native.ZmtpSocket(_native.SockType.DEALER, agent_id.encode())
+        self.dealer.connect(agent_listener)
+        self.push = _native.ZmtpSocket(_native.SockType.PUSH)
+        self.push.connect(trajectory_server)
+        self._stop = threading.Event()
+        self._handshake(handshake_timeout_s)
+        self._thread = threading.Thread(target=self._model_loop, daemon=True, name="rrl-ref-agent-models")
+        self._thread.start()
+
+    def _load(self, blob: bytes) -> ModelBlob:
+        from ..utils.checkpoint import reference_weights_from_bytes
+
+        w = reference_weights_from_bytes(blob)
+        self.version += 1
+        mb = ModelBlob(self.version, {"obs_dim": w["obs_dim"], "act_dim": w["act_dim"], "hidden": w["hidden"],
+                                      "discrete": True}, w["pi"], w["vf"])
+        self.on_model(mb)
+        return mb
+
+    def _recv_reply(self, timeout_s: float):
+        msg = self.dealer.recv(int(timeout_s * 1000))
+        if msg is None:
+            return None
+        _, frames = msg
+        body = [f for f in frames if f != b""]
+        return body[0] if body else None
+
+    def _handshake(self, timeout_s: float):
+        t0 = time.time()
+        while time.time() - t0 < timeout_s:
+            if not self.dealer.send([b"", b"GET_MODEL"], 1000):
+                time.sleep(1.0)
+                continue
+            rep = self._recv_reply(2.0)
+            if rep is None or rep.startswith(b"ERROR"):
+                time.sleep(1.0)  # agent_zmq.rs retries every second
+                continue
+            try:
+                self._load(rep)
+            except Exception as e:  # a model the agent cannot validate: ask again
+                self.bad_models += 1
+                print(f"[ReferenceZmqAgentTransport] bad model in the handshake: {e!r}", flush=True)
+                time.sleep(1.0)
+                continue
+            if self.dealer.send([b"", b"MODEL_SET"], 1000) and self._recv_reply(5.0) == b"ID_LOGGED":
+                return
+        raise TimeoutError("reference ZMQ handshake with the training server timed out")
+
+    def _model_loop(self):
+        while not self._stop.is_set():
+            msg = self.pull.recv(100)
+            if msg is None:
+                continue
+            _, frames = msg
+            for f in frames:
+                if not f:
+                    continue
+                try:
+                    self._load(f)
+                except Exception as e:
+                    self.bad_models += 1
+                    print(f"[ReferenceZmqAgentTransport] bad model update: {e!r}", flush=True)
+
+    def send_trajectory(self, payload: bytes) -> bool:
+        from ..utils.faults import injector
+
+        payload = injector().filter_upload(payload)
+        if payload is None:
+            return True
+        return self.push.send([payload], 10000)
+
+    def heartbeat(self):
+        pass  # the reference protocol has none (the server exempts reference agents from eviction)
+
+    def close(self):
+        self._stop.set()
+        self._thread.join(timeout=5)
+        self.dealer.close()
+        self.push.close()
+        self.pull.close()

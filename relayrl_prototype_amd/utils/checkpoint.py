@@ -119,3 +119,42 @@ def import_reference_weights(pt_path: str, obs_dim: int, act_dim: int, hidden: i
     if len(order) >= 12 and sizes[6:12] == vf_sizes:
         vf = np.concatenate(order[6:12]).astype(np.float32)
     return pi, vf
+
+
+def reference_weights_from_bytes(blob: bytes) -> Dict[str, Any]:
+    """A TorchScript policy archive as the reference server pushes it (training_zmq.rs:876-934,
+    agent_zmq.rs:625-698: the bytes of ``torch.jit.save`` of PolicyWithoutBaseline /
+    PolicyWithBaseline, kernel.py:87-143) -> flat fp32 weights and the dims, read from the
+    zip's raw ``data/N`` storages only (the archive's pickles are never executed).
+
+    The dims come from the storage sizes of the Linear stack [H*D, H, H*H, H, A*H, A]
+    (+ the value net's [H*D, H, H*H, H, H, 1] for PolicyWithBaseline)."""
+    import io
+
+    with zipfile.ZipFile(io.BytesIO(blob)) as z:
+        entries = {}
+        for n in z.namelist():
+            parts = n.split("/")
+            if len(parts) >= 2 and parts[-2] == "data" and parts[-1].isdigit():
+                entries[int(parts[-1])] = np.frombuffer(z.read(n), dtype="<f4").copy()
+    order = [entries[k] for k in sorted(entries)]
+    if len(order) < 6:
+        raise ValueError(f"a policy archive holds at least 6 storages, found {len(order)}")
+    s = [a.size for a in order]
+    H = s[1]
+    if H < 1 or s[0] % H or s[2] != H * H or s[3] != H or s[4] % H or s[5] * H != s[4]:
+        raise ValueError(f"storage sizes {s[:6]} are not a Linear-ReLU-Linear-ReLU-Linear policy")
+    D = s[0] // H
+    value_sizes = [H * D, H, H * H, H, H, 1]
+    first, second = order[:6], order[6:12]
+    if len(order) >= 12 and s[:6] == value_sizes and s[6:12] != value_sizes:
+        first, second = second, first  # a module that lists its baseline before its policy
+    sf = [a.size for a in first]
+    A = sf[5]
+    if sf != [H * D, H, H * H, H, A * H, A]:
+        raise ValueError(f"storage sizes {sf} are not a [{D}, {H}, {H}, A] policy")
+    pi = np.concatenate(first).astype(np.float32)
+    vf = None
+    if len(second) == 6 and [a.size for a in second] == value_sizes:
+        vf = np.concatenate(second).astype(np.float32)
+    return {"pi": pi, "vf": vf, "obs_dim": int(D), "act_dim": int(A), "hidden": int(H)}

@@ -1,0 +1,225 @@
+"""RelayRLAgent(wire_format="reference"): the reference agent's own ZMQ wire.
+
+A scripted endpoint plays the reference training server byte for byte -- ROUTER handshake
+(agent_zmq.rs:316-442 / training_zmq.rs:705-838), PULL for serde_pickle(Vec<RelayRLAction>)
+uploads (trajectory.rs:50-90) and a PUSH that connects to the PULL the agent binds on
+``training_server`` (training_zmq.rs:876-934 / agent_zmq.rs:625-698).  The model it serves is
+the reference's own shipped ``client_model.pt`` (read as zip storages, never unpickled).
+Parity against the real Rust server stays unpinned: it cannot be built here.
+"""
+import json
+import os
+import socket
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from relayrl_prototype_amd import _native
+from relayrl_prototype_amd.api.agent import RelayRLAgent
+from relayrl_prototype_amd.config import DEFAULT_CONFIG_CONTENT
+from relayrl_prototype_amd.transport import serde_pickle as sp
+
+REF_PT = "/root/reference/examples/REINFORCE_with_baseline/classic_control/cartpole/zmq/client_model.pt"
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _config(tmp_path, **algo):
+    cfg = json.loads(DEFAULT_CONFIG_CONTENT)
+    for k in ("training_server", "trajectory_server", "agent_listener"):
+        cfg["server"][k]["port"] = str(_port())
+    cfg["algorithms"]["REINFORCE"].update(algo)
+    p = tmp_path / "relayrl_config.json"
+    p.write_text(json.dumps(cfg))
+    return cfg, str(p)
+
+
+def _our_archive(seed: int, with_vf: bool):
+    """A TorchScript archive of our own export (models/policies.py), reference class layout."""
+    import torch
+
+    from relayrl_prototype_amd.models.policies import build_policy_module, torchscript_bytes
+    from relayrl_prototype_amd.ops import MLPSpec
+
+    g = torch.Generator().manual_seed(seed)
+    pi = MLPSpec(4, 128, 2).init(g)
+    vf = MLPSpec(4, 128, 1).init(g) if with_vf else None
+    return torchscript_bytes(build_policy_module(4, 2, 128, pi, vf)), pi.numpy()
+
+
+def _logits(pi: np.ndarray, obs: np.ndarray) -> np.ndarray:
+    """numpy forward of the flat [4, 128, 128, 2] policy (oracle for the agent's C++ policy)."""
+    o = 0
+    parts = []
+    for fi, fo in ((4, 128), (128, 128), (128, 2)):
+        w = pi[o:o + fi * fo].reshape(fo, fi)
+        o += fi * fo
+        b = pi[o:o + fo]
+        o += fo
+        parts.append((w, b))
+    h = obs.astype(np.float64)
+    for i, (w, b) in enumerate(parts):
+        h = w @ h + b
+        if i < 2:
+            h = np.maximum(h, 0)
+    return h
+
+
+class ScriptedReferenceServer:
+    def __init__(self, cfg, model_bytes: bytes):
+        s = cfg["server"]
+        self.model = model_bytes
+        self.router = _native.ZmtpSocket(_native.SockType.ROUTER)
+        self.router.bind(f"tcp://127.0.0.1:{s['agent_listener']['port']}")
+        self.pull = _native.ZmtpSocket(_native.SockType.PULL)
+        self.pull.bind(f"tcp://127.0.0.1:{s['trajectory_server']['port']}")
+        self.push_addr = f"tcp://127.0.0.1:{s['training_server']['port']}"
+        self.transcript = []
+        self.frames = []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._serve, daemon=True)
+        self._t.start()
+
+    def _serve(self):
+        while not self._stop.is_set():
+            msg = self.router.recv(50)
+            if msg is not None:
+                peer, frames = msg
+                self.transcript.append(frames)
+                body = [f for f in frames if f]
+                if body == [b"GET_MODEL"]:
+                    self.router.send([peer, b"", self.model], 5000)
+                elif body == [b"MODEL_SET"]:
+                    self.router.send([peer, b"", b"ID_LOGGED"], 5000)
+            m = self.pull.recv(10)
+            if m is not None:
+                self.frames.extend(m[1])
+
+    def push_model(self, blob: bytes):
+        push = _native.ZmtpSocket(_native.SockType.PUSH)  # a new PUSH per update, like training_zmq.rs
+        push.connect(self.push_addr)
+        ok = push.send([blob], 5000)
+        time.sleep(0.2)
+        push.close()
+        return ok
+
+    def close(self):
+        self._stop.set()
+        self._t.join(5)
+        self.router.close()
+        self.pull.close()
+
+
+@pytest.mark.skipif(not os.path.exists(REF_PT), reason="reference checkout not mounted")
+def test_reference_wire_against_scripted_reference_server(tmp_path, monkeypatch):
+    monkeypatch.setenv("RRL_QUIET_CONFIG", "1")
+    cfg, path = _config(tmp_path)
+    srv = ScriptedReferenceServer(cfg, open(REF_PT, "rb").read())
+    agent = None
+    try:
+        agent = RelayRLAgent(config_path=path, server_type="zmq", wire_format="reference", seed=0)
+        # the handshake transcript is exactly the reference agent's (no format frame)
+        assert [[f for f in fr if f] for fr in srv.transcript] == [[b"GET_MODEL"], [b"MODEL_SET"]]
+        p = agent.policy
+        # the shipped client_model.pt is a PolicyWithoutBaseline (6 storages: W1 b1 W2 b2 W3 b3)
+        assert (p.obs_dim, p.act_dim, p.hidden) == (4, 2, 128) and p.vf is None
+        from relayrl_prototype_amd.utils.checkpoint import import_reference_weights
+
+        pi_ref, _ = import_reference_weights(REF_PT, 4, 2)
+        x = np.array([0.1, -0.2, 0.3, 0.05], np.float32)
+        np.testing.assert_allclose(np.asarray(p.logits(x)).reshape(-1), _logits(pi_ref, x), rtol=1e-5, atol=1e-5)
+        # one 5-step episode -> one serde_pickle(Vec<RelayRLAction>) frame
+        obs = np.array([0.01, -0.02, 0.03, 0.04], np.float32)
+        r = 0.0
+        for t in range(5):
+            agent.request_for_action(obs + t, np.ones(2, np.float32), r)
+            r = 1.0
+        agent.flag_last_action(1.0)
+        t0 = time.time()
+        while not srv.frames and time.time() - t0 < 10:
+            time.sleep(0.02)
+        assert len(srv.frames) == 1 and sp.is_pickle_frame(srv.frames[0])
+        raw = sp.loads(srv.frames[0])  # the reference learner's pickle::from_slice::<Vec<RelayRLAction>>
+        assert isinstance(raw, list) and len(raw) == 6
+        for a in raw[:5]:
+            assert set(a) >= {"obs", "act", "mask", "rew", "data", "done", "reward_updated"}
+            assert a["done"] is False and sp.enum_variant(a["data"]["logp_a"])[0] == "Tensor"
+            assert "v" not in a["data"]  # no value head in this model: PolicyWithoutBaseline's step() dict
+            assert isinstance(a["obs"]["data"], (bytes, list))  # TensorData = a safetensors file
+        last = raw[5]
+        assert last["done"] is True and last["obs"] is None and last["act"] is None and last["rew"] == 0.0
+        acts = sp.actions_from_reference(raw)
+        np.testing.assert_allclose(acts[2].get_obs().reshape(-1), obs + 2)
+        assert [a.get_rew() for a in acts[:5]] == [1.0] * 5  # each action carries its own step's reward
+        # a model update pushed into the agent's bound PULL is picked up and swapped in
+        blob, pi_new = _our_archive(7, with_vf=True)
+        v0 = agent.model_version
+        assert srv.push_model(blob)
+        t0 = time.time()
+        while agent.model_version == v0 and time.time() - t0 < 10:
+            time.sleep(0.02)
+        assert agent.model_version == v0 + 1
+        assert agent.policy.vf is not None  # PolicyWithBaseline archive: policy storages first, then baseline
+        np.testing.assert_allclose(np.asarray(agent.policy.logits(x)).reshape(-1), _logits(pi_new, x), rtol=1e-5,
+                                   atol=1e-5)
+        agent.request_for_action(obs, np.ones(2, np.float32), 0.0)
+        agent.flag_last_action(0.0)
+        t0 = time.time()
+        while len(srv.frames) < 2 and time.time() - t0 < 10:
+            time.sleep(0.02)
+        raw2 = sp.loads(srv.frames[1])
+        assert sp.enum_variant(raw2[0]["data"]["v"])[0] == "Tensor"  # the baseline learner reads data['v']
+    finally:
+        if agent is not None:
+            agent.close()
+        srv.close()
+
+
+def test_reference_wire_trains_against_our_server(tmp_path, monkeypatch):
+    """Our ZMQ training server speaks both dialects: a reference-wire agent's uploads train
+    the learner and the new models reach it through the PULL it binds."""
+    from relayrl_prototype_amd.api.server import TrainingServer
+
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("RRL_QUIET_CONFIG", "1")
+    cfg, path = _config(tmp_path, traj_per_epoch=3, train_vf_iters=2, with_vf_baseline=True)
+    srv = TrainingServer("REINFORCE", 4, 2, 100000, env_dir=str(tmp_path), config_path=path, server_type="zmq",
+                         device="cpu")
+    agent = None
+    try:
+        agent = RelayRLAgent(config_path=path, server_type="zmq", wire_format="reference", seed=1)
+        v0 = agent.model_version
+        env = _native.VecEnv("CartPole-v1", 1, 5, 1)
+        obs = np.zeros((1, 4), np.float32)
+        rew = np.zeros(1, np.float32)
+        done = np.zeros(1, np.float32)
+        act = np.zeros(1, np.int32)
+        env.reset_ptr(obs.ctypes.data)
+        for _ in range(6):
+            r = 0.0
+            while True:
+                a = agent.request_for_action(obs[0].copy(), np.ones(2, np.float32), r)
+                act[0] = int(np.asarray(a.get_act()).reshape(-1)[0])
+                env.step_ptr(act.ctypes.data, obs.ctypes.data, rew.ctypes.data, done.ctypes.data)
+                r = float(rew[0])
+                if done[0] > 0:
+                    agent.flag_last_action(r)
+                    break
+        srv.wait_idle(60)
+        assert srv.service.updates >= 2
+        t0 = time.time()
+        while agent.model_version <= v0 + 1 and time.time() - t0 < 20:
+            time.sleep(0.05)
+        assert agent.model_version >= v0 + 2  # pushed TorchScript archives reached the bound PULL
+    finally:
+        if agent is not None:
+            agent.close()
+        srv.close(save=False)
