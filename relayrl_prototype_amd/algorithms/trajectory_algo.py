@@ -125,6 +125,87 @@ class FlatBuffer:
         return out
 
 
+class EpisodeIngest:
+    """Uploaded trajectories -> FlatBuffer paths with the learner's per-episode semantics.
+
+    Shared by the trajectory learner (REINFORCE.receive_trajectory, REINFORCE.py:70-95) and the
+    device engines' agent-upload staging (runtime/engine.py).  Columnar RRLC uploads are split
+    at their done flags; per-action uploads (RRLT, protobuf, decoded reference serde_pickle
+    frames) follow the reference's terminal-marker convention (an action without obs whose
+    reward closes the episode, agent_zmq.rs:605-610).  Finished episodes accumulate in
+    ``finished`` as (return, length)."""
+
+    def __init__(self, buffer: FlatBuffer):
+        self.buffer = buffer
+        self.ep_ret = 0.0
+        self.ep_len = 0
+        self.steps = 0
+        self.finished = []
+
+    def end_episode(self, terminal: bool):
+        self.buffer.finish_path(terminal)
+        self.finished.append((self.ep_ret, self.ep_len))
+        self.ep_ret, self.ep_len = 0.0, 0
+
+    def pop_finished(self):
+        out, self.finished = self.finished, []
+        return out
+
+    def add(self, trajectory) -> None:
+        if isinstance(trajectory, TrajectoryColumns):
+            self._columns(trajectory)
+        else:
+            self._actions(trajectory)
+
+    def _columns(self, c) -> None:
+        buf = self.buffer
+        n = len(c)
+        ends = np.flatnonzero(c.done[:n]) + 1
+        start = 0
+        for stop in list(ends) + ([n] if (len(ends) == 0 or ends[-1] != n) else []):
+            k = buf.store_block(c.obs[start:stop], c.act[start:stop], None if c.mask is None else c.mask[start:stop],
+                                c.rew[start:stop], None if c.logp is None else c.logp[start:stop])
+            self.steps += k
+            self.ep_ret += float(c.rew[start:start + k].sum())
+            self.ep_len += k
+            if k < stop - start:  # buffer full: cut the path here
+                if buf.ptr > buf.path_start:
+                    buf.finish_path(terminal=False)
+                return
+            if c.done[stop - 1]:
+                self.end_episode(terminal=True)
+            elif buf.ptr > buf.path_start:
+                # cut segment: bootstrap with V(s_T) when the agent shipped s_T, else V(s_last)
+                buf.finish_path(terminal=False, boot_obs=getattr(c, "next_obs", None))
+            start = stop
+
+    def _actions(self, trajectory) -> None:
+        buf = self.buffer
+        last = None
+        for a in trajectory.get_actions():
+            obs = a.get_obs()
+            if obs is None:  # reference-style terminal marker: its reward closes the episode
+                if a.get_done():
+                    if buf.ptr > buf.path_start:
+                        buf.rew[buf.ptr - 1] += a.get_rew()
+                    self.ep_ret += a.get_rew()
+                    self.end_episode(terminal=True)
+                continue
+            if buf.full():
+                break
+            data = a.get_data()
+            logp = data.get("logp_a")
+            buf.store(obs, a.get_act(), a.get_mask(), a.get_rew(), logp)
+            self.steps += 1
+            self.ep_ret += a.get_rew()
+            self.ep_len += 1
+            last = a
+            if a.get_done():
+                self.end_episode(terminal=True)
+        if last is not None and not last.get_done() and buf.ptr > buf.path_start:
+            buf.finish_path(terminal=False)  # truncated segment: bootstrap from V(s_last)
+
+
 class TrajectoryAlgorithm(AlgorithmAbstract):
     ALGO = "reinforce"
     CONFIG_NAME = "REINFORCE"
@@ -154,6 +235,7 @@ class TrajectoryAlgorithm(AlgorithmAbstract):
         np.random.seed(self.seed % (2**32))
         self.save_model_path = cfg.get_server_model_path()
         self.buffer = FlatBuffer(self.obs_dim, self.act_dim, buf_size, self.discrete)
+        self._ingest = EpisodeIngest(self.buffer)
         self.learner = self._make_learner(params, hidden)
         exp = self.exp_name()
         self.logger = EpochLogger(**setup_logger_kwargs(exp, self.seed, data_dir=os.path.join(env_dir, "logs")),
@@ -164,8 +246,6 @@ class TrajectoryAlgorithm(AlgorithmAbstract):
         self.traj = 0
         self.epoch = 0
         self.version = 0
-        self._ep_ret = 0.0
-        self._ep_len = 0
         self._t_epoch = time.perf_counter()
         self._steps_epoch = 0
         self.last_metrics: Dict[str, Any] = {}
@@ -188,10 +268,8 @@ class TrajectoryAlgorithm(AlgorithmAbstract):
         """REINFORCE.receive_trajectory (REINFORCE.py:70-95) with per-episode semantics."""
         self.traj += 1
         buf = self.buffer
-        if isinstance(trajectory, TrajectoryColumns):
-            self._receive_columns(trajectory)
-        else:
-            self._receive_actions(trajectory)
+        self._ingest.add(trajectory)
+        self._ingested()
         if (self.traj % self.traj_per_epoch == 0) or buf.full():
             self.epoch += 1
             self.train_model()
@@ -199,58 +277,12 @@ class TrajectoryAlgorithm(AlgorithmAbstract):
             return True
         return False
 
-    def _receive_columns(self, c) -> None:
-        buf = self.buffer
-        n = len(c)
-        ends = np.flatnonzero(c.done[:n]) + 1
-        start = 0
-        for stop in list(ends) + ([n] if (len(ends) == 0 or ends[-1] != n) else []):
-            k = buf.store_block(c.obs[start:stop], c.act[start:stop], None if c.mask is None else c.mask[start:stop],
-                                c.rew[start:stop], None if c.logp is None else c.logp[start:stop])
-            self._steps_epoch += k
-            self._ep_ret += float(c.rew[start:start + k].sum())
-            self._ep_len += k
-            if k < stop - start:  # buffer full: cut the path here
-                if buf.ptr > buf.path_start:
-                    buf.finish_path(terminal=False)
-                return
-            if c.done[stop - 1]:
-                self._end_episode(terminal=True)
-            elif buf.ptr > buf.path_start:
-                # cut segment: bootstrap with V(s_T) when the agent shipped s_T, else V(s_last)
-                buf.finish_path(terminal=False, boot_obs=getattr(c, "next_obs", None))
-            start = stop
-
-    def _receive_actions(self, trajectory) -> None:
-        buf = self.buffer
-        last = None
-        for a in trajectory.get_actions():
-            obs = a.get_obs()
-            if obs is None:  # reference-style terminal marker: its reward closes the episode
-                if a.get_done():
-                    if buf.ptr > buf.path_start:
-                        buf.rew[buf.ptr - 1] += a.get_rew()
-                    self._ep_ret += a.get_rew()
-                    self._end_episode(terminal=True)
-                continue
-            data = a.get_data()
-            logp = data.get("logp_a")
-            buf.store(obs, a.get_act(), a.get_mask(), a.get_rew(), logp)
-            self._steps_epoch += 1
-            self._ep_ret += a.get_rew()
-            self._ep_len += 1
-            last = a
-            if a.get_done():
-                self._end_episode(terminal=True)
-            if buf.full():
-                break
-        if last is not None and not last.get_done() and buf.ptr > buf.path_start:
-            buf.finish_path(terminal=False)  # truncated segment: bootstrap from V(s_last)
-
-    def _end_episode(self, terminal: bool):
-        self.buffer.finish_path(terminal)
-        self.logger.store(EpRet=self._ep_ret, EpLen=self._ep_len)
-        self._ep_ret, self._ep_len = 0.0, 0
+    def _ingested(self) -> None:
+        """Per-episode logger rows and the epoch's step count from the ingest."""
+        for ret, ln in self._ingest.pop_finished():
+            self.logger.store(EpRet=ret, EpLen=ln)
+        self._steps_epoch += self._ingest.steps
+        self._ingest.steps = 0
 
     def train_model(self) -> None:
         d = self.buffer.take(self.device)

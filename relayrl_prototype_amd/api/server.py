@@ -62,7 +62,7 @@ class TrainingServer:
                                                        os.path.join(env_dir, "engine"), self.cfg.get_server_model_path())
         else:
             self.algorithm = eng.EngineAlgorithm(self.engine_spec, env_dir, self.cfg.get_server_model_path(),
-                                                 device=device)
+                                                 device=device, agent_buf_size=buf_size)
         self._ckpt = None
         if checkpoint_dir and checkpoint_every > 0:
             from ..utils.checkpoint import periodic_checkpointer

@@ -141,7 +141,7 @@ class EngineAlgorithm(AlgorithmAbstract):
     ``save`` / ``model_bytes`` = the TorchScript policy (kernel.py:87-143 interface)."""
 
     def __init__(self, spec: EngineSpec, env_dir: str = ".", save_model_path: Optional[str] = None, comm=None,
-                 device=None, log: bool = True):
+                 device=None, log: bool = True, agent_buf_size: int = 1 << 20):
         self.spec = spec
         if device is None and torch.cuda.is_available():
             device = torch.device("cuda", torch.cuda.current_device())
@@ -152,6 +152,26 @@ class EngineAlgorithm(AlgorithmAbstract):
         self.version = 0
         self.epoch = 0
         self.ignored_trajectories = 0
+        # Agent uploads (the reference's "agents upload -> learner trains on them",
+        # training_zmq.rs:994-1031 / REINFORCE.py:70-95): staged on the host as concatenated
+        # paths and folded into the NEXT engine epoch's batch as extra rows (their own scan and
+        # bootstraps, rollout_learn.RolloutLearner._fold).  For the single-process MLP engines
+        # (vec / host); "agent_rows": false in the "mi355x" block / hyperparams turns it off.
+        lr = self.learner
+        self.agent_rows = (bool(spec.trainer.get("agent_rows", True)) and spec.kind in ("vec", "host")
+                           and lr is not None and (self.comm is None or self.comm.world == 1)
+                           and hasattr(self.trainer, "rl"))
+        self.agent_rows_total = 0
+        self.agent_episodes = 0
+        self.agent_trajectories = 0
+        self._agent_returns = []
+        if self.agent_rows:
+            from ..algorithms.trajectory_algo import EpisodeIngest, FlatBuffer
+
+            self._stage = FlatBuffer(lr.obs_dim, lr.act_dim, int(spec.trainer.get("agent_rows_cap", agent_buf_size)),
+                                     lr.discrete)
+            self._ingest = EpisodeIngest(self._stage)
+            self._stage_lock = threading.Lock()
         self.seed = int(spec.trainer.get("seed", 0))
         self.logger = None
         if log and self.rank == 0:
@@ -206,17 +226,51 @@ class EngineAlgorithm(AlgorithmAbstract):
 
     # ------------------------------------------------------------------ plugin contract
     def receive_trajectory(self, trajectory) -> bool:
-        # the engine learns from its own device envs; agent uploads are counted, not trained on
-        self.ignored_trajectories += 1
+        """Stage an agent upload for the next engine epoch (LearnerService worker thread).  The
+        engine's own epochs publish the models, so this never reports an update."""
+        if not self.agent_rows:
+            self.ignored_trajectories += 1  # multi-rank / pixel engines train on their own envs only
+            return False
+        with self._stage_lock:
+            if self._stage.full():
+                self.ignored_trajectories += 1  # staging full until the next epoch drains it
+                return False
+            self._ingest.add(trajectory)
+            self.agent_trajectories += 1
         return False
 
+    def _take_agent_rows(self):
+        if not self.agent_rows:
+            return None
+        with self._stage_lock:
+            if self._stage.ptr == 0:
+                return None
+            if self._stage.ptr > self._stage.path_start:  # an open path: close it, bootstrapped
+                self._stage.finish_path(terminal=False)
+            dev = self.learner.device
+            d = self._stage.take(dev)
+            fin = self._ingest.pop_finished()
+        self.agent_episodes += len(fin)
+        self._agent_returns.extend(r for r, _ in fin)
+        return d
+
     def train_model(self) -> None:
+        d = self._take_agent_rows()
+        if d is not None:
+            self.trainer.rl.pending_rows = d
         _epoch(self.trainer)
+        if d is not None:
+            self.agent_rows_total += int(self.trainer.rl.last_agent_rows)
         self.epoch += 1
         self.version += 1
 
     def epoch_metrics(self) -> Dict[str, Any]:
         m = self.trainer.metrics() or {}
+        if self.agent_rows:
+            m["AgentRows"] = int(getattr(self.trainer.rl, "last_agent_rows", 0))
+            rets, self._agent_returns = self._agent_returns, []
+            m["AgentEpisodes"] = len(rets)
+            m["AgentEpRet"] = sum(rets) / len(rets) if rets else float("nan")
         self.last_metrics = m
         return m
 
@@ -236,6 +290,9 @@ class EngineAlgorithm(AlgorithmAbstract):
                 lg.log_tabular(k, float(vv.get(k, nan)))
         lg.log_tabular("KL", float(m.get("KL", nan)))
         lg.log_tabular("Entropy", float(m.get("Entropy", nan)))
+        if self.agent_rows:  # uploads folded into this epoch's batch (and their episodes' mean return)
+            lg.log_tabular("AgentRows", float(m.get("AgentRows", 0)))
+            lg.log_tabular("AgentEpRet", float(m.get("AgentEpRet", nan)))
         for k, v in (extra or {}).items():
             lg.log_tabular(k, float(v))
         lg.dump_tabular()

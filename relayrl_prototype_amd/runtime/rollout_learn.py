@@ -7,7 +7,7 @@ from typing import Optional
 import torch
 
 from ..algorithms.learner import PGLearner
-from ..ops import FwdMode, gae_scan_tm, mlp_forward
+from ..ops import FwdMode, gae_scan_tm, mlp_forward, scan_flat
 from ..parallel.comm import Comm
 from ..utils.tracing import PhaseTimer
 
@@ -34,6 +34,9 @@ class RolloutLearner:
         self.ret = torch.zeros(shape, device=dev)
         self.adv_stats = torch.zeros(3, device=dev)
         self.stats_part = None
+        # agent uploads folded into the next batch (runtime/engine.py): a FlatBuffer.take() dict
+        self.pending_rows = None
+        self.last_agent_rows = 0
         if dev.type == "cuda":
             from ..ops import hip
 
@@ -72,14 +75,71 @@ class RolloutLearner:
                 self.ret.view(-1).copy_(ret.reshape(-1))
                 self.adv_stats.copy_(stats)
             self.comm.all_reduce_sum_(self.adv_stats)
-        inv_B = 1.0 / (B * self.comm.world)
         discrete = lr.discrete
         a = act.reshape(B) if discrete else None
         ac = None if discrete else act.reshape(B, -1)
         m = None if mask is None else mask.reshape(B, -1)
-        with tm.phase("Optimize"):
-            lr.optimize(obs_b, act=a, actc=ac, mask=m, adv=self.adv.view(-1), ret=self.ret.view(-1),
-                        adv_stats=self.adv_stats, logp_old=logp.reshape(-1), inv_B=inv_B)
+        adv_b, ret_b, logp_b = self.adv.view(-1), self.ret.view(-1), logp.reshape(-1)
+        extra, self.pending_rows = self.pending_rows, None
+        self.last_agent_rows = 0
+        if extra is not None and extra["obs"].shape[0] > 0:
+            with tm.phase("AgentRows"):
+                obs_b, a, ac, m, adv_b, ret_b, logp_b = self._fold(extra, obs_b, a, ac, m, adv_b, ret_b, logp_b)
+            B = obs_b.shape[0]
+        inv_B = 1.0 / (B * self.comm.world)
+        graphs = lr.vloop.use_graph if lr.vloop is not None else False
+        if self.last_agent_rows and lr.vloop is not None:
+            lr.vloop.use_graph = False  # a new batch shape every epoch: no graph capture
+        try:
+            with tm.phase("Optimize"):
+                lr.optimize(obs_b, act=a, actc=ac, mask=m, adv=adv_b, ret=ret_b, adv_stats=self.adv_stats,
+                            logp_old=logp_b, inv_B=inv_B)
+        finally:
+            if lr.vloop is not None:
+                lr.vloop.use_graph = graphs
+
+    def _fold(self, d, obs_b, a, ac, m, adv_b, ret_b, logp_b):
+        """Agent uploads (concatenated paths, FlatBuffer.take) appended to the device batch as
+        extra rows: their own flat segmented scan (finish_path semantics, REINFORCE.py:70-95 /
+        replay_buffer.py:48-79) with V(s) from the current value net and V(s_T) bootstraps for
+        cut paths, their advantage sums added to the batch statistics, then one concatenated
+        batch for the policy and value steps."""
+        lr = self.learner
+        H = lr.hidden
+        n = d["obs"].shape[0]
+        obs_e = d["obs"].to(obs_b.device)
+        boot = d["boot"]
+        val = None
+        if lr.vf is not None:
+            val = mlp_forward(FwdMode.VALUE, lr.vf.params, obs_e, 1, H)["v"]
+            boot = torch.where(torch.isnan(boot), val, boot)  # cut path without s_T: V(s_last)
+            bi = d["boot_idx"]
+            if bi.numel():
+                vb = mlp_forward(FwdMode.VALUE, lr.vf.params, d["boot_obs"], 1, H)["v"]
+                boot = boot.index_copy(0, bi.to(boot.device), vb.to(boot.dtype))
+        else:
+            boot = torch.nan_to_num(boot, nan=0.0)
+        adv_e, ret_e, st_e = scan_flat(d["rew"], d["done"], val, boot, self.gamma, self.lam)
+        self.adv_stats.add_(st_e.to(self.adv_stats.device))
+        if d["has_logp"]:
+            logp_e = d["logp"]
+        else:  # uploads without log-probs: the current policy's (PPO ratio 1 on those rows)
+            mode = FwdMode.CAT_EVAL if lr.discrete else FwdMode.GAUSS_EVAL
+            logp_e = mlp_forward(mode, lr.pi.params, obs_e, lr.act_dim, H, mask=d["mask"],
+                                 act_in=d["act"] if lr.discrete else None,
+                                 actc_in=None if lr.discrete else d["act"])["logp"]
+        cat = torch.cat
+        obs_c = cat([obs_b, obs_e])
+        if lr.discrete:
+            a = cat([a, d["act"].to(a.dtype)])
+        else:
+            ac = cat([ac, d["act"].reshape(n, -1)])
+        mask_e = d["mask"]
+        if m is not None or (lr.discrete and not bool((mask_e == 1).all())):
+            m_b = m if m is not None else torch.ones(obs_b.shape[0], lr.act_dim, device=obs_b.device)
+            m = cat([m_b, mask_e])
+        self.last_agent_rows = n
+        return obs_c, a, ac, m, cat([adv_b, adv_e]), cat([ret_b, ret_e]), cat([logp_b, logp_e.reshape(-1)])
 
 
 def episode_metrics(comm: Comm, n, s, sq, mx, mn, sum_len) -> dict:

@@ -82,11 +82,20 @@ def test_training_server_host_engine_cpu(cfgdir):
         for c in REF_COLS:
             assert c in header, c
         cols = read_progress(str(prog[0]))
-        assert cols["Epoch"] == [1.0, 2.0, 3.0]
-        # agent uploads are accepted but the engine trains on its own envs
+        assert cols["Epoch"] == [1.0, 2.0, 3.0] and cols["AgentRows"] == [0.0, 0.0, 0.0]
+        # agent uploads are staged and folded into the NEXT engine epoch as extra rows
+        for t in range(4):
+            agent.request_for_action(np.full(4, 0.01 * t, np.float32), None, 1.0)
         agent.flag_last_action(1.0)
         assert srv.wait_idle(10)
-        assert srv.algorithm.ignored_trajectories == 1
+        assert srv.algorithm.agent_trajectories == 1 and srv.algorithm.ignored_trajectories == 0
+        srv.train(epochs=1)
+        rl = srv.algorithm.trainer.rl
+        assert rl.last_agent_rows == 5  # the episode's 5 actions (the first one acted above)
+        lr = srv.algorithm.learner
+        assert int(lr.vloop.loss_last[:, 5].sum().item()) == 16 * 16 + 5  # the value loss counted them
+        cols = read_progress(str(prog[0]))
+        assert cols["AgentRows"][-1] == 5.0 and cols["AgentEpRet"][-1] == 5.0
         with pytest.raises(RuntimeError):
             TrainingServer("REINFORCE", 4, 2, 1000, env_dir=str(tmp / "env2"), config_path=cfgp,
                            server_type="local", training_port=str(free_port()), device="cpu").train(epochs=1)

@@ -59,3 +59,56 @@ def test_vec_engine_trains_cartpole_to_threshold(cuda, tmp_path, monkeypatch):
         agent.close()
     finally:
         srv.close(save=False)
+
+
+def test_vec_engine_folds_agent_uploads_into_the_batch(cuda, tmp_path, monkeypatch):
+    """an attached agent's episodes enter the engine's next batch as extra
+    rows -- the row count, the value-loss count and the progress.txt column include them."""
+    from relayrl_prototype_amd import _native
+    from relayrl_prototype_amd.api.agent import RelayRLAgent
+    from relayrl_prototype_amd.api.server import TrainingServer
+
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("RRL_QUIET_CONFIG", "1")
+    cfg = json.loads(DEFAULT_CONFIG_CONTENT)
+    for k in ("training_server", "trajectory_server", "agent_listener"):
+        cfg["server"][k]["port"] = str(free_port())
+    cfg["mi355x"] = {"engine": "vec", "envs_per_actor": 512, "rollout_len": 16}
+    p = tmp_path / "relayrl_config.json"
+    p.write_text(json.dumps(cfg))
+    hp = {"with_vf_baseline": True, "train_vf_iters": 3, "seed": 2}
+    srv = TrainingServer("REINFORCE", 4, 2, 100000, env_dir=str(tmp_path / "env"), config_path=str(p),
+                         server_type="local", hyperparams=hp)
+    try:
+        agent = RelayRLAgent(config_path=str(p), server_type="local", handshake_timeout_s=30)
+        srv.train(epochs=1)
+        env = _native.VecEnv("CartPole-v1", 1, 9, 1)
+        obs = np.zeros((1, 4), np.float32)
+        rew = np.zeros(1, np.float32)
+        done = np.zeros(1, np.float32)
+        act = np.zeros(1, np.int32)
+        env.reset_ptr(obs.ctypes.data)
+        rows = 0
+        for _ in range(3):
+            r = 0.0
+            while True:
+                a = agent.request_for_action(obs[0].copy(), np.ones(2, np.float32), r)
+                act[0] = int(np.asarray(a.get_act()).reshape(-1)[0])
+                env.step_ptr(act.ctypes.data, obs.ctypes.data, rew.ctypes.data, done.ctypes.data)
+                r = float(rew[0])
+                rows += 1
+                if done[0] > 0:
+                    agent.flag_last_action(r)
+                    break
+        assert srv.wait_idle(10)
+        res = srv.train(epochs=1)
+        algo = srv.algorithm
+        assert algo.trainer.rl.last_agent_rows == rows and algo.agent_rows_total == rows
+        ls = algo.learner.vloop.loss_last
+        assert int(ls[:, 5].sum().item()) == 512 * 16 + rows
+        assert res.metrics["AgentRows"] == rows and res.metrics["AgentEpisodes"] == 3
+        prog = list((tmp_path / "env" / "logs").rglob("progress.txt"))
+        assert read_progress(str(prog[0]))["AgentRows"] == [0.0, float(rows)]
+        agent.close()
+    finally:
+        srv.close(save=False)
