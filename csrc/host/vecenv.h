@@ -98,6 +98,7 @@ class VecEnv {
   std::string name_;
   int n_, obs_dim_, act_dim_, max_steps_;
   bool continuous_;
+  bool batch_hc_ = false;  // HalfCheetahSynth: 8 envs per vectorised physics pass
   std::vector<std::unique_ptr<Env>> envs_;
   std::vector<Rng> rngs_;
   std::vector<int> len_;
