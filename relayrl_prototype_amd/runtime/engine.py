@@ -380,6 +380,11 @@ class EngineRunner:
                     extra = {"Time": el}
                     if "EnvSteps" in m and el > 0:
                         extra["EnvStepsPerSec"] = (m["EnvSteps"] - steps0) / el
+                    # the threshold metric as progress columns, on every row (the
+                    # table's columns are fixed by its first row): the mean return of the newest
+                    # >= window episodes, and the TTT once it is reached (NaN before / unchecked)
+                    extra["WindowRet"] = win
+                    extra["TimeToThreshold"] = ttt if solved else float("nan")
                     algo.log_epoch(m, extra)
                 if publish_every and k % publish_every == 0:
                     self._publish()

@@ -117,6 +117,13 @@ def test_training_server_engine_from_config_block(cfgdir):
         assert srv.engine_spec.kind == "host" and srv.engine_spec.trainer["num_envs"] == 8
         res = srv.train(epochs=2, log_every=2, publish_every=2)
         assert res.epochs == 2 and srv.model_version == 2
+        # the threshold metric as progress columns: NaN until reached, then the TTT itself
+        res = srv.train(epochs=30, target_return=1.0, window=1)
+        assert res.solved and res.time_to_threshold_s is not None
+        cols = read_progress(str(next((tmp / "env" / "logs").rglob("progress.txt"))))
+        ttt = cols["TimeToThreshold"]
+        assert ttt[-1] == pytest.approx(res.time_to_threshold_s, rel=1e-3)
+        assert all(v != v for v in ttt[:-1]) and cols["WindowRet"][-1] >= 1.0
     finally:
         srv.close(save=False)
 
