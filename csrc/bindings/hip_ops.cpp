@@ -403,6 +403,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "relayrl_prototype_amd gfx950 HIP kernels";
   m.def("num_cus", &num_cus);
   m.def("device_cus", &device_cus);
+  m.def("relax_thread_capture_mode", []() {
+    // hipThreadExchangeStreamCaptureMode(relaxed) for the calling thread, for good: a helper
+    // thread's event waits then leave other threads' graph captures alone
+    hipStreamCaptureMode m = hipStreamCaptureModeRelaxed;
+    return (int)hipThreadExchangeStreamCaptureMode(&m);
+  });
   m.def("set_cu_limit", &set_cu_limit, "size grids for n CUs (0 = all); returns the previous limit");
   m.def("cu_masked_stream", &cu_masked_stream);
   m.def("destroy_stream", &destroy_stream);

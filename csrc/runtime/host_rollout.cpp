@@ -48,6 +48,13 @@ hipError_t spin(hipEvent_t ev, bool backoff) {
   }
 }
 
+// Scoped hipThreadExchangeStreamCaptureMode(relaxed) for the calling thread.
+struct RelaxedCapture {
+  hipStreamCaptureMode prev = hipStreamCaptureModeRelaxed;
+  RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&prev); }
+  ~RelaxedCapture() { (void)hipThreadExchangeStreamCaptureMode(&prev); }
+};
+
 }  // namespace
 
 HostRollout::HostRollout(std::vector<VecEnv*> envs, std::vector<int> bounds, int num_cu)
@@ -78,6 +85,10 @@ HostRollout::~HostRollout() {
 int HostRollout::run(const float* params, int H, int T, const RolloutBuffers& b, uint64_t seed, uint64_t step0,
                      hipStream_t s) {
   const auto t_run = Clock::now();
+  // This thread's event polls must not touch another thread's graph capture: the overlapped
+  // learner captures its value loop while a rollout runs, and HIP invalidates every active
+  // capture when a thread in the default (global) mode calls a synchronising API.
+  RelaxedCapture relaxed;
   const int N = bounds_.back(), D = D_, A = A_;
   const int halves = (int)envs_.size();
   const size_t act_w = cont_ ? (size_t)A : 1;  // action elements per env

@@ -371,6 +371,11 @@ class HostVecTrainer:
         def run():
             try:
                 torch.cuda.set_device(self.device)
+                # this thread's event waits must not invalidate the learner's graph capture
+                # (HIP drops every active capture when a default-mode thread synchronises)
+                from ..ops import hip
+
+                hip().relax_thread_capture_mode()
                 with torch.cuda.stream(self.actor_stream):
                     self.actor_stream.wait_event(snap)
                     t0 = time.perf_counter()
