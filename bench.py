@@ -87,6 +87,8 @@ def parse(argv=None):
     ap.add_argument("--al-num-envs", type=int, default=2048)
     ap.add_argument("--al-rollout-len", type=int, default=128)
     ap.add_argument("--al-vf-iters", type=int, default=80)
+    ap.add_argument("--al-deadline-s", type=float, default=150.0,
+                    help="wall-clock bound of the secondary actor-learner phase (then: recorded as failed)")
     return ap.parse_args(argv)
 
 
@@ -329,6 +331,27 @@ def actor_learner_probe(args, comm, on_gpu: bool) -> dict:
     return rec
 
 
+def _arm_deadline(seconds: float, rank: int, emit):
+    """Timer thread: after ``seconds`` rank 0 runs ``emit`` (prints the JSON line) and every
+    rank leaves with status 0 -- a rank blocked inside a collective cannot be unwound, and
+    each rank's own timer fires, so torchrun sees the whole group exit."""
+    import threading
+
+    def fire():
+        try:
+            if rank == 0:
+                emit()
+        finally:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 # ---------------------------------------------------------------------- main
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -392,26 +415,8 @@ def main(argv=None):
     per_rank_ms = comm.all_gather_object(round(dt_local / args.steps * 1e3, 3))
     phases = phase_probe(tr, comm, args.phase_steps) if args.phase_steps > 0 else None
     host_rec = host_path_probe(args.host_steps, comm) if (on_gpu and world == 1 and args.host_steps > 0) else None
-    al_rec = None
-    if args.actor_learner == "on" or (args.actor_learner == "auto" and world > 1):
-        al_rec = actor_learner_probe(args, comm, on_gpu)
-    ttt = ttt_ref = None
-    do_ttt = on_gpu and (args.ttt or world == 1) and not args.no_ttt
-    if do_ttt:
-        del tr
-        torch.cuda.empty_cache()
-        tuned = {"with_vf_baseline": True, "train_vf_iters": args.ttt_vf_iters, "pi_lr": args.ttt_pi_lr,
-                 "vf_lr": args.ttt_vf_lr, "gamma": 0.99, "lam": 0.95}
-        ref_hp = {"with_vf_baseline": True, "train_vf_iters": 80, "pi_lr": 3e-4, "vf_lr": 1e-3, "gamma": 0.98,
-                  "lam": 0.97}
-        shape = {"num_envs": args.ttt_envs, "rollout_len": args.ttt_rollout_len}
-        ttt = time_to_threshold(tuned, dict(shape, use_graphs=bool(args.ttt_graphs)), args.ttt_seeds,
-                                args.ttt_max_s, comm)
-        ref_shape = {"num_envs": args.ttt_ref_envs, "rollout_len": args.ttt_ref_rollout_len}
-        ttt_ref = time_to_threshold(ref_hp, dict(ref_shape, use_graphs=True), args.ttt_ref_seeds, args.ttt_max_s,
-                                    comm)
-    ref_cpu = collect_reference_cpu(ref_proc, args.ref_cpu_seconds)
-    if rank == 0:
+    def record(al_rec, ttt=None, ttt_ref=None, ref_cpu=None, do_ttt=False):
+        """The ONE JSON line (rank 0)."""
         algo = "REINFORCE" if args.no_baseline else "REINFORCE-with-baseline"
         rec = {
             "metric": METRIC,
@@ -481,7 +486,37 @@ def main(argv=None):
                 "criterion": "same (newest >= 100 episodes >= 475), reference hyperparameters, batch-1 per-step "
                              "TorchScript pipeline on one CPU thread, measured concurrently in this run",
                 "source": "benchmarks/reference_equivalent_cpu.py"}
-        print(json.dumps(rec), flush=True)
+        return rec
+
+    al_rec = None
+    if args.actor_learner == "on" or (args.actor_learner == "auto" and world > 1):
+        # a hung RCCL transfer in the secondary phase must not cost the headline: past the
+        # deadline rank 0 prints the line with the phase marked failed and every rank exits
+        guard = _arm_deadline(args.al_deadline_s, rank, lambda: print(json.dumps(record(
+            {"error": f"deadline: actor-learner phase did not finish within {args.al_deadline_s} s"})),
+            flush=True))
+        try:
+            al_rec = actor_learner_probe(args, comm, on_gpu)
+        finally:
+            guard.cancel()
+    ttt = ttt_ref = None
+    do_ttt = on_gpu and (args.ttt or world == 1) and not args.no_ttt
+    if do_ttt:
+        del tr
+        torch.cuda.empty_cache()
+        tuned = {"with_vf_baseline": True, "train_vf_iters": args.ttt_vf_iters, "pi_lr": args.ttt_pi_lr,
+                 "vf_lr": args.ttt_vf_lr, "gamma": 0.99, "lam": 0.95}
+        ref_hp = {"with_vf_baseline": True, "train_vf_iters": 80, "pi_lr": 3e-4, "vf_lr": 1e-3, "gamma": 0.98,
+                  "lam": 0.97}
+        shape = {"num_envs": args.ttt_envs, "rollout_len": args.ttt_rollout_len}
+        ttt = time_to_threshold(tuned, dict(shape, use_graphs=bool(args.ttt_graphs)), args.ttt_seeds,
+                                args.ttt_max_s, comm)
+        ref_shape = {"num_envs": args.ttt_ref_envs, "rollout_len": args.ttt_ref_rollout_len}
+        ttt_ref = time_to_threshold(ref_hp, dict(ref_shape, use_graphs=True), args.ttt_ref_seeds, args.ttt_max_s,
+                                    comm)
+    ref_cpu = collect_reference_cpu(ref_proc, args.ref_cpu_seconds)
+    if rank == 0:
+        print(json.dumps(record(al_rec, ttt, ttt_ref, ref_cpu, do_ttt)), flush=True)
     if comm.world > 1:
         import torch.distributed as dist
 

@@ -78,6 +78,10 @@ class ValueLoop:
         self._key = None
         self.loss_first = None
         self.loss_last = None
+        # called before a graph capture starts: a trainer whose helper thread issues HIP calls
+        # (host_trainer's overlapped rollout) quiesces it here -- HIP invalidates a capture when
+        # another thread synchronises on the device meanwhile, whatever that thread's mode
+        self.before_capture = None
 
     def _body(self, obs, ret, iters, inv_B, slab, ls_first, ls_last):
         H = self.net.spec.H
@@ -136,6 +140,8 @@ class ValueLoop:
         if g is None:
             if len(self._graphs) >= 4:
                 self._graphs.clear()
+            if self.before_capture is not None:
+                self.before_capture()
             # Warm up once eagerly (kernel attributes, allocator) on the real buffers,
             # then restore the optimiser state so the warm-up step leaves no trace.
             saved = [t.clone() for t in (self.net.params, self.net.m, self.net.v, self.net.step)]

@@ -155,6 +155,8 @@ class HostVecTrainer:
         self.snapshot_versions = []  # policy version each overlapped rollout acted with
         self._primed = False  # a completed rollout waits in self.bufs[self.cur]
         self._rollout_error = None
+        if self.overlap and self.learner.vloop is not None:
+            self.learner.vloop.before_capture = self._quiesce_rollout
         # first observation
         for h, env in enumerate(self.envs):
             env.reset_ptr(self.bufs[0].h_obs[0, bounds[h]].data_ptr())
@@ -387,6 +389,14 @@ class HostVecTrainer:
         th = threading.Thread(target=run, name="relayrl-host-rollout", daemon=True)
         th.start()
         self._pending = (th, idx)
+
+    def _quiesce_rollout(self):
+        """Let the rollout running ahead finish before the learner captures a graph (first
+        epoch on each buffer set only); ``_join_ahead`` still consumes it afterwards."""
+        if self._pending is not None:
+            t0 = time.perf_counter()
+            self._pending[0].join()
+            self.timings["wait_rollout_s"] += time.perf_counter() - t0
 
     def _join_ahead(self) -> int:
         th, idx = self._pending

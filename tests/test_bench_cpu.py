@@ -48,3 +48,17 @@ def test_bench_spawns_ranks_without_torchrun():
 def test_bench_rejects_world_size_mismatch():
     r = _run(["--gpus", "2", "--device", "cpu"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_bench_actor_learner_deadline_keeps_the_headline():
+    """A secondary phase that overruns its deadline (a hung transfer) still yields ONE JSON line
+    with the headline, the phase marked failed, and exit status 0 on every rank."""
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "1", "--device", "cpu", "--num-envs", "16",
+              "--rollout-len", "8", "--vf-iters", "2", "--phase-steps", "0", "--al-steps", "100000",
+              "--al-deadline-s", "3"], {"RRL_DIST_BACKEND": "gloo"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["value"] > 0 and rec["n_gpus"] == 2
+    assert rec["actor_learner"]["error"].startswith("deadline")
