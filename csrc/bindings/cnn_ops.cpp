@@ -39,6 +39,13 @@ int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, flo
                   float* ep_acc, int N, unsigned long long seed, unsigned long long step,
                   const unsigned long long* step_base, int max_steps, int reset_all, void* stream);
 int rrl_pong_render(const float* state, uint8_t* obs, int N, void* stream);
+int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
+                       const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2, uint16_t* y3, int N,
+                       int max_grid, void* stream);
+int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
+                  float* bias_part, int N, int grid, void* stream);
+int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
+                  float* bias_part, int N, int grid, void* stream);
 }
 
 namespace {
@@ -91,6 +98,65 @@ void conv_fwd(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& y
   rc_check(rrl_conv_fwd(x.data_ptr(), u8, bf(w), b.data_ptr<float>(), bf(y), N, H, W, C, KH, KW, S, Cout, relu, wk,
                         wn, stream()),
            "conv_fwd");
+}
+
+// Fused Nature-CNN conv stack (cnn_fused.hip): uint8 s2d frames [N][21][21][64] ->
+// a1 [N][20][20][32], a2 [N][9][9][64], a3 [N][7][7][64] (bf16, post-ReLU).
+void conv_stack_fwd(const Tensor& x, const Tensor& w1, const Tensor& b1, const Tensor& w2, const Tensor& b2,
+                    const Tensor& w3, const Tensor& b3, const Tensor& y1, const Tensor& y2, const Tensor& y3,
+                    int64_t N, int64_t probe, int64_t grid) {
+  TORCH_CHECK(N > 0, "conv_stack_fwd: N must be positive");
+  check(x, "x", at::kByte, N * 21 * 21 * 64);
+  check(w1, "w1", at::kBFloat16, 32 * 256);
+  check(w2, "w2", at::kBFloat16, 64 * 512);
+  check(w3, "w3", at::kBFloat16, 64 * 576);
+  check(b1, "b1", at::kFloat, 32);
+  check(b2, "b2", at::kFloat, 64);
+  check(b3, "b3", at::kFloat, 64);
+  check(y1, "y1", at::kBFloat16, N * 400 * 32);
+  check(y2, "y2", at::kBFloat16, N * 81 * 64);
+  check(y3, "y3", at::kBFloat16, N * 49 * 64);
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  rc_check(rrl_conv_stack_fwd(x.data_ptr<uint8_t>(), bf(w1), b1.data_ptr<float>(), bf(w2), b2.data_ptr<float>(),
+                              bf(w3), b3.data_ptr<float>(), bf(y1), bf(y2), bf(y3), (int)N,
+                              probe > 0 ? -(int)((probe << 16) | (grid > 0 ? grid : cus))
+                                        : (grid > 0 ? (int)grid : cus),
+                              stream()),
+           "conv_stack_fwd");
+}
+
+// Fused conv3 backward (cnn_fused.hip): da3 [N][49][64], W3 [64][3][3][64], a2 [N][81][64] ->
+// da2 = dgrad * (a2 > 0), dW3 partials [grid][64 * 576], db3 partials [grid * 8][64].
+void conv3_bwd(const Tensor& dy, const Tensor& w, const Tensor& xact, const Tensor& dx, const Tensor& part,
+               const Tensor& bias_part, int64_t N, int64_t grid) {
+  TORCH_CHECK(N > 0 && grid > 0 && grid <= N, "conv3_bwd: need 0 < grid <= N");
+  check(dy, "dy", at::kBFloat16, N * 49 * 64);
+  check(w, "w", at::kBFloat16, 64 * 576);
+  check(xact, "xact", at::kBFloat16, N * 81 * 64);
+  check(dx, "dx", at::kBFloat16, N * 81 * 64);
+  check(part, "part", at::kFloat, grid * 64 * 576);
+  check(bias_part, "bias_part", at::kFloat, grid * 512);
+  rc_check(rrl_conv3_bwd(bf(dy), bf(w), bf(xact), bf(dx), part.data_ptr<float>(), bias_part.data_ptr<float>(),
+                         (int)N, (int)grid, stream()),
+           "conv3_bwd");
+}
+
+// Fused conv2 backward (cnn_fused.hip): da2 [N][81][64], W2 [64][4][4][32], a1 [N][400][32] ->
+// da1 = dgrad * (a1 > 0), dW2 partials [grid][64 * 512], db2 partials [grid * 8][64].
+void conv2_bwd(const Tensor& dy, const Tensor& w, const Tensor& xact, const Tensor& dx, const Tensor& part,
+               const Tensor& bias_part, int64_t N, int64_t grid) {
+  TORCH_CHECK(N > 0 && grid > 0 && grid <= N, "conv2_bwd: need 0 < grid <= N");
+  check(dy, "dy", at::kBFloat16, N * 81 * 64);
+  check(w, "w", at::kBFloat16, 64 * 512);
+  check(xact, "xact", at::kBFloat16, N * 400 * 32);
+  check(dx, "dx", at::kBFloat16, N * 400 * 32);
+  check(part, "part", at::kFloat, grid * 64 * 512);
+  check(bias_part, "bias_part", at::kFloat, grid * 512);
+  rc_check(rrl_conv2_bwd(bf(dy), bf(w), bf(xact), bf(dx), part.data_ptr<float>(), bias_part.data_ptr<float>(),
+                         (int)N, (int)grid, stream()),
+           "conv2_bwd");
 }
 
 void gemm_dgrad(const Tensor& dy, const Tensor& w, const OptT& mask, const Tensor& out, int64_t M, int64_t Cout,
@@ -276,6 +342,12 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("KW"), pybind11::arg("S"), pybind11::arg("Cout"), pybind11::arg("relu"),
         pybind11::arg("work") = pybind11::none());
   m.def("gemm_dgrad", &gemm_dgrad);
+  m.def("conv_stack_fwd", &conv_stack_fwd, pybind11::arg("x"), pybind11::arg("w1"), pybind11::arg("b1"),
+        pybind11::arg("w2"), pybind11::arg("b2"), pybind11::arg("w3"), pybind11::arg("b3"), pybind11::arg("y1"),
+        pybind11::arg("y2"), pybind11::arg("y3"), pybind11::arg("N"), pybind11::arg("probe") = 0,
+        pybind11::arg("grid") = 0);
+  m.def("conv3_bwd", &conv3_bwd);
+  m.def("conv2_bwd", &conv2_bwd);
   m.def("col2im_mask", &col2im_mask);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("gemm_splits", &gemm_splits);

@@ -883,32 +883,51 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_kernel(const uint16_t* __r
       rm[k] = q < XC ? xa[q] : make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
-    // class GEMM: 7 tiles of 16 pixels (a, b) = (p / 10, p % 10), p < 100
+    // class GEMM: 7 tiles of 16 pixels (a, b) = (p / 10, p % 10), p < 100, in two batches of
+    // 4 and 3 tiles.  k-step outer, tiles inner: 8 / 6 independent accumulators per k-step
+    // with their fragment reads batched ahead (a tile-outer loop chained 8 dependent MFMAs
+    // per accumulator); all 7 tiles at once spilled
+    auto class_tiles = [&](auto tag) {
+      constexpr int T0 = decltype(tag)::value, NT = T0 == 0 ? 4 : 3;
+      f32x4_t acc0[NT], acc1[NT];
+      int rb[NT];
 #pragma unroll
-    for (int mt = 0; mt < 7; ++mt) {
-      f32x4_t acc0 = f32x4_t{0.f, 0.f, 0.f, 0.f}, acc1 = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      const int p = 16 * mt + i16;
-      const int pc = p < 100 ? p : 0;  // rows past the class are computed and discarded
-      const int a = pc / 10, b = pc - a * 10;
+      for (int u = 0; u < NT; ++u) {
+        acc0[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        acc1[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        const int p = 16 * (T0 + u) + i16;
+        const int pc = p < 100 ? p : 0;  // rows past the class are computed and discarded
+        const int a = pc / 10, b = pc - a * 10;
+        rb[u] = (a + 1) * 11 + (b + 1);
+      }
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
         const int t = ks >> 1, ti = t >> 1, tj = t & 1;
-        const int row = (a - ti + 1) * 11 + (b - tj + 1);
-        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(Yi + row * kD2Ld + (ks & 1) * 32 + 8 * g);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[ks][0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[ks][1], acc1, 0, 0, 0);
-      }
+        const int off = -(ti * 11 + tj) * kD2Ld + (ks & 1) * 32 + 8 * g;
+        bf16x8_t af[NT];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int q = 16 * mt + 4 * g + r;
-        if (q < 100) {
-          const int aa = q / 10, bb = q - aa * 10;
-          const int pix = (ph + 2 * aa) * 20 + pw + 2 * bb;
-          O[pix * kD2OutLd + i16] = f2bf(acc0[r]);
-          O[pix * kD2OutLd + 16 + i16] = f2bf(acc1[r]);
+        for (int u = 0; u < NT; ++u) af[u] = *reinterpret_cast<const bf16x8_t*>(Yi + rb[u] * kD2Ld + off);
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          acc0[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u], wf[ks][0], acc0[u], 0, 0, 0);
+          acc1[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u], wf[ks][1], acc1[u], 0, 0, 0);
         }
       }
-    }
+#pragma unroll
+      for (int u = 0; u < NT; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = 16 * (T0 + u) + 4 * g + r;
+          if (q < 100) {
+            const int aa = q / 10, bb = q - aa * 10;
+            const int pix = (ph + 2 * aa) * 20 + pw + 2 * bb;
+            O[pix * kD2OutLd + i16] = f2bf(acc0[u][r]);
+            O[pix * kD2OutLd + 16 + i16] = f2bf(acc1[u][r]);
+          }
+        }
+    };
+    class_tiles(std::integral_constant<int, 0>{});
+    class_tiles(std::integral_constant<int, 4>{});
     __syncthreads();
     uint4* xd = reinterpret_cast<uint4*>(dx + (size_t)n * 400 * 32);
 #pragma unroll
@@ -1088,24 +1107,35 @@ __global__ __launch_bounds__(256, 2) void conv3_dgrad_kernel(const uint16_t* __r
       rm[k] = q < XC ? xa[q] : make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
+    // k-step outer, 6 independent tile accumulators inner (reads batched ahead)
+    {
+      f32x4_t acc[6];
+      int rb[6];
 #pragma unroll
-    for (int mt = 0; mt < 6; ++mt) {
-      f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      const int p = 16 * mt + i16;
-      const int pc = p < 81 ? p : 0;
-      const int ih = pc / 9, iw = pc - ih * 9;
+      for (int mt = 0; mt < 6; ++mt) {
+        acc[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        const int p = 16 * mt + i16;
+        const int pc = p < 81 ? p : 0;
+        const int ih = pc / 9, iw = pc - ih * 9;
+        rb[mt] = (ih + 2) * 11 + (iw + 2);
+      }
 #pragma unroll
       for (int ks = 0; ks < 18; ++ks) {
         const int t = ks >> 1, kh = t / 3, kw = t - kh * 3;
-        const int row = (ih - kh + 2) * 11 + (iw - kw + 2);
-        const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(Yi + row * kD3Ld + (ks & 1) * 32 + 8 * g);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, wf[ks], acc, 0, 0, 0);
+        const int off = -(kh * 11 + kw) * kD3Ld + (ks & 1) * 32 + 8 * g;
+        bf16x8_t af[6];
+#pragma unroll
+        for (int mt = 0; mt < 6; ++mt) af[mt] = *reinterpret_cast<const bf16x8_t*>(Yi + rb[mt] * kD3Ld + off);
+#pragma unroll
+        for (int mt = 0; mt < 6; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], wf[ks], acc[mt], 0, 0, 0);
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int q = 16 * mt + 4 * g + r;
-        if (q < 81) O[q * kD3OutLd + 16 * wave + i16] = f2bf(acc[r]);
-      }
+      for (int mt = 0; mt < 6; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = 16 * mt + 4 * g + r;
+          if (q < 81) O[q * kD3OutLd + 16 * wave + i16] = f2bf(acc[mt][r]);
+        }
     }
     __syncthreads();
     uint4* xd = reinterpret_cast<uint4*>(dx + (size_t)n * 81 * 64);

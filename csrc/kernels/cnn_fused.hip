@@ -1,0 +1,726 @@
+// Fused Nature-CNN conv stack for the pixel A2C model (BASELINE.json config 4).
+//
+// Forward: conv1 (space-to-depth 2x2/1 over 21x21x64 uint8 frames -> 20x20x32) -> ReLU ->
+// conv2 (4x4/2 -> 9x9x64) -> ReLU -> conv3 (3x3/1 -> 7x7x64) -> ReLU in ONE persistent
+// launch, every intermediate activation resident in LDS.  The per-layer kernels this
+// replaces (conv1_fwd_s2d_kernel and conv_fwd_img_kernel x 2 in cnn.hip) each streamed
+// their input image from HBM and paid their own launch fill / drain; here a frame is read
+// once and a1 / a2 / a3 are written once (the backward pass needs them) and never re-read.
+//
+// Geometry per frame (bf16 activations, fp32 accumulate on v_mfma_f32_16x16x32_bf16):
+//   conv1  400 px x 32 co, K = 256 (4 taps x 64 s2d channels)   25 x 2 (px tile, co tile) units
+//   conv2   81 px x 64 co, K = 512 (16 taps x 32 channels)         6 x 4 units
+//   conv3   49 px x 64 co, K = 576 (9 taps x 64 channels)          4 x 4 units
+//
+// Eight waves, two per SIMD, split by LAYER so that each wave keeps only one layer's
+// weights in registers besides conv1's (all three layers' fragments are 168 VGPRs per
+// wave, which spilled at two waves per SIMD and starved the fragment reads at one):
+//   every wave        conv1 co tile (w & 1), pixel tiles (w >> 1) + 4 t       (32 VGPRs of W1)
+//   waves 0-3 ("A")   conv2 co tile w over all 6 pixel tiles of frame j       (64 VGPRs of W2)
+//   waves 4-7 ("B")   conv3 co tile w - 4 over all 4 pixel tiles of frame j-1 (72 VGPRs of W3)
+// so conv2 of frame j and conv3 of frame j-1 run side by side between the same two
+// barriers (a2 is double-buffered).  Each layer's k-step order matches the per-layer
+// kernels', so the fused outputs equal theirs up to fma contraction in the epilogue.
+//
+// Per iteration j (frame n_j = blockIdx.x + j * gridDim.x):
+//   store frame n_j (prefetched into registers) -> LDS; prefetch frame n_{j+1}      | B0 .. B1
+//   copy out a2(n_{j-1}) and a3(n_{j-2}); conv1(n_j) -> A1                          | B1 .. B2
+//   copy out a1(n_j); A: conv2(n_j) -> A2[j & 1]; B: conv3(n_{j-1}) -> A3          | B2 .. B0
+#include "gemm_bf16.h"
+
+namespace rrl {
+
+// Two fp32 -> packed bf16 pair (round to nearest even), a in the low half.  A vector
+// conversion, not inline asm: it lowers to gfx950's v_cvt_pk_bf16_f32 AND stays visible to
+// the hazard recognizer -- an asm cvt reading an MFMA result directly got no wait states
+// and read the accumulator registers before the MFMA had written them.
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t{a, b}), bf16x2_t));
+}
+// The MFMAs below run with the weights as the A operand and the activation rows as B, so
+// D = out^T: lane (i, g) holds 4 consecutive output channels 4g..4g+3 of pixel i, stored
+// as ONE 8-byte LDS write (2 cvt_pk) instead of 4 scalar bf16 conversions and 2-byte writes.
+__device__ __forceinline__ void store4_bf16(uint16_t* dst, float v0, float v1, float v2, float v3) {
+  *reinterpret_cast<uint2*>(dst) = make_uint2(pk_bf16(v0, v1), pk_bf16(v2, v3));
+}
+
+// v where the ReLU mask m (8 packed bf16 activations) is > 0, else 0 -- bitwise on the packed
+// halves (the masked values are already bf16: no round trip through fp32)
+__device__ __forceinline__ uint32_t relu_mask2(uint32_t v, uint32_t m) {
+  const uint32_t lo = ((m & 0x8000u) == 0u && (m & 0xffffu) != 0u) ? 0x0000ffffu : 0u;
+  const uint32_t hi = ((m & 0x80000000u) == 0u && (m >> 16) != 0u) ? 0xffff0000u : 0u;
+  return v & (lo | hi);
+}
+__device__ __forceinline__ uint4 relu_mask8(uint4 v, uint4 m) {
+  return make_uint4(relu_mask2(v.x, m.x), relu_mask2(v.y, m.y), relu_mask2(v.z, m.z), relu_mask2(v.w, m.w));
+}
+
+namespace cs {
+constexpr int kThreads = 512;
+constexpr int kFrameLd = 80;                  // frame row: 64 channels + 16 pad (bf16)
+constexpr int kFrameRows = 441;               // 21 x 21 s2d pixels
+constexpr int kA1Ld = 40;                     // a1 row: 32 co + 8 pad
+constexpr int kA2Ld = 72;                     // a2 / a3 rows: 64 co + 8 pad
+constexpr int kXi = 0;                                    // element offsets into LDS
+constexpr int kA1 = kXi + kFrameRows * kFrameLd;          // 35,280
+constexpr int kA2 = kA1 + 400 * kA1Ld;                    // 51,280 (two buffers of 81 rows)
+constexpr int kA3 = kA2 + 2 * 81 * kA2Ld;                 // 62,944
+constexpr int kLds = (kA3 + 49 * kA2Ld) * 2;              // 132,944 bytes
+constexpr int kXChunks = kFrameRows * 64 / 16;           // 16-byte chunks of one uint8 frame (1,764)
+constexpr int kXPerT = (kXChunks + kThreads - 1) / kThreads;
+static_assert(kA1 % 8 == 0 && kA2 % 8 == 0 && kA3 % 8 == 0, "16-byte aligned LDS regions");
+}  // namespace cs
+
+// PROBE (tools/cnn_kbench.py --probe, timing only -- outputs are garbage when != 0):
+// bit 0 skips the MFMAs, bit 1 the global stores, bit 2 re-reads frame 0 (L2-hot)
+template <int PROBE>
+__global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
+    const uint8_t* __restrict__ x, const uint16_t* __restrict__ w1, const float* __restrict__ b1,
+    const uint16_t* __restrict__ w2, const float* __restrict__ b2, const uint16_t* __restrict__ w3,
+    const float* __restrict__ b3, uint16_t* __restrict__ y1, uint16_t* __restrict__ y2,
+    uint16_t* __restrict__ y3, int N) {
+  using namespace cs;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Xi = smem + kXi;  // [441][80] frame as bf16 integers 0..255
+  uint16_t* A1 = smem + kA1;  // [400][40] conv1 output
+  uint16_t* A3 = smem + kA3;  // [49][72]  conv3 output
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const bool role_a = wave < 4;
+  const int ct = wave & 3;  // co tile of conv2 (A) / conv3 (B)
+
+  // stationary weights: B fragment = W[co][8 consecutive k], co = 16 * tile + i
+  const int c1 = wave & 1;
+  bf16x8_t f1[8], fw[18];  // fw: W2 (16 k-steps) on A waves, W3 (18) on B waves
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) f1[ks] = *reinterpret_cast<const bf16x8_t*>(w1 + (16 * c1 + i) * 256 + 32 * ks + 8 * g);
+  if (role_a) {
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) fw[ks] = *reinterpret_cast<const bf16x8_t*>(w2 + (16 * ct + i) * 512 + 32 * ks + 8 * g);
+    fw[16] = fw[17] = fw[0];
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) fw[ks] = *reinterpret_cast<const bf16x8_t*>(w3 + (16 * ct + i) * 576 + 32 * ks + 8 * g);
+  }
+  // biases of this lane's 4 output channels (co = 16 tile + 4 g + r)
+  const f32x4_t bias1 = *reinterpret_cast<const f32x4_t*>(b1 + 16 * c1 + 4 * g);
+  const f32x4_t bias23 = *reinterpret_cast<const f32x4_t*>((role_a ? b2 : b3) + 16 * ct + 4 * g);
+
+  const int G = gridDim.x, n0 = blockIdx.x;
+  uint4 rx[kXPerT];
+  auto gload = [&](size_t n) {
+    if (PROBE & 4) n = 0;
+    const uint4* xs = reinterpret_cast<const uint4*>(x + n * (kFrameRows * 64));
+#pragma unroll
+    for (int k = 0; k < kXPerT; ++k) {
+      const int q = tid + kThreads * k;
+      rx[k] = q < kXChunks ? xs[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (n0 < N) gload(n0);
+  // j runs two frames past this workgroup's last one to drain conv3 and the a3 copy-out
+  for (int j = 0; n0 + (j - 2) * G < N; ++j) {
+    const int n = n0 + j * G;        // conv1 / conv2 frame
+    const bool cur = n < N;
+    const bool prev = j >= 1 && n - G < N;  // conv3 frame
+    __syncthreads();  // B0: conv1 / conv2 / conv3 of the previous iteration are done
+    if (cur) {
+#pragma unroll
+      for (int k = 0; k < kXPerT; ++k) {
+        const int q = tid + kThreads * k;
+        if (q < kXChunks) {
+          uint16_t* d = Xi + (q >> 2) * kFrameLd + (q & 3) * 16;
+          *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(rx[k].x, rx[k].y));
+          *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(rx[k].z, rx[k].w));
+        }
+      }
+      if (n + G < N) gload((size_t)n + G);  // lands while this frame computes
+    }
+    __syncthreads();  // B1
+    // copy-outs of the previous iterations' a2 / a3 (conv1 touches neither buffer)
+    if (prev && !(PROBE & 2)) {
+      const uint16_t* A2p = smem + kA2 + ((j - 1) & 1) * 81 * kA2Ld;
+      uint4* yd = reinterpret_cast<uint4*>(y2 + (size_t)(n - G) * 81 * 64);
+      for (int q = tid; q < 81 * 8; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A2p + (q >> 3) * kA2Ld + (q & 7) * 8);
+    }
+    if (j >= 2 && !(PROBE & 2)) {
+      uint4* yd = reinterpret_cast<uint4*>(y3 + (size_t)(n - 2 * G) * 49 * 64);
+      for (int q = tid; q < 49 * 8; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A3 + (q >> 3) * kA2Ld + (q & 7) * 8);
+    }
+    // ---- conv1 (all waves): pixel tiles (wave >> 1) + 4 t, co tile c1
+    if (cur) {
+      constexpr int MT = 7;
+      f32x4_t acc[MT];
+      int r0[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        const int mt = min((wave >> 1) + 4 * t, 24);  // a tile past the frame recomputes tile 24
+        const int p = 16 * mt + i;
+        r0[t] = (p / 20) * 21 + p % 20;  // frame row of tap (0, 0)
+      }
+      // k-step outer, tiles inner: MT independent MFMAs per k-step, their reads batched ahead
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int tap = ks >> 1;
+        const int off = ((tap >> 1) * 21 + (tap & 1)) * kFrameLd + 32 * (ks & 1) + 8 * g;
+        bf16x8_t a[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) a[t] = *reinterpret_cast<const bf16x8_t*>(Xi + r0[t] * kFrameLd + off);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) if (!(PROBE & 1)) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[ks], a[t], acc[t], 0, 0, 0);
+        else acc[t][0] += (float)a[t][0];
+      }
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int mt = (wave >> 1) + 4 * t;
+        if (mt < 25) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(kU8Scale * acc[t][r] + bias1[r], 0.f);
+          store4_bf16(A1 + (16 * mt + i) * kA1Ld + 16 * c1 + 4 * g, v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
+    __syncthreads();  // B2: a1(n) complete
+    if (cur && !(PROBE & 2)) {
+      uint4* yd = reinterpret_cast<uint4*>(y1 + (size_t)n * 400 * 32);
+      for (int q = tid; q < 400 * 4; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A1 + (q >> 2) * kA1Ld + (q & 3) * 8);
+    }
+    if (role_a) {
+      // ---- conv2(n): co tile ct, all 6 pixel tiles (81 px; rows past the image are discarded)
+      if (cur) {
+        uint16_t* A2c = smem + kA2 + (j & 1) * 81 * kA2Ld;
+        constexpr int MT = 6;
+        f32x4_t acc[MT];
+        int r0[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          const int p = 16 * t + i;
+          const int pc = p < 81 ? p : 0;
+          const int oh = pc / 9, ow = pc - oh * 9;
+          r0[t] = 2 * oh * 20 + 2 * ow;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) {
+          const int off = ((ks >> 2) * 20 + (ks & 3)) * kA1Ld + 8 * g;
+          bf16x8_t a[MT];
+#pragma unroll
+          for (int t = 0; t < MT; ++t) a[t] = *reinterpret_cast<const bf16x8_t*>(A1 + r0[t] * kA1Ld + off);
+#pragma unroll
+          for (int t = 0; t < MT; ++t) if (!(PROBE & 1)) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks], a[t], acc[t], 0, 0, 0);
+          else acc[t][0] += (float)a[t][0];
+        }
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          const int p = 16 * t + i;
+          if (p < 81)
+            store4_bf16(A2c + p * kA2Ld + 16 * ct + 4 * g, fmaxf(acc[t][0] + bias23[0], 0.f),
+                        fmaxf(acc[t][1] + bias23[1], 0.f), fmaxf(acc[t][2] + bias23[2], 0.f),
+                        fmaxf(acc[t][3] + bias23[3], 0.f));
+        }
+      }
+    } else if (prev) {
+      // ---- conv3(n - G): co tile ct, all 4 pixel tiles (49 px), input a2 from the other buffer
+      const uint16_t* A2p = smem + kA2 + ((j - 1) & 1) * 81 * kA2Ld;
+      constexpr int MT = 4;
+      f32x4_t acc[MT];
+      int r0[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        const int p = 16 * t + i;
+        const int pc = p < 49 ? p : 0;
+        const int oh = pc / 7, ow = pc - oh * 7;
+        r0[t] = oh * 9 + ow;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 18; ++ks) {
+        const int tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
+        const int off = (kh * 9 + kw) * kA2Ld + 32 * (ks & 1) + 8 * g;
+        bf16x8_t a[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) a[t] = *reinterpret_cast<const bf16x8_t*>(A2p + r0[t] * kA2Ld + off);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) if (!(PROBE & 1)) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks], a[t], acc[t], 0, 0, 0);
+          else acc[t][0] += (float)a[t][0];
+      }
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int p = 16 * t + i;
+        if (p < 49)
+          store4_bf16(A3 + p * kA2Ld + 16 * ct + 4 * g, fmaxf(acc[t][0] + bias23[0], 0.f),
+                      fmaxf(acc[t][1] + bias23[1], 0.f), fmaxf(acc[t][2] + bias23[2], 0.f),
+                      fmaxf(acc[t][3] + bias23[3], 0.f));
+      }
+    }
+  }
+}
+
+}  // namespace rrl
+
+using namespace rrl;
+
+template <int PROBE>
+static int launch_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
+                                 const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
+                                 uint16_t* y3, int N, int max_grid, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_stack_fwd_kernel<PROBE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              cs::kLds);
+    attr = true;
+  }
+  if (N < 1) return 0;
+  const int grid = N < max_grid ? N : max_grid;  // one 133 KB-LDS workgroup per CU
+  hipLaunchKernelGGL(conv_stack_fwd_kernel<PROBE>, dim3(grid), dim3(cs::kThreads), cs::kLds, stream, x, w1, b1, w2,
+                     b2, w3, b3, y1, y2, y3, N);
+  return (int)hipGetLastError();
+}
+
+extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
+                                  const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
+                                  uint16_t* y3, int N, int max_grid, void* stream) {
+  // max_grid < 0: timing probe variant -max_grid >> 16 (tools/cnn_kbench.py), grid = -max_grid & 0xffff
+  hipStream_t st = (hipStream_t)stream;
+  if (max_grid >= 0) return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, max_grid, st);
+  const int probe = (-max_grid) >> 16, g = (-max_grid) & 0xffff;
+  switch (probe) {
+    case 1: return launch_conv_stack_fwd<1>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 2: return launch_conv_stack_fwd<2>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 3: return launch_conv_stack_fwd<3>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 4: return launch_conv_stack_fwd<4>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 7: return launch_conv_stack_fwd<7>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    default: return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+  }
+}
+
+// ============================================================================= conv3 backward
+// dgrad + wgrad + bias gradient of the third conv layer (9x9x64 -> 3x3/1 -> 7x7x64) in ONE
+// pass per image.  Both halves read the same two inputs -- the output gradient da3 [49][64]
+// and the input activation a2 [81][64] (also the ReLU mask of da2) -- so each is fetched
+// from HBM once instead of once per GEMM (the split-K implicit-GEMM wgrad + its partial
+// sums, the column-sum bias pass and conv3_dgrad_kernel in cnn.hip), and the weight
+// gradient accumulates in registers across all of a workgroup's images: one fp32 partial
+// per workgroup instead of one per split-K slice.
+//
+// LDS per image: da3 in a zero-bordered 11x11 image (row (oh + 2) * 11 + ow + 2), a2 as
+// [96 rows][72] (rows >= 81 zero), the dgrad staging tile [81][72].
+//   dgrad  da2[81 px][64 c] = sum_(tap, co) da3[px - tap][co] W3[co][tap][c]      (6 x 4 tiles)
+//          wave w: c tile (w & 3), pixel tiles 3 (w >> 2) + {0, 1, 2}, W3 fragments in registers
+//   wgrad  dW3[64 co][576 k] += da3^T (co x pos) . im2col(a2) (pos x k)            (4 x 36 tiles)
+//          positions run over 8 output rows x 8 columns (row 7 and column 7 read the zero
+//          border), so the 8 positions of one lane group are one output row and their a2
+//          pixels are 8 consecutive image rows: both operands are transposed LDS reads
+//          (ds_read_b64_tr_b16) with no im2col buffer; wave w: c block (w & 3) of all 4 co
+//          tiles, taps 0..4 (w < 4) or 5..8 (w >= 4)
+namespace c3b {
+constexpr int kThreads = 512;
+constexpr int kLd = 72;
+constexpr int kD = 0;                 // da3 bordered [121][72]
+constexpr int kX = kD + 121 * kLd;    // a2 [96][72]
+constexpr int kO = kX + 96 * kLd;     // dgrad staging [81][72]
+constexpr int kLds = (kO + 81 * kLd) * 2;  // 43,344 bytes
+constexpr int kYC = 49 * 8, kXC = 81 * 8;  // 16-byte chunks per image
+constexpr int kYPT = (kYC + kThreads - 1) / kThreads, kXPT = (kXC + kThreads - 1) / kThreads;
+}  // namespace c3b
+
+__device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* a0, int ld) {
+  typedef __attribute__((address_space(3))) s16x4_t lds_v4;
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0 + 4 * ld));
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+__global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                                     const uint16_t* __restrict__ w,
+                                                                     const uint16_t* __restrict__ xact,
+                                                                     uint16_t* __restrict__ dx,
+                                                                     float* __restrict__ part,
+                                                                     float* __restrict__ bias_part, int N) {
+  using namespace c3b;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Yi = smem + kD;
+  uint16_t* Xi = smem + kX;
+  uint16_t* O = smem + kO;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i16 = lane & 15, g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int ct = wave & 3, half = wave >> 2;
+
+  // dgrad B fragments: k-step ks = (tap t = ks >> 1, co block (ks & 1) * 32):
+  // W3[co0 + 8g + e][t][16 ct + i16], e = 0..7
+  bf16x8_t wf[18];
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks) {
+    const int t = ks >> 1, co0 = (ks & 1) * 32 + 8 * g;
+    typedef short s16x8_t __attribute__((ext_vector_type(8)));
+    s16x8_t v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (short)w[((co0 + e) * 9 + t) * 64 + 16 * ct + i16];
+    wf[ks] = __builtin_bit_cast(bf16x8_t, v);
+  }
+  // zero the da3 border and the a2 pad rows once (interiors are rewritten per image)
+  for (int q = tid; q < 121 * (kLd / 8); q += kThreads) {
+    const int r = q / (kLd / 8), oh = r / 11 - 2, ow = r % 11 - 2;
+    if (oh < 0 || oh > 6 || ow < 0 || ow > 6)
+      *reinterpret_cast<uint4*>(Yi + r * kLd + 8 * (q % (kLd / 8))) = make_uint4(0, 0, 0, 0);
+  }
+  for (int q = tid; q < 15 * (kLd / 8); q += kThreads)
+    *reinterpret_cast<uint4*>(Xi + (81 + q / (kLd / 8)) * kLd + 8 * (q % (kLd / 8))) = make_uint4(0, 0, 0, 0);
+
+  constexpr int NTAP = 5;  // taps of this wave's wgrad k tiles (4 on the second half)
+  const int tap0 = half * 5, ntap = half ? 4 : 5;
+  f32x4_t wacc[4][NTAP];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int t = 0; t < NTAP; ++t) wacc[c][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;  // db3[tid & 63] over positions (tid >> 6) + 8 k
+
+  uint4 ry[kYPT], rx[kXPT];
+  auto gload = [&](int n) {
+    const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 49 * 64);
+    const uint4* xs = reinterpret_cast<const uint4*>(xact + (size_t)n * 81 * 64);
+#pragma unroll
+    for (int k = 0; k < kYPT; ++k) {
+      const int q = tid + kThreads * k;
+      ry[k] = q < kYC ? ys[q] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < kXPT; ++k) {
+      const int q = tid + kThreads * k;
+      rx[k] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if ((int)blockIdx.x < N) gload(blockIdx.x);
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    __syncthreads();  // the previous image's reads of Yi / Xi / O are done
+#pragma unroll
+    for (int k = 0; k < kYPT; ++k) {
+      const int q = tid + kThreads * k;
+      if (q < kYC) {
+        const int pix = q >> 3, oh = pix / 7, ow = pix - oh * 7;
+        *reinterpret_cast<uint4*>(Yi + ((oh + 2) * 11 + ow + 2) * kLd + (q & 7) * 8) = ry[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kXPT; ++k) {
+      const int q = tid + kThreads * k;
+      if (q < kXC) *reinterpret_cast<uint4*>(Xi + (q >> 3) * kLd + (q & 7) * 8) = rx[k];
+    }
+    if (n + (int)gridDim.x < N) gload(n + gridDim.x);
+    __syncthreads();
+
+    // ---- wgrad: 2 position k-steps x (4 co tiles x ntap taps)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int oh = 4 * s + g;  // this lane group's output row (7 = zero border)
+      bf16x8_t af[4], bfr[NTAP];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) af[c] = tr_frag(Yi + ((oh + 2) * 11 + 2 + q4) * kLd + 16 * c + 4 * p4, kLd);
+#pragma unroll
+      for (int t = 0; t < NTAP; ++t) {
+        const int tap = min(tap0 + t, 8), kh = tap / 3, kw = tap - kh * 3;
+        bfr[t] = tr_frag(Xi + ((oh + kh) * 9 + kw + q4) * kLd + 16 * ct + 4 * p4, kLd);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int t = 0; t < NTAP; ++t) wacc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[c], bfr[t], wacc[c][t], 0, 0, 0);
+    }
+    // ---- dgrad: k-step outer, this wave's 3 pixel tiles inner
+    {
+      f32x4_t acc[3];
+      int rb[3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        const int p = 16 * (3 * half + u) + i16;
+        const int pc = p < 81 ? p : 0;
+        const int ih = pc / 9, iw = pc - ih * 9;
+        rb[u] = (ih + 2) * 11 + (iw + 2);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 18; ++ks) {
+        const int t = ks >> 1, kh = t / 3, kw = t - kh * 3;
+        const int off = -(kh * 11 + kw) * kLd + (ks & 1) * 32 + 8 * g;
+        bf16x8_t a[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) a[u] = *reinterpret_cast<const bf16x8_t*>(Yi + rb[u] * kLd + off);
+#pragma unroll
+        for (int u = 0; u < 3; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], a[u], acc[u], 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {  // D = da2^T: lane (i16, g) holds channels 4g..4g+3 of pixel i16
+        const int q = 16 * (3 * half + u) + i16;
+        if (q < 81) store4_bf16(O + q * kLd + 16 * ct + 4 * g, acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+      }
+    }
+    // ---- db3
+    for (int pos = tid >> 6; pos < 49; pos += 8) {
+      const int oh = pos / 7, ow = pos - oh * 7;
+      bsum += bf2f(Yi[((oh + 2) * 11 + ow + 2) * kLd + (tid & 63)]);
+    }
+    __syncthreads();  // dgrad staging complete
+    uint4* xd = reinterpret_cast<uint4*>(dx + (size_t)n * 81 * 64);
+    for (int q = tid; q < kXC; q += kThreads) {
+      const uint4 v = *reinterpret_cast<const uint4*>(O + (q >> 3) * kLd + (q & 7) * 8);
+      const uint4 m = *reinterpret_cast<const uint4*>(Xi + (q >> 3) * kLd + (q & 7) * 8);
+      xd[q] = relu_mask8(v, m);
+    }
+  }
+  // this workgroup's weight-gradient partial: part[blk][co][tap][c]
+  float* o = part + (size_t)blockIdx.x * 64 * 576;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int t = 0; t < NTAP; ++t)
+      if (t < ntap) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[(16 * c + 4 * g + r) * 576 + (tap0 + t) * 64 + 16 * ct + i16] = wacc[c][t][r];
+      }
+  bias_part[(size_t)blockIdx.x * kThreads + tid] = bsum;
+}
+
+extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
+                             float* bias_part, int N, int grid, void* stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv3_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
+    attr = true;
+  }
+  if (N < 1 || grid < 1) return 0;
+  hipLaunchKernelGGL(conv3_bwd_kernel, dim3(grid), dim3(c3b::kThreads), c3b::kLds, (hipStream_t)stream, dy, w, xact,
+                     dx, part, bias_part, N);
+  return (int)hipGetLastError();
+}
+
+// ============================================================================= conv2 backward
+// dgrad + wgrad + bias gradient of the second conv layer (20x20x32 -> 4x4/2 -> 9x9x64) in ONE
+// pass per image, software-pipelined with ONE barrier per image: while image j computes from
+// LDS buffer j & 1, image j + 1 (prefetched into registers one iteration earlier) is written
+// into the other buffer and image j + 2's loads are in flight.
+//
+// LDS images per buffer:
+//   da2  zero-bordered 12 x 12 (row (oh + 1) * 12 + ow + 1; 64 co + 8 pad)
+//   a1   split into its four stride-2 phase images (ph, pw) = (ih & 1, iw & 1), each 10 x 10
+//        positions (row (ih >> 1) * 10 + (iw >> 1), rows 100..115 zero; 32 c + 8 pad)
+//   dgrad  da1[ph + 2a][pw + 2b][c] = sum_(i, j, co) da2[a - i][b - j][co] W2[co][ph + 2i][pw + 2j][c]
+//          per phase class a 100 px x 32 c GEMM over K = (4 taps x 64 co); wave w: class w >> 1,
+//          c tile w & 1, W2 fragments in registers.  The weights are the MFMA's A operand, so a
+//          lane ends with 4 consecutive channels of one pixel: masked by a1 (from the phase
+//          image) and stored straight to HBM as 8 bytes.
+//   wgrad  dW2[64 co][(kh, kw, c) 512] += da2^T (co x pos) . im2col(a1) (pos x k): positions
+//          in runs of 4 output columns (9 per row -> runs at ow 0, 4, 8; the run past ow 8 reads
+//          the zero border), so each half of a transposed fragment read is 4 consecutive rows
+//          of the da2 image AND of one a1 phase image (stride-2 taps land on unit-stride phase
+//          rows); wave w: c block w & 1 of taps 4 (w >> 1) .. + 3, all 4 co tiles.
+namespace c2b {
+constexpr int kThreads = 512;
+constexpr int kDLd = 72, kPLd = 40;
+constexpr int kDRows = 144, kPRows = 116;
+constexpr int kBuf = kDRows * kDLd + 4 * kPRows * kPLd;  // elements per buffer (28,928)
+constexpr int kLds = 2 * kBuf * 2;                       // 115,712 bytes
+constexpr int kYC = 81 * 8, kXC = 400 * 4;               // 16-byte chunks per image
+constexpr int kYPT = (kYC + kThreads - 1) / kThreads, kXPT = (kXC + kThreads - 1) / kThreads;
+}  // namespace c2b
+
+__device__ __forceinline__ bf16x8_t tr_frag2(const uint16_t* a0, const uint16_t* a1) {
+  typedef __attribute__((address_space(3))) s16x4_t lds_v4;
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a1));
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+__global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                                     const uint16_t* __restrict__ w,
+                                                                     const uint16_t* __restrict__ xact,
+                                                                     uint16_t* __restrict__ dx,
+                                                                     float* __restrict__ part,
+                                                                     float* __restrict__ bias_part, int N) {
+  using namespace c2b;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i16 = lane & 15, g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  // dgrad role: phase class (ph, pw), c tile
+  const int cls = wave >> 1, ph = cls >> 1, pw = cls & 1, ct = wave & 1;
+  // wgrad role: c block, taps tau0 .. tau0 + 3
+  const int cb = wave & 1, tau0 = 4 * (wave >> 1);
+
+  // dgrad A fragments (weights): k-step ks = (tap t = ks >> 1 -> (ti, tj), co block (ks & 1) * 32):
+  // W2[co0 + 8g + e][ph + 2 ti][pw + 2 tj][16 ct + i16]
+  bf16x8_t wf[8];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) {
+    const int t = ks >> 1, kh = ph + 2 * (t >> 1), kw = pw + 2 * (t & 1), co0 = (ks & 1) * 32 + 8 * g;
+    typedef short s16x8_t __attribute__((ext_vector_type(8)));
+    s16x8_t v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (short)w[(((co0 + e) * 4 + kh) * 4 + kw) * 32 + 16 * ct + i16];
+    wf[ks] = __builtin_bit_cast(bf16x8_t, v);
+  }
+  // zero both buffers once: the da2 border and the phase-image pad rows are never rewritten
+  for (int q = tid; q < 2 * kBuf / 8; q += kThreads) *reinterpret_cast<uint4*>(smem + 8 * q) = make_uint4(0, 0, 0, 0);
+
+  f32x4_t wacc[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) wacc[c][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;  // db2[tid & 63] over positions (tid >> 6) + 8 k
+
+  uint4 ry[kYPT], rx[kXPT];
+  auto gload = [&](int n) {
+    const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 81 * 64);
+    const uint4* xs = reinterpret_cast<const uint4*>(xact + (size_t)n * 400 * 32);
+#pragma unroll
+    for (int k = 0; k < kYPT; ++k) {
+      const int q = tid + kThreads * k;
+      ry[k] = q < kYC ? ys[q] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < kXPT; ++k) {
+      const int q = tid + kThreads * k;
+      rx[k] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lstore = [&](int buf) {
+    uint16_t* D = smem + buf * kBuf;
+    uint16_t* P = D + kDRows * kDLd;
+#pragma unroll
+    for (int k = 0; k < kYPT; ++k) {
+      const int q = tid + kThreads * k;
+      if (q < kYC) {
+        const int pix = q >> 3, oh = pix / 9, ow = pix - oh * 9;
+        *reinterpret_cast<uint4*>(D + ((oh + 1) * 12 + ow + 1) * kDLd + (q & 7) * 8) = ry[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kXPT; ++k) {
+      const int q = tid + kThreads * k;
+      if (q < kXC) {
+        const int pix = q >> 2, ih = pix / 20, iw = pix - ih * 20;
+        const int phase = (ih & 1) * 2 + (iw & 1);
+        *reinterpret_cast<uint4*>(P + (phase * kPRows + (ih >> 1) * 10 + (iw >> 1)) * kPLd + (q & 3) * 8) = rx[k];
+      }
+    }
+  };
+
+  const int G = gridDim.x, n0 = blockIdx.x;
+  __syncthreads();  // zeroing done before the first image lands in buffer 0
+  if (n0 < N) {
+    gload(n0);
+    lstore(0);
+  }
+  if (n0 + G < N) gload(n0 + G);
+  for (int j = 0; n0 + j * G < N; ++j) {
+    const int n = n0 + j * G;
+    __syncthreads();  // buffer j & 1 holds image n; buffer (j + 1) & 1 is no longer read
+    if (n + G < N) {
+      lstore((j + 1) & 1);
+      if (n + 2 * G < N) gload(n + 2 * G);
+    }
+    const uint16_t* D = smem + (j & 1) * kBuf;
+    const uint16_t* P = D + kDRows * kDLd;
+
+    // ---- wgrad: 4 position k-steps (8 runs of 4 columns each), 4 co tiles x 4 taps
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      int oh[2], ow0[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int R = 2 * (4 * s + g) + h;  // run index; runs >= 27 read zero rows
+        oh[h] = R < 27 ? R / 3 : 9;
+        ow0[h] = R < 27 ? 4 * (R % 3) : 0;
+      }
+      bf16x8_t af[4], bfr[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        af[c] = tr_frag2(D + ((oh[0] + 1) * 12 + ow0[0] + 1 + q4) * kDLd + 16 * c + 4 * p4,
+                         D + ((oh[1] + 1) * 12 + ow0[1] + 1 + q4) * kDLd + 16 * c + 4 * p4);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int tau = tau0 + t, kh = tau >> 2, kw = tau & 3;
+        const uint16_t* Pp = P + ((kh & 1) * 2 + (kw & 1)) * kPRows * kPLd + 16 * cb + 4 * p4;
+        bfr[t] = tr_frag2(Pp + ((oh[0] + (kh >> 1)) * 10 + ow0[0] + (kw >> 1) + q4) * kPLd,
+                          Pp + ((oh[1] + (kh >> 1)) * 10 + ow0[1] + (kw >> 1) + q4) * kPLd);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) wacc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[c], bfr[t], wacc[c][t], 0, 0, 0);
+    }
+    // ---- dgrad of phase class (ph, pw), c tile ct: 7 pixel tiles in two batches
+    auto class_tiles = [&](auto tag) {
+      constexpr int T0 = decltype(tag)::value, NT = T0 == 0 ? 4 : 3;
+      f32x4_t acc[NT];
+      int rb[NT];
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        const int p = 16 * (T0 + u) + i16;
+        const int pc = p < 100 ? p : 0;  // rows past the class are computed and discarded
+        const int a = pc / 10, b = pc - a * 10;
+        rb[u] = (a + 1) * 12 + (b + 1);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int t = ks >> 1, ti = t >> 1, tj = t & 1;
+        const int off = -(ti * 12 + tj) * kDLd + (ks & 1) * 32 + 8 * g;
+        bf16x8_t bv[NT];
+#pragma unroll
+        for (int u = 0; u < NT; ++u) bv[u] = *reinterpret_cast<const bf16x8_t*>(D + rb[u] * kDLd + off);
+#pragma unroll
+        for (int u = 0; u < NT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], bv[u], acc[u], 0, 0, 0);
+      }
+      // D = da1^T: lane (i16, g) holds channels 16 ct + 4g .. + 3 of class pixel p
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        const int p = 16 * (T0 + u) + i16;
+        if (p < 100) {
+          const int a = p / 10, b = p - a * 10;
+          const uint2 m = *reinterpret_cast<const uint2*>(P + (cls * kPRows + a * 10 + b) * kPLd + 16 * ct + 4 * g);
+          const uint2 v = make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x),
+                                     relu_mask2(pk_bf16(acc[u][2], acc[u][3]), m.y));
+          *reinterpret_cast<uint2*>(dx + ((size_t)n * 400 + (ph + 2 * a) * 20 + pw + 2 * b) * 32 + 16 * ct + 4 * g) = v;
+        }
+      }
+    };
+    class_tiles(std::integral_constant<int, 0>{});
+    class_tiles(std::integral_constant<int, 4>{});
+    // ---- db2
+    for (int pos = tid >> 6; pos < 81; pos += 8) {
+      const int oh = pos / 9, ow = pos - oh * 9;
+      bsum += bf2f(D[((oh + 1) * 12 + ow + 1) * kDLd + (tid & 63)]);
+    }
+  }
+  // weight-gradient partial of this workgroup: part[blk][co][kh][kw][c]
+  float* o = part + (size_t)blockIdx.x * 64 * 512;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[(16 * c + 4 * g + r) * 512 + (tau0 + t) * 32 + 16 * cb + i16] = wacc[c][t][r];
+  bias_part[(size_t)blockIdx.x * kThreads + tid] = bsum;
+}
+
+extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
+                             float* bias_part, int N, int grid, void* stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c2b::kLds);
+    attr = true;
+  }
+  if (N < 1 || grid < 1) return 0;
+  hipLaunchKernelGGL(conv2_bwd_kernel, dim3(grid), dim3(c2b::kThreads), c2b::kLds, (hipStream_t)stream, dy, w, xact,
+                     dx, part, bias_part, N);
+  return (int)hipGetLastError();
+}

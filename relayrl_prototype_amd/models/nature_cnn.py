@@ -185,6 +185,10 @@ class DeviceNatureCNN:
         if not use_hip(self.params):
             raise RuntimeError("DeviceNatureCNN needs a GPU tensor (CPU runs use reference_forward)")
         self.h = hip()
+        # one fused launch for the conv stack's forward (RRL_CNN_FUSED=0: the per-layer kernels)
+        import os
+
+        self.fused_convs = os.environ.get("RRL_CNN_FUSED", "1") != "0"
         self.o = spec.offsets()
         self.P = self.o["P"]
         dev = self.device
@@ -219,9 +223,11 @@ class DeviceNatureCNN:
             s = int(self.h.gemm_splits(M, max(1, min(512 // max(tiles, 1), -(-M // 64)))))
             self._wplan[name] = s
             need = max(need, s * cout * K)
+        self.cus = int(self.h.device_cus())
+        need = max(need, min(B, self.cus) * CONVS[2].cout * CONVS[2].K)  # fused conv3 backward partials
         self.part = torch.empty(need, device=dev)
         self.bias_splits = 512
-        self.bias_part = torch.empty(self.bias_splits * HIDDEN, device=dev)
+        self.bias_part = torch.empty(max(self.bias_splits * HIDDEN, self.cus * 512), device=dev)
         self.sq_work = torch.empty(1024, device=dev)
         self.norm_sq = torch.empty(1, device=dev)
 
@@ -248,10 +254,16 @@ class DeviceNatureCNN:
         hid = self._rows(self.hid, row0, n, HIDDEN)
         x = obs_u8.contiguous()
         assert tuple(x.shape[1:]) == OBS_S2D, "device CNN takes space-to-depth observations [n, 21, 21, 64]"
-        for i, (L, y) in enumerate(zip((S2D,) + CONVS[1:], (a1, a2, a3)), 1):
-            h.conv_fwd(x, sh[o[f"w{i}"]:o[f"b{i}"]], p[o[f"b{i}"]:o[f"b{i}"] + L.cout], y, n, L.hin, L.hin, L.cin,
-                       L.k, L.k, L.s, L.cout, True)
-            x = y
+        if self.fused_convs:
+            # conv1 -> conv2 -> conv3 in one launch, activations LDS-resident (cnn_fused.hip)
+            h.conv_stack_fwd(x, *(t for i in (1, 2, 3) for t in (sh[o[f"w{i}"]:o[f"b{i}"]],
+                                                                     p[o[f"b{i}"]:o[f"b{i}"] + CONVS[i - 1].cout])),
+                             a1, a2, a3, n)
+        else:
+            for i, (L, y) in enumerate(zip((S2D,) + CONVS[1:], (a1, a2, a3)), 1):
+                h.conv_fwd(x, sh[o[f"w{i}"]:o[f"b{i}"]], p[o[f"b{i}"]:o[f"b{i}"] + L.cout], y, n, L.hin, L.hin,
+                           L.cin, L.k, L.k, L.s, L.cout, True)
+                x = y
         h.conv_fwd(a3, sh[o["wfc"]:o["bfc"]], p[o["bfc"]:o["bfc"] + HIDDEN], hid, n, 1, 1, FC_IN, 1, 1, 1, HIDDEN,
                    True, self.part)  # split-K when the batch is too small to fill the chip
         return hid
@@ -319,15 +331,28 @@ class DeviceNatureCNN:
 
             pending = dist.all_reduce(g[o["wfc"]:o["P"]], group=comm.group, async_op=True)
         # conv3
-        self._wgrad("c3", da3, a2, B, L3.hin, L3.cin, L3.k, L3.s, L3.cout, o["w3"])
-        self._bias(da3, B * L3.hout ** 2, L3.cout, o["b3"])
         da2 = self.da2[:B * L2.hout ** 2 * L2.cout]
-        self._dgrad(da3, sh[o["w3"]:o["b3"]], a2, da2, B, L3)
+        if self.fused_convs:
+            # dgrad + wgrad + bias in one pass over (da3, a2) per image (cnn_fused.hip)
+            nblk = min(B, self.cus)
+            h.conv3_bwd(da3, sh[o["w3"]:o["b3"]], a2, da2, self.part, self.bias_part, B, nblk)
+            h.sum_splits(self.part, nblk, L3.cout * L3.K, g[o["w3"]:o["b3"]])
+            h.sum_splits(self.bias_part, nblk * 8, L3.cout, g[o["b3"]:o["b3"] + L3.cout])
+        else:
+            self._wgrad("c3", da3, a2, B, L3.hin, L3.cin, L3.k, L3.s, L3.cout, o["w3"])
+            self._bias(da3, B * L3.hout ** 2, L3.cout, o["b3"])
+            self._dgrad(da3, sh[o["w3"]:o["b3"]], a2, da2, B, L3)
         # conv2
-        self._wgrad("c2", da2, a1, B, L2.hin, L2.cin, L2.k, L2.s, L2.cout, o["w2"])
-        self._bias(da2, B * L2.hout ** 2, L2.cout, o["b2"])
         da1 = self.da1[:B * L1.hout ** 2 * L1.cout]
-        self._dgrad(da2, sh[o["w2"]:o["b2"]], a1, da1, B, L2)
+        if self.fused_convs:
+            nblk = min(B, self.cus)
+            h.conv2_bwd(da2, sh[o["w2"]:o["b2"]], a1, da1, self.part, self.bias_part, B, nblk)
+            h.sum_splits(self.part, nblk, L2.cout * L2.K, g[o["w2"]:o["b2"]])
+            h.sum_splits(self.bias_part, nblk * 8, L2.cout, g[o["b2"]:o["b2"] + L2.cout])
+        else:
+            self._wgrad("c2", da2, a1, B, L2.hin, L2.cin, L2.k, L2.s, L2.cout, o["w2"])
+            self._bias(da2, B * L2.hout ** 2, L2.cout, o["b2"])
+            self._dgrad(da2, sh[o["w2"]:o["b2"]], a1, da1, B, L2)
         # conv1 (input = frames, no data gradient)
         # (its bias gradient comes out of the same pass over da1)
         self._wgrad("c1", da1, obs_u8.contiguous(), B, S2D.hin, S2D.cin, S2D.k, S2D.s, S2D.cout, o["w1"],

@@ -211,6 +211,11 @@ def test_full_model_forward_backward_matches_autograd(cuda):
                          "fc": (o["wfc"], o["bfc"]), "head": (o["head"], o["P"])}.items():
         e = relerr(gd[a:b], pe.grad[a:b])
         assert e < 5e-2, (name, e)
+        # biases separately (a wrong bias partial hides inside the weight block's norm)
+        if name.startswith("conv"):
+            L = CONVS[int(name[-1]) - 1]
+            eb = relerr(gd[b:b + L.cout], pe.grad[b:b + L.cout])
+            assert eb < 5e-2, (name, "bias", eb)
     st = stats.sum(0).cpu()
     assert abs(st[3].item() - B) < 1e-3
     assert abs(st[0].item() / B - pg.item()) < 2e-2 * max(1.0, abs(pg.item()))
@@ -413,3 +418,112 @@ def test_sum_splits_matches_torch(cuda, splits, n):
     out = torch.empty(n, device=cuda)
     hip().sum_splits(part.to(cuda).reshape(-1), splits, n, out)
     torch.testing.assert_close(out.cpu(), part.sum(0), rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("N", [1, 5, 300, 2048])
+def test_fused_conv_stack_matches_per_layer_kernels(cuda, N):
+    """conv_stack_fwd (conv1 -> conv2 -> conv3 in one launch, cnn_fused.hip) against the
+    per-layer kernels it replaces (same k-step order: equal up to fma contraction) and the
+    bf16-emulating fp32 oracle."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    spec = CNNSpec()
+    o = spec.offsets()
+    g = torch.Generator().manual_seed(N)
+    params = spec.init(N).to(cuda)
+    params += 0.01 * torch.randn(params.shape, generator=g).to(cuda)  # non-zero biases
+    sh = params.bfloat16()
+    x = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g).to(cuda)
+    outs = []
+    for fused in (True, False):
+        a1 = torch.full((N * 400 * 32,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        a2 = torch.full((N * 81 * 64,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        a3 = torch.full((N * FC_IN,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        if fused:
+            h.conv_stack_fwd(x, sh[o["w1"]:o["b1"]], params[o["b1"]:o["b1"] + 32], sh[o["w2"]:o["b2"]],
+                             params[o["b2"]:o["b2"] + 64], sh[o["w3"]:o["b3"]], params[o["b3"]:o["b3"] + 64], a1, a2,
+                             a3, N)
+        else:
+            from relayrl_prototype_amd.models.nature_cnn import S2D
+
+            src = x
+            for i, (L, y) in enumerate(zip((S2D,) + CONVS[1:], (a1, a2, a3)), 1):
+                h.conv_fwd(src, sh[o[f"w{i}"]:o[f"b{i}"]], params[o[f"b{i}"]:o[f"b{i}"] + L.cout], y, N, L.hin,
+                           L.hin, L.cin, L.k, L.k, L.s, L.cout, True)
+                src = y
+        torch.cuda.synchronize()
+        outs.append((a1, a2, a3))
+    for f, r in zip(outs[0], outs[1]):
+        assert torch.isfinite(f.float()).all()
+        # equal up to bf16 rounding flips where an fma contraction differs
+        assert relerr(f, r) < 2e-3
+    _, _, acts = reference_forward(spec, params.cpu(), x.cpu(), emulate_bf16=True)
+    for dev_a, ref_a in zip(outs[0], acts[:3]):
+        assert relerr(dev_a, ref_a.permute(0, 2, 3, 1).reshape(-1)) < 1e-2
+
+
+@pytest.mark.parametrize("B", [3, 300, 1500])
+def test_fused_conv_backward_matches_per_layer(cuda, B):
+    """The fused conv3 backward (dgrad + wgrad + bias in one pass, cnn_fused.hip) against the
+    per-layer kernels on the same stored activations: every parameter gradient."""
+    spec = CNNSpec(6)
+    o = spec.offsets()
+    params = spec.init(7)
+    params[o["wpi"]:o["bpi"]] *= 50.0
+    g = torch.Generator().manual_seed(B)
+    obs = torch.randint(0, 256, (B, 21, 21, 64), dtype=torch.uint8, generator=g).to(cuda)
+    act = torch.randint(0, 6, (B,), dtype=torch.int32, generator=g).to(cuda)
+    adv = torch.randn(B, generator=g).to(cuda)
+    ret = torch.randn(B, generator=g).to(cuda)
+    grads = []
+    for fused in (True, False):
+        m = DeviceNatureCNN(spec, cuda, max_batch=B, params=params)
+        m.fused_convs = fused
+        m.forward(obs, 0)
+        m.grad.fill_(float("nan"))
+        m.backward(obs, act, adv, ret, 0.5, 0.01)
+        torch.cuda.synchronize()
+        grads.append(m.grad.clone())
+    gf, gr = grads
+    assert torch.isfinite(gf).all()
+    for name, (a, b) in {"conv1": (o["w1"], o["b1"]), "conv2": (o["w2"], o["b2"]), "conv3": (o["w3"], o["b3"]),
+                         "fc": (o["wfc"], o["bfc"]), "head": (o["head"], o["P"])}.items():
+        assert relerr(gf[a:b], gr[a:b]) < 1e-4, name
+    for i, L in enumerate(CONVS, 1):
+        b0 = o[f"b{i}"]
+        assert relerr(gf[b0:b0 + L.cout], gr[b0:b0 + L.cout]) < 1e-4, f"b{i}"
+
+
+@pytest.mark.parametrize("li,N,grid", [(1, 3, 3), (1, 70, 16), (2, 5, 5), (2, 300, 64)])
+def test_fused_conv_bwd_kernels_match_autograd(cuda, li, N, grid):
+    """conv2_bwd / conv3_bwd (cnn_fused.hip) against fp32 autograd on the same bf16 operands:
+    masked data gradient, weight-gradient partials (summed over workgroups), bias partials."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    L = CONVS[li]
+    g = torch.Generator().manual_seed(li * 1000 + N)
+    x = _bf(torch.relu(torch.randn(N, L.hin, L.hin, L.cin, generator=g)))  # post-ReLU input (zeros = mask)
+    w = _bf(torch.randn(L.cout, L.k, L.k, L.cin, generator=g) * 0.05)
+    dy = _bf(torch.randn(N, L.hout, L.hout, L.cout, generator=g))
+    xd, wd, dyd = x.to(cuda).bfloat16(), w.to(cuda).bfloat16(), dy.to(cuda).bfloat16()
+    dx = torch.full((N * L.hin * L.hin * L.cin,), float("nan"), dtype=torch.bfloat16, device=cuda)
+    part = torch.full((grid * L.cout * L.K,), float("nan"), device=cuda)
+    bpart = torch.full((grid * 512,), float("nan"), device=cuda)
+    (h.conv2_bwd if li == 1 else h.conv3_bwd)(dyd.reshape(-1), wd.reshape(-1), xd.reshape(-1), dx, part, bpart, N, grid)
+    torch.cuda.synchronize()
+    xr = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    wr = w.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    y = F.conv2d(xr, wr, stride=L.s)
+    y.backward(dy.permute(0, 3, 1, 2))
+    dx_ref = (xr.grad * (xr > 0)).permute(0, 2, 3, 1).reshape(-1)
+    dw_ref = wr.grad.permute(0, 2, 3, 1).reshape(-1)
+    db_ref = dy.sum((0, 1, 2))
+    dxg = dx.float().cpu()
+    assert torch.isfinite(dxg).all()
+    assert relerr(dxg, dx_ref) < 1e-2
+    dw = part.view(grid, -1).sum(0).cpu()
+    assert relerr(dw, dw_ref) < 1e-3
+    db = bpart.view(grid * 8, 64).sum(0).cpu()
+    assert relerr(db, db_ref) < 1e-3

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the pixel-model conv kernels at the Pong A2C shapes (2,048-frame
+rollout forward, 10,240-frame update backward): per-launch microseconds from HIP events.
+
+    python tools/cnn_kbench.py [--which fwd,bwd3,dgrad2,wgrad1] [--iters 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--which", default="fwd,fwd_layers,bwd3,bwd3_layers,bwd2,dgrad2")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--frames", type=int, default=2048)
+    ap.add_argument("--bwd-frames", type=int, default=10240)
+    a = ap.parse_args()
+    from relayrl_prototype_amd.models.nature_cnn import CONVS, FC_IN, S2D, CNNSpec
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    dev = torch.device("cuda", 0)
+    spec = CNNSpec()
+    o = spec.offsets()
+    p = spec.init(1).to(dev)
+    sh = p.bfloat16()
+    Nf, Nb = a.frames, a.bwd_frames
+    N = max(Nf, Nb)
+    x = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, device=dev)
+    a1 = torch.empty(N * 400 * 32, dtype=torch.bfloat16, device=dev)
+    a2 = torch.empty(N * 81 * 64, dtype=torch.bfloat16, device=dev)
+    a3 = torch.empty(N * FC_IN, dtype=torch.bfloat16, device=dev)
+    da3 = (torch.randn(N * FC_IN, device=dev) * 0.01).bfloat16()
+    da2 = torch.empty_like(a2)
+    da1 = torch.empty_like(a1)
+    cus = int(h.device_cus())
+    part = torch.empty(cus * 64 * 576 * 4, device=dev)
+    bpart = torch.empty(cus * 512 * 4, device=dev)
+    W = {i: (sh[o[f"w{i}"]:o[f"b{i}"]], p[o[f"b{i}"]:o[f"b{i}"] + CONVS[i - 1].cout]) for i in (1, 2, 3)}
+    h.conv_stack_fwd(x, *W[1], *W[2], *W[3], a1, a2, a3, N)  # activations for the backward shapes
+
+    def fwd():
+        h.conv_stack_fwd(x, *W[1], *W[2], *W[3], a1, a2, a3, Nf)
+
+    def probe(k, grid=0):
+        return lambda: h.conv_stack_fwd(x, *W[1], *W[2], *W[3], a1, a2, a3, Nf, probe=k, grid=grid)
+
+    def fwd_layers():
+        src = x
+        for i, (L, y) in enumerate(zip((S2D,) + CONVS[1:], (a1, a2, a3)), 1):
+            h.conv_fwd(src, *W[i], y, Nf, L.hin, L.hin, L.cin, L.k, L.k, L.s, L.cout, True)
+            src = y
+
+    def bwd3():
+        h.conv3_bwd(da3, W[3][0], a2, da2, part, bpart, Nb, min(Nb, cus))
+
+    def bwd3_layers():
+        L = CONVS[2]
+        h.conv_dgrad(da3, W[3][0], a2, da2, Nb, L.hin, L.hin, L.cin, L.k, L.k, L.s, L.cout)
+
+    def dgrad2():
+        L = CONVS[1]
+        h.conv_dgrad(da2, W[2][0], a1, da1, Nb, L.hin, L.hin, L.cin, L.k, L.k, L.s, L.cout)
+
+    fns = {"p_nomfma": probe(1), "p_nostore": probe(2), "p_nostore_nomfma": probe(3), "p_hotframe": probe(4),
+           "p_all": probe(7), "fwd_g128": probe(0, 128), "fwd_g512": probe(0, 512), "fwd": fwd, "fwd_layers": fwd_layers, "bwd3": bwd3, "bwd3_layers": bwd3_layers, "dgrad2": dgrad2}
+    if hasattr(h, "conv2_bwd"):
+        def bwd2():
+            h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus))
+        fns["bwd2"] = bwd2
+    out = {}
+    for name in a.which.split(","):
+        f = fns[name]
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            f()
+        e1.record()
+        torch.cuda.synchronize()
+        out[name] = round(e0.elapsed_time(e1) * 1e3 / a.iters, 1)
+    print(json.dumps({"bench": "cnn_kbench", "frames_fwd": Nf, "frames_bwd": Nb, "us_per_launch": out}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
