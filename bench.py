@@ -81,6 +81,9 @@ def parse(argv=None):
     ap.add_argument("--host-steps", type=int, default=6,
                     help="1 GPU: also time the host-env data path (C++ env threads + the C++ rollout driver, "
                          "cartpole-reinforce-host preset, lag-1 overlap) for this many epochs; 0 = skip")
+    ap.add_argument("--pong-steps", type=int, default=20,
+                    help="1 GPU: also time the A2C Pong pixel update (BASELINE config #4: Nature CNN on bf16 MFMA, "
+                         "2048 envs x 5 steps) for this many updates; 0 = skip")
     ap.add_argument("--al-steps", type=int, default=10)
     ap.add_argument("--al-warmup", type=int, default=5)
     ap.add_argument("--al-env", default="LunarLanderSynth-v0")
@@ -229,6 +232,39 @@ def host_path_probe(steps: int, comm) -> dict:
         if tr is not None:
             tr.close()
             del tr
+        torch.cuda.empty_cache()
+    return rec
+
+
+def pong_probe(steps: int) -> dict:
+    """BASELINE config #4 on one GPU: A2C on PongSynth-v0 pixels (Nature CNN, bf16 MFMA: the
+    fused conv-stack forward and conv backward kernels of csrc/kernels/cnn_fused.hip), 2048
+    envs x 5 steps per update, the whole update captured as one hipGraph; 3 untimed warmup
+    updates, then ``steps`` timed ones.  Reported next to the headline."""
+    import torch
+
+    from relayrl_prototype_amd.runtime.pixel_trainer import PixelA2CConfig, PixelA2CTrainer
+
+    rec = {"config": "A2C PongSynth-v0, Nature-CNN, 2048 envs x 5 steps", "steps": steps, "warmup": 3,
+           "dtype": "bf16 (fp32 accumulate, fp32 master weights)"}
+    tr = None
+    try:
+        cfg = PixelA2CConfig(num_envs=2048, rollout_len=5)
+        tr = PixelA2CTrainer(cfg, device=torch.device("cuda", torch.cuda.current_device()))
+        for _ in range(3):
+            tr.train_epoch()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            tr.train_epoch()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        rec.update(env_steps_per_s=round(steps * cfg.num_envs * cfg.rollout_len / dt, 1),
+                   ms_per_update=round(dt / steps * 1e3, 3))
+    except Exception as e:  # noqa: BLE001 -- recorded; the headline still prints
+        rec["error"] = f"{type(e).__name__}: {e}"[:300]
+    finally:
+        del tr
         torch.cuda.empty_cache()
     return rec
 
@@ -415,6 +451,7 @@ def main(argv=None):
     per_rank_ms = comm.all_gather_object(round(dt_local / args.steps * 1e3, 3))
     phases = phase_probe(tr, comm, args.phase_steps) if args.phase_steps > 0 else None
     host_rec = host_path_probe(args.host_steps, comm) if (on_gpu and world == 1 and args.host_steps > 0) else None
+    pong_rec = pong_probe(args.pong_steps) if (on_gpu and world == 1 and args.pong_steps > 0) else None
     def record(al_rec, ttt=None, ttt_ref=None, ref_cpu=None, do_ttt=False):
         """The ONE JSON line (rank 0)."""
         algo = "REINFORCE" if args.no_baseline else "REINFORCE-with-baseline"
@@ -475,6 +512,8 @@ def main(argv=None):
                                                  "extra epochs after the timed region")
         if host_rec is not None:
             rec["host_env_path"] = host_rec
+        if pong_rec is not None:
+            rec["pong_a2c"] = pong_rec
         if al_rec is not None:
             rec["actor_learner"] = al_rec
         if ref_cpu is not None:

@@ -46,6 +46,8 @@ int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, u
                   float* bias_part, int N, int grid, void* stream);
 int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
                   float* bias_part, int N, int grid, void* stream);
+int rrl_conv1_wgrad8(const uint8_t* x, const uint16_t* dy, float* part, float* bias_part, int N, int grid,
+                     void* stream);
 }
 
 namespace {
@@ -157,6 +159,21 @@ void conv2_bwd(const Tensor& dy, const Tensor& w, const Tensor& xact, const Tens
   rc_check(rrl_conv2_bwd(bf(dy), bf(w), bf(xact), bf(dx), part.data_ptr<float>(), bias_part.data_ptr<float>(),
                          (int)N, (int)grid, stream()),
            "conv2_bwd");
+}
+
+// conv1 weight + bias gradient, 8-wave kernel (cnn_fused.hip): s2d frames [N][21][21][64], da1
+// [N][400][32] -> partials [2 grid][32 * 256] and [2 grid][32]; returns the slab count (2 grid).
+int64_t conv1_wgrad8(const Tensor& x, const Tensor& dy, const Tensor& part, const Tensor& bias_part, int64_t N,
+                     int64_t grid) {
+  TORCH_CHECK(N > 0 && grid > 0 && grid <= N, "conv1_wgrad8: need 0 < grid <= N");
+  check(x, "x", at::kByte, N * 441 * 64);
+  check(dy, "dy", at::kBFloat16, N * 400 * 32);
+  check(part, "part", at::kFloat, 2 * grid * 32 * 256);
+  check(bias_part, "bias_part", at::kFloat, 2 * grid * 32);
+  rc_check(rrl_conv1_wgrad8(x.data_ptr<uint8_t>(), bf(dy), part.data_ptr<float>(), bias_part.data_ptr<float>(), (int)N,
+                            (int)grid, stream()),
+           "conv1_wgrad8");
+  return 2 * grid;
 }
 
 void gemm_dgrad(const Tensor& dy, const Tensor& w, const OptT& mask, const Tensor& out, int64_t M, int64_t Cout,
@@ -348,6 +365,7 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("grid") = 0);
   m.def("conv3_bwd", &conv3_bwd);
   m.def("conv2_bwd", &conv2_bwd);
+  m.def("conv1_wgrad8", &conv1_wgrad8);
   m.def("col2im_mask", &col2im_mask);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("gemm_splits", &gemm_splits);

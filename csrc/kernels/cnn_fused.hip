@@ -724,3 +724,141 @@ extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16
                      dx, part, bias_part, N);
   return (int)hipGetLastError();
 }
+
+// ============================================================================= conv1 wgrad
+// dW1[co][kh][kw][c] (+ db1) of the space-to-depth first layer, 8 waves per workgroup (two per
+// SIMD, where cnn.hip's conv1_wgrad_s2d_kernel ran one): wave w computes tap (kh, kw) =
+// ((w & 3) >> 1, w & 1) over HALF of the 13 position chunks (w >> 2 picks the half), so the
+// two waves of a SIMD hide each other's transposed-read latency; each half leaves its own
+// partial slab (2 per workgroup).  Frame (as exact bf16 integers) and dY go through LDS once
+// per image with the next image prefetched into registers.
+namespace c1w {
+constexpr int kThreads = 512;
+constexpr int kLd = 80;
+constexpr int kXRows = 448, kYRows = 416;
+constexpr int kLds = (kXRows + kYRows) * kLd * 2;  // 138,240 bytes
+constexpr int kXC = 441 * 4, kYC = 400 * 4;       // 16-byte chunks per image
+constexpr int kXPT = (kXC + kThreads - 1) / kThreads, kYPT = (kYC + kThreads - 1) / kThreads;
+}  // namespace c1w
+
+__global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const uint8_t* __restrict__ x,
+                                                                        const uint16_t* __restrict__ dy,
+                                                                        float* __restrict__ part,
+                                                                        float* __restrict__ bias_part, int N) {
+  using namespace c1w;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Xi = smem;                // [448][80] frame, bf16 integers 0..255
+  uint16_t* Yi = smem + kXRows * kLd;  // [416][80] dY (rows 400.. zero)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tap = wave & 3, kh = tap >> 1, kw = tap & 1, half = wave >> 2;
+  const int kc0 = half ? 7 : 0, kc1 = half ? 13 : 7;
+  for (int q = tid; q < 16 * (kLd / 8); q += kThreads)
+    *reinterpret_cast<uint4*>(Yi + (400 + q / (kLd / 8)) * kLd + 8 * (q % (kLd / 8))) = make_uint4(0, 0, 0, 0);
+
+  f32x4_t acc[2][4], accb[2];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    accb[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  // db[co] = sum_p dY[p][co] rides on the tap-(0, 0) waves as an MFMA whose B is 1 in column 0
+  const bool do_bias = tap == 0;
+  bf16x8_t ones;
+  {
+    typedef short s16x8_t __attribute__((ext_vector_type(8)));
+    const short one = (lane & 15) == 0 ? (short)0x3f80 : (short)0;
+    s16x8_t v = {one, one, one, one, one, one, one, one};
+    ones = __builtin_bit_cast(bf16x8_t, v);
+  }
+  uint4 rx[kXPT], ry[kYPT];
+  auto gload = [&](int n) {
+    const uint4* xs = reinterpret_cast<const uint4*>(x + (size_t)n * 441 * 64);
+    const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 400 * 32);
+#pragma unroll
+    for (int i = 0; i < kXPT; ++i) {
+      const int q = tid + kThreads * i;
+      rx[i] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < kYPT; ++i) {
+      const int q = tid + kThreads * i;
+      ry[i] = q < kYC ? ys[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int n0 = blockIdx.x, G = gridDim.x;
+  if (n0 < N) gload(n0);
+  for (int n = n0; n < N; n += G) {
+    __syncthreads();  // the previous image's fragment reads are done
+#pragma unroll
+    for (int i = 0; i < kXPT; ++i) {
+      const int q = tid + kThreads * i;
+      if (q < kXC) {
+        uint16_t* d = Xi + (q >> 2) * kLd + (q & 3) * 16;
+        *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(rx[i].x, rx[i].y));
+        *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(rx[i].z, rx[i].w));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kYPT; ++i) {
+      const int q = tid + kThreads * i;
+      if (q < kYC) *reinterpret_cast<uint4*>(Yi + (q >> 2) * kLd + (q & 3) * 8) = ry[i];
+    }
+    if (n + G < N) gload(n + G);
+    __syncthreads();
+    // MFMA k-order: lane group g of a 32-pixel chunk takes pixels 4g..4g+3 and 16+4g..16+4g+3
+    // (a 4-pixel run never crosses an output row, so its frame rows are consecutive)
+#pragma unroll 1
+    for (int kc = kc0; kc < kc1; ++kc) {
+      const int pa = 32 * kc + 4 * g, pb = pa + 16;
+      const int ra = (pa < 400 ? (pa / 20 + kh) * 21 + pa % 20 + kw : 0) + qq;
+      const int rb = (pb < 400 ? (pb / 20 + kh) * 21 + pb % 20 + kw : 0) + qq;
+      bf16x8_t af[2], bfr[4];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+        af[mt] = tr_frag2(Yi + (pa + qq) * kLd + 16 * mt + 4 * pp, Yi + (pb + qq) * kLd + 16 * mt + 4 * pp);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        bfr[nt] = tr_frag2(Xi + ra * kLd + 16 * nt + 4 * pp, Xi + rb * kLd + 16 * nt + 4 * pp);
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) accb[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], ones, accb[mt], 0, 0, 0);
+      }
+    }
+  }
+  const int slab = 2 * blockIdx.x + half;
+  if (do_bias && (lane & 15) == 0) {
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias_part[(size_t)slab * 32 + 16 * mt + 4 * g + r] = accb[mt][r];
+  }
+  // part[slab][cout][kh][kw][c], raw-byte products scaled by 1/255
+  float* o = part + (size_t)slab * 32 * 256 + kh * 128 + kw * 64;
+  const int j = lane & 15;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[(16 * mt + 4 * g + r) * 256 + 16 * nt + j] = acc[mt][nt][r] * kU8Scale;
+}
+
+// returns the number of partial slabs written (2 per workgroup)
+extern "C" int rrl_conv1_wgrad8(const uint8_t* x, const uint16_t* dy, float* part, float* bias_part, int N, int grid,
+                                void* stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv1_wgrad8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c1w::kLds);
+    attr = true;
+  }
+  if (N < 1 || grid < 1) return 0;
+  hipLaunchKernelGGL(conv1_wgrad8_kernel, dim3(grid), dim3(c1w::kThreads), c1w::kLds, (hipStream_t)stream, x, dy, part,
+                     bias_part, N);
+  return (int)hipGetLastError();
+}

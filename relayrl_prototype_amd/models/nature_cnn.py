@@ -355,8 +355,13 @@ class DeviceNatureCNN:
             self._dgrad(da2, sh[o["w2"]:o["b2"]], a1, da1, B, L2)
         # conv1 (input = frames, no data gradient)
         # (its bias gradient comes out of the same pass over da1)
-        self._wgrad("c1", da1, obs_u8.contiguous(), B, S2D.hin, S2D.cin, S2D.k, S2D.s, S2D.cout, o["w1"],
-                    bias_off=o["b1"])
+        if self.fused_convs:
+            ns = int(h.conv1_wgrad8(obs_u8.contiguous(), da1, self.part, self.bias_part, B, min(B, self.cus)))
+            h.sum_splits(self.part, ns, S2D.cout * S2D.K, g[o["w1"]:o["b1"]])
+            h.sum_splits(self.bias_part, ns, S2D.cout, g[o["b1"]:o["b1"] + S2D.cout])
+        else:
+            self._wgrad("c1", da1, obs_u8.contiguous(), B, S2D.hin, S2D.cin, S2D.k, S2D.s, S2D.cout, o["w1"],
+                        bias_off=o["b1"])
         if pending is not None:
             comm.all_reduce_sum_(g[:o["wfc"]])
             pending.wait()

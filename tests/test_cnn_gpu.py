@@ -527,3 +527,25 @@ def test_fused_conv_bwd_kernels_match_autograd(cuda, li, N, grid):
     assert relerr(dw, dw_ref) < 1e-3
     db = bpart.view(grid * 8, 64).sum(0).cpu()
     assert relerr(db, db_ref) < 1e-3
+
+
+@pytest.mark.parametrize("N,grid", [(1, 1), (9, 4), (300, 64)])
+def test_conv1_wgrad8_matches_autograd(cuda, N, grid):
+    """8-wave conv1 weight / bias gradient (cnn_fused.hip) vs fp32 autograd on the s2d frames."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    g = torch.Generator().manual_seed(N)
+    x = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g)
+    dy = _bf(torch.randn(N, 20, 20, 32, generator=g))
+    part = torch.full((2 * grid * 32 * 256,), float("nan"), device=cuda)
+    bpart = torch.full((2 * grid * 32,), float("nan"), device=cuda)
+    ns = h.conv1_wgrad8(x.to(cuda), dy.to(cuda).bfloat16().reshape(-1), part, bpart, N, grid)
+    assert ns == 2 * grid
+    dw = part.view(ns, -1).sum(0).cpu()
+    db = bpart.view(ns, 32).sum(0).cpu()
+    w = torch.zeros(32, 8, 8, 4, requires_grad=True)
+    y = F.conv2d(obs_to_nchw(x), w.permute(0, 3, 1, 2), stride=4)
+    y.backward(dy.permute(0, 3, 1, 2))
+    assert relerr(dw, conv1_khkwc_to_s2d(w.grad).reshape(-1)) < 1e-3
+    assert relerr(db, dy.sum((0, 1, 2))) < 1e-3

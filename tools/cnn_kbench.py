@@ -16,7 +16,7 @@ import torch
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", default="fwd,fwd_layers,bwd3,bwd3_layers,bwd2,dgrad2")
+    ap.add_argument("--which", default="fwd,fwd_layers,bwd3,bwd3_layers,bwd2,dgrad2,wgrad1,wgrad1_8")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--frames", type=int, default=2048)
     ap.add_argument("--bwd-frames", type=int, default=10240)
@@ -68,8 +68,11 @@ def main():
         L = CONVS[1]
         h.conv_dgrad(da2, W[2][0], a1, da1, Nb, L.hin, L.hin, L.cin, L.k, L.k, L.s, L.cout)
 
-    fns = {"p_nomfma": probe(1), "p_nostore": probe(2), "p_nostore_nomfma": probe(3), "p_hotframe": probe(4),
-           "p_all": probe(7), "fwd_g128": probe(0, 128), "fwd_g512": probe(0, 512), "fwd": fwd, "fwd_layers": fwd_layers, "bwd3": bwd3, "bwd3_layers": bwd3_layers, "dgrad2": dgrad2}
+    fns = {}
+    fns["wgrad1_8"] = lambda: h.conv1_wgrad8(x[:Nb], da1, part, bpart, Nb, min(Nb, cus))
+    fns["wgrad1"] = lambda: h.conv_wgrad(da1, x[:Nb], part, 256, Nb, 21, 21, 64, 2, 2, 1, 32, bpart)
+    fns.update({"p_nomfma": probe(1), "p_nostore": probe(2), "p_nostore_nomfma": probe(3), "p_hotframe": probe(4),
+           "p_all": probe(7), "fwd_g128": probe(0, 128), "fwd_g512": probe(0, 512), "fwd": fwd, "fwd_layers": fwd_layers, "bwd3": bwd3, "bwd3_layers": bwd3_layers, "dgrad2": dgrad2})
     if hasattr(h, "conv2_bwd"):
         def bwd2():
             h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus))
