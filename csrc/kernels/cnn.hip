@@ -235,7 +235,22 @@ __global__ void __launch_bounds__(256) sum_splits_kernel(const float* __restrict
   const size_t n4 = n / 4;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   if (i4 < n4) {
-    for (int z = ph; z < splits; z += 16) {
+    // 8 slab loads in flight per thread (the fused conv backward kernels leave 256-512
+    // slabs of 8-37 K floats: one load per iteration was latency-bound)
+    int z = ph;
+    for (; z + 7 * 16 < splits; z += 8 * 16) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = reinterpret_cast<const float4*>(part + (size_t)(z + 16 * u) * n)[i4];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a.x += v[u].x;
+        a.y += v[u].y;
+        a.z += v[u].z;
+        a.w += v[u].w;
+      }
+    }
+    for (; z < splits; z += 16) {
       const float4 v = reinterpret_cast<const float4*>(part + (size_t)z * n)[i4];
       a.x += v.x;
       a.y += v.y;

@@ -62,7 +62,7 @@ constexpr int kThreads = 512;
 constexpr int kFrameLd = 80;                  // frame row: 64 channels + 16 pad (bf16)
 constexpr int kFrameRows = 441;               // 21 x 21 s2d pixels
 constexpr int kA1Ld = 40;                     // a1 row: 32 co + 8 pad
-constexpr int kA2Ld = 72;                     // a2 / a3 rows: 64 co + 8 pad
+constexpr int kA2Ld = 80;                     // a2 / a3 rows: 64 co + 16 pad (72 measured 2.5x conflict cycles on the conv3 reads, 80 1.75x)
 constexpr int kXi = 0;                                    // element offsets into LDS
 constexpr int kA1 = kXi + kFrameRows * kFrameLd;          // 35,280
 constexpr int kA2 = kA1 + 400 * kA1Ld;                    // 51,280 (two buffers of 81 rows)
