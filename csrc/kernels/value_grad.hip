@@ -120,11 +120,13 @@ struct Split8HM {  // hi + mid pieces (the lo piece of a stationary weight fragm
 
 typedef float vf32x2 __attribute__((ext_vector_type(2)));
 
-// Two fp32 -> packed bf16 pair (round to nearest even), a in the low half.
+// Two fp32 -> packed bf16 pair (round to nearest even), a in the low half.  A vector
+// conversion (lowers to v_cvt_pk_bf16_f32 on gfx950), not inline asm: the compiler's hazard
+// recognizer does not see into asm, and an asm convert that reads an MFMA result got no
+// wait states (a NaN-producing bug in cnn_fused.hip's first conv2 backward).
 RRL_DEV uint32_t cvt_pk_bf16(float a, float b) {
-  uint32_t r;
-  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
+  typedef __bf16 vbf16x2_cvt __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((vf32x2{a, b}), vbf16x2_cvt));
 }
 // The packed pair back as two fp32 (exact).
 RRL_DEV vf32x2 unpack_bf16(uint32_t p) {
