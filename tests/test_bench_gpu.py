@@ -51,7 +51,8 @@ def test_bench_two_ranks_gloo_shared_gpu(cuda):
     env = dict(os.environ, RRL_DIST_BACKEND="gloo", RRL_FORCE_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus", "2", "--steps", "2",
-           "--warmup", "1", "--num-envs", "1024", "--vf-iters", "4"]
+           "--warmup", "1", "--num-envs", "1024", "--vf-iters", "4", "--al-num-envs", "256", "--al-rollout-len", "32",
+           "--al-vf-iters", "8"]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     recs = _json_lines(r.stdout)
@@ -61,6 +62,13 @@ def test_bench_two_ranks_gloo_shared_gpu(cuda):
     assert rec["config"]["parallelism"] == "dp2"
     assert rec["config"]["global_batch"] == 2 * 1024 * 64  # weak scaling: per-rank envs fixed
     assert "time_to_threshold_s" not in rec
+    # the secondary actor -> learner phase ran on the GPU: device-env rollouts on both ranks, the
+    # remote rollout received into the learner's shard batch (K = 2), weights sent back with lag 1
+    al = rec["actor_learner"]
+    assert "error" not in al, al
+    assert al["K"] == 2 and al["L"] == 1 and al["versions_ok"] is True and al["env_steps_per_s"] > 0
+    assert al["per_rank"][0]["role"] == "learner" and al["per_rank"][1]["role"] == "actor"
+    assert al["gather_ms"][0] > 0 and al["weight_recv_ms"][1] is not None
 
 
 def test_bench_two_rccl_ranks(cuda):
