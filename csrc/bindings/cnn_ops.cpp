@@ -45,7 +45,7 @@ int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, co
 int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
                   float* bias_part, int N, int grid, void* stream);
 int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
-                  float* bias_part, int N, int grid, void* stream);
+                  float* bias_part, int N, int grid, int staged, void* stream);
 int rrl_conv1_wgrad8(const uint8_t* x, const uint16_t* dy, float* part, float* bias_part, int N, int grid,
                      void* stream);
 }
@@ -148,7 +148,7 @@ void conv3_bwd(const Tensor& dy, const Tensor& w, const Tensor& xact, const Tens
 // Fused conv2 backward (cnn_fused.hip): da2 [N][81][64], W2 [64][4][4][32], a1 [N][400][32] ->
 // da1 = dgrad * (a1 > 0), dW2 partials [grid][64 * 512], db2 partials [grid * 8][64].
 void conv2_bwd(const Tensor& dy, const Tensor& w, const Tensor& xact, const Tensor& dx, const Tensor& part,
-               const Tensor& bias_part, int64_t N, int64_t grid) {
+               const Tensor& bias_part, int64_t N, int64_t grid, int64_t staged) {
   TORCH_CHECK(N > 0 && grid > 0 && grid <= N, "conv2_bwd: need 0 < grid <= N");
   check(dy, "dy", at::kBFloat16, N * 81 * 64);
   check(w, "w", at::kBFloat16, 64 * 512);
@@ -157,7 +157,7 @@ void conv2_bwd(const Tensor& dy, const Tensor& w, const Tensor& xact, const Tens
   check(part, "part", at::kFloat, grid * 64 * 512);
   check(bias_part, "bias_part", at::kFloat, grid * 512);
   rc_check(rrl_conv2_bwd(bf(dy), bf(w), bf(xact), bf(dx), part.data_ptr<float>(), bias_part.data_ptr<float>(),
-                         (int)N, (int)grid, stream()),
+                         (int)N, (int)grid, (int)staged, stream()),
            "conv2_bwd");
 }
 
@@ -364,7 +364,9 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("y2"), pybind11::arg("y3"), pybind11::arg("N"), pybind11::arg("probe") = 0,
         pybind11::arg("grid") = 0);
   m.def("conv3_bwd", &conv3_bwd);
-  m.def("conv2_bwd", &conv2_bwd);
+  m.def("conv2_bwd", &conv2_bwd, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("xact"), pybind11::arg("dx"),
+        pybind11::arg("part"), pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"),
+        pybind11::arg("staged") = 0);
   m.def("conv1_wgrad8", &conv1_wgrad8);
   m.def("col2im_mask", &col2im_mask);
   m.def("conv_dgrad", &conv_dgrad);

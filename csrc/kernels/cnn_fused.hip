@@ -74,7 +74,8 @@ static_assert(kA1 % 8 == 0 && kA2 % 8 == 0 && kA3 % 8 == 0, "16-byte aligned LDS
 }  // namespace cs
 
 // PROBE (tools/cnn_kbench.py --probe, timing only -- outputs are garbage when != 0):
-// bit 0 skips the MFMAs, bit 1 the global stores, bit 2 re-reads frame 0 (L2-hot)
+// bit 0 skips the MFMAs, bit 1 the global stores, bit 2 re-reads frame 0 (L2-hot), bit 3
+// runs conv1 with one co tile per wave
 template <int PROBE>
 __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
     const uint8_t* __restrict__ x, const uint16_t* __restrict__ w1, const float* __restrict__ b1,
@@ -92,10 +93,18 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
   const int ct = wave & 3;  // co tile of conv2 (A) / conv3 (B)
 
   // stationary weights: B fragment = W[co][8 consecutive k], co = 16 * tile + i
-  const int c1 = wave & 1;
-  bf16x8_t f1[8], fw[18];  // fw: W2 (16 k-steps) on A waves, W3 (18) on B waves
+  // conv1: with C1BOTH (default) every wave computes both co tiles of its pixel tiles (each
+  // frame fragment read feeds two MFMAs; W1 for both tiles in registers): 63.6 -> 59.2 us per
+  // 2,048 frames; PROBE bit 3 selects the one-co-tile-per-wave split for comparison
+  constexpr bool C1BOTH = (PROBE & 8) == 0;
+  const int c1 = C1BOTH ? 0 : (wave & 1);
+  bf16x8_t f1[8], f1b[C1BOTH ? 8 : 1], fw[18];  // fw: W2 (16 k-steps) on A waves, W3 (18) on B waves
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) f1[ks] = *reinterpret_cast<const bf16x8_t*>(w1 + (16 * c1 + i) * 256 + 32 * ks + 8 * g);
+  if (C1BOTH) {
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) f1b[C1BOTH ? ks : 0] = *reinterpret_cast<const bf16x8_t*>(w1 + (16 + i) * 256 + 32 * ks + 8 * g);
+  }
   if (role_a) {
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) fw[ks] = *reinterpret_cast<const bf16x8_t*>(w2 + (16 * ct + i) * 512 + 32 * ks + 8 * g);
@@ -106,6 +115,7 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
   }
   // biases of this lane's 4 output channels (co = 16 tile + 4 g + r)
   const f32x4_t bias1 = *reinterpret_cast<const f32x4_t*>(b1 + 16 * c1 + 4 * g);
+  const f32x4_t bias1b = *reinterpret_cast<const f32x4_t*>(b1 + 16 + 4 * g);  // co tile 1 (C1BOTH)
   const f32x4_t bias23 = *reinterpret_cast<const f32x4_t*>((role_a ? b2 : b3) + 16 * ct + 4 * g);
 
   const int G = gridDim.x, n0 = blockIdx.x;
@@ -149,8 +159,46 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
       uint4* yd = reinterpret_cast<uint4*>(y3 + (size_t)(n - 2 * G) * 49 * 64);
       for (int q = tid; q < 49 * 8; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A3 + (q >> 3) * kA2Ld + (q & 7) * 8);
     }
+    // ---- conv1, C1BOTH: pixel tiles wave + 8 t (t < 3, and t = 3 on wave 0), both co tiles
+    if (cur && C1BOTH) {
+      constexpr int MT = 4;
+      f32x4_t acc0[MT], acc1[MT];
+      int r0[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        acc0[t] = acc1[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        const int p = 16 * min(wave + 8 * t, 24) + i;
+        r0[t] = (p / 20) * 21 + p % 20;
+      }
+      const int nt = wave == 0 ? 4 : 3;  // wave-uniform
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int tap = ks >> 1;
+        const int off = ((tap >> 1) * 21 + (tap & 1)) * kFrameLd + 32 * (ks & 1) + 8 * g;
+        bf16x8_t a[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+          if (t < nt) a[t] = *reinterpret_cast<const bf16x8_t*>(Xi + r0[t] * kFrameLd + off);
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+          if (t < nt) {
+            acc0[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[ks], a[t], acc0[t], 0, 0, 0);
+            acc1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1b[C1BOTH ? ks : 0], a[t], acc1[t], 0, 0, 0);
+          }
+      }
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+        if (t < nt) {
+          uint16_t* dst = A1 + (16 * (wave + 8 * t) + i) * kA1Ld + 4 * g;
+          store4_bf16(dst, fmaxf(kU8Scale * acc0[t][0] + bias1[0], 0.f), fmaxf(kU8Scale * acc0[t][1] + bias1[1], 0.f),
+                      fmaxf(kU8Scale * acc0[t][2] + bias1[2], 0.f), fmaxf(kU8Scale * acc0[t][3] + bias1[3], 0.f));
+          store4_bf16(dst + 16, fmaxf(kU8Scale * acc1[t][0] + bias1b[0], 0.f),
+                      fmaxf(kU8Scale * acc1[t][1] + bias1b[1], 0.f), fmaxf(kU8Scale * acc1[t][2] + bias1b[2], 0.f),
+                      fmaxf(kU8Scale * acc1[t][3] + bias1b[3], 0.f));
+        }
+    }
     // ---- conv1 (all waves): pixel tiles (wave >> 1) + 4 t, co tile c1
-    if (cur) {
+    if (cur && !C1BOTH) {
       constexpr int MT = 7;
       f32x4_t acc[MT];
       int r0[MT];
@@ -294,6 +342,7 @@ extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const fl
     case 3: return launch_conv_stack_fwd<3>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 4: return launch_conv_stack_fwd<4>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 7: return launch_conv_stack_fwd<7>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 8: return launch_conv_stack_fwd<8>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     default: return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
   }
 }
@@ -539,6 +588,9 @@ __device__ __forceinline__ bf16x8_t tr_frag2(const uint16_t* a0, const uint16_t*
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// STAGED: da1 goes through an LDS tile [400][40] and leaves as 16-byte row chunks after a
+// second barrier, instead of 8-byte stores straight from the MFMA registers
+template <bool STAGED>
 __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint16_t* __restrict__ dy,
                                                                      const uint16_t* __restrict__ w,
                                                                      const uint16_t* __restrict__ xact,
@@ -689,7 +741,9 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
           const uint2 m = *reinterpret_cast<const uint2*>(P + (cls * kPRows + a * 10 + b) * kPLd + 16 * ct + 4 * g);
           const uint2 v = make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x),
                                      relu_mask2(pk_bf16(acc[u][2], acc[u][3]), m.y));
-          *reinterpret_cast<uint2*>(dx + ((size_t)n * 400 + (ph + 2 * a) * 20 + pw + 2 * b) * 32 + 16 * ct + 4 * g) = v;
+          const int pix = (ph + 2 * a) * 20 + pw + 2 * b;
+          if (STAGED) *reinterpret_cast<uint2*>(smem + 2 * kBuf + pix * 40 + 16 * ct + 4 * g) = v;
+          else *reinterpret_cast<uint2*>(dx + ((size_t)n * 400 + pix) * 32 + 16 * ct + 4 * g) = v;
         }
       }
     };
@@ -699,6 +753,12 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
     for (int pos = tid >> 6; pos < 81; pos += 8) {
       const int oh = pos / 9, ow = pos - oh * 9;
       bsum += bf2f(D[((oh + 1) * 12 + ow + 1) * kDLd + (tid & 63)]);
+    }
+    if (STAGED) {
+      __syncthreads();  // staging tile complete (rewritten only after the next top barrier)
+      const uint16_t* O = smem + 2 * kBuf;
+      uint4* xd = reinterpret_cast<uint4*>(dx + (size_t)n * 400 * 32);
+      for (int q = tid; q < 400 * 4; q += kThreads) xd[q] = *reinterpret_cast<const uint4*>(O + (q >> 2) * 40 + (q & 3) * 8);
     }
   }
   // weight-gradient partial of this workgroup: part[blk][co][kh][kw][c]
@@ -712,16 +772,25 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
   bias_part[(size_t)blockIdx.x * kThreads + tid] = bsum;
 }
 
+// staged != 0: da1 through the LDS staging tile (measured slower: 229 vs 214 us, tools/cnn_kbench.py bwd2 / bwd2_direct)
 extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
-                             float* bias_part, int N, int grid, void* stream) {
+                             float* bias_part, int N, int grid, int staged, void* stream) {
   static bool attr = false;
+  constexpr int kStagedLds = c2b::kLds + 400 * 40 * 2;  // 147,712 bytes
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c2b::kLds);
+    (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              c2b::kLds);
+    (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kStagedLds);
     attr = true;
   }
   if (N < 1 || grid < 1) return 0;
-  hipLaunchKernelGGL(conv2_bwd_kernel, dim3(grid), dim3(c2b::kThreads), c2b::kLds, (hipStream_t)stream, dy, w, xact,
-                     dx, part, bias_part, N);
+  if (staged != 0)
+    hipLaunchKernelGGL(conv2_bwd_kernel<true>, dim3(grid), dim3(c2b::kThreads), kStagedLds, (hipStream_t)stream, dy, w,
+                       xact, dx, part, bias_part, N);
+  else
+    hipLaunchKernelGGL(conv2_bwd_kernel<false>, dim3(grid), dim3(c2b::kThreads), c2b::kLds, (hipStream_t)stream, dy,
+                       w, xact, dx, part, bias_part, N);
   return (int)hipGetLastError();
 }
 

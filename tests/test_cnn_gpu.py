@@ -495,8 +495,9 @@ def test_fused_conv_backward_matches_per_layer(cuda, B):
         assert relerr(gf[b0:b0 + L.cout], gr[b0:b0 + L.cout]) < 1e-4, f"b{i}"
 
 
-@pytest.mark.parametrize("li,N,grid", [(1, 3, 3), (1, 70, 16), (2, 5, 5), (2, 300, 64)])
-def test_fused_conv_bwd_kernels_match_autograd(cuda, li, N, grid):
+@pytest.mark.parametrize("li,N,grid,staged", [(1, 3, 3, 1), (1, 70, 16, 1), (1, 70, 16, 0), (2, 5, 5, 1),
+                                              (2, 300, 64, 1)])
+def test_fused_conv_bwd_kernels_match_autograd(cuda, li, N, grid, staged):
     """conv2_bwd / conv3_bwd (cnn_fused.hip) against fp32 autograd on the same bf16 operands:
     masked data gradient, weight-gradient partials (summed over workgroups), bias partials."""
     from relayrl_prototype_amd.ops import hip
@@ -511,7 +512,10 @@ def test_fused_conv_bwd_kernels_match_autograd(cuda, li, N, grid):
     dx = torch.full((N * L.hin * L.hin * L.cin,), float("nan"), dtype=torch.bfloat16, device=cuda)
     part = torch.full((grid * L.cout * L.K,), float("nan"), device=cuda)
     bpart = torch.full((grid * 512,), float("nan"), device=cuda)
-    (h.conv2_bwd if li == 1 else h.conv3_bwd)(dyd.reshape(-1), wd.reshape(-1), xd.reshape(-1), dx, part, bpart, N, grid)
+    if li == 1:
+        h.conv2_bwd(dyd.reshape(-1), wd.reshape(-1), xd.reshape(-1), dx, part, bpart, N, grid, staged=staged)
+    else:
+        h.conv3_bwd(dyd.reshape(-1), wd.reshape(-1), xd.reshape(-1), dx, part, bpart, N, grid)
     torch.cuda.synchronize()
     xr = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
     wr = w.permute(0, 3, 1, 2).clone().requires_grad_(True)
