@@ -32,7 +32,13 @@ int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, i
                  float* value, float* logits_out, unsigned long long seed, unsigned long long step,
                  const unsigned long long* step_base, int row_offset,
                  const int32_t* act_in, const float* adv, const float* ret, float inv_B, float vf_coef,
-                 float ent_coef, uint16_t* dh, float* dhead, float* stats, int grid, void* stream);
+                 float ent_coef, uint16_t* dh, float* dhead, float* stats, int grid, const float* part,
+                 int splits, const float* fc_b, uint16_t* h_out, void* stream);
+int rrl_fc_nt_part(const uint16_t* a, const uint16_t* b, float* part, int M, int N, int K, int splits, void* stream);
+int rrl_fc_nt_mask(const uint16_t* a, const uint16_t* b, const uint16_t* mask, uint16_t* out, int M, int N, int K,
+                   void* stream);
+int rrl_transpose_bf16(const uint16_t* in, uint16_t* out, int R, int C, void* stream);
+int rrl_fc_tn_part(const uint16_t* x, const uint16_t* y, float* part, int R, int I, int J, int splits, void* stream);
 int rrl_head_wgrad(const uint16_t* h, const float* dhead, int B, int A, float* part, int nblk, void* stream);
 int rrl_pong_state_size();
 int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
@@ -290,7 +296,7 @@ void a2c_head(int64_t mode, const Tensor& h, const Tensor& head_params, int64_t 
               const OptT& logp, const OptT& value, const OptT& logits, int64_t seed, int64_t step,
               int64_t row_offset, const OptT& act_in, const OptT& adv, const OptT& ret, double inv_B, double vf_coef,
               double ent_coef, const OptT& dh, const OptT& dhead, const OptT& stats, int64_t grid,
-              const OptT& step_base) {
+              const OptT& step_base, const OptT& part, int64_t splits, const OptT& fc_b) {
   constexpr int64_t F = 512;
   TORCH_CHECK(A >= 1 && A <= 16, "a2c_head: 1 <= A <= 16");
   TORCH_CHECK(mode == 0 || mode == 1, "a2c_head: mode must be 0 (rollout) or 1 (train)");
@@ -310,10 +316,61 @@ void a2c_head(int64_t mode, const Tensor& h, const Tensor& head_params, int64_t 
   if (mode == 1)
     TORCH_CHECK(ai && ad && re && dhp && dhd && st, "a2c_head train mode needs act_in, adv, ret, dh, dhead, stats");
   const unsigned long long* sb = opt_ptr<const unsigned long long>(step_base, "step_base", at::kLong, 1);
+  // part given: h is an OUTPUT, bf16(relu(fc_b + sum of the split-K partials)) (fc.hip)
+  const float* pp = opt_ptr<const float>(part, "part", at::kFloat, splits * B * F);
+  const float* fb = opt_ptr<const float>(fc_b, "fc_b", at::kFloat, pp ? F : 0);
+  if (pp) TORCH_CHECK(mode == 0 && fb && splits >= 1, "a2c_head: part needs mode 0, fc_b and splits >= 1");
   rc_check(rrl_a2c_head((int)mode, bf(h), head_params.data_ptr<float>(), B, A, ap, lp, vp, lo, (uint64_t)seed,
                         (uint64_t)step, sb, (int)row_offset, ai, ad, re, (float)inv_B, (float)vf_coef, (float)ent_coef,
-                        dhp, dhd, st, (int)grid, stream()),
+                        dhp, dhd, st, (int)grid, pp, (int)splits, fb, pp ? bf(h) : nullptr, stream()),
            "a2c_head");
+}
+
+// fp32 split-K partials part[splits][M][N] of a[M][K] . b[N][K]^T (fc.hip); returns the
+// number of splits used.
+int64_t fc_nt_part(const Tensor& a, const Tensor& b, const Tensor& part, int64_t M, int64_t N, int64_t K,
+                   int64_t splits) {
+  TORCH_CHECK(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 4 == 0 && splits >= 1, "fc_nt_part: bad shape");
+  check(a, "a", at::kBFloat16, M * K);
+  check(b, "b", at::kBFloat16, N * K);
+  const int64_t kt = K / 64, kps = (kt + splits - 1) / splits, used = (kt + kps - 1) / kps;
+  check(part, "part", at::kFloat, used * M * N);
+  const int rc = rrl_fc_nt_part(bf(a), bf(b), part.data_ptr<float>(), M, N, K, (int)splits, stream());
+  TORCH_CHECK(rc > 0, "fc_nt_part failed with code ", rc);
+  return rc;
+}
+
+// out[M][N] = (a[M][K] . b[N][K]^T) * (mask[M][N] > 0), bf16 (fc.hip)
+void fc_nt_mask(const Tensor& a, const Tensor& b, const Tensor& mask, const Tensor& out, int64_t M, int64_t N,
+                int64_t K) {
+  TORCH_CHECK(M > 0 && N > 0 && K > 0 && K % 64 == 0 && N % 4 == 0, "fc_nt_mask: bad shape");
+  check(a, "a", at::kBFloat16, M * K);
+  check(b, "b", at::kBFloat16, N * K);
+  check(mask, "mask", at::kBFloat16, M * N);
+  check(out, "out", at::kBFloat16, M * N);
+  rc_check(rrl_fc_nt_mask(bf(a), bf(b), bf(mask), bf(out), M, N, K, stream()), "fc_nt_mask");
+}
+
+// fp32 partials part[splits][I][J] of x[R][I]^T . y[R][J] (fc.hip, the fc weight gradient);
+// returns the number of splits used.
+int64_t fc_tn_part(const Tensor& x, const Tensor& y, const Tensor& part, int64_t R, int64_t I, int64_t J,
+                   int64_t splits) {
+  TORCH_CHECK(R >= 64 && R % 64 == 0 && I > 0 && J > 0 && I % 8 == 0 && J % 8 == 0 && splits >= 1,
+              "fc_tn_part: bad shape");
+  check(x, "x", at::kBFloat16, R * I);
+  check(y, "y", at::kBFloat16, R * J);
+  const int64_t rt = R / 64, kps = (rt + splits - 1) / splits, used = (rt + kps - 1) / kps;
+  check(part, "part", at::kFloat, used * I * J);
+  const int rc = rrl_fc_tn_part(bf(x), bf(y), part.data_ptr<float>(), R, I, J, (int)splits, stream());
+  TORCH_CHECK(rc > 0, "fc_tn_part failed with code ", rc);
+  return rc;
+}
+
+void transpose_bf16(const Tensor& in, const Tensor& out, int64_t R, int64_t C) {
+  TORCH_CHECK(R > 0 && C > 0 && R % 8 == 0 && C % 8 == 0, "transpose_bf16: R, C must be multiples of 8");
+  check(in, "in", at::kBFloat16, R * C);
+  check(out, "out", at::kBFloat16, R * C);
+  rc_check(rrl_transpose_bf16(bf(in), bf(out), R, C, stream()), "transpose_bf16");
 }
 
 void head_wgrad(const Tensor& h, const Tensor& dhead, int64_t B, int64_t A, const Tensor& part, int64_t nblk) {
@@ -389,7 +446,13 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("logits"), pybind11::arg("seed"), pybind11::arg("step"), pybind11::arg("row_offset"),
         pybind11::arg("act_in"), pybind11::arg("adv"), pybind11::arg("ret"), pybind11::arg("inv_B"),
         pybind11::arg("vf_coef"), pybind11::arg("ent_coef"), pybind11::arg("dh"), pybind11::arg("dhead"),
-        pybind11::arg("stats"), pybind11::arg("grid"), pybind11::arg("step_base") = pybind11::none());
+        pybind11::arg("stats"), pybind11::arg("grid"), pybind11::arg("step_base") = pybind11::none(),
+        pybind11::arg("part") = pybind11::none(), pybind11::arg("splits") = 0,
+        pybind11::arg("fc_b") = pybind11::none());
+  m.def("fc_nt_part", &fc_nt_part);
+  m.def("fc_nt_mask", &fc_nt_mask);
+  m.def("transpose_bf16", &transpose_bf16);
+  m.def("fc_tn_part", &fc_tn_part);
   m.def("head_wgrad", &head_wgrad);
   m.def("pong_state_size", &pong_state_size);
   m.def("pong_step", &pong_step, pybind11::arg("state"), pybind11::arg("act"), pybind11::arg("rew"),

@@ -424,6 +424,12 @@ struct HeadArgs {
   uint16_t* dh;           // [B][F] grad wrt fc pre-activation (masked), bf16
   float* dhead;           // [B][A+1] fp32: dlogits, dv
   float* stats;           // [gridDim.x][4]: pg loss, vf loss, entropy, count
+  // rollout mode straight from the fc GEMM's split-K partials (fc.hip): h = bf16(relu(
+  // fc_b + sum_z part[z][row][:])) is formed here and written to h_out for the backward
+  const float* part;      // [splits][B][F] or null (then h is read)
+  int splits;
+  const float* fc_b;      // [F]
+  uint16_t* h_out;        // [B][F]
 };
 
 template <bool TRAIN>
@@ -438,7 +444,27 @@ __global__ void __launch_bounds__(256) a2c_head_kernel(HeadArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float st_pg = 0.f, st_vf = 0.f, st_ent = 0.f, st_n = 0.f;
   for (int row = blockIdx.x * 4 + wave; row < a.B; row += gridDim.x * 4) {
-    const uint4 hv = *reinterpret_cast<const uint4*>(a.h + (size_t)row * F + 8 * lane);
+    uint4 hv;
+    if (!TRAIN && a.part) {
+      // split-K reduction + bias + ReLU + bf16 rounding (the order bias_act_kernel uses)
+      const float4 b0 = *reinterpret_cast<const float4*>(a.fc_b + 8 * lane);
+      const float4 b1 = *reinterpret_cast<const float4*>(a.fc_b + 8 * lane + 4);
+      float v[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      const float* pr = a.part + (size_t)row * F + 8 * lane;
+      const size_t zs = (size_t)a.B * F;
+      for (int z = 0; z < a.splits; ++z) {
+        const float4 p0 = *reinterpret_cast<const float4*>(pr + z * zs);
+        const float4 p1 = *reinterpret_cast<const float4*>(pr + z * zs + 4);
+        v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
+        v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      hv = pack_bf16x8(v);
+      *reinterpret_cast<uint4*>(a.h_out + (size_t)row * F + 8 * lane) = hv;
+    } else {
+      hv = *reinterpret_cast<const uint4*>(a.h + (size_t)row * F + 8 * lane);
+    }
     const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w};
     float x[8];
 #pragma unroll
@@ -1391,10 +1417,16 @@ int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, i
                  float* value, float* logits_out, unsigned long long seed, unsigned long long step,
                  const unsigned long long* step_base, int row_offset,
                  const int32_t* act_in, const float* adv, const float* ret, float inv_B, float vf_coef,
-                 float ent_coef, uint16_t* dh, float* dhead, float* stats, int grid, void* stream_) {
+                 float ent_coef, uint16_t* dh, float* dhead, float* stats, int grid, const float* part,
+                 int splits, const float* fc_b, uint16_t* h_out, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   if (A < 1 || A > kMaxAct) return -1;
+  if (part && (mode != 0 || !fc_b || !h_out || splits < 1)) return -1;
   HeadArgs a;
+  a.part = part;
+  a.splits = splits;
+  a.fc_b = fc_b;
+  a.h_out = h_out;
   a.h = h;
   a.w = head_params;
   a.bias = head_params + A * kHeadF;

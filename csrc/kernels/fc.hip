@@ -1,0 +1,431 @@
+// Fully connected layers of the pixel model (Nature CNN fc: 3136 -> 512) as one "NT"
+// bf16 MFMA GEMM on gfx950:
+//
+//   C[m][n] = sum_k A[m][k] * B[n][k]        A [M][K], B [N][K], both K-contiguous bf16
+//
+// The fc forward is A = a3 [rows][3136], B = Wfc [512][3136]; the fc data gradient is
+// A = dh [rows][512], B = Wfc^T [3136][512] (the transposed bf16 shadow the optimiser
+// writes next to the weights), so both stream 16-byte K-chunks of rows they already have.
+//
+// Why not gemm_bf16.h: that core stages operand tiles through registers into ONE LDS
+// buffer (two barriers per k-tile, loads exposed at every tile) and tiles 128x64 over 4
+// waves -- fine for the short-K implicit-im2col conv GEMMs, but the fc GEMMs are long-K
+// (3136) or wide-N (3136) streaming problems: at 2,048 rows the split-K fc forward ran at
+// ~0.3 PFLOP/s (21 us per call, profiles/r3_pong_a2c_kernels_fused.txt).  Here:
+//   * operand tiles go global -> LDS by DMA (global_load_lds_dwordx4): no staging
+//     registers, no ds_write pass; 3 LDS stages, two tiles in flight across ONE raw
+//     s_barrier per k-tile (counted vmcnt, never vmcnt(0) inside the loop);
+//   * the LDS image is lane-linear (the DMA writes base + 16 * lane) with an XOR swizzle
+//     applied on the SOURCE side: chunk (row, kc) of a [rows][8 x 16 B] image lives at
+//     row * 8 + (kc ^ ((row >> 1) & 7)), which makes every ds_read_b128 fragment read of
+//     16 rows x one k-chunk conflict-free (each of the instruction's four 16-lane groups
+//     touches 16 distinct 16-byte bank quads);
+//   * 128 x 128 x 64 tiles on 8 waves (2 x 4, 64 x 32 per wave), 96 KB of LDS: one
+//     workgroup of 8 waves per CU, two per SIMD;
+//   * operands swapped in the MFMA (A-operand = B rows, B-operand = A rows) so each lane
+//     owns 4 CONSECUTIVE n of one row m: 16-byte fp32 / 8-byte bf16 epilogue stores with
+//     no LDS round trip;
+//   * XCD-aware block order: consecutive logical tiles (m fastest) land on one XCD, so the
+//     workgroups sharing a B tile (the weights) share that XCD's L2.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "gemm_bf16.h"
+
+namespace rrl {
+
+constexpr int kFcBM = 128, kFcBN = 128, kFcBK = 64;
+constexpr int kFcImg = kFcBM * kFcBK;                        // bf16 elements per operand image
+constexpr int kFcStage = 2 * kFcImg;                         // A image + B image (32 KB)
+constexpr int kFcThreads = 512;
+template <int STAGES>
+constexpr int fc_lds_bytes() { return STAGES * kFcStage * 2; }
+
+// position (in 16-byte chunks) of chunk kc (0..7) of image row `row`
+__device__ __forceinline__ int fc_swz(int row, int kc) { return row * 8 + (kc ^ ((row >> 1) & 7)); }
+
+// fp32 split-K partials: part[z][m][n]
+struct FcPartEpi {
+  float* part;
+  int M, N;
+  typedef int Pre;  // nothing to prefetch
+  __device__ __forceinline__ Pre prefetch(int, int) const { return 0; }
+  __device__ __forceinline__ void operator()(int m, int n, f32x4_t v, int z, Pre) const {
+    if (m < M && n < N)
+      *reinterpret_cast<f32x4_t*>(part + ((size_t)z * M + m) * N + n) = v;
+  }
+};
+
+// bf16 data gradient with the ReLU mask of the layer input: out[m][n] = v * (mask[m][n] > 0)
+struct FcMaskEpi {
+  uint16_t* out;
+  const uint16_t* mask;
+  int M, N;
+  typedef uint2 Pre;  // the 4 mask values, loaded before the last k-tile's MFMAs
+  __device__ __forceinline__ Pre prefetch(int m, int n) const {
+    return (m < M && n < N) ? *reinterpret_cast<const uint2*>(mask + (size_t)m * N + n) : make_uint2(0, 0);
+  }
+  __device__ __forceinline__ void operator()(int m, int n, f32x4_t v, int, Pre mk) const {
+    if (m >= M || n >= N) return;
+    const size_t i = (size_t)m * N + n;
+    const float o0 = bf2f((uint16_t)(mk.x & 0xffff)) > 0.f ? v[0] : 0.f;
+    const float o1 = bf2f((uint16_t)(mk.x >> 16)) > 0.f ? v[1] : 0.f;
+    const float o2 = bf2f((uint16_t)(mk.y & 0xffff)) > 0.f ? v[2] : 0.f;
+    const float o3 = bf2f((uint16_t)(mk.y >> 16)) > 0.f ? v[3] : 0.f;
+    *reinterpret_cast<uint2*>(out + i) =
+        make_uint2((uint32_t)f2bf(o0) | ((uint32_t)f2bf(o1) << 16), (uint32_t)f2bf(o2) | ((uint32_t)f2bf(o3) << 16));
+  }
+};
+
+// One k-tile of one operand into its LDS image: the wave's two DMA instructions fill image
+// rows 16 w .. 16 w + 15 (8 rows x 8 chunks = the instruction's 64 lanes x 16 B each).
+__device__ __forceinline__ void fc_stage(const uint16_t* __restrict__ X, int rows, int K, int row0, int k0,
+                                         uint16_t* img, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r0 = 16 * wave + 8 * j;
+    const int r = r0 + (lane >> 3);
+    const int kc = (lane & 7) ^ ((r >> 1) & 7);
+    const int gr = min(row0 + r, rows - 1);  // rows past the end: a duplicate, masked in the epilogue
+    const uint16_t* src = X + (size_t)gr * K + k0 + 8 * kc;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(img + r0 * kFcBK), 16, 0, 0);
+  }
+}
+
+// STAGES = 3: two k-tiles in flight, one 8-wave workgroup per CU (96 KB); STAGES = 2: one
+// k-tile in flight, two workgroups per CU (64 KB each), so one workgroup's epilogue and
+// prologue overlap the other's main loop (short-K problems: the data gradient, K = 512).
+template <class Epi, int STAGES>
+__global__ void __launch_bounds__(kFcThreads, STAGES == 2 ? 2 : 1)
+fc_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, Epi epi, int M, int N, int K,
+             int tiles_m, int tiles_n, int ktiles_per_split, int m_fast) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // XCD-aware order: hardware block b runs on XCD b % 8; logical tile ids handed out so that
+  // each XCD takes a contiguous run of them (bijective for any grid size)
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int q = nwg >> 3, rem = nwg & 7, xcd = b & 7;
+  const int lid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  // n fastest: an XCD's run of tiles shares the A rows (the activations, read from HBM once)
+  // and cycles through the B tiles (the weights, small enough to stay in its L2)
+  int tm, tn, z;
+  if (m_fast) {  // (A/B alternative: an XCD's run shares the B tiles instead)
+    tm = lid % tiles_m;
+    const int rest = lid / tiles_m;
+    tn = rest % tiles_n, z = rest / tiles_n;
+  } else {
+    tn = lid % tiles_n;
+    const int rest = lid / tiles_n;
+    tm = rest % tiles_m, z = rest / tiles_m;
+  }
+  const int m0 = tm * kFcBM, n0 = tn * kFcBN;
+  const int kt0 = z * ktiles_per_split;
+  const int nk = min(K / kFcBK - kt0, ktiles_per_split);
+
+  const int wm = wave & 1, wn = wave >> 1;  // 2 x 4 waves: 64 rows (m) x 32 cols (n) each
+  const int g = lane >> 4, li = lane & 15;
+  f32x4_t acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  typename Epi::Pre pre[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) pre[i][j] = typename Epi::Pre{};
+  auto issue = [&](int t) {
+    uint16_t* st = smem + (t % STAGES) * kFcStage;
+    const int k0 = (kt0 + t) * kFcBK;
+    fc_stage(A, M, K, m0, k0, st, wave, lane);
+    fc_stage(B, N, K, n0, k0, st + kFcImg, wave, lane);
+  };
+#pragma unroll
+  for (int t = 0; t < STAGES - 1; ++t)
+    if (t < nk) issue(t);
+  for (int t = 0; t < nk; ++t) {
+    // tile t landed (this wave's 4 DMAs of it; the up to STAGES - 2 tiles issued after it may
+    // stay in flight), then a barrier publishes every wave's DMAs and retires every wave's
+    // reads of tile t - 1, whose stage the next issue overwrites
+    const int ahead = min(STAGES - 2, nk - 1 - t);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
+    if (t + 1 == nk) {  // no DMA in flight any more: the epilogue's own loads go out now
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) pre[i][j] = epi.prefetch(m0 + 64 * wm + 16 * i + li, n0 + 32 * wn + 16 * j + 4 * g);
+    }
+    const uint16_t* Ai = smem + (t % STAGES) * kFcStage;
+    const uint16_t* Bi = Ai + kFcImg;
+#pragma unroll
+    for (int s = 0; s < kFcBK / 32; ++s) {
+      const int kc = 4 * s + g;
+      bf16x8_t af[4], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = *reinterpret_cast<const bf16x8_t*>(Ai + 8 * fc_swz(64 * wm + 16 * i + li, kc));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bi + 8 * fc_swz(32 * wn + 16 * j + li, kc));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)  // D[n][m]: lane (g, li) holds n = 4 g .. 4 g + 3 of row m = li
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) epi(m0 + 64 * wm + 16 * i + li, n0 + 32 * wn + 16 * j + 4 * g, acc[i][j], z, pre[i][j]);
+}
+
+static int fc_m_fast() {
+  const char* e = getenv("RRL_FC_MFAST");
+  return e && e[0] == '1';
+}
+
+// LDS stage count per call site (0 = forward partials, 1 = data gradient); RRL_FC_STAGES =
+// "<fwd><dgrad>" (e.g. "32") overrides the defaults for A/B measurements.
+static int fc_stages(int site, int dflt) {
+  const char* e = getenv("RRL_FC_STAGES");  // read per call (A/B variants in one process)
+  if (!e || (int)strlen(e) <= site) return dflt;
+  return e[site] == '4' ? 4 : (e[site] == '3' ? 3 : (e[site] == '2' ? 2 : dflt));
+}
+
+template <class Epi, int STAGES>
+static int launch_fc_nt(const uint16_t* A, const uint16_t* B, Epi epi, int M, int N, int K, int splits,
+                        hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fc_nt_kernel<Epi, STAGES>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              fc_lds_bytes<STAGES>());
+    attr = true;
+  }
+  const int tiles_m = (M + kFcBM - 1) / kFcBM, tiles_n = (N + kFcBN - 1) / kFcBN;
+  const int kt = K / kFcBK;
+  const int kps = (kt + splits - 1) / splits;
+  splits = (kt + kps - 1) / kps;
+  const int grid = tiles_m * tiles_n * splits;
+  if (grid < 1) return 0;
+  hipLaunchKernelGGL((fc_nt_kernel<Epi, STAGES>), dim3(grid), dim3(kFcThreads), fc_lds_bytes<STAGES>(), st, A, B,
+                     epi, M, N, K, tiles_m, tiles_n, kps, fc_m_fast());
+  return (int)hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------- TN (weight gradient)
+//   C[i][j] = sum_r X[r][i] * Y[r][j]      X [R][I], Y [R][J] row-major bf16, R % 64 == 0
+// (the fc weight gradient: X = dh [rows][512], Y = a3 [rows][3136], C = dW [512][3136]).
+// Both operands are streamed as [64 r][128 col] images (256-B rows, 16 chunks of 16 B) and
+// their MFMA fragments come out of ds_read_b64_tr_b16 transposed reads.  The 32 lanes of a
+// b64 read touch 8 image rows x 32 B; with 256-B rows every row starts on bank 0, so the
+// chunks are XOR-swizzled by an even mask of (row & 3, row >> 3 & 1):
+//   chunk c of row r lives at r * 16 + (c ^ 2 * ((r & 3) | (r >> 3 & 1) << 2))
+// which spreads those 8 rows x 2 chunks over 16 distinct chunk slots (conflict-free).
+__device__ __forceinline__ int fc_tn_swz(int row, int c) { return row * 16 + (c ^ (2 * ((row & 3) | (((row >> 3) & 1) << 2)))); }
+
+__device__ __forceinline__ void fc_tn_stage(const uint16_t* __restrict__ X, int ld, int r0g, int col0, uint16_t* img,
+                                            int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r0 = 8 * wave + 4 * j;  // image rows r0 .. r0 + 3 (4 x 256 B = the instruction's 1 KB)
+    const int r = r0 + (lane >> 4);
+    const int c = (lane & 15) ^ (2 * ((r & 3) | (((r >> 3) & 1) << 2)));
+    const int col = min(col0 + 8 * c, ld - 8);  // columns past the end: a duplicate, masked in the epilogue
+    const uint16_t* src = X + (size_t)(r0g + r) * ld + col;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(img + r0 * 128), 16, 0, 0);
+  }
+}
+
+// MFMA operand fragment (8 consecutive r for image column col0 + (lane & 15)) from a
+// swizzled [64][128] image: two ds_read_b64_tr_b16, rows k0 .. k0 + 3 and k0 + 4 .. k0 + 7.
+__device__ __forceinline__ bf16x8_t fc_tn_frag(const uint16_t* img, int k0, int col0, int lane) {
+  const int q = (lane >> 2) & 3, p = lane & 3;
+  const int c = (col0 + 4 * p) >> 3, half = (p & 1) * 4;
+  typedef __attribute__((address_space(3))) s16x4_t lds_v4;
+  const uint16_t* a0 = img + 8 * fc_tn_swz(k0 + q, c) + half;
+  const uint16_t* a1 = img + 8 * fc_tn_swz(k0 + 4 + q, c) + half;
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a1));
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// 128 (i) x 128 (j) output tile per workgroup, 8 waves (2 x 4: 64 i x 32 j each), the R
+// reduction split over gridDim (split z takes r-tiles [z * kps, (z + 1) * kps)); fp32
+// partials part[z][I][J], 4 consecutive j per lane (16-byte stores).
+template <int STAGES>
+__global__ void __launch_bounds__(kFcThreads, STAGES == 2 ? 2 : 1)
+fc_tn_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, float* __restrict__ part, int R, int I,
+             int J, int tiles_i, int tiles_j, int rtiles_per_split) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int q = nwg >> 3, rem = nwg & 7, xcd = b & 7;
+  const int lid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  // i fastest: an XCD's run shares the Y tile (the activations, the big operand) across the
+  // dh column tiles
+  const int ti = lid % tiles_i, rest = lid / tiles_i;
+  const int tj = rest % tiles_j, z = rest / tiles_j;
+  const int i0 = ti * 128, j0 = tj * 128;
+  const int rt0 = z * rtiles_per_split;
+  const int nk = min(R / 64 - rt0, rtiles_per_split);
+  const int wi = wave & 1, wj = wave >> 1;
+  const int g = lane >> 4, li = lane & 15;
+  f32x4_t acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) acc[a][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  auto issue = [&](int t) {
+    uint16_t* st = smem + (t % STAGES) * kFcStage;
+    const int r0g = (rt0 + t) * 64;
+    fc_tn_stage(X, I, r0g, i0, st, wave, lane);
+    fc_tn_stage(Y, J, r0g, j0, st + kFcImg, wave, lane);
+  };
+#pragma unroll
+  for (int t = 0; t < STAGES - 1; ++t)
+    if (t < nk) issue(t);
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = min(STAGES - 2, nk - 1 - t);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
+    const uint16_t* Xi = smem + (t % STAGES) * kFcStage;
+    const uint16_t* Yi = Xi + kFcImg;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t xf[4], yf[2];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) xf[a] = fc_tn_frag(Xi, 32 * s + 8 * g, 64 * wi + 16 * a, lane);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) yf[c] = fc_tn_frag(Yi, 32 * s + 8 * g, 32 * wj + 16 * c, lane);
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)  // D[j][i]: lane (g, li) holds j = 4 g .. 4 g + 3 of i = li
+          acc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yf[c], xf[a], acc[a][c], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int i = i0 + 64 * wi + 16 * a + li, j = j0 + 32 * wj + 16 * c + 4 * g;
+      if (i < I && j < J) *reinterpret_cast<f32x4_t*>(part + ((size_t)z * I + i) * J + j) = acc[a][c];
+    }
+}
+
+template <int STAGES>
+static int launch_fc_tn(const uint16_t* X, const uint16_t* Y, float* part, int R, int I, int J, int splits,
+                        hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fc_tn_kernel<STAGES>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              fc_lds_bytes<STAGES>());
+    attr = true;
+  }
+  const int ti = (I + 127) / 128, tj = (J + 127) / 128, rt = R / 64;
+  const int kps = (rt + splits - 1) / splits;
+  splits = (rt + kps - 1) / kps;
+  hipLaunchKernelGGL((fc_tn_kernel<STAGES>), dim3(ti * tj * splits), dim3(kFcThreads), fc_lds_bytes<STAGES>(), st,
+                     X, Y, part, R, I, J, ti, tj, kps);
+  return (int)hipGetLastError();
+}
+
+// Transposed bf16 copy: out[c][r] = in[r][c] (the fc weight's [3136][512] shadow for the
+// data-gradient GEMM).  64 x 64 tiles through LDS, 16-byte loads and stores.
+__global__ void __launch_bounds__(256) transpose_bf16_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                             int R, int C) {
+  __shared__ uint16_t t[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  for (int q = threadIdx.x; q < 64 * 8; q += 256) {
+    const int r = q >> 3, c = (q & 7) * 8;
+    if (r0 + r < R && c0 + c < C) {
+      const uint4 v = *reinterpret_cast<const uint4*>(in + (size_t)(r0 + r) * C + c0 + c);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        t[r][c + 2 * e] = (uint16_t)(w[e] & 0xffff);
+        t[r][c + 2 * e + 1] = (uint16_t)(w[e] >> 16);
+      }
+    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < 64 * 8; q += 256) {
+    const int c = q >> 3, r = (q & 7) * 8;
+    if (c0 + c < C && r0 + r < R) {
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = (uint32_t)t[r + 2 * e][c] | ((uint32_t)t[r + 2 * e + 1][c] << 16);
+      *reinterpret_cast<uint4*>(out + (size_t)(c0 + c) * R + r0 + r) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
+}  // namespace rrl
+
+using namespace rrl;
+
+extern "C" {
+
+// fp32 split-K partials part[splits][M][N] of A[M][K] . B[N][K]^T (K % 64 == 0, N % 4 == 0).
+// Returns the number of splits actually used (<= splits), negative on a bad shape.
+int rrl_fc_nt_part(const uint16_t* a, const uint16_t* b, float* part, int M, int N, int K, int splits,
+                   void* stream_) {
+  if (K % kFcBK || N % 4 || M < 1 || N < 1 || splits < 1) return -1;
+  const int kt = K / kFcBK;
+  const int kps = (kt + splits - 1) / splits;
+  const int used = (kt + kps - 1) / kps;
+  const FcPartEpi epi{part, M, N};
+  hipStream_t st = (hipStream_t)stream_;
+  const int v = fc_stages(0, 4);
+  const int rc = v == 4 ? launch_fc_nt<FcPartEpi, 4>(a, b, epi, M, N, K, used, st)
+                        : (v == 3 ? launch_fc_nt<FcPartEpi, 3>(a, b, epi, M, N, K, used, st)
+                                  : launch_fc_nt<FcPartEpi, 2>(a, b, epi, M, N, K, used, st));
+  return rc ? -rc - 1000 : used;
+}
+
+// bf16 out[M][N] = (A[M][K] . B[N][K]^T) * (mask[M][N] > 0)   (K % 64 == 0, N % 4 == 0)
+int rrl_fc_nt_mask(const uint16_t* a, const uint16_t* b, const uint16_t* mask, uint16_t* out, int M, int N, int K,
+                   void* stream_) {
+  if (K % kFcBK || N % 4 || M < 1 || N < 1) return -1;
+  const FcMaskEpi epi{out, mask, M, N};
+  return fc_stages(1, 2) == 3 ? launch_fc_nt<FcMaskEpi, 3>(a, b, epi, M, N, K, 1, (hipStream_t)stream_)
+                              : launch_fc_nt<FcMaskEpi, 2>(a, b, epi, M, N, K, 1, (hipStream_t)stream_);
+}
+
+// fp32 partials part[splits][I][J] of X[R][I]^T . Y[R][J] (R % 64 == 0, I, J % 8 == 0);
+// returns the number of splits used.
+int rrl_fc_tn_part(const uint16_t* x, const uint16_t* y, float* part, int R, int I, int J, int splits,
+                   void* stream_) {
+  if (R % 64 || I % 8 || J % 8 || R < 64 || splits < 1) return -1;
+  const int rt = R / 64, kps = (rt + splits - 1) / splits, used = (rt + kps - 1) / kps;
+  hipStream_t st = (hipStream_t)stream_;
+  const int rc = fc_stages(2, 2) == 2 ? launch_fc_tn<2>(x, y, part, R, I, J, used, st)
+                                      : launch_fc_tn<3>(x, y, part, R, I, J, used, st);
+  return rc ? -rc - 1000 : used;
+}
+
+int rrl_transpose_bf16(const uint16_t* in, uint16_t* out, int R, int C, void* stream_) {
+  if (R % 8 || C % 8) return -1;
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3((C + 63) / 64, (R + 63) / 64), dim3(256), 0, (hipStream_t)stream_,
+                     in, out, R, C);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

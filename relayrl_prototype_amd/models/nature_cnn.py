@@ -189,11 +189,17 @@ class DeviceNatureCNN:
         import os
 
         self.fused_convs = os.environ.get("RRL_CNN_FUSED", "1") != "0"
+        # fc layer on the DMA-staged NT GEMM (fc.hip): forward as split-K partials reduced by
+        # the head kernel (bias + ReLU + bf16 + logits / value / sample in one launch), data
+        # gradient against a transposed bf16 shadow of Wfc (RRL_FC_NT=0: the gemm_bf16.h path)
+        self.fc_nt = os.environ.get("RRL_FC_NT", "1") != "0"
         self.o = spec.offsets()
         self.P = self.o["P"]
         dev = self.device
         self.shadow = torch.empty(self.P, dtype=torch.bfloat16, device=dev)
-        self.h.to_bf16(self.params, self.shadow)
+        self.wfc_t = torch.empty(FC_IN * HIDDEN, dtype=torch.bfloat16, device=dev)  # [3136][512]
+        self._fc_part = None
+        self.refresh_shadow()
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params)
         self.grad = torch.zeros_like(self.params)
@@ -225,6 +231,8 @@ class DeviceNatureCNN:
             need = max(need, s * cout * K)
         self.cus = int(self.h.device_cus())
         need = max(need, min(B, self.cus) * CONVS[2].cout * CONVS[2].K)  # fused conv3 backward partials
+        if self.fc_nt:
+            need = max(need, self.FC_WGRAD_SPLITS * HIDDEN * FC_IN)
         self.part = torch.empty(need, device=dev)
         self.bias_splits = 512
         self.bias_part = torch.empty(max(self.bias_splits * HIDDEN, self.cus * 512), device=dev)
@@ -241,9 +249,45 @@ class DeviceNatureCNN:
     def _rows(self, buf, row0, rows, per_row):
         return buf[row0 * per_row:(row0 + rows) * per_row]
 
-    def forward(self, obs_u8: torch.Tensor, row0: int = 0):
+    def refresh_shadow(self):
+        """bf16 copies of the fp32 master weights (after a load / broadcast; Adam writes the
+        flat shadow itself) and the transposed fc shadow for the data gradient."""
+        self.h.to_bf16(self.params, self.shadow)
+        self._transpose_fc()
+
+    def _transpose_fc(self):
+        o = self.o
+        self.h.transpose_bf16(self.shadow[o["wfc"]:o["bfc"]], self.wfc_t, HIDDEN, FC_IN)
+
+    # fc weight gradient (fc_tn_part): 100 output tiles x 5 row splits = 500 workgroups, two
+    # per CU (tools/fc_kbench.py)
+    FC_WGRAD_SPLITS = 5
+
+    @staticmethod
+    def fc_splits(n: int) -> int:
+        """split-K count of the fc forward: >= 256 workgroups of 128 x 128 tiles, at most 8."""
+        tiles = -(-n // 128) * (HIDDEN // 128)
+        return max(1, min(8, -(-256 // tiles)))
+
+    def _fc_head(self, a3, hid, n, **head):
+        """fc GEMM as split-K partials, then ONE head launch: bias + ReLU + bf16 hid (stored for
+        the backward) + logits / value / sampling."""
+        o = self.o
+        s = self.fc_splits(n)
+        need = s * n * HIDDEN
+        if self._fc_part is None or self._fc_part.numel() < need:
+            self._fc_part = torch.empty(need, device=self.device)
+        used = int(self.h.fc_nt_part(a3, self.shadow[o["wfc"]:o["bfc"]], self._fc_part, n, HIDDEN, FC_IN, s))
+        self.h.a2c_head(0, hid, self.params[o["head"]:], n, self.A, head.get("act"), head.get("logp"),
+                        head.get("value"), head.get("logits"), int(head.get("seed", 0)), int(head.get("step", 0)),
+                        int(head.get("row_offset", 0)), None, None, None, 0.0, 0.0, 0.0, None, None, None,
+                        max(1, min(1024, (n + 3) // 4)), head.get("step_base"), part=self._fc_part, splits=used,
+                        fc_b=self.params[o["bfc"]:o["bfc"] + HIDDEN])
+
+    def forward(self, obs_u8: torch.Tensor, row0: int = 0, fc: bool = True):
         """Conv stack + fc on obs [n, 84, 84, 4]; activations land in rows row0.. of the
-        stored buffers.  Returns the hidden [n * 512] view."""
+        stored buffers.  Returns the hidden [n * 512] view (with fc=False only the conv
+        stack runs and the view is not written yet)."""
         n = obs_u8.shape[0]
         assert row0 + n <= self.max_batch, "batch exceeds the model's activation buffers"
         h, o, sh, p = self.h, self.o, self.shadow, self.params
@@ -264,32 +308,37 @@ class DeviceNatureCNN:
                 h.conv_fwd(x, sh[o[f"w{i}"]:o[f"b{i}"]], p[o[f"b{i}"]:o[f"b{i}"] + L.cout], y, n, L.hin, L.hin,
                            L.cin, L.k, L.k, L.s, L.cout, True)
                 x = y
-        h.conv_fwd(a3, sh[o["wfc"]:o["bfc"]], p[o["bfc"]:o["bfc"] + HIDDEN], hid, n, 1, 1, FC_IN, 1, 1, 1, HIDDEN,
-                   True, self.part)  # split-K when the batch is too small to fill the chip
+        if fc:
+            h.conv_fwd(a3, sh[o["wfc"]:o["bfc"]], p[o["bfc"]:o["bfc"] + HIDDEN], hid, n, 1, 1, FC_IN, 1, 1, 1,
+                       HIDDEN, True, self.part)  # split-K when the batch is too small to fill the chip
         return hid
+
+    def _forward_head(self, obs_u8, row0, **head):
+        n = obs_u8.shape[0]
+        if self.fc_nt:
+            hid = self.forward(obs_u8, row0, fc=False)
+            self._fc_head(self._rows(self.a3, row0, n, FC_IN), hid, n, **head)
+            return
+        hid = self.forward(obs_u8, row0)
+        self.h.a2c_head(0, hid, self.params[self.o["head"]:], n, self.A, head.get("act"), head.get("logp"),
+                        head.get("value"), head.get("logits"), int(head.get("seed", 0)), int(head.get("step", 0)),
+                        int(head.get("row_offset", 0)), None, None, None, 0.0, 0.0, 0.0, None, None, None,
+                        max(1, min(1024, (n + 3) // 4)), head.get("step_base"))
 
     def act(self, obs_u8, row0, act_out, logp_out, value_out, seed: int, step: int, row_offset: int = 0,
             step_base=None):
         """Sample actions; the Philox step is ``step`` (+ the device counter ``step_base``)."""
-        hid = self.forward(obs_u8, row0)
-        n = obs_u8.shape[0]
-        self.h.a2c_head(0, hid, self.params[self.o["head"]:], n, self.A, act_out, logp_out, value_out, None,
-                        int(seed), int(step), int(row_offset), None, None, None, 0.0, 0.0, 0.0, None, None, None,
-                        max(1, min(1024, (n + 3) // 4)), step_base)
+        self._forward_head(obs_u8, row0, act=act_out, logp=logp_out, value=value_out, seed=seed, step=step,
+                           row_offset=row_offset, step_base=step_base)
 
     def value(self, obs_u8, row0, value_out):
-        hid = self.forward(obs_u8, row0)
-        n = obs_u8.shape[0]
-        self.h.a2c_head(0, hid, self.params[self.o["head"]:], n, self.A, None, None, value_out, None, 0, 0, 0, None,
-                        None, None, 0.0, 0.0, 0.0, None, None, None, max(1, min(1024, (n + 3) // 4)))
+        self._forward_head(obs_u8, row0, value=value_out)
 
     def logits(self, obs_u8):
         n = obs_u8.shape[0]
-        hid = self.forward(obs_u8, 0)
         lg = torch.empty(n, self.A, device=self.device)
         val = torch.empty(n, device=self.device)
-        self.h.a2c_head(0, hid, self.params[self.o["head"]:], n, self.A, None, None, val, lg, 0, 0, 0, None, None,
-                        None, 0.0, 0.0, 0.0, None, None, None, max(1, min(1024, (n + 3) // 4)))
+        self._forward_head(obs_u8, 0, value=val, logits=lg)
         return lg, val
 
     # ------------------------------------------------------------------ backward
@@ -322,10 +371,17 @@ class DeviceNatureCNN:
         h.head_wgrad(hid, dhead, B, self.A, hp, nb)
         h.sum_splits(hp, nb, self.spec.head_size, g[o["head"]:o["P"]])
         # fc
-        self._wgrad("fc", dh, a3, B, 1, FC_IN, 1, 1, HIDDEN, o["wfc"])
+        if self.fc_nt and B % 64 == 0:
+            used = int(h.fc_tn_part(dh, a3, self.part, B, HIDDEN, FC_IN, self.FC_WGRAD_SPLITS))
+            h.sum_splits(self.part, used, HIDDEN * FC_IN, g[o["wfc"]:o["bfc"]])
+        else:
+            self._wgrad("fc", dh, a3, B, 1, FC_IN, 1, 1, HIDDEN, o["wfc"])
         self._bias(dh, B, HIDDEN, o["bfc"])
         da3 = self.da3[:B * FC_IN]
-        h.gemm_dgrad(dh, sh[o["wfc"]:o["bfc"]], a3, da3, B, HIDDEN, FC_IN)
+        if self.fc_nt:
+            h.fc_nt_mask(dh, self.wfc_t, a3, da3, B, FC_IN, HIDDEN)
+        else:
+            h.gemm_dgrad(dh, sh[o["wfc"]:o["bfc"]], a3, da3, B, HIDDEN, FC_IN)
         if comm is not None and comm.world > 1:
             import torch.distributed as dist
 
@@ -406,6 +462,8 @@ class DeviceNatureCNN:
         self.h.adam_clip(self.params, self.m, self.v, self.grad, self.shadow,
                          self.norm_sq if max_grad_norm > 0 else None, float(max_grad_norm), float(lr),
                          float(betas[0]), float(betas[1]), float(eps), 0, self.step_t)
+        if self.fc_nt:
+            self._transpose_fc()
 
     def state_dict(self):
         return {"params": self.params, "m": self.m, "v": self.v, "step": self.step_t.cpu()}
@@ -415,4 +473,4 @@ class DeviceNatureCNN:
         self.m.copy_(st["m"])
         self.v.copy_(st["v"])
         self.step_t.fill_(int(st["step"][0]))
-        self.h.to_bf16(self.params, self.shadow)
+        self.refresh_shadow()

@@ -258,7 +258,7 @@ class PixelA2CTrainer:
             m = self.model
             for t in (m.params, m.m, m.v, m.step_t):
                 self.comm.broadcast_(t, src)
-            m.h.to_bf16(m.params, m.shadow)
+            m.refresh_shadow()
         else:
             with torch.no_grad():
                 self.comm.broadcast_(self.params.data, src)

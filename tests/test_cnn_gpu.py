@@ -553,3 +553,92 @@ def test_conv1_wgrad8_matches_autograd(cuda, N, grid):
     y.backward(dy.permute(0, 3, 1, 2))
     assert relerr(dw, conv1_khkwc_to_s2d(w.grad).reshape(-1)) < 1e-3
     assert relerr(db, dy.sum((0, 1, 2))) < 1e-3
+
+
+# ----------------------------------------------------------------------------- fc.hip
+@pytest.mark.parametrize("M,N,K,splits", [(37, 512, 3136, 1), (300, 512, 3136, 4), (2048, 512, 3136, 4),
+                                          (130, 3136, 512, 1), (64, 132, 128, 2)])
+def test_fc_nt_part_matches_fp32(cuda, M, N, K, splits):
+    """DMA-staged NT GEMM (swizzled LDS images, 3-stage ring): the split-K partials sum to
+    the fp32 product of the bf16 operands, for tile-ragged M and N."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    g = torch.Generator().manual_seed(M + N + K)
+    a = _bf(torch.randn(M, K, generator=g))
+    b = _bf(torch.randn(N, K, generator=g) * 0.05)
+    part = torch.full((splits * M * N,), float("nan"), device=cuda)
+    used = h.fc_nt_part(a.to(cuda).bfloat16().reshape(-1), b.to(cuda).bfloat16().reshape(-1), part, M, N, K, splits)
+    assert 1 <= used <= splits
+    got = part[:used * M * N].view(used, M, N).sum(0).cpu()
+    ref = a.double() @ b.double().t()
+    assert torch.isfinite(got).all()
+    assert ((got.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
+
+
+@pytest.mark.parametrize("M", [37, 1000])
+def test_fc_nt_mask_matches_fp32(cuda, M):
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    g = torch.Generator().manual_seed(M)
+    dh = _bf(torch.randn(M, HIDDEN, generator=g))
+    w = _bf(torch.randn(HIDDEN, FC_IN, generator=g) * 0.02)
+    a3 = _bf(F.relu(torch.randn(M, FC_IN, generator=g)))
+    wt = torch.empty(FC_IN * HIDDEN, dtype=torch.bfloat16, device=cuda)
+    h.transpose_bf16(w.to(cuda).bfloat16().reshape(-1), wt, HIDDEN, FC_IN)
+    assert torch.equal(wt.view(FC_IN, HIDDEN).cpu().float(), w.t())
+    out = torch.empty(M * FC_IN, dtype=torch.bfloat16, device=cuda)
+    h.fc_nt_mask(dh.to(cuda).bfloat16().reshape(-1), wt, a3.to(cuda).bfloat16().reshape(-1), out, M, FC_IN, HIDDEN)
+    ref = ((dh @ w) * (a3 > 0)).reshape(-1)
+    assert relerr(out, ref) < 4e-3
+    assert torch.equal((out.cpu().view(M, FC_IN) == 0) | (a3 > 0), torch.ones(M, FC_IN, dtype=torch.bool))
+
+
+@pytest.mark.parametrize("B", [48, 2048])
+def test_fc_head_fused_matches_separate(cuda, B, monkeypatch):
+    """fc as split-K partials reduced inside the head launch (RRL_FC_NT=1, the default) vs the
+    gemm_bf16.h fc + bias_act + head (RRL_FC_NT=0): same stored hidden units (to one bf16
+    rounding), same value / log-prob, same sampled actions."""
+    spec = CNNSpec(6)
+    params = spec.init(7)
+    o = spec.offsets()
+    params[o["wpi"]:o["bpi"]] *= 30.0
+    g = torch.Generator().manual_seed(B)
+    obs = torch.randint(0, 256, (B, 21, 21, 64), dtype=torch.uint8, generator=g).to(cuda)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("RRL_FC_NT", flag)
+        m = DeviceNatureCNN(spec, cuda, max_batch=B, params=params)
+        assert m.fc_nt == (flag == "1")
+        act = torch.empty(B, dtype=torch.int32, device=cuda)
+        logp = torch.empty(B, device=cuda)
+        val = torch.empty(B, device=cuda)
+        m.act(obs, 0, act, logp, val, seed=3, step=1)
+        outs.append((act.cpu(), logp.cpu(), val.cpu(), m.hid[:B * HIDDEN].float().cpu()))
+    (a1, l1, v1, h1), (a2, l2, v2, h2) = outs
+    assert relerr(h1, h2) < 5e-3
+    assert (h1 - h2).abs().max().item() <= 1e-2 * h2.abs().max().item()
+    assert torch.allclose(v1, v2, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(l1, l2, atol=1e-3)
+    assert (a1 != a2).float().mean().item() < 0.01
+
+
+@pytest.mark.parametrize("R,I,J,splits", [(64, 512, 3136, 1), (640, 512, 3136, 5), (10240, 512, 3136, 5),
+                                          (192, 136, 72, 2)])
+def test_fc_tn_part_matches_fp32(cuda, R, I, J, splits):
+    """Weight-gradient GEMM X^T . Y from row-major operands (transposed ds_read_b64_tr_b16
+    fragments of XOR-swizzled [64][128] images), split over rows into fp32 partials."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    g = torch.Generator().manual_seed(R + I + J)
+    x = _bf(torch.randn(R, I, generator=g))
+    y = _bf(F.relu(torch.randn(R, J, generator=g)))
+    part = torch.full((splits * I * J,), float("nan"), device=cuda)
+    used = h.fc_tn_part(x.to(cuda).bfloat16().reshape(-1), y.to(cuda).bfloat16().reshape(-1), part, R, I, J, splits)
+    assert 1 <= used <= splits
+    got = part[:used * I * J].view(used, I, J).sum(0).cpu()
+    ref = x.double().t() @ y.double()
+    assert torch.isfinite(got).all()
+    assert ((got.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
