@@ -84,6 +84,9 @@ def parse(argv=None):
     ap.add_argument("--pong-steps", type=int, default=20,
                     help="1 GPU: also time the A2C Pong pixel update (BASELINE config #4: Nature CNN on bf16 MFMA, "
                          "2048 envs x 5 steps) for this many updates; 0 = skip")
+    ap.add_argument("--pong-big-envs", type=int, default=8192,
+                    help="1 GPU: also time the A2C Pong update at this many envs (the six rollout forwards are "
+                         "latency-bound at 2048 frames per launch); 0 = skip")
     ap.add_argument("--al-steps", type=int, default=10)
     ap.add_argument("--al-warmup", type=int, default=5)
     ap.add_argument("--al-env", default="LunarLanderSynth-v0")
@@ -236,20 +239,21 @@ def host_path_probe(steps: int, comm) -> dict:
     return rec
 
 
-def pong_probe(steps: int) -> dict:
+def pong_probe(steps: int, num_envs: int = 2048) -> dict:
     """BASELINE config #4 on one GPU: A2C on PongSynth-v0 pixels (Nature CNN, bf16 MFMA: the
-    fused conv-stack forward and conv backward kernels of csrc/kernels/cnn_fused.hip), 2048
-    envs x 5 steps per update, the whole update captured as one hipGraph; 3 untimed warmup
-    updates, then ``steps`` timed ones.  Reported next to the headline."""
+    fused conv-stack forward and conv backward kernels of csrc/kernels/cnn_fused.hip, the fc
+    GEMMs of csrc/kernels/fc.hip), ``num_envs`` envs x 5 steps per update, the whole update
+    captured as one hipGraph; 3 untimed warmup updates, then ``steps`` timed ones.  Reported
+    next to the headline."""
     import torch
 
     from relayrl_prototype_amd.runtime.pixel_trainer import PixelA2CConfig, PixelA2CTrainer
 
-    rec = {"config": "A2C PongSynth-v0, Nature-CNN, 2048 envs x 5 steps", "steps": steps, "warmup": 3,
+    rec = {"config": f"A2C PongSynth-v0, Nature-CNN, {num_envs} envs x 5 steps", "steps": steps, "warmup": 3,
            "dtype": "bf16 (fp32 accumulate, fp32 master weights)"}
     tr = None
     try:
-        cfg = PixelA2CConfig(num_envs=2048, rollout_len=5)
+        cfg = PixelA2CConfig(num_envs=num_envs, rollout_len=5)
         tr = PixelA2CTrainer(cfg, device=torch.device("cuda", torch.cuda.current_device()))
         for _ in range(3):
             tr.train_epoch()
@@ -452,6 +456,8 @@ def main(argv=None):
     phases = phase_probe(tr, comm, args.phase_steps) if args.phase_steps > 0 else None
     host_rec = host_path_probe(args.host_steps, comm) if (on_gpu and world == 1 and args.host_steps > 0) else None
     pong_rec = pong_probe(args.pong_steps) if (on_gpu and world == 1 and args.pong_steps > 0) else None
+    pong_big = (pong_probe(args.pong_steps, args.pong_big_envs)
+                if (on_gpu and world == 1 and args.pong_steps > 0 and args.pong_big_envs > 0) else None)
     def record(al_rec, ttt=None, ttt_ref=None, ref_cpu=None, do_ttt=False):
         """The ONE JSON line (rank 0)."""
         algo = "REINFORCE" if args.no_baseline else "REINFORCE-with-baseline"
@@ -514,6 +520,8 @@ def main(argv=None):
             rec["host_env_path"] = host_rec
         if pong_rec is not None:
             rec["pong_a2c"] = pong_rec
+        if pong_big is not None:
+            rec["pong_a2c_big"] = pong_big
         if al_rec is not None:
             rec["actor_learner"] = al_rec
         if ref_cpu is not None:

@@ -2,10 +2,13 @@
 // Same contract as hip_ops.cpp: every tensor is validated (device, dtype, contiguity,
 // size) before a launch, launches go to the current HIP stream.
 #include <ATen/hip/HIPContext.h>
+#include <pybind11/stl.h>
 #include <torch/extension.h>
 
 #include <cstdint>
 #include <optional>
+#include <tuple>
+#include <vector>
 
 extern "C" {
 int rrl_conv_fwd(const void* x, int x_u8, const uint16_t* w, const float* b, uint16_t* y, int N, int H, int W,
@@ -21,6 +24,8 @@ int rrl_gemm_splits(int R, int splits);
 int rrl_conv_dgrad(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, int N, int H, int W,
                    int C, int KH, int KW, int S, int Cout, void* stream);
 int rrl_sum_splits(const float* part, int splits, long long n, float* out, void* stream);
+int rrl_sum_splits_multi(const float* const* parts, const int* splits, const long long* ns, float* const* outs,
+                         int count, void* stream);
 int rrl_colsum(const uint16_t* y, int M, int C, float* part, int splits, void* stream);
 int rrl_sumsq(const float* x, long long n, float* work, int work_n, float* out, void* stream);
 int rrl_adam_clip(float* p, float* m, float* v, const float* g, uint16_t* shadow, long long n, const float* norm_sq,
@@ -248,6 +253,29 @@ void sum_splits(const Tensor& part, int64_t splits, int64_t n, const Tensor& out
   rc_check(rrl_sum_splits(part.data_ptr<float>(), (int)splits, n, out.data_ptr<float>(), stream()), "sum_splits");
 }
 
+// [(part, splits, n, out), ...] (<= 8 segments) summed in one launch
+void sum_splits_multi(const std::vector<std::tuple<Tensor, int64_t, int64_t, Tensor>>& segs) {
+  TORCH_CHECK(!segs.empty() && segs.size() <= 8, "sum_splits_multi: 1..8 segments");
+  std::vector<const float*> parts;
+  std::vector<float*> outs;
+  std::vector<int> splits;
+  std::vector<long long> ns;
+  for (const auto& sgm : segs) {
+    const Tensor& part = std::get<0>(sgm);
+    const int64_t s = std::get<1>(sgm), n = std::get<2>(sgm);
+    const Tensor& out = std::get<3>(sgm);
+    TORCH_CHECK(s >= 1 && n >= 4 && n % 4 == 0, "sum_splits_multi: splits >= 1, n % 4 == 0");
+    check(part, "part", at::kFloat, s * n);
+    check(out, "out", at::kFloat, n);
+    parts.push_back(part.data_ptr<float>());
+    outs.push_back(out.data_ptr<float>());
+    splits.push_back((int)s);
+    ns.push_back(n);
+  }
+  rc_check(rrl_sum_splits_multi(parts.data(), splits.data(), ns.data(), outs.data(), (int)segs.size(), stream()),
+           "sum_splits_multi (16-byte aligned part / out needed)");
+}
+
 void colsum(const Tensor& y, int64_t M, int64_t C, const Tensor& part, int64_t splits) {
   check(y, "y", at::kBFloat16, M * C);
   check(part, "part", at::kFloat, splits * C);
@@ -434,6 +462,7 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("bias_part") = pybind11::none());
   m.def("sum_splits", &sum_splits);
   m.def("colsum", &colsum);
+  m.def("sum_splits_multi", &sum_splits_multi);
   m.def("sumsq", &sumsq);
   m.def("adam_clip", &adam_clip, pybind11::arg("p"), pybind11::arg("m"), pybind11::arg("v"), pybind11::arg("g"),
         pybind11::arg("shadow"), pybind11::arg("norm_sq"), pybind11::arg("max_norm"), pybind11::arg("lr"),

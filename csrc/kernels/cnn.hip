@@ -278,6 +278,66 @@ __global__ void __launch_bounds__(256) sum_splits_kernel(const float* __restrict
   }
 }
 
+// Several split sums in ONE launch (the conv layers' weight and bias partials at the end of
+// the backward: 6 launches -> 1, and the 32 / 64-float bias sums no longer run as single-
+// block kernels of their own).  Segment q covers blocks [first[q], first[q + 1]); each block
+// is the sum_splits_kernel block shape (16 float4 columns x 16 split phases).
+constexpr int kMaxSumSegs = 8;
+struct SumSegs {
+  const float* part[kMaxSumSegs];
+  float* out[kMaxSumSegs];
+  long long n[kMaxSumSegs];
+  int splits[kMaxSumSegs];
+  int first[kMaxSumSegs + 1];
+  int count;
+};
+__global__ void __launch_bounds__(256) sum_splits_multi_kernel(SumSegs sg) {
+  __shared__ float4 red[16][16];
+  int q = 0;
+#pragma unroll 1
+  while (q + 1 < sg.count && (int)blockIdx.x >= sg.first[q + 1]) ++q;
+  const float* part = sg.part[q];
+  const int splits = sg.splits[q];
+  const size_t n = (size_t)sg.n[q];
+  const int col = threadIdx.x & 15, ph = threadIdx.x >> 4;
+  const size_t i4 = (size_t)(blockIdx.x - sg.first[q]) * 16 + col;
+  const size_t n4 = n / 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i4 < n4) {
+    int z = ph;
+    for (; z + 7 * 16 < splits; z += 8 * 16) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = reinterpret_cast<const float4*>(part + (size_t)(z + 16 * u) * n)[i4];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a.x += v[u].x;
+        a.y += v[u].y;
+        a.z += v[u].z;
+        a.w += v[u].w;
+      }
+    }
+    for (; z < splits; z += 16) {
+      const float4 v = reinterpret_cast<const float4*>(part + (size_t)z * n)[i4];
+      a.x += v.x;
+      a.y += v.y;
+      a.z += v.z;
+      a.w += v.w;
+    }
+  }
+  red[ph][col] = a;
+  __syncthreads();
+  if (ph == 0 && i4 < n4) {
+    for (int k = 1; k < 16; ++k) {
+      a.x += red[k][col].x;
+      a.y += red[k][col].y;
+      a.z += red[k][col].z;
+      a.w += red[k][col].w;
+    }
+    reinterpret_cast<float4*>(sg.out[q])[i4] = a;
+  }
+}
+
 // Unaligned / odd-length split sums (e.g. the A2C head, n = 512 (A+1) + A+1): a block
 // owns 64 consecutive columns and splits the slab sum over 16 row groups (coalesced 256-B
 // rows per wave), folded through LDS -- the one-thread-per-column serial loop it replaces
@@ -432,16 +492,56 @@ struct HeadArgs {
   uint16_t* h_out;        // [B][F]
 };
 
-template <bool TRAIN>
+// Head weights live in REGISTERS: lane l holds features 8 l .. 8 l + 7 of every policy row
+// and of the value row, loaded once per wave before its rows (L2 hits after the first
+// wave), so there is no per-block LDS staging pass and no barrier in front of the rows --
+// at 2,048 rollout rows a block has one row per wave and that staging was most of the
+// launch.  AMAX = compile-time cap on A (8 covers Pong's 6; 16 = kMaxAct otherwise).
+template <int S>
+__device__ __forceinline__ void head_sum_part(float (&v)[8], const float* pr, size_t zs, int splits) {
+  if constexpr (S > 0) {  // compile-time split count: every load issued before the adds
+    float4 p[S][2];
+#pragma unroll
+    for (int z = 0; z < S; ++z) {
+      p[z][0] = *reinterpret_cast<const float4*>(pr + z * zs);
+      p[z][1] = *reinterpret_cast<const float4*>(pr + z * zs + 4);
+    }
+#pragma unroll
+    for (int z = 0; z < S; ++z) {
+      v[0] += p[z][0].x; v[1] += p[z][0].y; v[2] += p[z][0].z; v[3] += p[z][0].w;
+      v[4] += p[z][1].x; v[5] += p[z][1].y; v[6] += p[z][1].z; v[7] += p[z][1].w;
+    }
+  } else {
+    for (int z = 0; z < splits; ++z) {
+      const float4 p0 = *reinterpret_cast<const float4*>(pr + z * zs);
+      const float4 p1 = *reinterpret_cast<const float4*>(pr + z * zs + 4);
+      v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
+      v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
+    }
+  }
+}
+
+template <bool TRAIN, int AMAX>
 __global__ void __launch_bounds__(256) a2c_head_kernel(HeadArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float hs[];  // [(A+1)][F] + [A+1]
+  __shared__ float red[16];
   const int A = a.A, F = kHeadF;
-  for (int i = threadIdx.x; i < A * F; i += 256) hs[i] = a.w[i];
-  for (int i = threadIdx.x; i < F; i += 256) hs[A * F + i] = a.w_v[i];
-  if (threadIdx.x < A) hs[(A + 1) * F + threadIdx.x] = a.bias[threadIdx.x];
-  if (threadIdx.x == 0) hs[(A + 1) * F + A] = a.b_v[0];
-  __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float wv[8], wp[AMAX][8], bp[AMAX];
+  {
+    const float4 v0 = *reinterpret_cast<const float4*>(a.w_v + 8 * lane);
+    const float4 v1 = *reinterpret_cast<const float4*>(a.w_v + 8 * lane + 4);
+    wv[0] = v0.x; wv[1] = v0.y; wv[2] = v0.z; wv[3] = v0.w; wv[4] = v1.x; wv[5] = v1.y; wv[6] = v1.z; wv[7] = v1.w;
+#pragma unroll
+    for (int o = 0; o < AMAX; ++o) {  // rows past A: a clamped duplicate, never used
+      const int oc = o < A ? o : A - 1;
+      const float4 w0 = *reinterpret_cast<const float4*>(a.w + oc * F + 8 * lane);
+      const float4 w1 = *reinterpret_cast<const float4*>(a.w + oc * F + 8 * lane + 4);
+      wp[o][0] = w0.x; wp[o][1] = w0.y; wp[o][2] = w0.z; wp[o][3] = w0.w;
+      wp[o][4] = w1.x; wp[o][5] = w1.y; wp[o][6] = w1.z; wp[o][7] = w1.w;
+      bp[o] = a.bias[oc];
+    }
+  }
+  const float bv = a.b_v[0];
   float st_pg = 0.f, st_vf = 0.f, st_ent = 0.f, st_n = 0.f;
   for (int row = blockIdx.x * 4 + wave; row < a.B; row += gridDim.x * 4) {
     uint4 hv;
@@ -452,11 +552,11 @@ __global__ void __launch_bounds__(256) a2c_head_kernel(HeadArgs a) {
       float v[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
       const float* pr = a.part + (size_t)row * F + 8 * lane;
       const size_t zs = (size_t)a.B * F;
-      for (int z = 0; z < a.splits; ++z) {
-        const float4 p0 = *reinterpret_cast<const float4*>(pr + z * zs);
-        const float4 p1 = *reinterpret_cast<const float4*>(pr + z * zs + 4);
-        v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
-        v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
+      switch (a.splits) {
+        case 4: head_sum_part<4>(v, pr, zs, 4); break;
+        case 2: head_sum_part<2>(v, pr, zs, 2); break;
+        case 1: head_sum_part<1>(v, pr, zs, 1); break;
+        default: head_sum_part<0>(v, pr, zs, a.splits); break;
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -476,20 +576,16 @@ __global__ void __launch_bounds__(256) a2c_head_kernel(HeadArgs a) {
 #pragma unroll
     for (int o = 0; o < kMaxAct; ++o) logits[o] = -INFINITY;
     float vsum = 0.f;
-    {
-      const float* wr = hs + A * F + 8 * lane;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) vsum += wr[i] * x[i];
-    }
-    const float value = wave_sum(vsum) + hs[(A + 1) * F + A];
+    for (int i = 0; i < 8; ++i) vsum += wv[i] * x[i];
+    const float value = wave_sum(vsum) + bv;
 #pragma unroll
-    for (int o = 0; o < kMaxAct; ++o) {
+    for (int o = 0; o < AMAX; ++o) {
       if (o < A) {
-        const float* wr = hs + o * F + 8 * lane;
         float s = 0.f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) s += wr[i] * x[i];
-        logits[o] = wave_sum(s) + hs[(A + 1) * F + o];
+        for (int i = 0; i < 8; ++i) s += wp[o][i] * x[i];
+        logits[o] = wave_sum(s) + bp[o];
       }
     }
     const CatStats cs = cat_stats(A, logits);
@@ -524,13 +620,12 @@ __global__ void __launch_bounds__(256) a2c_head_kernel(HeadArgs a) {
       const float dv = a.inv_B * 2.f * a.vf_coef * (value - ret);
       float g[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) g[i] = dv * hs[A * F + 8 * lane + i];
+      for (int i = 0; i < 8; ++i) g[i] = dv * wv[i];
 #pragma unroll
-      for (int o = 0; o < kMaxAct; ++o)
+      for (int o = 0; o < AMAX; ++o)
         if (o < A) {
-          const float* wr = hs + o * F + 8 * lane;
 #pragma unroll
-          for (int i = 0; i < 8; ++i) g[i] += dz[o] * wr[i];
+          for (int i = 0; i < 8; ++i) g[i] += dz[o] * wp[o][i];
         }
       uint32_t ow[4];
 #pragma unroll
@@ -553,8 +648,6 @@ __global__ void __launch_bounds__(256) a2c_head_kernel(HeadArgs a) {
     }
   }
   if (TRAIN) {
-    __syncthreads();
-    float* red = hs;  // reuse
     if (lane == 0) {
       red[wave * 4 + 0] = st_pg;
       red[wave * 4 + 1] = st_vf;
@@ -581,7 +674,33 @@ __global__ void __launch_bounds__(256) head_wgrad_kernel(const uint16_t* __restr
   float bacc[kMaxAct + 1];
 #pragma unroll
   for (int o = 0; o <= kMaxAct; ++o) acc[o][0] = acc[o][1] = bacc[o] = 0.f;
-  for (int r = r0; r < r1; ++r) {
+  // 4 rows per step with every load issued before the FMAs (the per-row loop waited for
+  // each row's hidden units and head gradients in turn: a latency chain of ~40 rows)
+  // (heads with <= 8 outputs; the head-gradient loads are clamped, never branched around)
+  constexpr int kO = 8;
+  int r = r0;
+  for (; O <= kO && r + 4 <= r1; r += 4) {
+    uint32_t hv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) hv[u] = *reinterpret_cast<const uint32_t*>(h + (size_t)(r + u) * F + f);
+    float d[4][kO];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int o = 0; o < kO; ++o) d[u][o] = dhead[(size_t)(r + u) * O + min(o, O - 1)];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float x0 = bf2f((uint16_t)(hv[u] & 0xffff)), x1 = bf2f((uint16_t)(hv[u] >> 16));
+#pragma unroll
+      for (int o = 0; o < kO; ++o)
+        if (o < O) {
+          acc[o][0] += d[u][o] * x0;
+          acc[o][1] += d[u][o] * x1;
+          bacc[o] += d[u][o];
+        }
+    }
+  }
+  for (; r < r1; ++r) {
     const uint32_t hv = *reinterpret_cast<const uint32_t*>(h + (size_t)r * F + f);
     const float x0 = bf2f((uint16_t)(hv & 0xffff)), x1 = bf2f((uint16_t)(hv >> 16));
 #pragma unroll
@@ -1359,6 +1478,27 @@ int rrl_conv_wgrad(const uint16_t* dy, const void* x, int x_u8, float* part, flo
 // Actual number of splits launch_gemm uses for a reduction of length R.
 int rrl_gemm_splits(int R, int splits) { return rrl_gemm_splits_impl(R, splits); }
 
+// count segments (<= 8), each part / out 16-byte aligned with n % 4 == 0
+int rrl_sum_splits_multi(const float* const* parts, const int* splits, const long long* ns, float* const* outs,
+                         int count, void* stream_) {
+  if (count < 1 || count > kMaxSumSegs) return -1;
+  SumSegs sg{};
+  sg.count = count;
+  int blocks = 0;
+  for (int q = 0; q < count; ++q) {
+    if (((uintptr_t)parts[q] & 15) || ((uintptr_t)outs[q] & 15) || (ns[q] & 3) || splits[q] < 1) return -1;
+    sg.part[q] = parts[q];
+    sg.out[q] = outs[q];
+    sg.n[q] = ns[q];
+    sg.splits[q] = splits[q];
+    sg.first[q] = blocks;
+    blocks += (int)((ns[q] / 4 + 15) / 16);
+  }
+  sg.first[count] = blocks;
+  hipLaunchKernelGGL(sum_splits_multi_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream_, sg);
+  return (int)hipGetLastError();
+}
+
 int rrl_sum_splits(const float* part, int splits, long long n, float* out, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   if (((uintptr_t)part & 15) || ((uintptr_t)out & 15) || (n & 3)) {  // float4 path needs aligned rows
@@ -1453,11 +1593,13 @@ int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, i
   a.dh = dh;
   a.dhead = dhead;
   a.stats = stats;
-  const size_t lds = ((size_t)(A + 1) * kHeadF + A + 1) * sizeof(float);
-  if (mode == 0)
-    hipLaunchKernelGGL(a2c_head_kernel<false>, dim3(grid), dim3(256), lds, st, a);
-  else
-    hipLaunchKernelGGL(a2c_head_kernel<true>, dim3(grid), dim3(256), lds, st, a);
+  if (A <= 8) {
+    if (mode == 0) hipLaunchKernelGGL((a2c_head_kernel<false, 8>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((a2c_head_kernel<true, 8>), dim3(grid), dim3(256), 0, st, a);
+  } else {
+    if (mode == 0) hipLaunchKernelGGL((a2c_head_kernel<false, kMaxAct>), dim3(grid), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((a2c_head_kernel<true, kMaxAct>), dim3(grid), dim3(256), 0, st, a);
+  }
   return (int)hipGetLastError();
 }
 

@@ -236,6 +236,17 @@ class DeviceNatureCNN:
         self.part = torch.empty(need, device=dev)
         self.bias_splits = 512
         self.bias_part = torch.empty(max(self.bias_splits * HIDDEN, self.cus * 512), device=dev)
+        if self.fused_convs:
+            # per-layer partial slabs of the fused conv backward kernels, summed together in ONE
+            # launch at the end of the backward (sum_splits_multi)
+            nb = min(B, self.cus)
+            L1_, L2_, L3_ = CONVS
+            self.cpart = {"c3": torch.empty(nb * L3_.cout * L3_.K, device=dev),
+                          "c2": torch.empty(nb * L2_.cout * L2_.K, device=dev),
+                          "c1": torch.empty(2 * nb * S2D.cout * S2D.K, device=dev)}  # 2 slabs per workgroup
+            self.cbias = {"c3": torch.empty(nb * 8 * L3_.cout, device=dev),
+                          "c2": torch.empty(nb * 8 * L2_.cout, device=dev),
+                          "c1": torch.empty(2 * nb * S2D.cout, device=dev)}
         self.sq_work = torch.empty(1024, device=dev)
         self.norm_sq = torch.empty(1, device=dev)
 
@@ -362,7 +373,7 @@ class DeviceNatureCNN:
         hid = self.hid[:B * HIDDEN]
         dh = self.dh[:B * HIDDEN]
         dhead = self.dhead[:B * (self.A + 1)]
-        grid = max(1, min(self.head_grid, (B + 3) // 4))
+        grid = max(1, min(self.head_grid, (B + 15) // 16))  # ~4 rows per wave: the head weights load once per wave
         stats = self.stats[:grid * 4]
         h.a2c_head(1, hid, self.params[o["head"]:], B, self.A, None, None, None, None, 0, 0, 0, act, adv, ret,
                    1.0 / B, float(vf_coef), float(ent_coef), dh, dhead, stats, grid)
@@ -389,11 +400,12 @@ class DeviceNatureCNN:
         # conv3
         da2 = self.da2[:B * L2.hout ** 2 * L2.cout]
         if self.fused_convs:
-            # dgrad + wgrad + bias in one pass over (da3, a2) per image (cnn_fused.hip)
+            # dgrad + wgrad + bias in one pass over (da3, a2) per image (cnn_fused.hip); the
+            # slab sums of all three conv layers run in one launch at the end
             nblk = min(B, self.cus)
-            h.conv3_bwd(da3, sh[o["w3"]:o["b3"]], a2, da2, self.part, self.bias_part, B, nblk)
-            h.sum_splits(self.part, nblk, L3.cout * L3.K, g[o["w3"]:o["b3"]])
-            h.sum_splits(self.bias_part, nblk * 8, L3.cout, g[o["b3"]:o["b3"] + L3.cout])
+            h.conv3_bwd(da3, sh[o["w3"]:o["b3"]], a2, da2, self.cpart["c3"], self.cbias["c3"], B, nblk)
+            sums = [(self.cpart["c3"], nblk, L3.cout * L3.K, g[o["w3"]:o["b3"]]),
+                    (self.cbias["c3"], nblk * 8, L3.cout, g[o["b3"]:o["b3"] + L3.cout])]
         else:
             self._wgrad("c3", da3, a2, B, L3.hin, L3.cin, L3.k, L3.s, L3.cout, o["w3"])
             self._bias(da3, B * L3.hout ** 2, L3.cout, o["b3"])
@@ -402,9 +414,9 @@ class DeviceNatureCNN:
         da1 = self.da1[:B * L1.hout ** 2 * L1.cout]
         if self.fused_convs:
             nblk = min(B, self.cus)
-            h.conv2_bwd(da2, sh[o["w2"]:o["b2"]], a1, da1, self.part, self.bias_part, B, nblk)
-            h.sum_splits(self.part, nblk, L2.cout * L2.K, g[o["w2"]:o["b2"]])
-            h.sum_splits(self.bias_part, nblk * 8, L2.cout, g[o["b2"]:o["b2"] + L2.cout])
+            h.conv2_bwd(da2, sh[o["w2"]:o["b2"]], a1, da1, self.cpart["c2"], self.cbias["c2"], B, nblk)
+            sums += [(self.cpart["c2"], nblk, L2.cout * L2.K, g[o["w2"]:o["b2"]]),
+                     (self.cbias["c2"], nblk * 8, L2.cout, g[o["b2"]:o["b2"] + L2.cout])]
         else:
             self._wgrad("c2", da2, a1, B, L2.hin, L2.cin, L2.k, L2.s, L2.cout, o["w2"])
             self._bias(da2, B * L2.hout ** 2, L2.cout, o["b2"])
@@ -412,9 +424,11 @@ class DeviceNatureCNN:
         # conv1 (input = frames, no data gradient)
         # (its bias gradient comes out of the same pass over da1)
         if self.fused_convs:
-            ns = int(h.conv1_wgrad8(obs_u8.contiguous(), da1, self.part, self.bias_part, B, min(B, self.cus)))
-            h.sum_splits(self.part, ns, S2D.cout * S2D.K, g[o["w1"]:o["b1"]])
-            h.sum_splits(self.bias_part, ns, S2D.cout, g[o["b1"]:o["b1"] + S2D.cout])
+            ns = int(h.conv1_wgrad8(obs_u8.contiguous(), da1, self.cpart["c1"], self.cbias["c1"], B,
+                                    min(B, self.cus)))
+            sums += [(self.cpart["c1"], ns, S2D.cout * S2D.K, g[o["w1"]:o["b1"]]),
+                     (self.cbias["c1"], ns, S2D.cout, g[o["b1"]:o["b1"] + S2D.cout])]
+            h.sum_splits_multi(sums)
         else:
             self._wgrad("c1", da1, obs_u8.contiguous(), B, S2D.hin, S2D.cin, S2D.k, S2D.s, S2D.cout, o["w1"],
                         bias_off=o["b1"])

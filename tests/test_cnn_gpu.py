@@ -642,3 +642,21 @@ def test_fc_tn_part_matches_fp32(cuda, R, I, J, splits):
     ref = x.double().t() @ y.double()
     assert torch.isfinite(got).all()
     assert ((got.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
+
+
+def test_sum_splits_multi_matches_torch(cuda):
+    """Several slab sums in one launch (the conv layers' weight / bias partials)."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    g = torch.Generator(device=cuda).manual_seed(0)
+    shapes = [(256, 36864), (2048, 64), (256, 32768), (7, 32), (1, 8)]
+    segs, refs = [], []
+    for s, n in shapes:
+        p = torch.randn(s * n, device=cuda, generator=g)
+        out = torch.full((n,), float("nan"), device=cuda)
+        segs.append((p, s, n, out))
+        refs.append(p.view(s, n).double().sum(0))
+    h.sum_splits_multi(segs)
+    for (_, s, n, out), ref in zip(segs, refs):
+        assert torch.allclose(out.double(), ref, atol=1e-4, rtol=1e-5), (s, n)
