@@ -50,6 +50,9 @@ int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, flo
                   float* ep_acc, int N, unsigned long long seed, unsigned long long step,
                   const unsigned long long* step_base, int max_steps, int reset_all, void* stream);
 int rrl_pong_render(const float* state, uint8_t* obs, int N, void* stream);
+int rrl_pong_step_render(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
+                         float* ep_acc, uint8_t* obs, int N, unsigned long long seed, unsigned long long step,
+                         const unsigned long long* step_base, int max_steps, int reset_all, void* stream);
 int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
                        const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2, uint16_t* y3, int N,
                        int max_grid, void* stream);
@@ -415,7 +418,7 @@ int64_t pong_state_size() { return rrl_pong_state_size(); }
 
 void pong_step(const Tensor& state, const Tensor& act, const Tensor& rew, const Tensor& done, const Tensor& fin_ret,
                const Tensor& fin_len, const OptT& ep_acc, int64_t N, int64_t seed, int64_t step, int64_t max_steps,
-               bool reset_all, const OptT& step_base) {
+               bool reset_all, const OptT& step_base, const OptT& obs) {
   check(state, "state", at::kFloat, N * pong_state_size());
   check(act, "act", at::kInt, reset_all ? 0 : N);
   check(rew, "rew", at::kFloat, N);
@@ -424,6 +427,15 @@ void pong_step(const Tensor& state, const Tensor& act, const Tensor& rew, const 
   check(fin_len, "fin_len", at::kFloat, N);
   float* acc = opt_ptr<float>(ep_acc, "ep_acc", at::kFloat, 4 * N);
   const unsigned long long* sb = opt_ptr<const unsigned long long>(step_base, "step_base", at::kLong, 1);
+  if (obs.has_value() && obs->defined()) {  // step + render in one launch (pong.hip)
+    check(*obs, "obs", at::kByte, N * 84 * 84 * 4);
+    rc_check(rrl_pong_step_render(state.data_ptr<float>(), act.data_ptr<int32_t>(), rew.data_ptr<float>(),
+                                  done.data_ptr<float>(), fin_ret.data_ptr<float>(), fin_len.data_ptr<float>(), acc,
+                                  obs->data_ptr<uint8_t>(), (int)N, (uint64_t)seed, (uint64_t)step, sb,
+                                  (int)max_steps, reset_all ? 1 : 0, stream()),
+             "pong_step_render");
+    return;
+  }
   rc_check(rrl_pong_step(state.data_ptr<float>(), act.data_ptr<int32_t>(), rew.data_ptr<float>(),
                          done.data_ptr<float>(), fin_ret.data_ptr<float>(), fin_len.data_ptr<float>(), acc, (int)N,
                          (uint64_t)seed, (uint64_t)step, sb, (int)max_steps, reset_all ? 1 : 0, stream()),
@@ -487,6 +499,7 @@ void register_cnn_ops(pybind11::module_& m) {
   m.def("pong_step", &pong_step, pybind11::arg("state"), pybind11::arg("act"), pybind11::arg("rew"),
         pybind11::arg("done"), pybind11::arg("fin_ret"), pybind11::arg("fin_len"), pybind11::arg("ep_acc"),
         pybind11::arg("N"), pybind11::arg("seed"), pybind11::arg("step"), pybind11::arg("max_steps"),
-        pybind11::arg("reset_all"), pybind11::arg("step_base") = pybind11::none());
+        pybind11::arg("reset_all"), pybind11::arg("step_base") = pybind11::none(),
+        pybind11::arg("obs") = pybind11::none());
   m.def("pong_render", &pong_render);
 }

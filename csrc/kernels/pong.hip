@@ -47,12 +47,12 @@ RRL_DEV void reset_env(float* s, uint4 r) {
   for (int f = 0; f < 4; ++f) push_hist(s);
 }
 
-__global__ void pong_step_kernel(float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew,
-                                 float* __restrict__ done, float* __restrict__ fin_ret, float* __restrict__ fin_len,
-                                 float* __restrict__ ep_acc, int N, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
-                                 int reset_all, const unsigned long long* __restrict__ step_base) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= N) return;
+// One env's step (frame-skip 4); state row written back.  Shared by pong_step_kernel (one
+// thread per env) and pong_step_render_kernel (one workgroup per env).
+RRL_DEV void pong_step_env(int e, float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew,
+                           float* __restrict__ done, float* __restrict__ fin_ret, float* __restrict__ fin_len,
+                           float* __restrict__ ep_acc, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
+                           int reset_all, const unsigned long long* __restrict__ step_base) {
   if (step_base) {  // device step counter (graph replays): the host value is an offset
     const unsigned long long st = (((unsigned long long)step_hi << 32) | step_lo) + *step_base;
     step_lo = (uint32_t)st;
@@ -126,6 +126,16 @@ __global__ void pong_step_kernel(float* __restrict__ state, const int32_t* __res
   for (int i = 0; i < kPongState; ++i) state[(size_t)e * kPongState + i] = s[i];
 }
 
+__global__ void pong_step_kernel(float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew,
+                                 float* __restrict__ done, float* __restrict__ fin_ret, float* __restrict__ fin_len,
+                                 float* __restrict__ ep_acc, int N, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
+                                 int reset_all, const unsigned long long* __restrict__ step_base) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= N) return;
+  pong_step_env(e, state, act, rew, done, fin_ret, fin_len, ep_acc, key, step_lo, step_hi, max_steps, reset_all,
+                step_base);
+}
+
 // One thread per (env, row): 84 pixels x 4 frames = 21 x 16 B.  The observation is
 // written space-to-depth: obs[n][a][b][dy][dx][f] with y = 4a + dy, x = 4b + dx (i.e.
 // [N][21][21][64]), so the first 8x8/4 conv becomes a 2x2/1 conv over 64 contiguous
@@ -135,16 +145,24 @@ __global__ void pong_step_kernel(float* __restrict__ state, const int32_t* __res
 // order, so every wave stores 1 KB contiguously.  Chunk q of an env's [21][21][64] s2d
 // frame: a = q / 84 (block row), c = (q % 84) / 4 (block column), dy = q % 4 (row in the
 // 4x4 block) -> image row y = 4a + dy, pixels x = 4c .. 4c+3.
-__global__ void pong_render_kernel(const float* __restrict__ state, uint8_t* __restrict__ obs, int N) {
-  constexpr int kChunks = kPongHW * kPongHW * 4 / 16;  // 1764 per env
-  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (t >= (size_t)N * kChunks) return;
-  const int e = (int)(t / kChunks), q = (int)(t % kChunks);
+// 16-byte chunk q (0 .. 1763) of one env's s2d frame stack from its (bx, by, pa, po) history h.
+RRL_DEV uint4 pong_render_chunk(const float* h, int q) {
   const int a = q / 84, rem = q - a * 84, c = rem >> 2, dy = rem & 3;
-  const float* h = state + (size_t)e * kPongState + P_HIST;
   const float fy = (float)(4 * a + dy) + 0.5f;
   const bool wall = fy < kTop || fy >= kBot;
   uint32_t w[4] = {0u, 0u, 0u, 0u};
+  // rows with nothing lit in any frame (most of the screen): the wall / background pattern
+  // only -- whole waves skip the per-pixel tests below
+  bool lit = false;
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const float by = h[4 * f + 1], pa = h[4 * f + 2], po = h[4 * f + 3];
+    lit |= (fy >= by && fy < by + kBall) || fabsf(fy - pa) < kPadHalf || fabsf(fy - po) < kPadHalf;
+  }
+  if (!lit) {
+    const uint32_t v = wall ? 0x64646464u : 0u;
+    return make_uint4(v, v, v, v);
+  }
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
     const float bx = h[4 * f], by = h[4 * f + 1], pa = h[4 * f + 2], po = h[4 * f + 3];
@@ -161,7 +179,39 @@ __global__ void pong_render_kernel(const float* __restrict__ state, uint8_t* __r
       w[px] |= v << (8 * f);
     }
   }
-  *reinterpret_cast<uint4*>(obs + t * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__global__ void pong_render_kernel(const float* __restrict__ state, uint8_t* __restrict__ obs, int N) {
+  constexpr int kChunks = kPongHW * kPongHW * 4 / 16;  // 1764 per env
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= (size_t)N * kChunks) return;
+  const int e = (int)(t / kChunks), q = (int)(t % kChunks);
+  *reinterpret_cast<uint4*>(obs + t * 16) = pong_render_chunk(state + (size_t)e * kPongState + P_HIST, q);
+}
+
+// Step + render in one launch: workgroup e steps env e on one thread (the physics is a short
+// serial chain) and renders its 1,764 chunks on all 256 threads from the new history in LDS.
+// One launch per env step instead of two, and the tiny step kernel's own launch / drain is gone.
+__global__ void __launch_bounds__(256) pong_step_render_kernel(
+    float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew, float* __restrict__ done,
+    float* __restrict__ fin_ret, float* __restrict__ fin_len, float* __restrict__ ep_acc, uint8_t* __restrict__ obs,
+    uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps, int reset_all,
+    const unsigned long long* __restrict__ step_base) {
+  constexpr int kChunks = kPongHW * kPongHW * 4 / 16;
+  __shared__ float hist[16];
+  const int e = blockIdx.x;
+  if (threadIdx.x == 0) {
+    pong_step_env(e, state, act, rew, done, fin_ret, fin_len, ep_acc, key, step_lo, step_hi, max_steps, reset_all,
+                  step_base);
+    // the new history to LDS by the thread that wrote it (its own global writes, program order)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) hist[i] = state[(size_t)e * kPongState + P_HIST + i];
+  }
+  __syncthreads();
+  uint8_t* o = obs + (size_t)e * kChunks * 16;
+  for (int q = threadIdx.x; q < kChunks; q += 256)
+    *reinterpret_cast<uint4*>(o + (size_t)q * 16) = pong_render_chunk(hist, q);
 }
 
 }  // namespace rrl
@@ -180,6 +230,17 @@ int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, flo
   hipLaunchKernelGGL(pong_step_kernel, dim3((N + 255) / 256), dim3(256), 0, st, state, act, rew, done, fin_ret,
                      fin_len, ep_acc, N, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, reset_all,
                      step_base);
+  return (int)hipGetLastError();
+}
+
+int rrl_pong_step_render(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
+                         float* ep_acc, uint8_t* obs, int N, unsigned long long seed, unsigned long long step,
+                         const unsigned long long* step_base, int max_steps, int reset_all, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  if (N < 1) return 0;
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  hipLaunchKernelGGL(pong_step_render_kernel, dim3(N), dim3(256), 0, st, state, act, rew, done, fin_ret, fin_len,
+                     ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, reset_all, step_base);
   return (int)hipGetLastError();
 }
 

@@ -222,9 +222,8 @@ class DevicePong:
 
     def reset(self, obs_out: torch.Tensor):
         self.h.pong_step(self.state, self._dummy_act, self.rew, self.done, self.fin_ret, self.fin_len, None, self.N,
-                         self.seed, 0, self.max_steps, True, self.step_t)
+                         self.seed, 0, self.max_steps, True, self.step_t, obs=obs_out)
         self.advance(1)
-        self.h.pong_render(self.state, obs_out, self.N)
 
     def episode_stats(self):
         """(episodes, sum return, sum length, sum return^2) over all envs since the last reset."""
@@ -235,9 +234,9 @@ class DevicePong:
         with it (graph-captured rollouts) the caller advances once per rollout."""
         rew = self.rew if rew_out is None else rew_out
         done = self.done if done_out is None else done_out
+        # physics + render of the new 4-frame stack in one launch (one workgroup per env)
         self.h.pong_step(self.state, act, rew, done, self.fin_ret, self.fin_len, self.ep_acc, self.N, self.seed,
-                         0 if offset is None else int(offset), self.max_steps, False, self.step_t)
+                         0 if offset is None else int(offset), self.max_steps, False, self.step_t, obs=obs_out)
         if offset is None:
             self.advance(1)
-        self.h.pong_render(self.state, obs_out, self.N)
         return rew, done

@@ -248,6 +248,10 @@ class DeviceNatureCNN:
                           "c2": torch.empty(nb * 8 * L2_.cout, device=dev),
                           "c1": torch.empty(2 * nb * S2D.cout, device=dev)}
         self.sq_work = torch.empty(1024, device=dev)
+        # side stream for the head / fc weight gradients (backward, one rank; RRL_CNN_SIDE=0: off)
+        self.side_stream = torch.cuda.Stream(device=dev) if os.environ.get("RRL_CNN_SIDE", "1") != "0" else None
+        self._ev_fork = torch.cuda.Event()
+        self._ev_join = torch.cuda.Event()
         self.norm_sq = torch.empty(1, device=dev)
 
     @staticmethod
@@ -379,15 +383,33 @@ class DeviceNatureCNN:
                    1.0 / B, float(vf_coef), float(ent_coef), dh, dhead, stats, grid)
         nb = max(1, min(self.head_blocks, B))
         hp = self.head_part[:nb * self.spec.head_size]
-        h.head_wgrad(hid, dhead, B, self.A, hp, nb)
-        h.sum_splits(hp, nb, self.spec.head_size, g[o["head"]:o["P"]])
-        # fc
-        if self.fc_nt and B % 64 == 0:
-            used = int(h.fc_tn_part(dh, a3, self.part, B, HIDDEN, FC_IN, self.FC_WGRAD_SPLITS))
-            h.sum_splits(self.part, used, HIDDEN * FC_IN, g[o["wfc"]:o["bfc"]])
+        # The head / fc weight gradients depend only on (dh, dhead, hid, a3), not on the conv
+        # chain below: on one rank they run on a side stream, concurrently with the fc data
+        # gradient and the conv backward (their buffers -- head_part, part, bias_part -- are
+        # not touched by the fused conv path, which has its own slabs).  The DP path keeps one
+        # stream: its fc bucket all-reduce is issued as soon as these gradients are final.
+        side = (self.side_stream if (self.side_stream is not None and self.fused_convs and self.fc_nt
+                                     and B % 64 == 0 and (comm is None or comm.world <= 1)) else None)
+        if side is not None:
+            self._ev_fork.record()
+            side.wait_event(self._ev_fork)
+            ctx = torch.cuda.stream(side)
         else:
-            self._wgrad("fc", dh, a3, B, 1, FC_IN, 1, 1, HIDDEN, o["wfc"])
-        self._bias(dh, B, HIDDEN, o["bfc"])
+            import contextlib
+
+            ctx = contextlib.nullcontext()
+        with ctx:
+            h.head_wgrad(hid, dhead, B, self.A, hp, nb)
+            h.sum_splits(hp, nb, self.spec.head_size, g[o["head"]:o["P"]])
+            # fc
+            if self.fc_nt and B % 64 == 0:
+                used = int(h.fc_tn_part(dh, a3, self.part, B, HIDDEN, FC_IN, self.FC_WGRAD_SPLITS))
+                h.sum_splits(self.part, used, HIDDEN * FC_IN, g[o["wfc"]:o["bfc"]])
+            else:
+                self._wgrad("fc", dh, a3, B, 1, FC_IN, 1, 1, HIDDEN, o["wfc"])
+            self._bias(dh, B, HIDDEN, o["bfc"])
+            if side is not None:
+                self._ev_join.record(side)
         da3 = self.da3[:B * FC_IN]
         if self.fc_nt:
             h.fc_nt_mask(dh, self.wfc_t, a3, da3, B, FC_IN, HIDDEN)
@@ -432,6 +454,8 @@ class DeviceNatureCNN:
         else:
             self._wgrad("c1", da1, obs_u8.contiguous(), B, S2D.hin, S2D.cin, S2D.k, S2D.s, S2D.cout, o["w1"],
                         bias_off=o["b1"])
+        if side is not None:
+            torch.cuda.current_stream().wait_event(self._ev_join)
         if pending is not None:
             comm.all_reduce_sum_(g[:o["wfc"]])
             pending.wait()

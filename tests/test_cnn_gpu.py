@@ -660,3 +660,30 @@ def test_sum_splits_multi_matches_torch(cuda):
     h.sum_splits_multi(segs)
     for (_, s, n, out), ref in zip(segs, refs):
         assert torch.allclose(out.double(), ref, atol=1e-4, rtol=1e-5), (s, n)
+
+
+def test_pong_step_render_fused_matches_separate(cuda):
+    """One-launch step + render (a workgroup per env) == step kernel then render kernel, bitwise."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    N, S = 300, int(hip().pong_state_size())
+    g = torch.Generator().manual_seed(3)
+    st0 = torch.zeros(N * S, device=cuda)
+    o1 = torch.empty(N, 21, 21, 64, dtype=torch.uint8, device=cuda)
+    o2 = torch.empty_like(o1)
+    z = [torch.zeros(N, device=cuda) for _ in range(4)]
+    dummy = torch.zeros(N, dtype=torch.int32, device=cuda)
+    h.pong_step(st0, dummy, *z, None, N, 11, 0, 400, True)
+    s1, s2 = st0.clone(), st0.clone()
+    acc1, acc2 = torch.zeros(4 * N, device=cuda), torch.zeros(4 * N, device=cuda)
+    for t in range(1, 60):
+        a = torch.randint(0, 6, (N,), dtype=torch.int32, generator=g).to(cuda)
+        r1 = [torch.zeros(N, device=cuda) for _ in range(4)]
+        r2 = [torch.zeros(N, device=cuda) for _ in range(4)]
+        h.pong_step(s1, a, *r1, acc1, N, 11, t, 400, False)
+        h.pong_render(s1, o1, N)
+        h.pong_step(s2, a, *r2, acc2, N, 11, t, 400, False, obs=o2)
+        assert torch.equal(s1, s2) and torch.equal(o1, o2)
+        assert all(torch.equal(x, y) for x, y in zip(r1, r2))
+    assert torch.equal(acc1, acc2)
