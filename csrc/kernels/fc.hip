@@ -32,6 +32,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "gemm_bf16.h"
 
 namespace rrl {
@@ -78,6 +80,23 @@ struct FcMaskEpi {
         make_uint2((uint32_t)f2bf(o0) | ((uint32_t)f2bf(o1) << 16), (uint32_t)f2bf(o2) | ((uint32_t)f2bf(o3) << 16));
   }
 };
+
+// Same product, but the tile leaves through LDS: the accumulators are packed to bf16 into a
+// [128][136] image in the (now idle) stage buffers, then each thread moves 8 consecutive
+// columns of one row (16-byte mask load + 16-byte store, 256 contiguous bytes per 16 lanes)
+// -- the direct epilogue wrote 32-byte pieces of 16 rows per instruction, which left the
+// 0.26 GB data-gradient output / mask streams of a 40,960-row update at ~1.2 TB/s.
+// N % 8 == 0.
+struct FcMaskStagedEpi {
+  uint16_t* out;
+  const uint16_t* mask;
+  int M, N;
+  static constexpr int kLd = 136;  // bf16 row stride of the staging image
+};
+template <class Epi, class = void>
+struct FcStaged : std::false_type {};
+template <>
+struct FcStaged<FcMaskStagedEpi> : std::true_type {};
 
 // One k-tile of one operand into its LDS image: the wave's two DMA instructions fill image
 // rows 16 w .. 16 w + 15 (8 rows x 8 chunks = the instruction's 64 lanes x 16 B each).
@@ -132,11 +151,13 @@ fc_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, Epi
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  typename Epi::Pre pre[4][2];
+  typedef typename std::conditional<FcStaged<Epi>::value, FcPartEpi, Epi>::type DirectEpi;
+  typename DirectEpi::Pre pre[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) pre[i][j] = typename Epi::Pre{};
+    for (int j = 0; j < 2; ++j) pre[i][j] = typename DirectEpi::Pre{};
+  uint4 spre[4] = {};  // staged epilogue: this thread's 4 mask chunks
   auto issue = [&](int t) {
     uint16_t* st = smem + (t % STAGES) * kFcStage;
     const int k0 = (kt0 + t) * kFcBK;
@@ -159,10 +180,20 @@ fc_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, Epi
     asm volatile("" ::: "memory");
     if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
     if (t + 1 == nk) {  // no DMA in flight any more: the epilogue's own loads go out now
+      if constexpr (FcStaged<Epi>::value) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int k = 0; k < 4; ++k) {
+          const int c = tid + kFcThreads * k;
+          const int m = min(m0 + (c >> 4), M - 1), n = min(n0 + (c & 15) * 8, N - 8);  // clamped: no branch
+          spre[k] = *reinterpret_cast<const uint4*>(epi.mask + (size_t)m * N + n);
+        }
+      } else {
 #pragma unroll
-        for (int j = 0; j < 2; ++j) pre[i][j] = epi.prefetch(m0 + 64 * wm + 16 * i + li, n0 + 32 * wn + 16 * j + 4 * g);
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            pre[i][j] = epi.prefetch(m0 + 64 * wm + 16 * i + li, n0 + 32 * wn + 16 * j + 4 * g);
+      }
     }
     const uint16_t* Ai = smem + (t % STAGES) * kFcStage;
     const uint16_t* Bi = Ai + kFcImg;
@@ -183,10 +214,45 @@ fc_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, Epi
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
   }
+  if constexpr (FcStaged<Epi>::value) {
+    constexpr int LD = FcMaskStagedEpi::kLd;
+    uint16_t* T = smem;  // [128][LD] bf16 = 34,816 B over the idle stage buffers
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading the operand stages
+    asm volatile("" ::: "memory");
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) epi(m0 + 64 * wm + 16 * i + li, n0 + 32 * wn + 16 * j + 4 * g, acc[i][j], z, pre[i][j]);
+      for (int j = 0; j < 2; ++j)
+        *reinterpret_cast<uint2*>(T + (64 * wm + 16 * i + li) * LD + 32 * wn + 16 * j + 4 * g) =
+            make_uint2((uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16),
+                       (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = tid + kFcThreads * k, r = c >> 4, cc = (c & 15) * 8;
+      const int m = m0 + r, n = n0 + cc;
+      if (m >= M || n >= N) continue;
+      const uint4 v = *reinterpret_cast<const uint4*>(T + r * LD + cc);
+      const uint32_t vw[4] = {v.x, v.y, v.z, v.w}, mw[4] = {spre[k].x, spre[k].y, spre[k].z, spre[k].w};
+      uint32_t ow[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // keep where the layer input was > 0 (bf16 -> f32 is exact)
+        const uint32_t lo = bf2f((uint16_t)(mw[e] & 0xffff)) > 0.f ? 0x0000ffffu : 0u;
+        const uint32_t hi = bf2f((uint16_t)(mw[e] >> 16)) > 0.f ? 0xffff0000u : 0u;
+        ow[e] = vw[e] & (lo | hi);
+      }
+      *reinterpret_cast<uint4*>(epi.out + (size_t)m * N + n) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        epi(m0 + 64 * wm + 16 * i + li, n0 + 32 * wn + 16 * j + 4 * g, acc[i][j], z, pre[i][j]);
+  }
 }
 
 static int fc_m_fast() {
@@ -404,9 +470,22 @@ int rrl_fc_nt_part(const uint16_t* a, const uint16_t* b, float* part, int M, int
 int rrl_fc_nt_mask(const uint16_t* a, const uint16_t* b, const uint16_t* mask, uint16_t* out, int M, int N, int K,
                    void* stream_) {
   if (K % kFcBK || N % 4 || M < 1 || N < 1) return -1;
+  hipStream_t st = (hipStream_t)stream_;
+  // The staged epilogue pays when the output and mask streams leave the 256 MB Infinity
+  // Cache (40,960 x 3,136: 276 -> 220 us in tools/fc_kbench.py); at 10,240 rows inside the
+  // Pong update (both streams cache-resident, the side-stream weight gradients competing for
+  // the CUs) the direct epilogue measured 0.7 % faster end to end (profiles/r3_pong_*).
+  // RRL_FC_DIRECT_EPI = 1 / 0 forces either.
+  const char* e = getenv("RRL_FC_DIRECT_EPI");
+  const bool big = (long long)M * N * 2 > (96ll << 20);
+  if (N % 8 == 0 && (e && e[0] ? e[0] == '0' : big)) {
+    const FcMaskStagedEpi epi{out, mask, M, N};
+    return fc_stages(1, 2) == 3 ? launch_fc_nt<FcMaskStagedEpi, 3>(a, b, epi, M, N, K, 1, st)
+                                : launch_fc_nt<FcMaskStagedEpi, 2>(a, b, epi, M, N, K, 1, st);
+  }
   const FcMaskEpi epi{out, mask, M, N};
-  return fc_stages(1, 2) == 3 ? launch_fc_nt<FcMaskEpi, 3>(a, b, epi, M, N, K, 1, (hipStream_t)stream_)
-                              : launch_fc_nt<FcMaskEpi, 2>(a, b, epi, M, N, K, 1, (hipStream_t)stream_);
+  return fc_stages(1, 2) == 3 ? launch_fc_nt<FcMaskEpi, 3>(a, b, epi, M, N, K, 1, st)
+                              : launch_fc_nt<FcMaskEpi, 2>(a, b, epi, M, N, K, 1, st);
 }
 
 // fp32 partials part[splits][I][J] of X[R][I]^T . Y[R][J] (R % 64 == 0, I, J % 8 == 0);

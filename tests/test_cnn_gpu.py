@@ -576,10 +576,12 @@ def test_fc_nt_part_matches_fp32(cuda, M, N, K, splits):
     assert ((got.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
 
 
+@pytest.mark.parametrize("epi", ["0", "1"])  # RRL_FC_DIRECT_EPI: 0 = LDS-staged 16-byte epilogue, 1 = direct
 @pytest.mark.parametrize("M", [37, 1000])
-def test_fc_nt_mask_matches_fp32(cuda, M):
+def test_fc_nt_mask_matches_fp32(cuda, M, epi, monkeypatch):
     from relayrl_prototype_amd.ops import hip
 
+    monkeypatch.setenv("RRL_FC_DIRECT_EPI", epi)
     h = hip()
     g = torch.Generator().manual_seed(M)
     dh = _bf(torch.randn(M, HIDDEN, generator=g))

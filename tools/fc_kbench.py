@@ -42,6 +42,21 @@ def main():
     da3 = torch.empty(Mb * FC_IN, dtype=torch.bfloat16, device=dev)
     work = torch.empty(16 * Mf * HIDDEN, device=dev)
     wpart = torch.empty(8 * HIDDEN * FC_IN, device=dev)
+    Mx = 4 * Mb  # the 8192-env update (40,960 rows): outputs past the Infinity Cache
+    a3x = torch.randn(Mx * FC_IN, device=dev, generator=g).relu().bfloat16()
+    dhx = torch.randn(Mx * HIDDEN, device=dev, generator=g).bfloat16()
+    da3x = torch.empty(Mx * FC_IN, dtype=torch.bfloat16, device=dev)
+
+    def direct(fn):
+        def run():
+            os.environ["RRL_FC_DIRECT_EPI"] = "1"
+            try:
+                fn()
+            finally:
+                os.environ["RRL_FC_DIRECT_EPI"] = "0"  # forced staged for the other cases
+        return run
+
+    os.environ["RRL_FC_DIRECT_EPI"] = "0"
     cases = {
         "fwd_part_s4": lambda: h.fc_nt_part(a3, w, part, Mf, HIDDEN, FC_IN, 4),
         "fwd_part_s8": lambda: h.fc_nt_part(a3, w, part, Mf, HIDDEN, FC_IN, 8),
@@ -49,12 +64,15 @@ def main():
                                                     True, work),
         "dgrad_mask": lambda: h.fc_nt_mask(dh, wt, a3, da3, Mb, FC_IN, HIDDEN),
         "dgrad_old": lambda: h.gemm_dgrad(dh, w, a3, da3, Mb, HIDDEN, FC_IN),
+        "dgrad_mask_direct": direct(lambda: h.fc_nt_mask(dh, wt, a3, da3, Mb, FC_IN, HIDDEN)),
+        "dgrad40k_mask": lambda: h.fc_nt_mask(dhx, wt, a3x, da3x, Mx, FC_IN, HIDDEN),
+        "dgrad40k_mask_direct": direct(lambda: h.fc_nt_mask(dhx, wt, a3x, da3x, Mx, FC_IN, HIDDEN)),
         "wgrad_tn_s2": lambda: h.fc_tn_part(dh, a3, wpart, Mb, HIDDEN, FC_IN, 2),
         "wgrad_tn_s5": lambda: h.fc_tn_part(dh, a3, wpart, Mb, HIDDEN, FC_IN, 5),
         "wgrad_tn_s8": lambda: h.fc_tn_part(dh, a3, wpart, Mb, HIDDEN, FC_IN, 8),
         "wgrad_old_s2": lambda: h.conv_wgrad(dh, a3, wpart, 2, Mb, 1, 1, FC_IN, 1, 1, 1, HIDDEN),
     }
-    variants = os.environ.get("FC_VARIANTS", "322,422,323,32m2").split(",")
+    variants = os.environ.get("FC_VARIANTS", "422,432").split(",")
     res = {}
     for _ in range(5):
         for v in variants:
