@@ -43,7 +43,8 @@ int rrl_fc_nt_part(const uint16_t* a, const uint16_t* b, float* part, int M, int
 int rrl_fc_nt_mask(const uint16_t* a, const uint16_t* b, const uint16_t* mask, uint16_t* out, int M, int N, int K,
                    void* stream);
 int rrl_transpose_bf16(const uint16_t* in, uint16_t* out, int R, int C, void* stream);
-int rrl_fc_tn_part(const uint16_t* x, const uint16_t* y, float* part, int R, int I, int J, int splits, void* stream);
+int rrl_fc_tn_part(const uint16_t* x, const uint16_t* y, float* part, int R, int I, int J, int splits,
+                   const uint16_t* ones, float* bias_part, void* stream);
 int rrl_head_wgrad(const uint16_t* h, const float* dhead, int B, int A, float* part, int nblk, void* stream);
 int rrl_pong_state_size();
 int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
@@ -385,14 +386,20 @@ void fc_nt_mask(const Tensor& a, const Tensor& b, const Tensor& mask, const Tens
 // fp32 partials part[splits][I][J] of x[R][I]^T . y[R][J] (fc.hip, the fc weight gradient);
 // returns the number of splits used.
 int64_t fc_tn_part(const Tensor& x, const Tensor& y, const Tensor& part, int64_t R, int64_t I, int64_t J,
-                   int64_t splits) {
+                   int64_t splits, const OptT& ones, const OptT& bias_part) {
   TORCH_CHECK(R >= 64 && R % 64 == 0 && I > 0 && J > 0 && I % 8 == 0 && J % 8 == 0 && splits >= 1,
               "fc_tn_part: bad shape");
   check(x, "x", at::kBFloat16, R * I);
   check(y, "y", at::kBFloat16, R * J);
   const int64_t rt = R / 64, kps = (rt + splits - 1) / splits, used = (rt + kps - 1) / kps;
   check(part, "part", at::kFloat, used * I * J);
-  const int rc = rrl_fc_tn_part(bf(x), bf(y), part.data_ptr<float>(), R, I, J, (int)splits, stream());
+  // optional: bias gradient (row sums of x) through a column of ones in the padded last tile
+  const uint16_t* on = ones.has_value() && ones->defined() ? (check(*ones, "ones", at::kBFloat16, 8), bf(*ones))
+                                                           : nullptr;
+  float* bp = opt_ptr<float>(bias_part, "bias_part", at::kFloat, used * I);
+  TORCH_CHECK((on == nullptr) == (bp == nullptr) && (!bp || J % 128 != 0),
+              "fc_tn_part: ones and bias_part go together and need J % 128 != 0");
+  const int rc = rrl_fc_tn_part(bf(x), bf(y), part.data_ptr<float>(), R, I, J, (int)splits, on, bp, stream());
   TORCH_CHECK(rc > 0, "fc_tn_part failed with code ", rc);
   return rc;
 }
@@ -493,7 +500,9 @@ void register_cnn_ops(pybind11::module_& m) {
   m.def("fc_nt_part", &fc_nt_part);
   m.def("fc_nt_mask", &fc_nt_mask);
   m.def("transpose_bf16", &transpose_bf16);
-  m.def("fc_tn_part", &fc_tn_part);
+  m.def("fc_tn_part", &fc_tn_part, pybind11::arg("x"), pybind11::arg("y"), pybind11::arg("part"), pybind11::arg("R"),
+        pybind11::arg("I"), pybind11::arg("J"), pybind11::arg("splits"), pybind11::arg("ones") = pybind11::none(),
+        pybind11::arg("bias_part") = pybind11::none());
   m.def("head_wgrad", &head_wgrad);
   m.def("pong_state_size", &pong_state_size);
   m.def("pong_step", &pong_step, pybind11::arg("state"), pybind11::arg("act"), pybind11::arg("rew"),

@@ -299,15 +299,18 @@ static int launch_fc_nt(const uint16_t* A, const uint16_t* B, Epi epi, int M, in
 // which spreads those 8 rows x 2 chunks over 16 distinct chunk slots (conflict-free).
 __device__ __forceinline__ int fc_tn_swz(int row, int c) { return row * 16 + (c ^ (2 * ((row & 3) | (((row >> 3) & 1) << 2)))); }
 
+// Columns past the end read a duplicate chunk (masked in the epilogue) -- or, with ``ones``
+// (16 bytes of bf16 1.0), a column of ones, so the padded output columns of the last tile
+// carry sum_r X[r][i]: the bias gradient of the layer for free.
 __device__ __forceinline__ void fc_tn_stage(const uint16_t* __restrict__ X, int ld, int r0g, int col0, uint16_t* img,
-                                            int wave, int lane) {
+                                            int wave, int lane, const uint16_t* __restrict__ ones = nullptr) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int r0 = 8 * wave + 4 * j;  // image rows r0 .. r0 + 3 (4 x 256 B = the instruction's 1 KB)
     const int r = r0 + (lane >> 4);
     const int c = (lane & 15) ^ (2 * ((r & 3) | (((r >> 3) & 1) << 2)));
-    const int col = min(col0 + 8 * c, ld - 8);  // columns past the end: a duplicate, masked in the epilogue
-    const uint16_t* src = X + (size_t)(r0g + r) * ld + col;
+    const int col = min(col0 + 8 * c, ld - 8);
+    const uint16_t* src = (ones && col0 + 8 * c >= ld) ? ones : X + (size_t)(r0g + r) * ld + col;
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(img + r0 * 128), 16, 0, 0);
   }
 }
@@ -333,7 +336,8 @@ __device__ __forceinline__ bf16x8_t fc_tn_frag(const uint16_t* img, int k0, int 
 template <int STAGES>
 __global__ void __launch_bounds__(kFcThreads, STAGES == 2 ? 2 : 1)
 fc_tn_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, float* __restrict__ part, int R, int I,
-             int J, int tiles_i, int tiles_j, int rtiles_per_split) {
+             int J, int tiles_i, int tiles_j, int rtiles_per_split, const uint16_t* __restrict__ ones,
+             float* __restrict__ bias_part) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nwg = gridDim.x, b = blockIdx.x;
@@ -357,7 +361,7 @@ fc_tn_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, flo
     uint16_t* st = smem + (t % STAGES) * kFcStage;
     const int r0g = (rt0 + t) * 64;
     fc_tn_stage(X, I, r0g, i0, st, wave, lane);
-    fc_tn_stage(Y, J, r0g, j0, st + kFcImg, wave, lane);
+    fc_tn_stage(Y, J, r0g, j0, st + kFcImg, wave, lane, ones);
   };
 #pragma unroll
   for (int t = 0; t < STAGES - 1; ++t)
@@ -393,12 +397,13 @@ fc_tn_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, flo
     for (int c = 0; c < 2; ++c) {
       const int i = i0 + 64 * wi + 16 * a + li, j = j0 + 32 * wj + 16 * c + 4 * g;
       if (i < I && j < J) *reinterpret_cast<f32x4_t*>(part + ((size_t)z * I + i) * J + j) = acc[a][c];
+      if (bias_part && i < I && j == J) bias_part[(size_t)z * I + i] = acc[a][c][0];  // the ones column
     }
 }
 
 template <int STAGES>
 static int launch_fc_tn(const uint16_t* X, const uint16_t* Y, float* part, int R, int I, int J, int splits,
-                        hipStream_t st) {
+                        const uint16_t* ones, float* bias_part, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)fc_tn_kernel<STAGES>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -409,7 +414,7 @@ static int launch_fc_tn(const uint16_t* X, const uint16_t* Y, float* part, int R
   const int kps = (rt + splits - 1) / splits;
   splits = (rt + kps - 1) / kps;
   hipLaunchKernelGGL((fc_tn_kernel<STAGES>), dim3(ti * tj * splits), dim3(kFcThreads), fc_lds_bytes<STAGES>(), st,
-                     X, Y, part, R, I, J, ti, tj, kps);
+                     X, Y, part, R, I, J, ti, tj, kps, ones, bias_part);
   return (int)hipGetLastError();
 }
 
@@ -490,13 +495,16 @@ int rrl_fc_nt_mask(const uint16_t* a, const uint16_t* b, const uint16_t* mask, u
 
 // fp32 partials part[splits][I][J] of X[R][I]^T . Y[R][J] (R % 64 == 0, I, J % 8 == 0);
 // returns the number of splits used.
+// With ``ones`` + ``bias_part`` (J % 128 != 0 and J % 4 == 0: the last column tile has a pad
+// column, J itself): bias_part[splits][I] = the row sums of X, i.e. the layer's bias gradient.
 int rrl_fc_tn_part(const uint16_t* x, const uint16_t* y, float* part, int R, int I, int J, int splits,
-                   void* stream_) {
+                   const uint16_t* ones, float* bias_part, void* stream_) {
   if (R % 64 || I % 8 || J % 8 || R < 64 || splits < 1) return -1;
+  if ((ones == nullptr) != (bias_part == nullptr) || (bias_part && J % 128 == 0)) return -1;
   const int rt = R / 64, kps = (rt + splits - 1) / splits, used = (rt + kps - 1) / kps;
   hipStream_t st = (hipStream_t)stream_;
-  const int rc = fc_stages(2, 2) == 2 ? launch_fc_tn<2>(x, y, part, R, I, J, used, st)
-                                      : launch_fc_tn<3>(x, y, part, R, I, J, used, st);
+  const int rc = fc_stages(2, 2) == 2 ? launch_fc_tn<2>(x, y, part, R, I, J, used, ones, bias_part, st)
+                                      : launch_fc_tn<3>(x, y, part, R, I, J, used, ones, bias_part, st);
   return rc ? -rc - 1000 : used;
 }
 

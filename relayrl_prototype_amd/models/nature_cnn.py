@@ -193,6 +193,8 @@ class DeviceNatureCNN:
         # the head kernel (bias + ReLU + bf16 + logits / value / sample in one launch), data
         # gradient against a transposed bf16 shadow of Wfc (RRL_FC_NT=0: the gemm_bf16.h path)
         self.fc_nt = os.environ.get("RRL_FC_NT", "1") != "0"
+        # fc bias gradient inside the weight-gradient GEMM (a ones column in its padded tile)
+        self.fc_tn_bias = os.environ.get("RRL_FC_TN_BIAS", "0") != "0"
         self.o = spec.offsets()
         self.P = self.o["P"]
         dev = self.device
@@ -233,6 +235,8 @@ class DeviceNatureCNN:
         need = max(need, min(B, self.cus) * CONVS[2].cout * CONVS[2].K)  # fused conv3 backward partials
         if self.fc_nt:
             need = max(need, self.FC_WGRAD_SPLITS * HIDDEN * FC_IN)
+            self._ones8 = torch.ones(8, dtype=torch.bfloat16, device=dev)
+            self._fc_bias_part = torch.empty(self.FC_WGRAD_SPLITS * HIDDEN, device=dev)
         self.part = torch.empty(need, device=dev)
         self.bias_splits = 512
         self.bias_part = torch.empty(max(self.bias_splits * HIDDEN, self.cus * 512), device=dev)
@@ -402,12 +406,20 @@ class DeviceNatureCNN:
             h.head_wgrad(hid, dhead, B, self.A, hp, nb)
             h.sum_splits(hp, nb, self.spec.head_size, g[o["head"]:o["P"]])
             # fc
-            if self.fc_nt and B % 64 == 0:
+            if self.fc_nt and B % 64 == 0 and self.fc_tn_bias:
+                # weight AND bias gradient in one GEMM: the padded last column tile of a3 reads a
+                # column of ones, so its first pad column holds the column sums of dh (fc.hip)
+                used = int(h.fc_tn_part(dh, a3, self.part, B, HIDDEN, FC_IN, self.FC_WGRAD_SPLITS, ones=self._ones8,
+                                        bias_part=self._fc_bias_part))
+                h.sum_splits_multi([(self.part, used, HIDDEN * FC_IN, g[o["wfc"]:o["bfc"]]),
+                                    (self._fc_bias_part, used, HIDDEN, g[o["bfc"]:o["bfc"] + HIDDEN])])
+            elif self.fc_nt and B % 64 == 0:
                 used = int(h.fc_tn_part(dh, a3, self.part, B, HIDDEN, FC_IN, self.FC_WGRAD_SPLITS))
                 h.sum_splits(self.part, used, HIDDEN * FC_IN, g[o["wfc"]:o["bfc"]])
+                self._bias(dh, B, HIDDEN, o["bfc"])
             else:
                 self._wgrad("fc", dh, a3, B, 1, FC_IN, 1, 1, HIDDEN, o["wfc"])
-            self._bias(dh, B, HIDDEN, o["bfc"])
+                self._bias(dh, B, HIDDEN, o["bfc"])
             if side is not None:
                 self._ev_join.record(side)
         da3 = self.da3[:B * FC_IN]

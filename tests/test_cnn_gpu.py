@@ -212,9 +212,9 @@ def test_full_model_forward_backward_matches_autograd(cuda):
         e = relerr(gd[a:b], pe.grad[a:b])
         assert e < 5e-2, (name, e)
         # biases separately (a wrong bias partial hides inside the weight block's norm)
-        if name.startswith("conv"):
-            L = CONVS[int(name[-1]) - 1]
-            eb = relerr(gd[b:b + L.cout], pe.grad[b:b + L.cout])
+        if name.startswith("conv") or name == "fc":
+            nb = HIDDEN if name == "fc" else CONVS[int(name[-1]) - 1].cout
+            eb = relerr(gd[b:b + nb], pe.grad[b:b + nb])
             assert eb < 5e-2, (name, "bias", eb)
     st = stats.sum(0).cpu()
     assert abs(st[3].item() - B) < 1e-3
@@ -644,6 +644,17 @@ def test_fc_tn_part_matches_fp32(cuda, R, I, J, splits):
     ref = x.double().t() @ y.double()
     assert torch.isfinite(got).all()
     assert ((got.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
+    if J % 128:  # bias gradient through the ones column of the padded last tile
+        ones = torch.ones(8, dtype=torch.bfloat16, device=cuda)
+        bp = torch.full((splits * I,), float("nan"), device=cuda)
+        part.fill_(float("nan"))
+        used2 = h.fc_tn_part(x.to(cuda).bfloat16().reshape(-1), y.to(cuda).bfloat16().reshape(-1), part, R, I, J,
+                             splits, ones=ones, bias_part=bp)
+        assert used2 == used
+        assert torch.equal(part[:used * I * J].view(used, I, J).sum(0).cpu(), got)  # weights unchanged
+        bsum = bp[:used * I].view(used, I).sum(0).cpu().double()
+        bref = x.double().sum(0)
+        assert ((bsum - bref).abs().max() / bref.abs().max()).item() < 1e-5
 
 
 def test_sum_splits_multi_matches_torch(cuda):
