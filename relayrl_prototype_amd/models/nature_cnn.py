@@ -194,7 +194,7 @@ class DeviceNatureCNN:
         # gradient against a transposed bf16 shadow of Wfc (RRL_FC_NT=0: the gemm_bf16.h path)
         self.fc_nt = os.environ.get("RRL_FC_NT", "1") != "0"
         # fc bias gradient inside the weight-gradient GEMM (a ones column in its padded tile)
-        self.fc_tn_bias = os.environ.get("RRL_FC_TN_BIAS", "0") != "0"
+        self.fc_tn_bias = os.environ.get("RRL_FC_TN_BIAS", "1") != "0"
         self.o = spec.offsets()
         self.P = self.o["P"]
         dev = self.device
