@@ -42,7 +42,9 @@ PRESETS: Dict[str, Preset] = {
         "vec", {"env": "CartPole-v1", "num_envs": 32768, "rollout_len": 64, "with_baseline": True}),
     "lunarlander-reinforce-baseline": Preset(
         "lunarlander-reinforce-baseline", "REINFORCE-with-baseline LunarLander, actor GPUs -> learner group "
-        "(P2P rollout fan-in to learner shards, gradient all-reduce inside the group)",
+        "(P2P rollout fan-in to learner shards, gradient all-reduce inside the group; default learner_ranks=0 = "
+        "every rank learns its own rollout, K = 1 -- the fastest on one node; --set learner_ranks=L for L "
+        "learner shards fed by W/L actor blocks each, as in bench.py's world > 1 actor-learner phase)",
         "actor_learner", {"env": "LunarLanderSynth-v0", "num_envs": 2048, "rollout_len": 128, "with_baseline": True,
                           "learner_acts": True, "learner_ranks": 0, "num_threads": 8}),
     "pong-a2c": Preset(
