@@ -700,3 +700,26 @@ def test_pong_step_render_fused_matches_separate(cuda):
         assert torch.equal(s1, s2) and torch.equal(o1, o2)
         assert all(torch.equal(x, y) for x, y in zip(r1, r2))
     assert torch.equal(acc1, acc2)
+
+
+def test_pixel_update_side_stream_is_race_free(cuda, monkeypatch):
+    """The head / fc weight gradients on the side stream (fork / join inside the captured
+    update) give bitwise the same training trajectory as the single-stream backward: the two
+    streams touch disjoint buffers and the join orders them before the optimiser."""
+    from relayrl_prototype_amd.runtime.pixel_trainer import PixelA2CConfig, PixelA2CTrainer
+
+    cfg = dict(num_envs=64, rollout_len=4, seed=5)
+    runs = []
+    for side in ("1", "0"):
+        monkeypatch.setenv("RRL_CNN_SIDE", side)
+        tr = PixelA2CTrainer(PixelA2CConfig(use_graphs=True, **cfg), device=cuda)
+        assert (tr.model.side_stream is not None) == (side == "1")
+        for _ in range(5):  # eager warm-up, capture + replay, 3 replays
+            tr.train_epoch()
+        torch.cuda.synchronize()
+        runs.append(tr)
+    a, b = runs
+    assert a._graph is not None and b._graph is not None
+    assert torch.equal(a.act, b.act) and torch.equal(a.obs, b.obs)
+    torch.testing.assert_close(a.model.params, b.model.params, rtol=0, atol=0)
+    torch.testing.assert_close(a.model.grad, b.model.grad, rtol=0, atol=0)
