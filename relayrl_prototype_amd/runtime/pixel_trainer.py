@@ -68,6 +68,14 @@ class PixelA2CTrainer:
         self.sample_seed = (cfg.seed * 2654435761 + rank * 97 + 5) & 0x7FFFFFFFFFFFFFFF
         dev = self.device
         self.obs = torch.zeros((T + 1, N, 21, 21, 64), dtype=torch.uint8, device=dev)  # space-to-depth frames
+        # GPU: two observation buffers used alternately -- update k rolls out of buffer k % 2 and
+        # renders its last observation straight into slot 0 of the other one, where update k + 1
+        # starts (no obs[T] -> obs[0] copy of 58 MB per update); one captured graph per buffer
+        import os
+
+        two = dev.type == "cuda" and os.environ.get("RRL_PONG_OBS_COPY", "1") != "1"  # 1: the copy path (A/B)
+        self._obs_bufs = [self.obs, torch.zeros_like(self.obs)] if two else [self.obs]
+        self._par = 0
         self.act = torch.zeros((T, N), dtype=torch.int32, device=dev)
         self.logp = torch.zeros((T, N), device=dev)
         self.val = torch.zeros((T + 1, N), device=dev)
@@ -90,7 +98,8 @@ class PixelA2CTrainer:
 
             self._stats_part = torch.zeros(int(hip().scan_tm_parts(N)), 3, device=dev)
             self._stats_out = torch.zeros(3, device=dev)
-            self._graph = None
+            self._graph = None  # the graph of the current buffer parity (None before capture)
+            self._graphs = {}
             self._warm = False
         else:
             from ..envs.pong import PongRef
@@ -103,19 +112,21 @@ class PixelA2CTrainer:
         self.comm.barrier() if self.comm.world > 1 else None
 
     # ------------------------------------------------------------------ GPU
-    def _rollout_gpu(self):
-        cfg, m, N = self.cfg, self.model, self.cfg.num_envs
-        for t in range(cfg.rollout_len):
-            m.act(self.obs[t], t * N, self.act[t], self.logp[t], self.val[t], self.sample_seed, t,
+    def _rollout_gpu(self, base, nxt):
+        cfg, m, N, T = self.cfg, self.model, self.cfg.num_envs, self.cfg.rollout_len
+        for t in range(T):
+            m.act(base[t], t * N, self.act[t], self.logp[t], self.val[t], self.sample_seed, t,
                   step_base=self.sample_t)
-            self.env.step(self.act[t], self.obs[t + 1], self.rew[t], self.done[t], offset=t)
+            # the last observation goes straight to the next update's start slot
+            self.env.step(self.act[t], base[t + 1] if (t + 1 < T or nxt is None) else nxt[0], self.rew[t],
+                          self.done[t], offset=t)
         self.model.h.counter_add(self.sample_t, cfg.rollout_len)
         self.env.advance(cfg.rollout_len)
         # bootstrap V(obs[T]) with the pre-update weights; its activations go to the
         # scratch rows [T*N, (T+1)*N) so the stored rollout activations stay intact
-        m.value(self.obs[cfg.rollout_len], cfg.rollout_len * N, self.val[cfg.rollout_len])
+        m.value(base[T] if nxt is None else nxt[0], cfg.rollout_len * N, self.val[cfg.rollout_len])
 
-    def _update_gpu(self):
+    def _update_gpu(self, base):
         from ..ops import gae_scan_tm
 
         cfg, m = self.cfg, self.model
@@ -125,7 +136,7 @@ class PixelA2CTrainer:
             adv, ret, _ = gae_scan_tm(self.rew, self.done, self.val, cfg.gamma, 1.0, self.adv, self.ret,
                                       self._stats_part, self._stats_out)
         with self.timer.phase("Backward"):
-            stats = m.backward(self.obs[:T].reshape(B, 21, 21, 64), self.act.reshape(B), adv.reshape(B),
+            stats = m.backward(base[:T].reshape(B, 21, 21, 64), self.act.reshape(B), adv.reshape(B),
                                ret.reshape(B), cfg.vf_coef, cfg.ent_coef, comm=self.comm)
         with self.timer.phase("Optimize"):
             m.apply(cfg.lr, cfg.max_grad_norm, self.comm)
@@ -167,11 +178,14 @@ class PixelA2CTrainer:
         return torch.tensor([[pg.item() * B, vf.item() * B, ent.item() * B, float(B)]])
 
     # ------------------------------------------------------------------ API
-    def _gpu_update_body(self):
+    def _gpu_update_body(self, par: int):
+        base = self._obs_bufs[par]
+        nxt = self._obs_bufs[par ^ 1] if len(self._obs_bufs) == 2 else None
         with self.timer.phase("Rollout"):
-            self._rollout_gpu()
-        stats = self._update_gpu()
-        self.obs[0].copy_(self.obs[self.cfg.rollout_len])
+            self._rollout_gpu(base, nxt)
+        stats = self._update_gpu(base)
+        if nxt is None:
+            base[0].copy_(base[self.cfg.rollout_len])
         return stats
 
     def _graphable(self) -> bool:
@@ -181,24 +195,28 @@ class PixelA2CTrainer:
         cfg = self.cfg
         N, T = cfg.num_envs, cfg.rollout_len
         if self.on_gpu:
-            if self._graphable() and self._graph is not None:
-                self._graph.replay()
-                stats = self._graph_stats
+            par = self._par
+            if self._graphable() and par in self._graphs:
+                g, stats = self._graphs[par]
+                g.replay()
             elif self._graphable() and self._warm:
-                # capture once (kernel attributes / workspaces were set up by the eager warm-up)
+                # capture once per buffer parity (kernel attributes / workspaces were set up by the
+                # eager warm-up)
                 g = torch.cuda.CUDAGraph()
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
                     with torch.cuda.graph(g, stream=s):
-                        self._graph_stats = self._gpu_update_body()
+                        stats = self._gpu_update_body(par)
                 torch.cuda.current_stream().wait_stream(s)
-                self._graph = g
+                self._graphs[par] = (g, stats)
                 g.replay()  # the capture itself does not execute
-                stats = self._graph_stats
             else:
-                stats = self._gpu_update_body()
+                stats = self._gpu_update_body(par)
                 self._warm = True
+            self._graph = self._graphs.get(par, (None,))[0]
+            self._par = (self._par + 1) % len(self._obs_bufs)
+            self.obs = self._obs_bufs[self._par]
         else:
             with self.timer.phase("Rollout"):
                 self._rollout_cpu()

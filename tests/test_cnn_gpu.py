@@ -723,3 +723,24 @@ def test_pixel_update_side_stream_is_race_free(cuda, monkeypatch):
     assert torch.equal(a.act, b.act) and torch.equal(a.obs, b.obs)
     torch.testing.assert_close(a.model.params, b.model.params, rtol=0, atol=0)
     torch.testing.assert_close(a.model.grad, b.model.grad, rtol=0, atol=0)
+
+
+def test_pixel_alternating_obs_buffers_match_copy_path(cuda, monkeypatch):
+    """Two observation buffers used alternately (the last render of update k lands in slot 0 of
+    update k + 1's buffer) train exactly like the single buffer + obs[T] -> obs[0] copy."""
+    from relayrl_prototype_amd.runtime.pixel_trainer import PixelA2CConfig, PixelA2CTrainer
+
+    cfg = dict(num_envs=64, rollout_len=4, seed=8)
+    runs = []
+    for copy in ("0", "1"):
+        monkeypatch.setenv("RRL_PONG_OBS_COPY", copy)
+        tr = PixelA2CTrainer(PixelA2CConfig(use_graphs=True, **cfg), device=cuda)
+        assert len(tr._obs_bufs) == (1 if copy == "1" else 2)
+        for _ in range(5):
+            tr.train_epoch()
+        torch.cuda.synchronize()
+        runs.append(tr)
+    a, b = runs
+    assert torch.equal(a.obs[0], b.obs[0]) and torch.equal(a.act, b.act)  # the next update's start
+    torch.testing.assert_close(a.model.params, b.model.params, rtol=0, atol=0)
+    assert a.metrics()["EnvSteps"] == b.metrics()["EnvSteps"]
