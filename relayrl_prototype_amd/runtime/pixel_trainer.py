@@ -73,7 +73,7 @@ class PixelA2CTrainer:
         # starts (no obs[T] -> obs[0] copy of 58 MB per update); one captured graph per buffer
         import os
 
-        two = dev.type == "cuda" and os.environ.get("RRL_PONG_OBS_COPY", "1") != "1"  # 1: the copy path (A/B)
+        two = dev.type == "cuda" and os.environ.get("RRL_PONG_OBS_COPY", "0") != "1"  # 1: the copy path (A/B)
         self._obs_bufs = [self.obs, torch.zeros_like(self.obs)] if two else [self.obs]
         self._par = 0
         self.act = torch.zeros((T, N), dtype=torch.int32, device=dev)
