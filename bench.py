@@ -371,20 +371,27 @@ def actor_learner_probe(args, comm, on_gpu: bool) -> dict:
     return rec
 
 
-def _arm_deadline(seconds: float, rank: int, emit):
-    """Timer thread: after ``seconds`` rank 0 runs ``emit`` (prints the JSON line) and every
-    rank leaves with status 0 -- a rank blocked inside a collective cannot be unwound, and
-    each rank's own timer fires, so torchrun sees the whole group exit."""
+DEADLINE_EXIT = 3  # a hung secondary phase: the record still prints, the run reads as failed
+
+
+def _arm_deadline(seconds: float, rank: int, emit, cleanup=None):
+    """Timer thread: after ``seconds`` rank 0 runs ``emit`` (prints the JSON line with the
+    phase marked failed) and every rank leaves with status DEADLINE_EXIT (non-zero, so
+    torchrun and CI see the hang) -- a rank blocked inside a collective cannot be unwound,
+    and each rank's own timer fires, so torchrun sees the whole group exit.  ``cleanup``
+    (e.g. terminating the reference-CPU child) runs first."""
     import threading
 
     def fire():
         try:
+            if cleanup is not None:
+                cleanup()
             if rank == 0:
                 emit()
         finally:
             sys.stdout.flush()
             sys.stderr.flush()
-            os._exit(0)
+            os._exit(DEADLINE_EXIT)
 
     t = threading.Timer(seconds, fire)
     t.daemon = True
@@ -540,8 +547,9 @@ def main(argv=None):
         # a hung RCCL transfer in the secondary phase must not cost the headline: past the
         # deadline rank 0 prints the line with the phase marked failed and every rank exits
         guard = _arm_deadline(args.al_deadline_s, rank, lambda: print(json.dumps(record(
-            {"error": f"deadline: actor-learner phase did not finish within {args.al_deadline_s} s"})),
-            flush=True))
+            {"error": f"deadline: actor-learner phase did not finish within {args.al_deadline_s} s",
+             "exit_status": DEADLINE_EXIT})), flush=True),
+            cleanup=(lambda: ref_proc.kill()) if ref_proc is not None else None)
         try:
             al_rec = actor_learner_probe(args, comm, on_gpu)
         finally:
@@ -564,7 +572,7 @@ def main(argv=None):
     ref_cpu = collect_reference_cpu(ref_proc, args.ref_cpu_seconds)
     if rank == 0:
         print(json.dumps(record(al_rec, ttt, ttt_ref, ref_cpu, do_ttt)), flush=True)
-    if comm.world > 1:
+    if comm.enabled:
         import torch.distributed as dist
 
         try:

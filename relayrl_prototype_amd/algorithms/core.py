@@ -3,7 +3,9 @@
 ``FlatNet`` = one MLP as a single flat fp32 parameter vector + fused-Adam state (m, v,
 device step counter).  Gradients come out of the fused fwd+bwd kernel as per-workgroup
 slabs; with one rank the slabs feed the fused reduce+Adam kernel directly, with several
-ranks they are reduced to one flat vector, all-reduced over RCCL, then Adam runs on it.
+ranks (``Comm.multi``) they are reduced to one flat vector, all-reduced over RCCL, then Adam
+runs on it.  Both forms are captured into hipGraphs: RCCL collectives replay inside a graph,
+so the multi-rank value loop is one replay per epoch too (``Comm.graph_safe``).
 """
 from __future__ import annotations
 
@@ -43,7 +45,7 @@ class FlatNet:
     def apply(self, slab: torch.Tensor, comm: Optional[Comm] = None):
         """Reduce the gradient slabs (and all-reduce across ranks) then take one Adam step."""
         b1, b2 = self.betas
-        if comm is None or comm.world == 1:
+        if comm is None or not comm.multi:
             adam_step(self.params, self.m, self.v, self.step, self.ticket, self.lr, slab=slab, beta1=b1, beta2=b2,
                       eps=self.eps, weight_decay=self.weight_decay)
         else:
@@ -73,7 +75,9 @@ class ValueLoop:
     def __init__(self, net: FlatNet, comm: Optional[Comm], use_graph: bool = True):
         self.net = net
         self.comm = comm
-        self.use_graph = use_graph and net.device.type == "cuda" and (comm is None or comm.world == 1)
+        # with several ranks the loop's all-reduces are captured too (RCCL on the device); a
+        # gloo group issues host calls, which a graph cannot hold
+        self.use_graph = use_graph and net.device.type == "cuda" and (comm is None or comm.graph_safe)
         self._graphs = {}
         self._key = None
         self.loss_first = None
@@ -109,6 +113,22 @@ class ValueLoop:
         self.loss_last = ls
         self.net.apply(g, self.comm)
 
+    def prepare(self, B: int, iters: int, inv_B: float, dev) -> None:
+        """(Re)allocate the slab / loss buffers for this batch shape (before any capture)."""
+        shape_key = (B, iters, float(inv_B))
+        if self._key != shape_key:
+            ns = grad_slabs(B, dev)
+            self._slab = torch.empty(ns, self.net.P, device=dev)
+            self.loss_first = torch.zeros(ns, 8, device=dev)
+            self.loss_last = torch.zeros(ns, 8, device=dev)
+            self._graphs = {}
+            self._key = shape_key
+
+    def run_body(self, obs: torch.Tensor, ret: torch.Tensor, iters: int, inv_B: float):
+        """The loop's launches on the current stream (inside an enclosing capture, e.g.
+        PGLearner's whole-optimize graph); ``prepare`` must have run."""
+        self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last)
+
     def run(self, obs: torch.Tensor, ret: torch.Tensor, iters: int, inv_B: float):
         B = obs.shape[0]
         dev = obs.device
@@ -123,14 +143,7 @@ class ValueLoop:
                 self.loss_last = ls
                 self.net.apply(g, self.comm)
             return
-        ns = grad_slabs(B, dev)
-        shape_key = (B, iters, float(inv_B))
-        if self._key != shape_key:
-            self._slab = torch.empty(ns, self.net.P, device=dev)
-            self.loss_first = torch.zeros(ns, 8, device=dev)
-            self.loss_last = torch.zeros(ns, 8, device=dev)
-            self._graphs = {}
-            self._key = shape_key
+        self.prepare(B, iters, inv_B, dev)
         if not self.use_graph:
             self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last)
             return

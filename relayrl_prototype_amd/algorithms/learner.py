@@ -14,6 +14,12 @@ launch + one fused reduce+Adam launch (+ one RCCL all-reduce with several ranks)
             steps on disjoint minibatches (the usual PPO schedule); advantages keep the
             full-batch normalisation statistics.  M = 1 is the full-batch form, whose value
             loop is one hipGraph replay.
+
+hipGraphs: with ``use_graphs`` on a GPU the WHOLE epoch of updates (policy step(s) + the
+value loop, with their RCCL all-reduces at world > 1) is captured once per input-buffer set
+and replayed -- the multi-rank epoch is one replay instead of ~4 x (1 + train_vf_iters)
+eager launches.  Not capturable (eager, value loop still a graph): PPO with target_kl (its
+early stop reads the KL on the host), minibatches (a fresh permutation per epoch), gloo.
 """
 from __future__ import annotations
 
@@ -60,6 +66,11 @@ class PGLearner:
         self._pi_slab = None
         self._pi_loss = None
         self.last = {}
+        self.use_graphs = bool(use_graphs)
+        self.graphs_enabled = True  # toggled off for epochs with a changing batch (agent rows)
+        self.before_capture = None  # quiesce helper threads that issue HIP calls (host_trainer)
+        self._opt_graphs = {}
+        self.graph_replays = 0
 
     @property
     def head(self) -> int:
@@ -76,6 +87,11 @@ class PGLearner:
             self._pi_loss = torch.empty(ns, 8, device=self.device)
         return self._pi_slab[:ns], self._pi_loss[:ns]
 
+    def capturable(self) -> bool:
+        """The whole optimize() epoch can be one hipGraph."""
+        return (self.use_graphs and self.graphs_enabled and self.device.type == "cuda" and self.comm.graph_safe
+                and self.num_minibatches == 1 and not (self.algo == "ppo" and self.target_kl is not None))
+
     def optimize(self, obs, act=None, actc=None, mask=None, adv=None, ret=None, adv_stats=None, logp_old=None,
                  inv_B: Optional[float] = None):
         """One epoch of updates on a prepared batch (adv/ret already computed).
@@ -85,6 +101,78 @@ class PGLearner:
         B = obs.shape[0]
         if inv_B is None:
             inv_B = 1.0 / max(B * self.comm.world, 1)
+        if self.capturable():
+            return self._optimize_graph(obs, act, actc, mask, adv, ret, adv_stats, logp_old, float(inv_B))
+        return self._optimize_eager(obs, act, actc, mask, adv, ret, adv_stats, logp_old, inv_B)
+
+    def _nets(self):
+        return [n for n in (self.pi, self.vf) if n is not None]
+
+    def _optimize_graph(self, obs, act, actc, mask, adv, ret, adv_stats, logp_old, inv_B: float):
+        """Capture (once per input-buffer set) and replay the whole epoch of updates."""
+        B = obs.shape[0]
+        args = (obs, act, actc, mask, adv, ret, adv_stats, logp_old)
+        key = (B, inv_B) + tuple(0 if t is None else t.data_ptr() for t in args)
+        ent = self._opt_graphs.get(key)
+        if ent is None:
+            if len(self._opt_graphs) >= 4:
+                self._opt_graphs.clear()
+            self._slabs(B)
+            if self.vloop is not None:
+                self.vloop.prepare(B, self.train_vf_iters, inv_B, self.device)
+            if self.before_capture is not None:
+                self.before_capture()
+            nets = self._nets()
+            v0 = [n.version for n in nets]
+            state = [t.clone() for n in nets for t in (n.params, n.m, n.v, n.step)]
+            # warm up eagerly once on the real buffers (kernel attributes, allocator, RCCL
+            # communicator), then restore the optimiser state so the warm-up leaves no trace
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self._optimize_body(*args, inv_B, vf_iters=min(1, self.train_vf_iters))
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            it = iter(state)
+            for n in nets:
+                for t in (n.params, n.m, n.v, n.step):
+                    t.copy_(next(it))
+            for n, v in zip(nets, v0):
+                n.version = v
+            g = torch.cuda.CUDAGraph()
+            # thread_local: a host rollout thread (host_trainer overlap) may issue HIP calls meanwhile
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                last = self._optimize_body(*args, inv_B, vf_iters=self.train_vf_iters)
+            dv = [n.version - v for n, v in zip(nets, v0)]
+            for n, v in zip(nets, v0):
+                n.version = v
+            ent = (g, dict(last), dv)
+            self._opt_graphs[key] = ent
+        g, last, dv = ent
+        g.replay()
+        self.graph_replays += 1
+        for n, d in zip(self._nets(), dv):
+            n.version += d
+        self.last = dict(last)
+        return self.last
+
+    def _optimize_body(self, obs, act, actc, mask, adv, ret, adv_stats, logp_old, inv_B: float, vf_iters: int):
+        """Full-batch epoch (no host reads): the capturable form of _optimize_eager."""
+        H, A = self.hidden, self.act_dim
+        slab, ls = self._slabs(obs.shape[0])
+        pi_loss = None
+        for it in range(self.train_pi_iters):
+            out = mlp_grad(self.head, self.pi.params, obs, A, H, mask=mask, act=act, actc=actc, adv=adv,
+                           logp_old=logp_old, adv_stats=adv_stats, inv_B=inv_B, clip_eps=self.clip_ratio,
+                           ent_coef=self.ent_coef, grad_slab=slab, loss_slab=ls)
+            if it == 0:
+                pi_loss = out[1].sum(0)
+            self.pi.apply(out[0], self.comm)
+        if self.vloop is not None and vf_iters > 0:
+            self.vloop.run_body(obs, ret, vf_iters, inv_B)
+        return {"pi_loss": pi_loss, "kl_stop": None}
+
+    def _optimize_eager(self, obs, act, actc, mask, adv, ret, adv_stats, logp_old, inv_B):
+        B = obs.shape[0]
         H, A = self.hidden, self.act_dim
         M = self.num_minibatches
         slab, ls = self._slabs(B)

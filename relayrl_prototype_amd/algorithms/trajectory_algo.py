@@ -87,13 +87,18 @@ class FlatBuffer:
         self.ptr += n
         return n
 
-    def finish_path(self, terminal: bool = True, boot_obs=None):
+    def finish_path(self, terminal: bool = True, boot_obs=None, boot_value=None):
         """Close the current path.  A cut (non-terminal) path bootstraps with V(boot_obs) when
-        the agent shipped its next observation, else with V of its last state (nan marker)."""
+        the agent shipped its next observation, with ``boot_value`` when the uploader supplied
+        the bootstrap itself (the reference's finish_path(last_val), replay_buffer.py:48-79),
+        else with V of its last state (nan marker)."""
         if self.ptr > self.path_start:
             i = self.ptr - 1
             self.done[i] = 1.0
-            self.boot[i] = np.nan if not terminal else 0.0  # nan = bootstrap with a value
+            if boot_value is not None:
+                self.boot[i] = float(boot_value)
+            else:
+                self.boot[i] = np.nan if not terminal else 0.0  # nan = bootstrap with a value
             if not terminal and boot_obs is not None:
                 self.boot_obs[i] = np.asarray(boot_obs, np.float32).reshape(-1)[: self.obs_dim]
                 self.has_boot_obs[i] = True
@@ -142,8 +147,8 @@ class EpisodeIngest:
         self.steps = 0
         self.finished = []
 
-    def end_episode(self, terminal: bool):
-        self.buffer.finish_path(terminal)
+    def end_episode(self, terminal: bool, boot_value=None):
+        self.buffer.finish_path(terminal, boot_value=boot_value)
         self.finished.append((self.ep_ret, self.ep_len))
         self.ep_ret, self.ep_len = 0.0, 0
 
@@ -184,12 +189,13 @@ class EpisodeIngest:
         last = None
         for a in trajectory.get_actions():
             obs = a.get_obs()
-            if obs is None:  # reference-style terminal marker: its reward closes the episode
+            if obs is None:
+                # reference-style terminal marker (agent_zmq.rs:605-610): REINFORCE.py:86 calls
+                # finish_path(last_val=marker reward), i.e. the reward is the path's bootstrap
+                # V(s_T) -- discounted by gamma, 0 after a terminal state -- not a step reward
                 if a.get_done():
-                    if buf.ptr > buf.path_start:
-                        buf.rew[buf.ptr - 1] += a.get_rew()
-                    self.ep_ret += a.get_rew()
-                    self.end_episode(terminal=True)
+                    self.ep_ret += a.get_rew()  # REINFORCE.py:75 counts it in EpRet
+                    self.end_episode(terminal=False, boot_value=a.get_rew())
                 continue
             if buf.full():
                 break
@@ -303,7 +309,9 @@ class TrajectoryAlgorithm(AlgorithmAbstract):
                 vb = mlp_forward(FwdMode.VALUE, self.learner.vf.params, d["boot_obs"], 1, H)["v"]
                 boot = boot.index_copy(0, bi.to(boot.device), vb.to(boot.dtype))
         else:
-            boot = torch.nan_to_num(boot, nan=0.0)
+            # no value net: nothing to bootstrap with; the reference drops last_val too
+            # (replay_buffer.py:74-77)
+            boot = torch.zeros_like(boot)
         adv, ret, stats = scan_flat(d["rew"], d["done"], val, boot, self.gamma, self.lam)
         act = d["act"] if self.discrete else None
         actc = None if self.discrete else d["act"]

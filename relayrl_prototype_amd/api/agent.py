@@ -72,7 +72,6 @@ class RelayRLAgent:
         if wire_format == "reference" and self.server_type != "zmq":
             raise ValueError("wire_format='reference' is the reference's ZMQ wire; use server_type='zmq'")
         self.wire_format = wire_format
-        self._vals = []  # reference wire: V(s_t) of the recorded steps (the actions' data['v'])
         self._rec = EpisodeRecorder(self.max_traj_length)
         if model_path is not None:
             self._load_model_file(model_path)
@@ -158,15 +157,16 @@ class RelayRLAgent:
         else:
             raise ValueError(f"server_type must be zmq, grpc or local, not {self.server_type!r}")
 
-    def _reference_frame(self, cols, done: bool, next_obs=None) -> bytes:
-        """One episode as the reference agent's upload: serde_pickle(Vec<RelayRLAction>)."""
+    def _reference_frame(self, cols, vals, done: bool, next_obs=None) -> bytes:
+        """One episode as the reference agent's upload: serde_pickle(Vec<RelayRLAction>).
+        ``vals`` = V(s_t) per row (NaN without a value head), recorded next to each row's
+        log-prob in the EpisodeRecorder so the two cannot drift apart."""
         from ..transport.serde_pickle import reference_frame
 
         acts = []
-        vals = self._vals
         for i in range(len(cols)):
             data = {"logp_a": np.array([cols.logp[i]], np.float32)}
-            if i < len(vals) and vals[i] is not None:
+            if not np.isnan(vals[i]):
                 data["v"] = np.array([vals[i]], np.float32)
             acts.append(RelayRLAction(cols.obs[i], cols.act[i], None if cols.mask is None else cols.mask[i],
                                       float(cols.rew[i]), data, False, True))
@@ -176,13 +176,13 @@ class RelayRLAgent:
                 v = self.policy.value(np.asarray(next_obs, np.float32).reshape(1, -1))
             last = 0.0 if v is None else float(np.asarray(v).reshape(-1)[0])
         acts.append(RelayRLAction(None, None, None, last, None, True, False))  # agent_zmq.rs:605-610 marker
-        self._vals = []
         return reference_frame(acts)
 
     def _ship(self, done: bool, next_obs=None):
         if self.wire_format == "reference":
+            vals = self._rec.val[:self._rec.n].copy()
             cols = self._rec.take(self.agent_id, self.episodes_sent, done, next_obs)
-            self.transport.send_trajectory(self._reference_frame(cols, done, next_obs))
+            self.transport.send_trajectory(self._reference_frame(cols, vals, done, next_obs))
             self.episodes_sent += 1
             return
         cols = self._rec.take(self.agent_id, self.episodes_sent, done, next_obs)
@@ -232,10 +232,9 @@ class RelayRLAgent:
             act, data = p.step(obs_a, mask_a)
         a0 = np.asarray(act[0] if act.ndim >= 1 else act)
         logp = data.get("logp_a")
-        rec.record(obs_a, a0, mask_a, None if logp is None else logp[0])
-        if self.wire_format == "reference":
-            v = data.get("v")
-            self._vals.append(None if v is None else float(np.asarray(v).reshape(-1)[0]))
+        v = data.get("v")
+        rec.record(obs_a, a0, mask_a, None if logp is None else logp[0],
+                   None if v is None else float(np.asarray(v).reshape(-1)[0]))
         aux = {k: np.asarray(v[0], np.float32) for k, v in data.items()}
         action = RelayRLAction(obs_a, a0, mask_a, 0.0, aux, False, False)
         return action

@@ -200,7 +200,10 @@ class DeviceNatureCNN:
         dev = self.device
         self.shadow = torch.empty(self.P, dtype=torch.bfloat16, device=dev)
         self.wfc_t = torch.empty(FC_IN * HIDDEN, dtype=torch.bfloat16, device=dev)  # [3136][512]
-        self._fc_part = None
+        # split-K partials of the fc forward, sized once for every batch up to max_batch: a
+        # captured update graph holds this storage, so it must never be reallocated
+        fc_rows = max(self.fc_splits(n) * n for n in range(1, self.max_batch + 1)) if self.fc_nt else 0
+        self._fc_part = torch.empty(fc_rows * HIDDEN, device=dev) if self.fc_nt else None
         self.refresh_shadow()
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params)
@@ -293,9 +296,7 @@ class DeviceNatureCNN:
         the backward) + logits / value / sampling."""
         o = self.o
         s = self.fc_splits(n)
-        need = s * n * HIDDEN
-        if self._fc_part is None or self._fc_part.numel() < need:
-            self._fc_part = torch.empty(need, device=self.device)
+        assert s * n * HIDDEN <= self._fc_part.numel(), "fc split-K partials exceed the preallocated buffer"
         used = int(self.h.fc_nt_part(a3, self.shadow[o["wfc"]:o["bfc"]], self._fc_part, n, HIDDEN, FC_IN, s))
         self.h.a2c_head(0, hid, self.params[o["head"]:], n, self.A, head.get("act"), head.get("logp"),
                         head.get("value"), head.get("logits"), int(head.get("seed", 0)), int(head.get("step", 0)),
@@ -393,7 +394,7 @@ class DeviceNatureCNN:
         # not touched by the fused conv path, which has its own slabs).  The DP path keeps one
         # stream: its fc bucket all-reduce is issued as soon as these gradients are final.
         side = (self.side_stream if (self.side_stream is not None and self.fused_convs and self.fc_nt
-                                     and B % 64 == 0 and (comm is None or comm.world <= 1)) else None)
+                                     and B % 64 == 0 and (comm is None or not comm.multi)) else None)
         if side is not None:
             self._ev_fork.record()
             side.wait_event(self._ev_fork)
@@ -427,7 +428,7 @@ class DeviceNatureCNN:
             h.fc_nt_mask(dh, self.wfc_t, a3, da3, B, FC_IN, HIDDEN)
         else:
             h.gemm_dgrad(dh, sh[o["wfc"]:o["bfc"]], a3, da3, B, HIDDEN, FC_IN)
-        if comm is not None and comm.world > 1:
+        if comm is not None and comm.multi:
             import torch.distributed as dist
 
             pending = dist.all_reduce(g[o["wfc"]:o["P"]], group=comm.group, async_op=True)
@@ -503,7 +504,7 @@ class DeviceNatureCNN:
     # ------------------------------------------------------------------ optimizer
     def apply(self, lr: float, max_grad_norm: float = 0.5, comm=None, betas=(0.9, 0.999), eps: float = 1e-5):
         """(DP all-reduce) -> global-norm clip -> Adam -> bf16 shadow, all on device."""
-        if comm is not None and comm.world > 1 and not getattr(self, "_reduced", False):
+        if comm is not None and comm.multi and not getattr(self, "_reduced", False):
             comm.all_reduce_sum_(self.grad)
             self.grad.mul_(1.0 / comm.world)
         self._reduced = False

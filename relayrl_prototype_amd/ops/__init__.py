@@ -8,7 +8,6 @@ CPU tensors always go through :mod:`relayrl_prototype_amd.ops.reference`.
 from __future__ import annotations
 
 import importlib
-import os
 
 _HIP = None
 _HIP_ERR = None
@@ -49,8 +48,6 @@ def hip_available() -> bool:
 def use_hip(t) -> bool:
     """True when tensor ``t`` lives on the GPU (then the HIP kernel MUST be used)."""
     if not getattr(t, "is_cuda", False):
-        return False
-    if os.environ.get("RRL_FORCE_REFERENCE") == "1":
         return False
     hip()  # loud failure when missing on a GPU box
     return True

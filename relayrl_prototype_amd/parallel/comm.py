@@ -11,7 +11,14 @@ collective on ONE flat buffer:
 * advantage statistics -> ``all_reduce_sum_`` of a 3-float vector
 
 xGMI is point-to-point (7 links per GPU); the flat gradient of a 128x128 MLP is ~70 KB,
-so these are latency-bound: keep them fused, one call per optimiser step.
+so these are latency-bound: keep them fused, one call per optimiser step -- and capture the
+optimiser loops WITH their all-reduces into hipGraphs (RCCL collectives replay inside a
+graph), so a world > 1 epoch is not 80 x 4 eager launches.
+
+``RRL_FORCE_COLLECTIVES=1`` sends a ONE-rank process group through the world > 1 code path
+(``Comm.multi``): slab reduce -> real ``dist.all_reduce`` -> Adam, bucketed DP all-reduces,
+captured graphs.  A one-GPU box cannot host two RCCL ranks, so this is how the multi-rank
+path's RCCL calls (and their graph capture) are exercised and timed on one MI355X.
 """
 from __future__ import annotations
 
@@ -45,21 +52,39 @@ def collective_timeout() -> datetime.timedelta:
     return datetime.timedelta(seconds=float(os.environ.get("RRL_COLLECTIVE_TIMEOUT_S", "600")))
 
 
+def force_collectives() -> bool:
+    """RRL_FORCE_COLLECTIVES=1: a one-rank group takes the world > 1 code path."""
+    return os.environ.get("RRL_FORCE_COLLECTIVES", "0") == "1"
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
 def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> "Comm":
     """Initialise the default process group from the environment (torchrun) if world > 1.
     Backend: ``nccl`` (= RCCL over xGMI on ROCm) with GPUs, ``gloo`` on CPU; override with
     RRL_DIST_BACKEND."""
     rank, local, world = dist_env()
     local = local_device_index()
+    forced = world == 1 and force_collectives()
     if timeout_s is None:
         # a stalled rank turns into a collective timeout -> the rank exits -> torchrun restarts
         # the group (--max-restarts) and ranks auto-resume from their checkpoints
         timeout_s = float(os.environ.get("RRL_COLLECTIVE_TIMEOUT_S", "600"))
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or forced) and not dist.is_initialized():
         backend = backend or os.environ.get("RRL_DIST_BACKEND") or None
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if forced and "MASTER_PORT" not in os.environ:
+            os.environ["MASTER_PORT"] = str(_free_port())
         os.environ.setdefault("MASTER_PORT", "29500")
         if backend == "nccl":
             torch.cuda.set_device(local)
@@ -80,12 +105,17 @@ def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] =
 class Comm:
     """Thin wrapper so single-process code paths need no branches."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, collectives: Optional[bool] = None):
         self.group = group
         self.enabled = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if self.enabled else 1
         self.rank = dist.get_rank(group) if self.enabled else 0
         self.backend = dist.get_backend(group) if self.enabled else "none"
+        if collectives is None:
+            collectives = force_collectives()
+        # ``multi``: the world > 1 code path (real collectives), also for a forced one-rank group
+        self.forced = bool(self.enabled and self.world == 1 and collectives)
+        self.multi = self.world > 1 or self.forced
         # optional utils.tracing.PhaseTimer: every gradient / statistics all-reduce is timed as
         # the "AllReduce" phase (HIP events on the current stream bracket the RCCL call, which
         # the stream waits on); skipped while a hipGraph is being captured
@@ -95,8 +125,14 @@ class Comm:
     def is_master(self) -> bool:
         return self.rank == 0
 
+    @property
+    def graph_safe(self) -> bool:
+        """Collectives of this comm can be captured into a hipGraph: none are issued, or they
+        go through RCCL on the device (gloo collectives are host calls)."""
+        return (not self.multi) or self.backend == "nccl"
+
     def all_reduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world > 1:
+        if self.multi:
             tm = self.timer
             if tm is not None and tm.enabled and not (t.is_cuda and torch.cuda.is_current_stream_capturing()):
                 with tm.phase("AllReduce"):
@@ -106,22 +142,22 @@ class Comm:
         return t
 
     def all_reduce_max_(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world > 1:
+        if self.multi:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return t
 
     def all_reduce_min_(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world > 1:
+        if self.multi:
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
         return t
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
-        if self.world > 1:
+        if self.multi:
             dist.broadcast(t, src=src, group=self.group)
         return t
 
     def barrier(self):
-        if self.world > 1:
+        if self.multi:
             if self.backend == "nccl" and torch.cuda.is_available():
                 dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
             else:
@@ -133,7 +169,7 @@ class Comm:
         Implemented as grouped point-to-point send/recv (each actor->learner transfer
         rides its own xGMI link) rather than a ring gather.
         """
-        if self.world == 1:
+        if not self.multi:
             if out is not None:
                 out[0].copy_(t)
             return out
@@ -153,7 +189,7 @@ class Comm:
         return out
 
     def all_gather_object(self, obj):
-        if self.world == 1:
+        if not self.multi:
             return [obj]
         res = [None] * self.world
         dist.all_gather_object(res, obj, group=self.group)

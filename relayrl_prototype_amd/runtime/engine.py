@@ -419,7 +419,7 @@ class EngineRunner:
 
 def _agree(comm, flag: bool) -> bool:
     """True on every rank if it is true on any (wall-clock stops must not split the ranks)."""
-    if comm is None or comm.world == 1:
+    if comm is None or not comm.multi:
         return flag
     dev = "cuda" if comm.backend == "nccl" else "cpu"
     t = torch.tensor([1.0 if flag else 0.0], device=dev)
@@ -610,7 +610,7 @@ def run_engine_rank(spec: EngineSpec, env_dir: str, publish_dir: Optional[str], 
         algo.trainer.close()
     elif hasattr(algo.trainer, "finish"):
         algo.trainer.finish()
-    if comm.world > 1:
+    if comm.enabled:
         import torch.distributed as dist
 
         dist.destroy_process_group()

@@ -134,7 +134,7 @@ class HostVecTrainer:
                                  cfg.target_kl, cfg.ent_coef, self.device, cfg.seed, self.comm, cfg.use_graphs,
                                  cfg.log_std_init, num_minibatches=cfg.num_minibatches)
         self.timer = PhaseTimer(self.device, enabled=cfg.phase_timing)
-        if self.comm.world > 1 and cfg.phase_timing:
+        if self.comm.multi and cfg.phase_timing:
             self.comm.timer = self.timer
         self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.comm, self.timer)
         self.overlap = bool(cfg.overlap and cuda)
@@ -155,8 +155,10 @@ class HostVecTrainer:
         self.snapshot_versions = []  # policy version each overlapped rollout acted with
         self._primed = False  # a completed rollout waits in self.bufs[self.cur]
         self._rollout_error = None
-        if self.overlap and self.learner.vloop is not None:
-            self.learner.vloop.before_capture = self._quiesce_rollout
+        if self.overlap:
+            self.learner.before_capture = self._quiesce_rollout
+            if self.learner.vloop is not None:
+                self.learner.vloop.before_capture = self._quiesce_rollout
         # first observation
         for h, env in enumerate(self.envs):
             env.reset_ptr(self.bufs[0].h_obs[0, bounds[h]].data_ptr())
@@ -192,6 +194,7 @@ class HostVecTrainer:
         h.set_cu_limit(len(learner))
         # the learner was built for the whole chip: re-size its gradient slabs for its share
         self.learner._pi_slab = None
+        self.learner._opt_graphs.clear()
         if self.learner.vloop is not None:
             self.learner.vloop._key = None
         self.driver = h.HostRollout(self.envs, bounds, len(actor))
@@ -452,7 +455,7 @@ class HostVecTrainer:
 
     def sync_from_rank0(self, src: int = 0):
         """Rank ``src``'s learner state everywhere; each rank keeps its own env streams."""
-        if self.comm.world > 1:
+        if self.comm.multi:
             self.learner.broadcast_state_(self.comm, src)
             if self.overlap:
                 self.actor_params.copy_(self.learner.pi.params)

@@ -217,83 +217,97 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
     last: Dict = {}
     from ..utils.faults import maybe_kill_rank, maybe_stall_rank
 
-    ep = start + 1
-    while ep <= epochs:
-        try:
-            maybe_stall_rank(orig_rank if eg is not None else comm.rank, ep, out_dir)
-            _epoch(tr)
-            m = tr.metrics() if (ep % log_every == 0 or ep == epochs) else None
-        except Exception as e:
-            if eg is None:
-                raise
-            from ..parallel.elastic import Evicted
-
-            sd = tr.state_dict()
-            if hasattr(tr, "watchdog"):
-                tr.watchdog.close()
+    completed = False
+    try:
+        ep = start + 1
+        while ep <= epochs:
             try:
-                comm = eg.reform()
-            except Evicted as ev:
-                print(f"[elastic] {ev}", flush=True)
-                eg.close()
-                return {"Evicted": True, "Epoch": ep - 1}
-            if getattr(comm, "unchanged", False):
-                raise  # every rank is alive: not a lost peer
-            print(f"[elastic] rank {orig_rank}: re-formed without the lost rank(s) after {type(e).__name__}; "
-                  f"world {comm.world}, rank {comm.rank}, retrying epoch {ep}", flush=True)
-            ov = dict(overrides)
-            if preset.kind == "actor_learner":
-                from .actor_learner import Topology
+                maybe_stall_rank(orig_rank if eg is not None else comm.rank, ep, out_dir)
+                _epoch(tr)
+                m = tr.metrics() if (ep % log_every == 0 or ep == epochs) else None
+            except Exception as e:
+                if eg is None:
+                    raise
+                from ..parallel.elastic import Evicted
 
-                req = dict(preset.overrides)
-                req.update(overrides)
-                if int(req.get("learner_ranks", 0)):
-                    ov["learner_ranks"] = Topology.fit_learners(comm.world, int(req["learner_ranks"]),
-                                                                bool(req.get("learner_acts", True)))
-            tr = _make_trainer(preset, comm, dev, ov)
-            tr.load_state_dict(sd)
-            if hasattr(tr, "sync_from_rank0"):
-                tr.sync_from_rank0()
-            if comm.rank == 0 and logger is None:
-                kw = setup_logger_kwargs(f"relayrl-{name}", seed=int(overrides.get("seed", 0)), data_dir=out_dir)
-                logger = EpochLogger(**kw, quiet=True)
-            continue
-        if m is not None:
-            el = time.perf_counter() - t0
-            if comm.rank == 0 and m:
-                m = dict(m)
-                m["Time"] = el
-                if "EnvSteps" in m and el > 0:
-                    m["EnvStepsPerSec"] = m["EnvSteps"] / el
-                m["UpdatesPerSec"] = (ep - start) / el if el > 0 else 0.0
-                if dev.type == "cuda":
-                    m["HBMUsedGB"] = torch.cuda.max_memory_allocated(dev) / 2 ** 30
-                for k, v in m.items():
-                    if isinstance(v, (int, float)):
-                        logger.log_tabular(k, v)
-                logger.dump_tabular()
-                last = m
-                if on_metrics:
-                    on_metrics(m)
-        if checkpoint_every and ep % checkpoint_every == 0 and hasattr(tr, "state_dict"):
-            from ..utils.checkpoint import save_checkpoint
+                sd = tr.state_dict()
+                if hasattr(tr, "watchdog"):
+                    tr.watchdog.close()
+                # CU-masked streams / grid limit of the old trainer (host_trainer.close); no
+                # finish(): that would wait on transfers of the broken group
+                _release(tr, finish=False)
+                try:
+                    comm = eg.reform()
+                except Evicted as ev:
+                    print(f"[elastic] {ev}", flush=True)
+                    eg.close()
+                    return {"Evicted": True, "Epoch": ep - 1}
+                if getattr(comm, "unchanged", False):
+                    raise  # every rank is alive: not a lost peer
+                print(f"[elastic] rank {orig_rank}: re-formed without the lost rank(s) after {type(e).__name__}; "
+                      f"world {comm.world}, rank {comm.rank}, retrying epoch {ep}", flush=True)
+                ov = dict(overrides)
+                if preset.kind == "actor_learner":
+                    from .actor_learner import Topology
 
-            # keyed on the ORIGINAL (torchrun) rank: after an elastic shrink the survivors'
-            # new ranks would overwrite other ranks' directories
-            save_checkpoint(ckpt_dir(out_dir, name, orig_rank), {"trainer": tr.state_dict(), "epoch": ep,
-                                                                 "world": comm.world, "rank": comm.rank})
-        maybe_kill_rank(orig_rank, ep, out_dir)
-        ep += 1
-    if hasattr(tr, "close"):
-        tr.close()
-    elif hasattr(tr, "finish"):
-        tr.finish()
+                    req = dict(preset.overrides)
+                    req.update(overrides)
+                    if int(req.get("learner_ranks", 0)):
+                        ov["learner_ranks"] = Topology.fit_learners(comm.world, int(req["learner_ranks"]),
+                                                                    bool(req.get("learner_acts", True)))
+                tr = _make_trainer(preset, comm, dev, ov)
+                tr.load_state_dict(sd)
+                if hasattr(tr, "sync_from_rank0"):
+                    tr.sync_from_rank0()
+                if comm.rank == 0 and logger is None:
+                    kw = setup_logger_kwargs(f"relayrl-{name}", seed=int(overrides.get("seed", 0)), data_dir=out_dir)
+                    logger = EpochLogger(**kw, quiet=True)
+                continue
+            if m is not None:
+                el = time.perf_counter() - t0
+                if comm.rank == 0 and m:
+                    m = dict(m)
+                    m["Time"] = el
+                    if "EnvSteps" in m and el > 0:
+                        m["EnvStepsPerSec"] = m["EnvSteps"] / el
+                    m["UpdatesPerSec"] = (ep - start) / el if el > 0 else 0.0
+                    if dev.type == "cuda":
+                        m["HBMUsedGB"] = torch.cuda.max_memory_allocated(dev) / 2 ** 30
+                    for k, v in m.items():
+                        if isinstance(v, (int, float)):
+                            logger.log_tabular(k, v)
+                    logger.dump_tabular()
+                    last = m
+                    if on_metrics:
+                        on_metrics(m)
+            if checkpoint_every and ep % checkpoint_every == 0 and hasattr(tr, "state_dict"):
+                from ..utils.checkpoint import save_checkpoint
+
+                # keyed on the ORIGINAL (torchrun) rank: after an elastic shrink the survivors'
+                # new ranks would overwrite other ranks' directories
+                save_checkpoint(ckpt_dir(out_dir, name, orig_rank), {"trainer": tr.state_dict(), "epoch": ep,
+                                                                     "world": comm.world, "rank": comm.rank})
+            maybe_kill_rank(orig_rank, ep, out_dir)
+            ep += 1
+        completed = True
+    finally:
+        # also on an exception: a host trainer's CU limit is process-wide (host_trainer.close);
+        # finish() (pending transfers) only after a clean run
+        _release(tr, finish=completed)
     if eg is not None:
         last = dict(last)
         last["ElasticReforms"] = eg.reforms
         last["FinalWorld"] = comm.world
         eg.close()
     return last
+
+
+def _release(tr, finish: bool = True) -> None:
+    """close() (host trainer: CU-masked streams + the process-wide grid limit) or finish()."""
+    if hasattr(tr, "close"):
+        tr.close()
+    elif finish and hasattr(tr, "finish"):
+        tr.finish()
 
 
 def _run_agent_server(preset: Preset, epochs: int, out_dir: str, overrides: Dict) -> Dict:

@@ -14,9 +14,11 @@ One update on each rank (one process per GPU), everything device resident:
      overlapped with the conv backward (world > 1)
   5. global-norm clip + Adam + bf16 shadow weights in one kernel
 
-On one rank the whole update (~80 launches) is captured into a hipGraph after one eager
-warm-up update and replayed: RNG step counters and the Adam step live on the device, so
-replays draw fresh samples and bias corrections without host involvement.
+The whole update (~50 launches, plus the two bucketed RCCL all-reduces at world > 1) is
+captured into a hipGraph after one eager warm-up update and replayed: RNG step counters and
+the Adam step live on the device, so replays draw fresh samples and bias corrections without
+host involvement.  With several ranks the capture needs RCCL (``Comm.graph_safe``); the
+all-reduces then replay inside the graph on every rank.
 
 The CPU path (tests, no GPU) runs the same algorithm through the PyTorch oracle model
 and the numpy Pong reference.
@@ -46,7 +48,7 @@ class PixelA2CConfig:
     seed: int = 0
     max_episode_steps: int = 27000 // 4
     phase_timing: bool = False
-    use_graphs: bool = True        # capture the whole update as one hipGraph (world == 1)
+    use_graphs: bool = True        # capture the whole update (with its RCCL all-reduces) as one hipGraph
 
     def to_dict(self):
         return asdict(self)
@@ -109,7 +111,7 @@ class PixelA2CTrainer:
             self.env = PongRef(N, env_seed, cfg.max_episode_steps)
             self.obs[0] = torch.from_numpy(self.env.reset())
             self.gen = torch.Generator().manual_seed(self.sample_seed)
-        self.comm.barrier() if self.comm.world > 1 else None
+        self.comm.barrier() if self.comm.multi else None
 
     # ------------------------------------------------------------------ GPU
     def _rollout_gpu(self, base, nxt):
@@ -170,7 +172,7 @@ class PixelA2CTrainer:
                                      cfg.ent_coef)
         self.opt.zero_grad()
         loss.backward()
-        if self.comm.world > 1:
+        if self.comm.multi:
             self.comm.all_reduce_sum_(self.params.grad)
             self.params.grad.mul_(1.0 / self.comm.world)
         torch.nn.utils.clip_grad_norm_([self.params], cfg.max_grad_norm)
@@ -189,7 +191,8 @@ class PixelA2CTrainer:
         return stats
 
     def _graphable(self) -> bool:
-        return self.on_gpu and self.cfg.use_graphs and self.comm.world == 1 and not self.timer.enabled
+        # world > 1: the bucketed RCCL all-reduces are captured with the rest of the update
+        return self.on_gpu and self.cfg.use_graphs and self.comm.graph_safe and not self.timer.enabled
 
     def train_epoch(self):
         cfg = self.cfg
@@ -270,7 +273,7 @@ class PixelA2CTrainer:
 
     def sync_from_rank0(self, src: int = 0):
         """Rank ``src``'s model and optimiser state everywhere (elastic re-form / auto-resume)."""
-        if self.comm.world <= 1:
+        if not self.comm.multi:
             return
         if self.on_gpu:
             m = self.model

@@ -88,13 +88,17 @@ class RolloutLearner:
             B = obs_b.shape[0]
         inv_B = 1.0 / (B * self.comm.world)
         graphs = lr.vloop.use_graph if lr.vloop is not None else False
-        if self.last_agent_rows and lr.vloop is not None:
-            lr.vloop.use_graph = False  # a new batch shape every epoch: no graph capture
+        if self.last_agent_rows:
+            # a new batch shape every epoch: no graph capture
+            lr.graphs_enabled = False
+            if lr.vloop is not None:
+                lr.vloop.use_graph = False
         try:
             with tm.phase("Optimize"):
                 lr.optimize(obs_b, act=a, actc=ac, mask=m, adv=adv_b, ret=ret_b, adv_stats=self.adv_stats,
                             logp_old=logp_b, inv_B=inv_B)
         finally:
+            lr.graphs_enabled = True
             if lr.vloop is not None:
                 lr.vloop.use_graph = graphs
 
@@ -118,7 +122,7 @@ class RolloutLearner:
                 vb = mlp_forward(FwdMode.VALUE, lr.vf.params, d["boot_obs"], 1, H)["v"]
                 boot = boot.index_copy(0, bi.to(boot.device), vb.to(boot.dtype))
         else:
-            boot = torch.nan_to_num(boot, nan=0.0)
+            boot = torch.zeros_like(boot)  # no value net: last_val dropped (replay_buffer.py:74-77)
         adv_e, ret_e, st_e = scan_flat(d["rew"], d["done"], val, boot, self.gamma, self.lam)
         self.adv_stats.add_(st_e.to(self.adv_stats.device))
         if d["has_logp"]:

@@ -117,7 +117,7 @@ class VecTrainer:
                                  self.comm, cfg.use_graphs, num_minibatches=cfg.num_minibatches)
         self.pi, self.vf = self.learner.pi, self.learner.vf
         self.timer = PhaseTimer(dev, enabled=cfg.phase_timing)
-        if self.comm.world > 1 and cfg.phase_timing:
+        if self.comm.multi and cfg.phase_timing:
             self.comm.timer = self.timer  # AllReduce phase (gradient + statistics all-reduces)
         self.rl = RolloutLearner(self.learner, T, N, cfg.gamma, cfg.lam, self.comm, self.timer)
         self.env_seed = (cfg.seed * 0x9E3779B97F4A7C15 + rank * 0x632BE59BD9B4E019) & 0x7FFFFFFFFFFFFFFF
@@ -189,7 +189,7 @@ class VecTrainer:
         metrics() reads every column and the learner's loss slabs (~7 synchronising reads,
         a sizeable share of a 1 ms epoch)."""
         ns = self.ep_stats[:, :2].sum(0)
-        if self.comm.world > 1:
+        if self.comm.multi:
             ns = ns.double()
             if self.comm.backend != "nccl":
                 ns = ns.cpu()
@@ -206,7 +206,7 @@ class VecTrainer:
         """Rank ``src``'s learner state everywhere (after an elastic re-form, parallel/elastic.py,
         or an auto-resume where only some ranks hold the newest checkpoint); each rank keeps
         its own env streams."""
-        if self.comm.world > 1:
+        if self.comm.multi:
             self.learner.broadcast_state_(self.comm, src)
 
     def state_dict(self) -> dict:

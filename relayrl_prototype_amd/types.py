@@ -445,10 +445,11 @@ class EpisodeRecorder:
         self.mask = None if mask is None else np.zeros((c, mask.size), np.float32)
         self.rew = np.zeros(c, np.float32)
         self.logp = np.zeros(c, np.float32)
+        self.val = np.full(c, np.nan, np.float32)  # V(s_t) when the policy has a value head (reference wire)
         self.done = np.zeros(c, np.uint8)
         self._shapes = (obs.size, act.size, act.dtype.kind, None if mask is None else mask.size)
 
-    def record(self, obs: np.ndarray, act: np.ndarray, mask, logp) -> None:
+    def record(self, obs: np.ndarray, act: np.ndarray, mask, logp, val=None) -> None:
         key = (obs.size, act.size, act.dtype.kind, None if mask is None else mask.size)
         if self._shapes != key:
             if self.n:
@@ -461,6 +462,7 @@ class EpisodeRecorder:
             self.mask[i] = mask.reshape(-1)
         self.rew[i] = 0.0
         self.logp[i] = 0.0 if logp is None else float(logp)
+        self.val[i] = np.nan if val is None else float(val)
         self.done[i] = 0
         self.n = i + 1
 

@@ -52,13 +52,15 @@ def test_bench_rejects_world_size_mismatch():
 
 def test_bench_actor_learner_deadline_keeps_the_headline():
     """A secondary phase that overruns its deadline (a hung transfer) still yields ONE JSON line
-    with the headline, the phase marked failed, and exit status 0 on every rank."""
+    with the headline and the phase marked failed, and the run exits NON-zero (bench.DEADLINE_EXIT
+    on every rank) so torchrun / CI see the hang."""
     r = _run(["--gpus", "2", "--steps", "1", "--warmup", "1", "--device", "cpu", "--num-envs", "16",
               "--rollout-len", "8", "--vf-iters", "2", "--phase-steps", "0", "--al-steps", "100000",
               "--al-deadline-s", "3"], {"RRL_DIST_BACKEND": "gloo"})
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode != 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
     assert rec["value"] > 0 and rec["n_gpus"] == 2
     assert rec["actor_learner"]["error"].startswith("deadline")
+    assert rec["actor_learner"]["exit_status"] == 3
