@@ -14,10 +14,13 @@ action to the current episode.  Semantics (docs/COMPAT.md):
     in-process subscription) and are swapped atomically between steps.
 
 ``wire_format``: "columns" (one RRLC frame per episode, the default), "actions" (per-action
-RRLT frames / protobuf actions), or "reference" (ZMQ only): the reference agent's own wire,
-to train against a reference Rust training server -- GET_MODEL without a format frame,
+RRLT frames / protobuf actions), or "reference": the reference agent's own wire, to train
+against a reference Rust training server.  ZMQ: GET_MODEL without a format frame,
 ``serde_pickle(Vec<RelayRLAction>)`` uploads (trajectory.rs:50-90) and TorchScript model
 pushes into a PULL this agent binds on ``training_server`` (agent_zmq.rs:316-442, 625-698).
+gRPC: ``ClientPoll{first_time: 1}`` handshake, per-episode ``SendActions`` with safetensors
+tensor fields, then a synchronous ``ClientPoll{first_time: 0, version}`` that swaps in a
+non-empty model (agent_grpc.rs:318-360, 492-599).
 Uploads are per episode (the reference re-sent the whole history each time, defect A1); each
 action carries its OWN step's reward and ``data = {"logp_a", "v"}`` tensors, and the episode
 ends in the reference's terminal marker ``(None, None, None, rew, done=True)`` whose reward is
@@ -69,8 +72,8 @@ class RelayRLAgent:
         if wire_format not in ("columns", "actions", "reference"):
             raise ValueError("wire_format must be 'columns' (RRLC frames), 'actions' (per-action RRLT / protobuf) "
                              "or 'reference' (serde_pickle frames + TorchScript pushes, ZMQ only)")
-        if wire_format == "reference" and self.server_type != "zmq":
-            raise ValueError("wire_format='reference' is the reference's ZMQ wire; use server_type='zmq'")
+        if wire_format == "reference" and self.server_type not in ("zmq", "grpc"):
+            raise ValueError("wire_format='reference' is the reference's ZMQ / gRPC wire")
         self.wire_format = wire_format
         self._rec = EpisodeRecorder(self.max_traj_length)
         if model_path is not None:
@@ -148,6 +151,12 @@ class RelayRLAgent:
             host = self.train_server["host"]
             if host in ("*", "0.0.0.0"):
                 host = "127.0.0.1"
+            if self.wire_format == "reference":
+                from ..transport.grpc_transport import ReferenceGrpcAgentTransport
+
+                self.transport = ReferenceGrpcAgentTransport(f"{host}:{self.train_server['port']}", self._set_policy,
+                                                             handshake_timeout_s=self._handshake_timeout)
+                return
             self.transport = GrpcAgentTransport(f"{host}:{self.train_server['port']}", self._set_policy,
                                                 handshake_timeout_s=self._handshake_timeout)
         elif self.server_type == "local":
@@ -157,32 +166,41 @@ class RelayRLAgent:
         else:
             raise ValueError(f"server_type must be zmq, grpc or local, not {self.server_type!r}")
 
-    def _reference_frame(self, cols, vals, done: bool, next_obs=None) -> bytes:
-        """One episode as the reference agent's upload: serde_pickle(Vec<RelayRLAction>).
-        ``vals`` = V(s_t) per row (NaN without a value head), recorded next to each row's
-        log-prob in the EpisodeRecorder so the two cannot drift apart."""
-        from ..transport.serde_pickle import reference_frame
-
+    def _reference_actions(self, cols, vals, done: bool, next_obs=None):
+        """One episode as the reference agent's actions (agent_zmq.rs:458-571 / agent_grpc.rs:
+        372-455): obs / act / mask as f32 tensors (the agent casts all three to Float), the
+        step()'s dict as ``data`` -- ``logp_a`` and, with a value head, ``v`` -- then the terminal
+        marker ``(None, None, None, rew, done=True)`` (agent_zmq.rs:605-610).  ``vals`` = V(s_t)
+        per row (NaN without a value head), recorded next to each row's log-prob in the
+        EpisodeRecorder so the two cannot drift apart."""
         acts = []
+        grpc = self.server_type == "grpc"
         for i in range(len(cols)):
             data = {"logp_a": np.array([cols.logp[i]], np.float32)}
             if not np.isnan(vals[i]):
                 data["v"] = np.array([vals[i]], np.float32)
-            acts.append(RelayRLAction(cols.obs[i], cols.act[i], None if cols.mask is None else cols.mask[i],
-                                      float(cols.rew[i]), data, False, True))
+            acts.append(RelayRLAction(np.asarray(cols.obs[i], np.float32), np.asarray(cols.act[i], np.float32),
+                                      None if cols.mask is None else np.asarray(cols.mask[i], np.float32),
+                                      float(cols.rew[i]), data, False, not grpc))
         last = 0.0
         if not done and next_obs is not None and self.policy is not None:
             with self._policy_lock:
                 v = self.policy.value(np.asarray(next_obs, np.float32).reshape(1, -1))
             last = 0.0 if v is None else float(np.asarray(v).reshape(-1)[0])
         acts.append(RelayRLAction(None, None, None, last, None, True, False))  # agent_zmq.rs:605-610 marker
-        return reference_frame(acts)
+        return acts
 
     def _ship(self, done: bool, next_obs=None):
         if self.wire_format == "reference":
             vals = self._rec.val[:self._rec.n].copy()
             cols = self._rec.take(self.agent_id, self.episodes_sent, done, next_obs)
-            self.transport.send_trajectory(self._reference_frame(cols, vals, done, next_obs))
+            acts = self._reference_actions(cols, vals, done, next_obs)
+            if self.server_type == "grpc":
+                self.transport.send_actions(acts)  # SendActions, then the synchronous ClientPoll
+            else:
+                from ..transport.serde_pickle import reference_frame
+
+                self.transport.send_trajectory(reference_frame(acts))
             self.episodes_sent += 1
             return
         cols = self._rec.take(self.agent_id, self.episodes_sent, done, next_obs)

@@ -177,12 +177,17 @@ class TrainingServer:
     def close(self, save: bool = True):
         if self.engine is not None and hasattr(self.engine, "stop"):
             self.engine.stop()
-            self.engine.join(60)
+            try:
+                self.engine.join(60)
+            except Exception as e:  # a failed background run must not block the shutdown
+                print(f"[TrainingServer] engine ended with {e!r}", flush=True)
         tr = getattr(self.algorithm, "trainer", None)
         if tr is not None and hasattr(tr, "close"):  # releases the host trainer's CU-masked streams
             tr.close()
         self.disable_server()
         self.service.stop(drain=True)
+        if hasattr(self.algorithm, "close"):  # the multi-rank engine's relay sockets
+            self.algorithm.close()
         if self.tb is not None:
             self.tb.stop()
         if save:
@@ -198,15 +203,14 @@ class TrainingServer:
         """Run the device engine (see runtime/engine.py) until ``epochs`` epochs, the mean return of
         the newest >= ``window`` episodes reaching ``target_return``, or ``max_seconds``.  Returns a
         TrainResult (``time_to_threshold_s`` is measured from this server's construction);
-        ``background=True`` returns at once (``engine.join()`` for the result)."""
+        ``background=True`` returns at once (``engine.join()`` for the result; ``engine.stop()``
+        ends it after the current epoch, on every rank)."""
         if self.engine is None:
             raise RuntimeError("this server learns from agent uploads; construct it with engine=... "
                                "(or an \"engine\" entry in the config's \"mi355x\" block) to train on device envs")
         kw = dict(epochs=epochs, target_return=target_return, window=window, max_seconds=max_seconds,
                   log_every=log_every, publish_every=publish_every)
-        if background:
-            if not hasattr(self.engine, "start"):
-                raise RuntimeError("background training needs the in-process (world_size 1) engine")
+        if background:  # the agents keep being served meanwhile (both the in-process and the multi-rank engine)
             self.engine.start(**kw)
             return None
         return self.engine.train(**kw)

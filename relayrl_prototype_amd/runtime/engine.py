@@ -16,7 +16,9 @@ writes the reference's ``progress.txt`` columns (REINFORCE.py:127-139) through t
 EpochLogger and publishes each new policy to the server's ModelStore, so agents attached
 over ZMQ / gRPC / local keep receiving models exactly as with the trajectory learner.
 With ``world_size > 1`` the ranks run as a ``torch.distributed.run`` CHILD process (one
-rank per GPU, RCCL); rank 0 drops versioned weight files that the API process publishes.
+rank per GPU, RCCL); rank 0 is linked to the API process by an in-memory relay
+(engine_relay.py): agent uploads go in and are folded into rank 0's shard, every new policy
+comes out and is published to the agents -- no file on the weight path.
 """
 from __future__ import annotations
 
@@ -155,12 +157,15 @@ class EngineAlgorithm(AlgorithmAbstract):
         # Agent uploads (the reference's "agents upload -> learner trains on them",
         # training_zmq.rs:994-1031 / REINFORCE.py:70-95): staged on the host as concatenated
         # paths and folded into the NEXT engine epoch's batch as extra rows (their own scan and
-        # bootstraps, rollout_learn.RolloutLearner._fold).  For the single-process MLP engines
-        # (vec / host); "agent_rows": false in the "mi355x" block / hyperparams turns it off.
+        # bootstraps, rollout_learn.RolloutLearner._fold_scan).  For the MLP engines (vec /
+        # host); "agent_rows": false in the "mi355x" block / hyperparams turns it off.  With
+        # several ranks only rank 0 receives uploads (engine_relay.py) and every rank agrees on
+        # the global row count per epoch (RolloutLearner.count_sync).
         lr = self.learner
         self.agent_rows = (bool(spec.trainer.get("agent_rows", True)) and spec.kind in ("vec", "host")
-                           and lr is not None and (self.comm is None or self.comm.world == 1)
-                           and hasattr(self.trainer, "rl"))
+                           and lr is not None and hasattr(self.trainer, "rl"))
+        if self.agent_rows and self.comm is not None and self.comm.multi:
+            self.trainer.rl.count_sync = True
         self.agent_rows_total = 0
         self.agent_episodes = 0
         self.agent_trajectories = 0
@@ -340,6 +345,9 @@ class EngineRunner:
         self._stop = threading.Event()
         self.result: Optional[TrainResult] = None
         self._lock = threading.Lock()
+        # ranks whose stop request reaches one rank only (engine_relay STOP -> rank 0) agree on
+        # it with one all-reduce per epoch
+        self.agree_stop = False
 
     def _publish(self):
         if self.algo.publishes_policy:
@@ -364,7 +372,12 @@ class EngineRunner:
             steps0 = int(getattr(algo.trainer, "env_steps", 0)) * world
             solved, ttt, win = False, None, float("nan")
             m: Dict[str, Any] = {}
-            while not self._stop.is_set():
+            while True:
+                if self.agree_stop:
+                    if _agree(comm, self._stop.is_set()):
+                        break
+                elif self._stop.is_set():
+                    break
                 algo.train_model()
                 k = algo.epoch - e0
                 # every rank takes the same branches: metrics() / episode_sums() are collectives
@@ -429,15 +442,19 @@ def _agree(comm, flag: bool) -> bool:
 
 # ---------------------------------------------------------------------- multi-rank (child ranks)
 class RemoteEngineAlgorithm(AlgorithmAbstract):
-    """API-side view of an engine whose ranks run in a child ``torch.distributed.run``: holds
-    the newest policy rank 0 published (``publish_dir``) so the server can serve it."""
+    """API-side view of an engine whose ranks run in a child ``torch.distributed.run``.
+
+    Holds the newest policy rank 0 sent over the in-memory relay (engine_relay.py) so the
+    server can serve it, and forwards agent uploads to rank 0, which folds them into its
+    shard of the next epoch (training_zmq.rs:948-1058 -> REINFORCE.py:70-95)."""
 
     def __init__(self, spec: EngineSpec, obs_dim: int, act_dim: int, publish_dir: str,
                  save_model_path: Optional[str] = None):
         from ..ops.mlp import MLPSpec
+        from .engine_relay import ApiRelay
 
         self.spec = spec
-        self.publish_dir = publish_dir
+        self.publish_dir = publish_dir  # spec / result / logs of the child ranks (no weights)
         os.makedirs(publish_dir, exist_ok=True)
         self.save_model_path = save_model_path or os.path.join(os.getcwd(), "server_model.pt")
         self.obs_dim, self.act_dim = int(obs_dim), int(act_dim)
@@ -449,37 +466,41 @@ class RemoteEngineAlgorithm(AlgorithmAbstract):
         self.vf = MLPSpec(self.obs_dim, self.hidden, 1).init(g) if with_vf else None
         self.version = 0
         self.epoch = 0
+        self.accepts_uploads = (bool(spec.trainer.get("agent_rows", True)) and spec.kind in ("vec", "host"))
+        self.ignored_trajectories = 0
+        self.relay = ApiRelay()
+        self._lock = threading.Lock()
+        self._cv = threading.Condition(self._lock)
 
-    def poll(self) -> bool:
-        """Load a newer published policy if rank 0 wrote one; True when it did."""
-        p = os.path.join(self.publish_dir, "latest.json")
-        try:
-            meta = json.load(open(p))
-        except (OSError, ValueError):
-            return False
-        if int(meta["version"]) <= self.version:
-            return False
-        from safetensors.torch import load_file
-
-        t = load_file(os.path.join(self.publish_dir, meta["file"]))
-        self.pi = t["pi"]
-        if "vf" in t:
-            self.vf = t["vf"]
-        self.version = int(meta["version"])
-        self.epoch = int(meta.get("epoch", self.version))
+    def set_model(self, blob) -> bool:
+        """A model rank 0 sent (relay thread); True if it is newer than the one held."""
+        with self._cv:
+            if blob.version <= self.version:
+                return False
+            self.pi = torch.from_numpy(blob.pi)
+            self.vf = None if blob.vf is None else torch.from_numpy(blob.vf)
+            self.version = int(blob.version)
+            self.epoch = int(blob.meta.get("epoch", blob.version))
+            self._cv.notify_all()
         return True
 
+    def wait_version(self, version: int, timeout: float) -> bool:
+        with self._cv:
+            return self._cv.wait_for(lambda: self.version >= version, timeout)
+
     def get_weights(self) -> Dict[str, Any]:
-        w = {"pi": self.pi.clone(), "version": self.version, "obs_dim": self.obs_dim, "act_dim": self.act_dim,
-             "hidden": self.hidden, "discrete": self.discrete}
-        if self.vf is not None:
-            w["vf"] = self.vf.clone()
+        with self._lock:
+            w = {"pi": self.pi.clone(), "version": self.version, "obs_dim": self.obs_dim, "act_dim": self.act_dim,
+                 "hidden": self.hidden, "discrete": self.discrete}
+            if self.vf is not None:
+                w["vf"] = self.vf.clone()
         return w
 
     def policy_module(self):
         from ..models.policies import build_policy_module
 
-        return build_policy_module(self.obs_dim, self.act_dim, self.hidden, self.pi, self.vf, self.discrete)
+        w = self.get_weights()
+        return build_policy_module(self.obs_dim, self.act_dim, self.hidden, w["pi"], w.get("vf"), self.discrete)
 
     def model_bytes(self) -> bytes:
         from ..models.policies import torchscript_bytes
@@ -492,6 +513,10 @@ class RemoteEngineAlgorithm(AlgorithmAbstract):
         export_torchscript(self.policy_module(), path or self.save_model_path)
 
     def receive_trajectory(self, trajectory) -> bool:
+        """Forward an agent upload to rank 0 (queued until the ranks are up); the engine's own
+        epochs publish the models, so this never reports an update."""
+        if not self.accepts_uploads or not self.relay.send_upload(trajectory):
+            self.ignored_trajectories += 1
         return False
 
     def train_model(self) -> None:
@@ -500,30 +525,13 @@ class RemoteEngineAlgorithm(AlgorithmAbstract):
     def log_epoch(self) -> None:
         pass
 
-
-def publish_weights(algo: EngineAlgorithm, publish_dir: str) -> None:
-    """Rank 0: write the current policy as ``model_<version>.safetensors`` + ``latest.json``."""
-    from safetensors.torch import save_file
-
-    w = algo.get_weights()
-    os.makedirs(publish_dir, exist_ok=True)
-    name = f"model_{algo.version:08d}.safetensors"
-    t = {"pi": w["pi"].contiguous()}
-    if w.get("vf") is not None:
-        t["vf"] = w["vf"].contiguous()
-    save_file(t, os.path.join(publish_dir, name))
-    tmp = os.path.join(publish_dir, f"latest.json.tmp{os.getpid()}")
-    with open(tmp, "w") as f:
-        json.dump({"version": algo.version, "epoch": algo.epoch, "file": name}, f)
-    os.replace(tmp, os.path.join(publish_dir, "latest.json"))
-    old = os.path.join(publish_dir, f"model_{algo.version - 2:08d}.safetensors")
-    if algo.version >= 2 and os.path.exists(old):
-        os.remove(old)
+    def close(self) -> None:
+        self.relay.close()
 
 
 class MultiRankEngineRunner:
     """Runs the engine's ranks as a ``torch.distributed.run`` child (one rank per GPU over
-    RCCL) and republishes rank 0's policy files to the server's store."""
+    RCCL); rank 0's models arrive over the relay and go straight to the server's store."""
 
     def __init__(self, algo: RemoteEngineAlgorithm, service, env_dir: str, t_start: float):
         self.algo = algo
@@ -531,13 +539,14 @@ class MultiRankEngineRunner:
         self.env_dir = env_dir
         self.t_start = t_start
         self.result: Optional[TrainResult] = None
+        self.error: Optional[BaseException] = None
+        self._thread: Optional[threading.Thread] = None
+        algo.relay.on_model(self._on_model)
 
-    def _watch(self, stop: threading.Event):
-        while not stop.is_set():
-            if self.algo.poll():
-                self.service.updates += 1
-                self.service.publish_model()
-            stop.wait(0.05)
+    def _on_model(self, blob):
+        if self.algo.set_model(blob):
+            self.service.updates += 1
+            self.service.publish_model()
 
     def train(self, epochs: Optional[int] = None, target_return: Optional[float] = None, window: int = 100,
               max_seconds: Optional[float] = None, log_every: int = 1, publish_every: int = 1) -> TrainResult:
@@ -549,37 +558,58 @@ class MultiRankEngineRunner:
         res_path = os.path.join(self.algo.publish_dir, "result.json")
         if os.path.exists(res_path):
             os.remove(res_path)
-        argv = ["engine", "--spec", spec_path, "--env-dir", self.env_dir, "--publish-dir", self.algo.publish_dir,
+        argv = ["engine", "--spec", spec_path, "--env-dir", self.env_dir,
                 "--log-every", str(log_every), "--publish-every", str(publish_every), "--window", str(window),
-                "--t-start-wall", repr(time.time() - (time.perf_counter() - self.t_start)), "--result", res_path]
+                "--t-start-wall", repr(time.time() - (time.perf_counter() - self.t_start)), "--result", res_path,
+                "--version0", str(self.algo.version)] + self.algo.relay.argv()
         if epochs is not None:
             argv += ["--epochs", str(epochs)]
         if target_return is not None:
             argv += ["--target-return", str(target_return)]
         if max_seconds is not None:
             argv += ["--max-seconds", str(max_seconds)]
-        stop = threading.Event()
-        w = threading.Thread(target=self._watch, args=(stop,), daemon=True)
-        w.start()
-        try:
-            rc = spawn_ranks(argv, self.algo.spec.world_size)
-        finally:
-            stop.set()
-            w.join()
-        if self.algo.poll():
-            self.service.updates += 1
-            self.service.publish_model()
+        rc = spawn_ranks(argv, self.algo.spec.world_size)
         if rc != 0:
             raise RuntimeError(f"engine ranks exited with code {rc}")
         d = json.load(open(res_path))
+        final = int(d.pop("version", self.algo.version))
+        self.algo.wait_version(final, 10.0)  # the last MODEL frame is in flight over the relay
         self.result = TrainResult(**d)
         return self.result
 
+    # background training (TrainingServer.train(background=True))
+    def start(self, **kw):
+        self.error = None
 
-def run_engine_rank(spec: EngineSpec, env_dir: str, publish_dir: Optional[str], epochs: Optional[int],
-                    target_return: Optional[float], window: int, max_seconds: Optional[float], log_every: int,
-                    publish_every: int, t_start_wall: Optional[float], result_path: Optional[str]) -> int:
-    """One rank of a multi-GPU engine (``python -m relayrl_prototype_amd engine ...``)."""
+        def run():
+            try:
+                self.train(**kw)
+            except BaseException as e:  # noqa: BLE001 -- surfaced by join()
+                self.error = e
+
+        self._thread = threading.Thread(target=run, name="relayrl-engine-ranks", daemon=True)
+        self._thread.start()
+
+    def stop(self):
+        """Ask the ranks to stop after their current epoch (STOP over the relay; the ranks
+        agree on it with one all-reduce per epoch)."""
+        if self._thread is not None and self._thread.is_alive():
+            self.algo.relay.send_stop()
+
+    def join(self, timeout: Optional[float] = None) -> Optional[TrainResult]:
+        if self._thread is not None:
+            self._thread.join(timeout)
+        if self.error is not None:
+            raise self.error
+        return self.result
+
+
+def run_engine_rank(spec: EngineSpec, env_dir: str, epochs: Optional[int], target_return: Optional[float],
+                    window: int, max_seconds: Optional[float], log_every: int, publish_every: int,
+                    t_start_wall: Optional[float], result_path: Optional[str], relay_up: Optional[int] = None,
+                    relay_down: Optional[int] = None, version0: int = 0) -> int:
+    """One rank of a multi-GPU engine (``python -m relayrl_prototype_amd engine ...``).  Rank 0
+    ends the relay (engine_relay.py): agent uploads in, models out, STOP."""
     from ..parallel.comm import Comm, dist_env, init_distributed, local_device_index
 
     _, _, world = dist_env()
@@ -589,23 +619,38 @@ def run_engine_rank(spec: EngineSpec, env_dir: str, publish_dir: Optional[str], 
         dev = torch.device("cuda", local_device_index())
         torch.cuda.set_device(dev)
     algo = EngineAlgorithm(spec, env_dir, comm=comm, device=dev)
+    algo.version = int(version0)
+    relay = None
 
-    class _Pub:  # rank 0 publishes through files instead of a ModelStore
+    class _Pub:  # rank 0 sends every new policy to the API process from memory
         updates = 0
 
         def publish_model(self):
-            if algo.rank == 0 and publish_dir and algo.publishes_policy:
-                publish_weights(algo, publish_dir)
+            if relay is not None and algo.publishes_policy:
+                from .model_store import ModelBlob
+
+                w = algo.get_weights()
+                meta = {k: w[k] for k in ("obs_dim", "act_dim", "hidden", "discrete")}
+                meta["epoch"] = algo.epoch
+                relay.send_model(ModelBlob(int(w["version"]), meta, w["pi"].numpy(),
+                                           None if w.get("vf") is None else w["vf"].numpy()))
 
     # the clock of the threshold metric starts where the API object was built (parent process)
     t_start = time.perf_counter() - (time.time() - t_start_wall) if t_start_wall else time.perf_counter()
     r = EngineRunner(algo, _Pub(), t_start)
+    if relay_up is not None and comm.rank == 0:
+        from .engine_relay import RankRelay
+
+        relay = RankRelay(relay_up, relay_down, algo.receive_trajectory, r.stop)
+    r.agree_stop = relay_up is not None and comm.multi  # STOP reaches rank 0 only
     res = r.train(epochs, target_return, window, max_seconds, log_every, publish_every)
     if algo.rank == 0 and result_path:
         tmp = result_path + ".tmp"
         with open(tmp, "w") as f:
-            json.dump(res.to_dict(), f)
+            json.dump(dict(res.to_dict(), version=algo.version), f)
         os.replace(tmp, result_path)
+    if relay is not None:
+        relay.close()
     if hasattr(algo.trainer, "close"):
         algo.trainer.close()
     elif hasattr(algo.trainer, "finish"):

@@ -391,7 +391,9 @@ def main(argv=None) -> int:
     e = sub.add_parser("engine", help="one rank of a TrainingServer device engine (runtime/engine.py)")
     e.add_argument("--spec", required=True)
     e.add_argument("--env-dir", default=".")
-    e.add_argument("--publish-dir", default=None)
+    e.add_argument("--relay-up", type=int, default=None, help="rank 0: port of the upload / control PULL")
+    e.add_argument("--relay-down", type=int, default=None, help="rank 0: port of the API process's model PULL")
+    e.add_argument("--version0", type=int, default=0, help="model version the API process holds")
     e.add_argument("--epochs", type=int, default=None)
     e.add_argument("--target-return", type=float, default=None)
     e.add_argument("--window", type=int, default=100)
@@ -419,8 +421,8 @@ def main(argv=None) -> int:
         from .engine import EngineSpec, run_engine_rank
 
         spec = EngineSpec.from_json(open(a.spec).read())
-        return run_engine_rank(spec, a.env_dir, a.publish_dir, a.epochs, a.target_return, a.window, a.max_seconds,
-                               a.log_every, a.publish_every, a.t_start_wall, a.result)
+        return run_engine_rank(spec, a.env_dir, a.epochs, a.target_return, a.window, a.max_seconds, a.log_every,
+                               a.publish_every, a.t_start_wall, a.result, a.relay_up, a.relay_down, a.version0)
     if a.cmd == "plot":
         from ..utils.plot import main as plot_main
 

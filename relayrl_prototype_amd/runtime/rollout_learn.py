@@ -37,6 +37,9 @@ class RolloutLearner:
         # agent uploads folded into the next batch (runtime/engine.py): a FlatBuffer.take() dict
         self.pending_rows = None
         self.last_agent_rows = 0
+        # several ranks with uploads staged on one of them (runtime/engine.py): agree on the
+        # global row count each epoch (see learn)
+        self.count_sync = False
         if dev.type == "cuda":
             from ..ops import hip
 
@@ -74,21 +77,35 @@ class RolloutLearner:
                 self.adv.view(-1).copy_(adv.reshape(-1))
                 self.ret.view(-1).copy_(ret.reshape(-1))
                 self.adv_stats.copy_(stats)
+            extra, self.pending_rows = self.pending_rows, None
+            self.last_agent_rows = 0
+            folded = None
+            if extra is not None and extra["obs"].shape[0] > 0:
+                # the uploads' scan runs BEFORE the statistics all-reduce: their advantage sums
+                # and row count enter the global normalisation on every rank
+                with tm.phase("AgentRows"):
+                    folded = self._fold_scan(extra)
             self.comm.all_reduce_sum_(self.adv_stats)
         discrete = lr.discrete
         a = act.reshape(B) if discrete else None
         ac = None if discrete else act.reshape(B, -1)
         m = None if mask is None else mask.reshape(B, -1)
         adv_b, ret_b, logp_b = self.adv.view(-1), self.ret.view(-1), logp.reshape(-1)
-        extra, self.pending_rows = self.pending_rows, None
-        self.last_agent_rows = 0
-        if extra is not None and extra["obs"].shape[0] > 0:
-            with tm.phase("AgentRows"):
-                obs_b, a, ac, m, adv_b, ret_b, logp_b = self._fold(extra, obs_b, a, ac, m, adv_b, ret_b, logp_b)
-            B = obs_b.shape[0]
-        inv_B = 1.0 / (B * self.comm.world)
+        if folded is not None:
+            obs_b, a, ac, m, adv_b, ret_b, logp_b = self._fold_cat(folded, obs_b, a, ac, m, adv_b, ret_b, logp_b)
+        B = obs_b.shape[0]
+        any_rows = self.last_agent_rows > 0
+        if self.count_sync:
+            # several ranks, uploads staged on rank 0 only: the global row count (all-reduced
+            # statistics) sets the loss scale on every rank, and every rank goes eager when
+            # any rank folded rows (one host read per epoch, only in this mode)
+            total = int(round(float(self.adv_stats[2].item())))
+            inv_B = 1.0 / max(total, 1)
+            any_rows = total != self.T * self.N * self.K * self.comm.world
+        else:
+            inv_B = 1.0 / (B * self.comm.world)
         graphs = lr.vloop.use_graph if lr.vloop is not None else False
-        if self.last_agent_rows:
+        if any_rows:
             # a new batch shape every epoch: no graph capture
             lr.graphs_enabled = False
             if lr.vloop is not None:
@@ -102,16 +119,15 @@ class RolloutLearner:
             if lr.vloop is not None:
                 lr.vloop.use_graph = graphs
 
-    def _fold(self, d, obs_b, a, ac, m, adv_b, ret_b, logp_b):
-        """Agent uploads (concatenated paths, FlatBuffer.take) appended to the device batch as
-        extra rows: their own flat segmented scan (finish_path semantics, REINFORCE.py:70-95 /
-        replay_buffer.py:48-79) with V(s) from the current value net and V(s_T) bootstraps for
-        cut paths, their advantage sums added to the batch statistics, then one concatenated
-        batch for the policy and value steps."""
+    def _fold_scan(self, d):
+        """Agent uploads (concatenated paths, FlatBuffer.take): their own flat segmented scan
+        (finish_path semantics, REINFORCE.py:70-95 / replay_buffer.py:48-79) with V(s) from the
+        current value net and V(s_T) bootstraps for cut paths; their advantage sums are added to
+        this rank's batch statistics (before the all-reduce)."""
         lr = self.learner
         H = lr.hidden
-        n = d["obs"].shape[0]
-        obs_e = d["obs"].to(obs_b.device)
+        dev = self.adv_stats.device
+        obs_e = d["obs"].to(dev)
         boot = d["boot"]
         val = None
         if lr.vf is not None:
@@ -124,7 +140,7 @@ class RolloutLearner:
         else:
             boot = torch.zeros_like(boot)  # no value net: last_val dropped (replay_buffer.py:74-77)
         adv_e, ret_e, st_e = scan_flat(d["rew"], d["done"], val, boot, self.gamma, self.lam)
-        self.adv_stats.add_(st_e.to(self.adv_stats.device))
+        self.adv_stats.add_(st_e.to(dev))
         if d["has_logp"]:
             logp_e = d["logp"]
         else:  # uploads without log-probs: the current policy's (PPO ratio 1 on those rows)
@@ -132,18 +148,26 @@ class RolloutLearner:
             logp_e = mlp_forward(mode, lr.pi.params, obs_e, lr.act_dim, H, mask=d["mask"],
                                  act_in=d["act"] if lr.discrete else None,
                                  actc_in=None if lr.discrete else d["act"])["logp"]
+        return dict(d, obs=obs_e, adv=adv_e, ret=ret_e, logp=logp_e)
+
+    def _fold_cat(self, e, obs_b, a, ac, m, adv_b, ret_b, logp_b):
+        """The scanned uploads appended to the device batch as extra rows: one concatenated
+        batch for the policy and value steps."""
+        lr = self.learner
+        n = e["obs"].shape[0]
         cat = torch.cat
-        obs_c = cat([obs_b, obs_e])
+        obs_c = cat([obs_b, e["obs"]])
         if lr.discrete:
-            a = cat([a, d["act"].to(a.dtype)])
+            a = cat([a, e["act"].to(a.dtype)])
         else:
-            ac = cat([ac, d["act"].reshape(n, -1)])
-        mask_e = d["mask"]
+            ac = cat([ac, e["act"].reshape(n, -1)])
+        mask_e = e["mask"]
         if m is not None or (lr.discrete and not bool((mask_e == 1).all())):
             m_b = m if m is not None else torch.ones(obs_b.shape[0], lr.act_dim, device=obs_b.device)
             m = cat([m_b, mask_e])
         self.last_agent_rows = n
-        return obs_c, a, ac, m, cat([adv_b, adv_e]), cat([ret_b, ret_e]), cat([logp_b, logp_e.reshape(-1)])
+        return (obs_c, a, ac, m, cat([adv_b, e["adv"]]), cat([ret_b, e["ret"]]),
+                cat([logp_b, e["logp"].reshape(-1)]))
 
 
 def episode_metrics(comm: Comm, n, s, sq, mx, mn, sum_len) -> dict:

@@ -23,6 +23,12 @@ Extensions (reference tonic clients never call them, so wire compatibility holds
 frame instead of a per-action protobuf (one memcpy-sized message per episode).  The
 agent keeps a background long-poll thread for model updates, so an upload never waits
 on ``ClientPoll`` (the reference polled synchronously after every send, agent_grpc.rs).
+
+``ReferenceGrpcAgentTransport`` is the reference agent's OWN gRPC dialect, to train against a
+reference (tonic) training server: ``ClientPoll{first_time: 1, version: 0}`` every 500 ms
+until a TorchScript archive arrives, per-episode ``SendActions`` with safetensors tensor
+fields / JSON ``RelayRLData`` / ``reward_update_flag = false``, then one synchronous
+``ClientPoll{first_time: 0, version}`` that swaps the policy on a non-empty model.
 """
 from __future__ import annotations
 
@@ -320,4 +326,101 @@ class GrpcAgentTransport:
         self._stop.set()
         if self._poller is not None:
             self._poller.join(timeout=6)
+        self.channel.close()
+
+
+class ReferenceGrpcAgentTransport:
+    """The reference gRPC agent's wire (agent_grpc.rs:318-360 handshake, 492-533 SendActions,
+    540-599 poll and swap; grpc_utils.rs:31-129 action codec, 196-205 model decode).
+
+    Differences by design: the archive is read from its raw zip storages
+    (``utils.checkpoint.reference_weights_from_bytes``, nothing unpickled, no tempfile); an RPC
+    error is reported instead of ``process::exit(1)`` (agent_grpc.rs:528-531); the handshake
+    is bounded by ``handshake_timeout_s``.  The reference server always answers version 0
+    (training_grpc.rs:724,746,775), so ``server_version`` is echoed back as the reference does
+    and ``version`` counts the models this agent actually loaded."""
+
+    def __init__(self, address: str, on_model: Callable[[ModelBlob], None], handshake_timeout_s: float = 60.0,
+                 retry_interval_s: float = 0.5, rpc_timeout_s: float = 30.0):
+        import grpc
+
+        self.on_model = on_model
+        self.rpc_timeout_s = rpc_timeout_s
+        addr = address.replace("tcp://", "")
+        if addr.startswith("*:"):
+            addr = "127.0.0.1:" + addr[2:]
+        self.channel = grpc.insecure_channel(addr, options=[("grpc.max_receive_message_length", 256 << 20),
+                                                             ("grpc.max_send_message_length", 256 << 20)])
+        self._send = self.channel.unary_unary(f"/{SERVICE}/SendActions", request_serializer=PbTrajectory.SerializeToString,
+                                              response_deserializer=PbResponse.FromString)
+        self._poll = self.channel.unary_unary(f"/{SERVICE}/ClientPoll", request_serializer=PbRequest.SerializeToString,
+                                              response_deserializer=PbModel.FromString)
+        self.version = 0          # models loaded by this agent
+        self.server_version = 0   # the version field the server last answered (echoed in polls)
+        self.bad_models = 0
+        self.rejected = 0
+        t0 = time.time()
+        while True:
+            try:
+                r = self._poll(PbRequest(first_time=1, version=0), timeout=10)
+                if r.code == 1 and len(r.model) and self._load(r):
+                    break
+            except Exception as e:  # noqa: BLE001 -- server not up yet: retry like the reference
+                if time.time() - t0 > handshake_timeout_s:
+                    raise ConnectionError(f"gRPC server {addr}: {e!r}")
+            if time.time() - t0 > handshake_timeout_s:
+                raise TimeoutError("reference gRPC model handshake timed out")
+            time.sleep(retry_interval_s)  # agent_grpc.rs:357 (500 ms)
+
+    def _load(self, r) -> bool:
+        from ..utils.checkpoint import reference_weights_from_bytes
+
+        try:
+            w = reference_weights_from_bytes(bytes(r.model))
+        except Exception as e:  # noqa: BLE001 -- a model the agent cannot validate is skipped
+            self.bad_models += 1
+            print(f"[ReferenceGrpcAgentTransport] bad model: {e!r}", flush=True)
+            return False
+        self.version += 1
+        self.server_version = int(r.version)
+        self.on_model(ModelBlob(self.version, {"obs_dim": w["obs_dim"], "act_dim": w["act_dim"],
+                                               "hidden": w["hidden"], "discrete": True}, w["pi"], w["vf"]))
+        return True
+
+    def send_actions(self, actions) -> bool:
+        """One episode (its actions + the terminal marker) as ``SendActions``; on acceptance one
+        ``ClientPoll{first_time: 0}`` that swaps in a newer model if the server has one."""
+        from ..utils.faults import injector
+
+        inj = injector()
+        if inj.enabled and inj.filter_upload(b"x" * 32) is None:
+            return True  # injected loss
+        msg = PbTrajectory(actions=[action_to_pb(a) for a in actions])
+        for m in msg.actions:
+            m.reward_update_flag = False  # grpc_utils.rs:64 hard-codes it
+        try:
+            r = self._send(msg, timeout=self.rpc_timeout_s)
+        except Exception as e:  # noqa: BLE001 -- reported, not process::exit(1)
+            print(f"[ReferenceGrpcAgentTransport] SendActions failed: {e!r}", flush=True)
+            return False
+        if r.code != 1:
+            self.rejected += 1
+            return False
+        self.poll()
+        return True
+
+    def poll(self) -> bool:
+        try:
+            r = self._poll(PbRequest(first_time=0, version=self.server_version), timeout=self.rpc_timeout_s)
+        except Exception as e:  # noqa: BLE001
+            print(f"[ReferenceGrpcAgentTransport] ClientPoll failed: {e!r}", flush=True)
+            return False
+        if r.code == 1 and len(r.model):
+            return self._load(r)
+        return False
+
+    def heartbeat(self):
+        pass
+
+    def close(self):
         self.channel.close()

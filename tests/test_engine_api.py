@@ -129,8 +129,8 @@ def test_training_server_engine_from_config_block(cfgdir):
 
 
 def test_training_server_multi_rank_engine_gloo(cfgdir, monkeypatch):
-    """world_size 2: the ranks run in a torch.distributed.run child; rank 0's policy files are
-    republished by the API process."""
+    """world_size 2: the ranks run in a torch.distributed.run child; rank 0's policies reach the
+    API process (and its agents) over the in-memory relay, never through files."""
     tmp, cfgp = cfgdir
     monkeypatch.setenv("RRL_DIST_BACKEND", "gloo")
     hp = {"num_envs": 8, "rollout_len": 8, "train_vf_iters": 1, "num_threads": 1, "world_size": 2}
@@ -144,6 +144,75 @@ def test_training_server_multi_rank_engine_gloo(cfgdir, monkeypatch):
         prog = list((tmp / "env" / "logs").rglob("progress.txt"))
         assert len(prog) == 1  # rank 0 logs
         assert read_progress(str(prog[0]))["Epoch"] == [1.0, 2.0]
+        # a second run continues the version sequence
+        srv.train(epochs=1)
+        assert srv.model_version == 3 and agent.model_version == 3
         agent.close()
     finally:
         srv.close(save=False)
+    assert not list((tmp / "env").rglob("*.safetensors"))  # no weight files anywhere
+
+
+def drive_agent_against_background_engine(srv, agent, env_dir, seconds: float = 90.0):
+    """Background training + one agent stepping CartPole episodes until rank 0's progress.txt
+    shows folded agent rows and the agent has seen >= 2 model updates; then stop the ranks.
+    Returns (versions seen, AgentRows column, TrainResult)."""
+    import time
+
+    from relayrl_prototype_amd import _native
+
+    srv.train(max_seconds=seconds + 30, background=True)
+    env = _native.VecEnv("CartPole-v1", 1, 11, 1)
+    obs = np.zeros((1, 4), np.float32)
+    rew = np.zeros(1, np.float32)
+    done = np.zeros(1, np.float32)
+    act = np.zeros(1, np.int32)
+    env.reset_ptr(obs.ctypes.data)
+    versions = [agent.model_version]
+    rows = []
+    t0 = time.time()
+    while time.time() - t0 < seconds:
+        r = 0.0
+        while True:
+            a = agent.request_for_action(obs[0].copy(), np.ones(2, np.float32), r)
+            act[0] = int(np.asarray(a.get_act()).reshape(-1)[0])
+            env.step_ptr(act.ctypes.data, obs.ctypes.data, rew.ctypes.data, done.ctypes.data)
+            r = float(rew[0])
+            if done[0] > 0:
+                agent.flag_last_action(r)
+                break
+        if agent.model_version != versions[-1]:
+            versions.append(agent.model_version)
+        prog = list(env_dir.rglob("progress.txt"))
+        if prog:
+            rows = read_progress(str(prog[0])).get("AgentRows", [])
+        if len(versions) >= 3 and any(v > 0 for v in rows):
+            break
+        time.sleep(0.01)
+    srv.engine.stop()
+    res = srv.engine.join(60)
+    return versions, rows, res
+
+
+def test_zmq_agent_feeds_and_follows_a_two_rank_engine(cfgdir, monkeypatch):
+    """a ZMQ agent attached to a world_size=2 engine server while it trains in
+    the background contributes rows to rank 0's batches (AgentRows > 0 in progress.txt),
+    receives increasing model versions, and no file is on the weight path."""
+    tmp, cfgp = cfgdir
+    monkeypatch.setenv("RRL_DIST_BACKEND", "gloo")
+    hp = {"num_envs": 8, "rollout_len": 8, "train_vf_iters": 1, "num_threads": 1, "world_size": 2}
+    srv = TrainingServer("REINFORCE", 4, 2, 1000, env_dir=str(tmp / "env"), config_path=cfgp, server_type="zmq",
+                         device="cpu", hyperparams=hp, engine="host")
+    agent = None
+    try:
+        agent = RelayRLAgent(config_path=cfgp, server_type="zmq", handshake_timeout_s=30, seed=3)
+        versions, rows, res = drive_agent_against_background_engine(srv, agent, tmp / "env")
+        assert res is not None and res.epochs >= 1
+        assert any(v > 0 for v in rows), rows
+        assert len(versions) >= 3 and versions == sorted(versions), versions
+        assert srv.algorithm.relay.forwarded >= 1 and srv.algorithm.ignored_trajectories == 0
+    finally:
+        if agent is not None:
+            agent.close()
+        srv.close(save=False)
+    assert not list((tmp / "env").rglob("*.safetensors"))  # the weight path never touched a file

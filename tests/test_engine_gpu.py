@@ -112,3 +112,38 @@ def test_vec_engine_folds_agent_uploads_into_the_batch(cuda, tmp_path, monkeypat
         agent.close()
     finally:
         srv.close(save=False)
+
+
+def test_vec_engine_two_ranks_shared_gpu_serves_a_zmq_agent(cuda, tmp_path, monkeypatch):
+    """VERDICT r3 item 2 on the GPU: a world_size=2 vec engine (two gloo ranks sharing the one
+    GPU, RRL_FORCE_DEVICE) trains in the background while a ZMQ agent's episodes are relayed to
+    rank 0 and folded into its device batch, and the models reach the agent from rank 0's
+    memory over the relay."""
+    from relayrl_prototype_amd.api.agent import RelayRLAgent
+    from relayrl_prototype_amd.api.server import TrainingServer
+    from tests.test_engine_api import drive_agent_against_background_engine
+
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv("RRL_QUIET_CONFIG", "1")
+    monkeypatch.setenv("RRL_DIST_BACKEND", "gloo")
+    monkeypatch.setenv("RRL_FORCE_DEVICE", "0")
+    cfg = json.loads(DEFAULT_CONFIG_CONTENT)
+    for k in ("training_server", "trajectory_server", "agent_listener"):
+        cfg["server"][k]["port"] = str(free_port())
+    p = tmp_path / "relayrl_config.json"
+    p.write_text(json.dumps(cfg))
+    hp = {"num_envs": 1024, "rollout_len": 16, "train_vf_iters": 4, "world_size": 2, "with_vf_baseline": True}
+    srv = TrainingServer("REINFORCE", 4, 2, 1000, env_dir=str(tmp_path / "env"), config_path=str(p),
+                         server_type="zmq", hyperparams=hp, engine="vec")
+    agent = None
+    try:
+        agent = RelayRLAgent(config_path=str(p), server_type="zmq", handshake_timeout_s=30, seed=5)
+        versions, rows, res = drive_agent_against_background_engine(srv, agent, tmp_path / "env", seconds=60.0)
+        assert res is not None and res.epochs >= 1
+        assert any(v > 0 for v in rows), rows
+        assert len(versions) >= 3 and versions == sorted(versions), versions
+    finally:
+        if agent is not None:
+            agent.close()
+        srv.close(save=False)
+    assert not list((tmp_path / "env").rglob("*.safetensors"))
