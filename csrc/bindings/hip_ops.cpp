@@ -23,12 +23,13 @@ int rrl_mlp_forward(int mode, const float* params, const float* X, int B, int D,
                     float* actc_host, int num_cu, void* stream);
 int rrl_mlp_grad_slabs(int B, int num_cu);
 int rrl_set_value_grad_mode(int mode);
+int rrl_set_value_fwd_mode(int mode);
 int rrl_set_value_grad_tune(int tune);
 void rrl_set_value_grad_stamps(void* buf);
 int rrl_mlp_grad(int head, const float* params, const float* X, int B, int D, int A, int H,
                  const float* mask, const int* act, const float* actc, const float* adv, const float* ret,
                  const float* logp_old, const float* adv_stats, float inv_B, float clip_eps, float ent_coef,
-                 float* grad_slab, float* loss_slab, int P, int num_cu, void* stream);
+                 float* grad_slab, float* loss_slab, int P, const int* nvalid, const float* inv_B_dev, int num_cu, void* stream);
 int rrl_scan_tm_parts(int N);
 int rrl_gae_scan_tm(const float* rew, const float* done, const float* val, const float* tval, float* adv,
                     float* ret, float* stats_part, float* stats_out, int K, int T, int N, float gamma,
@@ -171,7 +172,7 @@ int64_t mlp_grad_slabs(int64_t B) { return rrl_mlp_grad_slabs((int)B, num_cus())
 void mlp_grad(int64_t head, const Tensor& params, const Tensor& X, int64_t A, int64_t H, const OptT& mask,
               const OptT& act, const OptT& actc, const OptT& adv, const OptT& ret, const OptT& logp_old,
               const OptT& adv_stats, double inv_B, double clip_eps, double ent_coef, const Tensor& grad_slab,
-              const Tensor& loss_slab) {
+              const Tensor& loss_slab, const OptT& nvalid, const OptT& inv_B_dev) {
   check_dev(params, "params", at::kFloat);
   check_dev(X, "X", at::kFloat);
   TORCH_CHECK(X.dim() == 2, "X must be [B, D]");
@@ -203,9 +204,12 @@ void mlp_grad(int64_t head, const Tensor& params, const Tensor& X, int64_t A, in
   const float* lpo = fptr(logp_old, "logp_old", B);
   if (head == 2 || head == 3) TORCH_CHECK(lpo != nullptr, "logp_old required for PPO heads");
   const float* st = fptr(adv_stats, "adv_stats", 3);
+  // device-side batch shape (graph replays with a changing batch): valid rows / 1 / global rows
+  const int* nv = iptr(nvalid, "nvalid", 1);
+  const float* ibd = fptr(inv_B_dev, "inv_B_dev", 1);
   const int rc = rrl_mlp_grad((int)head, params.data_ptr<float>(), X.data_ptr<float>(), (int)B, (int)D, (int)A,
                               (int)H, m, a, ac, ad, rt, lpo, st, (float)inv_B, (float)clip_eps, (float)ent_coef,
-                              grad_slab.data_ptr<float>(), loss_slab.data_ptr<float>(), (int)P, num_cus(),
+                              grad_slab.data_ptr<float>(), loss_slab.data_ptr<float>(), (int)P, nv, ibd, num_cus(),
                               cur_stream());
   check_rc(rc, "mlp_grad");
 }
@@ -420,6 +424,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_value_grad_mode", [](int64_t mode) { return (int64_t)rrl_set_value_grad_mode((int)mode); },
         "value-MSE gradient kernel: 1 = bf16x6 weight-stationary (H 128, D <= 8), 0 = fp32 MFMA; returns the "
         "previous mode (-1 queries without changing)");
+  m.def("set_value_fwd_mode", [](int64_t mode) { return (int64_t)rrl_set_value_fwd_mode((int)mode); },
+        "value forward: 1 = bf16x6 weight-stationary split kernel (H 128, D <= 24), 0 = fp32 MFMA; returns "
+        "the previous mode (-1 queries)");
   m.def("scan_tm_parts", &scan_tm_parts);
   m.def("gae_scan_tm", &gae_scan_tm);
   m.def("scan_flat_blocks", &scan_flat_blocks);

@@ -31,6 +31,12 @@ struct GradArgs {
   int P;
   int tune = 0;      // value_grad.hip scheduling variant (set by its launcher)
   unsigned long long* stamps = nullptr;  // diagnostic stamp sums (value_grad.hip STAMP build)
+  // Device-side batch shape (graph capture with a batch that changes between replays): rows
+  // >= *nvalid are inert (no loss, zero gradient; B stays the allocated capacity the grid and
+  // the clamped loads use), and *inv_B_dev replaces inv_B.  Null = the host values.
+  const int* nvalid = nullptr;
+  const float* inv_B_dev = nullptr;
+  float* vout = nullptr;  // value forward (value_grad.hip FWD instance): V of every row
 };
 
 // Weight-stationary bf16x6 gradient kernels (value_grad.hip): value head for H = 128,
@@ -40,5 +46,7 @@ bool value_grad_split_supported(int D, int H);
 int launch_value_grad_split(const GradArgs& a, int grid, hipStream_t s);
 bool policy_grad_split_supported(int D, int H, int A, int head);
 int launch_policy_grad_split(const GradArgs& a, int head, int grid, hipStream_t s);
+// Value forward V(x) on the same weight-stationary bf16x6 layers (fp32-accurate), p.vout.
+int launch_value_fwd_split(const GradArgs& a, int grid, hipStream_t s);
 
 }  // namespace rrl

@@ -10,6 +10,7 @@
 //   MODE_GAUSS_SAMPLE / MODE_GAUSS_EVAL: continuous policy (the reference's incomplete
 //                     ContinuousPolicyNetwork, kernel.py:49-75, completed).
 #include "common.h"
+#include "grad_args.h"
 #include "heads.h"
 
 namespace rrl {
@@ -194,6 +195,18 @@ static int dispatch_mode(int mode, const FwdArgs& a, int grid, hipStream_t s) {
   return -1;
 }
 
+extern "C" int rrl_set_value_grad_mode(int mode);  // mlp_grad.hip (-1 queries)
+
+// Value forward on the bf16x6 weight-stationary kernel (value_grad.hip FWD instance, ~0.6x the
+// fp32-MFMA kernel's time at H = 128) -- 1 -- or the fp32-MFMA kernel below -- 0.  The split
+// kernel also needs the bf16x6 gradient mode (rrl_set_value_grad_mode 1).
+static int g_value_fwd_mode = 1;
+extern "C" int rrl_set_value_fwd_mode(int mode) {
+  const int old = g_value_fwd_mode;
+  if (mode == 0 || mode == 1) g_value_fwd_mode = mode;
+  return old;
+}
+
 extern "C" int rrl_mlp_forward(int mode, const float* params, const float* X, int B, int D, int A,
                                int H, const float* mask, const int* act_in, const float* actc_in,
                                int* act_out, float* actc_out, float* out0, float* out1,
@@ -205,6 +218,20 @@ extern "C" int rrl_mlp_forward(int mode, const float* params, const float* X, in
   FwdArgs a{params, X, B, D, A, H, mask, act_in, actc_in, act_out, actc_out, out0, out1, logits_out,
             (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)step, (uint32_t)(step >> 32), row_offset, gate,
             x_copy, act_host, actc_host};
+  if (mode == MODE_VALUE && gate == nullptr && x_copy == nullptr && H == 128 && D <= 24 && g_value_fwd_mode == 1 &&
+      rrl_set_value_grad_mode(-1) == 1) {
+    GradArgs g{};
+    g.params = params;
+    g.X = X;
+    g.B = B;
+    g.D = D;
+    g.A = 1;
+    g.vout = out0;
+    int sg = (B + 63) / 64;
+    const int scap = num_cu > 0 ? num_cu : 256;
+    if (sg > scap) sg = scap;
+    return launch_value_fwd_split(g, sg, (hipStream_t)stream);
+  }
   const int tiles = (B + kTileB - 1) / kTileB;
   const int waves_needed = tiles;
   int grid = (waves_needed + 3) / 4;

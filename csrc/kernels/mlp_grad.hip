@@ -155,12 +155,15 @@ __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
     for (int t = 0; t < HT; ++t) acc3v[a][t] = zero4();
   }
   const int kr1 = input_kr_last(p.D, DT);
+  // device-side batch shape (grad_args.h): rows >= Bv inert, inv_B from memory
+  const int Bv = p.nvalid ? min(*p.nvalid, p.B) : p.B;
+  const float invB = p.inv_B_dev ? *p.inv_B_dev : p.inv_B;
 
   __syncthreads();
 
-  for (int base = blockIdx.x * 64; base < p.B; base += gridDim.x * 64) {
+  for (int base = blockIdx.x * 64; base < Bv; base += gridDim.x * 64) {
     const int row0 = base + 16 * wave;
-    const int nrows = max(0, min(16, p.B - row0));
+    const int nrows = max(0, min(16, Bv - row0));
     const bool valid = j < nrows;
     const int row = row0 + j;
 
@@ -178,7 +181,7 @@ __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
       const float v = head_dot<HT>(lds + L::W3, lds[L::B3], h2);
       const float target = valid ? p.ret[row] : 0.f;
       const float diff = v - target;
-      dout[0] = valid ? 2.f * diff * p.inv_B : 0.f;
+      dout[0] = valid ? 2.f * diff * invB : 0.f;
       if (count) {
         s_loss += diff * diff;
         s_val += v;
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
         loss_i = -fminf(s1, s2);
         if (count) s_clip += (fabsf(ratio - 1.f) > p.clip_eps) ? 1.f : 0.f;
       }
-      const float scale = valid ? p.inv_B : 0.f;
+      const float scale = valid ? invB : 0.f;
 #pragma unroll
       for (int a = 0; a < kMaxAct; ++a) {
         if (a < A) {
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(256, 1) void mlp_grad_kernel(GradArgs p) {
         loss_i = -fminf(s1, s2);
         if (count) s_clip += (fabsf(ratio - 1.f) > p.clip_eps) ? 1.f : 0.f;
       }
-      const float scale = valid ? p.inv_B : 0.f;
+      const float scale = valid ? invB : 0.f;
       float ent = 0.f;
 #pragma unroll
       for (int a = 0; a < kMaxAct; ++a) {
@@ -501,10 +504,13 @@ extern "C" int rrl_mlp_grad(int head, const float* params, const float* X, int B
                             const float* mask, const int* act, const float* actc, const float* adv,
                             const float* ret, const float* logp_old, const float* adv_stats,
                             float inv_B, float clip_eps, float ent_coef, float* grad_slab,
-                            float* loss_slab, int P, int num_cu, void* stream) {
+                            float* loss_slab, int P, const int* nvalid, const float* inv_B_dev, int num_cu,
+                            void* stream) {
   if (A < 1 || A > kMaxAct || D < 1 || D > 32) return -2;
   GradArgs a{params, X, B, D, A, mask, act, actc, adv, ret, logp_old, adv_stats, inv_B, clip_eps,
              ent_coef, grad_slab, loss_slab, P};
+  a.nvalid = nvalid;
+  a.inv_B_dev = inv_B_dev;
   const int grid = rrl_mlp_grad_slabs(B, num_cu);
   hipStream_t s = (hipStream_t)stream;
   if (head == HEAD_VALUE_MSE && g_value_grad_mode == 1 && value_grad_split_supported(D, H))

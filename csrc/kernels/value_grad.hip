@@ -64,11 +64,17 @@ constexpr bool vg_red_in_image(int DP, int NA) { return vg_base_bytes(DP, NA) + 
 constexpr int vg_lds_bytes(int DP, int NA) {
   return vg_base_bytes(DP, NA) + (vg_red_in_image(DP, NA) ? 0 : vg_red_bytes(NA));
 }
-// Factored value head (DP <= 8, see the kernel): after the W2 lo image, the relu'(h2) mask of
-// the slab as bytes [64 rows][4 lane groups][4 k-chunks] (byte = 8 features) and the table
-// byte -> 8 bf16 {0, 1} [256][8] that turns a byte into a dh1 B fragment.
-constexpr bool vg_factor(int DP, int HEAD) { return HEAD == HEAD_VALUE_MSE && DP <= 8; }
-constexpr int vg_mask_bytes(int DP, int HEAD) { return vg_factor(DP, HEAD) ? 64 * 16 + 256 * 16 : 0; }
+// Factored (rank-1) heads (see the kernel): the value head (DP <= 8), and the 2-action
+// categorical policy heads, whose logit gradients sum to zero per row (dlogit0 = -dlogit1),
+// so dh2 = dlogit1 (w3[1] - w3[0]) relu'(h2) is rank 1 like the value head's.  After the W2 lo
+// image: the relu'(h2) mask of the slab as bytes [64 rows][4 lane groups][4 k-chunks] (byte =
+// 8 features) and the table byte -> 8 bf16 {0, 1} [256][8] that turns a byte into a dh1 B
+// fragment.
+constexpr bool vg_factor(int DP, int HEAD, int NA) {
+  // (the policy heads' DMA'd inputs leave room for the mask plan at DP = 4 only: CartPole)
+  return (HEAD == HEAD_VALUE_MSE && DP <= 8) || ((HEAD == HEAD_PG_CAT || HEAD == HEAD_PPO_CAT) && NA == 2 && DP <= 4);
+}
+constexpr int vg_mask_bytes(int DP, int HEAD, int NA) { return vg_factor(DP, HEAD, NA) ? 64 * 16 + 256 * 16 : 0; }
 // The slab's head inputs, DMA'd from global memory: ret, or adv / logp_old / act (actc [64][NA]
 // for a Gaussian head).  Inside the dh2 image after the head partials when those live there.
 // (Policy heads only: the value head keeps its x slab and ret prefetched in registers, which
@@ -83,28 +89,31 @@ constexpr bool vg_split_head(int HEAD, int NA) {
 }
 // (+ the per-wave db3 / dlog_std sums [8][2 NA], accumulated in LDS across the slabs)
 constexpr int vg_dtab_bytes(int HEAD, int NA) { return vg_split_head(HEAD, NA) ? (64 + 16) * NA * 4 : 0; }
-// Outside the image the head inputs are double-buffered (DMA'd a slab ahead) when LDS allows.
-constexpr bool vg_hbuf2(int DP, int HEAD, int NA) {
-  return !vg_red_in_image(DP, NA) && vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD) +
-                                             2 * vg_hbuf_bytes(HEAD, NA) + vg_dtab_bytes(HEAD, NA) <=
-                                         160 * 1024;
-}
-// Factored value head: each wave's copy of the slab's dout [8 waves][64 rows] (the wave reads
-// its own rows back as b128 / b32 LDS reads instead of 20 ds_bpermutes per slab), last in LDS.
+// Factored heads: each wave's copy of the slab's dout [8 waves][64 rows] (the wave reads its
+// own rows back as b128 / b32 LDS reads instead of 20 ds_bpermutes per slab), last in LDS.
 // (Other value heads too, where LDS allows: 4 ds_bpermutes per slab there.)
-constexpr int vg_dw_bytes(int DP, int HEAD) {
-  return (vg_factor(DP, HEAD) || (HEAD == HEAD_VALUE_MSE && vg_lds_bytes(DP, 1) + 8 * 64 * 4 <= 160 * 1024))
+constexpr int vg_dw_bytes(int DP, int HEAD, int NA) {
+  return (vg_factor(DP, HEAD, NA) || (HEAD == HEAD_VALUE_MSE && vg_lds_bytes(DP, 1) + 8 * 64 * 4 <= 160 * 1024))
              ? 8 * 64 * 4
              : 0;
 }
+// Outside the image the head inputs are double-buffered (DMA'd a slab ahead) when LDS allows.
+constexpr bool vg_hbuf2(int DP, int HEAD, int NA) {
+  return !vg_red_in_image(DP, NA) && vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD, NA) +
+                                             2 * vg_hbuf_bytes(HEAD, NA) + vg_dtab_bytes(HEAD, NA) +
+                                             vg_dw_bytes(DP, HEAD, NA) <=
+                                         160 * 1024;
+}
 constexpr int vg_total_bytes(int DP, int HEAD, int NA) {
-  return vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD) +
+  return vg_lds_bytes(DP, NA) + vg_mask_bytes(DP, HEAD, NA) +
          (vg_red_in_image(DP, NA) ? 0 : (vg_hbuf2(DP, HEAD, NA) ? 2 : 1) * vg_hbuf_bytes(HEAD, NA)) +
-         vg_dtab_bytes(HEAD, NA) + vg_dw_bytes(DP, HEAD);
+         vg_dtab_bytes(HEAD, NA) + vg_dw_bytes(DP, HEAD, NA);
 }
 static_assert(vg_red_bytes(6) + vg_hbuf_bytes(HEAD_PPO_GAUSS, 6) <= 3 * kVgImg * 2, "head inputs in the dh2 image");
 static_assert(vg_total_bytes(8, HEAD_VALUE_MSE, 1) <= 160 * 1024, "factored LDS plan");
-static_assert(vg_dw_bytes(20, HEAD_VALUE_MSE) > 0 && vg_total_bytes(20, HEAD_VALUE_MSE, 1) <= 160 * 1024,
+static_assert(vg_total_bytes(4, HEAD_PG_CAT, 2) <= 160 * 1024 && vg_total_bytes(4, HEAD_PPO_CAT, 2) <= 160 * 1024,
+              "factored binary policy LDS plan");
+static_assert(vg_dw_bytes(20, HEAD_VALUE_MSE, 1) > 0 && vg_total_bytes(20, HEAD_VALUE_MSE, 1) <= 160 * 1024,
               "dout table of the D = 17..20 value kernel");
 static_assert(vg_lds_bytes(24, 1) <= 160 * 1024 && !vg_red_in_image(24, 1), "value-grad LDS plan");
 static_assert(vg_lds_bytes(20, 6) <= 160 * 1024, "value-grad LDS plan exceeds 160 KB");
@@ -362,7 +371,9 @@ RRL_DEV float wave_sum_vl(float v) {
 // production variant per input width (DP = 8 spills 4 VGPRs with the interleave)
 constexpr int vg_prod_v(int DP) { return DP <= 4 ? 3 : 1; }
 
-template <int DP, int HEAD, int NA, bool STAMP = false, int V = vg_prod_v(DP)>
+// FWD: the value forward only (layers 1 and 2 and the head dot product on the same
+// weight-stationary bf16x6 layout, V written to p.vout; no loss, no backward, no slabs).
+template <int DP, int HEAD, int NA, bool STAMP = false, int V = vg_prod_v(DP), bool FWD = false>
 __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   unsigned long long st_prev = 0, st_sum[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_entry = 0;  // STAMP: slots 10 / 11 = prologue / epilogue cycles per workgroup
@@ -372,6 +383,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   constexpr bool kGauss = HEAD == HEAD_PG_GAUSS || HEAD == HEAD_PPO_GAUSS;
   constexpr bool kPPO = HEAD == HEAD_PPO_CAT || HEAD == HEAD_PPO_GAUSS;
   static_assert(!kValue || NA == 1, "the value head has one output");
+  static_assert(!FWD || kValue, "the forward-only instance is the value head's");
   static_assert(NA >= 1 && NA <= 6, "NA <= 6 (LDS plan, two field groups)");
   static_assert(!vg_split_head(HEAD, NA) || (NA % 2 == 0 && NA <= 6),
                 "the dout table is read in output pairs; head MFMA lanes g = 0, 1 hold outputs 0..7");
@@ -387,7 +399,10 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   //  * dW2 needs dh2' = mask * dout of the wave's OWN 16 features only (A operand): its image
   //    pieces are mask * the pieces of the row's dout (one split per row, not per element),
   //    written and read back by the same wave.
-  constexpr bool kFactor = vg_factor(DP, HEAD);
+  constexpr bool kFactor = vg_factor(DP, HEAD, NA) && !FWD;
+  // 2-action categorical heads: the factored path runs on w3' = w3[1] - w3[0] and the row
+  // scalar d' = (dlogit1 - dlogit0) / 2 (their sum is zero up to fp32 rounding of p0 + p1 = 1)
+  constexpr bool kBin = kFactor && !kValue;
   constexpr bool kMaskB = kFactor && (V & 1);
   constexpr bool kInterleave = kMaskB && (V & 2);
   constexpr int NF = NA + 2;
@@ -407,10 +422,10 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   // head inputs of the current slab: [0, 64) ret or adv, [64, 128) logp_old, [128, ..) act
   // (int bits) or actc [64][NA]
   float* hbuf0 = kRedImg ? red + 8 * NA * 64
-                         : reinterpret_cast<float*>(reinterpret_cast<char*>(mk) + vg_mask_bytes(DP, HEAD));
+                         : reinterpret_cast<float*>(reinterpret_cast<char*>(mk) + vg_mask_bytes(DP, HEAD, NA));
   // kSplitHead: the slab's dout [64 rows][NA] (outside both images: read while dh2 is stored)
   float* dtab = reinterpret_cast<float*>(
-      reinterpret_cast<char*>(mk) + vg_mask_bytes(DP, HEAD) +
+      reinterpret_cast<char*>(mk) + vg_mask_bytes(DP, HEAD, NA) +
       (kRedImg ? 0 : (vg_hbuf2(DP, HEAD, NA) ? 2 : 1) * vg_hbuf_bytes(HEAD, NA)));
   float* hacc = dtab + 64 * NA;  // kSplitHead: [8 waves][db3[NA], dlog_std[NA]]
   if (kSplitHead && lane_id() < 2 * NA) hacc[(threadIdx.x >> 6) * 2 * NA + lane_id()] = 0.f;
@@ -426,6 +441,11 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   const int l = lane_id();
   const int j = l & 15, g = l >> 4, w = threadIdx.x >> 6;
   const int D = p.D;
+  // rows >= Bv are inert (p.nvalid: a batch shape that changes between graph replays); p.B
+  // stays the allocated capacity that every clamped load is bounded by
+  const int Bv = p.nvalid ? min(*p.nvalid, p.B) : p.B;
+  const int Bc = max(Bv, 1);  // x rows past Bv load duplicates of row Bv - 1 (finite data)
+  const float invB = p.inv_B_dev ? *p.inv_B_dev : p.inv_B;
   const FlatOffsets o = flat_offsets(D, kVgH, NA);
   float adv_mean = 0.f, adv_rstd = 1.f;
   if (!kValue && p.adv_stats != nullptr) {
@@ -473,7 +493,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       // hoisted out of the slab loop into a live register
       for (int k = wu; k < DP; k += 8) {
         const int q = 64 * k + l, row = q / DP, d = q % DP;
-        const long e = (long)min(b0 + row, p.B - 1) * D + min(d, D - 1);
+        const long e = (long)min(b0 + row, Bc - 1) * D + min(d, D - 1);
         __builtin_amdgcn_global_load_lds(static_cast<const uint32_t*>(static_cast<const void*>(p.X)) + e,
                                          (__attribute__((address_space(3))) void*)(dst + 64 * k), 4, 0, 0);
       }
@@ -484,9 +504,9 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       for (int i = 0; i < (kDmaIn ? 1 : XQ); ++i) {
         const int q = min((int)threadIdx.x + 512 * i, 64 * DP - 1);
         const int rl = q / DP, d = q % DP, b = b0 + rl;
-        xr[i] = p.X[(size_t)min(b, p.B - 1) * D + min(d, D - 1)];
+        xr[i] = p.X[(size_t)min(b, Bc - 1) * D + min(d, D - 1)];
       }
-      hin_r = p.ret[min(b0 + l, p.B - 1)];
+      if (!FWD) hin_r = p.ret[min(b0 + l, p.B - 1)];
     }
   };
   constexpr bool kHb2 = kDmaIn && vg_hbuf2(DP, HEAD, NA);
@@ -561,30 +581,35 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   // hi + mid pieces in registers; the lo pieces of W2 sit in the LDS image [o][i] that both
   // fragment kinds read once per 32-wide k-chunk (b128 for wA, transposed for wB)
   Split8HM wA[4], wB[4];
+  // the factored path's w3' (value head: w3; 2-action policy: w3[1] - w3[0]), from LDS
+  auto w3f = [&](int k) { return kBin ? vecs[3 * kVgH + k] - vecs[2 * kVgH + k] : vecs[2 * kVgH + k]; };
   vbf16x8 wBl[kFactor ? 4 : 1];  // lo pieces of A' (kFactor)
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
     // wA: A[m = own + j][k = 32c + 8g + e] = W2[m][k]      (forward)
     const floatx4 a0 = *reinterpret_cast<const floatx4*>(w2s + (own + j) * kW2Ld + 32 * c + 8 * g);
     const floatx4 a1 = *reinterpret_cast<const floatx4*>(w2s + (own + j) * kW2Ld + 32 * c + 8 * g + 4);
-    floatx4 b0, b1;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      // wB: A[m = own + j][k = 32c + 8g + e] = W2[k][m]      (backward data)
-      //     (kFactor: A'[m][k] = W2[k][m] * w3[k])
-      b0[e] = w2s[(32 * c + 8 * g + e) * kW2Ld + own + j];
-      b1[e] = w2s[(32 * c + 8 * g + 4 + e) * kW2Ld + own + j];
-      if (kFactor) {
-        b0[e] *= vecs[2 * kVgH + 32 * c + 8 * g + e];
-        b1[e] *= vecs[2 * kVgH + 32 * c + 8 * g + 4 + e];
-      }
-    }
-    const Split8 sa = split8(a0, a1), sb = split8(b0, b1);
+    const Split8 sa = split8(a0, a1);
     wA[c].h = sa.h;
     wA[c].m = sa.m;
-    wB[c].h = sb.h;
-    wB[c].m = sb.m;
-    if (kFactor) wBl[c % (kFactor ? 4 : 1)] = sb.l;
+    if constexpr (!FWD) {
+      floatx4 b0, b1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // wB: A[m = own + j][k = 32c + 8g + e] = W2[k][m]      (backward data)
+        //     (kFactor: A'[m][k] = W2[k][m] * w3'[k])
+        b0[e] = w2s[(32 * c + 8 * g + e) * kW2Ld + own + j];
+        b1[e] = w2s[(32 * c + 8 * g + 4 + e) * kW2Ld + own + j];
+        if (kFactor) {
+          b0[e] *= w3f(32 * c + 8 * g + e);
+          b1[e] *= w3f(32 * c + 8 * g + 4 + e);
+        }
+      }
+      const Split8 sb = split8(b0, b1);
+      wB[c].h = sb.h;
+      wB[c].m = sb.m;
+      if (kFactor) wBl[c % (kFactor ? 4 : 1)] = sb.l;
+    }
   }
   // per C-layout row own + 4g + r (re-read from LDS where used)
   const float* b1p = vecs + own + 4 * g;
@@ -626,10 +651,17 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   float tvs[kFactor ? 16 : 1];
 #pragma unroll
   for (int e = 0; e < (kFactor ? 16 : 1); ++e) tvs[e] = 0.f;
+  // fields: 0 db2' (x w3' in the epilogue), 1 dW3 row 0, 3 dW3 row 1.  kBin: tvs[4..7] hold
+  // sum d' h2 = dW3 row 1, and row 0 is its negative
   auto fold_tvs = [&]() {
     float tf[16];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) tf[e] = kFactor ? tvs[e % (kFactor ? 16 : 1)] : 0.f;
+    for (int e = 0; e < 16; ++e) {
+      constexpr int TN = kFactor ? 16 : 1;
+      if (!kFactor) tf[e] = 0.f;
+      else if (!kBin) tf[e] = tvs[e % TN];
+      else tf[e] = e < 4 ? tvs[e % TN] : e < 8 ? -tvs[e % TN] : e < 12 ? 0.f : tvs[(e - 8) % TN];
+    }
     return reduce_scatter16(tf, j);
   };
   float s_loss = 0.f, s_val = 0.f, s_cnt = 0.f, s_ent = 0.f, s_kl = 0.f, s_clip = 0.f;
@@ -639,7 +671,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
 
   VG_STAMP(0);
   if (STAMP) st_sum[10] = st_prev - st_entry;
-  for (int base = blockIdx.x * 64; base < p.B; base += gridDim.x * 64) {
+  for (int base = blockIdx.x * 64; base < Bv; base += gridDim.x * 64) {
     VG_STAMP(0);
     // ------------------------------------------------------------ x slab (DMA'd a slab ago)
     // (double-buffered by slab parity: the next slab's DMA targets the other half)
@@ -653,7 +685,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       for (int i = 0; i < (kDmaIn ? 1 : XQ); ++i) {
         const int q = (int)threadIdx.x + 512 * i;
         const int rl = q / DP, d = q % DP;
-        if (q < 64 * DP) xs[q] = (base + rl < p.B && d < D) ? xr[i] : 0.f;
+        if (q < 64 * DP) xs[q] = (base + rl < Bv && d < D) ? xr[i] : 0.f;
       }
     }
     __syncthreads();  // x (and kHb2 head inputs) visible; the previous slab's readers are done
@@ -785,6 +817,17 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     if (kDmaIn && !kHb2) vm_wait0();  // this wave's head-input DMAs
     __syncthreads();
     VG_STAMP(5);
+    if constexpr (FWD) {
+      // V of row l (wave 0): the 8 waves' partials in the grad kernel's summation order + b3
+      if (w == 0 && base + l < Bv) {
+        const float* r = red + l;
+        p.vout[base + l] = (((r[0] + r[64]) + (r[128] + r[192])) + ((r[256] + r[320]) + (r[384] + r[448]))) + hsc[0];
+      }
+      // next slab's x into registers (nothing else of this slab is read after the barrier
+      // above; the next slab's own barriers order its LDS writes after these reads)
+      if (base + (int)gridDim.x * 64 < Bv) prefetch_x(base + gridDim.x * 64, xsb + (parity & 1) * 64 * DP);
+      continue;
+    }
     // loss head: lane l handles batch row l (every wave computes the same 64 rows; wave 0's
     // lanes count each row once in the batch statistics and the head gradient sums)
     const bool lead = w == 0;
@@ -798,7 +841,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       const int a8 = l & 7, R = 8 * w + (l >> 3);
       const bool va = a8 < NA;
       const int ac = min(a8, NA - 1);
-      const bool ok = base + R < p.B;
+      const bool ok = base + R < Bv;
       const float* rr = red + R * NA + ac;
       constexpr int S = 64 * NA;  // wave stride
       const float outv = (((rr[0] + rr[S]) + (rr[2 * S] + rr[3 * S])) + ((rr[4 * S] + rr[5 * S]) + (rr[6 * S] + rr[7 * S]))) +
@@ -830,7 +873,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
         loss_i = -fminf(s1, s2);
         if (a8 == 0 && ok) s_clip += (fabsf(ratio - 1.f) > p.clip_eps) ? 1.f : 0.f;
       }
-      const float scale = (ok && va) ? p.inv_B : 0.f;
+      const float scale = (ok && va) ? invB : 0.f;
       const float iv = istd * istd;
       const float da = scale * dlogp * d * iv;
       const float dl = scale * (dlogp * (d * d * iv - 1.f) - p.ent_coef);
@@ -851,7 +894,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       }
     } else {
       const int b = base + l;
-      const bool ok = b < p.B;
+      const bool ok = b < Bv;
       const int bc = min(b, p.B - 1);
       const float hin = kDmaIn ? hbuf[l] : hin_r;
       const float hlp = kValue ? 0.f : hbuf[64 + l];
@@ -869,7 +912,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
       if (kValue) {
         const float v = outv[0];
         const float diff = v - (ok ? hin : 0.f);
-        dout[0] = ok ? 2.f * diff * p.inv_B : 0.f;
+        dout[0] = ok ? 2.f * diff * invB : 0.f;
         if (lead && ok) {
           s_loss += diff * diff;
           s_val += v;
@@ -912,7 +955,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
           loss_i = -fminf(s1, s2);
           if (lead && ok) s_clip += (fabsf(ratio - 1.f) > p.clip_eps) ? 1.f : 0.f;
         }
-        const float scale = ok ? p.inv_B : 0.f;
+        const float scale = ok ? invB : 0.f;
 #pragma unroll
         for (int a = 0; a < NA; ++a) {
           if (kGauss) {
@@ -953,7 +996,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     // below where there is one: __syncthreads waits for every outstanding vector memory op
     // (vmcnt 0), so a DMA issued just before it would stall the slab for its HBM latency
     auto prefetch_next = [&]() {
-      if (base + (int)gridDim.x * 64 < p.B) {
+      if (base + (int)gridDim.x * 64 < Bv) {
         prefetch_x(base + gridDim.x * 64, xsb + (parity & 1) * 64 * DP);
         if (kHb2) dma_head(base + gridDim.x * 64, hbuf0 + (parity & 1) * HBF);
       }
@@ -990,20 +1033,22 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     };
     // the wave's dout table (lane l writes row l; only this wave reads it back): kMaskB and the
     // non-factored value heads
-    constexpr bool kDwTab = vg_dw_bytes(DP, HEAD) > 0 && (kMaskB || !kFactor);
+    constexpr bool kDwTab = vg_dw_bytes(DP, HEAD, NA) > 0 && (kMaskB || !kFactor);
     float* dtw = reinterpret_cast<float*>(reinterpret_cast<char*>(vg_lds) + vg_total_bytes(DP, HEAD, NA) -
-                                          vg_dw_bytes(DP, HEAD)) + 64 * w;
+                                          vg_dw_bytes(DP, HEAD, NA)) + 64 * w;
     if (kFactor) {
-      float dv[4];  // dout of C-layout row 16 bt + j (the dh2' tiles)
+      // the row scalar of the rank-1 dh2: dout (value) or (dlogit1 - dlogit0) / 2 (kBin)
+      const float dfac = kBin ? 0.5f * (dout[NA - 1] - dout[0]) : dout[0];
+      float dv[4];  // dfac of C-layout row 16 bt + j (the dh2' tiles)
       if (kMaskB) {
-        dtw[l] = dout[0];
+        dtw[l] = dfac;
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int bt = 0; bt < 4; ++bt) dv[bt] = dtw[16 * bt + j];
       } else {
 #pragma unroll
-        for (int bt = 0; bt < 4; ++bt) dv[bt] = __shfl(dout[0], 16 * bt + j, 64);
+        for (int bt = 0; bt < 4; ++bt) dv[bt] = __shfl(dfac, 16 * bt + j, 64);
       }
       float* tv = tvs;  // fields: db2' (x w3 in the epilogue), dW3 row 0 (kTvPersist: kept over slabs)
       if (!kTvPersist) {
@@ -1096,8 +1141,8 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
             if (it + 1 < 16) cur = nxt;
           }
         }
-        // per-row scale of the transposed tile (rows 16 bt + 4 g + i): dout, or dout / hi(dout)
-        float sr = dout[0];  // lane l: row l
+        // per-row scale of the transposed tile (rows 16 bt + 4 g + i): dfac, or dfac / hi(dfac)
+        float sr = dfac;  // lane l: row l
         if (!kMaskB) {
           const float vh = __uint_as_float(cvt_pk_bf16(sr, sr) << 16);
           sr = vh != 0.f ? sr * __builtin_amdgcn_rcpf(vh) : 0.f;  // 1 ulp: within fp32 accuracy
@@ -1336,11 +1381,14 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
   }
 
   // ------------------------------------------------------------------ epilogue
+  if constexpr (FWD) return;
   if (kTvPersist) accv[0] += fold_tvs();
   float* slab = p.grad_slab + (size_t)blockIdx.x * p.P;
-  floatx4 w3s;  // kFactor: dW2 rows / db2 are w3 x the accumulated dh2' sums
+  // kFactor: dW2 rows / db2 are w3' x the accumulated dh2' sums (w3' = w3, or w3[1] - w3[0])
+  auto w3g = [&](int f) { return kBin ? P[o.w3 + kVgH + f] - P[o.w3 + f] : P[o.w3 + f]; };
+  floatx4 w3s;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) w3s[r] = kFactor ? P[o.w3 + own + 4 * g + r] : 1.f;
+  for (int r = 0; r < 4; ++r) w3s[r] = kFactor ? w3g(own + 4 * g + r) : 1.f;
 #pragma unroll
   for (int it = 0; it < 8; ++it) {
 #pragma unroll
@@ -1351,7 +1399,7 @@ __global__ __launch_bounds__(512, 1) void value_grad_split_kernel(GradArgs p) {
     const int f = 4 * q + (j >> 2), feat = own + 4 * g + (j & 3);
     if (f < NF) {
       const int off = f == 0 ? o.b2 : f == 1 ? o.w3 : f == 2 ? o.b1 : o.w3 + (f == 3 ? 1 : f - 2) * kVgH;
-      if (f != 2) slab[off + feat] = (kFactor && f == 0) ? accv[q] * P[o.w3 + feat] : accv[q];
+      if (f != 2) slab[off + feat] = (kFactor && f == 0) ? accv[q] * w3g(feat) : accv[q];
     }
   }
   if (kDw1Mfma) {
@@ -1491,6 +1539,32 @@ int launch_value_grad_split(const GradArgs& a, int grid, hipStream_t s) {
   if (a.D <= 16) return launch_vg<16, HEAD_VALUE_MSE, 1>(a, grid, s);
   if (a.D <= 20) return launch_vg<20, HEAD_VALUE_MSE, 1>(a, grid, s);  // HalfCheetahSynth (D = 17)
   return launch_vg<24, HEAD_VALUE_MSE, 1>(a, grid, s);
+}
+
+template <int DP>
+static int launch_fwd(const GradArgs& a0, int grid, hipStream_t s) {
+  constexpr int bytes = vg_total_bytes(DP, HEAD_VALUE_MSE, 1);
+  static_assert(bytes <= 160 * 1024, "value-forward LDS plan exceeds 160 KB");
+  auto* kern = value_grad_split_kernel<DP, HEAD_VALUE_MSE, 1, false, vg_prod_v(DP), true>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    attr_set = true;
+  }
+  GradArgs a = a0;
+  a.tune = 0;
+  a.stamps = nullptr;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), bytes, s, a);
+  return (int)hipGetLastError();
+}
+
+int launch_value_fwd_split(const GradArgs& a, int grid, hipStream_t s) {
+  if (a.vout == nullptr) return -2;
+  if (a.D <= 4) return launch_fwd<4>(a, grid, s);
+  if (a.D <= 8) return launch_fwd<8>(a, grid, s);
+  if (a.D <= 16) return launch_fwd<16>(a, grid, s);
+  if (a.D <= 20) return launch_fwd<20>(a, grid, s);
+  return launch_fwd<24>(a, grid, s);
 }
 
 template <int HEAD, int NA>

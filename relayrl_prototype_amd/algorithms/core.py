@@ -87,12 +87,12 @@ class ValueLoop:
         # another thread synchronises on the device meanwhile, whatever that thread's mode
         self.before_capture = None
 
-    def _body(self, obs, ret, iters, inv_B, slab, ls_first, ls_last):
+    def _body(self, obs, ret, iters, inv_B, slab, ls_first, ls_last, nvalid=None, inv_B_dev=None):
         H = self.net.spec.H
         for k in range(iters):
             ls = ls_first if k == 0 else ls_last
             mlp_grad(GradHead.VALUE_MSE, self.net.params, obs, 1, H, ret=ret, inv_B=inv_B, grad_slab=slab,
-                     loss_slab=ls)
+                     loss_slab=ls, nvalid=nvalid, inv_B_dev=inv_B_dev)
             self.net.apply(slab, self.comm)
 
     def step(self, obs: torch.Tensor, ret: torch.Tensor, inv_B: float, first: bool = False):
@@ -124,12 +124,13 @@ class ValueLoop:
             self._graphs = {}
             self._key = shape_key
 
-    def run_body(self, obs: torch.Tensor, ret: torch.Tensor, iters: int, inv_B: float):
+    def run_body(self, obs: torch.Tensor, ret: torch.Tensor, iters: int, inv_B: float, nvalid=None,
+                 inv_B_dev=None):
         """The loop's launches on the current stream (inside an enclosing capture, e.g.
         PGLearner's whole-optimize graph); ``prepare`` must have run."""
-        self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last)
+        self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last, nvalid, inv_B_dev)
 
-    def run(self, obs: torch.Tensor, ret: torch.Tensor, iters: int, inv_B: float):
+    def run(self, obs: torch.Tensor, ret: torch.Tensor, iters: int, inv_B: float, nvalid=None, inv_B_dev=None):
         B = obs.shape[0]
         dev = obs.device
         if iters <= 0:
@@ -137,7 +138,8 @@ class ValueLoop:
         if dev.type != "cuda":
             # CPU oracle path: autograd + torch Adam math
             for k in range(iters):
-                g, ls = mlp_grad(GradHead.VALUE_MSE, self.net.params, obs, 1, self.net.spec.H, ret=ret, inv_B=inv_B)
+                g, ls = mlp_grad(GradHead.VALUE_MSE, self.net.params, obs, 1, self.net.spec.H, ret=ret, inv_B=inv_B,
+                                 nvalid=nvalid, inv_B_dev=inv_B_dev)
                 if k == 0:
                     self.loss_first = ls
                 self.loss_last = ls
@@ -145,10 +147,12 @@ class ValueLoop:
             return
         self.prepare(B, iters, inv_B, dev)
         if not self.use_graph:
-            self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last)
+            self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last, nvalid, inv_B_dev)
             return
         v0 = self.net.version
-        gkey = (obs.data_ptr(), ret.data_ptr())  # one graph per input buffer set (double-buffered trainers)
+        # one graph per input buffer set (double-buffered trainers, padded agent-row batches)
+        gkey = (obs.data_ptr(), ret.data_ptr(), 0 if nvalid is None else nvalid.data_ptr(),
+                0 if inv_B_dev is None else inv_B_dev.data_ptr())
         g = self._graphs.get(gkey)
         if g is None:
             if len(self._graphs) >= 4:
@@ -161,14 +165,14 @@ class ValueLoop:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                self._body(obs, ret, 1, inv_B, self._slab, self.loss_first, self.loss_last)
+                self._body(obs, ret, 1, inv_B, self._slab, self.loss_first, self.loss_last, nvalid, inv_B_dev)
             torch.cuda.current_stream().wait_stream(s)
             for dst, src in zip((self.net.params, self.net.m, self.net.v, self.net.step), saved):
                 dst.copy_(src)
             g = torch.cuda.CUDAGraph()
             # thread_local: a host rollout thread (host_trainer overlap) may issue HIP calls meanwhile
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last)
+                self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last, nvalid, inv_B_dev)
             self._graphs[gkey] = g
         g.replay()
         self.net.version = v0 + iters

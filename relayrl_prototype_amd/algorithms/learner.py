@@ -93,8 +93,12 @@ class PGLearner:
                 and self.num_minibatches == 1 and not (self.algo == "ppo" and self.target_kl is not None))
 
     def optimize(self, obs, act=None, actc=None, mask=None, adv=None, ret=None, adv_stats=None, logp_old=None,
-                 inv_B: Optional[float] = None):
+                 inv_B: Optional[float] = None, nvalid=None, inv_B_dev=None):
         """One epoch of updates on a prepared batch (adv/ret already computed).
+
+        ``nvalid`` / ``inv_B_dev`` (device scalars, grad_args.h): only the first nvalid rows
+        count and the loss scale is read from memory -- a padded batch whose valid row count
+        changes every epoch (agent rows, rollout_learn.py) replays ONE captured graph.
 
         Returns a dict of *device* tensors (loss slabs) -- call ``summarize`` to sync.
         """
@@ -102,16 +106,20 @@ class PGLearner:
         if inv_B is None:
             inv_B = 1.0 / max(B * self.comm.world, 1)
         if self.capturable():
-            return self._optimize_graph(obs, act, actc, mask, adv, ret, adv_stats, logp_old, float(inv_B))
-        return self._optimize_eager(obs, act, actc, mask, adv, ret, adv_stats, logp_old, inv_B)
+            return self._optimize_graph(obs, act, actc, mask, adv, ret, adv_stats, logp_old, float(inv_B), nvalid,
+                                        inv_B_dev)
+        if (nvalid is not None or inv_B_dev is not None) and self.num_minibatches > 1:
+            raise ValueError("a device-side row count needs the full-batch schedule (num_minibatches 1)")
+        return self._optimize_eager(obs, act, actc, mask, adv, ret, adv_stats, logp_old, inv_B, nvalid, inv_B_dev)
 
     def _nets(self):
         return [n for n in (self.pi, self.vf) if n is not None]
 
-    def _optimize_graph(self, obs, act, actc, mask, adv, ret, adv_stats, logp_old, inv_B: float):
+    def _optimize_graph(self, obs, act, actc, mask, adv, ret, adv_stats, logp_old, inv_B: float, nvalid=None,
+                        inv_B_dev=None):
         """Capture (once per input-buffer set) and replay the whole epoch of updates."""
         B = obs.shape[0]
-        args = (obs, act, actc, mask, adv, ret, adv_stats, logp_old)
+        args = (obs, act, actc, mask, adv, ret, adv_stats, logp_old, nvalid, inv_B_dev)
         key = (B, inv_B) + tuple(0 if t is None else t.data_ptr() for t in args)
         ent = self._opt_graphs.get(key)
         if ent is None:
@@ -130,7 +138,7 @@ class PGLearner:
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):
-                self._optimize_body(*args, inv_B, vf_iters=min(1, self.train_vf_iters))
+                self._optimize_body(*args, inv_B=inv_B, vf_iters=min(1, self.train_vf_iters))
             torch.cuda.current_stream(self.device).wait_stream(s)
             it = iter(state)
             for n in nets:
@@ -141,7 +149,7 @@ class PGLearner:
             g = torch.cuda.CUDAGraph()
             # thread_local: a host rollout thread (host_trainer overlap) may issue HIP calls meanwhile
             with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                last = self._optimize_body(*args, inv_B, vf_iters=self.train_vf_iters)
+                last = self._optimize_body(*args, inv_B=inv_B, vf_iters=self.train_vf_iters)
             dv = [n.version - v for n, v in zip(nets, v0)]
             for n, v in zip(nets, v0):
                 n.version = v
@@ -155,7 +163,8 @@ class PGLearner:
         self.last = dict(last)
         return self.last
 
-    def _optimize_body(self, obs, act, actc, mask, adv, ret, adv_stats, logp_old, inv_B: float, vf_iters: int):
+    def _optimize_body(self, obs, act, actc, mask, adv, ret, adv_stats, logp_old, nvalid=None, inv_B_dev=None, *,
+                       inv_B: float, vf_iters: int):
         """Full-batch epoch (no host reads): the capturable form of _optimize_eager."""
         H, A = self.hidden, self.act_dim
         slab, ls = self._slabs(obs.shape[0])
@@ -163,15 +172,16 @@ class PGLearner:
         for it in range(self.train_pi_iters):
             out = mlp_grad(self.head, self.pi.params, obs, A, H, mask=mask, act=act, actc=actc, adv=adv,
                            logp_old=logp_old, adv_stats=adv_stats, inv_B=inv_B, clip_eps=self.clip_ratio,
-                           ent_coef=self.ent_coef, grad_slab=slab, loss_slab=ls)
+                           ent_coef=self.ent_coef, grad_slab=slab, loss_slab=ls, nvalid=nvalid, inv_B_dev=inv_B_dev)
             if it == 0:
                 pi_loss = out[1].sum(0)
             self.pi.apply(out[0], self.comm)
         if self.vloop is not None and vf_iters > 0:
-            self.vloop.run_body(obs, ret, vf_iters, inv_B)
+            self.vloop.run_body(obs, ret, vf_iters, inv_B, nvalid, inv_B_dev)
         return {"pi_loss": pi_loss, "kl_stop": None}
 
-    def _optimize_eager(self, obs, act, actc, mask, adv, ret, adv_stats, logp_old, inv_B):
+    def _optimize_eager(self, obs, act, actc, mask, adv, ret, adv_stats, logp_old, inv_B, nvalid=None,
+                        inv_B_dev=None):
         B = obs.shape[0]
         H, A = self.hidden, self.act_dim
         M = self.num_minibatches
@@ -190,7 +200,8 @@ class PGLearner:
 
                 out = mlp_grad(self.head, self.pi.params, sel(obs), A, H, mask=sel(mask), act=sel(act),
                                actc=sel(actc), adv=sel(adv), logp_old=sel(logp_old), adv_stats=adv_stats, inv_B=inv,
-                               clip_eps=self.clip_ratio, ent_coef=self.ent_coef, grad_slab=slab, loss_slab=ls)
+                               clip_eps=self.clip_ratio, ent_coef=self.ent_coef, grad_slab=slab, loss_slab=ls,
+                               nvalid=nvalid, inv_B_dev=inv_B_dev)
                 if step == 0:
                     pi_loss = out[1].sum(0).clone()
                 if self.algo == "ppo" and self.target_kl is not None and step > 0:
@@ -207,7 +218,7 @@ class PGLearner:
                 break
         if self.vloop is not None and self.train_vf_iters > 0:
             if M == 1:
-                self.vloop.run(obs, ret, self.train_vf_iters, inv_B)
+                self.vloop.run(obs, ret, self.train_vf_iters, inv_B, nvalid, inv_B_dev)
             else:
                 for ep in range(self.train_vf_iters):
                     for j, idx in enumerate(self.minibatches(B)):

@@ -114,6 +114,8 @@ class FlatBuffer:
             "rew": torch.from_numpy(self.rew[sl].copy()),
             "logp": torch.from_numpy(self.logp[sl].copy()),
             "has_logp": bool(self.has_logp[sl].all()) if n else False,
+            # decided on the host, before the copy: the device batch needs no mask buffer
+            "mask_trivial": bool((self.mask[sl] == 1).all()) if n else True,
             "done": torch.from_numpy(self.done[sl].copy()),
             "boot": torch.from_numpy(self.boot[sl].copy()),
         }

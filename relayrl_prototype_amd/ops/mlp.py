@@ -174,14 +174,27 @@ def set_value_grad_mode(mode: int) -> int:
 
 def mlp_grad(head: int, params, X, A: int, H: int, mask=None, act=None, actc=None, adv=None, ret=None,
              logp_old=None, adv_stats=None, inv_B: Optional[float] = None, clip_eps: float = 0.2,
-             ent_coef: float = 0.0, grad_slab=None, loss_slab=None):
+             ent_coef: float = 0.0, grad_slab=None, loss_slab=None, nvalid=None, inv_B_dev=None):
     """Fused forward+backward.  GPU: fills grad_slab [nslab, P] and loss_slab [nslab, 8] and
-    returns them; CPU: returns (grad [1, P], loss stats [1, 8]) computed with autograd."""
+    returns them; CPU: returns (grad [1, P], loss stats [1, 8]) computed with autograd.
+
+    ``nvalid`` (int32 [1]) / ``inv_B_dev`` (fp32 [1]): the batch shape read from device memory
+    -- rows >= nvalid are inert and inv_B_dev replaces inv_B -- so a captured graph can replay
+    a batch whose valid row count changes (agent rows folded into a fixed capacity)."""
     X = X.contiguous().float()
     B = X.shape[0]
     if inv_B is None:
         inv_B = 1.0 / max(B, 1)
     h = _hip_for(X)
+    if h is None and (nvalid is not None or inv_B_dev is not None):
+        n = B if nvalid is None else int(nvalid.reshape(-1)[0])
+        ib = inv_B if inv_B_dev is None else float(inv_B_dev.reshape(-1)[0])
+
+        def cut(t):
+            return None if t is None else t[:n]
+
+        return mlp_grad(head, params, X[:n], A, H, cut(mask), cut(act), cut(actc), cut(adv), cut(ret), cut(logp_old),
+                        adv_stats, ib, clip_eps, ent_coef)
     if h is None:
         g, st = ref.mlp_grad_ref(int(head), params, X, A, H, mask, act, actc, adv, ret, logp_old, adv_stats,
                                  inv_B, clip_eps, ent_coef)
@@ -203,7 +216,10 @@ def mlp_grad(head: int, params, X, A: int, H: int, mask=None, act=None, actc=Non
         loss_slab = torch.empty(ns, 8, device=X.device)
     mask, act, actc, adv, ret, logp_old = _f32(mask), _i32(act), _f32(actc), _f32(adv), _f32(ret), _f32(logp_old)
     off = 0
-    for lo, hi in grad_chunks(B):
+    chunks = grad_chunks(B)
+    if nvalid is not None and len(chunks) > 1:
+        raise ValueError("a device-side row count needs a single-launch batch (< 2^25 rows)")
+    for lo, hi in chunks:
         whole = lo == 0 and hi == B
 
         def rows(t):
@@ -212,7 +228,7 @@ def mlp_grad(head: int, params, X, A: int, H: int, mask=None, act=None, actc=Non
         n = int(h.mlp_grad_slabs(hi - lo))
         h.mlp_grad(int(head), params, rows(X), A, H, rows(mask), rows(act), rows(actc), rows(adv), rows(ret),
                    rows(logp_old), adv_stats, float(inv_B), float(clip_eps), float(ent_coef), grad_slab[off:off + n],
-                   loss_slab[off:off + n])
+                   loss_slab[off:off + n], nvalid, inv_B_dev)
         off += n
     return grad_slab[:ns], loss_slab[:ns]
 

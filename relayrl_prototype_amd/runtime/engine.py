@@ -164,8 +164,12 @@ class EngineAlgorithm(AlgorithmAbstract):
         lr = self.learner
         self.agent_rows = (bool(spec.trainer.get("agent_rows", True)) and spec.kind in ("vec", "host")
                            and lr is not None and hasattr(self.trainer, "rl"))
+        if self.agent_rows:
+            # padded device-side batch shape: epochs with uploads replay a captured graph
+            self.trainer.rl.agent_rows_enabled = True
+            self.trainer.rl.agent_cap = int(spec.trainer.get("agent_rows_cap", agent_buf_size))
         if self.agent_rows and self.comm is not None and self.comm.multi:
-            self.trainer.rl.count_sync = True
+            self.trainer.rl.count_sync = True  # fallback (non-capturable learners): host row count
         self.agent_rows_total = 0
         self.agent_episodes = 0
         self.agent_trajectories = 0

@@ -38,8 +38,16 @@ class RolloutLearner:
         self.pending_rows = None
         self.last_agent_rows = 0
         # several ranks with uploads staged on one of them (runtime/engine.py): agree on the
-        # global row count each epoch (see learn)
+        # global row count each epoch (see learn; the fallback of the padded path below)
         self.count_sync = False
+        # agent rows on a capturable learner: ONE padded batch [B + agent_cap] whose valid row
+        # count (nvalid) and loss scale (1 / global rows, from the all-reduced statistics) live
+        # on the device, so epochs with uploads replay a captured graph too
+        self.agent_rows_enabled = False
+        self.agent_cap = 0
+        self._pad = None
+        self._nvalid = None
+        self._inv_dev = None
         if dev.type == "cuda":
             from ..ops import hip
 
@@ -91,10 +99,15 @@ class RolloutLearner:
         ac = None if discrete else act.reshape(B, -1)
         m = None if mask is None else mask.reshape(B, -1)
         adv_b, ret_b, logp_b = self.adv.view(-1), self.ret.view(-1), logp.reshape(-1)
-        if folded is not None:
-            obs_b, a, ac, m, adv_b, ret_b, logp_b = self._fold_cat(folded, obs_b, a, ac, m, adv_b, ret_b, logp_b)
         B = obs_b.shape[0]
         any_rows = self.last_agent_rows > 0
+        if self._device_shape_ok(folded):
+            self._optimize_padded(folded, obs_b, a, ac, m, adv_b, ret_b, logp_b)
+            return
+        if folded is not None:
+            obs_b, a, ac, m, adv_b, ret_b, logp_b = self._fold_cat(folded, obs_b, a, ac, m, adv_b, ret_b, logp_b)
+            B = obs_b.shape[0]
+            any_rows = True
         if self.count_sync:
             # several ranks, uploads staged on rank 0 only: the global row count (all-reduced
             # statistics) sets the loss scale on every rank, and every rank goes eager when
@@ -149,6 +162,80 @@ class RolloutLearner:
                                  act_in=d["act"] if lr.discrete else None,
                                  actc_in=None if lr.discrete else d["act"])["logp"]
         return dict(d, obs=obs_e, adv=adv_e, ret=ret_e, logp=logp_e)
+
+    # ------------------------------------------------------------------ padded agent rows
+    def _device_shape_ok(self, folded) -> bool:
+        """Agent rows enabled, a capturable learner on the GPU, and this epoch's uploads (if
+        any) fit the padded capacity."""
+        lr = self.learner
+        if not (self.agent_rows_enabled and self.agent_cap > 0 and lr.device.type == "cuda" and lr.capturable()):
+            return False
+        return folded is None or folded["obs"].shape[0] <= self.agent_cap
+
+    def _pad_buffers(self, B, D, A, dev):
+        lr = self.learner
+        C = self.agent_cap
+        cap = B + C
+        p = {"obs": torch.zeros(cap, D, device=dev), "adv": torch.zeros(cap, device=dev),
+             "ret": torch.zeros(cap, device=dev), "logp": torch.zeros(cap, device=dev),
+             "mask": torch.ones(cap, A, device=dev) if lr.discrete else None}
+        p["act"] = torch.zeros(cap, dtype=torch.int32, device=dev) if lr.discrete else torch.zeros(cap, A, device=dev)
+        self._pad = p
+        self._nvalid = torch.zeros(1, dtype=torch.int32, device=dev)
+        return p
+
+    def _optimize_padded(self, folded, obs_b, a, ac, m, adv_b, ret_b, logp_b):
+        """Replayable epoch: the loss scale 1 / (global rows) is computed on the device from the
+        all-reduced statistics (identical on every rank); with uploads, the batch and the rows are
+        copied into the padded buffers and only the first nvalid rows count."""
+        lr = self.learner
+        dev = lr.device
+        B = obs_b.shape[0]
+        if folded is None and not self.comm.multi:
+            # one rank, no uploads: the host scale 1 / B is exact (no device scalar needed)
+            with self.timer.phase("Optimize"):
+                lr.optimize(obs_b, act=a, actc=ac, mask=m, adv=adv_b, ret=ret_b, adv_stats=self.adv_stats,
+                            logp_old=logp_b, inv_B=1.0 / B)
+            return
+        if self._inv_dev is None:
+            self._inv_dev = torch.zeros(1, device=dev)
+        torch.reciprocal(self.adv_stats[2:3], out=self._inv_dev)
+        with self.timer.phase("Optimize"):
+            if folded is None:
+                lr.optimize(obs_b, act=a, actc=ac, mask=m, adv=adv_b, ret=ret_b, adv_stats=self.adv_stats,
+                            logp_old=logp_b, inv_B=1.0 / (B * self.comm.world), inv_B_dev=self._inv_dev)
+                return
+            n = folded["obs"].shape[0]
+            D = obs_b.shape[1]
+            A = lr.act_dim
+            p = self._pad
+            if p is None or p["obs"].shape[0] != B + self.agent_cap or p["obs"].shape[1] != D:
+                p = self._pad_buffers(B, D, A, dev)
+            p["obs"][:B].copy_(obs_b)
+            p["obs"][B:B + n].copy_(folded["obs"])
+            for k, main, up in (("adv", adv_b, folded["adv"]), ("ret", ret_b, folded["ret"]),
+                                ("logp", logp_b, folded["logp"].reshape(-1))):
+                p[k][:B].copy_(main)
+                p[k][B:B + n].copy_(up)
+            if lr.discrete:
+                p["act"][:B].copy_(a)
+                p["act"][B:B + n].copy_(folded["act"].reshape(-1).to(torch.int32))
+            else:
+                p["act"][:B].copy_(ac)
+                p["act"][B:B + n].copy_(folded["act"].reshape(n, -1))
+            use_mask = lr.discrete and (m is not None or not folded.get("mask_trivial", False))
+            if use_mask:
+                if m is not None:
+                    p["mask"][:B].copy_(m)
+                else:
+                    p["mask"][:B].fill_(1.0)
+                p["mask"][B:B + n].copy_(folded["mask"])
+            self._nvalid.fill_(B + n)
+            self.last_agent_rows = n
+            lr.optimize(p["obs"], act=p["act"] if lr.discrete else None, actc=None if lr.discrete else p["act"],
+                        mask=p["mask"] if use_mask else None, adv=p["adv"], ret=p["ret"], adv_stats=self.adv_stats,
+                        logp_old=p["logp"], inv_B=1.0 / ((B + self.agent_cap) * self.comm.world), nvalid=self._nvalid,
+                        inv_B_dev=self._inv_dev)
 
     def _fold_cat(self, e, obs_b, a, ac, m, adv_b, ret_b, logp_b):
         """The scanned uploads appended to the device batch as extra rows: one concatenated

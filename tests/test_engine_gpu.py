@@ -147,3 +147,49 @@ def test_vec_engine_two_ranks_shared_gpu_serves_a_zmq_agent(cuda, tmp_path, monk
             agent.close()
         srv.close(save=False)
     assert not list((tmp_path / "env").rglob("*.safetensors"))
+
+
+def test_agent_rows_replay_a_captured_graph(cuda, tmp_path):
+    """epochs with folded agent rows replay a captured graph (padded batch,
+    device-side row count and loss scale, grad_args.h) and train the same weights as the eager
+    concatenated batch, within fp32 summation order; AgentRows stays exact."""
+    import torch
+
+    from relayrl_prototype_amd.runtime.engine import EngineAlgorithm, EngineSpec
+    from relayrl_prototype_amd.types import TrajectoryColumns
+
+    rng = np.random.default_rng(0)
+
+    def episode(n):
+        obs = rng.normal(size=(n, 4)).astype(np.float32) * 0.1
+        act = rng.integers(0, 2, size=(n, 1)).astype(np.int32)
+        rew = np.ones(n, np.float32)
+        done = np.zeros(n, np.uint8)
+        done[-1] = 1
+        logp = np.full(n, -0.69, np.float32)
+        return TrajectoryColumns(obs, act, rew, done, None, logp, "agent-0", 0)
+
+    uploads = {1: [episode(37), episode(12)], 2: [], 3: [episode(150)], 4: [episode(5), episode(60), episode(8)]}
+    res = {}
+    for graphs in (False, True):
+        spec = EngineSpec("vec", "CartPole-v1", "reinforce", 1,
+                          {"env": "CartPole-v1", "algo": "reinforce", "num_envs": 256, "rollout_len": 16,
+                           "train_vf_iters": 5, "use_graphs": graphs, "seed": 3, "with_baseline": True})
+        algo = EngineAlgorithm(spec, str(tmp_path / f"g{int(graphs)}"), device=cuda, log=False, agent_buf_size=512)
+        rows, replays = [], []
+        for ep in range(5):
+            for t in uploads.get(ep, []):
+                algo.receive_trajectory(t)
+            r0 = algo.learner.graph_replays
+            algo.train_model()
+            rows.append(int(algo.trainer.rl.last_agent_rows))
+            replays.append(algo.learner.graph_replays - r0)
+        torch.cuda.synchronize()
+        res[graphs] = (algo.learner.pi.params.cpu().clone(), algo.learner.vf.params.cpu().clone(), rows, replays,
+                       algo.trainer.rl._pad is not None)
+    e, g = res[False], res[True]
+    assert e[2] == g[2] == [0, 49, 0, 150, 73]
+    assert g[3] == [1, 1, 1, 1, 1] and e[3] == [0, 0, 0, 0, 0]  # every graph-run epoch replayed a graph
+    assert g[4] and not e[4]
+    torch.testing.assert_close(g[0], e[0], rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(g[1], e[1], rtol=2e-5, atol=2e-6)

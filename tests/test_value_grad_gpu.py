@@ -337,3 +337,115 @@ def test_gaussian_split_kernel_matches_oracle(cuda, head, D, B, A):
     assert int(ls[5].item()) == B and int(lf[5].item()) == B
     for k, name in ((0, "loss"), (1, "entropy"), (2, "kl"), (3, "clipfrac")):
         assert abs(ls[k].item() - lf[k].item()) <= 1e-4 * max(1.0, abs(lf[k].item())), (name, ls[k], lf[k])
+
+
+def _v64(params, X, D, H):
+    p = params.double()
+    o = 0
+    W1 = p[o:o + H * D].view(H, D); o += H * D
+    b1 = p[o:o + H]; o += H
+    W2 = p[o:o + H * H].view(H, H); o += H * H
+    b2 = p[o:o + H]; o += H
+    W3 = p[o:o + H].view(1, H); o += H
+    b3 = p[o:o + 1]
+    return (torch.relu(torch.relu(X.double() @ W1.T + b1) @ W2.T + b2) @ W3.T + b3)[:, 0]
+
+
+@pytest.mark.parametrize("D,B", [(4, 1), (4, 63), (4, 70001), (8, 33000), (3, 777), (17, 20000), (24, 4097)])
+def test_value_forward_split_matches_float64(cuda, D, B):
+    """The value forward on the bf16x6 weight-stationary kernel (value_grad.hip FWD instance)
+    is fp32-accurate: against float64 no worse than twice the fp32-MFMA forward's error."""
+    from relayrl_prototype_amd.ops import FwdMode, hip, mlp_forward
+
+    H = 128
+    g = torch.Generator().manual_seed(D * 7 + B)
+    pp = MLPSpec(D, H, 1, False).init(g)
+    pp = pp + 0.05 * torch.randn(pp.shape, generator=g)
+    X = torch.randn(B, D, generator=g) * 1.5
+    v64 = _v64(pp, X, D, H)
+    out = {}
+    for mode in (1, 0):
+        old = hip().set_value_fwd_mode(mode)
+        try:
+            out[mode] = mlp_forward(FwdMode.VALUE, pp.to(cuda), X.to(cuda), 1, H)["v"].double().cpu().reshape(-1)
+        finally:
+            hip().set_value_fwd_mode(old)
+    scale = max(v64.abs().max().item(), 1e-3)
+    err_split = (out[1] - v64).abs().max().item() / scale
+    err_fp32 = (out[0] - v64).abs().max().item() / scale
+    assert err_fp32 < 1e-5, err_fp32
+    assert err_split < 1e-5 and err_split <= 2.0 * err_fp32 + 2e-7, (err_split, err_fp32)
+
+
+def test_value_forward_mode_switch(cuda):
+    from relayrl_prototype_amd.ops import hip
+
+    old = hip().set_value_fwd_mode(-1)
+    assert old in (0, 1)
+    assert hip().set_value_fwd_mode(0) == old
+    assert hip().set_value_fwd_mode(old) == 0
+
+
+@pytest.mark.parametrize("head", ["VALUE_MSE", "PG_CAT", "PPO_CAT"])
+@pytest.mark.parametrize("D,A", [(4, 2), (8, 4)])
+def test_device_row_count_matches_a_cut_batch(cuda, head, D, A):
+    """grad_args.h nvalid / inv_B_dev: a capacity batch whose rows >= nvalid hold garbage (NaN)
+    gives the gradient of the first nvalid rows with the device inv_B (graph replays with a
+    changing agent-row count, rollout_learn.py)."""
+    H = 128
+    hd = getattr(GradHead, head)
+    Aeff = 1 if head == "VALUE_MSE" else A
+    g = torch.Generator().manual_seed(D * 131 + A)
+    pp = MLPSpec(D, H, Aeff, False).init(g)
+    pp = (pp + 0.05 * torch.randn(pp.shape, generator=g)).to(cuda)
+    cap, n = 9000, 5123
+    X = torch.randn(cap, D, generator=g).to(cuda)
+    X[n:] = float("nan")
+    ret = (torch.randn(cap, generator=g) * 5).to(cuda)
+    adv = torch.randn(cap, generator=g).to(cuda)
+    act = torch.randint(0, A, (cap,), generator=g, dtype=torch.int32).to(cuda)
+    lpo = (-torch.rand(cap, generator=g)).to(cuda)
+    stats = torch.tensor([adv[:n].sum().item(), (adv[:n] ** 2).sum().item(), float(n)], device=cuda)
+    kw = dict(ret=ret, adv=adv, act=act, logp_old=lpo, adv_stats=stats, mask=None, ent_coef=0.01)
+    if head == "VALUE_MSE":
+        kw = dict(ret=ret)
+    nv = torch.tensor([n], dtype=torch.int32, device=cuda)
+    ibd = torch.tensor([1.0 / 7777.0], device=cuda)
+    old = set_value_grad_mode(1)
+    try:
+        s_dev, l_dev = mlp_grad(hd, pp, X, A, H, inv_B=0.5, nvalid=nv, inv_B_dev=ibd, **kw)
+        s_dev = s_dev.sum(0, dtype=torch.float64)
+        l_dev = l_dev.sum(0)
+        cut = {k: (v[:n] if (torch.is_tensor(v) and k != "adv_stats") else v) for k, v in kw.items()}
+        s_ref, l_ref = mlp_grad(hd, pp, X[:n], A, H, inv_B=1.0 / 7777.0, **cut)
+        s_ref = s_ref.sum(0, dtype=torch.float64)
+        l_ref = l_ref.sum(0)
+        torch.cuda.synchronize()
+    finally:
+        set_value_grad_mode(old)
+    assert torch.isfinite(s_dev).all()
+    scale = s_ref.abs().max().item()
+    assert (s_dev - s_ref).abs().max().item() <= 1e-6 * scale, (s_dev - s_ref).abs().max().item() / scale
+    assert int(l_dev[5].item()) == n
+    assert abs(l_dev[0].item() - l_ref[0].item()) <= 1e-5 * max(1.0, abs(l_ref[0].item()))
+
+
+def test_binary_policy_head_factored_is_deterministic(cuda):
+    """The 2-action categorical head on the rank-1 factored path (dlogit0 = -dlogit1) gives
+    bitwise identical slabs across launches."""
+    H, D, A, B = 128, 4, 2, 40000
+    g = torch.Generator().manual_seed(99)
+    pp = (MLPSpec(D, H, A, False).init(g) + 0.05 * torch.randn(MLPSpec(D, H, A, False).P, generator=g)).to(cuda)
+    X = torch.randn(B, D, generator=g).to(cuda)
+    act = torch.randint(0, A, (B,), generator=g, dtype=torch.int32).to(cuda)
+    adv = torch.randn(B, generator=g).to(cuda)
+    stats = torch.tensor([adv.sum().item(), (adv * adv).sum().item(), float(B)], device=cuda)
+    old = set_value_grad_mode(1)
+    try:
+        ref, _ = mlp_grad(GradHead.PG_CAT, pp, X, A, H, act=act, adv=adv, adv_stats=stats)
+        ref = ref.clone()
+        for _ in range(5):
+            s, _ = mlp_grad(GradHead.PG_CAT, pp, X, A, H, act=act, adv=adv, adv_stats=stats)
+            assert torch.equal(s, ref)
+    finally:
+        set_value_grad_mode(old)

@@ -146,6 +146,9 @@ def main():
         us = timeit(lambda: mlp_forward(FwdMode.VALUE, pv, X, 1, H, out=out), a.iters)
         res["value_fwd_us"] = us
         res["value_fwd_TFLOPs"] = 2 * (D * H + H * H + H) * B / us / 1e6
+        old = hip().set_value_fwd_mode(0)  # the fp32-MFMA forward, for comparison
+        res["value_fwd_fp32mfma_us"] = timeit(lambda: mlp_forward(FwdMode.VALUE, pv, X, 1, H, out=out), a.iters)
+        hip().set_value_fwd_mode(old)
     if a.which in ("adam", "all"):
         ns = hip().mlp_grad_slabs(B)
         slab = torch.randn(ns, pv.numel(), device=dev) * 1e-3
