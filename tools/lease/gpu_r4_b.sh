@@ -12,3 +12,7 @@ tail -3 gpurun_out/gpu_tests.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python3 bench.py --steps 10 --warmup 3 --host-steps 0 --pong-steps 0 --ref-cpu-seconds 0 > gpurun_out/bench_quick.json 2> gpurun_out/bench_quick.err || { tail -20 gpurun_out/bench_quick.err; exit 1; }
 cut -c1-300 gpurun_out/bench_quick.json
+mkdir -p gpurun_out/prof_pong
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_pong -o run -- \
+  python3 benchmarks/pong_a2c_bench.py --num-envs 2048 --steps 40 --warmup 3 > gpurun_out/prof_pong/log.txt 2>&1 && echo PROF_OK
