@@ -308,6 +308,232 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
   }
 }
 
+// Co-tile PAIR split of the same stack (selected at run time, rrl_set_conv_stack_mode): the
+// stack is LDS-read bound -- every 16x16x32 MFMA above re-reads a 1 KiB activation fragment
+// (ds_read_b128, 4 LDS cycles at 256 B/clk/CU, ~1.6-2x with the tap-shifted rows' bank
+// conflicts) while four SIMDs issue one MFMA per 16 cycles each.  Here each conv2 / conv3
+// activation fragment feeds TWO MFMAs (two co tiles per wave), which halves those reads:
+//   waves 0-3 ("A")  conv1 co tile 0, pixel tiles w + 4 t        (W1 half: 32 VGPRs)
+//                    conv2 co tiles 2 (w & 1) + {0, 1}, pixel tiles 3 (w >> 1) + {0, 1, 2}
+//                    (W2 pair: 128 VGPRs)
+//   waves 4-7 ("B")  conv1 co tile 1, pixel tiles (w - 4) + 4 t  (W1 half: 32 VGPRs)
+//                    conv3 co tiles 2 (w & 1) + {0, 1}, pixel tiles 2 ((w - 4) >> 1) + {0, 1}
+//                    of frame j - 1 (W3 pair: 144 VGPRs)
+// conv1's fragments now feed one MFMA each (400 reads per frame instead of 200), conv2's and
+// conv3's half as many as before (192 + 144 instead of 384 + 288): 736 reads per frame vs
+// 872, and the B2 -> B0 phase -- where conv2 and conv3 run side by side -- drops from ~5.1k
+// LDS cycles (over its 2.7k MFMA cycles) to its MFMA floor.  Same LDS plan, same barriers,
+// same k-step orders (outputs equal the default split's up to fma contraction).
+#ifndef C1MT
+#define C1MT 3  // conv1 pixel tiles per accumulator batch (register budget of the pair split)
+#endif
+__global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_pair_kernel(
+    const uint8_t* __restrict__ x, const uint16_t* __restrict__ w1, const float* __restrict__ b1,
+    const uint16_t* __restrict__ w2, const float* __restrict__ b2, const uint16_t* __restrict__ w3,
+    const float* __restrict__ b3, uint16_t* __restrict__ y1, uint16_t* __restrict__ y2,
+    uint16_t* __restrict__ y3, int N) {
+  using namespace cs;
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  uint16_t* Xi = smem + kXi;
+  uint16_t* A1 = smem + kA1;
+  uint16_t* A3 = smem + kA3;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i = lane & 15, g = lane >> 4;
+  const bool role_a = wave < 4;
+  const int wl = wave & 3;
+  const int c1 = role_a ? 0 : 1;     // conv1 co tile of this wave
+  const int cp = 2 * (wave & 1);     // first co tile of this wave's conv2 / conv3 pair
+  const int pt0 = role_a ? 3 * (wl >> 1) : 2 * (wl >> 1);  // first pixel tile of conv2 / conv3
+
+  bf16x8_t f1[8], fw[2][18];
+#pragma unroll
+  for (int ks = 0; ks < 8; ++ks) f1[ks] = *reinterpret_cast<const bf16x8_t*>(w1 + (16 * c1 + i) * 256 + 32 * ks + 8 * g);
+  if (role_a) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks)
+        fw[c][ks] = *reinterpret_cast<const bf16x8_t*>(w2 + (16 * (cp + c) + i) * 512 + 32 * ks + 8 * g);
+      fw[c][16] = fw[c][17] = fw[c][0];
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+#pragma unroll
+      for (int ks = 0; ks < 18; ++ks)
+        fw[c][ks] = *reinterpret_cast<const bf16x8_t*>(w3 + (16 * (cp + c) + i) * 576 + 32 * ks + 8 * g);
+    }
+  }
+  const float* b23 = role_a ? b2 : b3;
+
+  const int G = gridDim.x, n0 = blockIdx.x;
+  uint4 rx[kXPerT];
+  auto gload = [&](size_t n) {
+    const uint4* xs = reinterpret_cast<const uint4*>(x + n * (kFrameRows * 64));
+#pragma unroll
+    for (int k = 0; k < kXPerT; ++k) {
+      const int q = tid + kThreads * k;
+      rx[k] = q < kXChunks ? xs[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (n0 < N) gload(n0);
+  for (int j = 0; n0 + (j - 2) * G < N; ++j) {
+    const int n = n0 + j * G;
+    const bool cur = n < N;
+    const bool prev = j >= 1 && n - G < N;
+    __syncthreads();  // B0
+    if (cur) {
+#pragma unroll
+      for (int k = 0; k < kXPerT; ++k) {
+        const int q = tid + kThreads * k;
+        if (q < kXChunks) {
+          uint16_t* d = Xi + (q >> 2) * kFrameLd + (q & 3) * 16;
+          *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(rx[k].x, rx[k].y));
+          *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(rx[k].z, rx[k].w));
+        }
+      }
+      if (n + G < N) gload((size_t)n + G);
+    }
+    __syncthreads();  // B1
+    if (prev) {
+      const uint16_t* A2p = smem + kA2 + ((j - 1) & 1) * 81 * kA2Ld;
+      uint4* yd = reinterpret_cast<uint4*>(y2 + (size_t)(n - G) * 81 * 64);
+      for (int q = tid; q < 81 * 8; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A2p + (q >> 3) * kA2Ld + (q & 7) * 8);
+    }
+    if (j >= 2) {
+      uint4* yd = reinterpret_cast<uint4*>(y3 + (size_t)(n - 2 * G) * 49 * 64);
+      for (int q = tid; q < 49 * 8; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A3 + (q >> 3) * kA2Ld + (q & 7) * 8);
+    }
+    // ---- conv1(n): co tile c1, pixel tiles wl + 4 t (7 on wl = 0, else 6), two batches
+    if (cur) {
+      const f32x4_t bias1 = *reinterpret_cast<const f32x4_t*>(b1 + 16 * c1 + 4 * g);
+#pragma unroll
+      for (int bb = 0; bb < 3; ++bb) {
+        constexpr int MT = C1MT;
+        f32x4_t acc[MT];
+        int r0[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          const int p = 16 * min(wl + 4 * (MT * bb + t), 24) + i;
+          r0[t] = (p / 20) * 21 + p % 20;
+        }
+        // tiles wl + 4 (MT bb + t) < 25: 7 on wave 0 of the role, else 6 (wave-uniform)
+        const int ntot = wl == 0 ? 7 : 6;
+        const int nt = min(MT, ntot - MT * bb);
+        if (nt <= 0) break;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          const int tap = ks >> 1;
+          const int off = ((tap >> 1) * 21 + (tap & 1)) * kFrameLd + 32 * (ks & 1) + 8 * g;
+          bf16x8_t a[MT];
+#pragma unroll
+          for (int t = 0; t < MT; ++t)
+            if (t < nt) a[t] = *reinterpret_cast<const bf16x8_t*>(Xi + r0[t] * kFrameLd + off);
+#pragma unroll
+          for (int t = 0; t < MT; ++t)
+            if (t < nt) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[ks], a[t], acc[t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+          if (t < nt) {
+            const int mt = wl + 4 * (MT * bb + t);
+            store4_bf16(A1 + (16 * mt + i) * kA1Ld + 16 * c1 + 4 * g, fmaxf(kU8Scale * acc[t][0] + bias1[0], 0.f),
+                        fmaxf(kU8Scale * acc[t][1] + bias1[1], 0.f), fmaxf(kU8Scale * acc[t][2] + bias1[2], 0.f),
+                        fmaxf(kU8Scale * acc[t][3] + bias1[3], 0.f));
+          }
+      }
+    }
+    __syncthreads();  // B2: a1(n) complete
+    if (cur) {
+      uint4* yd = reinterpret_cast<uint4*>(y1 + (size_t)n * 400 * 32);
+      for (int q = tid; q < 400 * 4; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A1 + (q >> 2) * kA1Ld + (q & 3) * 8);
+    }
+    if (role_a) {
+      // ---- conv2(n): co tiles cp, cp + 1 over pixel tiles pt0 .. pt0 + 2
+      if (cur) {
+        uint16_t* A2c = smem + kA2 + (j & 1) * 81 * kA2Ld;
+        constexpr int MT = 3;
+        f32x4_t acc[2][MT];
+        int r0[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          acc[0][t] = acc[1][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          const int p = 16 * (pt0 + t) + i;
+          const int pc = p < 81 ? p : 0;
+          const int oh = pc / 9, ow = pc - oh * 9;
+          r0[t] = 2 * oh * 20 + 2 * ow;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) {
+          const int off = ((ks >> 2) * 20 + (ks & 3)) * kA1Ld + 8 * g;
+          bf16x8_t a[MT];
+#pragma unroll
+          for (int t = 0; t < MT; ++t) a[t] = *reinterpret_cast<const bf16x8_t*>(A1 + r0[t] * kA1Ld + off);
+#pragma unroll
+          for (int t = 0; t < MT; ++t) {
+            acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[0][ks], a[t], acc[0][t], 0, 0, 0);
+            acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[1][ks], a[t], acc[1][t], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const f32x4_t bias = *reinterpret_cast<const f32x4_t*>(b23 + 16 * (cp + c) + 4 * g);
+#pragma unroll
+          for (int t = 0; t < MT; ++t) {
+            const int p = 16 * (pt0 + t) + i;
+            if (p < 81)
+              store4_bf16(A2c + p * kA2Ld + 16 * (cp + c) + 4 * g, fmaxf(acc[c][t][0] + bias[0], 0.f),
+                          fmaxf(acc[c][t][1] + bias[1], 0.f), fmaxf(acc[c][t][2] + bias[2], 0.f),
+                          fmaxf(acc[c][t][3] + bias[3], 0.f));
+          }
+        }
+      }
+    } else if (prev) {
+      // ---- conv3(n - G): co tiles cp, cp + 1 over pixel tiles pt0, pt0 + 1
+      const uint16_t* A2p = smem + kA2 + ((j - 1) & 1) * 81 * kA2Ld;
+      constexpr int MT = 2;
+      f32x4_t acc[2][MT];
+      int r0[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        acc[0][t] = acc[1][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        const int p = 16 * (pt0 + t) + i;
+        const int pc = p < 49 ? p : 0;
+        const int oh = pc / 7, ow = pc - oh * 7;
+        r0[t] = oh * 9 + ow;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 18; ++ks) {
+        const int tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
+        const int off = (kh * 9 + kw) * kA2Ld + 32 * (ks & 1) + 8 * g;
+        bf16x8_t a[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) a[t] = *reinterpret_cast<const bf16x8_t*>(A2p + r0[t] * kA2Ld + off);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[0][ks], a[t], acc[0][t], 0, 0, 0);
+          acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[1][ks], a[t], acc[1][t], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const f32x4_t bias = *reinterpret_cast<const f32x4_t*>(b23 + 16 * (cp + c) + 4 * g);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          const int p = 16 * (pt0 + t) + i;
+          if (p < 49)
+            store4_bf16(A3 + p * kA2Ld + 16 * (cp + c) + 4 * g, fmaxf(acc[c][t][0] + bias[0], 0.f),
+                        fmaxf(acc[c][t][1] + bias[1], 0.f), fmaxf(acc[c][t][2] + bias[2], 0.f),
+                        fmaxf(acc[c][t][3] + bias[3], 0.f));
+        }
+      }
+    }
+  }
+}
+
+static int g_conv_stack_mode = 1;  // 1: co-tile pair split (default), 0: the per-layer split above
+
 }  // namespace rrl
 
 using namespace rrl;
@@ -329,11 +555,30 @@ static int launch_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const flo
   return (int)hipGetLastError();
 }
 
+extern "C" int rrl_set_conv_stack_mode(int mode) {
+  const int old = g_conv_stack_mode;
+  if (mode == 0 || mode == 1) g_conv_stack_mode = mode;
+  return old;
+}
+
 extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
                                   const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
                                   uint16_t* y3, int N, int max_grid, void* stream) {
   // max_grid < 0: timing probe variant -max_grid >> 16 (tools/cnn_kbench.py), grid = -max_grid & 0xffff
   hipStream_t st = (hipStream_t)stream;
+  if (max_grid >= 0 && g_conv_stack_mode == 1) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)conv_stack_fwd_pair_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                cs::kLds);
+      attr = true;
+    }
+    if (N < 1) return 0;
+    const int grid = N < max_grid ? N : max_grid;
+    hipLaunchKernelGGL(conv_stack_fwd_pair_kernel, dim3(grid), dim3(cs::kThreads), cs::kLds, st, x, w1, b1, w2, b2, w3,
+                       b3, y1, y2, y3, N);
+    return (int)hipGetLastError();
+  }
   if (max_grid >= 0) return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, max_grid, st);
   const int probe = (-max_grid) >> 16, g = (-max_grid) & 0xffff;
   switch (probe) {

@@ -213,6 +213,9 @@ def test_reference_wire_trains_against_our_server(tmp_path, monkeypatch):
                 if done[0] > 0:
                     agent.flag_last_action(r)
                     break
+        t0 = time.time()  # the uploads travel over ZMQ asynchronously: wait for all 6 to land
+        while srv.service.received < 6 and time.time() - t0 < 30:
+            time.sleep(0.02)
         srv.wait_idle(60)
         assert srv.service.updates >= 2
         t0 = time.time()
