@@ -532,7 +532,7 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_pair_kernel(
   }
 }
 
-static int g_conv_stack_mode = 1;  // 1: co-tile pair split (default), 0: the per-layer split above
+static int g_conv_stack_mode = 0;  // 0: the per-layer split above (default), 1: the co-tile pair split
 
 }  // namespace rrl
 
