@@ -54,7 +54,6 @@ int rrl_pong_render(const float* state, uint8_t* obs, int N, void* stream);
 int rrl_pong_step_render(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
                          float* ep_acc, uint8_t* obs, int N, unsigned long long seed, unsigned long long step,
                          const unsigned long long* step_base, int max_steps, int reset_all, void* stream);
-int rrl_set_conv_stack_mode(int mode);
 int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
                        const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2, uint16_t* y3, int N,
                        int max_grid, void* stream);
@@ -464,9 +463,6 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("KW"), pybind11::arg("S"), pybind11::arg("Cout"), pybind11::arg("relu"),
         pybind11::arg("work") = pybind11::none());
   m.def("gemm_dgrad", &gemm_dgrad);
-  m.def("set_conv_stack_mode", [](int64_t mode) { return (int64_t)rrl_set_conv_stack_mode((int)mode); },
-        "fused conv stack forward: 1 = co-tile pair split (two MFMAs per activation fragment), 0 = the per-layer "
-        "split; returns the previous mode (-1 queries)");
   m.def("conv_stack_fwd", &conv_stack_fwd, pybind11::arg("x"), pybind11::arg("w1"), pybind11::arg("b1"),
         pybind11::arg("w2"), pybind11::arg("b2"), pybind11::arg("w3"), pybind11::arg("b3"), pybind11::arg("y1"),
         pybind11::arg("y2"), pybind11::arg("y3"), pybind11::arg("N"), pybind11::arg("probe") = 0,

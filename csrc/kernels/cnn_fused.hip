@@ -308,232 +308,6 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
   }
 }
 
-// Co-tile PAIR split of the same stack (selected at run time, rrl_set_conv_stack_mode): the
-// stack is LDS-read bound -- every 16x16x32 MFMA above re-reads a 1 KiB activation fragment
-// (ds_read_b128, 4 LDS cycles at 256 B/clk/CU, ~1.6-2x with the tap-shifted rows' bank
-// conflicts) while four SIMDs issue one MFMA per 16 cycles each.  Here each conv2 / conv3
-// activation fragment feeds TWO MFMAs (two co tiles per wave), which halves those reads:
-//   waves 0-3 ("A")  conv1 co tile 0, pixel tiles w + 4 t        (W1 half: 32 VGPRs)
-//                    conv2 co tiles 2 (w & 1) + {0, 1}, pixel tiles 3 (w >> 1) + {0, 1, 2}
-//                    (W2 pair: 128 VGPRs)
-//   waves 4-7 ("B")  conv1 co tile 1, pixel tiles (w - 4) + 4 t  (W1 half: 32 VGPRs)
-//                    conv3 co tiles 2 (w & 1) + {0, 1}, pixel tiles 2 ((w - 4) >> 1) + {0, 1}
-//                    of frame j - 1 (W3 pair: 144 VGPRs)
-// conv1's fragments now feed one MFMA each (400 reads per frame instead of 200), conv2's and
-// conv3's half as many as before (192 + 144 instead of 384 + 288): 736 reads per frame vs
-// 872, and the B2 -> B0 phase -- where conv2 and conv3 run side by side -- drops from ~5.1k
-// LDS cycles (over its 2.7k MFMA cycles) to its MFMA floor.  Same LDS plan, same barriers,
-// same k-step orders (outputs equal the default split's up to fma contraction).
-#ifndef C1MT
-#define C1MT 3  // conv1 pixel tiles per accumulator batch (register budget of the pair split)
-#endif
-__global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_pair_kernel(
-    const uint8_t* __restrict__ x, const uint16_t* __restrict__ w1, const float* __restrict__ b1,
-    const uint16_t* __restrict__ w2, const float* __restrict__ b2, const uint16_t* __restrict__ w3,
-    const float* __restrict__ b3, uint16_t* __restrict__ y1, uint16_t* __restrict__ y2,
-    uint16_t* __restrict__ y3, int N) {
-  using namespace cs;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* Xi = smem + kXi;
-  uint16_t* A1 = smem + kA1;
-  uint16_t* A3 = smem + kA3;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int i = lane & 15, g = lane >> 4;
-  const bool role_a = wave < 4;
-  const int wl = wave & 3;
-  const int c1 = role_a ? 0 : 1;     // conv1 co tile of this wave
-  const int cp = 2 * (wave & 1);     // first co tile of this wave's conv2 / conv3 pair
-  const int pt0 = role_a ? 3 * (wl >> 1) : 2 * (wl >> 1);  // first pixel tile of conv2 / conv3
-
-  bf16x8_t f1[8], fw[2][18];
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) f1[ks] = *reinterpret_cast<const bf16x8_t*>(w1 + (16 * c1 + i) * 256 + 32 * ks + 8 * g);
-  if (role_a) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-#pragma unroll
-      for (int ks = 0; ks < 16; ++ks)
-        fw[c][ks] = *reinterpret_cast<const bf16x8_t*>(w2 + (16 * (cp + c) + i) * 512 + 32 * ks + 8 * g);
-      fw[c][16] = fw[c][17] = fw[c][0];
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-#pragma unroll
-      for (int ks = 0; ks < 18; ++ks)
-        fw[c][ks] = *reinterpret_cast<const bf16x8_t*>(w3 + (16 * (cp + c) + i) * 576 + 32 * ks + 8 * g);
-    }
-  }
-  const float* b23 = role_a ? b2 : b3;
-
-  const int G = gridDim.x, n0 = blockIdx.x;
-  uint4 rx[kXPerT];
-  auto gload = [&](size_t n) {
-    const uint4* xs = reinterpret_cast<const uint4*>(x + n * (kFrameRows * 64));
-#pragma unroll
-    for (int k = 0; k < kXPerT; ++k) {
-      const int q = tid + kThreads * k;
-      rx[k] = q < kXChunks ? xs[q] : make_uint4(0, 0, 0, 0);
-    }
-  };
-  if (n0 < N) gload(n0);
-  for (int j = 0; n0 + (j - 2) * G < N; ++j) {
-    const int n = n0 + j * G;
-    const bool cur = n < N;
-    const bool prev = j >= 1 && n - G < N;
-    __syncthreads();  // B0
-    if (cur) {
-#pragma unroll
-      for (int k = 0; k < kXPerT; ++k) {
-        const int q = tid + kThreads * k;
-        if (q < kXChunks) {
-          uint16_t* d = Xi + (q >> 2) * kFrameLd + (q & 3) * 16;
-          *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(rx[k].x, rx[k].y));
-          *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(rx[k].z, rx[k].w));
-        }
-      }
-      if (n + G < N) gload((size_t)n + G);
-    }
-    __syncthreads();  // B1
-    if (prev) {
-      const uint16_t* A2p = smem + kA2 + ((j - 1) & 1) * 81 * kA2Ld;
-      uint4* yd = reinterpret_cast<uint4*>(y2 + (size_t)(n - G) * 81 * 64);
-      for (int q = tid; q < 81 * 8; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A2p + (q >> 3) * kA2Ld + (q & 7) * 8);
-    }
-    if (j >= 2) {
-      uint4* yd = reinterpret_cast<uint4*>(y3 + (size_t)(n - 2 * G) * 49 * 64);
-      for (int q = tid; q < 49 * 8; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A3 + (q >> 3) * kA2Ld + (q & 7) * 8);
-    }
-    // ---- conv1(n): co tile c1, pixel tiles wl + 4 t (7 on wl = 0, else 6), two batches
-    if (cur) {
-      const f32x4_t bias1 = *reinterpret_cast<const f32x4_t*>(b1 + 16 * c1 + 4 * g);
-#pragma unroll
-      for (int bb = 0; bb < 3; ++bb) {
-        constexpr int MT = C1MT;
-        f32x4_t acc[MT];
-        int r0[MT];
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-          const int p = 16 * min(wl + 4 * (MT * bb + t), 24) + i;
-          r0[t] = (p / 20) * 21 + p % 20;
-        }
-        // tiles wl + 4 (MT bb + t) < 25: 7 on wave 0 of the role, else 6 (wave-uniform)
-        const int ntot = wl == 0 ? 7 : 6;
-        const int nt = min(MT, ntot - MT * bb);
-        if (nt <= 0) break;
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-          const int tap = ks >> 1;
-          const int off = ((tap >> 1) * 21 + (tap & 1)) * kFrameLd + 32 * (ks & 1) + 8 * g;
-          bf16x8_t a[MT];
-#pragma unroll
-          for (int t = 0; t < MT; ++t)
-            if (t < nt) a[t] = *reinterpret_cast<const bf16x8_t*>(Xi + r0[t] * kFrameLd + off);
-#pragma unroll
-          for (int t = 0; t < MT; ++t)
-            if (t < nt) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f1[ks], a[t], acc[t], 0, 0, 0);
-        }
-#pragma unroll
-        for (int t = 0; t < MT; ++t)
-          if (t < nt) {
-            const int mt = wl + 4 * (MT * bb + t);
-            store4_bf16(A1 + (16 * mt + i) * kA1Ld + 16 * c1 + 4 * g, fmaxf(kU8Scale * acc[t][0] + bias1[0], 0.f),
-                        fmaxf(kU8Scale * acc[t][1] + bias1[1], 0.f), fmaxf(kU8Scale * acc[t][2] + bias1[2], 0.f),
-                        fmaxf(kU8Scale * acc[t][3] + bias1[3], 0.f));
-          }
-      }
-    }
-    __syncthreads();  // B2: a1(n) complete
-    if (cur) {
-      uint4* yd = reinterpret_cast<uint4*>(y1 + (size_t)n * 400 * 32);
-      for (int q = tid; q < 400 * 4; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A1 + (q >> 2) * kA1Ld + (q & 3) * 8);
-    }
-    if (role_a) {
-      // ---- conv2(n): co tiles cp, cp + 1 over pixel tiles pt0 .. pt0 + 2
-      if (cur) {
-        uint16_t* A2c = smem + kA2 + (j & 1) * 81 * kA2Ld;
-        constexpr int MT = 3;
-        f32x4_t acc[2][MT];
-        int r0[MT];
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          acc[0][t] = acc[1][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-          const int p = 16 * (pt0 + t) + i;
-          const int pc = p < 81 ? p : 0;
-          const int oh = pc / 9, ow = pc - oh * 9;
-          r0[t] = 2 * oh * 20 + 2 * ow;
-        }
-#pragma unroll
-        for (int ks = 0; ks < 16; ++ks) {
-          const int off = ((ks >> 2) * 20 + (ks & 3)) * kA1Ld + 8 * g;
-          bf16x8_t a[MT];
-#pragma unroll
-          for (int t = 0; t < MT; ++t) a[t] = *reinterpret_cast<const bf16x8_t*>(A1 + r0[t] * kA1Ld + off);
-#pragma unroll
-          for (int t = 0; t < MT; ++t) {
-            acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[0][ks], a[t], acc[0][t], 0, 0, 0);
-            acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[1][ks], a[t], acc[1][t], 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const f32x4_t bias = *reinterpret_cast<const f32x4_t*>(b23 + 16 * (cp + c) + 4 * g);
-#pragma unroll
-          for (int t = 0; t < MT; ++t) {
-            const int p = 16 * (pt0 + t) + i;
-            if (p < 81)
-              store4_bf16(A2c + p * kA2Ld + 16 * (cp + c) + 4 * g, fmaxf(acc[c][t][0] + bias[0], 0.f),
-                          fmaxf(acc[c][t][1] + bias[1], 0.f), fmaxf(acc[c][t][2] + bias[2], 0.f),
-                          fmaxf(acc[c][t][3] + bias[3], 0.f));
-          }
-        }
-      }
-    } else if (prev) {
-      // ---- conv3(n - G): co tiles cp, cp + 1 over pixel tiles pt0, pt0 + 1
-      const uint16_t* A2p = smem + kA2 + ((j - 1) & 1) * 81 * kA2Ld;
-      constexpr int MT = 2;
-      f32x4_t acc[2][MT];
-      int r0[MT];
-#pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        acc[0][t] = acc[1][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        const int p = 16 * (pt0 + t) + i;
-        const int pc = p < 49 ? p : 0;
-        const int oh = pc / 7, ow = pc - oh * 7;
-        r0[t] = oh * 9 + ow;
-      }
-#pragma unroll
-      for (int ks = 0; ks < 18; ++ks) {
-        const int tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
-        const int off = (kh * 9 + kw) * kA2Ld + 32 * (ks & 1) + 8 * g;
-        bf16x8_t a[MT];
-#pragma unroll
-        for (int t = 0; t < MT; ++t) a[t] = *reinterpret_cast<const bf16x8_t*>(A2p + r0[t] * kA2Ld + off);
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          acc[0][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[0][ks], a[t], acc[0][t], 0, 0, 0);
-          acc[1][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[1][ks], a[t], acc[1][t], 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const f32x4_t bias = *reinterpret_cast<const f32x4_t*>(b23 + 16 * (cp + c) + 4 * g);
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          const int p = 16 * (pt0 + t) + i;
-          if (p < 49)
-            store4_bf16(A3 + p * kA2Ld + 16 * (cp + c) + 4 * g, fmaxf(acc[c][t][0] + bias[0], 0.f),
-                        fmaxf(acc[c][t][1] + bias[1], 0.f), fmaxf(acc[c][t][2] + bias[2], 0.f),
-                        fmaxf(acc[c][t][3] + bias[3], 0.f));
-        }
-      }
-    }
-  }
-}
-
-static int g_conv_stack_mode = 0;  // 0: the per-layer split above (default), 1: the co-tile pair split
-
 }  // namespace rrl
 
 using namespace rrl;
@@ -555,30 +329,11 @@ static int launch_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const flo
   return (int)hipGetLastError();
 }
 
-extern "C" int rrl_set_conv_stack_mode(int mode) {
-  const int old = g_conv_stack_mode;
-  if (mode == 0 || mode == 1) g_conv_stack_mode = mode;
-  return old;
-}
-
 extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
                                   const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
                                   uint16_t* y3, int N, int max_grid, void* stream) {
   // max_grid < 0: timing probe variant -max_grid >> 16 (tools/cnn_kbench.py), grid = -max_grid & 0xffff
   hipStream_t st = (hipStream_t)stream;
-  if (max_grid >= 0 && g_conv_stack_mode == 1) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)conv_stack_fwd_pair_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                cs::kLds);
-      attr = true;
-    }
-    if (N < 1) return 0;
-    const int grid = N < max_grid ? N : max_grid;
-    hipLaunchKernelGGL(conv_stack_fwd_pair_kernel, dim3(grid), dim3(cs::kThreads), cs::kLds, st, x, w1, b1, w2, b2, w3,
-                       b3, y1, y2, y3, N);
-    return (int)hipGetLastError();
-  }
   if (max_grid >= 0) return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, max_grid, st);
   const int probe = (-max_grid) >> 16, g = (-max_grid) & 0xffff;
   switch (probe) {
@@ -601,10 +356,17 @@ extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const fl
 // gradient accumulates in registers across all of a workgroup's images: one fp32 partial
 // per workgroup instead of one per split-K slice.
 //
-// LDS per image: da3 in a zero-bordered 11x11 image (row (oh + 2) * 11 + ow + 2), a2 as
-// [96 rows][72] (rows >= 81 zero), the dgrad staging tile [81][72].
+// LDS, two buffers (image j computes from buffer j & 1 while image j + 1, prefetched into
+// registers one iteration earlier, is written into the other and image j + 2's loads are in
+// flight: ONE barrier per image, as conv2_bwd_kernel): da3 in a zero-bordered 11x11 image (row
+// (oh + 2) * 11 + ow + 2), a2 as [96 rows] (rows >= 81 zero); rows of 64 channels + 16 pad
+// (the single-buffered form with 72-element rows, three barriers per image and the dgrad
+// tile staged through LDS spent 59 % of its wave cycles parked, SQ_WAIT_ANY, and 58 % of its
+// LDS cycles on bank conflicts: profiles/r4_cnn_pmc.txt).
 //   dgrad  da2[81 px][64 c] = sum_(tap, co) da3[px - tap][co] W3[co][tap][c]      (6 x 4 tiles)
-//          wave w: c tile (w & 3), pixel tiles 3 (w >> 2) + {0, 1, 2}, W3 fragments in registers
+//          wave w: c tile (w & 3), pixel tiles 3 (w >> 2) + {0, 1, 2}, W3 fragments in registers;
+//          a lane ends with 4 consecutive channels of one pixel: masked by a2 (> 0) from the
+//          same buffer and stored straight to HBM as 8 bytes
 //   wgrad  dW3[64 co][576 k] += da3^T (co x pos) . im2col(a2) (pos x k)            (4 x 36 tiles)
 //          positions run over 8 output rows x 8 columns (row 7 and column 7 read the zero
 //          border), so the 8 positions of one lane group are one output row and their a2
@@ -613,13 +375,17 @@ extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const fl
 //          tiles, taps 0..4 (w < 4) or 5..8 (w >= 4)
 namespace c3b {
 constexpr int kThreads = 512;
-constexpr int kLd = 72;
-constexpr int kD = 0;                 // da3 bordered [121][72]
-constexpr int kX = kD + 121 * kLd;    // a2 [96][72]
-constexpr int kO = kX + 96 * kLd;     // dgrad staging [81][72]
-constexpr int kLds = (kO + 81 * kLd) * 2;  // 43,344 bytes
+#ifndef C3B_LD
+#define C3B_LD 80
+#endif
+constexpr int kLd = C3B_LD;
+constexpr int kD = 0;                        // da3 bordered [121][kLd]
+constexpr int kX = kD + 121 * kLd;           // a2 [96][kLd]
+constexpr int kBuf = kX + 96 * kLd;          // elements per buffer
+constexpr int kLds = 2 * kBuf * 2;           // 69,440 bytes at kLd = 80
 constexpr int kYC = 49 * 8, kXC = 81 * 8;  // 16-byte chunks per image
 constexpr int kYPT = (kYC + kThreads - 1) / kThreads, kXPT = (kXC + kThreads - 1) / kThreads;
+static_assert(kBuf % 8 == 0, "16-byte aligned buffers");
 }  // namespace c3b
 
 __device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* a0, int ld) {
@@ -639,9 +405,6 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
                                                                      float* __restrict__ bias_part, int N) {
   using namespace c3b;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* Yi = smem + kD;
-  uint16_t* Xi = smem + kX;
-  uint16_t* O = smem + kO;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i16 = lane & 15, g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
   const int ct = wave & 3, half = wave >> 2;
@@ -658,14 +421,8 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
     for (int e = 0; e < 8; ++e) v[e] = (short)w[((co0 + e) * 9 + t) * 64 + 16 * ct + i16];
     wf[ks] = __builtin_bit_cast(bf16x8_t, v);
   }
-  // zero the da3 border and the a2 pad rows once (interiors are rewritten per image)
-  for (int q = tid; q < 121 * (kLd / 8); q += kThreads) {
-    const int r = q / (kLd / 8), oh = r / 11 - 2, ow = r % 11 - 2;
-    if (oh < 0 || oh > 6 || ow < 0 || ow > 6)
-      *reinterpret_cast<uint4*>(Yi + r * kLd + 8 * (q % (kLd / 8))) = make_uint4(0, 0, 0, 0);
-  }
-  for (int q = tid; q < 15 * (kLd / 8); q += kThreads)
-    *reinterpret_cast<uint4*>(Xi + (81 + q / (kLd / 8)) * kLd + 8 * (q % (kLd / 8))) = make_uint4(0, 0, 0, 0);
+  // zero both buffers once: the da3 border and the a2 pad rows are never rewritten
+  for (int q = tid; q < 2 * kBuf / 8; q += kThreads) *reinterpret_cast<uint4*>(smem + 8 * q) = make_uint4(0, 0, 0, 0);
 
   constexpr int NTAP = 5;  // taps of this wave's wgrad k tiles (4 on the second half)
   const int tap0 = half * 5, ntap = half ? 4 : 5;
@@ -691,24 +448,40 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
       rx[k] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
     }
   };
-  if ((int)blockIdx.x < N) gload(blockIdx.x);
-  for (int n = blockIdx.x; n < N; n += gridDim.x) {
-    __syncthreads();  // the previous image's reads of Yi / Xi / O are done
+  auto lstore = [&](int buf) {
+    uint16_t* Y = smem + buf * kBuf + kD;
+    uint16_t* X = smem + buf * kBuf + kX;
 #pragma unroll
     for (int k = 0; k < kYPT; ++k) {
       const int q = tid + kThreads * k;
       if (q < kYC) {
         const int pix = q >> 3, oh = pix / 7, ow = pix - oh * 7;
-        *reinterpret_cast<uint4*>(Yi + ((oh + 2) * 11 + ow + 2) * kLd + (q & 7) * 8) = ry[k];
+        *reinterpret_cast<uint4*>(Y + ((oh + 2) * 11 + ow + 2) * kLd + (q & 7) * 8) = ry[k];
       }
     }
 #pragma unroll
     for (int k = 0; k < kXPT; ++k) {
       const int q = tid + kThreads * k;
-      if (q < kXC) *reinterpret_cast<uint4*>(Xi + (q >> 3) * kLd + (q & 7) * 8) = rx[k];
+      if (q < kXC) *reinterpret_cast<uint4*>(X + (q >> 3) * kLd + (q & 7) * 8) = rx[k];
     }
-    if (n + (int)gridDim.x < N) gload(n + gridDim.x);
-    __syncthreads();
+  };
+
+  const int G = gridDim.x, n0 = blockIdx.x;
+  __syncthreads();  // zeroing done before the first image lands in buffer 0
+  if (n0 < N) {
+    gload(n0);
+    lstore(0);
+  }
+  if (n0 + G < N) gload(n0 + G);
+  for (int j = 0; n0 + j * G < N; ++j) {
+    const int n = n0 + j * G;
+    __syncthreads();  // buffer j & 1 holds image n; buffer (j + 1) & 1 is no longer read
+    if (n + G < N) {
+      lstore((j + 1) & 1);
+      if (n + 2 * G < N) gload(n + 2 * G);
+    }
+    const uint16_t* Yi = smem + (j & 1) * kBuf + kD;
+    const uint16_t* Xi = smem + (j & 1) * kBuf + kX;
 
     // ---- wgrad: 2 position k-steps x (4 co tiles x ntap taps)
 #pragma unroll
@@ -749,23 +522,21 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
 #pragma unroll
         for (int u = 0; u < 3; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], a[u], acc[u], 0, 0, 0);
       }
+      // D = da2^T: lane (i16, g) holds channels 16 ct + 4g .. + 3 of pixel q, masked by a2 > 0
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {  // D = da2^T: lane (i16, g) holds channels 4g..4g+3 of pixel i16
+      for (int u = 0; u < 3; ++u) {
         const int q = 16 * (3 * half + u) + i16;
-        if (q < 81) store4_bf16(O + q * kLd + 16 * ct + 4 * g, acc[u][0], acc[u][1], acc[u][2], acc[u][3]);
+        if (q < 81) {
+          const uint2 m = *reinterpret_cast<const uint2*>(Xi + q * kLd + 16 * ct + 4 * g);
+          *reinterpret_cast<uint2*>(dx + ((size_t)n * 81 + q) * 64 + 16 * ct + 4 * g) =
+              make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x), relu_mask2(pk_bf16(acc[u][2], acc[u][3]), m.y));
+        }
       }
     }
     // ---- db3
     for (int pos = tid >> 6; pos < 49; pos += 8) {
       const int oh = pos / 7, ow = pos - oh * 7;
       bsum += bf2f(Yi[((oh + 2) * 11 + ow + 2) * kLd + (tid & 63)]);
-    }
-    __syncthreads();  // dgrad staging complete
-    uint4* xd = reinterpret_cast<uint4*>(dx + (size_t)n * 81 * 64);
-    for (int q = tid; q < kXC; q += kThreads) {
-      const uint4 v = *reinterpret_cast<const uint4*>(O + (q >> 3) * kLd + (q & 7) * 8);
-      const uint4 m = *reinterpret_cast<const uint4*>(Xi + (q >> 3) * kLd + (q & 7) * 8);
-      xd[q] = relu_mask8(v, m);
     }
   }
   // this workgroup's weight-gradient partial: part[blk][co][tap][c]

@@ -420,16 +420,14 @@ def test_sum_splits_matches_torch(cuda, splits, n):
     torch.testing.assert_close(out.cpu(), part.sum(0), rtol=1e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("mode", [1, 0])  # co-tile pair split (default) / per-layer wave split
 @pytest.mark.parametrize("N", [1, 5, 300, 2048])
-def test_fused_conv_stack_matches_per_layer_kernels(cuda, N, mode):
+def test_fused_conv_stack_matches_per_layer_kernels(cuda, N):
     """conv_stack_fwd (conv1 -> conv2 -> conv3 in one launch, cnn_fused.hip) against the
     per-layer kernels it replaces (same k-step order: equal up to fma contraction) and the
-    bf16-emulating fp32 oracle, in both wave splits of the fused kernel."""
+    bf16-emulating fp32 oracle."""
     from relayrl_prototype_amd.ops import hip
 
     h = hip()
-    old_mode = h.set_conv_stack_mode(mode)
     spec = CNNSpec()
     o = spec.offsets()
     g = torch.Generator().manual_seed(N)
@@ -463,7 +461,6 @@ def test_fused_conv_stack_matches_per_layer_kernels(cuda, N, mode):
     _, _, acts = reference_forward(spec, params.cpu(), x.cpu(), emulate_bf16=True)
     for dev_a, ref_a in zip(outs[0], acts[:3]):
         assert relerr(dev_a, ref_a.permute(0, 2, 3, 1).reshape(-1)) < 1e-2
-    h.set_conv_stack_mode(old_mode)
 
 
 @pytest.mark.parametrize("B", [3, 300, 1500])

@@ -16,7 +16,7 @@ import torch
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", default="fwd,fwd_pair,fwd_layers,bwd3,bwd3_layers,bwd2,dgrad2,wgrad1,wgrad1_8")
+    ap.add_argument("--which", default="fwd,fwd_layers,bwd3,bwd3_layers,bwd2,dgrad2,wgrad1,wgrad1_8")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--frames", type=int, default=2048)
     ap.add_argument("--bwd-frames", type=int, default=10240)
@@ -68,12 +68,7 @@ def main():
         L = CONVS[1]
         h.conv_dgrad(da2, W[2][0], a1, da1, Nb, L.hin, L.hin, L.cin, L.k, L.k, L.s, L.cout)
 
-    def fwd_pair():  # the co-tile pair split (rrl_set_conv_stack_mode 1) for comparison
-        old = h.set_conv_stack_mode(1)
-        fwd()
-        h.set_conv_stack_mode(old)
-
-    fns = {"fwd_pair": fwd_pair}
+    fns = {}
     fns["wgrad1_8"] = lambda: h.conv1_wgrad8(x[:Nb], da1, part, bpart, Nb, min(Nb, cus))
     fns["wgrad1"] = lambda: h.conv_wgrad(da1, x[:Nb], part, 256, Nb, 21, 21, 64, 2, 2, 1, 32, bpart)
     fns.update({"p_nomfma": probe(1), "p_nostore": probe(2), "p_nostore_nomfma": probe(3), "p_hotframe": probe(4),

@@ -2,11 +2,15 @@
 # TTT value-loop levers (slab-count sweep, stamps, epoch profile)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out/pmc_cs1 gpurun_out/pmc_cs2 gpurun_out/prof_flagship gpurun_out/prof_ttt
+mkdir -p gpurun_out/pmc_cs1 gpurun_out/pmc_cs2 gpurun_out/pmc_cs3 gpurun_out/pmc_cs4 gpurun_out/prof_flagship gpurun_out/prof_ttt
 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS \
-  --kernel-trace --output-format csv -d gpurun_out/pmc_cs1 -o run -- python3 tools/cnn_kbench.py --which fwd,fwd_pair --iters 2 > gpurun_out/pmc_cs1/log.txt 2>&1 && echo PASS1_OK && \
+  --kernel-trace --output-format csv -d gpurun_out/pmc_cs1 -o run -- python3 tools/cnn_kbench.py --which fwd,fwd_pair,bwd3,bwd2,wgrad1_8 --iters 2 > gpurun_out/pmc_cs1/log.txt 2>&1 && echo PASS1_OK && \
 timeout -s KILL 90 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_MFMA SQ_WAVES \
-  --kernel-trace --output-format csv -d gpurun_out/pmc_cs2 -o run -- python3 tools/cnn_kbench.py --which fwd,fwd_pair --iters 2 > gpurun_out/pmc_cs2/log.txt 2>&1 && echo PASS2_OK || exit 1
+  --kernel-trace --output-format csv -d gpurun_out/pmc_cs2 -o run -- python3 tools/cnn_kbench.py --which fwd,fwd_pair,bwd3,bwd2,wgrad1_8 --iters 2 > gpurun_out/pmc_cs2/log.txt 2>&1 && echo PASS2_OK && \
+timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE \
+  --kernel-trace --output-format csv -d gpurun_out/pmc_cs3 -o run -- python3 tools/cnn_kbench.py --which fwd,fwd_pair,bwd3,bwd2,wgrad1_8 --iters 2 > gpurun_out/pmc_cs3/log.txt 2>&1 && echo PASS3_OK && \
+timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE \
+  --kernel-trace --output-format csv -d gpurun_out/pmc_cs4 -o run -- python3 tools/cnn_kbench.py --which fwd,fwd_pair,bwd3,bwd2,wgrad1_8 --iters 2 > gpurun_out/pmc_cs4/log.txt 2>&1 && echo PASS4_OK || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_flagship -o run -- \
   python3 bench.py --steps 5 --warmup 2 --no-ttt --host-steps 0 --pong-steps 0 --ref-cpu-seconds 0 --phase-steps 0 > gpurun_out/prof_flagship/log.txt 2>&1 || exit 1
 grep metric gpurun_out/prof_flagship/log.txt | cut -c1-200
