@@ -601,10 +601,16 @@ extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16
 // LDS buffer j & 1, image j + 1 (prefetched into registers one iteration earlier) is written
 // into the other buffer and image j + 2's loads are in flight.
 //
-// LDS images per buffer:
-//   da2  zero-bordered 12 x 12 (row (oh + 1) * 12 + ow + 1; 64 co + 8 pad)
+// LDS images per buffer (layouts chosen with tools/lds_bank_model.py --conv2; the previous
+// 72- / 40-element padded rows ran the dgrad reads at 2.71 and the transposed reads at 1.9-2.0
+// LDS cycles per conflict-free cycle, 54 % of the kernel's LDS cycles were conflicts:
+// profiles/r4_cnn_pmc.txt):
+//   da2  zero-bordered 12 x 12 (position (oh + 1, ow + 1)), 64 channels, no pad, the 16-byte
+//        chunk c of position (y, x) stored at chunk c ^ ((x + 2 y) & 7): dgrad b128 reads 1.14,
+//        wgrad transposed reads 1.88
 //   a1   split into its four stride-2 phase images (ph, pw) = (ih & 1, iw & 1), each 10 x 10
-//        positions (row (ih >> 1) * 10 + (iw >> 1), rows 100..115 zero; 32 c + 8 pad)
+//        positions (row (ih >> 1) * 10 + (iw >> 1), rows 100..115 zero; 32 channels, no pad,
+//        chunk c of row y of the phase image at chunk c ^ (2 (y & 1))): transposed reads 1.31
 //   dgrad  da1[ph + 2a][pw + 2b][c] = sum_(i, j, co) da2[a - i][b - j][co] W2[co][ph + 2i][pw + 2j][c]
 //          per phase class a 100 px x 32 c GEMM over K = (4 taps x 64 co); wave w: class w >> 1,
 //          c tile w & 1, W2 fragments in registers.  The weights are the MFMA's A operand, so a
@@ -617,14 +623,20 @@ extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16
 //          rows); wave w: c block w & 1 of taps 4 (w >> 1) .. + 3, all 4 co tiles.
 namespace c2b {
 constexpr int kThreads = 512;
-constexpr int kDLd = 72, kPLd = 40;
+constexpr int kDLd = 64, kPLd = 32;
 constexpr int kDRows = 144, kPRows = 116;
-constexpr int kBuf = kDRows * kDLd + 4 * kPRows * kPLd;  // elements per buffer (28,928)
-constexpr int kLds = 2 * kBuf * 2;                       // 115,712 bytes
+constexpr int kBuf = kDRows * kDLd + 4 * kPRows * kPLd;  // elements per buffer (24,064)
+constexpr int kLds = 2 * kBuf * 2;                       // 96,256 bytes
 constexpr int kYC = 81 * 8, kXC = 400 * 4;               // 16-byte chunks per image
 constexpr int kYPT = (kYC + kThreads - 1) / kThreads, kXPT = (kXC + kThreads - 1) / kThreads;
+// element offsets: channel col of da2 position (y, x); of a1 phase image ph, position (y, x)
+__device__ __forceinline__ int doff(int y, int x, int col) {
+  return (y * 12 + x) * kDLd + ((((col >> 3) ^ (x + 2 * y)) & 7) << 3) + (col & 7);
+}
+__device__ __forceinline__ int poff(int ph, int y, int x, int col) {
+  return (ph * kPRows + y * 10 + x) * kPLd + ((((col >> 3) ^ (2 * y)) & 3) << 3) + (col & 7);
+}
 }  // namespace c2b
-
 
 // STAGED: da1 goes through an LDS tile [400][40] and leaves as 16-byte row chunks after a
 // second barrier, instead of 8-byte stores straight from the MFMA registers
@@ -667,38 +679,39 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
   float bsum = 0.f;  // db2[tid & 63] over positions (tid >> 6) + 8 k
 
   uint4 ry[kYPT], rx[kXPT];
-  auto gload = [&](int n) {
+  // gload / lstore take the thread index: inside the image loop an opaque copy, so the
+  // per-lane offsets are recomputed there instead of being kept live (spilled) across it
+  auto gload = [&](int n, int tq) {
     const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 81 * 64);
     const uint4* xs = reinterpret_cast<const uint4*>(xact + (size_t)n * 400 * 32);
 #pragma unroll
     for (int k = 0; k < kYPT; ++k) {
-      const int q = tid + kThreads * k;
+      const int q = tq + kThreads * k;
       ry[k] = q < kYC ? ys[q] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int k = 0; k < kXPT; ++k) {
-      const int q = tid + kThreads * k;
+      const int q = tq + kThreads * k;
       rx[k] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, int tq) {
     uint16_t* D = smem + buf * kBuf;
     uint16_t* P = D + kDRows * kDLd;
 #pragma unroll
     for (int k = 0; k < kYPT; ++k) {
-      const int q = tid + kThreads * k;
+      const int q = tq + kThreads * k;
       if (q < kYC) {
         const int pix = q >> 3, oh = pix / 9, ow = pix - oh * 9;
-        *reinterpret_cast<uint4*>(D + ((oh + 1) * 12 + ow + 1) * kDLd + (q & 7) * 8) = ry[k];
+        *reinterpret_cast<uint4*>(D + doff(oh + 1, ow + 1, (q & 7) * 8)) = ry[k];
       }
     }
 #pragma unroll
     for (int k = 0; k < kXPT; ++k) {
-      const int q = tid + kThreads * k;
+      const int q = tq + kThreads * k;
       if (q < kXC) {
         const int pix = q >> 2, ih = pix / 20, iw = pix - ih * 20;
-        const int phase = (ih & 1) * 2 + (iw & 1);
-        *reinterpret_cast<uint4*>(P + (phase * kPRows + (ih >> 1) * 10 + (iw >> 1)) * kPLd + (q & 3) * 8) = rx[k];
+        *reinterpret_cast<uint4*>(P + poff((ih & 1) * 2 + (iw & 1), ih >> 1, iw >> 1, (q & 3) * 8)) = rx[k];
       }
     }
   };
@@ -706,16 +719,19 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
   const int G = gridDim.x, n0 = blockIdx.x;
   __syncthreads();  // zeroing done before the first image lands in buffer 0
   if (n0 < N) {
-    gload(n0);
-    lstore(0);
+    gload(n0, tid);
+    lstore(0, tid);
   }
-  if (n0 + G < N) gload(n0 + G);
+  if (n0 + G < N) gload(n0 + G, tid);
   for (int j = 0; n0 + j * G < N; ++j) {
     const int n = n0 + j * G;
+    int to = tid;
+    asm volatile("" : "+v"(to));
+    const int go = (to & 63) >> 4, qo = (to >> 2) & 3, po = to & 3, io = to & 15;
     __syncthreads();  // buffer j & 1 holds image n; buffer (j + 1) & 1 is no longer read
     if (n + G < N) {
-      lstore((j + 1) & 1);
-      if (n + 2 * G < N) gload(n + 2 * G);
+      lstore((j + 1) & 1, to);
+      if (n + 2 * G < N) gload(n + 2 * G, to);
     }
     const uint16_t* D = smem + (j & 1) * kBuf;
     const uint16_t* P = D + kDRows * kDLd;
@@ -726,21 +742,21 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
       int oh[2], ow0[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int R = 2 * (4 * s + g) + h;  // run index; runs >= 27 read zero rows
+        const int R = 2 * (4 * s + go) + h;  // run index; runs >= 27 read zero rows
         oh[h] = R < 27 ? R / 3 : 9;
         ow0[h] = R < 27 ? 4 * (R % 3) : 0;
       }
       bf16x8_t af[4], bfr[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        af[c] = tr_frag2(D + ((oh[0] + 1) * 12 + ow0[0] + 1 + q4) * kDLd + 16 * c + 4 * p4,
-                         D + ((oh[1] + 1) * 12 + ow0[1] + 1 + q4) * kDLd + 16 * c + 4 * p4);
+        af[c] = tr_frag2(D + doff(oh[0] + 1, ow0[0] + 1 + qo, 16 * c + 4 * po),
+                         D + doff(oh[1] + 1, ow0[1] + 1 + qo, 16 * c + 4 * po));
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int tau = tau0 + t, kh = tau >> 2, kw = tau & 3;
-        const uint16_t* Pp = P + ((kh & 1) * 2 + (kw & 1)) * kPRows * kPLd + 16 * cb + 4 * p4;
-        bfr[t] = tr_frag2(Pp + ((oh[0] + (kh >> 1)) * 10 + ow0[0] + (kw >> 1) + q4) * kPLd,
-                          Pp + ((oh[1] + (kh >> 1)) * 10 + ow0[1] + (kw >> 1) + q4) * kPLd);
+        const int phs = (kh & 1) * 2 + (kw & 1);
+        bfr[t] = tr_frag2(P + poff(phs, oh[0] + (kh >> 1), ow0[0] + (kw >> 1) + qo, 16 * cb + 4 * po),
+                          P + poff(phs, oh[1] + (kh >> 1), ow0[1] + (kw >> 1) + qo, 16 * cb + 4 * po));
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c)
@@ -751,22 +767,23 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
     auto class_tiles = [&](auto tag) {
       constexpr int T0 = decltype(tag)::value, NT = T0 == 0 ? 4 : 3;
       f32x4_t acc[NT];
-      int rb[NT];
+      int ya[NT], xa[NT];  // da2 position of the tap-(0, 0) source of this lane's class pixel
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
         acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        const int p = 16 * (T0 + u) + i16;
+        const int p = 16 * (T0 + u) + io;
         const int pc = p < 100 ? p : 0;  // rows past the class are computed and discarded
         const int a = pc / 10, b = pc - a * 10;
-        rb[u] = (a + 1) * 12 + (b + 1);
+        ya[u] = a + 1;
+        xa[u] = b + 1;
       }
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
         const int t = ks >> 1, ti = t >> 1, tj = t & 1;
-        const int off = -(ti * 12 + tj) * kDLd + (ks & 1) * 32 + 8 * g;
         bf16x8_t bv[NT];
 #pragma unroll
-        for (int u = 0; u < NT; ++u) bv[u] = *reinterpret_cast<const bf16x8_t*>(D + rb[u] * kDLd + off);
+        for (int u = 0; u < NT; ++u)
+          bv[u] = *reinterpret_cast<const bf16x8_t*>(D + doff(ya[u] - ti, xa[u] - tj, (ks & 1) * 32 + 8 * go));
 #pragma unroll
         for (int u = 0; u < NT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], bv[u], acc[u], 0, 0, 0);
       }
@@ -776,7 +793,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
         const int p = 16 * (T0 + u) + i16;
         if (p < 100) {
           const int a = p / 10, b = p - a * 10;
-          const uint2 m = *reinterpret_cast<const uint2*>(P + (cls * kPRows + a * 10 + b) * kPLd + 16 * ct + 4 * g);
+          const uint2 m = *reinterpret_cast<const uint2*>(P + poff(cls, a, b, 16 * ct + 4 * g));
           const uint2 v = make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x),
                                      relu_mask2(pk_bf16(acc[u][2], acc[u][3]), m.y));
           const int pix = (ph + 2 * a) * 20 + pw + 2 * b;
@@ -788,9 +805,9 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
     class_tiles(std::integral_constant<int, 0>{});
     class_tiles(std::integral_constant<int, 4>{});
     // ---- db2
-    for (int pos = tid >> 6; pos < 81; pos += 8) {
+    for (int pos = to >> 6; pos < 81; pos += 8) {
       const int oh = pos / 9, ow = pos - oh * 9;
-      bsum += bf2f(D[((oh + 1) * 12 + ow + 1) * kDLd + (tid & 63)]);
+      bsum += bf2f(D[doff(oh + 1, ow + 1, to & 63)]);
     }
     if (STAGED) {
       __syncthreads();  // staging tile complete (rewritten only after the next top barrier)

@@ -103,6 +103,8 @@ def main():
           " shipped 11-wide/64 + chunk ^ (y + x) ->", conv3_bwd_da3(new_y))
     print("conv3_bwd a2 image (wgrad tr, cycles):                old 9-wide/72 ->", conv3_bwd_a2(old_x),
           " shipped 12-wide/80 ->", conv3_bwd_a2(new_x))
+    if "--conv2" in sys.argv:
+        search_conv2()
     if "--search" in sys.argv:
         res = []
         for ld in (64, 72, 80, 88):
@@ -126,6 +128,98 @@ def main():
         print("a2 image, best layouts:")
         for r in res[:6]:
             print("  ", r)
+
+
+def conv2_bwd_da2(el):
+    """(dgrad b128, wgrad transposed, LDS cycles per wave-image) of the da2 image; el(y, x, col)
+    addresses bordered position (y, x) = (oh + 1, ow + 1)"""
+    rd, rw = [], []
+    for cls in range(4):
+        for T0, NT in ((0, 4), (4, 3)):
+            for u in range(NT):
+                for ks in range(8):
+                    t = ks >> 1
+                    ti, tj = t >> 1, t & 1
+                    addr = []
+                    for i16, g, q4, p4 in lanes():
+                        p = 16 * (T0 + u) + i16
+                        pc = p if p < 100 else 0
+                        addr.append(2 * el(pc // 10 + 1 - ti, pc % 10 + 1 - tj, (ks & 1) * 32 + 8 * g))
+                    rd.append(b128(addr))
+
+    def run(s, g, h):
+        R = 2 * (4 * s + g) + h
+        return (R // 3, 4 * (R % 3)) if R < 27 else (9, 0)
+    for s in range(4):
+        for c in range(4):
+            for h in (0, 1):
+                addr = []
+                for i16, g, q4, p4 in lanes():
+                    oh, ow0 = run(s, g, h)
+                    addr.append(2 * el(oh + 1, ow0 + 1 + q4, 16 * c + 4 * p4))
+                rw.append(tr16(addr))
+    d, w = sum(rd) / len(rd), sum(rw) / len(rw)
+    # per wave-image: dgrad 7 tiles x 8 k-steps b128 (4 cycles), wgrad 4 x 4 x 2 transposed (2 cycles)
+    return round(d, 2), round(w, 2), 56 * 4 * d + 32 * 2 * w
+
+
+def conv2_bwd_a1(el):
+    """(wgrad transposed, LDS cycles per wave-image) of the a1 phase images; el(phase, y, x, col)"""
+    rw = []
+
+    def run(s, g, h):
+        R = 2 * (4 * s + g) + h
+        return (R // 3, 4 * (R % 3)) if R < 27 else (9, 0)
+    for s in range(4):
+        for w in range(8):
+            cb, tau0 = w & 1, 4 * (w >> 1)
+            for t in range(4):
+                tau = tau0 + t
+                kh, kw = tau >> 2, tau & 3
+                for h in (0, 1):
+                    addr = []
+                    for i16, g, q4, p4 in lanes():
+                        oh, ow0 = run(s, g, h)
+                        addr.append(2 * el((kh & 1) * 2 + (kw & 1), oh + (kh >> 1), ow0 + (kw >> 1) + q4, 16 * cb + 4 * p4))
+                    rw.append(tr16(addr))
+    w = sum(rw) / len(rw)
+    return round(w, 2), 32 * 2 * w
+
+
+def search_conv2():
+    none = lambda y, x: 0  # noqa: E731
+    print("conv2_bwd da2 image (dgrad b128, wgrad tr, cycles): current 12-wide/72 ->",
+          conv2_bwd_da2(swz(lambda y, x: y * 12 + x, 72, none)))
+    res = []
+    for ld in (64, 72, 80):
+        for W in (12, 13, 14, 16):
+            for a in range(8):
+                for b in range(8):
+                    f = (lambda y, x, a=a, b=b: a * x + b * y)
+                    d, w, c = conv2_bwd_da2(swz(lambda y, x, W=W: y * W + x, ld, f))
+                    res.append((round(c, 1), ld, W, f"chunk ^ ({a} x + {b} y)", d, w))
+    res.sort()
+    for r in res[:6]:
+        print("  ", r)
+
+    def a1el(W, ld, rows, f):
+        def el(ph, y, x, col):
+            r = ph * rows + y * W + x
+            return r * ld + ((((col >> 3) ^ f(y, x)) & 3) << 3) + (col & 7)
+        return el
+    print("conv2_bwd a1 phase images (wgrad tr, cycles): current 10-wide/40 ->", conv2_bwd_a1(a1el(10, 40, 116, none)))
+    res = []
+    for ld in (32, 40, 48, 56):
+        for W in (10, 11, 12, 16):
+            rows = max(116, ((11 * W + 15) // 16) * 16)
+            for a in range(4):
+                for b in range(4):
+                    f = (lambda y, x, a=a, b=b: a * x + b * y)
+                    w, c = conv2_bwd_a1(a1el(W, ld, rows, f))
+                    res.append((round(c, 1), ld, W, rows, f"chunk ^ ({a} x + {b} y)", w))
+    res.sort()
+    for r in res[:6]:
+        print("  ", r)
 
 
 if __name__ == "__main__":
