@@ -358,51 +358,31 @@ extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const fl
 //
 // LDS, two buffers (image j computes from buffer j & 1 while image j + 1, prefetched into
 // registers one iteration earlier, is written into the other and image j + 2's loads are in
-// flight: ONE barrier per image, as conv2_bwd_kernel).  (The single-buffered form -- three
-// barriers per image, the dgrad tile staged through LDS, 72-element rows -- spent 59 % of its
-// wave cycles parked, SQ_WAIT_ANY, and 58 % of its LDS cycles on bank conflicts:
-// profiles/r4_cnn_pmc.txt.)  Layouts chosen with a bank model of the MI355X lane groups
-// (ds_read_b128: 4 x 16 lanes, ds_read_b64_tr_b16: 2 x 32; tools/lds_bank_model.py):
-//   da3  zero-bordered 11 x 11 image, row (oh + 2) * 11 + ow + 2, 64 channels with NO pad and
-//        the 16-byte chunk c of image row (y, x) stored at chunk c ^ ((y + x) & 7): the dgrad
-//        b128 reads 2.0 -> 1.17 LDS cycles per conflict-free cycle, the wgrad transposed reads 2.0
-//   a2   9 x 9 image in rows of 12 (row ih * 12 + iw, 80-element rows; columns 9..11 and rows
-//        past the image zero): the wgrad transposed reads 2.0 -> 1.0 (an 8-position run of one
-//        lane group and the next group's run 12 rows later land on disjoint banks)
-//   dgrad  da2[81 px][64 c] = sum_(tap, co) da3[px - tap][co] W3[co][tap][c]      (6 x 4 tiles)
-//          wave w: c tile (w & 3), pixel tiles 3 (w >> 2) + {0, 1, 2}, W3 fragments in registers;
-//          a lane ends with 4 consecutive channels of one pixel: masked by a2 (> 0) from the
-//          same buffer and stored straight to HBM as 8 bytes
-//   wgrad  dW3[64 co][576 k] += da3^T (co x pos) . im2col(a2) (pos x k)            (4 x 36 tiles)
-//          positions run over 8 output rows x 8 columns (row 7 and column 7 read the zero
-//          border), so the 8 positions of one lane group are one output row and their a2
-//          pixels are 8 consecutive image positions: both operands are transposed LDS reads
-//          (ds_read_b64_tr_b16) with no im2col buffer; wave w: c block (w & 3) of all 4 co
-//          tiles, taps 0..4 (w < 4) or 5..8 (w >= 4)
+// flight: ONE barrier per image, as conv2_bwd_kernel): da3 in a zero-bordered 11x11 image (row
+// (oh + 2) * 11 + ow + 2), a2 as a 9 x 9 image in rows of 12 positions (ih * 12 + iw; pad
+// columns and rows zero, so an 8-position run of one lane group and the next group's run land
+// on disjoint banks: the wgrad transposed reads 2.0 -> 1.0 LDS cycles per conflict-free cycle
+// in tools/lds_bank_model.py), rows of 64 channels + 16 pad.  (The single-buffered form with
+// 72-element rows, three barriers per image and the dgrad tile staged through LDS spent 59 %
+// of its wave cycles parked, SQ_WAIT_ANY, and 58 % of its LDS cycles on bank conflicts:
+// profiles/r4_cnn_pmc.txt.  A chunk-swizzled da3 image cut the conflicts a further 84 % but
+// its per-read address arithmetic doubled the VALU work and the kernel did not speed up:
+// profiles/r4_cnn_swizzle_ab.txt.)
 namespace c3b {
 constexpr int kThreads = 512;
-constexpr int kYLd = 64, kXLd = 80, kXW = 12;
-constexpr int kD = 0;                          // da3 bordered [121][64], chunk-swizzled
-constexpr int kX = kD + 121 * kYLd;            // a2 [120][80]: (ih, iw) at row ih * 12 + iw
-constexpr int kBuf = kX + 120 * kXLd;          // elements per buffer (17,344)
-constexpr int kLds = 2 * kBuf * 2;             // 69,376 bytes
+#ifndef C3B_LD
+#define C3B_LD 80
+#endif
+constexpr int kLd = C3B_LD;
+constexpr int kD = 0;                        // da3 bordered [121][kLd]
+constexpr int kXW = 12;                      // a2 positions per LDS image row
+constexpr int kX = kD + 121 * kLd;           // a2 [120][kLd]: (ih, iw) at ih * 12 + iw
+constexpr int kBuf = kX + 120 * kLd;         // elements per buffer
+constexpr int kLds = 2 * kBuf * 2;           // 74,880 bytes at kLd = 80
 constexpr int kYC = 49 * 8, kXC = 81 * 8;  // 16-byte chunks per image
 constexpr int kYPT = (kYC + kThreads - 1) / kThreads, kXPT = (kXC + kThreads - 1) / kThreads;
-static_assert(kBuf % 8 == 0 && kX % 8 == 0, "16-byte aligned buffers");
-// element offset of channel col of bordered da3 position (y, x)
-__device__ __forceinline__ int yoff(int y, int x, int col) {
-  return (y * 11 + x) * kYLd + ((((col >> 3) ^ (y + x)) & 7) << 3) + (col & 7);
-}
+static_assert(kBuf % 8 == 0, "16-byte aligned buffers");
 }  // namespace c3b
-
-__device__ __forceinline__ bf16x8_t tr_frag2(const uint16_t* a0, const uint16_t* a1) {
-  typedef __attribute__((address_space(3))) s16x4_t lds_v4;
-  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0));
-  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a1));
-  typedef short s16x8_t __attribute__((ext_vector_type(8)));
-  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8_t, v);
-}
 
 __device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* a0, int ld) {
   typedef __attribute__((address_space(3))) s16x4_t lds_v4;
@@ -450,39 +430,37 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
   float bsum = 0.f;  // db3[tid & 63] over positions (tid >> 6) + 8 k
 
   uint4 ry[kYPT], rx[kXPT];
-  // gload / lstore take the thread index: inside the image loop an opaque copy, so their
-  // per-lane offsets are recomputed there rather than kept live (spilled) across the loop
-  auto gload = [&](int n, int tq) {
+  auto gload = [&](int n) {
     const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 49 * 64);
     const uint4* xs = reinterpret_cast<const uint4*>(xact + (size_t)n * 81 * 64);
 #pragma unroll
     for (int k = 0; k < kYPT; ++k) {
-      const int q = tq + kThreads * k;
+      const int q = tid + kThreads * k;
       ry[k] = q < kYC ? ys[q] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int k = 0; k < kXPT; ++k) {
-      const int q = tq + kThreads * k;
+      const int q = tid + kThreads * k;
       rx[k] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
     }
   };
-  auto lstore = [&](int buf, int tq) {
+  auto lstore = [&](int buf) {
     uint16_t* Y = smem + buf * kBuf + kD;
     uint16_t* X = smem + buf * kBuf + kX;
 #pragma unroll
     for (int k = 0; k < kYPT; ++k) {
-      const int q = tq + kThreads * k;
+      const int q = tid + kThreads * k;
       if (q < kYC) {
         const int pix = q >> 3, oh = pix / 7, ow = pix - oh * 7;
-        *reinterpret_cast<uint4*>(Y + yoff(oh + 2, ow + 2, (q & 7) * 8)) = ry[k];
+        *reinterpret_cast<uint4*>(Y + ((oh + 2) * 11 + ow + 2) * kLd + (q & 7) * 8) = ry[k];
       }
     }
 #pragma unroll
     for (int k = 0; k < kXPT; ++k) {
-      const int q = tq + kThreads * k;
+      const int q = tid + kThreads * k;
       if (q < kXC) {
         const int pix = q >> 3, ih = pix / 9, iw = pix - ih * 9;
-        *reinterpret_cast<uint4*>(X + (ih * kXW + iw) * kXLd + (q & 7) * 8) = rx[k];
+        *reinterpret_cast<uint4*>(X + (ih * kXW + iw) * kLd + (q & 7) * 8) = rx[k];
       }
     }
   };
@@ -490,36 +468,31 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
   const int G = gridDim.x, n0 = blockIdx.x;
   __syncthreads();  // zeroing done before the first image lands in buffer 0
   if (n0 < N) {
-    gload(n0, tid);
-    lstore(0, tid);
+    gload(n0);
+    lstore(0);
   }
-  if (n0 + G < N) gload(n0 + G, tid);
+  if (n0 + G < N) gload(n0 + G);
   for (int j = 0; n0 + j * G < N; ++j) {
     const int n = n0 + j * G;
-    int to = tid;
-    asm volatile("" : "+v"(to));
     __syncthreads();  // buffer j & 1 holds image n; buffer (j + 1) & 1 is no longer read
     if (n + G < N) {
-      lstore((j + 1) & 1, to);
-      if (n + 2 * G < N) gload(n + 2 * G, to);
+      lstore((j + 1) & 1);
+      if (n + 2 * G < N) gload(n + 2 * G);
     }
     const uint16_t* Yi = smem + (j & 1) * kBuf + kD;
     const uint16_t* Xi = smem + (j & 1) * kBuf + kX;
 
     // ---- wgrad: 2 position k-steps x (4 co tiles x ntap taps)
-    int go = g, qo = q4;  // opaque per image (see yb / xb below)
-    asm volatile("" : "+v"(go), "+v"(qo));
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int oh = 4 * s + g;  // this lane group's output row (7 = zero border)
       bf16x8_t af[4], bfr[NTAP];
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        af[c] = tr_frag2(Yi + yoff(4 * s + go + 2, 2 + qo, 16 * c + 4 * p4), Yi + yoff(4 * s + go + 2, 6 + qo, 16 * c + 4 * p4));
+      for (int c = 0; c < 4; ++c) af[c] = tr_frag(Yi + ((oh + 2) * 11 + 2 + q4) * kLd + 16 * c + 4 * p4, kLd);
 #pragma unroll
       for (int t = 0; t < NTAP; ++t) {
         const int tap = min(tap0 + t, 8), kh = tap / 3, kw = tap - kh * 3;
-        bfr[t] = tr_frag(Xi + ((oh + kh) * kXW + kw + q4) * kXLd + 16 * ct + 4 * p4, kXLd);
+        bfr[t] = tr_frag(Xi + ((oh + kh) * kXW + kw + q4) * kLd + 16 * ct + 4 * p4, kLd);
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c)
@@ -529,26 +502,22 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
     // ---- dgrad: k-step outer, this wave's 3 pixel tiles inner
     {
       f32x4_t acc[3];
-      int yb[3], xb[3];  // bordered da3 coordinates of the tap-(0, 0) source of this lane's pixel
+      int rb[3];
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
         acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         const int p = 16 * (3 * half + u) + i16;
         const int pc = p < 81 ? p : 0;
         const int ih = pc / 9, iw = pc - ih * 9;
-        yb[u] = ih + 2;
-        xb[u] = iw + 2;
-        // opaque per image: the 54 swizzled read addresses are formed next to their reads
-        // instead of being hoisted out of the image loop (98 spilled registers)
-        asm volatile("" : "+v"(yb[u]), "+v"(xb[u]));
+        rb[u] = (ih + 2) * 11 + (iw + 2);
       }
 #pragma unroll
       for (int ks = 0; ks < 18; ++ks) {
         const int t = ks >> 1, kh = t / 3, kw = t - kh * 3;
+        const int off = -(kh * 11 + kw) * kLd + (ks & 1) * 32 + 8 * g;
         bf16x8_t a[3];
 #pragma unroll
-        for (int u = 0; u < 3; ++u)
-          a[u] = *reinterpret_cast<const bf16x8_t*>(Yi + yoff(yb[u] - kh, xb[u] - kw, (ks & 1) * 32 + 8 * g));
+        for (int u = 0; u < 3; ++u) a[u] = *reinterpret_cast<const bf16x8_t*>(Yi + rb[u] * kLd + off);
 #pragma unroll
         for (int u = 0; u < 3; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], a[u], acc[u], 0, 0, 0);
       }
@@ -557,16 +526,16 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
       for (int u = 0; u < 3; ++u) {
         const int q = 16 * (3 * half + u) + i16;
         if (q < 81) {
-          const uint2 m = *reinterpret_cast<const uint2*>(Xi + ((q / 9) * kXW + q % 9) * kXLd + 16 * ct + 4 * g);
+          const uint2 m = *reinterpret_cast<const uint2*>(Xi + ((q / 9) * kXW + q % 9) * kLd + 16 * ct + 4 * g);
           *reinterpret_cast<uint2*>(dx + ((size_t)n * 81 + q) * 64 + 16 * ct + 4 * g) =
               make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x), relu_mask2(pk_bf16(acc[u][2], acc[u][3]), m.y));
         }
       }
     }
     // ---- db3
-    for (int pos = to >> 6; pos < 49; pos += 8) {
+    for (int pos = tid >> 6; pos < 49; pos += 8) {
       const int oh = pos / 7, ow = pos - oh * 7;
-      bsum += bf2f(Yi[yoff(oh + 2, ow + 2, to & 63)]);
+      bsum += bf2f(Yi[((oh + 2) * 11 + ow + 2) * kLd + (tid & 63)]);
     }
   }
   // this workgroup's weight-gradient partial: part[blk][co][tap][c]
@@ -601,16 +570,12 @@ extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16
 // LDS buffer j & 1, image j + 1 (prefetched into registers one iteration earlier) is written
 // into the other buffer and image j + 2's loads are in flight.
 //
-// LDS images per buffer (layouts chosen with tools/lds_bank_model.py --conv2; the previous
-// 72- / 40-element padded rows ran the dgrad reads at 2.71 and the transposed reads at 1.9-2.0
-// LDS cycles per conflict-free cycle, 54 % of the kernel's LDS cycles were conflicts:
-// profiles/r4_cnn_pmc.txt):
-//   da2  zero-bordered 12 x 12 (position (oh + 1, ow + 1)), 64 channels, no pad, the 16-byte
-//        chunk c of position (y, x) stored at chunk c ^ ((x + 2 y) & 7): dgrad b128 reads 1.14,
-//        wgrad transposed reads 1.88
+// LDS images per buffer:
+//   da2  zero-bordered 12 x 12 (row (oh + 1) * 12 + ow + 1; 64 co + 16 pad: tools/lds_bank_model.py
+//        --conv2; unpadded chunk-swizzled images cut the modelled LDS cycles 46 % more but their
+//        per-read address arithmetic made the kernel 25 % slower, profiles/r4_cnn_swizzle_ab.txt)
 //   a1   split into its four stride-2 phase images (ph, pw) = (ih & 1, iw & 1), each 10 x 10
-//        positions (row (ih >> 1) * 10 + (iw >> 1), rows 100..115 zero; 32 channels, no pad,
-//        chunk c of row y of the phase image at chunk c ^ (2 (y & 1))): transposed reads 1.31
+//        positions (row (ih >> 1) * 10 + (iw >> 1), rows 100..115 zero; 32 c + 8 pad)
 //   dgrad  da1[ph + 2a][pw + 2b][c] = sum_(i, j, co) da2[a - i][b - j][co] W2[co][ph + 2i][pw + 2j][c]
 //          per phase class a 100 px x 32 c GEMM over K = (4 taps x 64 co); wave w: class w >> 1,
 //          c tile w & 1, W2 fragments in registers.  The weights are the MFMA's A operand, so a
@@ -623,20 +588,22 @@ extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16
 //          rows); wave w: c block w & 1 of taps 4 (w >> 1) .. + 3, all 4 co tiles.
 namespace c2b {
 constexpr int kThreads = 512;
-constexpr int kDLd = 64, kPLd = 32;
+constexpr int kDLd = 80, kPLd = 40;  // 80: the dgrad b128 reads 2.71 -> 1.86 LDS cycles per conflict-free cycle (tools/lds_bank_model.py --conv2)
 constexpr int kDRows = 144, kPRows = 116;
-constexpr int kBuf = kDRows * kDLd + 4 * kPRows * kPLd;  // elements per buffer (24,064)
-constexpr int kLds = 2 * kBuf * 2;                       // 96,256 bytes
+constexpr int kBuf = kDRows * kDLd + 4 * kPRows * kPLd;  // elements per buffer (30,080)
+constexpr int kLds = 2 * kBuf * 2;                       // 120,320 bytes
 constexpr int kYC = 81 * 8, kXC = 400 * 4;               // 16-byte chunks per image
 constexpr int kYPT = (kYC + kThreads - 1) / kThreads, kXPT = (kXC + kThreads - 1) / kThreads;
-// element offsets: channel col of da2 position (y, x); of a1 phase image ph, position (y, x)
-__device__ __forceinline__ int doff(int y, int x, int col) {
-  return (y * 12 + x) * kDLd + ((((col >> 3) ^ (x + 2 * y)) & 7) << 3) + (col & 7);
-}
-__device__ __forceinline__ int poff(int ph, int y, int x, int col) {
-  return (ph * kPRows + y * 10 + x) * kPLd + ((((col >> 3) ^ (2 * y)) & 3) << 3) + (col & 7);
-}
 }  // namespace c2b
+
+__device__ __forceinline__ bf16x8_t tr_frag2(const uint16_t* a0, const uint16_t* a1) {
+  typedef __attribute__((address_space(3))) s16x4_t lds_v4;
+  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0));
+  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a1));
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
 
 // STAGED: da1 goes through an LDS tile [400][40] and leaves as 16-byte row chunks after a
 // second barrier, instead of 8-byte stores straight from the MFMA registers
@@ -679,39 +646,38 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
   float bsum = 0.f;  // db2[tid & 63] over positions (tid >> 6) + 8 k
 
   uint4 ry[kYPT], rx[kXPT];
-  // gload / lstore take the thread index: inside the image loop an opaque copy, so the
-  // per-lane offsets are recomputed there instead of being kept live (spilled) across it
-  auto gload = [&](int n, int tq) {
+  auto gload = [&](int n) {
     const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 81 * 64);
     const uint4* xs = reinterpret_cast<const uint4*>(xact + (size_t)n * 400 * 32);
 #pragma unroll
     for (int k = 0; k < kYPT; ++k) {
-      const int q = tq + kThreads * k;
+      const int q = tid + kThreads * k;
       ry[k] = q < kYC ? ys[q] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int k = 0; k < kXPT; ++k) {
-      const int q = tq + kThreads * k;
+      const int q = tid + kThreads * k;
       rx[k] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
     }
   };
-  auto lstore = [&](int buf, int tq) {
+  auto lstore = [&](int buf) {
     uint16_t* D = smem + buf * kBuf;
     uint16_t* P = D + kDRows * kDLd;
 #pragma unroll
     for (int k = 0; k < kYPT; ++k) {
-      const int q = tq + kThreads * k;
+      const int q = tid + kThreads * k;
       if (q < kYC) {
         const int pix = q >> 3, oh = pix / 9, ow = pix - oh * 9;
-        *reinterpret_cast<uint4*>(D + doff(oh + 1, ow + 1, (q & 7) * 8)) = ry[k];
+        *reinterpret_cast<uint4*>(D + ((oh + 1) * 12 + ow + 1) * kDLd + (q & 7) * 8) = ry[k];
       }
     }
 #pragma unroll
     for (int k = 0; k < kXPT; ++k) {
-      const int q = tq + kThreads * k;
+      const int q = tid + kThreads * k;
       if (q < kXC) {
         const int pix = q >> 2, ih = pix / 20, iw = pix - ih * 20;
-        *reinterpret_cast<uint4*>(P + poff((ih & 1) * 2 + (iw & 1), ih >> 1, iw >> 1, (q & 3) * 8)) = rx[k];
+        const int phase = (ih & 1) * 2 + (iw & 1);
+        *reinterpret_cast<uint4*>(P + (phase * kPRows + (ih >> 1) * 10 + (iw >> 1)) * kPLd + (q & 3) * 8) = rx[k];
       }
     }
   };
@@ -719,19 +685,16 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
   const int G = gridDim.x, n0 = blockIdx.x;
   __syncthreads();  // zeroing done before the first image lands in buffer 0
   if (n0 < N) {
-    gload(n0, tid);
-    lstore(0, tid);
+    gload(n0);
+    lstore(0);
   }
-  if (n0 + G < N) gload(n0 + G, tid);
+  if (n0 + G < N) gload(n0 + G);
   for (int j = 0; n0 + j * G < N; ++j) {
     const int n = n0 + j * G;
-    int to = tid;
-    asm volatile("" : "+v"(to));
-    const int go = (to & 63) >> 4, qo = (to >> 2) & 3, po = to & 3, io = to & 15;
     __syncthreads();  // buffer j & 1 holds image n; buffer (j + 1) & 1 is no longer read
     if (n + G < N) {
-      lstore((j + 1) & 1, to);
-      if (n + 2 * G < N) gload(n + 2 * G, to);
+      lstore((j + 1) & 1);
+      if (n + 2 * G < N) gload(n + 2 * G);
     }
     const uint16_t* D = smem + (j & 1) * kBuf;
     const uint16_t* P = D + kDRows * kDLd;
@@ -742,21 +705,21 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
       int oh[2], ow0[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int R = 2 * (4 * s + go) + h;  // run index; runs >= 27 read zero rows
+        const int R = 2 * (4 * s + g) + h;  // run index; runs >= 27 read zero rows
         oh[h] = R < 27 ? R / 3 : 9;
         ow0[h] = R < 27 ? 4 * (R % 3) : 0;
       }
       bf16x8_t af[4], bfr[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c)
-        af[c] = tr_frag2(D + doff(oh[0] + 1, ow0[0] + 1 + qo, 16 * c + 4 * po),
-                         D + doff(oh[1] + 1, ow0[1] + 1 + qo, 16 * c + 4 * po));
+        af[c] = tr_frag2(D + ((oh[0] + 1) * 12 + ow0[0] + 1 + q4) * kDLd + 16 * c + 4 * p4,
+                         D + ((oh[1] + 1) * 12 + ow0[1] + 1 + q4) * kDLd + 16 * c + 4 * p4);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int tau = tau0 + t, kh = tau >> 2, kw = tau & 3;
-        const int phs = (kh & 1) * 2 + (kw & 1);
-        bfr[t] = tr_frag2(P + poff(phs, oh[0] + (kh >> 1), ow0[0] + (kw >> 1) + qo, 16 * cb + 4 * po),
-                          P + poff(phs, oh[1] + (kh >> 1), ow0[1] + (kw >> 1) + qo, 16 * cb + 4 * po));
+        const uint16_t* Pp = P + ((kh & 1) * 2 + (kw & 1)) * kPRows * kPLd + 16 * cb + 4 * p4;
+        bfr[t] = tr_frag2(Pp + ((oh[0] + (kh >> 1)) * 10 + ow0[0] + (kw >> 1) + q4) * kPLd,
+                          Pp + ((oh[1] + (kh >> 1)) * 10 + ow0[1] + (kw >> 1) + q4) * kPLd);
       }
 #pragma unroll
       for (int c = 0; c < 4; ++c)
@@ -767,23 +730,22 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
     auto class_tiles = [&](auto tag) {
       constexpr int T0 = decltype(tag)::value, NT = T0 == 0 ? 4 : 3;
       f32x4_t acc[NT];
-      int ya[NT], xa[NT];  // da2 position of the tap-(0, 0) source of this lane's class pixel
+      int rb[NT];
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
         acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        const int p = 16 * (T0 + u) + io;
+        const int p = 16 * (T0 + u) + i16;
         const int pc = p < 100 ? p : 0;  // rows past the class are computed and discarded
         const int a = pc / 10, b = pc - a * 10;
-        ya[u] = a + 1;
-        xa[u] = b + 1;
+        rb[u] = (a + 1) * 12 + (b + 1);
       }
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
         const int t = ks >> 1, ti = t >> 1, tj = t & 1;
+        const int off = -(ti * 12 + tj) * kDLd + (ks & 1) * 32 + 8 * g;
         bf16x8_t bv[NT];
 #pragma unroll
-        for (int u = 0; u < NT; ++u)
-          bv[u] = *reinterpret_cast<const bf16x8_t*>(D + doff(ya[u] - ti, xa[u] - tj, (ks & 1) * 32 + 8 * go));
+        for (int u = 0; u < NT; ++u) bv[u] = *reinterpret_cast<const bf16x8_t*>(D + rb[u] * kDLd + off);
 #pragma unroll
         for (int u = 0; u < NT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], bv[u], acc[u], 0, 0, 0);
       }
@@ -793,7 +755,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
         const int p = 16 * (T0 + u) + i16;
         if (p < 100) {
           const int a = p / 10, b = p - a * 10;
-          const uint2 m = *reinterpret_cast<const uint2*>(P + poff(cls, a, b, 16 * ct + 4 * g));
+          const uint2 m = *reinterpret_cast<const uint2*>(P + (cls * kPRows + a * 10 + b) * kPLd + 16 * ct + 4 * g);
           const uint2 v = make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x),
                                      relu_mask2(pk_bf16(acc[u][2], acc[u][3]), m.y));
           const int pix = (ph + 2 * a) * 20 + pw + 2 * b;
@@ -805,9 +767,9 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
     class_tiles(std::integral_constant<int, 0>{});
     class_tiles(std::integral_constant<int, 4>{});
     // ---- db2
-    for (int pos = to >> 6; pos < 81; pos += 8) {
+    for (int pos = tid >> 6; pos < 81; pos += 8) {
       const int oh = pos / 9, ow = pos - oh * 9;
-      bsum += bf2f(D[doff(oh + 1, ow + 1, to & 63)]);
+      bsum += bf2f(D[((oh + 1) * 12 + ow + 1) * kDLd + (tid & 63)]);
     }
     if (STAGED) {
       __syncthreads();  // staging tile complete (rewritten only after the next top barrier)
@@ -831,7 +793,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
 extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
                              float* bias_part, int N, int grid, int staged, void* stream) {
   static bool attr = false;
-  constexpr int kStagedLds = c2b::kLds + 400 * 40 * 2;  // 147,712 bytes
+  constexpr int kStagedLds = c2b::kLds + 400 * 40 * 2;  // 152,320 bytes
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               c2b::kLds);

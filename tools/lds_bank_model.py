@@ -10,7 +10,12 @@ A group costs one LDS cycle per distinct address on its busiest bank; the number
 are LDS cycles per conflict-free cycle (1.0 = conflict-free).
 
     python tools/lds_bank_model.py            # conv3 backward: old vs shipped layouts
-    python tools/lds_bank_model.py --search   # the layout / swizzle search behind them
+    python tools/lds_bank_model.py --search   # the conv3 layout / swizzle search behind them
+    python tools/lds_bank_model.py --conv2    # the conv2 backward images
+
+A model, not a clock: the swizzled layouts it prefers need per-read XOR address arithmetic,
+which in these two-waves-per-SIMD kernels cost more than the conflicts they removed
+(profiles/r4_cnn_swizzle_ab.txt); the shipped layouts are the padding-only ones.
 """
 import sys
 
@@ -97,10 +102,12 @@ def main():
     none = lambda y, x: 0  # noqa: E731
     old_y = swz(lambda y, x: y * 11 + x, 72, none)
     old_x = swz(lambda y, x: y * 9 + x, 72, none)
-    new_y = swz(lambda y, x: y * 11 + x, 64, lambda y, x: y + x)
+    new_y = swz(lambda y, x: y * 11 + x, 80, none)
+    swz_y = swz(lambda y, x: y * 11 + x, 64, lambda y, x: y + x)
     new_x = swz(lambda y, x: y * 12 + x, 80, none)
     print("conv3_bwd da3 image (dgrad b128, wgrad tr, cycles):  old 11-wide/72 ->", conv3_bwd_da3(old_y),
-          " shipped 11-wide/64 + chunk ^ (y + x) ->", conv3_bwd_da3(new_y))
+          " shipped 11-wide/80 ->", conv3_bwd_da3(new_y), " swizzled 11-wide/64 + chunk ^ (y + x) (measured no",
+          "faster: its address arithmetic) ->", conv3_bwd_da3(swz_y))
     print("conv3_bwd a2 image (wgrad tr, cycles):                old 9-wide/72 ->", conv3_bwd_a2(old_x),
           " shipped 12-wide/80 ->", conv3_bwd_a2(new_x))
     if "--conv2" in sys.argv:

@@ -1,0 +1,12 @@
+# Round 4: padding-only LDS layouts of the conv backward kernels (after the swizzle A/B)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/prof_pong_e
+timeout -k 10 300 python -u -m pytest tests/test_cnn_gpu.py -q -x --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/cnn_tests.log 2>&1; rc=$?
+tail -3 gpurun_out/cnn_tests.log
+[ $rc -eq 0 ] || { grep -n "Error\|assert\|FAILED" gpurun_out/cnn_tests.log | head -20; exit $rc; }
+timeout -k 10 120 python -u tools/cnn_kbench.py --which fwd,bwd3,bwd2,wgrad1_8 > gpurun_out/kb_cnn_e.json 2>&1 && tail -1 gpurun_out/kb_cnn_e.json || exit 1
+timeout -k 10 300 python3 benchmarks/pong_a2c_bench.py --num-envs 2048 --steps 30 --warmup 3 > gpurun_out/pong_2048_e.json 2>&1 && tail -1 gpurun_out/pong_2048_e.json | cut -c1-200 || exit 1
+timeout -k 10 300 python3 benchmarks/pong_a2c_bench.py --num-envs 8192 --steps 20 --warmup 3 > gpurun_out/pong_8192_e.json 2>&1 && tail -1 gpurun_out/pong_8192_e.json | cut -c1-200 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_pong_e -o run -- \
+  python3 benchmarks/pong_a2c_bench.py --num-envs 2048 --steps 40 --warmup 3 > gpurun_out/prof_pong_e/log.txt 2>&1 && echo PROF_OK
