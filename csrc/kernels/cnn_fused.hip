@@ -61,13 +61,18 @@ namespace cs {
 constexpr int kThreads = 512;
 constexpr int kFrameLd = 80;                  // frame row: 64 channels + 16 pad (bf16)
 constexpr int kFrameRows = 441;               // 21 x 21 s2d pixels
+// the frame's 21 x 21 positions sit in LDS rows of 28 (position (a, b) at row 28 a + b): the
+// conv1 fragment reads of 16 consecutive output pixels then hit disjoint banks, 1.6 -> 1.0
+// LDS cycles per conflict-free cycle (tools/lds_bank_model.py --fwd)
+constexpr int kFrameW = 28;
+constexpr int kXiRows = 20 * kFrameW + 24;      // last position read: (20, 20)
 constexpr int kA1Ld = 40;                     // a1 row: 32 co + 8 pad
 constexpr int kA2Ld = 80;                     // a2 / a3 rows: 64 co + 16 pad (72 measured 2.5x conflict cycles on the conv3 reads, 80 1.75x)
 constexpr int kXi = 0;                                    // element offsets into LDS
-constexpr int kA1 = kXi + kFrameRows * kFrameLd;          // 35,280
-constexpr int kA2 = kA1 + 400 * kA1Ld;                    // 51,280 (two buffers of 81 rows)
-constexpr int kA3 = kA2 + 2 * 81 * kA2Ld;                 // 62,944
-constexpr int kLds = (kA3 + 49 * kA2Ld) * 2;              // 132,944 bytes
+constexpr int kA1 = kXi + kXiRows * kFrameLd;             // 46,720
+constexpr int kA2 = kA1 + 400 * kA1Ld;                    // 62,720 (two buffers of 81 rows)
+constexpr int kA3 = kA2 + 2 * 81 * kA2Ld;                 // 75,680
+constexpr int kLds = (kA3 + 49 * kA2Ld) * 2;              // 159,200 bytes
 constexpr int kXChunks = kFrameRows * 64 / 16;           // 16-byte chunks of one uint8 frame (1,764)
 constexpr int kXPerT = (kXChunks + kThreads - 1) / kThreads;
 static_assert(kA1 % 8 == 0 && kA2 % 8 == 0 && kA3 % 8 == 0, "16-byte aligned LDS regions");
@@ -84,7 +89,7 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
     uint16_t* __restrict__ y3, int N) {
   using namespace cs;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* Xi = smem + kXi;  // [441][80] frame as bf16 integers 0..255
+  uint16_t* Xi = smem + kXi;  // [21 x 28][80] frame as bf16 integers 0..255
   uint16_t* A1 = smem + kA1;  // [400][40] conv1 output
   uint16_t* A3 = smem + kA3;  // [49][72]  conv3 output
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -141,7 +146,8 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
       for (int k = 0; k < kXPerT; ++k) {
         const int q = tid + kThreads * k;
         if (q < kXChunks) {
-          uint16_t* d = Xi + (q >> 2) * kFrameLd + (q & 3) * 16;
+          const int pix = q >> 2, pa = pix / 21;
+          uint16_t* d = Xi + (pix + (kFrameW - 21) * pa) * kFrameLd + (q & 3) * 16;
           *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(rx[k].x, rx[k].y));
           *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(rx[k].z, rx[k].w));
         }
@@ -168,13 +174,13 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
       for (int t = 0; t < MT; ++t) {
         acc0[t] = acc1[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         const int p = 16 * min(wave + 8 * t, 24) + i;
-        r0[t] = (p / 20) * 21 + p % 20;
+        r0[t] = (p / 20) * kFrameW + p % 20;
       }
       const int nt = wave == 0 ? 4 : 3;  // wave-uniform
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
         const int tap = ks >> 1;
-        const int off = ((tap >> 1) * 21 + (tap & 1)) * kFrameLd + 32 * (ks & 1) + 8 * g;
+        const int off = ((tap >> 1) * kFrameW + (tap & 1)) * kFrameLd + 32 * (ks & 1) + 8 * g;
         bf16x8_t a[MT];
 #pragma unroll
         for (int t = 0; t < MT; ++t)
@@ -207,13 +213,13 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
         acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
         const int mt = min((wave >> 1) + 4 * t, 24);  // a tile past the frame recomputes tile 24
         const int p = 16 * mt + i;
-        r0[t] = (p / 20) * 21 + p % 20;  // frame row of tap (0, 0)
+        r0[t] = (p / 20) * kFrameW + p % 20;  // frame row of tap (0, 0)
       }
       // k-step outer, tiles inner: MT independent MFMAs per k-step, their reads batched ahead
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
         const int tap = ks >> 1;
-        const int off = ((tap >> 1) * 21 + (tap & 1)) * kFrameLd + 32 * (ks & 1) + 8 * g;
+        const int off = ((tap >> 1) * kFrameW + (tap & 1)) * kFrameLd + 32 * (ks & 1) + 8 * g;
         bf16x8_t a[MT];
 #pragma unroll
         for (int t = 0; t < MT; ++t) a[t] = *reinterpret_cast<const bf16x8_t*>(Xi + r0[t] * kFrameLd + off);

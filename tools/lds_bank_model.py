@@ -12,6 +12,7 @@ are LDS cycles per conflict-free cycle (1.0 = conflict-free).
     python tools/lds_bank_model.py            # conv3 backward: old vs shipped layouts
     python tools/lds_bank_model.py --search   # the conv3 layout / swizzle search behind them
     python tools/lds_bank_model.py --conv2    # the conv2 backward images
+    python tools/lds_bank_model.py --fwd      # the fused forward's frame image (conv1 reads)
 
 A model, not a clock: the swizzled layouts it prefers need per-read XOR address arithmetic,
 which in these two-waves-per-SIMD kernels cost more than the conflicts they removed
@@ -112,6 +113,9 @@ def main():
           " shipped 12-wide/80 ->", conv3_bwd_a2(new_x))
     if "--conv2" in sys.argv:
         search_conv2()
+    if "--fwd" in sys.argv:
+        print("conv_stack_fwd conv1 frame reads (ld, row width -> factor):",
+              {(ld, W): conv_stack_fwd_conv1(ld, W) for ld in (72, 80, 88) for W in (21, 24, 28, 32)})
     if "--search" in sys.argv:
         res = []
         for ld in (64, 72, 80, 88):
@@ -227,6 +231,21 @@ def search_conv2():
     res.sort()
     for r in res[:6]:
         print("  ", r)
+
+
+def conv_stack_fwd_conv1(ld, W):
+    """b128 factor of conv1's frame fragment reads, frame positions (a, b) at LDS row W a + b"""
+    r = []
+    for t in range(25):
+        for ks in range(8):
+            tap = ks >> 1
+            addr = []
+            for i16, g, q4, p4 in lanes():
+                p = 16 * t + i16
+                row = (p // 20 + (tap >> 1)) * W + p % 20 + (tap & 1)
+                addr.append(2 * (row * ld + 32 * (ks & 1) + 8 * g))
+            r.append(b128(addr))
+    return round(sum(r) / len(r), 2)
 
 
 if __name__ == "__main__":

@@ -1,4 +1,4 @@
-# Round 4: padding-only LDS layouts of the conv backward kernels (after the swizzle A/B)
+# Round 4: padding-only LDS layouts of the conv backward kernels (after the swizzle A/B), 28-wide frame rows in the fused forward
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/prof_pong_e
