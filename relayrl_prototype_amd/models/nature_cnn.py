@@ -204,6 +204,11 @@ class DeviceNatureCNN:
         # captured update graph holds this storage, so it must never be reallocated
         fc_rows = max(self.fc_splits(n) * n for n in range(1, self.max_batch + 1)) if self.fc_nt else 0
         self._fc_part = torch.empty(fc_rows * HIDDEN, device=dev) if self.fc_nt else None
+        # rollout fc + head in one GEMM launch over the full K with per-column-tile head
+        # partials (fc.hip fc_head_kernel) instead of split-K partials + the head's reduction;
+        # RRL_FC_HEAD=0 keeps the split-K form (A <= 7)
+        self.fc_head = self.fc_nt and self.A <= 7 and os.environ.get("RRL_FC_HEAD", "1") != "0"
+        self._head_part = torch.empty((HIDDEN // 64) * self.max_batch * 8, device=dev) if self.fc_head else None
         self.refresh_shadow()
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params)
@@ -295,6 +300,13 @@ class DeviceNatureCNN:
         """fc GEMM as split-K partials, then ONE head launch: bias + ReLU + bf16 hid (stored for
         the backward) + logits / value / sampling."""
         o = self.o
+        if self.fc_head:
+            self.h.fc_head_rollout(a3, self.shadow[o["wfc"]:o["bfc"]], self.params[o["bfc"]:o["bfc"] + HIDDEN],
+                                   self.params[o["head"]:], hid, self._head_part, n, self.A, act=head.get("act"),
+                                   logp=head.get("logp"), value=head.get("value"), logits=head.get("logits"),
+                                   seed=int(head.get("seed", 0)), step=int(head.get("step", 0)),
+                                   row_offset=int(head.get("row_offset", 0)), step_base=head.get("step_base"))
+            return
         s = self.fc_splits(n)
         assert s * n * HIDDEN <= self._fc_part.numel(), "fc split-K partials exceed the preallocated buffer"
         used = int(self.h.fc_nt_part(a3, self.shadow[o["wfc"]:o["bfc"]], self._fc_part, n, HIDDEN, FC_IN, s))

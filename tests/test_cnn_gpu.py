@@ -626,6 +626,42 @@ def test_fc_head_fused_matches_separate(cuda, B, monkeypatch):
     assert (a1 != a2).float().mean().item() < 0.01
 
 
+@pytest.mark.parametrize("B", [48, 130, 2048])
+def test_fc_head_rollout_matches_splitk_head(cuda, B, monkeypatch):
+    """The rollout fc + head as ONE full-K GEMM launch with per-column-tile head partials and a
+    finishing kernel (RRL_FC_HEAD=1, the default: fc.hip fc_head_kernel + cnn.hip
+    a2c_head_finish_kernel) vs split-K partials reduced in the head launch (RRL_FC_HEAD=0):
+    same stored hidden units (to one bf16 rounding), value / log-prob / logits within fp32
+    summation order, the same sampled actions (same Philox stream) but for near-ties."""
+    spec = CNNSpec(6)
+    params = spec.init(11)
+    o = spec.offsets()
+    params[o["wpi"]:o["bpi"]] *= 30.0
+    params[o["bfc"]:o["bfc"] + HIDDEN] += 0.05  # non-zero fc bias
+    g = torch.Generator().manual_seed(B + 1)
+    obs = torch.randint(0, 256, (B, 21, 21, 64), dtype=torch.uint8, generator=g).to(cuda)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("RRL_FC_HEAD", flag)
+        m = DeviceNatureCNN(spec, cuda, max_batch=B, params=params)
+        assert m.fc_head == (flag == "1")
+        act = torch.full((B,), -1, dtype=torch.int32, device=cuda)
+        logp = torch.full((B,), float("nan"), device=cuda)
+        val = torch.full((B,), float("nan"), device=cuda)
+        m.act(obs, 0, act, logp, val, seed=5, step=3)
+        lg, vv = m.logits(obs)
+        torch.cuda.synchronize()
+        outs.append((act.cpu(), logp.cpu(), val.cpu(), m.hid[:B * HIDDEN].float().cpu(), lg.cpu(), vv.cpu()))
+    (a1, l1, v1, h1, g1, w1), (a2, l2, v2, h2, g2, w2) = outs
+    assert torch.isfinite(l1).all() and torch.isfinite(v1).all() and (a1 >= 0).all() and (a1 < 6).all()
+    assert relerr(h1, h2) < 5e-3
+    assert torch.allclose(v1, v2, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(w1, w2, atol=1e-3, rtol=1e-3)
+    assert torch.allclose(g1, g2, atol=2e-3, rtol=1e-3)
+    assert torch.allclose(l1, l2, atol=1e-3)
+    assert (a1 != a2).float().mean().item() < 0.01
+
+
 @pytest.mark.parametrize("R,I,J,splits", [(64, 512, 3136, 1), (640, 512, 3136, 5), (10240, 512, 3136, 5),
                                           (192, 136, 72, 2)])
 def test_fc_tn_part_matches_fp32(cuda, R, I, J, splits):
