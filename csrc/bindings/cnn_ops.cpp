@@ -126,7 +126,7 @@ void conv_fwd(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& y
 // a1 [N][20][20][32], a2 [N][9][9][64], a3 [N][7][7][64] (bf16, post-ReLU).
 void conv_stack_fwd(const Tensor& x, const Tensor& w1, const Tensor& b1, const Tensor& w2, const Tensor& b2,
                     const Tensor& w3, const Tensor& b3, const Tensor& y1, const Tensor& y2, const Tensor& y3,
-                    int64_t N, int64_t probe, int64_t grid) {
+                    int64_t N, int64_t probe, int64_t grid, bool store12) {
   TORCH_CHECK(N > 0, "conv_stack_fwd: N must be positive");
   check(x, "x", at::kByte, N * 21 * 21 * 64);
   check(w1, "w1", at::kBFloat16, 32 * 256);
@@ -142,7 +142,8 @@ void conv_stack_fwd(const Tensor& x, const Tensor& w1, const Tensor& b1, const T
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   rc_check(rrl_conv_stack_fwd(x.data_ptr<uint8_t>(), bf(w1), b1.data_ptr<float>(), bf(w2), b2.data_ptr<float>(),
-                              bf(w3), b3.data_ptr<float>(), bf(y1), bf(y2), bf(y3), (int)N,
+                              bf(w3), b3.data_ptr<float>(), store12 ? bf(y1) : nullptr, store12 ? bf(y2) : nullptr,
+                              bf(y3), (int)N,
                               probe > 0 ? -(int)((probe << 16) | (grid > 0 ? grid : cus))
                                         : (grid > 0 ? (int)grid : cus),
                               stream()),
@@ -499,7 +500,7 @@ void register_cnn_ops(pybind11::module_& m) {
   m.def("conv_stack_fwd", &conv_stack_fwd, pybind11::arg("x"), pybind11::arg("w1"), pybind11::arg("b1"),
         pybind11::arg("w2"), pybind11::arg("b2"), pybind11::arg("w3"), pybind11::arg("b3"), pybind11::arg("y1"),
         pybind11::arg("y2"), pybind11::arg("y3"), pybind11::arg("N"), pybind11::arg("probe") = 0,
-        pybind11::arg("grid") = 0);
+        pybind11::arg("grid") = 0, pybind11::arg("store12") = true);
   m.def("conv3_bwd", &conv3_bwd);
   m.def("conv2_bwd", &conv2_bwd, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("xact"), pybind11::arg("dx"),
         pybind11::arg("part"), pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"),

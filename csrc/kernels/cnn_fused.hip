@@ -156,7 +156,7 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
     }
     __syncthreads();  // B1
     // copy-outs of the previous iterations' a2 / a3 (conv1 touches neither buffer)
-    if (prev && !(PROBE & 2)) {
+    if (prev && y2 && !(PROBE & 2)) {  // y2 / y1 null: a forward whose activations no backward reads
       const uint16_t* A2p = smem + kA2 + ((j - 1) & 1) * 81 * kA2Ld;
       uint4* yd = reinterpret_cast<uint4*>(y2 + (size_t)(n - G) * 81 * 64);
       for (int q = tid; q < 81 * 8; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A2p + (q >> 3) * kA2Ld + (q & 7) * 8);
@@ -239,7 +239,7 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
       }
     }
     __syncthreads();  // B2: a1(n) complete
-    if (cur && !(PROBE & 2)) {
+    if (cur && y1 && !(PROBE & 2)) {
       uint4* yd = reinterpret_cast<uint4*>(y1 + (size_t)n * 400 * 32);
       for (int q = tid; q < 400 * 4; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A1 + (q >> 2) * kA1Ld + (q & 3) * 8);
     }

@@ -316,10 +316,11 @@ class DeviceNatureCNN:
                         max(1, min(1024, (n + 3) // 4)), head.get("step_base"), part=self._fc_part, splits=used,
                         fc_b=self.params[o["bfc"]:o["bfc"] + HIDDEN])
 
-    def forward(self, obs_u8: torch.Tensor, row0: int = 0, fc: bool = True):
+    def forward(self, obs_u8: torch.Tensor, row0: int = 0, fc: bool = True, store_acts: bool = True):
         """Conv stack + fc on obs [n, 84, 84, 4]; activations land in rows row0.. of the
         stored buffers.  Returns the hidden [n * 512] view (with fc=False only the conv
-        stack runs and the view is not written yet)."""
+        stack runs and the view is not written yet).  store_acts=False: a1 / a2 are not
+        written (a forward no backward reads, e.g. the bootstrap value; fused path only)."""
         n = obs_u8.shape[0]
         assert row0 + n <= self.max_batch, "batch exceeds the model's activation buffers"
         h, o, sh, p = self.h, self.o, self.shadow, self.params
@@ -334,7 +335,7 @@ class DeviceNatureCNN:
             # conv1 -> conv2 -> conv3 in one launch, activations LDS-resident (cnn_fused.hip)
             h.conv_stack_fwd(x, *(t for i in (1, 2, 3) for t in (sh[o[f"w{i}"]:o[f"b{i}"]],
                                                                      p[o[f"b{i}"]:o[f"b{i}"] + CONVS[i - 1].cout])),
-                             a1, a2, a3, n)
+                             a1, a2, a3, n, store12=store_acts)
         else:
             for i, (L, y) in enumerate(zip((S2D,) + CONVS[1:], (a1, a2, a3)), 1):
                 h.conv_fwd(x, sh[o[f"w{i}"]:o[f"b{i}"]], p[o[f"b{i}"]:o[f"b{i}"] + L.cout], y, n, L.hin, L.hin,
@@ -345,10 +346,10 @@ class DeviceNatureCNN:
                        HIDDEN, True, self.part)  # split-K when the batch is too small to fill the chip
         return hid
 
-    def _forward_head(self, obs_u8, row0, **head):
+    def _forward_head(self, obs_u8, row0, store_acts=True, **head):
         n = obs_u8.shape[0]
         if self.fc_nt:
-            hid = self.forward(obs_u8, row0, fc=False)
+            hid = self.forward(obs_u8, row0, fc=False, store_acts=store_acts)
             self._fc_head(self._rows(self.a3, row0, n, FC_IN), hid, n, **head)
             return
         hid = self.forward(obs_u8, row0)
@@ -364,7 +365,8 @@ class DeviceNatureCNN:
                            row_offset=row_offset, step_base=step_base)
 
     def value(self, obs_u8, row0, value_out):
-        self._forward_head(obs_u8, row0, value=value_out)
+        """V(obs) into value_out (the rollout's bootstrap): no a1 / a2 stores, no backward reads them."""
+        self._forward_head(obs_u8, row0, store_acts=False, value=value_out)
 
     def logits(self, obs_u8):
         n = obs_u8.shape[0]
