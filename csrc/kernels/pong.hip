@@ -49,18 +49,16 @@ RRL_DEV void reset_env(float* s, uint4 r) {
 
 // One env's step (frame-skip 4); state row written back.  Shared by pong_step_kernel (one
 // thread per env) and pong_step_render_kernel (one workgroup per env).
-RRL_DEV void pong_step_env(int e, float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew,
-                           float* __restrict__ done, float* __restrict__ fin_ret, float* __restrict__ fin_len,
-                           float* __restrict__ ep_acc, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
-                           int reset_all, const unsigned long long* __restrict__ step_base) {
+// s: the env's state row, in registers (pong_step_env) or in LDS (pong_step_render_kernel).
+RRL_DEV void pong_step_state(int e, float* s, const int32_t* __restrict__ act, float* __restrict__ rew,
+                             float* __restrict__ done, float* __restrict__ fin_ret, float* __restrict__ fin_len,
+                             float* __restrict__ ep_acc, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
+                             int reset_all, const unsigned long long* __restrict__ step_base) {
   if (step_base) {  // device step counter (graph replays): the host value is an offset
     const unsigned long long st = (((unsigned long long)step_hi << 32) | step_lo) + *step_base;
     step_lo = (uint32_t)st;
     step_hi = (uint32_t)(st >> 32);
   }
-  float s[kPongState];
-#pragma unroll
-  for (int i = 0; i < kPongState; ++i) s[i] = state[(size_t)e * kPongState + i];
   const uint4 r0 = philox4x32(make_uint4((uint32_t)e, step_lo, step_hi, 0x51u), key);
   if (reset_all) {
     reset_env(s, r0);
@@ -122,6 +120,17 @@ RRL_DEV void pong_step_env(int e, float* __restrict__ state, const int32_t* __re
       reset_env(s, r1);
     }
   }
+}
+
+RRL_DEV void pong_step_env(int e, float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew,
+                           float* __restrict__ done, float* __restrict__ fin_ret, float* __restrict__ fin_len,
+                           float* __restrict__ ep_acc, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
+                           int reset_all, const unsigned long long* __restrict__ step_base) {
+  float s[kPongState];
+#pragma unroll
+  for (int i = 0; i < kPongState; ++i) s[i] = state[(size_t)e * kPongState + i];
+  pong_step_state(e, s, act, rew, done, fin_ret, fin_len, ep_acc, key, step_lo, step_hi, max_steps, reset_all,
+                  step_base);
 #pragma unroll
   for (int i = 0; i < kPongState; ++i) state[(size_t)e * kPongState + i] = s[i];
 }
@@ -182,6 +191,50 @@ RRL_DEV uint4 pong_render_chunk(const float* h, int q) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// The row-only half of pong_render_chunk, once per image row y (84 per env instead of once per
+// chunk: 21 chunks share a row): bit f = ball on the row in frame f, 4 + f = agent paddle,
+// 8 + f = opponent paddle, 12 = wall.  Same float comparisons, so the render stays bitwise.
+RRL_DEV uint32_t pong_row_flags(const float* h, int y) {
+  const float fy = (float)y + 0.5f;
+  uint32_t m = (fy < kTop || fy >= kBot) ? (1u << 12) : 0u;
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const float by = h[4 * f + 1], pa = h[4 * f + 2], po = h[4 * f + 3];
+    if (fy >= by && fy < by + kBall) m |= 1u << f;
+    if (fabsf(fy - pa) < kPadHalf) m |= 1u << (4 + f);
+    if (fabsf(fy - po) < kPadHalf) m |= 1u << (8 + f);
+  }
+  return m;
+}
+
+// pong_render_chunk from the per-row flags: an unlit row (most of the screen) is one LDS read
+// and a constant; lit rows keep only the per-pixel x tests.
+RRL_DEV uint4 pong_render_chunk_rows(const float* h, const uint32_t* rows, int q) {
+  const int a = q / 84, rem = q - a * 84, c = rem >> 2, dy = rem & 3;
+  const uint32_t m = rows[4 * a + dy];
+  const bool wall = (m >> 12) & 1u;
+  if ((m & 0xfffu) == 0u) {
+    const uint32_t v = wall ? 0x64646464u : 0u;
+    return make_uint4(v, v, v, v);
+  }
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const float bx = h[4 * f];
+    const bool b_on = (m >> f) & 1u, pa_on = (m >> (4 + f)) & 1u, po_on = (m >> (8 + f)) & 1u;
+#pragma unroll
+    for (int px = 0; px < 4; ++px) {
+      const float fx = (float)(4 * c + px) + 0.5f;
+      uint32_t v = wall ? 100u : 0u;
+      if (pa_on && fx >= kAgentX && fx < kAgentX + kPadW) v = 255u;
+      if (po_on && fx >= kOppX && fx < kOppX + kPadW) v = 255u;
+      if (b_on && fx >= bx && fx < bx + kBall) v = 255u;
+      w[px] |= v << (8 * f);
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 __global__ void pong_render_kernel(const float* __restrict__ state, uint8_t* __restrict__ obs, int N) {
   constexpr int kChunks = kPongHW * kPongHW * 4 / 16;  // 1764 per env
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -193,25 +246,33 @@ __global__ void pong_render_kernel(const float* __restrict__ state, uint8_t* __r
 // Step + render in one launch: workgroup e steps env e on one thread (the physics is a short
 // serial chain) and renders its 1,764 chunks on all 256 threads from the new history in LDS.
 // One launch per env step instead of two, and the tiny step kernel's own launch / drain is gone.
-__global__ void __launch_bounds__(256) pong_step_render_kernel(
+__global__ void __launch_bounds__(256, 8) pong_step_render_kernel(
     float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew, float* __restrict__ done,
     float* __restrict__ fin_ret, float* __restrict__ fin_len, float* __restrict__ ep_acc, uint8_t* __restrict__ obs,
     uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps, int reset_all,
     const unsigned long long* __restrict__ step_base) {
   constexpr int kChunks = kPongHW * kPongHW * 4 / 16;
-  __shared__ float hist[16];
-  const int e = blockIdx.x;
-  if (threadIdx.x == 0) {
-    pong_step_env(e, state, act, rew, done, fin_ret, fin_len, ep_acc, key, step_lo, step_hi, max_steps, reset_all,
-                  step_base);
-    // the new history to LDS by the thread that wrote it (its own global writes, program order)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) hist[i] = state[(size_t)e * kPongState + P_HIST + i];
-  }
+  __shared__ float ss[kPongState];
+  __shared__ uint32_t rows[kPongHW];
+  const int e = blockIdx.x, t = threadIdx.x;
+  // the state row moves in and out as one coalesced access and thread 0 steps it in LDS: held
+  // in registers it set the kernel at 67 VGPRs = 7 waves per SIMD, so 1/8 of the 2,048
+  // workgroups of a step waited for a second round
+  if (t < kPongState) ss[t] = state[(size_t)e * kPongState + t];
+  __syncthreads();
+  if (t == 0)
+    pong_step_state(e, ss, act, rew, done, fin_ret, fin_len, ep_acc, key, step_lo, step_hi, max_steps, reset_all,
+                    step_base);
+  __syncthreads();
+  if (t < kPongState) state[(size_t)e * kPongState + t] = ss[t];
+  const float* hist = ss + P_HIST;
+  // the render is VALU-bound (every chunk re-tested its row against 12 objects): the row tests
+  // once per row here, the chunks then read them (21 chunks per row)
+  if (t < kPongHW) rows[t] = pong_row_flags(hist, t);
   __syncthreads();
   uint8_t* o = obs + (size_t)e * kChunks * 16;
   for (int q = threadIdx.x; q < kChunks; q += 256)
-    *reinterpret_cast<uint4*>(o + (size_t)q * 16) = pong_render_chunk(hist, q);
+    *reinterpret_cast<uint4*>(o + (size_t)q * 16) = pong_render_chunk_rows(hist, rows, q);
 }
 
 }  // namespace rrl
