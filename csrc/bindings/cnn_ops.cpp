@@ -68,6 +68,8 @@ int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, u
                   float* bias_part, int N, int grid, int staged, void* stream);
 int rrl_conv1_wgrad8(const uint8_t* x, const uint16_t* dy, float* part, float* bias_part, int N, int grid,
                      void* stream);
+int rrl_conv21_bwd(const uint16_t* dy2, const uint16_t* w2, const uint16_t* a1, const uint8_t* x, float* part2,
+                   float* bias2, float* part1, float* bias1, int N, int grid, void* stream);
 }
 
 namespace {
@@ -195,6 +197,28 @@ int64_t conv1_wgrad8(const Tensor& x, const Tensor& dy, const Tensor& part, cons
                             (int)grid, stream()),
            "conv1_wgrad8");
   return 2 * grid;
+}
+
+// conv2 backward + conv1 weight gradient in one pass per image (cnn_fused.hip conv21_bwd_kernel):
+// da2 [N][81][64], W2, a1 [N][400][32], s2d frames [N][21][21][64] -> dW2 partials [grid][64 * 512],
+// db2 partials [grid * 8][64], dW1 partials [grid][32 * 256], db1 partials [grid][32]; da1 never
+// leaves LDS.  Returns the slab count of either layer (grid).
+int64_t conv21_bwd(const Tensor& dy2, const Tensor& w2, const Tensor& a1, const Tensor& x, const Tensor& part2,
+                   const Tensor& bias2, const Tensor& part1, const Tensor& bias1, int64_t N, int64_t grid) {
+  TORCH_CHECK(N > 0 && grid > 0 && grid <= N, "conv21_bwd: need 0 < grid <= N");
+  check(dy2, "dy2", at::kBFloat16, N * 81 * 64);
+  check(w2, "w2", at::kBFloat16, 64 * 512);
+  check(a1, "a1", at::kBFloat16, N * 400 * 32);
+  check(x, "x", at::kByte, N * 441 * 64);
+  check(part2, "part2", at::kFloat, grid * 64 * 512);
+  check(bias2, "bias2", at::kFloat, grid * 512);
+  check(part1, "part1", at::kFloat, grid * 32 * 256);
+  check(bias1, "bias1", at::kFloat, grid * 32);
+  const int rc = rrl_conv21_bwd(bf(dy2), bf(w2), bf(a1), x.data_ptr<uint8_t>(), part2.data_ptr<float>(),
+                                bias2.data_ptr<float>(), part1.data_ptr<float>(), bias1.data_ptr<float>(), (int)N,
+                                (int)grid, stream());
+  TORCH_CHECK(rc == grid, "conv21_bwd failed with code ", rc);
+  return rc;
 }
 
 void gemm_dgrad(const Tensor& dy, const Tensor& w, const OptT& mask, const Tensor& out, int64_t M, int64_t Cout,
@@ -502,6 +526,7 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("y2"), pybind11::arg("y3"), pybind11::arg("N"), pybind11::arg("probe") = 0,
         pybind11::arg("grid") = 0, pybind11::arg("store12") = true);
   m.def("conv3_bwd", &conv3_bwd);
+  m.def("conv21_bwd", &conv21_bwd);
   m.def("conv2_bwd", &conv2_bwd, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("xact"), pybind11::arg("dx"),
         pybind11::arg("part"), pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"),
         pybind11::arg("staged") = 0);

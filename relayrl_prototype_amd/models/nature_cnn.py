@@ -248,6 +248,8 @@ class DeviceNatureCNN:
         self.part = torch.empty(need, device=dev)
         self.bias_splits = 512
         self.bias_part = torch.empty(max(self.bias_splits * HIDDEN, self.cus * 512), device=dev)
+        # conv2 backward + conv1 weight gradient fused (RRL_CONV21=0: the two separate kernels)
+        self.conv21 = os.environ.get("RRL_CONV21", "1") != "0"
         if self.fused_convs:
             # per-layer partial slabs of the fused conv backward kernels, summed together in ONE
             # launch at the end of the backward (sum_splits_multi)
@@ -461,7 +463,18 @@ class DeviceNatureCNN:
             self._dgrad(da3, sh[o["w3"]:o["b3"]], a2, da2, B, L3)
         # conv2
         da1 = self.da1[:B * L1.hout ** 2 * L1.cout]
-        if self.fused_convs:
+        if self.fused_convs and self.conv21:
+            # conv2's dgrad + wgrad + bias and conv1's wgrad + bias in one pass per image: da1
+            # stays in LDS (cnn_fused.hip conv21_bwd_kernel)
+            nblk = min(B, self.cus)
+            ns = int(h.conv21_bwd(da2, sh[o["w2"]:o["b2"]], a1, obs_u8.contiguous(), self.cpart["c2"], self.cbias["c2"],
+                                  self.cpart["c1"], self.cbias["c1"], B, nblk))
+            sums += [(self.cpart["c2"], nblk, L2.cout * L2.K, g[o["w2"]:o["b2"]]),
+                     (self.cbias["c2"], nblk * 8, L2.cout, g[o["b2"]:o["b2"] + L2.cout]),
+                     (self.cpart["c1"], ns, S2D.cout * S2D.K, g[o["w1"]:o["b1"]]),
+                     (self.cbias["c1"], ns, S2D.cout, g[o["b1"]:o["b1"] + S2D.cout])]
+            h.sum_splits_multi(sums)
+        elif self.fused_convs:
             nblk = min(B, self.cus)
             h.conv2_bwd(da2, sh[o["w2"]:o["b2"]], a1, da1, self.cpart["c2"], self.cbias["c2"], B, nblk)
             sums += [(self.cpart["c2"], nblk, L2.cout * L2.K, g[o["w2"]:o["b2"]]),
@@ -470,15 +483,15 @@ class DeviceNatureCNN:
             self._wgrad("c2", da2, a1, B, L2.hin, L2.cin, L2.k, L2.s, L2.cout, o["w2"])
             self._bias(da2, B * L2.hout ** 2, L2.cout, o["b2"])
             self._dgrad(da2, sh[o["w2"]:o["b2"]], a1, da1, B, L2)
-        # conv1 (input = frames, no data gradient)
+        # conv1 (input = frames, no data gradient; with conv21 it ran above)
         # (its bias gradient comes out of the same pass over da1)
-        if self.fused_convs:
+        if self.fused_convs and not self.conv21:
             ns = int(h.conv1_wgrad8(obs_u8.contiguous(), da1, self.cpart["c1"], self.cbias["c1"], B,
                                     min(B, self.cus)))
             sums += [(self.cpart["c1"], ns, S2D.cout * S2D.K, g[o["w1"]:o["b1"]]),
                      (self.cbias["c1"], ns, S2D.cout, g[o["b1"]:o["b1"] + S2D.cout])]
             h.sum_splits_multi(sums)
-        else:
+        elif not self.fused_convs:
             self._wgrad("c1", da1, obs_u8.contiguous(), B, S2D.hin, S2D.cin, S2D.k, S2D.s, S2D.cout, o["w1"],
                         bias_off=o["b1"])
         if side is not None:

@@ -555,6 +555,38 @@ def test_conv1_wgrad8_matches_autograd(cuda, N, grid):
     assert relerr(db, dy.sum((0, 1, 2))) < 1e-3
 
 
+@pytest.mark.parametrize("N,grid", [(3, 3), (70, 16), (300, 64), (1500, 256)])
+def test_conv21_bwd_matches_separate_kernels(cuda, N, grid):
+    """conv2 backward + conv1 weight gradient in one pass (conv21_bwd_kernel: da1 stays in LDS)
+    against conv2_bwd_kernel + conv1_wgrad8_kernel on the same inputs: dW2, db2, dW1, db1."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    g = torch.Generator().manual_seed(N + grid)
+    x = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g).to(cuda)
+    dy2 = torch.randn(N * 81 * 64, generator=g).to(cuda).bfloat16()
+    w2 = (0.05 * torch.randn(64 * 512, generator=g)).to(cuda).bfloat16()
+    a1 = torch.relu(torch.randn(N * 400 * 32, generator=g)).to(cuda).bfloat16()
+    da1 = torch.empty(N * 400 * 32, dtype=torch.bfloat16, device=cuda)
+    ref = [torch.full((grid * 64 * 512,), float("nan"), device=cuda), torch.full((grid * 512,), float("nan"), device=cuda),
+           torch.full((2 * grid * 32 * 256,), float("nan"), device=cuda),
+           torch.full((2 * grid * 32,), float("nan"), device=cuda)]
+    h.conv2_bwd(dy2, w2, a1, da1, ref[0], ref[1], N, grid, 0)
+    ns = h.conv1_wgrad8(x, da1, ref[2], ref[3], N, grid)
+    out = [torch.full((grid * 64 * 512,), float("nan"), device=cuda), torch.full((grid * 512,), float("nan"), device=cuda),
+           torch.full((grid * 32 * 256,), float("nan"), device=cuda), torch.full((grid * 32,), float("nan"), device=cuda)]
+    n1 = h.conv21_bwd(dy2, w2, a1, x, out[0], out[1], out[2], out[3], N, grid)
+    assert n1 == grid
+    torch.cuda.synchronize()
+    pairs = {"dW2": (out[0].view(grid, -1).sum(0), ref[0].view(grid, -1).sum(0)),
+             "db2": (out[1].view(-1, 64).sum(0), ref[1].view(-1, 64).sum(0)),
+             "dW1": (out[2].view(grid, -1).sum(0), ref[2].view(ns, -1).sum(0)),
+             "db1": (out[3].view(grid, 32).sum(0), ref[3].view(ns, 32).sum(0))}
+    for name, (a, b) in pairs.items():
+        assert torch.isfinite(a).all(), name
+        assert relerr(a.cpu(), b.cpu()) < 1e-4, name
+
+
 # ----------------------------------------------------------------------------- fc.hip
 @pytest.mark.parametrize("M,N,K,splits", [(37, 512, 3136, 1), (300, 512, 3136, 4), (2048, 512, 3136, 4),
                                           (130, 3136, 512, 1), (64, 132, 128, 2)])
