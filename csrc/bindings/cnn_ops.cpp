@@ -40,11 +40,7 @@ int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, i
                  float ent_coef, uint16_t* dh, float* dhead, float* stats, int grid, const float* part,
                  int splits, const float* fc_b, uint16_t* h_out, void* stream);
 int rrl_fc_nt_part(const uint16_t* a, const uint16_t* b, float* part, int M, int N, int K, int splits, void* stream);
-int rrl_fc_head(const uint16_t* x, const uint16_t* w, const float* fc_b, const float* head_w, const float* head_wv,
-                int A, uint16_t* hid, float* hp, int M, int N, int K, void* stream);
-int rrl_a2c_head_finish(const float* hp, int ntiles, const float* head_params, int B, int A, int32_t* act, float* logp,
-                        float* value, float* logits_out, unsigned long long seed, unsigned long long step,
-                        const unsigned long long* step_base, int row_offset, void* stream);
+
 int rrl_fc_nt_mask(const uint16_t* a, const uint16_t* b, const uint16_t* mask, uint16_t* out, int M, int N, int K,
                    void* stream);
 int rrl_transpose_bf16(const uint16_t* in, uint16_t* out, int R, int C, void* stream);
@@ -68,8 +64,7 @@ int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, u
                   float* bias_part, int N, int grid, int staged, void* stream);
 int rrl_conv1_wgrad8(const uint8_t* x, const uint16_t* dy, float* part, float* bias_part, int N, int grid,
                      void* stream);
-int rrl_conv21_bwd(const uint16_t* dy2, const uint16_t* w2, const uint16_t* a1, const uint8_t* x, float* part2,
-                   float* bias2, float* part1, float* bias1, int N, int grid, void* stream);
+
 }
 
 namespace {
@@ -197,28 +192,6 @@ int64_t conv1_wgrad8(const Tensor& x, const Tensor& dy, const Tensor& part, cons
                             (int)grid, stream()),
            "conv1_wgrad8");
   return 2 * grid;
-}
-
-// conv2 backward + conv1 weight gradient in one pass per image (cnn_fused.hip conv21_bwd_kernel):
-// da2 [N][81][64], W2, a1 [N][400][32], s2d frames [N][21][21][64] -> dW2 partials [grid][64 * 512],
-// db2 partials [grid * 8][64], dW1 partials [grid][32 * 256], db1 partials [grid][32]; da1 never
-// leaves LDS.  Returns the slab count of either layer (grid).
-int64_t conv21_bwd(const Tensor& dy2, const Tensor& w2, const Tensor& a1, const Tensor& x, const Tensor& part2,
-                   const Tensor& bias2, const Tensor& part1, const Tensor& bias1, int64_t N, int64_t grid) {
-  TORCH_CHECK(N > 0 && grid > 0 && grid <= N, "conv21_bwd: need 0 < grid <= N");
-  check(dy2, "dy2", at::kBFloat16, N * 81 * 64);
-  check(w2, "w2", at::kBFloat16, 64 * 512);
-  check(a1, "a1", at::kBFloat16, N * 400 * 32);
-  check(x, "x", at::kByte, N * 441 * 64);
-  check(part2, "part2", at::kFloat, grid * 64 * 512);
-  check(bias2, "bias2", at::kFloat, grid * 512);
-  check(part1, "part1", at::kFloat, grid * 32 * 256);
-  check(bias1, "bias1", at::kFloat, grid * 32);
-  const int rc = rrl_conv21_bwd(bf(dy2), bf(w2), bf(a1), x.data_ptr<uint8_t>(), part2.data_ptr<float>(),
-                                bias2.data_ptr<float>(), part1.data_ptr<float>(), bias1.data_ptr<float>(), (int)N,
-                                (int)grid, stream());
-  TORCH_CHECK(rc == grid, "conv21_bwd failed with code ", rc);
-  return rc;
 }
 
 void gemm_dgrad(const Tensor& dy, const Tensor& w, const OptT& mask, const Tensor& out, int64_t M, int64_t Cout,
@@ -388,34 +361,6 @@ void a2c_head(int64_t mode, const Tensor& h, const Tensor& head_params, int64_t 
            "a2c_head");
 }
 
-// The rollout's fc layer + A2C head in two launches (fc.hip fc_head_kernel: 64 x 64 tiles over
-// the full K, h = bf16(relu(a . w^T + fc_b)) into hid and per-column-tile head partials into hp
-// [N / 64][M][8]; cnn.hip a2c_head_finish_kernel: sum, biases, Philox sampling).
-void fc_head_rollout(const Tensor& a, const Tensor& w, const Tensor& fc_b, const Tensor& head_params, const Tensor& hid,
-                     const Tensor& hp, int64_t M, int64_t A, const OptT& act, const OptT& logp, const OptT& value,
-                     const OptT& logits, int64_t seed, int64_t step, int64_t row_offset, const OptT& step_base) {
-  constexpr int64_t F = 512, K = 3136;
-  TORCH_CHECK(M > 0 && A >= 1 && A <= 7, "fc_head_rollout: M > 0, 1 <= A <= 7");
-  check(a, "a", at::kBFloat16, M * K);
-  check(w, "w", at::kBFloat16, F * K);
-  check(fc_b, "fc_b", at::kFloat, F);
-  check(head_params, "head_params", at::kFloat, (A + 1) * F + A + 1);
-  check(hid, "hid", at::kBFloat16, M * F);
-  check(hp, "hp", at::kFloat, (F / 64) * M * 8);
-  int32_t* ap = opt_ptr<int32_t>(act, "act", at::kInt, M);
-  float* lp = opt_ptr<float>(logp, "logp", at::kFloat, M);
-  float* vp = opt_ptr<float>(value, "value", at::kFloat, M);
-  float* lo = opt_ptr<float>(logits, "logits", at::kFloat, M * A);
-  const unsigned long long* sb = opt_ptr<const unsigned long long>(step_base, "step_base", at::kLong, 1);
-  const float* hw = head_params.data_ptr<float>();
-  rc_check(rrl_fc_head(bf(a), bf(w), fc_b.data_ptr<float>(), hw, hw + A * F + A, (int)A, bf(hid),
-                       hp.data_ptr<float>(), (int)M, (int)F, (int)K, stream()),
-           "fc_head");
-  rc_check(rrl_a2c_head_finish(hp.data_ptr<float>(), (int)(F / 64), hw, (int)M, (int)A, ap, lp, vp, lo, (uint64_t)seed,
-                               (uint64_t)step, sb, (int)row_offset, stream()),
-           "a2c_head_finish");
-}
-
 // fp32 split-K partials part[splits][M][N] of a[M][K] . b[N][K]^T (fc.hip); returns the
 // number of splits used.
 int64_t fc_nt_part(const Tensor& a, const Tensor& b, const Tensor& part, int64_t M, int64_t N, int64_t K,
@@ -526,7 +471,6 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("y2"), pybind11::arg("y3"), pybind11::arg("N"), pybind11::arg("probe") = 0,
         pybind11::arg("grid") = 0, pybind11::arg("store12") = true);
   m.def("conv3_bwd", &conv3_bwd);
-  m.def("conv21_bwd", &conv21_bwd);
   m.def("conv2_bwd", &conv2_bwd, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("xact"), pybind11::arg("dx"),
         pybind11::arg("part"), pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"),
         pybind11::arg("staged") = 0);
@@ -556,13 +500,6 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("stats"), pybind11::arg("grid"), pybind11::arg("step_base") = pybind11::none(),
         pybind11::arg("part") = pybind11::none(), pybind11::arg("splits") = 0,
         pybind11::arg("fc_b") = pybind11::none());
-  m.def("fc_head_rollout", &fc_head_rollout, "rollout fc + A2C head (fc_head_kernel + a2c_head_finish_kernel)",
-        pybind11::arg("a"), pybind11::arg("w"), pybind11::arg("fc_b"), pybind11::arg("head_params"),
-        pybind11::arg("hid"), pybind11::arg("hp"), pybind11::arg("M"), pybind11::arg("A"),
-        pybind11::arg("act") = pybind11::none(), pybind11::arg("logp") = pybind11::none(),
-        pybind11::arg("value") = pybind11::none(), pybind11::arg("logits") = pybind11::none(),
-        pybind11::arg("seed") = 0, pybind11::arg("step") = 0, pybind11::arg("row_offset") = 0,
-        pybind11::arg("step_base") = pybind11::none());
   m.def("fc_nt_part", &fc_nt_part);
   m.def("fc_nt_mask", &fc_nt_mask);
   m.def("transpose_bf16", &transpose_bf16);

@@ -661,37 +661,6 @@ __global__ void __launch_bounds__(256) a2c_head_kernel(HeadArgs a) {
   }
 }
 
-// The rollout head from fc_head_kernel's per-column-tile partials (fc.hip): one thread per row
-// sums the ntiles partials in tile order (slot 7 = the value), adds the biases and samples with
-// the same Philox stream and categorical helpers as a2c_head_kernel's rollout mode.
-__global__ void __launch_bounds__(256) a2c_head_finish_kernel(HeadArgs a, const float* __restrict__ hp, int ntiles) {
-  const int row = blockIdx.x * 256 + threadIdx.x;
-  if (row >= a.B) return;
-  const int A = a.A;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int t = 0; t < ntiles; ++t) {
-    const float4 p0 = *reinterpret_cast<const float4*>(hp + ((size_t)t * a.B + row) * 8);
-    const float4 p1 = *reinterpret_cast<const float4*>(hp + ((size_t)t * a.B + row) * 8 + 4);
-    acc[0] += p0.x; acc[1] += p0.y; acc[2] += p0.z; acc[3] += p0.w;
-    acc[4] += p1.x; acc[5] += p1.y; acc[6] += p1.z; acc[7] += p1.w;
-  }
-  float logits[kMaxAct];
-#pragma unroll
-  for (int o = 0; o < kMaxAct; ++o) logits[o] = (o < 7 && o < A) ? acc[o < 7 ? o : 0] + a.bias[o < A ? o : 0] : -INFINITY;
-  const float value = acc[7] + a.b_v[0];
-  const CatStats cs = cat_stats(A, logits);
-  unsigned long long st = ((unsigned long long)a.step_hi << 32) | a.step_lo;
-  if (a.step_base) st += *a.step_base;
-  const uint4 r = philox4x32(make_uint4((uint32_t)(row + a.row_offset), (uint32_t)st, (uint32_t)(st >> 32), 0x50u),
-                             make_uint2(a.seed_lo, a.seed_hi));
-  const int pick = cat_sample(A, logits, cs.lse, u01(r.x));
-  if (a.act) a.act[row] = pick;
-  if (a.logp) a.logp[row] = pick_logit(A, logits, pick) - cs.lse;
-  if (a.value) a.value[row] = value;
-  if (a.logits_out)
-    for (int o = 0; o < A; ++o) a.logits_out[(size_t)row * A + o] = logits[o];
-}
-
 // Head weight gradients: part[blk][ (A+1)*F + (A+1) ] = sum over the block's rows of
 // dhead[r][o] * h[r][f] (and dhead[r][o] for the biases).  Thread t owns f = 2t, 2t+1.
 __global__ void __launch_bounds__(256) head_wgrad_kernel(const uint16_t* __restrict__ h,
@@ -1584,31 +1553,6 @@ int rrl_to_bf16(const float* x, uint16_t* y, long long n, void* stream_) {
 }
 
 // mode 0: rollout (sample act / logp / value), 1: training (dh, dhead, stats).
-int rrl_a2c_head_finish(const float* hp, int ntiles, const float* head_params, int B, int A, int32_t* act, float* logp,
-                        float* value, float* logits_out, unsigned long long seed, unsigned long long step,
-                        const unsigned long long* step_base, int row_offset, void* stream_) {
-  if (A < 1 || A > 7 || B < 1 || ntiles < 1) return -1;
-  HeadArgs a{};
-  a.w = head_params;
-  a.bias = head_params + A * kHeadF;
-  a.w_v = a.bias + A;
-  a.b_v = a.w_v + kHeadF;
-  a.B = B;
-  a.A = A;
-  a.act = act;
-  a.logp = logp;
-  a.value = value;
-  a.logits_out = logits_out;
-  a.seed_lo = (uint32_t)seed;
-  a.seed_hi = (uint32_t)(seed >> 32);
-  a.step_lo = (uint32_t)step;
-  a.step_hi = (uint32_t)(step >> 32);
-  a.step_base = step_base;
-  a.row_offset = row_offset;
-  hipLaunchKernelGGL(a2c_head_finish_kernel, dim3((B + 255) / 256), dim3(256), 0, (hipStream_t)stream_, a, hp, ntiles);
-  return (int)hipGetLastError();
-}
-
 int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, int A, int32_t* act, float* logp,
                  float* value, float* logits_out, unsigned long long seed, unsigned long long step,
                  const unsigned long long* step_base, int row_offset,

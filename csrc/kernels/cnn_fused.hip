@@ -941,332 +941,6 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
       for (int r = 0; r < 4; ++r) o[(16 * mt + 4 * g + r) * 256 + 16 * nt + j] = acc[mt][nt][r] * kU8Scale;
 }
 
-// ============================================================================= conv2 + conv1 backward
-// conv2's dgrad + wgrad + bias and conv1's wgrad + bias in ONE pass per image: the data
-// gradient da1 [400][32] goes from conv2's dgrad registers into LDS and straight into conv1's
-// weight gradient instead of through HBM (conv2_bwd_kernel wrote 262 MB of da1 per 10,240-
-// image update and conv1_wgrad8_kernel read it back).  Same per-wave work split, k orders and
-// LDS image layouts as those two kernels (their comments), so the partials match theirs up to
-// fma contraction.  LDS: region A is time-shared -- conv2's inputs (da2 bordered image + the a1
-// phase images) until conv2 is done, then the da1 image -- and region X holds the frame:
-//   B0  (previous image's conv1 reads done) inputs -> A (borders / pad rows rewritten, since
-//       the da1 image overwrote them) and X; next image's loads issued
-//   B1  conv2 wgrad + dgrad (da1 masked by a1 > 0 kept in registers) + db2
-//   B2  da1 -> A (rows 400..415 zero)
-//   B3  conv1 wgrad + db1
-namespace c21 {
-constexpr int kThreads = 512;
-constexpr int kDLd = c2b::kDLd, kPLd = c2b::kPLd, kDRows = c2b::kDRows, kPRows = c2b::kPRows;
-constexpr int kP = kDRows * kDLd;                        // a1 phase images after the da2 image
-constexpr int kConv2 = kP + 4 * kPRows * kPLd;           // 30,080
-constexpr int kYLd = c1w::kLd, kYRows = c1w::kYRows;     // da1 image [416][80]
-constexpr int kRegionA = kYRows * kYLd > kConv2 ? kYRows * kYLd : kConv2;  // 33,280
-constexpr int kXLd = c1w::kLd, kXRows = c1w::kXRows;     // frame [448][80]
-constexpr int kStage = kRegionA + kXRows * kXLd;         // next image's a1, [400][32] by DMA
-constexpr int kLds = (kStage + 400 * 32) * 2;            // 163,840 bytes: all of it
-constexpr int kYC = 81 * 8, kAC = 400 * 4, kXC = 441 * 4;  // 16-byte chunks per image
-constexpr int kYPT = (kYC + kThreads - 1) / kThreads, kAPT = (kAC + kThreads - 1) / kThreads;
-constexpr int kADma = kAC / 64;  // 1 KB DMA instructions per a1 image (25)
-constexpr int kXPT = (kXC + kThreads - 1) / kThreads;
-static_assert(kRegionA % 8 == 0 && kP % 8 == 0 && kStage % 8 == 0 && kAC % 64 == 0, "16-byte aligned LDS regions");
-}  // namespace c21
-
-__global__ __launch_bounds__(c21::kThreads, 1) void conv21_bwd_kernel(
-    const uint16_t* __restrict__ dy2, const uint16_t* __restrict__ w2, const uint16_t* __restrict__ a1,
-    const uint8_t* __restrict__ x, float* __restrict__ part2, float* __restrict__ bias2, float* __restrict__ part1,
-    float* __restrict__ bias1, int N) {
-  using namespace c21;
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* RA = smem;              // region A: da2 + a1 phases, then da1
-  uint16_t* Xi = smem + kRegionA;   // frame, bf16 integers
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int i16 = lane & 15, g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
-  // conv2 roles (conv2_bwd_kernel): dgrad phase class / c tile, wgrad c block / taps
-  const int cls = wave >> 1, ph = cls >> 1, pw = cls & 1, ct = wave & 1;
-  const int cb = wave & 1, tau0 = 4 * (wave >> 1);
-  // conv1 roles: tap (w & 3) and HALF of the 64 input channels (w >> 2: column tiles 2 nh,
-  // 2 nh + 1) over all 13 position chunks -- half the accumulators of conv1_wgrad8_kernel's
-  // position split, which the register file (conv2's accumulators live beside them) needs
-  const int tap1 = wave & 3, kh1 = tap1 >> 1, kw1 = tap1 & 1, nh = wave >> 2;
-
-  bf16x8_t wf[8];  // conv2 dgrad A fragments
-#pragma unroll
-  for (int ks = 0; ks < 8; ++ks) {
-    const int t = ks >> 1, kh = ph + 2 * (t >> 1), kw = pw + 2 * (t & 1), co0 = (ks & 1) * 32 + 8 * g;
-    typedef short s16x8_t __attribute__((ext_vector_type(8)));
-    s16x8_t v;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (short)w2[(((co0 + e) * 4 + kh) * 4 + kw) * 32 + 16 * ct + i16];
-    wf[ks] = __builtin_bit_cast(bf16x8_t, v);
-  }
-  f32x4_t wacc[4][4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) wacc[c][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;  // db2[tid & 63]
-  f32x4_t acc1[2][2], accb[2];
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt) {
-    accb[mt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) acc1[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  }
-  const bool do_bias = tap1 == 0 && nh == 0;
-  bf16x8_t ones;
-  {
-    typedef short s16x8_t __attribute__((ext_vector_type(8)));
-    const short one = (lane & 15) == 0 ? (short)0x3f80 : (short)0;
-    s16x8_t v = {one, one, one, one, one, one, one, one};
-    ones = __builtin_bit_cast(bf16x8_t, v);
-  }
-
-  // the next image's da2 and frame are prefetched into registers, its a1 goes global -> LDS
-  // staging by DMA (no registers: those of a1 were spilled, and each spill store waited for its
-  // HBM load), copied into the phase images at B0
-  uint4 ry[kYPT], rx[kXPT];
-  uint16_t* Sa = smem + kStage;
-  const int wu = __builtin_amdgcn_readfirstlane(wave);
-  auto gload = [&](int n, int tid) {
-    const uint4* ys = reinterpret_cast<const uint4*>(dy2 + (size_t)n * 81 * 64);
-    const uint4* xs = reinterpret_cast<const uint4*>(x + (size_t)n * 441 * 64);
-#pragma unroll
-    for (int k = 0; k < kYPT; ++k) {
-      const int q = tid + kThreads * k;
-      ry[k] = q < kYC ? ys[q] : make_uint4(0, 0, 0, 0);
-    }
-    const uint4* as = reinterpret_cast<const uint4*>(a1 + (size_t)n * 400 * 32);
-    for (int c = wu; c < kADma; c += 8)
-      __builtin_amdgcn_global_load_lds(as + 64 * c + (tid & 63),
-                                       (__attribute__((address_space(3))) void*)(Sa + 512 * c), 16, 0, 0);
-#pragma unroll
-    for (int k = 0; k < kXPT; ++k) {
-      const int q = tid + kThreads * k;
-      rx[k] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
-    }
-  };
-  const uint4 z4 = make_uint4(0, 0, 0, 0);
-  const int G = gridDim.x, n0 = blockIdx.x;
-  if (n0 < N) gload(n0, tid);
-  for (int n = n0; n < N; n += G) {
-    // lane coordinates as opaque per-image values: the loop body's LDS addresses are formed
-    // next to their reads instead of being hoisted (and spilled) across the image loop
-    int to = tid;
-    asm volatile("" : "+v"(to));
-    const int i16 = to & 15, g = (to & 63) >> 4, q4 = (to >> 2) & 3, p4 = to & 3;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's a1 DMA has landed in the staging area
-    __syncthreads();  // B0: the previous image's conv1 reads of A / X are done; every wave's a1 DMA landed
-    {
-      uint16_t* D = RA;
-      uint16_t* P = RA + kP;
-#pragma unroll
-      for (int k = 0; k < kYPT; ++k) {
-        const int q = to + kThreads * k;
-        if (q < kYC) {
-          const int pix = q >> 3, oh = pix / 9, ow = pix - oh * 9;
-          *reinterpret_cast<uint4*>(D + ((oh + 1) * 12 + ow + 1) * kDLd + (q & 7) * 8) = ry[k];
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < kAPT; ++k) {
-        const int q = to + kThreads * k;
-        if (q < kAC) {
-          const int pix = q >> 2, ih = pix / 20, iw = pix - ih * 20;
-          const int phase = (ih & 1) * 2 + (iw & 1);
-          *reinterpret_cast<uint4*>(P + (phase * kPRows + (ih >> 1) * 10 + (iw >> 1)) * kPLd + (q & 3) * 8) =
-              *reinterpret_cast<const uint4*>(Sa + 8 * q);
-        }
-      }
-      // da2 border positions (63 of the 12 x 12, 8 chunks each) and the phase images' pad rows
-      // (16 per phase, 4 chunks each): zero again, the da1 image overwrote them
-      for (int q = to; q < 63 * 8 + 64 * 4; q += kThreads) {
-        if (q < 63 * 8) {
-          const int b = q >> 3;  // b-th border position in row-major order
-          int r;
-          if (b < 12) r = b;                                   // row 0
-          else if (b < 12 + 9 * 3) {                           // rows 1..9: columns 0, 10, 11
-            const int k = b - 12, rr = 1 + k / 3, cc = k % 3;
-            r = rr * 12 + (cc == 0 ? 0 : 9 + cc);
-          } else r = 120 + (b - 39);                           // rows 10, 11
-          *reinterpret_cast<uint4*>(D + r * kDLd + (q & 7) * 8) = z4;
-        } else {
-          const int k = q - 63 * 8, ph2 = k >> 6, row = 100 + ((k >> 2) & 15);
-          *reinterpret_cast<uint4*>(P + (ph2 * kPRows + row) * kPLd + (k & 3) * 8) = z4;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < kXPT; ++k) {
-        const int q = to + kThreads * k;
-        if (q < kXC) {
-          uint16_t* d = Xi + (q >> 2) * kXLd + (q & 3) * 16;
-          *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(rx[k].x, rx[k].y));
-          *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(rx[k].z, rx[k].w));
-        }
-      }
-    }
-    __syncthreads();  // B1
-    const uint16_t* D = RA;
-    const uint16_t* P = RA + kP;
-    // ---- conv2 wgrad (conv2_bwd_kernel)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      int oh[2], ow0[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int R = 2 * (4 * s + g) + h;
-        oh[h] = R < 27 ? R / 3 : 9;
-        ow0[h] = R < 27 ? 4 * (R % 3) : 0;
-      }
-      bf16x8_t af[4], bfr[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        af[c] = tr_frag2(D + ((oh[0] + 1) * 12 + ow0[0] + 1 + q4) * kDLd + 16 * c + 4 * p4,
-                         D + ((oh[1] + 1) * 12 + ow0[1] + 1 + q4) * kDLd + 16 * c + 4 * p4);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int tau = tau0 + t, kh = tau >> 2, kw = tau & 3;
-        const uint16_t* Pp = P + ((kh & 1) * 2 + (kw & 1)) * kPRows * kPLd + 16 * cb + 4 * p4;
-        bfr[t] = tr_frag2(Pp + ((oh[0] + (kh >> 1)) * 10 + ow0[0] + (kw >> 1) + q4) * kPLd,
-                          Pp + ((oh[1] + (kh >> 1)) * 10 + ow0[1] + (kw >> 1) + q4) * kPLd);
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) wacc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[c], bfr[t], wacc[c][t], 0, 0, 0);
-    }
-    // ---- conv2 dgrad: da1 of phase class (ph, pw), c tile ct, masked, kept in registers
-    uint2 dv[7];
-    auto class_tiles = [&](auto tag) {
-      constexpr int T0 = decltype(tag)::value, NT = T0 == 0 ? 4 : 3;
-      f32x4_t acc[NT];
-      int rb[NT];
-#pragma unroll
-      for (int u = 0; u < NT; ++u) {
-        acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        const int p = 16 * (T0 + u) + i16;
-        const int pc = p < 100 ? p : 0;
-        const int a = pc / 10, b = pc - a * 10;
-        rb[u] = (a + 1) * 12 + (b + 1);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        const int t = ks >> 1, ti = t >> 1, tj = t & 1;
-        const int off = -(ti * 12 + tj) * kDLd + (ks & 1) * 32 + 8 * g;
-        bf16x8_t bv[NT];
-#pragma unroll
-        for (int u = 0; u < NT; ++u) bv[u] = *reinterpret_cast<const bf16x8_t*>(D + rb[u] * kDLd + off);
-#pragma unroll
-        for (int u = 0; u < NT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], bv[u], acc[u], 0, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < NT; ++u) {
-        const int p = 16 * (T0 + u) + i16;
-        const int pc = p < 100 ? p : 0;
-        const int a = pc / 10, b = pc - a * 10;
-        const uint2 m = *reinterpret_cast<const uint2*>(P + (cls * kPRows + a * 10 + b) * kPLd + 16 * ct + 4 * g);
-        dv[T0 + u] = make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x),
-                                relu_mask2(pk_bf16(acc[u][2], acc[u][3]), m.y));
-      }
-    };
-    class_tiles(std::integral_constant<int, 0>{});
-    class_tiles(std::integral_constant<int, 4>{});
-    for (int pos = to >> 6; pos < 81; pos += 8) {  // db2
-      const int oh = pos / 9, ow = pos - oh * 9;
-      bsum += bf2f(D[((oh + 1) * 12 + ow + 1) * kDLd + (to & 63)]);
-    }
-    __syncthreads();  // B2: conv2's reads of A are done
-    // the next image's loads go out here, not at B0: no prefetch register is live across
-    // conv2 (its accumulators, dgrad weights and fragments fill the register file); they land
-    // during the da1 store and conv1's weight gradient
-    if (n + G < N) gload(n + G, to);
-    {
-      uint16_t* Y = RA;  // da1 image [416][80]: pixel rows, 32 channels
-#pragma unroll
-      for (int u = 0; u < 7; ++u) {
-        const int p = 16 * u + i16;
-        if (p < 100) {
-          const int a = p / 10, b = p - a * 10;
-          const int pix = (ph + 2 * a) * 20 + pw + 2 * b;
-          *reinterpret_cast<uint2*>(Y + pix * kYLd + 16 * ct + 4 * g) = dv[u];
-        }
-      }
-      if (to < 16 * 4) *reinterpret_cast<uint4*>(Y + (400 + (to >> 2)) * kYLd + (to & 3) * 8) = z4;
-    }
-    __syncthreads();  // B3
-    // ---- conv1 wgrad (conv1_wgrad8_kernel)
-    {
-      const uint16_t* Yi = RA;
-      const int qq = q4, pp = p4;
-#pragma unroll 1
-      for (int kc = 0; kc < 13; ++kc) {
-        const int pa = 32 * kc + 4 * g, pb = pa + 16;
-        const int xa = (pa < 400 ? (pa / 20 + kh1) * 21 + pa % 20 + kw1 : 0) + qq;
-        const int xb = (pb < 400 ? (pb / 20 + kh1) * 21 + pb % 20 + kw1 : 0) + qq;
-        bf16x8_t af[2], bfr[2];
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-          af[mt] = tr_frag2(Yi + (pa + qq) * kYLd + 16 * mt + 4 * pp, Yi + (pb + qq) * kYLd + 16 * mt + 4 * pp);
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt)
-          bfr[nt] = tr_frag2(Xi + xa * kXLd + 16 * (2 * nh + nt) + 4 * pp, Xi + xb * kXLd + 16 * (2 * nh + nt) + 4 * pp);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt)
-            acc1[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc1[mt][nt], 0, 0, 0);
-        if (do_bias) {
-#pragma unroll
-          for (int mt = 0; mt < 2; ++mt) accb[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], ones, accb[mt], 0, 0, 0);
-        }
-      }
-    }
-  }
-  // conv2 partials: part2[blk][co][kh][kw][c], bias2[blk * 512 + tid]
-  {
-    float* o = part2 + (size_t)blockIdx.x * 64 * 512;
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[(16 * c + 4 * g + r) * 512 + (tau0 + t) * 32 + 16 * cb + i16] = wacc[c][t][r];
-    bias2[(size_t)blockIdx.x * kThreads + tid] = bsum;
-  }
-  // conv1 partials: ONE slab per workgroup, part1[blk][co][kh][kw][c], bias1[blk][co]
-  {
-    const int slab = blockIdx.x;
-    if (do_bias && (lane & 15) == 0) {
-#pragma unroll
-      for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) bias1[(size_t)slab * 32 + 16 * mt + 4 * g + r] = accb[mt][r];
-    }
-    float* o = part1 + (size_t)slab * 32 * 256 + kh1 * 128 + kw1 * 64;
-    const int j = lane & 15;
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          o[(16 * mt + 4 * g + r) * 256 + 16 * (2 * nh + nt) + j] = acc1[mt][nt][r] * kU8Scale;
-  }
-}
-
-// returns the number of partial slabs of either layer (one per workgroup)
-extern "C" int rrl_conv21_bwd(const uint16_t* dy2, const uint16_t* w2, const uint16_t* a1, const uint8_t* x,
-                              float* part2, float* bias2, float* part1, float* bias1, int N, int grid, void* stream) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv21_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c21::kLds);
-    attr = true;
-  }
-  if (N < 1 || grid < 1) return 0;
-  hipLaunchKernelGGL(conv21_bwd_kernel, dim3(grid), dim3(c21::kThreads), c21::kLds, (hipStream_t)stream, dy2, w2, a1,
-                     x, part2, bias2, part1, bias1, N);
-  return (int)hipGetLastError() ? -1 : grid;
-}
-
 // returns the number of partial slabs written (2 per workgroup)
 extern "C" int rrl_conv1_wgrad8(const uint8_t* x, const uint16_t* dy, float* part, float* bias_part, int N, int grid,
                                 void* stream) {

@@ -288,160 +288,6 @@ static int launch_fc_nt(const uint16_t* A, const uint16_t* B, Epi epi, int M, in
   return (int)hipGetLastError();
 }
 
-// ----------------------------------------------------------------------------- fc + head partials
-// The rollout's fc layer and the first half of its A2C head in one launch (rows M = envs,
-// N = 512 hidden, K = 3136): 64 x 64 tiles over the FULL K -- at 2,048 rows that is 32 x 8 =
-// 256 tiles, one per CU, so no split-K partials are needed (fc_nt_part wrote 16.8 MB of fp32
-// partials per step that the head re-read) -- and an epilogue that forms h = bf16(relu(acc +
-// fc_b)), stores it for the backward, and reduces the tile's contribution to the head,
-// hp[tile_n][m][o] = sum over its 64 columns of w[o][n] h[m][n] (o < A: the policy logits,
-// o = A: the value).  cnn.hip's a2c_head_finish_kernel sums the N / 64 tiles' partials in a
-// fixed order, adds the biases and samples.  4 waves (2 x 2, 32 x 32 each), the same DMA
-// staging / swizzle / pipeline as fc_nt_kernel.
-constexpr int kFhB = 64;
-constexpr int kFhThreads = 256;
-constexpr int kFhImg = kFhB * kFcBK;  // bf16 elements per operand image
-constexpr int kFhStage = 2 * kFhImg;  // 16 KB
-template <int STAGES>
-constexpr int fh_lds_bytes() { return STAGES * kFhStage * 2; }
-
-struct FcHeadArgs {
-  uint16_t* hid;      // [M][N] bf16
-  float* hp;          // [N / 64][M][8]
-  const float* fc_b;  // [N]
-  const float* w;     // [A][N] policy head weights
-  const float* w_v;   // [N] value head weights
-  int A;              // <= 7
-};
-
-template <int STAGES>
-__global__ void __launch_bounds__(kFhThreads, 2)
-fc_head_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ W, FcHeadArgs h, int M, int N, int K,
-               int tiles_m, int tiles_n) {
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nwg = gridDim.x, b = blockIdx.x;
-  const int q = nwg >> 3, rem = nwg & 7, xcd = b & 7;
-  const int lid = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
-  // n fastest: an XCD's run of tiles shares the activation rows; the 3.2 MB of weights stay
-  // in every XCD's L2
-  const int tn = lid % tiles_n, tm = lid / tiles_n;
-  if (tm >= tiles_m) return;
-  const int m0 = tm * kFhB, n0 = tn * kFhB;
-  const int nk = K / kFcBK;
-  const int wm = wave & 1, wn = wave >> 1;
-  const int g = lane >> 4, li = lane & 15;
-  f32x4_t acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  auto issue = [&](int t) {
-    uint16_t* st = smem + (t % STAGES) * kFhStage;
-    fc_stage(X, M, K, m0, t * kFcBK, st, wave, lane);
-    fc_stage(W, N, K, n0, t * kFcBK, st + kFhImg, wave, lane);
-  };
-#pragma unroll
-  for (int t = 0; t < STAGES - 1; ++t)
-    if (t < nk) issue(t);
-  for (int t = 0; t < nk; ++t) {
-    const int ahead = min(STAGES - 2, nk - 1 - t);
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
-    const uint16_t* Ai = smem + (t % STAGES) * kFhStage;
-    const uint16_t* Bi = Ai + kFhImg;
-#pragma unroll
-    for (int s = 0; s < kFcBK / 32; ++s) {
-      const int kc = 4 * s + g;
-      bf16x8_t af[2], bfr[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(Ai + 8 * fc_swz(32 * wm + 16 * i + li, kc));
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bi + 8 * fc_swz(32 * wn + 16 * j + li, kc));
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)  // D[n][m]: lane (g, li) holds n = 4 g .. 4 g + 3 of row m = li
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
-  }
-  // ---- epilogue: h = bf16(relu(acc + fc_b)) and the tile's head partials per row
-  float ph[2][8];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) ph[i][k] = 0.f;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + 32 * wn + 16 * j + 4 * g;
-    const f32x4_t fb = *reinterpret_cast<const f32x4_t*>(h.fc_b + n);
-    const f32x4_t wv = *reinterpret_cast<const f32x4_t*>(h.w_v + n);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = m0 + 32 * wm + 16 * i + li;
-      uint16_t hb[4];
-      float hv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        hb[r] = f2bf(fmaxf(acc[i][j][r] + fb[r], 0.f));
-        hv[r] = bf2f(hb[r]);
-      }
-      if (m < M)
-        *reinterpret_cast<uint2*>(h.hid + (size_t)m * N + n) =
-            make_uint2((uint32_t)hb[0] | ((uint32_t)hb[1] << 16), (uint32_t)hb[2] | ((uint32_t)hb[3] << 16));
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ph[i][7] += wv[r] * hv[r];
-#pragma unroll
-      for (int o = 0; o < 7; ++o) {
-        if (o < h.A) {
-          const f32x4_t wo = *reinterpret_cast<const f32x4_t*>(h.w + (size_t)o * N + n);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) ph[i][o] += wo[r] * hv[r];
-        }
-      }
-    }
-  }
-  // over the 4 lane groups (the tile's 16 columns per lane group) ...
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      ph[i][k] += __shfl_xor(ph[i][k], 16);
-      ph[i][k] += __shfl_xor(ph[i][k], 32);
-    }
-  // ... and over the two column waves (wn) through LDS (the stages are idle now)
-  float* red = reinterpret_cast<float*>(smem);  // [2 wm][2 i][16 li][8]
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();  // every wave is done reading the operand stages
-  asm volatile("" ::: "memory");
-  if (wn == 1 && g == 0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) red[((wm * 2 + i) * 16 + li) * 8 + k] = ph[i][k];
-  }
-  __syncthreads();
-  if (wn == 0 && g == 0) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = m0 + 32 * wm + 16 * i + li;
-      if (m < M) {
-        float o8[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o8[k] = ph[i][k] + red[((wm * 2 + i) * 16 + li) * 8 + k];
-        float* dst = h.hp + ((size_t)tn * M + m) * 8;
-        *reinterpret_cast<f32x4_t*>(dst) = f32x4_t{o8[0], o8[1], o8[2], o8[3]};
-        *reinterpret_cast<f32x4_t*>(dst + 4) = f32x4_t{o8[4], o8[5], o8[6], o8[7]};
-      }
-    }
-  }
-}
-
 // ----------------------------------------------------------------------------- TN (weight gradient)
 //   C[i][j] = sum_r X[r][i] * Y[r][j]      X [R][I], Y [R][J] row-major bf16, R % 64 == 0
 // (the fc weight gradient: X = dh [rows][512], Y = a3 [rows][3136], C = dW [512][3136]).
@@ -660,32 +506,6 @@ int rrl_fc_tn_part(const uint16_t* x, const uint16_t* y, float* part, int R, int
   const int rc = fc_stages(2, 2) == 2 ? launch_fc_tn<2>(x, y, part, R, I, J, used, ones, bias_part, st)
                                       : launch_fc_tn<3>(x, y, part, R, I, J, used, ones, bias_part, st);
   return rc ? -rc - 1000 : used;
-}
-
-// The rollout fc + head partials (fc_head_kernel): hid [M][N] bf16, hp [N / 64][M][8] fp32.
-// N % 64 == 0, K % 64 == 0, 1 <= A <= 7.  Partial slot 7 holds the value.
-int rrl_fc_head(const uint16_t* x, const uint16_t* w, const float* fc_b, const float* head_w, const float* head_wv,
-                int A, uint16_t* hid, float* hp, int M, int N, int K, void* stream_) {
-  if (K % kFcBK || N % kFhB || M < 1 || A < 1 || A > 7) return -1;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fc_head_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              fh_lds_bytes<3>());
-    (void)hipFuncSetAttribute((const void*)fc_head_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              fh_lds_bytes<4>());
-    attr = true;
-  }
-  const int tiles_m = (M + kFhB - 1) / kFhB, tiles_n = N / kFhB;
-  const FcHeadArgs a{hid, hp, fc_b, head_w, head_wv, A};
-  // LDS stages (two or three k-tiles in flight); RRL_FH_STAGES = 3 / 4 for A/B measurements
-  const char* e = getenv("RRL_FH_STAGES");
-  if (e && e[0] == '3')
-    hipLaunchKernelGGL(fc_head_kernel<3>, dim3(tiles_m * tiles_n), dim3(kFhThreads), fh_lds_bytes<3>(),
-                       (hipStream_t)stream_, x, w, a, M, N, K, tiles_m, tiles_n);
-  else
-    hipLaunchKernelGGL(fc_head_kernel<4>, dim3(tiles_m * tiles_n), dim3(kFhThreads), fh_lds_bytes<4>(),
-                       (hipStream_t)stream_, x, w, a, M, N, K, tiles_m, tiles_n);
-  return (int)hipGetLastError();
 }
 
 int rrl_transpose_bf16(const uint16_t* in, uint16_t* out, int R, int C, void* stream_) {

@@ -204,11 +204,6 @@ class DeviceNatureCNN:
         # captured update graph holds this storage, so it must never be reallocated
         fc_rows = max(self.fc_splits(n) * n for n in range(1, self.max_batch + 1)) if self.fc_nt else 0
         self._fc_part = torch.empty(fc_rows * HIDDEN, device=dev) if self.fc_nt else None
-        # rollout fc + head in one GEMM launch over the full K with per-column-tile head
-        # partials (fc.hip fc_head_kernel) instead of split-K partials + the head's reduction;
-        # RRL_FC_HEAD=0 keeps the split-K form (A <= 7)
-        self.fc_head = self.fc_nt and self.A <= 7 and os.environ.get("RRL_FC_HEAD", "1") != "0"
-        self._head_part = torch.empty((HIDDEN // 64) * self.max_batch * 8, device=dev) if self.fc_head else None
         self.refresh_shadow()
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params)
@@ -248,8 +243,6 @@ class DeviceNatureCNN:
         self.part = torch.empty(need, device=dev)
         self.bias_splits = 512
         self.bias_part = torch.empty(max(self.bias_splits * HIDDEN, self.cus * 512), device=dev)
-        # conv2 backward + conv1 weight gradient fused (RRL_CONV21=0: the two separate kernels)
-        self.conv21 = os.environ.get("RRL_CONV21", "1") != "0"
         if self.fused_convs:
             # per-layer partial slabs of the fused conv backward kernels, summed together in ONE
             # launch at the end of the backward (sum_splits_multi)
@@ -302,13 +295,6 @@ class DeviceNatureCNN:
         """fc GEMM as split-K partials, then ONE head launch: bias + ReLU + bf16 hid (stored for
         the backward) + logits / value / sampling."""
         o = self.o
-        if self.fc_head:
-            self.h.fc_head_rollout(a3, self.shadow[o["wfc"]:o["bfc"]], self.params[o["bfc"]:o["bfc"] + HIDDEN],
-                                   self.params[o["head"]:], hid, self._head_part, n, self.A, act=head.get("act"),
-                                   logp=head.get("logp"), value=head.get("value"), logits=head.get("logits"),
-                                   seed=int(head.get("seed", 0)), step=int(head.get("step", 0)),
-                                   row_offset=int(head.get("row_offset", 0)), step_base=head.get("step_base"))
-            return
         s = self.fc_splits(n)
         assert s * n * HIDDEN <= self._fc_part.numel(), "fc split-K partials exceed the preallocated buffer"
         used = int(self.h.fc_nt_part(a3, self.shadow[o["wfc"]:o["bfc"]], self._fc_part, n, HIDDEN, FC_IN, s))
@@ -463,18 +449,7 @@ class DeviceNatureCNN:
             self._dgrad(da3, sh[o["w3"]:o["b3"]], a2, da2, B, L3)
         # conv2
         da1 = self.da1[:B * L1.hout ** 2 * L1.cout]
-        if self.fused_convs and self.conv21:
-            # conv2's dgrad + wgrad + bias and conv1's wgrad + bias in one pass per image: da1
-            # stays in LDS (cnn_fused.hip conv21_bwd_kernel)
-            nblk = min(B, self.cus)
-            ns = int(h.conv21_bwd(da2, sh[o["w2"]:o["b2"]], a1, obs_u8.contiguous(), self.cpart["c2"], self.cbias["c2"],
-                                  self.cpart["c1"], self.cbias["c1"], B, nblk))
-            sums += [(self.cpart["c2"], nblk, L2.cout * L2.K, g[o["w2"]:o["b2"]]),
-                     (self.cbias["c2"], nblk * 8, L2.cout, g[o["b2"]:o["b2"] + L2.cout]),
-                     (self.cpart["c1"], ns, S2D.cout * S2D.K, g[o["w1"]:o["b1"]]),
-                     (self.cbias["c1"], ns, S2D.cout, g[o["b1"]:o["b1"] + S2D.cout])]
-            h.sum_splits_multi(sums)
-        elif self.fused_convs:
+        if self.fused_convs:
             nblk = min(B, self.cus)
             h.conv2_bwd(da2, sh[o["w2"]:o["b2"]], a1, da1, self.cpart["c2"], self.cbias["c2"], B, nblk)
             sums += [(self.cpart["c2"], nblk, L2.cout * L2.K, g[o["w2"]:o["b2"]]),
@@ -483,15 +458,15 @@ class DeviceNatureCNN:
             self._wgrad("c2", da2, a1, B, L2.hin, L2.cin, L2.k, L2.s, L2.cout, o["w2"])
             self._bias(da2, B * L2.hout ** 2, L2.cout, o["b2"])
             self._dgrad(da2, sh[o["w2"]:o["b2"]], a1, da1, B, L2)
-        # conv1 (input = frames, no data gradient; with conv21 it ran above)
+        # conv1 (input = frames, no data gradient)
         # (its bias gradient comes out of the same pass over da1)
-        if self.fused_convs and not self.conv21:
+        if self.fused_convs:
             ns = int(h.conv1_wgrad8(obs_u8.contiguous(), da1, self.cpart["c1"], self.cbias["c1"], B,
                                     min(B, self.cus)))
             sums += [(self.cpart["c1"], ns, S2D.cout * S2D.K, g[o["w1"]:o["b1"]]),
                      (self.cbias["c1"], ns, S2D.cout, g[o["b1"]:o["b1"] + S2D.cout])]
             h.sum_splits_multi(sums)
-        elif not self.fused_convs:
+        else:
             self._wgrad("c1", da1, obs_u8.contiguous(), B, S2D.hin, S2D.cin, S2D.k, S2D.s, S2D.cout, o["w1"],
                         bias_off=o["b1"])
         if side is not None:

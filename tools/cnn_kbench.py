@@ -16,7 +16,7 @@ import torch
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", default="fwd,fwd_layers,bwd3,bwd3_layers,bwd2,bwd21,dgrad2,wgrad1,wgrad1_8")
+    ap.add_argument("--which", default="fwd,fwd_layers,bwd3,bwd3_layers,bwd2,dgrad2,wgrad1,wgrad1_8")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--frames", type=int, default=2048)
     ap.add_argument("--bwd-frames", type=int, default=10240)
@@ -81,10 +81,7 @@ def main():
             h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=1)
         fns["bwd2"] = bwd2
         fns["bwd2_staged"] = bwd2_staged
-    part1 = torch.empty(cus * 32 * 256, device=dev)
-    bpart1 = torch.empty(cus * 32, device=dev)
-    # conv2 backward + conv1 weight gradient in one pass (da1 stays in LDS) vs bwd2 + wgrad1_8
-    fns["bwd21"] = lambda: h.conv21_bwd(da2, W[2][0], a1, x[:Nb], part, bpart, part1, bpart1, Nb, min(Nb, cus))
+
     out = {}
     for name in a.which.split(","):
         f = fns[name]
