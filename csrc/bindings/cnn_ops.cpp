@@ -32,6 +32,7 @@ int rrl_adam_clip(float* p, float* m, float* v, const float* g, uint16_t* shadow
                   float max_norm, float lr, float b1, float b2, float eps, int step, const long long* step_dev,
                   void* stream);
 int rrl_counter_add(long long* c, long long inc, void* stream);
+int rrl_counter_add_n(long long* const* c, const long long* inc, int n, void* stream);
 int rrl_to_bf16(const float* x, uint16_t* y, long long n, void* stream);
 int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, int A, int32_t* act, float* logp,
                  float* value, float* logits_out, unsigned long long seed, unsigned long long step,
@@ -315,6 +316,21 @@ void adam_clip(const Tensor& p, const Tensor& m, const Tensor& v, const Tensor& 
            "adam_clip");
 }
 
+// several device counters in one launch: [(counter, inc), ...], at most 4 (distinct tensors)
+void counter_add_many(const std::vector<std::tuple<Tensor, int64_t>>& adds) {
+  TORCH_CHECK(!adds.empty() && adds.size() <= 4, "counter_add_many: 1..4 counters");
+  long long* cs[4];
+  long long incs[4];
+  for (size_t i = 0; i < adds.size(); ++i) {
+    const Tensor& c = std::get<0>(adds[i]);
+    check(c, "counter", at::kLong, 1);
+    cs[i] = (long long*)c.data_ptr();
+    incs[i] = std::get<1>(adds[i]);
+    for (size_t j = 0; j < i; ++j) TORCH_CHECK(cs[j] != cs[i], "counter_add_many: counters must be distinct");
+  }
+  rc_check(rrl_counter_add_n(cs, incs, (int)adds.size(), stream()), "counter_add_many");
+}
+
 void counter_add(const Tensor& c, int64_t inc) {
   check(c, "counter", at::kLong, 1);
   rc_check(rrl_counter_add((long long*)c.data_ptr(), inc, stream()),
@@ -491,6 +507,7 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("b1"), pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("step"),
         pybind11::arg("step_dev") = pybind11::none());
   m.def("counter_add", &counter_add);
+  m.def("counter_add_many", &counter_add_many);
   m.def("to_bf16", &to_bf16);
   m.def("a2c_head", &a2c_head, pybind11::arg("mode"), pybind11::arg("h"), pybind11::arg("head_params"),
         pybind11::arg("B"), pybind11::arg("A"), pybind11::arg("act"), pybind11::arg("logp"), pybind11::arg("value"),

@@ -1537,14 +1537,30 @@ int rrl_adam_clip(float* p, float* m, float* v, const float* g, uint16_t* shadow
   return (int)hipGetLastError();
 }
 
-__global__ void counter_add_kernel(long long* c, long long inc) { c[0] += inc; }
+struct CounterAdds {
+  long long* c[4];
+  long long inc[4];
+  int n;
+};
+__global__ void counter_add_kernel(CounterAdds a) {
+  if ((int)threadIdx.x < a.n) a.c[threadIdx.x][0] += a.inc[threadIdx.x];
+}
 
-// Device-side step counters advanced inside captured graphs.
-int rrl_counter_add(long long* c, long long inc, void* stream_) {
-  hipStream_t st = (hipStream_t)stream_;
-  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(1), 0, st, c, inc);
+// Device-side step counters advanced inside captured graphs (up to 4 in one launch: the Pong
+// update's sampling, env and Adam counters were three single-thread launches).
+int rrl_counter_add_n(long long* const* c, const long long* inc, int n, void* stream_) {
+  if (n < 1 || n > 4) return -1;
+  CounterAdds a{};
+  for (int i = 0; i < n; ++i) {
+    a.c[i] = c[i];
+    a.inc[i] = inc[i];
+  }
+  a.n = n;
+  hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream_, a);
   return (int)hipGetLastError();
 }
+
+int rrl_counter_add(long long* c, long long inc, void* stream_) { return rrl_counter_add_n(&c, &inc, 1, stream_); }
 
 int rrl_to_bf16(const float* x, uint16_t* y, long long n, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;

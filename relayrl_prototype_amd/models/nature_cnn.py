@@ -504,14 +504,17 @@ class DeviceNatureCNN:
         self.h.sum_splits(self.bias_part, s, C, self.grad[off:off + C])
 
     # ------------------------------------------------------------------ optimizer
-    def apply(self, lr: float, max_grad_norm: float = 0.5, comm=None, betas=(0.9, 0.999), eps: float = 1e-5):
-        """(DP all-reduce) -> global-norm clip -> Adam -> bf16 shadow, all on device."""
+    def apply(self, lr: float, max_grad_norm: float = 0.5, comm=None, betas=(0.9, 0.999), eps: float = 1e-5,
+              step_bumped: bool = False):
+        """(DP all-reduce) -> global-norm clip -> Adam -> bf16 shadow, all on device.
+        ``step_bumped``: the caller already advanced ``step_t`` (folded into another launch)."""
         if comm is not None and comm.multi and not getattr(self, "_reduced", False):
             comm.all_reduce_sum_(self.grad)
             self.grad.mul_(1.0 / comm.world)
         self._reduced = False
         self.h.sumsq(self.grad, self.sq_work, self.norm_sq)
-        self.h.counter_add(self.step_t, 1)
+        if not step_bumped:
+            self.h.counter_add(self.step_t, 1)
         self.h.adam_clip(self.params, self.m, self.v, self.grad, self.shadow,
                          self.norm_sq if max_grad_norm > 0 else None, float(max_grad_norm), float(lr),
                          float(betas[0]), float(betas[1]), float(eps), 0, self.step_t)

@@ -122,8 +122,10 @@ class PixelA2CTrainer:
             # the last observation goes straight to the next update's start slot
             self.env.step(self.act[t], base[t + 1] if (t + 1 < T or nxt is None) else nxt[0], self.rew[t],
                           self.done[t], offset=t)
-        self.model.h.counter_add(self.sample_t, cfg.rollout_len)
-        self.env.advance(cfg.rollout_len)
+        # the sampling, env and Adam step counters advance in ONE launch (the Adam step of this
+        # update's apply(step_bumped=True) below; every rollout is followed by one update)
+        self.model.h.counter_add_many([(self.sample_t, cfg.rollout_len), (self.env.step_t, cfg.rollout_len),
+                                       (m.step_t, 1)])
         # bootstrap V(obs[T]) with the pre-update weights; its activations go to the
         # scratch rows [T*N, (T+1)*N) so the stored rollout activations stay intact
         m.value(base[T] if nxt is None else nxt[0], cfg.rollout_len * N, self.val[cfg.rollout_len])
@@ -141,7 +143,7 @@ class PixelA2CTrainer:
             stats = m.backward(base[:T].reshape(B, 21, 21, 64), self.act.reshape(B), adv.reshape(B),
                                ret.reshape(B), cfg.vf_coef, cfg.ent_coef, comm=self.comm)
         with self.timer.phase("Optimize"):
-            m.apply(cfg.lr, cfg.max_grad_norm, self.comm)
+            m.apply(cfg.lr, cfg.max_grad_norm, self.comm, step_bumped=True)
         return stats
 
     # ------------------------------------------------------------------ CPU
