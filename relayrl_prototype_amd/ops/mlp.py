@@ -262,8 +262,11 @@ def adam_step(param, m, v, step_t, ticket_t, lr, grad=None, slab=None, beta1=0.9
            float(grad_scale), float(weight_decay))
 
 
-def gae_scan_tm(rew, done, val, gamma, lam, adv=None, ret=None, stats_part=None, stats_out=None, tval=None):
-    """Time-major GAE / discounted-return scan -> (adv, ret, stats[3]).
+def gae_scan_tm(rew, done, val, gamma, lam, adv=None, ret=None, stats_part=None, stats_out=None, tval=None,
+                stats=True):
+    """Time-major GAE / discounted-return scan -> (adv, ret, stats[3]).  ``stats=False``: the
+    caller does not use the advantage statistics; the GPU path skips their reduction launch and
+    returns None for them.
 
     ``rew`` / ``done`` / ``tval`` are [T, N], or [K, T, N] for a learner shard holding K
     actor blocks; ``val`` is flat [K*T*N + K*N]: V of every step, then the bootstrap value
@@ -283,7 +286,7 @@ def gae_scan_tm(rew, done, val, gamma, lam, adv=None, ret=None, stats_part=None,
     ret = torch.empty(rew.shape, device=dev) if ret is None else ret
     if stats_part is None:
         stats_part = torch.empty(int(h.scan_tm_parts(K * N)), 3, device=dev)
-    if stats_out is None:
+    if stats_out is None and stats:
         stats_out = torch.empty(3, device=dev)
     h.gae_scan_tm(rew.contiguous(), done.contiguous(), None if val is None else val.contiguous(), _f32(tval), adv, ret,
                   stats_part, stats_out, float(gamma), float(lam))

@@ -99,7 +99,6 @@ class PixelA2CTrainer:
             from ..ops import hip
 
             self._stats_part = torch.zeros(int(hip().scan_tm_parts(N)), 3, device=dev)
-            self._stats_out = torch.zeros(3, device=dev)
             self._graph = None  # the graph of the current buffer parity (None before capture)
             self._graphs = {}
             self._warm = False
@@ -138,7 +137,7 @@ class PixelA2CTrainer:
         B = N * T
         with self.timer.phase("Returns"):
             adv, ret, _ = gae_scan_tm(self.rew, self.done, self.val, cfg.gamma, 1.0, self.adv, self.ret,
-                                      self._stats_part, self._stats_out)
+                                      self._stats_part, stats=False)
         with self.timer.phase("Backward"):
             stats = m.backward(base[:T].reshape(B, 21, 21, 64), self.act.reshape(B), adv.reshape(B),
                                ret.reshape(B), cfg.vf_coef, cfg.ent_coef, comm=self.comm)
