@@ -40,7 +40,7 @@ int rrl_scan_flat(const float* rew, const float* done, const float* val, const f
 int rrl_stats_reduce(const float* part, int nparts, float* out, void* stream);
 int rrl_adam(float* param, float* m, float* v, const float* grad, const float* slab, int nslab,
              float* grad_out, int* step, unsigned* ticket, int P, float lr, float beta1, float beta2,
-             float eps, float grad_scale, float weight_decay, void* stream);
+             float eps, float grad_scale, float weight_decay, int step_add, int step_inc, void* stream);
 int rrl_reduce_slabs(const float* slab, int nslab, int P, float scale, float* out, void* stream);
 int rrl_env_dims(int env, int* D, int* A, int* NS, int* max_steps);
 int rrl_rollout_cont(int env, const float* params, const float* env_consts, int N, int T, int H, float* state,
@@ -274,7 +274,7 @@ void stats_reduce(const Tensor& part, const Tensor& out) {
 
 void adam(const Tensor& param, const Tensor& m, const Tensor& v, const OptT& grad, const OptT& slab,
           const OptT& grad_out, const Tensor& step, const Tensor& ticket, double lr, double beta1, double beta2,
-          double eps, double grad_scale, double weight_decay) {
+          double eps, double grad_scale, double weight_decay, int64_t step_add, int64_t step_inc) {
   check_dev(param, "param", at::kFloat);
   const int64_t P = param.numel();
   check_dev(m, "m", at::kFloat);
@@ -297,7 +297,7 @@ void adam(const Tensor& param, const Tensor& m, const Tensor& v, const OptT& gra
   const int rc = rrl_adam(param.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), g, s, (int)nslab, go,
                           step.data_ptr<int>(), reinterpret_cast<unsigned*>(ticket.data_ptr<int>()), (int)P, (float)lr,
                           (float)beta1, (float)beta2, (float)eps, (float)grad_scale, (float)weight_decay,
-                          cur_stream());
+                          (int)step_add, (int)step_inc, cur_stream());
   check_rc(rc, "adam");
 }
 
@@ -432,7 +432,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scan_flat_blocks", &scan_flat_blocks);
   m.def("scan_flat", &scan_flat);
   m.def("stats_reduce", &stats_reduce);
-  m.def("adam", &adam);
+  // step_add / step_inc: t = step + step_add + 1, the counter advances by step_inc (adam.hip)
+  m.def("adam", &adam, pybind11::arg("param"), pybind11::arg("m"), pybind11::arg("v"), pybind11::arg("grad"),
+        pybind11::arg("slab"), pybind11::arg("grad_out"), pybind11::arg("step"), pybind11::arg("ticket"),
+        pybind11::arg("lr"), pybind11::arg("beta1"), pybind11::arg("beta2"), pybind11::arg("eps"),
+        pybind11::arg("grad_scale"), pybind11::arg("weight_decay"), pybind11::arg("step_add") = 0,
+        pybind11::arg("step_inc") = 1);
   m.def("reduce_slabs", &reduce_slabs);
   m.def("env_dims", &env_dims);
   m.def("rollout_grid", &rollout_grid);

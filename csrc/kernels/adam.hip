@@ -4,7 +4,11 @@
 //
 // The step counter lives on the device so that an optimisation loop (e.g. the 80
 // value iterations, REINFORCE.py:110-115) can be captured into one hipGraph: every
-// block reads t from `step`, and the last block to finish (arrival ticket) bumps it.
+// block reads the counter s0 and uses t = s0 + step_add + 1; the last block to finish
+// (arrival ticket) sets the counter to s0 + step_inc.  A loop of K updates passes
+// step_add = k and step_inc = 0 (no ticket at all) for k < K - 1 and step_inc = K on the last
+// one: the ticket's 271-way serialised device-scope atomic (~3 us at the end of every update,
+// MI355X_MICROARCH.md fanin) is paid once per loop instead of once per update.
 #include "common.h"
 
 namespace rrl {
@@ -18,8 +22,9 @@ struct AdamArgs {
   int nslab;
   float* grad_out;    // optional: write the reduced gradient here
   int* step;          // device step counter
-  unsigned* ticket;   // device arrival counter (zeroed by the last block)
+  unsigned* ticket;   // device arrival counter (zeroed by the last block); null: step_inc == 0
   int P;
+  int step_add, step_inc;
   float lr, beta1, beta2, eps, grad_scale, weight_decay;
 };
 
@@ -54,7 +59,8 @@ RRL_DEV float slab_group_sum(const float* __restrict__ slab, int nslab, int P, i
 
 __global__ __launch_bounds__(1024) void adam_kernel(AdamArgs a) {
   __shared__ float part[kAdamGroups][kAdamCols];
-  const int t = *a.step + 1;
+  const int s0 = *a.step;
+  const int t = s0 + a.step_add + 1;
   const int col = threadIdx.x & (kAdamCols - 1);
   const int grp = threadIdx.x / kAdamCols;
   const int p = blockIdx.x * kAdamCols + col;
@@ -94,11 +100,11 @@ __global__ __launch_bounds__(1024) void adam_kernel(AdamArgs a) {
   }
   // arrival ticket: the last block bumps the step counter (every block read `step`
   // above, before its __syncthreads / ticket)
-  if (threadIdx.x == 0) {
+  if (a.ticket && threadIdx.x == 0) {
     const unsigned prev = atomicAdd(a.ticket, 1u);
     if (prev == gridDim.x - 1) {
       *a.ticket = 0u;
-      *a.step = t;
+      *a.step = s0 + a.step_inc;
     }
   }
 }
@@ -128,9 +134,11 @@ using namespace rrl;
 
 extern "C" int rrl_adam(float* param, float* m, float* v, const float* grad, const float* slab, int nslab,
                         float* grad_out, int* step, unsigned* ticket, int P, float lr, float beta1,
-                        float beta2, float eps, float grad_scale, float weight_decay, void* stream) {
-  AdamArgs a{param, m, v, grad, slab, nslab, grad_out, step, ticket, P, lr, beta1, beta2, eps, grad_scale,
-             weight_decay};
+                        float beta2, float eps, float grad_scale, float weight_decay, int step_add, int step_inc,
+                        void* stream) {
+  if (step_inc != 0 && ticket == nullptr) return -1;
+  AdamArgs a{param, m, v, grad, slab, nslab, grad_out, step, step_inc != 0 ? ticket : nullptr, P, step_add,
+             step_inc, lr, beta1, beta2, eps, grad_scale, weight_decay};
   const int grid = (P + kAdamCols - 1) / kAdamCols;
   hipLaunchKernelGGL(adam_kernel, dim3(grid < 1 ? 1 : grid), dim3(kAdamCols * kAdamGroups), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();

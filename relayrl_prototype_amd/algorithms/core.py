@@ -42,17 +42,18 @@ class FlatNet:
     def P(self) -> int:
         return self.spec.P
 
-    def apply(self, slab: torch.Tensor, comm: Optional[Comm] = None):
-        """Reduce the gradient slabs (and all-reduce across ranks) then take one Adam step."""
+    def apply(self, slab: torch.Tensor, comm: Optional[Comm] = None, step_add: int = 0, step_inc: int = 1):
+        """Reduce the gradient slabs (and all-reduce across ranks) then take one Adam step
+        (``step_add`` / ``step_inc``: see ops.adam_step, the loop form of the step counter)."""
         b1, b2 = self.betas
         if comm is None or not comm.multi:
             adam_step(self.params, self.m, self.v, self.step, self.ticket, self.lr, slab=slab, beta1=b1, beta2=b2,
-                      eps=self.eps, weight_decay=self.weight_decay)
+                      eps=self.eps, weight_decay=self.weight_decay, step_add=step_add, step_inc=step_inc)
         else:
             reduce_slabs(slab, 1.0, out=self.grad)
             comm.all_reduce_sum_(self.grad)
             adam_step(self.params, self.m, self.v, self.step, self.ticket, self.lr, grad=self.grad, beta1=b1,
-                      beta2=b2, eps=self.eps, weight_decay=self.weight_decay)
+                      beta2=b2, eps=self.eps, weight_decay=self.weight_decay, step_add=step_add, step_inc=step_inc)
         self.version += 1
 
     def state_dict(self) -> dict:
@@ -93,7 +94,8 @@ class ValueLoop:
             ls = ls_first if k == 0 else ls_last
             mlp_grad(GradHead.VALUE_MSE, self.net.params, obs, 1, H, ret=ret, inv_B=inv_B, grad_slab=slab,
                      loss_slab=ls, nvalid=nvalid, inv_B_dev=inv_B_dev)
-            self.net.apply(slab, self.comm)
+            # Adam step s0 + k + 1; only the last update of the loop advances the counter (by iters)
+            self.net.apply(slab, self.comm, step_add=k, step_inc=iters if k == iters - 1 else 0)
 
     def step(self, obs: torch.Tensor, ret: torch.Tensor, inv_B: float, first: bool = False):
         """One eager value step on a (mini)batch; ``first`` marks the step whose loss is

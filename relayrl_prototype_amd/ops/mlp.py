@@ -245,21 +245,24 @@ def reduce_slabs(slab: torch.Tensor, scale: float = 1.0, out=None):
 
 
 def adam_step(param, m, v, step_t, ticket_t, lr, grad=None, slab=None, beta1=0.9, beta2=0.999, eps=1e-8,
-              grad_scale=1.0, weight_decay=0.0, grad_out=None):
+              grad_scale=1.0, weight_decay=0.0, grad_out=None, step_add=0, step_inc=1):
     """One fused Adam update of a flat parameter vector; `step_t` is a 1-elem int32 tensor
-    holding the number of completed steps (incremented on the device)."""
+    holding the number of completed steps (advanced on the device).  The update uses step
+    t = step_t + step_add + 1 and leaves step_t + step_inc behind: a loop of K updates passes
+    (k, 0) for k < K - 1 and (K - 1, K) last, so only its last update pays the device-wide
+    arrival ticket that advances the counter (adam.hip)."""
     h = _hip_for(param)
     if h is None:
         g = grad if grad is not None else slab.sum(0)
         g = g * grad_scale
         if grad_out is not None:
             grad_out.copy_(g)
-        step = int(step_t.item()) + 1
-        ref.adam_ref(param, m, v, g, step, lr, beta1, beta2, eps, weight_decay)
-        step_t.fill_(step)
+        s0 = int(step_t.item())
+        ref.adam_ref(param, m, v, g, s0 + step_add + 1, lr, beta1, beta2, eps, weight_decay)
+        step_t.fill_(s0 + step_inc)
         return
     h.adam(param, m, v, grad, slab, grad_out, step_t, ticket_t, float(lr), float(beta1), float(beta2), float(eps),
-           float(grad_scale), float(weight_decay))
+           float(grad_scale), float(weight_decay), int(step_add), int(step_inc))
 
 
 def gae_scan_tm(rew, done, val, gamma, lam, adv=None, ret=None, stats_part=None, stats_out=None, tval=None,

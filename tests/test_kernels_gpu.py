@@ -182,6 +182,38 @@ def test_slab_reduction_and_adam_all_batchings(cuda, nslab):
     torch.testing.assert_close(pg.cpu(), pt.detach(), rtol=1e-5, atol=1e-6)
 
 
+def test_adam_loop_form_of_the_step_counter(cuda):
+    """A loop of K Adam updates passing (step_add, step_inc) = (k, 0) and (K - 1, K) last -- no
+    arrival ticket but on the last update -- equals K single updates bitwise (same bias
+    corrections), and leaves the counter at s0 + K; the CPU path agrees."""
+    torch.manual_seed(3)
+    P, K = 17_281, 6
+    slabs = [torch.randn(7, P, device=cuda) for _ in range(K)]
+    p0 = torch.randn(P, device=cuda)
+    outs = []
+    for loop in (False, True):
+        pg, m, v = p0.clone(), torch.zeros(P, device=cuda), torch.zeros(P, device=cuda)
+        step = torch.full((1,), 4, dtype=torch.int32, device=cuda)  # resumed after 4 updates
+        ticket = torch.zeros(1, dtype=torch.int32, device=cuda)
+        for k in range(K):
+            if loop:
+                adam_step(pg, m, v, step, ticket, 1e-3, slab=slabs[k], step_add=k, step_inc=K if k == K - 1 else 0)
+            else:
+                adam_step(pg, m, v, step, ticket, 1e-3, slab=slabs[k])
+        torch.cuda.synchronize()
+        assert int(step.item()) == 4 + K and int(ticket.item()) == 0
+        outs.append((pg.clone(), m.clone(), v.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    # the CPU (torch) path of the same loop
+    pc, mc, vc = p0.cpu(), torch.zeros(P), torch.zeros(P)
+    sc, tc = torch.full((1,), 4, dtype=torch.int32), torch.zeros(1, dtype=torch.int32)
+    for k in range(K):
+        adam_step(pc, mc, vc, sc, tc, 1e-3, slab=slabs[k].cpu(), step_add=k, step_inc=K if k == K - 1 else 0)
+    assert int(sc.item()) == 4 + K
+    torch.testing.assert_close(pc, outs[0][0].cpu(), rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("T,N,baseline", [(64, 1000, True), (128, 33, False), (7, 5000, True)])
 def test_gae_scan_tm(cuda, T, N, baseline):
     torch.manual_seed(T + N)

@@ -6,7 +6,9 @@ captured loop, the gradient kernel alone and the reduce+Adam kernel alone are ti
 
     python tools/ttt_levers_probe.py [--B 8192] [--iters 80] [--caps 0,96,64,32]
 
-One JSON line per cap: loop / grad / adam microseconds per iteration and the slab count.
+One JSON line per cap: loop / grad / adam microseconds per iteration and the slab count
+(adam_us: every update pays the arrival ticket; adam_loop_form_us: one ticket per loop, as
+ValueLoop runs it since round 4).
 (The stamp build -- ``tools/kbench.py grad --B 8192 --stamps`` -- gives the prologue /
 per-slab / epilogue split of the gradient kernel that prices the split-image lever.)
 """
@@ -88,10 +90,17 @@ def main():
                 for _ in range(a.iters):
                     adam_step(net.params, net.m, net.v, net.step, net.ticket, 1e-9, slab=slab)
 
+            def adams_loop():  # the loop form of the step counter: one arrival ticket per loop
+                for k in range(a.iters):
+                    adam_step(net.params, net.m, net.v, net.step, net.ticket, 1e-9, slab=slab, step_add=k,
+                              step_inc=a.iters if k == a.iters - 1 else 0)
+
             grad_us = graph_time(grads) / a.iters
             adam_us = graph_time(adams) / a.iters
+            adam_loop_us = graph_time(adams_loop) / a.iters
             print(json.dumps({"B": a.B, "cu_cap": cap, "slabs": ns, "loop_us_per_iter": round(loop_us, 2),
                               "grad_us": round(grad_us, 2), "adam_us": round(adam_us, 2),
+                              "adam_loop_form_us": round(adam_loop_us, 2),
                               "epoch_value_loop_ms": round(loop_us * a.iters / 1e3, 3)}), flush=True)
         finally:
             h.set_cu_limit(old)
