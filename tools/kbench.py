@@ -108,9 +108,12 @@ def main():
         slab = torch.empty(ns, pp.numel(), device=dev)
         ls = torch.empty(ns, 8, device=dev)
         st = torch.tensor([0.0, float(B), float(B)], device=dev)
-        us = timeit(lambda: mlp_grad(GradHead.PG_CAT, pp, X, 2, H, act=act, adv=adv, adv_stats=st, grad_slab=slab,
-                                     loss_slab=ls), a.iters)
+        fpg = lambda: mlp_grad(GradHead.PG_CAT, pp, X, 2, H, act=act, adv=adv, adv_stats=st, grad_slab=slab,  # noqa
+                               loss_slab=ls)
+        us = timeit(fpg, a.iters)
         res["policy_grad_us"] = us
+        if a.stamps:
+            run_stamps(fpg, ns, 0, "policy_cat2", B)
         old = hip().set_value_grad_mode(0)
         res["policy_grad_fp32mfma_us"] = timeit(lambda: mlp_grad(GradHead.PG_CAT, pp, X, 2, H, act=act, adv=adv,
                                                                  adv_stats=st, grad_slab=slab, loss_slab=ls), a.iters)
