@@ -257,6 +257,7 @@ class DeviceNatureCNN:
         self.sq_work = torch.empty(1024, device=dev)
         # side stream for the head / fc weight gradients (backward, one rank; RRL_CNN_SIDE=0: off)
         self.side_stream = torch.cuda.Stream(device=dev) if os.environ.get("RRL_CNN_SIDE", "1") != "0" else None
+        self.side_late = os.environ.get("RRL_CNN_SIDE_LATE", "0") == "1"
         self._ev_fork = torch.cuda.Event()
         self._ev_join = torch.cuda.Event()
         self.norm_sq = torch.empty(1, device=dev)
@@ -397,15 +398,8 @@ class DeviceNatureCNN:
         # stream: its fc bucket all-reduce is issued as soon as these gradients are final.
         side = (self.side_stream if (self.side_stream is not None and self.fused_convs and self.fc_nt
                                      and B % 64 == 0 and (comm is None or not comm.multi)) else None)
-        if side is not None:
-            self._ev_fork.record()
-            side.wait_event(self._ev_fork)
-            ctx = torch.cuda.stream(side)
-        else:
-            import contextlib
 
-            ctx = contextlib.nullcontext()
-        with ctx:
+        def weight_grads():  # head + fc weight / bias gradients
             h.head_wgrad(hid, dhead, B, self.A, hp, nb)
             h.sum_splits(hp, nb, self.spec.head_size, g[o["head"]:o["P"]])
             # fc
@@ -423,13 +417,29 @@ class DeviceNatureCNN:
             else:
                 self._wgrad("fc", dh, a3, B, 1, FC_IN, 1, 1, HIDDEN, o["wfc"])
                 self._bias(dh, B, HIDDEN, o["bfc"])
-            if side is not None:
+
+        def fork_weight_grads():
+            if side is None:
+                weight_grads()
+                return
+            self._ev_fork.record()
+            side.wait_event(self._ev_fork)
+            with torch.cuda.stream(side):
+                weight_grads()
                 self._ev_join.record(side)
+
+        # side_late: fork after the fc data gradient, so the side work runs beside the
+        # latency-bound conv3 backward (1 workgroup per CU, room for one fc_tn workgroup)
+        # instead of competing with the 2,000-workgroup fc data-gradient GEMM
+        if not (side is not None and self.side_late):
+            fork_weight_grads()
         da3 = self.da3[:B * FC_IN]
         if self.fc_nt:
             h.fc_nt_mask(dh, self.wfc_t, a3, da3, B, FC_IN, HIDDEN)
         else:
             h.gemm_dgrad(dh, sh[o["wfc"]:o["bfc"]], a3, da3, B, HIDDEN, FC_IN)
+        if side is not None and self.side_late:
+            fork_weight_grads()
         if comm is not None and comm.multi:
             import torch.distributed as dist
 
