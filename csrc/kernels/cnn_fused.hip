@@ -826,9 +826,12 @@ extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16
 // per image with the next image prefetched into registers.
 namespace c1w {
 constexpr int kThreads = 512;
-constexpr int kLd = 80;
-constexpr int kXRows = 448, kYRows = 416;
-constexpr int kLds = (kXRows + kYRows) * kLd * 2;  // 138,240 bytes
+// frame positions in LDS rows of 28 (as the fused forward) and dY rows of 48 elements: the
+// transposed fragment reads of both images conflict-free in tools/lds_bank_model.py (the frame
+// in 21-wide rows: 1.19 LDS cycles per conflict-free cycle)
+constexpr int kLd = 80, kYLd = 48, kXW = 28;
+constexpr int kXRows = 20 * kXW + 24, kYRows = 416;
+constexpr int kLds = (kXRows * kLd + kYRows * kYLd) * 2;  // 133,632 bytes
 constexpr int kXC = 441 * 4, kYC = 400 * 4;       // 16-byte chunks per image
 constexpr int kXPT = (kXC + kThreads - 1) / kThreads, kYPT = (kYC + kThreads - 1) / kThreads;
 }  // namespace c1w
@@ -839,13 +842,13 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
                                                                         float* __restrict__ bias_part, int N) {
   using namespace c1w;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  uint16_t* Xi = smem;                // [448][80] frame, bf16 integers 0..255
-  uint16_t* Yi = smem + kXRows * kLd;  // [416][80] dY (rows 400.. zero)
+  uint16_t* Xi = smem;                // [21 x 28][80] frame, bf16 integers 0..255
+  uint16_t* Yi = smem + kXRows * kLd;  // [416][48] dY (rows 400.. zero)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tap = wave & 3, kh = tap >> 1, kw = tap & 1, half = wave >> 2;
   const int kc0 = half ? 7 : 0, kc1 = half ? 13 : 7;
-  for (int q = tid; q < 16 * (kLd / 8); q += kThreads)
-    *reinterpret_cast<uint4*>(Yi + (400 + q / (kLd / 8)) * kLd + 8 * (q % (kLd / 8))) = make_uint4(0, 0, 0, 0);
+  for (int q = tid; q < 16 * (kYLd / 8); q += kThreads)
+    *reinterpret_cast<uint4*>(Yi + (400 + q / (kYLd / 8)) * kYLd + 8 * (q % (kYLd / 8))) = make_uint4(0, 0, 0, 0);
 
   f32x4_t acc[2][4], accb[2];
 #pragma unroll
@@ -887,7 +890,8 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
     for (int i = 0; i < kXPT; ++i) {
       const int q = tid + kThreads * i;
       if (q < kXC) {
-        uint16_t* d = Xi + (q >> 2) * kLd + (q & 3) * 16;
+        const int pix = q >> 2;
+        uint16_t* d = Xi + (pix + (kXW - 21) * (pix / 21)) * kLd + (q & 3) * 16;
         *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(rx[i].x, rx[i].y));
         *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(rx[i].z, rx[i].w));
       }
@@ -895,7 +899,7 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
 #pragma unroll
     for (int i = 0; i < kYPT; ++i) {
       const int q = tid + kThreads * i;
-      if (q < kYC) *reinterpret_cast<uint4*>(Yi + (q >> 2) * kLd + (q & 3) * 8) = ry[i];
+      if (q < kYC) *reinterpret_cast<uint4*>(Yi + (q >> 2) * kYLd + (q & 3) * 8) = ry[i];
     }
     if (n + G < N) gload(n + G);
     __syncthreads();
@@ -904,12 +908,12 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
 #pragma unroll 1
     for (int kc = kc0; kc < kc1; ++kc) {
       const int pa = 32 * kc + 4 * g, pb = pa + 16;
-      const int ra = (pa < 400 ? (pa / 20 + kh) * 21 + pa % 20 + kw : 0) + qq;
-      const int rb = (pb < 400 ? (pb / 20 + kh) * 21 + pb % 20 + kw : 0) + qq;
+      const int ra = (pa < 400 ? (pa / 20 + kh) * kXW + pa % 20 + kw : 0) + qq;
+      const int rb = (pb < 400 ? (pb / 20 + kh) * kXW + pb % 20 + kw : 0) + qq;
       bf16x8_t af[2], bfr[4];
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
-        af[mt] = tr_frag2(Yi + (pa + qq) * kLd + 16 * mt + 4 * pp, Yi + (pb + qq) * kLd + 16 * mt + 4 * pp);
+        af[mt] = tr_frag2(Yi + (pa + qq) * kYLd + 16 * mt + 4 * pp, Yi + (pb + qq) * kYLd + 16 * mt + 4 * pp);
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
         bfr[nt] = tr_frag2(Xi + ra * kLd + 16 * nt + 4 * pp, Xi + rb * kLd + 16 * nt + 4 * pp);
