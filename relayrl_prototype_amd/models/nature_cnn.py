@@ -257,7 +257,7 @@ class DeviceNatureCNN:
         self.sq_work = torch.empty(1024, device=dev)
         # side stream for the head / fc weight gradients (backward, one rank; RRL_CNN_SIDE=0: off)
         self.side_stream = torch.cuda.Stream(device=dev) if os.environ.get("RRL_CNN_SIDE", "1") != "0" else None
-        self.side_late = os.environ.get("RRL_CNN_SIDE_LATE", "1") == "1"
+        self.side_late = os.environ.get("RRL_CNN_SIDE_LATE", "0") == "1"
         self._ev_fork = torch.cuda.Event()
         self._ev_join = torch.cuda.Event()
         self.norm_sq = torch.empty(1, device=dev)
@@ -428,10 +428,10 @@ class DeviceNatureCNN:
                 weight_grads()
                 self._ev_join.record(side)
 
-        # side_late (default; RRL_CNN_SIDE_LATE=0: fork before it): fork after the fc data
-        # gradient (+0.5 % per update, profiles/r4_side_late_and_configs.txt), so the side work runs beside the
-        # latency-bound conv3 backward (1 workgroup per CU, room for one fc_tn workgroup)
-        # instead of competing with the 2,000-workgroup fc data-gradient GEMM
+        # RRL_CNN_SIDE_LATE=1: fork after the fc data gradient instead, so the side work runs
+        # beside the latency-bound conv3 backward rather than the 2,000-workgroup fc GEMM -- +0.5 %
+        # on one box, -3 to -3.4 % at 2,048 / 8,192 envs alternated on another
+        # (profiles/r4_side_late_and_configs.txt, r4_side_late_ab.txt): off by default
         if not (side is not None and self.side_late):
             fork_weight_grads()
         da3 = self.da3[:B * FC_IN]
