@@ -1,3 +1,5 @@
+# NOTE: a record of the run behind its profiles/r4_* files; the A/B options it passes (the pair conv split
+# fwd_split / fwd_pair, RRL_FC_HEAD, RRL_FH_STAGES, RRL_CONV21, bwd21) were removed after measuring slower.
 # Round 4: PMC of the conv stack forward (per-layer vs pair split), flagship kernel profile,
 # TTT value-loop levers (slab-count sweep, stamps, epoch profile)
 set -o pipefail

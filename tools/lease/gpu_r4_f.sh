@@ -1,3 +1,5 @@
+# NOTE: a record of the run behind its profiles/r4_* files; the A/B options it passes (the pair conv split
+# fwd_split / fwd_pair, RRL_FC_HEAD, RRL_FH_STAGES, RRL_CONV21, bwd21) were removed after measuring slower.
 # Round 4: padding-only LDS layouts of the conv backward kernels, 28-wide frame rows in the fused
 # forward, the rollout fc + head in one full-K GEMM launch (A/B against the split-K head), conv2 backward +
 # conv1 weight gradient fused (A/B), Pong render with row flags / LDS state
