@@ -292,6 +292,13 @@ class DeviceNatureCNN:
         tiles = -(-n // 128) * (HIDDEN // 128)
         return max(1, min(8, -(-256 // tiles)))
 
+    # rollout rows per wave of the head launch (4 waves per workgroup); RRL_HEAD_ROWS for A/B
+    HEAD_ROWS_PER_WAVE = int(os.environ.get("RRL_HEAD_ROWS", "1"))
+
+    def _head_grid(self, n: int) -> int:
+        r = max(1, self.HEAD_ROWS_PER_WAVE)
+        return max(1, min(1024, (n + 4 * r - 1) // (4 * r)))
+
     def _fc_head(self, a3, hid, n, **head):
         """fc GEMM as split-K partials, then ONE head launch: bias + ReLU + bf16 hid (stored for
         the backward) + logits / value / sampling."""
@@ -302,7 +309,7 @@ class DeviceNatureCNN:
         self.h.a2c_head(0, hid, self.params[o["head"]:], n, self.A, head.get("act"), head.get("logp"),
                         head.get("value"), head.get("logits"), int(head.get("seed", 0)), int(head.get("step", 0)),
                         int(head.get("row_offset", 0)), None, None, None, 0.0, 0.0, 0.0, None, None, None,
-                        max(1, min(1024, (n + 3) // 4)), head.get("step_base"), part=self._fc_part, splits=used,
+                        self._head_grid(n), head.get("step_base"), part=self._fc_part, splits=used,
                         fc_b=self.params[o["bfc"]:o["bfc"] + HIDDEN])
 
     def forward(self, obs_u8: torch.Tensor, row0: int = 0, fc: bool = True, store_acts: bool = True):
@@ -345,7 +352,7 @@ class DeviceNatureCNN:
         self.h.a2c_head(0, hid, self.params[self.o["head"]:], n, self.A, head.get("act"), head.get("logp"),
                         head.get("value"), head.get("logits"), int(head.get("seed", 0)), int(head.get("step", 0)),
                         int(head.get("row_offset", 0)), None, None, None, 0.0, 0.0, 0.0, None, None, None,
-                        max(1, min(1024, (n + 3) // 4)), head.get("step_base"))
+                        self._head_grid(n), head.get("step_base"))
 
     def act(self, obs_u8, row0, act_out, logp_out, value_out, seed: int, step: int, row_offset: int = 0,
             step_base=None):
