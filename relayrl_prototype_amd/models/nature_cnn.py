@@ -258,7 +258,6 @@ class DeviceNatureCNN:
         # side stream for the head / fc weight gradients (backward, one rank; RRL_CNN_SIDE=0: off)
         self.side_stream = torch.cuda.Stream(device=dev) if os.environ.get("RRL_CNN_SIDE", "1") != "0" else None
         self.side_late = os.environ.get("RRL_CNN_SIDE_LATE", "0") == "1"
-        self.head_rows = int(os.environ.get("RRL_HEAD_ROWS", "1"))  # rollout head rows per wave (A/B knob)
         self._ev_fork = torch.cuda.Event()
         self._ev_join = torch.cuda.Event()
         self.norm_sq = torch.empty(1, device=dev)
@@ -293,10 +292,11 @@ class DeviceNatureCNN:
         tiles = -(-n // 128) * (HIDDEN // 128)
         return max(1, min(8, -(-256 // tiles)))
 
-    def _head_grid(self, n: int) -> int:
-        """Workgroups of the rollout head launch: ``head_rows`` rows per wave, 4 waves each."""
-        r = max(1, self.head_rows)
-        return max(1, min(1024, (n + 4 * r - 1) // (4 * r)))
+    @staticmethod
+    def _head_grid(n: int) -> int:
+        """Workgroups of the rollout head launch: one row per wave, 4 waves each (2 or 4 rows per
+        wave measured 1.5 / 5 % slower per update: profiles/r4_head_rows_ab.txt)."""
+        return max(1, min(1024, (n + 3) // 4))
 
     def _fc_head(self, a3, hid, n, **head):
         """fc GEMM as split-K partials, then ONE head launch: bias + ReLU + bf16 hid (stored for

@@ -1,3 +1,4 @@
+# NOTE: a record of profiles/r4_head_rows_ab.txt; the RRL_HEAD_ROWS knob it sets was removed after the A/B.
 # Round 4: rollout head rows per wave (1 / 2 / 4), alternated twice on one box
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
