@@ -257,7 +257,15 @@ class DeviceNatureCNN:
         self.sq_work = torch.empty(1024, device=dev)
         # side stream for the head / fc weight gradients (backward, one rank; RRL_CNN_SIDE=0: off)
         self.side_stream = torch.cuda.Stream(device=dev) if os.environ.get("RRL_CNN_SIDE", "1") != "0" else None
-        self.side_late = os.environ.get("RRL_CNN_SIDE_LATE", "0") == "1"
+        # what the side stream takes (RRL_CNN_SIDE_MODE): "early" = head + fc weight gradients
+        # forked before the fc data gradient (the two fc GEMMs share the chip); "late" = the
+        # same work forked after it (beside conv3_bwd); "sums" = both fc GEMMs back to back on
+        # the main stream and only the memory-light head gradient + split sums forked beside
+        # conv3_bwd
+        self.side_mode = os.environ.get("RRL_CNN_SIDE_MODE", "early")
+        if os.environ.get("RRL_CNN_SIDE_LATE", "0") == "1":
+            self.side_mode = "late"
+        assert self.side_mode in ("early", "late", "sums"), self.side_mode
         self._ev_fork = torch.cuda.Event()
         self._ev_join = torch.cuda.Event()
         self.norm_sq = torch.empty(1, device=dev)
@@ -405,15 +413,21 @@ class DeviceNatureCNN:
         side = (self.side_stream if (self.side_stream is not None and self.fused_convs and self.fc_nt
                                      and B % 64 == 0 and (comm is None or not comm.multi)) else None)
 
+        fc_tn_used = []
+
+        def fc_tn():  # weight AND bias gradient of fc in one GEMM: the padded last column tile
+            # of a3 reads a column of ones, so its first pad column holds the column sums of dh
+            fc_tn_used.append(int(h.fc_tn_part(dh, a3, self.part, B, HIDDEN, FC_IN, self.FC_WGRAD_SPLITS,
+                                               ones=self._ones8, bias_part=self._fc_bias_part)))
+
         def weight_grads():  # head + fc weight / bias gradients
             h.head_wgrad(hid, dhead, B, self.A, hp, nb)
             h.sum_splits(hp, nb, self.spec.head_size, g[o["head"]:o["P"]])
             # fc
             if self.fc_nt and B % 64 == 0 and self.fc_tn_bias:
-                # weight AND bias gradient in one GEMM: the padded last column tile of a3 reads a
-                # column of ones, so its first pad column holds the column sums of dh (fc.hip)
-                used = int(h.fc_tn_part(dh, a3, self.part, B, HIDDEN, FC_IN, self.FC_WGRAD_SPLITS, ones=self._ones8,
-                                        bias_part=self._fc_bias_part))
+                if not fc_tn_used:  # side mode "sums" ran the GEMM on the main stream already
+                    fc_tn()
+                used = fc_tn_used[0]
                 h.sum_splits_multi([(self.part, used, HIDDEN * FC_IN, g[o["wfc"]:o["bfc"]]),
                                     (self._fc_bias_part, used, HIDDEN, g[o["bfc"]:o["bfc"] + HIDDEN])])
             elif self.fc_nt and B % 64 == 0:
@@ -434,18 +448,24 @@ class DeviceNatureCNN:
                 weight_grads()
                 self._ev_join.record(side)
 
-        # RRL_CNN_SIDE_LATE=1: fork after the fc data gradient instead, so the side work runs
+        # side mode "late": fork after the fc data gradient instead, so the side work runs
         # beside the latency-bound conv3 backward rather than the 2,000-workgroup fc GEMM -- +0.5 %
         # on one box, -3 to -3.4 % at 2,048 / 8,192 envs alternated on another
-        # (profiles/r4_side_late_and_configs.txt, r4_side_late_ab.txt): off by default
-        if not (side is not None and self.side_late):
+        # (profiles/r4_side_late_and_configs.txt, r4_side_late_ab.txt).  Mode "sums": the fc
+        # weight GEMM runs right after the data GEMM on the main stream (in "early" the two
+        # overlap and stretch each other: 48 + 42 us alone, ~126 us together in the trace)
+        mode = self.side_mode if side is not None else "early"
+        sums_mode = mode == "sums" and self.fc_nt and B % 64 == 0 and self.fc_tn_bias
+        if mode == "early" or (mode == "sums" and not sums_mode):
             fork_weight_grads()
         da3 = self.da3[:B * FC_IN]
         if self.fc_nt:
             h.fc_nt_mask(dh, self.wfc_t, a3, da3, B, FC_IN, HIDDEN)
         else:
             h.gemm_dgrad(dh, sh[o["wfc"]:o["bfc"]], a3, da3, B, HIDDEN, FC_IN)
-        if side is not None and self.side_late:
+        if sums_mode:
+            fc_tn()
+        if mode == "late" or sums_mode:
             fork_weight_grads()
         if comm is not None and comm.multi:
             import torch.distributed as dist

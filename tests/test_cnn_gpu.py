@@ -710,19 +710,22 @@ def test_pixel_update_side_stream_is_race_free(cuda, monkeypatch):
 
     cfg = dict(num_envs=64, rollout_len=4, seed=5)
     runs = []
-    for side in ("1", "0"):
+    for side, mode in (("0", "early"), ("1", "early"), ("1", "late"), ("1", "sums")):
         monkeypatch.setenv("RRL_CNN_SIDE", side)
+        monkeypatch.setenv("RRL_CNN_SIDE_MODE", mode)
         tr = PixelA2CTrainer(PixelA2CConfig(use_graphs=True, **cfg), device=cuda)
-        assert (tr.model.side_stream is not None) == (side == "1")
+        assert (tr.model.side_stream is not None) == (side == "1") and tr.model.side_mode == mode
         for _ in range(5):  # eager warm-up, capture + replay, 3 replays
             tr.train_epoch()
         torch.cuda.synchronize()
         runs.append(tr)
-    a, b = runs
-    assert a._graph is not None and b._graph is not None
-    assert torch.equal(a.act, b.act) and torch.equal(a.obs, b.obs)
-    torch.testing.assert_close(a.model.params, b.model.params, rtol=0, atol=0)
-    torch.testing.assert_close(a.model.grad, b.model.grad, rtol=0, atol=0)
+    b = runs[0]
+    assert b._graph is not None
+    for a in runs[1:]:
+        assert a._graph is not None
+        assert torch.equal(a.act, b.act) and torch.equal(a.obs, b.obs)
+        torch.testing.assert_close(a.model.params, b.model.params, rtol=0, atol=0)
+        torch.testing.assert_close(a.model.grad, b.model.grad, rtol=0, atol=0)
 
 
 def test_pixel_alternating_obs_buffers_match_copy_path(cuda, monkeypatch):
