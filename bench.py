@@ -509,7 +509,8 @@ def main(argv=None):
             rec["time_to_threshold_reference_hparams_s"] = None if ttt_ref[0] is None else round(ttt_ref[0], 4)
             rec["time_to_threshold"] = {
                 "criterion": "mean return of the newest >= 100 finished episodes >= 475 (gymnasium CartPole-v1), "
-                             "checked after every epoch",
+                             "checked after every epoch (its sums read one epoch behind, behind the next queued "
+                             "epoch: RRL_TTT_LAGGED_CHECK; the clock stops when they reach the host)",
                 "clock": "starts at TrainingServer(..., engine='vec') construction (api/server.py), stops after "
                          "the first solved epoch; includes trainer/buffer allocation",
                 "tuned": pack(ttt, {"gamma": 0.99, "lam": 0.95, "pi_lr": args.ttt_pi_lr, "vf_lr": args.ttt_vf_lr,

@@ -315,6 +315,15 @@ class EngineAlgorithm(AlgorithmAbstract):
         r = m.get("AverageEpRet", float("nan"))
         return n, (n * r if n > 0 and r == r else 0.0)
 
+    def episode_sums_async(self):
+        """A handle whose ``result()`` is episode_sums(), read without draining the stream when
+        the trainer supports it (VecTrainer.episode_sums_async), else computed now."""
+        if hasattr(self.trainer, "episode_sums_async"):
+            return self.trainer.episode_sums_async()
+        from .vec_trainer import PendingSums
+
+        return PendingSums(self.episode_sums())
+
     def state_dict(self) -> Dict[str, Any]:
         return {"trainer": self.trainer.state_dict(), "epoch": self.epoch, "version": self.version}
 
@@ -376,6 +385,13 @@ class EngineRunner:
             steps0 = int(getattr(algo.trainer, "env_steps", 0)) * world
             solved, ttt, win = False, None, float("nan")
             m: Dict[str, Any] = {}
+            # without per-epoch logging the threshold check runs one epoch behind: epoch k's
+            # episode sums are read after epoch k + 1 is queued, so the GPU never drains for
+            # the check (~3 % of a reference-hyperparameter epoch, docs/ROUND4.md); the clock
+            # stops when the solved epoch's sums reach the host, as before
+            lag = (check is not None and not log_every and hasattr(algo, "episode_sums_async")
+                   and os.environ.get("RRL_TTT_LAGGED_CHECK", "1") != "0")
+            pending = None
             while True:
                 if self.agree_stop:
                     if _agree(comm, self._stop.is_set()):
@@ -387,7 +403,15 @@ class EngineRunner:
                 # every rank takes the same branches: metrics() / episode_sums() are collectives
                 log_now = bool(log_every) and k % log_every == 0
                 m = algo.epoch_metrics() if log_now else {}
-                if check is not None:
+                if check is not None and lag:
+                    nxt = algo.episode_sums_async()
+                    if pending is not None:
+                        win = check.update(*pending.result())
+                        if check.solved(win):
+                            solved = True
+                            ttt = time.perf_counter() - self.t_start
+                    pending = nxt
+                elif check is not None:
                     win = check.update(*algo.episode_sums(m if log_now else None))
                     if check.solved(win):
                         solved = True
@@ -411,6 +435,11 @@ class EngineRunner:
                     break
                 if max_seconds is not None and _agree(comm, time.perf_counter() - t0 >= max_seconds):
                     break
+            if pending is not None and not solved:  # the last epoch's sums, still unread
+                win = check.update(*pending.result())
+                if check.solved(win):
+                    solved = True
+                    ttt = time.perf_counter() - self.t_start
             if not publish_every or (algo.epoch - e0) % publish_every:
                 self._publish()
             el = time.perf_counter() - t0

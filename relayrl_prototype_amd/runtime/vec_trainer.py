@@ -64,6 +64,21 @@ class SolvedCheck:
         return mean == mean and mean >= self.threshold
 
 
+class PendingSums:
+    """(episodes, return sum) of one epoch, read when needed: a pinned host slot + the event
+    recorded after the copy into it, or an already-known pair."""
+
+    def __init__(self, slot, event=None):
+        self.slot, self.event = slot, event
+
+    def result(self) -> tuple:
+        if self.event is None:
+            return tuple(self.slot)
+        self.event.synchronize()
+        n, s = self.slot.tolist()
+        return n, s
+
+
 @dataclass
 class VecTrainerConfig:
     env: str = "CartPole-v1"
@@ -196,6 +211,26 @@ class VecTrainer:
             self.comm.all_reduce_sum_(ns)
         n, s = ns.tolist()
         return n, s
+
+    def episode_sums_async(self) -> "PendingSums":
+        """episode_sums() without the synchronising read: the two sums are copied into a pinned
+        host slot behind the epoch on the stream, and the returned handle's ``result()`` waits
+        for that copy only.  The threshold loop (EngineRunner.train) consumes epoch k's handle
+        after it has queued epoch k + 1, so the GPU never drains for the check."""
+        if self.comm.multi and self.comm.backend != "nccl":
+            return PendingSums(self.episode_sums())  # host collective: synchronous anyway
+        ns = self.ep_stats[:, :2].sum(0).double()
+        if self.comm.multi:
+            self.comm.all_reduce_sum_(ns)
+        if not hasattr(self, "_sum_slots"):
+            self._sum_slots = [torch.empty(2, dtype=torch.float64, pin_memory=True) for _ in range(3)]
+            self._sum_k = 0
+        slot = self._sum_slots[self._sum_k % 3]  # a handle is consumed before the slot comes round
+        self._sum_k += 1
+        slot.copy_(ns, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return PendingSums(slot, ev)
 
     def average_ep_return(self) -> float:
         """The value metrics()["AverageEpRet"] would return, from one read."""
