@@ -65,22 +65,48 @@ constexpr int kFrameRows = 441;               // 21 x 21 s2d pixels
 // conv1 fragment reads of 16 consecutive output pixels then hit disjoint banks, 1.6 -> 1.0
 // LDS cycles per conflict-free cycle (tools/lds_bank_model.py --fwd)
 constexpr int kFrameW = 28;
-constexpr int kXiRows = 20 * kFrameW + 24;      // last position read: (20, 20)
-constexpr int kA1Ld = 40;                     // a1 row: 32 co + 8 pad
-constexpr int kA2Ld = 80;                     // a2 / a3 rows: 64 co + 16 pad (72 measured 2.5x conflict cycles on the conv3 reads, 80 1.75x)
+constexpr int kXiRows = 20 * kFrameW + 21;      // last position read: (20, 20)
+// a1 as four stride-2 phase images, (y, x) at row 100 * (2 (y & 1) + (x & 1)) + 10 (y >> 1) +
+// (x >> 1), rows of 48 elements: conv2 computes a 9 x 10 output grid (column 9 discarded), so
+// the 16 pixels of a fragment read 16 consecutive rows, and a 96-byte row stride puts 16
+// consecutive rows of either lane-group half on disjoint banks: 2.0 -> 1.0 LDS cycles per
+// conflict-free cycle (tools/lds_bank_model.py --fwd; 40-element rows stay at 2.0 whatever
+// the row order)
+constexpr int kA1Ld = 48;
+constexpr int kA2Ld = 80;                     // a2 rows: 64 co + 16 pad; conv3 computes a 7 x 9 grid
+                                              // (columns 7, 8 discarded): consecutive rows, 1.75 -> 1.0
+constexpr int kA3Ld = 64;                     // a3 rows: only copied out, never an MFMA operand
 constexpr int kXi = 0;                                    // element offsets into LDS
-constexpr int kA1 = kXi + kXiRows * kFrameLd;             // 46,720
-constexpr int kA2 = kA1 + 400 * kA1Ld;                    // 62,720 (two buffers of 81 rows)
-constexpr int kA3 = kA2 + 2 * 81 * kA2Ld;                 // 75,680
-constexpr int kLds = (kA3 + 49 * kA2Ld) * 2;              // 159,200 bytes
+constexpr int kA1 = kXi + kXiRows * kFrameLd;             // 46,480
+constexpr int kA2 = kA1 + 400 * kA1Ld;                    // 65,680 (two buffers of 81 rows)
+constexpr int kA3 = kA2 + 2 * 81 * kA2Ld;                 // 78,640
+constexpr int kLds = (kA3 + 49 * kA3Ld) * 2;              // 163,552 bytes
+// discarded grid positions read past their image: conv2 up to phase row 406 (inside the a2
+// buffers), conv3 up to buffer row 83 (inside a3) -- garbage in discarded output rows only
+static_assert(kA1 + 407 * kA1Ld <= kA3 && kA2 + (81 + 84) * kA2Ld <= kA3 + 49 * kA3Ld, "over-reads stay in LDS");
+static_assert(kLds <= 160 * 1024, "LDS per workgroup");
+__device__ __forceinline__ int a1_row(int p) {  // a1 pixel p = 20 y + x -> phase-image row
+  const int y = p / 20, x = p - 20 * (p / 20);
+  return 100 * (2 * (y & 1) + (x & 1)) + 10 * (y >> 1) + (x >> 1);
+}
+// layout of a PROBE variant: bit 4 = a1 as phase images in 48-element rows and conv2 over a
+// 9 x 10 grid (a3 rows of 64 to fit), bit 5 = conv3 over a 7 x 9 grid; neither = a1 as one
+// 20 x 20 image in 40-element rows, conv2 / conv3 over their 81 / 49 output pixels
+template <int PROBE>
+struct FwdLayout {
+  static constexpr bool kPhaseA1 = (PROBE & 16) != 0, kGrid3 = (PROBE & 32) != 0;
+  static constexpr int kA1Ld = kPhaseA1 ? 48 : 40, kA3Ld = kPhaseA1 ? 64 : 80;
+  static constexpr int kA1 = cs::kA1, kA2 = kA1 + 400 * kA1Ld, kA3 = kA2 + 2 * 81 * cs::kA2Ld;
+  static_assert((kA3 + 49 * kA3Ld) * 2 <= cs::kLds, "variant fits the launch's LDS");
+};
 constexpr int kXChunks = kFrameRows * 64 / 16;           // 16-byte chunks of one uint8 frame (1,764)
 constexpr int kXPerT = (kXChunks + kThreads - 1) / kThreads;
 static_assert(kA1 % 8 == 0 && kA2 % 8 == 0 && kA3 % 8 == 0, "16-byte aligned LDS regions");
 }  // namespace cs
 
-// PROBE (tools/cnn_kbench.py --probe, timing only -- outputs are garbage when != 0):
+// PROBE (tools/cnn_kbench.py --probe, timing only -- outputs are garbage when bits 0-2 are set):
 // bit 0 skips the MFMAs, bit 1 the global stores, bit 2 re-reads frame 0 (L2-hot), bit 3
-// runs conv1 with one co tile per wave
+// runs conv1 with one co tile per wave, bits 4-6 select earlier LDS layouts (FwdLayout)
 template <int PROBE>
 __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
     const uint8_t* __restrict__ x, const uint16_t* __restrict__ w1, const float* __restrict__ b1,
@@ -88,10 +114,13 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
     const float* __restrict__ b3, uint16_t* __restrict__ y1, uint16_t* __restrict__ y2,
     uint16_t* __restrict__ y3, int N) {
   using namespace cs;
+  using L = FwdLayout<PROBE>;
+  constexpr int kA1Ld = L::kA1Ld, kA3Ld = L::kA3Ld, kA1 = L::kA1, kA2 = L::kA2, kA3 = L::kA3;
+  auto a1r = [](int p) { return L::kPhaseA1 ? a1_row(p) : p; };
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Xi = smem + kXi;  // [21 x 28][80] frame as bf16 integers 0..255
-  uint16_t* A1 = smem + kA1;  // [400][40] conv1 output
-  uint16_t* A3 = smem + kA3;  // [49][72]  conv3 output
+  uint16_t* A1 = smem + kA1;  // 4 x [100][48] conv1 output, phase images (a1_row)
+  uint16_t* A3 = smem + kA3;  // [49][64]  conv3 output
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
   const bool role_a = wave < 4;
@@ -163,7 +192,7 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
     }
     if (j >= 2 && !(PROBE & 2)) {
       uint4* yd = reinterpret_cast<uint4*>(y3 + (size_t)(n - 2 * G) * 49 * 64);
-      for (int q = tid; q < 49 * 8; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A3 + (q >> 3) * kA2Ld + (q & 7) * 8);
+      for (int q = tid; q < 49 * 8; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A3 + (q >> 3) * kA3Ld + (q & 7) * 8);
     }
     // ---- conv1, C1BOTH: pixel tiles wave + 8 t (t < 3, and t = 3 on wave 0), both co tiles
     if (cur && C1BOTH) {
@@ -195,7 +224,7 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
 #pragma unroll
       for (int t = 0; t < MT; ++t)
         if (t < nt) {
-          uint16_t* dst = A1 + (16 * (wave + 8 * t) + i) * kA1Ld + 4 * g;
+          uint16_t* dst = A1 + a1r(16 * (wave + 8 * t) + i) * kA1Ld + 4 * g;
           store4_bf16(dst, fmaxf(kU8Scale * acc0[t][0] + bias1[0], 0.f), fmaxf(kU8Scale * acc0[t][1] + bias1[1], 0.f),
                       fmaxf(kU8Scale * acc0[t][2] + bias1[2], 0.f), fmaxf(kU8Scale * acc0[t][3] + bias1[3], 0.f));
           store4_bf16(dst + 16, fmaxf(kU8Scale * acc1[t][0] + bias1b[0], 0.f),
@@ -234,14 +263,14 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = fmaxf(kU8Scale * acc[t][r] + bias1[r], 0.f);
-          store4_bf16(A1 + (16 * mt + i) * kA1Ld + 16 * c1 + 4 * g, v[0], v[1], v[2], v[3]);
+          store4_bf16(A1 + a1r(16 * mt + i) * kA1Ld + 16 * c1 + 4 * g, v[0], v[1], v[2], v[3]);
         }
       }
     }
     __syncthreads();  // B2: a1(n) complete
     if (cur && y1 && !(PROBE & 2)) {
       uint4* yd = reinterpret_cast<uint4*>(y1 + (size_t)n * 400 * 32);
-      for (int q = tid; q < 400 * 4; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A1 + (q >> 2) * kA1Ld + (q & 3) * 8);
+      for (int q = tid; q < 400 * 4; q += kThreads) yd[q] = *reinterpret_cast<const uint4*>(A1 + a1r(q >> 2) * kA1Ld + (q & 3) * 8);
     }
     if (role_a) {
       // ---- conv2(n): co tile ct, all 6 pixel tiles (81 px; rows past the image are discarded)
@@ -253,14 +282,17 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
           acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-          const int p = 16 * t + i;
-          const int pc = p < 81 ? p : 0;
-          const int oh = pc / 9, ow = pc - oh * 9;
-          r0[t] = 2 * oh * 20 + 2 * ow;
+          if (L::kPhaseA1) {
+            r0[t] = 16 * t + i;  // grid position p = 10 oh + ow: phase row 10 oh + ow of tap (0, 0)
+          } else {
+            const int p = 16 * t + i, pc = p < 81 ? p : 0, oh = pc / 9, ow = pc - oh * 9;
+            r0[t] = 2 * oh * 20 + 2 * ow;
+          }
         }
 #pragma unroll
         for (int ks = 0; ks < 16; ++ks) {
-          const int off = ((ks >> 2) * 20 + (ks & 3)) * kA1Ld + 8 * g;
+          const int kh = ks >> 2, kw = ks & 3;
+          const int off = (L::kPhaseA1 ? 100 * (2 * (kh & 1) + (kw & 1)) + 10 * (kh >> 1) + (kw >> 1) : kh * 20 + kw) * kA1Ld + 8 * g;
           bf16x8_t a[MT];
 #pragma unroll
           for (int t = 0; t < MT; ++t) a[t] = *reinterpret_cast<const bf16x8_t*>(A1 + r0[t] * kA1Ld + off);
@@ -270,9 +302,9 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
         }
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
-          const int p = 16 * t + i;
-          if (p < 81)
-            store4_bf16(A2c + p * kA2Ld + 16 * ct + 4 * g, fmaxf(acc[t][0] + bias23[0], 0.f),
+          const int p = 16 * t + i, oh = p / 10, ow = p - 10 * (p / 10);
+          if (L::kPhaseA1 ? (p < 90 && ow < 9) : p < 81)
+            store4_bf16(A2c + (L::kPhaseA1 ? 9 * oh + ow : p) * kA2Ld + 16 * ct + 4 * g, fmaxf(acc[t][0] + bias23[0], 0.f),
                         fmaxf(acc[t][1] + bias23[1], 0.f), fmaxf(acc[t][2] + bias23[2], 0.f),
                         fmaxf(acc[t][3] + bias23[3], 0.f));
         }
@@ -286,10 +318,12 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
         acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        const int p = 16 * t + i;
-        const int pc = p < 49 ? p : 0;
-        const int oh = pc / 7, ow = pc - oh * 7;
-        r0[t] = oh * 9 + ow;
+        if (L::kGrid3) {
+          r0[t] = 16 * t + i;  // grid position p = 9 oh + ow = the a2 row of tap (0, 0)
+        } else {
+          const int p = 16 * t + i, pc = p < 49 ? p : 0, oh = pc / 7, ow = pc - oh * 7;
+          r0[t] = oh * 9 + ow;
+        }
       }
 #pragma unroll
       for (int ks = 0; ks < 18; ++ks) {
@@ -304,9 +338,9 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
       }
 #pragma unroll
       for (int t = 0; t < MT; ++t) {
-        const int p = 16 * t + i;
-        if (p < 49)
-          store4_bf16(A3 + p * kA2Ld + 16 * ct + 4 * g, fmaxf(acc[t][0] + bias23[0], 0.f),
+        const int p = 16 * t + i, oh = p / 9, ow = p - 9 * (p / 9);
+        if (L::kGrid3 ? (oh < 7 && ow < 7) : p < 49)
+          store4_bf16(A3 + (L::kGrid3 ? 7 * oh + ow : p) * kA3Ld + 16 * ct + 4 * g, fmaxf(acc[t][0] + bias23[0], 0.f),
                       fmaxf(acc[t][1] + bias23[1], 0.f), fmaxf(acc[t][2] + bias23[2], 0.f),
                       fmaxf(acc[t][3] + bias23[3], 0.f));
       }
@@ -349,6 +383,9 @@ extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const fl
     case 4: return launch_conv_stack_fwd<4>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 7: return launch_conv_stack_fwd<7>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 8: return launch_conv_stack_fwd<8>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 16: return launch_conv_stack_fwd<16>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 32: return launch_conv_stack_fwd<32>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 48: return launch_conv_stack_fwd<48>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     default: return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
   }
 }
@@ -583,7 +620,7 @@ extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16
 //   a1   split into its four stride-2 phase images (ph, pw) = (ih & 1, iw & 1), each 10 x 10
 //        positions (row (ih >> 1) * 10 + (iw >> 1), rows 100..115 zero; 32 c + 8 pad)
 //   dgrad  da1[ph + 2a][pw + 2b][c] = sum_(i, j, co) da2[a - i][b - j][co] W2[co][ph + 2i][pw + 2j][c]
-//          per phase class a 100 px x 32 c GEMM over K = (4 taps x 64 co); wave w: class w >> 1,
+//          per phase class a 100 px (10 x 12 grid) x 32 c GEMM over K = (4 taps x 64 co); wave w: class w >> 1,
 //          c tile w & 1, W2 fragments in registers.  The weights are the MFMA's A operand, so a
 //          lane ends with 4 consecutive channels of one pixel: masked by a1 (from the phase
 //          image) and stored straight to HBM as 8 bytes.
@@ -732,18 +769,19 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
 #pragma unroll
         for (int t = 0; t < 4; ++t) wacc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[c], bfr[t], wacc[c][t], 0, 0, 0);
     }
-    // ---- dgrad of phase class (ph, pw), c tile ct: 7 pixel tiles in two batches
+    // ---- dgrad of phase class (ph, pw), c tile ct: the class's 10 x 10 pixels as a 10 x 12
+    // grid (p = 12 a + b, columns 10, 11 and rows past 9 computed and discarded), 8 pixel tiles
+    // in two batches: the 16 pixels of a fragment then read 16 consecutive da2 rows, which
+    // 80-element rows put on disjoint banks -- 1.86 -> 1.0 LDS cycles per conflict-free cycle
+    // for 8 instead of 7 tiles (tools/lds_bank_model.py --conv2)
     auto class_tiles = [&](auto tag) {
-      constexpr int T0 = decltype(tag)::value, NT = T0 == 0 ? 4 : 3;
+      constexpr int T0 = decltype(tag)::value, NT = 4;
       f32x4_t acc[NT];
       int rb[NT];
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
         acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        const int p = 16 * (T0 + u) + i16;
-        const int pc = p < 100 ? p : 0;  // rows past the class are computed and discarded
-        const int a = pc / 10, b = pc - a * 10;
-        rb[u] = (a + 1) * 12 + (b + 1);
+        rb[u] = 16 * (T0 + u) + i16 + 13;  // (a + 1) * 12 + (b + 1); at most row 140 of 144
       }
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
@@ -758,9 +796,8 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
       // D = da1^T: lane (i16, g) holds channels 16 ct + 4g .. + 3 of class pixel p
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
-        const int p = 16 * (T0 + u) + i16;
-        if (p < 100) {
-          const int a = p / 10, b = p - a * 10;
+        const int p = 16 * (T0 + u) + i16, a = p / 12, b = p - 12 * (p / 12);
+        if (a < 10 && b < 10) {
           const uint2 m = *reinterpret_cast<const uint2*>(P + (cls * kPRows + a * 10 + b) * kPLd + 16 * ct + 4 * g);
           const uint2 v = make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x),
                                      relu_mask2(pk_bf16(acc[u][2], acc[u][3]), m.y));

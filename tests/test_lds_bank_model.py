@@ -32,3 +32,18 @@ def test_shipped_layout_factors():
     # fused forward: frame rows of 28 positions make conv1's reads conflict-free
     assert m.conv_stack_fwd_conv1(80, 21) == 1.6
     assert m.conv_stack_fwd_conv1(80, 28) == 1.0
+
+
+def test_forward_a1_a2_layout_factors():
+    # conv2 of the fused forward: stride-2 reads of 40-element rows 2.0; a 9 x 10 grid over
+    # phase images of 48-element rows 1.0 (40-element rows stay at 2.0)
+    assert m.conv_stack_fwd_conv2(40, False) == 2.0
+    assert m.conv_stack_fwd_conv2(40, True) == 2.0 and m.conv_stack_fwd_conv2(48, True) == 1.0
+    # conv3: 49 pixels 1.75, a 7 x 9 grid (consecutive rows) 1.0
+    assert m.conv_stack_fwd_conv3(80, False) == 1.75 and m.conv_stack_fwd_conv3(80, True) == 1.0
+
+
+def test_conv2_backward_dgrad_grid():
+    none = lambda y, x: 0  # noqa: E731
+    # the 10 x 12 dgrad grid reads consecutive da2 rows: 1.86 -> 1.0 for 8 instead of 7 tiles
+    assert m.conv2_bwd_da2(m.swz(lambda y, x: y * 12 + x, 80, none), grid12=True)[0] == 1.0

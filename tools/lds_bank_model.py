@@ -12,7 +12,7 @@ are LDS cycles per conflict-free cycle (1.0 = conflict-free).
     python tools/lds_bank_model.py            # conv3 backward: old vs shipped layouts
     python tools/lds_bank_model.py --search   # the conv3 layout / swizzle search behind them
     python tools/lds_bank_model.py --conv2    # the conv2 backward images
-    python tools/lds_bank_model.py --fwd      # the fused forward's frame image (conv1 reads)
+    python tools/lds_bank_model.py --fwd      # the fused forward's frame / a1 / a2 images
 
 A model, not a clock: the swizzled layouts it prefers need per-read XOR address arithmetic,
 which in these two-waves-per-SIMD kernels cost more than the conflicts they removed
@@ -116,6 +116,11 @@ def main():
     if "--fwd" in sys.argv:
         print("conv_stack_fwd conv1 frame reads (ld, row width -> factor):",
               {(ld, W): conv_stack_fwd_conv1(ld, W) for ld in (72, 80, 88) for W in (21, 24, 28, 32)})
+        print("conv_stack_fwd conv2 a1 reads (ld -> factor): stride-2 rows of 20",
+              {ld: conv_stack_fwd_conv2(ld, False) for ld in (40, 48, 56)}, " 9 x 10 grid on phase images",
+              {ld: conv_stack_fwd_conv2(ld, True) for ld in (40, 48, 56)})
+        print("conv_stack_fwd conv3 a2 reads (ld -> factor): 49 pixels", {ld: conv_stack_fwd_conv3(ld, False) for ld in (72, 80)},
+              " 7 x 9 grid", {ld: conv_stack_fwd_conv3(ld, True) for ld in (72, 80)})
     if "--search" in sys.argv:
         res = []
         for ld in (64, 72, 80, 88):
@@ -141,12 +146,14 @@ def main():
             print("  ", r)
 
 
-def conv2_bwd_da2(el):
+def conv2_bwd_da2(el, grid12=False):
     """(dgrad b128, wgrad transposed, LDS cycles per wave-image) of the da2 image; el(y, x, col)
-    addresses bordered position (y, x) = (oh + 1, ow + 1)"""
+    addresses bordered position (y, x) = (oh + 1, ow + 1).  grid12: each phase class's 10 x 10
+    dgrad pixels computed as a 10 x 12 grid, 8 tiles (the shipped form) instead of 7"""
     rd, rw = [], []
+    W = 12 if grid12 else 10
     for cls in range(4):
-        for T0, NT in ((0, 4), (4, 3)):
+        for T0, NT in ((0, 4), (4, 4 if grid12 else 3)):
             for u in range(NT):
                 for ks in range(8):
                     t = ks >> 1
@@ -154,8 +161,8 @@ def conv2_bwd_da2(el):
                     addr = []
                     for i16, g, q4, p4 in lanes():
                         p = 16 * (T0 + u) + i16
-                        pc = p if p < 100 else 0
-                        addr.append(2 * el(pc // 10 + 1 - ti, pc % 10 + 1 - tj, (ks & 1) * 32 + 8 * g))
+                        pc = p if (p < 100 or grid12) else 0
+                        addr.append(2 * el(pc // W + 1 - ti, pc % W + 1 - tj, (ks & 1) * 32 + 8 * g))
                     rd.append(b128(addr))
 
     def run(s, g, h):
@@ -170,8 +177,8 @@ def conv2_bwd_da2(el):
                     addr.append(2 * el(oh + 1, ow0 + 1 + q4, 16 * c + 4 * p4))
                 rw.append(tr16(addr))
     d, w = sum(rd) / len(rd), sum(rw) / len(rw)
-    # per wave-image: dgrad 7 tiles x 8 k-steps b128 (4 cycles), wgrad 4 x 4 x 2 transposed (2 cycles)
-    return round(d, 2), round(w, 2), 56 * 4 * d + 32 * 2 * w
+    # per wave-image: dgrad 7 (8) tiles x 8 k-steps b128 (4 cycles), wgrad 4 x 4 x 2 transposed (2 cycles)
+    return round(d, 2), round(w, 2), (64 if grid12 else 56) * 4 * d + 32 * 2 * w
 
 
 def conv2_bwd_a1(el):
@@ -199,8 +206,10 @@ def conv2_bwd_a1(el):
 
 def search_conv2():
     none = lambda y, x: 0  # noqa: E731
-    print("conv2_bwd da2 image (dgrad b128, wgrad tr, cycles): current 12-wide/72 ->",
-          conv2_bwd_da2(swz(lambda y, x: y * 12 + x, 72, none)))
+    print("conv2_bwd da2 image (dgrad b128, wgrad tr, cycles): 12-wide/72 ->",
+          conv2_bwd_da2(swz(lambda y, x: y * 12 + x, 72, none)), " 12-wide/80 ->",
+          conv2_bwd_da2(swz(lambda y, x: y * 12 + x, 80, none)), " 12-wide/80, 10 x 12 dgrad grid (shipped) ->",
+          conv2_bwd_da2(swz(lambda y, x: y * 12 + x, 80, none), grid12=True))
     res = []
     for ld in (64, 72, 80):
         for W in (12, 13, 14, 16):
@@ -243,6 +252,49 @@ def conv_stack_fwd_conv1(ld, W):
             for i16, g, q4, p4 in lanes():
                 p = 16 * t + i16
                 row = (p // 20 + (tap >> 1)) * W + p % 20 + (tap & 1)
+                addr.append(2 * (row * ld + 32 * (ks & 1) + 8 * g))
+            r.append(b128(addr))
+    return round(sum(r) / len(r), 2)
+
+
+def conv_stack_fwd_conv2(ld, grid10):
+    """b128 factor of the fused forward's conv2 reads of a1: grid10=False -- 81 output pixels
+    read from the 20 x 20 image in rows of 20 (stride-2 positions); True -- a 9 x 10 grid
+    (column 9 discarded) read from four stride-2 phase images of 100 rows (the shipped form)"""
+    r = []
+    for t in range(6):
+        for ks in range(16):
+            kh, kw = ks >> 2, ks & 3
+            addr = []
+            for i16, g, q4, p4 in lanes():
+                p = 16 * t + i16
+                if grid10:
+                    oh, ow = p // 10, p % 10
+                    row = ((kh & 1) * 2 + (kw & 1)) * 100 + (oh + (kh >> 1)) * 10 + ow + (kw >> 1)
+                else:
+                    pc = p if p < 81 else 0
+                    row = 2 * (pc // 9) * 20 + 2 * (pc % 9) + kh * 20 + kw
+                addr.append(2 * (row * ld + 8 * g))
+            r.append(b128(addr))
+    return round(sum(r) / len(r), 2)
+
+
+def conv_stack_fwd_conv3(ld, grid9):
+    """b128 factor of the fused forward's conv3 reads of a2 (9 x 9 image, rows of 9): grid9=False
+    -- 49 output pixels; True -- a 7 x 9 grid (columns 7, 8 discarded, the shipped form)"""
+    r = []
+    for t in range(4):
+        for ks in range(18):
+            tap = ks >> 1
+            kh, kw = tap // 3, tap % 3
+            addr = []
+            for i16, g, q4, p4 in lanes():
+                p = 16 * t + i16
+                if grid9:
+                    row = p + kh * 9 + kw
+                else:
+                    pc = p if p < 49 else 0
+                    row = (pc // 7) * 9 + pc % 7 + kh * 9 + kw
                 addr.append(2 * (row * ld + 32 * (ks & 1) + 8 * g))
             r.append(b128(addr))
     return round(sum(r) / len(r), 2)
