@@ -747,3 +747,34 @@ def test_pixel_alternating_obs_buffers_match_copy_path(cuda, monkeypatch):
     assert torch.equal(a.obs[0], b.obs[0]) and torch.equal(a.act, b.act)  # the next update's start
     torch.testing.assert_close(a.model.params, b.model.params, rtol=0, atol=0)
     assert a.metrics()["EnvSteps"] == b.metrics()["EnvSteps"]
+
+
+@pytest.mark.parametrize("probe", [16, 32, 48])
+def test_fused_conv_stack_layout_variants_are_bitwise_equal(cuda, probe):
+    """The forward's LDS layout variants (FwdLayout probe bits: a1 as stride-2 phase images with
+    conv2 over a 9 x 10 grid, conv3 over a 7 x 9 grid) run the same MFMA k-order per output:
+    a1 / a2 / a3 bitwise equal to the default layout's, discarded grid positions never stored."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    spec = CNNSpec()
+    o = spec.offsets()
+    N = 700
+    g = torch.Generator().manual_seed(probe)
+    params = spec.init(probe).to(cuda)
+    params += 0.01 * torch.randn(params.shape, generator=g).to(cuda)
+    sh = params.bfloat16()
+    x = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g).to(cuda)
+    outs = []
+    for pr in (0, probe):
+        a1 = torch.full((N * 400 * 32,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        a2 = torch.full((N * 81 * 64,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        a3 = torch.full((N * FC_IN,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        h.conv_stack_fwd(x, sh[o["w1"]:o["b1"]], params[o["b1"]:o["b1"] + 32], sh[o["w2"]:o["b2"]],
+                         params[o["b2"]:o["b2"] + 64], sh[o["w3"]:o["b3"]], params[o["b3"]:o["b3"] + 64], a1, a2, a3,
+                         N, probe=pr)
+        torch.cuda.synchronize()
+        outs.append((a1, a2, a3))
+    for f, r in zip(*outs):
+        assert torch.isfinite(f.float()).all()
+        assert torch.equal(f, r)
