@@ -66,42 +66,40 @@ constexpr int kFrameRows = 441;               // 21 x 21 s2d pixels
 // LDS cycles per conflict-free cycle (tools/lds_bank_model.py --fwd)
 constexpr int kFrameW = 28;
 constexpr int kXiRows = 20 * kFrameW + 21;      // last position read: (20, 20)
-// a1 as four stride-2 phase images, (y, x) at row 100 * (2 (y & 1) + (x & 1)) + 10 (y >> 1) +
-// (x >> 1), rows of 48 elements: conv2 computes a 9 x 10 output grid (column 9 discarded), so
-// the 16 pixels of a fragment read 16 consecutive rows, and a 96-byte row stride puts 16
-// consecutive rows of either lane-group half on disjoint banks: 2.0 -> 1.0 LDS cycles per
-// conflict-free cycle (tools/lds_bank_model.py --fwd; 40-element rows stay at 2.0 whatever
-// the row order)
-constexpr int kA1Ld = 48;
-constexpr int kA2Ld = 80;                     // a2 rows: 64 co + 16 pad; conv3 computes a 7 x 9 grid
-                                              // (columns 7, 8 discarded): consecutive rows, 1.75 -> 1.0
-constexpr int kA3Ld = 64;                     // a3 rows: only copied out, never an MFMA operand
+constexpr int kA2Ld = 80;  // a2 / a3 rows: 64 co + 16 pad (72 measured 2.5x conflict cycles on the conv3 reads, 80 1.75x)
+// Measured and not shipped (FwdLayout PROBE bits, profiles/r4_fwd_layouts.txt):
+//  bit 4: a1 as four stride-2 phase images, (y, x) at row 100 (2 (y & 1) + (x & 1)) +
+//   10 (y >> 1) + (x >> 1), rows of 48 elements, conv2 over a 9 x 10 grid -- its fragment reads
+//   model conflict-free (2.0 -> 1.0; 40-element rows stay at 2.0 in any row order) and PMC
+//   counted -37 % bank-conflict cycles, but the kernel ran 58.9 -> 67.2 us: SQ_WAIT_ANY +80 %;
+//  bit 5: conv3 over a 7 x 9 grid (consecutive a2 rows, 1.75 -> 1.0 modelled): -2 % Pong
+//   env-steps/s at 8,192 envs alternated in the same process.
 constexpr int kXi = 0;                                    // element offsets into LDS
 constexpr int kA1 = kXi + kXiRows * kFrameLd;             // 46,480
-constexpr int kA2 = kA1 + 400 * kA1Ld;                    // 65,680 (two buffers of 81 rows)
-constexpr int kA3 = kA2 + 2 * 81 * kA2Ld;                 // 78,640
-constexpr int kLds = (kA3 + 49 * kA3Ld) * 2;              // 163,552 bytes
-// discarded grid positions read past their image: conv2 up to phase row 406 (inside the a2
-// buffers), conv3 up to buffer row 83 (inside a3) -- garbage in discarded output rows only
-static_assert(kA1 + 407 * kA1Ld <= kA3 && kA2 + (81 + 84) * kA2Ld <= kA3 + 49 * kA3Ld, "over-reads stay in LDS");
+constexpr int kLds = (kA1 + 400 * 48 + 2 * 81 * kA2Ld + 49 * 64) * 2;  // 163,552 bytes: the largest variant
 static_assert(kLds <= 160 * 1024, "LDS per workgroup");
 __device__ __forceinline__ int a1_row(int p) {  // a1 pixel p = 20 y + x -> phase-image row
   const int y = p / 20, x = p - 20 * (p / 20);
   return 100 * (2 * (y & 1) + (x & 1)) + 10 * (y >> 1) + (x >> 1);
 }
 // layout of a PROBE variant: bit 4 = a1 as phase images in 48-element rows and conv2 over a
-// 9 x 10 grid (a3 rows of 64 to fit), bit 5 = conv3 over a 7 x 9 grid; neither = a1 as one
-// 20 x 20 image in 40-element rows, conv2 / conv3 over their 81 / 49 output pixels
+// 9 x 10 grid (a3 rows of 64 to fit), bit 5 = conv3 over a 7 x 9 grid; default = a1 as one
+// 20 x 20 image in 40-element rows (conv2 over its 81 output pixels), conv3 over its 49 output
+// pixels, a3 rows of 80
 template <int PROBE>
 struct FwdLayout {
   static constexpr bool kPhaseA1 = (PROBE & 16) != 0, kGrid3 = (PROBE & 32) != 0;
   static constexpr int kA1Ld = kPhaseA1 ? 48 : 40, kA3Ld = kPhaseA1 ? 64 : 80;
   static constexpr int kA1 = cs::kA1, kA2 = kA1 + 400 * kA1Ld, kA3 = kA2 + 2 * 81 * cs::kA2Ld;
-  static_assert((kA3 + 49 * kA3Ld) * 2 <= cs::kLds, "variant fits the launch's LDS");
+  static_assert((kA3 + 49 * kA3Ld) * 2 <= cs::kLds, "variant fits in LDS");
+  // discarded grid positions read past their image -- conv2 up to phase row 406, conv3 up to
+  // buffer row 83 -- garbage in discarded output rows only, always inside the allocation
+  static_assert(!kPhaseA1 || kA1 + 407 * kA1Ld <= kA3, "conv2 over-read stays below a3");
+  static_assert(!kGrid3 || kA2 + (81 + 84) * cs::kA2Ld <= cs::kLds / 2, "conv3 over-read stays in LDS");
+  static_assert(kA1 % 8 == 0 && kA2 % 8 == 0 && kA3 % 8 == 0, "16-byte aligned LDS regions");
 };
 constexpr int kXChunks = kFrameRows * 64 / 16;           // 16-byte chunks of one uint8 frame (1,764)
 constexpr int kXPerT = (kXChunks + kThreads - 1) / kThreads;
-static_assert(kA1 % 8 == 0 && kA2 % 8 == 0 && kA3 % 8 == 0, "16-byte aligned LDS regions");
 }  // namespace cs
 
 // PROBE (tools/cnn_kbench.py --probe, timing only -- outputs are garbage when bits 0-2 are set):
@@ -356,15 +354,17 @@ template <int PROBE>
 static int launch_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
                                  const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
                                  uint16_t* y3, int N, int max_grid, hipStream_t stream) {
+  using L = FwdLayout<PROBE>;
+  constexpr int lds = (L::kA3 + 49 * L::kA3Ld) * 2;  // 158,720 bytes for the shipped layout
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)conv_stack_fwd_kernel<PROBE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              cs::kLds);
+                              lds);
     attr = true;
   }
   if (N < 1) return 0;
-  const int grid = N < max_grid ? N : max_grid;  // one 133 KB-LDS workgroup per CU
-  hipLaunchKernelGGL(conv_stack_fwd_kernel<PROBE>, dim3(grid), dim3(cs::kThreads), cs::kLds, stream, x, w1, b1, w2,
+  const int grid = N < max_grid ? N : max_grid;  // one 155 KB-LDS workgroup per CU
+  hipLaunchKernelGGL(conv_stack_fwd_kernel<PROBE>, dim3(grid), dim3(cs::kThreads), lds, stream, x, w1, b1, w2,
                      b2, w3, b3, y1, y2, y3, N);
   return (int)hipGetLastError();
 }
@@ -649,8 +649,9 @@ __device__ __forceinline__ bf16x8_t tr_frag2(const uint16_t* a0, const uint16_t*
 }
 
 // STAGED: da1 goes through an LDS tile [400][40] and leaves as 16-byte row chunks after a
-// second barrier, instead of 8-byte stores straight from the MFMA registers
-template <bool STAGED>
+// second barrier, instead of 8-byte stores straight from the MFMA registers.  GRID12 = false:
+// the dgrad over each class's 100 pixels in 7 tiles (the A/B baseline of the 10 x 12 grid)
+template <bool STAGED, bool GRID12 = true>
 __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint16_t* __restrict__ dy,
                                                                      const uint16_t* __restrict__ w,
                                                                      const uint16_t* __restrict__ xact,
@@ -775,13 +776,19 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
     // 80-element rows put on disjoint banks -- 1.86 -> 1.0 LDS cycles per conflict-free cycle
     // for 8 instead of 7 tiles (tools/lds_bank_model.py --conv2)
     auto class_tiles = [&](auto tag) {
-      constexpr int T0 = decltype(tag)::value, NT = 4;
+      constexpr int T0 = decltype(tag)::value, NT = (GRID12 || T0 == 0) ? 4 : 3;
+      constexpr int W = GRID12 ? 12 : 10;  // grid width
       f32x4_t acc[NT];
       int rb[NT];
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
         acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        rb[u] = 16 * (T0 + u) + i16 + 13;  // (a + 1) * 12 + (b + 1); at most row 140 of 144
+        if (GRID12) {
+          rb[u] = 16 * (T0 + u) + i16 + 13;  // (a + 1) * 12 + (b + 1); at most row 140 of 144
+        } else {
+          const int p = 16 * (T0 + u) + i16, pc = p < 100 ? p : 0, a = pc / 10, b = pc - a * 10;
+          rb[u] = (a + 1) * 12 + (b + 1);
+        }
       }
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
@@ -796,7 +803,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
       // D = da1^T: lane (i16, g) holds channels 16 ct + 4g .. + 3 of class pixel p
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
-        const int p = 16 * (T0 + u) + i16, a = p / 12, b = p - 12 * (p / 12);
+        const int p = 16 * (T0 + u) + i16, a = p / W, b = p - W * (p / W);
         if (a < 10 && b < 10) {
           const uint2 m = *reinterpret_cast<const uint2*>(P + (cls * kPRows + a * 10 + b) * kPLd + 16 * ct + 4 * g);
           const uint2 v = make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x),
@@ -832,7 +839,8 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
   bias_part[(size_t)blockIdx.x * kThreads + tid] = bsum;
 }
 
-// staged != 0: da1 through the LDS staging tile (measured slower: 229 vs 214 us, tools/cnn_kbench.py bwd2 / bwd2_direct)
+// variant 1: da1 through the LDS staging tile (measured slower: 229 vs 214 us, tools/cnn_kbench.py
+// bwd2 / bwd2_direct); 2: the 7-tile dgrad (A/B baseline of the 10 x 12 grid)
 extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
                              float* bias_part, int N, int grid, int staged, void* stream) {
   static bool attr = false;
@@ -840,14 +848,19 @@ extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               c2b::kLds);
+    (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<false, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, c2b::kLds);
     (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               kStagedLds);
     attr = true;
   }
   if (N < 1 || grid < 1) return 0;
-  if (staged != 0)
+  if (staged == 1)
     hipLaunchKernelGGL(conv2_bwd_kernel<true>, dim3(grid), dim3(c2b::kThreads), kStagedLds, (hipStream_t)stream, dy, w,
                        xact, dx, part, bias_part, N);
+  else if (staged == 2)
+    hipLaunchKernelGGL((conv2_bwd_kernel<false, false>), dim3(grid), dim3(c2b::kThreads), c2b::kLds,
+                       (hipStream_t)stream, dy, w, xact, dx, part, bias_part, N);
   else
     hipLaunchKernelGGL(conv2_bwd_kernel<false>, dim3(grid), dim3(c2b::kThreads), c2b::kLds, (hipStream_t)stream, dy,
                        w, xact, dx, part, bias_part, N);

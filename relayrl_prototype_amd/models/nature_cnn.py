@@ -189,6 +189,13 @@ class DeviceNatureCNN:
         import os
 
         self.fused_convs = os.environ.get("RRL_CNN_FUSED", "1") != "0"
+        # LDS layout variant of the fused forward (cnn_fused.hip FwdLayout, for A/B runs):
+        # 0 = shipped, 16 = a1 as phase images, 32 = conv3 over a 7 x 9 grid, 48 = both
+        self.fwd_layout = int(os.environ.get("RRL_CNN_FWD_LAYOUT", "0"))
+        assert self.fwd_layout in (0, 16, 32, 48), "RRL_CNN_FWD_LAYOUT: 0, 16, 32 or 48"
+        # conv2 backward variant (A/B runs): 0 = dgrad over a 10 x 12 grid, 2 = over 7 tiles
+        self.bwd2_variant = int(os.environ.get("RRL_CNN_BWD2_VARIANT", "0"))
+        assert self.bwd2_variant in (0, 2), "RRL_CNN_BWD2_VARIANT: 0 or 2"
         # fc layer on the DMA-staged NT GEMM (fc.hip): forward as split-K partials reduced by
         # the head kernel (bias + ReLU + bf16 + logits / value / sample in one launch), data
         # gradient against a transposed bf16 shadow of Wfc (RRL_FC_NT=0: the gemm_bf16.h path)
@@ -338,7 +345,7 @@ class DeviceNatureCNN:
             # conv1 -> conv2 -> conv3 in one launch, activations LDS-resident (cnn_fused.hip)
             h.conv_stack_fwd(x, *(t for i in (1, 2, 3) for t in (sh[o[f"w{i}"]:o[f"b{i}"]],
                                                                      p[o[f"b{i}"]:o[f"b{i}"] + CONVS[i - 1].cout])),
-                             a1, a2, a3, n, store12=store_acts)
+                             a1, a2, a3, n, probe=self.fwd_layout, store12=store_acts)
         else:
             for i, (L, y) in enumerate(zip((S2D,) + CONVS[1:], (a1, a2, a3)), 1):
                 h.conv_fwd(x, sh[o[f"w{i}"]:o[f"b{i}"]], p[o[f"b{i}"]:o[f"b{i}"] + L.cout], y, n, L.hin, L.hin,
@@ -488,7 +495,8 @@ class DeviceNatureCNN:
         da1 = self.da1[:B * L1.hout ** 2 * L1.cout]
         if self.fused_convs:
             nblk = min(B, self.cus)
-            h.conv2_bwd(da2, sh[o["w2"]:o["b2"]], a1, da1, self.cpart["c2"], self.cbias["c2"], B, nblk)
+            h.conv2_bwd(da2, sh[o["w2"]:o["b2"]], a1, da1, self.cpart["c2"], self.cbias["c2"], B, nblk,
+                        staged=self.bwd2_variant)
             sums += [(self.cpart["c2"], nblk, L2.cout * L2.K, g[o["w2"]:o["b2"]]),
                      (self.cbias["c2"], nblk * 8, L2.cout, g[o["b2"]:o["b2"] + L2.cout])]
         else:

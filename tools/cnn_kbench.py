@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--which", default="fwd,fwd_layers,bwd3,bwd3_layers,bwd2,dgrad2,wgrad1,wgrad1_8")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=1, help="repeat the list, alternating its order; median per kernel")
     ap.add_argument("--frames", type=int, default=2048)
     ap.add_argument("--bwd-frames", type=int, default=10240)
     a = ap.parse_args()
@@ -72,7 +73,7 @@ def main():
     fns["wgrad1_8"] = lambda: h.conv1_wgrad8(x[:Nb], da1, part, bpart, Nb, min(Nb, cus))
     fns["wgrad1"] = lambda: h.conv_wgrad(da1, x[:Nb], part, 256, Nb, 21, 21, 64, 2, 2, 1, 32, bpart)
     fns.update({"p_nomfma": probe(1), "p_nostore": probe(2), "p_nostore_nomfma": probe(3), "p_hotframe": probe(4),
-           "p_all": probe(7), "fwd_c1split": probe(8), "fwd_g128": probe(0, 128), "fwd_l16": probe(16), "fwd_l32": probe(32), "fwd_l48": probe(48), "fwd_g512": probe(0, 512), "fwd": fwd, "fwd_layers": fwd_layers, "bwd3": bwd3, "bwd3_layers": bwd3_layers, "dgrad2": dgrad2})
+           "p_all": probe(7), "fwd_c1split": probe(8), "fwd_g128": probe(0, 128), "fwd_phase_a1": probe(16), "fwd_c3_grid": probe(32), "fwd_phase_a1_c3_grid": probe(48), "fwd_g512": probe(0, 512), "fwd": fwd, "fwd_layers": fwd_layers, "bwd3": bwd3, "bwd3_layers": bwd3_layers, "dgrad2": dgrad2})
     if hasattr(h, "conv2_bwd"):
         def bwd2():
             h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus))
@@ -81,20 +82,26 @@ def main():
             h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=1)
         fns["bwd2"] = bwd2
         fns["bwd2_staged"] = bwd2_staged
+        fns["bwd2_7tiles"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=2)
 
-    out = {}
-    for name in a.which.split(","):
-        f = fns[name]
-        for _ in range(3):
-            f()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(a.iters):
-            f()
-        e1.record()
-        torch.cuda.synchronize()
-        out[name] = round(e0.elapsed_time(e1) * 1e3 / a.iters, 1)
+    # --rounds R: the list R times, every other round in reverse order (the first kernel timed
+    # in a process reads slow), median per kernel
+    names = a.which.split(",")
+    times = {n: [] for n in names}
+    for r in range(a.rounds):
+        for name in (names if r % 2 == 0 else names[::-1]):
+            f = fns[name]
+            for _ in range(3):
+                f()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                f()
+            e1.record()
+            torch.cuda.synchronize()
+            times[name].append(e0.elapsed_time(e1) * 1e3 / a.iters)
+    out = {n: round(sorted(t)[len(t) // 2], 1) for n, t in times.items()}
     print(json.dumps({"bench": "cnn_kbench", "frames_fwd": Nf, "frames_bwd": Nb, "us_per_launch": out}), flush=True)
 
 
