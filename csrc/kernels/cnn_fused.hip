@@ -71,9 +71,9 @@ constexpr int kA2Ld = 80;  // a2 / a3 rows: 64 co + 16 pad (72 measured 2.5x con
 //  bit 4: a1 as four stride-2 phase images, (y, x) at row 100 (2 (y & 1) + (x & 1)) +
 //   10 (y >> 1) + (x >> 1), rows of 48 elements, conv2 over a 9 x 10 grid -- its fragment reads
 //   model conflict-free (2.0 -> 1.0; 40-element rows stay at 2.0 in any row order) and PMC
-//   counted -37 % bank-conflict cycles, but the kernel ran 58.9 -> 67.2 us: SQ_WAIT_ANY +80 %;
-//  bit 5: conv3 over a 7 x 9 grid (consecutive a2 rows, 1.75 -> 1.0 modelled): -2 % Pong
-//   env-steps/s at 8,192 envs alternated in the same process.
+//   counted -37 % bank-conflict cycles, but the kernel ran 58.9 -> 67.2 us (SQ_WAIT_ANY +80 %);
+//  bit 5: conv3 over a 7 x 9 grid (consecutive a2 rows, 1.75 -> 1.0 modelled): 54.8 -> 58.7 us
+//   per 2,048 frames, Pong -1 to -2 % in an ABBA run on one box.
 constexpr int kXi = 0;                                    // element offsets into LDS
 constexpr int kA1 = kXi + kXiRows * kFrameLd;             // 46,480
 constexpr int kLds = (kA1 + 400 * 48 + 2 * 81 * kA2Ld + 49 * 64) * 2;  // 163,552 bytes: the largest variant
@@ -354,7 +354,7 @@ template <int PROBE>
 static int launch_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
                                  const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
                                  uint16_t* y3, int N, int max_grid, hipStream_t stream) {
-  using L = FwdLayout<PROBE>;
+  using L = cs::FwdLayout<PROBE>;
   constexpr int lds = (L::kA3 + 49 * L::kA3Ld) * 2;  // 158,720 bytes for the shipped layout
   static bool attr = false;
   if (!attr) {
@@ -620,7 +620,7 @@ extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16
 //   a1   split into its four stride-2 phase images (ph, pw) = (ih & 1, iw & 1), each 10 x 10
 //        positions (row (ih >> 1) * 10 + (iw >> 1), rows 100..115 zero; 32 c + 8 pad)
 //   dgrad  da1[ph + 2a][pw + 2b][c] = sum_(i, j, co) da2[a - i][b - j][co] W2[co][ph + 2i][pw + 2j][c]
-//          per phase class a 100 px (10 x 12 grid) x 32 c GEMM over K = (4 taps x 64 co); wave w: class w >> 1,
+//          per phase class a 100 px x 32 c GEMM over K = (4 taps x 64 co); wave w: class w >> 1,
 //          c tile w & 1, W2 fragments in registers.  The weights are the MFMA's A operand, so a
 //          lane ends with 4 consecutive channels of one pixel: masked by a1 (from the phase
 //          image) and stored straight to HBM as 8 bytes.
@@ -649,9 +649,12 @@ __device__ __forceinline__ bf16x8_t tr_frag2(const uint16_t* a0, const uint16_t*
 }
 
 // STAGED: da1 goes through an LDS tile [400][40] and leaves as 16-byte row chunks after a
-// second barrier, instead of 8-byte stores straight from the MFMA registers.  GRID12 = false:
-// the dgrad over each class's 100 pixels in 7 tiles (the A/B baseline of the 10 x 12 grid)
-template <bool STAGED, bool GRID12 = true>
+// second barrier, instead of 8-byte stores straight from the MFMA registers.  GRID12: the dgrad
+// over a 10 x 12 grid per phase class (p = 12 a + b, columns 10, 11 and rows past 9 computed and
+// discarded), 8 tiles: the 16 pixels of a fragment read 16 consecutive da2 rows, 1.86 -> 1.0
+// modelled LDS factor (tools/lds_bank_model.py --conv2) -- measured 203.7 -> 205.8 us and Pong
+// -0.1 to -0.4 % in an ABBA run (profiles/r4_bwd2_grid_ab.txt): not shipped
+template <bool STAGED, bool GRID12 = false>
 __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint16_t* __restrict__ dy,
                                                                      const uint16_t* __restrict__ w,
                                                                      const uint16_t* __restrict__ xact,
@@ -770,11 +773,8 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
 #pragma unroll
         for (int t = 0; t < 4; ++t) wacc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[c], bfr[t], wacc[c][t], 0, 0, 0);
     }
-    // ---- dgrad of phase class (ph, pw), c tile ct: the class's 10 x 10 pixels as a 10 x 12
-    // grid (p = 12 a + b, columns 10, 11 and rows past 9 computed and discarded), 8 pixel tiles
-    // in two batches: the 16 pixels of a fragment then read 16 consecutive da2 rows, which
-    // 80-element rows put on disjoint banks -- 1.86 -> 1.0 LDS cycles per conflict-free cycle
-    // for 8 instead of 7 tiles (tools/lds_bank_model.py --conv2)
+    // ---- dgrad of phase class (ph, pw), c tile ct: 7 pixel tiles in two batches (rows past the
+    // class are computed and discarded; GRID12: 8 tiles of the 10 x 12 grid)
     auto class_tiles = [&](auto tag) {
       constexpr int T0 = decltype(tag)::value, NT = (GRID12 || T0 == 0) ? 4 : 3;
       constexpr int W = GRID12 ? 12 : 10;  // grid width
@@ -840,7 +840,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
 }
 
 // variant 1: da1 through the LDS staging tile (measured slower: 229 vs 214 us, tools/cnn_kbench.py
-// bwd2 / bwd2_direct); 2: the 7-tile dgrad (A/B baseline of the 10 x 12 grid)
+// bwd2 / bwd2_direct); 2: the dgrad over the 10 x 12 grid (measured no faster)
 extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
                              float* bias_part, int N, int grid, int staged, void* stream) {
   static bool attr = false;
@@ -848,7 +848,7 @@ extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               c2b::kLds);
-    (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<false, false>,
+    (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<false, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, c2b::kLds);
     (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               kStagedLds);
@@ -859,7 +859,7 @@ extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16
     hipLaunchKernelGGL(conv2_bwd_kernel<true>, dim3(grid), dim3(c2b::kThreads), kStagedLds, (hipStream_t)stream, dy, w,
                        xact, dx, part, bias_part, N);
   else if (staged == 2)
-    hipLaunchKernelGGL((conv2_bwd_kernel<false, false>), dim3(grid), dim3(c2b::kThreads), c2b::kLds,
+    hipLaunchKernelGGL((conv2_bwd_kernel<false, true>), dim3(grid), dim3(c2b::kThreads), c2b::kLds,
                        (hipStream_t)stream, dy, w, xact, dx, part, bias_part, N);
   else
     hipLaunchKernelGGL(conv2_bwd_kernel<false>, dim3(grid), dim3(c2b::kThreads), c2b::kLds, (hipStream_t)stream, dy,

@@ -193,7 +193,7 @@ class DeviceNatureCNN:
         # 0 = shipped, 16 = a1 as phase images, 32 = conv3 over a 7 x 9 grid, 48 = both
         self.fwd_layout = int(os.environ.get("RRL_CNN_FWD_LAYOUT", "0"))
         assert self.fwd_layout in (0, 16, 32, 48), "RRL_CNN_FWD_LAYOUT: 0, 16, 32 or 48"
-        # conv2 backward variant (A/B runs): 0 = dgrad over a 10 x 12 grid, 2 = over 7 tiles
+        # conv2 backward variant (A/B runs): 0 = dgrad over 7 tiles per class, 2 = a 10 x 12 grid
         self.bwd2_variant = int(os.environ.get("RRL_CNN_BWD2_VARIANT", "0"))
         assert self.bwd2_variant in (0, 2), "RRL_CNN_BWD2_VARIANT: 0 or 2"
         # fc layer on the DMA-staged NT GEMM (fc.hip): forward as split-K partials reduced by

@@ -495,8 +495,8 @@ def test_fused_conv_backward_matches_per_layer(cuda, B):
         assert relerr(gf[b0:b0 + L.cout], gr[b0:b0 + L.cout]) < 1e-4, f"b{i}"
 
 
-@pytest.mark.parametrize("li,N,grid,staged", [(1, 3, 3, 1), (1, 70, 16, 1), (1, 70, 16, 0), (2, 5, 5, 1),
-                                              (2, 300, 64, 1)])
+@pytest.mark.parametrize("li,N,grid,staged", [(1, 3, 3, 1), (1, 70, 16, 1), (1, 70, 16, 0), (1, 70, 16, 2),
+                                              (2, 5, 5, 1), (2, 300, 64, 1)])
 def test_fused_conv_bwd_kernels_match_autograd(cuda, li, N, grid, staged):
     """conv2_bwd / conv3_bwd (cnn_fused.hip) against fp32 autograd on the same bf16 operands:
     masked data gradient, weight-gradient partials (summed over workgroups), bias partials."""
@@ -778,3 +778,28 @@ def test_fused_conv_stack_layout_variants_are_bitwise_equal(cuda, probe):
     for f, r in zip(*outs):
         assert torch.isfinite(f.float()).all()
         assert torch.equal(f, r)
+
+
+def test_conv2_bwd_dgrad_grids_are_bitwise_equal(cuda):
+    """The conv2 backward's dgrad over the class's 100 pixels in 7 tiles (shipped) and over a
+    10 x 12 grid per phase class (variant 2) run the same k-order per output: da1, the weight
+    and the bias partials bitwise equal."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    L = CONVS[1]
+    N, grid = 333, 64
+    g = torch.Generator().manual_seed(12)
+    x = torch.relu(torch.randn(N * L.hin * L.hin * L.cin, generator=g)).bfloat16().to(cuda)
+    w = (torch.randn(L.cout * L.K, generator=g) * 0.05).bfloat16().to(cuda)
+    dy = torch.randn(N * L.hout * L.hout * L.cout, generator=g).bfloat16().to(cuda)
+    outs = []
+    for variant in (0, 2):
+        dx = torch.full((N * L.hin * L.hin * L.cin,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        part = torch.full((grid * L.cout * L.K,), float("nan"), device=cuda)
+        bpart = torch.full((grid * 512,), float("nan"), device=cuda)
+        h.conv2_bwd(dy, w, x, dx, part, bpart, N, grid, staged=variant)
+        torch.cuda.synchronize()
+        outs.append((dx, part, bpart))
+    for a, b in zip(*outs):
+        assert torch.isfinite(a.float()).all() and torch.equal(a, b)

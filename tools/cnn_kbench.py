@@ -82,7 +82,7 @@ def main():
             h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=1)
         fns["bwd2"] = bwd2
         fns["bwd2_staged"] = bwd2_staged
-        fns["bwd2_7tiles"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=2)
+        fns["bwd2_grid12"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=2)
 
     # --rounds R: the list R times, every other round in reverse order (the first kernel timed
     # in a process reads slow), median per kernel
