@@ -65,7 +65,7 @@ constexpr int kFrameRows = 441;               // 21 x 21 s2d pixels
 // conv1 fragment reads of 16 consecutive output pixels then hit disjoint banks, 1.6 -> 1.0
 // LDS cycles per conflict-free cycle (tools/lds_bank_model.py --fwd)
 constexpr int kFrameW = 28;
-constexpr int kXiRows = 20 * kFrameW + 21;      // last position read: (20, 20)
+constexpr int kXiRows = 20 * kFrameW + 24;      // last position read: (20, 20) at row 580
 constexpr int kA2Ld = 80;  // a2 / a3 rows: 64 co + 16 pad (72 measured 2.5x conflict cycles on the conv3 reads, 80 1.75x)
 // Measured and not shipped (FwdLayout PROBE bits, profiles/r4_fwd_layouts.txt):
 //  bit 4: a1 as four stride-2 phase images, (y, x) at row 100 (2 (y & 1) + (x & 1)) +
@@ -75,8 +75,9 @@ constexpr int kA2Ld = 80;  // a2 / a3 rows: 64 co + 16 pad (72 measured 2.5x con
 //  bit 5: conv3 over a 7 x 9 grid (consecutive a2 rows, 1.75 -> 1.0 modelled): 54.8 -> 58.7 us
 //   per 2,048 frames, Pong -1 to -2 % in an ABBA run on one box.
 constexpr int kXi = 0;                                    // element offsets into LDS
-constexpr int kA1 = kXi + kXiRows * kFrameLd;             // 46,480
-constexpr int kLds = (kA1 + 400 * 48 + 2 * 81 * kA2Ld + 49 * 64) * 2;  // 163,552 bytes: the largest variant
+constexpr int kA1 = kXi + kXiRows * kFrameLd;             // 46,720
+// the largest variant (phase a1, its frame image cut to the 581 rows read): 163,552 bytes
+constexpr int kLds = ((kXiRows - 3) * kFrameLd + 400 * 48 + 2 * 81 * kA2Ld + 49 * 64) * 2;
 static_assert(kLds <= 160 * 1024, "LDS per workgroup");
 __device__ __forceinline__ int a1_row(int p) {  // a1 pixel p = 20 y + x -> phase-image row
   const int y = p / 20, x = p - 20 * (p / 20);
@@ -90,7 +91,8 @@ template <int PROBE>
 struct FwdLayout {
   static constexpr bool kPhaseA1 = (PROBE & 16) != 0, kGrid3 = (PROBE & 32) != 0;
   static constexpr int kA1Ld = kPhaseA1 ? 48 : 40, kA3Ld = kPhaseA1 ? 64 : 80;
-  static constexpr int kA1 = cs::kA1, kA2 = kA1 + 400 * kA1Ld, kA3 = kA2 + 2 * 81 * cs::kA2Ld;
+  static constexpr int kA1 = kPhaseA1 ? cs::kA1 - 3 * cs::kFrameLd : cs::kA1;
+  static constexpr int kA2 = kA1 + 400 * kA1Ld, kA3 = kA2 + 2 * 81 * cs::kA2Ld;
   static_assert((kA3 + 49 * kA3Ld) * 2 <= cs::kLds, "variant fits in LDS");
   // discarded grid positions read past their image -- conv2 up to phase row 406, conv3 up to
   // buffer row 83 -- garbage in discarded output rows only, always inside the allocation
@@ -117,7 +119,7 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
   auto a1r = [](int p) { return L::kPhaseA1 ? a1_row(p) : p; };
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Xi = smem + kXi;  // [21 x 28][80] frame as bf16 integers 0..255
-  uint16_t* A1 = smem + kA1;  // 4 x [100][48] conv1 output, phase images (a1_row)
+  uint16_t* A1 = smem + kA1;  // [400][40] conv1 output (PROBE bit 4: 4 x [100][48] phase images)
   uint16_t* A3 = smem + kA3;  // [49][64]  conv3 output
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int i = lane & 15, g = lane >> 4;
@@ -355,7 +357,7 @@ static int launch_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const flo
                                  const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
                                  uint16_t* y3, int N, int max_grid, hipStream_t stream) {
   using L = cs::FwdLayout<PROBE>;
-  constexpr int lds = (L::kA3 + 49 * L::kA3Ld) * 2;  // 158,720 bytes for the shipped layout
+  constexpr int lds = (L::kA3 + 49 * L::kA3Ld) * 2;  // 159,200 bytes for the shipped layout
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)conv_stack_fwd_kernel<PROBE>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -803,8 +805,9 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
       // D = da1^T: lane (i16, g) holds channels 16 ct + 4g .. + 3 of class pixel p
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
-        const int p = 16 * (T0 + u) + i16, a = p / W, b = p - W * (p / W);
-        if (a < 10 && b < 10) {
+        const int p = 16 * (T0 + u) + i16;
+        if (GRID12 ? (p / 12 < 10 && p % 12 < 10) : p < 100) {
+          const int a = p / W, b = p - a * W;
           const uint2 m = *reinterpret_cast<const uint2*>(P + (cls * kPRows + a * 10 + b) * kPLd + 16 * ct + 4 * g);
           const uint2 v = make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x),
                                      relu_mask2(pk_bf16(acc[u][2], acc[u][3]), m.y));
