@@ -209,6 +209,7 @@ class DeviceNatureCNN:
         self.wfc_t = torch.empty(FC_IN * HIDDEN, dtype=torch.bfloat16, device=dev)  # [3136][512]
         # split-K partials of the fc forward, sized once for every batch up to max_batch: a
         # captured update graph holds this storage, so it must never be reallocated
+        self.FC_SPLIT_CAP = int(os.environ.get("RRL_FC_SPLITS", str(self.FC_SPLIT_CAP)))
         fc_rows = max(self.fc_splits(n) * n for n in range(1, self.max_batch + 1)) if self.fc_nt else 0
         self._fc_part = torch.empty(fc_rows * HIDDEN, device=dev) if self.fc_nt else None
         self.refresh_shadow()
@@ -301,11 +302,13 @@ class DeviceNatureCNN:
     # per CU (tools/fc_kbench.py)
     FC_WGRAD_SPLITS = 5
 
-    @staticmethod
-    def fc_splits(n: int) -> int:
+    # cap of the fc forward's split-K count (RRL_FC_SPLITS, for A/B runs)
+    FC_SPLIT_CAP = 8
+
+    def fc_splits(self, n: int) -> int:
         """split-K count of the fc forward: >= 256 workgroups of 128 x 128 tiles, at most 8."""
         tiles = -(-n // 128) * (HIDDEN // 128)
-        return max(1, min(8, -(-256 // tiles)))
+        return max(1, min(self.FC_SPLIT_CAP, -(-256 // tiles)))
 
     @staticmethod
     def _head_grid(n: int) -> int:
