@@ -38,6 +38,7 @@ int rrl_scan_flat_blocks(int L);
 int rrl_scan_flat(const float* rew, const float* done, const float* val, const float* boot, float* adv,
                   float* ret, float* work, float* stats_out, int L, float gamma, float lam, void* stream);
 int rrl_stats_reduce(const float* part, int nparts, float* out, void* stream);
+int rrl_column_sums(const float* part, int rows, int ld, int cols, double* out, void* stream);
 int rrl_adam(float* param, float* m, float* v, const float* grad, const float* slab, int nslab,
              float* grad_out, int* step, unsigned* ticket, int P, float lr, float beta1, float beta2,
              float eps, float grad_scale, float weight_decay, int step_add, int step_inc, void* stream);
@@ -272,6 +273,17 @@ void stats_reduce(const Tensor& part, const Tensor& out) {
            "stats_reduce");
 }
 
+void column_sums(const Tensor& part, int64_t cols, const Tensor& out) {
+  check_dev(part, "part", at::kFloat);
+  TORCH_CHECK(part.dim() == 2 && part.is_contiguous(), "column_sums: part must be a contiguous [rows, ld] tensor");
+  TORCH_CHECK(cols >= 1 && cols <= 8 && cols <= part.size(1), "column_sums: 1 <= cols <= min(8, ld)");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kDouble && out.numel() >= cols && out.is_contiguous(),
+              "column_sums: out must be a contiguous float64 device tensor of >= cols elements");
+  check_rc(rrl_column_sums(part.data_ptr<float>(), (int)part.size(0), (int)part.size(1), (int)cols,
+                           out.data_ptr<double>(), cur_stream()),
+           "column_sums");
+}
+
 void adam(const Tensor& param, const Tensor& m, const Tensor& v, const OptT& grad, const OptT& slab,
           const OptT& grad_out, const Tensor& step, const Tensor& ticket, double lr, double beta1, double beta2,
           double eps, double grad_scale, double weight_decay, int64_t step_add, int64_t step_inc) {
@@ -432,6 +444,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scan_flat_blocks", &scan_flat_blocks);
   m.def("scan_flat", &scan_flat);
   m.def("stats_reduce", &stats_reduce);
+  m.def("column_sums", &column_sums, "double column sums of the first cols columns of a [rows, ld] fp32 tensor");
   // step_add / step_inc: t = step + step_add + 1, the counter advances by step_inc (adam.hip)
   m.def("adam", &adam, pybind11::arg("param"), pybind11::arg("m"), pybind11::arg("v"), pybind11::arg("grad"),
         pybind11::arg("slab"), pybind11::arg("grad_out"), pybind11::arg("step"), pybind11::arg("ticket"),

@@ -119,6 +119,38 @@ __global__ __launch_bounds__(256) void stats_reduce_kernel(const float* part, in
   }
 }
 
+// Column sums, in double, of the first `cols` (<= 8) columns of a [rows][ld] fp32 array (single
+// block; the per-epoch episode sums of the threshold check: one launch where a strided torch
+// reduction + cast were two at ~14 us).
+__global__ __launch_bounds__(256) void column_sums_kernel(const float* part, int rows, int ld, int cols, double* out) {
+  __shared__ double red[8][4];
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k = threadIdx.x; k < rows; k += blockDim.x)
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < cols) acc[q] += (double)part[(size_t)k * ld + q];
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    double v = acc[q];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) red[q][w] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < cols) {
+    double v = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) v += red[threadIdx.x][k];
+    out[threadIdx.x] = v;
+  }
+}
+
+extern "C" int rrl_column_sums(const float* part, int rows, int ld, int cols, double* out, void* stream) {
+  if (rows < 0 || cols < 1 || cols > 8 || ld < cols) return -1;
+  hipLaunchKernelGGL(column_sums_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, part, rows, ld, cols, out);
+  return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------------------ flat segmented scan
 // Element t of two coupled recurrences (adv, ret):
 //   nd = 1 - done_t ; v_next = done_t ? boot_t : val_{t+1}
