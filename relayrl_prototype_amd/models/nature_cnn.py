@@ -276,6 +276,13 @@ class DeviceNatureCNN:
         assert self.side_mode in ("early", "late", "sums"), self.side_mode
         self._ev_fork = torch.cuda.Event()
         self._ev_join = torch.cuda.Event()
+        self._ev_t_fork = torch.cuda.Event()
+        self._ev_t_join = torch.cuda.Event()
+        self._wfc_t_stale = self._wfc_t_pending = False
+        # RRL_CNN_DEFER_TRANSPOSE=1: the transposed-Wfc refresh after Adam moves to the side stream
+        # beside the next rollout -- +0.3 % at 2,048 envs, -0.5 % at 8,192 in an ABBA run
+        # (profiles/r4_defer_transpose_ab.txt): off by default
+        self.defer_transpose = os.environ.get("RRL_CNN_DEFER_TRANSPOSE", "0") == "1"
         self.norm_sq = torch.empty(1, device=dev)
 
     @staticmethod
@@ -291,8 +298,11 @@ class DeviceNatureCNN:
     def refresh_shadow(self):
         """bf16 copies of the fp32 master weights (after a load / broadcast; Adam writes the
         flat shadow itself) and the transposed fc shadow for the data gradient."""
+        if getattr(self, "_wfc_t_pending", False):
+            self._wfc_t_ready()  # a side-stream refresh in flight finishes first
         self.h.to_bf16(self.params, self.shadow)
         self._transpose_fc()
+        self._wfc_t_stale = False
 
     def _transpose_fc(self):
         o = self.o
@@ -470,6 +480,7 @@ class DeviceNatureCNN:
             fork_weight_grads()
         da3 = self.da3[:B * FC_IN]
         if self.fc_nt:
+            self._wfc_t_ready()
             h.fc_nt_mask(dh, self.wfc_t, a3, da3, B, FC_IN, HIDDEN)
         else:
             h.gemm_dgrad(dh, sh[o["wfc"]:o["bfc"]], a3, da3, B, HIDDEN, FC_IN)
@@ -567,7 +578,32 @@ class DeviceNatureCNN:
                          self.norm_sq if max_grad_norm > 0 else None, float(max_grad_norm), float(lr),
                          float(betas[0]), float(betas[1]), float(eps), 0, self.step_t)
         if self.fc_nt:
+            if self.side_stream is not None and self.defer_transpose:
+                # the transposed Wfc shadow is first read by the next backward's fc data gradient:
+                # begin_update() runs the transpose on the side stream beside the rollout
+                self._wfc_t_stale = True
+            else:
+                self._transpose_fc()
+
+    def begin_update(self):
+        """Start of an update (before its rollout): a transposed-Wfc refresh left by the last
+        apply() runs on the side stream, joined before the backward's fc data gradient."""
+        if self._wfc_t_stale and self.side_stream is not None and not self._wfc_t_pending:
+            self._ev_t_fork.record()
+            self.side_stream.wait_event(self._ev_t_fork)
+            with torch.cuda.stream(self.side_stream):
+                self._transpose_fc()
+                self._ev_t_join.record(self.side_stream)
+            self._wfc_t_stale, self._wfc_t_pending = False, True
+
+    def _wfc_t_ready(self):
+        """Order the transposed Wfc shadow before its first reader."""
+        if self._wfc_t_pending:
+            torch.cuda.current_stream().wait_event(self._ev_t_join)
+            self._wfc_t_pending = False
+        elif self._wfc_t_stale:
             self._transpose_fc()
+            self._wfc_t_stale = False
 
     def state_dict(self):
         return {"params": self.params, "m": self.m, "v": self.v, "step": self.step_t.cpu()}

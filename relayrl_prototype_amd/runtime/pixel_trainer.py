@@ -115,6 +115,7 @@ class PixelA2CTrainer:
     # ------------------------------------------------------------------ GPU
     def _rollout_gpu(self, base, nxt):
         cfg, m, N, T = self.cfg, self.model, self.cfg.num_envs, self.cfg.rollout_len
+        m.begin_update()  # the transposed Wfc refresh beside the rollout (side stream)
         for t in range(T):
             m.act(base[t], t * N, self.act[t], self.logp[t], self.val[t], self.sample_seed, t,
                   step_base=self.sample_t)

@@ -1,4 +1,4 @@
-# Round 4: vectorised clip + Adam and sum of squares of the Pong model: CNN GPU tests, Pong, kernel profile
+# Round 4: vectorised clip + Adam and sum of squares, the Wfc transpose beside the rollout: CNN GPU tests, Pong, kernel profile
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 ls -la --time-style=+%H:%M:%S relayrl_prototype_amd/_hip_ops*.so

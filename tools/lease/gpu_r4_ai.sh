@@ -1,0 +1,10 @@
+# Round 4: the Wfc transpose beside the rollout (RRL_CNN_DEFER_TRANSPOSE 1) vs after Adam (0),
+# Pong ABBA on one box
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+i=0
+for v in A B B A A B B A; do i=$((i+1)); for n in 2048 8192; do
+  if [ $v = A ]; then d=1; else d=0; fi
+  RRL_CNN_DEFER_TRANSPOSE=$d timeout -k 10 300 python3 benchmarks/pong_a2c_bench.py --num-envs $n --steps 60 --warmup 5 > gpurun_out/pong_ai_${n}_$v.$i.json 2>&1 || exit 1
+  echo "$n $v(defer $d) run$i $(tail -1 gpurun_out/pong_ai_${n}_$v.$i.json | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]/1e6,3))')"
+done; done
