@@ -276,6 +276,10 @@ class DeviceNatureCNN:
         assert self.side_mode in ("early", "late", "sums"), self.side_mode
         self._ev_fork = torch.cuda.Event()
         self._ev_join = torch.cuda.Event()
+        self._ev_c3, self._ev_c3_done = torch.cuda.Event(), torch.cuda.Event()
+        self._ev_c2, self._ev_c2_done = torch.cuda.Event(), torch.cuda.Event()
+        # RRL_CNN_SIDE_CONV_SUMS=1 (off): see backward(); ABBA -0.0 / -0.4 % at 2,048 / 8,192 envs
+        self.side_conv_sums = os.environ.get("RRL_CNN_SIDE_CONV_SUMS", "0") == "1"
         self._ev_t_fork = torch.cuda.Event()
         self._ev_t_join = torch.cuda.Event()
         self._wfc_t_stale = self._wfc_t_pending = False
@@ -474,6 +478,23 @@ class DeviceNatureCNN:
         # (profiles/r4_side_late_and_configs.txt, r4_side_late_ab.txt).  Mode "sums": the fc
         # weight GEMM runs right after the data GEMM on the main stream (in "early" the two
         # overlap and stretch each other: 48 + 42 us alone, ~126 us together in the trace)
+        # RRL_CNN_SIDE_CONV_SUMS=1: each conv layer's slab sum forks onto the side stream as soon
+        # as its backward kernel is done (conv3's beside conv2's backward, conv2's beside conv1's),
+        # leaving only conv1's sum on the main stream's tail: the tail sum 23 -> 6 us, but every
+        # cross-stream edge of the replayed graph costs the main stream ~9 us (kernel trace:
+        # conv3 -> conv2 and conv2 -> conv1 gaps of 9-10 us), so no gain (profiles/r4_side_conv_sums_ab.txt)
+        side_sums = side is not None and self.fused_convs and self.side_conv_sums
+
+        side_last = [self._ev_join]  # the side stream's last join event (one event per record)
+
+        def fork_sums(segs, ev, ev_done):
+            ev.record()
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                h.sum_splits_multi(segs)
+                ev_done.record(side)
+            side_last[0] = ev_done
+
         mode = self.side_mode if side is not None else "early"
         sums_mode = mode == "sums" and self.fc_nt and B % 64 == 0 and self.fc_tn_bias
         if mode == "early" or (mode == "sums" and not sums_mode):
@@ -501,6 +522,9 @@ class DeviceNatureCNN:
             h.conv3_bwd(da3, sh[o["w3"]:o["b3"]], a2, da2, self.cpart["c3"], self.cbias["c3"], B, nblk)
             sums = [(self.cpart["c3"], nblk, L3.cout * L3.K, g[o["w3"]:o["b3"]]),
                     (self.cbias["c3"], nblk * 8, L3.cout, g[o["b3"]:o["b3"] + L3.cout])]
+            if side_sums:  # conv3's slabs are final: summed on the side stream beside conv2 / conv1
+                fork_sums(sums, self._ev_c3, self._ev_c3_done)
+                sums = []
         else:
             self._wgrad("c3", da3, a2, B, L3.hin, L3.cin, L3.k, L3.s, L3.cout, o["w3"])
             self._bias(da3, B * L3.hout ** 2, L3.cout, o["b3"])
@@ -513,6 +537,9 @@ class DeviceNatureCNN:
                         staged=self.bwd2_variant)
             sums += [(self.cpart["c2"], nblk, L2.cout * L2.K, g[o["w2"]:o["b2"]]),
                      (self.cbias["c2"], nblk * 8, L2.cout, g[o["b2"]:o["b2"] + L2.cout])]
+            if side_sums:
+                fork_sums(sums, self._ev_c2, self._ev_c2_done)
+                sums = []
         else:
             self._wgrad("c2", da2, a1, B, L2.hin, L2.cin, L2.k, L2.s, L2.cout, o["w2"])
             self._bias(da2, B * L2.hout ** 2, L2.cout, o["b2"])
@@ -529,7 +556,7 @@ class DeviceNatureCNN:
             self._wgrad("c1", da1, obs_u8.contiguous(), B, S2D.hin, S2D.cin, S2D.k, S2D.s, S2D.cout, o["w1"],
                         bias_off=o["b1"])
         if side is not None:
-            torch.cuda.current_stream().wait_event(self._ev_join)
+            torch.cuda.current_stream().wait_event(side_last[0])
         if pending is not None:
             comm.all_reduce_sum_(g[:o["wfc"]])
             pending.wait()

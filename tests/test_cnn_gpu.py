@@ -710,11 +710,12 @@ def test_pixel_update_side_stream_is_race_free(cuda, monkeypatch):
 
     cfg = dict(num_envs=64, rollout_len=4, seed=5)
     runs = []
-    for side, mode, defer in (("0", "early", "0"), ("1", "early", "0"), ("1", "late", "0"), ("1", "sums", "0"),
-                              ("1", "early", "1")):
+    for side, mode, defer, csums in (("0", "early", "0", "1"), ("1", "early", "0", "1"), ("1", "late", "0", "1"),
+                                     ("1", "sums", "0", "1"), ("1", "early", "1", "1"), ("1", "early", "0", "0")):
         monkeypatch.setenv("RRL_CNN_SIDE", side)
         monkeypatch.setenv("RRL_CNN_SIDE_MODE", mode)
         monkeypatch.setenv("RRL_CNN_DEFER_TRANSPOSE", defer)
+        monkeypatch.setenv("RRL_CNN_SIDE_CONV_SUMS", csums)
         tr = PixelA2CTrainer(PixelA2CConfig(use_graphs=True, **cfg), device=cuda)
         assert (tr.model.side_stream is not None) == (side == "1") and tr.model.side_mode == mode
         for _ in range(5):  # eager warm-up, capture + replay, 3 replays
