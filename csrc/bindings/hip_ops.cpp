@@ -33,7 +33,7 @@ int rrl_mlp_grad(int head, const float* params, const float* X, int B, int D, in
 int rrl_scan_tm_parts(int N);
 int rrl_gae_scan_tm(const float* rew, const float* done, const float* val, const float* tval, float* adv,
                     float* ret, float* stats_part, float* stats_out, int K, int T, int N, float gamma,
-                    float lam, void* stream);
+                    float lam, long long* const* cnt, const long long* inc, int ncnt, void* stream);
 int rrl_scan_flat_blocks(int L);
 int rrl_scan_flat(const float* rew, const float* done, const float* val, const float* boot, float* adv,
                   float* ret, float* work, float* stats_out, int L, float gamma, float lam, void* stream);
@@ -218,7 +218,8 @@ void mlp_grad(int64_t head, const Tensor& params, const Tensor& X, int64_t A, in
 int64_t scan_tm_parts(int64_t N) { return rrl_scan_tm_parts((int)N); }
 
 void gae_scan_tm(const Tensor& rew, const Tensor& done, const OptT& val, const OptT& tval, const Tensor& adv,
-                 const Tensor& ret, const Tensor& stats_part, const OptT& stats_out, double gamma, double lam) {
+                 const Tensor& ret, const Tensor& stats_part, const OptT& stats_out, double gamma, double lam,
+                 const std::vector<std::tuple<Tensor, int64_t>>& counters) {
   // rew [T, N] or [K, T, N] (K actor blocks of one learner shard); val [K*T*N + K*N]
   check_dev(rew, "rew", at::kFloat);
   TORCH_CHECK(rew.dim() == 2 || rew.dim() == 3, "rew must be [T, N] or [K, T, N]");
@@ -235,9 +236,19 @@ void gae_scan_tm(const Tensor& rew, const Tensor& done, const OptT& val, const O
   check_dev(stats_part, "stats_part", at::kFloat);
   check_numel(stats_part, "stats_part", scan_tm_parts(K * N) * 3);
   float* so = fptr_mut(stats_out, "stats_out", 3);
+  // device step counters advanced by the same launch (int64 scalars on this device)
+  TORCH_CHECK(counters.size() <= 3, "gae_scan_tm: at most 3 counters");
+  long long* cnt[3] = {nullptr, nullptr, nullptr};
+  long long inc[3] = {0, 0, 0};
+  for (size_t q = 0; q < counters.size(); ++q) {
+    const Tensor& c = std::get<0>(counters[q]);
+    TORCH_CHECK(c.is_cuda() && c.scalar_type() == at::kLong && c.numel() == 1, "gae_scan_tm: counter must be an int64 scalar on the device");
+    cnt[q] = reinterpret_cast<long long*>(c.data_ptr<int64_t>());
+    inc[q] = (long long)std::get<1>(counters[q]);
+  }
   const int rc = rrl_gae_scan_tm(rew.data_ptr<float>(), done.data_ptr<float>(), v, tv, adv.data_ptr<float>(),
                                  ret.data_ptr<float>(), stats_part.data_ptr<float>(), so, (int)K, (int)T, (int)N,
-                                 (float)gamma, (float)lam, cur_stream());
+                                 (float)gamma, (float)lam, cnt, inc, (int)counters.size(), cur_stream());
   check_rc(rc, "gae_scan_tm");
 }
 
@@ -440,7 +451,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "value forward: 1 = bf16x6 weight-stationary split kernel (H 128, D <= 24), 0 = fp32 MFMA; returns "
         "the previous mode (-1 queries)");
   m.def("scan_tm_parts", &scan_tm_parts);
-  m.def("gae_scan_tm", &gae_scan_tm);
+  m.def("gae_scan_tm", &gae_scan_tm, pybind11::arg("rew"), pybind11::arg("done"), pybind11::arg("val"),
+        pybind11::arg("tval"), pybind11::arg("adv"), pybind11::arg("ret"), pybind11::arg("stats_part"),
+        pybind11::arg("stats_out"), pybind11::arg("gamma"), pybind11::arg("lam"),
+        pybind11::arg("counters") = std::vector<std::tuple<Tensor, int64_t>>{});
   m.def("scan_flat_blocks", &scan_flat_blocks);
   m.def("scan_flat", &scan_flat);
   m.def("stats_reduce", &stats_reduce);

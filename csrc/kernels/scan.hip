@@ -29,9 +29,13 @@ struct ScanTM {
   float* stats_part;   // [nblocks][3] adv sum / sumsq / count
   int T, N, K;
   float gamma, lam;
+  long long* cnt[3];   // device step counters advanced by block 0 (the Pong update's sampling /
+  long long inc[3];    // env / Adam counters: one launch fewer per update), ncnt of them
+  int ncnt;
 };
 
 __global__ __launch_bounds__(256) void gae_scan_tm_kernel(ScanTM p) {
+  if (blockIdx.x == 0 && (int)threadIdx.x < p.ncnt) p.cnt[threadIdx.x][0] += p.inc[threadIdx.x];
   const int col = blockIdx.x * blockDim.x + threadIdx.x;  // column = block k, env n
   float s = 0.f, ss = 0.f, c = 0.f;
   if (col < p.K * p.N) {
@@ -301,10 +305,16 @@ extern "C" int rrl_scan_tm_parts(int N) { return (N + 255) / 256; }
 // nparts of rrl_scan_tm_parts(K * N)
 extern "C" int rrl_gae_scan_tm(const float* rew, const float* done, const float* val, const float* tval,
                                float* adv, float* ret, float* stats_part, float* stats_out, int K, int T, int N,
-                               float gamma, float lam, void* stream) {
+                               float gamma, float lam, long long* const* cnt, const long long* inc, int ncnt,
+                               void* stream) {
+  if (ncnt < 0 || ncnt > 3) return -1;
   hipStream_t s = (hipStream_t)stream;
   const int nb = rrl_scan_tm_parts(K * N);
-  ScanTM p{rew, done, val, tval, adv, ret, stats_part, T, N, K, gamma, lam};
+  ScanTM p{rew, done, val, tval, adv, ret, stats_part, T, N, K, gamma, lam, {}, {}, ncnt};
+  for (int i = 0; i < ncnt; ++i) {
+    p.cnt[i] = cnt[i];
+    p.inc[i] = inc[i];
+  }
   hipLaunchKernelGGL(gae_scan_tm_kernel, dim3(nb), dim3(256), 0, s, p);
   if (stats_out) hipLaunchKernelGGL(stats_reduce_kernel, dim3(1), dim3(256), 0, s, stats_part, nb, stats_out);
   return (int)hipGetLastError();

@@ -266,10 +266,11 @@ def adam_step(param, m, v, step_t, ticket_t, lr, grad=None, slab=None, beta1=0.9
 
 
 def gae_scan_tm(rew, done, val, gamma, lam, adv=None, ret=None, stats_part=None, stats_out=None, tval=None,
-                stats=True):
+                stats=True, counters=()):
     """Time-major GAE / discounted-return scan -> (adv, ret, stats[3]).  ``stats=False``: the
     caller does not use the advantage statistics; the GPU path skips their reduction launch and
-    returns None for them.
+    returns None for them.  ``counters``: (int64 device scalar, increment) pairs (at most 3)
+    advanced by the same launch (the Pong update's step counters: one launch fewer).
 
     ``rew`` / ``done`` / ``tval`` are [T, N], or [K, T, N] for a learner shard holding K
     actor blocks; ``val`` is flat [K*T*N + K*N]: V of every step, then the bootstrap value
@@ -281,6 +282,8 @@ def gae_scan_tm(rew, done, val, gamma, lam, adv=None, ret=None, stats_part=None,
         a, r, s = ref.gae_scan_tm_ref(rew, done, val, gamma, lam, tval)
         if stats_out is not None:
             stats_out.copy_(s)
+        for c, inc in counters:
+            c += int(inc)
         return a, r, s
     K = rew.shape[0] if rew.dim() == 3 else 1
     T, N = rew.shape[-2], rew.shape[-1]
@@ -292,7 +295,7 @@ def gae_scan_tm(rew, done, val, gamma, lam, adv=None, ret=None, stats_part=None,
     if stats_out is None and stats:
         stats_out = torch.empty(3, device=dev)
     h.gae_scan_tm(rew.contiguous(), done.contiguous(), None if val is None else val.contiguous(), _f32(tval), adv, ret,
-                  stats_part, stats_out, float(gamma), float(lam))
+                  stats_part, stats_out, float(gamma), float(lam), counters=[(c, int(i)) for c, i in counters])
     return adv, ret, stats_out
 
 

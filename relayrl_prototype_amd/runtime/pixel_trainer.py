@@ -122,10 +122,8 @@ class PixelA2CTrainer:
             # the last observation goes straight to the next update's start slot
             self.env.step(self.act[t], base[t + 1] if (t + 1 < T or nxt is None) else nxt[0], self.rew[t],
                           self.done[t], offset=t)
-        # the sampling, env and Adam step counters advance in ONE launch (the Adam step of this
-        # update's apply(step_bumped=True) below; every rollout is followed by one update)
-        self.model.h.counter_add_many([(self.sample_t, cfg.rollout_len), (self.env.step_t, cfg.rollout_len),
-                                       (m.step_t, 1)])
+        # the sampling, env and Adam step counters advance inside the update's scan launch
+        # (_update_gpu; every rollout is followed by one update)
         # bootstrap V(obs[T]) with the pre-update weights; its activations go to the
         # scratch rows [T*N, (T+1)*N) so the stored rollout activations stay intact
         m.value(base[T] if nxt is None else nxt[0], cfg.rollout_len * N, self.val[cfg.rollout_len])
@@ -137,8 +135,11 @@ class PixelA2CTrainer:
         N, T = cfg.num_envs, cfg.rollout_len
         B = N * T
         with self.timer.phase("Returns"):
+            # + the sampling / env / Adam step counters of this rollout and update (the Adam step of
+            # apply(step_bumped=True) below): no launch of their own
             adv, ret, _ = gae_scan_tm(self.rew, self.done, self.val, cfg.gamma, 1.0, self.adv, self.ret,
-                                      self._stats_part, stats=False)
+                                      self._stats_part, stats=False,
+                                      counters=((self.sample_t, T), (self.env.step_t, T), (m.step_t, 1)))
         with self.timer.phase("Backward"):
             stats = m.backward(base[:T].reshape(B, 21, 21, 64), self.act.reshape(B), adv.reshape(B),
                                ret.reshape(B), cfg.vf_coef, cfg.ent_coef, comm=self.comm)
