@@ -29,8 +29,9 @@ int rrl_sum_splits_multi(const float* const* parts, const int* splits, const lon
 int rrl_colsum(const uint16_t* y, int M, int C, float* part, int splits, void* stream);
 int rrl_sumsq(const float* x, long long n, float* work, int work_n, float* out, void* stream);
 int rrl_adam_clip(float* p, float* m, float* v, const float* g, uint16_t* shadow, long long n, const float* norm_sq,
-                  float max_norm, float lr, float b1, float b2, float eps, int step, const long long* step_dev,
+                  float max_norm, float lr, float b1, float b2, float eps, int step, const long long* step_dev, int norm_parts,
                   void* stream);
+int rrl_sumsq_partial(const float* x, long long n, float* work, int work_n, void* stream);
 int rrl_counter_add(long long* c, long long inc, void* stream);
 int rrl_counter_add_n(long long* const* c, const long long* inc, int n, void* stream);
 int rrl_to_bf16(const float* x, uint16_t* y, long long n, void* stream);
@@ -301,7 +302,7 @@ void sumsq(const Tensor& x, const Tensor& work, const Tensor& out) {
 
 void adam_clip(const Tensor& p, const Tensor& m, const Tensor& v, const Tensor& g, const OptT& shadow,
                const OptT& norm_sq, double max_norm, double lr, double b1, double b2, double eps, int64_t step,
-               const OptT& step_dev) {
+               const OptT& step_dev, int64_t norm_parts) {
   const int64_t n = p.numel();
   check(p, "p", at::kFloat, n);
   check(m, "m", at::kFloat, n);
@@ -310,10 +311,22 @@ void adam_clip(const Tensor& p, const Tensor& m, const Tensor& v, const Tensor& 
   const long long* sd = opt_ptr<const long long>(step_dev, "step_dev", at::kLong, 1);
   TORCH_CHECK(sd != nullptr || step >= 1, "adam step must be >= 1");
   uint16_t* sh = opt_ptr<uint16_t>(shadow, "shadow", at::kBFloat16, n);
-  const float* ns = opt_ptr<const float>(norm_sq, "norm_sq", at::kFloat, 1);
+  TORCH_CHECK(norm_parts >= 0 && norm_parts <= 1024, "adam_clip: norm_parts in 0..1024");
+  // norm_parts > 0: norm_sq holds that many sum-of-squares partials, else the squared norm
+  const float* ns = opt_ptr<const float>(norm_sq, "norm_sq", at::kFloat, norm_parts > 0 ? norm_parts : 1);
   rc_check(rrl_adam_clip(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr<float>(), sh, n,
-                         ns, (float)max_norm, (float)lr, (float)b1, (float)b2, (float)eps, (int)step, sd, stream()),
+                         ns, (float)max_norm, (float)lr, (float)b1, (float)b2, (float)eps, (int)step, sd,
+                         (int)norm_parts, stream()),
            "adam_clip");
+}
+
+// sum-of-squares partials of x into work (the clip + Adam launch reduces them: norm_parts)
+int64_t sumsq_partial(const Tensor& x, const Tensor& work) {
+  check(x, "x", at::kFloat, 0);
+  check(work, "work", at::kFloat, 0);
+  const int g = rrl_sumsq_partial(x.data_ptr<float>(), x.numel(), work.data_ptr<float>(), (int)work.numel(), stream());
+  TORCH_CHECK(g > 0, "sumsq_partial failed");
+  return g;
 }
 
 // several device counters in one launch: [(counter, inc), ...], at most 4 (distinct tensors)
@@ -505,7 +518,8 @@ void register_cnn_ops(pybind11::module_& m) {
   m.def("adam_clip", &adam_clip, pybind11::arg("p"), pybind11::arg("m"), pybind11::arg("v"), pybind11::arg("g"),
         pybind11::arg("shadow"), pybind11::arg("norm_sq"), pybind11::arg("max_norm"), pybind11::arg("lr"),
         pybind11::arg("b1"), pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("step"),
-        pybind11::arg("step_dev") = pybind11::none());
+        pybind11::arg("step_dev") = pybind11::none(), pybind11::arg("norm_parts") = 0);
+  m.def("sumsq_partial", &sumsq_partial);
   m.def("counter_add", &counter_add);
   m.def("counter_add_many", &counter_add_many);
   m.def("to_bf16", &to_bf16);

@@ -436,12 +436,24 @@ __global__ void sum_small_kernel(const float* __restrict__ part, int n, float* _
   if (threadIdx.x == 0) out[0] = red[0] + red[1] + red[2] + red[3];
 }
 
+// The squared norm from the sum-of-squares partials, reduced inside every clip + Adam block in
+// sum_small_kernel's exact order (256 threads): the same float, one launch fewer per update.
+__device__ __forceinline__ float block_sum_parts(const float* __restrict__ part, int n) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += part[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
 // Adam with global-norm clipping (scale = min(1, max_norm / ||g||), norm from the device)
 // and a bf16 shadow copy of the updated parameters for the next forward.
 __global__ void adam_clip_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                  const float* __restrict__ g, uint16_t* __restrict__ shadow, size_t n,
                                  const float* __restrict__ norm_sq, float max_norm, float lr, float b1, float b2,
-                                 float eps, float bc1, float bc2, const long long* __restrict__ step_dev) {
+                                 float eps, float bc1, float bc2, const long long* __restrict__ step_dev, int norm_parts) {
   if (step_dev) {  // bias corrections from the device step counter (capturable in a hipGraph)
     const float t = (float)(*step_dev);
     bc1 = 1.f - powf(b1, t);
@@ -449,7 +461,7 @@ __global__ void adam_clip_kernel(float* __restrict__ p, float* __restrict__ m, f
   }
   float scale = 1.f;
   if (norm_sq != nullptr && max_norm > 0.f) {
-    const float nrm = sqrtf(norm_sq[0]);
+    const float nrm = sqrtf(norm_parts > 0 ? block_sum_parts(norm_sq, norm_parts) : norm_sq[0]);
     scale = nrm > max_norm ? max_norm / (nrm + 1e-6f) : 1.f;
   }
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -471,7 +483,7 @@ __global__ void adam_clip_kernel(float* __restrict__ p, float* __restrict__ m, f
 __global__ void adam_clip4_kernel(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                                   const float* __restrict__ g, uint16_t* __restrict__ shadow, size_t n,
                                   const float* __restrict__ norm_sq, float max_norm, float lr, float b1, float b2,
-                                  float eps, float bc1, float bc2, const long long* __restrict__ step_dev) {
+                                  float eps, float bc1, float bc2, const long long* __restrict__ step_dev, int norm_parts) {
   if (step_dev) {
     const float t = (float)(*step_dev);
     bc1 = 1.f - powf(b1, t);
@@ -479,7 +491,7 @@ __global__ void adam_clip4_kernel(float* __restrict__ p, float* __restrict__ m, 
   }
   float scale = 1.f;
   if (norm_sq != nullptr && max_norm > 0.f) {
-    const float nrm = sqrtf(norm_sq[0]);
+    const float nrm = sqrtf(norm_parts > 0 ? block_sum_parts(norm_sq, norm_parts) : norm_sq[0]);
     scale = nrm > max_norm ? max_norm / (nrm + 1e-6f) : 1.f;
   }
   auto upd = [&](float pi, float mi, float vi, float gi, float& po, float& mo, float& vo) {
@@ -1596,19 +1608,32 @@ int rrl_sumsq(const float* x, long long n, float* work, int work_n, float* out, 
   return (int)hipGetLastError();
 }
 
+// sum-of-squares partials only (the clip + Adam launch reduces them itself, norm_parts = the return)
+int rrl_sumsq_partial(const float* x, long long n, float* work, int work_n, void* stream_) {
+  hipStream_t st = (hipStream_t)stream_;
+  const int g = work_n < 1 ? 1 : (work_n > 1024 ? 1024 : work_n);
+  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0)
+    hipLaunchKernelGGL(sumsq_partial_kernel<true>, dim3(g), dim3(256), 0, st, x, (size_t)n, work);
+  else
+    hipLaunchKernelGGL(sumsq_partial_kernel<false>, dim3(g), dim3(256), 0, st, x, (size_t)n, work);
+  const int rc = (int)hipGetLastError();
+  return rc != 0 ? -rc : g;
+}
+
+// norm_parts > 0: norm_sq holds that many sum-of-squares partials (rrl_sumsq_partial)
 int rrl_adam_clip(float* p, float* m, float* v, const float* g, uint16_t* shadow, long long n, const float* norm_sq,
                   float max_norm, float lr, float b1, float b2, float eps, int step, const long long* step_dev,
-                  void* stream_) {
+                  int norm_parts, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   const float bc1 = 1.f - powf(b1, (float)step), bc2 = 1.f - powf(b2, (float)step);
   const bool vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v) |
                      reinterpret_cast<uintptr_t>(g)) & 15) == 0 && (reinterpret_cast<uintptr_t>(shadow) & 7) == 0;
   if (vec)
     hipLaunchKernelGGL(adam_clip4_kernel, dim3(grid_for((size_t)(n / 4 + 1), 256, 8192)), dim3(256), 0, st, p, m, v, g,
-                       shadow, (size_t)n, norm_sq, max_norm, lr, b1, b2, eps, bc1, bc2, step_dev);
+                       shadow, (size_t)n, norm_sq, max_norm, lr, b1, b2, eps, bc1, bc2, step_dev, norm_parts);
   else
     hipLaunchKernelGGL(adam_clip_kernel, dim3(grid_for((size_t)n, 256, 8192)), dim3(256), 0, st, p, m, v, g, shadow,
-                       (size_t)n, norm_sq, max_norm, lr, b1, b2, eps, bc1, bc2, step_dev);
+                       (size_t)n, norm_sq, max_norm, lr, b1, b2, eps, bc1, bc2, step_dev, norm_parts);
   return (int)hipGetLastError();
 }
 

@@ -598,12 +598,13 @@ class DeviceNatureCNN:
             comm.all_reduce_sum_(self.grad)
             self.grad.mul_(1.0 / comm.world)
         self._reduced = False
-        self.h.sumsq(self.grad, self.sq_work, self.norm_sq)
+        # sum-of-squares partials; the clip + Adam launch reduces them itself (one launch fewer)
+        parts = int(self.h.sumsq_partial(self.grad, self.sq_work)) if max_grad_norm > 0 else 0
         if not step_bumped:
             self.h.counter_add(self.step_t, 1)
         self.h.adam_clip(self.params, self.m, self.v, self.grad, self.shadow,
-                         self.norm_sq if max_grad_norm > 0 else None, float(max_grad_norm), float(lr),
-                         float(betas[0]), float(betas[1]), float(eps), 0, self.step_t)
+                         self.sq_work if max_grad_norm > 0 else None, float(max_grad_norm), float(lr),
+                         float(betas[0]), float(betas[1]), float(eps), 0, self.step_t, norm_parts=parts)
         if self.fc_nt:
             if self.side_stream is not None and self.defer_transpose:
                 # the transposed Wfc shadow is first read by the next backward's fc data gradient:

@@ -249,6 +249,35 @@ def test_adam_clip_matches_torch(cuda):
     assert torch.equal(sh.cpu(), p.cpu().bfloat16())
 
 
+def test_adam_clip_norm_parts_equals_two_launch_norm(cuda):
+    """The clip + Adam launch reducing the sum-of-squares partials itself (norm_parts) gives
+    bitwise the update of the separate sumsq -> sum_small -> adam_clip sequence."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    n = 300007
+    g = torch.Generator().manual_seed(3)
+    p0 = torch.randn(n, generator=g).to(cuda)
+    gr = (torch.randn(n, generator=g) * 5).to(cuda)
+    outs = []
+    for fused in (False, True):
+        p, mm, vv = p0.clone(), torch.zeros(n, device=cuda), torch.zeros(n, device=cuda)
+        sh = torch.empty(n, dtype=torch.bfloat16, device=cuda)
+        work = torch.empty(1024, device=cuda)
+        nsq = torch.empty(1, device=cuda)
+        for i in range(1, 4):
+            if fused:
+                parts = int(h.sumsq_partial(gr, work))
+                h.adam_clip(p, mm, vv, gr, sh, work, 0.5, 1e-3, 0.9, 0.999, 1e-5, i, norm_parts=parts)
+            else:
+                h.sumsq(gr, work, nsq)
+                h.adam_clip(p, mm, vv, gr, sh, nsq, 0.5, 1e-3, 0.9, 0.999, 1e-5, i)
+        torch.cuda.synchronize()
+        outs.append((p, mm, vv, sh))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_head_sampling_distribution(cuda):
     spec = CNNSpec(6)
     B = 4096

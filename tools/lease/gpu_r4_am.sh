@@ -1,4 +1,4 @@
-# Round 4: the Pong update's step counters advanced inside the scan launch: GPU tests touching the
+# Round 4: step counters inside the scan launch, the norm reduction inside the clip + Adam launch: GPU tests touching the
 # scan / Pong trainer, Pong 2,048 / 8,192 envs, kernel profile
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
