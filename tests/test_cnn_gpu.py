@@ -704,6 +704,25 @@ def test_sum_splits_multi_matches_torch(cuda):
         assert torch.allclose(out.double(), ref, atol=1e-4, rtol=1e-5), (s, n)
 
 
+@pytest.mark.parametrize("shapes", [[(5, 1605632), (5, 512)], [(1, 1028), (8, 64), (3, 4)]])
+def test_sum_splits_few_matches_torch(cuda, shapes):
+    """Few-split sums (every segment <= 8 splits: the fc weight / bias gradient's 5) take the
+    one-column-per-thread launch."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    g = torch.Generator(device=cuda).manual_seed(1)
+    segs, refs = [], []
+    for s, n in shapes:
+        p = torch.randn(s * n, device=cuda, generator=g)
+        out = torch.full((n,), float("nan"), device=cuda)
+        segs.append((p, s, n, out))
+        refs.append(p.view(s, n).double().sum(0))
+    h.sum_splits_multi(segs)
+    for (_, s, n, out), ref in zip(segs, refs):
+        assert torch.allclose(out.double(), ref, atol=1e-5, rtol=1e-6), (s, n)
+
+
 def test_pong_step_render_fused_matches_separate(cuda):
     """One-launch step + render (a workgroup per env) == step kernel then render kernel, bitwise."""
     from relayrl_prototype_amd.ops import hip
