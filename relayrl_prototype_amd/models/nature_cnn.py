@@ -231,7 +231,9 @@ class DeviceNatureCNN:
         self.da1 = torch.empty(B * L1.hout ** 2 * L1.cout, dtype=bf, device=dev)
         self.dhead = torch.empty(B * (self.A + 1), dtype=torch.float32, device=dev)
         self.head_grid = max(1, min(1024, (B + 3) // 4))
-        self.stats = torch.empty(self.head_grid * 4, device=dev)
+        # backward head: rows per wave (RRL_HEAD_BWD_ROWS, for A/B runs; grid = B / (4 x rows))
+        self.head_bwd_rows = max(1, int(os.environ.get("RRL_HEAD_BWD_ROWS", "4")))
+        self.stats = torch.empty(max(self.head_grid, (B + 3) // 4) * 4, device=dev)
         self.head_blocks = max(1, min(256, (B + 31) // 32))
         self.head_part = torch.empty(self.head_blocks * spec.head_size, device=dev)
         # split-K plan for the weight gradients (enough workgroups to fill 256 CUs)
@@ -423,7 +425,8 @@ class DeviceNatureCNN:
         hid = self.hid[:B * HIDDEN]
         dh = self.dh[:B * HIDDEN]
         dhead = self.dhead[:B * (self.A + 1)]
-        grid = max(1, min(self.head_grid, (B + 15) // 16))  # ~4 rows per wave: the head weights load once per wave
+        r = self.head_bwd_rows  # ~4 rows per wave by default: the head weights load once per wave
+        grid = max(1, min(self.stats.numel() // 4, (B + 4 * r - 1) // (4 * r)))
         stats = self.stats[:grid * 4]
         h.a2c_head(1, hid, self.params[o["head"]:], B, self.A, None, None, None, None, 0, 0, 0, act, adv, ret,
                    1.0 / B, float(vf_coef), float(ent_coef), dh, dhead, stats, grid)
