@@ -593,7 +593,18 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[(16 * c + 4 * g + r) * 576 + (tap0 + t) * 64 + 16 * ct + i16] = wacc[c][t][r];
       }
-  bias_part[(size_t)blockIdx.x * kThreads + tid] = bsum;
+  // the bias partial folded over the 8 waves in LDS: 64 values per workgroup (the end-of-backward
+  // slab sum's bias segments had 8 x the splits and were its longest blocks)
+  __syncthreads();  // every wave is past its last LDS read of the image buffers
+  float* red = reinterpret_cast<float*>(smem);
+  red[tid] = bsum;
+  __syncthreads();
+  if (tid < 64) {
+    float sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) sb += red[w * 64 + tid];
+    bias_part[(size_t)blockIdx.x * 64 + tid] = sb;
+  }
 }
 
 extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
@@ -839,7 +850,18 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[(16 * c + 4 * g + r) * 512 + (tau0 + t) * 32 + 16 * cb + i16] = wacc[c][t][r];
-  bias_part[(size_t)blockIdx.x * kThreads + tid] = bsum;
+  // the bias partial folded over the 8 waves in LDS: 64 values per workgroup (the end-of-backward
+  // slab sum's bias segments had 8 x the splits and were its longest blocks)
+  __syncthreads();  // every wave is past its last LDS read of the image buffers
+  float* red = reinterpret_cast<float*>(smem);
+  red[tid] = bsum;
+  __syncthreads();
+  if (tid < 64) {
+    float sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) sb += red[w * 64 + tid];
+    bias_part[(size_t)blockIdx.x * 64 + tid] = sb;
+  }
 }
 
 // variant 1: da1 through the LDS staging tile (measured slower: 229 vs 214 us, tools/cnn_kbench.py

@@ -524,7 +524,7 @@ class DeviceNatureCNN:
             nblk = min(B, self.cus)
             h.conv3_bwd(da3, sh[o["w3"]:o["b3"]], a2, da2, self.cpart["c3"], self.cbias["c3"], B, nblk)
             sums = [(self.cpart["c3"], nblk, L3.cout * L3.K, g[o["w3"]:o["b3"]]),
-                    (self.cbias["c3"], nblk * 8, L3.cout, g[o["b3"]:o["b3"] + L3.cout])]
+                    (self.cbias["c3"], nblk, L3.cout, g[o["b3"]:o["b3"] + L3.cout])]
             if side_sums:  # conv3's slabs are final: summed on the side stream beside conv2 / conv1
                 fork_sums(sums, self._ev_c3, self._ev_c3_done)
                 sums = []
@@ -539,7 +539,7 @@ class DeviceNatureCNN:
             h.conv2_bwd(da2, sh[o["w2"]:o["b2"]], a1, da1, self.cpart["c2"], self.cbias["c2"], B, nblk,
                         staged=self.bwd2_variant)
             sums += [(self.cpart["c2"], nblk, L2.cout * L2.K, g[o["w2"]:o["b2"]]),
-                     (self.cbias["c2"], nblk * 8, L2.cout, g[o["b2"]:o["b2"] + L2.cout])]
+                     (self.cbias["c2"], nblk, L2.cout, g[o["b2"]:o["b2"] + L2.cout])]
             if side_sums:
                 fork_sums(sums, self._ev_c2, self._ev_c2_done)
                 sums = []
