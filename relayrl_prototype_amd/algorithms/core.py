@@ -15,6 +15,7 @@ import torch
 
 from ..ops import MLPSpec, GradHead, adam_step, mlp_grad, reduce_slabs, grad_slabs
 from ..parallel.comm import Comm
+from ..utils.tracing import gc_paused
 
 
 class FlatNet:
@@ -173,7 +174,7 @@ class ValueLoop:
                 dst.copy_(src)
             g = torch.cuda.CUDAGraph()
             # thread_local: a host rollout thread (host_trainer overlap) may issue HIP calls meanwhile
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            with gc_paused(), torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last, nvalid, inv_B_dev)
             self._graphs[gkey] = g
         g.replay()

@@ -29,6 +29,7 @@ import torch
 
 from ..ops import GradHead, MLPSpec, mlp_grad, grad_slabs
 from ..parallel.comm import Comm
+from ..utils.tracing import gc_paused
 from .core import FlatNet, ValueLoop
 
 
@@ -148,7 +149,7 @@ class PGLearner:
                 n.version = v
             g = torch.cuda.CUDAGraph()
             # thread_local: a host rollout thread (host_trainer overlap) may issue HIP calls meanwhile
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            with gc_paused(), torch.cuda.graph(g, capture_error_mode="thread_local"):
                 last = self._optimize_body(*args, inv_B=inv_B, vf_iters=self.train_vf_iters)
             dv = [n.version - v for n, v in zip(nets, v0)]
             for n, v in zip(nets, v0):

@@ -32,7 +32,7 @@ import torch
 
 from ..models.nature_cnn import CNNSpec, DeviceNatureCNN, a2c_loss, reference_forward
 from ..parallel.comm import Comm
-from ..utils.tracing import PhaseTimer
+from ..utils.tracing import PhaseTimer, gc_paused
 
 
 @dataclass
@@ -212,7 +212,7 @@ class PixelA2CTrainer:
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
-                    with torch.cuda.graph(g, stream=s):
+                    with gc_paused(), torch.cuda.graph(g, stream=s):
                         stats = self._gpu_update_body(par)
                 torch.cuda.current_stream().wait_stream(s)
                 self._graphs[par] = (g, stats)

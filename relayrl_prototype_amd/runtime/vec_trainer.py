@@ -221,6 +221,7 @@ class VecTrainer:
             return PendingSums(self.episode_sums())  # host collective: synchronous anyway
         if not hasattr(self, "_sum_slots"):
             self._sum_slots = [torch.empty(2, dtype=torch.float64, pin_memory=True) for _ in range(3)]
+            self._sum_events = [torch.cuda.Event() for _ in range(3)]  # reused: no event per epoch
             self._sum_k = 0
             self._sum_dev = torch.empty(2, dtype=torch.float64, device=self.device)
         ns = self._sum_dev
@@ -228,9 +229,9 @@ class VecTrainer:
         if self.comm.multi:
             self.comm.all_reduce_sum_(ns)
         slot = self._sum_slots[self._sum_k % 3]  # a handle is consumed before the slot comes round
+        ev = self._sum_events[self._sum_k % 3]
         self._sum_k += 1
         slot.copy_(ns, non_blocking=True)
-        ev = torch.cuda.Event()
         ev.record()
         return PendingSums(slot, ev)
 

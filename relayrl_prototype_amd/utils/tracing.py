@@ -162,3 +162,19 @@ def torch_profiler(path: str, cuda: bool = True):
     with torch.profiler.profile(activities=acts, record_shapes=False) as prof:
         yield prof
     prof.export_chrome_trace(path)
+
+
+@contextlib.contextmanager
+def gc_paused():
+    """No automatic garbage collection inside the block: a hipGraph capture must not run
+    finalizers that destroy HIP events / streams of unrelated, unreachable objects (a collection
+    triggered by an allocation inside the capture aborted a capture once)."""
+    import gc
+
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
