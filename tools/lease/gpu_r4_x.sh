@@ -1,4 +1,5 @@
 # Round 4: conv2-backward dgrad grid A/B inside the Pong update (RRL_CNN_BWD2_VARIANT 0 = 10 x 12
+# NOTE: ran against a .so whose rebuild had failed: variant 2 launched the staged-epilogue kernel (profiles/r4_bwd2_grid_ab.txt)
 # grid, 2 = 7 tiles), alternated 3x on one box; kernel times over 4 alternating-order rounds
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"

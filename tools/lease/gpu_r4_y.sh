@@ -1,4 +1,5 @@
 # Round 4: forward conv3-grid A/B inside the Pong update with per-variant LDS allocations
+# NOTE: ran against a .so whose rebuild had failed: there layout 0 was the 7 x 9 conv3 grid and 32 the 49-pixel conv3 (profiles/r4_fwd_layouts.txt)
 # (RRL_CNN_FWD_LAYOUT 0 = conv3 over its 49 pixels, 32 = over a 7 x 9 grid), alternated 3x
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
