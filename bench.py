@@ -87,6 +87,12 @@ def parse(argv=None):
     ap.add_argument("--pong-big-envs", type=int, default=8192,
                     help="1 GPU: also time the A2C Pong update at this many envs (the six rollout forwards are "
                          "latency-bound at 2048 frames per launch); 0 = skip")
+    ap.add_argument("--convergence", choices=("auto", "on", "off"), default="auto",
+                    help="1 GPU: wall-clock / env steps to the return thresholds of BASELINE configs #3-#5 "
+                         "(benchmarks/convergence_bench.py: A2C PongSynth, REINFORCE-with-baseline LunarLanderSynth, "
+                         "PPO HalfCheetahSynth); auto = on with one GPU")
+    ap.add_argument("--conv-seeds", type=int, default=3, help="seeds of each convergence preset (median reported)")
+    ap.add_argument("--conv-budget-s", type=float, default=30.0, help="wall-clock budget per convergence run")
     ap.add_argument("--al-steps", type=int, default=10)
     ap.add_argument("--al-warmup", type=int, default=5)
     ap.add_argument("--al-env", default="LunarLanderSynth-v0")
@@ -271,6 +277,49 @@ def pong_probe(steps: int, num_envs: int = 2048) -> dict:
         del tr
         torch.cuda.empty_cache()
     return rec
+
+
+def convergence_probe(seeds: int, budget_s: float) -> dict:
+    """BASELINE configs #3-#5 learn: per preset and seed, the wall-clock (from trainer
+    construction) and env steps at which the mean return of the newest >= 100 finished
+    episodes first reaches each threshold (benchmarks/convergence_bench.py); the median over
+    seeds per threshold (None if any seed missed it within the budget).  The full curves live
+    in profiles/ (convergence_bench.py --out)."""
+    import statistics
+
+    import torch
+
+    from benchmarks.convergence_bench import CONV, run
+
+    out = {}
+    for name in ("pong-a2c", "lunarlander-reinforce-baseline", "halfcheetah-ppo"):
+        runs = []
+        for seed in range(1, seeds + 1):
+            try:
+                r = run(name, {}, 0, budget_s, 10 ** 9, seed)
+            except Exception as e:  # noqa: BLE001 -- recorded; the headline still prints
+                runs.append({"error": f"{type(e).__name__}: {e}"[:300]})
+                continue
+            finally:
+                torch.cuda.empty_cache()
+            runs.append(r)
+        ok = [r for r in runs if "error" not in r]
+        rec = {"note": CONV[name]["note"], "seeds": seeds, "budget_s": budget_s,
+               "overrides": ok[0]["overrides"] if ok else None}
+        th = {}
+        for t in CONV[name]["thresholds"]:
+            hits = [r["thresholds"].get(str(t)) for r in ok]
+            done = len(hits) == seeds and all(h is not None for h in hits)
+            th[str(t)] = {"median_s": round(statistics.median(h["s"] for h in hits), 3) if done else None,
+                          "median_env_steps": int(statistics.median(h["env_steps"] for h in hits)) if done else None,
+                          "per_seed_s": [None if h is None else h["s"] for h in hits]}
+        rec["thresholds"] = th
+        rec["last_window_ret"] = [r["last_window_ret"] for r in ok]
+        errs = [r["error"] for r in runs if "error" in r]
+        if errs:
+            rec["errors"] = errs
+        out[name] = rec
+    return out
 
 
 # ---------------------------------------------------------------------- comm-phase observability
@@ -465,6 +514,10 @@ def main(argv=None):
     pong_rec = pong_probe(args.pong_steps) if (on_gpu and world == 1 and args.pong_steps > 0) else None
     pong_big = (pong_probe(args.pong_steps, args.pong_big_envs)
                 if (on_gpu and world == 1 and args.pong_steps > 0 and args.pong_big_envs > 0) else None)
+    conv = None
+    if on_gpu and (args.convergence == "on" or (args.convergence == "auto" and world == 1)):
+        conv = convergence_probe(args.conv_seeds, args.conv_budget_s)
+
     def record(al_rec, ttt=None, ttt_ref=None, ref_cpu=None, do_ttt=False):
         """The ONE JSON line (rank 0)."""
         algo = "REINFORCE" if args.no_baseline else "REINFORCE-with-baseline"
@@ -530,6 +583,10 @@ def main(argv=None):
             rec["pong_a2c"] = pong_rec
         if pong_big is not None:
             rec["pong_a2c_big"] = pong_big
+        if conv is not None:
+            rec["convergence"] = dict(conv, criterion="mean return of the newest >= 100 finished episodes >= "
+                                      "threshold, checked every epoch; clock from trainer construction",
+                                      data="synthetic device envs (docs/ENVS.md), random-init weights")
         if al_rec is not None:
             rec["actor_learner"] = al_rec
         if ref_cpu is not None:

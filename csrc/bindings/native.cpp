@@ -190,7 +190,23 @@ PYBIND11_MODULE(_native, m) {
         for (auto& p : s.peers()) l.append(py::bytes(p));
         return l;
       })
-      .def("num_connections", &zmtp::Socket::num_connections);
+      .def("num_connections", &zmtp::Socket::num_connections)
+      .def("num_threads", &zmtp::Socket::num_threads)
+      .def("set_inbox_limits", &zmtp::Socket::set_inbox_limits, py::arg("max_messages"), py::arg("max_bytes"))
+      .def("inbox_size", &zmtp::Socket::inbox_size)
+      .def("inbox_bytes", &zmtp::Socket::inbox_bytes)
+      .def("stats", [](zmtp::Socket& s) {
+        const zmtp::Stats st = s.stats();
+        py::dict d;
+        d["accepted"] = st.accepted;
+        d["handshakes"] = st.handshakes;
+        d["dropped"] = st.dropped;
+        d["bad_handshakes"] = st.bad_handshakes;
+        d["messages_in"] = st.messages_in;
+        d["bytes_in"] = st.bytes_in;
+        d["inbox_waits"] = st.inbox_waits;
+        return d;
+      });
 
   m.def("env_names", &env_names);
   m.def("env_constants", &env_constants);

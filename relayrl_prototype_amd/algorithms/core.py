@@ -15,6 +15,7 @@ import torch
 
 from ..ops import MLPSpec, GradHead, adam_step, mlp_grad, reduce_slabs, grad_slabs
 from ..parallel.comm import Comm
+from ..utils.faults import maybe_stall_at
 from ..utils.tracing import gc_paused
 
 
@@ -81,7 +82,9 @@ class ValueLoop:
         # gloo group issues host calls, which a graph cannot hold
         self.use_graph = use_graph and net.device.type == "cuda" and (comm is None or comm.graph_safe)
         self._graphs = {}
+        self._bufs = {}  # shape key -> (slab, loss_first, loss_last): captured graphs keep theirs
         self._key = None
+        self._slab = None
         self.loss_first = None
         self.loss_last = None
         # called before a graph capture starts: a trainer whose helper thread issues HIP calls
@@ -91,7 +94,10 @@ class ValueLoop:
 
     def _body(self, obs, ret, iters, inv_B, slab, ls_first, ls_last, nvalid=None, inv_B_dev=None):
         H = self.net.spec.H
+        hook = not torch.cuda.is_current_stream_capturing()
         for k in range(iters):
+            if hook:
+                maybe_stall_at("viter", k)
             ls = ls_first if k == 0 else ls_last
             mlp_grad(GradHead.VALUE_MSE, self.net.params, obs, 1, H, ret=ret, inv_B=inv_B, grad_slab=slab,
                      loss_slab=ls, nvalid=nvalid, inv_B_dev=inv_B_dev)
@@ -117,15 +123,30 @@ class ValueLoop:
         self.net.apply(g, self.comm)
 
     def prepare(self, B: int, iters: int, inv_B: float, dev) -> None:
-        """(Re)allocate the slab / loss buffers for this batch shape (before any capture)."""
+        """Select (allocating once per shape) the slab / loss buffers of this batch shape
+        (before any capture).  Buffers are never reallocated under a graph that uses them:
+        each shape keeps its own set, and every graph entry holds a reference to the set it
+        was captured with (a padded agent-row batch used to free the buffers of
+        the unpadded batch's graph)."""
         shape_key = (B, iters, float(inv_B))
         if self._key != shape_key:
-            ns = grad_slabs(B, dev)
-            self._slab = torch.empty(ns, self.net.P, device=dev)
-            self.loss_first = torch.zeros(ns, 8, device=dev)
-            self.loss_last = torch.zeros(ns, 8, device=dev)
-            self._graphs = {}
-            self._key = shape_key
+            bufs = self._bufs.get(shape_key)
+            if bufs is None:
+                if len(self._bufs) >= 8:
+                    self._bufs.clear()  # graphs still hold theirs
+                ns = grad_slabs(B, dev)
+                bufs = (torch.empty(ns, self.net.P, device=dev), torch.zeros(ns, 8, device=dev),
+                        torch.zeros(ns, 8, device=dev))
+                self._bufs[shape_key] = bufs
+            self.use_bufs(shape_key, bufs)
+
+    def use_bufs(self, shape_key, bufs) -> None:
+        self._key = shape_key
+        self._slab, self.loss_first, self.loss_last = bufs
+
+    @property
+    def bufs(self):
+        return self._key, (self._slab, self.loss_first, self.loss_last)
 
     def run_body(self, obs: torch.Tensor, ret: torch.Tensor, iters: int, inv_B: float, nvalid=None,
                  inv_B_dev=None):
@@ -141,6 +162,7 @@ class ValueLoop:
         if dev.type != "cuda":
             # CPU oracle path: autograd + torch Adam math
             for k in range(iters):
+                maybe_stall_at("viter", k)
                 g, ls = mlp_grad(GradHead.VALUE_MSE, self.net.params, obs, 1, self.net.spec.H, ret=ret, inv_B=inv_B,
                                  nvalid=nvalid, inv_B_dev=inv_B_dev)
                 if k == 0:
@@ -154,20 +176,22 @@ class ValueLoop:
             return
         v0 = self.net.version
         # one graph per input buffer set (double-buffered trainers, padded agent-row batches)
+        # and batch shape; the entry keeps the buffers it was captured with
         gkey = (obs.data_ptr(), ret.data_ptr(), 0 if nvalid is None else nvalid.data_ptr(),
-                0 if inv_B_dev is None else inv_B_dev.data_ptr())
-        g = self._graphs.get(gkey)
-        if g is None:
+                0 if inv_B_dev is None else inv_B_dev.data_ptr(), self._key)
+        ent = self._graphs.get(gkey)
+        if ent is None:
             if len(self._graphs) >= 4:
                 self._graphs.clear()
             if self.before_capture is not None:
                 self.before_capture()
-            # Warm up once eagerly (kernel attributes, allocator) on the real buffers,
-            # then restore the optimiser state so the warm-up step leaves no trace.
+            # Warm up once eagerly (kernel attributes, allocator) on the real buffers, with the
+            # collectives muted (rank-local, Comm.muted), then restore the optimiser state so
+            # the warm-up step leaves no trace.
             saved = [t.clone() for t in (self.net.params, self.net.m, self.net.v, self.net.step)]
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
+            with torch.cuda.stream(s), _muted(self.comm):
                 self._body(obs, ret, 1, inv_B, self._slab, self.loss_first, self.loss_last, nvalid, inv_B_dev)
             torch.cuda.current_stream().wait_stream(s)
             for dst, src in zip((self.net.params, self.net.m, self.net.v, self.net.step), saved):
@@ -176,6 +200,16 @@ class ValueLoop:
             # thread_local: a host rollout thread (host_trainer overlap) may issue HIP calls meanwhile
             with gc_paused(), torch.cuda.graph(g, capture_error_mode="thread_local"):
                 self._body(obs, ret, iters, inv_B, self._slab, self.loss_first, self.loss_last, nvalid, inv_B_dev)
-            self._graphs[gkey] = g
+            ent = (g, self.bufs)
+            self._graphs[gkey] = ent
+        g, (key, bufs) = ent
+        self.use_bufs(key, bufs)
         g.replay()
         self.net.version = v0 + iters
+
+
+def _muted(comm: Optional[Comm]):
+    """comm.muted() (no collectives), or a no-op context without a comm."""
+    import contextlib
+
+    return comm.muted() if comm is not None else contextlib.nullcontext()

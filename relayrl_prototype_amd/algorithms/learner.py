@@ -30,7 +30,7 @@ import torch
 from ..ops import GradHead, MLPSpec, mlp_grad, grad_slabs
 from ..parallel.comm import Comm
 from ..utils.tracing import gc_paused
-from .core import FlatNet, ValueLoop
+from .core import FlatNet, ValueLoop, _muted
 
 
 class PGLearner:
@@ -84,6 +84,7 @@ class PGLearner:
             return None, None
         ns = grad_slabs(B, self.device)
         if self._pi_slab is None or self._pi_slab.shape[0] < ns:
+            # (captured graphs keep the old slab alive through their entries)
             self._pi_slab = torch.empty(ns, self.pi.P, device=self.device)
             self._pi_loss = torch.empty(ns, 8, device=self.device)
         return self._pi_slab[:ns], self._pi_loss[:ns]
@@ -134,11 +135,15 @@ class PGLearner:
             nets = self._nets()
             v0 = [n.version for n in nets]
             state = [t.clone() for n in nets for t in (n.params, n.m, n.v, n.step)]
-            # warm up eagerly once on the real buffers (kernel attributes, allocator, RCCL
-            # communicator), then restore the optimiser state so the warm-up leaves no trace
+            # warm up eagerly once on the real buffers (kernel attributes, allocator), then
+            # restore the optimiser state so the warm-up leaves no trace.  The warm-up's
+            # collectives are muted (Comm.muted): whether this rank captures now is a rank-local
+            # decision (its own input buffers / agent rows / cache), so a real all-reduce here
+            # would pair with another rank's unrelated calls.  The RCCL communicator
+            # already exists: the statistics all-reduce of the same epoch ran before this.
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(s):
+            with torch.cuda.stream(s), _muted(self.comm):
                 self._optimize_body(*args, inv_B=inv_B, vf_iters=min(1, self.train_vf_iters))
             torch.cuda.current_stream(self.device).wait_stream(s)
             it = iter(state)
@@ -154,9 +159,15 @@ class PGLearner:
             dv = [n.version - v for n, v in zip(nets, v0)]
             for n, v in zip(nets, v0):
                 n.version = v
-            ent = (g, dict(last), dv)
+            # the entry holds every buffer the graph reads or writes: a later capture for another
+            # batch shape selects / grows other buffers, and these must not be freed (and reused
+            # by the caching allocator) under this graph
+            keep = (self._pi_slab, self._pi_loss, self.vloop.bufs if self.vloop is not None else None)
+            ent = (g, dict(last), dv, keep)
             self._opt_graphs[key] = ent
-        g, last, dv = ent
+        g, last, dv, keep = ent
+        if keep[2] is not None:
+            self.vloop.use_bufs(*keep[2])  # summarize() reads this graph's value-loss slabs
         g.replay()
         self.graph_replays += 1
         for n, d in zip(self._nets(), dv):
@@ -256,6 +267,18 @@ class PGLearner:
         if self.last.get("kl_stop") is not None:
             out["StopIter"] = self.last["kl_stop"]
         return out
+
+    def state_tensors(self):
+        """The live tensors that ARE this learner's state (parameters, Adam moments, device
+        step counters): the elastic epoch-start snapshot copies these on the device."""
+        return [t for n in self._nets() for t in (n.params, n.m, n.v, n.step)]
+
+    def drop_graphs(self):
+        """Forget every captured graph (after a process-group re-form their RCCL collectives
+        belong to a destroyed communicator and must never replay)."""
+        self._opt_graphs.clear()
+        if self.vloop is not None:
+            self.vloop._graphs.clear()
 
     def broadcast_state_(self, comm: Comm, src: int = 0):
         """Overwrite this learner's parameters and Adam state with rank ``src``'s (after an

@@ -116,10 +116,33 @@ class Comm:
         # ``multi``: the world > 1 code path (real collectives), also for a forced one-rank group
         self.forced = bool(self.enabled and self.world == 1 and collectives)
         self.multi = self.world > 1 or self.forced
+        # muted(): collectives become no-ops (same launches otherwise) -- for rank-local eager
+        # warm-ups before a graph capture, which other ranks may not run at the same time
+        self._muted = False
         # optional utils.tracing.PhaseTimer: every gradient / statistics all-reduce is timed as
         # the "AllReduce" phase (HIP events on the current stream bracket the RCCL call, which
         # the stream waits on); skipped while a hipGraph is being captured
         self.timer = None
+
+    def muted(self):
+        """Context manager: this comm's collectives do nothing inside it.  A graph capture is
+        preceded by one eager warm-up of the same body; the capture decision is rank-local
+        (a new input-buffer set on one rank, agent rows folded on rank 0 only, a per-rank
+        cache eviction), so a warm-up that issued real collectives would pair with another
+        rank's unrelated calls.  The captured body itself issues no collective until replay,
+        and every rank's graphs carry the same collective sequence (one gradient all-reduce
+        of P floats per optimiser step), whatever their batch shapes."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            prev, self._muted = self._muted, True
+            try:
+                yield self
+            finally:
+                self._muted = prev
+
+        return cm()
 
     @property
     def is_master(self) -> bool:
@@ -132,7 +155,7 @@ class Comm:
         return (not self.multi) or self.backend == "nccl"
 
     def all_reduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
-        if self.multi:
+        if self.multi and not self._muted:
             tm = self.timer
             if tm is not None and tm.enabled and not (t.is_cuda and torch.cuda.is_current_stream_capturing()):
                 with tm.phase("AllReduce"):
@@ -142,17 +165,17 @@ class Comm:
         return t
 
     def all_reduce_max_(self, t: torch.Tensor) -> torch.Tensor:
-        if self.multi:
+        if self.multi and not self._muted:
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return t
 
     def all_reduce_min_(self, t: torch.Tensor) -> torch.Tensor:
-        if self.multi:
+        if self.multi and not self._muted:
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
         return t
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
-        if self.multi:
+        if self.multi and not self._muted:
             dist.broadcast(t, src=src, group=self.group)
         return t
 

@@ -41,6 +41,7 @@ import torch.distributed as dist
 
 from ..algorithms.learner import PGLearner
 from ..parallel.comm import Comm, collective_timeout
+from ..utils.faults import maybe_stall_at
 from ..utils.tracing import PhaseTimer
 from .rollout_learn import RolloutLearner
 
@@ -152,6 +153,7 @@ class _Actor:
             self.eng = HostVecTrainer(hcfg, comm, device=self.device)
             self.params = self.eng.learner.pi.params
         self.need_tobs = need_tobs
+        self.verify = bool(cfg.verify_versions)
         self.seq = 0
         self.header = torch.zeros(HDR, dtype=torch.float64, device=self.device)
 
@@ -164,7 +166,9 @@ class _Actor:
         """-> (obs_train [T,N,D], obs_last [N,D], act, logp, rew, done, tobs|None, header[HDR])"""
         e = self.eng
         T = e.cfg.rollout_len
-        ck = weight_checksum(self.params)  # queued before the rollout: same weights it reads
+        # queued before the rollout: same weights it reads (only checked with verify_versions:
+        # otherwise no fp64 reduction per rollout)
+        ck = weight_checksum(self.params) if self.verify else None
         if self.kind == "device":
             e.rollout()
             e.epoch += 1
@@ -190,7 +194,8 @@ class _Actor:
         h[0] = float(self.seq)
         h[1:7].copy_(stats)
         h[7] = float(version)
-        h[8:10].copy_(ck)
+        if ck is not None:
+            h[8:10].copy_(ck)
         if self.need_tobs and tobs is None:
             tobs = torch.zeros_like(obs[:T])
         return (obs[:T], obs[T], act, logp, rew, done, tobs if self.need_tobs else None, h)
@@ -342,6 +347,7 @@ class ActorLearner:
 
     def _gather(self, parts):
         """Fan-in: own rollout -> slot 0 (device copy), remote actors -> their slots (P2P)."""
+        maybe_stall_at("gather")
         ops = []
         for k, a in enumerate(self.shard):
             dst = self._slot(k)
@@ -362,6 +368,7 @@ class ActorLearner:
             self._pending_peers = []
 
     def _send_rollout(self, parts):
+        maybe_stall_at("send")
         dst = self.topo.learner_of(self.rank)
         ops = [dist.P2POp(dist.isend, p.contiguous(), dst) for p in parts if p is not None]
         for w in dist.batch_isend_irecv(ops):
@@ -505,6 +512,23 @@ class ActorLearner:
         self.comm.broadcast_(vec, src)
         self.epoch, self.version = int(vec[0].item()), int(vec[1].item())
         self._front_version = self.version
+
+    # ------------------------------------------------------------------ elastic snapshot
+    def snapshot_tensors(self):
+        ts = self.learner.state_tensors() if self.learner is not None else []
+        if self.learner is None:
+            ts.append(self.front)
+        return ts
+
+    def counters(self) -> dict:
+        return {"epoch": self.epoch, "version": self.version, "received": self.received,
+                "_front_version": getattr(self, "_front_version", 0)}
+
+    def set_counters(self, c: dict):
+        self.epoch, self.version, self.received = int(c["epoch"]), int(c["version"]), int(c["received"])
+        self._front_version = int(c["_front_version"])
+        if self.learner is not None and self.actor is not None:
+            self.actor.params.copy_(self.learner.pi.params)
 
     # ------------------------------------------------------------------ checkpoint
     def state_dict(self) -> dict:

@@ -214,6 +214,31 @@ class EngineAlgorithm(AlgorithmAbstract):
             w["vf"] = lr.vf.params.detach().cpu().clone()
         return w
 
+    def weights_async(self):
+        """get_weights() without draining the stream: the parameters are copied into pinned
+        host slots behind the queued work (two slot sets, alternating) and ``result()`` waits
+        for that copy only -- rank 0 of a multi-rank engine publishes every epoch this way and
+        sends each snapshot one epoch later (run_engine_rank)."""
+        lr = self.learner
+        if lr is None or lr.pi.params.device.type != "cuda":
+            w = self.get_weights()
+            return _ReadyWeights(w)
+        if not hasattr(self, "_wslots"):
+            self._wslots = [{"pi": torch.empty(lr.pi.params.numel(), pin_memory=True),
+                             "vf": (torch.empty(lr.vf.params.numel(), pin_memory=True) if lr.vf is not None
+                                    else None), "ev": torch.cuda.Event()} for _ in range(2)]
+            self._wk = 0
+        sl = self._wslots[self._wk % 2]
+        self._wk += 1
+        sl["ev"].synchronize()  # the copy that last used this slot set (two snapshots ago)
+        sl["pi"].copy_(lr.pi.params.detach(), non_blocking=True)
+        if sl["vf"] is not None:
+            sl["vf"].copy_(lr.vf.params.detach(), non_blocking=True)
+        sl["ev"].record()
+        meta = {"version": self.version, "obs_dim": lr.obs_dim, "act_dim": lr.act_dim, "hidden": lr.hidden,
+                "discrete": lr.discrete, "epoch": self.epoch}
+        return _PendingWeights(sl, meta)
+
     def policy_module(self):
         from ..models.policies import build_policy_module
 
@@ -332,6 +357,26 @@ class EngineAlgorithm(AlgorithmAbstract):
         self.epoch, self.version = int(sd["epoch"]), int(sd["version"])
 
 
+class _ReadyWeights:
+    def __init__(self, w):
+        self.w = w
+
+    def result(self) -> Dict[str, Any]:
+        return self.w
+
+
+class _PendingWeights:
+    def __init__(self, slot, meta):
+        self.slot, self.meta = slot, meta
+
+    def result(self) -> Dict[str, Any]:
+        self.slot["ev"].synchronize()
+        w = dict(self.meta, pi=self.slot["pi"].clone())
+        if self.slot["vf"] is not None:
+            w["vf"] = self.slot["vf"].clone()
+        return w
+
+
 @dataclass
 class TrainResult:
     epochs: int
@@ -389,14 +434,20 @@ class EngineRunner:
             # episode sums are read after epoch k + 1 is queued, so the GPU never drains for
             # the check (~3 % of a reference-hyperparameter epoch, docs/ROUND4.md); the clock
             # stops when the solved epoch's sums reach the host, as before
-            lag = (check is not None and not log_every and hasattr(algo, "episode_sums_async")
+            # (only trainers with a non-draining read: the others' sums are synchronous anyway,
+            # and the lag would only run one extra epoch past the threshold -- ADVICE r4)
+            lag = (check is not None and not log_every and hasattr(algo.trainer, "episode_sums_async")
                    and os.environ.get("RRL_TTT_LAGGED_CHECK", "1") != "0")
             pending = None
+            # several ranks: the stop request (STOP reaches rank 0 only) and the wall-clock
+            # limit are agreed through a device flag, all-reduced behind each epoch and read one
+            # epoch later -- the same decision on every rank at the same epoch, and no stream
+            # drain per epoch (the old form was an all-reduce + .item() at the
+            # top of every epoch)
+            multi = comm is not None and comm.multi
+            agree = LaggedFlag(comm) if (multi and (self.agree_stop or max_seconds is not None)) else None
             while True:
-                if self.agree_stop:
-                    if _agree(comm, self._stop.is_set()):
-                        break
-                elif self._stop.is_set():
+                if agree is None and self._stop.is_set():
                     break
                 algo.train_model()
                 k = algo.epoch - e0
@@ -433,7 +484,11 @@ class EngineRunner:
                     break
                 if epochs is not None and k >= epochs:
                     break
-                if max_seconds is not None and _agree(comm, time.perf_counter() - t0 >= max_seconds):
+                if agree is not None:
+                    timeout = max_seconds is not None and time.perf_counter() - t0 >= max_seconds
+                    if agree.post(self._stop.is_set() or timeout):
+                        break
+                elif max_seconds is not None and time.perf_counter() - t0 >= max_seconds:
                     break
             if pending is not None and not solved:  # the last epoch's sums, still unread
                 win = check.update(*pending.result())
@@ -463,14 +518,40 @@ class EngineRunner:
         return self.result
 
 
-def _agree(comm, flag: bool) -> bool:
-    """True on every rank if it is true on any (wall-clock stops must not split the ranks)."""
-    if comm is None or not comm.multi:
-        return flag
-    dev = "cuda" if comm.backend == "nccl" else "cpu"
-    t = torch.tensor([1.0 if flag else 0.0], device=dev)
-    comm.all_reduce_max_(t)
-    return bool(t.item() > 0)
+class LaggedFlag:
+    """A boolean the ranks agree on (true on every rank if it was true on any), decided one
+    epoch late without draining the stream: ``post(flag)`` writes this epoch's local flag into
+    a device scalar, all-reduces it (MAX) on the stream behind the epoch and copies the result
+    into a pinned slot with an event; it returns the agreed flag of the PREVIOUS post, waiting
+    only for that older event (the epoch just queued keeps the GPU busy meanwhile).  Every
+    rank posts once per epoch, so every rank sees the same sequence of agreed values.  A gloo
+    group all-reduces on the host (synchronous, nothing to overlap)."""
+
+    def __init__(self, comm):
+        self.comm = comm
+        self.on_dev = comm.backend == "nccl" and torch.cuda.is_available()
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.on_dev else torch.device("cpu")
+        self.flag = torch.zeros(1, device=dev)
+        self.slots = [torch.zeros(1, pin_memory=self.on_dev) for _ in range(2)]
+        self.events = [torch.cuda.Event() for _ in range(2)] if self.on_dev else None
+        self.k = 0
+        self.posts = 0
+
+    def post(self, flag: bool) -> bool:
+        self.flag.fill_(1.0 if flag else 0.0)
+        self.comm.all_reduce_max_(self.flag)
+        i = self.k % 2
+        self.k += 1
+        self.posts += 1
+        if not self.on_dev:
+            return bool(self.flag[0] > 0)
+        self.slots[i].copy_(self.flag, non_blocking=True)
+        self.events[i].record()
+        if self.k == 1:
+            return False
+        j = 1 - i
+        self.events[j].synchronize()
+        return bool(self.slots[j][0] > 0)
 
 
 # ---------------------------------------------------------------------- multi-rank (child ranks)
@@ -601,6 +682,7 @@ class MultiRankEngineRunner:
             argv += ["--target-return", str(target_return)]
         if max_seconds is not None:
             argv += ["--max-seconds", str(max_seconds)]
+        self.algo.relay.reset_control()  # no stale STOP / upload port of a previous run
         rc = spawn_ranks(argv, self.algo.spec.world_size)
         if rc != 0:
             raise RuntimeError(f"engine ranks exited with code {rc}")
@@ -655,28 +737,45 @@ def run_engine_rank(spec: EngineSpec, env_dir: str, epochs: Optional[int], targe
     algo.version = int(version0)
     relay = None
 
-    class _Pub:  # rank 0 sends every new policy to the API process from memory
+    class _Pub:
+        """Rank 0 sends every new policy to the API process from memory.  The snapshot is an
+        asynchronous copy into pinned memory (EngineAlgorithm.weights_async) and goes out at
+        the NEXT publish, once the copy is done: no stream drain per published epoch; flush()
+        sends the last one."""
         updates = 0
+        pending = None
 
         def publish_model(self):
             if relay is not None and algo.publishes_policy:
-                from .model_store import ModelBlob
+                prev, self.pending = self.pending, algo.weights_async()
+                if prev is not None:
+                    self._send(prev.result())
 
-                w = algo.get_weights()
-                meta = {k: w[k] for k in ("obs_dim", "act_dim", "hidden", "discrete")}
-                meta["epoch"] = algo.epoch
-                relay.send_model(ModelBlob(int(w["version"]), meta, w["pi"].numpy(),
-                                           None if w.get("vf") is None else w["vf"].numpy()))
+        def flush(self):
+            if self.pending is not None:
+                self._send(self.pending.result())
+                self.pending = None
+
+        @staticmethod
+        def _send(w):
+            from .model_store import ModelBlob
+
+            meta = {k: w[k] for k in ("obs_dim", "act_dim", "hidden", "discrete")}
+            meta["epoch"] = w.get("epoch", algo.epoch)
+            relay.send_model(ModelBlob(int(w["version"]), meta, w["pi"].numpy(),
+                                       None if w.get("vf") is None else w["vf"].numpy()))
 
     # the clock of the threshold metric starts where the API object was built (parent process)
     t_start = time.perf_counter() - (time.time() - t_start_wall) if t_start_wall else time.perf_counter()
-    r = EngineRunner(algo, _Pub(), t_start)
+    pub = _Pub()
+    r = EngineRunner(algo, pub, t_start)
     if relay_up is not None and comm.rank == 0:
         from .engine_relay import RankRelay
 
         relay = RankRelay(relay_up, relay_down, algo.receive_trajectory, r.stop)
     r.agree_stop = relay_up is not None and comm.multi  # STOP reaches rank 0 only
     res = r.train(epochs, target_return, window, max_seconds, log_every, publish_every)
+    pub.flush()  # the last snapshot (the final version the API process waits for)
     if algo.rank == 0 and result_path:
         tmp = result_path + ".tmp"
         with open(tmp, "w") as f:

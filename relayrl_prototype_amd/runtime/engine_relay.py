@@ -12,8 +12,11 @@ reference's defining loop across the process boundary:
   models    rank 0, every ``publish_every`` epochs -> ``MODEL`` frame (RRLM flat weights, from
             rank 0's memory) over a local ZMTP PUSH -> the API process's PULL -> ModelStore ->
             every attached agent (training_zmq.rs:876-934 -> agent_zmq.rs:625-698)
-  control   ``STOP`` (background training stopped) API -> rank 0; the ranks agree on it with
-            one all-reduce per epoch (EngineRunner.agree_stop)
+  control   ``HELLO <port>`` rank 0 -> API: rank 0 binds its upload PULL on a free port (no
+            port picked, closed and re-bound across processes) and reports it; the API
+            process then connects its upload PUSH.  ``STOP`` (background training stopped)
+            API -> rank 0, sent ahead of any queued upload; the ranks agree on it through the
+            per-epoch all-reduce the engine already runs (EngineRunner.agree_stop)
 
 Nothing on the weight path touches a file (files are checkpoint-only).  Both
 links are 127.0.0.1 TCP through the C++ ZMTP sockets (csrc/host/zmtp.cpp): connect is
@@ -24,6 +27,7 @@ from __future__ import annotations
 
 import queue
 import threading
+import time
 from typing import Callable, Optional
 
 from .. import _native
@@ -33,23 +37,13 @@ from ..types import RelayRLTrajectory, TrajectoryColumns
 TRAJ = b"TRAJ"
 MODEL = b"MODEL"
 STOP = b"STOP"
-
-
-def _free_port() -> int:
-    import socket
-
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+HELLO = b"HELLO"
 
 
 def encode_upload(traj) -> bytes:
-    """An upload as one frame: columnar RRLC, or per-action RRLT (incl. reference frames
-    already decoded to actions, terminal markers kept)."""
-    if isinstance(traj, TrajectoryColumns):
-        return traj.encode()
+    """An upload as one frame: columnar RRLC (TrajectoryColumns), or per-action RRLT
+    (RelayRLTrajectory, incl. reference frames already decoded to actions, terminal markers
+    kept) -- both types encode themselves."""
     return traj.encode()
 
 
@@ -60,16 +54,17 @@ def decode_upload(buf: bytes):
 
 
 class ApiRelay:
-    """API-process side: PUSH uploads / control to rank 0, PULL models from rank 0."""
+    """API-process side: PUSH uploads / control to rank 0, PULL models (and rank 0's HELLO)."""
 
     def __init__(self, max_backlog: int = 65536):
         self.down = _native.ZmtpSocket(_native.SockType.PULL)
         self.down_port = self.down.bind("tcp://127.0.0.1:0")
-        self.up_port = _free_port()  # rank 0 binds its PULL here
-        self.up = _native.ZmtpSocket(_native.SockType.PUSH)
-        self.up.connect(f"tcp://127.0.0.1:{self.up_port}")
+        self.up = None  # connected when rank 0 reports its upload port (HELLO)
+        self.up_port = None
+        self._up_lock = threading.Lock()
         self._q: "queue.Queue" = queue.Queue(maxsize=max_backlog)
         self._stop = threading.Event()
+        self._stop_req = threading.Event()  # a STOP to deliver ahead of the queued uploads
         self.forwarded = 0
         self.dropped = 0
         self.models = 0
@@ -80,7 +75,7 @@ class ApiRelay:
             t.start()
 
     def argv(self):
-        return ["--relay-up", str(self.up_port), "--relay-down", str(self.down_port)]
+        return ["--relay-up", "0", "--relay-down", str(self.down_port)]
 
     def on_model(self, fn: Callable[[ModelBlob], None]) -> None:
         self._on_model = fn
@@ -94,20 +89,53 @@ class ApiRelay:
             return False
 
     def send_stop(self) -> None:
-        self._q.put([STOP])
+        """Never blocks: a flag the send loop serves before any queued upload."""
+        self._stop_req.set()
+
+    def reset_control(self) -> None:
+        """Before a new train(): a STOP meant for the previous run must not end this one, and
+        the previous ranks' upload port is gone."""
+        self._stop_req.clear()
+        with self._up_lock:
+            if self.up is not None:
+                self.up.close()
+            self.up, self.up_port = None, None
+
+    def _connect_up(self, port: int) -> None:
+        with self._up_lock:
+            if self.up_port == port:
+                return
+            if self.up is not None:
+                self.up.close()
+            self.up = _native.ZmtpSocket(_native.SockType.PUSH)
+            self.up.connect(f"tcp://127.0.0.1:{port}")
+            self.up_port = port
+
+    def _send(self, frames) -> bool:
+        with self._up_lock:
+            up = self.up
+        return up is not None and up.send(frames, 200)
 
     def _send_loop(self):
+        pending = None
         while not self._stop.is_set():
-            try:
-                frames = self._q.get(timeout=0.1)
-            except queue.Empty:
+            if self._stop_req.is_set():
+                if self._send([STOP]):
+                    self._stop_req.clear()
+                else:
+                    time.sleep(0.01)  # rank 0 not up (yet / any more)
                 continue
-            # blocks until rank 0's PULL is up (the ranks may still be starting)
-            while not self._stop.is_set():
-                if self.up.send(frames, 200):
-                    if frames[0] == TRAJ:
-                        self.forwarded += 1
-                    break
+            if pending is None:
+                try:
+                    pending = self._q.get(timeout=0.05)
+                except queue.Empty:
+                    continue
+            # waits (in 200 ms slices, STOP first) until rank 0's PULL is up
+            if self._send(pending):
+                self.forwarded += 1
+                pending = None
+            elif self.up is None:
+                time.sleep(0.01)
 
     def _recv_loop(self):
         while not self._stop.is_set():
@@ -115,7 +143,12 @@ class ApiRelay:
             if msg is None:
                 continue
             frames = msg[1]
-            if len(frames) >= 2 and frames[0] == MODEL:
+            if len(frames) >= 2 and frames[0] == HELLO:
+                try:
+                    self._connect_up(int(bytes(frames[1]).decode()))
+                except ValueError:
+                    continue
+            elif len(frames) >= 2 and frames[0] == MODEL:
                 try:
                     blob = ModelBlob.decode(frames[1])
                 except ValueError:
@@ -128,7 +161,9 @@ class ApiRelay:
         self._stop.set()
         for t in self._threads:
             t.join(timeout=5)
-        self.up.close()
+        with self._up_lock:
+            if self.up is not None:
+                self.up.close()
         self.down.close()
 
 
@@ -136,10 +171,13 @@ class RankRelay:
     """Rank-0 side: PULL uploads / control from the API process, PUSH models to it."""
 
     def __init__(self, up_port: int, down_port: int, on_upload: Callable, on_stop: Callable[[], None]):
+        """``up_port`` 0: bind a free port and report it to the API process (HELLO)."""
         self.pull = _native.ZmtpSocket(_native.SockType.PULL)
-        self.pull.bind(f"tcp://127.0.0.1:{int(up_port)}")
+        self.port = self.pull.bind(f"tcp://127.0.0.1:{int(up_port or 0)}")
         self.push = _native.ZmtpSocket(_native.SockType.PUSH)
         self.push.connect(f"tcp://127.0.0.1:{int(down_port)}")
+        if not self.push.send([HELLO, str(self.port).encode()], 30000):
+            raise RuntimeError("engine relay: the API process did not accept rank 0's HELLO")
         self.on_upload = on_upload
         self.on_stop = on_stop
         self.received = 0

@@ -438,6 +438,19 @@ class HostVecTrainer:
         if self._pending is not None:
             self._join_ahead()
 
+    # elastic epoch-start snapshot (launcher.EpochSnapshot): device tensors + host counters
+    def snapshot_tensors(self):
+        return self.learner.state_tensors()
+
+    def counters(self) -> dict:
+        return {"epoch": self.epoch, "env_steps": self.env_steps, "global_step": self.global_step}
+
+    def set_counters(self, c: dict):
+        self.finish()
+        self.epoch, self.env_steps, self.global_step = int(c["epoch"]), int(c["env_steps"]), int(c["global_step"])
+        if self.overlap:
+            self.actor_params.copy_(self.learner.pi.params)
+
     def state_dict(self) -> dict:
         """Learner state + counters.  The C++ env threads' states are not exported: a resumed
         host trainer starts fresh episodes (its env seeds advance with the epoch)."""

@@ -105,6 +105,53 @@ def _filter(cls, kw: Dict) -> Dict:
     return {k: v for k, v in kw.items() if k in names}
 
 
+class EpochSnapshot:
+    """The trainer's state at the START of the running epoch, kept on the device (elastic
+    mode): learner parameters, Adam moments and step counters (+ device env state where the
+    trainer has it) copied into preallocated buffers on the stream -- no host sync per epoch
+    -- and the host counters.  A failure inside an epoch can leave k of its updates applied
+    (a fault in the value loop's 40th all-reduce leaves 39 value steps and the policy step);
+    the survivors restore this snapshot before they re-form, so the retried epoch starts
+    from a consistent state, not from ``state_dict()`` of the broken
+    trainer."""
+
+    def __init__(self):
+        self.bufs = None
+        self.counters = None
+
+    def take(self, tr) -> None:
+        if not hasattr(tr, "snapshot_tensors"):
+            return
+        ts = tr.snapshot_tensors()
+        if self.bufs is None or len(self.bufs) != len(ts) or any(
+                b.shape != t.shape or b.device != t.device for b, t in zip(self.bufs, ts)):
+            self.bufs = [t.detach().clone() for t in ts]
+        else:
+            for b, t in zip(self.bufs, ts):
+                b.copy_(t.detach())
+        self.counters = dict(tr.counters())
+
+    @property
+    def taken(self) -> bool:
+        return self.counters is not None
+
+    def restore(self, tr) -> None:
+        import torch
+
+        with torch.no_grad():
+            for t, b in zip(tr.snapshot_tensors(), self.bufs):
+                t.copy_(b)
+        tr.set_counters(self.counters)
+
+
+def _drop_graphs(tr) -> None:
+    """Forget the captured graphs of a trainer whose process group broke: they hold RCCL
+    collectives of the destroyed communicator."""
+    for obj in (tr, getattr(tr, "learner", None)):
+        if obj is not None and hasattr(obj, "drop_graphs"):
+            obj.drop_graphs()
+
+
 def _epoch(tr):
     if hasattr(tr, "train_epoch"):
         return tr.train_epoch()
@@ -217,11 +264,18 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
     last: Dict = {}
     from ..utils.faults import maybe_kill_rank, maybe_stall_rank
 
+    from ..utils.faults import set_context
+
     completed = False
+    snap = EpochSnapshot() if eg is not None else None
+    dump = os.environ.get("RRL_ELASTIC_DUMP") if eg is not None else None
     try:
         ep = start + 1
         while ep <= epochs:
             try:
+                set_context(orig_rank if eg is not None else comm.rank, ep, out_dir)
+                if snap is not None:
+                    snap.take(tr)
                 maybe_stall_rank(orig_rank if eg is not None else comm.rank, ep, out_dir)
                 _epoch(tr)
                 m = tr.metrics() if (ep % log_every == 0 or ep == epochs) else None
@@ -230,9 +284,22 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
                     raise
                 from ..parallel.elastic import Evicted
 
-                sd = tr.state_dict()
                 if hasattr(tr, "watchdog"):
                     tr.watchdog.close()
+                if hasattr(tr, "finish") and not hasattr(tr, "watchdog"):
+                    # a host trainer's rollout thread running ahead (its own envs, no peers)
+                    try:
+                        tr.finish()
+                    except Exception:  # noqa: BLE001
+                        pass
+                if dump:
+                    _dump_state(dump, f"failed_r{orig_rank}.pt", tr)
+                # the epoch-start state, not the broken trainer's: the failed epoch may have
+                # applied part of its updates before the collective that failed
+                if snap is not None and snap.taken:
+                    snap.restore(tr)
+                sd = tr.state_dict()
+                _drop_graphs(tr)
                 # CU-masked streams / grid limit of the old trainer (host_trainer.close); no
                 # finish(): that would wait on transfers of the broken group
                 _release(tr, finish=False)
@@ -244,6 +311,14 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
                     return {"Evicted": True, "Epoch": ep - 1}
                 if getattr(comm, "unchanged", False):
                     raise  # every rank is alive: not a lost peer
+                if dump:
+                    # the restored snapshot as a resumable checkpoint under the NEW rank: a
+                    # fault-free run of the shrunken group resumed from it must end the retried
+                    # epoch with the same weights (tests/test_elastic.py)
+                    from ..utils.checkpoint import save_checkpoint
+
+                    save_checkpoint(ckpt_dir(dump, name, comm.rank), {"trainer": sd, "epoch": ep - 1,
+                                                                      "world": comm.world, "rank": comm.rank})
                 print(f"[elastic] rank {orig_rank}: re-formed without the lost rank(s) after {type(e).__name__}; "
                       f"world {comm.world}, rank {comm.rank}, retrying epoch {ep}", flush=True)
                 ov = dict(overrides)
@@ -300,6 +375,15 @@ def run_preset(name: str, epochs: int, out_dir: str = "runs", overrides: Optiona
         last["FinalWorld"] = comm.world
         eg.close()
     return last
+
+
+def _dump_state(d: str, fname: str, tr) -> None:
+    """Test hook (RRL_ELASTIC_DUMP): the broken trainer's learner state as it failed."""
+    import torch
+
+    os.makedirs(d, exist_ok=True)
+    sd = tr.state_dict()
+    torch.save(sd.get("learner", sd), os.path.join(d, fname))
 
 
 def _release(tr, finish: bool = True) -> None:

@@ -247,6 +247,30 @@ class PixelA2CTrainer:
                "Entropy": st[2] / cnt}
         return out
 
+    # elastic epoch-start snapshot (launcher.EpochSnapshot): device tensors + host counters
+    def snapshot_tensors(self):
+        if not self.on_gpu:
+            ts = [self.params.data]
+            for st in self.opt.state.values():
+                ts += [v for v in st.values() if torch.is_tensor(v)]
+            return ts
+        m = self.model
+        return [m.params, m.m, m.v, m.step_t, self.env.state, self.env.step_t, self.env.ep_acc, self.sample_t,
+                self.obs[0]]
+
+    def counters(self) -> dict:
+        return {"updates": self.updates, "total_steps": self.total_steps}
+
+    def set_counters(self, c: dict):
+        self.updates, self.total_steps = int(c["updates"]), int(c["total_steps"])
+        if self.on_gpu:
+            self.model.refresh_shadow()
+
+    def drop_graphs(self):
+        if self.on_gpu:
+            self._graphs.clear()
+            self._graph = None
+
     def state_dict(self) -> dict:
         st = {"updates": self.updates, "total_steps": self.total_steps, "obs0": self.obs[0].cpu(),
               "cfg": self.cfg.to_dict()}
@@ -291,7 +315,21 @@ class PixelA2CTrainer:
                     if torch.is_tensor(v):
                         self.comm.broadcast_(v, src)
 
+    def episode_sums(self) -> tuple:
+        """(finished episodes, sum of their returns) since the previous call, global over
+        ranks: the windowed threshold check (vec_trainer.SolvedCheck) needs the newest
+        episodes, not metrics()' running mean since the start.  One synchronising read."""
+        tot = (self.env.episode_stats() if self.on_gpu else self.ep_sum.clone())[:2].double()
+        if self.comm.multi:
+            tot = tot if (self.comm.backend == "nccl" or not tot.is_cuda) else tot.cpu()
+            self.comm.all_reduce_sum_(tot)
+        n, s = tot.tolist()
+        n0, s0 = getattr(self, "_sums_seen", (0.0, 0.0))
+        self._sums_seen = (n, s)
+        return n - n0, s - s0
+
     def reset_episode_stats(self):
         self.ep_sum.zero_()
+        self._sums_seen = (0.0, 0.0)
         if self.on_gpu:
             self.env.ep_acc.zero_()

@@ -247,6 +247,16 @@ class VecTrainer:
         if self.comm.multi:
             self.learner.broadcast_state_(self.comm, src)
 
+    # elastic epoch-start snapshot (launcher.EpochSnapshot): device tensors + host counters
+    def snapshot_tensors(self):
+        return self.learner.state_tensors() + [self.state, self.ep_len, self.ep_ret]
+
+    def counters(self) -> dict:
+        return {"epoch": self.epoch, "env_steps": self.env_steps, "_first": self._first}
+
+    def set_counters(self, c: dict):
+        self.epoch, self.env_steps, self._first = int(c["epoch"]), int(c["env_steps"]), bool(c["_first"])
+
     def state_dict(self) -> dict:
         return {"learner": self.learner.state_dict(), "epoch": self.epoch, "env_steps": self.env_steps,
                 "env_state": self.state.cpu(), "ep_len": self.ep_len.cpu(), "ep_ret": self.ep_ret.cpu(),

@@ -20,6 +20,12 @@ Process-level faults for the elastic-restart path (runtime/launcher.py):
     RRL_FAULT_STALL="2:2:60" -- rank 2 hangs for 60 s before epoch 2 (a stuck actor), once
                               per run directory: its peers' step watchdogs
                               (utils/watchdog.py) exit them, torchrun restarts the group.
+    RRL_FAULT_STALL_AT="2:3:viter:40:60" -- rank 2 hangs for 60 s at a named site INSIDE
+                              epoch 3, once per run directory: ``viter`` = before the 40th
+                              value-loop update (its all-reduce), ``gather`` = a learner before
+                              receiving its shard, ``send`` = an actor before sending its
+                              rollout.  The peers fail mid-epoch, with part of the epoch's
+                              updates applied (the elastic epoch-start snapshot's test case).
 """
 from __future__ import annotations
 
@@ -117,3 +123,37 @@ def maybe_stall_rank(rank: int, epoch: int, run_dir: str) -> None:
     open(marker, "w").close()
     print(f"[faults] injected stall of rank {rank} before epoch {epoch} ({sec} s)", flush=True)
     time.sleep(float(sec))
+
+
+_CTX = {"rank": -1, "epoch": -1, "run_dir": "."}
+_AT = None  # parsed RRL_FAULT_STALL_AT, or False when unset
+
+
+def set_context(rank: int, epoch: int, run_dir: str) -> None:
+    """The launcher's (original) rank, the epoch about to run and the run directory: the
+    coordinates of the mid-epoch stall sites (maybe_stall_at)."""
+    _CTX.update(rank=int(rank), epoch=int(epoch), run_dir=run_dir)
+
+
+def maybe_stall_at(site: str, index: int = 0) -> None:
+    """Hang once if RRL_FAULT_STALL_AT names (this rank, the current epoch, ``site``, ``index``)."""
+    global _AT
+    if _AT is None:
+        spec = os.environ.get("RRL_FAULT_STALL_AT", "")
+        if spec:
+            r, e, st, i, sec = spec.split(":")
+            _AT = (int(r), int(e), st, int(i), float(sec))
+        else:
+            _AT = False
+    if not _AT:
+        return
+    r, e, st, i, sec = _AT
+    if (r, e, st, i) != (_CTX["rank"], _CTX["epoch"], site, int(index)):
+        return
+    marker = os.path.join(_CTX["run_dir"], f".stall_at_fired_r{r}_e{e}_{st}{i}")
+    if os.path.exists(marker):
+        return
+    os.makedirs(_CTX["run_dir"], exist_ok=True)
+    open(marker, "w").close()
+    print(f"[faults] injected stall of rank {r} in epoch {e} at {st}[{i}] ({sec} s)", flush=True)
+    time.sleep(sec)

@@ -89,3 +89,65 @@ def test_elastic_actor_learner_continues_without_stalled_actor(tmp_path):
     assert m["FinalWorld"] == 3 and m["ElasticReforms"] == 1 and m["Epoch"] == 5, m
     # 3 actors do not split over 2 learner shards: the rebuilt topology fits 1 learner
     assert m["WorldSize"] == 3 and m["LearnerRanks"] == 1
+
+
+def _train(tmp, out, gpus, epochs, extra_env, extra_args, sets):
+    env = dict(os.environ, PYTHONPATH=REPO, RRL_QUIET_CONFIG="1", OMP_NUM_THREADS="1", RRL_COLLECTIVE_TIMEOUT_S="10",
+               **extra_env)
+    cmd = [sys.executable, "-m", "relayrl_prototype_amd", "train", "--preset", "lunarlander-reinforce-baseline",
+           "--gpus", str(gpus), "--epochs", str(epochs), "--out", str(out), "--checkpoint-every", "1"] + extra_args + \
+          ["--set"] + sets
+    return subprocess.run(cmd, cwd=str(tmp), env=env, capture_output=True, text=True, timeout=280)
+
+
+def _learner(out, rank):
+    from relayrl_prototype_amd.utils.checkpoint import load_checkpoint
+
+    st = load_checkpoint(os.path.join(str(out), f"lunarlander-reinforce-baseline_ckpt_r{rank}"))
+    return st["epoch"], st["trainer"]["learner"]
+
+
+def _assert_same_learner(a, b):
+    for net in ("pi", "vf"):
+        for k in ("params", "m", "v", "step"):
+            assert torch.equal(a[net][k], b[net][k]), (net, k, (a[net][k] - b[net][k]).abs().max())
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("site", ["gather", "viter"])
+def test_elastic_retry_restores_the_epoch_start_state(tmp_path, site):
+    """a rank stalls INSIDE epoch 3 -- (gather) an actor-only rank before
+    sending its rollout, so the learner fails in its gather; (viter) a learner before its 40th
+    value-loop update, so the other learners fail in that update's all-reduce with the policy
+    step and 39 value steps already applied.  The survivors restore the epoch-start snapshot
+    (launcher.EpochSnapshot), re-form and retry epoch 3; their weights and Adam state after it
+    must EQUAL a fault-free run of the shrunken group resumed from that same snapshot."""
+    sets = ["num_envs=4", "rollout_len=8", "num_threads=1", "train_vf_iters=80"]
+    if site == "gather":
+        stall, sets = "2:3:send:0:45", sets + ["learner_ranks=1"]  # rank 0 learns, ranks 1-2 act
+    else:
+        stall, sets = "2:3:viter:40:45", sets + ["learner_ranks=0"]  # every rank learns its own rollout
+    out, dump, ref = tmp_path / "run", tmp_path / "dump", tmp_path / "ref"
+    r = _train(tmp_path, out, 3, 3, {"RRL_FAULT_STALL_AT": stall, "RRL_ELASTIC_DUMP": str(dump)}, ["--elastic"], sets)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert "re-formed without the lost rank" in r.stdout, r.stdout[-3000:]
+    for k in (0, 1):
+        assert (dump / f"lunarlander-reinforce-baseline_ckpt_r{k}").exists()
+    snap_ep, snap = _learner(dump, 0)
+    assert snap_ep == 2
+    failed = torch.load(dump / "failed_r0.pt", weights_only=True)
+    if site == "viter":
+        # the survivors had applied part of epoch 3 before the all-reduce failed
+        assert not torch.equal(failed["vf"]["params"], snap["vf"]["params"])
+        assert int(failed["vf"]["step"]) == int(snap["vf"]["step"]) + 40
+    # the fault-free reference: 2 ranks resumed from the snapshot the survivors restored
+    import shutil
+
+    shutil.copytree(dump, ref, ignore=shutil.ignore_patterns("*.pt"))
+    r2 = _train(tmp_path, ref, 2, 3, {}, ["--auto-resume"], sets)
+    assert r2.returncode == 0, (r2.stdout[-3000:], r2.stderr[-3000:])
+    for k in (0, 1) if site == "viter" else (0,):
+        e_a, a = _learner(out, k)
+        e_b, b = _learner(ref, k)
+        assert e_a == e_b == 3
+        _assert_same_learner(a, b)

@@ -23,10 +23,12 @@ class _Algo:
     publishes_policy = False
     comm = None
 
-    def __init__(self, per_epoch):
+    def __init__(self, per_epoch, async_trainer=True):
         self.per_epoch = per_epoch  # (episodes, return sum) of each epoch
         self.epoch = 0
         self.trainer = _Trainer()
+        if async_trainer:  # like VecTrainer: a non-draining read exists
+            self.trainer.episode_sums_async = self.episode_sums_async
         self.reads = []  # epochs whose sums were read, in order, and when (epochs done then)
 
     def train_model(self):
@@ -83,3 +85,12 @@ def test_logging_keeps_the_synchronous_check(monkeypatch):
     algo = _Algo(SUMS)
     r = EngineRunner(algo, _Service(), 0.0).train(epochs=10, target_return=47.5, window=10, log_every=1)
     assert r.epochs == 3 and [k for k, _ in algo.reads] == [1, 2, 3]
+
+
+def test_trainers_without_an_async_read_keep_the_synchronous_check(monkeypatch):
+    """host / pixel / actor-learner trainers have no non-draining read; the lag
+    would only add an epoch past the threshold (TTT, epoch count and final model off by one)."""
+    monkeypatch.setenv("RRL_TTT_LAGGED_CHECK", "1")
+    algo = _Algo(SUMS, async_trainer=False)
+    r = EngineRunner(algo, _Service(), 0.0).train(epochs=10, target_return=47.5, window=10, log_every=0)
+    assert r.epochs == 3 and algo.reads == [(1, 1), (2, 2), (3, 3)]

@@ -1,0 +1,208 @@
+"""ZMTP server under the reference agent's connection pattern (trajectory.rs:69-90: a new zmq
+context + PUSH connection per upload, and the shipped notebooks upload every env step).
+
+The server socket serves every connection from ONE epoll I/O thread (csrc/host/zmtp.cpp):
+thousands of short-lived peers must neither grow the thread count nor lose a frame, and the
+inbox is bounded in bytes (TCP backpressure on the senders, no drops)."""
+import os
+import socket
+import threading
+import time
+
+import pytest
+
+from relayrl_prototype_amd import _native
+
+GREETING = b"\xff" + b"\x00" * 8 + b"\x7f" + bytes([3, 0]) + b"NULL".ljust(20, b"\x00") + b"\x00" + b"\x00" * 31
+assert len(GREETING) == 64
+
+
+def _ready(sock_type: bytes) -> bytes:
+    body = b"\x05READY" + bytes([11]) + b"Socket-Type" + len(sock_type).to_bytes(4, "big") + sock_type
+    return bytes([0x04, len(body)]) + body
+
+
+def _frame(payload: bytes, more: bool = False) -> bytes:
+    if len(payload) > 255:
+        return bytes([0x02 | (0x01 if more else 0)]) + len(payload).to_bytes(8, "big") + payload
+    return bytes([0x01 if more else 0x00, len(payload)]) + payload
+
+
+def _threads() -> int:
+    return len(os.listdir("/proc/self/task"))
+
+
+def _upload_once(port: int, payload: bytes):
+    """One reference-agent upload: connect, handshake, one message, close."""
+    s = socket.create_connection(("127.0.0.1", port))
+    s.sendall(GREETING + _ready(b"PUSH") + _frame(payload))
+    s.close()
+
+
+def test_5000_short_lived_push_connections_keep_threads_bounded():
+    pull = _native.ZmtpSocket(_native.SockType.PULL)
+    port = pull.bind("tcp://127.0.0.1:0")
+    base = _threads()
+    n_clients, per = 8, 625
+    peak = [base]
+    stop = threading.Event()
+
+    def sample():
+        while not stop.is_set():
+            peak[0] = max(peak[0], _threads())
+            time.sleep(0.005)
+
+    def client(k):
+        for i in range(per):
+            _upload_once(port, b"traj-%d-%d" % (k, i))
+
+    mon = threading.Thread(target=sample)
+    mon.start()
+    cl = [threading.Thread(target=client, args=(k,)) for k in range(n_clients)]
+    for t in cl:
+        t.start()
+    got = set()
+    deadline = time.time() + 120
+    while len(got) < n_clients * per and time.time() < deadline:
+        m = pull.recv(1000)
+        if m is None:
+            continue
+        _, frames = m
+        assert len(frames) == 1
+        got.add(bytes(frames[0]))
+    for t in cl:
+        t.join()
+    stop.set()
+    mon.join()
+    assert got == {b"traj-%d-%d" % (k, i) for k in range(n_clients) for i in range(per)}
+    # the sampler + 8 client threads are ours; the socket adds its single I/O thread
+    assert peak[0] <= base + 1 + n_clients + 1, (base, peak[0])
+    assert pull.num_threads() == 1
+    t_end = time.time() + 10
+    while pull.stats()["dropped"] < n_clients * per and time.time() < t_end:
+        time.sleep(0.05)
+    st = pull.stats()
+    assert st["accepted"] == n_clients * per and st["handshakes"] == n_clients * per, st
+    assert st["dropped"] == n_clients * per and st["bad_handshakes"] == 0, st
+    assert pull.num_connections() == 0
+    pull.close()
+    assert pull.num_threads() == 0
+
+
+def test_native_push_per_upload_closes_fast_and_joins_threads():
+    """The reference wire's connection-per-upload through our own PUSH (types.py send path)."""
+    pull = _native.ZmtpSocket(_native.SockType.PULL)
+    port = pull.bind("tcp://127.0.0.1:0")
+    base = _threads()
+    t0 = time.perf_counter()
+    for i in range(300):
+        push = _native.ZmtpSocket(_native.SockType.PUSH)
+        push.connect(f"tcp://127.0.0.1:{port}")
+        assert push.send([b"u%d" % i], 5000)
+        push.close()
+        assert push.num_threads() == 0
+    el = time.perf_counter() - t0
+    got = []
+    while len(got) < 300:
+        m = pull.recv(5000)
+        assert m is not None
+        got.append(bytes(m[1][0]))
+    assert sorted(got) == sorted(b"u%d" % i for i in range(300))
+    assert _threads() <= base + 1
+    # close() ends the connect thread's wait at once (no 50 ms poll per upload)
+    assert el < 15.0, el
+    pull.close()
+
+
+def test_inbox_is_bounded_in_bytes_and_pushes_back():
+    pull = _native.ZmtpSocket(_native.SockType.PULL)
+    pull.set_inbox_limits(1 << 20, 1 << 20)  # 1 MiB
+    port = pull.bind("tcp://127.0.0.1:0")
+    push = _native.ZmtpSocket(_native.SockType.PUSH)
+    push.connect(f"tcp://127.0.0.1:{port}")
+    blob = [bytes([k]) * (256 << 10) for k in range(24)]  # 24 x 256 KiB = 6 MiB
+    sent = []
+
+    def sender():
+        for b in blob:
+            sent.append(push.send([b], 20000))
+
+    th = threading.Thread(target=sender)
+    th.start()
+    time.sleep(1.0)  # nothing is received meanwhile
+    held = pull.inbox_bytes()
+    assert held <= (1 << 20) + (256 << 10) + 4096, held
+    assert pull.stats()["inbox_waits"] >= 1
+    out = []
+    while len(out) < len(blob):
+        m = pull.recv(10000)
+        assert m is not None
+        out.append(bytes(m[1][0]))
+    th.join()
+    assert all(sent)
+    assert out == blob  # in order, intact, nothing dropped
+    push.close()
+    pull.close()
+
+
+def test_multipart_split_across_reads_and_commands_ignored():
+    pull = _native.ZmtpSocket(_native.SockType.PULL)
+    port = pull.bind("tcp://127.0.0.1:0")
+    s = socket.create_connection(("127.0.0.1", port))
+    wire = GREETING + _ready(b"PUSH") + bytes([0x04, 5]) + b"\x04PING" + _frame(b"a" * 300, more=True) + \
+        _frame(b"b" * 3)
+    for i in range(len(wire)):  # one byte per write: every parser state sees partial input
+        s.sendall(wire[i:i + 1])
+        if i % 64 == 0:
+            time.sleep(0.001)
+    m = pull.recv(5000)
+    assert m is not None and [bytes(f) for f in m[1]] == [b"a" * 300, b"b" * 3]
+    s.close()
+    pull.close()
+
+
+def test_bad_and_silent_handshakes_are_dropped_without_blocking_others():
+    pull = _native.ZmtpSocket(_native.SockType.PULL)
+    port = pull.bind("tcp://127.0.0.1:0")
+    silent = socket.create_connection(("127.0.0.1", port))  # never speaks
+    bad = socket.create_connection(("127.0.0.1", port))
+    bad.sendall(b"GET / HTTP/1.1\r\n" + b"x" * 64)
+    wrong = socket.create_connection(("127.0.0.1", port))
+    wrong.sendall(GREETING + _ready(b"PULL"))  # PULL -> PULL is not a valid pair
+    _upload_once(port, b"ok")  # served while the silent peer holds its handshake
+    m = pull.recv(5000)
+    assert m is not None and bytes(m[1][0]) == b"ok"
+    t_end = time.time() + 8
+    while pull.stats()["bad_handshakes"] < 3 and time.time() < t_end:
+        time.sleep(0.1)
+    assert pull.stats()["bad_handshakes"] == 3, pull.stats()
+    for s in (silent, bad, wrong):
+        s.close()
+    pull.close()
+
+
+@pytest.mark.parametrize("n_dealers", [16])
+def test_router_serves_many_dealers_concurrently(n_dealers):
+    router = _native.ZmtpSocket(_native.SockType.ROUTER)
+    port = router.bind("tcp://127.0.0.1:0")
+    dealers = []
+    for d in range(n_dealers):
+        s = _native.ZmtpSocket(_native.SockType.DEALER, b"agent-%d" % d)
+        s.connect(f"tcp://127.0.0.1:{port}")
+        dealers.append(s)
+    for d, s in enumerate(dealers):
+        assert s.send([b"", b"GET_MODEL-%d" % d], 5000)
+    seen = {}
+    for _ in range(n_dealers):
+        m = router.recv(5000)
+        assert m is not None
+        peer, frames = m
+        seen[bytes(peer)] = bytes(frames[-1])
+        assert router.send([bytes(peer), b"", b"model-for-" + bytes(peer)], 5000)
+    assert seen == {b"agent-%d" % d: b"GET_MODEL-%d" % d for d in range(n_dealers)}
+    for d, s in enumerate(dealers):
+        r = s.recv(5000)
+        assert r is not None and bytes(r[1][-1]) == b"model-for-agent-%d" % d
+        s.close()
+    assert router.num_threads() == 1
+    router.close()
