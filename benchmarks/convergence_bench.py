@@ -35,12 +35,13 @@ CONV = {
         thresholds=[0.0, 100.0], window=100, budget=120.0,
         note="LunarLanderSynth-v0 (point-mass lander, gymnasium shaping, +-100 terminal bonus)"),
     "halfcheetah-ppo": dict(
-        preset="halfcheetah-ppo", overrides={},
+        preset="halfcheetah-ppo", overrides={"num_minibatches": 16},
         thresholds=[450.0, 500.0, 550.0], window=100, budget=120.0,
-        note="HalfCheetahSynth-v0 (s' = tanh(A s + B u) + noise, reward s'[8] - 0.1|u|^2, 1000 steps)"),
+        note="HalfCheetahSynth-v0 (s' = tanh(A s + B u) + noise, reward s'[8] - 0.1|u|^2, 1000 steps); 16 shuffled "
+             "minibatches per PPO epoch (the preset's full-batch schedule reaches 500 at ~9 s, plateaus ~563)"),
     "pong-a2c": dict(
         preset="pong-a2c", overrides={"num_envs": 2048},
-        thresholds=[-15.0, -5.0, 0.0, 10.0], window=100, budget=150.0,
+        thresholds=[-15.0, -5.0, 0.0, 10.0, 15.0, 19.0], window=100, budget=150.0,
         note="PongSynth-v0 vs the tracking opponent; 0 = wins as many points as it loses"),
 }
 

@@ -45,7 +45,7 @@ class RelayRLAgent:
                  server_type: str = "zmq", training_port: Optional[str] = None,
                  training_prefix: Optional[str] = None, training_host: Optional[str] = None,
                  agent_id: Optional[str] = None, seed: Optional[int] = None, handshake_timeout_s: float = 60.0,
-                 wire_format: str = "columns"):
+                 wire_format: str = "columns", connection_per_upload: bool = False):
         from ..transport.zmq_transport import make_agent_id
 
         self.config_path = resolve_config_json_path(config_path)
@@ -75,6 +75,8 @@ class RelayRLAgent:
         if wire_format == "reference" and self.server_type not in ("zmq", "grpc"):
             raise ValueError("wire_format='reference' is the reference's ZMQ / gRPC wire")
         self.wire_format = wire_format
+        # reference ZMQ wire only: a new TCP connection per upload, as the reference agent does
+        self.connection_per_upload = bool(connection_per_upload)
         self._rec = EpisodeRecorder(self.max_traj_length)
         if model_path is not None:
             self._load_model_file(model_path)
@@ -141,7 +143,8 @@ class RelayRLAgent:
 
                 ts = dict(self.train_server)  # the PULL this agent binds (agent_zmq.rs:625-640)
                 self.transport = ReferenceZmqAgentTransport(self.agent_id, address(al), address(tr), address(ts),
-                                                            self._set_policy, self._handshake_timeout)
+                                                            self._set_policy, self._handshake_timeout,
+                                                            self.connection_per_upload)
                 return
             self.transport = ZmqAgentTransport(self.agent_id, address(al), address(tr), self._set_policy,
                                                self._handshake_timeout)

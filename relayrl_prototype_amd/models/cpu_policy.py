@@ -14,7 +14,7 @@ from typing import Dict, Optional, Tuple
 
 import numpy as np
 
-from ..ops.mlp import MLPSpec
+from .mlp_spec import MLPSpec
 
 HALF_LOG_2PI = 0.9189385332046727
 

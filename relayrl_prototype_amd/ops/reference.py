@@ -123,15 +123,16 @@ def normalize_adv(adv, adv_stats):
 
 
 def mlp_grad_ref(head, params, X, A, H, mask=None, act=None, actc=None, adv=None, ret=None, logp_old=None,
-                 adv_stats=None, inv_B=None, clip_eps=0.2, ent_coef=0.0):
-    """Returns (flat gradient, stats dict) of sum_i loss_i * inv_B (+ entropy bonus)."""
+                 adv_stats=None, inv_B=None, clip_eps=0.2, ent_coef=0.0, dtype=torch.float32):
+    """Returns (flat gradient, stats dict) of sum_i loss_i * inv_B (+ entropy bonus);
+    ``dtype=torch.float64`` gives the float64 oracle (tools/grad_fuzz_probe.py)."""
     B, D = X.shape
     gaussian = head in (HEAD_PPO_GAUSS, HEAD_PG_GAUSS)
     Aeff = 1 if head == HEAD_VALUE_MSE else A
     if inv_B is None:
         inv_B = 1.0 / max(B, 1)
-    p = params.detach().float().clone().requires_grad_(True)
-    out, log_std = trunk(p, X.float(), D, H, Aeff, gaussian)
+    p = params.detach().to(dtype).clone().requires_grad_(True)
+    out, log_std = trunk(p, X.to(dtype), D, H, Aeff, gaussian)
     stats = {}
     if head == HEAD_VALUE_MSE:
         v = out[:, 0]
@@ -139,7 +140,7 @@ def mlp_grad_ref(head, params, X, A, H, mask=None, act=None, actc=None, adv=None
         loss = li.sum() * inv_B
         stats.update(loss=li.sum().item(), v=v.sum().item(), count=B)
     else:
-        advn = normalize_adv(adv.float(), adv_stats)
+        advn = normalize_adv(adv.to(dtype), None if adv_stats is None else adv_stats.to(dtype))
         if not gaussian:
             logits = masked_logits(out, mask)
             logp_all = torch.log_softmax(logits, dim=-1)

@@ -212,7 +212,9 @@ class PixelA2CTrainer:
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(s):
-                    with gc_paused(), torch.cuda.graph(g, stream=s):
+                    # thread_local: HIP calls of other threads (a server's transport / relay
+                    # threads) neither fail nor invalidate this capture
+                    with gc_paused(), torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                         stats = self._gpu_update_body(par)
                 torch.cuda.current_stream().wait_stream(s)
                 self._graphs[par] = (g, stats)

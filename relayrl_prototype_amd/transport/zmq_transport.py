@@ -301,7 +301,9 @@ class ReferenceZmqAgentTransport:
         ``"ERROR: ..."``); the agent loads it, then ``["", "MODEL_SET"]`` -> ``["", "ID_LOGGED"]``;
         retried every second until the timeout;
       * uploads (trajectory.rs:50-90): ``serde_pickle(Vec<RelayRLAction>)`` frames on a PUSH to
-        ``trajectory_server`` (one connection for all uploads, not a new context per send);
+        ``trajectory_server`` -- one connection for all uploads, or, with
+        ``connection_per_upload``, a new connection + handshake per upload exactly like the
+        reference agent (its new zmq context + PUSH per send; the server's fan-in test case);
       * model updates (agent_zmq.rs:625-698): the agent BINDS a PULL on its ``training_server``
         address and the server PUSH-connects to it, one TorchScript archive per update.  A
         receive thread blocks with a timeout (no busy poll) and swaps the policy.
@@ -309,11 +311,14 @@ class ReferenceZmqAgentTransport:
     nothing in them is unpickled or executed)."""
 
     def __init__(self, agent_id: str, agent_listener: str, trajectory_server: str, training_server: str,
-                 on_model: Callable[[ModelBlob], None], handshake_timeout_s: float = 60.0):
+                 on_model: Callable[[ModelBlob], None], handshake_timeout_s: float = 60.0,
+                 connection_per_upload: bool = False):
         self.agent_id = agent_id
         self.on_model = on_model
         self.version = 0
         self.bad_models = 0
+        self.trajectory_server = trajectory_server
+        self.connection_per_upload = bool(connection_per_upload)
         self.pull = _native.ZmtpSocket(_native.SockType.PULL)
         self.pull.bind(training_server)  # before the handshake: the server may push at once
         self.dealer = _native.ZmtpSocket(_native.SockType.DEALER, agent_id.encode())
@@ -385,6 +390,13 @@ class ReferenceZmqAgentTransport:
         payload = injector().filter_upload(payload)
         if payload is None:
             return True
+        if self.connection_per_upload:
+            s = _native.ZmtpSocket(_native.SockType.PUSH)
+            try:
+                s.connect(self.trajectory_server)
+                return s.send([payload], 10000)
+            finally:
+                s.close()
         return self.push.send([payload], 10000)
 
     def heartbeat(self):

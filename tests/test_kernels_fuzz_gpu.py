@@ -3,7 +3,7 @@ random obs / action dims, hidden sizes and batch sizes (including batches that a
 multiples of the 16-row tiles or of the 64-row staging images)."""
 import pytest
 import torch
-from hypothesis import HealthCheck, given, settings
+from hypothesis import HealthCheck, assume, given, settings
 from hypothesis import strategies as st
 
 from relayrl_prototype_amd.ops import FwdMode, GradHead, MLPSpec, mlp_forward, mlp_grad
@@ -36,8 +36,17 @@ def test_forward_logits_value_fuzz(cuda, D, A, H, B, seed):  # D up to 32: two i
 def test_grad_fuzz(cuda, head, D, A, H, B, seed):
     g = torch.Generator().manual_seed(seed)
     Aeff = 1 if head == GradHead.VALUE_MSE else A
-    pp = MLPSpec(D, H, Aeff).init(g)
+    sp = MLPSpec(D, H, Aeff)
+    pp = sp.init(g)
     X = torch.randn(B, D, generator=g)
+    # a ReLU tie (|pre-activation| ~ rounding) flips relu' between two correct fp32 evaluation
+    # orders and moves a whole dW2 / b2 row: not a kernel error (seed 1000000, D 1, A 5, B 45:
+    # |z2| = 9.6e-9 against a median of 0.2, tools/grad_fuzz_probe.py)
+    o = sp.offsets()
+    p64, x64 = pp.double(), X.double()
+    z1 = x64 @ p64[o["w1"]:o["b1"]].view(H, D).T + p64[o["b1"]:o["w2"]]
+    z2 = z1.clamp(min=0) @ p64[o["w2"]:o["b2"]].view(H, H).T + p64[o["b2"]:o["w3"]]
+    assume(min(z1.abs().min().item(), z2.abs().min().item()) > 1e-6)
     act = torch.randint(0, A, (B,), dtype=torch.int32, generator=g)
     adv = torch.randn(B, generator=g)
     ret = torch.randn(B, generator=g)

@@ -206,3 +206,28 @@ def test_router_serves_many_dealers_concurrently(n_dealers):
         s.close()
     assert router.num_threads() == 1
     router.close()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("transport", ["zmq", "zmq-ref", "grpc"])
+def test_many_agent_processes_fan_in_without_drops(transport):
+    """8 agent PROCESSES upload at once to one TrainingServer (the reference's distribution
+    mode), paced like the reference bench (network_benchmarks.rs: a wait between actions,
+    10-action uploads); zmq-ref opens a new connection per upload like trajectory.rs:69-90.
+    Every upload is received and processed; the server's thread count does not grow with the
+    connections."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from benchmarks.fanin_bench import run
+
+    r = run(transport, 8, 3.0, 5, 10, "trajectory")
+    assert r["agent_processes_ok"] == 8, r
+    assert r["uploads_sent"] > 8 * 10 and r["drops"] == 0 and r["drained"], r
+    th0, peak, end = r["server_threads"]
+    import torch
+
+    # the CPU learner's first update starts torch's intra-op pool; grpc has its own server pool
+    allow = torch.get_num_threads() + (24 if transport == "grpc" else 4)
+    assert peak - th0 <= allow, r
+    assert r["uploads_received"] > 40 * 8  # far more connections than threads (zmq-ref: one per upload)

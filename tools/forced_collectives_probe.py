@@ -95,10 +95,77 @@ def bench(comm, plain, epochs: int, warmup: int) -> dict:
     return rec
 
 
+def syncs(comm, plain, epochs: int) -> dict:
+    """the multi-rank engine loop (EngineRunner with the stop agreement of a
+    relay-attached rank 0, ``log_every=0``) on the forced path: synchronising host reads per
+    steady-state epoch (Tensor.item / tolist / cpu, torch.cuda.synchronize), counted by hooks,
+    and the epoch time against the world-1 graph path."""
+    import tempfile
+    from collections import Counter
+
+    from relayrl_prototype_amd.runtime.engine import EngineAlgorithm, EngineRunner, EngineSpec
+
+    counts = Counter()
+    active = [False]
+    orig = {"item": torch.Tensor.item, "tolist": torch.Tensor.tolist, "cpu": torch.Tensor.cpu,
+            "synchronize": torch.cuda.synchronize, "event_wait": torch.cuda.Event.synchronize}
+
+    def hook(name, fn):
+        def w(*a, **k):
+            if active[0]:
+                counts[name] += 1
+            return fn(*a, **k)
+        return w
+
+    torch.Tensor.item = hook("item", orig["item"])
+    torch.Tensor.tolist = hook("tolist", orig["tolist"])
+    torch.Tensor.cpu = hook("cpu", orig["cpu"])
+    torch.cuda.synchronize = hook("synchronize", orig["synchronize"])
+    torch.cuda.Event.synchronize = hook("event_wait", orig["event_wait"])
+
+    class _Pub:
+        updates = 0
+
+        def publish_model(self):
+            pass
+
+    rec = {}
+    try:
+        for name, c, agree in (("forced_relay", comm, True), ("world1", plain, False)):
+            spec = EngineSpec("vec", "LunarLanderSynth-v0", "reinforce", 1,
+                              {"env": "LunarLanderSynth-v0", "algo": "reinforce", "num_envs": 2048, "rollout_len": 128,
+                               "train_vf_iters": 80, "seed": 1, "use_graphs": True})
+            algo = EngineAlgorithm(spec, tempfile.mkdtemp(), comm=c, device=torch.device("cuda", 0), log=False)
+            r = EngineRunner(algo, _Pub(), time.perf_counter())
+            r.agree_stop = agree
+            r.train(epochs=4, log_every=0, publish_every=0)  # warm-up + captures
+            orig["synchronize"]()
+            counts.clear()
+            active[0] = True
+            t0 = time.perf_counter()
+            r.train(epochs=epochs, log_every=0, publish_every=0)
+            active[0] = False
+            orig["synchronize"]()
+            el = time.perf_counter() - t0
+            rec[name + "_ms_per_epoch"] = round(el / epochs * 1e3, 3)
+            rec[name + "_sync_reads_per_epoch"] = round(sum(v for k, v in counts.items() if k != "event_wait") / epochs, 3)
+            rec[name + "_lagged_event_waits_per_epoch"] = round(counts["event_wait"] / epochs, 3)
+            rec[name + "_hooks"] = dict(counts)
+            del r, algo
+            torch.cuda.empty_cache()
+    finally:
+        torch.Tensor.item, torch.Tensor.tolist, torch.Tensor.cpu = orig["item"], orig["tolist"], orig["cpu"]
+        torch.cuda.synchronize, torch.cuda.Event.synchronize = orig["synchronize"], orig["event_wait"]
+    rec["relay_overhead_pct"] = round((rec["forced_relay_ms_per_epoch"] / rec["world1_ms_per_epoch"] - 1) * 100, 2)
+    rec["syncs_config"] = "LunarLanderSynth-v0 REINFORCE-with-baseline, 2048 envs x 128 steps, 80 value iterations"
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--bench", action="store_true")
+    ap.add_argument("--syncs", action="store_true")
     ap.add_argument("--epochs", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     a = ap.parse_args()
@@ -110,6 +177,8 @@ def main():
         out.update(check(comm))
     if a.bench:
         out.update(bench(comm, Comm(collectives=False), a.epochs, a.warmup))
+    if a.syncs:
+        out.update(syncs(comm, Comm(collectives=False), max(a.epochs, 20)))
     import torch.distributed as dist
 
     dist.destroy_process_group()
