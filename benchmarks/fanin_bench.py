@@ -16,11 +16,11 @@ One row per (transport, agents, wait_ms):
                           trains in the background
              trajectory   (CPU) the trajectory learner (REINFORCE, algorithms/trajectory_algo.py)
 
-Reported: uploads/s and agent env steps/s the server ingested, ingestion lag (agent send ->
-learner service processed, p50 / p99, native wire: matched on (agent id, episode seq)),
-drops (sent - received, plus the learner's own rejections), the drain time after the agents
-stop, and the server's thread count before / during / after (the ZMTP server serves every
-connection from one I/O thread).
+Reported: uploads/s the learner service processed while the agents ran, agent env steps/s,
+ingestion lag (agent send -> learner service processed, p50 / p99, native wire: matched on
+(agent id, episode seq)), the backlog at the stop and the time to drain it, drops (sent -
+received after the drain, plus the learner's own rejections), and the server's thread count
+before / during / after (the ZMTP server serves every connection from one I/O thread).
 
     python benchmarks/fanin_bench.py --agents 16 64 --transports zmq zmq-ref grpc --seconds 10
     python benchmarks/fanin_bench.py --agents 16 --paced 25 50 100 --traj-size 10
@@ -149,12 +149,10 @@ def run(transport, n_agents, seconds, wait_ms, traj_size, learner) -> dict:
     while time.time() < stop_at:
         th_peak = max(th_peak, threads())
         time.sleep(0.05)
+    received_in_window = srv.service.received  # processed while the agents were running
     for p in ps:
         p.join(timeout=120)
     t_agents_done = time.time()
-    drained = srv.wait_idle(120)
-    drain_s = time.time() - t_agents_done
-    received = srv.service.received
     rows = []
     for o in outs:
         try:
@@ -162,6 +160,21 @@ def run(transport, n_agents, seconds, wait_ms, traj_size, learner) -> dict:
         except (OSError, ValueError):
             pass
     sent = sum(len(r["sends"]) for r in rows)
+    # drain: uploads still in the socket inbox / decode / service queue at the stop
+    backlog = sent - srv.service.received
+    last, t_change = -1, time.time()
+    while time.time() - t_agents_done < 120:
+        r = srv.service.received
+        if r >= sent:
+            break
+        if r != last:
+            last, t_change = r, time.time()
+        elif time.time() - t_change > 10:
+            break  # no progress: the rest is lost
+        time.sleep(0.01)
+    drained = srv.wait_idle(60) and srv.service.received >= sent
+    drain_s = time.time() - t_agents_done
+    received = srv.service.received
     steps = sum(r["steps"] for r in rows)
     lags, send_ms = [], []
     for r in rows:
@@ -178,7 +191,8 @@ def run(transport, n_agents, seconds, wait_ms, traj_size, learner) -> dict:
     res = {"transport": transport, "agents": n_agents, "learner": learner, "wait_ms": wait_ms,
            "traj_size": traj_size or "cartpole", "seconds": seconds, "agent_processes_ok": len(rows),
            "uploads_sent": sent, "uploads_received": received, "drops": sent - received, "learner_rejected": rejected,
-           "uploads_per_s": round(received / seconds, 1), "agent_env_steps_per_s": round(steps / seconds, 1),
+           "uploads_per_s": round(received_in_window / seconds, 1), "backlog_at_stop": backlog,
+           "agent_env_steps_per_s": round(steps / seconds, 1),
            "send_call_ms_p50": pct(send_ms, 0.5), "send_call_ms_p99": pct(send_ms, 0.99),
            "ingest_lag_ms_p50": pct(lags, 0.5), "ingest_lag_ms_p99": pct(lags, 0.99), "lag_samples": len(lags),
            "drain_s": round(drain_s, 3), "drained": drained, "server_threads": [th0, th_peak, threads()]}

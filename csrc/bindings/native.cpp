@@ -11,6 +11,8 @@
 #include "vecenv_bind.h"
 #include "zmtp.h"
 
+void bind_pickle(pybind11::module_& m);  // pickle_native.cpp
+
 namespace py = pybind11;
 using namespace rrl;
 
@@ -208,6 +210,7 @@ PYBIND11_MODULE(_native, m) {
         return d;
       });
 
+  bind_pickle(m);
   m.def("env_names", &env_names);
   m.def("env_constants", &env_constants);
   bind_vecenv(m);

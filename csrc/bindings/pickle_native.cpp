@@ -1,0 +1,424 @@
+// Native data-only pickle codec for the reference ZMQ trajectory frames
+// (serde_pickle(Vec<RelayRLAction>), trajectory.rs:50-90 -> training_zmq.rs:994-1012).
+//
+// transport/serde_pickle.py holds the reference semantics in Python (``loads`` / ``dumps``).
+// Its interpreter runs ~25,000 opcodes per CartPole episode (every safetensors byte of every
+// tensor is a BININT1 inside a list), ~19 ms per frame: a server fed by many reference agents
+// ingests ~50 uploads/s.  This is the same interpreter in C++:
+//
+//   * ``pickle_loads(buf, u8_lists_as_bytes)``: the SAME opcode subset (containers, scalars,
+//     strings, bytes, memo); every opcode that imports or calls (GLOBAL, REDUCE, BUILD, INST,
+//     OBJ, NEWOBJ, EXT*, PERSID, ...) is an error, so a frame can never execute anything.
+//     With ``u8_lists_as_bytes`` a list built only from integers 0..255 comes back as a
+//     ``bytearray`` (serde's Vec<u8>), not as a list of Python ints.
+//   * ``pickle_dumps(obj, bytes_as_u8_list)``: the writer serde_pickle uses (protocol 3, no
+//     memo; lists in APPENDS chunks of 1000), byte-identical to serde_pickle.dumps; with
+//     ``bytes_as_u8_list`` a bytes object is written as a list of u8 ints (Vec<u8>).
+#include <pybind11/pybind11.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace {
+
+constexpr int kMaxDepth = 64;
+constexpr size_t kMaxStack = 1u << 20;
+constexpr size_t kMaxMemo = 1u << 16;
+
+struct FrameError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+class Reader {
+ public:
+  Reader(const uint8_t* p, size_t n) : p_(p), n_(n) {}
+  const uint8_t* take(size_t k) {
+    if (pos_ + k > n_) throw FrameError("truncated frame");
+    const uint8_t* out = p_ + pos_;
+    pos_ += k;
+    return out;
+  }
+  uint8_t u8() { return *take(1); }
+  template <class T>
+  T le() {
+    T v;
+    std::memcpy(&v, take(sizeof(T)), sizeof(T));
+    return v;
+  }
+
+ private:
+  const uint8_t* p_;
+  size_t n_;
+  size_t pos_ = 0;
+};
+
+py::object key_of(const py::object& k) {
+  if (py::isinstance<py::list>(k) || py::isinstance<py::dict>(k) || py::isinstance<py::set>(k) ||
+      py::isinstance<py::bytearray>(k))
+    throw FrameError("unhashable key");
+  return k;
+}
+
+bool all_u8(const std::vector<py::object>& items, size_t from) {
+  for (size_t i = from; i < items.size(); ++i) {
+    PyObject* o = items[i].ptr();
+    if (!PyLong_CheckExact(o)) return false;
+    int overflow = 0;
+    const long v = PyLong_AsLongAndOverflow(o, &overflow);
+    if (overflow || v < 0 || v > 255) return false;
+  }
+  return true;
+}
+
+py::object loads(const py::bytes& frame, bool u8_as_bytes) {
+  char* data = nullptr;
+  Py_ssize_t n = 0;
+  if (PyBytes_AsStringAndSize(frame.ptr(), &data, &n) != 0) throw py::error_already_set();
+  Reader r(reinterpret_cast<const uint8_t*>(data), (size_t)n);
+  std::vector<py::object> stack;
+  std::vector<size_t> marks;
+  std::unordered_map<uint32_t, py::object> memo;
+  auto pop_value = [&]() {
+    if (stack.empty() || (!marks.empty() && marks.back() == stack.size())) throw FrameError("stack underflow");
+    py::object v = std::move(stack.back());
+    stack.pop_back();
+    return v;
+  };
+  auto pop_mark = [&]() -> size_t {  // index of the first item above the mark
+    if (marks.empty()) throw FrameError("MARK not found");
+    const size_t m = marks.back();
+    marks.pop_back();
+    return m;
+  };
+  auto top = [&]() -> py::object& {
+    if (stack.empty() || (!marks.empty() && marks.back() == stack.size())) throw FrameError("stack underflow");
+    return stack.back();
+  };
+  // the container below the items [from, end): no MARK may sit between them
+  auto container_below = [&](size_t from) -> py::object& {
+    if (from == 0 || stack.size() < from || (!marks.empty() && marks.back() >= from)) throw FrameError("stack underflow");
+    return stack[from - 1];
+  };
+  auto as_list = [&](py::object& o) {  // a bytearray still being built as a Vec<u8> -> list of ints
+    if (u8_as_bytes && py::isinstance<py::bytearray>(o)) {
+      py::list l;
+      const char* b = PyByteArray_AsString(o.ptr());
+      for (Py_ssize_t i = 0; i < PyByteArray_Size(o.ptr()); ++i) l.append(py::int_((unsigned char)b[i]));
+      o = l;
+    }
+  };
+  // list APPEND / APPENDS onto the container, with the u8 fast form
+  auto extend_top = [&](size_t from) {
+    py::object& tgt = container_below(from);
+    if (u8_as_bytes && py::isinstance<py::bytearray>(tgt)) {
+      if (all_u8(stack, from)) {
+        std::string chunk(stack.size() - from, '\0');
+        for (size_t i = from; i < stack.size(); ++i) chunk[i - from] = (char)PyLong_AsLong(stack[i].ptr());
+        const Py_ssize_t old = PyByteArray_Size(tgt.ptr());
+        if (PyByteArray_Resize(tgt.ptr(), old + (Py_ssize_t)chunk.size()) != 0) throw py::error_already_set();
+        std::memcpy(PyByteArray_AsString(tgt.ptr()) + old, chunk.data(), chunk.size());
+        stack.resize(from);
+        return;
+      }
+      as_list(tgt);  // not a Vec<u8> after all
+    }
+    if (!py::isinstance<py::list>(tgt)) throw FrameError("expected a list on the stack");
+    py::list l = tgt.cast<py::list>();
+    for (size_t i = from; i < stack.size(); ++i) l.append(stack[i]);
+    stack.resize(from);
+  };
+  for (;;) {
+    if (stack.size() > kMaxStack || memo.size() > kMaxMemo) throw FrameError("frame too large");
+    const uint8_t op = r.u8();
+    switch (op) {
+      case 0x80: r.take(1); break;  // PROTO
+      case 0x95: r.take(8); break;  // FRAME
+      case 0x2E:                    // STOP
+        if (stack.size() != 1 || !marks.empty()) throw FrameError("bad stack at STOP");
+        return stack[0];
+      case 0x4E: stack.push_back(py::none()); break;
+      case 0x88: stack.push_back(py::bool_(true)); break;
+      case 0x89: stack.push_back(py::bool_(false)); break;
+      case 0x4B: stack.push_back(py::int_(r.u8())); break;                // BININT1
+      case 0x4D: stack.push_back(py::int_(r.le<uint16_t>())); break;      // BININT2
+      case 0x4A: stack.push_back(py::int_(r.le<int32_t>())); break;       // BININT
+      case 0x8A:                                                          // LONG1
+      case 0x8B: {                                                        // LONG4
+        int64_t k = op == 0x8A ? r.u8() : r.le<int32_t>();
+        if (k < 0 || k > 64) throw FrameError("LONG4 too large");
+        const uint8_t* b = r.take((size_t)k);
+        PyObject* v = k ? _PyLong_FromByteArray(b, (size_t)k, /*little_endian=*/1, /*is_signed=*/1) : PyLong_FromLong(0);
+        if (!v) throw py::error_already_set();
+        stack.push_back(py::reinterpret_steal<py::object>(v));
+        break;
+      }
+      case 0x47: {  // BINFLOAT (big-endian double)
+        const uint8_t* b = r.take(8);
+        uint64_t u = 0;
+        for (int i = 0; i < 8; ++i) u = (u << 8) | b[i];
+        double d;
+        std::memcpy(&d, &u, 8);
+        stack.push_back(py::float_(d));
+        break;
+      }
+      case 0x58:    // BINUNICODE
+      case 0x8C:    // SHORT_BINUNICODE
+      case 0x8D: {  // BINUNICODE8
+        const uint64_t k = op == 0x58 ? r.le<uint32_t>() : (op == 0x8C ? r.u8() : r.le<uint64_t>());
+        if (k > (uint64_t)n) throw FrameError("truncated frame");
+        const char* s = reinterpret_cast<const char*>(r.take((size_t)k));
+        PyObject* v = PyUnicode_DecodeUTF8(s, (Py_ssize_t)k, "strict");
+        if (!v) throw py::error_already_set();
+        stack.push_back(py::reinterpret_steal<py::object>(v));
+        break;
+      }
+      case 0x42:    // BINBYTES
+      case 0x43:    // SHORT_BINBYTES
+      case 0x8E: {  // BINBYTES8
+        const uint64_t k = op == 0x42 ? r.le<uint32_t>() : (op == 0x43 ? r.u8() : r.le<uint64_t>());
+        if (k > (uint64_t)n) throw FrameError("truncated frame");
+        const char* s = reinterpret_cast<const char*>(r.take((size_t)k));
+        stack.push_back(py::bytes(s, (size_t)k));
+        break;
+      }
+      case 0x28:  // MARK
+        if ((int)marks.size() >= kMaxDepth) throw FrameError("nesting too deep");
+        marks.push_back(stack.size());
+        break;
+      case 0x5D:  // EMPTY_LIST
+        if (u8_as_bytes) stack.push_back(py::reinterpret_steal<py::object>(PyByteArray_FromStringAndSize("", 0)));
+        else stack.push_back(py::list());
+        break;
+      case 0x7D: stack.push_back(py::dict()); break;
+      case 0x29: stack.push_back(py::tuple()); break;
+      case 0x8F: stack.push_back(py::set()); break;
+      case 0x61: {  // APPEND
+        if (stack.empty() || (!marks.empty() && marks.back() == stack.size())) throw FrameError("stack underflow");
+        extend_top(stack.size() - 1);
+        break;
+      }
+      case 0x65: extend_top(pop_mark()); break;  // APPENDS
+      case 0x73: {                               // SETITEM
+        py::object v = pop_value();
+        py::object k = pop_value();
+        py::object& d = top();
+        if (!py::isinstance<py::dict>(d)) throw FrameError("expected a dict on the stack");
+        d.cast<py::dict>()[key_of(k)] = v;
+        break;
+      }
+      case 0x75: {  // SETITEMS
+        const size_t m = pop_mark();
+        if ((stack.size() - m) % 2) throw FrameError("odd SETITEMS");
+        py::object& c = container_below(m);
+        if (!py::isinstance<py::dict>(c)) throw FrameError("expected a dict on the stack");
+        py::dict d = c.cast<py::dict>();
+        for (size_t i = m; i < stack.size(); i += 2) d[key_of(stack[i])] = stack[i + 1];
+        stack.resize(m);
+        break;
+      }
+      case 0x90: {  // ADDITEMS
+        const size_t m = pop_mark();
+        py::object& c = container_below(m);
+        if (!py::isinstance<py::set>(c)) throw FrameError("expected a set on the stack");
+        py::set s = c.cast<py::set>();
+        for (size_t i = m; i < stack.size(); ++i) s.add(key_of(stack[i]));
+        stack.resize(m);
+        break;
+      }
+      case 0x91: {  // FROZENSET
+        const size_t m = pop_mark();
+        py::set s;
+        for (size_t i = m; i < stack.size(); ++i) s.add(key_of(stack[i]));
+        stack.resize(m);
+        stack.push_back(py::reinterpret_steal<py::object>(PyFrozenSet_New(s.ptr())));
+        break;
+      }
+      case 0x74: {  // TUPLE
+        const size_t m = pop_mark();
+        py::tuple t(stack.size() - m);
+        for (size_t i = m; i < stack.size(); ++i) t[i - m] = stack[i];
+        stack.resize(m);
+        stack.push_back(t);
+        break;
+      }
+      case 0x85:
+      case 0x86:
+      case 0x87: {  // TUPLE1..3
+        const size_t k = op - 0x84;
+        if (stack.size() < k || (!marks.empty() && marks.back() > stack.size() - k)) throw FrameError("stack underflow");
+        py::tuple t(k);
+        for (size_t i = 0; i < k; ++i) t[i] = stack[stack.size() - k + i];
+        stack.resize(stack.size() - k);
+        stack.push_back(t);
+        break;
+      }
+      // (serde_pickle writes no memo; a memoised list is built as a list, not in the u8 form)
+      case 0x71: as_list(top()); memo[r.u8()] = top(); break;                 // BINPUT
+      case 0x72: as_list(top()); memo[r.le<uint32_t>()] = top(); break;       // LONG_BINPUT
+      case 0x94: as_list(top()); memo[(uint32_t)memo.size()] = top(); break;  // MEMOIZE
+      case 0x68:                                            // BINGET
+      case 0x6A: {                                          // LONG_BINGET
+        const uint32_t k = op == 0x68 ? r.u8() : r.le<uint32_t>();
+        auto it = memo.find(k);
+        if (it == memo.end()) throw FrameError("memo key not found");
+        stack.push_back(it->second);
+        break;
+      }
+      case 0x30:  // POP
+        if (!marks.empty() && marks.back() == stack.size()) {
+          marks.pop_back();
+        } else {
+          if (stack.empty()) throw FrameError("stack underflow");
+          stack.pop_back();
+        }
+        break;
+      case 0x31: stack.resize(pop_mark()); break;  // POP_MARK
+      default: {
+        char msg[80];
+        snprintf(msg, sizeof(msg), "opcode 0x%02x is not allowed in a trajectory frame", op);
+        throw FrameError(msg);
+      }
+    }
+  }
+}
+
+void dump(const py::handle& o, std::string& out, int depth, bool bytes_u8) {
+  if (depth > kMaxDepth) throw std::invalid_argument("nesting too deep");
+  PyObject* p = o.ptr();
+  auto put_u32 = [&](uint32_t v) { out.append(reinterpret_cast<const char*>(&v), 4); };
+  auto dump_int = [&](long long v) {
+    if (v >= 0 && v < 256) {
+      out.push_back('K');
+      out.push_back((char)v);
+    } else if (v >= 0 && v < 65536) {
+      out.push_back('M');
+      const uint16_t u = (uint16_t)v;
+      out.append(reinterpret_cast<const char*>(&u), 2);
+    } else {
+      out.push_back('J');
+      const int32_t s = (int32_t)v;
+      out.append(reinterpret_cast<const char*>(&s), 4);
+    }
+  };
+  if (p == Py_None) {
+    out.push_back('N');
+  } else if (p == Py_True) {
+    out.push_back('\x88');
+  } else if (p == Py_False) {
+    out.push_back('\x89');
+  } else if (PyLong_Check(p)) {
+    int overflow = 0;
+    const long long v = PyLong_AsLongLongAndOverflow(p, &overflow);
+    if (!overflow && v >= -2147483648LL && v < 2147483648LL) {
+      dump_int(v);
+    } else {  // LONG1, as Python's int.to_bytes((bit_length + 8) // 8, "little", signed=True)
+      const size_t bits = _PyLong_NumBits(p);
+      const size_t k = (bits + 8) / 8;
+      std::string raw(k, '\0');
+      if (_PyLong_AsByteArray(reinterpret_cast<PyLongObject*>(p), reinterpret_cast<unsigned char*>(&raw[0]), k,
+                              /*little_endian=*/1, /*is_signed=*/1) != 0)
+        throw py::error_already_set();
+      out.push_back('\x8a');
+      out.push_back((char)k);
+      out += raw;
+    }
+  } else if (PyFloat_Check(p)) {
+    const double d = PyFloat_AsDouble(p);
+    uint64_t u;
+    std::memcpy(&u, &d, 8);
+    out.push_back('G');
+    for (int i = 7; i >= 0; --i) out.push_back((char)((u >> (8 * i)) & 0xFF));
+  } else if (PyUnicode_Check(p)) {
+    Py_ssize_t k = 0;
+    const char* s = PyUnicode_AsUTF8AndSize(p, &k);
+    if (!s) throw py::error_already_set();
+    out.push_back('X');
+    put_u32((uint32_t)k);
+    out.append(s, (size_t)k);
+  } else if (PyBytes_Check(p) || PyByteArray_Check(p)) {
+    const char* s = PyBytes_Check(p) ? PyBytes_AS_STRING(p) : PyByteArray_AS_STRING(p);
+    const size_t k = (size_t)(PyBytes_Check(p) ? PyBytes_GET_SIZE(p) : PyByteArray_GET_SIZE(p));
+    if (bytes_u8) {  // serde's Vec<u8>: a list of ints, APPENDS chunks of 1000
+      out.push_back(']');
+      for (size_t i = 0; i < k; i += 1000) {
+        out.push_back('(');
+        for (size_t j = i; j < k && j < i + 1000; ++j) {
+          out.push_back('K');
+          out.push_back(s[j]);
+        }
+        out.push_back('e');
+      }
+    } else if (k < 256) {
+      out.push_back('C');
+      out.push_back((char)k);
+      out.append(s, k);
+    } else {
+      out.push_back('B');
+      put_u32((uint32_t)k);
+      out.append(s, k);
+    }
+  } else if (PyTuple_Check(p)) {
+    const Py_ssize_t k = PyTuple_GET_SIZE(p);
+    if (k == 0) {
+      out.push_back(')');
+    } else {
+      out.push_back('(');
+      for (Py_ssize_t i = 0; i < k; ++i) dump(PyTuple_GET_ITEM(p, i), out, depth + 1, bytes_u8);
+      out.push_back('t');
+    }
+  } else if (PyList_Check(p)) {
+    const Py_ssize_t k = PyList_GET_SIZE(p);
+    out.push_back(']');
+    for (Py_ssize_t i = 0; i < k; i += 1000) {
+      out.push_back('(');
+      for (Py_ssize_t j = i; j < k && j < i + 1000; ++j) dump(PyList_GET_ITEM(p, j), out, depth + 1, bytes_u8);
+      out.push_back('e');
+    }
+  } else if (PyDict_Check(p)) {
+    out.push_back('}');
+    if (PyDict_GET_SIZE(p) > 0) {
+      out.push_back('(');
+      PyObject *k, *v;
+      Py_ssize_t pos = 0;
+      while (PyDict_Next(p, &pos, &k, &v)) {
+        dump(k, out, depth + 1, bytes_u8);
+        dump(v, out, depth + 1, bytes_u8);
+      }
+      out.push_back('u');
+    }
+  } else {
+    throw py::type_error(std::string("cannot serialise ") + Py_TYPE(p)->tp_name);
+  }
+}
+
+}  // namespace
+
+void bind_pickle(py::module_& m) {
+  static py::exception<FrameError> frame_error(m, "PickleFrameError", PyExc_ValueError);
+  m.def(
+      "pickle_loads",
+      [](const py::bytes& b, bool u8_lists_as_bytes) {
+        try {
+          return loads(b, u8_lists_as_bytes);
+        } catch (const FrameError& e) {
+          PyErr_SetString(frame_error.ptr(), e.what());
+          throw py::error_already_set();
+        }
+      },
+      py::arg("frame"), py::arg("u8_lists_as_bytes") = false,
+      "Data-only pickle interpreter (transport/serde_pickle.py semantics) in C++");
+  m.def(
+      "pickle_dumps",
+      [](const py::handle& o, bool bytes_as_u8_list) {
+        std::string out = "\x80\x03";
+        dump(o, out, 0, bytes_as_u8_list);
+        out.push_back('.');
+        return py::bytes(out);
+      },
+      py::arg("obj"), py::arg("bytes_as_u8_list") = false, "serde_pickle-style writer (protocol 3, no memo)");
+}

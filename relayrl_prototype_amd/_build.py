@@ -142,7 +142,8 @@ def build_hip(verbose=False, force=False) -> str:
 
 def build_native(verbose=False, force=False) -> str:
     hdir = os.path.join(CSRC, "host")
-    srcs = sorted(glob.glob(os.path.join(hdir, "*.cpp"))) + [os.path.join(CSRC, "bindings", "native.cpp")]
+    srcs = sorted(glob.glob(os.path.join(hdir, "*.cpp"))) + [os.path.join(CSRC, "bindings", "native.cpp"),
+                                                             os.path.join(CSRC, "bindings", "pickle_native.cpp")]
     headers = sorted(glob.glob(os.path.join(hdir, "*.h")))
     odir = os.path.join(BUILD, "native")
     os.makedirs(odir, exist_ok=True)

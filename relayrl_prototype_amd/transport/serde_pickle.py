@@ -13,6 +13,11 @@ call one -- GLOBAL, STACK_GLOBAL, REDUCE, BUILD, INST, OBJ, NEWOBJ, EXT*, PERSID
 error, so a frame can never execute anything.  ``dumps`` writes the same subset the way
 serde_pickle does (protocol 3, no memo); tests use it to build reference-shaped fixtures.
 
+``loads_fast`` / ``reference_frame`` run the same interpreter / writer in C++
+(csrc/bindings/pickle_native.cpp, ~100x faster: the Python interpreter executes one opcode
+per safetensors byte), Vec<u8> lists coming back as ``bytearray``; ``loads`` / ``dumps`` stay
+the reference semantics the native codec is tested against (tests/test_pickle_native.py).
+
 ``actions_from_reference`` maps the decoded list onto :class:`RelayRLAction`s (TensorData =
 {shape, dtype, data: bytes of a one-tensor safetensors file}, action.rs:193-352), and
 :class:`CumulativeDeduper` strips the prefix a reference agent re-sends with every upload
@@ -43,7 +48,14 @@ def is_pickle_frame(buf: bytes) -> bool:
 
 def loads(buf: bytes) -> Any:
     """Decode a data-only pickle (protocols 2-5 opcode subset); raises PickleFrameError on
-    any opcode outside the subset."""
+    any opcode outside the subset and on any malformed frame."""
+    try:
+        return _loads(buf)
+    except (IndexError, KeyError, TypeError) as e:  # e.g. BINPUT on an empty stack, BINGET of an unknown key
+        raise PickleFrameError(f"malformed frame: {type(e).__name__}") from None
+
+
+def _loads(buf: bytes) -> Any:
     mv = memoryview(buf)
     n = len(mv)
     pos = 0
@@ -198,6 +210,24 @@ def loads(buf: bytes) -> Any:
             raise PickleFrameError(f"opcode 0x{op:02x} is not allowed in a trajectory frame")
 
 
+def loads_fast(buf: bytes) -> Any:
+    """``loads`` in C++, lists of u8 (serde's Vec<u8>) as ``bytearray`` (so an EMPTY list of
+    any type is an empty bytearray; the consumers below accept both)."""
+    try:
+        from .. import _native
+    except ImportError:  # the host runtime is not built: the reference interpreter
+        return loads(buf)
+    try:
+        return _native.pickle_loads(bytes(buf), True)
+    except _native.PickleFrameError as e:
+        raise PickleFrameError(str(e)) from None
+
+
+def _seq(v) -> list:
+    """A decoded sequence (list, tuple, or a Vec<u8> bytearray from loads_fast) as a list."""
+    return list(v)
+
+
 def _key(k):
     if isinstance(k, (list, dict, set)):
         raise PickleFrameError("unhashable key")
@@ -290,7 +320,7 @@ def _tensordata(d: Any):
     raw = bytes(data) if isinstance(data, (bytes, bytearray, list, tuple)) else None
     if raw is None:
         raise PickleFrameError("TensorData.data must be bytes or a list of u8")
-    return tensordata_from_json({"shape": list(d.get("shape", [])), "dtype": dt, "data": raw})
+    return tensordata_from_json({"shape": _seq(d.get("shape", [])), "dtype": dt, "data": raw})
 
 
 def actions_from_reference(obj: Any):
@@ -299,6 +329,8 @@ def actions_from_reference(obj: Any):
 
     if isinstance(obj, dict) and "actions" in obj:  # a whole RelayRLTrajectory struct
         obj = obj["actions"]
+    if isinstance(obj, bytearray) and not obj:  # loads_fast: an empty list
+        obj = []
     if not isinstance(obj, (list, tuple)):
         raise PickleFrameError("expected a list of actions")
     out = []
@@ -319,10 +351,17 @@ def actions_from_reference(obj: Any):
 
 def reference_frame(actions) -> bytes:
     """[RelayRLAction] -> the frame a reference agent would send (serde_pickle of the
-    actions' serde form; enums in serde_pickle's default ``{variant: value}`` / name form)."""
-    out = []
-    for a in actions:
-        d = a.to_json_dict()
+    actions' serde form; enums in serde_pickle's default ``{variant: value}`` / name form;
+    TensorData.data as a list of u8).  Written by the C++ writer when the host runtime is
+    built (bytes as Vec<u8> lists), else by ``dumps``: byte-identical output."""
+    out = [a.to_json_dict() for a in actions]
+    try:
+        from .. import _native
+
+        return _native.pickle_dumps(out, True)
+    except ImportError:
+        pass
+    for d in out:
         for key in ("obs", "act", "mask"):
             if d[key] is not None:
                 d[key] = dict(d[key], data=list(d[key]["data"]))
@@ -331,7 +370,6 @@ def reference_frame(actions) -> bytes:
                 (kind, val), = v.items()
                 if kind == "Tensor":
                     d["data"][k] = {"Tensor": dict(val, data=list(val["data"]))}
-        out.append(d)
     return dumps(out)
 
 

@@ -157,7 +157,7 @@ class ZmqTrainingEndpoint:
         if TrajectoryColumns.is_frame(f):
             return TrajectoryColumns.decode(f)
         if serde_pickle.is_pickle_frame(f):
-            acts = self.dedupe.new_actions(serde_pickle.actions_from_reference(serde_pickle.loads(f)))
+            acts = self.dedupe.new_actions(serde_pickle.actions_from_reference(serde_pickle.loads_fast(f)))
             self.reference_frames += 1
             self._touch_reference_agents()
             if not acts:

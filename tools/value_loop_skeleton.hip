@@ -122,21 +122,34 @@ __device__ void phase_grad(const Args& a, int it) {
   if (acc == 12345.f) a.sink[b] = acc;  // keeps the reads (never true in practice)
 }
 
-// phase 2: workgroup b reduces its share of the P columns over the G slabs, then Adam
+// phase 2: workgroup b reduces its share of the P columns over the G slabs, then Adam.
+// 512 threads = 128 columns x 4 slab quarters (independent loads in flight), LDS combine.
 __device__ void phase_adam(const Args& a, int it) {
+  __shared__ float part[4][128];
   const int share = (a.P + a.G - 1) / a.G;
   const int lo = blockIdx.x * share;
   const int hi = min(a.P, lo + share);
   const float b1 = 0.9f, b2 = 0.999f, lr = 1e-3f;
   const float bc1 = 1.f - __powf(b1, (float)(it + 1)), bc2 = 1.f - __powf(b2, (float)(it + 1));
-  for (int i = lo + threadIdx.x; i < hi; i += kThreads) {
+  const int c = threadIdx.x & 127, q = threadIdx.x >> 7;
+  for (int base = lo; base < hi; base += 128) {
+    const int i = base + c;
     float g = 0.f;
-    for (int k = 0; k < a.G; ++k) g += a.slab[(size_t)k * a.P + i];
-    const float m = b1 * a.m[i] + (1.f - b1) * g;
-    const float v = b2 * a.v[i] + (1.f - b2) * g * g;
-    a.m[i] = m;
-    a.v[i] = v;
-    a.params[i] -= lr * (m / bc1) / (sqrtf(v / bc2) + 1e-8f);
+    if (i < hi) {
+#pragma unroll 8
+      for (int k = q; k < a.G; k += 4) g += a.slab[(size_t)k * a.P + i];
+    }
+    part[q][c] = g;
+    __syncthreads();
+    if (q == 0 && i < hi) {
+      g = (part[0][c] + part[1][c]) + (part[2][c] + part[3][c]);
+      const float m = b1 * a.m[i] + (1.f - b1) * g;
+      const float v = b2 * a.v[i] + (1.f - b2) * g * g;
+      a.m[i] = m;
+      a.v[i] = v;
+      a.params[i] -= lr * (m / bc1) / (sqrtf(v / bc2) + 1e-8f);
+    }
+    __syncthreads();
   }
 }
 
