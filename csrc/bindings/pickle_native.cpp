@@ -14,13 +14,17 @@
 //   * ``pickle_dumps(obj, bytes_as_u8_list)``: the writer serde_pickle uses (protocol 3, no
 //     memo; lists in APPENDS chunks of 1000), byte-identical to serde_pickle.dumps; with
 //     ``bytes_as_u8_list`` a bytes object is written as a list of u8 ints (Vec<u8>).
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
+#include <cmath>
 #include <cstring>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
 #include <vector>
+
+#include "codec.h"
 
 namespace py = pybind11;
 
@@ -396,6 +400,190 @@ void dump(const py::handle& o, std::string& out, int depth, bool bytes_u8) {
   }
 }
 
+// ------------------------------------------------------------------ reference frame -> columns
+// serde enum in any serde_pickle representation -> (variant, payload) (serde_pickle.enum_variant)
+std::pair<std::string, py::object> variant(const py::handle& v) {
+  if (py::isinstance<py::str>(v)) return {v.cast<std::string>(), py::none()};
+  if (py::isinstance<py::dict>(v)) {
+    py::dict d = py::reinterpret_borrow<py::dict>(v);
+    if (d.size() == 1)
+      for (auto kv : d) return {py::str(kv.first).cast<std::string>(), py::reinterpret_borrow<py::object>(kv.second)};
+  }
+  if (py::isinstance<py::tuple>(v) || py::isinstance<py::list>(v)) {
+    py::sequence q = py::reinterpret_borrow<py::sequence>(v);
+    if ((q.size() == 1 || q.size() == 2) && py::isinstance<py::str>(q[0]))
+      return {q[0].cast<std::string>(), q.size() == 2 ? py::object(q[1]) : py::object(py::none())};
+  }
+  throw FrameError("not an enum value");
+}
+
+std::string byte_payload(const py::handle& data) {
+  if (py::isinstance<py::bytearray>(data)) {
+    return std::string(PyByteArray_AsString(data.ptr()), (size_t)PyByteArray_Size(data.ptr()));
+  }
+  if (py::isinstance<py::bytes>(data)) return data.cast<std::string>();
+  if (py::isinstance<py::list>(data) || py::isinstance<py::tuple>(data)) {
+    py::sequence q = py::reinterpret_borrow<py::sequence>(data);
+    std::string out(q.size(), '\0');
+    for (size_t i = 0; i < q.size(); ++i) {
+      const long v = q[i].cast<long>();
+      if (v < 0 || v > 255) throw FrameError("TensorData.data must be bytes or a list of u8");
+      out[i] = (char)v;
+    }
+    return out;
+  }
+  throw FrameError("TensorData.data must be bytes or a list of u8");
+}
+
+// TensorData {shape, dtype, data: one-tensor safetensors file} -> float32 values; false if None
+bool tensor_f32(const py::handle& td, std::vector<float>& out) {
+  if (td.is_none()) return false;
+  if (!py::isinstance<py::dict>(td)) throw FrameError("TensorData must be a dict with shape / dtype / data");
+  py::dict d = py::reinterpret_borrow<py::dict>(td);
+  if (!d.contains("data")) throw FrameError("TensorData must be a dict with shape / dtype / data");
+  rrl::Tensor t;
+  try {
+    t = rrl::st_decode(byte_payload(d["data"]));
+  } catch (const std::exception& e) {
+    throw FrameError(std::string("TensorData: ") + e.what());
+  }
+  const int64_t n = t.numel();
+  out.resize((size_t)n);
+  const char* r = t.raw.data();
+  for (int64_t i = 0; i < n; ++i) {
+    switch (t.dtype) {
+      case rrl::DType::Byte: out[i] = (float)(uint8_t)r[i]; break;
+      case rrl::DType::Bool: out[i] = r[i] ? 1.f : 0.f; break;
+      case rrl::DType::Short: { int16_t v; std::memcpy(&v, r + 2 * i, 2); out[i] = (float)v; break; }
+      case rrl::DType::Int: { int32_t v; std::memcpy(&v, r + 4 * i, 4); out[i] = (float)v; break; }
+      case rrl::DType::Long: { int64_t v; std::memcpy(&v, r + 8 * i, 8); out[i] = (float)v; break; }
+      case rrl::DType::Float: { float v; std::memcpy(&v, r + 4 * i, 4); out[i] = v; break; }
+      case rrl::DType::Double: { double v; std::memcpy(&v, r + 8 * i, 8); out[i] = (float)v; break; }
+    }
+  }
+  return true;
+}
+
+// one column of per-action vectors (all present rows must have the same length)
+struct Col {
+  std::vector<float> vals;
+  std::vector<uint8_t> has;
+  long width = -1;
+  void add(bool present, const std::vector<float>& v) {
+    has.push_back(present ? 1 : 0);
+    if (present) {
+      if (width < 0) {
+        width = (long)v.size();
+        // earlier absent rows: zero-filled at the new width
+        vals.assign((has.size() - 1) * (size_t)width, 0.f);
+      } else if ((long)v.size() != width) {
+        throw FrameError("ragged tensors in one frame");
+      }
+      vals.insert(vals.end(), v.begin(), v.end());
+    } else if (width >= 0) {
+      vals.insert(vals.end(), (size_t)width, 0.f);
+    }
+  }
+  py::object array(size_t n, float fill) const {
+    if (width < 0) return py::none();
+    py::array_t<float> a({(py::ssize_t)n, (py::ssize_t)width});
+    float* p = a.mutable_data();
+    std::memcpy(p, vals.data(), vals.size() * sizeof(float));
+    for (size_t i = 0; i < n; ++i)
+      if (!has[i])
+        for (long k = 0; k < width; ++k) p[i * width + k] = fill;
+    return std::move(a);
+  }
+};
+
+template <class T>
+py::array_t<T> vec_array(const std::vector<T>& v) {
+  py::array_t<T> a((py::ssize_t)v.size());
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+  return a;
+}
+
+// serde_pickle(Vec<RelayRLAction>) (or a RelayRLTrajectory struct) straight to float32 columns:
+// the per-action objects of serde_pickle.actions_from_reference are never built.
+py::dict reference_columns(const py::bytes& frame) {
+  py::object root = loads(frame, true);
+  if (py::isinstance<py::dict>(root)) {
+    py::dict d = root.cast<py::dict>();
+    if (d.contains("actions")) root = d["actions"];
+  }
+  if (py::isinstance<py::bytearray>(root) && PyByteArray_Size(root.ptr()) == 0) root = py::list();
+  if (!py::isinstance<py::list>(root) && !py::isinstance<py::tuple>(root)) throw FrameError("expected a list of actions");
+  py::sequence acts = py::reinterpret_borrow<py::sequence>(root);
+  const size_t n = acts.size();
+  Col obs, act, mask;
+  std::vector<float> rew, logp, v, tmp;
+  std::vector<uint8_t> done, has_logp, has_v;
+  rew.reserve(n);
+  for (size_t i = 0; i < n; ++i) {
+    py::handle a = acts[i];
+    if (!py::isinstance<py::dict>(a)) throw FrameError("an action must be a dict");
+    py::dict ad = py::reinterpret_borrow<py::dict>(a);
+    auto field = [&](const char* k) -> py::object { return ad.contains(k) ? py::object(ad[k]) : py::object(py::none()); };
+    bool p = tensor_f32(field("obs"), tmp);
+    obs.add(p, tmp);
+    p = tensor_f32(field("act"), tmp);
+    act.add(p, tmp);
+    p = tensor_f32(field("mask"), tmp);
+    mask.add(p, tmp);
+    py::object r = field("rew");
+    rew.push_back(r.is_none() ? 0.f : r.cast<float>());
+    py::object dn = field("done");
+    done.push_back(!dn.is_none() && dn.cast<bool>() ? 1 : 0);
+    float lp = NAN, vv = NAN;
+    uint8_t hl = 0, hv = 0;
+    py::object data = field("data");
+    if (!data.is_none()) {
+      if (!py::isinstance<py::dict>(data)) throw FrameError("RelayRLAction.data must be a dict");
+      for (auto kv : data.cast<py::dict>()) {
+        const std::string key = py::str(kv.first).cast<std::string>();
+        if (key != "logp_a" && key != "v") continue;
+        auto var = variant(kv.second);
+        float x = NAN;
+        if (var.first == "Tensor") {
+          if (!tensor_f32(var.second, tmp) || tmp.empty()) continue;
+          x = tmp[0];
+        } else if (var.first == "Float" || var.first == "Double" || var.first == "Int" || var.first == "Long" ||
+                   var.first == "Short" || var.first == "Byte") {
+          x = var.second.cast<float>();
+        } else {
+          continue;
+        }
+        if (key == "logp_a") {
+          lp = x;
+          hl = 1;
+        } else {
+          vv = x;
+          hv = 1;
+        }
+      }
+    }
+    logp.push_back(lp);
+    has_logp.push_back(hl);
+    v.push_back(vv);
+    has_v.push_back(hv);
+  }
+  py::dict out;
+  out["n"] = n;
+  out["obs"] = obs.array(n, 0.f);
+  out["has_obs"] = vec_array(obs.has);
+  out["act"] = act.array(n, 0.f);
+  out["has_act"] = vec_array(act.has);
+  out["mask"] = mask.array(n, 1.f);
+  out["has_mask"] = vec_array(mask.has);
+  out["rew"] = vec_array(rew);
+  out["done"] = vec_array(done);
+  out["logp"] = vec_array(logp);
+  out["has_logp"] = vec_array(has_logp);
+  out["v"] = vec_array(v);
+  out["has_v"] = vec_array(has_v);
+  return out;
+}
+
 }  // namespace
 
 void bind_pickle(py::module_& m) {
@@ -421,4 +609,16 @@ void bind_pickle(py::module_& m) {
         return py::bytes(out);
       },
       py::arg("obj"), py::arg("bytes_as_u8_list") = false, "serde_pickle-style writer (protocol 3, no memo)");
+  m.def(
+      "reference_columns",
+      [](const py::bytes& b) {
+        try {
+          return reference_columns(b);
+        } catch (const FrameError& e) {
+          PyErr_SetString(frame_error.ptr(), e.what());
+          throw py::error_already_set();
+        }
+      },
+      py::arg("frame"),
+      "serde_pickle(Vec<RelayRLAction>) -> float32 columns (obs/act/mask, rew, done, logp, v + presence flags)");
 }

@@ -21,7 +21,7 @@ from ..ops import FwdMode, mlp_forward, scan_flat
 from ..utils.logger import EpochLogger, setup_logger_kwargs
 from .base import AlgorithmAbstract
 from .learner import PGLearner
-from ..types import TrajectoryColumns
+from ..types import ReferenceColumns, TrajectoryColumns
 
 
 class FlatBuffer:
@@ -65,8 +65,9 @@ class FlatBuffer:
         self.done[i] = 0.0
         self.ptr += 1
 
-    def store_block(self, obs, act, mask, rew, logp=None) -> int:
-        """Append up to ``len(rew)`` rows at once (columnar RRLC uploads); returns rows stored."""
+    def store_block(self, obs, act, mask, rew, logp=None, has_logp=None) -> int:
+        """Append up to ``len(rew)`` rows at once (columnar uploads); returns rows stored.
+        ``has_logp`` (per row) marks which rows carry a log-prob (reference uploads)."""
         i = self.ptr
         n = min(int(rew.shape[0]), self.size - i)
         if n <= 0:
@@ -81,7 +82,7 @@ class FlatBuffer:
         self.rew[sl] = rew[:n]
         if logp is not None:
             self.logp[sl] = logp[:n]
-        self.has_logp[sl] = logp is not None
+        self.has_logp[sl] = (logp is not None) if has_logp is None else has_logp[:n]
         self.done[sl] = 0.0
         self.has_boot_obs[sl] = False
         self.ptr += n
@@ -161,8 +162,48 @@ class EpisodeIngest:
     def add(self, trajectory) -> None:
         if isinstance(trajectory, TrajectoryColumns):
             self._columns(trajectory)
+        elif isinstance(trajectory, ReferenceColumns):
+            self._reference_columns(trajectory)
         else:
             self._actions(trajectory)
+
+    def _reference_columns(self, c) -> None:
+        """``_actions`` on natively decoded reference rows, a run of action rows at a time: a
+        run ends at a terminal marker (no observation) or after a done row."""
+        buf = self.buffer
+        n = len(c)
+        has_obs = c.has_obs.astype(bool)
+        done = c.done.astype(bool)
+        stops = np.flatnonzero(~has_obs | done)  # markers and done rows end runs
+        last_done = None  # done flag of the last stored row (None: nothing stored)
+        i = 0
+        while i < n:
+            if not has_obs[i]:  # reference terminal marker: its reward is the path's bootstrap
+                if done[i]:
+                    self.ep_ret += float(c.rew[i])
+                    self.end_episode(terminal=False, boot_value=float(c.rew[i]))
+                i += 1
+                continue
+            if buf.full():
+                break
+            k_stop = stops[np.searchsorted(stops, i)] if len(stops) and stops[-1] >= i else n
+            j = k_stop + 1 if (k_stop < n and has_obs[k_stop]) else k_stop  # a done row belongs to its run
+            seg = slice(i, j)
+            act = c.act[seg] if c.act is not None else np.zeros((j - i, 1), np.float32)  # no action: 0
+            k = buf.store_block(c.obs[seg], act, None if c.mask is None else c.mask[seg], c.rew[seg], c.logp[seg],
+                                has_logp=c.has_logp[seg].astype(bool))
+            self.steps += k
+            self.ep_ret += float(c.rew[i:i + k].sum())
+            self.ep_len += k
+            if k:
+                last_done = bool(done[i + k - 1])
+            if k < j - i:
+                break  # buffer full
+            if done[j - 1]:
+                self.end_episode(terminal=True)
+            i = j
+        if last_done is False and buf.ptr > buf.path_start:
+            buf.finish_path(terminal=False)  # truncated segment: bootstrap from V(s_last)
 
     def _columns(self, c) -> None:
         buf = self.buffer

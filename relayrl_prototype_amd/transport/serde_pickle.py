@@ -373,6 +373,43 @@ def reference_frame(actions) -> bytes:
     return dumps(out)
 
 
+class ColumnDeduper:
+    """CumulativeDeduper for natively decoded reference uploads (types.ReferenceColumns): the
+    same rule -- an upload that strictly extends a remembered one whose last row is done keeps
+    only its new rows -- with the digests taken over the float32 columns of the rows."""
+
+    def __init__(self, capacity: int = 4096):
+        self.capacity = capacity
+        self._seen: "OrderedDict[bytes, Tuple[int, bytes]]" = OrderedDict()
+        self.stripped = 0
+
+    @staticmethod
+    def _digest(c, k: int) -> bytes:
+        h = hashlib.blake2b(digest_size=16)
+        for a in (c.has_obs, c.obs, c.has_act, c.act, c.rew, c.done):
+            if a is not None:
+                h.update(a[:k].tobytes())
+        return h.digest()
+
+    def new_rows(self, c):
+        n = len(c)
+        if n == 0:
+            return c
+        head = self._digest(c, 1)
+        prev = self._seen.get(head)
+        keep = c
+        if prev is not None:
+            n_prev, dig = prev
+            if n > n_prev and c.done[n_prev - 1] and self._digest(c, n_prev) == dig:
+                keep = c.tail(n_prev)
+                self.stripped += n_prev
+        self._seen[head] = (n, self._digest(c, n))
+        self._seen.move_to_end(head)
+        while len(self._seen) > self.capacity:
+            self._seen.popitem(last=False)
+        return keep
+
+
 class CumulativeDeduper:
     """Reference agents re-send every earlier episode with each upload (the trajectory is
     only cleared at max_length, trajectory.rs:160-204), each over a NEW connection, so the

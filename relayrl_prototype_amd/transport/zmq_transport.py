@@ -28,7 +28,7 @@ from typing import Callable, Optional
 
 from .. import _native
 from ..runtime.model_store import ModelBlob
-from ..types import RelayRLTrajectory, TrajectoryColumns
+from ..types import ReferenceColumns, RelayRLTrajectory, TrajectoryColumns
 
 FMT_TORCHSCRIPT = b"TORCHSCRIPT"
 FMT_RRLM = b"RRLM"
@@ -42,13 +42,14 @@ def make_agent_id() -> str:
 class ZmqTrainingEndpoint:
     def __init__(self, service, agent_listener: str, trajectory_server: str, multiactor: bool = True,
                  verbose: bool = False, model_push_addr: Optional[str] = None):
-        from .serde_pickle import CumulativeDeduper
+        from .serde_pickle import ColumnDeduper, CumulativeDeduper
 
         self.service = service
         self.model_push_addr = model_push_addr
         self.ref_agents = set()   # identities that did the reference handshake
         self._model_push = None   # PUSH -> reference agents' bound PULL (lazy)
         self.dedupe = CumulativeDeduper()
+        self.dedupe_cols = ColumnDeduper()
         self.reference_frames = 0
         self.multiactor = multiactor
         self.verbose = verbose
@@ -157,9 +158,14 @@ class ZmqTrainingEndpoint:
         if TrajectoryColumns.is_frame(f):
             return TrajectoryColumns.decode(f)
         if serde_pickle.is_pickle_frame(f):
-            acts = self.dedupe.new_actions(serde_pickle.actions_from_reference(serde_pickle.loads_fast(f)))
             self.reference_frames += 1
             self._touch_reference_agents()
+            try:  # natively, straight to columns (rows of a consistent shape)
+                rows = self.dedupe_cols.new_rows(ReferenceColumns.decode(f))
+                return rows if len(rows) else None
+            except ValueError:  # ragged tensors / unusual encodings: the per-action path
+                pass
+            acts = self.dedupe.new_actions(serde_pickle.actions_from_reference(serde_pickle.loads_fast(f)))
             if not acts:
                 return None
             t = RelayRLTrajectory(max(len(acts), 1), None, "reference-agent")

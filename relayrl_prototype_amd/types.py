@@ -430,6 +430,66 @@ class TrajectoryColumns:
         return t
 
 
+class ReferenceColumns:
+    """A reference agent's upload (serde_pickle(Vec<RelayRLAction>), trajectory.rs:50-90) decoded
+    natively into float32 columns (csrc/bindings/pickle_native.cpp ``reference_columns``): the
+    action rows, the reference's terminal markers (rows without an observation,
+    agent_zmq.rs:605-610) kept in place as ``has_obs == 0``.  EpisodeIngest applies the
+    per-action semantics of the actions path to whole runs of rows at once; ``get_actions()``
+    materialises RelayRLAction objects for plugin algorithms that want them.  Reference
+    uploads carry no agent identity (a new connection per upload)."""
+
+    _COLS = ("n", "obs", "has_obs", "act", "has_act", "mask", "has_mask", "rew", "done", "logp", "has_logp", "v",
+             "has_v")
+    __slots__ = _COLS + ("agent_id", "seq", "trajectory_server")
+
+    def __init__(self, cols: dict):
+        for k in self._COLS:
+            setattr(self, k, cols[k])
+        self.agent_id = "reference-agent"  # the upload's connection carries no identity
+        self.seq = 0
+        self.trajectory_server = None
+
+    @staticmethod
+    def decode(frame: bytes) -> "ReferenceColumns":
+        return ReferenceColumns(_native.reference_columns(bytes(frame)))
+
+    def __len__(self):
+        return int(self.n)
+
+    def tail(self, start: int) -> "ReferenceColumns":
+        """Rows [start, n) (the deduper strips a re-sent prefix)."""
+        d = {}
+        for k in self._COLS[1:]:
+            a = getattr(self, k)
+            d[k] = None if a is None else a[start:]
+        d["n"] = max(0, int(self.n) - start)
+        return ReferenceColumns(d)
+
+    @property
+    def actions(self) -> List["RelayRLAction"]:
+        """RelayRLTrajectory's attribute view (materialised on each access)."""
+        return self.get_actions()
+
+    def get_actions(self) -> List["RelayRLAction"]:
+        out = []
+        for i in range(len(self)):
+            def row(a, h):
+                return None if a is None or not h[i] else a[i].copy()
+
+            data = None
+            if self.has_logp[i] or self.has_v[i]:
+                data = {}
+                if self.has_logp[i]:
+                    data["logp_a"] = np.float32(self.logp[i])
+                if self.has_v[i]:
+                    data["v"] = np.float32(self.v[i])
+            out.append(RelayRLAction(row(self.obs, self.has_obs), row(self.act, self.has_act),
+                                     row(self.mask, self.has_mask), float(self.rew[i]), data, bool(self.done[i]),
+                                     False))
+        return out
+
+
 class EpisodeRecorder:
     """Preallocated per-agent episode columns; one row written per ``request_for_action``."""
 

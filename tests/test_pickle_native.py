@@ -132,3 +132,104 @@ def test_native_decode_is_much_faster():
         sp.loads_fast(f)
     t_nat = (time.perf_counter() - t0) / 50
     assert t_nat * 20 < t_py, (t_nat, t_py)
+
+
+# ---------------------------------------------------------------- reference frames -> columns
+def _ref_episode(rng, n, marker_done=True, logp=True, mask=True, dtype=np.float32, truncated=False):
+    acts = []
+    for i in range(n):
+        data = {}
+        if logp and rng.random() > 0.1:
+            data["logp_a"] = np.array([rng.normal()], np.float32)
+        if rng.random() > 0.5:
+            data["v"] = np.array([rng.normal()], np.float32)
+        done = (i == n - 1) and not truncated and rng.random() < 0.3  # some episodes end on the action
+        acts.append(RelayRLAction(rng.normal(size=4).astype(dtype), np.array([float(rng.integers(0, 2))], np.float32),
+                                  np.ones(2, np.float32) if mask else None, float(rng.normal()), data or None, done,
+                                  True))
+    if not truncated:
+        acts.append(RelayRLAction(None, None, None, float(rng.normal()), None, marker_done, False))
+    return acts
+
+
+def _ingest(traj, size=10 ** 4):
+    from relayrl_prototype_amd.algorithms.trajectory_algo import EpisodeIngest, FlatBuffer
+
+    buf = FlatBuffer(4, 2, size, True)
+    ing = EpisodeIngest(buf)
+    for t in traj:
+        ing.add(t)
+    n = buf.ptr
+    return {"ptr": n, "path_start": buf.path_start, "steps": ing.steps, "finished": ing.pop_finished(),
+            "obs": buf.obs[:n].copy(), "act": buf.act[:n].copy(), "mask": buf.mask[:n].copy(),
+            "rew": buf.rew[:n].copy(), "logp": np.where(buf.has_logp[:n], buf.logp[:n], 0).copy(),
+            "has_logp": buf.has_logp[:n].copy(), "done": buf.done[:n].copy(),
+            "boot": np.nan_to_num(buf.boot[:n], nan=-12345.0).copy(), "ep": (ing.ep_ret, ing.ep_len)}
+
+
+@pytest.mark.parametrize("size", [10 ** 4, 37])  # 37: the buffer fills in the middle of an upload
+@pytest.mark.parametrize("seed", range(6))
+def test_reference_columns_ingest_equals_the_action_path(seed, size):
+    from relayrl_prototype_amd.types import ReferenceColumns, RelayRLTrajectory
+
+    rng = np.random.default_rng(seed)
+    frames = []
+    for e in range(5):
+        acts = []
+        for _ in range(int(rng.integers(1, 3))):  # cumulative-style uploads with several episodes
+            acts += _ref_episode(rng, int(rng.integers(1, 12)), marker_done=rng.random() > 0.2,
+                                 logp=seed % 3 != 0, mask=seed % 2 == 0, truncated=(e == 4 and seed % 2 == 1),
+                                 dtype=np.float64 if seed == 5 else np.float32)
+        frames.append(sp.reference_frame(acts))
+    via_actions = []
+    for f in frames:
+        t = RelayRLTrajectory(10 ** 6, None, "reference-agent")
+        t.actions = sp.actions_from_reference(sp.loads(f))
+        via_actions.append(t)
+    a = _ingest(via_actions, size)
+    b = _ingest([ReferenceColumns.decode(f) for f in frames], size)
+    assert a["ptr"] == b["ptr"] and a["path_start"] == b["path_start"] and a["steps"] == b["steps"]
+    np.testing.assert_allclose(np.array(a["finished"], np.float64).reshape(-1, 2),
+                               np.array(b["finished"], np.float64).reshape(-1, 2), rtol=1e-6, atol=1e-5)
+    np.testing.assert_allclose(np.array(a["ep"]), np.array(b["ep"]), rtol=1e-6, atol=1e-5)
+    for k in ("obs", "act", "mask", "rew", "logp", "has_logp", "done", "boot"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_reference_columns_get_actions_and_dedupe():
+    from relayrl_prototype_amd.types import ReferenceColumns
+
+    rng = np.random.default_rng(9)
+    ep1 = _ref_episode(rng, 5)
+    ep2 = _ref_episode(rng, 3)
+    c1 = ReferenceColumns.decode(sp.reference_frame(ep1))
+    ref = sp.actions_from_reference(sp.loads(sp.reference_frame(ep1)))
+    got = c1.get_actions()
+    assert len(got) == len(ref)
+    for x, y in zip(got, ref):
+        for fx, fy in ((x.get_obs(), y.get_obs()), (x.get_act(), y.get_act()), (x.get_mask(), y.get_mask())):
+            assert (fx is None) == (fy is None)
+            if fx is not None:
+                np.testing.assert_array_equal(np.asarray(fx, np.float32).reshape(-1), np.asarray(fy).reshape(-1))
+        assert x.get_rew() == pytest.approx(y.get_rew()) and x.get_done() == y.get_done()
+        lx, ly = (x.get_data() or {}).get("logp_a"), (y.get_data() or {}).get("logp_a")
+        assert (lx is None) == (ly is None)
+        if lx is not None:
+            assert float(np.asarray(lx).reshape(-1)[0]) == pytest.approx(float(np.asarray(ly).reshape(-1)[0]))
+    d = sp.ColumnDeduper()
+    assert len(d.new_rows(c1)) == len(c1)
+    c12 = ReferenceColumns.decode(sp.reference_frame(ep1 + ep2))  # the reference re-sends ep1 with ep2
+    kept = d.new_rows(c12)
+    assert len(kept) == len(ep2) and d.stripped == len(ep1)
+    np.testing.assert_array_equal(kept.rew, c12.rew[len(ep1):])
+
+
+def test_native_column_decode_speed():
+    from relayrl_prototype_amd.types import ReferenceColumns
+
+    f = sp.reference_frame(_episode(25, np.random.default_rng(4)))
+    t0 = time.perf_counter()
+    for _ in range(200):
+        ReferenceColumns.decode(f)
+    t = (time.perf_counter() - t0) / 200
+    assert t < 2e-3, t  # ~19 ms through the Python interpreter + per-action objects
