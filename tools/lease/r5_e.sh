@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 5, lease E: the GPU suite after the native reference-frame path, then the reference-wire
+# fan-in rows against the GPU learner.
+cd "$(dirname "$0")/../.."
+mkdir -p gpurun_out
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread \
+    > gpurun_out/r5e_gpu_tests.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/r5e_gpu_tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 400 python -u benchmarks/fanin_bench.py --agents 16 64 --transports zmq-ref --seconds 10 \
+    --out gpurun_out/r5e_fanin.jsonl > gpurun_out/r5e_fanin.log 2>&1 || exit $?
+exit $rc
