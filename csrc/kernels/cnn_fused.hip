@@ -348,6 +348,232 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
   }
 }
 
+// ============================================================================= 16-wave forward
+// The same conv stack as a THREE-stage layer pipeline over 16 waves (4 per SIMD):
+//   waves 0-7   conv1 of frame n_j        (both co tiles, pixel tiles w + 8 t)
+//   waves 8-11  conv2 of frame n_{j-1}    (co tile w - 8, all 6 pixel tiles)
+//   waves 12-15 conv3 of frame n_{j-2}    (co tile w - 12, all 4 pixel tiles)
+// all between the same two barriers, so every SIMD holds two conv1 waves, one conv2 and one
+// conv3 wave and interleaves their MFMAs and LDS reads (conv_stack_fwd_kernel above has two
+// waves per SIMD and runs conv1 alone between its own barriers).  What makes it fit:
+//   * the frame stays uint8 in LDS (55.8 KB instead of 93 KB as bf16): each lane reads 16
+//     channels of one position per tap (ONE ds_read_b128 feeds both k-steps of the tap: lane
+//     group g carries channels 16 g + 8 h .. + 7 in k-step h, the weight fragments use the same
+//     order) and widens them to bf16 in registers -- exact, 0..255 fit the bf16 mantissa;
+//     96-byte position rows make those reads conflict-free (tools/lds_bank_model.py --fwd16);
+//   * a1 / a2 double-buffered (stage j writes one buffer while stage j + 1 reads the other);
+//   * a1 / a2 / a3 leave for HBM straight from the epilogue registers (8 bytes per lane), so
+//     no copy-out pass reads LDS and a3 needs no LDS image at all;
+//   * one fragment array serves every role's stationary weights (72 VGPRs: conv3's 18 k-steps;
+//     conv1 uses 16, conv2 16), each role's tiles in passes small enough for 128 registers.
+// Per iteration j: B0 | frame n_j: registers -> LDS, next frame's loads issued | B1 | the
+// three stages.  j runs two frames past this workgroup's last one to drain conv2 / conv3.
+#ifndef CS16_C2_MT
+#define CS16_C2_MT 2
+#endif
+#ifndef CS16_C3_MT
+#define CS16_C3_MT 2
+#endif
+namespace cs16 {
+constexpr int kThreads = 1024;
+constexpr int kFW = 28;                       // frame positions per LDS row group (as cs::kFrameW)
+constexpr int kFS = 96;                       // bytes per frame position: 64 channels + 32 pad
+constexpr int kFRows = 20 * kFW + 21;         // last position read: (20, 20)
+constexpr int kFBytes = kFRows * kFS;         // 55,776
+constexpr int kA1Ld = 40, kA2Ld = 80;         // bf16 row strides (as the 8-wave kernel)
+constexpr int kA1Elems = 400 * kA1Ld, kA2Elems = 81 * kA2Ld;
+constexpr int kA1Off = kFBytes;               // byte offsets
+constexpr int kA2Off = kA1Off + 2 * kA1Elems * 2;
+constexpr int kLds = kA2Off + 2 * kA2Elems * 2;  // 145,696 bytes
+constexpr int kXChunks = 441 * 4;              // 16-byte chunks of one uint8 frame
+constexpr int kXPerT = (kXChunks + kThreads - 1) / kThreads;
+static_assert(kLds <= 160 * 1024, "LDS per workgroup");
+static_assert(kA1Off % 16 == 0 && kA2Off % 16 == 0, "16-byte aligned LDS regions");
+}  // namespace cs16
+
+__device__ __forceinline__ bf16x8_t u8x8_frag(uint32_t lo, uint32_t hi) {
+  return __builtin_bit_cast(bf16x8_t, u8x8_to_bf16x8(make_uint2(lo, hi)));
+}
+
+struct Stack16Args {
+  const uint8_t* x;
+  const uint16_t *w1, *w2, *w3;
+  const float *b1, *b2, *b3;
+  uint16_t *y1, *y2, *y3;
+  int N;
+};
+
+// One role's whole loop (stationary weights, per-iteration stage), so each role's registers are
+// allocated on their own; every role meets the same two barriers per iteration.
+template <int ROLE>
+__device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* smem, int tid, int wave) {
+  using namespace cs16;
+  uint8_t* F = reinterpret_cast<uint8_t*>(smem);
+  const int lane = tid & 63, i = lane & 15, g = lane >> 4;
+  const int ct = wave & 3;  // co tile of conv2 / conv3
+  // stationary weights, A fragments W[co = 16 tile + i][8 consecutive k]:
+  //   conv1 fw[8 c + 2 tap + h] = W1[16 c + i][64 tap + 16 g + 8 h ..]; conv2 / conv3 fw[ks] = W[..][32 ks + 8 g ..]
+  constexpr int NF = ROLE == 3 ? 18 : 16;
+  bf16x8_t fw[NF];
+  f32x4_t bias0, bias1;
+  if constexpr (ROLE == 1) {
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+        fw[8 * c + ks] = *reinterpret_cast<const bf16x8_t*>(A.w1 + (16 * c + i) * 256 + 64 * (ks >> 1) + 16 * g + 8 * (ks & 1));
+    bias0 = *reinterpret_cast<const f32x4_t*>(A.b1 + 4 * g);
+    bias1 = *reinterpret_cast<const f32x4_t*>(A.b1 + 16 + 4 * g);
+  } else {
+    const uint16_t* w = ROLE == 2 ? A.w2 : A.w3;
+    constexpr int K = ROLE == 2 ? 512 : 576;
+#pragma unroll
+    for (int ks = 0; ks < NF; ++ks) fw[ks] = *reinterpret_cast<const bf16x8_t*>(w + (16 * ct + i) * K + 32 * ks + 8 * g);
+    bias0 = bias1 = *reinterpret_cast<const f32x4_t*>((ROLE == 2 ? A.b2 : A.b3) + 16 * ct + 4 * g);
+  }
+
+  const int G = gridDim.x, n0 = blockIdx.x, N = A.N;
+  uint4 rx[kXPerT];
+  auto gload = [&](size_t n) {
+    const uint4* xs = reinterpret_cast<const uint4*>(A.x + n * (441 * 64));
+#pragma unroll
+    for (int k = 0; k < kXPerT; ++k) {
+      const int q = tid + kThreads * k;
+      rx[k] = q < kXChunks ? xs[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  if (n0 < N) gload(n0);
+  for (int j = 0; n0 + (j - 2) * G < N; ++j) {
+    const int n = n0 + j * G;
+    __syncthreads();  // B0: the previous iteration's stages are done (F free, a1 / a2 buffers complete)
+    if (n < N) {
+#pragma unroll
+      for (int k = 0; k < kXPerT; ++k) {
+        const int q = tid + kThreads * k;
+        if (q < kXChunks) {
+          const int pix = q >> 2, pa = pix / 21;
+          *reinterpret_cast<uint4*>(F + (pix + (kFW - 21) * pa) * kFS + (q & 3) * 16) = rx[k];
+        }
+      }
+      if (n + G < N) gload((size_t)n + G);  // lands while this frame computes
+    }
+    __syncthreads();  // B1: F holds frame n
+    if constexpr (ROLE == 1) {
+      // ---- conv1(n): pixel tiles wave + 8 t, one tile at a time, both co tiles
+      if (n < N) {
+        uint16_t* A1c = smem + kA1Off / 2 + (j & 1) * kA1Elems;
+        const int ntile = wave == 0 ? 4 : 3;  // 25 tiles over 8 waves (wave-uniform)
+        for (int t = 0; t < ntile; ++t) {
+          const int p = 16 * (wave + 8 * t) + i;
+          const uint8_t* src = F + ((p / 20) * kFW + p % 20) * kFS + 16 * g;
+          f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int tap = 0; tap < 4; ++tap) {
+            const uint4 raw = *reinterpret_cast<const uint4*>(src + ((tap >> 1) * kFW + (tap & 1)) * kFS);
+            const bf16x8_t lo = u8x8_frag(raw.x, raw.y), hi = u8x8_frag(raw.z, raw.w);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[2 * tap], lo, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[8 + 2 * tap], lo, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[2 * tap + 1], hi, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[8 + 2 * tap + 1], hi, acc1, 0, 0, 0);
+          }
+          const uint2 v0 = make_uint2(pk_bf16(fmaxf(kU8Scale * acc0[0] + bias0[0], 0.f), fmaxf(kU8Scale * acc0[1] + bias0[1], 0.f)),
+                                      pk_bf16(fmaxf(kU8Scale * acc0[2] + bias0[2], 0.f), fmaxf(kU8Scale * acc0[3] + bias0[3], 0.f)));
+          const uint2 v1 = make_uint2(pk_bf16(fmaxf(kU8Scale * acc1[0] + bias1[0], 0.f), fmaxf(kU8Scale * acc1[1] + bias1[1], 0.f)),
+                                      pk_bf16(fmaxf(kU8Scale * acc1[2] + bias1[2], 0.f), fmaxf(kU8Scale * acc1[3] + bias1[3], 0.f)));
+          *reinterpret_cast<uint2*>(A1c + p * kA1Ld + 4 * g) = v0;
+          *reinterpret_cast<uint2*>(A1c + p * kA1Ld + 16 + 4 * g) = v1;
+          if (A.y1) {
+            uint16_t* yd = A.y1 + ((size_t)n * 400 + p) * 32;
+            *reinterpret_cast<uint2*>(yd + 4 * g) = v0;
+            *reinterpret_cast<uint2*>(yd + 16 + 4 * g) = v1;
+          }
+        }
+      }
+    } else if constexpr (ROLE == 2) {
+      // ---- conv2(n - G): co tile ct, 6 pixel tiles in passes (81 px; the rest discarded)
+      if (j >= 1 && n - G < N) {
+        const uint16_t* A1p = smem + kA1Off / 2 + ((j - 1) & 1) * kA1Elems;
+        uint16_t* A2c = smem + kA2Off / 2 + ((j - 1) & 1) * kA2Elems;
+        constexpr int MT = CS16_C2_MT;
+#pragma unroll
+        for (int pass = 0; pass < 6 / MT; ++pass) {
+          f32x4_t acc[MT];
+          int r0[MT];
+#pragma unroll
+          for (int u = 0; u < MT; ++u) {
+            acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            const int p = 16 * (MT * pass + u) + i, pc = p < 81 ? p : 0, oh = pc / 9, ow = pc - oh * 9;
+            r0[u] = 2 * oh * 20 + 2 * ow;
+          }
+#pragma unroll
+          for (int ks = 0; ks < 16; ++ks) {
+            const int off = ((ks >> 2) * 20 + (ks & 3)) * kA1Ld + 8 * g;
+            bf16x8_t a[MT];
+#pragma unroll
+            for (int u = 0; u < MT; ++u) a[u] = *reinterpret_cast<const bf16x8_t*>(A1p + r0[u] * kA1Ld + off);
+#pragma unroll
+            for (int u = 0; u < MT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks], a[u], acc[u], 0, 0, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < MT; ++u) {
+            const int p = 16 * (MT * pass + u) + i;
+            if (p < 81) {
+              const uint2 v = make_uint2(pk_bf16(fmaxf(acc[u][0] + bias0[0], 0.f), fmaxf(acc[u][1] + bias0[1], 0.f)),
+                                         pk_bf16(fmaxf(acc[u][2] + bias0[2], 0.f), fmaxf(acc[u][3] + bias0[3], 0.f)));
+              *reinterpret_cast<uint2*>(A2c + p * kA2Ld + 16 * ct + 4 * g) = v;
+              if (A.y2) *reinterpret_cast<uint2*>(A.y2 + ((size_t)(n - G) * 81 + p) * 64 + 16 * ct + 4 * g) = v;
+            }
+          }
+        }
+      }
+    } else {
+      // ---- conv3(n - 2G): co tile ct, 4 pixel tiles in passes (49 px), straight to HBM
+      if (j >= 2 && n - 2 * G < N) {
+        const uint16_t* A2p = smem + kA2Off / 2 + ((j - 2) & 1) * kA2Elems;
+        constexpr int MT = CS16_C3_MT;
+#pragma unroll
+        for (int pass = 0; pass < 4 / MT; ++pass) {
+          f32x4_t acc[MT];
+          int r0[MT];
+#pragma unroll
+          for (int u = 0; u < MT; ++u) {
+            acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            const int p = 16 * (MT * pass + u) + i, pc = p < 49 ? p : 0, oh = pc / 7, ow = pc - oh * 7;
+            r0[u] = oh * 9 + ow;
+          }
+#pragma unroll
+          for (int ks = 0; ks < 18; ++ks) {
+            const int tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
+            const int off = (kh * 9 + kw) * kA2Ld + 32 * (ks & 1) + 8 * g;
+            bf16x8_t a[MT];
+#pragma unroll
+            for (int u = 0; u < MT; ++u) a[u] = *reinterpret_cast<const bf16x8_t*>(A2p + r0[u] * kA2Ld + off);
+#pragma unroll
+            for (int u = 0; u < MT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks], a[u], acc[u], 0, 0, 0);
+          }
+#pragma unroll
+          for (int u = 0; u < MT; ++u) {
+            const int p = 16 * (MT * pass + u) + i;
+            if (p < 49)
+              *reinterpret_cast<uint2*>(A.y3 + ((size_t)(n - 2 * G) * 49 + p) * 64 + 16 * ct + 4 * g) =
+                  make_uint2(pk_bf16(fmaxf(acc[u][0] + bias0[0], 0.f), fmaxf(acc[u][1] + bias0[1], 0.f)),
+                             pk_bf16(fmaxf(acc[u][2] + bias0[2], 0.f), fmaxf(acc[u][3] + bias0[3], 0.f)));
+          }
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(cs16::kThreads, 1) void conv_stack16_fwd_kernel(Stack16Args args) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (wave < 8) stack16_role<1>(args, smem, tid, wave);
+  else if (wave < 12) stack16_role<2>(args, smem, tid, wave);
+  else stack16_role<3>(args, smem, tid, wave);
+}
+
 }  // namespace rrl
 
 using namespace rrl;
@@ -371,14 +597,46 @@ static int launch_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const flo
   return (int)hipGetLastError();
 }
 
+static int launch_conv_stack16_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
+                                   const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
+                                   uint16_t* y3, int N, int max_grid, hipStream_t stream) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_stack16_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              cs16::kLds);
+    attr = true;
+  }
+  if (N < 1) return 0;
+  const int grid = N < max_grid ? N : max_grid;  // one 146 KB-LDS workgroup per CU
+  const Stack16Args args{x, w1, w2, w3, b1, b2, b3, y1, y2, y3, N};
+  hipLaunchKernelGGL(conv_stack16_fwd_kernel, dim3(grid), dim3(cs16::kThreads), cs16::kLds, stream, args);
+  return (int)hipGetLastError();
+}
+
+// RRL_CONV_FWD = 8 / 16 picks the 8-wave or the 16-wave kernel (default below)
+static bool conv_fwd16() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("RRL_CONV_FWD");
+    v = (e && e[0]) ? (atoi(e) == 16) : 0;
+  }
+  return v == 1;
+}
+
 extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
                                   const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
                                   uint16_t* y3, int N, int max_grid, void* stream) {
-  // max_grid < 0: timing probe variant -max_grid >> 16 (tools/cnn_kbench.py), grid = -max_grid & 0xffff
+  // max_grid < 0: timing probe variant -max_grid >> 16 (tools/cnn_kbench.py), grid = -max_grid & 0xffff;
+  // probe 64 = the 16-wave kernel, probe 128 = the 8-wave kernel (whatever RRL_CONV_FWD says)
   hipStream_t st = (hipStream_t)stream;
-  if (max_grid >= 0) return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, max_grid, st);
+  if (max_grid >= 0) {
+    if (conv_fwd16()) return launch_conv_stack16_fwd(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, max_grid, st);
+    return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, max_grid, st);
+  }
   const int probe = (-max_grid) >> 16, g = (-max_grid) & 0xffff;
   switch (probe) {
+    case 64: return launch_conv_stack16_fwd(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 128: return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 1: return launch_conv_stack_fwd<1>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 2: return launch_conv_stack_fwd<2>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 3: return launch_conv_stack_fwd<3>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);

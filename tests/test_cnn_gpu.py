@@ -449,11 +449,12 @@ def test_sum_splits_matches_torch(cuda, splits, n):
     torch.testing.assert_close(out.cpu(), part.sum(0), rtol=1e-5, atol=1e-4)
 
 
+@pytest.mark.parametrize("variant", [128, 64], ids=["8wave", "16wave"])
 @pytest.mark.parametrize("N", [1, 5, 300, 2048])
-def test_fused_conv_stack_matches_per_layer_kernels(cuda, N):
-    """conv_stack_fwd (conv1 -> conv2 -> conv3 in one launch, cnn_fused.hip) against the
-    per-layer kernels it replaces (same k-step order: equal up to fma contraction) and the
-    bf16-emulating fp32 oracle."""
+def test_fused_conv_stack_matches_per_layer_kernels(cuda, N, variant):
+    """conv_stack_fwd (conv1 -> conv2 -> conv3 in one launch, cnn_fused.hip; the 8-wave kernel and
+    the 16-wave three-stage pipeline) against the per-layer kernels it replaces (equal up to fma
+    contraction / summation order) and the bf16-emulating fp32 oracle."""
     from relayrl_prototype_amd.ops import hip
 
     h = hip()
@@ -472,7 +473,7 @@ def test_fused_conv_stack_matches_per_layer_kernels(cuda, N):
         if fused:
             h.conv_stack_fwd(x, sh[o["w1"]:o["b1"]], params[o["b1"]:o["b1"] + 32], sh[o["w2"]:o["b2"]],
                              params[o["b2"]:o["b2"] + 64], sh[o["w3"]:o["b3"]], params[o["b3"]:o["b3"] + 64], a1, a2,
-                             a3, N)
+                             a3, N, probe=variant)
         else:
             from relayrl_prototype_amd.models.nature_cnn import S2D
 
@@ -817,7 +818,7 @@ def test_fused_conv_stack_layout_variants_are_bitwise_equal(cuda, probe):
     sh = params.bfloat16()
     x = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g).to(cuda)
     outs = []
-    for pr in (0, probe):
+    for pr in (128, probe):  # 128: the 8-wave kernel these layouts belong to
         a1 = torch.full((N * 400 * 32,), float("nan"), dtype=torch.bfloat16, device=cuda)
         a2 = torch.full((N * 81 * 64,), float("nan"), dtype=torch.bfloat16, device=cuda)
         a3 = torch.full((N * FC_IN,), float("nan"), dtype=torch.bfloat16, device=cuda)
@@ -829,6 +830,37 @@ def test_fused_conv_stack_layout_variants_are_bitwise_equal(cuda, probe):
     for f, r in zip(*outs):
         assert torch.isfinite(f.float()).all()
         assert torch.equal(f, r)
+
+
+@pytest.mark.parametrize("variant", [128, 64], ids=["8wave", "16wave"])
+def test_fused_conv_stack_without_stored_activations(cuda, variant):
+    """The bootstrap forward (no backward reads a1 / a2: y1 / y2 not written) leaves a3 bitwise
+    equal to the full forward's and the a1 / a2 buffers untouched -- both kernels, with frames
+    that do not divide the grid (workgroups with 2 and 3 frames, the pipeline drain)."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    spec = CNNSpec()
+    o = spec.offsets()
+    N = 700
+    g = torch.Generator().manual_seed(variant)
+    params = spec.init(variant).to(cuda)
+    params += 0.01 * torch.randn(params.shape, generator=g).to(cuda)
+    sh = params.bfloat16()
+    x = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g).to(cuda)
+    outs = []
+    for store12 in (True, False):
+        a1 = torch.full((N * 400 * 32,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        a2 = torch.full((N * 81 * 64,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        a3 = torch.full((N * FC_IN,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        h.conv_stack_fwd(x, sh[o["w1"]:o["b1"]], params[o["b1"]:o["b1"] + 32], sh[o["w2"]:o["b2"]],
+                         params[o["b2"]:o["b2"] + 64], sh[o["w3"]:o["b3"]], params[o["b3"]:o["b3"] + 64], a1, a2, a3,
+                         N, probe=variant, store12=store12)
+        torch.cuda.synchronize()
+        outs.append((a1, a2, a3))
+    assert torch.isfinite(outs[0][2].float()).all()
+    assert torch.equal(outs[0][2], outs[1][2])
+    assert torch.isnan(outs[1][0].float()).all() and torch.isnan(outs[1][1].float()).all()
 
 
 def test_conv2_bwd_dgrad_grids_are_bitwise_equal(cuda):

@@ -73,7 +73,7 @@ def main():
     fns["wgrad1_8"] = lambda: h.conv1_wgrad8(x[:Nb], da1, part, bpart, Nb, min(Nb, cus))
     fns["wgrad1"] = lambda: h.conv_wgrad(da1, x[:Nb], part, 256, Nb, 21, 21, 64, 2, 2, 1, 32, bpart)
     fns.update({"p_nomfma": probe(1), "p_nostore": probe(2), "p_nostore_nomfma": probe(3), "p_hotframe": probe(4),
-           "p_all": probe(7), "fwd_c1split": probe(8), "fwd_g128": probe(0, 128), "fwd_phase_a1": probe(16), "fwd_c3_grid": probe(32), "fwd_phase_a1_c3_grid": probe(48), "fwd_g512": probe(0, 512), "fwd": fwd, "fwd_layers": fwd_layers, "bwd3": bwd3, "bwd3_layers": bwd3_layers, "dgrad2": dgrad2})
+           "p_all": probe(7), "fwd_c1split": probe(8), "fwd_g128": probe(0, 128), "fwd_phase_a1": probe(16), "fwd_c3_grid": probe(32), "fwd_phase_a1_c3_grid": probe(48), "fwd_g512": probe(0, 512), "fwd8": probe(128), "fwd16": probe(64), "fwd": fwd, "fwd_layers": fwd_layers, "bwd3": bwd3, "bwd3_layers": bwd3_layers, "dgrad2": dgrad2})
     if hasattr(h, "conv2_bwd"):
         def bwd2():
             h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus))
