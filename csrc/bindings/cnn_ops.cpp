@@ -61,7 +61,7 @@ int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, co
                        const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2, uint16_t* y3, int N,
                        int max_grid, void* stream);
 int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
-                  float* bias_part, int N, int grid, void* stream);
+                  float* bias_part, int N, int grid, int variant, void* stream);
 int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
                   float* bias_part, int N, int grid, int staged, void* stream);
 int rrl_conv1_wgrad8(const uint8_t* x, const uint16_t* dy, float* part, float* bias_part, int N, int grid,
@@ -152,7 +152,7 @@ void conv_stack_fwd(const Tensor& x, const Tensor& w1, const Tensor& b1, const T
 // Fused conv3 backward (cnn_fused.hip): da3 [N][49][64], W3 [64][3][3][64], a2 [N][81][64] ->
 // da2 = dgrad * (a2 > 0), dW3 partials [grid][64 * 576], db3 partials [grid * 8][64].
 void conv3_bwd(const Tensor& dy, const Tensor& w, const Tensor& xact, const Tensor& dx, const Tensor& part,
-               const Tensor& bias_part, int64_t N, int64_t grid) {
+               const Tensor& bias_part, int64_t N, int64_t grid, int64_t variant) {
   TORCH_CHECK(N > 0 && grid > 0 && grid <= N, "conv3_bwd: need 0 < grid <= N");
   check(dy, "dy", at::kBFloat16, N * 49 * 64);
   check(w, "w", at::kBFloat16, 64 * 576);
@@ -161,7 +161,7 @@ void conv3_bwd(const Tensor& dy, const Tensor& w, const Tensor& xact, const Tens
   check(part, "part", at::kFloat, grid * 64 * 576);
   check(bias_part, "bias_part", at::kFloat, grid * 512);
   rc_check(rrl_conv3_bwd(bf(dy), bf(w), bf(xact), bf(dx), part.data_ptr<float>(), bias_part.data_ptr<float>(),
-                         (int)N, (int)grid, stream()),
+                         (int)N, (int)grid, (int)variant, stream()),
            "conv3_bwd");
 }
 
@@ -499,7 +499,9 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("w2"), pybind11::arg("b2"), pybind11::arg("w3"), pybind11::arg("b3"), pybind11::arg("y1"),
         pybind11::arg("y2"), pybind11::arg("y3"), pybind11::arg("N"), pybind11::arg("probe") = 0,
         pybind11::arg("grid") = 0, pybind11::arg("store12") = true);
-  m.def("conv3_bwd", &conv3_bwd);
+  m.def("conv3_bwd", &conv3_bwd, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("xact"), pybind11::arg("dx"),
+        pybind11::arg("part"), pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"),
+        pybind11::arg("variant") = 0);
   m.def("conv2_bwd", &conv2_bwd, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("xact"), pybind11::arg("dx"),
         pybind11::arg("part"), pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"),
         pybind11::arg("staged") = 0);

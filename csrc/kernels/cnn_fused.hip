@@ -380,15 +380,26 @@ constexpr int kFW = 28;                       // frame positions per LDS row gro
 constexpr int kFS = 96;                       // bytes per frame position: 64 channels + 32 pad
 constexpr int kFRows = 20 * kFW + 21;         // last position read: (20, 20)
 constexpr int kFBytes = kFRows * kFS;         // 55,776
-constexpr int kA1Ld = 40, kA2Ld = 80;         // bf16 row strides (as the 8-wave kernel)
-constexpr int kA1Elems = 400 * kA1Ld, kA2Elems = 81 * kA2Ld;
-constexpr int kA1Off = kFBytes;               // byte offsets
-constexpr int kA2Off = kA1Off + 2 * kA1Elems * 2;
-constexpr int kLds = kA2Off + 2 * kA2Elems * 2;  // 145,696 bytes
 constexpr int kXChunks = 441 * 4;              // 16-byte chunks of one uint8 frame
 constexpr int kXPerT = (kXChunks + kThreads - 1) / kThreads;
-static_assert(kLds <= 160 * 1024, "LDS per workgroup");
-static_assert(kA1Off % 16 == 0 && kA2Off % 16 == 0, "16-byte aligned LDS regions");
+// a1 / a2 images per layout V (the 8-wave kernel's FwdLayout bits): default -- a1 as one 20 x 20
+// image in 40-element rows, conv2 over its 81 output pixels (stride-2 reads: 2.0 LDS cycles per
+// conflict-free cycle in tools/lds_bank_model.py), conv3 over its 49; bit 16 -- a1 as four
+// stride-2 phase images in 48-element rows, conv2 over a 9 x 10 grid (1.0); bit 32 -- conv3
+// over a 7 x 9 grid of a2 (1.75 -> 1.0).  Discarded grid positions read past the image into rows
+// that stay inside their buffer (garbage in discarded outputs only).
+template <int V>
+struct L16 {
+  static constexpr bool kPhaseA1 = (V & 16) != 0, kGrid3 = (V & 32) != 0;
+  static constexpr int kA1Ld = kPhaseA1 ? 48 : 40, kA2Ld = 80;
+  static constexpr int kA1Rows = kPhaseA1 ? 407 : 400, kA2Rows = kGrid3 ? 84 : 81;
+  static constexpr int kA1Elems = kA1Rows * kA1Ld, kA2Elems = kA2Rows * kA2Ld;
+  static constexpr int kA1Off = kFBytes;         // byte offsets
+  static constexpr int kA2Off = kA1Off + 2 * kA1Elems * 2;
+  static constexpr int kLds = kA2Off + 2 * kA2Elems * 2;  // 145,696 bytes (default) .. 160,800 (bits 16 | 32)
+  static_assert(kLds <= 160 * 1024, "LDS per workgroup");
+  static_assert(kA1Off % 16 == 0 && kA2Off % 16 == 0, "16-byte aligned LDS regions");
+};
 }  // namespace cs16
 
 __device__ __forceinline__ bf16x8_t u8x8_frag(uint32_t lo, uint32_t hi) {
@@ -405,9 +416,12 @@ struct Stack16Args {
 
 // One role's whole loop (stationary weights, per-iteration stage), so each role's registers are
 // allocated on their own; every role meets the same two barriers per iteration.
-template <int ROLE>
+template <int ROLE, int V>
 __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* smem, int tid, int wave) {
   using namespace cs16;
+  using L = L16<V>;
+  constexpr int kA1Ld = L::kA1Ld, kA2Ld = L::kA2Ld, kA1Elems = L::kA1Elems, kA2Elems = L::kA2Elems;
+  constexpr int kA1Off = L::kA1Off, kA2Off = L::kA2Off;
   uint8_t* F = reinterpret_cast<uint8_t*>(smem);
   const int lane = tid & 63, i = lane & 15, g = lane >> 4;
   const int ct = wave & 3;  // co tile of conv2 / conv3
@@ -480,8 +494,9 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
                                       pk_bf16(fmaxf(kU8Scale * acc0[2] + bias0[2], 0.f), fmaxf(kU8Scale * acc0[3] + bias0[3], 0.f)));
           const uint2 v1 = make_uint2(pk_bf16(fmaxf(kU8Scale * acc1[0] + bias1[0], 0.f), fmaxf(kU8Scale * acc1[1] + bias1[1], 0.f)),
                                       pk_bf16(fmaxf(kU8Scale * acc1[2] + bias1[2], 0.f), fmaxf(kU8Scale * acc1[3] + bias1[3], 0.f)));
-          *reinterpret_cast<uint2*>(A1c + p * kA1Ld + 4 * g) = v0;
-          *reinterpret_cast<uint2*>(A1c + p * kA1Ld + 16 + 4 * g) = v1;
+          const int ar = L::kPhaseA1 ? cs::a1_row(p) : p;
+          *reinterpret_cast<uint2*>(A1c + ar * kA1Ld + 4 * g) = v0;
+          *reinterpret_cast<uint2*>(A1c + ar * kA1Ld + 16 + 4 * g) = v1;
           if (A.y1) {
             uint16_t* yd = A.y1 + ((size_t)n * 400 + p) * 32;
             *reinterpret_cast<uint2*>(yd + 4 * g) = v0;
@@ -503,11 +518,12 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
           for (int u = 0; u < MT; ++u) {
             acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
             const int p = 16 * (MT * pass + u) + i, pc = p < 81 ? p : 0, oh = pc / 9, ow = pc - oh * 9;
-            r0[u] = 2 * oh * 20 + 2 * ow;
+            r0[u] = L::kPhaseA1 ? p : 2 * oh * 20 + 2 * ow;  // phase: grid position 10 oh + ow = row of tap (0, 0)
           }
 #pragma unroll
           for (int ks = 0; ks < 16; ++ks) {
-            const int off = ((ks >> 2) * 20 + (ks & 3)) * kA1Ld + 8 * g;
+            const int kh = ks >> 2, kw = ks & 3;
+            const int off = (L::kPhaseA1 ? 100 * (2 * (kh & 1) + (kw & 1)) + 10 * (kh >> 1) + (kw >> 1) : kh * 20 + kw) * kA1Ld + 8 * g;
             bf16x8_t a[MT];
 #pragma unroll
             for (int u = 0; u < MT; ++u) a[u] = *reinterpret_cast<const bf16x8_t*>(A1p + r0[u] * kA1Ld + off);
@@ -516,12 +532,13 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
           }
 #pragma unroll
           for (int u = 0; u < MT; ++u) {
-            const int p = 16 * (MT * pass + u) + i;
-            if (p < 81) {
+            const int p = 16 * (MT * pass + u) + i, oh = p / 10, ow = p - 10 * (p / 10);
+            if (L::kPhaseA1 ? (p < 90 && ow < 9) : p < 81) {
+              const int q = L::kPhaseA1 ? 9 * oh + ow : p;
               const uint2 v = make_uint2(pk_bf16(fmaxf(acc[u][0] + bias0[0], 0.f), fmaxf(acc[u][1] + bias0[1], 0.f)),
                                          pk_bf16(fmaxf(acc[u][2] + bias0[2], 0.f), fmaxf(acc[u][3] + bias0[3], 0.f)));
-              *reinterpret_cast<uint2*>(A2c + p * kA2Ld + 16 * ct + 4 * g) = v;
-              if (A.y2) *reinterpret_cast<uint2*>(A.y2 + ((size_t)(n - G) * 81 + p) * 64 + 16 * ct + 4 * g) = v;
+              *reinterpret_cast<uint2*>(A2c + q * kA2Ld + 16 * ct + 4 * g) = v;
+              if (A.y2) *reinterpret_cast<uint2*>(A.y2 + ((size_t)(n - G) * 81 + q) * 64 + 16 * ct + 4 * g) = v;
             }
           }
         }
@@ -539,7 +556,7 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
           for (int u = 0; u < MT; ++u) {
             acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
             const int p = 16 * (MT * pass + u) + i, pc = p < 49 ? p : 0, oh = pc / 7, ow = pc - oh * 7;
-            r0[u] = oh * 9 + ow;
+            r0[u] = L::kGrid3 ? p : oh * 9 + ow;  // grid: position 9 oh + ow = the a2 row of tap (0, 0)
           }
 #pragma unroll
           for (int ks = 0; ks < 18; ++ks) {
@@ -553,9 +570,9 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
           }
 #pragma unroll
           for (int u = 0; u < MT; ++u) {
-            const int p = 16 * (MT * pass + u) + i;
-            if (p < 49)
-              *reinterpret_cast<uint2*>(A.y3 + ((size_t)(n - 2 * G) * 49 + p) * 64 + 16 * ct + 4 * g) =
+            const int p = 16 * (MT * pass + u) + i, oh = p / 9, ow = p - 9 * (p / 9);
+            if (L::kGrid3 ? (oh < 7 && ow < 7) : p < 49)
+              *reinterpret_cast<uint2*>(A.y3 + ((size_t)(n - 2 * G) * 49 + (L::kGrid3 ? 7 * oh + ow : p)) * 64 + 16 * ct + 4 * g) =
                   make_uint2(pk_bf16(fmaxf(acc[u][0] + bias0[0], 0.f), fmaxf(acc[u][1] + bias0[1], 0.f)),
                              pk_bf16(fmaxf(acc[u][2] + bias0[2], 0.f), fmaxf(acc[u][3] + bias0[3], 0.f)));
           }
@@ -565,13 +582,14 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
   }
 }
 
+template <int V>
 __global__ __launch_bounds__(cs16::kThreads, 1) void conv_stack16_fwd_kernel(Stack16Args args) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (wave < 8) stack16_role<1>(args, smem, tid, wave);
-  else if (wave < 12) stack16_role<2>(args, smem, tid, wave);
-  else stack16_role<3>(args, smem, tid, wave);
+  if (wave < 8) stack16_role<1, V>(args, smem, tid, wave);
+  else if (wave < 12) stack16_role<2, V>(args, smem, tid, wave);
+  else stack16_role<3, V>(args, smem, tid, wave);
 }
 
 }  // namespace rrl
@@ -597,19 +615,20 @@ static int launch_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const flo
   return (int)hipGetLastError();
 }
 
+template <int V>
 static int launch_conv_stack16_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
                                    const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
                                    uint16_t* y3, int N, int max_grid, hipStream_t stream) {
+  constexpr int lds = cs16::L16<V>::kLds;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_stack16_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              cs16::kLds);
+    (void)hipFuncSetAttribute((const void*)conv_stack16_fwd_kernel<V>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
   if (N < 1) return 0;
-  const int grid = N < max_grid ? N : max_grid;  // one 146 KB-LDS workgroup per CU
+  const int grid = N < max_grid ? N : max_grid;  // one 146-161 KB-LDS workgroup per CU
   const Stack16Args args{x, w1, w2, w3, b1, b2, b3, y1, y2, y3, N};
-  hipLaunchKernelGGL(conv_stack16_fwd_kernel, dim3(grid), dim3(cs16::kThreads), cs16::kLds, stream, args);
+  hipLaunchKernelGGL(conv_stack16_fwd_kernel<V>, dim3(grid), dim3(cs16::kThreads), lds, stream, args);
   return (int)hipGetLastError();
 }
 
@@ -627,15 +646,19 @@ extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const fl
                                   const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
                                   uint16_t* y3, int N, int max_grid, void* stream) {
   // max_grid < 0: timing probe variant -max_grid >> 16 (tools/cnn_kbench.py), grid = -max_grid & 0xffff;
-  // probe 64 = the 16-wave kernel, probe 128 = the 8-wave kernel (whatever RRL_CONV_FWD says)
+  // probe 64 (+ 16 / 32 / 48: its layout bits) = the 16-wave kernel, probe 128 = the 8-wave kernel
+  // (whatever RRL_CONV_FWD says)
   hipStream_t st = (hipStream_t)stream;
   if (max_grid >= 0) {
-    if (conv_fwd16()) return launch_conv_stack16_fwd(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, max_grid, st);
+    if (conv_fwd16()) return launch_conv_stack16_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, max_grid, st);
     return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, max_grid, st);
   }
   const int probe = (-max_grid) >> 16, g = (-max_grid) & 0xffff;
   switch (probe) {
-    case 64: return launch_conv_stack16_fwd(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 64: return launch_conv_stack16_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 64 + 16: return launch_conv_stack16_fwd<16>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 64 + 32: return launch_conv_stack16_fwd<32>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 64 + 48: return launch_conv_stack16_fwd<48>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 128: return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 1: return launch_conv_stack_fwd<1>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 2: return launch_conv_stack_fwd<2>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
@@ -865,14 +888,228 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
   }
 }
 
+// 16-wave form of conv3_bwd_kernel (the conv2_bwd16_kernel split): waves 0-7 the dgrad (co tile
+// w & 3, pixel tiles 3 (w >> 2) ..: W3 fragments, and they stage the next image), waves 8-15 the
+// wgrad (c tile w & 3, taps 5 ((w - 8) >> 2) ..: the 20 weight-gradient accumulators).  Same LDS
+// images, k-orders and partial layout as conv3_bwd_kernel: its outputs bitwise.
+#ifndef C3B16_MT
+#define C3B16_MT 3
+#endif
+#ifndef C3B16_SCHED
+#define C3B16_SCHED 0
+#endif
+namespace c3b16 {
+constexpr int kThreads = 1024;
+constexpr int kStage = 512;
+constexpr int kYPT = (c3b::kYC + kStage - 1) / kStage, kXPT = (c3b::kXC + kStage - 1) / kStage;
+}  // namespace c3b16
+
+template <int ROLE>  // 0 = dgrad, 1 = wgrad
+__device__ __forceinline__ void conv3_bwd16_role(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ w,
+                                                 const uint16_t* __restrict__ xact, uint16_t* __restrict__ dx,
+                                                 float* __restrict__ part, float* __restrict__ bias_part, int N,
+                                                 uint16_t* smem, int tid, int wave) {
+  using namespace c3b;
+  constexpr int T = c3b16::kStage;
+  const int lane = tid & 63;
+  const int ct = wave & 3, half = (wave >> 2) & 1;
+  bf16x8_t wf[ROLE == 0 ? 18 : 1];
+  constexpr int NTAP = 5;
+  const int tap0 = half * 5, ntap = half ? 4 : 5;
+  f32x4_t wacc[ROLE == 1 ? 4 : 1][NTAP];
+  if constexpr (ROLE == 0) {
+    const int i16 = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) {
+      const int t = ks >> 1, co0 = (ks & 1) * 32 + 8 * g;
+      typedef short s16x8_t __attribute__((ext_vector_type(8)));
+      s16x8_t v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (short)w[((co0 + e) * 9 + t) * 64 + 16 * ct + i16];
+      wf[ks] = __builtin_bit_cast(bf16x8_t, v);
+      __builtin_amdgcn_sched_barrier(0);  // one fragment's 8 loads at a time (all 144 at once spill)
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int t = 0; t < NTAP; ++t) wacc[c][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int q = tid; q < 2 * kBuf / 8; q += c3b16::kThreads) *reinterpret_cast<uint4*>(smem + 8 * q) = make_uint4(0, 0, 0, 0);
+  float bsum = 0.f;  // dgrad waves: db3[tid & 63] over positions (tid >> 6) + 8 k
+
+  int tv = tid;  // behind an empty asm each iteration: addresses recomputed, not hoisted into registers
+  uint4 ry[ROLE == 0 ? c3b16::kYPT : 1], rx[ROLE == 0 ? c3b16::kXPT : 1];
+  auto gload = [&](int n) {
+    if constexpr (ROLE == 1) return;
+    const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 49 * 64);
+    const uint4* xs = reinterpret_cast<const uint4*>(xact + (size_t)n * 81 * 64);
+#pragma unroll
+    for (int k = 0; k < c3b16::kYPT; ++k) {
+      const int q = tv + T * k;
+      ry[k] = q < kYC ? ys[q] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < c3b16::kXPT; ++k) {
+      const int q = tv + T * k;
+      rx[k] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lstore = [&](int buf) {
+    if constexpr (ROLE == 1) return;
+    uint16_t* Y = smem + buf * kBuf + kD;
+    uint16_t* X = smem + buf * kBuf + kX;
+#pragma unroll
+    for (int k = 0; k < c3b16::kYPT; ++k) {
+      const int q = tv + T * k;
+      if (q < kYC) {
+        const int pix = q >> 3, oh = pix / 7, ow = pix - oh * 7;
+        *reinterpret_cast<uint4*>(Y + ((oh + 2) * 11 + ow + 2) * kLd + (q & 7) * 8) = ry[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < c3b16::kXPT; ++k) {
+      const int q = tv + T * k;
+      if (q < kXC) {
+        const int pix = q >> 3, ih = pix / 9, iw = pix - ih * 9;
+        *reinterpret_cast<uint4*>(X + (ih * kXW + iw) * kLd + (q & 7) * 8) = rx[k];
+      }
+    }
+  };
+
+  const int G = gridDim.x, n0 = blockIdx.x;
+  __syncthreads();  // zeroing done before the first image lands in buffer 0
+  if (n0 < N) {
+    gload(n0);
+    lstore(0);
+  }
+  if (n0 + G < N) gload(n0 + G);
+  for (int j = 0; n0 + j * G < N; ++j) {
+    const int n = n0 + j * G;
+    __syncthreads();  // buffer j & 1 holds image n; buffer (j + 1) & 1 is no longer read
+    asm volatile("" : "+v"(tv));
+    const int i16 = tv & 15, g = (tv >> 4) & 3, q4 = (tv >> 2) & 3, p4 = tv & 3;
+    if (n + G < N) {
+      lstore((j + 1) & 1);
+      if (n + 2 * G < N) gload(n + 2 * G);
+    }
+    const uint16_t* Yi = smem + (j & 1) * kBuf + kD;
+    const uint16_t* Xi = smem + (j & 1) * kBuf + kX;
+    if constexpr (ROLE == 1) {
+      // ---- wgrad: 2 position k-steps x (4 co tiles x ntap taps)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int oh = 4 * s + g;  // this lane group's output row (7 = zero border)
+        bf16x8_t af[4], bfr[NTAP];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) af[c] = tr_frag(Yi + ((oh + 2) * 11 + 2 + q4) * kLd + 16 * c + 4 * p4, kLd);
+#pragma unroll
+        for (int t = 0; t < NTAP; ++t) {
+          const int tap = min(tap0 + t, 8), kh = tap / 3, kw = tap - kh * 3;
+          bfr[t] = tr_frag(Xi + ((oh + kh) * kXW + kw + q4) * kLd + 16 * ct + 4 * p4, kLd);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int t = 0; t < NTAP; ++t) wacc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[c], bfr[t], wacc[c][t], 0, 0, 0);
+      }
+    } else {
+      // ---- dgrad: this wave's 3 pixel tiles, C3B16_MT at a time (k-step outer, tiles inner)
+      auto tiles = [&](auto tag) {
+        constexpr int U0 = decltype(tag)::value, MT = U0 + C3B16_MT <= 3 ? C3B16_MT : 3 - U0;
+        f32x4_t acc[MT];
+        int rb[MT];
+#pragma unroll
+        for (int u = 0; u < MT; ++u) {
+          acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          const int p = 16 * (3 * half + U0 + u) + i16;
+          const int pc = p < 81 ? p : 0;
+          const int ih = pc / 9, iw = pc - ih * 9;
+          rb[u] = (ih + 2) * 11 + (iw + 2);
+        }
+#pragma unroll
+        for (int ks = 0; ks < 18; ++ks) {
+          const int t = ks >> 1, kh = t / 3, kw = t - kh * 3;
+          const int off = -(kh * 11 + kw) * kLd + (ks & 1) * 32 + 8 * g;
+          bf16x8_t a[MT];
+#pragma unroll
+          for (int u = 0; u < MT; ++u) a[u] = *reinterpret_cast<const bf16x8_t*>(Yi + rb[u] * kLd + off);
+#pragma unroll
+          for (int u = 0; u < MT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], a[u], acc[u], 0, 0, 0);
+          if (C3B16_SCHED && (ks % C3B16_SCHED) == C3B16_SCHED - 1) __builtin_amdgcn_sched_barrier(0);  // bound the reads in flight
+        }
+#pragma unroll
+        for (int u = 0; u < MT; ++u) {
+          const int q = 16 * (3 * half + U0 + u) + i16;
+          if (q < 81) {
+            const uint2 m = *reinterpret_cast<const uint2*>(Xi + ((q / 9) * kXW + q % 9) * kLd + 16 * ct + 4 * g);
+            *reinterpret_cast<uint2*>(dx + ((size_t)n * 81 + q) * 64 + 16 * ct + 4 * g) =
+                make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x), relu_mask2(pk_bf16(acc[u][2], acc[u][3]), m.y));
+          }
+        }
+      };
+      tiles(std::integral_constant<int, 0>{});
+      if constexpr (C3B16_MT < 3) tiles(std::integral_constant<int, C3B16_MT>{});
+      if constexpr (C3B16_MT == 1) tiles(std::integral_constant<int, 2>{});
+      // ---- db3
+      for (int pos = tid >> 6; pos < 49; pos += 8) {
+        const int oh = pos / 7, ow = pos - oh * 7;
+        bsum += bf2f(Yi[((oh + 2) * 11 + ow + 2) * kLd + (tid & 63)]);
+      }
+    }
+  }
+  if constexpr (ROLE == 1) {  // this workgroup's weight-gradient partial: part[blk][co][tap][c]
+    const int i16 = lane & 15, g = lane >> 4;
+    float* o = part + (size_t)blockIdx.x * 64 * 576;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int t = 0; t < NTAP; ++t)
+        if (t < ntap) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[(16 * c + 4 * g + r) * 576 + (tap0 + t) * 64 + 16 * ct + i16] = wacc[c][t][r];
+        }
+  }
+  __syncthreads();  // every wave is past its last LDS read of the image buffers
+  float* red = reinterpret_cast<float*>(smem);
+  if (ROLE == 0) red[tid] = bsum;
+  __syncthreads();
+  if (tid < 64) {
+    float sb = 0.f;
+#pragma unroll
+    for (int w8 = 0; w8 < 8; ++w8) sb += red[w8 * 64 + tid];
+    bias_part[(size_t)blockIdx.x * 64 + tid] = sb;
+  }
+}
+
+__global__ __launch_bounds__(c3b16::kThreads, 1) void conv3_bwd16_kernel(const uint16_t* __restrict__ dy,
+                                                                         const uint16_t* __restrict__ w,
+                                                                         const uint16_t* __restrict__ xact,
+                                                                         uint16_t* __restrict__ dx,
+                                                                         float* __restrict__ part,
+                                                                         float* __restrict__ bias_part, int N) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (wave < 8) conv3_bwd16_role<0>(dy, w, xact, dx, part, bias_part, N, smem, tid, wave);
+  else conv3_bwd16_role<1>(dy, w, xact, dx, part, bias_part, N, smem, tid, wave);
+}
+
+// variant 1: the 16-wave kernel
 extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
-                             float* bias_part, int N, int grid, void* stream) {
+                             float* bias_part, int N, int grid, int variant, void* stream) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)conv3_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
+    (void)hipFuncSetAttribute((const void*)conv3_bwd16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
     attr = true;
   }
   if (N < 1 || grid < 1) return 0;
+  if (variant == 1) {
+    hipLaunchKernelGGL(conv3_bwd16_kernel, dim3(grid), dim3(c3b16::kThreads), c3b::kLds, (hipStream_t)stream, dy, w,
+                       xact, dx, part, bias_part, N);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(conv3_bwd_kernel, dim3(grid), dim3(c3b::kThreads), c3b::kLds, (hipStream_t)stream, dy, w, xact,
                      dx, part, bias_part, N);
   return (int)hipGetLastError();
@@ -1122,8 +1359,239 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
   }
 }
 
+// 16-wave form of conv2_bwd_kernel (4 waves per SIMD instead of 2): the dgrad and the wgrad of
+// an image run on DIFFERENT waves -- waves 0-7 the dgrad (phase class w >> 1, c tile w & 1: W2
+// fragments + 4 accumulators), waves 8-15 the wgrad (c block w & 1, taps 4 ((w - 8) >> 1) ..
+// + 3: the 16 weight-gradient accumulators) -- instead of one after the other on the same 8
+// waves, so neither role carries the other's registers (<= 128 each) and a SIMD interleaves two
+// dgrad and two wgrad waves.  Same LDS images, k-orders, partial layout and one barrier per image
+// as conv2_bwd_kernel: its outputs bitwise.  All 1,024 threads stage the next image.
+#ifndef C2B16_SCHED
+#define C2B16_SCHED 0
+#endif
+#ifndef C2B16_NT
+#define C2B16_NT 4
+#endif
+namespace c2b16 {
+constexpr int kThreads = 1024;
+constexpr int kStage = 512;  // the dgrad waves stage the next image (the wgrad waves' registers are full)
+constexpr int kYPT = (c2b::kYC + kStage - 1) / kStage, kXPT = (c2b::kXC + kStage - 1) / kStage;
+}  // namespace c2b16
+
+template <int ROLE>  // 0 = dgrad, 1 = wgrad
+__device__ __forceinline__ void conv2_bwd16_role(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ w,
+                                                 const uint16_t* __restrict__ xact, uint16_t* __restrict__ dx,
+                                                 float* __restrict__ part, float* __restrict__ bias_part, int N,
+                                                 uint16_t* smem, int tid, int wave) {
+  using namespace c2b;
+  constexpr int T = c2b16::kStage;
+  const int lane = tid & 63;
+  const int i16 = lane & 15, g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int cls = wave >> 1, ph = cls >> 1, pw = cls & 1, ct = wave & 1;  // dgrad role (waves 0-7)
+  const int cb = wave & 1, tau0 = 4 * ((wave - 8) >> 1);                 // wgrad role (waves 8-15)
+  bf16x8_t wf[ROLE == 0 ? 8 : 1];
+  f32x4_t wacc[ROLE == 1 ? 4 : 1][4];
+  if constexpr (ROLE == 0) {
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int t = ks >> 1, kh = ph + 2 * (t >> 1), kw = pw + 2 * (t & 1), co0 = (ks & 1) * 32 + 8 * g;
+      typedef short s16x8_t __attribute__((ext_vector_type(8)));
+      s16x8_t v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (short)w[(((co0 + e) * 4 + kh) * 4 + kw) * 32 + 16 * ct + i16];
+      wf[ks] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) wacc[c][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int q = tid; q < 2 * kBuf / 8; q += c2b16::kThreads) *reinterpret_cast<uint4*>(smem + 8 * q) = make_uint4(0, 0, 0, 0);
+  float bsum = 0.f;  // dgrad waves: db2[tid & 63] over positions (tid >> 6) + 8 k
+
+  // tv: tid behind an empty asm each iteration, so the loop-invariant staging / fragment addresses
+  // are recomputed (a few VALU) instead of hoisted out of the loop into registers this 4-wave-per-SIMD
+  // kernel does not have
+  int tv = tid;
+  uint4 ry[ROLE == 0 ? c2b16::kYPT : 1], rx[ROLE == 0 ? c2b16::kXPT : 1];
+  auto gload = [&](int n) {
+    if constexpr (ROLE == 1) return;
+    const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 81 * 64);
+    const uint4* xs = reinterpret_cast<const uint4*>(xact + (size_t)n * 400 * 32);
+#pragma unroll
+    for (int k = 0; k < c2b16::kYPT; ++k) {
+      const int q = tv + T * k;
+      ry[k] = q < kYC ? ys[q] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < c2b16::kXPT; ++k) {
+      const int q = tv + T * k;
+      rx[k] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lstore = [&](int buf) {
+    if constexpr (ROLE == 1) return;
+    uint16_t* D = smem + buf * kBuf;
+    uint16_t* P = D + kDRows * kDLd;
+#pragma unroll
+    for (int k = 0; k < c2b16::kYPT; ++k) {
+      const int q = tv + T * k;
+      if (q < kYC) {
+        const int pix = q >> 3, oh = pix / 9, ow = pix - oh * 9;
+        *reinterpret_cast<uint4*>(D + ((oh + 1) * 12 + ow + 1) * kDLd + (q & 7) * 8) = ry[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < c2b16::kXPT; ++k) {
+      const int q = tv + T * k;
+      if (q < kXC) {
+        const int pix = q >> 2, ih = pix / 20, iw = pix - ih * 20;
+        const int phase = (ih & 1) * 2 + (iw & 1);
+        *reinterpret_cast<uint4*>(P + (phase * kPRows + (ih >> 1) * 10 + (iw >> 1)) * kPLd + (q & 3) * 8) = rx[k];
+      }
+    }
+  };
+
+  const int G = gridDim.x, n0 = blockIdx.x;
+  __syncthreads();  // zeroing done before the first image lands in buffer 0
+  if (n0 < N) {
+    gload(n0);
+    lstore(0);
+  }
+  if (n0 + G < N) gload(n0 + G);
+  for (int j = 0; n0 + j * G < N; ++j) {
+    const int n = n0 + j * G;
+    __syncthreads();  // buffer j & 1 holds image n; buffer (j + 1) & 1 is no longer read
+    asm volatile("" : "+v"(tv));
+    const int i16 = tv & 15, g = (tv >> 4) & 3, q4 = (tv >> 2) & 3, p4 = tv & 3;
+    if (n + G < N) {
+      lstore((j + 1) & 1);
+      if (n + 2 * G < N) gload(n + 2 * G);
+    }
+    const uint16_t* D = smem + (j & 1) * kBuf;
+    const uint16_t* P = D + kDRows * kDLd;
+    if constexpr (ROLE == 1) {
+      // ---- wgrad: 4 position k-steps (8 runs of 4 columns each), 4 co tiles x 4 taps
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        int oh[2], ow0[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int R = 2 * (4 * s + g) + h;  // run index; runs >= 27 read zero rows
+          oh[h] = R < 27 ? R / 3 : 9;
+          ow0[h] = R < 27 ? 4 * (R % 3) : 0;
+        }
+        bf16x8_t af[4], bfr[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          af[c] = tr_frag2(D + ((oh[0] + 1) * 12 + ow0[0] + 1 + q4) * kDLd + 16 * c + 4 * p4,
+                           D + ((oh[1] + 1) * 12 + ow0[1] + 1 + q4) * kDLd + 16 * c + 4 * p4);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int tau = tau0 + t, kh = tau >> 2, kw = tau & 3;
+          const uint16_t* Pp = P + ((kh & 1) * 2 + (kw & 1)) * kPRows * kPLd + 16 * cb + 4 * p4;
+          bfr[t] = tr_frag2(Pp + ((oh[0] + (kh >> 1)) * 10 + ow0[0] + (kw >> 1) + q4) * kPLd,
+                            Pp + ((oh[1] + (kh >> 1)) * 10 + ow0[1] + (kw >> 1) + q4) * kPLd);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) wacc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[c], bfr[t], wacc[c][t], 0, 0, 0);
+      }
+    } else {
+      // ---- dgrad of phase class (ph, pw), c tile ct: 7 pixel tiles in batches of C2B16_NT (+ 1)
+      auto class_tiles = [&](auto tag) {
+        constexpr int T0 = decltype(tag)::value, NT = T0 == 6 ? 1 : (C2B16_NT == 4 && T0 == 4 ? 3 : C2B16_NT);
+        f32x4_t acc[NT];
+        int rb[NT];
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          const int p = 16 * (T0 + u) + i16, pc = p < 100 ? p : 0, a = pc / 10, b = pc - a * 10;
+          rb[u] = (a + 1) * 12 + (b + 1);
+        }
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          const int t = ks >> 1, ti = t >> 1, tj = t & 1;
+          const int off = -(ti * 12 + tj) * kDLd + (ks & 1) * 32 + 8 * g;
+          bf16x8_t bv[NT];
+#pragma unroll
+          for (int u = 0; u < NT; ++u) bv[u] = *reinterpret_cast<const bf16x8_t*>(D + rb[u] * kDLd + off);
+#pragma unroll
+          for (int u = 0; u < NT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], bv[u], acc[u], 0, 0, 0);
+          if (C2B16_SCHED) __builtin_amdgcn_sched_barrier(0);  // keep the reads of later k-steps from piling up in registers
+        }
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          const int p = 16 * (T0 + u) + i16;
+          if (p < 100) {
+            const int a = p / 10, b = p - a * 10;
+            const uint2 m = *reinterpret_cast<const uint2*>(P + (cls * kPRows + a * 10 + b) * kPLd + 16 * ct + 4 * g);
+            const uint2 v = make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x),
+                                       relu_mask2(pk_bf16(acc[u][2], acc[u][3]), m.y));
+            const int pix = (ph + 2 * a) * 20 + pw + 2 * b;
+            *reinterpret_cast<uint2*>(dx + ((size_t)n * 400 + pix) * 32 + 16 * ct + 4 * g) = v;
+          }
+        }
+      };
+      if constexpr (C2B16_NT == 2) {
+        class_tiles(std::integral_constant<int, 0>{});
+        class_tiles(std::integral_constant<int, 2>{});
+        class_tiles(std::integral_constant<int, 4>{});
+        class_tiles(std::integral_constant<int, 6>{});
+      } else if constexpr (C2B16_NT == 3) {
+        class_tiles(std::integral_constant<int, 0>{});
+        class_tiles(std::integral_constant<int, 3>{});
+        class_tiles(std::integral_constant<int, 6>{});
+      } else {
+        class_tiles(std::integral_constant<int, 0>{});
+        class_tiles(std::integral_constant<int, 4>{});
+      }
+      // ---- db2
+      for (int pos = tid >> 6; pos < 81; pos += 8) {
+        const int oh = pos / 9, ow = pos - oh * 9;
+        bsum += bf2f(D[((oh + 1) * 12 + ow + 1) * kDLd + (tid & 63)]);
+      }
+    }
+  }
+  if constexpr (ROLE == 1) {  // weight-gradient partial of this workgroup: part[blk][co][kh][kw][c]
+    float* o = part + (size_t)blockIdx.x * 64 * 512;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[(16 * c + 4 * g + r) * 512 + (tau0 + t) * 32 + 16 * cb + i16] = wacc[c][t][r];
+  }
+  __syncthreads();  // every wave is past its last LDS read of the image buffers
+  float* red = reinterpret_cast<float*>(smem);
+  if (ROLE == 0) red[tid] = bsum;
+  __syncthreads();
+  if (tid < 64) {
+    float sb = 0.f;
+#pragma unroll
+    for (int w8 = 0; w8 < 8; ++w8) sb += red[w8 * 64 + tid];
+    bias_part[(size_t)blockIdx.x * 64 + tid] = sb;
+  }
+}
+
+__global__ __launch_bounds__(c2b16::kThreads, 1) void conv2_bwd16_kernel(const uint16_t* __restrict__ dy,
+                                                                         const uint16_t* __restrict__ w,
+                                                                         const uint16_t* __restrict__ xact,
+                                                                         uint16_t* __restrict__ dx,
+                                                                         float* __restrict__ part,
+                                                                         float* __restrict__ bias_part, int N) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (wave < 8) conv2_bwd16_role<0>(dy, w, xact, dx, part, bias_part, N, smem, tid, wave);
+  else conv2_bwd16_role<1>(dy, w, xact, dx, part, bias_part, N, smem, tid, wave);
+}
+
 // variant 1: da1 through the LDS staging tile (measured slower: 229 vs 214 us, tools/cnn_kbench.py
-// bwd2 / bwd2_direct); 2: the dgrad over the 10 x 12 grid (measured no faster)
+// bwd2 / bwd2_direct); 2: the dgrad over the 10 x 12 grid (measured no faster); 3: the
+// 16-wave kernel (conv2_bwd16_kernel)
 extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
                              float* bias_part, int N, int grid, int staged, void* stream) {
   static bool attr = false;
@@ -1138,7 +1606,15 @@ extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16
     attr = true;
   }
   if (N < 1 || grid < 1) return 0;
-  if (staged == 1)
+  if (staged == 3) {
+    static bool attr16 = false;
+    if (!attr16) {
+      (void)hipFuncSetAttribute((const void*)conv2_bwd16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c2b::kLds);
+      attr16 = true;
+    }
+    hipLaunchKernelGGL(conv2_bwd16_kernel, dim3(grid), dim3(c2b16::kThreads), c2b::kLds, (hipStream_t)stream, dy, w,
+                       xact, dx, part, bias_part, N);
+  } else if (staged == 1)
     hipLaunchKernelGGL(conv2_bwd_kernel<true>, dim3(grid), dim3(c2b::kThreads), kStagedLds, (hipStream_t)stream, dy, w,
                        xact, dx, part, bias_part, N);
   else if (staged == 2)

@@ -195,7 +195,9 @@ class DeviceNatureCNN:
         assert self.fwd_layout in (0, 16, 32, 48), "RRL_CNN_FWD_LAYOUT: 0, 16, 32 or 48"
         # conv2 backward variant (A/B runs): 0 = dgrad over 7 tiles per class, 2 = a 10 x 12 grid
         self.bwd2_variant = int(os.environ.get("RRL_CNN_BWD2_VARIANT", "0"))
-        assert self.bwd2_variant in (0, 2), "RRL_CNN_BWD2_VARIANT: 0 or 2"
+        assert self.bwd2_variant in (0, 2, 3), "RRL_CNN_BWD2_VARIANT: 0, 2 or 3 (16 waves)"
+        self.bwd3_variant = int(os.environ.get("RRL_CNN_BWD3_VARIANT", "0"))
+        assert self.bwd3_variant in (0, 1), "RRL_CNN_BWD3_VARIANT: 0 or 1 (16 waves)"
         # fc layer on the DMA-staged NT GEMM (fc.hip): forward as split-K partials reduced by
         # the head kernel (bias + ReLU + bf16 + logits / value / sample in one launch), data
         # gradient against a transposed bf16 shadow of Wfc (RRL_FC_NT=0: the gemm_bf16.h path)
@@ -522,7 +524,8 @@ class DeviceNatureCNN:
             # dgrad + wgrad + bias in one pass over (da3, a2) per image (cnn_fused.hip); the
             # slab sums of all three conv layers run in one launch at the end
             nblk = min(B, self.cus)
-            h.conv3_bwd(da3, sh[o["w3"]:o["b3"]], a2, da2, self.cpart["c3"], self.cbias["c3"], B, nblk)
+            h.conv3_bwd(da3, sh[o["w3"]:o["b3"]], a2, da2, self.cpart["c3"], self.cbias["c3"], B, nblk,
+                        variant=self.bwd3_variant)
             sums = [(self.cpart["c3"], nblk, L3.cout * L3.K, g[o["w3"]:o["b3"]]),
                     (self.cbias["c3"], nblk, L3.cout, g[o["b3"]:o["b3"] + L3.cout])]
             if side_sums:  # conv3's slabs are final: summed on the side stream beside conv2 / conv1

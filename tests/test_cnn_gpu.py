@@ -801,8 +801,8 @@ def test_pixel_alternating_obs_buffers_match_copy_path(cuda, monkeypatch):
     assert a.metrics()["EnvSteps"] == b.metrics()["EnvSteps"]
 
 
-@pytest.mark.parametrize("probe", [16, 32, 48])
-def test_fused_conv_stack_layout_variants_are_bitwise_equal(cuda, probe):
+@pytest.mark.parametrize("base,probe", [(128, 16), (128, 32), (128, 48), (64, 80), (64, 96), (64, 112)])
+def test_fused_conv_stack_layout_variants_are_bitwise_equal(cuda, base, probe):
     """The forward's LDS layout variants (FwdLayout probe bits: a1 as stride-2 phase images with
     conv2 over a 9 x 10 grid, conv3 over a 7 x 9 grid) run the same MFMA k-order per output:
     a1 / a2 / a3 bitwise equal to the default layout's, discarded grid positions never stored."""
@@ -818,7 +818,7 @@ def test_fused_conv_stack_layout_variants_are_bitwise_equal(cuda, probe):
     sh = params.bfloat16()
     x = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g).to(cuda)
     outs = []
-    for pr in (128, probe):  # 128: the 8-wave kernel these layouts belong to
+    for pr in (base, probe):  # base 128: the 8-wave kernel, 64: the 16-wave kernel (+ layout bits)
         a1 = torch.full((N * 400 * 32,), float("nan"), dtype=torch.bfloat16, device=cuda)
         a2 = torch.full((N * 81 * 64,), float("nan"), dtype=torch.bfloat16, device=cuda)
         a3 = torch.full((N * FC_IN,), float("nan"), dtype=torch.bfloat16, device=cuda)
@@ -863,10 +863,36 @@ def test_fused_conv_stack_without_stored_activations(cuda, variant):
     assert torch.isnan(outs[1][0].float()).all() and torch.isnan(outs[1][1].float()).all()
 
 
-def test_conv2_bwd_dgrad_grids_are_bitwise_equal(cuda):
-    """The conv2 backward's dgrad over the class's 100 pixels in 7 tiles (shipped) and over a
-    10 x 12 grid per phase class (variant 2) run the same k-order per output: da1, the weight
-    and the bias partials bitwise equal."""
+def test_conv3_bwd_16wave_is_bitwise_equal(cuda):
+    """The 16-wave conv3 backward (dgrad and wgrad on separate waves) runs the 8-wave kernel's
+    k-order per output: da2, the weight and the bias partials bitwise equal."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    L = CONVS[2]
+    N, grid = 333, 64
+    g = torch.Generator().manual_seed(13)
+    x = torch.relu(torch.randn(N * L.hin * L.hin * L.cin, generator=g)).bfloat16().to(cuda)
+    w = (torch.randn(L.cout * L.K, generator=g) * 0.05).bfloat16().to(cuda)
+    dy = torch.randn(N * L.hout * L.hout * L.cout, generator=g).bfloat16().to(cuda)
+    outs = []
+    for v in (0, 1):
+        dx = torch.full((N * L.hin * L.hin * L.cin,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        part = torch.full((grid * L.cout * L.K,), float("nan"), device=cuda)
+        bpart = torch.full((grid * 512,), float("nan"), device=cuda)
+        h.conv3_bwd(dy, w, x, dx, part, bpart, N, grid, variant=v)
+        torch.cuda.synchronize()
+        outs.append((dx, part, bpart[:grid * 64]))
+    for a, b in zip(*outs):
+        assert torch.isfinite(a.float()).all() and torch.equal(a, b)
+
+
+@pytest.mark.parametrize("variant", [2, 3], ids=["grid12", "16wave"])
+def test_conv2_bwd_dgrad_grids_are_bitwise_equal(cuda, variant):
+    """The conv2 backward's dgrad over the class's 100 pixels in 7 tiles (shipped) against the
+    dgrad over a 10 x 12 grid per phase class (variant 2) and the 16-wave kernel with dgrad and
+    wgrad on separate waves (variant 3): the same k-order per output, so da1, the weight and the
+    bias partials are bitwise equal."""
     from relayrl_prototype_amd.ops import hip
 
     h = hip()
@@ -877,11 +903,11 @@ def test_conv2_bwd_dgrad_grids_are_bitwise_equal(cuda):
     w = (torch.randn(L.cout * L.K, generator=g) * 0.05).bfloat16().to(cuda)
     dy = torch.randn(N * L.hout * L.hout * L.cout, generator=g).bfloat16().to(cuda)
     outs = []
-    for variant in (0, 2):
+    for v in (0, variant):
         dx = torch.full((N * L.hin * L.hin * L.cin,), float("nan"), dtype=torch.bfloat16, device=cuda)
         part = torch.full((grid * L.cout * L.K,), float("nan"), device=cuda)
         bpart = torch.full((grid * 512,), float("nan"), device=cuda)
-        h.conv2_bwd(dy, w, x, dx, part, bpart, N, grid, staged=variant)
+        h.conv2_bwd(dy, w, x, dx, part, bpart, N, grid, staged=v)
         torch.cuda.synchronize()
         outs.append((dx, part, bpart[:grid * 64]))  # one 64-channel bias partial per workgroup
     for a, b in zip(*outs):

@@ -61,6 +61,9 @@ def main():
     def bwd3():
         h.conv3_bwd(da3, W[3][0], a2, da2, part, bpart, Nb, min(Nb, cus))
 
+    def bwd3_16():
+        h.conv3_bwd(da3, W[3][0], a2, da2, part, bpart, Nb, min(Nb, cus), variant=1)
+
     def bwd3_layers():
         L = CONVS[2]
         h.conv_dgrad(da3, W[3][0], a2, da2, Nb, L.hin, L.hin, L.cin, L.k, L.k, L.s, L.cout)
@@ -73,7 +76,7 @@ def main():
     fns["wgrad1_8"] = lambda: h.conv1_wgrad8(x[:Nb], da1, part, bpart, Nb, min(Nb, cus))
     fns["wgrad1"] = lambda: h.conv_wgrad(da1, x[:Nb], part, 256, Nb, 21, 21, 64, 2, 2, 1, 32, bpart)
     fns.update({"p_nomfma": probe(1), "p_nostore": probe(2), "p_nostore_nomfma": probe(3), "p_hotframe": probe(4),
-           "p_all": probe(7), "fwd_c1split": probe(8), "fwd_g128": probe(0, 128), "fwd_phase_a1": probe(16), "fwd_c3_grid": probe(32), "fwd_phase_a1_c3_grid": probe(48), "fwd_g512": probe(0, 512), "fwd8": probe(128), "fwd16": probe(64), "fwd": fwd, "fwd_layers": fwd_layers, "bwd3": bwd3, "bwd3_layers": bwd3_layers, "dgrad2": dgrad2})
+           "p_all": probe(7), "fwd_c1split": probe(8), "fwd_g128": probe(0, 128), "fwd_phase_a1": probe(16), "fwd_c3_grid": probe(32), "fwd_phase_a1_c3_grid": probe(48), "fwd_g512": probe(0, 512), "fwd8": probe(128), "fwd16": probe(64), "fwd16_phase": probe(80), "fwd16_grid3": probe(96), "fwd16_both": probe(112), "fwd": fwd, "fwd_layers": fwd_layers, "bwd3": bwd3, "bwd3_16": bwd3_16, "bwd3_layers": bwd3_layers, "dgrad2": dgrad2})
     if hasattr(h, "conv2_bwd"):
         def bwd2():
             h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus))
@@ -82,6 +85,7 @@ def main():
             h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=1)
         fns["bwd2"] = bwd2
         fns["bwd2_staged"] = bwd2_staged
+        fns["bwd2_16"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=3)
         fns["bwd2_grid12"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=2)
 
     # --rounds R: the list R times, every other round in reverse order (the first kernel timed

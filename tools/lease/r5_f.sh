@@ -9,14 +9,15 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-me
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/r5f_gpu_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 120 python -u tools/cnn_kbench.py --which fwd8,fwd16 --rounds 4 --iters 20 \
+timeout -k 10 120 python -u tools/cnn_kbench.py --which fwd8,fwd16,fwd16_phase,fwd16_grid3,fwd16_both,bwd2,bwd2_16,bwd3,bwd3_16 --rounds 4 --iters 20 \
     > gpurun_out/r5f_kbench.jsonl 2> gpurun_out/r5f_kbench.err || exit $?
-timeout -k 10 120 python -u tools/cnn_kbench.py --which fwd8,fwd16 --rounds 4 --iters 10 --frames 8192 \
+timeout -k 10 120 python -u tools/cnn_kbench.py --which fwd8,fwd16,fwd16_phase,fwd16_grid3,fwd16_both --rounds 4 --iters 10 --frames 8192 \
     >> gpurun_out/r5f_kbench.jsonl 2>> gpurun_out/r5f_kbench.err || exit $?
 for envs in 2048 8192; do
   for v in 8 16 16 8; do
-    echo "{\"conv_fwd\": $v, \"envs\": $envs}" >> gpurun_out/r5f_pong.jsonl
-    RRL_CONV_FWD=$v timeout -k 10 200 python -u benchmarks/pong_a2c_bench.py --num-envs $envs --steps 40 --warmup 5 \
+    b2=0; b3=0; [ $v = 16 ] && b2=3 && b3=1
+    echo "{\"conv_fwd\": $v, \"bwd2\": $b2, \"bwd3\": $b3, \"envs\": $envs}" >> gpurun_out/r5f_pong.jsonl
+    RRL_CONV_FWD=$v RRL_CNN_BWD2_VARIANT=$b2 RRL_CNN_BWD3_VARIANT=$b3 timeout -k 10 200 python -u benchmarks/pong_a2c_bench.py --num-envs $envs --steps 40 --warmup 5 \
         >> gpurun_out/r5f_pong.jsonl 2>> gpurun_out/r5f_pong.err || exit $?
   done
 done
