@@ -189,15 +189,20 @@ class DeviceNatureCNN:
         import os
 
         self.fused_convs = os.environ.get("RRL_CNN_FUSED", "1") != "0"
-        # LDS layout variant of the fused forward (cnn_fused.hip FwdLayout, for A/B runs):
-        # 0 = shipped, 16 = a1 as phase images, 32 = conv3 over a 7 x 9 grid, 48 = both
+        # variant of the fused forward (cnn_fused.hip, for A/B runs): 0 = the default kernel
+        # (RRL_CONV_FWD), 128 = the 8-wave kernel, 16 / 32 / 48 = its LDS layouts (a1 as phase
+        # images, conv3 over a 7 x 9 grid, both); 64 = the 16-wave kernel, 80 / 96 / 112 = its layouts
         self.fwd_layout = int(os.environ.get("RRL_CNN_FWD_LAYOUT", "0"))
-        assert self.fwd_layout in (0, 16, 32, 48), "RRL_CNN_FWD_LAYOUT: 0, 16, 32 or 48"
+        assert self.fwd_layout in (0, 16, 32, 48, 64, 80, 96, 112, 128), "RRL_CNN_FWD_LAYOUT"
         # conv2 backward variant (A/B runs): 0 = dgrad over 7 tiles per class, 2 = a 10 x 12 grid
         self.bwd2_variant = int(os.environ.get("RRL_CNN_BWD2_VARIANT", "0"))
         assert self.bwd2_variant in (0, 2, 3), "RRL_CNN_BWD2_VARIANT: 0, 2 or 3 (16 waves)"
         self.bwd3_variant = int(os.environ.get("RRL_CNN_BWD3_VARIANT", "0"))
         assert self.bwd3_variant in (0, 1), "RRL_CNN_BWD3_VARIANT: 0 or 1 (16 waves)"
+        # conv2 backward + conv1 weight gradient in C row chunks, each chunk's da1 read back by
+        # conv1_wgrad8 right after conv2_bwd wrote it (RRL_CNN_BWD21_CHUNKS, for A/B runs: a half
+        # batch's da1 fits the 256 MB Infinity Cache, the whole one does not at 10,240 frames)
+        self.bwd21_chunks = max(1, int(os.environ.get("RRL_CNN_BWD21_CHUNKS", "1")))
         # fc layer on the DMA-staged NT GEMM (fc.hip): forward as split-K partials reduced by
         # the head kernel (bias + ReLU + bf16 + logits / value / sample in one launch), data
         # gradient against a transposed bf16 shadow of Wfc (RRL_FC_NT=0: the gemm_bf16.h path)
@@ -259,13 +264,15 @@ class DeviceNatureCNN:
             # per-layer partial slabs of the fused conv backward kernels, summed together in ONE
             # launch at the end of the backward (sum_splits_multi)
             nb = min(B, self.cus)
+            C = self.bwd21_chunks
             L1_, L2_, L3_ = CONVS
             self.cpart = {"c3": torch.empty(nb * L3_.cout * L3_.K, device=dev),
-                          "c2": torch.empty(nb * L2_.cout * L2_.K, device=dev),
-                          "c1": torch.empty(2 * nb * S2D.cout * S2D.K, device=dev)}  # 2 slabs per workgroup
+                          "c2": torch.empty(C * nb * L2_.cout * L2_.K, device=dev),
+                          "c1": torch.empty(C * 2 * nb * S2D.cout * S2D.K, device=dev)}  # 2 slabs per workgroup
+            # bias partials: 64 per workgroup written, 512 per workgroup checked by the binding
             self.cbias = {"c3": torch.empty(nb * 8 * L3_.cout, device=dev),
-                          "c2": torch.empty(nb * 8 * L2_.cout, device=dev),
-                          "c1": torch.empty(2 * nb * S2D.cout, device=dev)}
+                          "c2": torch.empty((C + 1) * nb * 8 * L2_.cout, device=dev),
+                          "c1": torch.empty(C * 2 * nb * S2D.cout, device=dev)}
         self.sq_work = torch.empty(1024, device=dev)
         # side stream for the head / fc weight gradients (backward, one rank; RRL_CNN_SIDE=0: off)
         self.side_stream = torch.cuda.Stream(device=dev) if os.environ.get("RRL_CNN_SIDE", "1") != "0" else None
@@ -537,7 +544,30 @@ class DeviceNatureCNN:
             self._dgrad(da3, sh[o["w3"]:o["b3"]], a2, da2, B, L3)
         # conv2
         da1 = self.da1[:B * L1.hout ** 2 * L1.cout]
-        if self.fused_convs:
+        c1_slabs = None
+        if self.fused_convs and self.bwd21_chunks > 1 and not side_sums:
+            # conv2 backward + conv1 weight gradient chunk by chunk; each chunk's partial slabs
+            # follow the previous chunk's, so the one slab sum at the end covers them all
+            C = self.bwd21_chunks
+            n2 = n1 = 0
+            S2, S1, P2, P1 = L2.cout * L2.K, S2D.cout * S2D.K, L2.hout ** 2 * L2.cout, L1.hout ** 2 * L1.cout
+            x8 = obs_u8.contiguous()
+            for k in range(C):
+                b0, b1 = B * k // C, B * (k + 1) // C
+                nk = b1 - b0
+                if nk < 1:
+                    continue
+                nblk = min(nk, self.cus)
+                h.conv2_bwd(da2[b0 * P2:b1 * P2], sh[o["w2"]:o["b2"]], a1[b0 * P1:b1 * P1], da1[b0 * P1:b1 * P1],
+                            self.cpart["c2"][n2 * S2:], self.cbias["c2"][n2 * L2.cout:], nk, nblk,
+                            staged=self.bwd2_variant)
+                n2 += nblk
+                n1 += int(h.conv1_wgrad8(x8[b0:b1], da1[b0 * P1:b1 * P1], self.cpart["c1"][n1 * S1:],
+                                         self.cbias["c1"][n1 * S2D.cout:], nk, nblk))
+            sums += [(self.cpart["c2"], n2, S2, g[o["w2"]:o["b2"]]),
+                     (self.cbias["c2"], n2, L2.cout, g[o["b2"]:o["b2"] + L2.cout])]
+            c1_slabs = n1
+        elif self.fused_convs:
             nblk = min(B, self.cus)
             h.conv2_bwd(da2, sh[o["w2"]:o["b2"]], a1, da1, self.cpart["c2"], self.cbias["c2"], B, nblk,
                         staged=self.bwd2_variant)
@@ -553,8 +583,8 @@ class DeviceNatureCNN:
         # conv1 (input = frames, no data gradient)
         # (its bias gradient comes out of the same pass over da1)
         if self.fused_convs:
-            ns = int(h.conv1_wgrad8(obs_u8.contiguous(), da1, self.cpart["c1"], self.cbias["c1"], B,
-                                    min(B, self.cus)))
+            ns = c1_slabs if c1_slabs is not None else int(
+                h.conv1_wgrad8(obs_u8.contiguous(), da1, self.cpart["c1"], self.cbias["c1"], B, min(B, self.cus)))
             sums += [(self.cpart["c1"], ns, S2D.cout * S2D.K, g[o["w1"]:o["b1"]]),
                      (self.cbias["c1"], ns, S2D.cout, g[o["b1"]:o["b1"] + S2D.cout])]
             h.sum_splits_multi(sums)

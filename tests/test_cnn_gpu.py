@@ -780,6 +780,36 @@ def test_pixel_update_side_stream_is_race_free(cuda, monkeypatch):
         torch.testing.assert_close(a.model.grad, b.model.grad, rtol=0, atol=0)
 
 
+def test_pixel_update_16wave_backward_and_chunks(cuda, monkeypatch):
+    """The 16-wave conv2 / conv3 backward kernels (bitwise equal to the 8-wave ones) train the
+    same trajectory bitwise; conv2_bwd + conv1_wgrad8 in two row chunks (RRL_CNN_BWD21_CHUNKS)
+    change only the grouping of the weight-gradient slab sums (fp32 reassociation)."""
+    from relayrl_prototype_amd.runtime.pixel_trainer import PixelA2CConfig, PixelA2CTrainer
+
+    cfg = dict(num_envs=300, rollout_len=4, seed=9)
+    runs = []
+    for b2, b3, chunks in (("0", "0", "1"), ("3", "1", "1"), ("0", "0", "2")):
+        monkeypatch.setenv("RRL_CNN_FWD_LAYOUT", "128")
+        monkeypatch.setenv("RRL_CNN_BWD2_VARIANT", b2)
+        monkeypatch.setenv("RRL_CNN_BWD3_VARIANT", b3)
+        monkeypatch.setenv("RRL_CNN_BWD21_CHUNKS", chunks)
+        tr = PixelA2CTrainer(PixelA2CConfig(use_graphs=True, **cfg), device=cuda)
+        for _ in range(3 if chunks == "1" else 1):
+            tr.train_epoch()
+        torch.cuda.synchronize()
+        runs.append(tr)
+    base, w16, ch = runs
+    assert torch.equal(w16.act, base.act)
+    torch.testing.assert_close(w16.model.params, base.model.params, rtol=0, atol=0)
+    # one update from the same state: gradients equal up to fp32 summation order
+    monkeypatch.setenv("RRL_CNN_BWD21_CHUNKS", "1")
+    ref = PixelA2CTrainer(PixelA2CConfig(use_graphs=True, **cfg), device=cuda)
+    ref.train_epoch()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(ch.model.grad, ref.model.grad, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(ch.model.params, ref.model.params, rtol=1e-4, atol=1e-6)
+
+
 def test_pixel_alternating_obs_buffers_match_copy_path(cuda, monkeypatch):
     """Two observation buffers used alternately (the last render of update k lands in slot 0 of
     update k + 1's buffer) train exactly like the single buffer + obs[T] -> obs[0] copy."""
