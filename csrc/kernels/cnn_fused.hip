@@ -388,6 +388,10 @@ constexpr int kXPerT = (kXChunks + kThreads - 1) / kThreads;
 // stride-2 phase images in 48-element rows, conv2 over a 9 x 10 grid (1.0); bit 32 -- conv3
 // over a 7 x 9 grid of a2 (1.75 -> 1.0).  Discarded grid positions read past the image into rows
 // that stay inside their buffer (garbage in discarded outputs only).
+// Measured slower and removed: the activations copied out through LDS with 16-byte stores one
+// iteration later (a double-buffered a3 image, a third pipeline stage): 58.8 / 214.0 us against
+// 51.8 / 177.3 us per 2,048 / 8,192 frames (profiles/r5_cnn16_kbench.jsonl) -- the epilogue's
+// 8-byte stores are not what bounds this kernel.
 template <int V>
 struct L16 {
   static constexpr bool kPhaseA1 = (V & 16) != 0, kGrid3 = (V & 32) != 0;
@@ -571,10 +575,12 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
 #pragma unroll
           for (int u = 0; u < MT; ++u) {
             const int p = 16 * (MT * pass + u) + i, oh = p / 9, ow = p - 9 * (p / 9);
-            if (L::kGrid3 ? (oh < 7 && ow < 7) : p < 49)
-              *reinterpret_cast<uint2*>(A.y3 + ((size_t)(n - 2 * G) * 49 + (L::kGrid3 ? 7 * oh + ow : p)) * 64 + 16 * ct + 4 * g) =
-                  make_uint2(pk_bf16(fmaxf(acc[u][0] + bias0[0], 0.f), fmaxf(acc[u][1] + bias0[1], 0.f)),
-                             pk_bf16(fmaxf(acc[u][2] + bias0[2], 0.f), fmaxf(acc[u][3] + bias0[3], 0.f)));
+            if (L::kGrid3 ? (oh < 7 && ow < 7) : p < 49) {
+              const int q = L::kGrid3 ? 7 * oh + ow : p;
+              const uint2 v = make_uint2(pk_bf16(fmaxf(acc[u][0] + bias0[0], 0.f), fmaxf(acc[u][1] + bias0[1], 0.f)),
+                                         pk_bf16(fmaxf(acc[u][2] + bias0[2], 0.f), fmaxf(acc[u][3] + bias0[3], 0.f)));
+              *reinterpret_cast<uint2*>(A.y3 + ((size_t)(n - 2 * G) * 49 + q) * 64 + 16 * ct + 4 * g) = v;
+            }
           }
         }
       }
@@ -632,12 +638,13 @@ static int launch_conv_stack16_fwd(const uint8_t* x, const uint16_t* w1, const f
   return (int)hipGetLastError();
 }
 
-// RRL_CONV_FWD = 8 / 16 picks the 8-wave or the 16-wave kernel (default below)
+// RRL_CONV_FWD = 8 / 16 picks the 8-wave or the 16-wave kernel; default 16 (Pong A2C +2.3 % at
+// 2,048 envs, +3.4 % at 8,192 in ABBA runs: profiles/r5_pong_16wave_ab_*.jsonl)
 static bool conv_fwd16() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("RRL_CONV_FWD");
-    v = (e && e[0]) ? (atoi(e) == 16) : 0;
+    v = (e && e[0]) ? (atoi(e) == 16) : 1;
   }
   return v == 1;
 }

@@ -190,7 +190,7 @@ class DeviceNatureCNN:
 
         self.fused_convs = os.environ.get("RRL_CNN_FUSED", "1") != "0"
         # variant of the fused forward (cnn_fused.hip, for A/B runs): 0 = the default kernel
-        # (RRL_CONV_FWD), 128 = the 8-wave kernel, 16 / 32 / 48 = its LDS layouts (a1 as phase
+        # (RRL_CONV_FWD, default the 16-wave one), 128 = the 8-wave kernel, 16 / 32 / 48 = its LDS layouts (a1 as phase
         # images, conv3 over a 7 x 9 grid, both); 64 = the 16-wave kernel, 80 / 96 / 112 = its layouts
         self.fwd_layout = int(os.environ.get("RRL_CNN_FWD_LAYOUT", "0"))
         assert self.fwd_layout in (0, 16, 32, 48, 64, 80, 96, 112, 128), "RRL_CNN_FWD_LAYOUT"
