@@ -494,9 +494,12 @@ def test_fused_conv_stack_matches_per_layer_kernels(cuda, N, variant):
 
 
 @pytest.mark.parametrize("B", [3, 300, 1500])
-def test_fused_conv_backward_matches_per_layer(cuda, B):
+def test_fused_conv_backward_matches_per_layer(cuda, B, monkeypatch):
     """The fused conv3 backward (dgrad + wgrad + bias in one pass, cnn_fused.hip) against the
-    per-layer kernels on the same stored activations: every parameter gradient."""
+    per-layer kernels on the same stored activations: every parameter gradient.  The fused side's
+    forward is the 8-wave kernel, whose conv1 k-order is the per-layer kernel's (the 16-wave
+    forward sums conv1 in another order: a few bf16 activations flip, and with them ReLU masks)."""
+    monkeypatch.setenv("RRL_CNN_FWD_LAYOUT", "128")
     spec = CNNSpec(6)
     o = spec.offsets()
     params = spec.init(7)
