@@ -41,6 +41,22 @@ struct FrameError : std::runtime_error {
 class Reader {
  public:
   Reader(const uint8_t* p, size_t n) : p_(p), n_(n) {}
+  // "K b K b ... e" right after a MARK (serde's Vec<u8> chunk: up to 1000 BININT1 + APPENDS):
+  // the bytes appended to ``out`` and the run consumed; anything else leaves the position as it was
+  bool u8_run(std::string& out) {
+    size_t q = pos_;
+    const size_t start = out.size();
+    while (q + 1 < n_ && p_[q] == 0x4B) {
+      out.push_back((char)p_[q + 1]);
+      q += 2;
+    }
+    if (q < n_ && p_[q] == 0x65) {
+      pos_ = q + 1;
+      return true;
+    }
+    out.resize(start);
+    return false;
+  }
   const uint8_t* take(size_t k) {
     if (pos_ + k > n_) throw FrameError("truncated frame");
     const uint8_t* out = p_ + pos_;
@@ -87,6 +103,7 @@ py::object loads(const py::bytes& frame, bool u8_as_bytes) {
   std::vector<py::object> stack;
   std::vector<size_t> marks;
   std::unordered_map<uint32_t, py::object> memo;
+  std::string run;  // scratch of the u8 fast form
   auto pop_value = [&]() {
     if (stack.empty() || (!marks.empty() && marks.back() == stack.size())) throw FrameError("stack underflow");
     py::object v = std::move(stack.back());
@@ -191,6 +208,19 @@ py::object loads(const py::bytes& frame, bool u8_as_bytes) {
         break;
       }
       case 0x28:  // MARK
+        // u8 form: a MARK that opens a pure "K b ... APPENDS" run onto a Vec<u8> being built goes
+        // straight into the bytearray, no Python int per byte (~20,000 of them per CartPole frame)
+        if (u8_as_bytes && !stack.empty() && (marks.empty() || marks.back() < stack.size()) &&
+            PyByteArray_Check(stack.back().ptr())) {
+          run.clear();
+          if (r.u8_run(run)) {
+            PyObject* ba = stack.back().ptr();
+            const Py_ssize_t old = PyByteArray_Size(ba);
+            if (PyByteArray_Resize(ba, old + (Py_ssize_t)run.size()) != 0) throw py::error_already_set();
+            if (!run.empty()) std::memcpy(PyByteArray_AsString(ba) + old, run.data(), run.size());
+            break;
+          }
+        }
         if ((int)marks.size() >= kMaxDepth) throw FrameError("nesting too deep");
         marks.push_back(stack.size());
         break;
@@ -435,23 +465,52 @@ std::string byte_payload(const py::handle& data) {
   throw FrameError("TensorData.data must be bytes or a list of u8");
 }
 
-// TensorData {shape, dtype, data: one-tensor safetensors file} -> float32 values; false if None
-bool tensor_f32(const py::handle& td, std::vector<float>& out) {
+// TensorData {shape, dtype, data: one-tensor safetensors file} -> float32 values; false if None.
+// Headers are parsed once per distinct header text per frame (every obs of a frame has the same
+// one): ``cache`` maps header bytes -> (dtype, shape, data range).
+using HeaderCache = std::unordered_map<std::string, rrl::StHeader>;
+bool tensor_f32(const py::handle& td, std::vector<float>& out, HeaderCache& cache) {
   if (td.is_none()) return false;
   if (!py::isinstance<py::dict>(td)) throw FrameError("TensorData must be a dict with shape / dtype / data");
   py::dict d = py::reinterpret_borrow<py::dict>(td);
   if (!d.contains("data")) throw FrameError("TensorData must be a dict with shape / dtype / data");
-  rrl::Tensor t;
-  try {
-    t = rrl::st_decode(byte_payload(d["data"]));
-  } catch (const std::exception& e) {
-    throw FrameError(std::string("TensorData: ") + e.what());
+  py::object data = d["data"];
+  std::string owned;
+  const char* p = nullptr;
+  size_t n = 0;
+  if (py::isinstance<py::bytearray>(data)) {
+    p = PyByteArray_AsString(data.ptr());
+    n = (size_t)PyByteArray_Size(data.ptr());
+  } else if (py::isinstance<py::bytes>(data)) {
+    p = PyBytes_AsString(data.ptr());
+    n = (size_t)PyBytes_Size(data.ptr());
+  } else {
+    owned = byte_payload(data);
+    p = owned.data();
+    n = owned.size();
   }
-  const int64_t n = t.numel();
-  out.resize((size_t)n);
-  const char* r = t.raw.data();
-  for (int64_t i = 0; i < n; ++i) {
-    switch (t.dtype) {
+  if (n < 8) throw FrameError("TensorData: safetensors: file too short");
+  uint64_t hl = 0;
+  for (int i = 0; i < 8; ++i) hl |= (uint64_t)(uint8_t)p[i] << (8 * i);
+  if (hl > n - 8) throw FrameError("TensorData: safetensors: header length out of range");
+  std::string key(p + 8, (size_t)hl);
+  auto it = cache.find(key);
+  if (it == cache.end()) {
+    try {
+      it = cache.emplace(std::move(key), rrl::st_header(p + 8, (size_t)hl)).first;
+    } catch (const std::exception& e) {
+      throw FrameError(std::string("TensorData: ") + e.what());
+    }
+  }
+  const rrl::StHeader& h = it->second;
+  const size_t base = 8 + (size_t)hl;
+  if (base + (size_t)h.off1 > n) throw FrameError("TensorData: safetensors: bad data offsets");
+  int64_t cnt = 1;
+  for (auto s : h.shape) cnt *= s;
+  out.resize((size_t)cnt);
+  const char* r = p + base + h.off0;
+  for (int64_t i = 0; i < cnt; ++i) {
+    switch (h.dtype) {
       case rrl::DType::Byte: out[i] = (float)(uint8_t)r[i]; break;
       case rrl::DType::Bool: out[i] = r[i] ? 1.f : 0.f; break;
       case rrl::DType::Short: { int16_t v; std::memcpy(&v, r + 2 * i, 2); out[i] = (float)v; break; }
@@ -516,6 +575,7 @@ py::dict reference_columns(const py::bytes& frame) {
   py::sequence acts = py::reinterpret_borrow<py::sequence>(root);
   const size_t n = acts.size();
   Col obs, act, mask;
+  HeaderCache hc;
   std::vector<float> rew, logp, v, tmp;
   std::vector<uint8_t> done, has_logp, has_v;
   rew.reserve(n);
@@ -524,11 +584,11 @@ py::dict reference_columns(const py::bytes& frame) {
     if (!py::isinstance<py::dict>(a)) throw FrameError("an action must be a dict");
     py::dict ad = py::reinterpret_borrow<py::dict>(a);
     auto field = [&](const char* k) -> py::object { return ad.contains(k) ? py::object(ad[k]) : py::object(py::none()); };
-    bool p = tensor_f32(field("obs"), tmp);
+    bool p = tensor_f32(field("obs"), tmp, hc);
     obs.add(p, tmp);
-    p = tensor_f32(field("act"), tmp);
+    p = tensor_f32(field("act"), tmp, hc);
     act.add(p, tmp);
-    p = tensor_f32(field("mask"), tmp);
+    p = tensor_f32(field("mask"), tmp, hc);
     mask.add(p, tmp);
     py::object r = field("rew");
     rew.push_back(r.is_none() ? 0.f : r.cast<float>());
@@ -545,7 +605,7 @@ py::dict reference_columns(const py::bytes& frame) {
         auto var = variant(kv.second);
         float x = NAN;
         if (var.first == "Tensor") {
-          if (!tensor_f32(var.second, tmp) || tmp.empty()) continue;
+          if (!tensor_f32(var.second, tmp, hc) || tmp.empty()) continue;
           x = tmp[0];
         } else if (var.first == "Float" || var.first == "Double" || var.first == "Int" || var.first == "Long" ||
                    var.first == "Short" || var.first == "Byte") {

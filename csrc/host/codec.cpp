@@ -108,19 +108,15 @@ static void skip_value(const std::string& s, size_t& i) {
   while (i < s.size() && s[i] != ',' && s[i] != '}' && s[i] != ']') ++i;
 }
 
-Tensor st_decode(const std::string& file, const std::string& name) {
-  if (file.size() < 8) throw std::runtime_error("safetensors: file too short");
-  uint64_t hl = 0;
-  for (int i = 0; i < 8; ++i) hl |= (uint64_t)(uint8_t)file[i] << (8 * i);
-  if (8 + hl > file.size()) throw std::runtime_error("safetensors: header length out of range");
-  const std::string h = file.substr(8, hl);
+StHeader st_header(const char* header_json, size_t len, const std::string& name) {
+  const std::string h(header_json, len);
   size_t i = 0;
   expect(h, i, '{');
   bool found = false;
-  Tensor t;
-  int64_t off0 = 0, off1 = 0;
+  StHeader t;
   while (true) {
     i = skip_ws(h, i);
+    if (i >= h.size()) throw std::runtime_error("safetensors header: unterminated");
     if (h[i] == '}') break;
     std::string key = parse_string(h, i);
     expect(h, i, ':');
@@ -129,6 +125,7 @@ Tensor st_decode(const std::string& file, const std::string& name) {
       expect(h, i, '{');
       while (true) {
         i = skip_ws(h, i);
+        if (i >= h.size()) throw std::runtime_error("safetensors header: unterminated");
         if (h[i] == '}') {
           ++i;
           break;
@@ -140,37 +137,52 @@ Tensor st_decode(const std::string& file, const std::string& name) {
         } else if (k == "shape") {
           expect(h, i, '[');
           i = skip_ws(h, i);
-          while (h[i] != ']') {
+          while (i < h.size() && h[i] != ']') {
             t.shape.push_back(parse_int(h, i));
             i = skip_ws(h, i);
-            if (h[i] == ',') ++i;
+            if (i < h.size() && h[i] == ',') ++i;
             i = skip_ws(h, i);
           }
           ++i;
         } else if (k == "data_offsets") {
           expect(h, i, '[');
-          off0 = parse_int(h, i);
+          t.off0 = parse_int(h, i);
           expect(h, i, ',');
-          off1 = parse_int(h, i);
+          t.off1 = parse_int(h, i);
           expect(h, i, ']');
         } else {
           skip_value(h, i);
         }
         i = skip_ws(h, i);
-        if (h[i] == ',') ++i;
+        if (i < h.size() && h[i] == ',') ++i;
       }
     } else {
       skip_value(h, i);
     }
     i = skip_ws(h, i);
-    if (h[i] == ',') ++i;
+    if (i < h.size() && h[i] == ',') ++i;
   }
   if (!found) throw std::runtime_error("safetensors: tensor '" + name + "' not found");
-  const size_t base = 8 + hl;
-  if (off1 < off0 || base + (size_t)off1 > file.size()) throw std::runtime_error("safetensors: bad data offsets");
-  t.raw = file.substr(base + off0, off1 - off0);
-  if ((int64_t)t.raw.size() != t.numel() * (int64_t)dtype_size(t.dtype))
+  if (t.off1 < t.off0) throw std::runtime_error("safetensors: bad data offsets");
+  int64_t n = 1;
+  for (auto d : t.shape) n *= d;
+  if (t.off1 - t.off0 != n * (int64_t)dtype_size(t.dtype))
     throw std::runtime_error("safetensors: data size does not match shape");
+  return t;
+}
+
+Tensor st_decode(const std::string& file, const std::string& name) {
+  if (file.size() < 8) throw std::runtime_error("safetensors: file too short");
+  uint64_t hl = 0;
+  for (int i = 0; i < 8; ++i) hl |= (uint64_t)(uint8_t)file[i] << (8 * i);
+  if (8 + hl > file.size()) throw std::runtime_error("safetensors: header length out of range");
+  const StHeader sh = st_header(file.data() + 8, (size_t)hl, name);
+  const size_t base = 8 + hl;
+  if (base + (size_t)sh.off1 > file.size()) throw std::runtime_error("safetensors: bad data offsets");
+  Tensor t;
+  t.dtype = sh.dtype;
+  t.shape = sh.shape;
+  t.raw = file.substr(base + sh.off0, sh.off1 - sh.off0);
   return t;
 }
 

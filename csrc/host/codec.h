@@ -37,6 +37,14 @@ struct Tensor {
 
 std::string st_encode(const Tensor& t, const std::string& name = "tensor");
 Tensor st_decode(const std::string& file, const std::string& name = "tensor");
+// The header of one tensor in a safetensors file: dtype, shape and its byte range within the data
+// section (the section starts at 8 + header length).  st_decode = st_header + the range's bytes.
+struct StHeader {
+  DType dtype = DType::Float;
+  std::vector<int64_t> shape;
+  int64_t off0 = 0, off1 = 0;
+};
+StHeader st_header(const char* header_json, size_t len, const std::string& name = "tensor");
 
 // ----------------------------------------------------------------- RelayRLData / action
 // Externally tagged aux value (action.rs:207-218): Tensor or a scalar / string.
