@@ -114,6 +114,19 @@ def test_code_execution_opcodes_are_rejected(op):
         _native.pickle_loads(b"\x80\x03" + op + b"os\nsystem\n.")
 
 
+@pytest.mark.parametrize("vals", [list(range(256)) * 9,                      # 2,304 bytes: 3 APPENDS chunks
+                                  list(range(200)) * 6 + [300, 5],            # an int > 255 in the 2nd chunk
+                                  [7] * 1000 + [-1],                          # a negative in the 2nd chunk
+                                  [], [0], [255] * 1000])
+def test_u8_runs_decode_like_the_interpreter(vals):
+    """The u8 fast form (a MARK opening a pure BININT1 + APPENDS run onto a Vec<u8> goes straight
+    into the bytearray) gives the interpreter's value, including lists that stop being Vec<u8>
+    in a later chunk, nested and as dict values."""
+    for obj in (vals, [vals, vals[:3]], {"data": vals, "shape": [len(vals)]}):
+        f = sp.dumps(obj)
+        assert _norm(_native.pickle_loads(f, True)) == sp.loads(f) == _native.pickle_loads(f)
+
+
 def test_memo_and_marks():
     # memoised list referenced twice, tuples, sets, LONG1, BINFLOAT, nested marks
     f = (b"\x80\x03]q\x00(K\x01K\x02eh\x00\x86(\x8a\x02\x00\x01G?\xf0\x00\x00\x00\x00\x00\x00t\x8f(K\x05\x90\x87.")
