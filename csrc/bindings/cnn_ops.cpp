@@ -52,20 +52,21 @@ int rrl_head_wgrad(const uint16_t* h, const float* dhead, int B, int A, float* p
 int rrl_pong_state_size();
 int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
                   float* ep_acc, int N, unsigned long long seed, unsigned long long step,
-                  const unsigned long long* step_base, int max_steps, int reset_all, void* stream);
+                  const unsigned long long* step_base, int max_steps, int reset_all, float* hist_out, void* stream);
 int rrl_pong_render(const float* state, uint8_t* obs, int N, void* stream);
 int rrl_pong_step_render(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
                          float* ep_acc, uint8_t* obs, int N, unsigned long long seed, unsigned long long step,
                          const unsigned long long* step_base, int max_steps, int reset_all, void* stream);
-int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
-                       const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2, uint16_t* y3, int N,
-                       int max_grid, void* stream);
+int rrl_conv_stack_fwd(const uint8_t* x, const float* hist, const uint16_t* w1, const float* b1,
+                       const uint16_t* w2, const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1,
+                       uint16_t* y2, uint16_t* y3, int N, int max_grid, void* stream);
 int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
                   float* bias_part, int N, int grid, int variant, void* stream);
 int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
                   float* bias_part, int N, int grid, int staged, void* stream);
-int rrl_conv1_wgrad8(const uint8_t* x, const uint16_t* dy, float* part, float* bias_part, int N, int grid,
-                     void* stream);
+int rrl_conv1_wgrad8(const uint8_t* x, const float* hist, const uint16_t* dy, float* part, float* bias_part, int N,
+                     int grid, void* stream);
+int rrl_pong_render_hist(const float* hist, uint8_t* obs, int N, void* stream);
 
 }
 
@@ -123,11 +124,14 @@ void conv_fwd(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& y
 
 // Fused Nature-CNN conv stack (cnn_fused.hip): uint8 s2d frames [N][21][21][64] ->
 // a1 [N][20][20][32], a2 [N][9][9][64], a3 [N][7][7][64] (bf16, post-ReLU).
-void conv_stack_fwd(const Tensor& x, const Tensor& w1, const Tensor& b1, const Tensor& w2, const Tensor& b2,
+void conv_stack_fwd(const OptT& x, const Tensor& w1, const Tensor& b1, const Tensor& w2, const Tensor& b2,
                     const Tensor& w3, const Tensor& b3, const Tensor& y1, const Tensor& y2, const Tensor& y3,
-                    int64_t N, int64_t probe, int64_t grid, bool store12) {
+                    int64_t N, int64_t probe, int64_t grid, bool store12, const OptT& hist) {
   TORCH_CHECK(N > 0, "conv_stack_fwd: N must be positive");
-  check(x, "x", at::kByte, N * 21 * 21 * 64);
+  // fused render: PongSynth frame histories [N][16] instead of s2d frames (cnn_fused.hip)
+  const float* hp = opt_ptr<const float>(hist, "hist", at::kFloat, N * 16);
+  const uint8_t* xp = opt_ptr<const uint8_t>(x, "x", at::kByte, N * 21 * 21 * 64);
+  TORCH_CHECK(hp || xp, "conv_stack_fwd: x (s2d frames) or hist (frame histories) is required");
   check(w1, "w1", at::kBFloat16, 32 * 256);
   check(w2, "w2", at::kBFloat16, 64 * 512);
   check(w3, "w3", at::kBFloat16, 64 * 576);
@@ -140,7 +144,7 @@ void conv_stack_fwd(const Tensor& x, const Tensor& w1, const Tensor& b1, const T
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  rc_check(rrl_conv_stack_fwd(x.data_ptr<uint8_t>(), bf(w1), b1.data_ptr<float>(), bf(w2), b2.data_ptr<float>(),
+  rc_check(rrl_conv_stack_fwd(xp, hp, bf(w1), b1.data_ptr<float>(), bf(w2), b2.data_ptr<float>(),
                               bf(w3), b3.data_ptr<float>(), store12 ? bf(y1) : nullptr, store12 ? bf(y2) : nullptr,
                               bf(y3), (int)N,
                               probe > 0 ? -(int)((probe << 16) | (grid > 0 ? grid : cus))
@@ -183,15 +187,17 @@ void conv2_bwd(const Tensor& dy, const Tensor& w, const Tensor& xact, const Tens
 
 // conv1 weight + bias gradient, 8-wave kernel (cnn_fused.hip): s2d frames [N][21][21][64], da1
 // [N][400][32] -> partials [2 grid][32 * 256] and [2 grid][32]; returns the slab count (2 grid).
-int64_t conv1_wgrad8(const Tensor& x, const Tensor& dy, const Tensor& part, const Tensor& bias_part, int64_t N,
-                     int64_t grid) {
+int64_t conv1_wgrad8(const OptT& x, const Tensor& dy, const Tensor& part, const Tensor& bias_part, int64_t N,
+                     int64_t grid, const OptT& hist) {
   TORCH_CHECK(N > 0 && grid > 0 && grid <= N, "conv1_wgrad8: need 0 < grid <= N");
-  check(x, "x", at::kByte, N * 441 * 64);
+  const float* hp = opt_ptr<const float>(hist, "hist", at::kFloat, N * 16);
+  const uint8_t* xp = opt_ptr<const uint8_t>(x, "x", at::kByte, N * 441 * 64);
+  TORCH_CHECK(hp || xp, "conv1_wgrad8: x (s2d frames) or hist (frame histories) is required");
   check(dy, "dy", at::kBFloat16, N * 400 * 32);
   check(part, "part", at::kFloat, 2 * grid * 32 * 256);
   check(bias_part, "bias_part", at::kFloat, 2 * grid * 32);
-  rc_check(rrl_conv1_wgrad8(x.data_ptr<uint8_t>(), bf(dy), part.data_ptr<float>(), bias_part.data_ptr<float>(), (int)N,
-                            (int)grid, stream()),
+  rc_check(rrl_conv1_wgrad8(xp, hp, bf(dy), part.data_ptr<float>(), bias_part.data_ptr<float>(), (int)N, (int)grid,
+                            stream()),
            "conv1_wgrad8");
   return 2 * grid;
 }
@@ -457,7 +463,7 @@ int64_t pong_state_size() { return rrl_pong_state_size(); }
 
 void pong_step(const Tensor& state, const Tensor& act, const Tensor& rew, const Tensor& done, const Tensor& fin_ret,
                const Tensor& fin_len, const OptT& ep_acc, int64_t N, int64_t seed, int64_t step, int64_t max_steps,
-               bool reset_all, const OptT& step_base, const OptT& obs) {
+               bool reset_all, const OptT& step_base, const OptT& obs, const OptT& hist) {
   check(state, "state", at::kFloat, N * pong_state_size());
   check(act, "act", at::kInt, reset_all ? 0 : N);
   check(rew, "rew", at::kFloat, N);
@@ -475,10 +481,18 @@ void pong_step(const Tensor& state, const Tensor& act, const Tensor& rew, const 
              "pong_step_render");
     return;
   }
+  float* hout = opt_ptr<float>(hist, "hist", at::kFloat, N * 16);  // the new frame histories (fused render)
   rc_check(rrl_pong_step(state.data_ptr<float>(), act.data_ptr<int32_t>(), rew.data_ptr<float>(),
                          done.data_ptr<float>(), fin_ret.data_ptr<float>(), fin_len.data_ptr<float>(), acc, (int)N,
-                         (uint64_t)seed, (uint64_t)step, sb, (int)max_steps, reset_all ? 1 : 0, stream()),
+                         (uint64_t)seed, (uint64_t)step, sb, (int)max_steps, reset_all ? 1 : 0, hout, stream()),
            "pong_step");
+}
+
+// s2d observations drawn from frame histories [N][16] (the fused-render path's reference)
+void pong_render_hist(const Tensor& hist, const Tensor& obs, int64_t N) {
+  check(hist, "hist", at::kFloat, N * 16);
+  check(obs, "obs", at::kByte, N * 84 * 84 * 4);
+  rc_check(rrl_pong_render_hist(hist.data_ptr<float>(), obs.data_ptr<uint8_t>(), (int)N, stream()), "pong_render_hist");
 }
 
 void pong_render(const Tensor& state, const Tensor& obs, int64_t N) {
@@ -498,14 +512,15 @@ void register_cnn_ops(pybind11::module_& m) {
   m.def("conv_stack_fwd", &conv_stack_fwd, pybind11::arg("x"), pybind11::arg("w1"), pybind11::arg("b1"),
         pybind11::arg("w2"), pybind11::arg("b2"), pybind11::arg("w3"), pybind11::arg("b3"), pybind11::arg("y1"),
         pybind11::arg("y2"), pybind11::arg("y3"), pybind11::arg("N"), pybind11::arg("probe") = 0,
-        pybind11::arg("grid") = 0, pybind11::arg("store12") = true);
+        pybind11::arg("grid") = 0, pybind11::arg("store12") = true, pybind11::arg("hist") = pybind11::none());
   m.def("conv3_bwd", &conv3_bwd, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("xact"), pybind11::arg("dx"),
         pybind11::arg("part"), pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"),
         pybind11::arg("variant") = 0);
   m.def("conv2_bwd", &conv2_bwd, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("xact"), pybind11::arg("dx"),
         pybind11::arg("part"), pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"),
         pybind11::arg("staged") = 0);
-  m.def("conv1_wgrad8", &conv1_wgrad8);
+  m.def("conv1_wgrad8", &conv1_wgrad8, pybind11::arg("x"), pybind11::arg("dy"), pybind11::arg("part"),
+        pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"), pybind11::arg("hist") = pybind11::none());
   m.def("col2im_mask", &col2im_mask);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("gemm_splits", &gemm_splits);
@@ -545,6 +560,7 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("done"), pybind11::arg("fin_ret"), pybind11::arg("fin_len"), pybind11::arg("ep_acc"),
         pybind11::arg("N"), pybind11::arg("seed"), pybind11::arg("step"), pybind11::arg("max_steps"),
         pybind11::arg("reset_all"), pybind11::arg("step_base") = pybind11::none(),
-        pybind11::arg("obs") = pybind11::none());
+        pybind11::arg("obs") = pybind11::none(), pybind11::arg("hist") = pybind11::none());
   m.def("pong_render", &pong_render);
+  m.def("pong_render_hist", &pong_render_hist);
 }

@@ -27,6 +27,7 @@
 //   copy out a2(n_{j-1}) and a3(n_{j-2}); conv1(n_j) -> A1                          | B1 .. B2
 //   copy out a1(n_j); A: conv2(n_j) -> A2[j & 1]; B: conv3(n_{j-1}) -> A3          | B2 .. B0
 #include "gemm_bf16.h"
+#include "pong_render.h"
 
 namespace rrl {
 
@@ -392,9 +393,12 @@ constexpr int kXPerT = (kXChunks + kThreads - 1) / kThreads;
 // iteration later (a double-buffered a3 image, a third pipeline stage): 58.8 / 214.0 us against
 // 51.8 / 177.3 us per 2,048 / 8,192 frames (profiles/r5_cnn16_kbench.jsonl) -- the epilogue's
 // 8-byte stores are not what bounds this kernel.
+// bit 2 -- fused render: the frames are drawn in the kernel from 16-float PongSynth frame
+// histories (pong_render.h) instead of read from an observation tensor; the workgroup's history
+// rows sit in LDS behind the a2 buffers (64 B per frame, sized at launch)
 template <int V>
 struct L16 {
-  static constexpr bool kPhaseA1 = (V & 16) != 0, kGrid3 = (V & 32) != 0;
+  static constexpr bool kPhaseA1 = (V & 16) != 0, kGrid3 = (V & 32) != 0, kRender = (V & 2) != 0;
   static constexpr int kA1Ld = kPhaseA1 ? 48 : 40, kA2Ld = 80;
   static constexpr int kA1Rows = kPhaseA1 ? 407 : 400, kA2Rows = kGrid3 ? 84 : 81;
   static constexpr int kA1Elems = kA1Rows * kA1Ld, kA2Elems = kA2Rows * kA2Ld;
@@ -412,6 +416,7 @@ __device__ __forceinline__ bf16x8_t u8x8_frag(uint32_t lo, uint32_t hi) {
 
 struct Stack16Args {
   const uint8_t* x;
+  const float* hist;  // fused render: [N][16] frame histories (x unused)
   const uint16_t *w1, *w2, *w3;
   const float *b1, *b2, *b3;
   uint16_t *y1, *y2, *y3;
@@ -451,8 +456,10 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
   }
 
   const int G = gridDim.x, n0 = blockIdx.x, N = A.N;
-  uint4 rx[kXPerT];
+  float* H = reinterpret_cast<float*>(smem + L::kLds / 2);  // fused render: [frames of this workgroup][16]
+  uint4 rx[L::kRender ? 1 : kXPerT];
   auto gload = [&](size_t n) {
+    if constexpr (L::kRender) return;
     const uint4* xs = reinterpret_cast<const uint4*>(A.x + n * (441 * 64));
 #pragma unroll
     for (int k = 0; k < kXPerT; ++k) {
@@ -460,11 +467,27 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
       rx[k] = q < kXChunks ? xs[q] : make_uint4(0, 0, 0, 0);
     }
   };
+  if constexpr (L::kRender) {  // every history row this workgroup draws (published by the first B0)
+    const int J = n0 < N ? (N - n0 + G - 1) / G : 0;
+    for (int t = tid; t < 4 * J; t += kThreads)
+      *reinterpret_cast<float4*>(H + 4 * t) =
+          *reinterpret_cast<const float4*>(A.hist + (size_t)(n0 + (t >> 2) * G) * kPongHist + 4 * (t & 3));
+  }
   if (n0 < N) gload(n0);
   for (int j = 0; n0 + (j - 2) * G < N; ++j) {
     const int n = n0 + j * G;
     __syncthreads();  // B0: the previous iteration's stages are done (F free, a1 / a2 buffers complete)
-    if (n < N) {
+    if constexpr (L::kRender) {
+      // fused render: the conv1 waves (whose 64 weight registers leave room for it) draw the
+      // frame's 1,764 chunks, 4 each
+      if (ROLE == 1 && n < N) {
+        for (int q = tid; q < kXChunks; q += 512) {
+          const int pix = q >> 2, pa = pix / 21;
+          *reinterpret_cast<uint4*>(F + (pix + (kFW - 21) * pa) * kFS + (q & 3) * 16) =
+              pong_render_chunk(H + j * kPongHist, q);
+        }
+      }
+    } else if (n < N) {
 #pragma unroll
       for (int k = 0; k < kXPerT; ++k) {
         const int q = tid + kThreads * k;
@@ -621,19 +644,28 @@ static int launch_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const flo
   return (int)hipGetLastError();
 }
 
+constexpr int cs16_hist_bytes = kPongHist * 4;
+
 template <int V>
-static int launch_conv_stack16_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
-                                   const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
-                                   uint16_t* y3, int N, int max_grid, hipStream_t stream) {
-  constexpr int lds = cs16::L16<V>::kLds;
+static int launch_conv_stack16_fwd(const uint8_t* x, const float* hist, const uint16_t* w1, const float* b1,
+                                   const uint16_t* w2, const float* b2, const uint16_t* w3, const float* b3,
+                                   uint16_t* y1, uint16_t* y2, uint16_t* y3, int N, int max_grid, hipStream_t stream) {
+  using L = cs16::L16<V>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_stack16_fwd_kernel<V>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    (void)hipFuncSetAttribute((const void*)conv_stack16_fwd_kernel<V>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     attr = true;
   }
   if (N < 1) return 0;
   const int grid = N < max_grid ? N : max_grid;  // one 146-161 KB-LDS workgroup per CU
-  const Stack16Args args{x, w1, w2, w3, b1, b2, b3, y1, y2, y3, N};
+  int lds = L::kLds;
+  if (L::kRender) {
+    if (!hist) return -2;
+    lds += ((N + grid - 1) / grid) * cs16_hist_bytes;  // the workgroup's history rows
+    if (lds > 160 * 1024) return -3;                    // too many frames per workgroup for LDS
+  }
+  const Stack16Args args{x, hist, w1, w2, w3, b1, b2, b3, y1, y2, y3, N};
   hipLaunchKernelGGL(conv_stack16_fwd_kernel<V>, dim3(grid), dim3(cs16::kThreads), lds, stream, args);
   return (int)hipGetLastError();
 }
@@ -649,23 +681,30 @@ static bool conv_fwd16() {
   return v == 1;
 }
 
-extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
-                                  const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1, uint16_t* y2,
-                                  uint16_t* y3, int N, int max_grid, void* stream) {
+extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const float* hist, const uint16_t* w1, const float* b1,
+                                  const uint16_t* w2, const float* b2, const uint16_t* w3, const float* b3,
+                                  uint16_t* y1, uint16_t* y2, uint16_t* y3, int N, int max_grid, void* stream) {
   // max_grid < 0: timing probe variant -max_grid >> 16 (tools/cnn_kbench.py), grid = -max_grid & 0xffff;
   // probe 64 (+ 16 / 32 / 48: its layout bits) = the 16-wave kernel, probe 128 = the 8-wave kernel
-  // (whatever RRL_CONV_FWD says)
+  // (whatever RRL_CONV_FWD says).  hist (PongSynth frame histories [N][16]): the 16-wave kernel
+  // draws the frames itself (fused render), x is not read.
   hipStream_t st = (hipStream_t)stream;
+  if (hist) {
+    const int g = max_grid >= 0 ? max_grid : ((-max_grid) & 0xffff);
+    const int probe = max_grid >= 0 ? 64 : ((-max_grid) >> 16);
+    if (probe != 64) return -4;  // the fused render exists for the default 16-wave layout only
+    return launch_conv_stack16_fwd<2>(x, hist, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+  }
   if (max_grid >= 0) {
-    if (conv_fwd16()) return launch_conv_stack16_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, max_grid, st);
+    if (conv_fwd16()) return launch_conv_stack16_fwd<0>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, max_grid, st);
     return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, max_grid, st);
   }
   const int probe = (-max_grid) >> 16, g = (-max_grid) & 0xffff;
   switch (probe) {
-    case 64: return launch_conv_stack16_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
-    case 64 + 16: return launch_conv_stack16_fwd<16>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
-    case 64 + 32: return launch_conv_stack16_fwd<32>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
-    case 64 + 48: return launch_conv_stack16_fwd<48>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 64: return launch_conv_stack16_fwd<0>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 64 + 16: return launch_conv_stack16_fwd<16>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 64 + 32: return launch_conv_stack16_fwd<32>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 64 + 48: return launch_conv_stack16_fwd<48>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 128: return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 1: return launch_conv_stack_fwd<1>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 2: return launch_conv_stack_fwd<2>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
@@ -1652,7 +1691,11 @@ constexpr int kXC = 441 * 4, kYC = 400 * 4;       // 16-byte chunks per image
 constexpr int kXPT = (kXC + kThreads - 1) / kThreads, kYPT = (kYC + kThreads - 1) / kThreads;
 }  // namespace c1w
 
+// RENDER: the frames are drawn from PongSynth frame histories hist[N][16] (pong_render.h), the
+// workgroup's rows staged in LDS behind dY, instead of read from an observation tensor
+template <bool RENDER>
 __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const uint8_t* __restrict__ x,
+                                                                        const float* __restrict__ hist,
                                                                         const uint16_t* __restrict__ dy,
                                                                         float* __restrict__ part,
                                                                         float* __restrict__ bias_part, int N) {
@@ -1683,13 +1726,15 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
     ones = __builtin_bit_cast(bf16x8_t, v);
   }
   uint4 rx[kXPT], ry[kYPT];
+  float* H = reinterpret_cast<float*>(smem + kLds / 2);  // RENDER: [images of this workgroup][16]
   auto gload = [&](int n) {
     const uint4* xs = reinterpret_cast<const uint4*>(x + (size_t)n * 441 * 64);
     const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 400 * 32);
 #pragma unroll
     for (int i = 0; i < kXPT; ++i) {
       const int q = tid + kThreads * i;
-      rx[i] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
+      if constexpr (RENDER) rx[i] = make_uint4(0, 0, 0, 0);
+      else rx[i] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < kYPT; ++i) {
@@ -1699,6 +1744,12 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
   };
   const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
   const int n0 = blockIdx.x, G = gridDim.x;
+  if constexpr (RENDER) {  // every history row this workgroup draws (published by the loop's first barrier)
+    const int J = n0 < N ? (N - n0 + G - 1) / G : 0;
+    for (int t = tid; t < 4 * J; t += kThreads)
+      *reinterpret_cast<float4*>(H + 4 * t) =
+          *reinterpret_cast<const float4*>(hist + (size_t)(n0 + (t >> 2) * G) * kPongHist + 4 * (t & 3));
+  }
   if (n0 < N) gload(n0);
   for (int n = n0; n < N; n += G) {
     __syncthreads();  // the previous image's fragment reads are done
@@ -1708,8 +1759,11 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
       if (q < kXC) {
         const int pix = q >> 2;
         uint16_t* d = Xi + (pix + (kXW - 21) * (pix / 21)) * kLd + (q & 3) * 16;
-        *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(rx[i].x, rx[i].y));
-        *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(rx[i].z, rx[i].w));
+        uint4 v;
+        if constexpr (RENDER) v = pong_render_chunk(H + ((n - n0) / G) * kPongHist, q);
+        else v = rx[i];
+        *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(v.x, v.y));
+        *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(v.z, v.w));
       }
     }
 #pragma unroll
@@ -1761,16 +1815,27 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
       for (int r = 0; r < 4; ++r) o[(16 * mt + 4 * g + r) * 256 + 16 * nt + j] = acc[mt][nt][r] * kU8Scale;
 }
 
-// returns the number of partial slabs written (2 per workgroup)
-extern "C" int rrl_conv1_wgrad8(const uint8_t* x, const uint16_t* dy, float* part, float* bias_part, int N, int grid,
-                                void* stream) {
+// returns the number of partial slabs written (2 per workgroup); hist (PongSynth frame histories
+// [N][16]): the frames are drawn in the kernel, x is not read
+extern "C" int rrl_conv1_wgrad8(const uint8_t* x, const float* hist, const uint16_t* dy, float* part,
+                                float* bias_part, int N, int grid, void* stream) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv1_wgrad8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c1w::kLds);
+    (void)hipFuncSetAttribute((const void*)conv1_wgrad8_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              c1w::kLds);
+    (void)hipFuncSetAttribute((const void*)conv1_wgrad8_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     attr = true;
   }
   if (N < 1 || grid < 1) return 0;
-  hipLaunchKernelGGL(conv1_wgrad8_kernel, dim3(grid), dim3(c1w::kThreads), c1w::kLds, (hipStream_t)stream, x, dy, part,
-                     bias_part, N);
+  if (hist) {
+    const int lds = c1w::kLds + ((N + grid - 1) / grid) * kPongHist * 4;
+    if (lds > 160 * 1024) return -3;  // too many images per workgroup for the LDS history rows
+    hipLaunchKernelGGL(conv1_wgrad8_kernel<true>, dim3(grid), dim3(c1w::kThreads), lds, (hipStream_t)stream, x, hist,
+                       dy, part, bias_part, N);
+  } else {
+    hipLaunchKernelGGL(conv1_wgrad8_kernel<false>, dim3(grid), dim3(c1w::kThreads), c1w::kLds, (hipStream_t)stream, x,
+                       hist, dy, part, bias_part, N);
+  }
   return (int)hipGetLastError();
 }

@@ -7,18 +7,16 @@
 // 4-frame stack straight into the uint8 NHWC observation tensor the conv stack reads
 // (channel f = frame f, oldest first), so observations never touch the host.
 #include "common.h"
+#include "pong_render.h"
 
 namespace rrl {
 
 constexpr int kPongState = 32;  // floats per env
-constexpr int kPongHW = 84;
 // state layout
 enum : int {
   P_BX = 0, P_BY, P_VX, P_VY, P_PA, P_PO, P_SA, P_SO, P_T, P_RET,
   P_HIST = 16  // 4 frames x (bx, by, pa, po)
 };
-constexpr float kTop = 2.f, kBot = 82.f, kPadHalf = 5.f, kBall = 2.f;
-constexpr float kAgentX = 76.f, kOppX = 6.f, kPadW = 2.f;
 constexpr float kPadSpeed = 2.5f, kOppSpeed = 1.6f, kMaxVy = 3.0f, kMaxVx = 3.0f;
 
 RRL_DEV void serve(float* s, uint4 r) {
@@ -125,7 +123,7 @@ RRL_DEV void pong_step_state(int e, float* s, const int32_t* __restrict__ act, f
 RRL_DEV void pong_step_env(int e, float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew,
                            float* __restrict__ done, float* __restrict__ fin_ret, float* __restrict__ fin_len,
                            float* __restrict__ ep_acc, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
-                           int reset_all, const unsigned long long* __restrict__ step_base) {
+                           int reset_all, const unsigned long long* __restrict__ step_base, float* __restrict__ hist_out) {
   float s[kPongState];
 #pragma unroll
   for (int i = 0; i < kPongState; ++i) s[i] = state[(size_t)e * kPongState + i];
@@ -133,62 +131,23 @@ RRL_DEV void pong_step_env(int e, float* __restrict__ state, const int32_t* __re
                   step_base);
 #pragma unroll
   for (int i = 0; i < kPongState; ++i) state[(size_t)e * kPongState + i] = s[i];
+  if (hist_out) {  // the new frame history: all a fused-render conv kernel needs to draw the observation
+#pragma unroll
+    for (int i = 0; i < kPongHist; i += 4)
+      *reinterpret_cast<float4*>(hist_out + (size_t)e * kPongHist + i) =
+          make_float4(s[P_HIST + i], s[P_HIST + i + 1], s[P_HIST + i + 2], s[P_HIST + i + 3]);
+  }
 }
 
 __global__ void pong_step_kernel(float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew,
                                  float* __restrict__ done, float* __restrict__ fin_ret, float* __restrict__ fin_len,
                                  float* __restrict__ ep_acc, int N, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
-                                 int reset_all, const unsigned long long* __restrict__ step_base) {
+                                 int reset_all, const unsigned long long* __restrict__ step_base,
+                                 float* __restrict__ hist_out) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= N) return;
   pong_step_env(e, state, act, rew, done, fin_ret, fin_len, ep_acc, key, step_lo, step_hi, max_steps, reset_all,
-                step_base);
-}
-
-// One thread per (env, row): 84 pixels x 4 frames = 21 x 16 B.  The observation is
-// written space-to-depth: obs[n][a][b][dy][dx][f] with y = 4a + dy, x = 4b + dx (i.e.
-// [N][21][21][64]), so the first 8x8/4 conv becomes a 2x2/1 conv over 64 contiguous
-// channels and its im2col reads 8-byte runs; a 16-byte chunk of 4 pixels x 4 frames of
-// one row lands contiguously at (a, b, dy).
-// One thread per 16-byte output chunk (4 pixels x 4 frames of one row), chunks in memory
-// order, so every wave stores 1 KB contiguously.  Chunk q of an env's [21][21][64] s2d
-// frame: a = q / 84 (block row), c = (q % 84) / 4 (block column), dy = q % 4 (row in the
-// 4x4 block) -> image row y = 4a + dy, pixels x = 4c .. 4c+3.
-// 16-byte chunk q (0 .. 1763) of one env's s2d frame stack from its (bx, by, pa, po) history h.
-RRL_DEV uint4 pong_render_chunk(const float* h, int q) {
-  const int a = q / 84, rem = q - a * 84, c = rem >> 2, dy = rem & 3;
-  const float fy = (float)(4 * a + dy) + 0.5f;
-  const bool wall = fy < kTop || fy >= kBot;
-  uint32_t w[4] = {0u, 0u, 0u, 0u};
-  // rows with nothing lit in any frame (most of the screen): the wall / background pattern
-  // only -- whole waves skip the per-pixel tests below
-  bool lit = false;
-#pragma unroll
-  for (int f = 0; f < 4; ++f) {
-    const float by = h[4 * f + 1], pa = h[4 * f + 2], po = h[4 * f + 3];
-    lit |= (fy >= by && fy < by + kBall) || fabsf(fy - pa) < kPadHalf || fabsf(fy - po) < kPadHalf;
-  }
-  if (!lit) {
-    const uint32_t v = wall ? 0x64646464u : 0u;
-    return make_uint4(v, v, v, v);
-  }
-#pragma unroll
-  for (int f = 0; f < 4; ++f) {
-    const float bx = h[4 * f], by = h[4 * f + 1], pa = h[4 * f + 2], po = h[4 * f + 3];
-    const bool b_on = fy >= by && fy < by + kBall;
-    const bool pa_on = fabsf(fy - pa) < kPadHalf;
-    const bool po_on = fabsf(fy - po) < kPadHalf;
-#pragma unroll
-    for (int px = 0; px < 4; ++px) {
-      const float fx = (float)(4 * c + px) + 0.5f;
-      uint32_t v = wall ? 100u : 0u;
-      if (pa_on && fx >= kAgentX && fx < kAgentX + kPadW) v = 255u;
-      if (po_on && fx >= kOppX && fx < kOppX + kPadW) v = 255u;
-      if (b_on && fx >= bx && fx < bx + kBall) v = 255u;
-      w[px] |= v << (8 * f);
-    }
-  }
-  return make_uint4(w[0], w[1], w[2], w[3]);
+                step_base, hist_out);
 }
 
 // The row-only half of pong_render_chunk, once per image row y (84 per env instead of once per
@@ -285,12 +244,12 @@ int rrl_pong_state_size() { return kPongState; }
 
 int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
                   float* ep_acc, int N, unsigned long long seed, unsigned long long step,
-                  const unsigned long long* step_base, int max_steps, int reset_all, void* stream_) {
+                  const unsigned long long* step_base, int max_steps, int reset_all, float* hist_out, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
   hipLaunchKernelGGL(pong_step_kernel, dim3((N + 255) / 256), dim3(256), 0, st, state, act, rew, done, fin_ret,
                      fin_len, ep_acc, N, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, reset_all,
-                     step_base);
+                     step_base, hist_out);
   return (int)hipGetLastError();
 }
 
@@ -302,6 +261,21 @@ int rrl_pong_step_render(float* state, const int32_t* act, float* rew, float* do
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
   hipLaunchKernelGGL(pong_step_render_kernel, dim3(N), dim3(256), 0, st, state, act, rew, done, fin_ret, fin_len,
                      ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, reset_all, step_base);
+  return (int)hipGetLastError();
+}
+
+// obs[n] drawn from the frame-history rows hist[n][16] (the fused-render path's reference)
+__global__ void pong_render_hist_kernel(const float* __restrict__ hist, uint8_t* __restrict__ obs, int N) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= (size_t)N * kPongChunks) return;
+  const int e = (int)(t / kPongChunks), q = (int)(t % kPongChunks);
+  *reinterpret_cast<uint4*>(obs + t * 16) = pong_render_chunk(hist + (size_t)e * kPongHist, q);
+}
+
+int rrl_pong_render_hist(const float* hist, uint8_t* obs, int N, void* stream_) {
+  const size_t t = (size_t)N * kPongChunks;
+  hipLaunchKernelGGL(pong_render_hist_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, (hipStream_t)stream_,
+                     hist, obs, N);
   return (int)hipGetLastError();
 }
 

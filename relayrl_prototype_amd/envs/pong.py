@@ -220,23 +220,35 @@ class DevicePong:
     def advance(self, k: int):
         self.h.counter_add(self.step_t, int(k))
 
-    def reset(self, obs_out: torch.Tensor):
-        self.h.pong_step(self.state, self._dummy_act, self.rew, self.done, self.fin_ret, self.fin_len, None, self.N,
-                         self.seed, 0, self.max_steps, True, self.step_t, obs=obs_out)
+    def reset(self, obs_out: torch.Tensor = None, hist_out: torch.Tensor = None):
+        """Reset every env; the first observation is rendered into ``obs_out`` ([N, 21, 21, 64]) or,
+        for the fused-render path, only its frame history goes to ``hist_out`` ([N, 16])."""
+        if hist_out is not None:
+            self.h.pong_step(self.state, self._dummy_act, self.rew, self.done, self.fin_ret, self.fin_len, None,
+                             self.N, self.seed, 0, self.max_steps, True, self.step_t, hist=hist_out)
+        else:
+            self.h.pong_step(self.state, self._dummy_act, self.rew, self.done, self.fin_ret, self.fin_len, None,
+                             self.N, self.seed, 0, self.max_steps, True, self.step_t, obs=obs_out)
         self.advance(1)
 
     def episode_stats(self):
         """(episodes, sum return, sum length, sum return^2) over all envs since the last reset."""
         return self.ep_acc.double().sum(0)
 
-    def step(self, act: torch.Tensor, obs_out: torch.Tensor, rew_out=None, done_out=None, offset: int = None):
+    def step(self, act: torch.Tensor, obs_out: torch.Tensor = None, rew_out=None, done_out=None, offset: int = None,
+             hist_out: torch.Tensor = None):
         """One env step.  Without ``offset`` the device counter is advanced after the step;
-        with it (graph-captured rollouts) the caller advances once per rollout."""
+        with it (graph-captured rollouts) the caller advances once per rollout.  ``hist_out``
+        ([N, 16]) instead of ``obs_out``: physics only, the new frame histories written for a
+        fused-render conv stack (no 57 MB observation write per step at 2,048 envs)."""
         rew = self.rew if rew_out is None else rew_out
         done = self.done if done_out is None else done_out
-        # physics + render of the new 4-frame stack in one launch (one workgroup per env)
-        self.h.pong_step(self.state, act, rew, done, self.fin_ret, self.fin_len, self.ep_acc, self.N, self.seed,
-                         0 if offset is None else int(offset), self.max_steps, False, self.step_t, obs=obs_out)
+        if hist_out is not None:  # physics (one thread per env) + the 64-byte history row
+            self.h.pong_step(self.state, act, rew, done, self.fin_ret, self.fin_len, self.ep_acc, self.N, self.seed,
+                             0 if offset is None else int(offset), self.max_steps, False, self.step_t, hist=hist_out)
+        else:  # physics + render of the new 4-frame stack in one launch (one workgroup per env)
+            self.h.pong_step(self.state, act, rew, done, self.fin_ret, self.fin_len, self.ep_acc, self.N, self.seed,
+                             0 if offset is None else int(offset), self.max_steps, False, self.step_t, obs=obs_out)
         if offset is None:
             self.advance(1)
         return rew, done

@@ -354,11 +354,19 @@ class DeviceNatureCNN:
                         self._head_grid(n), head.get("step_base"), part=self._fc_part, splits=used,
                         fc_b=self.params[o["bfc"]:o["bfc"] + HIDDEN])
 
+    @staticmethod
+    def is_hist(obs) -> bool:
+        """PongSynth frame histories [n, 16] float32 (4 frames x (bx, by, pa, po)) instead of s2d
+        frames: the fused-render path, where the conv kernels draw the observation themselves."""
+        return obs.dtype == torch.float32 and obs.dim() == 2 and obs.shape[1] == 16
+
     def forward(self, obs_u8: torch.Tensor, row0: int = 0, fc: bool = True, store_acts: bool = True):
         """Conv stack + fc on obs [n, 84, 84, 4]; activations land in rows row0.. of the
         stored buffers.  Returns the hidden [n * 512] view (with fc=False only the conv
         stack runs and the view is not written yet).  store_acts=False: a1 / a2 are not
-        written (a forward no backward reads, e.g. the bootstrap value; fused path only)."""
+        written (a forward no backward reads, e.g. the bootstrap value; fused path only).
+        ``obs_u8`` may be PongSynth frame histories [n, 16] (``is_hist``): the 16-wave conv stack
+        then renders the frames in LDS and no observation tensor exists."""
         n = obs_u8.shape[0]
         assert row0 + n <= self.max_batch, "batch exceeds the model's activation buffers"
         h, o, sh, p = self.h, self.o, self.shadow, self.params
@@ -368,8 +376,13 @@ class DeviceNatureCNN:
         a3 = self._rows(self.a3, row0, n, FC_IN)
         hid = self._rows(self.hid, row0, n, HIDDEN)
         x = obs_u8.contiguous()
-        assert tuple(x.shape[1:]) == OBS_S2D, "device CNN takes space-to-depth observations [n, 21, 21, 64]"
-        if self.fused_convs:
+        if self.is_hist(x):
+            assert self.fused_convs and self.fwd_layout in (0, 64), "fused render: the 16-wave conv stack only"
+            h.conv_stack_fwd(None, *(t for i in (1, 2, 3) for t in (sh[o[f"w{i}"]:o[f"b{i}"]],
+                                                                        p[o[f"b{i}"]:o[f"b{i}"] + CONVS[i - 1].cout])),
+                             a1, a2, a3, n, store12=store_acts, hist=x)
+        elif self.fused_convs:
+            assert tuple(x.shape[1:]) == OBS_S2D, "device CNN takes space-to-depth observations [n, 21, 21, 64]"
             # conv1 -> conv2 -> conv3 in one launch, activations LDS-resident (cnn_fused.hip)
             h.conv_stack_fwd(x, *(t for i in (1, 2, 3) for t in (sh[o[f"w{i}"]:o[f"b{i}"]],
                                                                      p[o[f"b{i}"]:o[f"b{i}"] + CONVS[i - 1].cout])),
@@ -552,6 +565,7 @@ class DeviceNatureCNN:
             n2 = n1 = 0
             S2, S1, P2, P1 = L2.cout * L2.K, S2D.cout * S2D.K, L2.hout ** 2 * L2.cout, L1.hout ** 2 * L1.cout
             x8 = obs_u8.contiguous()
+            hist = self.is_hist(x8)
             for k in range(C):
                 b0, b1 = B * k // C, B * (k + 1) // C
                 nk = b1 - b0
@@ -562,8 +576,8 @@ class DeviceNatureCNN:
                             self.cpart["c2"][n2 * S2:], self.cbias["c2"][n2 * L2.cout:], nk, nblk,
                             staged=self.bwd2_variant)
                 n2 += nblk
-                n1 += int(h.conv1_wgrad8(x8[b0:b1], da1[b0 * P1:b1 * P1], self.cpart["c1"][n1 * S1:],
-                                         self.cbias["c1"][n1 * S2D.cout:], nk, nblk))
+                n1 += int(h.conv1_wgrad8(None if hist else x8[b0:b1], da1[b0 * P1:b1 * P1], self.cpart["c1"][n1 * S1:],
+                                         self.cbias["c1"][n1 * S2D.cout:], nk, nblk, hist=x8[b0:b1] if hist else None))
             sums += [(self.cpart["c2"], n2, S2, g[o["w2"]:o["b2"]]),
                      (self.cbias["c2"], n2, L2.cout, g[o["b2"]:o["b2"] + L2.cout])]
             c1_slabs = n1
@@ -583,8 +597,11 @@ class DeviceNatureCNN:
         # conv1 (input = frames, no data gradient)
         # (its bias gradient comes out of the same pass over da1)
         if self.fused_convs:
+            x8 = obs_u8.contiguous()
+            hist = self.is_hist(x8)
             ns = c1_slabs if c1_slabs is not None else int(
-                h.conv1_wgrad8(obs_u8.contiguous(), da1, self.cpart["c1"], self.cbias["c1"], B, min(B, self.cus)))
+                h.conv1_wgrad8(None if hist else x8, da1, self.cpart["c1"], self.cbias["c1"], B, min(B, self.cus),
+                               hist=x8 if hist else None))
             sums += [(self.cpart["c1"], ns, S2D.cout * S2D.K, g[o["w1"]:o["b1"]]),
                      (self.cbias["c1"], ns, S2D.cout, g[o["b1"]:o["b1"] + S2D.cout])]
             h.sum_splits_multi(sums)

@@ -49,6 +49,9 @@ class PixelA2CConfig:
     max_episode_steps: int = 27000 // 4
     phase_timing: bool = False
     use_graphs: bool = True        # capture the whole update (with its RCCL all-reduces) as one hipGraph
+    # GPU: the conv kernels draw the observations themselves from 16-float frame histories (no
+    # [T+1, N, 21, 21, 64] observation tensor is written or read); None = RRL_PONG_FUSED_RENDER
+    fused_render: Optional[bool] = None
 
     def to_dict(self):
         return asdict(self)
@@ -69,12 +72,18 @@ class PixelA2CTrainer:
         env_seed = (cfg.seed * 1000003 + rank * 7919 + 17) & 0x7FFFFFFFFFFFFFFF
         self.sample_seed = (cfg.seed * 2654435761 + rank * 97 + 5) & 0x7FFFFFFFFFFFFFFF
         dev = self.device
-        self.obs = torch.zeros((T + 1, N, 21, 21, 64), dtype=torch.uint8, device=dev)  # space-to-depth frames
+        import os
+
+        if cfg.fused_render is None:
+            cfg.fused_render = os.environ.get("RRL_PONG_FUSED_RENDER", "0") == "1"
+        self.fused_render = bool(cfg.fused_render) and self.on_gpu
+        if self.fused_render:  # the frame histories the conv kernels render from
+            self.obs = torch.zeros((T + 1, N, 16), dtype=torch.float32, device=dev)
+        else:
+            self.obs = torch.zeros((T + 1, N, 21, 21, 64), dtype=torch.uint8, device=dev)  # space-to-depth frames
         # GPU: two observation buffers used alternately -- update k rolls out of buffer k % 2 and
         # renders its last observation straight into slot 0 of the other one, where update k + 1
         # starts (no obs[T] -> obs[0] copy of 58 MB per update); one captured graph per buffer
-        import os
-
         two = dev.type == "cuda" and os.environ.get("RRL_PONG_OBS_COPY", "0") != "1"  # 1: the copy path (A/B)
         self._obs_bufs = [self.obs, torch.zeros_like(self.obs)] if two else [self.obs]
         self._par = 0
@@ -92,7 +101,10 @@ class PixelA2CTrainer:
 
             self.model = DeviceNatureCNN(self.spec, dev, max_batch=N * (T + 1), seed=cfg.seed)
             self.env = DevicePong(N, dev, env_seed, cfg.max_episode_steps)
-            self.env.reset(self.obs[0])
+            if self.fused_render:
+                self.env.reset(hist_out=self.obs[0])
+            else:
+                self.env.reset(self.obs[0])
             self.sample_t = torch.zeros(1, dtype=torch.int64, device=dev)  # Philox step of the action sampler
             self.adv = torch.zeros(T, N, device=dev)
             self.ret = torch.zeros(T, N, device=dev)
@@ -120,8 +132,11 @@ class PixelA2CTrainer:
             m.act(base[t], t * N, self.act[t], self.logp[t], self.val[t], self.sample_seed, t,
                   step_base=self.sample_t)
             # the last observation goes straight to the next update's start slot
-            self.env.step(self.act[t], base[t + 1] if (t + 1 < T or nxt is None) else nxt[0], self.rew[t],
-                          self.done[t], offset=t)
+            out = base[t + 1] if (t + 1 < T or nxt is None) else nxt[0]
+            if self.fused_render:
+                self.env.step(self.act[t], None, self.rew[t], self.done[t], offset=t, hist_out=out)
+            else:
+                self.env.step(self.act[t], out, self.rew[t], self.done[t], offset=t)
         # the sampling, env and Adam step counters advance inside the update's scan launch
         # (_update_gpu; every rollout is followed by one update)
         # bootstrap V(obs[T]) with the pre-update weights; its activations go to the
@@ -141,7 +156,8 @@ class PixelA2CTrainer:
                                       self._stats_part, stats=False,
                                       counters=((self.sample_t, T), (self.env.step_t, T), (m.step_t, 1)))
         with self.timer.phase("Backward"):
-            stats = m.backward(base[:T].reshape(B, 21, 21, 64), self.act.reshape(B), adv.reshape(B),
+            x = base[:T].reshape(B, 16) if self.fused_render else base[:T].reshape(B, 21, 21, 64)
+            stats = m.backward(x, self.act.reshape(B), adv.reshape(B),
                                ret.reshape(B), cfg.vf_coef, cfg.ent_coef, comm=self.comm)
         with self.timer.phase("Optimize"):
             m.apply(cfg.lr, cfg.max_grad_norm, self.comm, step_bumped=True)

@@ -813,6 +813,125 @@ def test_pixel_update_16wave_backward_and_chunks(cuda, monkeypatch):
     torch.testing.assert_close(ch.model.params, ref.model.params, rtol=1e-4, atol=1e-6)
 
 
+def _pong_histories(cuda, N, steps=40, seed=3):
+    """Frame histories of N PongSynth envs after ``steps`` random-action steps, and the s2d
+    observations the env's own step + render kernel drew for the same states."""
+    from relayrl_prototype_amd.envs.pong import DevicePong
+
+    env = DevicePong(N, cuda, seed)
+    obs = torch.zeros(N, 21, 21, 64, dtype=torch.uint8, device=cuda)
+    hist = torch.zeros(N, 16, device=cuda)
+    env.reset(obs)
+    g = torch.Generator().manual_seed(seed)
+    for _ in range(steps):
+        a = torch.randint(0, 6, (N,), dtype=torch.int32, generator=g).to(cuda)
+        env.step(a, obs)
+    # the history rows of the same states (pong state layout: P_HIST = 16 .. 31)
+    hist.copy_(env.state.view(N, -1)[:, 16:32])
+    return hist, obs
+
+
+def test_fused_render_draws_the_env_observation(cuda):
+    """pong_render_hist(frame histories) == the observation pong_step's render wrote, bitwise;
+    the history-output step kernel writes the same rows as the state's history slice."""
+    from relayrl_prototype_amd.envs.pong import DevicePong
+    from relayrl_prototype_amd.ops import hip
+
+    N = 777
+    hist, obs = _pong_histories(cuda, N)
+    drawn = torch.full_like(obs, 7)
+    hip().pong_render_hist(hist, drawn, N)
+    torch.cuda.synchronize()
+    assert torch.equal(drawn, obs)
+    # step with hist_out: same physics, rows equal to the state's history
+    e1, e2 = DevicePong(N, cuda, 5), DevicePong(N, cuda, 5)
+    o = torch.zeros(N, 21, 21, 64, dtype=torch.uint8, device=cuda)
+    h = torch.zeros(N, 16, device=cuda)
+    e1.reset(o)
+    e2.reset(hist_out=h)
+    g = torch.Generator().manual_seed(1)
+    for _ in range(30):
+        a = torch.randint(0, 6, (N,), dtype=torch.int32, generator=g).to(cuda)
+        e1.step(a, o)
+        e2.step(a, None, hist_out=h)
+        torch.cuda.synchronize()
+        assert torch.equal(e1.state, e2.state) and torch.equal(e1.rew, e2.rew) and torch.equal(e1.done, e2.done)
+        assert torch.equal(h, e2.state.view(N, -1)[:, 16:32])
+        hip().pong_render_hist(h, drawn[:N], N)
+        assert torch.equal(drawn[:N], o)
+
+
+@pytest.mark.parametrize("N", [5, 300, 2048])
+def test_fused_render_conv_stack_equals_the_obs_path(cuda, N):
+    """The 16-wave conv stack drawing its frames from histories (fused render) writes a1 / a2 / a3
+    bitwise equal to the same kernel reading the rendered observations."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    spec = CNNSpec()
+    o = spec.offsets()
+    params = spec.init(N).to(cuda)
+    params += 0.01 * torch.randn(params.shape, generator=torch.Generator().manual_seed(N)).to(cuda)
+    sh = params.bfloat16()
+    hist, obs = _pong_histories(cuda, N, seed=N)
+    W = [sh[o["w1"]:o["b1"]], params[o["b1"]:o["b1"] + 32], sh[o["w2"]:o["b2"]], params[o["b2"]:o["b2"] + 64],
+         sh[o["w3"]:o["b3"]], params[o["b3"]:o["b3"] + 64]]
+    outs = []
+    for fused in (False, True):
+        a1 = torch.full((N * 400 * 32,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        a2 = torch.full((N * 81 * 64,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        a3 = torch.full((N * FC_IN,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        if fused:
+            h.conv_stack_fwd(None, *W, a1, a2, a3, N, hist=hist)
+        else:
+            h.conv_stack_fwd(obs, *W, a1, a2, a3, N, probe=64)
+        torch.cuda.synchronize()
+        outs.append((a1, a2, a3))
+    for f, r in zip(*outs):
+        assert torch.isfinite(f.float()).all() and torch.equal(f, r)
+
+
+def test_fused_render_conv1_wgrad_equals_the_obs_path(cuda):
+    """conv1_wgrad8 drawing its frames from histories: weight and bias partials bitwise equal."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    N, grid = 1500, 256
+    hist, obs = _pong_histories(cuda, N, seed=11)
+    dy = torch.randn(N * 400 * 32, generator=torch.Generator().manual_seed(2)).bfloat16().to(cuda)
+    outs = []
+    for fused in (False, True):
+        part = torch.full((2 * grid * 32 * 256,), float("nan"), device=cuda)
+        bpart = torch.full((2 * grid * 32,), float("nan"), device=cuda)
+        ns = h.conv1_wgrad8(None, dy, part, bpart, N, grid, hist=hist) if fused else \
+            h.conv1_wgrad8(obs, dy, part, bpart, N, grid)
+        torch.cuda.synchronize()
+        outs.append((part[:ns * 32 * 256], bpart[:ns * 32]))
+    for f, r in zip(*outs):
+        assert torch.isfinite(f).all() and torch.equal(f, r)
+
+
+def test_pixel_update_fused_render_matches_the_obs_path(cuda, monkeypatch):
+    """A2C with the fused render (frame histories, no observation tensor) trains the same
+    trajectory bitwise as with rendered observations (both on the 16-wave forward), captured."""
+    from relayrl_prototype_amd.runtime.pixel_trainer import PixelA2CConfig, PixelA2CTrainer
+
+    monkeypatch.setenv("RRL_CNN_FWD_LAYOUT", "64")
+    runs = []
+    for fused in (False, True):
+        tr = PixelA2CTrainer(PixelA2CConfig(num_envs=300, rollout_len=4, seed=6, use_graphs=True,
+                                            fused_render=fused), device=cuda)
+        assert tr.fused_render == fused and tr.obs.dtype == (torch.float32 if fused else torch.uint8)
+        for _ in range(5):
+            tr.train_epoch()
+        torch.cuda.synchronize()
+        runs.append(tr)
+    a, b = runs
+    assert torch.equal(a.act, b.act) and torch.equal(a.rew, b.rew)
+    torch.testing.assert_close(a.model.params, b.model.params, rtol=0, atol=0)
+    assert a.metrics()["EnvSteps"] == b.metrics()["EnvSteps"]
+
+
 def test_pixel_alternating_obs_buffers_match_copy_path(cuda, monkeypatch):
     """Two observation buffers used alternately (the last render of update k lands in slot 0 of
     update k + 1's buffer) train exactly like the single buffer + obs[T] -> obs[0] copy."""
