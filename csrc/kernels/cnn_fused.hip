@@ -369,6 +369,10 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
 //     conv1 uses 16, conv2 16), each role's tiles in passes small enough for 128 registers.
 // Per iteration j: B0 | frame n_j: registers -> LDS, next frame's loads issued | B1 | the
 // three stages.  j runs two frames past this workgroup's last one to drain conv2 / conv3.
+#ifndef CS16_RENDER_THREADS  // fused render: the conv1 waves (threads 0..511) draw the frame
+#define CS16_RENDER_THREADS 512
+#define CS16_RENDER_ROLES(r) ((r) == 1)
+#endif
 #ifndef CS16_C2_MT
 #define CS16_C2_MT 2
 #endif
@@ -394,8 +398,7 @@ constexpr int kXPerT = (kXChunks + kThreads - 1) / kThreads;
 // 51.8 / 177.3 us per 2,048 / 8,192 frames (profiles/r5_cnn16_kbench.jsonl) -- the epilogue's
 // 8-byte stores are not what bounds this kernel.
 // bit 2 -- fused render: the frames are drawn in the kernel from 16-float PongSynth frame
-// histories (pong_render.h) instead of read from an observation tensor; the workgroup's history
-// rows sit in LDS behind the a2 buffers (64 B per frame, sized at launch)
+// histories (pong_render.h) instead of read from an observation tensor
 template <int V>
 struct L16 {
   static constexpr bool kPhaseA1 = (V & 16) != 0, kGrid3 = (V & 32) != 0, kRender = (V & 2) != 0;
@@ -409,6 +412,19 @@ struct L16 {
   static_assert(kA1Off % 16 == 0 && kA2Off % 16 == 0, "16-byte aligned LDS regions");
 };
 }  // namespace cs16
+
+// A frame-history row every lane reads in full: loaded once per wave and kept in SGPRs
+// (readfirstlane), so the fused render adds no vector registers to the conv waves.
+__device__ __forceinline__ void uniform_row(const float* __restrict__ row, float (&hv)[kPongHist]) {
+#pragma unroll
+  for (int i = 0; i < kPongHist; i += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(row + i);
+    hv[i] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v.x)));
+    hv[i + 1] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v.y)));
+    hv[i + 2] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v.z)));
+    hv[i + 3] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v.w)));
+  }
+}
 
 __device__ __forceinline__ bf16x8_t u8x8_frag(uint32_t lo, uint32_t hi) {
   return __builtin_bit_cast(bf16x8_t, u8x8_to_bf16x8(make_uint2(lo, hi)));
@@ -456,7 +472,6 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
   }
 
   const int G = gridDim.x, n0 = blockIdx.x, N = A.N;
-  float* H = reinterpret_cast<float*>(smem + L::kLds / 2);  // fused render: [frames of this workgroup][16]
   uint4 rx[L::kRender ? 1 : kXPerT];
   auto gload = [&](size_t n) {
     if constexpr (L::kRender) return;
@@ -467,24 +482,20 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
       rx[k] = q < kXChunks ? xs[q] : make_uint4(0, 0, 0, 0);
     }
   };
-  if constexpr (L::kRender) {  // every history row this workgroup draws (published by the first B0)
-    const int J = n0 < N ? (N - n0 + G - 1) / G : 0;
-    for (int t = tid; t < 4 * J; t += kThreads)
-      *reinterpret_cast<float4*>(H + 4 * t) =
-          *reinterpret_cast<const float4*>(A.hist + (size_t)(n0 + (t >> 2) * G) * kPongHist + 4 * (t & 3));
-  }
   if (n0 < N) gload(n0);
   for (int j = 0; n0 + (j - 2) * G < N; ++j) {
     const int n = n0 + j * G;
     __syncthreads();  // B0: the previous iteration's stages are done (F free, a1 / a2 buffers complete)
     if constexpr (L::kRender) {
-      // fused render: the conv1 waves (whose 64 weight registers leave room for it) draw the
-      // frame's 1,764 chunks, 4 each
-      if (ROLE == 1 && n < N) {
-        for (int q = tid; q < kXChunks; q += 512) {
+      // fused render: every thread draws <= 2 of the frame's 1,764 chunks; the history row has a
+      // wave-uniform address, so its 16 floats come in through scalar loads into SGPRs
+      if (CS16_RENDER_ROLES(ROLE) && n < N) {
+        float hv[kPongHist];
+        uniform_row(A.hist + (size_t)n * kPongHist, hv);
+        constexpr int T = CS16_RENDER_THREADS;
+        for (int q = tid; q < kXChunks; q += T) {
           const int pix = q >> 2, pa = pix / 21;
-          *reinterpret_cast<uint4*>(F + (pix + (kFW - 21) * pa) * kFS + (q & 3) * 16) =
-              pong_render_chunk(H + j * kPongHist, q);
+          *reinterpret_cast<uint4*>(F + (pix + (kFW - 21) * pa) * kFS + (q & 3) * 16) = pong_render_chunk(hv, q);
         }
       }
     } else if (n < N) {
@@ -644,8 +655,6 @@ static int launch_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const flo
   return (int)hipGetLastError();
 }
 
-constexpr int cs16_hist_bytes = kPongHist * 4;
-
 template <int V>
 static int launch_conv_stack16_fwd(const uint8_t* x, const float* hist, const uint16_t* w1, const float* b1,
                                    const uint16_t* w2, const float* b2, const uint16_t* w3, const float* b3,
@@ -659,12 +668,8 @@ static int launch_conv_stack16_fwd(const uint8_t* x, const float* hist, const ui
   }
   if (N < 1) return 0;
   const int grid = N < max_grid ? N : max_grid;  // one 146-161 KB-LDS workgroup per CU
-  int lds = L::kLds;
-  if (L::kRender) {
-    if (!hist) return -2;
-    lds += ((N + grid - 1) / grid) * cs16_hist_bytes;  // the workgroup's history rows
-    if (lds > 160 * 1024) return -3;                    // too many frames per workgroup for LDS
-  }
+  const int lds = L::kLds;
+  if (L::kRender && !hist) return -2;
   const Stack16Args args{x, hist, w1, w2, w3, b1, b2, b3, y1, y2, y3, N};
   hipLaunchKernelGGL(conv_stack16_fwd_kernel<V>, dim3(grid), dim3(cs16::kThreads), lds, stream, args);
   return (int)hipGetLastError();
@@ -1691,8 +1696,8 @@ constexpr int kXC = 441 * 4, kYC = 400 * 4;       // 16-byte chunks per image
 constexpr int kXPT = (kXC + kThreads - 1) / kThreads, kYPT = (kYC + kThreads - 1) / kThreads;
 }  // namespace c1w
 
-// RENDER: the frames are drawn from PongSynth frame histories hist[N][16] (pong_render.h), the
-// workgroup's rows staged in LDS behind dY, instead of read from an observation tensor
+// RENDER: the frames are drawn from PongSynth frame histories hist[N][16] (pong_render.h)
+// instead of read from an observation tensor
 template <bool RENDER>
 __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const uint8_t* __restrict__ x,
                                                                         const float* __restrict__ hist,
@@ -1726,7 +1731,6 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
     ones = __builtin_bit_cast(bf16x8_t, v);
   }
   uint4 rx[kXPT], ry[kYPT];
-  float* H = reinterpret_cast<float*>(smem + kLds / 2);  // RENDER: [images of this workgroup][16]
   auto gload = [&](int n) {
     const uint4* xs = reinterpret_cast<const uint4*>(x + (size_t)n * 441 * 64);
     const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 400 * 32);
@@ -1744,15 +1748,11 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
   };
   const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
   const int n0 = blockIdx.x, G = gridDim.x;
-  if constexpr (RENDER) {  // every history row this workgroup draws (published by the loop's first barrier)
-    const int J = n0 < N ? (N - n0 + G - 1) / G : 0;
-    for (int t = tid; t < 4 * J; t += kThreads)
-      *reinterpret_cast<float4*>(H + 4 * t) =
-          *reinterpret_cast<const float4*>(hist + (size_t)(n0 + (t >> 2) * G) * kPongHist + 4 * (t & 3));
-  }
   if (n0 < N) gload(n0);
   for (int n = n0; n < N; n += G) {
     __syncthreads();  // the previous image's fragment reads are done
+    float hv[RENDER ? kPongHist : 1];
+    if constexpr (RENDER) uniform_row(hist + (size_t)n * kPongHist, hv);
 #pragma unroll
     for (int i = 0; i < kXPT; ++i) {
       const int q = tid + kThreads * i;
@@ -1760,7 +1760,7 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
         const int pix = q >> 2;
         uint16_t* d = Xi + (pix + (kXW - 21) * (pix / 21)) * kLd + (q & 3) * 16;
         uint4 v;
-        if constexpr (RENDER) v = pong_render_chunk(H + ((n - n0) / G) * kPongHist, q);
+        if constexpr (RENDER) v = pong_render_chunk(hv, q);
         else v = rx[i];
         *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(v.x, v.y));
         *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(v.z, v.w));
@@ -1829,10 +1829,8 @@ extern "C" int rrl_conv1_wgrad8(const uint8_t* x, const float* hist, const uint1
   }
   if (N < 1 || grid < 1) return 0;
   if (hist) {
-    const int lds = c1w::kLds + ((N + grid - 1) / grid) * kPongHist * 4;
-    if (lds > 160 * 1024) return -3;  // too many images per workgroup for the LDS history rows
-    hipLaunchKernelGGL(conv1_wgrad8_kernel<true>, dim3(grid), dim3(c1w::kThreads), lds, (hipStream_t)stream, x, hist,
-                       dy, part, bias_part, N);
+    hipLaunchKernelGGL(conv1_wgrad8_kernel<true>, dim3(grid), dim3(c1w::kThreads), c1w::kLds, (hipStream_t)stream, x,
+                       hist, dy, part, bias_part, N);
   } else {
     hipLaunchKernelGGL(conv1_wgrad8_kernel<false>, dim3(grid), dim3(c1w::kThreads), c1w::kLds, (hipStream_t)stream, x,
                        hist, dy, part, bias_part, N);
