@@ -369,10 +369,6 @@ __global__ __launch_bounds__(cs::kThreads, 1) void conv_stack_fwd_kernel(
 //     conv1 uses 16, conv2 16), each role's tiles in passes small enough for 128 registers.
 // Per iteration j: B0 | frame n_j: registers -> LDS, next frame's loads issued | B1 | the
 // three stages.  j runs two frames past this workgroup's last one to drain conv2 / conv3.
-#ifndef CS16_RENDER_THREADS  // fused render: the conv1 waves (threads 0..511) draw the frame
-#define CS16_RENDER_THREADS 512
-#define CS16_RENDER_ROLES(r) ((r) == 1)
-#endif
 #ifndef CS16_C2_MT
 #define CS16_C2_MT 2
 #endif
@@ -405,13 +401,20 @@ struct L16 {
   static constexpr int kA1Ld = kPhaseA1 ? 48 : 40, kA2Ld = 80;
   static constexpr int kA1Rows = kPhaseA1 ? 407 : 400, kA2Rows = kGrid3 ? 84 : 81;
   static constexpr int kA1Elems = kA1Rows * kA1Ld, kA2Elems = kA2Rows * kA2Ld;
-  static constexpr int kA1Off = kFBytes;         // byte offsets
+  // fused render: TWO frame buffers (the conv1 waves draw frame j + 1 while frame j is read) of
+  // 441 positions x 64 B, 16-byte chunks XOR-swizzled (rfs_chunk: 2.0 -> 1.6 LDS cycles per
+  // conflict-free cycle on the conv1 reads, tools/lds_bank_model.py)
+  static constexpr int kRFBytes = 441 * 64;
+  static constexpr int kA1Off = kRender ? 2 * kRFBytes : kFBytes;  // byte offsets
   static constexpr int kA2Off = kA1Off + 2 * kA1Elems * 2;
   static constexpr int kLds = kA2Off + 2 * kA2Elems * 2;  // 145,696 bytes (default) .. 160,800 (bits 16 | 32)
   static_assert(kLds <= 160 * 1024, "LDS per workgroup");
   static_assert(kA1Off % 16 == 0 && kA2Off % 16 == 0, "16-byte aligned LDS regions");
 };
 }  // namespace cs16
+
+// chunk c of frame position r in the fused-render frame buffer (positions contiguous, 64 B each)
+__device__ __forceinline__ int rfs_chunk(int r, int c) { return r * 64 + 16 * (c ^ (2 * ((r >> 2) & 1))); }
 
 // A frame-history row every lane reads in full: loaded once per wave and kept in SGPRs
 // (readfirstlane), so the fused render adds no vector registers to the conv waves.
@@ -482,22 +485,25 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
       rx[k] = q < kXChunks ? xs[q] : make_uint4(0, 0, 0, 0);
     }
   };
+  // fused render: the conv1 waves draw frame n into buffer b (the history row has a wave-uniform
+  // address: its 16 floats go to SGPRs); they do it for frame n + G right after their conv1 of
+  // frame n, beside the longer conv2 / conv3 work of the other waves, so the pipeline keeps ONE
+  // barrier per iteration
+  auto render = [&](int nn, int b) {
+    float hv[kPongHist];
+    uniform_row(A.hist + (size_t)nn * kPongHist, hv);
+    uint8_t* Fb = F + b * L::kRFBytes;
+    for (int q = tid; q < kXChunks; q += 512) *reinterpret_cast<uint4*>(Fb + rfs_chunk(q >> 2, q & 3)) = pong_render_chunk(hv, q);
+  };
+  if constexpr (L::kRender) {
+    if (ROLE == 1 && n0 < N) render(n0, 0);
+  }
   if (n0 < N) gload(n0);
   for (int j = 0; n0 + (j - 2) * G < N; ++j) {
     const int n = n0 + j * G;
     __syncthreads();  // B0: the previous iteration's stages are done (F free, a1 / a2 buffers complete)
     if constexpr (L::kRender) {
-      // fused render: every thread draws <= 2 of the frame's 1,764 chunks; the history row has a
-      // wave-uniform address, so its 16 floats come in through scalar loads into SGPRs
-      if (CS16_RENDER_ROLES(ROLE) && n < N) {
-        float hv[kPongHist];
-        uniform_row(A.hist + (size_t)n * kPongHist, hv);
-        constexpr int T = CS16_RENDER_THREADS;
-        for (int q = tid; q < kXChunks; q += T) {
-          const int pix = q >> 2, pa = pix / 21;
-          *reinterpret_cast<uint4*>(F + (pix + (kFW - 21) * pa) * kFS + (q & 3) * 16) = pong_render_chunk(hv, q);
-        }
-      }
+      // (fused render: frame n is already in buffer j & 1)
     } else if (n < N) {
 #pragma unroll
       for (int k = 0; k < kXPerT; ++k) {
@@ -509,7 +515,7 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
       }
       if (n + G < N) gload((size_t)n + G);  // lands while this frame computes
     }
-    __syncthreads();  // B1: F holds frame n
+    if constexpr (!L::kRender) __syncthreads();  // B1: F holds frame n
     if constexpr (ROLE == 1) {
       // ---- conv1(n): pixel tiles wave + 8 t, one tile at a time, both co tiles
       if (n < N) {
@@ -518,10 +524,16 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
         for (int t = 0; t < ntile; ++t) {
           const int p = 16 * (wave + 8 * t) + i;
           const uint8_t* src = F + ((p / 20) * kFW + p % 20) * kFS + 16 * g;
+          const uint8_t* Fb = F + (j & 1) * L::kRFBytes;
+          const int r0 = (p / 20) * 21 + p % 20;  // fused render: positions in rows of 21
           f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int tap = 0; tap < 4; ++tap) {
-            const uint4 raw = *reinterpret_cast<const uint4*>(src + ((tap >> 1) * kFW + (tap & 1)) * kFS);
+            uint4 raw;
+            if constexpr (L::kRender)
+              raw = *reinterpret_cast<const uint4*>(Fb + rfs_chunk(r0 + (tap >> 1) * 21 + (tap & 1), g));
+            else
+              raw = *reinterpret_cast<const uint4*>(src + ((tap >> 1) * kFW + (tap & 1)) * kFS);
             const bf16x8_t lo = u8x8_frag(raw.x, raw.y), hi = u8x8_frag(raw.z, raw.w);
             acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[2 * tap], lo, acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[8 + 2 * tap], lo, acc1, 0, 0, 0);
@@ -541,6 +553,9 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
             *reinterpret_cast<uint2*>(yd + 16 + 4 * g) = v1;
           }
         }
+      }
+      if constexpr (L::kRender) {
+        if (n + G < N) render(n + G, (j + 1) & 1);
       }
     } else if constexpr (ROLE == 2) {
       // ---- conv2(n - G): co tile ct, 6 pixel tiles in passes (81 px; the rest discarded)
@@ -1731,39 +1746,54 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
     ones = __builtin_bit_cast(bf16x8_t, v);
   }
   uint4 rx[kXPT], ry[kYPT];
-  auto gload = [&](int n) {
-    const uint4* xs = reinterpret_cast<const uint4*>(x + (size_t)n * 441 * 64);
-    const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 400 * 32);
+  // the next image's frame chunks: loaded (observations) or drawn (RENDER: the history row's 16
+  // floats in SGPRs) into the same registers
+  auto xload = [&](int n) {
+    if constexpr (RENDER) {
+      float hv[kPongHist];
+      uniform_row(hist + (size_t)n * kPongHist, hv);
 #pragma unroll
-    for (int i = 0; i < kXPT; ++i) {
-      const int q = tid + kThreads * i;
-      if constexpr (RENDER) rx[i] = make_uint4(0, 0, 0, 0);
-      else rx[i] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
+      for (int i = 0; i < kXPT; ++i) {
+        const int q = tid + kThreads * i;
+        rx[i] = q < kXC ? pong_render_chunk(hv, q) : make_uint4(0, 0, 0, 0);
+      }
+    } else {
+      const uint4* xs = reinterpret_cast<const uint4*>(x + (size_t)n * 441 * 64);
+#pragma unroll
+      for (int i = 0; i < kXPT; ++i) {
+        const int q = tid + kThreads * i;
+        rx[i] = q < kXC ? xs[q] : make_uint4(0, 0, 0, 0);
+      }
     }
+  };
+  auto gload = [&](int n) {
+    const uint4* ys = reinterpret_cast<const uint4*>(dy + (size_t)n * 400 * 32);
 #pragma unroll
     for (int i = 0; i < kYPT; ++i) {
       const int q = tid + kThreads * i;
       ry[i] = q < kYC ? ys[q] : make_uint4(0, 0, 0, 0);
     }
   };
+  // RENDER: the first half of the waves draws the next frame before its MFMAs, the second half
+  // (the other wave of each SIMD) after them, so one wave's VALU drawing runs beside the other's
+  // matrix work
+  const bool draw_late = RENDER && half;
   const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
   const int n0 = blockIdx.x, G = gridDim.x;
-  if (n0 < N) gload(n0);
+  if (n0 < N) {
+    gload(n0);
+    xload(n0);
+  }
   for (int n = n0; n < N; n += G) {
     __syncthreads();  // the previous image's fragment reads are done
-    float hv[RENDER ? kPongHist : 1];
-    if constexpr (RENDER) uniform_row(hist + (size_t)n * kPongHist, hv);
 #pragma unroll
     for (int i = 0; i < kXPT; ++i) {
       const int q = tid + kThreads * i;
       if (q < kXC) {
         const int pix = q >> 2;
         uint16_t* d = Xi + (pix + (kXW - 21) * (pix / 21)) * kLd + (q & 3) * 16;
-        uint4 v;
-        if constexpr (RENDER) v = pong_render_chunk(hv, q);
-        else v = rx[i];
-        *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(v.x, v.y));
-        *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(v.z, v.w));
+        *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(rx[i].x, rx[i].y));
+        *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(rx[i].z, rx[i].w));
       }
     }
 #pragma unroll
@@ -1771,7 +1801,10 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
       const int q = tid + kThreads * i;
       if (q < kYC) *reinterpret_cast<uint4*>(Yi + (q >> 2) * kYLd + (q & 3) * 8) = ry[i];
     }
-    if (n + G < N) gload(n + G);
+    if (n + G < N) {
+      gload(n + G);
+      if (!draw_late) xload(n + G);
+    }
     __syncthreads();
     // MFMA k-order: lane group g of a 32-pixel chunk takes pixels 4g..4g+3 and 16+4g..16+4g+3
     // (a 4-pixel run never crosses an output row, so its frame rows are consecutive)
@@ -1796,6 +1829,7 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
         for (int mt = 0; mt < 2; ++mt) accb[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], ones, accb[mt], 0, 0, 0);
       }
     }
+    if (draw_late && n + G < N) xload(n + G);
   }
   const int slab = 2 * blockIdx.x + half;
   if (do_bias && (lane & 15) == 0) {
