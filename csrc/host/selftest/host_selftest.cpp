@@ -4,8 +4,14 @@
 // concurrent piece of ours: ZMTP sockets (acceptor / reader threads, multi-peer
 // ROUTER, PUSH fan-in from several threads, close while peers are live), the VecEnv
 // thread pool, the codecs on malformed input, and NativePolicy.
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <string>
 #include <thread>
@@ -68,6 +74,71 @@ static void test_codec() {
     st_decode(bad);
   } catch (const std::exception&) {
   }
+  // the header parser on every truncation of a real header: throws or parses, never reads past it
+  uint64_t hl = 0;
+  for (int i = 0; i < 8; ++i) hl |= (uint64_t)(uint8_t)f[i] << (8 * i);
+  const std::string hdr = f.substr(8, hl);
+  for (size_t cut = 0; cut <= hdr.size(); ++cut) {
+    std::string h = hdr.substr(0, cut);  // an exact-size heap copy: ASan sees any over-read
+    try {
+      StHeader sh = st_header(h.data(), h.size());
+      CHECK(sh.off1 >= sh.off0);
+    } catch (const std::exception&) {
+    }
+  }
+}
+
+// raw TCP peer for the handshake tests: connects and writes ``bytes`` (maybe nothing), then waits
+static int raw_peer(int port, const std::string& bytes) {
+  const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  CHECK(fd >= 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)port);
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  CHECK(::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) == 0);
+  if (!bytes.empty()) CHECK(::write(fd, bytes.data(), bytes.size()) == (ssize_t)bytes.size());
+  return fd;
+}
+
+// the round-5 I/O thread: connection-per-upload churn from several threads, garbage and silent
+// handshakes among them, a byte-bounded inbox under large messages, close with peers mid-handshake
+static void test_zmtp_fanin() {
+  zmtp::Socket pull(zmtp::SockType::PULL);
+  const int port = pull.bind("tcp://127.0.0.1:0");
+  const std::string ep = "tcp://127.0.0.1:" + std::to_string(port);
+  pull.set_inbox_limits(64, 1 << 20);
+  const int garbage = raw_peer(port, std::string(64, '\x5a'));  // not a ZMTP greeting
+  const int silent = raw_peer(port, "");                          // never greets
+  constexpr int kThreads = 4, kConns = 60;
+  std::vector<std::thread> senders;
+  for (int t = 0; t < kThreads; ++t)
+    senders.emplace_back([&, t] {
+      for (int i = 0; i < kConns; ++i) {  // a new connection (and handshake) per upload
+        zmtp::Socket push(zmtp::SockType::PUSH);
+        push.connect(ep);
+        const std::string body = (i % 10 == 0) ? std::string(200000, (char)('a' + t)) : std::to_string(t * 1000 + i);
+        CHECK(push.send({body}, 10000));
+        push.close();
+      }
+    });
+  int got = 0, big = 0;
+  zmtp::Message m;
+  while (got < kThreads * kConns && pull.recv(m, 10000)) {
+    ++got;
+    if (m.frames[0].size() == 200000) ++big;
+    CHECK(pull.inbox_bytes() <= (1u << 20) + 200000 + 64);  // one message may straddle the bound
+  }
+  for (auto& s : senders) s.join();
+  CHECK(got == kThreads * kConns && big == kThreads * kConns / 10);
+  const zmtp::Stats st = pull.stats();
+  CHECK(st.messages_in == (uint64_t)(kThreads * kConns));
+  // close while the silent / garbage peers are still connected and a fresh one is mid-handshake
+  const int late = raw_peer(port, std::string("\xff\0\0\0\0\0\0\0\x01\x7f", 10));
+  pull.close();
+  ::close(garbage);
+  ::close(silent);
+  ::close(late);
 }
 
 static void test_zmtp() {
@@ -150,6 +221,7 @@ int main() {
   test_policy();
   test_vecenv();
   test_zmtp();
+  test_zmtp_fanin();
   std::printf("host selftest OK\n");
   return 0;
 }
