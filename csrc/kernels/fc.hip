@@ -448,6 +448,506 @@ __global__ void __launch_bounds__(256) transpose_bf16_kernel(const uint16_t* __r
   }
 }
 
+
+// ----------------------------------------------------------------------------- persistent big tiles
+// The kernels above run 128 x 128 tiles, 64 x 32 per wave, one tile per workgroup: per k-tile
+// each workgroup pulls 32 KB through L2 for 2.1 MFLOP (64 FLOP/B), and every tile pays its own
+// prologue (first DMA latency) and epilogue (store tail) -- at the Pong shapes 0.5-0.8 PFLOP/s
+// (profiles/r3_fc_kbench.jsonl).  These are PERSISTENT: one 512-thread workgroup per CU walks
+// a flat sequence of (tile, k-tile) steps, so the LDS ring runs straight across tile
+// boundaries (the next tile's first k-tiles are in flight during this tile's epilogue), with
+// 256 x 128 tiles (85 FLOP/B) and 64 x 64 per wave (16 MFMAs per 8 fragment reads).
+//
+// vmcnt accounting: LDS-DMA, the epilogue's stores and its prefetch loads all count on one
+// in-order counter, so the wait for step u's DMA must know how many vector-memory ops were
+// issued after it: the next step's DMA (D per wave) and the epilogue of a tile that ended at
+// step u - 1 or u - 2 (E per wave).  Every wave issues EXACTLY E epilogue ops -- lanes with
+// nothing to store write a private dummy slot instead of branching around the store -- and
+// every item has >= 2 k-tiles, so at most one epilogue sits in that window.
+template <int N>
+__device__ __forceinline__ void fcp_vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int D, int E>
+__device__ __forceinline__ void fcp_wait_window(bool next_dma, bool epi) {
+  if (next_dma) {
+    if (epi) fcp_vm_wait<D + E>();
+    else fcp_vm_wait<D>();
+  } else {
+    if (epi) fcp_vm_wait<E>();
+    else fcp_vm_wait<0>();
+  }
+}
+
+// XCD-aware logical id of a persistent block (bijective for any grid size)
+__device__ __forceinline__ int fcp_lid() {
+  const int G = gridDim.x, b = blockIdx.x;
+  const int q = G >> 3, rem = G & 7, xcd = b & 7;
+  return (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+}
+
+// rows row0 .. row0 + R - 1 of a K-contiguous operand, k-tile k0, into a swizzled [R][64] image
+// (the fc_swz layout): R / 64 DMA instructions per wave, 8 rows each
+template <int R>
+__device__ __forceinline__ void fcp_stage(const uint16_t* __restrict__ X, int rows, int K, int row0, int k0,
+                                          uint16_t* img, int wave, int lane) {
+#pragma unroll
+  for (int jj = 0; jj < R / 64; ++jj) {
+    const int r0 = 8 * (wave + 8 * jj);
+    const int r = r0 + (lane >> 3);
+    const int kc = (lane & 7) ^ ((r >> 1) & 7);
+    const int gr = min(row0 + r, rows - 1);  // past the end: a duplicate row, never stored
+    __builtin_amdgcn_global_load_lds(X + (size_t)gr * K + k0 + 8 * kc,
+                                     (__attribute__((address_space(3))) void*)(img + r0 * kFcBK), 16, 0, 0);
+  }
+}
+
+// fc_tn_frag through inline asm: the ds_read_tr16_b64 builtin makes hipcc wait vmcnt(0) before
+// every read while an LDS-DMA is in flight (it cannot tell which LDS the read touches), which
+// drains the whole ring each k-tile.  The asm reads are invisible to the compiler's counters, so
+// fcp_lgkm_wait retires them (tied to the fragments) before the MFMAs use them.
+__device__ __forceinline__ s16x4_t fcp_tr_b64(const uint16_t* p) {
+  s16x4_t v;
+  const uint32_t a = (uint32_t)(size_t)(const __attribute__((address_space(3))) uint16_t*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+__device__ __forceinline__ bf16x8_t fcp_tn_frag(const uint16_t* img, int k0, int col0, int lane) {
+  const int q = (lane >> 2) & 3, p = lane & 3;
+  const int c = (col0 + 4 * p) >> 3, half = (p & 1) * 4;
+  const s16x4_t lo = fcp_tr_b64(img + 8 * fc_tn_swz(k0 + q, c) + half);
+  const s16x4_t hi = fcp_tr_b64(img + 8 * fc_tn_swz(k0 + 4 + q, c) + half);
+  typedef short s16x8_t __attribute__((ext_vector_type(8)));
+  const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+template <int FI, int FJ>
+__device__ __forceinline__ void fcp_lgkm_wait(bf16x8_t (&x)[FI], bf16x8_t (&y)[FJ]) {
+  static_assert(FI == 4 && FJ == 4, "tie list written for 4 + 4 fragments");
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(y[0]), "+v"(y[1]),
+               "+v"(y[2]), "+v"(y[3]));
+}
+
+// 64 lanes x 16 B that epilogue lanes with nothing to store write (a device global: no allocation,
+// nothing to do inside a graph capture)
+__device__ __attribute__((aligned(16))) float fcp_dummy[64 * 4];
+
+struct FcpPart {  // fp32 split-K partials part[z][M][N]
+  float* part;
+  static constexpr int kOpsPerFrag = 1;
+  static constexpr bool kPrefetch = false;
+};
+struct FcpMask {  // bf16 out = product * (mask > 0), mask loads prefetched during the last k-tile
+  uint16_t* out;
+  const uint16_t* mask;
+  static constexpr int kOpsPerFrag = 2;
+  static constexpr bool kPrefetch = true;
+};
+
+template <int BM, int BN, int WGM, int STAGES>
+struct FcpCfg {
+  static constexpr int WGN = 8 / WGM;
+  static constexpr int TM = BM / WGM, TN = BN / WGN;  // per-wave tile
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int ImgA = BM * kFcBK, ImgB = BN * kFcBK;
+  static constexpr int Stage = ImgA + ImgB;
+  static constexpr int LdsBytes = STAGES * Stage * 2;
+  static constexpr int D = (BM + BN) / 64;  // DMA instructions per wave per k-tile
+  static_assert(WGM * WGN == 8 && TM % 16 == 0 && TN % 16 == 0 && BM % 64 == 0 && BN % 64 == 0, "tile shape");
+  static_assert(STAGES == 2 || STAGES == 3, "ring depth");
+  static_assert(LdsBytes <= 160 * 1024, "LDS");
+};
+
+// One 16-byte LDS-DMA piece.  Kept in a __device__ function: an amdgcn builtin called directly in
+// a lambda inside a kernel template makes hipcc's HOST pass drop the kernel's launch stub
+// without a diagnostic (the .so then fails to load with an undefined symbol).
+__device__ __forceinline__ void fcp_glds(const uint16_t* src, uint16_t* dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+// bf16 pair (round to nearest even, NaN kept) in one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t fcp_pk_bf16(float a, float b) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){a, b}, bf2));
+}
+// keep-mask of a word of two bf16: 0xffff per half whose value is > 0 (sign clear, not zero;
+// the layer input is a ReLU output)
+__device__ __forceinline__ uint32_t fcp_pos_mask(uint32_t w) {
+  return (((int32_t)(w << 16) > 0) ? 0x0000ffffu : 0u) | (((int32_t)w > 0xffff) ? 0xffff0000u : 0u);
+}
+
+// C[m][n] = sum_k A[m][k] B[n][k]; items = (n-tile fastest, m-tile, split z), block lid takes
+// items lid, lid + G, ...  Per-item work (the tile decode, the lanes' DMA source rows) is done
+// once per item; a k-step adds only the k offset.
+template <int BM, int BN, int WGM, int STAGES, class Epi>
+__global__ void __launch_bounds__(kFcThreads, 1)
+fcp_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, Epi epi, int M, int N, int K,
+              int tiles_m, int tiles_n, int kps, int items) {
+  using C = FcpCfg<BM, BN, WGM, STAGES>;
+  constexpr int FM = C::FM, FN = C::FN, E = Epi::kOpsPerFrag * FM * FN;
+  constexpr int JA = BM / 64, JB = BN / 64;  // DMA instructions per wave per operand
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = gridDim.x, lid = fcp_lid();
+  const int ktot = K / kFcBK, tmn = tiles_m * tiles_n;
+  int S = 0;
+  for (int it = lid; it < items; it += G) S += min(ktot - (it / tmn) * kps, kps);
+
+  // issue cursor: the current item's lane source rows (k offset added per step)
+  const uint16_t* pa[JA];
+  const uint16_t* pb[JB];
+  int i_it = lid, i_kt = 0, i_nk = 0, i_k = 0, i_slot = 0, i_u = 0;
+  auto issue_item = [&](int it) {
+    const int tn = it % tiles_n, rest = it / tiles_n, tm = rest % tiles_m, z = rest / tiles_m;
+    i_nk = min(ktot - z * kps, kps);
+    i_k = z * kps * kFcBK;
+#pragma unroll
+    for (int jj = 0; jj < JA; ++jj) {
+      const int r = 8 * (wave + 8 * jj) + (lane >> 3), kc = (lane & 7) ^ ((r >> 1) & 7);
+      pa[jj] = A + (size_t)min(tm * BM + r, M - 1) * K + 8 * kc;  // past the end: a duplicate row
+    }
+#pragma unroll
+    for (int jj = 0; jj < JB; ++jj) {
+      const int r = 8 * (wave + 8 * jj) + (lane >> 3), kc = (lane & 7) ^ ((r >> 1) & 7);
+      pb[jj] = B + (size_t)min(tn * BN + r, N - 1) * K + 8 * kc;
+    }
+  };
+  if (S) issue_item(lid);
+  auto issue = [&]() {
+    uint16_t* st = smem + i_slot * C::Stage;
+#pragma unroll
+    for (int jj = 0; jj < JA; ++jj)
+      fcp_glds(pa[jj] + i_k, st + 8 * (wave + 8 * jj) * kFcBK);
+#pragma unroll
+    for (int jj = 0; jj < JB; ++jj)
+      fcp_glds(pb[jj] + i_k, st + C::ImgA + 8 * (wave + 8 * jj) * kFcBK);
+    ++i_u;
+    i_slot = i_slot + 1 == STAGES ? 0 : i_slot + 1;
+    i_k += kFcBK;
+    if (++i_kt == i_nk) {
+      i_kt = 0;
+      i_it += G;
+      if (i_it < items) issue_item(i_it);
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < STAGES - 1; ++t)
+    if (i_u < S) issue();
+
+  const int wm = wave % WGM, wn = wave / WGM;
+  const int g = lane >> 4, li = lane & 15;
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  uint2 pre[FM][FN];
+  // compute cursor
+  int c_it = lid, c_kt = 0, c_nk = 0, c_z = 0, mb = 0, nb = 0, c_slot = 0;
+  auto compute_item = [&](int it) {
+    const int tn = it % tiles_n, rest = it / tiles_n, tm = rest % tiles_m;
+    c_z = rest / tiles_m;
+    c_nk = min(ktot - c_z * kps, kps);
+    mb = tm * BM + C::TM * wm + li;
+    nb = tn * BN + C::TN * wn + 4 * g;
+  };
+  if (S) compute_item(lid);
+  bool e1 = false, e2 = false;  // an epilogue ran at step u - 1 / u - 2
+  for (int u = 0; u < S; ++u) {
+    if constexpr (STAGES == 3) fcp_wait_window<C::D, E>(u + 1 < S, e1 || e2);
+    else fcp_wait_window<C::D, E>(false, e1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // DMA(u) visible to all; every wave done reading step u - 1's stage
+    asm volatile("" ::: "memory");
+    if (i_u < S) issue();
+    const bool last = c_kt + 1 == c_nk;
+    const uint16_t* Ai = smem + c_slot * C::Stage;
+    const uint16_t* Bi = Ai + C::ImgA;
+    c_slot = c_slot + 1 == STAGES ? 0 : c_slot + 1;
+    auto compute = [&]() {
+#pragma unroll
+      for (int s = 0; s < kFcBK / 32; ++s) {
+        const int kc = 4 * s + g;
+        bf16x8_t af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          af[i] = *reinterpret_cast<const bf16x8_t*>(Ai + 8 * fc_swz(C::TM * wm + 16 * i + li, kc));
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          bfr[j] = *reinterpret_cast<const bf16x8_t*>(Bi + 8 * fc_swz(C::TN * wn + 16 * j + li, kc));
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+    };
+    e2 = e1;
+    e1 = last;
+    if (!last) {
+      compute();
+      ++c_kt;
+      continue;
+    }
+    // the tile's last k-tile: (mask prefetch,) MFMAs, epilogue -- on ONE path, so the compiler's
+    // wait for the prefetched mask sits at its use, not at every later load
+    if constexpr (Epi::kPrefetch) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const uint16_t* mrow = epi.mask + (size_t)min(mb + 16 * i, M - 1) * N;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) pre[i][j] = *reinterpret_cast<const uint2*>(mrow + min(nb + 16 * j, N - 4));
+      }
+    }
+    compute();
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = mb + 16 * i;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = nb + 16 * j;
+        const bool ok = m < M && n < N;
+        const f32x4_t v = acc[i][j];
+        if constexpr (Epi::kPrefetch) {
+          const uint2 o = make_uint2(fcp_pk_bf16(v[0], v[1]) & fcp_pos_mask(pre[i][j].x),
+                                     fcp_pk_bf16(v[2], v[3]) & fcp_pos_mask(pre[i][j].y));
+          uint2* dst = ok ? reinterpret_cast<uint2*>(epi.out + (size_t)m * N + n)
+                          : reinterpret_cast<uint2*>(fcp_dummy + 4 * lane);
+          *dst = o;
+        } else {
+          f32x4_t* dst = ok ? reinterpret_cast<f32x4_t*>(epi.part + ((size_t)c_z * M + m) * N + n)
+                            : reinterpret_cast<f32x4_t*>(fcp_dummy + 4 * lane);
+          *dst = v;
+        }
+        acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    c_kt = 0;
+    c_it += G;
+    if (c_it < items) compute_item(c_it);
+  }
+}
+
+// X^T . Y (the fc weight gradient) on the same persistent ring: items = (i-tile fastest, j-tile,
+// split z) over [64 r] x [128 col] sub-images (the fc_tn layout: ds_read_b64_tr_b16 fragments);
+// with BIAS the padded columns past J read ``ones`` and column J's sums land in bias_part.
+template <int BI, int BJ, int WGI, int STAGES, bool BIAS>
+__global__ void __launch_bounds__(kFcThreads, 1)
+fcp_tn_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, float* __restrict__ part, int R, int I,
+              int J, int tiles_i, int tiles_j, int kps, int items, const uint16_t* __restrict__ ones,
+              float* __restrict__ bias_part) {
+  constexpr int WGJ = 8 / WGI, TI = BI / WGI, TJ = BJ / WGJ, FI = TI / 16, FJ = TJ / 16;
+  constexpr int HX = BI / 128, HY = BJ / 128;  // sub-images per operand, 2 DMA instructions each per wave
+  constexpr int ImgX = BI * 64, ImgY = BJ * 64, Stage = ImgX + ImgY;
+  constexpr int D = 2 * (HX + HY), E = FI * FJ * (BIAS ? 2 : 1);
+  static_assert(BI % 128 == 0 && BJ % 128 == 0 && TI % 16 == 0 && TJ % 16 == 0 && (TI <= 128) && (TJ <= 128), "tile");
+  static_assert(STAGES * Stage * 2 <= 160 * 1024, "LDS");
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = gridDim.x, lid = fcp_lid();
+  const int rtot = R / 64, tij = tiles_i * tiles_j;
+  int S = 0;
+  for (int it = lid; it < items; it += G) S += min(rtot - (it / tij) * kps, kps);
+
+  // lane sources: image rows r0 + (lane >> 4), r0 = 8 wave + 4 jj; 16-byte chunk (lane & 15)
+  // XOR-swizzled (fc_tn_swz); a step moves 64 rows down (ones-column lanes stay put)
+  const uint16_t* px[HX][2];
+  const uint16_t* py[HY][2];
+  size_t ystep[HY][2];
+  int i_it = lid, i_kt = 0, i_nk = 0, i_slot = 0, i_u = 0;
+  const size_t xstep = (size_t)64 * I;
+  auto issue_item = [&](int it) {
+    const int ti = it % tiles_i, rest = it / tiles_i, tj = rest % tiles_j, z = rest / tiles_j;
+    i_nk = min(rtot - z * kps, kps);
+    const size_t r0g = (size_t)z * kps * 64;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int r = 8 * wave + 4 * jj + (lane >> 4);
+      const int c = (lane & 15) ^ (2 * ((r & 3) | (((r >> 3) & 1) << 2)));
+#pragma unroll
+      for (int h = 0; h < HX; ++h) px[h][jj] = X + (r0g + r) * I + min(ti * BI + 128 * h + 8 * c, I - 8);
+#pragma unroll
+      for (int h = 0; h < HY; ++h) {
+        const int col = tj * BJ + 128 * h + 8 * c;
+        const bool one = BIAS && col >= J;
+        py[h][jj] = one ? ones : Y + (r0g + r) * J + min(col, J - 8);
+        ystep[h][jj] = one ? 0 : (size_t)64 * J;
+      }
+    }
+  };
+  if (S) issue_item(lid);
+  auto issue = [&]() {
+    uint16_t* st = smem + i_slot * Stage;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int r0 = 8 * wave + 4 * jj;
+#pragma unroll
+      for (int h = 0; h < HX; ++h) {
+        fcp_glds(px[h][jj], st + h * kFcImg + r0 * 128);
+        px[h][jj] += xstep;
+      }
+#pragma unroll
+      for (int h = 0; h < HY; ++h) {
+        fcp_glds(py[h][jj], st + ImgX + h * kFcImg + r0 * 128);
+        py[h][jj] += ystep[h][jj];
+      }
+    }
+    ++i_u;
+    i_slot = i_slot + 1 == STAGES ? 0 : i_slot + 1;
+    if (++i_kt == i_nk) {
+      i_kt = 0;
+      i_it += G;
+      if (i_it < items) issue_item(i_it);
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < STAGES - 1; ++t)
+    if (i_u < S) issue();
+
+  const int wi = wave % WGI, wj = wave / WGI;
+  const int g = lane >> 4, li = lane & 15;
+  f32x4_t acc[FI][FJ];
+#pragma unroll
+  for (int a = 0; a < FI; ++a)
+#pragma unroll
+    for (int c = 0; c < FJ; ++c) acc[a][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  int c_it = lid, c_kt = 0, c_nk = 0, c_slot = 0, ib = 0, jb = 0, c_z = 0;
+  auto compute_item = [&](int it) {
+    const int ti = it % tiles_i, rest = it / tiles_i, tj = rest % tiles_j;
+    c_z = rest / tiles_j;
+    c_nk = min(rtot - c_z * kps, kps);
+    ib = ti * BI + TI * wi + li;
+    jb = tj * BJ + TJ * wj + 4 * g;
+  };
+  if (S) compute_item(lid);
+  bool e1 = false, e2 = false;
+  // the wave's columns inside its operand images: sub-image (TI * wi) / 128, offset (TI * wi) % 128
+  const int xo = (TI * wi / 128) * kFcImg, xc = TI * wi % 128;
+  const int yo = ImgX + (TJ * wj / 128) * kFcImg, yc = TJ * wj % 128;
+  for (int u = 0; u < S; ++u) {
+    if constexpr (STAGES == 3) fcp_wait_window<D, E>(u + 1 < S, e1 || e2);
+    else fcp_wait_window<D, E>(false, e1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (i_u < S) issue();
+    const bool last = c_kt + 1 == c_nk;
+    const uint16_t* st = smem + c_slot * Stage;
+    c_slot = c_slot + 1 == STAGES ? 0 : c_slot + 1;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t xf[FI], yf[FJ];
+#pragma unroll
+      for (int a = 0; a < FI; ++a) xf[a] = fcp_tn_frag(st + xo, 32 * s + 8 * g, xc + 16 * a, lane);
+#pragma unroll
+      for (int c = 0; c < FJ; ++c) yf[c] = fcp_tn_frag(st + yo, 32 * s + 8 * g, yc + 16 * c, lane);
+      fcp_lgkm_wait<FI, FJ>(xf, yf);
+#pragma unroll
+      for (int a = 0; a < FI; ++a)
+#pragma unroll
+        for (int c = 0; c < FJ; ++c) acc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yf[c], xf[a], acc[a][c], 0, 0, 0);
+    }
+    e2 = e1;
+    e1 = last;
+    if (!last) {
+      ++c_kt;
+      continue;
+    }
+#pragma unroll
+    for (int a = 0; a < FI; ++a) {
+      const int i = ib + 16 * a;
+#pragma unroll
+      for (int c = 0; c < FJ; ++c) {
+        const int j = jb + 16 * c;
+        f32x4_t* dst = (i < I && j < J) ? reinterpret_cast<f32x4_t*>(part + ((size_t)c_z * I + i) * J + j)
+                                        : reinterpret_cast<f32x4_t*>(fcp_dummy + 4 * lane);
+        *dst = acc[a][c];
+        if constexpr (BIAS) {  // the ones column
+          float* bd = (i < I && j == J) ? bias_part + (size_t)c_z * I + i : fcp_dummy + 4 * lane;
+          *bd = acc[a][c][0];
+        }
+        acc[a][c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    c_kt = 0;
+    c_it += G;
+    if (c_it < items) compute_item(c_it);
+  }
+}
+
+static int fcp_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+  }
+  return cus;
+}
+
+// split count for a persistent launch: the largest s <= max_splits whose items (tiles x s) fit
+// one round of CUs, each split keeping >= 2 k-tiles; returns (kps, used splits)
+static void fcp_splits(int tiles, int ktiles, int max_splits, int cus, int* kps, int* used) {
+  int s = 1;
+  for (int c = 2; c <= max_splits; ++c)
+    if (tiles * c <= cus && ktiles / c >= 2) s = c;
+  int k = (ktiles + s - 1) / s;
+  if (ktiles - (s - 1) * k < 2 && s > 1) {  // a remainder split of one k-tile: rebalance
+    s -= 1;
+    k = (ktiles + s - 1) / s;
+  }
+  *kps = k;
+  *used = (ktiles + k - 1) / k;
+}
+
+// 0 = the 128 x 128 kernels above, 1 = persistent big tiles.  RRL_FC_BIG (read per call) forces
+// one; unset, each call site takes the kernel that measured faster at its size
+// (tools/fc_kbench.py, profiles/r5_fc_persistent_kbench.jsonl): the persistent tiles for the
+// forward at >= 4,096 rows and the weight gradient at >= 20,480 rows, never for the data gradient.
+static int fc_big(bool auto_big = false) {
+  const char* e = getenv("RRL_FC_BIG");
+  if (!e || !e[0]) return auto_big ? 1 : 0;
+  return e[0] != '0';
+}
+
+template <int BM, int BN, int WGM, int STAGES, class Epi>
+static int launch_fcp_nt(const uint16_t* A, const uint16_t* B, Epi epi, int M, int N, int K, int kps, int used,
+                         hipStream_t st) {
+  using C = FcpCfg<BM, BN, WGM, STAGES>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fcp_nt_kernel<BM, BN, WGM, STAGES, Epi>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LdsBytes);
+    attr = true;
+  }
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  const int items = tiles_m * tiles_n * used;
+  const int grid = min(items, fcp_cus());
+  hipLaunchKernelGGL((fcp_nt_kernel<BM, BN, WGM, STAGES, Epi>), dim3(grid), dim3(kFcThreads), C::LdsBytes, st, A, B,
+                     epi, M, N, K, tiles_m, tiles_n, kps, items);
+  return (int)hipGetLastError();
+}
+
+template <int BI, int BJ, int WGI, int STAGES, bool BIAS>
+static int launch_fcp_tn(const uint16_t* X, const uint16_t* Y, float* part, int R, int I, int J, int kps, int used,
+                         const uint16_t* ones, float* bias_part, hipStream_t st) {
+  constexpr int lds = STAGES * (BI + BJ) * 64 * 2;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fcp_tn_kernel<BI, BJ, WGI, STAGES, BIAS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  const int ti = (I + BI - 1) / BI, tj = (J + BJ - 1) / BJ, items = ti * tj * used;
+  const int grid = min(items, fcp_cus());
+  hipLaunchKernelGGL((fcp_tn_kernel<BI, BJ, WGI, STAGES, BIAS>), dim3(grid), dim3(kFcThreads), lds, st, X, Y, part, R,
+                     I, J, ti, tj, kps, items, ones, bias_part);
+  return (int)hipGetLastError();
+}
+
 }  // namespace rrl
 
 using namespace rrl;
@@ -464,6 +964,14 @@ int rrl_fc_nt_part(const uint16_t* a, const uint16_t* b, float* part, int M, int
   const int used = (kt + kps - 1) / kps;
   const FcPartEpi epi{part, M, N};
   hipStream_t st = (hipStream_t)stream_;
+  const int big = fc_big(M >= 4096);
+  if (big && kt >= 2) {  // 256 x 128 persistent tiles
+    const int tiles = ((M + 255) / 256) * ((N + 127) / 128);
+    int kps2, used2;
+    fcp_splits(tiles, kt, splits, fcp_cus(), &kps2, &used2);
+    const int rc = launch_fcp_nt<256, 128, 4, 3>(a, b, FcpPart{part}, M, N, K, kps2, used2, st);
+    return rc ? -rc - 1000 : used2;
+  }
   const int v = fc_stages(0, 4);
   const int rc = v == 4 ? launch_fc_nt<FcPartEpi, 4>(a, b, epi, M, N, K, used, st)
                         : (v == 3 ? launch_fc_nt<FcPartEpi, 3>(a, b, epi, M, N, K, used, st)
@@ -476,6 +984,8 @@ int rrl_fc_nt_mask(const uint16_t* a, const uint16_t* b, const uint16_t* mask, u
                    void* stream_) {
   if (K % kFcBK || N % 4 || M < 1 || N < 1) return -1;
   hipStream_t st = (hipStream_t)stream_;
+  if (fc_big(false) && K / kFcBK >= 2)  // 256 x 128 persistent tiles, whole K per item
+    return launch_fcp_nt<256, 128, 4, 3>(a, b, FcpMask{out, mask}, M, N, K, K / kFcBK, 1, st);
   // The staged epilogue pays when the output and mask streams leave the 256 MB Infinity
   // Cache (40,960 x 3,136: 276 -> 220 us in tools/fc_kbench.py); at 10,240 rows inside the
   // Pong update (both streams cache-resident, the side-stream weight gradients competing for
@@ -501,8 +1011,16 @@ int rrl_fc_tn_part(const uint16_t* x, const uint16_t* y, float* part, int R, int
                    const uint16_t* ones, float* bias_part, void* stream_) {
   if (R % 64 || I % 8 || J % 8 || R < 64 || splits < 1) return -1;
   if ((ones == nullptr) != (bias_part == nullptr) || (bias_part && J % 128 == 0)) return -1;
-  const int rt = R / 64, kps = (rt + splits - 1) / splits, used = (rt + kps - 1) / kps;
   hipStream_t st = (hipStream_t)stream_;
+  if (fc_big(R >= 20480) && R / 64 >= 2 && I % 4 == 0) {  // 256 x 128 persistent tiles
+    const int tiles = ((I + 255) / 256) * ((J + 127) / 128);
+    int kps2, used2;
+    fcp_splits(tiles, R / 64, splits, fcp_cus(), &kps2, &used2);
+    const int rc = bias_part ? launch_fcp_tn<256, 128, 4, 3, true>(x, y, part, R, I, J, kps2, used2, ones, bias_part, st)
+                             : launch_fcp_tn<256, 128, 4, 3, false>(x, y, part, R, I, J, kps2, used2, ones, bias_part, st);
+    return rc ? -rc - 1000 : used2;
+  }
+  const int rt = R / 64, kps = (rt + splits - 1) / splits, used = (rt + kps - 1) / kps;
   const int rc = fc_stages(2, 2) == 2 ? launch_fc_tn<2>(x, y, part, R, I, J, used, ones, bias_part, st)
                                       : launch_fc_tn<3>(x, y, part, R, I, J, used, ones, bias_part, st);
   return rc ? -rc - 1000 : used;

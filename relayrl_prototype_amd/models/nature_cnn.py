@@ -20,6 +20,7 @@ are tested against and the CPU path of the trainer.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -217,7 +218,8 @@ class DeviceNatureCNN:
         # split-K partials of the fc forward, sized once for every batch up to max_batch: a
         # captured update graph holds this storage, so it must never be reallocated
         self.FC_SPLIT_CAP = int(os.environ.get("RRL_FC_SPLITS", str(self.FC_SPLIT_CAP)))
-        fc_rows = max(self.fc_splits(n) * n for n in range(1, self.max_batch + 1)) if self.fc_nt else 0
+        fc_rows = (max(self.fc_splits(n, big) * n for n in range(1, self.max_batch + 1) for big in (False, True))
+                   if self.fc_nt else 0)
         self._fc_part = torch.empty(fc_rows * HIDDEN, device=dev) if self.fc_nt else None
         self.refresh_shadow()
         self.m = torch.zeros_like(self.params)
@@ -330,9 +332,14 @@ class DeviceNatureCNN:
     # cap of the fc forward's split-K count (RRL_FC_SPLITS, for A/B runs)
     FC_SPLIT_CAP = 8
 
-    def fc_splits(self, n: int) -> int:
-        """split-K count of the fc forward: >= 256 workgroups of 128 x 128 tiles, at most 8."""
-        tiles = -(-n // 128) * (HIDDEN // 128)
+    def fc_splits(self, n: int, big=None) -> int:
+        """split-K count of the fc forward: enough items for 256 CUs, at most 8 -- of the
+        persistent 256 x 128 tiles (fc.hip ``fcp_nt_kernel``: >= 4,096 rows, or RRL_FC_BIG=1)
+        or of the 128 x 128 one-tile-per-workgroup kernel."""
+        if big is None:  # the same choice as fc.hip's rrl_fc_nt_part
+            e = os.environ.get("RRL_FC_BIG", "")
+            big = (e != "0") if e else n >= 4096
+        tiles = -(-n // (256 if big else 128)) * (HIDDEN // 128)
         return max(1, min(self.FC_SPLIT_CAP, -(-256 // tiles)))
 
     @staticmethod

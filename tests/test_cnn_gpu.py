@@ -589,32 +589,40 @@ def test_conv1_wgrad8_matches_autograd(cuda, N, grid):
 
 
 # ----------------------------------------------------------------------------- fc.hip
+@pytest.mark.parametrize("big", ["1", "0"])  # RRL_FC_BIG: persistent 256 x 128 tiles / 128 x 128 per workgroup
 @pytest.mark.parametrize("M,N,K,splits", [(37, 512, 3136, 1), (300, 512, 3136, 4), (2048, 512, 3136, 4),
-                                          (130, 3136, 512, 1), (64, 132, 128, 2)])
-def test_fc_nt_part_matches_fp32(cuda, M, N, K, splits):
+                                          (2048, 512, 3136, 8), (8192, 512, 3136, 2), (130, 3136, 512, 1),
+                                          (5000, 3136, 512, 1), (64, 132, 128, 2)])
+def test_fc_nt_part_matches_fp32(cuda, M, N, K, splits, big, monkeypatch):
     """DMA-staged NT GEMM (swizzled LDS images, 3-stage ring): the split-K partials sum to
-    the fp32 product of the bf16 operands, for tile-ragged M and N."""
+    the fp32 product of the bf16 operands, for tile-ragged M and N; the persistent kernel walks
+    several tiles per workgroup at (5000, 3136, 512) (500 tiles on 256 CUs)."""
     from relayrl_prototype_amd.ops import hip
 
+    monkeypatch.setenv("RRL_FC_BIG", big)
     h = hip()
     g = torch.Generator().manual_seed(M + N + K)
-    a = _bf(torch.randn(M, K, generator=g))
-    b = _bf(torch.randn(N, K, generator=g) * 0.05)
+    a = _bf(torch.randn(M, K, generator=g)).to(cuda)
+    b = _bf(torch.randn(N, K, generator=g) * 0.05).to(cuda)
     part = torch.full((splits * M * N,), float("nan"), device=cuda)
-    used = h.fc_nt_part(a.to(cuda).bfloat16().reshape(-1), b.to(cuda).bfloat16().reshape(-1), part, M, N, K, splits)
+    used = h.fc_nt_part(a.bfloat16().reshape(-1), b.bfloat16().reshape(-1), part, M, N, K, splits)
     assert 1 <= used <= splits
-    got = part[:used * M * N].view(used, M, N).sum(0).cpu()
+    got = part[:used * M * N].view(used, M, N).sum(0)
     ref = a.double() @ b.double().t()
     assert torch.isfinite(got).all()
     assert ((got.double() - ref).abs().max() / ref.abs().max()).item() < 1e-5
 
 
+@pytest.mark.parametrize("big", ["1", "0"])
 @pytest.mark.parametrize("epi", ["0", "1"])  # RRL_FC_DIRECT_EPI: 0 = LDS-staged 16-byte epilogue, 1 = direct
-@pytest.mark.parametrize("M", [37, 1000])
-def test_fc_nt_mask_matches_fp32(cuda, M, epi, monkeypatch):
+@pytest.mark.parametrize("M", [37, 1000, 10240])
+def test_fc_nt_mask_matches_fp32(cuda, M, epi, big, monkeypatch):
     from relayrl_prototype_amd.ops import hip
 
+    if big == "1" and epi == "1":
+        pytest.skip("the persistent kernel has one epilogue")
     monkeypatch.setenv("RRL_FC_DIRECT_EPI", epi)
+    monkeypatch.setenv("RRL_FC_BIG", big)
     h = hip()
     g = torch.Generator().manual_seed(M)
     dh = _bf(torch.randn(M, HIDDEN, generator=g))
@@ -659,13 +667,16 @@ def test_fc_head_fused_matches_separate(cuda, B, monkeypatch):
     assert (a1 != a2).float().mean().item() < 0.01
 
 
+@pytest.mark.parametrize("big", ["1", "0"])
 @pytest.mark.parametrize("R,I,J,splits", [(64, 512, 3136, 1), (640, 512, 3136, 5), (10240, 512, 3136, 5),
-                                          (192, 136, 72, 2)])
-def test_fc_tn_part_matches_fp32(cuda, R, I, J, splits):
+                                          (192, 136, 72, 2), (256, 4096, 3136, 1)])
+def test_fc_tn_part_matches_fp32(cuda, R, I, J, splits, big, monkeypatch):
     """Weight-gradient GEMM X^T . Y from row-major operands (transposed ds_read_b64_tr_b16
-    fragments of XOR-swizzled [64][128] images), split over rows into fp32 partials."""
+    fragments of XOR-swizzled [64][128] images), split over rows into fp32 partials; at
+    (256, 4096, 3136) the persistent kernel walks 400 tiles on 256 CUs."""
     from relayrl_prototype_amd.ops import hip
 
+    monkeypatch.setenv("RRL_FC_BIG", big)
     h = hip()
     g = torch.Generator().manual_seed(R + I + J)
     x = _bf(torch.randn(R, I, generator=g))

@@ -43,6 +43,7 @@ def main():
     work = torch.empty(16 * Mf * HIDDEN, device=dev)
     wpart = torch.empty(8 * HIDDEN * FC_IN, device=dev)
     Mx = 4 * Mb  # the 8192-env update (40,960 rows): outputs past the Infinity Cache
+    partx = torch.empty(2 * 4 * Mf * HIDDEN, device=dev)
     a3x = torch.randn(Mx * FC_IN, device=dev, generator=g).relu().bfloat16()
     dhx = torch.randn(Mx * HIDDEN, device=dev, generator=g).bfloat16()
     da3x = torch.empty(Mx * FC_IN, dtype=torch.bfloat16, device=dev)
@@ -60,6 +61,7 @@ def main():
     cases = {
         "fwd_part_s4": lambda: h.fc_nt_part(a3, w, part, Mf, HIDDEN, FC_IN, 4),
         "fwd_part_s8": lambda: h.fc_nt_part(a3, w, part, Mf, HIDDEN, FC_IN, 8),
+        "fwd8k_part_s2": lambda: h.fc_nt_part(a3x, w, partx, 4 * Mf, HIDDEN, FC_IN, 2),
         "fwd_old_gemm_bias_act": lambda: h.conv_fwd(a3[:Mf * FC_IN], w, b, hid, Mf, 1, 1, FC_IN, 1, 1, 1, HIDDEN,
                                                     True, work),
         "dgrad_mask": lambda: h.fc_nt_mask(dh, wt, a3, da3, Mb, FC_IN, HIDDEN),
@@ -70,14 +72,20 @@ def main():
         "wgrad_tn_s2": lambda: h.fc_tn_part(dh, a3, wpart, Mb, HIDDEN, FC_IN, 2),
         "wgrad_tn_s5": lambda: h.fc_tn_part(dh, a3, wpart, Mb, HIDDEN, FC_IN, 5),
         "wgrad_tn_s8": lambda: h.fc_tn_part(dh, a3, wpart, Mb, HIDDEN, FC_IN, 8),
+        "wgrad40k_tn_s5": lambda: h.fc_tn_part(dhx, a3x, wpart, Mx, HIDDEN, FC_IN, 5),
         "wgrad_old_s2": lambda: h.conv_wgrad(dh, a3, wpart, 2, Mb, 1, 1, FC_IN, 1, 1, 1, HIDDEN),
     }
-    variants = os.environ.get("FC_VARIANTS", "422,432").split(",")
+    # "b" in a variant = the persistent 256 x 128 kernels (RRL_FC_BIG=1), else the 128 x 128 ones
+    variants = os.environ.get("FC_VARIANTS", "422,b").split(",")
+    only = [c for c in os.environ.get("FC_CASES", "").split(",") if c]
+    if only:
+        cases = {k: v for k, v in cases.items() if k in only}
     res = {}
-    for _ in range(5):
+    for _ in range(int(os.environ.get("FC_ROUNDS", "5"))):
         for v in variants:
-            os.environ["RRL_FC_STAGES"] = v.replace("m", "")
+            os.environ["RRL_FC_STAGES"] = v.replace("m", "").replace("b", "")
             os.environ["RRL_FC_MFAST"] = "1" if "m" in v else "0"
+            os.environ["RRL_FC_BIG"] = "1" if "b" in v else "0"
             for k, fn in cases.items():
                 if "old" in k and v != variants[0]:
                     continue
