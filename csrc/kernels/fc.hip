@@ -315,19 +315,36 @@ __device__ __forceinline__ void fc_tn_stage(const uint16_t* __restrict__ X, int 
   }
 }
 
-// MFMA operand fragment (8 consecutive r for image column col0 + (lane & 15)) from a
-// swizzled [64][128] image: two ds_read_b64_tr_b16, rows k0 .. k0 + 3 and k0 + 4 .. k0 + 7.
-__device__ __forceinline__ bf16x8_t fc_tn_frag(const uint16_t* img, int k0, int col0, int lane) {
+// MFMA operand fragment (8 consecutive r for image column col0 + (lane & 15)) from a swizzled
+// [64][128] image: two ds_read_b64_tr_b16, rows k0 .. k0 + 3 and k0 + 4 .. k0 + 7.  Inline asm: the
+// ds_read_tr16_b64 builtin makes hipcc wait vmcnt(0) before
+// every read while an LDS-DMA is in flight (it cannot tell which LDS the read touches), which
+// drains the whole ring each k-tile.  The asm reads are invisible to the compiler's counters, so
+// fcp_lgkm_wait retires them (tied to the fragments) before the MFMAs use them.
+__device__ __forceinline__ s16x4_t fcp_tr_b64(const uint16_t* p) {
+  s16x4_t v;
+  const uint32_t a = (uint32_t)(size_t)(const __attribute__((address_space(3))) uint16_t*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+__device__ __forceinline__ bf16x8_t fcp_tn_frag(const uint16_t* img, int k0, int col0, int lane) {
   const int q = (lane >> 2) & 3, p = lane & 3;
   const int c = (col0 + 4 * p) >> 3, half = (p & 1) * 4;
-  typedef __attribute__((address_space(3))) s16x4_t lds_v4;
-  const uint16_t* a0 = img + 8 * fc_tn_swz(k0 + q, c) + half;
-  const uint16_t* a1 = img + 8 * fc_tn_swz(k0 + 4 + q, c) + half;
-  s16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a0));
-  s16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a1));
+  const s16x4_t lo = fcp_tr_b64(img + 8 * fc_tn_swz(k0 + q, c) + half);
+  const s16x4_t hi = fcp_tr_b64(img + 8 * fc_tn_swz(k0 + 4 + q, c) + half);
   typedef short s16x8_t __attribute__((ext_vector_type(8)));
-  s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
   return __builtin_bit_cast(bf16x8_t, v);
+}
+template <int FI, int FJ>
+__device__ __forceinline__ void fcp_lgkm_wait(bf16x8_t (&x)[FI], bf16x8_t (&y)[FJ]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // empty volatile asms stay after the wait and make every fragment an output of it, so no MFMA
+  // that reads one can be scheduled above the wait
+#pragma unroll
+  for (int a = 0; a < FI; ++a) asm volatile("" : "+v"(x[a]));
+#pragma unroll
+  for (int c = 0; c < FJ; ++c) asm volatile("" : "+v"(y[c]));
 }
 
 // 128 (i) x 128 (j) output tile per workgroup, 8 waves (2 x 4: 64 i x 32 j each), the R
@@ -381,9 +398,10 @@ fc_tn_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, flo
     for (int s = 0; s < 2; ++s) {
       bf16x8_t xf[4], yf[2];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) xf[a] = fc_tn_frag(Xi, 32 * s + 8 * g, 64 * wi + 16 * a, lane);
+      for (int a = 0; a < 4; ++a) xf[a] = fcp_tn_frag(Xi, 32 * s + 8 * g, 64 * wi + 16 * a, lane);
 #pragma unroll
-      for (int c = 0; c < 2; ++c) yf[c] = fc_tn_frag(Yi, 32 * s + 8 * g, 32 * wj + 16 * c, lane);
+      for (int c = 0; c < 2; ++c) yf[c] = fcp_tn_frag(Yi, 32 * s + 8 * g, 32 * wj + 16 * c, lane);
+      fcp_lgkm_wait<4, 2>(xf, yf);
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -502,32 +520,6 @@ __device__ __forceinline__ void fcp_stage(const uint16_t* __restrict__ X, int ro
     __builtin_amdgcn_global_load_lds(X + (size_t)gr * K + k0 + 8 * kc,
                                      (__attribute__((address_space(3))) void*)(img + r0 * kFcBK), 16, 0, 0);
   }
-}
-
-// fc_tn_frag through inline asm: the ds_read_tr16_b64 builtin makes hipcc wait vmcnt(0) before
-// every read while an LDS-DMA is in flight (it cannot tell which LDS the read touches), which
-// drains the whole ring each k-tile.  The asm reads are invisible to the compiler's counters, so
-// fcp_lgkm_wait retires them (tied to the fragments) before the MFMAs use them.
-__device__ __forceinline__ s16x4_t fcp_tr_b64(const uint16_t* p) {
-  s16x4_t v;
-  const uint32_t a = (uint32_t)(size_t)(const __attribute__((address_space(3))) uint16_t*)p;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
-  return v;
-}
-__device__ __forceinline__ bf16x8_t fcp_tn_frag(const uint16_t* img, int k0, int col0, int lane) {
-  const int q = (lane >> 2) & 3, p = lane & 3;
-  const int c = (col0 + 4 * p) >> 3, half = (p & 1) * 4;
-  const s16x4_t lo = fcp_tr_b64(img + 8 * fc_tn_swz(k0 + q, c) + half);
-  const s16x4_t hi = fcp_tr_b64(img + 8 * fc_tn_swz(k0 + 4 + q, c) + half);
-  typedef short s16x8_t __attribute__((ext_vector_type(8)));
-  const s16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8_t, v);
-}
-template <int FI, int FJ>
-__device__ __forceinline__ void fcp_lgkm_wait(bf16x8_t (&x)[FI], bf16x8_t (&y)[FJ]) {
-  static_assert(FI == 4 && FJ == 4, "tie list written for 4 + 4 fragments");
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(y[0]), "+v"(y[1]),
-               "+v"(y[2]), "+v"(y[3]));
 }
 
 // 64 lanes x 16 B that epilogue lanes with nothing to store write (a device global: no allocation,
