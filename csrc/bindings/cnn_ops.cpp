@@ -67,6 +67,12 @@ int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, u
 int rrl_conv1_wgrad8(const uint8_t* x, const float* hist, const uint16_t* dy, float* part, float* bias_part, int N,
                      int grid, void* stream);
 int rrl_pong_render_hist(const float* hist, uint8_t* obs, int N, void* stream);
+int rrl_pong_head_step_render(const float* part, int splits, const float* fc_b, const float* head_params, int A,
+                              uint16_t* h_out, int32_t* act, float* logp, float* value, unsigned long long sample_seed,
+                              unsigned long long sample_step, const unsigned long long* sample_base, float* state,
+                              float* rew, float* done, float* fin_ret, float* fin_len, float* ep_acc, uint8_t* obs,
+                              int N, unsigned long long seed, unsigned long long step,
+                              const unsigned long long* step_base, int max_steps, void* stream);
 
 }
 
@@ -488,6 +494,42 @@ void pong_step(const Tensor& state, const Tensor& act, const Tensor& rew, const 
            "pong_step");
 }
 
+// Fused rollout step (pong.hip): the policy head from the fc split-K partials + env step +
+// render, one workgroup per env.  Same outputs as a2c_head(mode 0, part=...) then pong_step(obs=...).
+void pong_head_step(const Tensor& part, int64_t splits, const Tensor& fc_b, const Tensor& head_params, int64_t A,
+                    const Tensor& h_out, const Tensor& act, const Tensor& logp, const Tensor& value, int64_t sample_seed,
+                    int64_t sample_step, const OptT& sample_base, const Tensor& state, const Tensor& rew,
+                    const Tensor& done, const Tensor& fin_ret, const Tensor& fin_len, const OptT& ep_acc,
+                    const Tensor& obs, int64_t N, int64_t seed, int64_t step, const OptT& step_base,
+                    int64_t max_steps) {
+  constexpr int64_t F = 512;
+  TORCH_CHECK(A >= 1 && A <= 8 && splits >= 1 && N >= 1, "pong_head_step: 1 <= A <= 8, splits >= 1");
+  check(part, "part", at::kFloat, splits * N * F);
+  check(fc_b, "fc_b", at::kFloat, F);
+  check(head_params, "head_params", at::kFloat, A * F + A + F + 1);
+  check(h_out, "h_out", at::kBFloat16, N * F);
+  check(act, "act", at::kInt, N);
+  check(logp, "logp", at::kFloat, N);
+  check(value, "value", at::kFloat, N);
+  check(state, "state", at::kFloat, N * pong_state_size());
+  check(rew, "rew", at::kFloat, N);
+  check(done, "done", at::kFloat, N);
+  check(fin_ret, "fin_ret", at::kFloat, N);
+  check(fin_len, "fin_len", at::kFloat, N);
+  check(obs, "obs", at::kByte, N * 84 * 84 * 4);
+  float* acc = opt_ptr<float>(ep_acc, "ep_acc", at::kFloat, 4 * N);
+  const unsigned long long* sb = opt_ptr<const unsigned long long>(step_base, "step_base", at::kLong, 1);
+  const unsigned long long* ssb = opt_ptr<const unsigned long long>(sample_base, "sample_base", at::kLong, 1);
+  rc_check(rrl_pong_head_step_render(part.data_ptr<float>(), (int)splits, fc_b.data_ptr<float>(),
+                                     head_params.data_ptr<float>(), (int)A, bf(h_out), act.data_ptr<int32_t>(),
+                                     logp.data_ptr<float>(), value.data_ptr<float>(), (uint64_t)sample_seed,
+                                     (uint64_t)sample_step, ssb, state.data_ptr<float>(), rew.data_ptr<float>(),
+                                     done.data_ptr<float>(), fin_ret.data_ptr<float>(), fin_len.data_ptr<float>(), acc,
+                                     obs.data_ptr<uint8_t>(), (int)N, (uint64_t)seed, (uint64_t)step, sb,
+                                     (int)max_steps, stream()),
+           "pong_head_step");
+}
+
 // s2d observations drawn from frame histories [N][16] (the fused-render path's reference)
 void pong_render_hist(const Tensor& hist, const Tensor& obs, int64_t N) {
   check(hist, "hist", at::kFloat, N * 16);
@@ -561,6 +603,13 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("N"), pybind11::arg("seed"), pybind11::arg("step"), pybind11::arg("max_steps"),
         pybind11::arg("reset_all"), pybind11::arg("step_base") = pybind11::none(),
         pybind11::arg("obs") = pybind11::none(), pybind11::arg("hist") = pybind11::none());
+  m.def("pong_head_step", &pong_head_step, pybind11::arg("part"), pybind11::arg("splits"), pybind11::arg("fc_b"),
+        pybind11::arg("head_params"), pybind11::arg("A"), pybind11::arg("h_out"), pybind11::arg("act"),
+        pybind11::arg("logp"), pybind11::arg("value"), pybind11::arg("sample_seed"), pybind11::arg("sample_step"),
+        pybind11::arg("sample_base"), pybind11::arg("state"), pybind11::arg("rew"), pybind11::arg("done"),
+        pybind11::arg("fin_ret"), pybind11::arg("fin_len"), pybind11::arg("ep_acc"), pybind11::arg("obs"),
+        pybind11::arg("N"), pybind11::arg("seed"), pybind11::arg("step"), pybind11::arg("step_base"),
+        pybind11::arg("max_steps"));
   m.def("pong_render", &pong_render);
   m.def("pong_render_hist", &pong_render_hist);
 }

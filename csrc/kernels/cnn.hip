@@ -14,6 +14,7 @@
 //                                                   split over batch x spatial -> fp32 partials
 #include "gemm_bf16.h"
 #include "heads.h"
+#include "a2c_head.h"
 
 namespace rrl {
 
@@ -563,71 +564,13 @@ __global__ void to_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict
 }
 
 // ----------------------------------------------------------------------------- A2C head
-// One wave per row: lane owns features 8*lane .. 8*lane+7 of h (F = 512 -> 64 lanes x 8).
-// Head weights (A + 1 rows of F fp32: policy rows then the value row, and A + 1 biases)
-// are staged in LDS per block.
-constexpr int kHeadF = 512;
-
-struct HeadArgs {
-  const uint16_t* h;      // [B][F] post-ReLU fc output
-  const float* w;         // [A][F] policy rows; value row at w_v
-  const float* bias;      // [A]
-  const float* w_v;       // [F]
-  const float* b_v;       // [1]
-  int B, A;
-  // rollout outputs
-  int32_t* act;
-  float* logp;
-  float* value;
-  float* logits_out;      // optional [B][A]
-  uint32_t seed_lo, seed_hi, step_lo, step_hi;
-  const unsigned long long* step_base;  // optional device counter added to the step (graph replays)
-  int row_offset;
-  // training inputs / outputs
-  const int32_t* act_in;
-  const float* adv;
-  const float* ret;
-  float inv_B, vf_coef, ent_coef;
-  uint16_t* dh;           // [B][F] grad wrt fc pre-activation (masked), bf16
-  float* dhead;           // [B][A+1] fp32: dlogits, dv
-  float* stats;           // [gridDim.x][4]: pg loss, vf loss, entropy, count
-  // rollout mode straight from the fc GEMM's split-K partials (fc.hip): h = bf16(relu(
-  // fc_b + sum_z part[z][row][:])) is formed here and written to h_out for the backward
-  const float* part;      // [splits][B][F] or null (then h is read)
-  int splits;
-  const float* fc_b;      // [F]
-  uint16_t* h_out;        // [B][F]
-};
+// (HeadArgs, head_sum_part: a2c_head.h, shared with the fused Pong head + step kernel)
 
 // Head weights live in REGISTERS: lane l holds features 8 l .. 8 l + 7 of every policy row
 // and of the value row, loaded once per wave before its rows (L2 hits after the first
 // wave), so there is no per-block LDS staging pass and no barrier in front of the rows --
 // at 2,048 rollout rows a block has one row per wave and that staging was most of the
 // launch.  AMAX = compile-time cap on A (8 covers Pong's 6; 16 = kMaxAct otherwise).
-template <int S>
-__device__ __forceinline__ void head_sum_part(float (&v)[8], const float* pr, size_t zs, int splits) {
-  if constexpr (S > 0) {  // compile-time split count: every load issued before the adds
-    float4 p[S][2];
-#pragma unroll
-    for (int z = 0; z < S; ++z) {
-      p[z][0] = *reinterpret_cast<const float4*>(pr + z * zs);
-      p[z][1] = *reinterpret_cast<const float4*>(pr + z * zs + 4);
-    }
-#pragma unroll
-    for (int z = 0; z < S; ++z) {
-      v[0] += p[z][0].x; v[1] += p[z][0].y; v[2] += p[z][0].z; v[3] += p[z][0].w;
-      v[4] += p[z][1].x; v[5] += p[z][1].y; v[6] += p[z][1].z; v[7] += p[z][1].w;
-    }
-  } else {
-    for (int z = 0; z < splits; ++z) {
-      const float4 p0 = *reinterpret_cast<const float4*>(pr + z * zs);
-      const float4 p1 = *reinterpret_cast<const float4*>(pr + z * zs + 4);
-      v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
-      v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
-    }
-  }
-}
-
 template <bool TRAIN, int AMAX>
 __global__ void __launch_bounds__(256) a2c_head_kernel(HeadArgs a) {
   __shared__ float red[16];

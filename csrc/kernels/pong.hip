@@ -8,6 +8,7 @@
 // (channel f = frame f, oldest first), so observations never touch the host.
 #include "common.h"
 #include "pong_render.h"
+#include "a2c_head.h"
 
 namespace rrl {
 
@@ -48,7 +49,7 @@ RRL_DEV void reset_env(float* s, uint4 r) {
 // One env's step (frame-skip 4); state row written back.  Shared by pong_step_kernel (one
 // thread per env) and pong_step_render_kernel (one workgroup per env).
 // s: the env's state row, in registers (pong_step_env) or in LDS (pong_step_render_kernel).
-RRL_DEV void pong_step_state(int e, float* s, const int32_t* __restrict__ act, float* __restrict__ rew,
+RRL_DEV void pong_step_state(int e, float* s, int a, float* __restrict__ rew,
                              float* __restrict__ done, float* __restrict__ fin_ret, float* __restrict__ fin_len,
                              float* __restrict__ ep_acc, uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps,
                              int reset_all, const unsigned long long* __restrict__ step_base) {
@@ -61,7 +62,6 @@ RRL_DEV void pong_step_state(int e, float* s, const int32_t* __restrict__ act, f
   if (reset_all) {
     reset_env(s, r0);
   } else {
-    const int a = act[e];
     const float dir = (a == 2 || a == 4) ? -1.f : ((a == 3 || a == 5) ? 1.f : 0.f);  // RIGHT = up, LEFT = down
     float reward = 0.f;
     bool point = false;
@@ -127,7 +127,7 @@ RRL_DEV void pong_step_env(int e, float* __restrict__ state, const int32_t* __re
   float s[kPongState];
 #pragma unroll
   for (int i = 0; i < kPongState; ++i) s[i] = state[(size_t)e * kPongState + i];
-  pong_step_state(e, s, act, rew, done, fin_ret, fin_len, ep_acc, key, step_lo, step_hi, max_steps, reset_all,
+  pong_step_state(e, s, reset_all ? 0 : act[e], rew, done, fin_ret, fin_len, ep_acc, key, step_lo, step_hi, max_steps, reset_all,
                   step_base);
 #pragma unroll
   for (int i = 0; i < kPongState; ++i) state[(size_t)e * kPongState + i] = s[i];
@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(256, 8) pong_step_render_kernel(
   if (t < kPongState) ss[t] = state[(size_t)e * kPongState + t];
   __syncthreads();
   if (t == 0)
-    pong_step_state(e, ss, act, rew, done, fin_ret, fin_len, ep_acc, key, step_lo, step_hi, max_steps, reset_all,
+    pong_step_state(e, ss, reset_all ? 0 : act[e], rew, done, fin_ret, fin_len, ep_acc, key, step_lo, step_hi, max_steps, reset_all,
                     step_base);
   __syncthreads();
   if (t < kPongState) state[(size_t)e * kPongState + t] = ss[t];
@@ -234,6 +234,39 @@ __global__ void __launch_bounds__(256, 8) pong_step_render_kernel(
     *reinterpret_cast<uint4*>(o + (size_t)q * 16) = pong_render_chunk_rows(hist, rows, q);
 }
 
+
+// The rollout step's policy head fused in front of the env step: one workgroup per env, wave 0
+// forms the env's hidden row from the fc split-K partials and samples its action
+// (a2c_rollout_row_streamed: bitwise the a2c_head_kernel result), thread 0 steps the physics
+// with it, and the workgroup renders the new frame stack -- one launch instead of head + step
+// (the head launch was ~10 us per rollout step at 2,048 envs, mostly its fixed cost).
+template <int AMAX>
+__global__ void __launch_bounds__(256, 8) pong_head_step_render_kernel(
+    HeadArgs ha, float* __restrict__ state, float* __restrict__ rew, float* __restrict__ done,
+    float* __restrict__ fin_ret, float* __restrict__ fin_len, float* __restrict__ ep_acc, uint8_t* __restrict__ obs,
+    uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps, const unsigned long long* __restrict__ step_base) {
+  constexpr int kChunks = kPongHW * kPongHW * 4 / 16;
+  __shared__ float ss[kPongState];
+  __shared__ uint32_t rows[kPongHW];
+  __shared__ int pick_s;
+  const int e = blockIdx.x, t = threadIdx.x;
+  if (t < kPongState) ss[t] = state[(size_t)e * kPongState + t];
+  if (t < 64) {
+    const int pick = a2c_rollout_row_streamed<AMAX>(ha, e, t);
+    if (t == 0) pick_s = pick;
+  }
+  __syncthreads();
+  if (t == 0)
+    pong_step_state(e, ss, pick_s, rew, done, fin_ret, fin_len, ep_acc, key, step_lo, step_hi, max_steps, 0, step_base);
+  __syncthreads();
+  if (t < kPongState) state[(size_t)e * kPongState + t] = ss[t];
+  const float* hist = ss + P_HIST;
+  if (t < kPongHW) rows[t] = pong_row_flags(hist, t);
+  __syncthreads();
+  uint8_t* o = obs + (size_t)e * kChunks * 16;
+  for (int q = threadIdx.x; q < kChunks; q += 256)
+    *reinterpret_cast<uint4*>(o + (size_t)q * 16) = pong_render_chunk_rows(hist, rows, q);
+}
 }  // namespace rrl
 
 using namespace rrl;
@@ -283,6 +316,41 @@ int rrl_pong_render(const float* state, uint8_t* obs, int N, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   const size_t t = (size_t)N * (kPongHW * kPongHW * 4 / 16);
   hipLaunchKernelGGL(pong_render_kernel, dim3((unsigned)((t + 255) / 256)), dim3(256), 0, st, state, obs, N);
+  return (int)hipGetLastError();
+}
+
+
+// Fused rollout step: head (from the fc split-K partials part[splits][N][512]) + env step +
+// render.  head_params = [A x 512 policy rows | A biases | 512 value row | value bias].
+int rrl_pong_head_step_render(const float* part, int splits, const float* fc_b, const float* head_params, int A,
+                              uint16_t* h_out, int32_t* act, float* logp, float* value, unsigned long long sample_seed,
+                              unsigned long long sample_step, const unsigned long long* sample_base, float* state,
+                              float* rew, float* done, float* fin_ret, float* fin_len, float* ep_acc, uint8_t* obs,
+                              int N, unsigned long long seed, unsigned long long step,
+                              const unsigned long long* step_base, int max_steps, void* stream_) {
+  if (N < 1 || A < 1 || A > 8 || splits < 1 || !part || !fc_b || !h_out) return -1;
+  HeadArgs a = {};
+  a.part = part;
+  a.splits = splits;
+  a.fc_b = fc_b;
+  a.h_out = h_out;
+  a.w = head_params;
+  a.bias = head_params + A * kHeadF;
+  a.w_v = a.bias + A;
+  a.b_v = a.w_v + kHeadF;
+  a.B = N;
+  a.A = A;
+  a.act = act;
+  a.logp = logp;
+  a.value = value;
+  a.seed_lo = (uint32_t)sample_seed;
+  a.seed_hi = (uint32_t)(sample_seed >> 32);
+  a.step_lo = (uint32_t)sample_step;
+  a.step_hi = (uint32_t)(sample_step >> 32);
+  a.step_base = sample_base;
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  hipLaunchKernelGGL(pong_head_step_render_kernel<8>, dim3(N), dim3(256), 0, (hipStream_t)stream_, a, state, rew, done,
+                     fin_ret, fin_len, ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, step_base);
   return (int)hipGetLastError();
 }
 

@@ -235,6 +235,23 @@ class DevicePong:
         """(episodes, sum return, sum length, sum return^2) over all envs since the last reset."""
         return self.ep_acc.double().sum(0)
 
+    def step_head(self, part, splits: int, fc_b, head_params, A: int, h_out, act_out, logp_out, value_out,
+                  sample_seed: int, sample_step: int, sample_base, obs_out, rew_out=None, done_out=None,
+                  offset: int = None):
+        """The policy head fused in front of one env step (pong.hip ``pong_head_step_render_kernel``):
+        from the fc split-K partials ``part`` of this step's observations, write the hidden units
+        (``h_out``), sample the actions (``act_out`` / ``logp_out`` / ``value_out``, bitwise what
+        ``DeviceNatureCNN.act`` gives), step every env with them and render ``obs_out``."""
+        rew = self.rew if rew_out is None else rew_out
+        done = self.done if done_out is None else done_out
+        self.h.pong_head_step(part, int(splits), fc_b, head_params, int(A), h_out, act_out, logp_out, value_out,
+                              int(sample_seed), int(sample_step), sample_base, self.state, rew, done, self.fin_ret,
+                              self.fin_len, self.ep_acc, obs_out, self.N, self.seed, 0 if offset is None else int(offset),
+                              self.step_t, self.max_steps)
+        if offset is None:
+            self.advance(1)
+        return rew, done
+
     def step(self, act: torch.Tensor, obs_out: torch.Tensor = None, rew_out=None, done_out=None, offset: int = None,
              hist_out: torch.Tensor = None):
         """One env step.  Without ``offset`` the device counter is advanced after the step;

@@ -404,6 +404,24 @@ class DeviceNatureCNN:
                        HIDDEN, True, self.part)  # split-K when the batch is too small to fill the chip
         return hid
 
+    def forward_fc_partials(self, obs_u8, row0: int):
+        """Conv stack + the fc GEMM's split-K partials for rows row0.. (no head): the fused Pong
+        rollout step (``DevicePong.step_head``) forms the hidden units and samples from them.
+        Returns (partials, splits used, hidden-unit view [n * 512] the head writes)."""
+        assert self.fc_nt, "the fused head needs the split-K fc (RRL_FC_NT=1)"
+        n = obs_u8.shape[0]
+        hid = self.forward(obs_u8, row0, fc=False)
+        s = self.fc_splits(n)
+        assert s * n * HIDDEN <= self._fc_part.numel(), "fc split-K partials exceed the preallocated buffer"
+        used = int(self.h.fc_nt_part(self._rows(self.a3, row0, n, FC_IN), self.shadow[self.o["wfc"]:self.o["bfc"]],
+                                     self._fc_part, n, HIDDEN, FC_IN, s))
+        return self._fc_part, used, hid
+
+    def head_params(self):
+        """(fc bias [512], head parameters: A policy rows | A biases | value row | value bias)."""
+        o = self.o
+        return self.params[o["bfc"]:o["bfc"] + HIDDEN], self.params[o["head"]:]
+
     def _forward_head(self, obs_u8, row0, store_acts=True, **head):
         n = obs_u8.shape[0]
         if self.fc_nt:

@@ -101,6 +101,12 @@ class PixelA2CTrainer:
 
             self.model = DeviceNatureCNN(self.spec, dev, max_batch=N * (T + 1), seed=cfg.seed)
             self.env = DevicePong(N, dev, env_seed, cfg.max_episode_steps)
+            # the rollout's policy head inside the env-step launch: +1.6 % at 2,048 envs, -0.3 % at
+            # 8,192 (profiles/r5_pong_fused_head_ab.jsonl), so on up to 4,096 envs by default;
+            # RRL_PONG_FUSED_HEAD=1 / 0 forces it on / off
+            fh = os.environ.get("RRL_PONG_FUSED_HEAD", "")
+            self.fused_head = ((fh == "1") if fh else N <= 4096) and not self.fused_render and \
+                self.model.fc_nt and self.model.A <= 8
             if self.fused_render:
                 self.env.reset(hist_out=self.obs[0])
             else:
@@ -129,10 +135,16 @@ class PixelA2CTrainer:
         cfg, m, N, T = self.cfg, self.model, self.cfg.num_envs, self.cfg.rollout_len
         m.begin_update()  # the transposed Wfc refresh beside the rollout (side stream)
         for t in range(T):
-            m.act(base[t], t * N, self.act[t], self.logp[t], self.val[t], self.sample_seed, t,
-                  step_base=self.sample_t)
             # the last observation goes straight to the next update's start slot
             out = base[t + 1] if (t + 1 < T or nxt is None) else nxt[0]
+            if self.fused_head:  # conv stack + fc partials, then head + env step + render in one launch
+                part, used, hid = m.forward_fc_partials(base[t], t * N)
+                fc_b, hp = m.head_params()
+                self.env.step_head(part, used, fc_b, hp, m.A, hid, self.act[t], self.logp[t], self.val[t],
+                                   self.sample_seed, t, self.sample_t, out, self.rew[t], self.done[t], offset=t)
+                continue
+            m.act(base[t], t * N, self.act[t], self.logp[t], self.val[t], self.sample_seed, t,
+                  step_base=self.sample_t)
             if self.fused_render:
                 self.env.step(self.act[t], None, self.rew[t], self.done[t], offset=t, hist_out=out)
             else:

@@ -842,6 +842,49 @@ def _pong_histories(cuda, N, steps=40, seed=3):
     return hist, obs
 
 
+@pytest.mark.parametrize("N", [37, 2048])
+def test_fused_head_step_equals_head_then_step(cuda, N):
+    """pong_head_step_render_kernel (the policy head inside the env-step launch) vs the head
+    launch (a2c_head from the fc split-K partials) followed by the step + render launch: the
+    same actions, log-probs, values, stored hidden units, env state, rewards, dones and
+    rendered observations -- bitwise -- over several steps from mid-episode states."""
+    import copy
+
+    from relayrl_prototype_amd.envs.pong import DevicePong
+
+    spec = CNNSpec(6)
+    m = DeviceNatureCNN(spec, cuda, max_batch=N, seed=5)
+    envs = [DevicePong(N, cuda, 11), DevicePong(N, cuda, 11)]
+    obs = [torch.zeros(N, 21, 21, 64, dtype=torch.uint8, device=cuda) for _ in range(2)]
+    for e, o in zip(envs, obs):
+        e.reset(o)
+    sample_t = torch.full((1,), 3, dtype=torch.int64, device=cuda)
+    for t in range(6):
+        outs = []
+        for k in range(2):
+            act = torch.full((N,), -1, dtype=torch.int32, device=cuda)
+            logp = torch.full((N,), float("nan"), device=cuda)
+            val = torch.full((N,), float("nan"), device=cuda)
+            rew = torch.full((N,), float("nan"), device=cuda)
+            done = torch.full((N,), float("nan"), device=cuda)
+            nxt = torch.zeros_like(obs[k])
+            if k == 0:
+                m.act(obs[k], 0, act, logp, val, 123, t, step_base=sample_t)
+                envs[k].step(act, nxt, rew, done, offset=t)
+            else:
+                part, used, hid = m.forward_fc_partials(obs[k], 0)
+                fc_b, hp = m.head_params()
+                envs[k].step_head(part, used, fc_b, hp, m.A, hid, act, logp, val, 123, t, sample_t, nxt, rew, done,
+                                  offset=t)
+            torch.cuda.synchronize()
+            outs.append((act.clone(), logp.clone(), val.clone(), m.hid[:N * 512].clone(), rew.clone(), done.clone(),
+                         envs[k].state.clone()))
+            obs[k] = nxt
+        for a, b in zip(*outs):
+            assert torch.equal(a, b)
+        assert torch.equal(obs[0], obs[1])
+
+
 def test_fused_render_draws_the_env_observation(cuda):
     """pong_render_hist(frame histories) == the observation pong_step's render wrote, bitwise;
     the history-output step kernel writes the same rows as the state's history slice."""
