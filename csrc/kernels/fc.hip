@@ -978,14 +978,14 @@ int rrl_fc_nt_mask(const uint16_t* a, const uint16_t* b, const uint16_t* mask, u
   hipStream_t st = (hipStream_t)stream_;
   if (fc_big(false) && K / kFcBK >= 2)  // 256 x 128 persistent tiles, whole K per item
     return launch_fcp_nt<256, 128, 4, 3>(a, b, FcpMask{out, mask}, M, N, K, K / kFcBK, 1, st);
-  // The staged epilogue pays when the output and mask streams leave the 256 MB Infinity
-  // Cache (40,960 x 3,136: 276 -> 220 us in tools/fc_kbench.py); at 10,240 rows inside the
-  // Pong update (both streams cache-resident, the side-stream weight gradients competing for
-  // the CUs) the direct epilogue measured 0.7 % faster end to end (profiles/r3_pong_*).
-  // RRL_FC_DIRECT_EPI = 1 / 0 forces either.
+  // The LDS-staged epilogue (16-byte mask loads and stores): 276 -> 220 us at 40,960 x 3,136 in
+  // tools/fc_kbench.py, and since the round-5 weight-gradient change (its transposed reads no
+  // longer drain the DMA ring, so the side-stream GEMM beside this one is shorter) also faster
+  // at 10,240 rows inside the Pong update: +1.0 % end to end (profiles/r5_pong_side_epi_ab.txt;
+  // round 3 had measured the direct epilogue 0.7 % faster there).  RRL_FC_DIRECT_EPI = 1 forces
+  // the direct epilogue.
   const char* e = getenv("RRL_FC_DIRECT_EPI");
-  const bool big = (long long)M * N * 2 > (96ll << 20);
-  if (N % 8 == 0 && (e && e[0] ? e[0] == '0' : big)) {
+  if (N % 8 == 0 && !(e && e[0] == '1')) {
     const FcMaskStagedEpi epi{out, mask, M, N};
     return fc_stages(1, 2) == 3 ? launch_fc_nt<FcMaskStagedEpi, 3>(a, b, epi, M, N, K, 1, st)
                                 : launch_fc_nt<FcMaskStagedEpi, 2>(a, b, epi, M, N, K, 1, st);
