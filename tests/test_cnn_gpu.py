@@ -701,6 +701,37 @@ def test_fc_tn_part_matches_fp32(cuda, R, I, J, splits, big, monkeypatch):
         assert ((bsum - bref).abs().max() / bref.abs().max()).item() < 1e-5
 
 
+def test_persistent_fc_kernels_in_the_full_update(cuda, monkeypatch):
+    """The 8,192-env sizes take the persistent 256 x 128 fc kernels (forward at >= 4,096 rows,
+    weight + bias gradient at >= 20,480 rows): 5 rollout forwards of 4,096 rows and the backward
+    over all 20,480 rows give the same gradient as the 128 x 128 kernels (RRL_FC_BIG=0) up to
+    fp32 summation order and the bf16 rounding of the stored hidden units."""
+    spec = CNNSpec(6)
+    params = spec.init(11)
+    N, T = 4096, 5
+    B = N * T
+    g = torch.Generator().manual_seed(2)
+    obs = torch.randint(0, 256, (B, 21, 21, 64), dtype=torch.uint8, generator=g).to(cuda)
+    act = torch.randint(0, 6, (B,), dtype=torch.int32, generator=g).to(cuda)
+    adv = torch.randn(B, generator=g).to(cuda)
+    ret = torch.randn(B, generator=g).to(cuda)
+    grads, hids = [], []
+    for big in ("0", "1"):
+        monkeypatch.setenv("RRL_FC_BIG", big)
+        m = DeviceNatureCNN(spec, cuda, max_batch=B, params=params)
+        a_out = torch.empty(N, dtype=torch.int32, device=cuda)
+        lp, v = torch.empty(N, device=cuda), torch.empty(N, device=cuda)
+        for t in range(T):
+            m.act(obs[t * N:(t + 1) * N], t * N, a_out, lp, v, seed=1, step=t)
+        m.backward(obs, act, adv, ret, 0.5, 0.01)
+        torch.cuda.synchronize()
+        grads.append(m.grad.clone())
+        hids.append(m.hid[:B * HIDDEN].float().clone())
+    assert torch.isfinite(grads[1]).all()
+    assert relerr(hids[1], hids[0]) < 5e-3
+    assert relerr(grads[1], grads[0]) < 1e-2
+
+
 def test_sum_splits_multi_matches_torch(cuda):
     """Several slab sums in one launch (the conv layers' weight / bias partials)."""
     from relayrl_prototype_amd.ops import hip
