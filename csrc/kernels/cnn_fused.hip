@@ -398,6 +398,7 @@ constexpr int kXPerT = (kXChunks + kThreads - 1) / kThreads;
 template <int V>
 struct L16 {
   static constexpr bool kPhaseA1 = (V & 16) != 0, kGrid3 = (V & 32) != 0, kRender = (V & 2) != 0;
+  static constexpr bool kSetprio = (V & 4) != 0;  // s_setprio 1 around each role's MFMA clusters
   static constexpr int kA1Ld = kPhaseA1 ? 48 : 40, kA2Ld = 80;
   static constexpr int kA1Rows = kPhaseA1 ? 407 : 400, kA2Rows = kGrid3 ? 84 : 81;
   static constexpr int kA1Elems = kA1Rows * kA1Ld, kA2Elems = kA2Rows * kA2Ld;
@@ -527,6 +528,7 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
           const uint8_t* Fb = F + (j & 1) * L::kRFBytes;
           const int r0 = (p / 20) * 21 + p % 20;  // fused render: positions in rows of 21
           f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (L::kSetprio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int tap = 0; tap < 4; ++tap) {
             uint4 raw;
@@ -540,6 +542,7 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
             acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[2 * tap + 1], hi, acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[8 + 2 * tap + 1], hi, acc1, 0, 0, 0);
           }
+          if constexpr (L::kSetprio) __builtin_amdgcn_s_setprio(0);
           const uint2 v0 = make_uint2(pk_bf16(fmaxf(kU8Scale * acc0[0] + bias0[0], 0.f), fmaxf(kU8Scale * acc0[1] + bias0[1], 0.f)),
                                       pk_bf16(fmaxf(kU8Scale * acc0[2] + bias0[2], 0.f), fmaxf(kU8Scale * acc0[3] + bias0[3], 0.f)));
           const uint2 v1 = make_uint2(pk_bf16(fmaxf(kU8Scale * acc1[0] + bias1[0], 0.f), fmaxf(kU8Scale * acc1[1] + bias1[1], 0.f)),
@@ -573,6 +576,7 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
             const int p = 16 * (MT * pass + u) + i, pc = p < 81 ? p : 0, oh = pc / 9, ow = pc - oh * 9;
             r0[u] = L::kPhaseA1 ? p : 2 * oh * 20 + 2 * ow;  // phase: grid position 10 oh + ow = row of tap (0, 0)
           }
+          if constexpr (L::kSetprio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int ks = 0; ks < 16; ++ks) {
             const int kh = ks >> 2, kw = ks & 3;
@@ -583,6 +587,7 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
 #pragma unroll
             for (int u = 0; u < MT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks], a[u], acc[u], 0, 0, 0);
           }
+          if constexpr (L::kSetprio) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
           for (int u = 0; u < MT; ++u) {
             const int p = 16 * (MT * pass + u) + i, oh = p / 10, ow = p - 10 * (p / 10);
@@ -611,6 +616,7 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
             const int p = 16 * (MT * pass + u) + i, pc = p < 49 ? p : 0, oh = pc / 7, ow = pc - oh * 7;
             r0[u] = L::kGrid3 ? p : oh * 9 + ow;  // grid: position 9 oh + ow = the a2 row of tap (0, 0)
           }
+          if constexpr (L::kSetprio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int ks = 0; ks < 18; ++ks) {
             const int tap = ks >> 1, kh = tap / 3, kw = tap - kh * 3;
@@ -621,6 +627,7 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
 #pragma unroll
             for (int u = 0; u < MT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[ks], a[u], acc[u], 0, 0, 0);
           }
+          if constexpr (L::kSetprio) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
           for (int u = 0; u < MT; ++u) {
             const int p = 16 * (MT * pass + u) + i, oh = p / 9, ow = p - 9 * (p / 9);
@@ -725,6 +732,7 @@ extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const float* hist, const uin
     case 64 + 16: return launch_conv_stack16_fwd<16>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 64 + 32: return launch_conv_stack16_fwd<32>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 64 + 48: return launch_conv_stack16_fwd<48>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 64 + 4: return launch_conv_stack16_fwd<4>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 128: return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 1: return launch_conv_stack_fwd<1>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 2: return launch_conv_stack_fwd<2>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
@@ -785,6 +793,11 @@ __device__ __forceinline__ bf16x8_t tr_frag(const uint16_t* a0, int ld) {
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// SP (wave priority): 1 = s_setprio 1 around each MFMA cluster (cdna_hip_programming.md T5: keeps
+// the compiler from moving MFMAs across the clusters' boundaries; also the form without the 8-byte
+// per-image spill reload of SP 0) -- the shipped kernel; 0 = without; 2 = the static form, waves
+// 4-7 (the younger half) at priority 1 for the whole kernel
+template <int SP = 0>
 __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint16_t* __restrict__ dy,
                                                                      const uint16_t* __restrict__ w,
                                                                      const uint16_t* __restrict__ xact,
@@ -864,6 +877,9 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
     lstore(0);
   }
   if (n0 + G < N) gload(n0 + G);
+  if constexpr (SP == 2) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   for (int j = 0; n0 + j * G < N; ++j) {
     const int n = n0 + j * G;
     __syncthreads();  // buffer j & 1 holds image n; buffer (j + 1) & 1 is no longer read
@@ -875,6 +891,7 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
     const uint16_t* Xi = smem + (j & 1) * kBuf + kX;
 
     // ---- wgrad: 2 position k-steps x (4 co tiles x ntap taps)
+    if constexpr (SP == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int oh = 4 * s + g;  // this lane group's output row (7 = zero border)
@@ -891,6 +908,7 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
 #pragma unroll
         for (int t = 0; t < NTAP; ++t) wacc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[c], bfr[t], wacc[c][t], 0, 0, 0);
     }
+    if constexpr (SP == 1) __builtin_amdgcn_s_setprio(0);
     // ---- dgrad: k-step outer, this wave's 3 pixel tiles inner
     {
       f32x4_t acc[3];
@@ -903,6 +921,7 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
         const int ih = pc / 9, iw = pc - ih * 9;
         rb[u] = (ih + 2) * 11 + (iw + 2);
       }
+      if constexpr (SP == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 18; ++ks) {
         const int t = ks >> 1, kh = t / 3, kw = t - kh * 3;
@@ -913,6 +932,7 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
 #pragma unroll
         for (int u = 0; u < 3; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], a[u], acc[u], 0, 0, 0);
       }
+      if constexpr (SP == 1) __builtin_amdgcn_s_setprio(0);
       // D = da2^T: lane (i16, g) holds channels 16 ct + 4g .. + 3 of pixel q, masked by a2 > 0
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
@@ -1166,7 +1186,9 @@ extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16
                              float* bias_part, int N, int grid, int variant, void* stream) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv3_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
+    (void)hipFuncSetAttribute((const void*)conv3_bwd_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
+    (void)hipFuncSetAttribute((const void*)conv3_bwd_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
+    (void)hipFuncSetAttribute((const void*)conv3_bwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
     (void)hipFuncSetAttribute((const void*)conv3_bwd16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
     attr = true;
   }
@@ -1176,8 +1198,18 @@ extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16
                        xact, dx, part, bias_part, N);
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(conv3_bwd_kernel, dim3(grid), dim3(c3b::kThreads), c3b::kLds, (hipStream_t)stream, dy, w, xact,
-                     dx, part, bias_part, N);
+  // variant 0 (default): s_setprio 1 around the MFMA clusters (SP 1): 163.6 -> 144.7 us per
+  // 10,240 images, Pong +1.3 % / +1.4 % at 2,048 / 8,192 envs (profiles/r5_setprio_ab.txt);
+  // 2 = without it (SP 0), 3 = the static form (SP 2)
+  if (variant == 2)
+    hipLaunchKernelGGL(conv3_bwd_kernel<0>, dim3(grid), dim3(c3b::kThreads), c3b::kLds, (hipStream_t)stream, dy, w,
+                       xact, dx, part, bias_part, N);
+  else if (variant == 3)
+    hipLaunchKernelGGL(conv3_bwd_kernel<2>, dim3(grid), dim3(c3b::kThreads), c3b::kLds, (hipStream_t)stream, dy, w,
+                       xact, dx, part, bias_part, N);
+  else
+    hipLaunchKernelGGL(conv3_bwd_kernel<1>, dim3(grid), dim3(c3b::kThreads), c3b::kLds, (hipStream_t)stream, dy, w,
+                       xact, dx, part, bias_part, N);
   return (int)hipGetLastError();
 }
 
@@ -1228,7 +1260,7 @@ __device__ __forceinline__ bf16x8_t tr_frag2(const uint16_t* a0, const uint16_t*
 // discarded), 8 tiles: the 16 pixels of a fragment read 16 consecutive da2 rows, 1.86 -> 1.0
 // modelled LDS factor (tools/lds_bank_model.py --conv2) -- measured 203.7 -> 205.8 us and Pong
 // -0.1 to -0.4 % in an ABBA run (profiles/r4_bwd2_grid_ab.txt): not shipped
-template <bool STAGED, bool GRID12 = false>
+template <bool STAGED, bool GRID12 = false, int SP = 0>  // SP: wave priority, as conv3_bwd_kernel
 __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint16_t* __restrict__ dy,
                                                                      const uint16_t* __restrict__ w,
                                                                      const uint16_t* __restrict__ xact,
@@ -1310,6 +1342,9 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
     lstore(0);
   }
   if (n0 + G < N) gload(n0 + G);
+  if constexpr (SP == 2) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   for (int j = 0; n0 + j * G < N; ++j) {
     const int n = n0 + j * G;
     __syncthreads();  // buffer j & 1 holds image n; buffer (j + 1) & 1 is no longer read
@@ -1321,6 +1356,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
     const uint16_t* P = D + kDRows * kDLd;
 
     // ---- wgrad: 4 position k-steps (8 runs of 4 columns each), 4 co tiles x 4 taps
+    if constexpr (SP == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       int oh[2], ow0[2];
@@ -1347,6 +1383,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
 #pragma unroll
         for (int t = 0; t < 4; ++t) wacc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[c], bfr[t], wacc[c][t], 0, 0, 0);
     }
+    if constexpr (SP == 1) __builtin_amdgcn_s_setprio(0);
     // ---- dgrad of phase class (ph, pw), c tile ct: 7 pixel tiles in two batches (rows past the
     // class are computed and discarded; GRID12: 8 tiles of the 10 x 12 grid)
     auto class_tiles = [&](auto tag) {
@@ -1364,6 +1401,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
           rb[u] = (a + 1) * 12 + (b + 1);
         }
       }
+      if constexpr (SP == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
         const int t = ks >> 1, ti = t >> 1, tj = t & 1;
@@ -1374,6 +1412,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
 #pragma unroll
         for (int u = 0; u < NT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], bv[u], acc[u], 0, 0, 0);
       }
+      if constexpr (SP == 1) __builtin_amdgcn_s_setprio(0);
       // D = da1^T: lane (i16, g) holds channels 16 ct + 4g .. + 3 of class pixel p
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
@@ -1669,6 +1708,10 @@ extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16
                               hipFuncAttributeMaxDynamicSharedMemorySize, c2b::kLds);
     (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               kStagedLds);
+    (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<false, false, 1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, c2b::kLds);
+    (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<false, false, 2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, c2b::kLds);
     attr = true;
   }
   if (N < 1 || grid < 1) return 0;
@@ -1680,6 +1723,13 @@ extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16
     }
     hipLaunchKernelGGL(conv2_bwd16_kernel, dim3(grid), dim3(c2b16::kThreads), c2b::kLds, (hipStream_t)stream, dy, w,
                        xact, dx, part, bias_part, N);
+  } else if (staged == 4 || staged == 5) {  // wave-priority A/B forms (SP 1 / 2)
+    if (staged == 4)
+      hipLaunchKernelGGL((conv2_bwd_kernel<false, false, 1>), dim3(grid), dim3(c2b::kThreads), c2b::kLds,
+                         (hipStream_t)stream, dy, w, xact, dx, part, bias_part, N);
+    else
+      hipLaunchKernelGGL((conv2_bwd_kernel<false, false, 2>), dim3(grid), dim3(c2b::kThreads), c2b::kLds,
+                         (hipStream_t)stream, dy, w, xact, dx, part, bias_part, N);
   } else if (staged == 1)
     hipLaunchKernelGGL(conv2_bwd_kernel<true>, dim3(grid), dim3(c2b::kThreads), kStagedLds, (hipStream_t)stream, dy, w,
                        xact, dx, part, bias_part, N);
@@ -1713,7 +1763,7 @@ constexpr int kXPT = (kXC + kThreads - 1) / kThreads, kYPT = (kYC + kThreads - 1
 
 // RENDER: the frames are drawn from PongSynth frame histories hist[N][16] (pong_render.h)
 // instead of read from an observation tensor
-template <bool RENDER>
+template <bool RENDER, bool SP = false>  // SP: s_setprio 1 around each chunk's MFMAs (A/B)
 __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const uint8_t* __restrict__ x,
                                                                         const float* __restrict__ hist,
                                                                         const uint16_t* __restrict__ dy,
@@ -1820,6 +1870,7 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
         bfr[nt] = tr_frag2(Xi + ra * kLd + 16 * nt + 4 * pp, Xi + rb * kLd + 16 * nt + 4 * pp);
+      if constexpr (SP) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
@@ -1828,6 +1879,7 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) accb[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], ones, accb[mt], 0, 0, 0);
       }
+      if constexpr (SP) __builtin_amdgcn_s_setprio(0);
     }
     if (draw_late && n + G < N) xload(n + G);
   }
@@ -1862,6 +1914,18 @@ extern "C" int rrl_conv1_wgrad8(const uint8_t* x, const float* hist, const uint1
     attr = true;
   }
   if (N < 1 || grid < 1) return 0;
+  const char* sp = getenv("RRL_CNN_WGRAD1_SETPRIO");  // A/B: 1 = the s_setprio form (read per call)
+  if (!hist && sp && sp[0] == '1') {
+    static bool attr_sp = false;
+    if (!attr_sp) {
+      (void)hipFuncSetAttribute((const void*)conv1_wgrad8_kernel<false, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, c1w::kLds);
+      attr_sp = true;
+    }
+    hipLaunchKernelGGL((conv1_wgrad8_kernel<false, true>), dim3(grid), dim3(c1w::kThreads), c1w::kLds,
+                       (hipStream_t)stream, x, hist, dy, part, bias_part, N);
+    return (int)hipGetLastError();
+  }
   if (hist) {
     hipLaunchKernelGGL(conv1_wgrad8_kernel<true>, dim3(grid), dim3(c1w::kThreads), c1w::kLds, (hipStream_t)stream, x,
                        hist, dy, part, bias_part, N);

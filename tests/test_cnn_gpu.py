@@ -566,11 +566,13 @@ def test_fused_conv_bwd_kernels_match_autograd(cuda, li, N, grid, staged):
     assert relerr(db, db_ref) < 1e-3
 
 
+@pytest.mark.parametrize("sp", ["0", "1"])  # RRL_CNN_WGRAD1_SETPRIO: the s_setprio form
 @pytest.mark.parametrize("N,grid", [(1, 1), (9, 4), (300, 64)])
-def test_conv1_wgrad8_matches_autograd(cuda, N, grid):
+def test_conv1_wgrad8_matches_autograd(cuda, N, grid, sp, monkeypatch):
     """8-wave conv1 weight / bias gradient (cnn_fused.hip) vs fp32 autograd on the s2d frames."""
     from relayrl_prototype_amd.ops import hip
 
+    monkeypatch.setenv("RRL_CNN_WGRAD1_SETPRIO", sp)
     h = hip()
     g = torch.Generator().manual_seed(N)
     x = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g)
@@ -1038,7 +1040,7 @@ def test_pixel_alternating_obs_buffers_match_copy_path(cuda, monkeypatch):
     assert a.metrics()["EnvSteps"] == b.metrics()["EnvSteps"]
 
 
-@pytest.mark.parametrize("base,probe", [(128, 16), (128, 32), (128, 48), (64, 80), (64, 96), (64, 112)])
+@pytest.mark.parametrize("base,probe", [(128, 16), (128, 32), (128, 48), (64, 80), (64, 96), (64, 112), (64, 68)])
 def test_fused_conv_stack_layout_variants_are_bitwise_equal(cuda, base, probe):
     """The forward's LDS layout variants (FwdLayout probe bits: a1 as stride-2 phase images with
     conv2 over a 9 x 10 grid, conv3 over a 7 x 9 grid) run the same MFMA k-order per output:
@@ -1100,9 +1102,11 @@ def test_fused_conv_stack_without_stored_activations(cuda, variant):
     assert torch.isnan(outs[1][0].float()).all() and torch.isnan(outs[1][1].float()).all()
 
 
-def test_conv3_bwd_16wave_is_bitwise_equal(cuda):
+@pytest.mark.parametrize("variant", [1, 2, 3], ids=["16wave", "no_setprio", "setprio_static"])
+def test_conv3_bwd_16wave_is_bitwise_equal(cuda, variant):
     """The 16-wave conv3 backward (dgrad and wgrad on separate waves) runs the 8-wave kernel's
-    k-order per output: da2, the weight and the bias partials bitwise equal."""
+    k-order per output: da2, the weight and the bias partials bitwise equal; so do the other
+    wave-priority forms (2: none, 3: static) of the 8-wave kernel (shipped: s_setprio clusters)."""
     from relayrl_prototype_amd.ops import hip
 
     h = hip()
@@ -1113,7 +1117,7 @@ def test_conv3_bwd_16wave_is_bitwise_equal(cuda):
     w = (torch.randn(L.cout * L.K, generator=g) * 0.05).bfloat16().to(cuda)
     dy = torch.randn(N * L.hout * L.hout * L.cout, generator=g).bfloat16().to(cuda)
     outs = []
-    for v in (0, 1):
+    for v in (0, variant):
         dx = torch.full((N * L.hin * L.hin * L.cin,), float("nan"), dtype=torch.bfloat16, device=cuda)
         part = torch.full((grid * L.cout * L.K,), float("nan"), device=cuda)
         bpart = torch.full((grid * 512,), float("nan"), device=cuda)
@@ -1124,7 +1128,7 @@ def test_conv3_bwd_16wave_is_bitwise_equal(cuda):
         assert torch.isfinite(a.float()).all() and torch.equal(a, b)
 
 
-@pytest.mark.parametrize("variant", [2, 3], ids=["grid12", "16wave"])
+@pytest.mark.parametrize("variant", [2, 3, 4, 5], ids=["grid12", "16wave", "setprio", "setprio_static"])
 def test_conv2_bwd_dgrad_grids_are_bitwise_equal(cuda, variant):
     """The conv2 backward's dgrad over the class's 100 pixels in 7 tiles (shipped) against the
     dgrad over a 10 x 12 grid per phase class (variant 2) and the 16-wave kernel with dgrad and

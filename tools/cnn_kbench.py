@@ -74,6 +74,15 @@ def main():
 
     fns = {}
     fns["wgrad1_8"] = lambda: h.conv1_wgrad8(x[:Nb], da1, part, bpart, Nb, min(Nb, cus))
+
+    def wgrad1_8_sp():  # the s_setprio form (RRL_CNN_WGRAD1_SETPRIO, read per call)
+        os.environ["RRL_CNN_WGRAD1_SETPRIO"] = "1"
+        try:
+            h.conv1_wgrad8(x[:Nb], da1, part, bpart, Nb, min(Nb, cus))
+        finally:
+            os.environ["RRL_CNN_WGRAD1_SETPRIO"] = "0"
+    fns["wgrad1_8_sp"] = wgrad1_8_sp
+    fns["fwd16_sp"] = probe(68)
     fns["wgrad1"] = lambda: h.conv_wgrad(da1, x[:Nb], part, 256, Nb, 21, 21, 64, 2, 2, 1, 32, bpart)
     fns.update({"p_nomfma": probe(1), "p_nostore": probe(2), "p_nostore_nomfma": probe(3), "p_hotframe": probe(4),
            "p_all": probe(7), "fwd_c1split": probe(8), "fwd_g128": probe(0, 128), "fwd_phase_a1": probe(16), "fwd_c3_grid": probe(32), "fwd_phase_a1_c3_grid": probe(48), "fwd_g512": probe(0, 512), "fwd8": probe(128), "fwd16": probe(64), "fwd16_phase": probe(80), "fwd16_grid3": probe(96), "fwd16_both": probe(112), "fwd": fwd, "fwd_layers": fwd_layers, "bwd3": bwd3, "bwd3_16": bwd3_16, "bwd3_layers": bwd3_layers, "dgrad2": dgrad2})
@@ -87,6 +96,12 @@ def main():
         fns["bwd2_staged"] = bwd2_staged
         fns["bwd2_16"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=3)
         fns["bwd2_grid12"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=2)
+        # wave priority (s_setprio): 4 = around each MFMA cluster, 5 = waves 4-7 raised for the kernel
+        fns["bwd2_sp1"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=4)
+        fns["bwd2_sp2"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=5)
+    # conv3 backward wave priority: bwd3 = the shipped s_setprio-cluster form, bwd3_sp0 = without
+    fns["bwd3_sp0"] = lambda: h.conv3_bwd(da3, W[3][0], a2, da2, part, bpart, Nb, min(Nb, cus), variant=2)
+    fns["bwd3_sp2"] = lambda: h.conv3_bwd(da3, W[3][0], a2, da2, part, bpart, Nb, min(Nb, cus), variant=3)
 
     # --rounds R: the list R times, every other round in reverse order (the first kernel timed
     # in a process reads slow), median per kernel
