@@ -399,6 +399,8 @@ template <int V>
 struct L16 {
   static constexpr bool kPhaseA1 = (V & 16) != 0, kGrid3 = (V & 32) != 0, kRender = (V & 2) != 0;
   static constexpr bool kSetprio = (V & 4) != 0;  // s_setprio 1 around each role's MFMA clusters
+  // static wave priority for the whole kernel (A/B): bit 1 raises the conv2 role, bit 8 the conv3 role
+  static constexpr int kPrioRole2 = (V & 1) ? 2 : 0, kPrioRole3 = (V & 8) ? 2 : 0;
   static constexpr int kA1Ld = kPhaseA1 ? 48 : 40, kA2Ld = 80;
   static constexpr int kA1Rows = kPhaseA1 ? 407 : 400, kA2Rows = kGrid3 ? 84 : 81;
   static constexpr int kA1Elems = kA1Rows * kA1Ld, kA2Elems = kA2Rows * kA2Ld;
@@ -454,6 +456,8 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
   uint8_t* F = reinterpret_cast<uint8_t*>(smem);
   const int lane = tid & 63, i = lane & 15, g = lane >> 4;
   const int ct = wave & 3;  // co tile of conv2 / conv3
+  if constexpr (ROLE == 2 && L::kPrioRole2) __builtin_amdgcn_s_setprio(L::kPrioRole2);
+  if constexpr (ROLE == 3 && L::kPrioRole3) __builtin_amdgcn_s_setprio(L::kPrioRole3);
   // stationary weights, A fragments W[co = 16 tile + i][8 consecutive k]:
   //   conv1 fw[8 c + 2 tap + h] = W1[16 c + i][64 tap + 16 g + 8 h ..]; conv2 / conv3 fw[ks] = W[..][32 ks + 8 g ..]
   constexpr int NF = ROLE == 3 ? 18 : 16;
@@ -733,6 +737,9 @@ extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const float* hist, const uin
     case 64 + 32: return launch_conv_stack16_fwd<32>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 64 + 48: return launch_conv_stack16_fwd<48>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 64 + 4: return launch_conv_stack16_fwd<4>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 64 + 1: return launch_conv_stack16_fwd<1>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 64 + 8: return launch_conv_stack16_fwd<8>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
+    case 64 + 9: return launch_conv_stack16_fwd<9>(x, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 128: return launch_conv_stack_fwd<0>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 1: return launch_conv_stack_fwd<1>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);
     case 2: return launch_conv_stack_fwd<2>(x, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st);

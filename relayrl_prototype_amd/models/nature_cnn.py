@@ -194,7 +194,7 @@ class DeviceNatureCNN:
         # (RRL_CONV_FWD, default the 16-wave one), 128 = the 8-wave kernel, 16 / 32 / 48 = its LDS layouts (a1 as phase
         # images, conv3 over a 7 x 9 grid, both); 64 = the 16-wave kernel, 80 / 96 / 112 = its layouts
         self.fwd_layout = int(os.environ.get("RRL_CNN_FWD_LAYOUT", "0"))
-        assert self.fwd_layout in (0, 16, 32, 48, 64, 68, 80, 96, 112, 128), "RRL_CNN_FWD_LAYOUT"
+        assert self.fwd_layout in (0, 16, 32, 48, 64, 65, 68, 72, 73, 80, 96, 112, 128), "RRL_CNN_FWD_LAYOUT"
         # conv2 backward variant (A/B runs): 0 = dgrad over 7 tiles per class, 2 = a 10 x 12 grid
         self.bwd2_variant = int(os.environ.get("RRL_CNN_BWD2_VARIANT", "0"))
         assert self.bwd2_variant in (0, 2, 3, 4, 5), "RRL_CNN_BWD2_VARIANT: 0, 2, 3 (16 waves), 4 / 5 (wave priority)"

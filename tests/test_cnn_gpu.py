@@ -1040,7 +1040,8 @@ def test_pixel_alternating_obs_buffers_match_copy_path(cuda, monkeypatch):
     assert a.metrics()["EnvSteps"] == b.metrics()["EnvSteps"]
 
 
-@pytest.mark.parametrize("base,probe", [(128, 16), (128, 32), (128, 48), (64, 80), (64, 96), (64, 112), (64, 68)])
+@pytest.mark.parametrize("base,probe", [(128, 16), (128, 32), (128, 48), (64, 80), (64, 96), (64, 112), (64, 68),
+                                       (64, 65), (64, 72), (64, 73)])
 def test_fused_conv_stack_layout_variants_are_bitwise_equal(cuda, base, probe):
     """The forward's LDS layout variants (FwdLayout probe bits: a1 as stride-2 phase images with
     conv2 over a 9 x 10 grid, conv3 over a 7 x 9 grid) run the same MFMA k-order per output:

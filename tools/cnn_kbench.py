@@ -83,6 +83,9 @@ def main():
             os.environ["RRL_CNN_WGRAD1_SETPRIO"] = "0"
     fns["wgrad1_8_sp"] = wgrad1_8_sp
     fns["fwd16_sp"] = probe(68)
+    fns["fwd16_prio2"] = probe(65)  # static priority: the conv2 role
+    fns["fwd16_prio3"] = probe(72)  # the conv3 role
+    fns["fwd16_prio23"] = probe(73)
     fns["wgrad1"] = lambda: h.conv_wgrad(da1, x[:Nb], part, 256, Nb, 21, 21, 64, 2, 2, 1, 32, bpart)
     fns.update({"p_nomfma": probe(1), "p_nostore": probe(2), "p_nostore_nomfma": probe(3), "p_hotframe": probe(4),
            "p_all": probe(7), "fwd_c1split": probe(8), "fwd_g128": probe(0, 128), "fwd_phase_a1": probe(16), "fwd_c3_grid": probe(32), "fwd_phase_a1_c3_grid": probe(48), "fwd_g512": probe(0, 512), "fwd8": probe(128), "fwd16": probe(64), "fwd16_phase": probe(80), "fwd16_grid3": probe(96), "fwd16_both": probe(112), "fwd": fwd, "fwd_layers": fwd_layers, "bwd3": bwd3, "bwd3_16": bwd3_16, "bwd3_layers": bwd3_layers, "dgrad2": dgrad2})
