@@ -898,7 +898,7 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
     const uint16_t* Xi = smem + (j & 1) * kBuf + kX;
 
     // ---- wgrad: 2 position k-steps x (4 co tiles x ntap taps)
-    if constexpr (SP == 1) __builtin_amdgcn_s_setprio(1);
+    if constexpr (SP == 1 || SP == 3) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int oh = 4 * s + g;  // this lane group's output row (7 = zero border)
@@ -915,7 +915,7 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
 #pragma unroll
         for (int t = 0; t < NTAP; ++t) wacc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[c], bfr[t], wacc[c][t], 0, 0, 0);
     }
-    if constexpr (SP == 1) __builtin_amdgcn_s_setprio(0);
+    if constexpr (SP == 1 || SP == 3) __builtin_amdgcn_s_setprio(0);
     // ---- dgrad: k-step outer, this wave's 3 pixel tiles inner
     {
       f32x4_t acc[3];
@@ -928,7 +928,7 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
         const int ih = pc / 9, iw = pc - ih * 9;
         rb[u] = (ih + 2) * 11 + (iw + 2);
       }
-      if constexpr (SP == 1) __builtin_amdgcn_s_setprio(1);
+      if constexpr (SP == 1 || SP == 4) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 18; ++ks) {
         const int t = ks >> 1, kh = t / 3, kw = t - kh * 3;
@@ -939,7 +939,7 @@ __global__ __launch_bounds__(c3b::kThreads, 1) void conv3_bwd_kernel(const uint1
 #pragma unroll
         for (int u = 0; u < 3; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], a[u], acc[u], 0, 0, 0);
       }
-      if constexpr (SP == 1) __builtin_amdgcn_s_setprio(0);
+      if constexpr (SP == 1 || SP == 4) __builtin_amdgcn_s_setprio(0);
       // D = da2^T: lane (i16, g) holds channels 16 ct + 4g .. + 3 of pixel q, masked by a2 > 0
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
@@ -1214,6 +1214,16 @@ extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16
   else if (variant == 3)
     hipLaunchKernelGGL(conv3_bwd_kernel<2>, dim3(grid), dim3(c3b::kThreads), c3b::kLds, (hipStream_t)stream, dy, w,
                        xact, dx, part, bias_part, N);
+  else if (variant == 4 || variant == 5) {  // the priority pair around the wgrad / dgrad cluster only
+    static bool attr_sp = false;
+    if (!attr_sp) {
+      (void)hipFuncSetAttribute((const void*)conv3_bwd_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
+      (void)hipFuncSetAttribute((const void*)conv3_bwd_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
+      attr_sp = true;
+    }
+    hipLaunchKernelGGL(variant == 4 ? conv3_bwd_kernel<3> : conv3_bwd_kernel<4>, dim3(grid), dim3(c3b::kThreads),
+                       c3b::kLds, (hipStream_t)stream, dy, w, xact, dx, part, bias_part, N);
+  }
   else
     hipLaunchKernelGGL(conv3_bwd_kernel<1>, dim3(grid), dim3(c3b::kThreads), c3b::kLds, (hipStream_t)stream, dy, w,
                        xact, dx, part, bias_part, N);
@@ -1363,7 +1373,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
     const uint16_t* P = D + kDRows * kDLd;
 
     // ---- wgrad: 4 position k-steps (8 runs of 4 columns each), 4 co tiles x 4 taps
-    if constexpr (SP == 1) __builtin_amdgcn_s_setprio(1);
+    if constexpr (SP == 1 || SP == 3) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       int oh[2], ow0[2];
@@ -1390,7 +1400,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
 #pragma unroll
         for (int t = 0; t < 4; ++t) wacc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[c], bfr[t], wacc[c][t], 0, 0, 0);
     }
-    if constexpr (SP == 1) __builtin_amdgcn_s_setprio(0);
+    if constexpr (SP == 1 || SP == 3) __builtin_amdgcn_s_setprio(0);
     // ---- dgrad of phase class (ph, pw), c tile ct: 7 pixel tiles in two batches (rows past the
     // class are computed and discarded; GRID12: 8 tiles of the 10 x 12 grid)
     auto class_tiles = [&](auto tag) {
@@ -1408,7 +1418,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
           rb[u] = (a + 1) * 12 + (b + 1);
         }
       }
-      if constexpr (SP == 1) __builtin_amdgcn_s_setprio(1);
+      if constexpr (SP == 1 || SP == 4) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
         const int t = ks >> 1, ti = t >> 1, tj = t & 1;
@@ -1419,7 +1429,7 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
 #pragma unroll
         for (int u = 0; u < NT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], bv[u], acc[u], 0, 0, 0);
       }
-      if constexpr (SP == 1) __builtin_amdgcn_s_setprio(0);
+      if constexpr (SP == 1 || SP == 4) __builtin_amdgcn_s_setprio(0);
       // D = da1^T: lane (i16, g) holds channels 16 ct + 4g .. + 3 of class pixel p
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
@@ -1730,13 +1740,21 @@ extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16
     }
     hipLaunchKernelGGL(conv2_bwd16_kernel, dim3(grid), dim3(c2b16::kThreads), c2b::kLds, (hipStream_t)stream, dy, w,
                        xact, dx, part, bias_part, N);
-  } else if (staged == 4 || staged == 5) {  // wave-priority A/B forms (SP 1 / 2)
-    if (staged == 4)
-      hipLaunchKernelGGL((conv2_bwd_kernel<false, false, 1>), dim3(grid), dim3(c2b::kThreads), c2b::kLds,
-                         (hipStream_t)stream, dy, w, xact, dx, part, bias_part, N);
-    else
-      hipLaunchKernelGGL((conv2_bwd_kernel<false, false, 2>), dim3(grid), dim3(c2b::kThreads), c2b::kLds,
-                         (hipStream_t)stream, dy, w, xact, dx, part, bias_part, N);
+  } else if (staged >= 4 && staged <= 7) {  // wave-priority A/B forms: SP 1 (both clusters) / 2 (static) /
+    // 3 (the wgrad cluster only) / 4 (the dgrad cluster only)
+    static bool attr_sp = false;
+    if (!attr_sp) {
+      (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<false, false, 3>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, c2b::kLds);
+      (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<false, false, 4>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, c2b::kLds);
+      attr_sp = true;
+    }
+    auto* k = staged == 4 ? conv2_bwd_kernel<false, false, 1>
+                          : (staged == 5 ? conv2_bwd_kernel<false, false, 2>
+                                         : (staged == 6 ? conv2_bwd_kernel<false, false, 3> : conv2_bwd_kernel<false, false, 4>));
+    hipLaunchKernelGGL(k, dim3(grid), dim3(c2b::kThreads), c2b::kLds, (hipStream_t)stream, dy, w, xact, dx, part,
+                       bias_part, N);
   } else if (staged == 1)
     hipLaunchKernelGGL(conv2_bwd_kernel<true>, dim3(grid), dim3(c2b::kThreads), kStagedLds, (hipStream_t)stream, dy, w,
                        xact, dx, part, bias_part, N);

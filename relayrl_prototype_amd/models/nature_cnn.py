@@ -197,10 +197,10 @@ class DeviceNatureCNN:
         assert self.fwd_layout in (0, 16, 32, 48, 64, 65, 68, 72, 73, 80, 96, 112, 128), "RRL_CNN_FWD_LAYOUT"
         # conv2 backward variant (A/B runs): 0 = dgrad over 7 tiles per class, 2 = a 10 x 12 grid
         self.bwd2_variant = int(os.environ.get("RRL_CNN_BWD2_VARIANT", "0"))
-        assert self.bwd2_variant in (0, 2, 3, 4, 5), "RRL_CNN_BWD2_VARIANT: 0, 2, 3 (16 waves), 4 / 5 (wave priority)"
+        assert self.bwd2_variant in (0, 2, 3, 4, 5, 6, 7), "RRL_CNN_BWD2_VARIANT: 0, 2, 3 (16 waves), 4-7 (wave priority)"
         self.bwd3_variant = int(os.environ.get("RRL_CNN_BWD3_VARIANT", "0"))
-        assert self.bwd3_variant in (0, 1, 2, 3), \
-            "RRL_CNN_BWD3_VARIANT: 0 (s_setprio clusters), 1 (16 waves), 2 (no s_setprio), 3 (static priority)"
+        assert self.bwd3_variant in (0, 1, 2, 3, 4, 5), \
+            "RRL_CNN_BWD3_VARIANT: 0 (s_setprio clusters), 1 (16 waves), 2 (no s_setprio), 3 (static), 4 / 5 (one cluster)"
         # conv2 backward + conv1 weight gradient in C row chunks, each chunk's da1 read back by
         # conv1_wgrad8 right after conv2_bwd wrote it (RRL_CNN_BWD21_CHUNKS, for A/B runs: a half
         # batch's da1 fits the 256 MB Infinity Cache, the whole one does not at 10,240 frames)

@@ -1103,7 +1103,8 @@ def test_fused_conv_stack_without_stored_activations(cuda, variant):
     assert torch.isnan(outs[1][0].float()).all() and torch.isnan(outs[1][1].float()).all()
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3], ids=["16wave", "no_setprio", "setprio_static"])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5],
+                         ids=["16wave", "no_setprio", "setprio_static", "setprio_wgrad", "setprio_dgrad"])
 def test_conv3_bwd_16wave_is_bitwise_equal(cuda, variant):
     """The 16-wave conv3 backward (dgrad and wgrad on separate waves) runs the 8-wave kernel's
     k-order per output: da2, the weight and the bias partials bitwise equal; so do the other
@@ -1129,7 +1130,8 @@ def test_conv3_bwd_16wave_is_bitwise_equal(cuda, variant):
         assert torch.isfinite(a.float()).all() and torch.equal(a, b)
 
 
-@pytest.mark.parametrize("variant", [2, 3, 4, 5], ids=["grid12", "16wave", "setprio", "setprio_static"])
+@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6, 7],
+                         ids=["grid12", "16wave", "setprio", "setprio_static", "setprio_wgrad", "setprio_dgrad"])
 def test_conv2_bwd_dgrad_grids_are_bitwise_equal(cuda, variant):
     """The conv2 backward's dgrad over the class's 100 pixels in 7 tiles (shipped) against the
     dgrad over a 10 x 12 grid per phase class (variant 2) and the 16-wave kernel with dgrad and
