@@ -116,7 +116,7 @@ __device__ __forceinline__ void fc_stage(const uint16_t* __restrict__ X, int row
 // STAGES = 3: two k-tiles in flight, one 8-wave workgroup per CU (96 KB); STAGES = 2: one
 // k-tile in flight, two workgroups per CU (64 KB each), so one workgroup's epilogue and
 // prologue overlap the other's main loop (short-K problems: the data gradient, K = 512).
-template <class Epi, int STAGES>
+template <class Epi, int STAGES, bool SP = false>  // SP: s_setprio 1 around the k-tile's MFMAs (A/B)
 __global__ void __launch_bounds__(kFcThreads, STAGES == 2 ? 2 : 1)
 fc_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, Epi epi, int M, int N, int K,
              int tiles_m, int tiles_n, int ktiles_per_split, int m_fast) {
@@ -197,6 +197,7 @@ fc_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, Epi
     }
     const uint16_t* Ai = smem + (t % STAGES) * kFcStage;
     const uint16_t* Bi = Ai + kFcImg;
+    if constexpr (SP) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < kFcBK / 32; ++s) {
       const int kc = 4 * s + g;
@@ -213,6 +214,7 @@ fc_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B, Epi
         for (int j = 0; j < 2; ++j)  // D[n][m]: lane (g, li) holds n = 4 g .. 4 g + 3 of row m = li
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
+    if constexpr (SP) __builtin_amdgcn_s_setprio(0);
   }
   if constexpr (FcStaged<Epi>::value) {
     constexpr int LD = FcMaskStagedEpi::kLd;
@@ -268,12 +270,28 @@ static int fc_stages(int site, int dflt) {
   return e[site] == '4' ? 4 : (e[site] == '3' ? 3 : (e[site] == '2' ? 2 : dflt));
 }
 
+static bool fc_setprio() {  // RRL_FC_SETPRIO=1: the s_setprio forms (A/B), read per call
+  const char* e = getenv("RRL_FC_SETPRIO");
+  return e && e[0] == '1';
+}
+
+template <class Epi, int STAGES, bool SP = false>
+static int launch_fc_nt_sp(const uint16_t* A, const uint16_t* B, Epi epi, int M, int N, int K, int splits,
+                           hipStream_t st);
+
 template <class Epi, int STAGES>
 static int launch_fc_nt(const uint16_t* A, const uint16_t* B, Epi epi, int M, int N, int K, int splits,
                         hipStream_t st) {
+  return fc_setprio() ? launch_fc_nt_sp<Epi, STAGES, true>(A, B, epi, M, N, K, splits, st)
+                      : launch_fc_nt_sp<Epi, STAGES, false>(A, B, epi, M, N, K, splits, st);
+}
+
+template <class Epi, int STAGES, bool SP>
+static int launch_fc_nt_sp(const uint16_t* A, const uint16_t* B, Epi epi, int M, int N, int K, int splits,
+                           hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fc_nt_kernel<Epi, STAGES>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)fc_nt_kernel<Epi, STAGES, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               fc_lds_bytes<STAGES>());
     attr = true;
   }
@@ -283,7 +301,7 @@ static int launch_fc_nt(const uint16_t* A, const uint16_t* B, Epi epi, int M, in
   splits = (kt + kps - 1) / kps;
   const int grid = tiles_m * tiles_n * splits;
   if (grid < 1) return 0;
-  hipLaunchKernelGGL((fc_nt_kernel<Epi, STAGES>), dim3(grid), dim3(kFcThreads), fc_lds_bytes<STAGES>(), st, A, B,
+  hipLaunchKernelGGL((fc_nt_kernel<Epi, STAGES, SP>), dim3(grid), dim3(kFcThreads), fc_lds_bytes<STAGES>(), st, A, B,
                      epi, M, N, K, tiles_m, tiles_n, kps, fc_m_fast());
   return (int)hipGetLastError();
 }
@@ -350,7 +368,7 @@ __device__ __forceinline__ void fcp_lgkm_wait(bf16x8_t (&x)[FI], bf16x8_t (&y)[F
 // 128 (i) x 128 (j) output tile per workgroup, 8 waves (2 x 4: 64 i x 32 j each), the R
 // reduction split over gridDim (split z takes r-tiles [z * kps, (z + 1) * kps)); fp32
 // partials part[z][I][J], 4 consecutive j per lane (16-byte stores).
-template <int STAGES>
+template <int STAGES, bool SP = false>
 __global__ void __launch_bounds__(kFcThreads, STAGES == 2 ? 2 : 1)
 fc_tn_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, float* __restrict__ part, int R, int I,
              int J, int tiles_i, int tiles_j, int rtiles_per_split, const uint16_t* __restrict__ ones,
@@ -394,6 +412,7 @@ fc_tn_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, flo
     if (t + STAGES - 1 < nk) issue(t + STAGES - 1);
     const uint16_t* Xi = smem + (t % STAGES) * kFcStage;
     const uint16_t* Yi = Xi + kFcImg;
+    if constexpr (SP) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8_t xf[4], yf[2];
@@ -408,6 +427,7 @@ fc_tn_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, flo
         for (int c = 0; c < 2; ++c)  // D[j][i]: lane (g, li) holds j = 4 g .. 4 g + 3 of i = li
           acc[a][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(yf[c], xf[a], acc[a][c], 0, 0, 0);
     }
+    if constexpr (SP) __builtin_amdgcn_s_setprio(0);
   }
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -419,21 +439,28 @@ fc_tn_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, flo
     }
 }
 
-template <int STAGES>
-static int launch_fc_tn(const uint16_t* X, const uint16_t* Y, float* part, int R, int I, int J, int splits,
-                        const uint16_t* ones, float* bias_part, hipStream_t st) {
+template <int STAGES, bool SP>
+static int launch_fc_tn_sp(const uint16_t* X, const uint16_t* Y, float* part, int R, int I, int J, int splits,
+                           const uint16_t* ones, float* bias_part, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fc_tn_kernel<STAGES>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)fc_tn_kernel<STAGES, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               fc_lds_bytes<STAGES>());
     attr = true;
   }
   const int ti = (I + 127) / 128, tj = (J + 127) / 128, rt = R / 64;
   const int kps = (rt + splits - 1) / splits;
   splits = (rt + kps - 1) / kps;
-  hipLaunchKernelGGL((fc_tn_kernel<STAGES>), dim3(ti * tj * splits), dim3(kFcThreads), fc_lds_bytes<STAGES>(), st,
+  hipLaunchKernelGGL((fc_tn_kernel<STAGES, SP>), dim3(ti * tj * splits), dim3(kFcThreads), fc_lds_bytes<STAGES>(), st,
                      X, Y, part, R, I, J, ti, tj, kps, ones, bias_part);
   return (int)hipGetLastError();
+}
+
+template <int STAGES>
+static int launch_fc_tn(const uint16_t* X, const uint16_t* Y, float* part, int R, int I, int J, int splits,
+                        const uint16_t* ones, float* bias_part, hipStream_t st) {
+  return fc_setprio() ? launch_fc_tn_sp<STAGES, true>(X, Y, part, R, I, J, splits, ones, bias_part, st)
+                      : launch_fc_tn_sp<STAGES, false>(X, Y, part, R, I, J, splits, ones, bias_part, st);
 }
 
 // Transposed bf16 copy: out[c][r] = in[r][c] (the fc weight's [3136][512] shadow for the

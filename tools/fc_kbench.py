@@ -83,9 +83,10 @@ def main():
     res = {}
     for _ in range(int(os.environ.get("FC_ROUNDS", "5"))):
         for v in variants:
-            os.environ["RRL_FC_STAGES"] = v.replace("m", "").replace("b", "")
+            os.environ["RRL_FC_STAGES"] = v.replace("m", "").replace("b", "").replace("p", "")
             os.environ["RRL_FC_MFAST"] = "1" if "m" in v else "0"
             os.environ["RRL_FC_BIG"] = "1" if "b" in v else "0"
+            os.environ["RRL_FC_SETPRIO"] = "1" if "p" in v else "0"
             for k, fn in cases.items():
                 if "old" in k and v != variants[0]:
                     continue
