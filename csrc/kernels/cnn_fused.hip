@@ -1431,6 +1431,38 @@ __global__ __launch_bounds__(c2b::kThreads, 1) void conv2_bwd_kernel(const uint1
       }
       if constexpr (SP == 1 || SP == 4) __builtin_amdgcn_s_setprio(0);
       // D = da1^T: lane (i16, g) holds channels 16 ct + 4g .. + 3 of class pixel p
+      if constexpr (SP == 8 && !STAGED && !GRID12) {
+        // 16-byte stores (A/B): lanes g and g ^ 1 (same pixel row i16) swap halves through
+        // ds_swizzle, so the even lane stores channels 4g .. 4g + 7 of tile u's pixel and the odd
+        // lane those of tile u + 1's pixel -- one 16-byte store instruction per pair of tiles
+        uint2 v[NT];
+        int pix[NT];
+        bool okp[NT];
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          const int p = 16 * (T0 + u) + i16;
+          okp[u] = p < 100;
+          const int pc = okp[u] ? p : 0, a = pc / 10, b = pc - a * 10;
+          const uint2 m = *reinterpret_cast<const uint2*>(P + (cls * kPRows + a * 10 + b) * kPLd + 16 * ct + 4 * g);
+          v[u] = make_uint2(relu_mask2(pk_bf16(acc[u][0], acc[u][1]), m.x), relu_mask2(pk_bf16(acc[u][2], acc[u][3]), m.y));
+          pix[u] = (ph + 2 * a) * 20 + pw + 2 * b;
+        }
+        const bool odd = (g & 1) != 0;
+        const int ch = 16 * ct + 4 * (g & ~1);
+#pragma unroll
+        for (int u = 0; u + 1 < NT; u += 2) {
+          const uint2 send = odd ? v[u] : v[u + 1];
+          const uint32_t rx = (uint32_t)__builtin_amdgcn_ds_swizzle((int)send.x, 0x401F);
+          const uint32_t ry = (uint32_t)__builtin_amdgcn_ds_swizzle((int)send.y, 0x401F);
+          const uint4 o = odd ? make_uint4(rx, ry, v[u + 1].x, v[u + 1].y) : make_uint4(v[u].x, v[u].y, rx, ry);
+          if (odd ? okp[u + 1] : okp[u])
+            *reinterpret_cast<uint4*>(dx + ((size_t)n * 400 + (odd ? pix[u + 1] : pix[u])) * 32 + ch) = o;
+        }
+        if constexpr (NT & 1) {
+          if (okp[NT - 1]) *reinterpret_cast<uint2*>(dx + ((size_t)n * 400 + pix[NT - 1]) * 32 + 16 * ct + 4 * g) = v[NT - 1];
+        }
+        return;
+      }
 #pragma unroll
       for (int u = 0; u < NT; ++u) {
         const int p = 16 * (T0 + u) + i16;
@@ -1753,6 +1785,16 @@ extern "C" int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16
     auto* k = staged == 4 ? conv2_bwd_kernel<false, false, 1>
                           : (staged == 5 ? conv2_bwd_kernel<false, false, 2>
                                          : (staged == 6 ? conv2_bwd_kernel<false, false, 3> : conv2_bwd_kernel<false, false, 4>));
+    hipLaunchKernelGGL(k, dim3(grid), dim3(c2b::kThreads), c2b::kLds, (hipStream_t)stream, dy, w, xact, dx, part,
+                       bias_part, N);
+  } else if (staged == 8) {  // 16-byte da1 stores through lane swaps (A/B)
+    static bool attr8 = false;
+    if (!attr8) {
+      (void)hipFuncSetAttribute((const void*)conv2_bwd_kernel<false, false, 8>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, c2b::kLds);
+      attr8 = true;
+    }
+    auto* k = conv2_bwd_kernel<false, false, 8>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(c2b::kThreads), c2b::kLds, (hipStream_t)stream, dy, w, xact, dx, part,
                        bias_part, N);
   } else if (staged == 1)

@@ -197,7 +197,8 @@ class DeviceNatureCNN:
         assert self.fwd_layout in (0, 16, 32, 48, 64, 65, 68, 72, 73, 80, 96, 112, 128), "RRL_CNN_FWD_LAYOUT"
         # conv2 backward variant (A/B runs): 0 = dgrad over 7 tiles per class, 2 = a 10 x 12 grid
         self.bwd2_variant = int(os.environ.get("RRL_CNN_BWD2_VARIANT", "0"))
-        assert self.bwd2_variant in (0, 2, 3, 4, 5, 6, 7), "RRL_CNN_BWD2_VARIANT: 0, 2, 3 (16 waves), 4-7 (wave priority)"
+        assert self.bwd2_variant in (0, 2, 3, 4, 5, 6, 7, 8), \
+            "RRL_CNN_BWD2_VARIANT: 0, 2, 3 (16 waves), 4-7 (wave priority), 8 (16-byte da1 stores)"
         self.bwd3_variant = int(os.environ.get("RRL_CNN_BWD3_VARIANT", "0"))
         assert self.bwd3_variant in (0, 1, 2, 3, 4, 5), \
             "RRL_CNN_BWD3_VARIANT: 0 (s_setprio clusters), 1 (16 waves), 2 (no s_setprio), 3 (static), 4 / 5 (one cluster)"

@@ -1130,8 +1130,9 @@ def test_conv3_bwd_16wave_is_bitwise_equal(cuda, variant):
         assert torch.isfinite(a.float()).all() and torch.equal(a, b)
 
 
-@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6, 7],
-                         ids=["grid12", "16wave", "setprio", "setprio_static", "setprio_wgrad", "setprio_dgrad"])
+@pytest.mark.parametrize("variant", [2, 3, 4, 5, 6, 7, 8],
+                         ids=["grid12", "16wave", "setprio", "setprio_static", "setprio_wgrad", "setprio_dgrad",
+                              "store16"])
 def test_conv2_bwd_dgrad_grids_are_bitwise_equal(cuda, variant):
     """The conv2 backward's dgrad over the class's 100 pixels in 7 tiles (shipped) against the
     dgrad over a 10 x 12 grid per phase class (variant 2) and the 16-wave kernel with dgrad and

@@ -104,6 +104,7 @@ def main():
         fns["bwd2_sp2"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=5)
         fns["bwd2_sp_w"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=6)
         fns["bwd2_sp_d"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=7)
+        fns["bwd2_st16"] = lambda: h.conv2_bwd(da2, W[2][0], a1, da1, part, bpart, Nb, min(Nb, cus), staged=8)
     # conv3 backward wave priority: bwd3 = the shipped s_setprio-cluster form, bwd3_sp0 = without
     fns["bwd3_sp0"] = lambda: h.conv3_bwd(da3, W[3][0], a2, da2, part, bpart, Nb, min(Nb, cus), variant=2)
     fns["bwd3_sp2"] = lambda: h.conv3_bwd(da3, W[3][0], a2, da2, part, bpart, Nb, min(Nb, cus), variant=3)
