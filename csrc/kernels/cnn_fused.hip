@@ -997,7 +997,7 @@ constexpr int kStage = 512;
 constexpr int kYPT = (c3b::kYC + kStage - 1) / kStage, kXPT = (c3b::kXC + kStage - 1) / kStage;
 }  // namespace c3b16
 
-template <int ROLE>  // 0 = dgrad, 1 = wgrad
+template <int ROLE, int SP = 0>  // 0 = dgrad, 1 = wgrad; SP 1: s_setprio around the MFMA clusters
 __device__ __forceinline__ void conv3_bwd16_role(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ w,
                                                  const uint16_t* __restrict__ xact, uint16_t* __restrict__ dx,
                                                  float* __restrict__ part, float* __restrict__ bias_part, int N,
@@ -1090,6 +1090,7 @@ __device__ __forceinline__ void conv3_bwd16_role(const uint16_t* __restrict__ dy
     const uint16_t* Xi = smem + (j & 1) * kBuf + kX;
     if constexpr (ROLE == 1) {
       // ---- wgrad: 2 position k-steps x (4 co tiles x ntap taps)
+      if constexpr (SP == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const int oh = 4 * s + g;  // this lane group's output row (7 = zero border)
@@ -1106,6 +1107,7 @@ __device__ __forceinline__ void conv3_bwd16_role(const uint16_t* __restrict__ dy
 #pragma unroll
           for (int t = 0; t < NTAP; ++t) wacc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[c], bfr[t], wacc[c][t], 0, 0, 0);
       }
+      if constexpr (SP == 1) __builtin_amdgcn_s_setprio(0);
     } else {
       // ---- dgrad: this wave's 3 pixel tiles, C3B16_MT at a time (k-step outer, tiles inner)
       auto tiles = [&](auto tag) {
@@ -1120,6 +1122,7 @@ __device__ __forceinline__ void conv3_bwd16_role(const uint16_t* __restrict__ dy
           const int ih = pc / 9, iw = pc - ih * 9;
           rb[u] = (ih + 2) * 11 + (iw + 2);
         }
+        if constexpr (SP == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int ks = 0; ks < 18; ++ks) {
           const int t = ks >> 1, kh = t / 3, kw = t - kh * 3;
@@ -1131,6 +1134,7 @@ __device__ __forceinline__ void conv3_bwd16_role(const uint16_t* __restrict__ dy
           for (int u = 0; u < MT; ++u) acc[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], a[u], acc[u], 0, 0, 0);
           if (C3B16_SCHED && (ks % C3B16_SCHED) == C3B16_SCHED - 1) __builtin_amdgcn_sched_barrier(0);  // bound the reads in flight
         }
+        if constexpr (SP == 1) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
         for (int u = 0; u < MT; ++u) {
           const int q = 16 * (3 * half + U0 + u) + i16;
@@ -1175,6 +1179,7 @@ __device__ __forceinline__ void conv3_bwd16_role(const uint16_t* __restrict__ dy
   }
 }
 
+template <int SP = 0>
 __global__ __launch_bounds__(c3b16::kThreads, 1) void conv3_bwd16_kernel(const uint16_t* __restrict__ dy,
                                                                          const uint16_t* __restrict__ w,
                                                                          const uint16_t* __restrict__ xact,
@@ -1184,8 +1189,8 @@ __global__ __launch_bounds__(c3b16::kThreads, 1) void conv3_bwd16_kernel(const u
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (wave < 8) conv3_bwd16_role<0>(dy, w, xact, dx, part, bias_part, N, smem, tid, wave);
-  else conv3_bwd16_role<1>(dy, w, xact, dx, part, bias_part, N, smem, tid, wave);
+  if (wave < 8) conv3_bwd16_role<0, SP>(dy, w, xact, dx, part, bias_part, N, smem, tid, wave);
+  else conv3_bwd16_role<1, SP>(dy, w, xact, dx, part, bias_part, N, smem, tid, wave);
 }
 
 // variant 1: the 16-wave kernel
@@ -1196,13 +1201,14 @@ extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16
     (void)hipFuncSetAttribute((const void*)conv3_bwd_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
     (void)hipFuncSetAttribute((const void*)conv3_bwd_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
     (void)hipFuncSetAttribute((const void*)conv3_bwd_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
-    (void)hipFuncSetAttribute((const void*)conv3_bwd16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
+    (void)hipFuncSetAttribute((const void*)conv3_bwd16_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
+    (void)hipFuncSetAttribute((const void*)conv3_bwd16_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, c3b::kLds);
     attr = true;
   }
   if (N < 1 || grid < 1) return 0;
-  if (variant == 1) {
-    hipLaunchKernelGGL(conv3_bwd16_kernel, dim3(grid), dim3(c3b16::kThreads), c3b::kLds, (hipStream_t)stream, dy, w,
-                       xact, dx, part, bias_part, N);
+  if (variant == 1 || variant == 6) {  // the 16-wave kernel (6: with s_setprio around its MFMA clusters)
+    hipLaunchKernelGGL(variant == 6 ? conv3_bwd16_kernel<1> : conv3_bwd16_kernel<0>, dim3(grid), dim3(c3b16::kThreads),
+                       c3b::kLds, (hipStream_t)stream, dy, w, xact, dx, part, bias_part, N);
     return (int)hipGetLastError();
   }
   // variant 0 (default): s_setprio 1 around the MFMA clusters (SP 1): 163.6 -> 144.7 us per

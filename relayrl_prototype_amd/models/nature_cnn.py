@@ -200,7 +200,7 @@ class DeviceNatureCNN:
         assert self.bwd2_variant in (0, 2, 3, 4, 5, 6, 7, 8), \
             "RRL_CNN_BWD2_VARIANT: 0, 2, 3 (16 waves), 4-7 (wave priority), 8 (16-byte da1 stores)"
         self.bwd3_variant = int(os.environ.get("RRL_CNN_BWD3_VARIANT", "0"))
-        assert self.bwd3_variant in (0, 1, 2, 3, 4, 5), \
+        assert self.bwd3_variant in (0, 1, 2, 3, 4, 5, 6), \
             "RRL_CNN_BWD3_VARIANT: 0 (s_setprio clusters), 1 (16 waves), 2 (no s_setprio), 3 (static), 4 / 5 (one cluster)"
         # conv2 backward + conv1 weight gradient in C row chunks, each chunk's da1 read back by
         # conv1_wgrad8 right after conv2_bwd wrote it (RRL_CNN_BWD21_CHUNKS, for A/B runs: a half

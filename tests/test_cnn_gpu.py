@@ -1103,8 +1103,8 @@ def test_fused_conv_stack_without_stored_activations(cuda, variant):
     assert torch.isnan(outs[1][0].float()).all() and torch.isnan(outs[1][1].float()).all()
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5],
-                         ids=["16wave", "no_setprio", "setprio_static", "setprio_wgrad", "setprio_dgrad"])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6],
+                         ids=["16wave", "no_setprio", "setprio_static", "setprio_wgrad", "setprio_dgrad", "16wave_setprio"])
 def test_conv3_bwd_16wave_is_bitwise_equal(cuda, variant):
     """The 16-wave conv3 backward (dgrad and wgrad on separate waves) runs the 8-wave kernel's
     k-order per output: da2, the weight and the bias partials bitwise equal; so do the other

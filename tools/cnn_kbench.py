@@ -110,6 +110,7 @@ def main():
     fns["bwd3_sp2"] = lambda: h.conv3_bwd(da3, W[3][0], a2, da2, part, bpart, Nb, min(Nb, cus), variant=3)
     fns["bwd3_sp_w"] = lambda: h.conv3_bwd(da3, W[3][0], a2, da2, part, bpart, Nb, min(Nb, cus), variant=4)
     fns["bwd3_sp_d"] = lambda: h.conv3_bwd(da3, W[3][0], a2, da2, part, bpart, Nb, min(Nb, cus), variant=5)
+    fns["bwd3_16_sp"] = lambda: h.conv3_bwd(da3, W[3][0], a2, da2, part, bpart, Nb, min(Nb, cus), variant=6)
 
     # --rounds R: the list R times, every other round in reverse order (the first kernel timed
     # in a process reads slow), median per kernel
