@@ -284,11 +284,14 @@ class DeviceNatureCNN:
         # forked before the fc data gradient (the two fc GEMMs share the chip); "late" = the
         # same work forked after it (beside conv3_bwd); "sums" = both fc GEMMs back to back on
         # the main stream and only the memory-light head gradient + split sums forked beside
-        # conv3_bwd
-        self.side_mode = os.environ.get("RRL_CNN_SIDE_MODE", "early")
+        # conv3_bwd; "early_main" (default) = "early" with the side work captured AFTER the fc data
+        # gradient: same graph edges, but the replay now dispatches the main branch's kernel
+        # first (fork gap on the main stream 14 -> 6 us, join 10 -> 6 us; Pong +2.3 % at 2,048
+        # envs, +-0 at 8,192: profiles/r5_pong_side_early_main_ab.txt)
+        self.side_mode = os.environ.get("RRL_CNN_SIDE_MODE", "early_main")
         if os.environ.get("RRL_CNN_SIDE_LATE", "0") == "1":
             self.side_mode = "late"
-        assert self.side_mode in ("early", "late", "sums"), self.side_mode
+        assert self.side_mode in ("early", "early_main", "late", "sums"), self.side_mode
         self._ev_fork = torch.cuda.Event()
         self._ev_join = torch.cuda.Event()
         self._ev_c3, self._ev_c3_done = torch.cuda.Event(), torch.cuda.Event()
@@ -514,11 +517,12 @@ class DeviceNatureCNN:
                 self._wgrad("fc", dh, a3, B, 1, FC_IN, 1, 1, HIDDEN, o["wfc"])
                 self._bias(dh, B, HIDDEN, o["bfc"])
 
-        def fork_weight_grads():
+        def fork_weight_grads(recorded=False):
             if side is None:
                 weight_grads()
                 return
-            self._ev_fork.record()
+            if not recorded:
+                self._ev_fork.record()
             side.wait_event(self._ev_fork)
             with torch.cuda.stream(side):
                 weight_grads()
@@ -551,6 +555,8 @@ class DeviceNatureCNN:
         sums_mode = mode == "sums" and self.fc_nt and B % 64 == 0 and self.fc_tn_bias
         if mode == "early" or (mode == "sums" and not sums_mode):
             fork_weight_grads()
+        elif mode == "early_main":
+            self._ev_fork.record()
         da3 = self.da3[:B * FC_IN]
         if self.fc_nt:
             self._wfc_t_ready()
@@ -561,6 +567,8 @@ class DeviceNatureCNN:
             fc_tn()
         if mode == "late" or sums_mode:
             fork_weight_grads()
+        elif mode == "early_main":
+            fork_weight_grads(recorded=True)
         if comm is not None and comm.multi:
             import torch.distributed as dist
 

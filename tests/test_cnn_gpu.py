@@ -807,7 +807,8 @@ def test_pixel_update_side_stream_is_race_free(cuda, monkeypatch):
     cfg = dict(num_envs=64, rollout_len=4, seed=5)
     runs = []
     for side, mode, defer, csums in (("0", "early", "0", "1"), ("1", "early", "0", "1"), ("1", "late", "0", "1"),
-                                     ("1", "sums", "0", "1"), ("1", "early", "1", "1"), ("1", "early", "0", "0")):
+                                     ("1", "sums", "0", "1"), ("1", "early", "1", "1"), ("1", "early", "0", "0"),
+                                     ("1", "early_main", "0", "1")):
         monkeypatch.setenv("RRL_CNN_SIDE", side)
         monkeypatch.setenv("RRL_CNN_SIDE_MODE", mode)
         monkeypatch.setenv("RRL_CNN_DEFER_TRANSPOSE", defer)
