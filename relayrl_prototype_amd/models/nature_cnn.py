@@ -298,6 +298,9 @@ class DeviceNatureCNN:
         self._ev_c2, self._ev_c2_done = torch.cuda.Event(), torch.cuda.Event()
         # RRL_CNN_SIDE_CONV_SUMS=1 (off): see backward(); ABBA -0.0 / -0.4 % at 2,048 / 8,192 envs
         self.side_conv_sums = os.environ.get("RRL_CNN_SIDE_CONV_SUMS", "0") == "1"
+        # RRL_CNN_SIDE_FC_FIRST=1: the side stream runs the fc weight GEMM before the head gradient
+        # (the GEMM then overlaps the fc data gradient more: -2.3 % at 2,048 / 8,192 envs)
+        self.side_fc_first = os.environ.get("RRL_CNN_SIDE_FC_FIRST", "0") == "1"
         self._ev_t_fork = torch.cuda.Event()
         self._ev_t_join = torch.cuda.Event()
         self._wfc_t_stale = self._wfc_t_pending = False
@@ -499,10 +502,18 @@ class DeviceNatureCNN:
             fc_tn_used.append(int(h.fc_tn_part(dh, a3, self.part, B, HIDDEN, FC_IN, self.FC_WGRAD_SPLITS,
                                                ones=self._ones8, bias_part=self._fc_bias_part)))
 
-        def weight_grads():  # head + fc weight / bias gradients
+        def head_grads():
             h.head_wgrad(hid, dhead, B, self.A, hp, nb)
             h.sum_splits(hp, nb, self.spec.head_size, g[o["head"]:o["P"]])
-            # fc
+
+        def weight_grads():  # head + fc weight / bias gradients
+            if not self.side_fc_first:
+                head_grads()
+            fc_grads()
+            if self.side_fc_first:
+                head_grads()
+
+        def fc_grads():
             if self.fc_nt and B % 64 == 0 and self.fc_tn_bias:
                 if not fc_tn_used:  # side mode "sums" ran the GEMM on the main stream already
                     fc_tn()

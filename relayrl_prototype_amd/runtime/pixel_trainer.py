@@ -232,6 +232,8 @@ class PixelA2CTrainer:
             par = self._par
             if self._graphable() and par in self._graphs:
                 g, stats = self._graphs[par]
+                # (replayed on a high-priority stream instead: -52 % at 2,048 envs, -30 % at 8,192,
+                # profiles/r5_pong_side_early_main_ab.txt)
                 g.replay()
             elif self._graphable() and self._warm:
                 # capture once per buffer parity (kernel attributes / workspaces were set up by the

@@ -9,8 +9,10 @@ tail -2 gpurun_out/r5ai_tests.log
 rm -f gpurun_out/r5ai_pong.jsonl
 cfg() {
   case $1 in
-    A) echo "RRL_CNN_SIDE_MODE=early" ;;
+    A) echo "RRL_CNN_SIDE_MODE=${A_MODE:-early}" ;;
     M) echo "RRL_CNN_SIDE_MODE=early_main" ;;
+    F) echo "RRL_CNN_SIDE_FC_FIRST=1" ;;
+    P) echo "RRL_PIXEL_REPLAY_PRIO=1" ;;
   esac
 }
 RUNS=${RUNS:-"2048 A|2048 M|2048 M|2048 A|2048 A|2048 M|8192 A|8192 M|8192 M|8192 A|8192 A|8192 M"}
