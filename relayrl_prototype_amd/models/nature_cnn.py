@@ -288,10 +288,11 @@ class DeviceNatureCNN:
         # gradient: same graph edges, but the replay now dispatches the main branch's kernel
         # first (fork gap on the main stream 14 -> 6 us, join 10 -> 6 us; Pong +2.3 % at 2,048
         # envs, +-0 at 8,192: profiles/r5_pong_side_early_main_ab.txt)
+        # "c3" = the side work forked after the conv3 backward (beside conv2 / conv1)
         self.side_mode = os.environ.get("RRL_CNN_SIDE_MODE", "early_main")
         if os.environ.get("RRL_CNN_SIDE_LATE", "0") == "1":
             self.side_mode = "late"
-        assert self.side_mode in ("early", "early_main", "late", "sums"), self.side_mode
+        assert self.side_mode in ("early", "early_main", "late", "sums", "c3"), self.side_mode
         self._ev_fork = torch.cuda.Event()
         self._ev_join = torch.cuda.Event()
         self._ev_c3, self._ev_c3_done = torch.cuda.Event(), torch.cuda.Event()
@@ -538,6 +539,7 @@ class DeviceNatureCNN:
             with torch.cuda.stream(side):
                 weight_grads()
                 self._ev_join.record(side)
+            side_last[0] = self._ev_join  # (mode "c3" forks after the conv slab sums' forks)
 
         # side mode "late": fork after the fc data gradient instead, so the side work runs
         # beside the latency-bound conv3 backward rather than the 2,000-workgroup fc GEMM -- +0.5 %
@@ -601,6 +603,8 @@ class DeviceNatureCNN:
             self._wgrad("c3", da3, a2, B, L3.hin, L3.cin, L3.k, L3.s, L3.cout, o["w3"])
             self._bias(da3, B * L3.hout ** 2, L3.cout, o["b3"])
             self._dgrad(da3, sh[o["w3"]:o["b3"]], a2, da2, B, L3)
+        if mode == "c3":
+            self._ev_fork.record()
         # conv2
         da1 = self.da1[:B * L1.hout ** 2 * L1.cout]
         c1_slabs = None
@@ -640,6 +644,8 @@ class DeviceNatureCNN:
             self._wgrad("c2", da2, a1, B, L2.hin, L2.cin, L2.k, L2.s, L2.cout, o["w2"])
             self._bias(da2, B * L2.hout ** 2, L2.cout, o["b2"])
             self._dgrad(da2, sh[o["w2"]:o["b2"]], a1, da1, B, L2)
+        if mode == "c3":  # captured after conv2's kernels: the replay dispatches them first
+            fork_weight_grads(recorded=True)
         # conv1 (input = frames, no data gradient)
         # (its bias gradient comes out of the same pass over da1)
         if self.fused_convs:

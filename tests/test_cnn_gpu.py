@@ -808,7 +808,8 @@ def test_pixel_update_side_stream_is_race_free(cuda, monkeypatch):
     runs = []
     for side, mode, defer, csums in (("0", "early", "0", "1"), ("1", "early", "0", "1"), ("1", "late", "0", "1"),
                                      ("1", "sums", "0", "1"), ("1", "early", "1", "1"), ("1", "early", "0", "0"),
-                                     ("1", "early_main", "0", "1"), ("1", "early_fc", "0", "1")):
+                                     ("1", "early_main", "0", "1"), ("1", "early_fc", "0", "1"),
+                                     ("1", "c3", "0", "1")):
         monkeypatch.setenv("RRL_CNN_SIDE_FC_FIRST", "1" if mode == "early_fc" else "0")
         mode = "early_main" if mode == "early_fc" else mode
         monkeypatch.setenv("RRL_CNN_SIDE", side)

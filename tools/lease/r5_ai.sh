@@ -12,6 +12,7 @@ cfg() {
     A) echo "RRL_CNN_SIDE_MODE=${A_MODE:-early}" ;;
     M) echo "RRL_CNN_SIDE_MODE=early_main" ;;
     F) echo "RRL_CNN_SIDE_FC_FIRST=1" ;;
+    C) echo "RRL_CNN_SIDE_MODE=c3" ;;
     P) echo "RRL_PIXEL_REPLAY_PRIO=1" ;;
   esac
 }
@@ -32,6 +33,6 @@ for k,v in sorted(agg.items()): print(k, v)
 PY
 [ -n "$SKIP_PROF" ] && exit 0
 mkdir -p gpurun_out/prof_early_main
-export TMPDIR=/tmp RRL_CNN_SIDE_MODE=early_main
+export TMPDIR=/tmp RRL_CNN_SIDE_MODE=${PROF_MODE:-early_main}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_early_main -o run -- \
   python3 benchmarks/pong_a2c_bench.py --num-envs 2048 --steps 10 --warmup 3 > gpurun_out/prof_early_main/log.txt 2>&1 || exit $?
