@@ -593,9 +593,36 @@ __global__ void __launch_bounds__(256) a2c_head_kernel(HeadArgs a) {
   }
   const float bv = a.b_v[0];
   float st_pg = 0.f, st_vf = 0.f, st_ent = 0.f, st_n = 0.f;
-  for (int row = blockIdx.x * 4 + wave; row < a.B; row += gridDim.x * 4) {
+  // TRAIN: the next row's inputs are loaded before this row's math (one row-load latency per
+  // wave instead of one per row; the backward runs ~4 rows per wave)
+  const int rstride = gridDim.x * 4;
+  uint4 hv_n = make_uint4(0u, 0u, 0u, 0u);
+  int act_n = 0;
+  float adv_n = 0.f, ret_n = 0.f;
+  if (TRAIN && blockIdx.x * 4 + wave < a.B) {
+    const int r0 = blockIdx.x * 4 + wave;
+    hv_n = *reinterpret_cast<const uint4*>(a.h + (size_t)r0 * F + 8 * lane);
+    act_n = a.act_in[r0];
+    adv_n = a.adv[r0];
+    ret_n = a.ret[r0];
+  }
+  for (int row = blockIdx.x * 4 + wave; row < a.B; row += rstride) {
     uint4 hv;
-    if (!TRAIN && a.part) {
+    int act_c = 0;
+    float adv_c = 0.f, ret_c = 0.f;
+    if (TRAIN) {
+      hv = hv_n;
+      act_c = act_n;
+      adv_c = adv_n;
+      ret_c = ret_n;
+      const int nr = row + rstride;
+      if (nr < a.B) {
+        hv_n = *reinterpret_cast<const uint4*>(a.h + (size_t)nr * F + 8 * lane);
+        act_n = a.act_in[nr];
+        adv_n = a.adv[nr];
+        ret_n = a.ret[nr];
+      }
+    } else if (a.part) {
       // split-K reduction + bias + ReLU + bf16 rounding (the order bias_act_kernel uses)
       const float4 b0 = *reinterpret_cast<const float4*>(a.fc_b + 8 * lane);
       const float4 b1 = *reinterpret_cast<const float4*>(a.fc_b + 8 * lane + 4);
@@ -653,8 +680,8 @@ __global__ void __launch_bounds__(256) a2c_head_kernel(HeadArgs a) {
           for (int o = 0; o < A; ++o) a.logits_out[(size_t)row * A + o] = logits[o];
       }
     } else {
-      const int act = a.act_in[row];
-      const float adv = a.adv[row], ret = a.ret[row];
+      const int act = act_c;
+      const float adv = adv_c, ret = ret_c;
       const float lp = pick_logit(A, logits, act) - cs.lse;
       // d/dz of  -adv*logp(a) - ent_coef*H  (mean over B), d/dv of vf_coef*(v-ret)^2
       float dz[kMaxAct];
@@ -1381,6 +1408,129 @@ static int grid_for(size_t n, int per_block = 256, int cap = 4096) {
   return (int)g;
 }
 
+// Rollout head with the weights streamed from L1 / L2 per row (a2c_rollout_row_streamed,
+// bitwise the a2c_head_kernel<false> result) instead of held in 80 registers: 79 VGPRs, 6 waves
+// per SIMD instead of a2c_head_kernel's 3 (139 VGPRs) -- the rollout head from 4,096 rows.
+template <int AMAX>
+__global__ void __launch_bounds__(256) a2c_head_streamed_kernel(HeadArgs a) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int row = blockIdx.x * 4 + wave; row < a.B; row += gridDim.x * 4)
+    (void)a2c_rollout_row_streamed<AMAX>(a, row, lane);
+}
+
+// The head backward with the same streamed weights (float4 pairs re-read per row from L1 for
+// the logits and again for dh, 107 VGPRs instead of 160): bitwise the a2c_head_kernel<true>
+// result (same products, same order), 4 waves per SIMD instead of 3 -- and slower (the L1
+// re-reads cost more than the waves gain), so opt-in: RRL_HEAD_STREAMED=1.
+template <int AMAX>
+__global__ void __launch_bounds__(256) a2c_head_train_streamed_kernel(HeadArgs a) {
+  __shared__ float red[16];
+  const int A = a.A, F = kHeadF;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float st_pg = 0.f, st_vf = 0.f, st_ent = 0.f, st_n = 0.f;
+  for (int row = blockIdx.x * 4 + wave; row < a.B; row += gridDim.x * 4) {
+    const uint4 hv = *reinterpret_cast<const uint4*>(a.h + (size_t)row * F + 8 * lane);
+    const int act = a.act_in[row];
+    const float adv = a.adv[row], ret = a.ret[row];
+    const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w};
+    float x[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      x[2 * i] = bf2f((uint16_t)(hw[i] & 0xffff));
+      x[2 * i + 1] = bf2f((uint16_t)(hw[i] >> 16));
+    }
+    float logits[kMaxAct];
+#pragma unroll
+    for (int o = 0; o < kMaxAct; ++o) logits[o] = -INFINITY;
+    float wv[8];
+    {
+      const float4 v0 = *reinterpret_cast<const float4*>(a.w_v + 8 * lane);
+      const float4 v1 = *reinterpret_cast<const float4*>(a.w_v + 8 * lane + 4);
+      wv[0] = v0.x; wv[1] = v0.y; wv[2] = v0.z; wv[3] = v0.w; wv[4] = v1.x; wv[5] = v1.y; wv[6] = v1.z; wv[7] = v1.w;
+    }
+    float vsum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) vsum += wv[i] * x[i];
+    const float value = wave_sum(vsum) + a.b_v[0];
+#pragma unroll
+    for (int o = 0; o < AMAX; ++o) {
+      if (o < A) {
+        const float4 w0 = *reinterpret_cast<const float4*>(a.w + o * F + 8 * lane);
+        const float4 w1 = *reinterpret_cast<const float4*>(a.w + o * F + 8 * lane + 4);
+        const float wp[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += wp[i] * x[i];
+        logits[o] = wave_sum(s) + a.bias[o];
+      }
+    }
+    const CatStats cs = cat_stats(A, logits);
+    const float lp = pick_logit(A, logits, act) - cs.lse;
+    float dz[kMaxAct];
+#pragma unroll
+    for (int o = 0; o < kMaxAct; ++o) {
+      dz[o] = 0.f;
+      if (o < A) {
+        const float lpo = logits[o] - cs.lse;
+        const float p = __expf(lpo);
+        dz[o] = a.inv_B * (-adv * ((o == act ? 1.f : 0.f) - p) + a.ent_coef * p * (lpo + cs.entropy));
+      }
+    }
+    const float dv = a.inv_B * 2.f * a.vf_coef * (value - ret);
+    float g[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g[i] = dv * wv[i];
+#pragma unroll
+    for (int o = 0; o < AMAX; ++o)
+      if (o < A) {
+        const float4 w0 = *reinterpret_cast<const float4*>(a.w + o * F + 8 * lane);
+        const float4 w1 = *reinterpret_cast<const float4*>(a.w + o * F + 8 * lane + 4);
+        const float wp[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) g[i] += dz[o] * wp[i];
+      }
+    uint32_t ow[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float lo = x[2 * i] > 0.f ? g[2 * i] : 0.f, hi = x[2 * i + 1] > 0.f ? g[2 * i + 1] : 0.f;
+      ow[i] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    }
+    *reinterpret_cast<uint4*>(a.dh + (size_t)row * F + 8 * lane) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    float mine = dv;
+#pragma unroll
+    for (int o = 0; o < kMaxAct; ++o)
+      if (o < A && lane == o) mine = dz[o];
+    if (lane <= A) a.dhead[(size_t)row * (A + 1) + lane] = mine;
+    if (lane == 0) {
+      st_pg += -adv * lp;
+      st_vf += (value - ret) * (value - ret);
+      st_ent += cs.entropy;
+      st_n += 1.f;
+    }
+  }
+  if (lane == 0) {
+    red[wave * 4 + 0] = st_pg;
+    red[wave * 4 + 1] = st_vf;
+    red[wave * 4 + 2] = st_ent;
+    red[wave * 4 + 3] = st_n;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4)
+    a.stats[blockIdx.x * 4 + threadIdx.x] = red[threadIdx.x] + red[4 + threadIdx.x] + red[8 + threadIdx.x] +
+                                            red[12 + threadIdx.x];
+}
+
+// RRL_HEAD_STREAMED (read per call): unset = the streamed rollout head from 4,096 rows (20.0 vs
+// 24.5 us per 8,192 rows; 11.1 vs 10.7 us at 2,048) and the register backward; 1 = both
+// streamed (the backward measured slower: 80.6 vs 68.3 us at 40,960 rows, 28.6 vs 24.2 at
+// 10,240 -- profiles/r5_head_streamed_ab.txt); 0 = neither.
+static bool head_streamed(bool train, int B) {
+  const char* e = getenv("RRL_HEAD_STREAMED");
+  if (e && e[0] == '1') return true;
+  if (e && e[0] == '0') return false;
+  return !train && B >= 4096;
+}
+
 extern "C" {
 
 // Forward conv (or fc as a 1x1 conv on H = W = 1): y bf16 [N*OH*OW][Cout].  When the
@@ -1686,6 +1836,16 @@ int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, i
   a.dh = dh;
   a.dhead = dhead;
   a.stats = stats;
+  if (A <= 8 && head_streamed(mode != 0, B)) {
+    if (mode == 0 && part && !logits_out) {
+      hipLaunchKernelGGL((a2c_head_streamed_kernel<8>), dim3(grid), dim3(256), 0, st, a);
+      return (int)hipGetLastError();
+    }
+    if (mode != 0) {
+      hipLaunchKernelGGL((a2c_head_train_streamed_kernel<8>), dim3(grid), dim3(256), 0, st, a);
+      return (int)hipGetLastError();
+    }
+  }
   if (A <= 8) {
     if (mode == 0) hipLaunchKernelGGL((a2c_head_kernel<false, 8>), dim3(grid), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((a2c_head_kernel<true, 8>), dim3(grid), dim3(256), 0, st, a);

@@ -27,6 +27,10 @@ from typing import Dict, Optional
 import torch
 import torch.nn.functional as F
 
+# RRL_HEAD_GRID_CAP: workgroup cap of the rollout head launch (4 rows per workgroup, so rows
+# past 4 x cap run 2+ rows per wave)
+_HEAD_GRID_CAP = max(1, int(os.environ.get("RRL_HEAD_GRID_CAP", "1024")))
+
 FRAME_HW = 84
 FRAMES = 4
 HIDDEN = 512
@@ -355,7 +359,7 @@ class DeviceNatureCNN:
     def _head_grid(n: int) -> int:
         """Workgroups of the rollout head launch: one row per wave, 4 waves each (2 or 4 rows per
         wave measured 1.5 / 5 % slower per update: profiles/r4_head_rows_ab.txt)."""
-        return max(1, min(1024, (n + 3) // 4))
+        return max(1, min(_HEAD_GRID_CAP, (n + 3) // 4))
 
     def _fc_head(self, a3, hid, n, **head):
         """fc GEMM as split-K partials, then ONE head launch: bias + ReLU + bf16 hid (stored for

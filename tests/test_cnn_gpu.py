@@ -185,9 +185,9 @@ def test_fc_dgrad_masked(cuda):
     assert relerr(out, ((dh @ w) * (a3 > 0)).reshape(-1)) < 1e-2
 
 
-def test_full_model_forward_backward_matches_autograd(cuda):
+@pytest.mark.parametrize("B", [48, 50])  # 3-4 rows per wave in the head backward (next-row prefetch, tail)
+def test_full_model_forward_backward_matches_autograd(cuda, B):
     spec = CNNSpec(6)
-    B = 48
     params = spec.init(4)
     # larger head weights so the policy gradient is not negligible next to the value part
     o = spec.offsets()
@@ -920,6 +920,46 @@ def test_fused_head_step_equals_head_then_step(cuda, N):
         for a, b in zip(*outs):
             assert torch.equal(a, b)
         assert torch.equal(obs[0], obs[1])
+
+
+@pytest.mark.parametrize("N", [37, 5000])
+def test_streamed_rollout_head_is_bitwise_equal(cuda, N, monkeypatch):
+    """a2c_head_streamed_kernel (RRL_HEAD_STREAMED=1: weights read per row, 79 VGPRs) gives
+    the register-resident head's actions, log-probs, values and stored hidden units bitwise;
+    N = 5000 runs 2 rows per wave on part of the grid (grid cap 1024).  Its backward twin
+    gives the same gradients, dh and loss stats."""
+    spec = CNNSpec(6)
+    m = DeviceNatureCNN(spec, cuda, max_batch=N, seed=5)
+    g = torch.Generator().manual_seed(3)
+    obs = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g).to(cuda)
+    sample_t = torch.full((1,), 7, dtype=torch.int64, device=cuda)
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("RRL_HEAD_STREAMED", flag)
+        act = torch.full((N,), -1, dtype=torch.int32, device=cuda)
+        logp = torch.full((N,), float("nan"), device=cuda)
+        val = torch.full((N,), float("nan"), device=cuda)
+        m.hid.zero_()
+        m.act(obs, 0, act, logp, val, 123, 4, step_base=sample_t)
+        torch.cuda.synchronize()
+        outs.append((act.clone(), logp.clone(), val.clone(), m.hid[:N * 512].clone()))
+    assert (outs[0][0] >= 0).all()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    # the streamed head backward (a2c_head_train_streamed_kernel): same gradients and loss stats
+    act = outs[0][0]
+    adv = torch.randn(N, generator=g).to(cuda)
+    ret = torch.randn(N, generator=g).to(cuda)
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("RRL_HEAD_STREAMED", flag)
+        m.forward(obs, 0)
+        stats = m.backward(obs, act, adv, ret, 0.5, 0.01)
+        torch.cuda.synchronize()
+        res.append((m.grad.clone(), stats.clone(), m.dh[:N * 512].clone()))
+    assert res[0][1][:, 3].sum().item() == N
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
 
 
 def test_fused_render_draws_the_env_observation(cuda):
