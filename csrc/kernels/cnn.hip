@@ -1520,6 +1520,175 @@ __global__ void __launch_bounds__(256) a2c_head_train_streamed_kernel(HeadArgs a
                                             red[12 + threadIdx.x];
 }
 
+// The head backward on fp32 MFMA (v_mfma_f32_16x16x4_f32: exact f32 products): one wave per
+// 16-row tile.  The register kernel above spends its time in 7 wave-wide reductions and
+// ~400 VALU ops per row; here
+//   (1) logits + value of 16 rows = hid[16 x 512] . [W; w_v]^T    (128 MFMAs, 4 accumulators),
+//       hid staged in LDS (16 x 1,040 B rows), [W; w_v] once per workgroup (16 KiB);
+//   (2) 16 lanes (one per row) form the softmax, the loss gradients dz / dv and the stats;
+//   (3) dh[16 x 512] = [dz | dv][16 x 8] . [W; w_v]   (32 column tiles x 2 MFMAs), masked by
+//       hid > 0 and rounded to bf16 IN PLACE of the hid tile, which then leaves as 16-B rows.
+// Same math as a2c_head_kernel<true>; the sums run in another order (fp32-accurate, not
+// bitwise).  A <= 7 (A + 1 outputs in one 8-wide k block).
+constexpr int kHmRow = 520;                       // hid / dh tile row stride, bf16 elements (1,040 B)
+constexpr int kHmWave = 16 * kHmRow * 2 + 16 * 17 * 4 + 16 * 8 * 4;  // 18,240 B of LDS per wave
+constexpr int kHmW = 8 * kHeadF * 4;  // [W; w_v; 0] as f32 rows, 16 KiB per workgroup
+__global__ void __launch_bounds__(256) a2c_head_train_mfma_kernel(HeadArgs a, int stats_rows) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char hm_smem[];
+  const int A = a.A, F = kHeadF, B = a.B;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* Wl = reinterpret_cast<float*>(hm_smem);  // row o < A: W[o]; o == A: w_v; else zeros
+  uint16_t* H = reinterpret_cast<uint16_t*>(hm_smem + kHmW + wave * kHmWave);
+  float* Lg = reinterpret_cast<float*>(hm_smem + kHmW + wave * kHmWave + 16 * kHmRow * 2);
+  float* G = Lg + 16 * 17;
+  const int li = lane & 15, q = lane >> 4;
+  for (int i = threadIdx.x; i < 8 * F / 4; i += 256) {
+    const int o = i / (F / 4), c = i % (F / 4);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (o < A) v = *reinterpret_cast<const float4*>(a.w + o * F + 4 * c);
+    else if (o == A) v = *reinterpret_cast<const float4*>(a.w_v + 4 * c);
+    *reinterpret_cast<float4*>(Wl + o * F + 4 * c) = v;
+  }
+  __syncthreads();
+  // this lane's weight row for the B operand of (1): output j = li (rows 8..15 are zero outputs)
+  const float* wrow = li < 8 ? Wl + li * F : nullptr;
+  float st_pg = 0.f, st_vf = 0.f, st_ent = 0.f, st_n = 0.f;
+  const int ntiles = (B + 15) >> 4;
+  for (int tile = blockIdx.x * 4 + wave; tile < ntiles; tile += gridDim.x * 4) {
+    const int row0 = tile * 16;
+    // stage hid rows row0 .. row0 + 15 (rows past B: a clamped duplicate, never stored)
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int c = lane + 64 * t, r = c >> 6, c16 = c & 63;
+      const int gr = min(row0 + r, B - 1);
+      *reinterpret_cast<uint4*>(H + r * kHmRow + c16 * 8) =
+          *reinterpret_cast<const uint4*>(a.h + (size_t)gr * F + c16 * 8);
+    }
+    // per-row inputs for (2), loaded early
+    int act = 0;
+    float adv = 0.f, ret = 0.f;
+    const int myrow = row0 + li;
+    if (lane < 16 && myrow < B) {
+      act = a.act_in[myrow];
+      adv = a.adv[myrow];
+      ret = a.ret[myrow];
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // (1): lane (li, q) covers k = 128 q .. 128 q + 127 of row li (A operand) and of output li (B)
+    f32x4_t acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc[u] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    const uint16_t* hr = H + li * kHmRow + 128 * q;
+#pragma unroll 2
+    for (int s8 = 0; s8 < 16; ++s8) {
+      const uint4 hv = *reinterpret_cast<const uint4*>(hr + 8 * s8);
+      float4 w0 = make_float4(0.f, 0.f, 0.f, 0.f), w1 = w0;
+      if (wrow) {
+        w0 = *reinterpret_cast<const float4*>(wrow + 128 * q + 8 * s8);
+        w1 = *reinterpret_cast<const float4*>(wrow + 128 * q + 8 * s8 + 4);
+      }
+      const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w};
+      const float wk[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xv = bf2f((uint16_t)(e & 1 ? hw[e >> 1] >> 16 : hw[e >> 1] & 0xffff));
+        acc[e & 3] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv, wk[e], acc[e & 3], 0, 0, 0);
+      }
+    }
+    // D[row = 4 q + r][out = li]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Lg[(4 * q + r) * 17 + li] = (acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // (2): lane li < 16 owns row row0 + li
+    if (lane < 16) {
+      float gz[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (myrow < B) {
+        float logits[kMaxAct];
+#pragma unroll
+        for (int o = 0; o < kMaxAct; ++o) logits[o] = o < A ? Lg[li * 17 + o] + a.bias[o] : -INFINITY;
+        const float value = Lg[li * 17 + A] + a.b_v[0];
+        const CatStats cs = cat_stats(A, logits);
+        const float lp = pick_logit(A, logits, act) - cs.lse;
+#pragma unroll
+        for (int o = 0; o < 8; ++o)
+          if (o < A) {
+            const float lpo = logits[o] - cs.lse;
+            const float p = __expf(lpo);
+            gz[o] = a.inv_B * (-adv * ((o == act ? 1.f : 0.f) - p) + a.ent_coef * p * (lpo + cs.entropy));
+          }
+        const float dv = a.inv_B * 2.f * a.vf_coef * (value - ret);
+#pragma unroll
+        for (int o = 0; o < 8; ++o)
+          if (o == A) gz[o] = dv;
+#pragma unroll
+        for (int o = 0; o < 8; ++o)
+          if (o <= A) a.dhead[(size_t)myrow * (A + 1) + o] = gz[o];
+        st_pg += -adv * lp;
+        st_vf += (value - ret) * (value - ret);
+        st_ent += cs.entropy;
+        st_n += 1.f;
+      }
+#pragma unroll
+      for (int o = 0; o < 8; ++o) G[li * 8 + o] = gz[o];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // (3): A operand G[row li][o = q | 4 + q], B operand [W; w_v][o][k = 16 kt + li]
+    const float g0 = G[li * 8 + q], g1 = G[li * 8 + 4 + q];
+    const float* b0row = Wl + q * F;
+    const float* b1row = Wl + (4 + q) * F;
+#pragma unroll 4
+    for (int kt = 0; kt < 32; ++kt) {
+      const int k = 16 * kt + li;
+      const float b0 = b0row[k], b1 = b1row[k];
+      f32x4_t d = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      d = __builtin_amdgcn_mfma_f32_16x16x4f32(g0, b0, d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x4f32(g1, b1, d, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // D[row = 4 q + r][k]: keep where hid > 0, bf16, in place
+        uint16_t* p = H + (4 * q + r) * kHmRow + k;
+        const float xv = bf2f(*p);
+        *p = f2bf(xv > 0.f ? d[r] : 0.f);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int c = lane + 64 * t, r = c >> 6, c16 = c & 63;
+      if (row0 + r < B)
+        *reinterpret_cast<uint4*>(a.dh + (size_t)(row0 + r) * F + c16 * 8) =
+            *reinterpret_cast<const uint4*>(H + r * kHmRow + c16 * 8);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();  // the next tile's staging overwrites H
+  }
+  __shared__ float red[16];
+  st_pg = wave_sum(st_pg);
+  st_vf = wave_sum(st_vf);
+  st_ent = wave_sum(st_ent);
+  st_n = wave_sum(st_n);
+  if (lane == 0) {
+    red[wave * 4 + 0] = st_pg;
+    red[wave * 4 + 1] = st_vf;
+    red[wave * 4 + 2] = st_ent;
+    red[wave * 4 + 3] = st_n;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4)
+    a.stats[blockIdx.x * 4 + threadIdx.x] = red[threadIdx.x] + red[4 + threadIdx.x] + red[8 + threadIdx.x] +
+                                            red[12 + threadIdx.x];
+  if (blockIdx.x == 0)  // stats rows past this grid (the caller sums stats_rows rows)
+    for (int i = threadIdx.x; i < (stats_rows - (int)gridDim.x) * 4; i += 256) a.stats[gridDim.x * 4 + i] = 0.f;
+}
+
+static bool head_mfma() {  // RRL_HEAD_MFMA=1: the MFMA head backward (A/B), read per call
+  const char* e = getenv("RRL_HEAD_MFMA");
+  return e && e[0] == '1';
+}
+
 // RRL_HEAD_STREAMED (read per call): unset = the streamed rollout head from 4,096 rows (20.0 vs
 // 24.5 us per 8,192 rows; 11.1 vs 10.7 us at 2,048) and the register backward; 1 = both
 // streamed (the backward measured slower: 80.6 vs 68.3 us at 40,960 rows, 28.6 vs 24.2 at
@@ -1836,6 +2005,18 @@ int rrl_a2c_head(int mode, const uint16_t* h, const float* head_params, int B, i
   a.dh = dh;
   a.dhead = dhead;
   a.stats = stats;
+  if (mode != 0 && A <= 7 && head_mfma()) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)a2c_head_train_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kHmW + 4 * kHmWave);
+      attr = true;
+    }
+    const int ntiles = (B + 15) / 16;
+    const int g = std::max(1, std::min(grid, (ntiles + 3) / 4));
+    hipLaunchKernelGGL(a2c_head_train_mfma_kernel, dim3(g), dim3(256), kHmW + 4 * kHmWave, st, a, grid);
+    return (int)hipGetLastError();
+  }
   if (A <= 8 && head_streamed(mode != 0, B)) {
     if (mode == 0 && part && !logits_out) {
       hipLaunchKernelGGL((a2c_head_streamed_kernel<8>), dim3(grid), dim3(256), 0, st, a);

@@ -186,7 +186,9 @@ def test_fc_dgrad_masked(cuda):
 
 
 @pytest.mark.parametrize("B", [48, 50])  # 3-4 rows per wave in the head backward (next-row prefetch, tail)
-def test_full_model_forward_backward_matches_autograd(cuda, B):
+@pytest.mark.parametrize("mfma", ["0", "1"])  # RRL_HEAD_MFMA: the fp32-MFMA head backward (partial last tile at 50)
+def test_full_model_forward_backward_matches_autograd(cuda, B, mfma, monkeypatch):
+    monkeypatch.setenv("RRL_HEAD_MFMA", mfma)
     spec = CNNSpec(6)
     params = spec.init(4)
     # larger head weights so the policy gradient is not negligible next to the value part
@@ -960,6 +962,41 @@ def test_streamed_rollout_head_is_bitwise_equal(cuda, N, monkeypatch):
     assert res[0][1][:, 3].sum().item() == N
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N", [37, 5000])
+def test_mfma_head_backward_matches_register_kernel(cuda, N, monkeypatch):
+    """a2c_head_train_mfma_kernel (RRL_HEAD_MFMA=1: fp32 MFMA, exact f32 products summed in
+    another order) vs a2c_head_kernel<true>: dhead / loss stats to fp32 rounding, dh to one bf16
+    ulp where a sum lands on a rounding boundary, and the resulting gradients."""
+    spec = CNNSpec(6)
+    params = spec.init(2)
+    o = spec.offsets()
+    params[o["wpi"]:o["bpi"]] *= 50.0
+    m = DeviceNatureCNN(spec, cuda, max_batch=N, params=params)
+    g = torch.Generator().manual_seed(9)
+    obs = torch.randint(0, 256, (N, 21, 21, 64), dtype=torch.uint8, generator=g).to(cuda)
+    act = torch.randint(0, 6, (N,), dtype=torch.int32, generator=g).to(cuda)
+    adv = torch.randn(N, generator=g).to(cuda)
+    ret = torch.randn(N, generator=g).to(cuda)
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("RRL_HEAD_MFMA", flag)
+        m.forward(obs, 0)
+        m.dh.fill_(float("nan"))
+        m.dhead.fill_(float("nan"))
+        stats = m.backward(obs, act, adv, ret, 0.5, 0.01)
+        torch.cuda.synchronize()
+        res.append((m.grad.clone(), stats.sum(0).cpu(), m.dh[:N * 512].float().cpu(),
+                    m.dhead[:N * 7].clone().cpu()))
+    (g0, s0, dh0, dd0), (g1, s1, dh1, dd1) = res
+    assert torch.isfinite(dh1).all() and torch.isfinite(dd1).all()
+    assert s1[3].item() == N
+    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dd1, dd0, rtol=1e-4, atol=1e-9)
+    torch.testing.assert_close(dh1, dh0, rtol=8e-3, atol=1e-9)
+    assert (dh1 == dh0).float().mean().item() > 0.9
+    assert relerr(g1, g0) < 1e-3
 
 
 def test_fused_render_draws_the_env_observation(cuda):
