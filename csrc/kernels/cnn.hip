@@ -514,6 +514,17 @@ __global__ void adam_clip4_kernel(float* __restrict__ p, float* __restrict__ m, 
                                   const float* __restrict__ g, uint16_t* __restrict__ shadow, size_t n,
                                   const float* __restrict__ norm_sq, float max_norm, float lr, float b1, float b2,
                                   float eps, float bc1, float bc2, const long long* __restrict__ step_dev, int norm_parts) {
+  // this thread's first float4 of p / m / v / g is loaded before the norm reduction and the
+  // bias corrections, so the two latencies overlap (one float4 per thread at the Pong size)
+  const size_t n4 = n / 4, stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  float4 pv = make_float4(0.f, 0.f, 0.f, 0.f), mv = pv, vv = pv, gv = pv;
+  if (i < n4) {
+    pv = reinterpret_cast<const float4*>(p)[i];
+    mv = reinterpret_cast<const float4*>(m)[i];
+    vv = reinterpret_cast<const float4*>(v)[i];
+    gv = reinterpret_cast<const float4*>(g)[i];
+  }
   if (step_dev) {
     const float t = (float)(*step_dev);
     bc1 = 1.f - powf(b1, t);
@@ -531,10 +542,13 @@ __global__ void adam_clip4_kernel(float* __restrict__ p, float* __restrict__ m, 
     const float denom = sqrtf(vo / bc2) + eps;
     po = pi - lr * (mo / bc1) / denom;
   };
-  const size_t n4 = n / 4;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
-    const float4 pv = reinterpret_cast<const float4*>(p)[i], mv = reinterpret_cast<const float4*>(m)[i];
-    const float4 vv = reinterpret_cast<const float4*>(v)[i], gv = reinterpret_cast<const float4*>(g)[i];
+  for (; i < n4; i += stride) {
+    if (i != blockIdx.x * (size_t)blockDim.x + threadIdx.x) {
+      pv = reinterpret_cast<const float4*>(p)[i];
+      mv = reinterpret_cast<const float4*>(m)[i];
+      vv = reinterpret_cast<const float4*>(v)[i];
+      gv = reinterpret_cast<const float4*>(g)[i];
+    }
     float4 po, mo, vo;
     upd(pv.x, mv.x, vv.x, gv.x, po.x, mo.x, vo.x);
     upd(pv.y, mv.y, vv.y, gv.y, po.y, mo.y, vo.y);
