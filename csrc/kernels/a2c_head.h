@@ -73,8 +73,9 @@ __device__ __forceinline__ void head_sum_part(float (&v)[8], const float* pr, si
 // part[z][row])) stored to h_out, then the same logits / value / sample arithmetic, in the same
 // order, as a2c_head_kernel<false, AMAX> -- so the two paths agree bitwise.  Lane 0 writes
 // act / logp / value and returns the action; other lanes return -1.
+// (WV / WP: where the value / policy weight rows are read -- a.w_v / a.w, or an LDS copy)
 template <int AMAX>
-RRL_DEV int a2c_rollout_row_streamed(const HeadArgs& a, int row, int lane) {
+RRL_DEV int a2c_rollout_row_streamed(const HeadArgs& a, int row, int lane, const float* WV, const float* WP) {
   const int A = a.A, F = kHeadF;
   const float4 b0 = *reinterpret_cast<const float4*>(a.fc_b + 8 * lane);
   const float4 b1 = *reinterpret_cast<const float4*>(a.fc_b + 8 * lane + 4);
@@ -103,8 +104,8 @@ RRL_DEV int a2c_rollout_row_streamed(const HeadArgs& a, int row, int lane) {
   for (int o = 0; o < kMaxAct; ++o) logits[o] = -INFINITY;
   float vsum = 0.f;
   {
-    const float4 w0 = *reinterpret_cast<const float4*>(a.w_v + 8 * lane);
-    const float4 w1 = *reinterpret_cast<const float4*>(a.w_v + 8 * lane + 4);
+    const float4 w0 = *reinterpret_cast<const float4*>(WV + 8 * lane);
+    const float4 w1 = *reinterpret_cast<const float4*>(WV + 8 * lane + 4);
     const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
     for (int i = 0; i < 8; ++i) vsum += wv[i] * x[i];
@@ -113,8 +114,8 @@ RRL_DEV int a2c_rollout_row_streamed(const HeadArgs& a, int row, int lane) {
 #pragma unroll
   for (int o = 0; o < AMAX; ++o) {
     if (o < A) {
-      const float4 w0 = *reinterpret_cast<const float4*>(a.w + o * F + 8 * lane);
-      const float4 w1 = *reinterpret_cast<const float4*>(a.w + o * F + 8 * lane + 4);
+      const float4 w0 = *reinterpret_cast<const float4*>(WP + o * F + 8 * lane);
+      const float4 w1 = *reinterpret_cast<const float4*>(WP + o * F + 8 * lane + 4);
       const float wp[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       float s = 0.f;
 #pragma unroll
@@ -135,6 +136,10 @@ RRL_DEV int a2c_rollout_row_streamed(const HeadArgs& a, int row, int lane) {
     if (a.value) a.value[row] = value;
   }
   return pick;
+}
+template <int AMAX>
+RRL_DEV int a2c_rollout_row_streamed(const HeadArgs& a, int row, int lane) {
+  return a2c_rollout_row_streamed<AMAX>(a, row, lane, a.w_v, a.w);
 }
 
 }  // namespace rrl

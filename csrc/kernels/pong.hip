@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(256, 8) pong_step_render_kernel(
 // (a2c_rollout_row_streamed: bitwise the a2c_head_kernel result), thread 0 steps the physics
 // with it, and the workgroup renders the new frame stack -- one launch instead of head + step
 // (the head launch was ~10 us per rollout step at 2,048 envs, mostly its fixed cost).
-template <int AMAX>
+template <int AMAX, bool WLDS>
 __global__ void __launch_bounds__(256, 8) pong_head_step_render_kernel(
     HeadArgs ha, float* __restrict__ state, float* __restrict__ rew, float* __restrict__ done,
     float* __restrict__ fin_ret, float* __restrict__ fin_len, float* __restrict__ ep_acc, uint8_t* __restrict__ obs,
@@ -251,7 +251,21 @@ __global__ void __launch_bounds__(256, 8) pong_head_step_render_kernel(
   __shared__ int pick_s;
   const int e = blockIdx.x, t = threadIdx.x;
   if (t < kPongState) ss[t] = state[(size_t)e * kPongState + t];
-  if (t < 64) {
+  if constexpr (WLDS) {
+    // waves 1-3 copy the head weights (w_v, then the A policy rows) into LDS while wave 0 sums
+    // the fc partials: one L2 round trip instead of one per output row (RRL_PONG_HEAD_WLDS)
+    __shared__ __attribute__((aligned(16))) float wl[(AMAX + 1) * kHeadF];
+    const int nf4 = (ha.A + 1) * (kHeadF / 4);
+    for (int i = t - 64; i >= 0 && i < nf4; i += 192) {
+      const float* src = i < kHeadF / 4 ? ha.w_v + 4 * i : ha.w + 4 * (i - kHeadF / 4);
+      *reinterpret_cast<float4*>(wl + 4 * i) = *reinterpret_cast<const float4*>(src);
+    }
+    __syncthreads();
+    if (t < 64) {
+      const int pick = a2c_rollout_row_streamed<AMAX>(ha, e, t, wl, wl + kHeadF);
+      if (t == 0) pick_s = pick;
+    }
+  } else if (t < 64) {
     const int pick = a2c_rollout_row_streamed<AMAX>(ha, e, t);
     if (t == 0) pick_s = pick;
   }
@@ -349,8 +363,14 @@ int rrl_pong_head_step_render(const float* part, int splits, const float* fc_b, 
   a.step_hi = (uint32_t)(sample_step >> 32);
   a.step_base = sample_base;
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
-  hipLaunchKernelGGL(pong_head_step_render_kernel<8>, dim3(N), dim3(256), 0, (hipStream_t)stream_, a, state, rew, done,
-                     fin_ret, fin_len, ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, step_base);
+  const char* wl_env = getenv("RRL_PONG_HEAD_WLDS");
+  if (wl_env && wl_env[0] == '1') {  // the head weights through LDS (A/B)
+    hipLaunchKernelGGL((pong_head_step_render_kernel<8, true>), dim3(N), dim3(256), 0, (hipStream_t)stream_, a, state, rew, done,
+                       fin_ret, fin_len, ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, step_base);
+  } else {
+    hipLaunchKernelGGL((pong_head_step_render_kernel<8, false>), dim3(N), dim3(256), 0, (hipStream_t)stream_, a, state, rew, done,
+                       fin_ret, fin_len, ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, step_base);
+  }
   return (int)hipGetLastError();
 }
 

@@ -882,7 +882,8 @@ def _pong_histories(cuda, N, steps=40, seed=3):
 
 
 @pytest.mark.parametrize("N", [37, 2048])
-def test_fused_head_step_equals_head_then_step(cuda, N):
+@pytest.mark.parametrize("wlds", ["0", "1"])  # RRL_PONG_HEAD_WLDS: head weights through LDS
+def test_fused_head_step_equals_head_then_step(cuda, N, wlds, monkeypatch):
     """pong_head_step_render_kernel (the policy head inside the env-step launch) vs the head
     launch (a2c_head from the fc split-K partials) followed by the step + render launch: the
     same actions, log-probs, values, stored hidden units, env state, rewards, dones and
@@ -891,6 +892,7 @@ def test_fused_head_step_equals_head_then_step(cuda, N):
 
     from relayrl_prototype_amd.envs.pong import DevicePong
 
+    monkeypatch.setenv("RRL_PONG_HEAD_WLDS", wlds)
     spec = CNNSpec(6)
     m = DeviceNatureCNN(spec, cuda, max_batch=N, seed=5)
     envs = [DevicePong(N, cuda, 11), DevicePong(N, cuda, 11)]
