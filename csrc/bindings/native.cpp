@@ -195,6 +195,8 @@ PYBIND11_MODULE(_native, m) {
       .def("num_connections", &zmtp::Socket::num_connections)
       .def("num_threads", &zmtp::Socket::num_threads)
       .def("set_inbox_limits", &zmtp::Socket::set_inbox_limits, py::arg("max_messages"), py::arg("max_bytes"))
+      .def("set_max_message_size", &zmtp::Socket::set_max_message_size, py::arg("max_bytes"))
+      .def("max_message_size", &zmtp::Socket::max_message_size)
       .def("inbox_size", &zmtp::Socket::inbox_size)
       .def("inbox_bytes", &zmtp::Socket::inbox_bytes)
       .def("stats", [](zmtp::Socket& s) {
@@ -207,6 +209,7 @@ PYBIND11_MODULE(_native, m) {
         d["messages_in"] = st.messages_in;
         d["bytes_in"] = st.bytes_in;
         d["inbox_waits"] = st.inbox_waits;
+        d["oversized"] = st.oversized;
         return d;
       });
 

@@ -504,7 +504,9 @@ bool tensor_f32(const py::handle& td, std::vector<float>& out, HeaderCache& cach
   }
   const rrl::StHeader& h = it->second;
   const size_t base = 8 + (size_t)hl;
-  if (base + (size_t)h.off1 > n) throw FrameError("TensorData: safetensors: bad data offsets");
+  // st_header guarantees 0 <= off0 <= off1 and off1 - off0 == count * dtype size
+  if (h.off0 < 0 || h.off1 < h.off0 || (uint64_t)h.off1 > n - base)
+    throw FrameError("TensorData: safetensors: bad data offsets");
   int64_t cnt = 1;
   for (auto s : h.shape) cnt *= s;
   out.resize((size_t)cnt);

@@ -1,5 +1,6 @@
 #include "codec.h"
 
+#include <cstdint>
 #include <cstring>
 #include <sstream>
 
@@ -163,11 +164,17 @@ StHeader st_header(const char* header_json, size_t len, const std::string& name)
     if (i < h.size() && h[i] == ',') ++i;
   }
   if (!found) throw std::runtime_error("safetensors: tensor '" + name + "' not found");
-  if (t.off1 < t.off0) throw std::runtime_error("safetensors: bad data offsets");
+  // untrusted input (any ZMQ / gRPC peer): offsets must be a non-negative ordered range and the
+  // element count must not overflow -- callers then only have to check off1 against the buffer
+  if (t.off0 < 0 || t.off1 < t.off0) throw std::runtime_error("safetensors: bad data offsets");
+  const int64_t esz = (int64_t)dtype_size(t.dtype);
   int64_t n = 1;
-  for (auto d : t.shape) n *= d;
-  if (t.off1 - t.off0 != n * (int64_t)dtype_size(t.dtype))
-    throw std::runtime_error("safetensors: data size does not match shape");
+  for (auto d : t.shape) {
+    if (d < 0) throw std::runtime_error("safetensors: negative shape dimension");
+    if (d != 0 && n > (INT64_MAX / esz) / d) throw std::runtime_error("safetensors: shape overflows");
+    n *= d;
+  }
+  if (t.off1 - t.off0 != n * esz) throw std::runtime_error("safetensors: data size does not match shape");
   return t;
 }
 
@@ -175,10 +182,10 @@ Tensor st_decode(const std::string& file, const std::string& name) {
   if (file.size() < 8) throw std::runtime_error("safetensors: file too short");
   uint64_t hl = 0;
   for (int i = 0; i < 8; ++i) hl |= (uint64_t)(uint8_t)file[i] << (8 * i);
-  if (8 + hl > file.size()) throw std::runtime_error("safetensors: header length out of range");
+  if (hl > file.size() - 8) throw std::runtime_error("safetensors: header length out of range");
   const StHeader sh = st_header(file.data() + 8, (size_t)hl, name);
   const size_t base = 8 + hl;
-  if (base + (size_t)sh.off1 > file.size()) throw std::runtime_error("safetensors: bad data offsets");
+  if ((uint64_t)sh.off1 > file.size() - base) throw std::runtime_error("safetensors: bad data offsets");
   Tensor t;
   t.dtype = sh.dtype;
   t.shape = sh.shape;

@@ -10,6 +10,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstring>
 #include <stdexcept>
@@ -483,14 +484,16 @@ bool Socket::parse(const std::shared_ptr<Conn>& c) {
     uint64_t size = 0;
     const size_t hl = frame_head(p, avail, flags, size);
     if (hl == 0) break;
-    if (size > (k.state == 1 ? kMaxCommand : kMaxFrame)) {
+    // a claimed size is only a claim: the frame (plus the message's earlier parts) must fit
+    // the per-socket message cap before we keep buffering it; rx grows as bytes arrive
+    const uint64_t cap = k.state == 1 ? kMaxCommand : std::min<uint64_t>(kMaxFrame, max_msg_bytes_.load());
+    if (size > cap || (k.state == 2 && !(flags & 0x04) && k.part_bytes + size > cap)) {
+      std::lock_guard<std::mutex> s(smu_);
+      stats_.oversized++;
       ok = false;
       break;
     }
-    if (avail - hl < size) {
-      k.rx.reserve(k.off + hl + size);  // one allocation for a large frame
-      break;
-    }
+    if (avail - hl < size) break;
     std::string body(p + hl, (size_t)size);
     k.off += hl + (size_t)size;
     if (k.state == 1) {
@@ -707,6 +710,8 @@ size_t Socket::num_threads() {
     if (t.joinable()) ++n;
   return n;
 }
+
+void Socket::set_max_message_size(size_t max_bytes) { max_msg_bytes_ = max_bytes ? max_bytes : 1; }
 
 void Socket::set_inbox_limits(size_t max_messages, size_t max_bytes) {
   std::lock_guard<std::mutex> g(qmu_);

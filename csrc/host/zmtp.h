@@ -47,6 +47,7 @@ struct Stats {
   uint64_t messages_in = 0;    // messages queued to the inbox
   uint64_t bytes_in = 0;       // frame payload bytes queued
   uint64_t inbox_waits = 0;    // times the I/O thread waited for inbox space (backpressure)
+  uint64_t oversized = 0;      // connections dropped for a frame / message over the size cap
 };
 
 struct Conn;
@@ -77,6 +78,10 @@ class Socket {
   // inbox bounds: messages and payload bytes (a single larger message is still accepted
   // into an empty inbox)
   void set_inbox_limits(size_t max_messages, size_t max_bytes);
+  // largest multipart message (sum of its frames) a peer may send; a peer that exceeds it is
+  // dropped before the bytes are buffered (untrusted peers cannot make us allocate more)
+  void set_max_message_size(size_t max_bytes);
+  size_t max_message_size() const { return max_msg_bytes_.load(); }
   size_t inbox_size();
   size_t inbox_bytes();
   Stats stats();
@@ -119,6 +124,7 @@ class Socket {
   size_t inbox_bytes_ = 0;
   size_t inbox_cap_ = 1 << 16;
   size_t inbox_byte_cap_ = size_t(1) << 30;
+  std::atomic<size_t> max_msg_bytes_{size_t(256) << 20};
   std::mutex smu_;
   Stats stats_;
 };

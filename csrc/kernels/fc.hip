@@ -913,8 +913,10 @@ static void fcp_splits(int tiles, int ktiles, int max_splits, int cus, int* kps,
   int s = 1;
   for (int c = 2; c <= max_splits; ++c)
     if (tiles * c <= cus && ktiles / c >= 2) s = c;
+  // rebalance until the splits actually used (ceil(ktiles / k), which can be < s: kt = 13 with
+  // s = 5 gives k = 3 and splits 3,3,3,3,1) all keep >= 2 k-tiles, the last one included
   int k = (ktiles + s - 1) / s;
-  if (ktiles - (s - 1) * k < 2 && s > 1) {  // a remainder split of one k-tile: rebalance
+  while (s > 1 && ktiles - ((ktiles + k - 1) / k - 1) * k < 2) {
     s -= 1;
     k = (ktiles + s - 1) / s;
   }

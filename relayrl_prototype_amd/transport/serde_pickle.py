@@ -30,6 +30,8 @@ import struct
 from collections import OrderedDict
 from typing import Any, List, Optional, Tuple
 
+import numpy as np
+
 MAX_DEPTH = 64
 MAX_STACK = 1 << 20   # values on the interpreter stack (a frame holds ~10 per action)
 MAX_MEMO = 1 << 16
@@ -373,51 +375,20 @@ def reference_frame(actions) -> bytes:
     return dumps(out)
 
 
-class ColumnDeduper:
-    """CumulativeDeduper for natively decoded reference uploads (types.ReferenceColumns): the
-    same rule -- an upload that strictly extends a remembered one whose last row is done keeps
-    only its new rows -- with the digests taken over the float32 columns of the rows."""
-
-    def __init__(self, capacity: int = 4096):
-        self.capacity = capacity
-        self._seen: "OrderedDict[bytes, Tuple[int, bytes]]" = OrderedDict()
-        self.stripped = 0
-
-    @staticmethod
-    def _digest(c, k: int) -> bytes:
-        h = hashlib.blake2b(digest_size=16)
-        for a in (c.has_obs, c.obs, c.has_act, c.act, c.rew, c.done):
-            if a is not None:
-                h.update(a[:k].tobytes())
-        return h.digest()
-
-    def new_rows(self, c):
-        n = len(c)
-        if n == 0:
-            return c
-        head = self._digest(c, 1)
-        prev = self._seen.get(head)
-        keep = c
-        if prev is not None:
-            n_prev, dig = prev
-            if n > n_prev and c.done[n_prev - 1] and self._digest(c, n_prev) == dig:
-                keep = c.tail(n_prev)
-                self.stripped += n_prev
-        self._seen[head] = (n, self._digest(c, n))
-        self._seen.move_to_end(head)
-        while len(self._seen) > self.capacity:
-            self._seen.popitem(last=False)
-        return keep
-
-
-class CumulativeDeduper:
+class ReferenceDeduper:
     """Reference agents re-send every earlier episode with each upload (the trajectory is
     only cleared at max_length, trajectory.rs:160-204), each over a NEW connection, so the
     learner would train on the same actions again and again.  Uploads are matched by a
-    digest of their first action.  An upload keeps only its new actions when it strictly
-    extends a remembered upload AT AN EPISODE BOUNDARY: the remembered prefix must end in
-    a ``done`` action, which every cumulative re-send does (the agent sends right after
-    appending a done marker, trajectory.rs:172-203).
+    digest of their first row.  An upload keeps only its new rows when it strictly extends a
+    remembered upload AT AN EPISODE BOUNDARY: the remembered prefix must end in a ``done``
+    row, which every cumulative re-send does (the agent sends right after appending a done
+    marker, trajectory.rs:172-203).
+
+    One deduper serves both decode paths of the ZMQ endpoint -- natively decoded columns
+    (``new_rows``, types.ReferenceColumns) and per-action objects (``new_actions``, the path
+    for ragged frames) -- with ONE digest definition over a canonical row encoding
+    (``flag, f32 obs | flag, f32 act | f32 rew, u8 done``), so an agent whose first upload went
+    one way and whose re-send goes the other is still stripped.
 
     Residual ambiguity: the sender is not part of the key -- each reference upload comes
     over a fresh PUSH connection with no identity, so two agents cannot be told apart.  An
@@ -432,28 +403,87 @@ class CumulativeDeduper:
         self._seen: "OrderedDict[bytes, Tuple[int, bytes]]" = OrderedDict()
         self.stripped = 0
 
+    # canonical row bytes ------------------------------------------------------------
     @staticmethod
-    def _digest(actions) -> bytes:
+    def _row_bytes(a) -> bytes:
+        out = []
+        for t in (a.get_obs(), a.get_act()):
+            if t is None:
+                out.append(b"\x00")
+            else:
+                out.append(b"\x01" + np.ascontiguousarray(np.asarray(t, np.float32).reshape(-1)).tobytes())
+        out.append(struct.pack("<fB", float(a.get_rew()), 1 if a.get_done() else 0))
+        return b"".join(out)
+
+    @staticmethod
+    def _digest_actions(actions) -> bytes:
         h = hashlib.blake2b(digest_size=16)
         for a in actions:
-            for t in (a.get_obs(), a.get_act()):
-                h.update(b"-" if t is None else t.tobytes())
-            h.update(struct.pack("<f?", a.get_rew(), a.get_done()))
+            h.update(ReferenceDeduper._row_bytes(a))
         return h.digest()
+
+    @staticmethod
+    def _digest_cols(c, k: int) -> bytes:
+        """The same byte stream as ``_digest_actions`` over rows [0, k), built per run of rows
+        with the same (has_obs, has_act) pattern as one fixed-width byte matrix."""
+        h = hashlib.blake2b(digest_size=16)
+        ho = np.asarray(c.has_obs[:k], bool)
+        ha = np.asarray(c.has_act[:k], bool)
+        pat = ho.astype(np.int8) * 2 + ha.astype(np.int8)
+        cuts = np.flatnonzero(np.diff(pat)) + 1
+        starts = np.concatenate(([0], cuts)).astype(int)
+        ends = np.concatenate((cuts, [k])).astype(int)
+        rew = np.asarray(c.rew, np.float32)
+        done = np.asarray(c.done).astype(np.uint8)
+        for s0, e0 in zip(starts, ends):
+            if e0 <= s0:
+                continue
+            parts = []
+            n = e0 - s0
+            for has, arr in ((ho[s0], c.obs), (ha[s0], c.act)):
+                if has:
+                    parts.append(np.ones((n, 1), np.uint8))
+                    parts.append(np.ascontiguousarray(np.asarray(arr[s0:e0], np.float32).reshape(n, -1)).view(np.uint8))
+                else:
+                    parts.append(np.zeros((n, 1), np.uint8))
+            parts.append(rew[s0:e0].reshape(n, 1).view(np.uint8))
+            parts.append(done[s0:e0].reshape(n, 1))
+            h.update(np.concatenate(parts, axis=1).tobytes())
+        return h.digest()
+
+    # the shared rule -----------------------------------------------------------------
+    def _keep_from(self, n: int, head: bytes, prefix_digest, full_digest, done_at) -> int:
+        """Index of the first row to keep (0 = keep all), updating the memory."""
+        start = 0
+        prev = self._seen.get(head)
+        if prev is not None:
+            n_prev, dig = prev
+            if n > n_prev and done_at(n_prev - 1) and prefix_digest(n_prev) == dig:
+                start = n_prev
+                self.stripped += n_prev
+        self._seen[head] = (n, full_digest())
+        self._seen.move_to_end(head)
+        while len(self._seen) > self.capacity:
+            self._seen.popitem(last=False)
+        return start
+
+    def new_rows(self, c):
+        n = len(c)
+        if n == 0:
+            return c
+        start = self._keep_from(n, self._digest_cols(c, 1), lambda k: self._digest_cols(c, k),
+                                lambda: self._digest_cols(c, n), lambda i: bool(c.done[i]))
+        return c.tail(start) if start else c
 
     def new_actions(self, actions) -> list:
         if not actions:
             return actions
-        head = self._digest(actions[:1])
-        prev = self._seen.get(head)
-        keep = actions
-        if prev is not None:
-            n_prev, dig = prev
-            if len(actions) > n_prev and actions[n_prev - 1].get_done() and self._digest(actions[:n_prev]) == dig:
-                keep = actions[n_prev:]
-                self.stripped += n_prev
-        self._seen[head] = (len(actions), self._digest(actions))
-        self._seen.move_to_end(head)
-        while len(self._seen) > self.capacity:
-            self._seen.popitem(last=False)
-        return keep
+        n = len(actions)
+        start = self._keep_from(n, self._digest_actions(actions[:1]), lambda k: self._digest_actions(actions[:k]),
+                                lambda: self._digest_actions(actions), lambda i: bool(actions[i].get_done()))
+        return actions[start:] if start else actions
+
+
+# the two decode paths' historical names: one class, one digest
+ColumnDeduper = ReferenceDeduper
+CumulativeDeduper = ReferenceDeduper

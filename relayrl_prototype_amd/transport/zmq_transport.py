@@ -42,14 +42,13 @@ def make_agent_id() -> str:
 class ZmqTrainingEndpoint:
     def __init__(self, service, agent_listener: str, trajectory_server: str, multiactor: bool = True,
                  verbose: bool = False, model_push_addr: Optional[str] = None):
-        from .serde_pickle import ColumnDeduper, CumulativeDeduper
+        from .serde_pickle import ReferenceDeduper
 
         self.service = service
         self.model_push_addr = model_push_addr
         self.ref_agents = set()   # identities that did the reference handshake
         self._model_push = None   # PUSH -> reference agents' bound PULL (lazy)
-        self.dedupe = CumulativeDeduper()
-        self.dedupe_cols = ColumnDeduper()
+        self.dedupe = ReferenceDeduper()  # one memory for the column and the per-action decode paths
         self.reference_frames = 0
         self.multiactor = multiactor
         self.verbose = verbose
@@ -161,7 +160,7 @@ class ZmqTrainingEndpoint:
             self.reference_frames += 1
             self._touch_reference_agents()
             try:  # natively, straight to columns (rows of a consistent shape)
-                rows = self.dedupe_cols.new_rows(ReferenceColumns.decode(f))
+                rows = self.dedupe.new_rows(ReferenceColumns.decode(f))
                 return rows if len(rows) else None
             except ValueError:  # ragged tensors / unusual encodings: the per-action path
                 pass

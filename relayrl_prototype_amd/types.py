@@ -471,6 +471,17 @@ class ReferenceColumns:
         """RelayRLTrajectory's attribute view (materialised on each access)."""
         return self.get_actions()
 
+    def to_trajectory(self) -> "RelayRLTrajectory":
+        """The same rows as a per-action RelayRLTrajectory, terminal markers kept in place (the
+        form the ZMQ endpoint's fallback path produces for a ragged reference frame)."""
+        t = RelayRLTrajectory(max(len(self), 1), None, self.agent_id)
+        t.actions = self.get_actions()
+        return t
+
+    def encode(self) -> bytes:
+        """One RRLT frame (the multi-rank engine relay forwards uploads as frames)."""
+        return self.to_trajectory().encode()
+
     def get_actions(self) -> List["RelayRLAction"]:
         out = []
         for i in range(len(self)):

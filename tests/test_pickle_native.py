@@ -246,3 +246,71 @@ def test_native_column_decode_speed():
         ReferenceColumns.decode(f)
     t = (time.perf_counter() - t0) / 200
     assert t < 2e-3, t  # ~19 ms through the Python interpreter + per-action objects
+
+
+# ---------------------------------------------------------------- hostile TensorData headers
+def _st_file(header: str, payload: bytes = b"\0" * 16) -> bytes:
+    h = header.encode()
+    return struct.pack("<Q", len(h)) + h + payload
+
+
+def _frame_with_obs(st_bytes: bytes) -> bytes:
+    a = RelayRLAction(np.zeros(4, np.float32), np.array([0.0], np.float32), None, 1.0, None, False, True)
+    d = a.to_json_dict()
+    d["obs"] = dict(d["obs"], data=list(st_bytes))
+    d["act"] = dict(d["act"], data=list(d["act"]["data"]))
+    return sp.dumps([d])
+
+
+@pytest.mark.parametrize("header", [
+    '{"tensor":{"dtype":"F32","shape":[40],"data_offsets":[-160,0]}}',          # before the buffer
+    '{"tensor":{"dtype":"F32","shape":[4],"data_offsets":[-8,8]}}',
+    '{"tensor":{"dtype":"F32","shape":[-4],"data_offsets":[16,0]}}',            # negative dim
+    '{"tensor":{"dtype":"F32","shape":[-2,-2],"data_offsets":[0,16]}}',         # negatives that multiply to +4
+    '{"tensor":{"dtype":"F32","shape":[4611686018427387904,4],"data_offsets":[0,0]}}',  # product overflows to 0
+    '{"tensor":{"dtype":"F64","shape":[2305843009213693952],"data_offsets":[0,0]}}',
+    '{"tensor":{"dtype":"F32","shape":[4],"data_offsets":[9223372036854775800,9223372036854775816]}}',
+    '{"tensor":{"dtype":"F32","shape":[4],"data_offsets":[0,99999999999999999999999]}}',  # stoll overflow
+    '{"tensor":{"dtype":"F32","shape":[4],"data_offsets":[8,24]}}',             # past the end
+])
+def test_hostile_safetensors_headers_are_rejected(header):
+    """data_offsets / shapes from a peer must never make the reader touch memory
+    outside the TensorData bytes (a negative off0 used to read heap memory before the buffer)."""
+    from relayrl_prototype_amd.types import ReferenceColumns
+
+    f = _frame_with_obs(_st_file(header))
+    with pytest.raises(ValueError):
+        ReferenceColumns.decode(f)
+    with pytest.raises(Exception):  # the gRPC path's safetensors reader (codec.cpp st_decode)
+        _native.st_decode(_st_file(header))
+
+
+def test_valid_tensor_still_decodes_after_hardening():
+    from relayrl_prototype_amd.types import ReferenceColumns
+
+    payload = np.arange(4, dtype=np.float32).tobytes()
+    f = _frame_with_obs(_st_file('{"tensor":{"dtype":"F32","shape":[4],"data_offsets":[0,16]}}', payload))
+    c = ReferenceColumns.decode(f)
+    np.testing.assert_array_equal(c.obs[0], np.arange(4, dtype=np.float32))
+
+
+def test_one_deduper_across_the_column_and_action_paths():
+    """an agent's first upload decoded natively to columns and its cumulative re-send
+    decoded per action (e.g. a later ragged tensor) must still have the re-sent prefix stripped,
+    and vice versa: both paths share one digest."""
+    from relayrl_prototype_amd.types import ReferenceColumns
+
+    rng = np.random.default_rng(11)
+    ep1 = _ref_episode(rng, 6)
+    ep2 = _ref_episode(rng, 4)
+    f1, f12 = sp.reference_frame(ep1), sp.reference_frame(ep1 + ep2)
+    d = sp.ReferenceDeduper()
+    assert len(d.new_rows(ReferenceColumns.decode(f1))) == len(ep1)
+    kept = d.new_actions(sp.actions_from_reference(sp.loads(f12)))
+    assert len(kept) == len(ep2) and d.stripped == len(ep1)
+    d2 = sp.ReferenceDeduper()
+    assert len(d2.new_actions(sp.actions_from_reference(sp.loads(f1)))) == len(ep1)
+    kept = d2.new_rows(ReferenceColumns.decode(f12))
+    assert len(kept) == len(ep2) and d2.stripped == len(ep1)
+    assert sp.ReferenceDeduper._digest_cols(ReferenceColumns.decode(f12), len(ep1) + len(ep2)) == \
+        sp.ReferenceDeduper._digest_actions(sp.actions_from_reference(sp.loads(f12)))

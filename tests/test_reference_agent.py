@@ -226,3 +226,28 @@ def test_reference_wire_trains_against_our_server(tmp_path, monkeypatch):
         if agent is not None:
             agent.close()
         srv.close(save=False)
+
+
+def test_reference_columns_relay_through_the_engine_link():
+    """a multi-rank engine server forwards every upload as one frame
+    (runtime/engine_relay.encode_upload).  A reference upload arrives as ReferenceColumns; it must
+    encode (as RRLT, terminal markers kept) and decode to the same actions on rank 0."""
+    import numpy as np
+
+    from relayrl_prototype_amd.runtime.engine_relay import decode_upload, encode_upload
+    from relayrl_prototype_amd.transport import serde_pickle as sp
+    from relayrl_prototype_amd.types import ReferenceColumns, RelayRLAction
+
+    rng = np.random.default_rng(0)
+    acts = [RelayRLAction(rng.normal(size=4).astype(np.float32), np.array([i % 2], np.float32),
+                          np.ones(2, np.float32), float(i), {"logp_a": np.array([-0.5], np.float32)}, False, True)
+            for i in range(6)]
+    acts.append(RelayRLAction(None, None, None, 0.25, None, True, False))
+    cols = ReferenceColumns.decode(sp.reference_frame(acts))
+    back = decode_upload(encode_upload(cols))
+    got = back.get_actions()
+    assert len(got) == 7 and got[-1].get_obs() is None and got[-1].get_done()
+    assert got[-1].get_rew() == 0.25
+    for a, b in zip(got[:-1], acts[:-1]):
+        np.testing.assert_array_equal(np.asarray(a.get_obs()).reshape(-1), b.get_obs().reshape(-1))
+        assert a.get_rew() == b.get_rew()

@@ -231,3 +231,45 @@ def test_many_agent_processes_fan_in_without_drops(transport):
     allow = torch.get_num_threads() + (24 if transport == "grpc" else 4)
     assert peak - th0 <= allow, r
     assert r["uploads_received"] > 40 * 8  # far more connections than threads (zmq-ref: one per upload)
+
+
+def _rss_kb() -> int:
+    with open("/proc/self/status") as f:
+        for line in f:
+            if line.startswith("VmRSS:"):
+                return int(line.split()[1])
+    return 0
+
+
+def test_claimed_frame_size_is_not_allocated_and_oversized_peers_are_dropped():
+    """a peer's 8-byte length is only a claim -- a 4 GiB header with no payload must not
+    reserve 4 GiB, and a frame (or a multipart message's running total) over the socket's message
+    cap drops that connection while others keep being served."""
+    pull = _native.ZmtpSocket(_native.SockType.PULL)
+    port = pull.bind("tcp://127.0.0.1:0")
+    assert pull.max_message_size() == 256 << 20
+    pull.set_max_message_size(1 << 20)
+    rss0 = _rss_kb()
+    liars = []
+    for _ in range(8):  # each claims a 1 GiB frame (under the 4 GiB frame guard), sends 10 bytes
+        s = socket.create_connection(("127.0.0.1", port))
+        s.sendall(GREETING + _ready(b"PUSH") + bytes([0x02]) + (1 << 30).to_bytes(8, "big") + b"x" * 10)
+        liars.append(s)
+    multi = socket.create_connection(("127.0.0.1", port))  # 3 x 400 KB parts: over 1 MiB in total
+    multi.sendall(GREETING + _ready(b"PUSH") + b"".join(_frame(b"m" * 400_000, more=True) for _ in range(3)))
+    _upload_once(port, b"ok")
+    m = pull.recv(5000)
+    assert m is not None and bytes(m[1][0]) == b"ok"
+    t_end = time.time() + 5
+    while pull.stats()["oversized"] < 9 and time.time() < t_end:
+        time.sleep(0.05)
+    assert pull.stats()["oversized"] == 9, pull.stats()
+    assert _rss_kb() - rss0 < 200_000  # 8 GiB claimed; nothing near it reserved
+    pull.set_max_message_size(4 << 20)  # a legitimately large message still passes
+    s = socket.create_connection(("127.0.0.1", port))
+    s.sendall(GREETING + _ready(b"PUSH") + b"".join(_frame(b"m" * 400_000, more=i < 2) for i in range(3)))
+    m = pull.recv(5000)
+    assert m is not None and sum(len(f) for f in m[1]) == 1_200_000
+    for x in liars + [multi, s]:
+        x.close()
+    pull.close()
