@@ -52,6 +52,13 @@ def parse(argv=None):
     ap.add_argument("--ttt", action="store_true",
                     help="also measure wall-clock to the threshold with several ranks (default: one GPU only)")
     ap.add_argument("--no-ttt", action="store_true", help="skip the time-to-threshold measurement")
+    ap.add_argument("--multi-ttt-seeds", type=int, default=2,
+                    help="world > 1: seeds of each time-to-threshold measurement (the whole-node record carries "
+                         "both halves of the metric; one GPU uses --ttt-seeds / --ttt-ref-seeds)")
+    ap.add_argument("--preflight-deadline-s", type=float, default=90.0,
+                    help="world > 1: deadline of the collective preflight (parallel/preflight.py: RCCL init, "
+                         "70 KB all-reduce, P2P ring, a captured all-reduce replayed 3x vs eager); a node that "
+                         "fails the capture part runs with eager collectives, one that fails RCCL reports it")
     # tuned TTT defaults: tools/ttt_sweep.py --grid r2 / r2refine (round 2, 10 seeds): 256 envs x 64 steps,
     # 10 value iterations, pi lr 2e-2 (median 9.8 ms after construction vs 13.7 ms for the round-1 1024 x 64,
     # 5 iterations, pi lr 1e-2)
@@ -462,8 +469,29 @@ def main(argv=None):
     from relayrl_prototype_amd.parallel.comm import init_distributed, local_device_index
 
     on_gpu = args.device == "gpu"
+    preflight = None
     if int(world_env or 1) > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if os.environ.get("RRL_PREFLIGHT", "1") != "0":
+            # before this process touches the GPU: prove RCCL + graph capture in child processes
+            from relayrl_prototype_amd.parallel.comm import local_device_index
+            from relayrl_prototype_amd.parallel.preflight import run_preflight
+
+            pf_backend = os.environ.get("RRL_DIST_BACKEND") or ("nccl" if on_gpu else "gloo")
+            preflight = run_preflight(pf_backend, local_device_index(), args.preflight_deadline_s)
+            if preflight is not None and not preflight["rccl_ok"]:
+                if int(os.environ.get("RANK", "0")) == 0:
+                    bad = [r for r in preflight["per_rank"] if not r.get("rccl_ok")]
+                    print(json.dumps({"metric": METRIC, "value": None, "unit": "env_steps/s", "n_gpus": int(world_env),
+                                      "steps": args.steps, "warmup": args.warmup, "higher_is_better": True,
+                                      "scaling": "weak", "vs_baseline": None,
+                                      "error": "collective preflight failed: " + "; ".join(
+                                          f"rank {r['rank']} at {r.get('stage')}: {r.get('error')}" for r in bad[:4]),
+                                      "preflight": preflight}), flush=True)
+                return 2
+            if preflight is not None and not preflight["graphs_ok"]:
+                args.no_graphs = True  # eager collectives everywhere (value loop, TTT runs)
+                args.ttt_graphs = False
         # a hung peer becomes an exception inside 90 s (recorded in the JSON by the secondary
         # actor-learner phase) instead of a 10-minute wait or a torn-down process
         os.environ.setdefault("RRL_COLLECTIVE_TIMEOUT_S", "90")
@@ -547,6 +575,9 @@ def main(argv=None):
             },
             "backend": comm.backend,
             "rccl_world": world if comm.backend == "nccl" else 0,
+            # collectives / optimiser loops replayed from hipGraphs (False: eager, e.g. after a failed
+            # capture preflight or over gloo)
+            "graphs": bool(cfg.use_graphs and comm.graph_safe) if on_gpu else False,
             "per_rank_env_steps_per_s": per_rank,
             "per_rank_ms_per_step": per_rank_ms,
             "final_avg_ep_ret": None if m["AverageEpRet"] != m["AverageEpRet"] else round(m["AverageEpRet"], 2),
@@ -589,6 +620,8 @@ def main(argv=None):
                                       data="synthetic device envs (docs/ENVS.md), random-init weights")
         if al_rec is not None:
             rec["actor_learner"] = al_rec
+        if preflight is not None:
+            rec["preflight"] = preflight
         if ref_cpu is not None:
             rec["reference_equivalent_cpu"] = {
                 "env_steps_per_s": round(ref_cpu.get("value", 0.0), 1),
@@ -613,7 +646,9 @@ def main(argv=None):
         finally:
             guard.cancel()
     ttt = ttt_ref = None
-    do_ttt = on_gpu and (args.ttt or world == 1) and not args.no_ttt
+    do_ttt = on_gpu and not args.no_ttt
+    if do_ttt and world > 1:  # the whole-node record carries both halves of the metric
+        args.ttt_seeds = args.ttt_ref_seeds = args.multi_ttt_seeds
     if do_ttt:
         del tr
         torch.cuda.empty_cache()
@@ -625,8 +660,8 @@ def main(argv=None):
         ttt = time_to_threshold(tuned, dict(shape, use_graphs=bool(args.ttt_graphs)), args.ttt_seeds,
                                 args.ttt_max_s, comm)
         ref_shape = {"num_envs": args.ttt_ref_envs, "rollout_len": args.ttt_ref_rollout_len}
-        ttt_ref = time_to_threshold(ref_hp, dict(ref_shape, use_graphs=True), args.ttt_ref_seeds, args.ttt_max_s,
-                                    comm)
+        ttt_ref = time_to_threshold(ref_hp, dict(ref_shape, use_graphs=not args.no_graphs), args.ttt_ref_seeds,
+                                    args.ttt_max_s, comm)
     ref_cpu = collect_reference_cpu(ref_proc, args.ref_cpu_seconds)
     if rank == 0:
         print(json.dumps(record(al_rec, ttt, ttt_ref, ref_cpu, do_ttt)), flush=True)

@@ -41,6 +41,23 @@ class AlgorithmAbstract(ABC):
         """Write the epoch's statistics."""
 
 
+def infer_next_obs(act, obs, mask=None):
+    """BaseKernel.py:6-22's placeholder model of the next observation: obs + act."""
+    import torch
+
+    return obs + torch.as_tensor(act, dtype=torch.float32)
+
+
+def mlp(sizes, activation, output_activation=nn.Identity) -> nn.Sequential:
+    """Linear layers of ``sizes`` with ``activation`` between them and ``output_activation``
+    after the last (BaseKernel.py:25-39 contract)."""
+    layers = []
+    for j in range(len(sizes) - 1):
+        layers.append(nn.Linear(sizes[j], sizes[j + 1]))
+        layers.append((activation if j < len(sizes) - 2 else output_activation)())
+    return nn.Sequential(*layers)
+
+
 class ForwardKernelAbstract(nn.Module, ABC):
     @abstractmethod
     def forward(self, obs, mask, *args, **kwargs):

@@ -60,6 +60,9 @@ def load_algorithm_class(name: str, algorithm_dir: Optional[str] = None):
     if algorithm_dir:
         path = os.path.join(algorithm_dir, name, name + ".py")
         if os.path.exists(path):
+            from .compat import install_reference_aliases
+
+            install_reference_aliases()  # _common._algorithms.* / utils.logger import paths
             if algorithm_dir not in sys.path:
                 sys.path.insert(0, algorithm_dir)
             mod = importlib.import_module(f"{name}.{name}")

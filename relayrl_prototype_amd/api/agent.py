@@ -78,6 +78,7 @@ class RelayRLAgent:
         # reference ZMQ wire only: a new TCP connection per upload, as the reference agent does
         self.connection_per_upload = bool(connection_per_upload)
         self._rec = EpisodeRecorder(self.max_traj_length)
+        self._aux = []  # per-action step() dicts of a TorchScript (plugin) policy
         if model_path is not None:
             self._load_model_file(model_path)
         self._connect()
@@ -85,20 +86,37 @@ class RelayRLAgent:
 
     # ------------------------------------------------------------------ models
     def _load_model_file(self, path: str):
-        """Initial model from a TorchScript file WE exported (flat weights recovered)."""
+        """Initial model from a TorchScript file: the built-in MLP layout is recovered as flat
+        weights (native policy); any other architecture runs through its ``step``
+        (o3_agent.rs:72-80 CModule::load + agent_wrapper.rs validate_model)."""
         import torch
 
         from ..models.policies import flat_from_module, module_dims
 
         m = torch.jit.load(path, map_location="cpu")
-        obs_dim, act_dim, hidden, discrete = module_dims(m)
-        pi, vf = flat_from_module(m, discrete)
+        try:
+            obs_dim, act_dim, hidden, discrete = module_dims(m)
+            pi, vf = flat_from_module(m, discrete)
+        except Exception:  # noqa: BLE001 -- a plugin's own network
+            with open(path, "rb") as f:
+                self._set_policy(ModelBlob.from_torchscript(0, f.read()))
+            return
         self._set_policy(ModelBlob(0, {"obs_dim": obs_dim, "act_dim": act_dim, "hidden": int(hidden),
                                        "discrete": discrete}, pi.numpy(), None if vf is None else vf.numpy()))
 
     def _set_policy(self, blob: ModelBlob):
         m = blob.meta
+        if blob.is_torchscript:  # validated before it replaces the running policy
+            from ..models.ts_policy import TorchScriptPolicy
+
+            pol = TorchScriptPolicy(blob.torchscript())
+            pol.version = blob.version
+            with self._policy_lock:
+                self.policy = pol
+            return
         with self._policy_lock:
+            if getattr(self.policy, "is_torchscript", False):
+                self.policy = None
             if self.policy is None or (self.policy.obs_dim, self.policy.act_dim, self.policy.hidden) != (
                     m["obs_dim"], m["act_dim"], m["hidden"]):
                 seed = self._seed if self._seed is not None else (hash(self.agent_id) & 0x7FFFFFFF)
@@ -169,7 +187,11 @@ class RelayRLAgent:
         else:
             raise ValueError(f"server_type must be zmq, grpc or local, not {self.server_type!r}")
 
-    def _reference_actions(self, cols, vals, done: bool, next_obs=None):
+    @property
+    def _ts_policy(self) -> bool:
+        return bool(getattr(self.policy, "is_torchscript", False))
+
+    def _reference_actions(self, cols, vals, done: bool, next_obs=None, aux=None):
         """One episode as the reference agent's actions (agent_zmq.rs:458-571 / agent_grpc.rs:
         372-455): obs / act / mask as f32 tensors (the agent casts all three to Float), the
         step()'s dict as ``data`` -- ``logp_a`` and, with a value head, ``v`` -- then the terminal
@@ -179,9 +201,12 @@ class RelayRLAgent:
         acts = []
         grpc = self.server_type == "grpc"
         for i in range(len(cols)):
-            data = {"logp_a": np.array([cols.logp[i]], np.float32)}
-            if not np.isnan(vals[i]):
-                data["v"] = np.array([vals[i]], np.float32)
+            if aux is not None:  # a TorchScript policy: its step()'s whole dict (convert_generic_dict)
+                data = aux[i]
+            else:
+                data = {"logp_a": np.array([cols.logp[i]], np.float32)}
+                if not np.isnan(vals[i]):
+                    data["v"] = np.array([vals[i]], np.float32)
             acts.append(RelayRLAction(np.asarray(cols.obs[i], np.float32), np.asarray(cols.act[i], np.float32),
                                       None if cols.mask is None else np.asarray(cols.mask[i], np.float32),
                                       float(cols.rew[i]), data, False, not grpc))
@@ -194,6 +219,10 @@ class RelayRLAgent:
         return acts
 
     def _ship(self, done: bool, next_obs=None):
+        if self._ts_policy:
+            self._ship_plugin(done, next_obs)
+            return
+        self._aux.clear()
         if self.wire_format == "reference":
             vals = self._rec.val[:self._rec.n].copy()
             cols = self._rec.take(self.agent_id, self.episodes_sent, done, next_obs)
@@ -220,6 +249,36 @@ class RelayRLAgent:
             self.transport.send_trajectory_obj(cols)
         self.episodes_sent += 1
 
+    def _ship_plugin(self, done: bool, next_obs=None):
+        """A custom plugin's model is running: the episode goes out in the reference's action
+        layout -- each action with its step()'s dict, then the terminal marker whose reward is the
+        finish_path bootstrap (agent_zmq.rs:458-610) -- which is what a plugin's
+        receive_trajectory iterates over (REINFORCE.py:70-95).  Per-action RRLT frames /
+        protobuf actions carry the dicts; RRLC columns could not."""
+        vals = self._rec.val[:self._rec.n].copy()
+        aux = list(self._aux) if len(self._aux) == self._rec.n else None  # None: the model changed mid-episode
+        self._aux.clear()
+        cols = self._rec.take(self.agent_id, self.episodes_sent, done, next_obs)
+        acts = self._reference_actions(cols, vals, done, next_obs, aux)
+        if self.wire_format == "reference":
+            if self.server_type == "grpc":
+                self.transport.send_actions(acts)
+            else:
+                from ..transport.serde_pickle import reference_frame
+
+                self.transport.send_trajectory(reference_frame(acts))
+        else:
+            t = RelayRLTrajectory(self.max_traj_length, None, agent_id=self.agent_id)
+            t.seq = self.episodes_sent
+            t.actions = acts
+            if self.server_type == "zmq":
+                self.transport.send_trajectory(t.encode())
+            elif self.server_type == "grpc":
+                self.transport.send_trajectory_pb(t)
+            else:
+                self.transport.send_trajectory_obj(t)
+        self.episodes_sent += 1
+
     @property
     def traj(self) -> RelayRLTrajectory:
         """The current (unshipped) episode as reference-style actions (a copy)."""
@@ -233,6 +292,7 @@ class RelayRLAgent:
 
     def clear_episode(self) -> None:
         self._rec.n = 0
+        self._aux.clear()
 
     # ------------------------------------------------------------------ API
     def request_for_action(self, obs, mask=None, reward: float = 0.0) -> RelayRLAction:
@@ -251,6 +311,8 @@ class RelayRLAgent:
             p = self.policy
             mask_a = np.ones(p.act_dim, np.float32) if mask is None else np.asarray(mask, np.float32)
             act, data = p.step(obs_a, mask_a)
+        if getattr(p, "is_torchscript", False):
+            return self._record_plugin_step(obs_a, mask_a, act, data)
         a0 = np.asarray(act[0] if act.ndim >= 1 else act)
         logp = data.get("logp_a")
         v = data.get("v")
@@ -259,6 +321,23 @@ class RelayRLAgent:
         aux = {k: np.asarray(v[0], np.float32) for k, v in data.items()}
         action = RelayRLAction(obs_a, a0, mask_a, 0.0, aux, False, False)
         return action
+
+    def _record_plugin_step(self, obs_a, mask_a, act, data) -> RelayRLAction:
+        """A TorchScript policy's step, recorded as the reference agent does: the action tensor
+        as returned (float32) and the converted dict as the action's data."""
+        def first(v):
+            a = np.asarray(v, np.float32).reshape(-1)
+            return float(a[0]) if a.size else None
+
+        a0 = np.asarray(act, np.float32)
+        if a0.ndim > 1 and a0.shape[0] == 1:  # a batched [1, ...] step on a [1, D] observation
+            a0 = a0[0]
+        logp = data.get("logp_a")
+        v = data.get("v")
+        self._rec.record(obs_a, a0.reshape(-1), mask_a, None if logp is None else first(logp),
+                         None if v is None else first(v))
+        self._aux.append(data)
+        return RelayRLAction(obs_a, a0, mask_a, 0.0, data, False, False)
 
     def flag_last_action(self, reward: float = 0.0, done: bool = True, truncated: bool = False,
                          next_obs=None) -> None:

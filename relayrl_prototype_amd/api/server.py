@@ -68,7 +68,8 @@ class TrainingServer:
             from ..utils.checkpoint import periodic_checkpointer
 
             self._ckpt = periodic_checkpointer(checkpoint_dir, checkpoint_every)
-        self.service = LearnerService(self.algorithm, checkpoint_fn=self._ckpt)
+        self.service = LearnerService(self.algorithm, checkpoint_fn=self._ckpt,
+                                      model_path=self.cfg.get_server_model_path())
         self.service.start()
         if self.engine_spec is not None:
             if self.engine_spec.world_size > 1:

@@ -287,6 +287,10 @@ class ConfigLoader:
 
     # ------------------------------------------------------------------ setters
     def _set_algorithm_params(self, algo: str):
+        block = (self._cfg.get("algorithms") or {}).get(algo)
+        if algo not in AVAILABLE_ALGORITHMS and isinstance(block, dict):
+            # a custom plugin's own block (rf/README.md:231-253): returned as written
+            return {algo: {k: v for k, v in block.items() if not k.startswith("_")}}
         if algo not in AVAILABLE_ALGORITHMS:
             _log("[ConfigLoader - set_algorithm_params] Failed to load algorithm hyperparameters, loading defaults...")
             return None

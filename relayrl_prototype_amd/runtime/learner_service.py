@@ -18,8 +18,18 @@ from .model_store import ModelBlob, ModelStore
 
 
 class LearnerService:
-    def __init__(self, algorithm, max_queue: int = 100000, checkpoint_fn=None):
+    """``algorithm`` is a built-in (flat-weight ``get_weights()``) or any ``AlgorithmAbstract``
+    plugin (rf/README.md:156-229): a plugin's model is the TorchScript file its ``save()`` writes
+    (``save_model_path`` attribute, else ``model_path`` = the config's server model path), read
+    back after every update and published as a TorchScript-payload blob -- what the reference
+    server does (training_zmq.rs:752-785, 901-919: save_model, then the file's bytes to agents).
+    Plugins receive every upload in the reference's per-action layout (``as_reference_trajectory``)."""
+
+    def __init__(self, algorithm, max_queue: int = 100000, checkpoint_fn=None, model_path: Optional[str] = None):
         self.algorithm = algorithm
+        self.model_path = model_path
+        self.plugin = not callable(getattr(algorithm, "get_weights", None))
+        self._plugin_version = 0
         self.store = ModelStore()
         self.q: "queue.Queue" = queue.Queue(maxsize=max_queue)
         self._stop = threading.Event()
@@ -40,13 +50,33 @@ class LearnerService:
 
     # ------------------------------------------------------------------ models
     def publish_model(self) -> ModelBlob:
-        w = self.algorithm.get_weights()
-        meta = {k: w[k] for k in ("obs_dim", "act_dim", "hidden", "discrete")}
-        meta["algorithm"] = type(self.algorithm).__name__
-        blob = ModelBlob(int(w["version"]), meta, w["pi"].numpy(), None if w.get("vf") is None else w["vf"].numpy(),
-                         _ts_fn=self.algorithm.model_bytes)
+        """Publish the algorithm's current model.  Returns after a pointer swap: transports
+        deliver on their own threads (model_store.LatestWorker); the TorchScript archive of a
+        built-in is built from the blob's own weights, lazily, by whoever needs it."""
+        if self.plugin:
+            blob = self._plugin_blob()
+        else:
+            w = self.algorithm.get_weights()
+            meta = {k: w[k] for k in ("obs_dim", "act_dim", "hidden", "discrete")}
+            meta["algorithm"] = type(self.algorithm).__name__
+            blob = ModelBlob(int(w["version"]), meta, w["pi"].numpy(),
+                             None if w.get("vf") is None else w["vf"].numpy())
         self.store.publish(blob)
         return blob
+
+    def _plugin_model_file(self) -> str:
+        p = getattr(self.algorithm, "save_model_path", None) or self.model_path
+        if not p:
+            raise RuntimeError(f"plugin {type(self.algorithm).__name__} has no save_model_path and the server no "
+                               "model path: cannot locate the TorchScript its save() writes")
+        return str(p)
+
+    def _plugin_blob(self) -> ModelBlob:
+        self.algorithm.save()
+        with open(self._plugin_model_file(), "rb") as f:
+            archive = f.read()
+        self._plugin_version += 1
+        return ModelBlob.from_torchscript(self._plugin_version, archive, {"algorithm": type(self.algorithm).__name__})
 
     # ------------------------------------------------------------------ agents
     def register_agent(self, agent_id: str, info: Optional[Dict[str, Any]] = None):
@@ -54,6 +84,14 @@ class LearnerService:
             rec = self.agents.setdefault(agent_id, {"seq": -1, "last_seen": time.time(), "trajectories": 0})
             rec.update(info or {})
             rec["last_seen"] = time.time()
+
+    def forget_agents(self, agent_ids) -> None:
+        """A transport found these agents unreachable (e.g. a reference PULL gone): stop
+        tracking them; one that comes back re-registers through its handshake."""
+        with self._agents_lock:
+            for a in agent_ids:
+                if a in self.agents:
+                    self.evicted[a] = self.agents.pop(a)
 
     def stale_agents(self, timeout_s: float):
         now = time.time()
@@ -122,6 +160,10 @@ class LearnerService:
                 rec["last_seen"] = time.time()
                 rec["trajectories"] += 1
         self.received += 1
+        if self.plugin:
+            from ..types import as_reference_trajectory
+
+            traj = as_reference_trajectory(traj)
         updated = bool(self.algorithm.receive_trajectory(traj))
         if updated:
             self.updates += 1

@@ -373,18 +373,16 @@ class ReferenceGrpcAgentTransport:
             time.sleep(retry_interval_s)  # agent_grpc.rs:357 (500 ms)
 
     def _load(self, r) -> bool:
-        from ..utils.checkpoint import reference_weights_from_bytes
+        from ..runtime.model_store import blob_from_archive
 
         try:
-            w = reference_weights_from_bytes(bytes(r.model))
+            self.on_model(blob_from_archive(self.version + 1, bytes(r.model)))
         except Exception as e:  # noqa: BLE001 -- a model the agent cannot validate is skipped
             self.bad_models += 1
             print(f"[ReferenceGrpcAgentTransport] bad model: {e!r}", flush=True)
             return False
         self.version += 1
         self.server_version = int(r.version)
-        self.on_model(ModelBlob(self.version, {"obs_dim": w["obs_dim"], "act_dim": w["act_dim"],
-                                               "hidden": w["hidden"], "discrete": True}, w["pi"], w["vf"]))
         return True
 
     def send_actions(self, actions) -> bool:

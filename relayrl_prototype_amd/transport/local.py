@@ -35,6 +35,7 @@ class LocalAgentTransport:
         self.service = lookup(address)
         self.on_model = on_model
         self.agent_id = agent_id
+        self._worker = None
         self.service.register_agent(agent_id)
         self.service.store.subscribe(self._on_model)
         blob = self.service.store.latest()
@@ -42,10 +43,19 @@ class LocalAgentTransport:
             on_model(blob)
 
     def _on_model(self, blob):
-        self.on_model(blob)
+        if blob.is_torchscript:  # a plugin's archive: loaded + validated off the learner thread
+            if self._worker is None:
+                from ..runtime.model_store import LatestWorker
+
+                self._worker = LatestWorker(self.on_model, name="rrl-local-model")
+            self._worker(blob)
+        else:  # flat weights: a pointer swap / memcpy into the native policy
+            self.on_model(blob)
 
     def send_trajectory_obj(self, traj) -> bool:
         return self.service.submit(traj)
 
     def close(self):
         self.service.store.unsubscribe(self._on_model)
+        if self._worker is not None:
+            self._worker.close()

@@ -27,7 +27,7 @@ import time
 from typing import Callable, Optional
 
 from .. import _native
-from ..runtime.model_store import ModelBlob
+from ..runtime.model_store import LatestWorker, ModelBlob
 from ..types import ReferenceColumns, RelayRLTrajectory, TrajectoryColumns
 
 FMT_TORCHSCRIPT = b"TORCHSCRIPT"
@@ -41,7 +41,8 @@ def make_agent_id() -> str:
 
 class ZmqTrainingEndpoint:
     def __init__(self, service, agent_listener: str, trajectory_server: str, multiactor: bool = True,
-                 verbose: bool = False, model_push_addr: Optional[str] = None):
+                 verbose: bool = False, model_push_addr: Optional[str] = None, ref_push_timeout_ms: int = 50,
+                 ref_push_max_failures: int = 3):
         from .serde_pickle import ReferenceDeduper
 
         self.service = service
@@ -64,7 +65,17 @@ class ZmqTrainingEndpoint:
                          threading.Thread(target=self._listen_traj, daemon=True, name="rrl-zmq-traj")]
         for t in self._threads:
             t.start()
-        service.store.subscribe(self._on_model)
+        # model delivery runs on its own thread, newest-wins: ModelStore.publish returns at once
+        # and a slow or departed agent never stalls the learner (training_zmq.rs:876-934 queued
+        # into a libzmq PUSH the same way)
+        self.ref_push_timeout_ms = ref_push_timeout_ms
+        self.ref_push_max_failures = ref_push_max_failures
+        self._ref_push_failures = 0
+        self._ref_push_dead = False  # set after N failed pushes; re-armed by GET_MODEL / uploads
+        self.ref_pushes = 0
+        self.ref_push_timeouts = 0
+        self._publisher = LatestWorker(self._on_model, name="rrl-zmq-publisher")
+        service.store.subscribe(self._publisher)
         if hasattr(service, "on_evict"):
             service.on_evict(self._on_evict)
 
@@ -79,9 +90,16 @@ class ZmqTrainingEndpoint:
             for peer in [p for p in self.agents if p in ids]:
                 del self.agents[peer]
 
+    def _rearm_reference_push(self):
+        with self._lock:
+            self._ref_push_dead = False
+            self._ref_push_failures = 0
+
     def _touch_reference_agents(self):
         """A reference upload arrived: refresh every reference agent's last_seen (the upload's
-        PUSH connection carries no identity, training_zmq.rs:971-1012)."""
+        PUSH connection carries no identity, training_zmq.rs:971-1012) and re-arm a push route
+        dropped after failed sends (the agent is evidently alive)."""
+        self._rearm_reference_push()
         with self._lock:
             ref = list(self.ref_agents)
         for peer in ref:
@@ -115,6 +133,8 @@ class ZmqTrainingEndpoint:
                             self.agents[peer] = fmt
                         else:  # reference agent: updates go to its bound PULL, not the ROUTER
                             self.ref_agents.add(peer)
+                            self._ref_push_dead = False
+                            self._ref_push_failures = 0
                     self.service.register_agent(peer.decode(errors="replace"),
                                                 None if len(body) > 1 else {"exempt": True, "reference": True})
                     self.router.send([peer, b"", self._model_payload(fmt)], 5000)
@@ -173,26 +193,53 @@ class ZmqTrainingEndpoint:
         return RelayRLTrajectory.decode(f)
 
     def _on_model(self, blob: ModelBlob):
+        """Publisher thread (LatestWorker): one blob, the newest, at a time."""
         with self._lock:
             agents = list(self.agents.items())
-            push_ref = bool(self.ref_agents) and self.model_push_addr is not None
-        if push_ref:
-            if self._model_push is None:
-                self._model_push = _native.ZmtpSocket(_native.SockType.PUSH)
-                self._model_push.connect(self.model_push_addr)
-            if not self._model_push.send([blob.torchscript()], 1000):
-                self._log("model push to", self.model_push_addr, "timed out")
-        if not agents:
-            return
+            push_ref = bool(self.ref_agents) and self.model_push_addr is not None and not self._ref_push_dead
         enc = {}
-        for peer, fmt in agents:
+        for peer, fmt in agents:  # our agents first: an RRLM frame is a memcpy, no export
             if fmt not in enc:
                 enc[fmt] = blob.encode() if fmt == FMT_RRLM else blob.torchscript()
             self.router.send([peer, b"", b"MODEL", str(blob.version).encode(), enc[fmt]], 1000)
+        if push_ref:
+            self._push_reference(blob)
+
+    def _push_reference(self, blob: ModelBlob):
+        """One TorchScript frame to the reference agents' bound PULL (agent_zmq.rs:625-698),
+        built once per version.  A PUSH with no peer waits for one: after
+        ``ref_push_max_failures`` consecutive timeouts the route is dropped -- the reference
+        agents are unregistered from the learner -- until a GET_MODEL or a reference upload
+        shows one is alive again."""
+        if self._model_push is None:
+            self._model_push = _native.ZmtpSocket(_native.SockType.PUSH)
+            self._model_push.connect(self.model_push_addr)
+        if self._model_push.send([blob.torchscript()], self.ref_push_timeout_ms):
+            self.ref_pushes += 1
+            with self._lock:
+                self._ref_push_failures = 0
+            return
+        self.ref_push_timeouts += 1
+        self._log("model push to", self.model_push_addr, "timed out")
+        with self._lock:
+            self._ref_push_failures += 1
+            if self._ref_push_failures < self.ref_push_max_failures:
+                return
+            self._ref_push_dead = True
+            gone = [p.decode(errors="replace") for p in self.ref_agents]
+            self.ref_agents.clear()
+        if hasattr(self.service, "forget_agents"):
+            self.service.forget_agents(gone)
+        self._log("reference push route dropped after", self.ref_push_max_failures, "failed sends:", gone)
+
+    def flush(self, timeout_s: float = 10.0) -> bool:
+        """Wait until the newest published model has been handed to every route."""
+        return self._publisher.flush(timeout_s)
 
     def close(self):
         self._stop.set()
-        self.service.store.unsubscribe(self._on_model)
+        self.service.store.unsubscribe(self._publisher)
+        self._publisher.close()
         for t in self._threads:
             t.join(timeout=5)
         self.router.close()
@@ -336,13 +383,11 @@ class ReferenceZmqAgentTransport:
         self._thread.start()
 
     def _load(self, blob: bytes) -> ModelBlob:
-        from ..utils.checkpoint import reference_weights_from_bytes
+        from ..runtime.model_store import blob_from_archive
 
-        w = reference_weights_from_bytes(blob)
+        mb = blob_from_archive(self.version + 1, blob)
+        self.on_model(mb)  # raises if the agent cannot validate it (the version is not taken)
         self.version += 1
-        mb = ModelBlob(self.version, {"obs_dim": w["obs_dim"], "act_dim": w["act_dim"], "hidden": w["hidden"],
-                                      "discrete": True}, w["pi"], w["vf"])
-        self.on_model(mb)
         return mb
 
     def _recv_reply(self, timeout_s: float):

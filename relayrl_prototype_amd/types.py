@@ -501,6 +501,34 @@ class ReferenceColumns:
         return out
 
 
+def as_reference_trajectory(traj) -> "RelayRLTrajectory":
+    """Any upload as the reference's per-action layout, the form plugin algorithms iterate
+    (REINFORCE.py:70-95): actions with ``done=False`` and their data, each episode closed by the
+    terminal marker ``(None, None, None, last_val, done=True)`` (agent_zmq.rs:605-610).
+
+    * RelayRLTrajectory (RRLT / protobuf / reference frames): unchanged;
+    * ReferenceColumns: its rows, markers already in place;
+    * TrajectoryColumns (our agents' RRLC): rows + a marker; the marker's reward is 0 (a
+      terminal state has no future; a cut segment's V(s_T) is the plugin's to estimate --
+      agents running a plugin's model send actions with the marker already valued)."""
+    if isinstance(traj, RelayRLTrajectory):
+        return traj
+    if isinstance(traj, ReferenceColumns):
+        return traj.to_trajectory()
+    if isinstance(traj, TrajectoryColumns):
+        acts = []
+        for a in traj.get_actions():
+            acts.append(RelayRLAction(a.get_obs(), a.get_act(), a.get_mask(), a.get_rew(), a.get_data(), False,
+                                      True))
+        if len(acts):
+            acts.append(RelayRLAction(None, None, None, 0.0, None, True, False))
+        t = RelayRLTrajectory(traj.max_length, None, agent_id=traj.agent_id)
+        t.seq = traj.seq
+        t.actions = acts
+        return t
+    return traj
+
+
 class EpisodeRecorder:
     """Preallocated per-agent episode columns; one row written per ``request_for_action``."""
 

@@ -131,15 +131,25 @@ def reference_weights_from_bytes(blob: bytes) -> Dict[str, Any]:
     (+ the value net's [H*D, H, H*H, H, H, 1] for PolicyWithBaseline)."""
     import io
 
+    import re
+
+    acts = set()
     with zipfile.ZipFile(io.BytesIO(blob)) as z:
         entries = {}
         for n in z.namelist():
             parts = n.split("/")
             if len(parts) >= 2 and parts[-2] == "data" and parts[-1].isdigit():
                 entries[int(parts[-1])] = np.frombuffer(z.read(n), dtype="<f4").copy()
+            elif n.endswith("/torch/nn/modules/activation.py"):  # TorchScript source text, read not run
+                acts |= set(re.findall(r"^class (\w+)\(", z.read(n).decode("utf-8", "replace"), re.M))
     order = [entries[k] for k in sorted(entries)]
-    if len(order) < 6:
-        raise ValueError(f"a policy archive holds at least 6 storages, found {len(order)}")
+    # the layout is recognised only when it is exactly ours: ReLU activations and 6 (policy) or
+    # 12 (policy + baseline) storages -- anything else (a plugin's tanh net, extra parameters)
+    # is an arbitrary TorchScript model that the agent runs through its step()
+    if acts - {"ReLU"}:
+        raise ValueError(f"activations {sorted(acts)} are not the ReLU MLP layout")
+    if len(order) not in (6, 12):
+        raise ValueError(f"a policy archive holds 6 or 12 storages, found {len(order)}")
     s = [a.size for a in order]
     H = s[1]
     if H < 1 or s[0] % H or s[2] != H * H or s[3] != H or s[4] % H or s[5] * H != s[4]:
@@ -155,6 +165,8 @@ def reference_weights_from_bytes(blob: bytes) -> Dict[str, Any]:
         raise ValueError(f"storage sizes {sf} are not a [{D}, {H}, {H}, A] policy")
     pi = np.concatenate(first).astype(np.float32)
     vf = None
-    if len(second) == 6 and [a.size for a in second] == value_sizes:
+    if len(second) == 6:
+        if [a.size for a in second] != value_sizes:
+            raise ValueError(f"storage sizes {[a.size for a in second]} are not a [{D}, {H}, {H}, 1] baseline")
         vf = np.concatenate(second).astype(np.float32)
     return {"pi": pi, "vf": vf, "obs_dim": int(D), "act_dim": int(A), "hidden": int(H)}

@@ -64,3 +64,37 @@ def test_bench_actor_learner_deadline_keeps_the_headline():
     assert rec["value"] > 0 and rec["n_gpus"] == 2
     assert rec["actor_learner"]["error"].startswith("deadline")
     assert rec["actor_learner"]["exit_status"] == 3
+
+
+def _line(r):
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, (r.stdout, r.stderr[-2000:])
+    return json.loads(lines[0])
+
+
+_SMALL = ["--gpus", "2", "--steps", "1", "--warmup", "1", "--device", "cpu", "--num-envs", "16", "--rollout-len", "8",
+          "--vf-iters", "2", "--phase-steps", "0", "--actor-learner", "off"]
+
+
+def test_preflight_capture_failure_falls_back_to_eager_collectives():
+    """the collective preflight runs in child processes before the ranks touch the
+    device; a failed graph-capture check turns graphs off and the run still yields a valid line."""
+    r = _run(_SMALL, {"RRL_DIST_BACKEND": "gloo", "RRL_PREFLIGHT_INJECT": "capture"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _line(r)
+    assert rec["value"] > 0 and rec["graphs"] is False
+    pf = rec["preflight"]
+    assert pf["rccl_ok"] is True and pf["graphs_ok"] is False and len(pf["per_rank"]) == 2
+    assert all(p["stage"] in ("capture", "done") for p in pf["per_rank"])
+
+
+def test_preflight_collective_failure_reports_instead_of_hanging():
+    for inject, extra in (("rccl", []), ("hang", ["--preflight-deadline-s", "25"])):
+        r = _run(_SMALL + extra, {"RRL_DIST_BACKEND": "gloo", "RRL_PREFLIGHT_INJECT": inject}, timeout=200)
+        assert r.returncode != 0, (inject, r.stderr[-2000:])
+        rec = _line(r)
+        assert rec["value"] is None and rec["error"].startswith("collective preflight failed"), rec
+        assert rec["preflight"]["rccl_ok"] is False
+        if inject == "hang":
+            stages = {p["stage"] for p in rec["preflight"]["per_rank"]}
+            assert "timeout" in stages, rec["preflight"]

@@ -1,0 +1,145 @@
+"""Model delivery never stalls the learner.
+
+``ModelStore.publish`` swaps a pointer and wakes each transport's publisher thread
+(model_store.LatestWorker); the ZMQ endpoint's thread sends the newest blob to every route and
+pushes TorchScript to reference agents' bound PULL with a short timeout, dropping that route
+after a few failed sends (training_zmq.rs:876-934 queued into a libzmq PUSH and returned)."""
+import time
+
+import numpy as np
+import pytest
+
+from relayrl_prototype_amd import _native
+from relayrl_prototype_amd.api.server import TrainingServer
+from relayrl_prototype_amd.config import address
+from relayrl_prototype_amd.runtime.model_store import LatestWorker, ModelBlob, ModelStore
+from relayrl_prototype_amd.utils.checkpoint import reference_weights_from_bytes
+
+from test_api_e2e import cfgdir  # noqa: F401  (fixture)
+
+
+def _reference_handshake(srv, identity=b"AGENT_ID-ref1"):
+    """The reference agent's GET_MODEL without a format frame (agent_zmq.rs:316-442)."""
+    d = _native.ZmtpSocket(_native.SockType.DEALER, identity)
+    al = dict(srv.cfg.get_agent_listener())
+    al["host"] = "127.0.0.1"
+    d.connect(address(al))
+    assert d.send([b"", b"GET_MODEL"], 5000)
+    rep = d.recv(10000)
+    assert rep is not None
+    body = [f for f in rep[1] if f != b""]
+    reference_weights_from_bytes(body[0])  # a TorchScript archive of the MLP layout
+    return d
+
+
+def _timed_publishes(srv, n=10):
+    out = []
+    for _ in range(n):
+        srv.algorithm.version += 1
+        t0 = time.perf_counter()
+        srv.service.publish_model()
+        out.append(time.perf_counter() - t0)
+    return out
+
+
+def test_departed_reference_agent_costs_the_learner_nothing(cfgdir):  # noqa: F811
+    tmp, cfgp = cfgdir
+    srv = TrainingServer("REINFORCE", 4, 2, 10000, env_dir=str(tmp / "env"), config_path=cfgp, server_type="zmq",
+                         device="cpu")
+    try:
+        ep = srv._endpoints[0]
+        d = _reference_handshake(srv)
+        d.close()  # the agent is gone; its PULL was never bound
+        assert ep.ref_agents
+        ts = _timed_publishes(srv)
+        assert max(ts) < 5e-3, ts  # round 5: 1.03 s each
+        t_end = time.time() + 10
+        while not ep._ref_push_dead and time.time() < t_end:
+            srv.algorithm.version += 1
+            srv.service.publish_model()
+            time.sleep(0.06)
+        assert ep._ref_push_dead and not ep.ref_agents
+        assert ep.ref_push_timeouts >= ep.ref_push_max_failures
+        assert not any(a.startswith("AGENT_ID-ref1") for a in srv.service.agents)
+        # once dropped, publishing does not even try the route
+        before = ep.ref_push_timeouts
+        ts = _timed_publishes(srv, 5)
+        assert ep.flush(5) and ep.ref_push_timeouts == before
+        # a new handshake re-arms it
+        d = _reference_handshake(srv, b"AGENT_ID-ref2")
+        assert not ep._ref_push_dead and ep.ref_agents
+        d.close()
+    finally:
+        srv.close(save=False)
+
+
+def test_live_reference_agent_gets_the_newest_model_without_stalling(cfgdir):  # noqa: F811
+    tmp, cfgp = cfgdir
+    srv = TrainingServer("REINFORCE", 4, 2, 10000, env_dir=str(tmp / "env"), config_path=cfgp, server_type="zmq",
+                         device="cpu")
+    pull = _native.ZmtpSocket(_native.SockType.PULL)
+    ts_addr = dict(srv.cfg.get_train_server())
+    ts_addr["host"] = "127.0.0.1"
+    pull.bind(address(ts_addr))  # what the reference agent binds (agent_zmq.rs:625-640)
+    try:
+        ep = srv._endpoints[0]
+        d = _reference_handshake(srv)
+        g = np.random.default_rng(0)
+        pis = []
+        ts = []
+        for _ in range(10):
+            lr = srv.algorithm.learner
+            with __import__("torch").no_grad():
+                lr.pi.params.add_(__import__("torch").from_numpy(g.normal(size=lr.pi.params.shape).astype(np.float32)))
+            srv.algorithm.version += 1
+            t0 = time.perf_counter()
+            blob = srv.service.publish_model()
+            ts.append(time.perf_counter() - t0)
+            pis.append(blob.pi.copy())
+        assert np.median(ts) < 2e-3 and max(ts) < 5e-3, ts  # round 5: 31 ms (TorchScript export inline)
+        assert ep.flush(10)
+        got = []
+        while True:
+            m = pull.recv(2000)
+            if m is None:
+                break
+            got.append(reference_weights_from_bytes(m[1][0])["pi"])
+        assert got, "no model pushed"
+        # newest-wins: whatever was skipped, the last archive the agent holds is the last version
+        np.testing.assert_array_equal(got[-1], pis[-1])
+        assert ep.ref_push_timeouts == 0 and not ep._ref_push_dead
+        d.close()
+    finally:
+        pull.close()
+        srv.close(save=False)
+
+
+def test_latest_worker_collapses_to_the_newest():
+    import threading
+
+    seen = []
+    gate = threading.Event()
+
+    def slow(b):
+        gate.wait(5)
+        seen.append(b.version)
+
+    w = LatestWorker(slow)
+    st = ModelStore()
+    st.subscribe(w)
+    t0 = time.perf_counter()
+    for v in range(1, 101):
+        st.publish(ModelBlob(v, {}, np.zeros(1, np.float32)))
+    assert time.perf_counter() - t0 < 0.05  # the publisher never waits on the slow subscriber
+    gate.set()
+    assert w.flush(5)
+    assert seen[-1] == 100 and len(seen) <= 3 and w.skipped >= 97
+    w.close()
+
+
+def test_torchscript_payload_blob_round_trip():
+    b = ModelBlob.from_torchscript(7, b"PK\x03\x04 not really a zip", {"algorithm": "X"})
+    back = ModelBlob.decode(b.encode())
+    assert back.is_torchscript and back.version == 7 and back.torchscript() == b"PK\x03\x04 not really a zip"
+    with pytest.raises(ValueError):
+        ModelBlob.decode(b.encode()[:-1])
