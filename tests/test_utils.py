@@ -189,10 +189,51 @@ def test_plot_utils(tmp_path):
         d.mkdir(parents=True)
         (d / "progress.txt").write_text("Epoch\tAverageEpRet\n" + "".join(f"{i}\t{i * (s + 1)}.0\n" for i in range(5)))
     runs = get_datasets(str(tmp_path))
-    assert len(runs) == 2 and runs[0]["data"]["AverageEpRet"][4] == 4.0
-    assert get_newest_dataset(str(tmp_path)).endswith("progress.txt")
+    assert len(runs) == 2 and runs[0]["AverageEpRet"].iloc[4] == 4.0
+    assert list(runs[1]["Unit"].unique()) == [1] and (runs[0]["Performance"] == runs[0]["AverageEpRet"]).all()
+    assert get_newest_dataset(str(tmp_path), return_file_root=True).endswith("exp_s1")
+    assert list(get_newest_dataset(str(tmp_path)).columns) == ["Epoch", "AverageEpRet"]
     out = tmp_path / "curve.png"
-    make_plots([str(tmp_path)], values=["AverageEpRet"], smooth_k=2, out=str(out))
+    make_plots([str(tmp_path) + "/"], xaxis="Epoch", values=["AverageEpRet"], smooth=2, out=str(out))
+    assert out.exists() and out.stat().st_size > 1000
+
+
+def test_plot_selects_runs_by_name_from_a_logs_tree(tmp_path):
+    """prefixes, --select / --exclude, --legend, --count and --est as in the
+    reference CLI (plot.py:178-253)."""
+    import json as _json
+
+    from relayrl_prototype_amd.utils.plot import get_all_datasets, main, plot_data
+
+    logs = tmp_path / "logs"
+    for name, scale in (("relayrl-reinforce-info", 1), ("relayrl-reinforce-vf-info", 2), ("relayrl-ppo-info", 3)):
+        for seed in range(2):
+            d = logs / name / f"{name}_s{seed}"
+            d.mkdir(parents=True)
+            (d / "config.json").write_text(_json.dumps({"exp_name": name}))
+            (d / "progress.txt").write_text("Epoch\tEnvSteps\tAverageEpRet\n" + "".join(
+                f"{i}\t{1000 * i}\t{scale * i + seed}.0\n" for i in range(6)))
+    data = get_all_datasets([str(logs / "relayrl-reinforce")], verbose=False)  # a prefix: both reinforce dirs
+    assert sorted({d["Condition1"].iloc[0] for d in data}) == ["relayrl-reinforce-info", "relayrl-reinforce-vf-info"]
+    data = get_all_datasets([str(logs / "relayrl-")], select=["vf"], verbose=False)
+    assert {d["Condition1"].iloc[0] for d in data} == {"relayrl-reinforce-vf-info"} and len(data) == 2
+    data = get_all_datasets([str(logs / "relayrl-")], exclude=["vf", "ppo"], legend=["base"], verbose=False)
+    assert {d["Condition1"].iloc[0] for d in data} == {"base"}
+    assert sorted(d["Condition2"].iloc[0] for d in data) == ["base-0", "base-1"]
+    with pytest.raises(ValueError):
+        get_all_datasets([str(logs / "relayrl-")], legend=["a"], verbose=False)
+    import matplotlib
+
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+
+    fig = plt.figure()
+    conds = plot_data(get_all_datasets([str(logs / "relayrl-")], select=["reinforce"], verbose=False),
+                      xaxis="EnvSteps", value="Performance", condition="Condition2", estimator=np.max, ax=fig.gca())
+    assert len(conds) == 4  # --count: one curve per run
+    out = tmp_path / "two.png"
+    main([str(logs / "relayrl-reinforce"), "--legend", "no-vf", "vf", "-y", "AverageEpRet", "--est", "max",
+          "--smooth", "1", "--out", str(out)])
     assert out.exists() and out.stat().st_size > 1000
 
 
