@@ -25,57 +25,15 @@
 #include <vector>
 
 #include "codec.h"
+#include "pickle_vm.h"
+#include "st_tensor.h"
 
 namespace py = pybind11;
 
 namespace {
 
-constexpr int kMaxDepth = 64;
-constexpr size_t kMaxStack = 1u << 20;
-constexpr size_t kMaxMemo = 1u << 16;
-
-struct FrameError : std::runtime_error {
-  using std::runtime_error::runtime_error;
-};
-
-class Reader {
- public:
-  Reader(const uint8_t* p, size_t n) : p_(p), n_(n) {}
-  // "K b K b ... e" right after a MARK (serde's Vec<u8> chunk: up to 1000 BININT1 + APPENDS):
-  // the bytes appended to ``out`` and the run consumed; anything else leaves the position as it was
-  bool u8_run(std::string& out) {
-    size_t q = pos_;
-    const size_t start = out.size();
-    while (q + 1 < n_ && p_[q] == 0x4B) {
-      out.push_back((char)p_[q + 1]);
-      q += 2;
-    }
-    if (q < n_ && p_[q] == 0x65) {
-      pos_ = q + 1;
-      return true;
-    }
-    out.resize(start);
-    return false;
-  }
-  const uint8_t* take(size_t k) {
-    if (pos_ + k > n_) throw FrameError("truncated frame");
-    const uint8_t* out = p_ + pos_;
-    pos_ += k;
-    return out;
-  }
-  uint8_t u8() { return *take(1); }
-  template <class T>
-  T le() {
-    T v;
-    std::memcpy(&v, take(sizeof(T)), sizeof(T));
-    return v;
-  }
-
- private:
-  const uint8_t* p_;
-  size_t n_;
-  size_t pos_ = 0;
-};
+using rrl::pickle::FrameError;
+using rrl::pickle::kMaxDepth;
 
 py::object key_of(const py::object& k) {
   if (py::isinstance<py::list>(k) || py::isinstance<py::dict>(k) || py::isinstance<py::set>(k) ||
@@ -84,241 +42,83 @@ py::object key_of(const py::object& k) {
   return k;
 }
 
-bool all_u8(const std::vector<py::object>& items, size_t from) {
-  for (size_t i = from; i < items.size(); ++i) {
-    PyObject* o = items[i].ptr();
-    if (!PyLong_CheckExact(o)) return false;
-    int overflow = 0;
-    const long v = PyLong_AsLongAndOverflow(o, &overflow);
-    if (overflow || v < 0 || v > 255) return false;
+// rrl::pickle::run over Python objects (csrc/host/pickle_vm.h: the opcode loop, shared with the
+// sanitizer fuzz harness); with the u8 form an EMPTY_LIST starts as a bytearray (serde's Vec<u8>)
+struct PyBuilder {
+  using V = py::object;
+  V none() { return py::none(); }
+  V boolean(bool v) { return py::bool_(v); }
+  V small_int(int64_t v) { return py::int_(v); }
+  V long_bytes(const uint8_t* p, size_t k) {
+    PyObject* v = k ? _PyLong_FromByteArray(p, k, /*little_endian=*/1, /*is_signed=*/1) : PyLong_FromLong(0);
+    if (!v) throw py::error_already_set();
+    return py::reinterpret_steal<py::object>(v);
   }
-  return true;
-}
+  V real(double d) { return py::float_(d); }
+  V str(const char* s, size_t k) {
+    PyObject* v = PyUnicode_DecodeUTF8(s, (Py_ssize_t)k, "strict");
+    if (!v) throw py::error_already_set();
+    return py::reinterpret_steal<py::object>(v);
+  }
+  V bytes(const char* s, size_t k) { return py::bytes(s, k); }
+  V empty_list(bool u8) {
+    if (u8) return py::reinterpret_steal<py::object>(PyByteArray_FromStringAndSize("", 0));
+    return py::list();
+  }
+  V empty_dict() { return py::dict(); }
+  V empty_tuple() { return py::tuple(); }
+  V empty_set() { return py::set(); }
+  bool is_bytearray(const V& o) { return PyByteArray_Check(o.ptr()); }
+  void bytearray_append(V& o, const char* s, size_t k) {
+    const Py_ssize_t old = PyByteArray_Size(o.ptr());
+    if (PyByteArray_Resize(o.ptr(), old + (Py_ssize_t)k) != 0) throw py::error_already_set();
+    if (k) std::memcpy(PyByteArray_AsString(o.ptr()) + old, s, k);
+  }
+  void bytearray_to_list(V& o) {
+    py::list l;
+    const char* b = PyByteArray_AsString(o.ptr());
+    for (Py_ssize_t i = 0; i < PyByteArray_Size(o.ptr()); ++i) l.append(py::int_((unsigned char)b[i]));
+    o = l;
+  }
+  bool u8_value(const V& o, uint8_t& out) {
+    if (!PyLong_CheckExact(o.ptr())) return false;
+    int overflow = 0;
+    const long v = PyLong_AsLongAndOverflow(o.ptr(), &overflow);
+    if (overflow || v < 0 || v > 255) return false;
+    out = (uint8_t)v;
+    return true;
+  }
+  bool is_list(const V& o) { return PyList_Check(o.ptr()); }
+  void list_extend(V& o, const V* items, size_t k) {
+    for (size_t i = 0; i < k; ++i)
+      if (PyList_Append(o.ptr(), items[i].ptr()) != 0) throw py::error_already_set();
+  }
+  bool is_dict(const V& o) { return PyDict_Check(o.ptr()); }
+  void dict_set(V& d, const V& k, const V& v) {
+    if (PyDict_SetItem(d.ptr(), key_of(k).ptr(), v.ptr()) != 0) throw py::error_already_set();
+  }
+  bool is_set(const V& o) { return PySet_Check(o.ptr()); }
+  void set_add(V& s, const V& k) {
+    if (PySet_Add(s.ptr(), key_of(k).ptr()) != 0) throw py::error_already_set();
+  }
+  V tuple(const V* items, size_t k) {
+    py::tuple t(k);
+    for (size_t i = 0; i < k; ++i) t[i] = items[i];
+    return std::move(t);
+  }
+  V frozenset(const V* items, size_t k) {
+    py::set s;
+    for (size_t i = 0; i < k; ++i) set_add(s, items[i]);
+    return py::reinterpret_steal<py::object>(PyFrozenSet_New(s.ptr()));
+  }
+};
 
 py::object loads(const py::bytes& frame, bool u8_as_bytes) {
   char* data = nullptr;
   Py_ssize_t n = 0;
   if (PyBytes_AsStringAndSize(frame.ptr(), &data, &n) != 0) throw py::error_already_set();
-  Reader r(reinterpret_cast<const uint8_t*>(data), (size_t)n);
-  std::vector<py::object> stack;
-  std::vector<size_t> marks;
-  std::unordered_map<uint32_t, py::object> memo;
-  std::string run;  // scratch of the u8 fast form
-  auto pop_value = [&]() {
-    if (stack.empty() || (!marks.empty() && marks.back() == stack.size())) throw FrameError("stack underflow");
-    py::object v = std::move(stack.back());
-    stack.pop_back();
-    return v;
-  };
-  auto pop_mark = [&]() -> size_t {  // index of the first item above the mark
-    if (marks.empty()) throw FrameError("MARK not found");
-    const size_t m = marks.back();
-    marks.pop_back();
-    return m;
-  };
-  auto top = [&]() -> py::object& {
-    if (stack.empty() || (!marks.empty() && marks.back() == stack.size())) throw FrameError("stack underflow");
-    return stack.back();
-  };
-  // the container below the items [from, end): no MARK may sit between them
-  auto container_below = [&](size_t from) -> py::object& {
-    if (from == 0 || stack.size() < from || (!marks.empty() && marks.back() >= from)) throw FrameError("stack underflow");
-    return stack[from - 1];
-  };
-  auto as_list = [&](py::object& o) {  // a bytearray still being built as a Vec<u8> -> list of ints
-    if (u8_as_bytes && py::isinstance<py::bytearray>(o)) {
-      py::list l;
-      const char* b = PyByteArray_AsString(o.ptr());
-      for (Py_ssize_t i = 0; i < PyByteArray_Size(o.ptr()); ++i) l.append(py::int_((unsigned char)b[i]));
-      o = l;
-    }
-  };
-  // list APPEND / APPENDS onto the container, with the u8 fast form
-  auto extend_top = [&](size_t from) {
-    py::object& tgt = container_below(from);
-    if (u8_as_bytes && py::isinstance<py::bytearray>(tgt)) {
-      if (all_u8(stack, from)) {
-        std::string chunk(stack.size() - from, '\0');
-        for (size_t i = from; i < stack.size(); ++i) chunk[i - from] = (char)PyLong_AsLong(stack[i].ptr());
-        const Py_ssize_t old = PyByteArray_Size(tgt.ptr());
-        if (PyByteArray_Resize(tgt.ptr(), old + (Py_ssize_t)chunk.size()) != 0) throw py::error_already_set();
-        std::memcpy(PyByteArray_AsString(tgt.ptr()) + old, chunk.data(), chunk.size());
-        stack.resize(from);
-        return;
-      }
-      as_list(tgt);  // not a Vec<u8> after all
-    }
-    if (!py::isinstance<py::list>(tgt)) throw FrameError("expected a list on the stack");
-    py::list l = tgt.cast<py::list>();
-    for (size_t i = from; i < stack.size(); ++i) l.append(stack[i]);
-    stack.resize(from);
-  };
-  for (;;) {
-    if (stack.size() > kMaxStack || memo.size() > kMaxMemo) throw FrameError("frame too large");
-    const uint8_t op = r.u8();
-    switch (op) {
-      case 0x80: r.take(1); break;  // PROTO
-      case 0x95: r.take(8); break;  // FRAME
-      case 0x2E:                    // STOP
-        if (stack.size() != 1 || !marks.empty()) throw FrameError("bad stack at STOP");
-        return stack[0];
-      case 0x4E: stack.push_back(py::none()); break;
-      case 0x88: stack.push_back(py::bool_(true)); break;
-      case 0x89: stack.push_back(py::bool_(false)); break;
-      case 0x4B: stack.push_back(py::int_(r.u8())); break;                // BININT1
-      case 0x4D: stack.push_back(py::int_(r.le<uint16_t>())); break;      // BININT2
-      case 0x4A: stack.push_back(py::int_(r.le<int32_t>())); break;       // BININT
-      case 0x8A:                                                          // LONG1
-      case 0x8B: {                                                        // LONG4
-        int64_t k = op == 0x8A ? r.u8() : r.le<int32_t>();
-        if (k < 0 || k > 64) throw FrameError("LONG4 too large");
-        const uint8_t* b = r.take((size_t)k);
-        PyObject* v = k ? _PyLong_FromByteArray(b, (size_t)k, /*little_endian=*/1, /*is_signed=*/1) : PyLong_FromLong(0);
-        if (!v) throw py::error_already_set();
-        stack.push_back(py::reinterpret_steal<py::object>(v));
-        break;
-      }
-      case 0x47: {  // BINFLOAT (big-endian double)
-        const uint8_t* b = r.take(8);
-        uint64_t u = 0;
-        for (int i = 0; i < 8; ++i) u = (u << 8) | b[i];
-        double d;
-        std::memcpy(&d, &u, 8);
-        stack.push_back(py::float_(d));
-        break;
-      }
-      case 0x58:    // BINUNICODE
-      case 0x8C:    // SHORT_BINUNICODE
-      case 0x8D: {  // BINUNICODE8
-        const uint64_t k = op == 0x58 ? r.le<uint32_t>() : (op == 0x8C ? r.u8() : r.le<uint64_t>());
-        if (k > (uint64_t)n) throw FrameError("truncated frame");
-        const char* s = reinterpret_cast<const char*>(r.take((size_t)k));
-        PyObject* v = PyUnicode_DecodeUTF8(s, (Py_ssize_t)k, "strict");
-        if (!v) throw py::error_already_set();
-        stack.push_back(py::reinterpret_steal<py::object>(v));
-        break;
-      }
-      case 0x42:    // BINBYTES
-      case 0x43:    // SHORT_BINBYTES
-      case 0x8E: {  // BINBYTES8
-        const uint64_t k = op == 0x42 ? r.le<uint32_t>() : (op == 0x43 ? r.u8() : r.le<uint64_t>());
-        if (k > (uint64_t)n) throw FrameError("truncated frame");
-        const char* s = reinterpret_cast<const char*>(r.take((size_t)k));
-        stack.push_back(py::bytes(s, (size_t)k));
-        break;
-      }
-      case 0x28:  // MARK
-        // u8 form: a MARK that opens a pure "K b ... APPENDS" run onto a Vec<u8> being built goes
-        // straight into the bytearray, no Python int per byte (~20,000 of them per CartPole frame)
-        if (u8_as_bytes && !stack.empty() && (marks.empty() || marks.back() < stack.size()) &&
-            PyByteArray_Check(stack.back().ptr())) {
-          run.clear();
-          if (r.u8_run(run)) {
-            PyObject* ba = stack.back().ptr();
-            const Py_ssize_t old = PyByteArray_Size(ba);
-            if (PyByteArray_Resize(ba, old + (Py_ssize_t)run.size()) != 0) throw py::error_already_set();
-            if (!run.empty()) std::memcpy(PyByteArray_AsString(ba) + old, run.data(), run.size());
-            break;
-          }
-        }
-        if ((int)marks.size() >= kMaxDepth) throw FrameError("nesting too deep");
-        marks.push_back(stack.size());
-        break;
-      case 0x5D:  // EMPTY_LIST
-        if (u8_as_bytes) stack.push_back(py::reinterpret_steal<py::object>(PyByteArray_FromStringAndSize("", 0)));
-        else stack.push_back(py::list());
-        break;
-      case 0x7D: stack.push_back(py::dict()); break;
-      case 0x29: stack.push_back(py::tuple()); break;
-      case 0x8F: stack.push_back(py::set()); break;
-      case 0x61: {  // APPEND
-        if (stack.empty() || (!marks.empty() && marks.back() == stack.size())) throw FrameError("stack underflow");
-        extend_top(stack.size() - 1);
-        break;
-      }
-      case 0x65: extend_top(pop_mark()); break;  // APPENDS
-      case 0x73: {                               // SETITEM
-        py::object v = pop_value();
-        py::object k = pop_value();
-        py::object& d = top();
-        if (!py::isinstance<py::dict>(d)) throw FrameError("expected a dict on the stack");
-        d.cast<py::dict>()[key_of(k)] = v;
-        break;
-      }
-      case 0x75: {  // SETITEMS
-        const size_t m = pop_mark();
-        if ((stack.size() - m) % 2) throw FrameError("odd SETITEMS");
-        py::object& c = container_below(m);
-        if (!py::isinstance<py::dict>(c)) throw FrameError("expected a dict on the stack");
-        py::dict d = c.cast<py::dict>();
-        for (size_t i = m; i < stack.size(); i += 2) d[key_of(stack[i])] = stack[i + 1];
-        stack.resize(m);
-        break;
-      }
-      case 0x90: {  // ADDITEMS
-        const size_t m = pop_mark();
-        py::object& c = container_below(m);
-        if (!py::isinstance<py::set>(c)) throw FrameError("expected a set on the stack");
-        py::set s = c.cast<py::set>();
-        for (size_t i = m; i < stack.size(); ++i) s.add(key_of(stack[i]));
-        stack.resize(m);
-        break;
-      }
-      case 0x91: {  // FROZENSET
-        const size_t m = pop_mark();
-        py::set s;
-        for (size_t i = m; i < stack.size(); ++i) s.add(key_of(stack[i]));
-        stack.resize(m);
-        stack.push_back(py::reinterpret_steal<py::object>(PyFrozenSet_New(s.ptr())));
-        break;
-      }
-      case 0x74: {  // TUPLE
-        const size_t m = pop_mark();
-        py::tuple t(stack.size() - m);
-        for (size_t i = m; i < stack.size(); ++i) t[i - m] = stack[i];
-        stack.resize(m);
-        stack.push_back(t);
-        break;
-      }
-      case 0x85:
-      case 0x86:
-      case 0x87: {  // TUPLE1..3
-        const size_t k = op - 0x84;
-        if (stack.size() < k || (!marks.empty() && marks.back() > stack.size() - k)) throw FrameError("stack underflow");
-        py::tuple t(k);
-        for (size_t i = 0; i < k; ++i) t[i] = stack[stack.size() - k + i];
-        stack.resize(stack.size() - k);
-        stack.push_back(t);
-        break;
-      }
-      // (serde_pickle writes no memo; a memoised list is built as a list, not in the u8 form)
-      case 0x71: as_list(top()); memo[r.u8()] = top(); break;                 // BINPUT
-      case 0x72: as_list(top()); memo[r.le<uint32_t>()] = top(); break;       // LONG_BINPUT
-      case 0x94: as_list(top()); memo[(uint32_t)memo.size()] = top(); break;  // MEMOIZE
-      case 0x68:                                            // BINGET
-      case 0x6A: {                                          // LONG_BINGET
-        const uint32_t k = op == 0x68 ? r.u8() : r.le<uint32_t>();
-        auto it = memo.find(k);
-        if (it == memo.end()) throw FrameError("memo key not found");
-        stack.push_back(it->second);
-        break;
-      }
-      case 0x30:  // POP
-        if (!marks.empty() && marks.back() == stack.size()) {
-          marks.pop_back();
-        } else {
-          if (stack.empty()) throw FrameError("stack underflow");
-          stack.pop_back();
-        }
-        break;
-      case 0x31: stack.resize(pop_mark()); break;  // POP_MARK
-      default: {
-        char msg[80];
-        snprintf(msg, sizeof(msg), "opcode 0x%02x is not allowed in a trajectory frame", op);
-        throw FrameError(msg);
-      }
-    }
-  }
+  PyBuilder b;
+  return rrl::pickle::run(reinterpret_cast<const uint8_t*>(data), (size_t)n, b, u8_as_bytes);
 }
 
 void dump(const py::handle& o, std::string& out, int depth, bool bytes_u8) {
@@ -466,9 +266,8 @@ std::string byte_payload(const py::handle& data) {
 }
 
 // TensorData {shape, dtype, data: one-tensor safetensors file} -> float32 values; false if None.
-// Headers are parsed once per distinct header text per frame (every obs of a frame has the same
-// one): ``cache`` maps header bytes -> (dtype, shape, data range).
-using HeaderCache = std::unordered_map<std::string, rrl::StHeader>;
+// The bytes go through rrl::st_tensor_f32 (csrc/host/st_tensor.h, shared with the fuzz harness).
+using HeaderCache = rrl::StHeaderCache;
 bool tensor_f32(const py::handle& td, std::vector<float>& out, HeaderCache& cache) {
   if (td.is_none()) return false;
   if (!py::isinstance<py::dict>(td)) throw FrameError("TensorData must be a dict with shape / dtype / data");
@@ -489,38 +288,12 @@ bool tensor_f32(const py::handle& td, std::vector<float>& out, HeaderCache& cach
     p = owned.data();
     n = owned.size();
   }
-  if (n < 8) throw FrameError("TensorData: safetensors: file too short");
-  uint64_t hl = 0;
-  for (int i = 0; i < 8; ++i) hl |= (uint64_t)(uint8_t)p[i] << (8 * i);
-  if (hl > n - 8) throw FrameError("TensorData: safetensors: header length out of range");
-  std::string key(p + 8, (size_t)hl);
-  auto it = cache.find(key);
-  if (it == cache.end()) {
-    try {
-      it = cache.emplace(std::move(key), rrl::st_header(p + 8, (size_t)hl)).first;
-    } catch (const std::exception& e) {
-      throw FrameError(std::string("TensorData: ") + e.what());
-    }
-  }
-  const rrl::StHeader& h = it->second;
-  const size_t base = 8 + (size_t)hl;
-  // st_header guarantees 0 <= off0 <= off1 and off1 - off0 == count * dtype size
-  if (h.off0 < 0 || h.off1 < h.off0 || (uint64_t)h.off1 > n - base)
-    throw FrameError("TensorData: safetensors: bad data offsets");
-  int64_t cnt = 1;
-  for (auto s : h.shape) cnt *= s;
-  out.resize((size_t)cnt);
-  const char* r = p + base + h.off0;
-  for (int64_t i = 0; i < cnt; ++i) {
-    switch (h.dtype) {
-      case rrl::DType::Byte: out[i] = (float)(uint8_t)r[i]; break;
-      case rrl::DType::Bool: out[i] = r[i] ? 1.f : 0.f; break;
-      case rrl::DType::Short: { int16_t v; std::memcpy(&v, r + 2 * i, 2); out[i] = (float)v; break; }
-      case rrl::DType::Int: { int32_t v; std::memcpy(&v, r + 4 * i, 4); out[i] = (float)v; break; }
-      case rrl::DType::Long: { int64_t v; std::memcpy(&v, r + 8 * i, 8); out[i] = (float)v; break; }
-      case rrl::DType::Float: { float v; std::memcpy(&v, r + 4 * i, 4); out[i] = v; break; }
-      case rrl::DType::Double: { double v; std::memcpy(&v, r + 8 * i, 8); out[i] = (float)v; break; }
-    }
+  try {
+    rrl::st_tensor_f32(p, n, out, cache);
+  } catch (const FrameError&) {
+    throw;
+  } catch (const std::exception& e) {
+    throw FrameError(std::string("TensorData: ") + e.what());
   }
   return true;
 }
