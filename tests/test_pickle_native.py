@@ -314,3 +314,46 @@ def test_one_deduper_across_the_column_and_action_paths():
     assert len(kept) == len(ep2) and d2.stripped == len(ep1)
     assert sp.ReferenceDeduper._digest_cols(ReferenceColumns.decode(f12), len(ep1) + len(ep2)) == \
         sp.ReferenceDeduper._digest_actions(sp.actions_from_reference(sp.loads(f12)))
+
+
+_BIG_FRAMES = {}
+
+
+def _big_frame(n):
+    if n not in _BIG_FRAMES:
+        _BIG_FRAMES[n] = sp.reference_frame(_episode(n, np.random.default_rng(n)))
+    return _BIG_FRAMES[n]
+
+
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(st.sampled_from([8, 25, 54]), st.lists(st.tuples(st.floats(0, 1), st.integers(1, 255)), max_size=6),
+       st.floats(0.5, 1.0))
+def test_mutated_frames_up_to_64kb_match_the_reference_interpreter(n, flips, keep):
+    """real reference frames of up to ~64 KB (54 actions), byte-flipped and
+    truncated, give the interpreter's value or the interpreter's kind of error -- the frame sizes
+    where APPENDS runs, long length fields and many memo-free containers actually occur."""
+    f = bytearray(_big_frame(n))
+    assert len(f) <= 65536
+    for pos, x in flips:
+        i = min(len(f) - 1, int(pos * len(f)))
+        f[i] ^= x
+    f = bytes(f[:max(2, int(keep * len(f)))])
+    try:
+        ref = _norm(sp.loads(f))
+    except Exception as e:  # noqa: BLE001
+        ref = type(e)
+    try:
+        nat = _norm(_native.pickle_loads(f, True))
+    except Exception as e:  # noqa: BLE001
+        nat = type(e)
+    if isinstance(ref, type):
+        assert isinstance(nat, type), (ref, nat)
+        assert issubclass(nat, ValueError) == issubclass(ref, ValueError), (ref, nat)
+    else:
+        assert nat == ref
+    try:  # the column decoder on the same bytes: a value or a ValueError, never anything else
+        from relayrl_prototype_amd.types import ReferenceColumns
+
+        ReferenceColumns.decode(f)
+    except ValueError:
+        pass

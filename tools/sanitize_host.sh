@@ -1,11 +1,23 @@
 #!/bin/bash
 # Sanitizer builds of the C++ host runtime (SURVEY §5.2 -- the reference has none).
 #   tools/sanitize_host.sh           # ASan+UBSan and TSan builds, then run both
+#   tools/sanitize_host.sh fuzz N SEED_FILE...
+#                                    # ASan+UBSan build of the network-facing parsers (pickle VM,
+#                                    # TensorData reader, safetensors decoder) driven by N mutants
 # Host code only: GPU sanitizers (xnack+) are not available on the MI355X pool.
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 OUT="${ROOT}/build/sanitize"
 mkdir -p "$OUT"
+if [ "${1:-}" = "fuzz" ]; then
+  shift
+  CXX="${CXX:-g++}"
+  $CXX -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined \
+    -I "$ROOT/csrc/host" "$ROOT/csrc/host/selftest/parser_fuzz.cpp" "$ROOT/csrc/host/codec.cpp" -o "$OUT/parser_fuzz_asan"
+  echo "== parser fuzz (ASan + UBSan)"
+  ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 "$OUT/parser_fuzz_asan" "$@"
+  exit $?
+fi
 SRCS="$ROOT/csrc/host/selftest/host_selftest.cpp $ROOT/csrc/host/codec.cpp $ROOT/csrc/host/zmtp.cpp $ROOT/csrc/host/vecenv.cpp $ROOT/csrc/host/policy.cpp"
 CXX="${CXX:-g++}"
 $CXX -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined \
