@@ -26,6 +26,7 @@
 
 #include "codec.h"
 #include "pickle_vm.h"
+#include "ref_columns.h"
 #include "st_tensor.h"
 
 namespace py = pybind11;
@@ -231,105 +232,6 @@ void dump(const py::handle& o, std::string& out, int depth, bool bytes_u8) {
 }
 
 // ------------------------------------------------------------------ reference frame -> columns
-// serde enum in any serde_pickle representation -> (variant, payload) (serde_pickle.enum_variant)
-std::pair<std::string, py::object> variant(const py::handle& v) {
-  if (py::isinstance<py::str>(v)) return {v.cast<std::string>(), py::none()};
-  if (py::isinstance<py::dict>(v)) {
-    py::dict d = py::reinterpret_borrow<py::dict>(v);
-    if (d.size() == 1)
-      for (auto kv : d) return {py::str(kv.first).cast<std::string>(), py::reinterpret_borrow<py::object>(kv.second)};
-  }
-  if (py::isinstance<py::tuple>(v) || py::isinstance<py::list>(v)) {
-    py::sequence q = py::reinterpret_borrow<py::sequence>(v);
-    if ((q.size() == 1 || q.size() == 2) && py::isinstance<py::str>(q[0]))
-      return {q[0].cast<std::string>(), q.size() == 2 ? py::object(q[1]) : py::object(py::none())};
-  }
-  throw FrameError("not an enum value");
-}
-
-std::string byte_payload(const py::handle& data) {
-  if (py::isinstance<py::bytearray>(data)) {
-    return std::string(PyByteArray_AsString(data.ptr()), (size_t)PyByteArray_Size(data.ptr()));
-  }
-  if (py::isinstance<py::bytes>(data)) return data.cast<std::string>();
-  if (py::isinstance<py::list>(data) || py::isinstance<py::tuple>(data)) {
-    py::sequence q = py::reinterpret_borrow<py::sequence>(data);
-    std::string out(q.size(), '\0');
-    for (size_t i = 0; i < q.size(); ++i) {
-      const long v = q[i].cast<long>();
-      if (v < 0 || v > 255) throw FrameError("TensorData.data must be bytes or a list of u8");
-      out[i] = (char)v;
-    }
-    return out;
-  }
-  throw FrameError("TensorData.data must be bytes or a list of u8");
-}
-
-// TensorData {shape, dtype, data: one-tensor safetensors file} -> float32 values; false if None.
-// The bytes go through rrl::st_tensor_f32 (csrc/host/st_tensor.h, shared with the fuzz harness).
-using HeaderCache = rrl::StHeaderCache;
-bool tensor_f32(const py::handle& td, std::vector<float>& out, HeaderCache& cache) {
-  if (td.is_none()) return false;
-  if (!py::isinstance<py::dict>(td)) throw FrameError("TensorData must be a dict with shape / dtype / data");
-  py::dict d = py::reinterpret_borrow<py::dict>(td);
-  if (!d.contains("data")) throw FrameError("TensorData must be a dict with shape / dtype / data");
-  py::object data = d["data"];
-  std::string owned;
-  const char* p = nullptr;
-  size_t n = 0;
-  if (py::isinstance<py::bytearray>(data)) {
-    p = PyByteArray_AsString(data.ptr());
-    n = (size_t)PyByteArray_Size(data.ptr());
-  } else if (py::isinstance<py::bytes>(data)) {
-    p = PyBytes_AsString(data.ptr());
-    n = (size_t)PyBytes_Size(data.ptr());
-  } else {
-    owned = byte_payload(data);
-    p = owned.data();
-    n = owned.size();
-  }
-  try {
-    rrl::st_tensor_f32(p, n, out, cache);
-  } catch (const FrameError&) {
-    throw;
-  } catch (const std::exception& e) {
-    throw FrameError(std::string("TensorData: ") + e.what());
-  }
-  return true;
-}
-
-// one column of per-action vectors (all present rows must have the same length)
-struct Col {
-  std::vector<float> vals;
-  std::vector<uint8_t> has;
-  long width = -1;
-  void add(bool present, const std::vector<float>& v) {
-    has.push_back(present ? 1 : 0);
-    if (present) {
-      if (width < 0) {
-        width = (long)v.size();
-        // earlier absent rows: zero-filled at the new width
-        vals.assign((has.size() - 1) * (size_t)width, 0.f);
-      } else if ((long)v.size() != width) {
-        throw FrameError("ragged tensors in one frame");
-      }
-      vals.insert(vals.end(), v.begin(), v.end());
-    } else if (width >= 0) {
-      vals.insert(vals.end(), (size_t)width, 0.f);
-    }
-  }
-  py::object array(size_t n, float fill) const {
-    if (width < 0) return py::none();
-    py::array_t<float> a({(py::ssize_t)n, (py::ssize_t)width});
-    float* p = a.mutable_data();
-    std::memcpy(p, vals.data(), vals.size() * sizeof(float));
-    for (size_t i = 0; i < n; ++i)
-      if (!has[i])
-        for (long k = 0; k < width; ++k) p[i * width + k] = fill;
-    return std::move(a);
-  }
-};
-
 template <class T>
 py::array_t<T> vec_array(const std::vector<T>& v) {
   py::array_t<T> a((py::ssize_t)v.size());
@@ -337,85 +239,45 @@ py::array_t<T> vec_array(const std::vector<T>& v) {
   return a;
 }
 
-// serde_pickle(Vec<RelayRLAction>) (or a RelayRLTrajectory struct) straight to float32 columns:
-// the per-action objects of serde_pickle.actions_from_reference are never built.
+py::object col_array(const rrl::RefCol& c, size_t n, float fill) {
+  if (c.width < 0) return py::none();
+  py::array_t<float> a({(py::ssize_t)n, (py::ssize_t)c.width});
+  float* p = a.mutable_data();
+  std::memcpy(p, c.vals.data(), c.vals.size() * sizeof(float));
+  for (size_t i = 0; i < n; ++i)
+    if (!c.has[i])
+      for (long k = 0; k < c.width; ++k) p[i * c.width + k] = fill;
+  return std::move(a);
+}
+
+// serde_pickle(Vec<RelayRLAction>) (or a RelayRLTrajectory struct) straight to float32 columns,
+// decoded by the pure-C++ node-tree path (csrc/host/ref_columns.h) with the GIL RELEASED: the
+// per-action objects of serde_pickle.actions_from_reference are never built, and no Python object
+// either until the arrays below.
 py::dict reference_columns(const py::bytes& frame) {
-  py::object root = loads(frame, true);
-  if (py::isinstance<py::dict>(root)) {
-    py::dict d = root.cast<py::dict>();
-    if (d.contains("actions")) root = d["actions"];
+  char* data = nullptr;
+  Py_ssize_t len = 0;
+  if (PyBytes_AsStringAndSize(frame.ptr(), &data, &len) != 0) throw py::error_already_set();
+  rrl::RefColumns rc;
+  {
+    py::gil_scoped_release nogil;  // ``frame`` is referenced by the caller for the whole call
+    rrl::reference_columns_tree(reinterpret_cast<const uint8_t*>(data), (size_t)len, rc);
   }
-  if (py::isinstance<py::bytearray>(root) && PyByteArray_Size(root.ptr()) == 0) root = py::list();
-  if (!py::isinstance<py::list>(root) && !py::isinstance<py::tuple>(root)) throw FrameError("expected a list of actions");
-  py::sequence acts = py::reinterpret_borrow<py::sequence>(root);
-  const size_t n = acts.size();
-  Col obs, act, mask;
-  HeaderCache hc;
-  std::vector<float> rew, logp, v, tmp;
-  std::vector<uint8_t> done, has_logp, has_v;
-  rew.reserve(n);
-  for (size_t i = 0; i < n; ++i) {
-    py::handle a = acts[i];
-    if (!py::isinstance<py::dict>(a)) throw FrameError("an action must be a dict");
-    py::dict ad = py::reinterpret_borrow<py::dict>(a);
-    auto field = [&](const char* k) -> py::object { return ad.contains(k) ? py::object(ad[k]) : py::object(py::none()); };
-    bool p = tensor_f32(field("obs"), tmp, hc);
-    obs.add(p, tmp);
-    p = tensor_f32(field("act"), tmp, hc);
-    act.add(p, tmp);
-    p = tensor_f32(field("mask"), tmp, hc);
-    mask.add(p, tmp);
-    py::object r = field("rew");
-    rew.push_back(r.is_none() ? 0.f : r.cast<float>());
-    py::object dn = field("done");
-    done.push_back(!dn.is_none() && dn.cast<bool>() ? 1 : 0);
-    float lp = NAN, vv = NAN;
-    uint8_t hl = 0, hv = 0;
-    py::object data = field("data");
-    if (!data.is_none()) {
-      if (!py::isinstance<py::dict>(data)) throw FrameError("RelayRLAction.data must be a dict");
-      for (auto kv : data.cast<py::dict>()) {
-        const std::string key = py::str(kv.first).cast<std::string>();
-        if (key != "logp_a" && key != "v") continue;
-        auto var = variant(kv.second);
-        float x = NAN;
-        if (var.first == "Tensor") {
-          if (!tensor_f32(var.second, tmp, hc) || tmp.empty()) continue;
-          x = tmp[0];
-        } else if (var.first == "Float" || var.first == "Double" || var.first == "Int" || var.first == "Long" ||
-                   var.first == "Short" || var.first == "Byte") {
-          x = var.second.cast<float>();
-        } else {
-          continue;
-        }
-        if (key == "logp_a") {
-          lp = x;
-          hl = 1;
-        } else {
-          vv = x;
-          hv = 1;
-        }
-      }
-    }
-    logp.push_back(lp);
-    has_logp.push_back(hl);
-    v.push_back(vv);
-    has_v.push_back(hv);
-  }
+  const size_t n = rc.n;
   py::dict out;
   out["n"] = n;
-  out["obs"] = obs.array(n, 0.f);
-  out["has_obs"] = vec_array(obs.has);
-  out["act"] = act.array(n, 0.f);
-  out["has_act"] = vec_array(act.has);
-  out["mask"] = mask.array(n, 1.f);
-  out["has_mask"] = vec_array(mask.has);
-  out["rew"] = vec_array(rew);
-  out["done"] = vec_array(done);
-  out["logp"] = vec_array(logp);
-  out["has_logp"] = vec_array(has_logp);
-  out["v"] = vec_array(v);
-  out["has_v"] = vec_array(has_v);
+  out["obs"] = col_array(rc.obs, n, 0.f);
+  out["has_obs"] = vec_array(rc.obs.has);
+  out["act"] = col_array(rc.act, n, 0.f);
+  out["has_act"] = vec_array(rc.act.has);
+  out["mask"] = col_array(rc.mask, n, 1.f);
+  out["has_mask"] = vec_array(rc.mask.has);
+  out["rew"] = vec_array(rc.rew);
+  out["done"] = vec_array(rc.done);
+  out["logp"] = vec_array(rc.logp);
+  out["has_logp"] = vec_array(rc.has_logp);
+  out["v"] = vec_array(rc.v);
+  out["has_v"] = vec_array(rc.has_v);
   return out;
 }
 

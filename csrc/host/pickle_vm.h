@@ -51,17 +51,15 @@ class Reader {
   // the bytes appended to ``out`` and the run consumed; anything else leaves the position as it was
   bool u8_run(std::string& out) {
     size_t q = pos_;
-    const size_t start = out.size();
-    while (q + 1 < n_ && p_[q] == 0x4B) {
-      out.push_back((char)p_[q + 1]);
-      q += 2;
-    }
-    if (q < n_ && p_[q] == 0x65) {
-      pos_ = q + 1;
-      return true;
-    }
-    out.resize(start);
-    return false;
+    while (q + 1 < n_ && p_[q] == 0x4B) q += 2;  // scan first: one resize, no per-byte push
+    if (q >= n_ || p_[q] != 0x65) return false;
+    const size_t k = (q - pos_) / 2, start = out.size();
+    out.resize(start + k);
+    char* d = &out[0] + start;
+    const uint8_t* src = p_ + pos_ + 1;
+    for (size_t i = 0; i < k; ++i) d[i] = (char)src[2 * i];
+    pos_ = q + 1;
+    return true;
   }
   const uint8_t* take(size_t k) {
     if (k > n_ - pos_) throw FrameError("truncated frame");  // (pos_ <= n_ always)
@@ -90,6 +88,8 @@ typename B::V run(const uint8_t* data, size_t n, B& b, bool u8_form) {
   Reader r(data, n);
   std::vector<V> stack;
   std::vector<size_t> marks;
+  stack.reserve(64);
+  marks.reserve(kMaxDepth);
   std::unordered_map<uint32_t, V> memo;
   std::string run;  // scratch of the u8 fast form
   auto above_mark = [&](size_t k) { return !marks.empty() && marks.back() > stack.size() - k; };

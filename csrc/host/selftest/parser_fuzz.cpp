@@ -4,6 +4,7 @@
 //   * rrl::pickle::run (csrc/host/pickle_vm.h) -- the opcode loop every reference ZMQ upload
 //     reaches first (the server's decoder instantiates the same template over Python objects);
 //   * rrl::st_tensor_f32 (csrc/host/st_tensor.h) -- every TensorData payload inside those frames;
+//   * rrl::reference_columns_tree (csrc/host/ref_columns.h) -- the server's frame -> columns decoder;
 //   * rrl::st_decode / st_header (csrc/host/codec.cpp) -- the gRPC path's safetensors tensors.
 //
 // usage: parser_fuzz ITERATIONS SEED_FILE...   (seeds: real reference frames and safetensors
@@ -24,128 +25,19 @@
 #include <vector>
 
 #include "codec.h"
+#include "pickle_tree.h"
 #include "pickle_vm.h"
+#include "ref_columns.h"
 #include "st_tensor.h"
 
 namespace {
 
 using rrl::pickle::FrameError;
-
-struct Node {
-  enum Kind { None, Bool, Int, Big, Float, Str, Bytes, ByteArr, List, Dict, Tuple, Set, Frozen } k = None;
-  int64_t i = 0;
-  double f = 0;
-  std::string s;             // Str / Bytes / ByteArr / Big payload
-  std::vector<Node*> items;  // List / Tuple / Set / Frozen; Dict: key, value, key, value, ...
-};
-
-bool valid_utf8(const char* s, size_t n) {
-  size_t i = 0;
-  while (i < n) {
-    const uint8_t c = (uint8_t)s[i];
-    size_t k;
-    if (c < 0x80) k = 0;
-    else if ((c >> 5) == 6) k = 1;
-    else if ((c >> 4) == 14) k = 2;
-    else if ((c >> 3) == 30) k = 3;
-    else return false;
-    if (k > n - i - 1) return false;
-    for (size_t j = 1; j <= k; ++j)
-      if (((uint8_t)s[i + j] >> 6) != 2) return false;
-    i += k + 1;
-  }
-  return true;
-}
-
-// values are arena nodes: a memo can make a list contain itself, so nothing is reference-counted
-struct NodeBuilder {
-  using V = Node*;
-  std::vector<std::unique_ptr<Node>> arena;
-  Node* make(Node::Kind k) {
-    arena.emplace_back(new Node());
-    arena.back()->k = k;
-    return arena.back().get();
-  }
-  V none() { return make(Node::None); }
-  V boolean(bool v) {
-    Node* n = make(Node::Bool);
-    n->i = v;
-    return n;
-  }
-  V small_int(int64_t v) {
-    Node* n = make(Node::Int);
-    n->i = v;
-    return n;
-  }
-  V long_bytes(const uint8_t* p, size_t k) {
-    Node* n = make(Node::Big);
-    n->s.assign(reinterpret_cast<const char*>(p), k);
-    return n;
-  }
-  V real(double d) {
-    Node* n = make(Node::Float);
-    n->f = d;
-    return n;
-  }
-  V str(const char* s, size_t k) {
-    if (!valid_utf8(s, k)) throw FrameError("invalid UTF-8");
-    Node* n = make(Node::Str);
-    n->s.assign(s, k);
-    return n;
-  }
-  V bytes(const char* s, size_t k) {
-    Node* n = make(Node::Bytes);
-    n->s.assign(s, k);
-    return n;
-  }
-  V empty_list(bool u8) { return make(u8 ? Node::ByteArr : Node::List); }
-  V empty_dict() { return make(Node::Dict); }
-  V empty_tuple() { return make(Node::Tuple); }
-  V empty_set() { return make(Node::Set); }
-  bool is_bytearray(const V& o) { return o->k == Node::ByteArr; }
-  void bytearray_append(V& o, const char* s, size_t k) { o->s.append(s, k); }
-  void bytearray_to_list(V& o) {
-    for (unsigned char c : o->s) o->items.push_back(small_int(c));
-    o->s.clear();
-    o->k = Node::List;
-  }
-  bool u8_value(const V& o, uint8_t& out) {
-    if (o->k != Node::Int || o->i < 0 || o->i > 255) return false;
-    out = (uint8_t)o->i;
-    return true;
-  }
-  bool is_list(const V& o) { return o->k == Node::List; }
-  void list_extend(V& o, const V* items, size_t k) { o->items.insert(o->items.end(), items, items + k); }
-  bool is_dict(const V& o) { return o->k == Node::Dict; }
-  static void hashable(const V& k) {
-    if (k->k == Node::List || k->k == Node::Dict || k->k == Node::Set || k->k == Node::ByteArr)
-      throw FrameError("unhashable key");
-  }
-  void dict_set(V& d, const V& k, const V& v) {
-    hashable(k);
-    d->items.push_back(k);
-    d->items.push_back(v);
-  }
-  bool is_set(const V& o) { return o->k == Node::Set; }
-  void set_add(V& s, const V& k) {
-    hashable(k);
-    s->items.push_back(k);
-  }
-  V tuple(const V* items, size_t k) {
-    Node* n = make(Node::Tuple);
-    n->items.assign(items, items + k);
-    return n;
-  }
-  V frozenset(const V* items, size_t k) {
-    Node* n = make(Node::Frozen);
-    for (size_t i = 0; i < k; ++i) hashable(items[i]);
-    n->items.assign(items, items + k);
-    return n;
-  }
-};
+using rrl::pickle::Node;
+using rrl::pickle::NodeBuilder;
 
 struct Stats {
-  uint64_t runs = 0, accepted = 0, rejected = 0, tensors = 0, tensors_ok = 0, st_ok = 0, st_bad = 0;
+  uint64_t runs = 0, accepted = 0, rejected = 0, tensors = 0, tensors_ok = 0, st_ok = 0, st_bad = 0, columns_ok = 0;
 };
 
 // every TensorData-like {.., "data": bytes} below the root goes through the column reader
@@ -326,6 +218,13 @@ void run_all(const std::string& in, Stats& st) {
       ++st.rejected;
     }
   }
+  // the server's column decoder (ref_columns.h, the GIL-free path every reference upload takes)
+  try {
+    rrl::RefColumns rc;
+    rrl::reference_columns_tree(reinterpret_cast<const uint8_t*>(in.data()), in.size(), rc);
+    ++st.columns_ok;
+  } catch (const std::exception&) {
+  }
   // the same bytes as a safetensors file (gRPC path) and as a bare TensorData payload
   try {
     const rrl::Tensor t = rrl::st_decode(in, "tensor");
@@ -385,9 +284,9 @@ int main(int argc, char** argv) {
     run_all(cur, st);
   }
   std::printf("parser fuzz OK: %ld inputs, %llu VM runs (%llu accepted, %llu rejected), %llu tensors read "
-              "(%llu valid), st_decode %llu ok / %llu rejected, seeds decoded %llu\n",
+              "(%llu valid), st_decode %llu ok / %llu rejected, column frames %llu, seeds decoded %llu\n",
               iters, (unsigned long long)st.runs, (unsigned long long)st.accepted, (unsigned long long)st.rejected,
               (unsigned long long)st.tensors, (unsigned long long)st.tensors_ok, (unsigned long long)st.st_ok,
-              (unsigned long long)st.st_bad, (unsigned long long)seed_ok);
+              (unsigned long long)st.st_bad, (unsigned long long)st.columns_ok, (unsigned long long)seed_ok);
   return 0;
 }

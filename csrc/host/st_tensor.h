@@ -14,8 +14,13 @@
 
 namespace rrl {
 
-// header text -> parsed header; every obs of a frame carries the same one
-using StHeaderCache = std::unordered_map<std::string, StHeader>;
+// header text -> parsed header; every obs of a frame carries the same one, so the last header
+// is checked first by a byte compare (no key string built on the hit path)
+struct StHeaderCache {
+  std::unordered_map<std::string, StHeader> map;
+  const std::string* last_key = nullptr;
+  const StHeader* last = nullptr;
+};
 
 // Throws std::runtime_error on anything malformed; never reads outside [p, p + n).
 inline void st_tensor_f32(const char* p, size_t n, std::vector<float>& out, StHeaderCache& cache) {
@@ -23,10 +28,14 @@ inline void st_tensor_f32(const char* p, size_t n, std::vector<float>& out, StHe
   uint64_t hl = 0;
   for (int i = 0; i < 8; ++i) hl |= (uint64_t)(uint8_t)p[i] << (8 * i);
   if (hl > n - 8) throw std::runtime_error("safetensors: header length out of range");
-  std::string key(p + 8, (size_t)hl);
-  auto it = cache.find(key);
-  if (it == cache.end()) it = cache.emplace(std::move(key), st_header(p + 8, (size_t)hl)).first;
-  const StHeader& h = it->second;
+  if (cache.last == nullptr || cache.last_key->size() != hl || std::memcmp(cache.last_key->data(), p + 8, hl) != 0) {
+    std::string key(p + 8, (size_t)hl);
+    auto it = cache.map.find(key);
+    if (it == cache.map.end()) it = cache.map.emplace(std::move(key), st_header(p + 8, (size_t)hl)).first;
+    cache.last_key = &it->first;  // (unordered_map nodes are stable)
+    cache.last = &it->second;
+  }
+  const StHeader& h = *cache.last;
   const size_t base = 8 + (size_t)hl;
   // st_header guarantees 0 <= off0 <= off1 and off1 - off0 == count * dtype size
   if (h.off0 < 0 || h.off1 < h.off0 || (uint64_t)h.off1 > n - base)

@@ -42,7 +42,7 @@ def make_agent_id() -> str:
 class ZmqTrainingEndpoint:
     def __init__(self, service, agent_listener: str, trajectory_server: str, multiactor: bool = True,
                  verbose: bool = False, model_push_addr: Optional[str] = None, ref_push_timeout_ms: int = 50,
-                 ref_push_max_failures: int = 3):
+                 ref_push_max_failures: int = 3, decode_threads: int = 4):
         from .serde_pickle import ReferenceDeduper
 
         self.service = service
@@ -50,6 +50,10 @@ class ZmqTrainingEndpoint:
         self.ref_agents = set()   # identities that did the reference handshake
         self._model_push = None   # PUSH -> reference agents' bound PULL (lazy)
         self.dedupe = ReferenceDeduper()  # one memory for the column and the per-action decode paths
+        from concurrent.futures import ThreadPoolExecutor
+
+        self._decoders = ThreadPoolExecutor(max_workers=decode_threads, thread_name_prefix="rrl-zmq-decode")
+        self._last_touch = 0.0
         self.reference_frames = 0
         self.multiactor = multiactor
         self.verbose = verbose
@@ -99,6 +103,10 @@ class ZmqTrainingEndpoint:
         """A reference upload arrived: refresh every reference agent's last_seen (the upload's
         PUSH connection carries no identity, training_zmq.rs:971-1012) and re-arm a push route
         dropped after failed sends (the agent is evidently alive)."""
+        now = time.monotonic()
+        if now - self._last_touch < 0.5:  # liveness has a granularity of seconds: once per 0.5 s
+            return
+        self._last_touch = now
         self._rearm_reference_push()
         with self._lock:
             ref = list(self.ref_agents)
@@ -156,14 +164,24 @@ class ZmqTrainingEndpoint:
                 self._log("listener error", e)
 
     def _listen_traj(self):
+        """Receive -> decode -> (in arrival order) dedupe + submit.  Reference frames are decoded
+        to columns by C++ with the GIL released (ref_columns.h), on ``decode_threads`` workers
+        at once; the ordered second stage keeps each agent's cumulative re-sends in sequence for
+        the deduper."""
+        from collections import deque
+
+        pend = deque()  # (frame, future of its stage-1 decode or None)
         while not self._stop.is_set():
-            msg = self.pull.recv(100)
-            if msg is None:
-                continue
-            _, frames = msg
-            for f in frames:
+            msg = self.pull.recv(0 if pend else 100)
+            if msg is not None:
+                for f in msg[1]:
+                    fut = self._decoders.submit(self._decode_stage1, f) if self._is_reference(f) else None
+                    pend.append((f, fut))
+            # finish in order: everything already decoded, or (no new input) wait for the head
+            while pend and (pend[0][1] is None or pend[0][1].done() or msg is None):
+                f, fut = pend.popleft()
                 try:
-                    traj = self._decode_traj(f)
+                    traj = self._decode_traj(f, None if fut is None else fut.result())
                 except Exception as e:
                     self.bad_frames += 1
                     self._log("bad trajectory frame", e)
@@ -171,7 +189,22 @@ class ZmqTrainingEndpoint:
                 if traj is not None:
                     self.service.submit(traj)
 
-    def _decode_traj(self, f: bytes):
+    @staticmethod
+    def _is_reference(f: bytes) -> bool:
+        from . import serde_pickle
+
+        return not TrajectoryColumns.is_frame(f) and serde_pickle.is_pickle_frame(f)
+
+    @staticmethod
+    def _decode_stage1(f: bytes):
+        """Worker thread: a reference frame to columns (GIL released inside), or the exception
+        that sends it down the per-action path."""
+        try:
+            return ReferenceColumns.decode(f)
+        except ValueError as e:
+            return e
+
+    def _decode_traj(self, f: bytes, cols=None):
         from . import serde_pickle
 
         if TrajectoryColumns.is_frame(f):
@@ -179,11 +212,12 @@ class ZmqTrainingEndpoint:
         if serde_pickle.is_pickle_frame(f):
             self.reference_frames += 1
             self._touch_reference_agents()
-            try:  # natively, straight to columns (rows of a consistent shape)
-                rows = self.dedupe.new_rows(ReferenceColumns.decode(f))
+            if cols is None:
+                cols = self._decode_stage1(f)
+            if not isinstance(cols, Exception):  # natively, straight to columns
+                rows = self.dedupe.new_rows(cols)
                 return rows if len(rows) else None
-            except ValueError:  # ragged tensors / unusual encodings: the per-action path
-                pass
+            # ragged tensors / unusual encodings: the per-action path
             acts = self.dedupe.new_actions(serde_pickle.actions_from_reference(serde_pickle.loads_fast(f)))
             if not acts:
                 return None
@@ -242,6 +276,7 @@ class ZmqTrainingEndpoint:
         self._publisher.close()
         for t in self._threads:
             t.join(timeout=5)
+        self._decoders.shutdown(wait=False)
         self.router.close()
         self.pull.close()
         if self._model_push is not None:
