@@ -35,6 +35,9 @@ CXX = os.environ.get("CXX", "g++")
 
 HIP_OPS = os.path.join(PKG_DIR, "_hip_ops" + EXT)
 NATIVE = os.path.join(PKG_DIR, "_native" + EXT)
+H2GRPC = os.path.join(PKG_DIR, "_h2grpc" + EXT)
+# nghttp2 (HTTP/2 framing + HPACK) as the image ships it; the native gRPC server links it
+NGHTTP2_PREFIX = os.environ.get("RRL_NGHTTP2_PREFIX", "/opt/conda")
 
 
 def _jobs() -> int:
@@ -166,10 +169,37 @@ def build_native(verbose=False, force=False) -> str:
     return NATIVE
 
 
-def build(targets=("native", "hip"), verbose=False, force=False):
+def build_h2(verbose=False, force=False):
+    """``_h2grpc``: the native gRPC server (csrc/net/h2grpc.cpp) -- a module of its own because
+    it links nghttp2; skipped (the transport falls back to grpc.aio) where nghttp2 is absent."""
+    inc = os.path.join(NGHTTP2_PREFIX, "include")
+    lib = os.path.join(NGHTTP2_PREFIX, "lib")
+    if not os.path.exists(os.path.join(inc, "nghttp2", "nghttp2.h")) or not glob.glob(os.path.join(lib, "libnghttp2.so*")):
+        print(f"[build] nghttp2 not found under {NGHTTP2_PREFIX}: _h2grpc skipped", flush=True)
+        return None
+    ndir = os.path.join(CSRC, "net")
+    srcs = [os.path.join(ndir, "h2grpc.cpp"), os.path.join(CSRC, "bindings", "h2grpc_bind.cpp")]
+    deps = srcs + [os.path.join(ndir, "h2grpc.h")]
+    if not (force or _newer(H2GRPC, deps)):
+        return H2GRPC
+    cmd = [CXX, "-O3", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden", "-pthread", "-I", ndir, "-I", inc]
+    for i in _py_includes():
+        cmd += ["-I", i]
+    # no rpath: a search path of /opt/conda/lib would also resolve libstdc++ there (an older one);
+    # transport/h2_native.py preloads libnghttp2 (it needs libc only) by its full path instead
+    cmd += srcs + [f"-L{lib}", "-lnghttp2", "-o", H2GRPC]
+    _run(cmd, verbose)
+    return H2GRPC
+
+
+def build(targets=("native", "hip", "h2"), verbose=False, force=False):
     out = []
     if "native" in targets:
         out.append(build_native(verbose, force))
+    if "h2" in targets:
+        p = build_h2(verbose, force)
+        if p:
+            out.append(p)
     if "hip" in targets:
         out.append(build_hip(verbose, force))
     return out
@@ -177,11 +207,11 @@ def build(targets=("native", "hip"), verbose=False, force=False):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--target", choices=["all", "hip", "native"], default="all")
+    ap.add_argument("--target", choices=["all", "hip", "native", "h2"], default="all")
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
     a = ap.parse_args(argv)
-    t = ("native", "hip") if a.target == "all" else (a.target,)
+    t = ("native", "hip", "h2") if a.target == "all" else (a.target,)
     for p in build(t, verbose=a.verbose, force=a.force):
         print(p)
 

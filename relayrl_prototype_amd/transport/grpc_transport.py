@@ -156,7 +156,99 @@ def trajectory_from_pb(m, max_length: int = 1000) -> RelayRLTrajectory:
 
 
 # ---------------------------------------------------------------------- server
-class GrpcTrainingEndpoint:
+def GrpcTrainingEndpoint(service, address: str, idle_timeout_ms: int = 30, native: Optional[bool] = None, **kw):
+    """The RelayRLRoute server: the native one (C++ HTTP/2, csrc/net/h2grpc.cpp) when its module
+    loads, else grpc.aio.  ``native=True`` requires it, ``False`` forces grpc.aio;
+    RRL_GRPC_NATIVE=0 does the latter too."""
+    from .h2_native import ERROR, load
+
+    mod = load() if native is not False else None
+    if mod is not None:
+        return NativeGrpcTrainingEndpoint(service, address, idle_timeout_ms, mod, **kw)
+    if native:
+        from . import h2_native
+
+        raise RuntimeError(f"native gRPC server unavailable: {h2_native.ERROR}")
+    if native is None and ERROR is not None and "RRL_GRPC_NATIVE" not in ERROR:
+        print(f"[grpc] native server unavailable ({ERROR}); serving with grpc.aio", flush=True)
+    return AioGrpcTrainingEndpoint(service, address, idle_timeout_ms, **kw)
+
+
+class NativeGrpcTrainingEndpoint:
+    """RelayRLRoute on the native server: every RPC is parsed, queued and answered in C++ on one
+    epoll thread (h2grpc.cpp); Python only consumes the queued uploads here -- one thread,
+    decode + ``service.submit`` -- and hands each new model version to the server's model cell
+    from a publisher thread (newest-wins).  A TorchScript archive a reference-dialect poll needs
+    is built here on request (``NEED_TS``), once per version."""
+
+    def __init__(self, service, address: str, idle_timeout_ms: int, mod, max_inbox: int = 65536,
+                 max_inbox_bytes: int = 1 << 30, **_ignored):
+        from ..runtime.model_store import LatestWorker
+
+        self.service = service
+        self._mod = mod
+        addr = address.replace("tcp://", "")
+        host, port = addr.rsplit(":", 1)
+        if host in ("*", ""):
+            host = "0.0.0.0"
+        self.server = mod.GrpcServer(host, int(port), max_inbox, max_inbox_bytes, max(0, int(idle_timeout_ms)))
+        self.port = self.server.port
+        self.bad_frames = 0
+        self.rejected = 0
+        self._stop = threading.Event()
+        blob = service.store.latest()
+        if blob is not None:
+            self._set_model(blob)
+        self._publisher = LatestWorker(self._set_model, name="rrl-grpc-publisher")
+        service.store.subscribe(self._publisher)
+        self._thread = threading.Thread(target=self._consume, name="rrl-grpc-consumer", daemon=True)
+        self._thread.start()
+
+    def _set_model(self, blob):
+        self.server.set_model(int(blob.version), blob.encode(), blob._ts)
+
+    def _consume(self):
+        from ..types import TrajectoryColumns
+
+        mod = self._mod
+        while not self._stop.is_set():
+            it = self.server.recv(100)
+            if it is None:
+                continue
+            kind, body, aux = it
+            try:
+                if kind == mod.NEED_TS:
+                    blob = self.service.store.latest()
+                    if blob is not None and blob.version == aux:
+                        self.server.set_model_ts(aux, blob.torchscript())
+                    continue
+                if kind == mod.ACTIONS:
+                    traj = trajectory_from_pb(PbTrajectory.FromString(body))
+                    traj.agent_id = ""
+                else:
+                    traj = TrajectoryColumns.decode(body) if TrajectoryColumns.is_frame(body) else \
+                        RelayRLTrajectory.decode(body)
+            except Exception as e:  # noqa: BLE001 -- a bad upload is counted, the server keeps serving
+                self.bad_frames += 1
+                print(f"[grpc] bad upload: {e!r}", flush=True)
+                continue
+            self.service.submit(traj)  # blocking: a full learner queue parks the uploads in C++
+
+    def flush(self, timeout_s: float = 10.0) -> bool:
+        return self._publisher.flush(timeout_s)
+
+    def stats(self) -> dict:
+        return self.server.stats()
+
+    def close(self, grace: float = 0.5):
+        self.service.store.unsubscribe(self._publisher)
+        self._publisher.close()
+        self._stop.set()
+        self._thread.join(timeout=5)
+        self.server.close()
+
+
+class AioGrpcTrainingEndpoint:
     """The RelayRLRoute server on ``grpc.aio``: one event-loop thread serves every RPC.
 
     The thread-pool server (round 5) handed each request from grpc's polling thread to a pool
