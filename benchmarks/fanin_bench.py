@@ -52,8 +52,19 @@ def _agent_main(idx, cfg_path, transport, wait_ms, traj_size, start_at, stop_at,
     st = {"zmq": "zmq", "zmq-ref": "zmq", "grpc": "grpc"}[transport]
     wire = "reference" if transport == "zmq-ref" else "columns"
     kw = {"connection_per_upload": True, "training_port": str(train_port)} if transport == "zmq-ref" else {}
-    agent = RelayRLAgent(config_path=cfg_path, server_type=st, wire_format=wire, agent_id=f"fanin-{idx}",
-                         seed=idx, **kw)
+    for attempt in range(5):
+        try:
+            agent = RelayRLAgent(config_path=cfg_path, server_type=st, wire_format=wire, agent_id=f"fanin-{idx}",
+                                 seed=idx, **kw)
+            break
+        except RuntimeError as e:
+            # a reference agent binds its own PULL port; the parent's free_port() can be taken
+            # again (by another agent's outgoing connection) before the child binds it
+            if transport != "zmq-ref" or "already in use" not in str(e) or attempt == 4:
+                raise
+            from relayrl_prototype_amd.utils.addresses import free_port
+
+            kw["training_port"] = str(free_port())
     env = _native.VecEnv("CartPole-v1", 1, 1000 + idx, 1)
     o = np.zeros((1, 4), np.float32)
     r = np.zeros(1, np.float32)

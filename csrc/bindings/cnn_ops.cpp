@@ -56,23 +56,28 @@ int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, flo
 int rrl_pong_render(const float* state, uint8_t* obs, int N, void* stream);
 int rrl_pong_step_render(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
                          float* ep_acc, uint8_t* obs, int N, unsigned long long seed, unsigned long long step,
-                         const unsigned long long* step_base, int max_steps, int reset_all, void* stream);
-int rrl_conv_stack_fwd(const uint8_t* x, const float* hist, const uint16_t* w1, const float* b1,
+                         const unsigned long long* step_base, int max_steps, int reset_all, uint8_t* frames,
+                         int32_t* fidx, int R, void* stream);
+int rrl_pong_ring_fill(const float* state, uint8_t* frames, int32_t* fidx, int N, int R, unsigned long long step,
+                       const unsigned long long* step_base, void* stream);
+int rrl_conv_stack_fwd(const uint8_t* x, const float* hist, const uint8_t* frames, const int32_t* fidx,
+                       const uint16_t* w1, const float* b1,
                        const uint16_t* w2, const float* b2, const uint16_t* w3, const float* b3, uint16_t* y1,
                        uint16_t* y2, uint16_t* y3, int N, int max_grid, void* stream);
 int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
                   float* bias_part, int N, int grid, int variant, void* stream);
 int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
                   float* bias_part, int N, int grid, int staged, void* stream);
-int rrl_conv1_wgrad8(const uint8_t* x, const float* hist, const uint16_t* dy, float* part, float* bias_part, int N,
-                     int grid, void* stream);
+int rrl_conv1_wgrad8(const uint8_t* x, const float* hist, const uint8_t* frames, const int32_t* fidx,
+                     const uint16_t* dy, float* part, float* bias_part, int N, int grid, void* stream);
 int rrl_pong_render_hist(const float* hist, uint8_t* obs, int N, void* stream);
 int rrl_pong_head_step_render(const float* part, int splits, const float* fc_b, const float* head_params, int A,
                               uint16_t* h_out, int32_t* act, float* logp, float* value, unsigned long long sample_seed,
                               unsigned long long sample_step, const unsigned long long* sample_base, float* state,
                               float* rew, float* done, float* fin_ret, float* fin_len, float* ep_acc, uint8_t* obs,
                               int N, unsigned long long seed, unsigned long long step,
-                              const unsigned long long* step_base, int max_steps, void* stream);
+                              const unsigned long long* step_base, int max_steps, uint8_t* frames, int32_t* fidx,
+                              int R, void* stream);
 
 }
 
@@ -100,6 +105,29 @@ void rc_check(int rc, const char* what) {
               " (", (rc > 0 ? hipGetErrorString((hipError_t)rc) : "unsupported shape"), ")");
 }
 uint16_t* bf(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+
+constexpr int64_t kFrameBytes = 7056;  // one PongSynth frame in the ring (pong_render.h)
+
+// A frame-ring store written by a step launch over N envs: frames [R][N][7056] uint8, fidx [N][4]
+uint8_t* ring_store(const OptT& frames, const OptT& fidx, int64_t N, int64_t R) {
+  TORCH_CHECK(R >= 5, "frame ring: ring_slots >= 5 (a rollout's T + 4)");
+  TORCH_CHECK(R * N < (int64_t(1) << 31), "frame ring: R * N must fit int32 frame rows");
+  check(*frames, "frames", at::kByte, R * N * kFrameBytes);
+  TORCH_CHECK(fidx.has_value() && fidx->defined(), "frame ring: fidx is required with frames");
+  check(*fidx, "fidx", at::kInt, 4 * N);
+  return frames->data_ptr<uint8_t>();
+}
+
+// A frame ring read by the conv kernels for N observations: every fidx row must index a whole
+// frame of the store (its values come from pong_step / pong_ring_fill, which write rows < R * E)
+const uint8_t* ring_frames(const OptT& frames, const OptT& fidx, int64_t N) {
+  if (!frames.has_value() || !frames->defined()) return nullptr;
+  check(*frames, "frames", at::kByte, kFrameBytes);
+  TORCH_CHECK(frames->numel() % kFrameBytes == 0, "frames: whole 7056-byte frames");
+  TORCH_CHECK(fidx.has_value() && fidx->defined(), "frame ring: fidx is required with frames");
+  check(*fidx, "fidx", at::kInt, 4 * N);
+  return frames->data_ptr<uint8_t>();
+}
 
 struct Geo {
   int64_t N, H, W, C, KH, KW, S;
@@ -132,12 +160,16 @@ void conv_fwd(const Tensor& x, const Tensor& w, const Tensor& b, const Tensor& y
 // a1 [N][20][20][32], a2 [N][9][9][64], a3 [N][7][7][64] (bf16, post-ReLU).
 void conv_stack_fwd(const OptT& x, const Tensor& w1, const Tensor& b1, const Tensor& w2, const Tensor& b2,
                     const Tensor& w3, const Tensor& b3, const Tensor& y1, const Tensor& y2, const Tensor& y3,
-                    int64_t N, int64_t probe, int64_t grid, bool store12, const OptT& hist) {
+                    int64_t N, int64_t probe, int64_t grid, bool store12, const OptT& hist, const OptT& frames,
+                    const OptT& fidx) {
   TORCH_CHECK(N > 0, "conv_stack_fwd: N must be positive");
   // fused render: PongSynth frame histories [N][16] instead of s2d frames (cnn_fused.hip)
   const float* hp = opt_ptr<const float>(hist, "hist", at::kFloat, N * 16);
   const uint8_t* xp = opt_ptr<const uint8_t>(x, "x", at::kByte, N * 21 * 21 * 64);
-  TORCH_CHECK(hp || xp, "conv_stack_fwd: x (s2d frames) or hist (frame histories) is required");
+  // frame ring: the PongSynth frame store + the observations' frame rows fidx [N][4]
+  const uint8_t* fp = ring_frames(frames, fidx, N);
+  const int32_t* ip = fp ? fidx->data_ptr<int32_t>() : nullptr;
+  TORCH_CHECK(hp || xp || fp, "conv_stack_fwd: x (s2d frames), hist (frame histories) or frames + fidx is required");
   check(w1, "w1", at::kBFloat16, 32 * 256);
   check(w2, "w2", at::kBFloat16, 64 * 512);
   check(w3, "w3", at::kBFloat16, 64 * 576);
@@ -150,7 +182,7 @@ void conv_stack_fwd(const OptT& x, const Tensor& w1, const Tensor& b1, const Ten
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  rc_check(rrl_conv_stack_fwd(xp, hp, bf(w1), b1.data_ptr<float>(), bf(w2), b2.data_ptr<float>(),
+  rc_check(rrl_conv_stack_fwd(xp, hp, fp, ip, bf(w1), b1.data_ptr<float>(), bf(w2), b2.data_ptr<float>(),
                               bf(w3), b3.data_ptr<float>(), store12 ? bf(y1) : nullptr, store12 ? bf(y2) : nullptr,
                               bf(y3), (int)N,
                               probe > 0 ? -(int)((probe << 16) | (grid > 0 ? grid : cus))
@@ -194,15 +226,17 @@ void conv2_bwd(const Tensor& dy, const Tensor& w, const Tensor& xact, const Tens
 // conv1 weight + bias gradient, 8-wave kernel (cnn_fused.hip): s2d frames [N][21][21][64], da1
 // [N][400][32] -> partials [2 grid][32 * 256] and [2 grid][32]; returns the slab count (2 grid).
 int64_t conv1_wgrad8(const OptT& x, const Tensor& dy, const Tensor& part, const Tensor& bias_part, int64_t N,
-                     int64_t grid, const OptT& hist) {
+                     int64_t grid, const OptT& hist, const OptT& frames, const OptT& fidx) {
   TORCH_CHECK(N > 0 && grid > 0 && grid <= N, "conv1_wgrad8: need 0 < grid <= N");
   const float* hp = opt_ptr<const float>(hist, "hist", at::kFloat, N * 16);
   const uint8_t* xp = opt_ptr<const uint8_t>(x, "x", at::kByte, N * 441 * 64);
-  TORCH_CHECK(hp || xp, "conv1_wgrad8: x (s2d frames) or hist (frame histories) is required");
+  const uint8_t* fp = ring_frames(frames, fidx, N);
+  const int32_t* ip = fp ? fidx->data_ptr<int32_t>() : nullptr;
+  TORCH_CHECK(hp || xp || fp, "conv1_wgrad8: x (s2d frames), hist (frame histories) or frames + fidx is required");
   check(dy, "dy", at::kBFloat16, N * 400 * 32);
   check(part, "part", at::kFloat, 2 * grid * 32 * 256);
   check(bias_part, "bias_part", at::kFloat, 2 * grid * 32);
-  rc_check(rrl_conv1_wgrad8(xp, hp, bf(dy), part.data_ptr<float>(), bias_part.data_ptr<float>(), (int)N, (int)grid,
+  rc_check(rrl_conv1_wgrad8(xp, hp, fp, ip, bf(dy), part.data_ptr<float>(), bias_part.data_ptr<float>(), (int)N, (int)grid,
                             stream()),
            "conv1_wgrad8");
   return 2 * grid;
@@ -245,6 +279,8 @@ bool conv_dgrad(const Tensor& dy, const Tensor& w, const Tensor& xact, const Ten
 }
 
 int64_t gemm_splits(int64_t R, int64_t splits) { return rrl_gemm_splits((int)R, (int)splits); }
+
+
 
 int64_t conv_wgrad(const Tensor& dy, const Tensor& x, const Tensor& part, int64_t splits, int64_t N, int64_t H,
                    int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t S, int64_t Cout, const OptT& bias_part) {
@@ -469,7 +505,8 @@ int64_t pong_state_size() { return rrl_pong_state_size(); }
 
 void pong_step(const Tensor& state, const Tensor& act, const Tensor& rew, const Tensor& done, const Tensor& fin_ret,
                const Tensor& fin_len, const OptT& ep_acc, int64_t N, int64_t seed, int64_t step, int64_t max_steps,
-               bool reset_all, const OptT& step_base, const OptT& obs, const OptT& hist) {
+               bool reset_all, const OptT& step_base, const OptT& obs, const OptT& hist, const OptT& frames,
+               const OptT& fidx, int64_t ring_slots) {
   check(state, "state", at::kFloat, N * pong_state_size());
   check(act, "act", at::kInt, reset_all ? 0 : N);
   check(rew, "rew", at::kFloat, N);
@@ -478,12 +515,21 @@ void pong_step(const Tensor& state, const Tensor& act, const Tensor& rew, const 
   check(fin_len, "fin_len", at::kFloat, N);
   float* acc = opt_ptr<float>(ep_acc, "ep_acc", at::kFloat, 4 * N);
   const unsigned long long* sb = opt_ptr<const unsigned long long>(step_base, "step_base", at::kLong, 1);
+  if (frames.has_value() && frames->defined()) {  // step + ONE new frame into the frame ring (pong.hip)
+    uint8_t* fp = ring_store(frames, fidx, N, ring_slots);
+    rc_check(rrl_pong_step_render(state.data_ptr<float>(), act.data_ptr<int32_t>(), rew.data_ptr<float>(),
+                                  done.data_ptr<float>(), fin_ret.data_ptr<float>(), fin_len.data_ptr<float>(), acc,
+                                  nullptr, (int)N, (uint64_t)seed, (uint64_t)step, sb, (int)max_steps,
+                                  reset_all ? 1 : 0, fp, fidx->data_ptr<int32_t>(), (int)ring_slots, stream()),
+             "pong_step_render (frame ring)");
+    return;
+  }
   if (obs.has_value() && obs->defined()) {  // step + render in one launch (pong.hip)
     check(*obs, "obs", at::kByte, N * 84 * 84 * 4);
     rc_check(rrl_pong_step_render(state.data_ptr<float>(), act.data_ptr<int32_t>(), rew.data_ptr<float>(),
                                   done.data_ptr<float>(), fin_ret.data_ptr<float>(), fin_len.data_ptr<float>(), acc,
                                   obs->data_ptr<uint8_t>(), (int)N, (uint64_t)seed, (uint64_t)step, sb,
-                                  (int)max_steps, reset_all ? 1 : 0, stream()),
+                                  (int)max_steps, reset_all ? 1 : 0, nullptr, nullptr, 0, stream()),
              "pong_step_render");
     return;
   }
@@ -500,8 +546,8 @@ void pong_head_step(const Tensor& part, int64_t splits, const Tensor& fc_b, cons
                     const Tensor& h_out, const Tensor& act, const Tensor& logp, const Tensor& value, int64_t sample_seed,
                     int64_t sample_step, const OptT& sample_base, const Tensor& state, const Tensor& rew,
                     const Tensor& done, const Tensor& fin_ret, const Tensor& fin_len, const OptT& ep_acc,
-                    const Tensor& obs, int64_t N, int64_t seed, int64_t step, const OptT& step_base,
-                    int64_t max_steps) {
+                    const OptT& obs, int64_t N, int64_t seed, int64_t step, const OptT& step_base,
+                    int64_t max_steps, const OptT& frames, const OptT& fidx, int64_t ring_slots) {
   constexpr int64_t F = 512;
   TORCH_CHECK(A >= 1 && A <= 8 && splits >= 1 && N >= 1, "pong_head_step: 1 <= A <= 8, splits >= 1");
   check(part, "part", at::kFloat, splits * N * F);
@@ -516,7 +562,15 @@ void pong_head_step(const Tensor& part, int64_t splits, const Tensor& fc_b, cons
   check(done, "done", at::kFloat, N);
   check(fin_ret, "fin_ret", at::kFloat, N);
   check(fin_len, "fin_len", at::kFloat, N);
-  check(obs, "obs", at::kByte, N * 84 * 84 * 4);
+  uint8_t* fp = nullptr;
+  uint8_t* op = nullptr;
+  if (frames.has_value() && frames->defined()) {
+    fp = ring_store(frames, fidx, N, ring_slots);
+  } else {
+    TORCH_CHECK(obs.has_value() && obs->defined(), "pong_head_step: obs or frames + fidx is required");
+    check(*obs, "obs", at::kByte, N * 84 * 84 * 4);
+    op = obs->data_ptr<uint8_t>();
+  }
   float* acc = opt_ptr<float>(ep_acc, "ep_acc", at::kFloat, 4 * N);
   const unsigned long long* sb = opt_ptr<const unsigned long long>(step_base, "step_base", at::kLong, 1);
   const unsigned long long* ssb = opt_ptr<const unsigned long long>(sample_base, "sample_base", at::kLong, 1);
@@ -525,9 +579,20 @@ void pong_head_step(const Tensor& part, int64_t splits, const Tensor& fc_b, cons
                                      logp.data_ptr<float>(), value.data_ptr<float>(), (uint64_t)sample_seed,
                                      (uint64_t)sample_step, ssb, state.data_ptr<float>(), rew.data_ptr<float>(),
                                      done.data_ptr<float>(), fin_ret.data_ptr<float>(), fin_len.data_ptr<float>(), acc,
-                                     obs.data_ptr<uint8_t>(), (int)N, (uint64_t)seed, (uint64_t)step, sb,
-                                     (int)max_steps, stream()),
+                                     op, (int)N, (uint64_t)seed, (uint64_t)step, sb, (int)max_steps, fp,
+                                     fp ? fidx->data_ptr<int32_t>() : nullptr, (int)ring_slots, stream()),
            "pong_head_step");
+}
+
+// The frame ring rebuilt from the env state (a restore): frames of steps st - 3 .. st, fidx [N][4]
+void pong_ring_fill(const Tensor& state, const Tensor& frames, const Tensor& fidx, int64_t N, int64_t ring_slots,
+                    int64_t step, const OptT& step_base) {
+  check(state, "state", at::kFloat, N * pong_state_size());
+  uint8_t* fp = ring_store(frames, fidx, N, ring_slots);
+  const unsigned long long* sb = opt_ptr<const unsigned long long>(step_base, "step_base", at::kLong, 1);
+  rc_check(rrl_pong_ring_fill(state.data_ptr<float>(), fp, fidx.data_ptr<int32_t>(), (int)N, (int)ring_slots,
+                              (uint64_t)step, sb, stream()),
+           "pong_ring_fill");
 }
 
 // s2d observations drawn from frame histories [N][16] (the fused-render path's reference)
@@ -554,7 +619,8 @@ void register_cnn_ops(pybind11::module_& m) {
   m.def("conv_stack_fwd", &conv_stack_fwd, pybind11::arg("x"), pybind11::arg("w1"), pybind11::arg("b1"),
         pybind11::arg("w2"), pybind11::arg("b2"), pybind11::arg("w3"), pybind11::arg("b3"), pybind11::arg("y1"),
         pybind11::arg("y2"), pybind11::arg("y3"), pybind11::arg("N"), pybind11::arg("probe") = 0,
-        pybind11::arg("grid") = 0, pybind11::arg("store12") = true, pybind11::arg("hist") = pybind11::none());
+        pybind11::arg("grid") = 0, pybind11::arg("store12") = true, pybind11::arg("hist") = pybind11::none(),
+        pybind11::arg("frames") = pybind11::none(), pybind11::arg("fidx") = pybind11::none());
   m.def("conv3_bwd", &conv3_bwd, pybind11::arg("dy"), pybind11::arg("w"), pybind11::arg("xact"), pybind11::arg("dx"),
         pybind11::arg("part"), pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"),
         pybind11::arg("variant") = 0);
@@ -562,7 +628,8 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("part"), pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"),
         pybind11::arg("staged") = 0);
   m.def("conv1_wgrad8", &conv1_wgrad8, pybind11::arg("x"), pybind11::arg("dy"), pybind11::arg("part"),
-        pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"), pybind11::arg("hist") = pybind11::none());
+        pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"), pybind11::arg("hist") = pybind11::none(),
+        pybind11::arg("frames") = pybind11::none(), pybind11::arg("fidx") = pybind11::none());
   m.def("col2im_mask", &col2im_mask);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("gemm_splits", &gemm_splits);
@@ -602,14 +669,19 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("done"), pybind11::arg("fin_ret"), pybind11::arg("fin_len"), pybind11::arg("ep_acc"),
         pybind11::arg("N"), pybind11::arg("seed"), pybind11::arg("step"), pybind11::arg("max_steps"),
         pybind11::arg("reset_all"), pybind11::arg("step_base") = pybind11::none(),
-        pybind11::arg("obs") = pybind11::none(), pybind11::arg("hist") = pybind11::none());
+        pybind11::arg("obs") = pybind11::none(), pybind11::arg("hist") = pybind11::none(),
+        pybind11::arg("frames") = pybind11::none(), pybind11::arg("fidx") = pybind11::none(),
+        pybind11::arg("ring_slots") = 0);
   m.def("pong_head_step", &pong_head_step, pybind11::arg("part"), pybind11::arg("splits"), pybind11::arg("fc_b"),
         pybind11::arg("head_params"), pybind11::arg("A"), pybind11::arg("h_out"), pybind11::arg("act"),
         pybind11::arg("logp"), pybind11::arg("value"), pybind11::arg("sample_seed"), pybind11::arg("sample_step"),
         pybind11::arg("sample_base"), pybind11::arg("state"), pybind11::arg("rew"), pybind11::arg("done"),
         pybind11::arg("fin_ret"), pybind11::arg("fin_len"), pybind11::arg("ep_acc"), pybind11::arg("obs"),
         pybind11::arg("N"), pybind11::arg("seed"), pybind11::arg("step"), pybind11::arg("step_base"),
-        pybind11::arg("max_steps"));
+        pybind11::arg("max_steps"), pybind11::arg("frames") = pybind11::none(), pybind11::arg("fidx") = pybind11::none(),
+        pybind11::arg("ring_slots") = 0);
+  m.def("pong_ring_fill", &pong_ring_fill, pybind11::arg("state"), pybind11::arg("frames"), pybind11::arg("fidx"),
+        pybind11::arg("N"), pybind11::arg("ring_slots"), pybind11::arg("step"), pybind11::arg("step_base") = pybind11::none());
   m.def("pong_render", &pong_render);
   m.def("pong_render_hist", &pong_render_hist);
 }

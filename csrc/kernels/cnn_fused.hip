@@ -398,6 +398,9 @@ constexpr int kXPerT = (kXChunks + kThreads - 1) / kThreads;
 template <int V>
 struct L16 {
   static constexpr bool kPhaseA1 = (V & 16) != 0, kGrid3 = (V & 32) != 0, kRender = (V & 2) != 0;
+  // bit 64 -- frame ring: the frame's 4 frames are read from the PongSynth frame store through
+  // the observation's frame rows fidx[n][4] (pong_render.h) and interleaved into the same LDS image
+  static constexpr bool kRing = (V & 64) != 0;
   static constexpr bool kSetprio = (V & 4) != 0;  // s_setprio 1 around each role's MFMA clusters
   // static wave priority for the whole kernel (A/B): bit 1 raises the conv2 role, bit 8 the conv3 role
   static constexpr int kPrioRole2 = (V & 1) ? 2 : 0, kPrioRole3 = (V & 8) ? 2 : 0;
@@ -439,6 +442,8 @@ __device__ __forceinline__ bf16x8_t u8x8_frag(uint32_t lo, uint32_t hi) {
 struct Stack16Args {
   const uint8_t* x;
   const float* hist;  // fused render: [N][16] frame histories (x unused)
+  const uint8_t* frames;  // frame ring: [R][E][7056] frame store and the frame rows fidx[N][4] (x unused)
+  const int32_t* fidx;
   const uint16_t *w1, *w2, *w3;
   const float *b1, *b2, *b3;
   uint16_t *y1, *y2, *y3;
@@ -481,8 +486,24 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
 
   const int G = gridDim.x, n0 = blockIdx.x, N = A.N;
   uint4 rx[L::kRender ? 1 : kXPerT];
+  static_assert(kXPerT >= 2, "the ring form keeps 4 x 8 raw bytes per thread in rx[0..1]");
   auto gload = [&](size_t n) {
     if constexpr (L::kRender) return;
+    if constexpr (L::kRing) {
+      // unit tid < 882: position tid >> 1, rows 2 (tid & 1) .. + 1 of frames 0..3 (8 bytes each),
+      // kept raw until the LDS store (the loads stay in flight while this frame computes)
+      if (tid < 2 * kPongFramePos) {
+        const int4 fr = *reinterpret_cast<const int4*>(A.fidx + 4 * n);  // wave-uniform
+        const size_t off = (size_t)(tid >> 1) * 16 + 8 * (tid & 1);
+        const uint2 f0 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.x * kPongFrameBytes + off);
+        const uint2 f1 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.y * kPongFrameBytes + off);
+        const uint2 f2 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.z * kPongFrameBytes + off);
+        const uint2 f3 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.w * kPongFrameBytes + off);
+        rx[0] = make_uint4(f0.x, f0.y, f1.x, f1.y);
+        rx[1] = make_uint4(f2.x, f2.y, f3.x, f3.y);
+      }
+      return;
+    }
     const uint4* xs = reinterpret_cast<const uint4*>(A.x + n * (441 * 64));
 #pragma unroll
     for (int k = 0; k < kXPerT; ++k) {
@@ -509,6 +530,16 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
     __syncthreads();  // B0: the previous iteration's stages are done (F free, a1 / a2 buffers complete)
     if constexpr (L::kRender) {
       // (fused render: frame n is already in buffer j & 1)
+    } else if constexpr (L::kRing) {
+      if (n < N) {
+        if (tid < 2 * kPongFramePos) {  // rows 2h, 2h + 1 of position pix, interleaved across the 4 frames
+          const int pix = tid >> 1, pa = pix / 21, h = tid & 1;
+          uint8_t* d = F + (pix + (kFW - 21) * pa) * kFS + 32 * h;
+          *reinterpret_cast<uint4*>(d) = pong_interleave_row(rx[0].x, rx[0].z, rx[1].x, rx[1].z);
+          *reinterpret_cast<uint4*>(d + 16) = pong_interleave_row(rx[0].y, rx[0].w, rx[1].y, rx[1].w);
+        }
+        if (n + G < N) gload((size_t)n + G);
+      }
     } else if (n < N) {
 #pragma unroll
       for (int k = 0; k < kXPerT; ++k) {
@@ -684,7 +715,8 @@ static int launch_conv_stack_fwd(const uint8_t* x, const uint16_t* w1, const flo
 template <int V>
 static int launch_conv_stack16_fwd(const uint8_t* x, const float* hist, const uint16_t* w1, const float* b1,
                                    const uint16_t* w2, const float* b2, const uint16_t* w3, const float* b3,
-                                   uint16_t* y1, uint16_t* y2, uint16_t* y3, int N, int max_grid, hipStream_t stream) {
+                                   uint16_t* y1, uint16_t* y2, uint16_t* y3, int N, int max_grid, hipStream_t stream,
+                                   const uint8_t* frames = nullptr, const int32_t* fidx = nullptr) {
   using L = cs16::L16<V>;
   static bool attr = false;
   if (!attr) {
@@ -696,7 +728,8 @@ static int launch_conv_stack16_fwd(const uint8_t* x, const float* hist, const ui
   const int grid = N < max_grid ? N : max_grid;  // one 146-161 KB-LDS workgroup per CU
   const int lds = L::kLds;
   if (L::kRender && !hist) return -2;
-  const Stack16Args args{x, hist, w1, w2, w3, b1, b2, b3, y1, y2, y3, N};
+  if (L::kRing && (!frames || !fidx)) return -2;
+  const Stack16Args args{x, hist, frames, fidx, w1, w2, w3, b1, b2, b3, y1, y2, y3, N};
   hipLaunchKernelGGL(conv_stack16_fwd_kernel<V>, dim3(grid), dim3(cs16::kThreads), lds, stream, args);
   return (int)hipGetLastError();
 }
@@ -712,7 +745,8 @@ static bool conv_fwd16() {
   return v == 1;
 }
 
-extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const float* hist, const uint16_t* w1, const float* b1,
+extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const float* hist, const uint8_t* frames, const int32_t* fidx,
+                                  const uint16_t* w1, const float* b1,
                                   const uint16_t* w2, const float* b2, const uint16_t* w3, const float* b3,
                                   uint16_t* y1, uint16_t* y2, uint16_t* y3, int N, int max_grid, void* stream) {
   // max_grid < 0: timing probe variant -max_grid >> 16 (tools/cnn_kbench.py), grid = -max_grid & 0xffff;
@@ -720,6 +754,12 @@ extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const float* hist, const uin
   // (whatever RRL_CONV_FWD says).  hist (PongSynth frame histories [N][16]): the 16-wave kernel
   // draws the frames itself (fused render), x is not read.
   hipStream_t st = (hipStream_t)stream;
+  if (frames) {  // frame ring (frames [R][E][7056] + fidx [N][4]): the default 16-wave layout only
+    const int g = max_grid >= 0 ? max_grid : ((-max_grid) & 0xffff);
+    const int probe = max_grid >= 0 ? 64 : ((-max_grid) >> 16);
+    if (probe != 64) return -4;
+    return launch_conv_stack16_fwd<64>(nullptr, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st, frames, fidx);
+  }
   if (hist) {
     const int g = max_grid >= 0 ? max_grid : ((-max_grid) & 0xffff);
     const int probe = max_grid >= 0 ? 64 : ((-max_grid) >> 16);
@@ -1836,12 +1876,16 @@ constexpr int kXPT = (kXC + kThreads - 1) / kThreads, kYPT = (kYC + kThreads - 1
 
 // RENDER: the frames are drawn from PongSynth frame histories hist[N][16] (pong_render.h)
 // instead of read from an observation tensor
-template <bool RENDER, bool SP = false>  // SP: s_setprio 1 around each chunk's MFMAs (A/B)
+// RING: the frames are read from the PongSynth frame store through the frame rows fidx[N][4]
+// (pong_render.h) and interleaved into the observation's channel order -- the same LDS image
+template <bool RENDER, bool SP = false, bool RING = false>  // SP: s_setprio 1 around each chunk's MFMAs (A/B)
 __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const uint8_t* __restrict__ x,
                                                                         const float* __restrict__ hist,
                                                                         const uint16_t* __restrict__ dy,
                                                                         float* __restrict__ part,
-                                                                        float* __restrict__ bias_part, int N) {
+                                                                        float* __restrict__ bias_part, int N,
+                                                                        const uint8_t* __restrict__ frames = nullptr,
+                                                                        const int32_t* __restrict__ fidx = nullptr) {
   using namespace c1w;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Xi = smem;                // [21 x 28][80] frame, bf16 integers 0..255
@@ -1871,8 +1915,25 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
   uint4 rx[kXPT], ry[kYPT];
   // the next image's frame chunks: loaded (observations) or drawn (RENDER: the history row's 16
   // floats in SGPRs) into the same registers
+  static_assert(kXPT >= 4, "the ring form keeps two units of 4 x 8 raw bytes per thread");
   auto xload = [&](int n) {
-    if constexpr (RENDER) {
+    if constexpr (RING) {
+      // units u = tid, tid + 512 (< 882): position u >> 1, rows 2 (u & 1) .. + 1 of frames 0..3
+      const int4 fr = *reinterpret_cast<const int4*>(fidx + 4 * (size_t)n);  // wave-uniform
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int u = tid + kThreads * k;
+        if (u < 2 * kPongFramePos) {
+          const size_t off = (size_t)(u >> 1) * 16 + 8 * (u & 1);
+          const uint2 f0 = *reinterpret_cast<const uint2*>(frames + (size_t)fr.x * kPongFrameBytes + off);
+          const uint2 f1 = *reinterpret_cast<const uint2*>(frames + (size_t)fr.y * kPongFrameBytes + off);
+          const uint2 f2 = *reinterpret_cast<const uint2*>(frames + (size_t)fr.z * kPongFrameBytes + off);
+          const uint2 f3 = *reinterpret_cast<const uint2*>(frames + (size_t)fr.w * kPongFrameBytes + off);
+          rx[2 * k] = make_uint4(f0.x, f0.y, f1.x, f1.y);
+          rx[2 * k + 1] = make_uint4(f2.x, f2.y, f3.x, f3.y);
+        }
+      }
+    } else if constexpr (RENDER) {
       float hv[kPongHist];
       uniform_row(hist + (size_t)n * kPongHist, hv);
 #pragma unroll
@@ -1909,8 +1970,24 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
   }
   for (int n = n0; n < N; n += G) {
     __syncthreads();  // the previous image's fragment reads are done
+    if constexpr (RING) {
 #pragma unroll
-    for (int i = 0; i < kXPT; ++i) {
+      for (int k = 0; k < 2; ++k) {
+        const int u = tid + kThreads * k;
+        if (u < 2 * kPongFramePos) {  // observation chunks dy = 2h, 2h + 1 of position pix as bf16
+          const int pix = u >> 1, h = u & 1;
+          const uint4 c0 = pong_interleave_row(rx[2 * k].x, rx[2 * k].z, rx[2 * k + 1].x, rx[2 * k + 1].z);
+          const uint4 c1 = pong_interleave_row(rx[2 * k].y, rx[2 * k].w, rx[2 * k + 1].y, rx[2 * k + 1].w);
+          uint16_t* d = Xi + (pix + (kXW - 21) * (pix / 21)) * kLd + 32 * h;
+          *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(c0.x, c0.y));
+          *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(c0.z, c0.w));
+          *reinterpret_cast<uint4*>(d + 16) = u8x8_to_bf16x8(make_uint2(c1.x, c1.y));
+          *reinterpret_cast<uint4*>(d + 24) = u8x8_to_bf16x8(make_uint2(c1.z, c1.w));
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < (RING ? 0 : kXPT); ++i) {
       const int q = tid + kThreads * i;
       if (q < kXC) {
         const int pix = q >> 2;
@@ -1976,9 +2053,22 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
 
 // returns the number of partial slabs written (2 per workgroup); hist (PongSynth frame histories
 // [N][16]): the frames are drawn in the kernel, x is not read
-extern "C" int rrl_conv1_wgrad8(const uint8_t* x, const float* hist, const uint16_t* dy, float* part,
-                                float* bias_part, int N, int grid, void* stream) {
+extern "C" int rrl_conv1_wgrad8(const uint8_t* x, const float* hist, const uint8_t* frames, const int32_t* fidx,
+                                const uint16_t* dy, float* part, float* bias_part, int N, int grid, void* stream) {
   static bool attr = false;
+  if (frames) {  // frame ring: frames [R][E][7056], fidx [N][4]
+    static bool attr_ring = false;
+    if (!attr_ring) {
+      (void)hipFuncSetAttribute((const void*)conv1_wgrad8_kernel<false, false, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, c1w::kLds);
+      attr_ring = true;
+    }
+    if (N < 1 || grid < 1) return 0;
+    if (!fidx) return -2;
+    hipLaunchKernelGGL((conv1_wgrad8_kernel<false, false, true>), dim3(grid), dim3(c1w::kThreads), c1w::kLds,
+                       (hipStream_t)stream, nullptr, nullptr, dy, part, bias_part, N, frames, fidx);
+    return (int)hipGetLastError();
+  }
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)conv1_wgrad8_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               c1w::kLds);

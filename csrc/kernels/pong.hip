@@ -16,6 +16,7 @@ constexpr int kPongState = 32;  // floats per env
 // state layout
 enum : int {
   P_BX = 0, P_BY, P_VX, P_VY, P_PA, P_PO, P_SA, P_SO, P_T, P_RET,
+  P_VALID,     // distinct frames in the stack (1 after a reset .. 4): the frame ring's reset clamp
   P_HIST = 16  // 4 frames x (bx, by, pa, po)
 };
 constexpr float kPadSpeed = 2.5f, kOppSpeed = 1.6f, kMaxVy = 3.0f, kMaxVx = 3.0f;
@@ -44,6 +45,7 @@ RRL_DEV void reset_env(float* s, uint4 r) {
   s[P_PO] = 42.f;
   serve(s, r);
   for (int f = 0; f < 4; ++f) push_hist(s);
+  s[P_VALID] = 1.f;
 }
 
 // One env's step (frame-skip 4); state row written back.  Shared by pong_step_kernel (one
@@ -101,6 +103,7 @@ RRL_DEV void pong_step_state(int e, float* s, int a, float* __restrict__ rew,
     s[P_T] += 1.f;
     s[P_RET] += reward;
     push_hist(s);
+    s[P_VALID] = fminf(s[P_VALID] + 1.f, 4.f);
     const bool over = s[P_SA] >= 21.f || s[P_SO] >= 21.f || (max_steps > 0 && s[P_T] >= (float)max_steps);
     rew[e] = reward;
     done[e] = over ? 1.f : 0.f;
@@ -202,14 +205,73 @@ __global__ void pong_render_kernel(const float* __restrict__ state, uint8_t* __r
   *reinterpret_cast<uint4*>(obs + t * 16) = pong_render_chunk(state + (size_t)e * kPongState + P_HIST, q);
 }
 
+// Frame-ring output of a step launch (pong_render.h): frames [R][N][7056] and the frame rows of
+// each env's new observation, fidx[N][4] (oldest first); frames == nullptr: no ring
+struct RingOut {
+  uint8_t* frames;
+  int32_t* fidx;
+  int R;
+};
+
+RRL_DEV long long pong_abs_step(uint32_t lo, uint32_t hi, const unsigned long long* base) {
+  unsigned long long st = ((unsigned long long)hi << 32) | lo;
+  if (base) st += *base;
+  return (long long)st;
+}
+
+// Env e's workgroup (grid = N envs, state already stepped in LDS) writes the newest frame of its
+// history into slot st and the observation's 4 frame rows: frame f is the one of step st - (3 - f),
+// clamped to the env's last reset (P_VALID distinct frames), so a reset needs no re-render of older
+// slots -- which the earlier observations of the same rollout still read.
+RRL_DEV void pong_ring_write(const RingOut& ro, int e, int N, const float* ss, uint32_t* rows, long long st) {
+  const float* h3 = ss + P_HIST + 12;  // the newest frame (bx, by, pa, po)
+  const int t = threadIdx.x;
+  if (t < kPongHW) rows[t] = pong_frame_row_flags(h3[1], h3[2], h3[3], t);
+  if (t < 4) {
+    const int valid = (int)ss[P_VALID];
+    const int age = min(3 - t, max(valid, 1) - 1);
+    ro.fidx[4 * (size_t)e + t] = pong_ring_slot(st - age, ro.R) * N + e;
+  }
+  __syncthreads();
+  uint8_t* fo = ro.frames + ((size_t)pong_ring_slot(st, ro.R) * N + e) * kPongFrameBytes;
+  for (int q = t; q < kPongFramePos; q += blockDim.x)
+    *reinterpret_cast<uint4*>(fo + 16 * q) = pong_frame_chunk(h3[0], rows, q);
+}
+
+// The ring rebuilt from the env state alone (a restored checkpoint / elastic snapshot): the 4-frame
+// stack IS a function of the 16-float history, so frames 0..3 of every env are drawn into slots
+// st - 3 .. st and the observation points at them.  One workgroup per env.
+__global__ void __launch_bounds__(256) pong_ring_fill_kernel(const float* __restrict__ state, RingOut ro,
+                                                             uint32_t step_lo, uint32_t step_hi,
+                                                             const unsigned long long* __restrict__ step_base) {
+  __shared__ uint32_t rows[4][kPongHW];
+  __shared__ float hv[kPongHist];
+  const int e = blockIdx.x, N = gridDim.x, t = threadIdx.x;
+  if (t < kPongHist) hv[t] = state[(size_t)e * kPongState + P_HIST + t];
+  __syncthreads();
+  const long long st = pong_abs_step(step_lo, step_hi, step_base);
+  for (int q = t; q < 4 * kPongHW; q += 256) {
+    const int f = q / kPongHW, y = q - f * kPongHW;
+    rows[f][y] = pong_frame_row_flags(hv[4 * f + 1], hv[4 * f + 2], hv[4 * f + 3], y);
+  }
+  if (t < 4) ro.fidx[4 * (size_t)e + t] = pong_ring_slot(st - 3 + t, ro.R) * N + e;
+  __syncthreads();
+  for (int q = t; q < 4 * kPongFramePos; q += 256) {
+    const int f = q / kPongFramePos, p = q - f * kPongFramePos;
+    uint8_t* fo = ro.frames + ((size_t)pong_ring_slot(st - 3 + f, ro.R) * N + e) * kPongFrameBytes;
+    *reinterpret_cast<uint4*>(fo + 16 * p) = pong_frame_chunk(hv[4 * f], rows[f], p);
+  }
+}
+
 // Step + render in one launch: workgroup e steps env e on one thread (the physics is a short
 // serial chain) and renders its 1,764 chunks on all 256 threads from the new history in LDS.
 // One launch per env step instead of two, and the tiny step kernel's own launch / drain is gone.
+template <bool RING>
 __global__ void __launch_bounds__(256, 8) pong_step_render_kernel(
     float* __restrict__ state, const int32_t* __restrict__ act, float* __restrict__ rew, float* __restrict__ done,
     float* __restrict__ fin_ret, float* __restrict__ fin_len, float* __restrict__ ep_acc, uint8_t* __restrict__ obs,
     uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps, int reset_all,
-    const unsigned long long* __restrict__ step_base) {
+    const unsigned long long* __restrict__ step_base, RingOut ro) {
   constexpr int kChunks = kPongHW * kPongHW * 4 / 16;
   __shared__ float ss[kPongState];
   __shared__ uint32_t rows[kPongHW];
@@ -224,6 +286,10 @@ __global__ void __launch_bounds__(256, 8) pong_step_render_kernel(
                     step_base);
   __syncthreads();
   if (t < kPongState) state[(size_t)e * kPongState + t] = ss[t];
+  if constexpr (RING) {  // one new frame + the observation's frame rows
+    pong_ring_write(ro, e, gridDim.x, ss, rows, pong_abs_step(step_lo, step_hi, step_base));
+    return;
+  }
   const float* hist = ss + P_HIST;
   // the render is VALU-bound (every chunk re-tested its row against 12 objects): the row tests
   // once per row here, the chunks then read them (21 chunks per row)
@@ -240,11 +306,12 @@ __global__ void __launch_bounds__(256, 8) pong_step_render_kernel(
 // (a2c_rollout_row_streamed: bitwise the a2c_head_kernel result), thread 0 steps the physics
 // with it, and the workgroup renders the new frame stack -- one launch instead of head + step
 // (the head launch was ~10 us per rollout step at 2,048 envs, mostly its fixed cost).
-template <int AMAX, bool WLDS>
+template <int AMAX, bool WLDS, bool RING = false>
 __global__ void __launch_bounds__(256, 8) pong_head_step_render_kernel(
     HeadArgs ha, float* __restrict__ state, float* __restrict__ rew, float* __restrict__ done,
     float* __restrict__ fin_ret, float* __restrict__ fin_len, float* __restrict__ ep_acc, uint8_t* __restrict__ obs,
-    uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps, const unsigned long long* __restrict__ step_base) {
+    uint2 key, uint32_t step_lo, uint32_t step_hi, int max_steps, const unsigned long long* __restrict__ step_base,
+    RingOut ro) {
   constexpr int kChunks = kPongHW * kPongHW * 4 / 16;
   __shared__ float ss[kPongState];
   __shared__ uint32_t rows[kPongHW];
@@ -274,6 +341,10 @@ __global__ void __launch_bounds__(256, 8) pong_head_step_render_kernel(
     pong_step_state(e, ss, pick_s, rew, done, fin_ret, fin_len, ep_acc, key, step_lo, step_hi, max_steps, 0, step_base);
   __syncthreads();
   if (t < kPongState) state[(size_t)e * kPongState + t] = ss[t];
+  if constexpr (RING) {
+    pong_ring_write(ro, e, gridDim.x, ss, rows, pong_abs_step(step_lo, step_hi, step_base));
+    return;
+  }
   const float* hist = ss + P_HIST;
   if (t < kPongHW) rows[t] = pong_row_flags(hist, t);
   __syncthreads();
@@ -300,14 +371,32 @@ int rrl_pong_step(float* state, const int32_t* act, float* rew, float* done, flo
   return (int)hipGetLastError();
 }
 
+// frames != nullptr: the frame-ring form (frames [R][N][7056], fidx [N][4]; obs unused)
 int rrl_pong_step_render(float* state, const int32_t* act, float* rew, float* done, float* fin_ret, float* fin_len,
                          float* ep_acc, uint8_t* obs, int N, unsigned long long seed, unsigned long long step,
-                         const unsigned long long* step_base, int max_steps, int reset_all, void* stream_) {
+                         const unsigned long long* step_base, int max_steps, int reset_all, uint8_t* frames,
+                         int32_t* fidx, int R, void* stream_) {
   hipStream_t st = (hipStream_t)stream_;
   if (N < 1) return 0;
+  if (frames && (!fidx || R < 5)) return -1;
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
-  hipLaunchKernelGGL(pong_step_render_kernel, dim3(N), dim3(256), 0, st, state, act, rew, done, fin_ret, fin_len,
-                     ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, reset_all, step_base);
+  const RingOut ro{frames, fidx, R};
+  if (frames)
+    hipLaunchKernelGGL(pong_step_render_kernel<true>, dim3(N), dim3(256), 0, st, state, act, rew, done, fin_ret, fin_len,
+                       ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, reset_all, step_base, ro);
+  else
+    hipLaunchKernelGGL(pong_step_render_kernel<false>, dim3(N), dim3(256), 0, st, state, act, rew, done, fin_ret, fin_len,
+                       ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, reset_all, step_base, ro);
+  return (int)hipGetLastError();
+}
+
+// the ring rebuilt from the env state (restore): frames of steps st - 3 .. st and fidx [N][4]
+int rrl_pong_ring_fill(const float* state, uint8_t* frames, int32_t* fidx, int N, int R, unsigned long long step,
+                       const unsigned long long* step_base, void* stream_) {
+  if (N < 1) return 0;
+  if (!frames || !fidx || R < 5) return -1;
+  hipLaunchKernelGGL(pong_ring_fill_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream_, state, RingOut{frames, fidx, R},
+                     (uint32_t)step, (uint32_t)(step >> 32), step_base);
   return (int)hipGetLastError();
 }
 
@@ -341,8 +430,11 @@ int rrl_pong_head_step_render(const float* part, int splits, const float* fc_b, 
                               unsigned long long sample_step, const unsigned long long* sample_base, float* state,
                               float* rew, float* done, float* fin_ret, float* fin_len, float* ep_acc, uint8_t* obs,
                               int N, unsigned long long seed, unsigned long long step,
-                              const unsigned long long* step_base, int max_steps, void* stream_) {
+                              const unsigned long long* step_base, int max_steps, uint8_t* frames, int32_t* fidx,
+                              int R, void* stream_) {
   if (N < 1 || A < 1 || A > 8 || splits < 1 || !part || !fc_b || !h_out) return -1;
+  if (frames && (!fidx || R < 5)) return -1;
+  const RingOut ro{frames, fidx, R};
   HeadArgs a = {};
   a.part = part;
   a.splits = splits;
@@ -364,12 +456,16 @@ int rrl_pong_head_step_render(const float* part, int splits, const float* fc_b, 
   a.step_base = sample_base;
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
   const char* wl_env = getenv("RRL_PONG_HEAD_WLDS");
-  if (wl_env && wl_env[0] == '1') {  // the head weights through LDS (A/B)
+  if (frames) {  // frame ring: one new frame per env
+    hipLaunchKernelGGL((pong_head_step_render_kernel<8, false, true>), dim3(N), dim3(256), 0, (hipStream_t)stream_, a, state,
+                       rew, done, fin_ret, fin_len, ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps,
+                       step_base, ro);
+  } else if (wl_env && wl_env[0] == '1') {  // the head weights through LDS (A/B)
     hipLaunchKernelGGL((pong_head_step_render_kernel<8, true>), dim3(N), dim3(256), 0, (hipStream_t)stream_, a, state, rew, done,
-                       fin_ret, fin_len, ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, step_base);
+                       fin_ret, fin_len, ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, step_base, ro);
   } else {
     hipLaunchKernelGGL((pong_head_step_render_kernel<8, false>), dim3(N), dim3(256), 0, (hipStream_t)stream_, a, state, rew, done,
-                       fin_ret, fin_len, ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, step_base);
+                       fin_ret, fin_len, ep_acc, obs, key, (uint32_t)step, (uint32_t)(step >> 32), max_steps, step_base, ro);
   }
   return (int)hipGetLastError();
 }

@@ -58,4 +58,70 @@ RRL_DEV uint4 pong_render_chunk(const float* h, int q) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// ----------------------------------------------------------------------------- frame ring
+// The 4-frame stack of consecutive observations shares 3 frames, so the ring path renders ONE
+// frame per env step into a frame store and describes an observation by the store rows of its 4
+// frames (fidx[n][4], oldest first) -- 7 KB written per env step instead of 28 KB, and the
+// frames of a rollout (T + 3 per env) are small enough to stay in the 256 MB MALL between the
+// forward and the conv1 weight gradient that re-read them.
+//
+// A stored frame is one 84 x 84 image in space-to-depth order: frame[a][b][dy][dx] (y = 4a + dy,
+// x = 4b + dx), 441 positions x 16 bytes, so the 16-byte chunk of position (a, b) is the 4 x 4
+// block the observation's 64 channels interleave across frames (obs[a][b][dy][dx][f]).
+constexpr int kPongFrameBytes = 7056;  // 441 x 16
+constexpr int kPongFramePos = 441;
+
+// the row-flag bits of one frame (bit 0 ball, 1 agent paddle, 2 opponent paddle, 3 wall):
+// the same float comparisons as pong_row_flags / pong_render_chunk, so frames are bitwise the
+// corresponding bytes of the 4-frame render
+RRL_DEV uint32_t pong_frame_row_flags(float by, float pa, float po, int y) {
+  const float fy = (float)y + 0.5f;
+  uint32_t m = (fy < kTop || fy >= kBot) ? 8u : 0u;
+  if (fy >= by && fy < by + kBall) m |= 1u;
+  if (fabsf(fy - pa) < kPadHalf) m |= 2u;
+  if (fabsf(fy - po) < kPadHalf) m |= 4u;
+  return m;
+}
+
+// 16-byte chunk of s2d position pos (0 .. 440) of one frame with ball x bx, from its 84 row flags
+RRL_DEV uint4 pong_frame_chunk(float bx, const uint32_t* rows, int pos) {
+  const int a = pos / 21, b = pos - 21 * a;
+  uint32_t w[4];
+#pragma unroll
+  for (int dy = 0; dy < 4; ++dy) {
+    const uint32_t m = rows[4 * a + dy];
+    const bool wall = (m >> 3) & 1u;
+    if ((m & 7u) == 0u) {
+      w[dy] = wall ? 0x64646464u : 0u;
+      continue;
+    }
+    uint32_t v4 = 0u;
+#pragma unroll
+    for (int px = 0; px < 4; ++px) {
+      const float fx = (float)(4 * b + px) + 0.5f;
+      uint32_t v = wall ? 100u : 0u;
+      if ((m & 2u) && fx >= kAgentX && fx < kAgentX + kPadW) v = 255u;
+      if ((m & 4u) && fx >= kOppX && fx < kOppX + kPadW) v = 255u;
+      if ((m & 1u) && fx >= bx && fx < bx + kBall) v = 255u;
+      v4 |= v << (8 * px);
+    }
+    w[dy] = v4;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Observation bytes from the frame ring: the 8-byte pieces (rows dy0, dy0 + 1 of one position) of
+// frames 0..3 -> the two 16-byte s2d chunks (dy0, dy0 + 1) of the observation, whose byte
+// 4 dx + f is frame f's pixel dx: a 4 x 4 byte transpose per row
+__host__ __device__ __forceinline__ uint4 pong_interleave_row(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  const uint32_t o0 = (a & 0xffu) | ((b & 0xffu) << 8) | ((c & 0xffu) << 16) | (d << 24);
+  const uint32_t o1 = ((a >> 8) & 0xffu) | (b & 0xff00u) | ((c & 0xff00u) << 8) | ((d & 0xff00u) << 16);
+  const uint32_t o2 = ((a >> 16) & 0xffu) | ((b >> 8) & 0xff00u) | (c & 0xff0000u) | ((d & 0xff0000u) << 8);
+  const uint32_t o3 = (a >> 24) | ((b >> 16) & 0xff00u) | ((c >> 8) & 0xff0000u) | (d & 0xff000000u);
+  return make_uint4(o0, o1, o2, o3);
+}
+
+// store row of a frame slot: frames are [R slots][N envs][7056 B]
+RRL_DEV int pong_ring_slot(long long k, int R) { return (int)(((k % R) + R) % R); }
+
 }  // namespace rrl

@@ -26,7 +26,7 @@ OBS_SHAPE = (21, 21, 64)
 NHWC_SHAPE = (84, 84, 4)
 STATE = 32
 HW = 84
-BX, BY, VX, VY, PA, PO, SA, SO, T, RET = range(10)
+BX, BY, VX, VY, PA, PO, SA, SO, T, RET, VALID = range(11)  # VALID: distinct frames in the stack (1..4)
 HIST = 16
 TOP, BOT, PAD_HALF, BALL = 2.0, 82.0, 5.0, 2.0
 AGENT_X, OPP_X, PAD_W = 76.0, 6.0, 2.0
@@ -91,6 +91,7 @@ class PongRef:
         self._serve(s, idx, r)
         for _ in range(4):
             self._push_hist(s, idx)
+        s[idx, VALID] = 1.0
 
     def reset(self):
         rows = np.arange(self.N, dtype=np.uint32)
@@ -152,6 +153,7 @@ class PongRef:
         s[:, T] += 1
         s[:, RET] += reward
         self._push_hist(s, np.arange(N))
+        s[:, VALID] = np.minimum(s[:, VALID] + f32(1), f32(4))
         over = (s[:, SA] >= 21) | (s[:, SO] >= 21) | ((self.max_steps > 0) & (s[:, T] >= self.max_steps))
         fin_ret = np.where(over, s[:, RET], 0).astype(f32)
         fin_len = np.where(over, s[:, T], 0).astype(f32)
@@ -187,6 +189,50 @@ class PongRef:
         return obs
 
 
+FRAME_BYTES = 7056  # one 84 x 84 frame in s2d order [21][21][4][4] (pong_render.h)
+
+
+class FrameRing:
+    """The frame store of the frame-ring observation path (csrc/kernels/pong_render.h): ``R``
+    slots of one frame per env, ``frames`` [R, N, 7056] uint8.  Each env step renders ONE new
+    frame (slot ``step mod R``); an observation is the int32 row [4] of its frames' store rows
+    (``slot * N + env``, oldest first).  ``R >= T + 4`` keeps every frame of a rollout's
+    observations (steps t0 - 3 .. t0 + T) alive until the update has read them."""
+
+    def __init__(self, num_envs: int, slots: int, device):
+        if slots < 5:
+            raise ValueError("a frame ring needs >= 5 slots (rollout_len + 4)")
+        self.N, self.R = int(num_envs), int(slots)
+        self.frames = torch.zeros(self.R * self.N * FRAME_BYTES, dtype=torch.uint8, device=device)
+
+    def obs(self, fidx: torch.Tensor) -> "FrameRingObs":
+        return FrameRingObs(self.frames, fidx)
+
+    def gather_s2d(self, fidx: torch.Tensor) -> torch.Tensor:
+        """The observations [n, 21, 21, 64] the frame rows ``fidx`` [n, 4] describe (tests)."""
+        fr = self.frames.view(-1, 441, 4, 4)[fidx.long()]            # [n, f, pos, dy, dx]
+        return fr.permute(0, 2, 3, 4, 1).reshape(-1, 21, 21, 64).contiguous()
+
+
+class FrameRingObs:
+    """A batch of observations as frame rows ``fidx`` [n, 4] into a ``FrameRing``'s store: what
+    ``DeviceNatureCNN`` takes in place of an s2d uint8 tensor (slicing gives sub-batches)."""
+    __slots__ = ("frames", "fidx")
+
+    def __init__(self, frames: torch.Tensor, fidx: torch.Tensor):
+        self.frames, self.fidx = frames, fidx.reshape(-1, 4)
+
+    @property
+    def shape(self):
+        return (self.fidx.shape[0], 4)
+
+    def contiguous(self):
+        return FrameRingObs(self.frames, self.fidx.contiguous())
+
+    def __getitem__(self, sl):
+        return FrameRingObs(self.frames, self.fidx[sl])
+
+
 class DevicePong:
     """Kernel-driven batch of PongSynth envs on one device."""
 
@@ -220,10 +266,16 @@ class DevicePong:
     def advance(self, k: int):
         self.h.counter_add(self.step_t, int(k))
 
-    def reset(self, obs_out: torch.Tensor = None, hist_out: torch.Tensor = None):
+    def reset(self, obs_out: torch.Tensor = None, hist_out: torch.Tensor = None, ring=None):
         """Reset every env; the first observation is rendered into ``obs_out`` ([N, 21, 21, 64]) or,
-        for the fused-render path, only its frame history goes to ``hist_out`` ([N, 16])."""
-        if hist_out is not None:
+        for the fused-render path, only its frame history goes to ``hist_out`` ([N, 16]); ``ring``
+        (a ``FrameRing`` and its fidx row [N, 4]): the reset frame into the ring."""
+        if ring is not None:
+            fr, fidx = ring
+            self.h.pong_step(self.state, self._dummy_act, self.rew, self.done, self.fin_ret, self.fin_len, None,
+                             self.N, self.seed, 0, self.max_steps, True, self.step_t, frames=fr.frames, fidx=fidx,
+                             ring_slots=fr.R)
+        elif hist_out is not None:
             self.h.pong_step(self.state, self._dummy_act, self.rew, self.done, self.fin_ret, self.fin_len, None,
                              self.N, self.seed, 0, self.max_steps, True, self.step_t, hist=hist_out)
         else:
@@ -231,36 +283,50 @@ class DevicePong:
                              self.N, self.seed, 0, self.max_steps, True, self.step_t, obs=obs_out)
         self.advance(1)
 
+    def ring_fill(self, ring, fidx: torch.Tensor):
+        """Rebuild the frame ring's last 4 frames and the current observation's frame rows from the
+        env state alone (after a checkpoint / snapshot restore): the observation produced by the
+        last step is step ``step_t - 1``."""
+        self.h.pong_ring_fill(self.state, ring.frames, fidx, self.N, ring.R, -1, self.step_t)
+
     def episode_stats(self):
         """(episodes, sum return, sum length, sum return^2) over all envs since the last reset."""
         return self.ep_acc.double().sum(0)
 
     def step_head(self, part, splits: int, fc_b, head_params, A: int, h_out, act_out, logp_out, value_out,
                   sample_seed: int, sample_step: int, sample_base, obs_out, rew_out=None, done_out=None,
-                  offset: int = None):
+                  offset: int = None, ring=None):
         """The policy head fused in front of one env step (pong.hip ``pong_head_step_render_kernel``):
         from the fc split-K partials ``part`` of this step's observations, write the hidden units
         (``h_out``), sample the actions (``act_out`` / ``logp_out`` / ``value_out``, bitwise what
-        ``DeviceNatureCNN.act`` gives), step every env with them and render ``obs_out``."""
+        ``DeviceNatureCNN.act`` gives), step every env with them and render ``obs_out`` -- or, with
+        ``ring`` (a ``FrameRing``), the one new frame into the ring and the frame rows to ``obs_out``
+        ([N, 4] int32)."""
         rew = self.rew if rew_out is None else rew_out
         done = self.done if done_out is None else done_out
+        rk = {} if ring is None else {"frames": ring.frames, "fidx": obs_out, "ring_slots": ring.R}
         self.h.pong_head_step(part, int(splits), fc_b, head_params, int(A), h_out, act_out, logp_out, value_out,
                               int(sample_seed), int(sample_step), sample_base, self.state, rew, done, self.fin_ret,
-                              self.fin_len, self.ep_acc, obs_out, self.N, self.seed, 0 if offset is None else int(offset),
-                              self.step_t, self.max_steps)
+                              self.fin_len, self.ep_acc, None if ring is not None else obs_out, self.N, self.seed,
+                              0 if offset is None else int(offset), self.step_t, self.max_steps, **rk)
         if offset is None:
             self.advance(1)
         return rew, done
 
     def step(self, act: torch.Tensor, obs_out: torch.Tensor = None, rew_out=None, done_out=None, offset: int = None,
-             hist_out: torch.Tensor = None):
+             hist_out: torch.Tensor = None, ring=None):
         """One env step.  Without ``offset`` the device counter is advanced after the step;
         with it (graph-captured rollouts) the caller advances once per rollout.  ``hist_out``
         ([N, 16]) instead of ``obs_out``: physics only, the new frame histories written for a
-        fused-render conv stack (no 57 MB observation write per step at 2,048 envs)."""
+        fused-render conv stack (no 57 MB observation write per step at 2,048 envs).  ``ring`` (a
+        ``FrameRing``): one new frame per env into the ring, the frame rows to ``obs_out`` ([N, 4])."""
         rew = self.rew if rew_out is None else rew_out
         done = self.done if done_out is None else done_out
-        if hist_out is not None:  # physics (one thread per env) + the 64-byte history row
+        if ring is not None:  # physics + ONE new frame (7 KB instead of the 28 KB stack)
+            self.h.pong_step(self.state, act, rew, done, self.fin_ret, self.fin_len, self.ep_acc, self.N, self.seed,
+                             0 if offset is None else int(offset), self.max_steps, False, self.step_t,
+                             frames=ring.frames, fidx=obs_out, ring_slots=ring.R)
+        elif hist_out is not None:  # physics (one thread per env) + the 64-byte history row
             self.h.pong_step(self.state, act, rew, done, self.fin_ret, self.fin_len, self.ep_acc, self.N, self.seed,
                              0 if offset is None else int(offset), self.max_steps, False, self.step_t, hist=hist_out)
         else:  # physics + render of the new 4-frame stack in one launch (one workgroup per env)

@@ -378,7 +378,22 @@ class DeviceNatureCNN:
     def is_hist(obs) -> bool:
         """PongSynth frame histories [n, 16] float32 (4 frames x (bx, by, pa, po)) instead of s2d
         frames: the fused-render path, where the conv kernels draw the observation themselves."""
-        return obs.dtype == torch.float32 and obs.dim() == 2 and obs.shape[1] == 16
+        return torch.is_tensor(obs) and obs.dtype == torch.float32 and obs.dim() == 2 and obs.shape[1] == 16
+
+    @staticmethod
+    def is_ring(obs) -> bool:
+        """Frame-ring observations (``envs.pong.FrameRingObs``): frame rows into a frame store, read
+        and interleaved by the conv kernels themselves (csrc/kernels/pong_render.h)."""
+        return hasattr(obs, "fidx") and hasattr(obs, "frames")
+
+    @classmethod
+    def _c1_src(cls, x) -> dict:
+        """The conv1 weight gradient's frame source keywords for observations ``x``."""
+        if cls.is_ring(x):
+            return {"frames": x.frames, "fidx": x.fidx}
+        if cls.is_hist(x):
+            return {"hist": x}
+        return {}
 
     def forward(self, obs_u8: torch.Tensor, row0: int = 0, fc: bool = True, store_acts: bool = True):
         """Conv stack + fc on obs [n, 84, 84, 4]; activations land in rows row0.. of the
@@ -396,7 +411,12 @@ class DeviceNatureCNN:
         a3 = self._rows(self.a3, row0, n, FC_IN)
         hid = self._rows(self.hid, row0, n, HIDDEN)
         x = obs_u8.contiguous()
-        if self.is_hist(x):
+        if self.is_ring(x):
+            assert self.fused_convs and self.fwd_layout in (0, 64), "frame ring: the 16-wave conv stack only"
+            h.conv_stack_fwd(None, *(t for i in (1, 2, 3) for t in (sh[o[f"w{i}"]:o[f"b{i}"]],
+                                                                        p[o[f"b{i}"]:o[f"b{i}"] + CONVS[i - 1].cout])),
+                             a1, a2, a3, n, store12=store_acts, frames=x.frames, fidx=x.fidx)
+        elif self.is_hist(x):
             assert self.fused_convs and self.fwd_layout in (0, 64), "fused render: the 16-wave conv stack only"
             h.conv_stack_fwd(None, *(t for i in (1, 2, 3) for t in (sh[o[f"w{i}"]:o[f"b{i}"]],
                                                                         p[o[f"b{i}"]:o[f"b{i}"] + CONVS[i - 1].cout])),
@@ -619,7 +639,7 @@ class DeviceNatureCNN:
             n2 = n1 = 0
             S2, S1, P2, P1 = L2.cout * L2.K, S2D.cout * S2D.K, L2.hout ** 2 * L2.cout, L1.hout ** 2 * L1.cout
             x8 = obs_u8.contiguous()
-            hist = self.is_hist(x8)
+            raw = not (self.is_hist(x8) or self.is_ring(x8))
             for k in range(C):
                 b0, b1 = B * k // C, B * (k + 1) // C
                 nk = b1 - b0
@@ -630,8 +650,8 @@ class DeviceNatureCNN:
                             self.cpart["c2"][n2 * S2:], self.cbias["c2"][n2 * L2.cout:], nk, nblk,
                             staged=self.bwd2_variant)
                 n2 += nblk
-                n1 += int(h.conv1_wgrad8(None if hist else x8[b0:b1], da1[b0 * P1:b1 * P1], self.cpart["c1"][n1 * S1:],
-                                         self.cbias["c1"][n1 * S2D.cout:], nk, nblk, hist=x8[b0:b1] if hist else None))
+                n1 += int(h.conv1_wgrad8(x8[b0:b1] if raw else None, da1[b0 * P1:b1 * P1], self.cpart["c1"][n1 * S1:],
+                                         self.cbias["c1"][n1 * S2D.cout:], nk, nblk, **self._c1_src(x8[b0:b1])))
             sums += [(self.cpart["c2"], n2, S2, g[o["w2"]:o["b2"]]),
                      (self.cbias["c2"], n2, L2.cout, g[o["b2"]:o["b2"] + L2.cout])]
             c1_slabs = n1
@@ -654,10 +674,10 @@ class DeviceNatureCNN:
         # (its bias gradient comes out of the same pass over da1)
         if self.fused_convs:
             x8 = obs_u8.contiguous()
-            hist = self.is_hist(x8)
+            raw = not (self.is_hist(x8) or self.is_ring(x8))
             ns = c1_slabs if c1_slabs is not None else int(
-                h.conv1_wgrad8(None if hist else x8, da1, self.cpart["c1"], self.cbias["c1"], B, min(B, self.cus),
-                               hist=x8 if hist else None))
+                h.conv1_wgrad8(x8 if raw else None, da1, self.cpart["c1"], self.cbias["c1"], B, min(B, self.cus),
+                               **self._c1_src(x8)))
             sums += [(self.cpart["c1"], ns, S2D.cout * S2D.K, g[o["w1"]:o["b1"]]),
                      (self.cbias["c1"], ns, S2D.cout, g[o["b1"]:o["b1"] + S2D.cout])]
             h.sum_splits_multi(sums)

@@ -52,6 +52,10 @@ class PixelA2CConfig:
     # GPU: the conv kernels draw the observations themselves from 16-float frame histories (no
     # [T+1, N, 21, 21, 64] observation tensor is written or read); None = RRL_PONG_FUSED_RENDER
     fused_render: Optional[bool] = None
+    # GPU: each env step renders ONE new frame into a frame ring (envs/pong.FrameRing) and an
+    # observation is 4 frame rows; the conv kernels interleave the frames as they load them (7 KB
+    # instead of 28 KB written per env step).  None = RRL_PONG_FRAME_RING
+    frame_ring: Optional[bool] = None
 
     def to_dict(self):
         return asdict(self)
@@ -77,8 +81,17 @@ class PixelA2CTrainer:
         if cfg.fused_render is None:
             cfg.fused_render = os.environ.get("RRL_PONG_FUSED_RENDER", "0") == "1"
         self.fused_render = bool(cfg.fused_render) and self.on_gpu
+        if cfg.frame_ring is None:
+            cfg.frame_ring = os.environ.get("RRL_PONG_FRAME_RING", "0") == "1"
+        self.ring = None
         if self.fused_render:  # the frame histories the conv kernels render from
             self.obs = torch.zeros((T + 1, N, 16), dtype=torch.float32, device=dev)
+        elif cfg.frame_ring and self.on_gpu:
+            from ..envs.pong import FrameRing
+
+            # T + 4 slots: a rollout's observations read the frames of steps t0 - 3 .. t0 + T
+            self.ring = FrameRing(N, T + 4, dev)
+            self.obs = torch.zeros((T + 1, N, 4), dtype=torch.int32, device=dev)  # frame rows per observation
         else:
             self.obs = torch.zeros((T + 1, N, 21, 21, 64), dtype=torch.uint8, device=dev)  # space-to-depth frames
         # GPU: two observation buffers used alternately -- update k rolls out of buffer k % 2 and
@@ -109,6 +122,8 @@ class PixelA2CTrainer:
                 self.model.fc_nt and self.model.A <= 8
             if self.fused_render:
                 self.env.reset(hist_out=self.obs[0])
+            elif self.ring is not None:
+                self.env.reset(ring=(self.ring, self.obs[0]))
             else:
                 self.env.reset(self.obs[0])
             self.sample_t = torch.zeros(1, dtype=torch.int64, device=dev)  # Philox step of the action sampler
@@ -131,29 +146,35 @@ class PixelA2CTrainer:
         self.comm.barrier() if self.comm.multi else None
 
     # ------------------------------------------------------------------ GPU
+    def _ob(self, rows):
+        """Observations for the model: the s2d / history rows themselves, or frame rows of the ring."""
+        return rows if self.ring is None else self.ring.obs(rows)
+
     def _rollout_gpu(self, base, nxt):
         cfg, m, N, T = self.cfg, self.model, self.cfg.num_envs, self.cfg.rollout_len
+        ring = self.ring
         m.begin_update()  # the transposed Wfc refresh beside the rollout (side stream)
         for t in range(T):
             # the last observation goes straight to the next update's start slot
             out = base[t + 1] if (t + 1 < T or nxt is None) else nxt[0]
             if self.fused_head:  # conv stack + fc partials, then head + env step + render in one launch
-                part, used, hid = m.forward_fc_partials(base[t], t * N)
+                part, used, hid = m.forward_fc_partials(self._ob(base[t]), t * N)
                 fc_b, hp = m.head_params()
                 self.env.step_head(part, used, fc_b, hp, m.A, hid, self.act[t], self.logp[t], self.val[t],
-                                   self.sample_seed, t, self.sample_t, out, self.rew[t], self.done[t], offset=t)
+                                   self.sample_seed, t, self.sample_t, out, self.rew[t], self.done[t], offset=t,
+                                   ring=ring)
                 continue
-            m.act(base[t], t * N, self.act[t], self.logp[t], self.val[t], self.sample_seed, t,
+            m.act(self._ob(base[t]), t * N, self.act[t], self.logp[t], self.val[t], self.sample_seed, t,
                   step_base=self.sample_t)
             if self.fused_render:
                 self.env.step(self.act[t], None, self.rew[t], self.done[t], offset=t, hist_out=out)
             else:
-                self.env.step(self.act[t], out, self.rew[t], self.done[t], offset=t)
+                self.env.step(self.act[t], out, self.rew[t], self.done[t], offset=t, ring=ring)
         # the sampling, env and Adam step counters advance inside the update's scan launch
         # (_update_gpu; every rollout is followed by one update)
         # bootstrap V(obs[T]) with the pre-update weights; its activations go to the
         # scratch rows [T*N, (T+1)*N) so the stored rollout activations stay intact
-        m.value(base[T] if nxt is None else nxt[0], cfg.rollout_len * N, self.val[cfg.rollout_len])
+        m.value(self._ob(base[T] if nxt is None else nxt[0]), cfg.rollout_len * N, self.val[cfg.rollout_len])
 
     def _update_gpu(self, base):
         from ..ops import gae_scan_tm
@@ -168,7 +189,10 @@ class PixelA2CTrainer:
                                       self._stats_part, stats=False,
                                       counters=((self.sample_t, T), (self.env.step_t, T), (m.step_t, 1)))
         with self.timer.phase("Backward"):
-            x = base[:T].reshape(B, 16) if self.fused_render else base[:T].reshape(B, 21, 21, 64)
+            if self.ring is not None:
+                x = self.ring.obs(base[:T].reshape(B, 4))
+            else:
+                x = base[:T].reshape(B, 16) if self.fused_render else base[:T].reshape(B, 21, 21, 64)
             stats = m.backward(x, self.act.reshape(B), adv.reshape(B),
                                ret.reshape(B), cfg.vf_coef, cfg.ent_coef, comm=self.comm)
         with self.timer.phase("Optimize"):
@@ -287,8 +311,9 @@ class PixelA2CTrainer:
                 ts += [v for v in st.values() if torch.is_tensor(v)]
             return ts
         m = self.model
-        return [m.params, m.m, m.v, m.step_t, self.env.state, self.env.step_t, self.env.ep_acc, self.sample_t,
-                self.obs[0]]
+        ts = [m.params, m.m, m.v, m.step_t, self.env.state, self.env.step_t, self.env.ep_acc, self.sample_t,
+              self.obs[0]]
+        return ts + ([self.ring.frames] if self.ring is not None else [])
 
     def counters(self) -> dict:
         return {"updates": self.updates, "total_steps": self.total_steps}
@@ -319,12 +344,24 @@ class PixelA2CTrainer:
     def load_state_dict(self, st: dict):
         self.updates = int(st["updates"])
         self.total_steps = int(st["total_steps"])
-        self.obs[0].copy_(st["obs0"].to(self.device))
+        obs0 = st["obs0"]
+        if obs0.shape == self.obs[0].shape and obs0.dtype == self.obs.dtype:
+            self.obs[0].copy_(obs0.to(self.device))
         if self.on_gpu:
             self.model.load_state_dict({k: v.to(self.device) for k, v in st["model"].items()})
             self.env.state.copy_(st["env_state"].to(self.device))
             self.env.step_count = int(st["env_step"])
             self.sample_t.fill_(int(st.get("sample_step", self.updates * self.cfg.rollout_len)))
+            # the observation is a function of the env state: rebuilt when the checkpoint's
+            # observation form differs (s2d vs frame ring), and always for the ring (its frames
+            # are not in the checkpoint)
+            if self.ring is not None:
+                self.env.ring_fill(self.ring, self.obs[0])
+            elif obs0.shape != self.obs[0].shape or obs0.dtype != self.obs.dtype:
+                if self.fused_render:
+                    self.obs[0].copy_(self.env.state.view(self.cfg.num_envs, -1)[:, 16:32])
+                else:
+                    self.env.h.pong_render(self.env.state, self.obs[0], self.cfg.num_envs)
         else:
             with torch.no_grad():
                 self.params.copy_(st["params"])

@@ -117,3 +117,31 @@ def test_pixel_trainer_dp_gloo():
     res = _run(_worker_pixel_dp)
     for rank, ok, _ in res:
         assert ok is True, (rank, ok)
+
+
+def test_frame_ring_layout_gives_the_s2d_observation():
+    """FrameRing's store layout (one s2d frame [21][21][4][4] per slot and env) and frame rows:
+    gathering frames 0..3 of PongRef's stack through fidx reproduces its s2d observation, and a
+    reset env's clamped rows (all pointing at one frame) give its 4 identical frames."""
+    from relayrl_prototype_amd.envs.pong import VALID, FrameRing
+
+    N = 5
+    env = PongRef(N, seed=3, max_steps=4)
+    env.reset()
+    for _ in range(3):
+        env.step(np.random.default_rng(0).integers(0, 6, N))
+    stack = env.render_nhwc()                       # [N, 84, 84, 4]
+    ring = FrameRing(N, 7, "cpu")
+    fr = ring.frames.view(7, N, 21, 4, 21, 4)      # [slot][env][a][dy][b][dx] as an image view
+    for f in range(4):                              # frame f of the stack into slot f
+        img = torch.from_numpy(stack[..., f].copy()).view(N, 21, 4, 21, 4)
+        fr[f].copy_(img)
+    # the store is s2d per frame: [slot][env][a][b][dy][dx]
+    ring.frames.copy_(fr.permute(0, 1, 2, 4, 3, 5).contiguous().view(-1))
+    fidx = torch.tensor([[f * N + e for f in range(4)] for e in range(N)], dtype=torch.int32)
+    assert torch.equal(ring.gather_s2d(fidx), torch.from_numpy(env.render()))
+    # the oracle's count of distinct frames: 1 after a reset, +1 per step up to 4
+    assert set(np.unique(env.s[:, VALID]).tolist()) <= {1.0, 2.0, 3.0, 4.0}
+    same = torch.full((1, 4), 2 * N, dtype=torch.int32)
+    o = ring.gather_s2d(same).view(1, 21, 21, 16, 4)
+    assert all(torch.equal(o[..., f], o[..., 0]) for f in range(4))
