@@ -69,7 +69,7 @@ int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, u
 int rrl_conv2_bwd(const uint16_t* dy, const uint16_t* w, const uint16_t* xact, uint16_t* dx, float* part,
                   float* bias_part, int N, int grid, int staged, void* stream);
 int rrl_conv1_wgrad8(const uint8_t* x, const float* hist, const uint8_t* frames, const int32_t* fidx,
-                     const uint16_t* dy, float* part, float* bias_part, int N, int grid, void* stream);
+                     const uint16_t* dy, float* part, float* bias_part, int N, int grid, int T, void* stream);
 int rrl_pong_render_hist(const float* hist, uint8_t* obs, int N, void* stream);
 int rrl_pong_head_step_render(const float* part, int splits, const float* fc_b, const float* head_params, int A,
                               uint16_t* h_out, int32_t* act, float* logp, float* value, unsigned long long sample_seed,
@@ -226,7 +226,7 @@ void conv2_bwd(const Tensor& dy, const Tensor& w, const Tensor& xact, const Tens
 // conv1 weight + bias gradient, 8-wave kernel (cnn_fused.hip): s2d frames [N][21][21][64], da1
 // [N][400][32] -> partials [2 grid][32 * 256] and [2 grid][32]; returns the slab count (2 grid).
 int64_t conv1_wgrad8(const OptT& x, const Tensor& dy, const Tensor& part, const Tensor& bias_part, int64_t N,
-                     int64_t grid, const OptT& hist, const OptT& frames, const OptT& fidx) {
+                     int64_t grid, const OptT& hist, const OptT& frames, const OptT& fidx, int64_t env_major_T) {
   TORCH_CHECK(N > 0 && grid > 0 && grid <= N, "conv1_wgrad8: need 0 < grid <= N");
   const float* hp = opt_ptr<const float>(hist, "hist", at::kFloat, N * 16);
   const uint8_t* xp = opt_ptr<const uint8_t>(x, "x", at::kByte, N * 441 * 64);
@@ -236,8 +236,11 @@ int64_t conv1_wgrad8(const OptT& x, const Tensor& dy, const Tensor& part, const 
   check(dy, "dy", at::kBFloat16, N * 400 * 32);
   check(part, "part", at::kFloat, 2 * grid * 32 * 256);
   check(bias_part, "bias_part", at::kFloat, 2 * grid * 32);
+  // env_major_T > 1 (frame ring): the rows are a T-step rollout, visited env-major (rows of one env
+  // back to back share 3 of their 4 frames)
+  TORCH_CHECK(env_major_T <= 1 || (fp && N % env_major_T == 0), "conv1_wgrad8: env_major_T needs the ring and T | N");
   rc_check(rrl_conv1_wgrad8(xp, hp, fp, ip, bf(dy), part.data_ptr<float>(), bias_part.data_ptr<float>(), (int)N, (int)grid,
-                            stream()),
+                            (int)env_major_T, stream()),
            "conv1_wgrad8");
   return 2 * grid;
 }
@@ -629,7 +632,8 @@ void register_cnn_ops(pybind11::module_& m) {
         pybind11::arg("staged") = 0);
   m.def("conv1_wgrad8", &conv1_wgrad8, pybind11::arg("x"), pybind11::arg("dy"), pybind11::arg("part"),
         pybind11::arg("bias_part"), pybind11::arg("N"), pybind11::arg("grid"), pybind11::arg("hist") = pybind11::none(),
-        pybind11::arg("frames") = pybind11::none(), pybind11::arg("fidx") = pybind11::none());
+        pybind11::arg("frames") = pybind11::none(), pybind11::arg("fidx") = pybind11::none(),
+        pybind11::arg("env_major_T") = 0);
   m.def("col2im_mask", &col2im_mask);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("gemm_splits", &gemm_splits);

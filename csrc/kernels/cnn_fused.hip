@@ -415,6 +415,9 @@ struct L16 {
   static constexpr int kA2Off = kA1Off + 2 * kA1Elems * 2;
   static constexpr int kLds = kA2Off + 2 * kA2Elems * 2;  // 145,696 bytes (default) .. 160,800 (bits 16 | 32)
   static_assert(kLds <= 160 * 1024, "LDS per workgroup");
+  // frame ring: the table of this workgroup's images' frame rows after the images (16 KB)
+  static constexpr int kLdsTotal = kLds + (kRing ? kRingTab * 16 : 0);
+  static_assert(kLdsTotal <= 160 * 1024, "LDS per workgroup with the frame-row table");
   static_assert(kA1Off % 16 == 0 && kA2Off % 16 == 0, "16-byte aligned LDS regions");
 };
 }  // namespace cs16
@@ -487,23 +490,23 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
   const int G = gridDim.x, n0 = blockIdx.x, N = A.N;
   uint4 rx[L::kRender ? 1 : kXPerT];
   static_assert(kXPerT >= 2, "the ring form keeps 4 x 8 raw bytes per thread in rx[0..1]");
-  auto gload = [&](size_t n) {
-    if constexpr (L::kRender) return;
-    if constexpr (L::kRing) {
-      // unit tid < 882: position tid >> 1, rows 2 (tid & 1) .. + 1 of frames 0..3 (8 bytes each),
-      // kept raw until the LDS store (the loads stay in flight while this frame computes)
-      if (tid < 2 * kPongFramePos) {
-        const int4 fr = *reinterpret_cast<const int4*>(A.fidx + 4 * n);  // wave-uniform
-        const size_t off = (size_t)(tid >> 1) * 16 + 8 * (tid & 1);
-        const uint2 f0 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.x * kPongFrameBytes + off);
-        const uint2 f1 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.y * kPongFrameBytes + off);
-        const uint2 f2 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.z * kPongFrameBytes + off);
-        const uint2 f3 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.w * kPongFrameBytes + off);
-        rx[0] = make_uint4(f0.x, f0.y, f1.x, f1.y);
-        rx[1] = make_uint4(f2.x, f2.y, f3.x, f3.y);
-      }
-      return;
+  const int4* rtab = reinterpret_cast<const int4*>(reinterpret_cast<const uint8_t*>(smem) + L::kLds);
+  // frame ring: unit tid < 882 loads position tid >> 1, rows 2 (tid & 1) .. + 1 of frames 0..3 (8
+  // bytes each) of the image with frame rows fr, kept raw until the LDS store (the loads stay in
+  // flight while this frame computes)
+  auto gload_ring = [&](int4 fr) {
+    if (tid < 2 * kPongFramePos) {
+      const size_t off = (size_t)(tid >> 1) * 16 + 8 * (tid & 1);
+      const uint2 f0 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.x * kPongFrameBytes + off);
+      const uint2 f1 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.y * kPongFrameBytes + off);
+      const uint2 f2 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.z * kPongFrameBytes + off);
+      const uint2 f3 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.w * kPongFrameBytes + off);
+      rx[0] = make_uint4(f0.x, f0.y, f1.x, f1.y);
+      rx[1] = make_uint4(f2.x, f2.y, f3.x, f3.y);
     }
+  };
+  auto gload = [&](size_t n) {
+    if constexpr (L::kRender || L::kRing) return;
     const uint4* xs = reinterpret_cast<const uint4*>(A.x + n * (441 * 64));
 #pragma unroll
     for (int k = 0; k < kXPerT; ++k) {
@@ -524,7 +527,11 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
   if constexpr (L::kRender) {
     if (ROLE == 1 && n0 < N) render(n0, 0);
   }
-  if (n0 < N) gload(n0);
+  if constexpr (L::kRing) {  // the first image's rows straight from fidx: no wait on the table
+    if (n0 < N) gload_ring(uniform_int4(*reinterpret_cast<const int4*>(A.fidx + 4 * (size_t)n0)));
+  } else if (n0 < N) {
+    gload(n0);
+  }
   for (int j = 0; n0 + (j - 2) * G < N; ++j) {
     const int n = n0 + j * G;
     __syncthreads();  // B0: the previous iteration's stages are done (F free, a1 / a2 buffers complete)
@@ -532,13 +539,15 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
       // (fused render: frame n is already in buffer j & 1)
     } else if constexpr (L::kRing) {
       if (n < N) {
+        // the next image's frame rows: read from the table before this image's stores
+        const int4 frn = n + G < N ? ring_row(rtab, A.fidx, n0, G, j + 1) : make_int4(0, 0, 0, 0);
         if (tid < 2 * kPongFramePos) {  // rows 2h, 2h + 1 of position pix, interleaved across the 4 frames
           const int pix = tid >> 1, pa = pix / 21, h = tid & 1;
           uint8_t* d = F + (pix + (kFW - 21) * pa) * kFS + 32 * h;
           *reinterpret_cast<uint4*>(d) = pong_interleave_row(rx[0].x, rx[0].z, rx[1].x, rx[1].z);
           *reinterpret_cast<uint4*>(d + 16) = pong_interleave_row(rx[0].y, rx[0].w, rx[1].y, rx[1].w);
         }
-        if (n + G < N) gload((size_t)n + G);
+        if (n + G < N) gload_ring(frn);
       }
     } else if (n < N) {
 #pragma unroll
@@ -683,6 +692,11 @@ template <int V>
 __global__ __launch_bounds__(cs16::kThreads, 1) void conv_stack16_fwd_kernel(Stack16Args args) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x;
+  if constexpr (cs16::L16<V>::kRing) {
+    // this workgroup's images' frame rows into LDS, once; first read (image 1's) after barrier B0
+    ring_stage_table(reinterpret_cast<int4*>(reinterpret_cast<uint8_t*>(smem) + cs16::L16<V>::kLds), args.fidx, args.N,
+                     blockIdx.x, gridDim.x, tid, cs16::kThreads);
+  }
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (wave < 8) stack16_role<1, V>(args, smem, tid, wave);
   else if (wave < 12) stack16_role<2, V>(args, smem, tid, wave);
@@ -726,7 +740,7 @@ static int launch_conv_stack16_fwd(const uint8_t* x, const float* hist, const ui
   }
   if (N < 1) return 0;
   const int grid = N < max_grid ? N : max_grid;  // one 146-161 KB-LDS workgroup per CU
-  const int lds = L::kLds;
+  const int lds = L::kLdsTotal;
   if (L::kRender && !hist) return -2;
   if (L::kRing && (!frames || !fidx)) return -2;
   const Stack16Args args{x, hist, frames, fidx, w1, w2, w3, b1, b2, b3, y1, y2, y3, N};
@@ -1870,6 +1884,8 @@ constexpr int kThreads = 512;
 constexpr int kLd = 80, kYLd = 48, kXW = 28;
 constexpr int kXRows = 20 * kXW + 24, kYRows = 416;
 constexpr int kLds = (kXRows * kLd + kYRows * kYLd) * 2;  // 133,632 bytes
+constexpr int kLdsRing = kLds + kRingTab * 16;              // + the frame ring's frame-row table
+static_assert(kLds % 16 == 0 && kLdsRing <= 160 * 1024, "LDS per workgroup");
 constexpr int kXC = 441 * 4, kYC = 400 * 4;       // 16-byte chunks per image
 constexpr int kXPT = (kXC + kThreads - 1) / kThreads, kYPT = (kYC + kThreads - 1) / kThreads;
 }  // namespace c1w
@@ -1885,7 +1901,8 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
                                                                         float* __restrict__ part,
                                                                         float* __restrict__ bias_part, int N,
                                                                         const uint8_t* __restrict__ frames = nullptr,
-                                                                        const int32_t* __restrict__ fidx = nullptr) {
+                                                                        const int32_t* __restrict__ fidx = nullptr,
+                                                                        int T = 0) {
   using namespace c1w;
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   uint16_t* Xi = smem;                // [21 x 28][80] frame, bf16 integers 0..255
@@ -1916,10 +1933,37 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
   // the next image's frame chunks: loaded (observations) or drawn (RENDER: the history row's 16
   // floats in SGPRs) into the same registers
   static_assert(kXPT >= 4, "the ring form keeps two units of 4 x 8 raw bytes per thread");
+  // This workgroup's images, in order k = 0 .. K - 1: n0 + k G, or (T > 1, rows t E + e of a
+  // T-step rollout over E envs) env-major -- the T rows of env e = n0 + q G back to back, so with
+  // the frame ring the 4-frame observations of consecutive images share 3 frames and those are
+  // re-read from this CU's L2 (the weight gradient is a sum over images: the order only
+  // reassociates it)
+  const int n0 = blockIdx.x, G = gridDim.x;
+  const int E = T > 1 ? N / T : N;
+  const int K = T > 1 ? (n0 < E ? T * ((E - n0 + G - 1) / G) : 0) : ring_images(N, n0, G);
+  auto img = [&](int k) -> int {
+    if (T > 1) {
+      const int q = k / T, t = k - q * T;
+      return t * E + n0 + q * G;
+    }
+    return n0 + k * G;
+  };
+  // frame ring: this workgroup's images' frame rows, staged in LDS after the images once (read
+  // from the table a stage ahead; images past it read fidx directly)
+  int4* rtab = reinterpret_cast<int4*>(reinterpret_cast<uint8_t*>(smem) + kLds);
+  if constexpr (RING) {
+    for (int k = tid; k < min(K, kRingTab); k += kThreads) rtab[k] = *reinterpret_cast<const int4*>(fidx + 4 * (size_t)img(k));
+  }
+  auto ring_entry = [&](int k) -> int4 {
+    return uniform_int4(k < kRingTab ? rtab[k] : *reinterpret_cast<const int4*>(fidx + 4 * (size_t)img(k)));
+  };
+  // the frame rows of the image xload reads next (RING): read from the table a stage ahead
+  int4 fr_next = make_int4(0, 0, 0, 0);
   auto xload = [&](int n) {
     if constexpr (RING) {
       // units u = tid, tid + 512 (< 882): position u >> 1, rows 2 (u & 1) .. + 1 of frames 0..3
-      const int4 fr = *reinterpret_cast<const int4*>(fidx + 4 * (size_t)n);  // wave-uniform
+      const int4 fr = fr_next;
+      (void)n;
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const int u = tid + kThreads * k;
@@ -1963,13 +2007,20 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
   // matrix work
   const bool draw_late = RENDER && half;
   const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-  const int n0 = blockIdx.x, G = gridDim.x;
-  if (n0 < N) {
-    gload(n0);
-    xload(n0);
+  if (K > 0) {
+    const int n = img(0);
+    gload(n);
+    // the first image's rows straight from fidx (the table is first read after the loop's barrier)
+    if constexpr (RING) fr_next = uniform_int4(*reinterpret_cast<const int4*>(fidx + 4 * (size_t)n));
+    xload(n);
   }
-  for (int n = n0; n < N; n += G) {
+  for (int k = 0; k < K; ++k) {
+    const bool more = k + 1 < K;
+    const int nn = more ? img(k + 1) : 0;  // the next image
     __syncthreads();  // the previous image's fragment reads are done
+    if constexpr (RING) {
+      if (more) fr_next = ring_entry(k + 1);  // before this image's stores
+    }
     if constexpr (RING) {
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
@@ -2001,9 +2052,9 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
       const int q = tid + kThreads * i;
       if (q < kYC) *reinterpret_cast<uint4*>(Yi + (q >> 2) * kYLd + (q & 3) * 8) = ry[i];
     }
-    if (n + G < N) {
-      gload(n + G);
-      if (!draw_late) xload(n + G);
+    if (more) {
+      gload(nn);
+      if (!draw_late) xload(nn);
     }
     __syncthreads();
     // MFMA k-order: lane group g of a 32-pixel chunk takes pixels 4g..4g+3 and 16+4g..16+4g+3
@@ -2031,7 +2082,7 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
       }
       if constexpr (SP) __builtin_amdgcn_s_setprio(0);
     }
-    if (draw_late && n + G < N) xload(n + G);
+    if (draw_late && more) xload(nn);
   }
   const int slab = 2 * blockIdx.x + half;
   if (do_bias && (lane & 15) == 0) {
@@ -2053,20 +2104,22 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
 
 // returns the number of partial slabs written (2 per workgroup); hist (PongSynth frame histories
 // [N][16]): the frames are drawn in the kernel, x is not read
+// T > 1 (frame ring only): the N = T E rows are a T-step rollout over E envs, visited env-major
 extern "C" int rrl_conv1_wgrad8(const uint8_t* x, const float* hist, const uint8_t* frames, const int32_t* fidx,
-                                const uint16_t* dy, float* part, float* bias_part, int N, int grid, void* stream) {
+                                const uint16_t* dy, float* part, float* bias_part, int N, int grid, int T,
+                                void* stream) {
   static bool attr = false;
   if (frames) {  // frame ring: frames [R][E][7056], fidx [N][4]
     static bool attr_ring = false;
     if (!attr_ring) {
       (void)hipFuncSetAttribute((const void*)conv1_wgrad8_kernel<false, false, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, c1w::kLds);
+                                hipFuncAttributeMaxDynamicSharedMemorySize, c1w::kLdsRing);
       attr_ring = true;
     }
     if (N < 1 || grid < 1) return 0;
-    if (!fidx) return -2;
-    hipLaunchKernelGGL((conv1_wgrad8_kernel<false, false, true>), dim3(grid), dim3(c1w::kThreads), c1w::kLds,
-                       (hipStream_t)stream, nullptr, nullptr, dy, part, bias_part, N, frames, fidx);
+    if (!fidx || (T > 1 && N % T != 0)) return -2;
+    hipLaunchKernelGGL((conv1_wgrad8_kernel<false, false, true>), dim3(grid), dim3(c1w::kThreads), c1w::kLdsRing,
+                       (hipStream_t)stream, nullptr, nullptr, dy, part, bias_part, N, frames, fidx, T);
     return (int)hipGetLastError();
   }
   if (!attr) {

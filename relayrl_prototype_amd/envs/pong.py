@@ -205,8 +205,10 @@ class FrameRing:
         self.N, self.R = int(num_envs), int(slots)
         self.frames = torch.zeros(self.R * self.N * FRAME_BYTES, dtype=torch.uint8, device=device)
 
-    def obs(self, fidx: torch.Tensor) -> "FrameRingObs":
-        return FrameRingObs(self.frames, fidx)
+    def obs(self, fidx: torch.Tensor, rollout_len: int = 0) -> "FrameRingObs":
+        """Observations of frame rows ``fidx``; ``rollout_len`` T > 1 marks them as a T-step
+        rollout's rows (t-major, T x E): the conv1 weight gradient may then visit them env-major."""
+        return FrameRingObs(self.frames, fidx, rollout_len)
 
     def gather_s2d(self, fidx: torch.Tensor) -> torch.Tensor:
         """The observations [n, 21, 21, 64] the frame rows ``fidx`` [n, 4] describe (tests)."""
@@ -217,19 +219,19 @@ class FrameRing:
 class FrameRingObs:
     """A batch of observations as frame rows ``fidx`` [n, 4] into a ``FrameRing``'s store: what
     ``DeviceNatureCNN`` takes in place of an s2d uint8 tensor (slicing gives sub-batches)."""
-    __slots__ = ("frames", "fidx")
+    __slots__ = ("frames", "fidx", "rollout_len")
 
-    def __init__(self, frames: torch.Tensor, fidx: torch.Tensor):
-        self.frames, self.fidx = frames, fidx.reshape(-1, 4)
+    def __init__(self, frames: torch.Tensor, fidx: torch.Tensor, rollout_len: int = 0):
+        self.frames, self.fidx, self.rollout_len = frames, fidx.reshape(-1, 4), int(rollout_len)
 
     @property
     def shape(self):
         return (self.fidx.shape[0], 4)
 
     def contiguous(self):
-        return FrameRingObs(self.frames, self.fidx.contiguous())
+        return FrameRingObs(self.frames, self.fidx.contiguous(), self.rollout_len)
 
-    def __getitem__(self, sl):
+    def __getitem__(self, sl):  # a slice is no longer a whole T x E rollout block
         return FrameRingObs(self.frames, self.fidx[sl])
 
 

@@ -388,9 +388,15 @@ class DeviceNatureCNN:
 
     @classmethod
     def _c1_src(cls, x) -> dict:
-        """The conv1 weight gradient's frame source keywords for observations ``x``."""
+        """The conv1 weight gradient's frame source keywords for observations ``x``.  Frame-ring
+        rows of a whole T-step rollout are visited env-major (RRL_CNN_WGRAD1_ENV_MAJOR, default on):
+        the T observations of one env share frames, which then come from the CU's L2."""
         if cls.is_ring(x):
-            return {"frames": x.frames, "fidx": x.fidx}
+            kw = {"frames": x.frames, "fidx": x.fidx}
+            T = getattr(x, "rollout_len", 0)
+            if T > 1 and x.fidx.shape[0] % T == 0 and os.environ.get("RRL_CNN_WGRAD1_ENV_MAJOR", "1") == "1":
+                kw["env_major_T"] = T
+            return kw
         if cls.is_hist(x):
             return {"hist": x}
         return {}

@@ -190,7 +190,7 @@ class PixelA2CTrainer:
                                       counters=((self.sample_t, T), (self.env.step_t, T), (m.step_t, 1)))
         with self.timer.phase("Backward"):
             if self.ring is not None:
-                x = self.ring.obs(base[:T].reshape(B, 4))
+                x = self.ring.obs(base[:T].reshape(B, 4), rollout_len=T)
             else:
                 x = base[:T].reshape(B, 16) if self.fused_render else base[:T].reshape(B, 21, 21, 64)
             stats = m.backward(x, self.act.reshape(B), adv.reshape(B),

@@ -200,6 +200,36 @@ def test_ring_conv1_wgrad_equals_the_obs_path(cuda):
         assert torch.isfinite(f).all() and torch.equal(f, r)
 
 
+@pytest.mark.parametrize("E,T,grid", [(2048, 5, 256), (300, 4, 256), (37, 5, 16)])
+def test_ring_conv1_wgrad_env_major_order(cuda, E, T, grid):
+    """The env-major visit order (the T rows of one env back to back) sums the same products in
+    another order: the reduced weight / bias gradients match the row order to fp32 reassociation,
+    and every row is visited once (a row-count check through the bias of a constant dY)."""
+    from relayrl_prototype_amd.ops import hip
+
+    h = hip()
+    N = E * T
+    ring, fidx, _ = _ring_batch(cuda, N, 3)
+    g = torch.Generator().manual_seed(5)
+    dy = torch.randn(N * 400 * 32, generator=g).bfloat16().to(cuda)
+    res = []
+    for em in (0, T):
+        part = torch.full((2 * grid * 32 * 256,), float("nan"), device=cuda)
+        bpart = torch.full((2 * grid * 32,), float("nan"), device=cuda)
+        ns = h.conv1_wgrad8(None, dy, part, bpart, N, grid, frames=ring.frames, fidx=fidx, env_major_T=em)
+        torch.cuda.synchronize()
+        res.append((part[:ns * 32 * 256].view(ns, -1).double().sum(0), bpart[:ns * 32].view(ns, -1).double().sum(0)))
+    (w0, b0), (w1, b1) = res
+    torch.testing.assert_close(w1, w0, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(b1, b0, rtol=1e-5, atol=1e-4)
+    ones = torch.ones(N * 400 * 32, dtype=torch.bfloat16, device=cuda)
+    part = torch.zeros(2 * grid * 32 * 256, device=cuda)
+    bpart = torch.zeros(2 * grid * 32, device=cuda)
+    ns = h.conv1_wgrad8(None, ones, part, bpart, N, grid, frames=ring.frames, fidx=fidx, env_major_T=T)
+    torch.cuda.synchronize()
+    assert torch.equal(bpart[:ns * 32].view(ns, 32).sum(0).cpu(), torch.full((32,), float(N * 400)))
+
+
 @pytest.mark.parametrize("fused_head", ["1", "0"])
 def test_pixel_update_frame_ring_matches_the_obs_path(cuda, monkeypatch, fused_head):
     """A2C on the frame ring trains the same trajectory bitwise as on 4-frame observations
@@ -209,6 +239,7 @@ def test_pixel_update_frame_ring_matches_the_obs_path(cuda, monkeypatch, fused_h
 
     monkeypatch.setenv("RRL_CNN_FWD_LAYOUT", "64")
     monkeypatch.setenv("RRL_PONG_FUSED_HEAD", fused_head)
+    monkeypatch.setenv("RRL_CNN_WGRAD1_ENV_MAJOR", "0")  # the row order: bitwise the obs path
     runs = []
     for ring in (False, True):
         tr = PixelA2CTrainer(PixelA2CConfig(num_envs=300, rollout_len=4, seed=6, use_graphs=True, max_episode_steps=7,
@@ -235,3 +266,20 @@ def test_pixel_update_frame_ring_matches_the_obs_path(cuda, monkeypatch, fused_h
     c.train_epoch()
     torch.cuda.synchronize()
     torch.testing.assert_close(c.model.params, a.model.params, rtol=0, atol=0)
+
+
+def test_pixel_update_frame_ring_env_major_wgrad(cuda, monkeypatch):
+    """The shipped ring update (conv1 weight gradient env-major) differs from the row order only by
+    fp32 reassociation of dW1: one update from the same state gives the same gradients to 1e-4."""
+    from relayrl_prototype_amd.runtime.pixel_trainer import PixelA2CConfig, PixelA2CTrainer
+
+    monkeypatch.setenv("RRL_CNN_FWD_LAYOUT", "64")
+    grads = []
+    for em in ("0", "1"):
+        monkeypatch.setenv("RRL_CNN_WGRAD1_ENV_MAJOR", em)
+        tr = PixelA2CTrainer(PixelA2CConfig(num_envs=512, rollout_len=5, seed=2, use_graphs=False, frame_ring=True,
+                                            fused_render=False), device=cuda)
+        tr.train_epoch()
+        torch.cuda.synchronize()
+        grads.append(tr.model.grad.clone())
+    torch.testing.assert_close(grads[1], grads[0], rtol=1e-4, atol=1e-6)

@@ -74,6 +74,21 @@ def main():
 
     fns = {}
     fns["wgrad1_8"] = lambda: h.conv1_wgrad8(x[:Nb], da1, part, bpart, Nb, min(Nb, cus))
+    # frame ring (envs/pong.FrameRing): R = 9 slots x Nf envs; row n = t Nf + e of a T-step rollout
+    # reads frames t .. t + 3 of env e (the rollout's sharing pattern, 3 of 4 frames shared by rows
+    # t and t + 1 of one env)
+    R = 9
+    frames = torch.randint(0, 256, (R * Nf * 7056,), dtype=torch.uint8, device=dev)
+    rows = torch.arange(N, device=dev)
+    e, t = rows % Nf, rows // Nf
+    fidx = torch.stack([((t + f) % R) * Nf + e for f in range(4)], 1).int().contiguous()
+    Tb = Nb // Nf if Nb % Nf == 0 else 0
+    fns["fwd16_ring"] = lambda: h.conv_stack_fwd(None, *W[1], *W[2], *W[3], a1, a2, a3, Nf, frames=frames,
+                                                 fidx=fidx[:Nf])
+    fns["wgrad1_8_ring"] = lambda: h.conv1_wgrad8(None, da1, part, bpart, Nb, min(Nb, cus), frames=frames,
+                                                  fidx=fidx[:Nb])
+    fns["wgrad1_8_ring_em"] = lambda: h.conv1_wgrad8(None, da1, part, bpart, Nb, min(Nb, cus), frames=frames,
+                                                     fidx=fidx[:Nb], env_major_T=Tb)
 
     def wgrad1_8_sp():  # the s_setprio form (RRL_CNN_WGRAD1_SETPRIO, read per call)
         os.environ["RRL_CNN_WGRAD1_SETPRIO"] = "1"
