@@ -54,7 +54,9 @@ class PixelA2CConfig:
     fused_render: Optional[bool] = None
     # GPU: each env step renders ONE new frame into a frame ring (envs/pong.FrameRing) and an
     # observation is 4 frame rows; the conv kernels interleave the frames as they load them (7 KB
-    # instead of 28 KB written per env step).  None = RRL_PONG_FRAME_RING
+    # instead of 28 KB written per env step: step launch 24.9 -> 19.4 us, update 1186.7 ->
+    # 1166.6 us at 2,048 envs, ABBA +0.4 % / +1.0 % at 2,048 / 8,192 envs,
+    # profiles/r6_pong_ring_v3_ab.txt).  None = RRL_PONG_FRAME_RING (default on)
     frame_ring: Optional[bool] = None
 
     def to_dict(self):
@@ -82,11 +84,12 @@ class PixelA2CTrainer:
             cfg.fused_render = os.environ.get("RRL_PONG_FUSED_RENDER", "0") == "1"
         self.fused_render = bool(cfg.fused_render) and self.on_gpu
         if cfg.frame_ring is None:
-            cfg.frame_ring = os.environ.get("RRL_PONG_FRAME_RING", "0") == "1"
+            cfg.frame_ring = os.environ.get("RRL_PONG_FRAME_RING", "1") == "1"
         self.ring = None
         if self.fused_render:  # the frame histories the conv kernels render from
             self.obs = torch.zeros((T + 1, N, 16), dtype=torch.float32, device=dev)
-        elif cfg.frame_ring and self.on_gpu:
+        elif cfg.frame_ring and self.on_gpu and os.environ.get("RRL_CNN_FUSED", "1") != "0" and \
+                int(os.environ.get("RRL_CNN_FWD_LAYOUT", "0")) in (0, 64):  # the 16-wave conv stack reads the ring
             from ..envs.pong import FrameRing
 
             # T + 4 slots: a rollout's observations read the frames of steps t0 - 3 .. t0 + T
@@ -113,6 +116,7 @@ class PixelA2CTrainer:
             from ..envs.pong import DevicePong
 
             self.model = DeviceNatureCNN(self.spec, dev, max_batch=N * (T + 1), seed=cfg.seed)
+            assert self.ring is None or (self.model.fused_convs and self.model.fwd_layout in (0, 64))
             self.env = DevicePong(N, dev, env_seed, cfg.max_episode_steps)
             # the rollout's policy head inside the env-step launch: +1.6 % at 2,048 envs, -0.3 % at
             # 8,192 (profiles/r5_pong_fused_head_ab.jsonl), so on up to 4,096 envs by default;

@@ -1090,7 +1090,7 @@ def test_pixel_update_fused_render_matches_the_obs_path(cuda, monkeypatch):
     runs = []
     for fused in (False, True):
         tr = PixelA2CTrainer(PixelA2CConfig(num_envs=300, rollout_len=4, seed=6, use_graphs=True,
-                                            fused_render=fused), device=cuda)
+                                            fused_render=fused, frame_ring=False), device=cuda)
         assert tr.fused_render == fused and tr.obs.dtype == (torch.float32 if fused else torch.uint8)
         for _ in range(5):
             tr.train_epoch()
