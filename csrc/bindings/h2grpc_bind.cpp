@@ -14,8 +14,9 @@ PYBIND11_MODULE(_h2grpc, m) {
   m.attr("ACTIONS") = (int)rrl::h2::kActions;
   m.attr("NEED_TS") = (int)rrl::h2::kNeedTs;
   py::class_<Server>(m, "GrpcServer")
-      .def(py::init<const std::string&, int, size_t, size_t, int>(), py::arg("host"), py::arg("port"),
-           py::arg("max_inbox") = 65536, py::arg("max_bytes") = size_t(1) << 30, py::arg("idle_timeout_ms") = 30)
+      .def(py::init<const std::string&, int, size_t, size_t, int, size_t>(), py::arg("host"), py::arg("port"),
+           py::arg("max_inbox") = 65536, py::arg("max_bytes") = size_t(1) << 30, py::arg("idle_timeout_ms") = 30,
+           py::arg("max_request") = size_t(256) << 20)
       .def_property_readonly("port", &Server::port)
       .def(
           "recv",
@@ -62,6 +63,7 @@ PYBIND11_MODULE(_h2grpc, m) {
         d["bytes_in"] = st.bytes_in;
         d["inbox_waits"] = st.inbox_waits;
         d["dropped_conns"] = st.dropped_conns;
+        d["refused_streams"] = st.refused_streams;
         return d;
       });
 }

@@ -21,7 +21,6 @@ namespace h2 {
 namespace {
 
 constexpr const char* kPrefix = "/relayrl_grpc.RelayRLRoute/";
-constexpr size_t kMaxRequest = size_t(256) << 20;  // the Python server's max_receive_message_length
 
 // --------------------------------------------------------------------------- protobuf (wire)
 void put_varint(std::string& o, uint64_t v) {
@@ -137,6 +136,7 @@ struct Conn {
   bool want_out = false;
   std::map<int32_t, Stream> streams;
   std::vector<std::pair<int32_t, std::string>> done_reqs;  // (stream, path) completed by the last recv
+  size_t held = 0;  // request bytes this connection holds (stream bodies + parked uploads)
   ~Conn() {
     if (sess) nghttp2_session_del(sess);
     if (fd >= 0) ::close(fd);
@@ -163,12 +163,18 @@ int on_data_chunk(nghttp2_session* s, uint8_t, int32_t sid, const uint8_t* data,
   auto* c = static_cast<Conn*>(ud);
   auto it = c->streams.find(sid);
   if (it == c->streams.end()) return 0;
-  if (it->second.body.size() + len > kMaxRequest + 5) {
+  // a message past max_request, or past what one connection may hold (max_conn_bytes: bodies still
+  // arriving on its streams + its uploads parked behind a full inbox -- without it one peer could
+  // open every concurrent stream and fill each with a maximum-size body): the stream is refused
+  if (it->second.body.size() + len > c->srv->max_request() + 5 || c->held + len > c->srv->max_conn_bytes()) {
     nghttp2_submit_rst_stream(s, NGHTTP2_FLAG_NONE, sid, NGHTTP2_REFUSED_STREAM);
+    c->held -= std::min(c->held, it->second.body.size());
     c->streams.erase(it);
+    c->srv->count_refused();
     return 0;
   }
   it->second.body.append(reinterpret_cast<const char*>(data), len);
+  c->held += len;
   return 0;
 }
 int on_frame_recv(nghttp2_session*, const nghttp2_frame* f, void* ud) {
@@ -183,7 +189,12 @@ int on_frame_recv(nghttp2_session*, const nghttp2_frame* f, void* ud) {
   return 0;
 }
 int on_stream_close(nghttp2_session*, int32_t sid, uint32_t, void* ud) {
-  static_cast<Conn*>(ud)->streams.erase(sid);
+  auto* c = static_cast<Conn*>(ud);
+  auto it = c->streams.find(sid);
+  if (it != c->streams.end()) {  // a body still held (a stream reset before its end)
+    c->held -= std::min(c->held, it->second.body.size());
+    c->streams.erase(it);
+  }
   return 0;
 }
 ssize_t read_resp(nghttp2_session* s, int32_t sid, uint8_t* buf, size_t length, uint32_t* flags,
@@ -225,8 +236,10 @@ uint64_t tag(uint64_t kind, int fd) { return (kind << 32) | (uint32_t)fd; }
 
 }  // namespace
 
-Server::Server(const std::string& host, int port, size_t max_inbox, size_t max_bytes, int idle_timeout_ms)
-    : idle_ms_(std::max(0, idle_timeout_ms)), cap_items_(std::max<size_t>(1, max_inbox)),
+Server::Server(const std::string& host, int port, size_t max_inbox, size_t max_bytes, int idle_timeout_ms,
+               size_t max_request)
+    : idle_ms_(std::max(0, idle_timeout_ms)), max_request_(std::max<size_t>(1, max_request)),
+      max_conn_bytes_(2 * (std::max<size_t>(1, max_request) + 5)), cap_items_(std::max<size_t>(1, max_inbox)),
       cap_bytes_(std::max<size_t>(1, max_bytes)) {
   lfd_ = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
   if (lfd_ < 0) throw std::runtime_error("socket() failed");
@@ -262,6 +275,11 @@ Server::Server(const std::string& host, int port, size_t max_inbox, size_t max_b
 
 Server::~Server() { close(); }
 
+void Server::count_refused() {
+  std::lock_guard<std::mutex> g(smu_);
+  stats_.refused_streams++;
+}
+
 void Server::wake() {
   uint64_t one = 1;
   ssize_t r = ::write(wake_fd_, &one, sizeof(one));
@@ -286,8 +304,13 @@ void Server::close() {
 bool Server::recv(Item& out, int timeout_ms) {
   std::unique_lock<std::mutex> g(qmu_);
   auto ready = [&] { return closed_.load() || !inbox_.empty(); };
+  // a timed wait through system_clock, as host/zmtp.cpp's timed_wait: libstdc++ implements
+  // steady_clock waits (wait_for) with pthread_cond_clockwait, which the GCC 11 ThreadSanitizer
+  // runtime does not intercept (every timed wait would read as a double lock in
+  // tools/sanitize_host.sh h2); a wall-clock jump only lengthens or shortens one bounded wait
   if (timeout_ms < 0) qcv_.wait(g, ready);
-  else if (!qcv_.wait_for(g, std::chrono::milliseconds(timeout_ms), ready)) return false;
+  else if (!qcv_.wait_until(g, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms), ready))
+    return false;
   if (inbox_.empty()) return false;
   out = std::move(inbox_.front());
   inbox_.pop_front();
@@ -426,6 +449,7 @@ void Server::on_readable(const std::shared_ptr<Conn>& c) {
         auto it = c->streams.find(d.first);
         if (it == c->streams.end()) continue;
         std::string body = std::move(it->second.body);
+        c->held -= std::min(c->held, body.size());  // dispatch re-counts what it parks
         dispatch(c, d.first, d.second, body);
       }
       if ((size_t)k >= budget) break;
@@ -552,6 +576,7 @@ void Server::dispatch(const std::shared_ptr<Conn>& c, int32_t stream, const std:
     if (try_push(std::move(it), bytes)) {
       respond(c, stream, action_response(1, "received"));
     } else {  // inbox full: this agent's call waits for room (the learner's backpressure)
+      c->held += bytes;
       Blocked b;
       b.conn = c;
       b.stream = stream;
@@ -658,6 +683,7 @@ void Server::service_parked() {
       }
       const size_t bytes = b.item.body.size() + 64;
       if (try_push(std::move(b.item), bytes)) {
+        c->held -= std::min(c->held, bytes);
         respond(c, b.stream, action_response(1, "received"));
         touched.push_back(c);
       } else {
@@ -688,8 +714,11 @@ void Server::service_parked() {
         touched.push_back(c);
         std::lock_guard<std::mutex> g(smu_);
         stats_.polls_timeout++;
-      } else if (newer) {  // a newer model whose archive is not built yet
+      } else if (newer) {  // a newer model whose archive was not built at the snapshot above
+        // (it may be by now: answer_poll re-reads the cell and can respond, so flush this conn --
+        // the sanitizer harness caught polls left unanswered here, csrc/net/selftest/h2_selftest.cpp)
         answer_poll(c, p.stream, false, p.deadline);
+        touched.push_back(c);
       } else {
         parked_.push_back(p);
       }

@@ -43,20 +43,24 @@ struct Item {
 
 struct Stats {
   uint64_t accepted = 0, requests = 0, frames = 0, actions = 0, polls = 0, polls_parked = 0, polls_timeout = 0,
-           bad_requests = 0, bytes_in = 0, inbox_waits = 0, dropped_conns = 0;
+           bad_requests = 0, bytes_in = 0, inbox_waits = 0, dropped_conns = 0, refused_streams = 0;
 };
 
 struct Conn;
 
 class Server {
  public:
-  // host "*" / "0.0.0.0" = all interfaces; port 0 = a free port
-  Server(const std::string& host, int port, size_t max_inbox, size_t max_bytes, int idle_timeout_ms);
+  // host "*" / "0.0.0.0" = all interfaces; port 0 = a free port; max_request: the largest request
+  // message (a connection holds at most two of them: bodies in flight + uploads parked on a full inbox)
+  Server(const std::string& host, int port, size_t max_inbox, size_t max_bytes, int idle_timeout_ms,
+         size_t max_request = size_t(256) << 20);
   ~Server();
   Server(const Server&) = delete;
   Server& operator=(const Server&) = delete;
 
   int port() const { return port_; }
+  size_t max_request() const { return max_request_; }
+  size_t max_conn_bytes() const { return max_conn_bytes_; }
   // the learner side: next queued item, false on timeout / closed
   bool recv(Item& out, int timeout_ms);
   // the newest model; ``ts`` may be empty (built on demand through kNeedTs)
@@ -95,9 +99,15 @@ class Server {
   void respond(const std::shared_ptr<Conn>& c, int32_t stream, std::string msg);
   void respond_status(const std::shared_ptr<Conn>& c, int32_t stream, int code, const char* message);
 
+ public:  // (the nghttp2 callbacks, I/O thread)
+  void count_refused();
+
+ private:
+
   int port_ = 0;
   int lfd_ = -1, epfd_ = -1, wake_fd_ = -1;
   int idle_ms_;
+  size_t max_request_, max_conn_bytes_;
   std::atomic<bool> closed_{false};
   std::thread io_;
   std::map<int, std::shared_ptr<Conn>> conns_;  // I/O thread only

@@ -120,3 +120,36 @@ def test_training_server_uses_the_native_server(cfgdir):  # noqa: F811
         assert st["frames"] >= 4 and st["actions"] >= 8 and st["polls"] >= 3
     finally:
         srv.close(save=False)
+
+
+def test_oversized_requests_are_refused_and_the_server_lives():
+    """max_request caps one message and twice that caps what one connection may hold (bodies in
+    flight + uploads parked on a full inbox): larger uploads are refused with a stream reset
+    instead of being buffered, and the connection keeps serving."""
+    s = mod.GrpcServer("127.0.0.1", 0, max_inbox=1, max_request=256 << 10)
+    ch, send, _, _ = _stubs(s.port)
+    try:
+        with pytest.raises(grpc.RpcError):
+            send(PbFrame(frame=b"y" * (300 << 10)), timeout=10)
+        assert send(PbFrame(frame=b"small"), timeout=10).code == 1
+        assert s.recv(1000)[1] == b"small"
+        # the inbox holds one item: park uploads of 200 KB until the connection's 2 x 256 KB is
+        # reached -- the rest are refused, nothing is buffered past the cap
+        assert send(PbFrame(frame=b"first"), timeout=10).code == 1  # fills the 1-item inbox
+        with cf.ThreadPoolExecutor(8) as ex:
+            futs = [ex.submit(send, PbFrame(frame=bytes([i]) * (200 << 10)), timeout=20) for i in range(8)]
+            time.sleep(1.0)
+            got = [s.recv(2000) for _ in range(9)]
+            ok = err = 0
+            for f in futs:
+                try:
+                    ok += f.result().code == 1
+                except grpc.RpcError:
+                    err += 1
+        assert ok >= 2 and err >= 1 and ok + err == 8, (ok, err)
+        assert got[0][1] == b"first" and sum(g is not None for g in got) == 1 + ok
+        assert s.stats()["refused_streams"] >= err
+        assert send(PbFrame(frame=b"after"), timeout=10).code == 1 and s.recv(1000)[1] == b"after"
+    finally:
+        ch.close()
+        s.close()

@@ -67,3 +67,25 @@ def test_network_parsers_survive_200k_mutants_under_asan_ubsan(tmp_path):
     m = re.search(r"\((\d+) accepted, (\d+) rejected\), (\d+) tensors read \((\d+) valid\)", out)
     acc, rej, tens, ok = map(int, m.groups())
     assert acc > 50_000 and rej > 50_000 and tens > 50_000 and ok > 1_000, out[-500:]  # both sides exercised
+
+
+@pytest.mark.skipif(shutil.which("g++") is None or not os.path.exists("/opt/conda/include/nghttp2/nghttp2.h"),
+                    reason="no host compiler / nghttp2 headers")
+def test_native_grpc_server_under_asan_ubsan_tsan_and_20k_mutants():
+    """The native gRPC server (csrc/net/h2grpc.cpp) parses whatever a TCP peer sends: built without
+    Python with an nghttp2 client harness (csrc/net/selftest/h2_selftest.cpp) it serves 8
+    concurrent clients (uploads, long polls, TorchScript on demand, model publishes, a 5-deep
+    inbox for backpressure) under ASan + UBSan and TSan with every upload delivered once, then
+    takes 20,000 mutated HTTP/2 client streams and a flood past its per-connection byte cap
+    (streams refused, not buffered) and still serves a valid client."""
+    r = subprocess.run([os.path.join(REPO, "tools", "sanitize_host.sh"), "h2", "8", "150", "20000", "5"],
+                       capture_output=True, text=True, timeout=900)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert out.count("traffic: 8 clients x 150 calls") == 2 and out.count("-- ok") == 3, out[-2000:]
+    assert "fuzz: 20000 mutants" in out
+    assert "ThreadSanitizer" not in out and "AddressSanitizer" not in out and "runtime error" not in out
+    import re
+
+    refused = int(re.search(r"(\d+) refused streams", out).group(1))
+    assert refused > 0, out[-1000:]
