@@ -389,12 +389,16 @@ class DeviceNatureCNN:
     @classmethod
     def _c1_src(cls, x) -> dict:
         """The conv1 weight gradient's frame source keywords for observations ``x``.  Frame-ring
-        rows of a whole T-step rollout are visited env-major (RRL_CNN_WGRAD1_ENV_MAJOR, default on):
-        the T observations of one env share frames, which then come from the CU's L2."""
+        rows of a whole T-step rollout are visited env-major from 4,096 envs (the T observations of
+        one env share frames, which then come from the CU's L2): at 8,192 envs that measured
+        493.7 -> 486.9 us per launch, at 2,048 -- whose ring, 130 MB, stays in the Infinity Cache
+        anyway -- 126.5 -> 129.9 us (profiles/r6_pong_ring_v4_ab.txt).  RRL_CNN_WGRAD1_ENV_MAJOR =
+        1 / 0 forces it on / off."""
         if cls.is_ring(x):
             kw = {"frames": x.frames, "fidx": x.fidx}
             T = getattr(x, "rollout_len", 0)
-            if T > 1 and x.fidx.shape[0] % T == 0 and os.environ.get("RRL_CNN_WGRAD1_ENV_MAJOR", "1") == "1":
+            em = os.environ.get("RRL_CNN_WGRAD1_ENV_MAJOR", "")
+            if T > 1 and x.fidx.shape[0] % T == 0 and (em == "1" or (em == "" and x.fidx.shape[0] // T >= 4096)):
                 kw["env_major_T"] = T
             return kw
         if cls.is_hist(x):
