@@ -49,6 +49,14 @@ def main():
     el = el.item()
     steps = a.steps * a.num_envs * a.rollout_len * comm.world
     m = tr.metrics()
+    # data parallel: every rank must hold the same parameters after the all-reduced updates
+    sync = None
+    if comm.world > 1:
+        p = (tr.model.params if tr.on_gpu else tr.params).detach()
+        hi, lo = p.clone(), p.clone()
+        comm.all_reduce_max_(hi)
+        comm.all_reduce_min_(lo)
+        sync = bool(torch.equal(hi, lo))
     if comm.rank == 0:
         out = {"metric": "env_steps_per_sec (A2C PongSynth-v0 pixels, Nature-CNN)", "value": steps / el,
                "unit": "env_steps/s", "n_gpus": comm.world, "steps": a.steps, "warmup": a.warmup,
@@ -56,7 +64,10 @@ def main():
                "dtype": "bf16 (fp32 accumulate, fp32 master weights)", "data": "synthetic env, random-init weights",
                "config": {"model": "NatureCNN-A2C", "global_batch": a.num_envs * a.rollout_len * comm.world,
                           "seq_len": a.rollout_len, "parallelism": f"dp{comm.world}"},
-               "train": {k: m[k] for k in ("AverageEpRet", "Episodes", "LossPi", "LossV", "Entropy")}}
+               "train": {k: m[k] for k in ("AverageEpRet", "Episodes", "LossPi", "LossV", "Entropy")},
+               "frame_ring": getattr(tr, "ring", None) is not None}
+        if sync is not None:
+            out["params_in_sync"] = sync
         if a.phase_timing:
             out["phases_ms"] = tr.timer.columns()
         print(json.dumps(out), flush=True)

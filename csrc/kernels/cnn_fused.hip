@@ -527,8 +527,12 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
   if constexpr (L::kRender) {
     if (ROLE == 1 && n0 < N) render(n0, 0);
   }
-  if constexpr (L::kRing) {  // the first image's rows straight from fidx: no wait on the table
+  if constexpr (L::kRing) {
+    // the first image's rows straight from fidx and its frame loads issued first; then this
+    // workgroup's images' rows staged in LDS (first read, image 1's, after barrier B0) -- staged
+    // before, the table's global loads and LDS stores sat in front of the first frame loads
     if (n0 < N) gload_ring(uniform_int4(*reinterpret_cast<const int4*>(A.fidx + 4 * (size_t)n0)));
+    ring_stage_table(const_cast<int4*>(rtab), A.fidx, N, n0, G, tid, kThreads);
   } else if (n0 < N) {
     gload(n0);
   }
@@ -692,11 +696,6 @@ template <int V>
 __global__ __launch_bounds__(cs16::kThreads, 1) void conv_stack16_fwd_kernel(Stack16Args args) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   const int tid = threadIdx.x;
-  if constexpr (cs16::L16<V>::kRing) {
-    // this workgroup's images' frame rows into LDS, once; first read (image 1's) after barrier B0
-    ring_stage_table(reinterpret_cast<int4*>(reinterpret_cast<uint8_t*>(smem) + cs16::L16<V>::kLds), args.fidx, args.N,
-                     blockIdx.x, gridDim.x, tid, cs16::kThreads);
-  }
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (wave < 8) stack16_role<1, V>(args, smem, tid, wave);
   else if (wave < 12) stack16_role<2, V>(args, smem, tid, wave);
@@ -1932,7 +1931,7 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
   uint4 rx[kXPT], ry[kYPT];
   // the next image's frame chunks: loaded (observations) or drawn (RENDER: the history row's 16
   // floats in SGPRs) into the same registers
-  static_assert(kXPT >= 4, "the ring form keeps two units of 4 x 8 raw bytes per thread");
+  static_assert(kXPT >= 4, "the ring form keeps one position's 4 x 16 raw bytes per thread");
   // This workgroup's images, in order k = 0 .. K - 1: n0 + k G, or (T > 1, rows t E + e of a
   // T-step rollout over E envs) env-major -- the T rows of env e = n0 + q G back to back, so with
   // the frame ring the 4-frame observations of consecutive images share 3 frames and those are
@@ -1951,9 +1950,6 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
   // frame ring: this workgroup's images' frame rows, staged in LDS after the images once (read
   // from the table a stage ahead; images past it read fidx directly)
   int4* rtab = reinterpret_cast<int4*>(reinterpret_cast<uint8_t*>(smem) + kLds);
-  if constexpr (RING) {
-    for (int k = tid; k < min(K, kRingTab); k += kThreads) rtab[k] = *reinterpret_cast<const int4*>(fidx + 4 * (size_t)img(k));
-  }
   auto ring_entry = [&](int k) -> int4 {
     return uniform_int4(k < kRingTab ? rtab[k] : *reinterpret_cast<const int4*>(fidx + 4 * (size_t)img(k)));
   };
@@ -1961,21 +1957,16 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
   int4 fr_next = make_int4(0, 0, 0, 0);
   auto xload = [&](int n) {
     if constexpr (RING) {
-      // units u = tid, tid + 512 (< 882): position u >> 1, rows 2 (u & 1) .. + 1 of frames 0..3
+      // thread tid < 441: position tid, all 16 bytes of frames 0..3 (one 16-byte load per frame:
+      // half the load instructions of 8-byte row pieces; the 4 registers the s2d path uses)
       const int4 fr = fr_next;
       (void)n;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int u = tid + kThreads * k;
-        if (u < 2 * kPongFramePos) {
-          const size_t off = (size_t)(u >> 1) * 16 + 8 * (u & 1);
-          const uint2 f0 = *reinterpret_cast<const uint2*>(frames + (size_t)fr.x * kPongFrameBytes + off);
-          const uint2 f1 = *reinterpret_cast<const uint2*>(frames + (size_t)fr.y * kPongFrameBytes + off);
-          const uint2 f2 = *reinterpret_cast<const uint2*>(frames + (size_t)fr.z * kPongFrameBytes + off);
-          const uint2 f3 = *reinterpret_cast<const uint2*>(frames + (size_t)fr.w * kPongFrameBytes + off);
-          rx[2 * k] = make_uint4(f0.x, f0.y, f1.x, f1.y);
-          rx[2 * k + 1] = make_uint4(f2.x, f2.y, f3.x, f3.y);
-        }
+      if (tid < kPongFramePos) {
+        const size_t off = (size_t)tid * 16;
+        rx[0] = *reinterpret_cast<const uint4*>(frames + (size_t)fr.x * kPongFrameBytes + off);
+        rx[1] = *reinterpret_cast<const uint4*>(frames + (size_t)fr.y * kPongFrameBytes + off);
+        rx[2] = *reinterpret_cast<const uint4*>(frames + (size_t)fr.z * kPongFrameBytes + off);
+        rx[3] = *reinterpret_cast<const uint4*>(frames + (size_t)fr.w * kPongFrameBytes + off);
       }
     } else if constexpr (RENDER) {
       float hv[kPongHist];
@@ -2014,6 +2005,9 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
     if constexpr (RING) fr_next = uniform_int4(*reinterpret_cast<const int4*>(fidx + 4 * (size_t)n));
     xload(n);
   }
+  if constexpr (RING) {  // staged after the first image's loads are in flight
+    for (int k = tid; k < min(K, kRingTab); k += kThreads) rtab[k] = *reinterpret_cast<const int4*>(fidx + 4 * (size_t)img(k));
+  }
   for (int k = 0; k < K; ++k) {
     const bool more = k + 1 < K;
     const int nn = more ? img(k + 1) : 0;  // the next image
@@ -2022,18 +2016,15 @@ __global__ __launch_bounds__(c1w::kThreads, 1) void conv1_wgrad8_kernel(const ui
       if (more) fr_next = ring_entry(k + 1);  // before this image's stores
     }
     if constexpr (RING) {
+      if (tid < kPongFramePos) {  // the 4 observation chunks (dy = 0..3) of position tid, as bf16
+        const uint32_t f0[4] = {rx[0].x, rx[0].y, rx[0].z, rx[0].w}, f1[4] = {rx[1].x, rx[1].y, rx[1].z, rx[1].w};
+        const uint32_t f2[4] = {rx[2].x, rx[2].y, rx[2].z, rx[2].w}, f3[4] = {rx[3].x, rx[3].y, rx[3].z, rx[3].w};
+        uint16_t* d = Xi + (tid + (kXW - 21) * (tid / 21)) * kLd;
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int u = tid + kThreads * k;
-        if (u < 2 * kPongFramePos) {  // observation chunks dy = 2h, 2h + 1 of position pix as bf16
-          const int pix = u >> 1, h = u & 1;
-          const uint4 c0 = pong_interleave_row(rx[2 * k].x, rx[2 * k].z, rx[2 * k + 1].x, rx[2 * k + 1].z);
-          const uint4 c1 = pong_interleave_row(rx[2 * k].y, rx[2 * k].w, rx[2 * k + 1].y, rx[2 * k + 1].w);
-          uint16_t* d = Xi + (pix + (kXW - 21) * (pix / 21)) * kLd + 32 * h;
-          *reinterpret_cast<uint4*>(d) = u8x8_to_bf16x8(make_uint2(c0.x, c0.y));
-          *reinterpret_cast<uint4*>(d + 8) = u8x8_to_bf16x8(make_uint2(c0.z, c0.w));
-          *reinterpret_cast<uint4*>(d + 16) = u8x8_to_bf16x8(make_uint2(c1.x, c1.y));
-          *reinterpret_cast<uint4*>(d + 24) = u8x8_to_bf16x8(make_uint2(c1.z, c1.w));
+        for (int dy = 0; dy < 4; ++dy) {
+          const uint4 c = pong_interleave_row(f0[dy], f1[dy], f2[dy], f3[dy]);
+          *reinterpret_cast<uint4*>(d + 16 * dy) = u8x8_to_bf16x8(make_uint2(c.x, c.y));
+          *reinterpret_cast<uint4*>(d + 16 * dy + 8) = u8x8_to_bf16x8(make_uint2(c.z, c.w));
         }
       }
     }

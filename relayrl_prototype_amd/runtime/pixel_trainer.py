@@ -315,17 +315,23 @@ class PixelA2CTrainer:
                 ts += [v for v in st.values() if torch.is_tensor(v)]
             return ts
         m = self.model
-        ts = [m.params, m.m, m.v, m.step_t, self.env.state, self.env.step_t, self.env.ep_acc, self.sample_t,
-              self.obs[0]]
-        return ts + ([self.ring.frames] if self.ring is not None else [])
+        # (the frame ring's frames are not snapshotted -- up to 520 MB per epoch at 8,192 envs: the
+        # restore rebuilds them from the env state, set_counters)
+        return [m.params, m.m, m.v, m.step_t, self.env.state, self.env.step_t, self.env.ep_acc, self.sample_t,
+                self.obs[0]]
 
     def counters(self) -> dict:
         return {"updates": self.updates, "total_steps": self.total_steps}
 
     def set_counters(self, c: dict):
+        """After an elastic snapshot restore (launcher.EpochSnapshot): host counters, the bf16
+        shadow weights and -- frame ring -- the ring's frames and the current observation's rows,
+        rebuilt from the restored env state."""
         self.updates, self.total_steps = int(c["updates"]), int(c["total_steps"])
         if self.on_gpu:
             self.model.refresh_shadow()
+            if self.ring is not None:
+                self.env.ring_fill(self.ring, self.obs[0])
 
     def drop_graphs(self):
         if self.on_gpu:

@@ -283,3 +283,55 @@ def test_pixel_update_frame_ring_env_major_wgrad(cuda, monkeypatch):
         torch.cuda.synchronize()
         grads.append(tr.model.grad.clone())
     torch.testing.assert_close(grads[1], grads[0], rtol=1e-4, atol=1e-6)
+
+
+def test_pong_ring_data_parallel_two_gloo_ranks_shared_gpu(cuda):
+    """Two ranks of the Pong A2C bench (frame ring on) on one GPU over gloo: the all-reduced
+    updates leave bitwise the same parameters on both ranks."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, RRL_DIST_BACKEND="gloo", RRL_FORCE_DEVICE="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+           f"--master-port={port}", "benchmarks/pong_a2c_bench.py", "--gpus", "2", "--num-envs", "128", "--steps", "3",
+           "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=repo, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    assert rec["n_gpus"] == 2 and rec["frame_ring"] is True and rec["params_in_sync"] is True and rec["value"] > 0
+
+
+def test_ring_elastic_snapshot_restore_replays_the_epochs(cuda):
+    """The elastic epoch-start snapshot (launcher.EpochSnapshot) leaves the ring's frames out and
+    the restore rebuilds them from the env state (set_counters -> pong_ring_fill): two epochs
+    replayed after a restore -- over a frame store scribbled in between -- are bitwise the two
+    epochs that followed the snapshot."""
+    from relayrl_prototype_amd.runtime.launcher import EpochSnapshot
+    from relayrl_prototype_amd.runtime.pixel_trainer import PixelA2CConfig, PixelA2CTrainer
+
+    tr = PixelA2CTrainer(PixelA2CConfig(num_envs=300, rollout_len=4, seed=3, use_graphs=True, max_episode_steps=7,
+                                        frame_ring=True, fused_render=False), device=cuda)
+    for _ in range(3):  # eager warm-up, capture + replay of both buffer parities
+        tr.train_epoch()
+    snap = EpochSnapshot()
+    snap.take(tr)
+    assert all(t.data_ptr() != tr.ring.frames.data_ptr() for t in tr.snapshot_tensors())
+    runs = []
+    for _ in range(2):
+        for _ in range(2):
+            tr.train_epoch()
+        torch.cuda.synchronize()
+        runs.append((tr.model.params.clone(), tr.act.clone(), tr.rew.clone()))
+        tr.ring.frames.fill_(7)  # whatever the store held is gone
+        snap.restore(tr)
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
