@@ -401,6 +401,14 @@ struct L16 {
   // bit 64 -- frame ring: the frame's 4 frames are read from the PongSynth frame store through
   // the observation's frame rows fidx[n][4] (pong_render.h) and interleaved into the same LDS image
   static constexpr bool kRing = (V & 64) != 0;
+  // bit 128 (with 64) -- the ring's frames as one 16-byte load per (position, frame) on a pair of
+  // lanes (frames 0, 1 / 2, 3), which swap the rows the other one stores through DPP: half the
+  // load instructions of the 8-byte row pieces (A/B, tools/cnn_kbench.py fwd16_ring16)
+  static constexpr bool kRing16 = kRing && (V & 128) != 0;
+  // bit 256 (with 64) -- only the conv1 waves (tid < 441) load and store the frame: one 16-byte
+  // load per frame per position, every load instruction 1 KB of one frame; the conv2 / conv3 waves
+  // hold no frame registers (A/B, tools/cnn_kbench.py fwd16_ring_wide)
+  static constexpr bool kRingWide = kRing && (V & 256) != 0;
   static constexpr bool kSetprio = (V & 4) != 0;  // s_setprio 1 around each role's MFMA clusters
   // static wave priority for the whole kernel (A/B): bit 1 raises the conv2 role, bit 8 the conv3 role
   static constexpr int kPrioRole2 = (V & 1) ? 2 : 0, kPrioRole3 = (V & 8) ? 2 : 0;
@@ -488,13 +496,35 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
   }
 
   const int G = gridDim.x, n0 = blockIdx.x, N = A.N;
-  uint4 rx[L::kRender ? 1 : kXPerT];
+  uint4 rx[L::kRender ? 1 : (L::kRingWide ? (ROLE == 1 ? 4 : 1) : kXPerT)];
   static_assert(kXPerT >= 2, "the ring form keeps 4 x 8 raw bytes per thread in rx[0..1]");
   const int4* rtab = reinterpret_cast<const int4*>(reinterpret_cast<const uint8_t*>(smem) + L::kLds);
   // frame ring: unit tid < 882 loads position tid >> 1, rows 2 (tid & 1) .. + 1 of frames 0..3 (8
   // bytes each) of the image with frame rows fr, kept raw until the LDS store (the loads stay in
   // flight while this frame computes)
   auto gload_ring = [&](int4 fr) {
+    if constexpr (L::kRingWide) {
+      if constexpr (ROLE == 1) {
+        if (tid < kPongFramePos) {  // position tid of frames 0..3
+          const size_t off = (size_t)tid * 16;
+          rx[0] = *reinterpret_cast<const uint4*>(A.frames + (size_t)fr.x * kPongFrameBytes + off);
+          rx[1] = *reinterpret_cast<const uint4*>(A.frames + (size_t)fr.y * kPongFrameBytes + off);
+          rx[2] = *reinterpret_cast<const uint4*>(A.frames + (size_t)fr.z * kPongFrameBytes + off);
+          rx[3] = *reinterpret_cast<const uint4*>(A.frames + (size_t)fr.w * kPongFrameBytes + off);
+        }
+      }
+      return;
+    }
+    if constexpr (L::kRing16) {
+      if (tid < 2 * kPongFramePos) {  // position tid >> 1, frames 2 fp and 2 fp + 1, all 4 rows
+        const int fp = tid & 1;
+        const size_t off = (size_t)(tid >> 1) * 16;
+        const int ra = fp ? fr.z : fr.x, rb = fp ? fr.w : fr.y;
+        rx[0] = *reinterpret_cast<const uint4*>(A.frames + (size_t)ra * kPongFrameBytes + off);
+        rx[1] = *reinterpret_cast<const uint4*>(A.frames + (size_t)rb * kPongFrameBytes + off);
+      }
+      return;
+    }
     if (tid < 2 * kPongFramePos) {
       const size_t off = (size_t)(tid >> 1) * 16 + 8 * (tid & 1);
       const uint2 f0 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.x * kPongFrameBytes + off);
@@ -545,7 +575,37 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
       if (n < N) {
         // the next image's frame rows: read from the table before this image's stores
         const int4 frn = n + G < N ? ring_row(rtab, A.fidx, n0, G, j + 1) : make_int4(0, 0, 0, 0);
-        if (tid < 2 * kPongFramePos) {  // rows 2h, 2h + 1 of position pix, interleaved across the 4 frames
+        if constexpr (L::kRingWide) {
+          if constexpr (ROLE == 1) {
+            if (tid < kPongFramePos) {  // the 4 observation chunks (dy = 0..3) of position tid
+              const int pa = tid / 21;
+              uint8_t* d = F + (tid + (kFW - 21) * pa) * kFS;
+              *reinterpret_cast<uint4*>(d) = pong_interleave_row(rx[0].x, rx[1].x, rx[2].x, rx[3].x);
+              *reinterpret_cast<uint4*>(d + 16) = pong_interleave_row(rx[0].y, rx[1].y, rx[2].y, rx[3].y);
+              *reinterpret_cast<uint4*>(d + 32) = pong_interleave_row(rx[0].z, rx[1].z, rx[2].z, rx[3].z);
+              *reinterpret_cast<uint4*>(d + 48) = pong_interleave_row(rx[0].w, rx[1].w, rx[2].w, rx[3].w);
+            }
+          }
+        } else if constexpr (L::kRing16) {
+          if (tid < 2 * kPongFramePos) {
+            // lane fp (of an adjacent pair) holds frames 2 fp, 2 fp + 1 and stores rows 2 fp, 2 fp + 1:
+            // it keeps those rows of its frames and swaps the other two rows with its partner
+            const int pix = tid >> 1, pa = pix / 21, fp = tid & 1;
+            const uint32_t s0 = fp ? rx[0].x : rx[0].z, s1 = fp ? rx[0].y : rx[0].w;
+            const uint32_t s2 = fp ? rx[1].x : rx[1].z, s3 = fp ? rx[1].y : rx[1].w;
+            const uint32_t k0 = fp ? rx[0].z : rx[0].x, k1 = fp ? rx[0].w : rx[0].y;
+            const uint32_t k2 = fp ? rx[1].z : rx[1].x, k3 = fp ? rx[1].w : rx[1].y;
+            // quad_perm [1, 0, 3, 2]: each lane reads its pair partner
+            const uint32_t r0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)s0, 0xB1, 0xF, 0xF, false);
+            const uint32_t r1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)s1, 0xB1, 0xF, 0xF, false);
+            const uint32_t r2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)s2, 0xB1, 0xF, 0xF, false);
+            const uint32_t r3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)s3, 0xB1, 0xF, 0xF, false);
+            uint8_t* d = F + (pix + (kFW - 21) * pa) * kFS + 32 * fp;
+            *reinterpret_cast<uint4*>(d) = fp ? pong_interleave_row(r0, r2, k0, k2) : pong_interleave_row(k0, k2, r0, r2);
+            *reinterpret_cast<uint4*>(d + 16) =
+                fp ? pong_interleave_row(r1, r3, k1, k3) : pong_interleave_row(k1, k3, r1, r3);
+          }
+        } else if (tid < 2 * kPongFramePos) {  // rows 2h, 2h + 1 of position pix, interleaved across the 4 frames
           const int pix = tid >> 1, pa = pix / 21, h = tid & 1;
           uint8_t* d = F + (pix + (kFW - 21) * pa) * kFS + 32 * h;
           *reinterpret_cast<uint4*>(d) = pong_interleave_row(rx[0].x, rx[0].z, rx[1].x, rx[1].z);
@@ -770,6 +830,10 @@ extern "C" int rrl_conv_stack_fwd(const uint8_t* x, const float* hist, const uin
   if (frames) {  // frame ring (frames [R][E][7056] + fidx [N][4]): the default 16-wave layout only
     const int g = max_grid >= 0 ? max_grid : ((-max_grid) & 0xffff);
     const int probe = max_grid >= 0 ? 64 : ((-max_grid) >> 16);
+    if (probe == 64 + 256)  // the conv1-waves-only, 1 KB-per-load form (A/B)
+      return launch_conv_stack16_fwd<64 + 256>(nullptr, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st, frames, fidx);
+    if (probe == 64 + 128)  // the 16-byte-load + DPP form (A/B)
+      return launch_conv_stack16_fwd<64 + 128>(nullptr, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st, frames, fidx);
     if (probe != 64) return -4;
     return launch_conv_stack16_fwd<64>(nullptr, nullptr, w1, b1, w2, b2, w3, b3, y1, y2, y3, N, g, st, frames, fidx);
   }

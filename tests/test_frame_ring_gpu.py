@@ -166,18 +166,25 @@ def test_ring_conv_stack_equals_the_obs_path(cuda, N):
     W = [sh[o["w1"]:o["b1"]], params[o["b1"]:o["b1"] + 32], sh[o["w2"]:o["b2"]], params[o["b2"]:o["b2"] + 64],
          sh[o["w3"]:o["b3"]], params[o["b3"]:o["b3"] + 64]]
     outs = []
-    for use_ring in (False, True):
+    # ring16: 16-byte loads on lane pairs + DPP row swap (probe 192); ring_wide: the conv1 waves load
+    # whole positions of the 4 frames (probe 320)
+    for form in ("s2d", "ring", "ring16", "ring_wide"):
         a1 = torch.full((N * 400 * 32,), float("nan"), dtype=torch.bfloat16, device=cuda)
         a2 = torch.full((N * 81 * 64,), float("nan"), dtype=torch.bfloat16, device=cuda)
         a3 = torch.full((N * FC_IN,), float("nan"), dtype=torch.bfloat16, device=cuda)
-        if use_ring:
+        if form == "ring":
             h.conv_stack_fwd(None, *W, a1, a2, a3, N, frames=ring.frames, fidx=fidx)
+        elif form == "ring16":
+            h.conv_stack_fwd(None, *W, a1, a2, a3, N, probe=192, frames=ring.frames, fidx=fidx)
+        elif form == "ring_wide":
+            h.conv_stack_fwd(None, *W, a1, a2, a3, N, probe=320, frames=ring.frames, fidx=fidx)
         else:
             h.conv_stack_fwd(obs, *W, a1, a2, a3, N, probe=64)
         torch.cuda.synchronize()
         outs.append((a1, a2, a3))
-    for f, r in zip(*outs):
-        assert torch.isfinite(f.float()).all() and torch.equal(f, r)
+    for other in outs[1:]:
+        for f, r in zip(other, outs[0]):
+            assert torch.isfinite(f.float()).all() and torch.equal(f, r)
 
 
 def test_ring_conv1_wgrad_equals_the_obs_path(cuda):

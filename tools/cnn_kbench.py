@@ -85,6 +85,10 @@ def main():
     Tb = Nb // Nf if Nb % Nf == 0 else 0
     fns["fwd16_ring"] = lambda: h.conv_stack_fwd(None, *W[1], *W[2], *W[3], a1, a2, a3, Nf, frames=frames,
                                                  fidx=fidx[:Nf])
+    fns["fwd16_ring16"] = lambda: h.conv_stack_fwd(None, *W[1], *W[2], *W[3], a1, a2, a3, Nf, probe=192,
+                                                   frames=frames, fidx=fidx[:Nf])
+    fns["fwd16_ring_wide"] = lambda: h.conv_stack_fwd(None, *W[1], *W[2], *W[3], a1, a2, a3, Nf, probe=320,
+                                                      frames=frames, fidx=fidx[:Nf])
     fns["wgrad1_8_ring"] = lambda: h.conv1_wgrad8(None, da1, part, bpart, Nb, min(Nb, cus), frames=frames,
                                                   fidx=fidx[:Nb])
     fns["wgrad1_8_ring_em"] = lambda: h.conv1_wgrad8(None, da1, part, bpart, Nb, min(Nb, cus), frames=frames,
