@@ -58,7 +58,7 @@ int rrl_pong_step_render(float* state, const int32_t* act, float* rew, float* do
                          float* ep_acc, uint8_t* obs, int N, unsigned long long seed, unsigned long long step,
                          const unsigned long long* step_base, int max_steps, int reset_all, uint8_t* frames,
                          int32_t* fidx, int R, void* stream);
-int rrl_pong_ring_fill(const float* state, uint8_t* frames, int32_t* fidx, int N, int R, unsigned long long step,
+int rrl_pong_ring_fill(float* state, uint8_t* frames, int32_t* fidx, int N, int R, unsigned long long step,
                        const unsigned long long* step_base, void* stream);
 int rrl_conv_stack_fwd(const uint8_t* x, const float* hist, const uint8_t* frames, const int32_t* fidx,
                        const uint16_t* w1, const float* b1,

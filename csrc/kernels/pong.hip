@@ -240,14 +240,18 @@ RRL_DEV void pong_ring_write(const RingOut& ro, int e, int N, const float* ss, u
 
 // The ring rebuilt from the env state alone (a restored checkpoint / elastic snapshot): the 4-frame
 // stack IS a function of the 16-float history, so frames 0..3 of every env are drawn into slots
-// st - 3 .. st and the observation points at them.  One workgroup per env.
-__global__ void __launch_bounds__(256) pong_ring_fill_kernel(const float* __restrict__ state, RingOut ro,
+// st - 3 .. st and the observation points at them.  The slots now hold 4 frames of history each,
+// so the env's distinct-frame count becomes 4 (a checkpoint from before the count existed has 0
+// there; a recently reset env's older history frames are copies of its reset frame, so pointing at
+// them is the same observation).  One workgroup per env.
+__global__ void __launch_bounds__(256) pong_ring_fill_kernel(float* __restrict__ state, RingOut ro,
                                                              uint32_t step_lo, uint32_t step_hi,
                                                              const unsigned long long* __restrict__ step_base) {
   __shared__ uint32_t rows[4][kPongHW];
   __shared__ float hv[kPongHist];
   const int e = blockIdx.x, N = gridDim.x, t = threadIdx.x;
   if (t < kPongHist) hv[t] = state[(size_t)e * kPongState + P_HIST + t];
+  if (t == 0) state[(size_t)e * kPongState + P_VALID] = 4.f;
   __syncthreads();
   const long long st = pong_abs_step(step_lo, step_hi, step_base);
   for (int q = t; q < 4 * kPongHW; q += 256) {
@@ -391,7 +395,7 @@ int rrl_pong_step_render(float* state, const int32_t* act, float* rew, float* do
 }
 
 // the ring rebuilt from the env state (restore): frames of steps st - 3 .. st and fidx [N][4]
-int rrl_pong_ring_fill(const float* state, uint8_t* frames, int32_t* fidx, int N, int R, unsigned long long step,
+int rrl_pong_ring_fill(float* state, uint8_t* frames, int32_t* fidx, int N, int R, unsigned long long step,
                        const unsigned long long* step_base, void* stream_) {
   if (N < 1) return 0;
   if (!frames || !fidx || R < 5) return -1;

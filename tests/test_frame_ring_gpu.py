@@ -76,7 +76,11 @@ def test_ring_fill_rebuilds_the_observation_from_state(cuda):
         e_ring.step(a, fidx, ring=ring)
     ring2 = FrameRing(N, 7, cuda)
     fidx2 = torch.full((N, 4), -1, dtype=torch.int32, device=cuda)
+    # a checkpoint from before the distinct-frame count (state slot 10) existed holds 0 there: the
+    # fill makes it 4, the frames it drew being the env's whole history
+    e_ring.state.view(N, -1)[:, 10] = 0.0
     e_ring.ring_fill(ring2, fidx2)
+    assert (e_ring.state.view(N, -1)[:, 10] == 4.0).all()
     torch.cuda.synchronize()
     assert torch.equal(ring2.gather_s2d(fidx2), obs)
     # and stepping on from the rebuilt ring stays on the observation path
