@@ -430,6 +430,15 @@ struct L16 {
 };
 }  // namespace cs16
 
+// The frame ring's load / store unit of thread tid in the 16-wave forward: position
+// 32 (tid / 64) + tid % 32, rows 2h, 2h + 1 with h = (tid / 32) % 2 -- the two halves of a wave
+// take the two row pairs of the same 32 positions, so each 16-byte LDS store instruction's lanes
+// land 96 bytes apart in distinct bank groups (the pairing of adjacent lanes on one position put
+// lanes 1 and 6 of every 8 on the same banks: 2-way conflicts in the store phase every barrier
+// waits for); each load instruction still reads 512 contiguous bytes of a frame
+__device__ __forceinline__ int ring_pos(int tid) { return 32 * (tid >> 6) + (tid & 31); }
+__device__ __forceinline__ int ring_half(int tid) { return (tid >> 5) & 1; }
+
 // chunk c of frame position r in the fused-render frame buffer (positions contiguous, 64 B each)
 __device__ __forceinline__ int rfs_chunk(int r, int c) { return r * 64 + 16 * (c ^ (2 * ((r >> 2) & 1))); }
 
@@ -525,8 +534,8 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
       }
       return;
     }
-    if (tid < 2 * kPongFramePos) {
-      const size_t off = (size_t)(tid >> 1) * 16 + 8 * (tid & 1);
+    if (ring_pos(tid) < kPongFramePos) {
+      const size_t off = (size_t)ring_pos(tid) * 16 + 8 * ring_half(tid);
       const uint2 f0 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.x * kPongFrameBytes + off);
       const uint2 f1 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.y * kPongFrameBytes + off);
       const uint2 f2 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.z * kPongFrameBytes + off);
@@ -605,8 +614,8 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
             *reinterpret_cast<uint4*>(d + 16) =
                 fp ? pong_interleave_row(r1, r3, k1, k3) : pong_interleave_row(k1, k3, r1, r3);
           }
-        } else if (tid < 2 * kPongFramePos) {  // rows 2h, 2h + 1 of position pix, interleaved across the 4 frames
-          const int pix = tid >> 1, pa = pix / 21, h = tid & 1;
+        } else if (ring_pos(tid) < kPongFramePos) {  // rows 2h, 2h + 1 of position pix, interleaved across the 4 frames
+          const int pix = ring_pos(tid), pa = pix / 21, h = ring_half(tid);
           uint8_t* d = F + (pix + (kFW - 21) * pa) * kFS + 32 * h;
           *reinterpret_cast<uint4*>(d) = pong_interleave_row(rx[0].x, rx[0].z, rx[1].x, rx[1].z);
           *reinterpret_cast<uint4*>(d + 16) = pong_interleave_row(rx[0].y, rx[0].w, rx[1].y, rx[1].w);
