@@ -23,20 +23,52 @@ uint64_t splitmix(uint64_t& s) {
   return z ^ (z >> 31);
 }
 
-// y[O] = act(b + x[I] @ Wt[I][O]).  The inner loop runs over contiguous outputs so the
-// compiler vectorises it; target_clones picks AVX-512 / AVX2 at load time.
-RRL_TARGET_CLONES void dense(const float* __restrict x, int I,
-                                                                         const float* __restrict wt,
-                                                                         const float* __restrict b, int O,
-                                                                         float* __restrict y, bool relu) {
-  for (int o = 0; o < O; ++o) y[o] = b[o];
+// y[O] = act(b + x[I] @ Wt[I][O]).  Outputs in blocks of 64 whose accumulators stay in
+// registers across the whole input loop (4 zmm / 8 ymm), so each weight row is one streamed
+// load + FMA; the plain axpy form stored and reloaded y on every input (128 x 128 layer:
+// 1.12-1.24 -> 0.73-0.80 us at batch 1).  target_clones picks AVX-512 / AVX2 at load time.
+RRL_TARGET_CLONES void dense(const float* __restrict x, int I, const float* __restrict wt,
+                             const float* __restrict b, int O, float* __restrict y, bool relu) {
+  constexpr int kB = 64;
+  int o0 = 0;
+  for (; o0 + kB <= O; o0 += kB) {
+    float acc[kB];
+    for (int k = 0; k < kB; ++k) acc[k] = b[o0 + k];
+    for (int i = 0; i < I; ++i) {
+      const float xi = x[i];
+      const float* w = wt + static_cast<size_t>(i) * O + o0;
+#pragma GCC unroll 64
+      for (int k = 0; k < kB; ++k) acc[k] += xi * w[k];
+    }
+    for (int k = 0; k < kB; ++k) y[o0 + k] = relu ? (acc[k] > 0.f ? acc[k] : 0.f) : acc[k];
+  }
+  if (o0 == O) return;
+  for (int o = o0; o < O; ++o) y[o] = b[o];
   for (int i = 0; i < I; ++i) {
     const float xi = x[i];
     const float* w = wt + static_cast<size_t>(i) * O;
-    for (int o = 0; o < O; ++o) y[o] += xi * w[o];
+    for (int o = o0; o < O; ++o) y[o] += xi * w[o];
   }
   if (relu)
-    for (int o = 0; o < O; ++o) y[o] = y[o] > 0.f ? y[o] : 0.f;
+    for (int o = o0; o < O; ++o) y[o] = y[o] > 0.f ? y[o] : 0.f;
+}
+
+// y[O] = b + W[O][I] @ x for a narrow head (the action logits, the value): one vectorised dot
+// product per output -- through dense()'s tail each output was a serial chain of I FMAs on y[o]
+RRL_TARGET_CLONES void dense_dot(const float* __restrict x, int I, const float* __restrict w,
+                                 const float* __restrict b, int O, float* __restrict y) {
+  for (int o = 0; o < O; ++o) {
+    const float* wr = w + static_cast<size_t>(o) * I;
+    float part[16] = {};
+    int i = 0;
+    for (; i + 16 <= I; i += 16)
+#pragma GCC unroll 16
+      for (int k = 0; k < 16; ++k) part[k] += x[i + k] * wr[i + k];
+    float s = 0.f;
+    for (; i < I; ++i) s += x[i] * wr[i];
+    for (int k = 0; k < 16; ++k) s += part[k];
+    y[o] = b[o] + s;
+  }
 }
 }  // namespace
 
@@ -44,6 +76,9 @@ NativePolicy::NativePolicy(int D_, int H_, int A_, bool disc, uint64_t seed) : D
   if (D <= 0 || H <= 0 || A <= 0) throw std::invalid_argument("NativePolicy: dims must be positive");
   uint64_t s = seed;
   for (auto& w : s_) w = splitmix(s);
+  h1_.resize(H);
+  h2_.resize(H);
+  z_.resize(A);
 }
 
 void NativePolicy::unpack(Net& n, const float* p, int D, int H, int O, bool gaussian) {
@@ -61,6 +96,7 @@ void NativePolicy::unpack(Net& n, const float* p, int D, int H, int O, bool gaus
   n.b2.assign(p, p + H);
   p += H;
   transpose(p, O, H, n.w3t);
+  n.w3.assign(p, p + static_cast<size_t>(O) * H);
   p += static_cast<size_t>(O) * H;
   n.b3.assign(p, p + O);
   p += O;
@@ -83,7 +119,8 @@ void NativePolicy::load(const float* pi, int64_t n_pi, const float* vf, int64_t 
 void NativePolicy::trunk(const Net& n, int O, const float* x, float* out, float* h1, float* h2) const {
   dense(x, D, n.w1t.data(), n.b1.data(), H, h1, true);
   dense(h1, H, n.w2t.data(), n.b2.data(), H, h2, true);
-  dense(h2, H, n.w3t.data(), n.b3.data(), O, out, false);
+  if (O < 16) dense_dot(h2, H, n.w3.data(), n.b3.data(), O, out);
+  else dense(h2, H, n.w3t.data(), n.b3.data(), O, out, false);
 }
 
 double NativePolicy::uniform() {  // xoshiro256+ -> [0, 1)
@@ -125,7 +162,7 @@ void NativePolicy::value(const float* obs, int N, float* out) const {
 
 void NativePolicy::step(const float* obs, const float* mask, int N, int32_t* act_i, float* act_f, float* logp,
                         float* v) {
-  std::vector<float> h1(H), h2(H), z(A);
+  std::vector<float>&h1 = h1_, &h2 = h2_, &z = z_;
   constexpr double kHalfLog2Pi = 0.9189385332046727;
   for (int r = 0; r < N; ++r) {
     const float* x = obs + static_cast<size_t>(r) * D;

@@ -26,10 +26,12 @@ class NativePolicy {
  private:
   struct Net {
     std::vector<float> w1t, b1, w2t, b2, w3t, b3, log_std;  // w*t: [in][out]
+    std::vector<float> w3;  // the head [out][in] as well: dot products for narrow heads
   };
   void trunk(const Net& n, int out_dim, const float* x, float* out, float* h1, float* h2) const;
   static void unpack(Net& n, const float* p, int D, int H, int O, bool gaussian);
   Net pi_, vf_;
+  std::vector<float> h1_, h2_, z_;  // step()'s scratch (step is not reentrant: it advances the RNG)
   bool has_vf_ = false;
   uint64_t s_[4];
   double uniform();

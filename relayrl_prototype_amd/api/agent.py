@@ -310,6 +310,15 @@ class RelayRLAgent:
         with self._policy_lock:
             p = self.policy
             mask_a = np.ones(p.act_dim, np.float32) if mask is None else np.asarray(mask, np.float32)
+            nat = getattr(p, "_nat", None)
+            if nat is not None and obs_a.size == p.obs_dim and mask_a.size == p.act_dim:
+                # the built-in MLP: policy step and the episode row in one native call
+                sink = rec.sink(p.obs_dim, p.discrete, p.act_dim)
+                obs_a, mask_a = np.ascontiguousarray(obs_a), np.ascontiguousarray(mask_a)
+                a0, logp, v = nat.step_row(obs_a, mask_a, sink, rec.n)
+                rec.n += 1
+                aux = {"logp_a": logp} if v is None else {"logp_a": logp, "v": v}
+                return RelayRLAction._trusted(obs_a, a0, mask_a, aux)
             act, data = p.step(obs_a, mask_a)
         if getattr(p, "is_torchscript", False):
             return self._record_plugin_step(obs_a, mask_a, act, data)

@@ -110,6 +110,15 @@ class RelayRLAction:
         self._done = bool(done)
         self._reward_updated = bool(reward_updated)
 
+    @classmethod
+    def _trusted(cls, obs, act, mask, data) -> "RelayRLAction":
+        """A step's record from arrays already in canonical form (contiguous, supported dtypes:
+        the agent's native step), without re-validating them -- request_for_action's fast path."""
+        a = object.__new__(cls)
+        a._obs, a._act, a._mask, a._rew, a._data = obs, act, mask, 0.0, data
+        a._done = a._reward_updated = False
+        return a
+
     # getters (o3_action.rs:96-160)
     def get_obs(self) -> Optional[np.ndarray]:
         return self._obs
@@ -536,6 +545,7 @@ class EpisodeRecorder:
         self.capacity = int(capacity)
         self.n = 0
         self._shapes = None
+        self._sink = None
 
     def _alloc(self, obs, act, mask):
         c = self.capacity
@@ -547,6 +557,21 @@ class EpisodeRecorder:
         self.val = np.full(c, np.nan, np.float32)  # V(s_t) when the policy has a value head (reference wire)
         self.done = np.zeros(c, np.uint8)
         self._shapes = (obs.size, act.size, act.dtype.kind, None if mask is None else mask.size)
+        self._sink = None
+
+    def sink(self, obs_size: int, discrete: bool, act_dim: int):
+        """The columns as a native ``RowSink`` for ``NativePolicy.step_row`` (which writes one
+        row per call from C++), allocated for these shapes as ``record`` would for the policy's
+        actions (0-d int32 when discrete, [act_dim] float32 otherwise) and [act_dim] masks."""
+        key = (obs_size, 1, "i", act_dim) if discrete else (obs_size, act_dim, "f", act_dim)
+        if self._shapes != key:
+            if self.n:
+                raise ValueError("observation/action shapes changed within an episode")
+            act = np.zeros((), np.int32) if discrete else np.zeros(act_dim, np.float32)
+            self._alloc(np.empty(obs_size, np.float32), act, np.empty(act_dim, np.float32))
+        if self._sink is None:
+            self._sink = _native.RowSink(self.obs, self.act, self.mask, self.logp, self.val, self.rew, self.done)
+        return self._sink
 
     def record(self, obs: np.ndarray, act: np.ndarray, mask, logp, val=None) -> None:
         key = (obs.size, act.size, act.dtype.kind, None if mask is None else mask.size)

@@ -52,7 +52,8 @@ def test_departed_reference_agent_costs_the_learner_nothing(cfgdir):  # noqa: F8
         d.close()  # the agent is gone; its PULL was never bound
         assert ep.ref_agents
         ts = _timed_publishes(srv)
-        assert max(ts) < 5e-3, ts  # round 5: 1.03 s each
+        # a pointer swap + wake-up: ~0.02-0.2 ms; the bound leaves room for a loaded CI host
+        assert np.median(ts) < 2e-3 and max(ts) < 50e-3, ts  # round 5: 1.03 s each
         t_end = time.time() + 10
         while not ep._ref_push_dead and time.time() < t_end:
             srv.algorithm.version += 1
@@ -96,7 +97,7 @@ def test_live_reference_agent_gets_the_newest_model_without_stalling(cfgdir):  #
             blob = srv.service.publish_model()
             ts.append(time.perf_counter() - t0)
             pis.append(blob.pi.copy())
-        assert np.median(ts) < 2e-3 and max(ts) < 5e-3, ts  # round 5: 31 ms (TorchScript export inline)
+        assert np.median(ts) < 2e-3 and max(ts) < 20e-3, ts  # round 5: 31 ms (TorchScript export inline)
         assert ep.flush(10)
         got = []
         while True:

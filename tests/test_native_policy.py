@@ -62,3 +62,74 @@ def test_native_policy_rejects_bad_sizes():
     n = _native.NativePolicy(4, 16, 2, True)
     with pytest.raises(ValueError):
         n.load(np.zeros(10, np.float32))
+
+
+@pytest.mark.parametrize("H,A", [(100, 3), (128, 20), (192, 2)])
+def test_native_forward_blocked_and_tail_widths(H, A):
+    """dense(): 64-wide register blocks plus the axpy tail (H = 100, 192), the dot-product head
+    (A < 16) and the transposed head (A = 20)."""
+    p = _policy(True, D=5, H=H, A=A)
+    x = np.random.default_rng(3).standard_normal((17, 5)).astype(np.float32)
+    np.testing.assert_allclose(p._nat.logits(x), p.logits(x), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(p._nat.value(x), p.value(x), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("discrete", [True, False])
+@pytest.mark.parametrize("vf", [True, False])
+def test_step_row_matches_step_and_writes_the_episode_row(discrete, vf):
+    """NativePolicy.step_row (request_for_action's native path): the same draws as step() on
+    the same RNG stream, and the row written into the EpisodeRecorder's columns."""
+    from relayrl_prototype_amd.types import EpisodeRecorder
+
+    a, b = _policy(discrete, vf=vf), _policy(discrete, vf=vf)
+    rec = EpisodeRecorder(8)
+    sink = rec.sink(6, discrete, 3)
+    rng = np.random.default_rng(4)
+    for i in range(8):
+        x = rng.standard_normal(6).astype(np.float32)
+        m = np.array([1, 0, 1], np.float32) if discrete else np.ones(3, np.float32)
+        act, data = a.step(x, m)
+        a0, logp, v = b._nat.step_row(x, m, sink, i)
+        rec.n += 1
+        if discrete:
+            assert a0.shape == () and a0.dtype == np.int32 and int(a0) == int(act[0]) and int(a0) != 1
+        else:
+            assert a0.shape == (3,) and np.array_equal(a0, act[0])
+        assert logp.shape == () and logp == data["logp_a"][0]
+        if vf:
+            assert v.shape == () and v == data["v"][0]
+        else:
+            assert v is None
+        np.testing.assert_array_equal(rec.obs[i], x)
+        np.testing.assert_array_equal(rec.mask[i], m)
+        np.testing.assert_array_equal(rec.act[i], np.asarray(a0).reshape(-1))
+        assert rec.logp[i] == logp and rec.rew[i] == 0 and rec.done[i] == 0
+        assert (np.isnan(rec.val[i]) if not vf else rec.val[i] == v)
+    with pytest.raises(IndexError):
+        b._nat.step_row(x, m, sink, 8)
+    with pytest.raises(ValueError):
+        b._nat.step_row(np.zeros(5, np.float32), m, sink, 0)
+    with pytest.raises(ValueError):  # a sink allocated for the other action kind
+        b._nat.step_row(x, m, EpisodeRecorder(4).sink(6, not discrete, 3), 0)
+
+
+def test_agent_fast_path_records_what_it_returns(tmp_path):
+    from relayrl_prototype_amd.api.agent import RelayRLAgent
+
+    p = _policy(True)
+    ag = RelayRLAgent.__new__(RelayRLAgent)  # the step path only: no transport
+    import threading
+
+    from relayrl_prototype_amd.types import EpisodeRecorder
+
+    ag.enabled, ag.policy, ag._policy_lock, ag._rec, ag._aux = True, p, threading.Lock(), EpisodeRecorder(16), []
+    rng = np.random.default_rng(6)
+    xs = rng.standard_normal((5, 6))  # float64 in, float32 recorded
+    for k, x in enumerate(xs):
+        act = ag.request_for_action(x, None, float(k))
+        assert act.get_obs().dtype == np.float32 and np.array_equal(act.get_obs(), x.astype(np.float32))
+        assert set(act.get_data()) == {"logp_a", "v"}
+    r = ag._rec
+    assert r.n == 5
+    np.testing.assert_array_equal(r.obs[:5], xs.astype(np.float32))
+    np.testing.assert_array_equal(r.rew[:4], [1, 2, 3, 4])  # each reward lands on the previous action
