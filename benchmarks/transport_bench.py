@@ -90,7 +90,8 @@ def bench(server_type, reps=200, wire="columns"):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--types", nargs="*", default=["local", "zmq", "grpc"])
-    ap.add_argument("--wire", nargs="*", default=["columns", "actions"])
+    ap.add_argument("--wire", nargs="*", default=["columns", "actions"],
+                    help="columns | actions | reference (the reference agent's own wire)")
     a = ap.parse_args()
     for t in a.types:
         for w in a.wire:

@@ -17,6 +17,7 @@
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -281,6 +282,185 @@ py::dict reference_columns(const py::bytes& frame) {
   return out;
 }
 
+// ------------------------------------------------------------------ columns -> reference frame
+// The frame a reference agent sends for one episode (agent_zmq.rs:458-610 -> trajectory.rs:50-90),
+// written straight from the agent's float32 columns: byte-identical to
+// serde_pickle.reference_frame over api.agent's per-action RelayRLAction list, without building
+// ~8 Python objects and 4 safetensors byte lists per action.  Row i is
+//   {"obs": TD, "act": TD, "mask": TD | None, "rew": rew[i], "data": {"logp_a": {"Tensor": TD},
+//    ["v": {"Tensor": TD}]}, "done": False, "reward_updated": reward_updated}
+// (TD = {"shape": [w], "dtype": "Float", "data": [u8 of a one-tensor safetensors file]}, "v" only
+// where val[i] is not NaN), then the terminal marker {obs, act, mask: None, "rew": last,
+// "data": None, "done": True, "reward_updated": False}.
+struct RefFrameWriter {
+  std::string& o;
+  void u32(uint32_t v) { o.append(reinterpret_cast<const char*>(&v), 4); }
+  void key(const char* s) {
+    const uint32_t k = (uint32_t)std::strlen(s);
+    o.push_back('X');
+    u32(k);
+    o.append(s, k);
+  }
+  void small(long long v) {  // the ints here: shape entries, u8 values
+    if (v >= 0 && v < 256) {
+      o.push_back('K');
+      o.push_back((char)v);
+    } else if (v >= 0 && v < 65536) {
+      o.push_back('M');
+      const uint16_t u = (uint16_t)v;
+      o.append(reinterpret_cast<const char*>(&u), 2);
+    } else {
+      o.push_back('J');
+      const int32_t s = (int32_t)v;
+      o.append(reinterpret_cast<const char*>(&s), 4);
+    }
+  }
+  void real(double d) {
+    uint64_t u;
+    std::memcpy(&u, &d, 8);
+    o.push_back('G');
+    for (int i = 7; i >= 0; --i) o.push_back((char)((u >> (8 * i)) & 0xFF));
+  }
+  // the safetensors file of a [width] float32 tensor is a fixed prefix (length + JSON header,
+  // which only depend on the width) and the raw bytes: the prefix is built once per width
+  std::vector<std::pair<long, std::string>> prefixes;
+  const std::string& prefix(long width) {
+    for (const auto& pw : prefixes)
+      if (pw.first == width) return pw.second;
+    rrl::Tensor t;
+    t.dtype = rrl::DType::Float;
+    t.shape = {width};
+    t.raw.assign(sizeof(float) * (size_t)width, '\0');
+    std::string f = rrl::st_encode(t);
+    f.resize(f.size() - t.raw.size());
+    prefixes.emplace_back(width, std::move(f));
+    return prefixes.back().second;
+  }
+  // serde's Vec<u8> of the bytes a[0..na) then b[0..nb): a list of K ints in APPENDS chunks of 1000
+  void u8list(const char* a, size_t na, const char* b, size_t nb) {
+    const size_t k = na + nb;
+    o.push_back(']');
+    for (size_t i = 0; i < k; i += 1000) {
+      const size_t e = std::min(k, i + 1000);
+      const size_t base = o.size();
+      o.resize(base + 2 + 2 * (e - i));
+      char* d = &o[base];
+      *d++ = '(';
+      for (size_t j = i; j < e; ++j) {
+        *d++ = 'K';
+        *d++ = j < na ? a[j] : b[j - na];
+      }
+      *d = 'e';
+    }
+  }
+  void td(const float* p, long width) {
+    const std::string& pre = prefix(width);
+    o.push_back('}');
+    o.push_back('(');
+    key("shape");
+    o.push_back(']');
+    o.push_back('(');
+    small(width);
+    o.push_back('e');
+    key("dtype");
+    key("Float");
+    key("data");
+    u8list(pre.data(), pre.size(), reinterpret_cast<const char*>(p), sizeof(float) * (size_t)width);
+    o.push_back('u');
+  }
+  void tensor_entry(const char* name, const float* p) {  // "name": {"Tensor": TD of [1]}
+    key(name);
+    o.push_back('}');
+    o.push_back('(');
+    key("Tensor");
+    td(p, 1);
+    o.push_back('u');
+  }
+};
+
+template <class A>
+const float* f32_rows(const A& a, size_t n, long& width, const char* what) {
+  if (a.ndim() != 2 || (size_t)a.shape(0) != n) throw std::invalid_argument(std::string(what) + " must be [n][w]");
+  width = (long)a.shape(1);
+  return a.data();
+}
+
+py::bytes reference_frame_columns(py::array_t<float, py::array::c_style | py::array::forcecast> obs,
+                                  py::array_t<float, py::array::c_style | py::array::forcecast> act, py::object mask,
+                                  py::array_t<float, py::array::c_style | py::array::forcecast> rew,
+                                  py::array_t<float, py::array::c_style | py::array::forcecast> logp,
+                                  py::array_t<float, py::array::c_style | py::array::forcecast> val, double last,
+                                  bool reward_updated) {
+  using farr = py::array_t<float, py::array::c_style | py::array::forcecast>;
+  const size_t n = (size_t)rew.size();
+  if ((size_t)logp.size() != n || (size_t)val.size() != n) throw std::invalid_argument("rew / logp / val lengths differ");
+  long wo = 0, wa = 0, wm = 0;
+  const float* po = f32_rows(obs, n, wo, "obs");
+  const float* pa = f32_rows(act, n, wa, "act");
+  farr m;
+  const float* pm = nullptr;
+  if (!mask.is_none()) {
+    m = mask.cast<farr>();
+    pm = f32_rows(m, n, wm, "mask");
+  }
+  const float *pr = rew.data(), *pl = logp.data(), *pv = val.data();
+  std::string out = "\x80\x03";
+  {
+    py::gil_scoped_release nogil;  // the arrays are held by this frame's arguments
+    out.reserve(64 + (n + 1) * (size_t)(700 + 240 * (wo + wa + wm)));
+    RefFrameWriter w{out, {}};
+    const size_t total = n + 1;
+    out.push_back(']');
+    for (size_t c = 0; c < total; c += 1000) {
+      out.push_back('(');
+      for (size_t i = c; i < total && i < c + 1000; ++i) {
+        out.push_back('}');
+        out.push_back('(');
+        if (i < n) {
+          w.key("obs");
+          w.td(po + i * wo, wo);
+          w.key("act");
+          w.td(pa + i * wa, wa);
+          w.key("mask");
+          if (pm) w.td(pm + i * wm, wm);
+          else out.push_back('N');
+          w.key("rew");
+          w.real((double)pr[i]);
+          w.key("data");
+          out.push_back('}');
+          out.push_back('(');
+          w.tensor_entry("logp_a", pl + i);
+          if (!std::isnan(pv[i])) w.tensor_entry("v", pv + i);
+          out.push_back('u');
+          w.key("done");
+          out.push_back('\x89');
+          w.key("reward_updated");
+          out.push_back(reward_updated ? '\x88' : '\x89');
+        } else {
+          w.key("obs");
+          out.push_back('N');
+          w.key("act");
+          out.push_back('N');
+          w.key("mask");
+          out.push_back('N');
+          w.key("rew");
+          w.real(last);
+          w.key("data");
+          out.push_back('N');
+          w.key("done");
+          out.push_back('\x88');
+          w.key("reward_updated");
+          out.push_back('\x89');
+        }
+        out.push_back('u');
+      }
+      out.push_back('e');
+    }
+    out.push_back('.');
+  }
+  return py::bytes(out);
+}
+
 }  // namespace
 
 void bind_pickle(py::module_& m) {
@@ -318,4 +498,7 @@ void bind_pickle(py::module_& m) {
       },
       py::arg("frame"),
       "serde_pickle(Vec<RelayRLAction>) -> float32 columns (obs/act/mask, rew, done, logp, v + presence flags)");
+  m.def("reference_frame_columns", &reference_frame_columns, py::arg("obs"), py::arg("act"), py::arg("mask"),
+        py::arg("rew"), py::arg("logp"), py::arg("val"), py::arg("last"), py::arg("reward_updated"),
+        "one episode's float32 columns -> the reference agent's serde_pickle(Vec<RelayRLAction>) frame");
 }

@@ -210,13 +210,17 @@ class RelayRLAgent:
             acts.append(RelayRLAction(np.asarray(cols.obs[i], np.float32), np.asarray(cols.act[i], np.float32),
                                       None if cols.mask is None else np.asarray(cols.mask[i], np.float32),
                                       float(cols.rew[i]), data, False, not grpc))
-        last = 0.0
-        if not done and next_obs is not None and self.policy is not None:
-            with self._policy_lock:
-                v = self.policy.value(np.asarray(next_obs, np.float32).reshape(1, -1))
-            last = 0.0 if v is None else float(np.asarray(v).reshape(-1)[0])
-        acts.append(RelayRLAction(None, None, None, last, None, True, False))  # agent_zmq.rs:605-610 marker
+        acts.append(RelayRLAction(None, None, None, self._reference_last(done, next_obs), None, True,
+                                  False))  # agent_zmq.rs:605-610 marker
         return acts
+
+    def _reference_last(self, done: bool, next_obs=None) -> float:
+        """The terminal marker's reward: 0 for a finished episode, V(s_T) for a cut one."""
+        if done or next_obs is None or self.policy is None:
+            return 0.0
+        with self._policy_lock:
+            v = self.policy.value(np.asarray(next_obs, np.float32).reshape(1, -1))
+        return 0.0 if v is None else float(np.asarray(v).reshape(-1)[0])
 
     def _ship(self, done: bool, next_obs=None):
         if self._ts_policy:
@@ -226,13 +230,16 @@ class RelayRLAgent:
         if self.wire_format == "reference":
             vals = self._rec.val[:self._rec.n].copy()
             cols = self._rec.take(self.agent_id, self.episodes_sent, done, next_obs)
-            acts = self._reference_actions(cols, vals, done, next_obs)
             if self.server_type == "grpc":
-                self.transport.send_actions(acts)  # SendActions, then the synchronous ClientPoll
+                self.transport.send_actions(self._reference_actions(cols, vals, done, next_obs))  # then ClientPoll
             else:
-                from ..transport.serde_pickle import reference_frame
+                # the same bytes as reference_frame(self._reference_actions(...)), written from the
+                # columns in C++ (tests/test_reference_agent.py)
+                from .. import _native
 
-                self.transport.send_trajectory(reference_frame(acts))
+                act = np.asarray(cols.act, np.float32)  # [n][w] from the recorder
+                self.transport.send_trajectory(_native.reference_frame_columns(
+                    cols.obs, act, cols.mask, cols.rew, cols.logp, vals, self._reference_last(done, next_obs), True))
             self.episodes_sent += 1
             return
         cols = self._rec.take(self.agent_id, self.episodes_sent, done, next_obs)

@@ -251,3 +251,37 @@ def test_reference_columns_relay_through_the_engine_link():
     for a, b in zip(got[:-1], acts[:-1]):
         np.testing.assert_array_equal(np.asarray(a.get_obs()).reshape(-1), b.get_obs().reshape(-1))
         assert a.get_rew() == b.get_rew()
+
+
+@pytest.mark.parametrize("n,discrete,masked,done", [(7, True, True, True), (1201, True, True, False),
+                                                     (5, False, False, False), (0, True, True, True)])
+def test_native_reference_frame_is_byte_identical(n, discrete, masked, done):
+    """_native.reference_frame_columns (the reference-wire agent's upload, written from the
+    columns in C++) against serde_pickle.reference_frame over the per-action RelayRLAction list
+    the agent used to build: the same bytes, and they decode to the same columns."""
+    from relayrl_prototype_amd.types import TrajectoryColumns
+
+    rng = np.random.default_rng(n)
+    D, A = 4, 2 if discrete else 3
+    obs = rng.standard_normal((n, D)).astype(np.float32)
+    act = (rng.integers(0, A, (n, 1)).astype(np.int32) if discrete else rng.standard_normal((n, A)).astype(np.float32))
+    mask = rng.integers(0, 2, (n, A)).astype(np.float32) if masked else None
+    rew = rng.standard_normal(n).astype(np.float32)
+    logp = rng.standard_normal(n).astype(np.float32)
+    vals = rng.standard_normal(n).astype(np.float32)
+    vals[::3] = np.nan  # rows without a value head output carry no "v"
+    cols = TrajectoryColumns(obs, act, rew, np.zeros(n, np.uint8), mask, logp, "a", 0)
+    ag = RelayRLAgent.__new__(RelayRLAgent)
+    ag.server_type, ag.policy = "zmq", None
+    last = 0.0 if done else 1.25
+    acts = ag._reference_actions(cols, vals, done)
+    acts[-1]._rew = last  # the cut episode's bootstrap (V(s_T) from the policy in the agent)
+    want = sp.reference_frame(acts)
+    got = _native.reference_frame_columns(obs, act.astype(np.float32), mask, rew, logp, vals,
+                                          last, True)
+    assert got == want
+    rc = _native.reference_columns(got)
+    assert rc["n"] == n + 1 and rc["done"][-1] == 1
+    if n:
+        np.testing.assert_array_equal(rc["obs"][:n], obs)
+        np.testing.assert_array_equal(rc["has_v"][:n], ~np.isnan(vals))
