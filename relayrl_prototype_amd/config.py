@@ -21,7 +21,7 @@ from __future__ import annotations
 import copy
 import json
 import os
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, Optional
 
 DEFAULT_CONFIG_FILENAME = "relayrl_config.json"
 

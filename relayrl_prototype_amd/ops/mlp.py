@@ -7,7 +7,6 @@ kernels stage the whole net into LDS with one sweep.
 """
 from __future__ import annotations
 
-import math
 from dataclasses import dataclass
 from enum import IntEnum
 from typing import Optional

@@ -28,7 +28,7 @@ from __future__ import annotations
 import hashlib
 import struct
 from collections import OrderedDict
-from typing import Any, List, Optional, Tuple
+from typing import Any, List, Tuple
 
 import numpy as np
 

@@ -18,7 +18,7 @@ import ctypes
 import os
 import time
 from collections import defaultdict
-from typing import Dict, List, Optional
+from typing import Dict, List
 
 _ROCTX = None
 _ROCTX_TRIED = False
