@@ -160,7 +160,11 @@ inline void reference_columns_tree(const uint8_t* frame, size_t len, RefColumns&
   if (root->k == Node::Dict) {
     if (const Node* a = get(root, "actions")) root = a;
   }
-  static const Node kEmptyList{Node::List};
+  static const Node kEmptyList = [] {
+    Node e;
+    e.k = Node::List;
+    return e;
+  }();
   if (root->k == Node::ByteArr && root->s.empty()) root = &kEmptyList;
   if (root->k != Node::List && root->k != Node::Tuple) throw FrameError("expected a list of actions");
   const size_t n = root->items.size();

@@ -522,9 +522,7 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
           rx[3] = *reinterpret_cast<const uint4*>(A.frames + (size_t)fr.w * kPongFrameBytes + off);
         }
       }
-      return;
-    }
-    if constexpr (L::kRing16) {
+    } else if constexpr (L::kRing16) {
       if (tid < 2 * kPongFramePos) {  // position tid >> 1, frames 2 fp and 2 fp + 1, all 4 rows
         const int fp = tid & 1;
         const size_t off = (size_t)(tid >> 1) * 16;
@@ -532,16 +530,16 @@ __device__ __forceinline__ void stack16_role(const Stack16Args& A, uint16_t* sme
         rx[0] = *reinterpret_cast<const uint4*>(A.frames + (size_t)ra * kPongFrameBytes + off);
         rx[1] = *reinterpret_cast<const uint4*>(A.frames + (size_t)rb * kPongFrameBytes + off);
       }
-      return;
-    }
-    if (ring_pos(tid) < kPongFramePos) {
-      const size_t off = (size_t)ring_pos(tid) * 16 + 8 * ring_half(tid);
-      const uint2 f0 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.x * kPongFrameBytes + off);
-      const uint2 f1 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.y * kPongFrameBytes + off);
-      const uint2 f2 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.z * kPongFrameBytes + off);
-      const uint2 f3 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.w * kPongFrameBytes + off);
-      rx[0] = make_uint4(f0.x, f0.y, f1.x, f1.y);
-      rx[1] = make_uint4(f2.x, f2.y, f3.x, f3.y);
+    } else if constexpr (L::kRing) {
+      if (ring_pos(tid) < kPongFramePos) {
+        const size_t off = (size_t)ring_pos(tid) * 16 + 8 * ring_half(tid);
+        const uint2 f0 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.x * kPongFrameBytes + off);
+        const uint2 f1 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.y * kPongFrameBytes + off);
+        const uint2 f2 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.z * kPongFrameBytes + off);
+        const uint2 f3 = *reinterpret_cast<const uint2*>(A.frames + (size_t)fr.w * kPongFrameBytes + off);
+        rx[0] = make_uint4(f0.x, f0.y, f1.x, f1.y);
+        rx[1] = make_uint4(f2.x, f2.y, f3.x, f3.y);
+      }
     }
   };
   auto gload = [&](size_t n) {
@@ -1672,7 +1670,7 @@ __device__ __forceinline__ void conv2_bwd16_role(const uint16_t* __restrict__ dy
   using namespace c2b;
   constexpr int T = c2b16::kStage;
   const int lane = tid & 63;
-  const int i16 = lane & 15, g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int i16 = lane & 15, g = lane >> 4;
   const int cls = wave >> 1, ph = cls >> 1, pw = cls & 1, ct = wave & 1;  // dgrad role (waves 0-7)
   const int cb = wave & 1, tau0 = 4 * ((wave - 8) >> 1);                 // wgrad role (waves 8-15)
   bf16x8_t wf[ROLE == 0 ? 8 : 1];

@@ -175,7 +175,8 @@ static int launch_fwd(const FwdArgs& a, int grid, hipStream_t s) {
   const size_t lds = (size_t)L::floats(A) * sizeof(float);
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute((const void*)mlp_forward_kernel<DT, HT, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    (void)hipFuncSetAttribute((const void*)mlp_forward_kernel<DT, HT, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              163840);
     attr_set = true;
   }
   hipLaunchKernelGGL((mlp_forward_kernel<DT, HT, MODE>), dim3(grid), dim3(256), lds, s, a);
