@@ -7,6 +7,9 @@
 //                                       requests and a publisher thread sets new models; every
 //                                       upload must arrive once, every call must end with
 //                                       grpc-status 0;
+//   h2_selftest rate THREADS SECS BYTES the ingest ceiling (an -O2 build, tools/h2_rate.sh): THREADS
+//                                       clients send BYTES-byte SendFrame uploads back to back for
+//                                       SECS; one JSON line with uploads/s and call latency;
 //   h2_selftest fuzz N SEED             N mutated client byte streams (byte flips, truncations,
 //                                       splices, random insertions, huge DATA / HEADERS lengths,
 //                                       a flood of streams past the per-connection byte cap) sent
@@ -25,6 +28,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -313,6 +317,63 @@ int traffic(int threads, int calls) {
   return fails ? 1 : 0;
 }
 
+// ------------------------------------------------------------------ rate (optimised build)
+// The server's ingest ceiling without Python agents: THREADS native clients (one HTTP/2
+// connection each) send SendFrame uploads of BYTES back to back for SECONDS while one consumer
+// thread drains the inbox, as the learner's ingest thread does.  Prints uploads/s, MB/s and the
+// per-call latency percentiles (the unary round trip, ack included).
+int rate(int threads, double seconds, int bytes) {
+  Server srv("127.0.0.1", 0, /*max_inbox=*/1024, /*max_bytes=*/size_t(1) << 28, /*idle_timeout_ms=*/20);
+  std::atomic<bool> stop{false}, done_sending{false};
+  std::atomic<long> got{0};
+  std::thread consumer([&] {
+    Item it;
+    while (!done_sending || srv.recv(it, 0)) {
+      if (srv.recv(it, 20) && it.kind == rrl::h2::kFrame) got++;
+    }
+  });
+  std::vector<std::vector<double>> lat(threads);
+  std::atomic<long> sent{0}, bad{0};
+  const std::string frame((size_t)bytes, 'f');
+  const std::string req = pb_bytes(1, frame);
+  std::vector<std::thread> cl;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int t = 0; t < threads; ++t) {
+    cl.emplace_back([&, t] {
+      Client c(srv.port());
+      while (!stop) {
+        std::string out;
+        const auto a = std::chrono::steady_clock::now();
+        const std::string st = c.call("SendFrame", req, &out);
+        lat[t].push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count());
+        if (st != "0" || resp_code(out) != 1) bad++;
+        sent++;
+      }
+    });
+  }
+  std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+  stop = true;
+  for (auto& th : cl) th.join();
+  const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const auto t1 = std::chrono::steady_clock::now();
+  while (got < sent && std::chrono::steady_clock::now() - t1 < std::chrono::seconds(10))
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+  done_sending = true;
+  consumer.join();
+  srv.close();
+  std::vector<double> all;
+  for (auto& v : lat) all.insert(all.end(), v.begin(), v.end());
+  std::sort(all.begin(), all.end());
+  auto pct = [&](double q) { return all.empty() ? 0.0 : all[std::min(all.size() - 1, (size_t)(q * all.size()))]; };
+  CHECK(bad == 0);
+  CHECK(got == sent);
+  std::printf("{\"bench\": \"h2grpc_rate\", \"clients\": %d, \"frame_bytes\": %d, \"seconds\": %.2f, \"uploads\": %ld, "
+              "\"uploads_per_s\": %.0f, \"MB_per_s\": %.1f, \"call_us_p50\": %.1f, \"call_us_p99\": %.1f, \"ok\": %s}\n",
+              threads, bytes, el, (long)sent, sent / el, sent * (double)bytes / el / 1e6, pct(0.5), pct(0.99),
+              fails ? "false" : "true");
+  return fails ? 1 : 0;
+}
+
 // ------------------------------------------------------------------ fuzz (ASan + UBSan)
 // the bytes of a valid client conversation: preface, SETTINGS, then requests of every method
 std::string conversation(std::mt19937& rng) {
@@ -484,7 +545,9 @@ int fuzz(long n, unsigned seed) {
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "traffic";
   if (mode == "traffic") return traffic(argc > 2 ? std::atoi(argv[2]) : 8, argc > 3 ? std::atoi(argv[3]) : 200);
+  if (mode == "rate")
+    return rate(argc > 2 ? std::atoi(argv[2]) : 8, argc > 3 ? std::atof(argv[3]) : 3.0, argc > 4 ? std::atoi(argv[4]) : 4096);
   if (mode == "fuzz") return fuzz(argc > 2 ? std::atol(argv[2]) : 2000, argc > 3 ? (unsigned)std::atoi(argv[3]) : 1);
-  std::fprintf(stderr, "usage: h2_selftest traffic [THREADS CALLS] | fuzz [N SEED]\n");
+  std::fprintf(stderr, "usage: h2_selftest traffic [THREADS CALLS] | fuzz [N SEED] | rate [THREADS SECONDS BYTES]\n");
   return 2;
 }
