@@ -10,9 +10,11 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -216,7 +218,64 @@ static void test_policy() {
   for (int i = 0; i < 33; ++i) CHECK(act[i] >= 0 && act[i] < A);
 }
 
-int main() {
+// The ZMTP PULL endpoint's ingest ceiling (an -O2 build, tools/zmtp_rate.sh): CLIENTS PUSH sockets
+// send BYTES-byte messages back to back for SECONDS -- over one connection each, or (reconnect)
+// with a new connection and handshake per message, as reference agents upload -- while one thread
+// drains the PULL.  One JSON line.
+static int zmtp_rate(int clients, double seconds, int bytes, bool reconnect) {
+  zmtp::Socket pull(zmtp::SockType::PULL);
+  const int port = pull.bind("tcp://127.0.0.1:0");
+  const std::string ep = "tcp://127.0.0.1:" + std::to_string(port);
+  pull.set_inbox_limits(4096, size_t(1) << 28);
+  std::atomic<bool> stop{false};
+  std::atomic<long> sent{0};
+  std::atomic<int> finished{0};
+  const std::string body((size_t)bytes, 'z');
+  std::vector<std::thread> cl;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int c = 0; c < clients; ++c)
+    cl.emplace_back([&] {
+      std::unique_ptr<zmtp::Socket> push;
+      while (!stop) {
+        if (!push) {
+          push.reset(new zmtp::Socket(zmtp::SockType::PUSH));
+          push->connect(ep);
+        }
+        CHECK(push->send({body}, 10000));
+        sent++;
+        if (reconnect) {
+          push->close();
+          push.reset();
+        }
+      }
+      if (push) push->close();
+      finished++;
+    });
+  long got = 0;
+  zmtp::Message m;
+  double el = 0;
+  // keep draining until every sender has stopped (a sender blocked on a full inbox must finish)
+  while (finished.load() < clients) {
+    if (pull.recv(m, 20)) ++got;
+    if (!stop && std::chrono::steady_clock::now() - t0 > std::chrono::duration<double>(seconds)) {
+      stop = true;
+      el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+  }
+  for (auto& t : cl) t.join();
+  while (got < sent && pull.recv(m, 2000)) ++got;
+  pull.close();
+  CHECK(got == sent);
+  std::printf("{\"bench\": \"zmtp_rate\", \"clients\": %d, \"connection_per_message\": %s, \"bytes\": %d, "
+              "\"seconds\": %.2f, \"messages\": %ld, \"messages_per_s\": %.0f, \"MB_per_s\": %.1f}\n",
+              clients, reconnect ? "true" : "false", bytes, el, got, got / el, got * (double)bytes / el / 1e6);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "zmtp-rate")
+    return zmtp_rate(argc > 2 ? std::atoi(argv[2]) : 8, argc > 3 ? std::atof(argv[3]) : 3.0,
+                     argc > 4 ? std::atoi(argv[4]) : 4096, argc > 5 && std::string(argv[5]) == "reconnect");
   test_codec();
   test_policy();
   test_vecenv();
