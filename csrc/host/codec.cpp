@@ -219,8 +219,8 @@ struct R {
   const std::string& b;
   size_t i = 0;
   explicit R(const std::string& s) : b(s) {}
-  void need(size_t n) {
-    if (i + n > b.size()) throw std::runtime_error("RRLT: truncated frame");
+  void need(uint64_t n) {  // n may be any 64-bit length field: compared against what is left
+    if (n > b.size() - i) throw std::runtime_error("RRLT: truncated frame");
   }
   uint8_t u8() {
     need(1);
@@ -252,8 +252,22 @@ struct R {
     need(n);
     t.raw = b.substr(i, n);
     i += n;
-    if ((int64_t)t.raw.size() != t.numel() * (int64_t)dtype_size(t.dtype))
-      throw std::runtime_error("RRLT: tensor size mismatch");
+    // the element count from the (untrusted) shape without overflow: every dim >= 0 and the
+    // product bounded by the bytes actually present
+    const uint64_t es = dtype_size(t.dtype), cap = t.raw.size() / es;
+    uint64_t cnt = 1;
+    bool zero = false;
+    for (int64_t d : t.shape) {
+      if (d < 0) throw std::runtime_error("RRLT: negative dimension");
+      if (d == 0) {
+        zero = true;
+      } else if (!zero) {
+        if ((uint64_t)d > cap / cnt) throw std::runtime_error("RRLT: tensor size mismatch");
+        cnt *= (uint64_t)d;
+      }
+    }
+    if (zero) cnt = 0;
+    if (cnt * es != t.raw.size()) throw std::runtime_error("RRLT: tensor size mismatch");
     return t;
   }
 };
@@ -307,7 +321,10 @@ Trajectory traj_decode(const std::string& buf) {
   t.agent_id = r.str();
   t.seq = r.pod<uint64_t>();
   uint32_t n = r.pod<uint32_t>();
-  if (n > (1u << 28)) throw std::runtime_error("RRLT: absurd action count");
+  // every action takes at least 5 bytes (flags + reward): a count the frame cannot hold is refused
+  // before anything is allocated for it (a 24-byte frame claiming 2^28 actions used to reserve
+  // ~100 GB of Action records)
+  if (n > (buf.size() - r.i) / 5) throw std::runtime_error("RRLT: action count exceeds the frame");
   t.actions.resize(n);
   for (uint32_t k = 0; k < n; ++k) {
     Action& a = t.actions[k];

@@ -5,7 +5,9 @@
 //     reaches first (the server's decoder instantiates the same template over Python objects);
 //   * rrl::st_tensor_f32 (csrc/host/st_tensor.h) -- every TensorData payload inside those frames;
 //   * rrl::reference_columns_tree (csrc/host/ref_columns.h) -- the server's frame -> columns decoder;
-//   * rrl::st_decode / st_header (csrc/host/codec.cpp) -- the gRPC path's safetensors tensors.
+//   * rrl::st_decode / st_header (csrc/host/codec.cpp) -- the gRPC path's safetensors tensors;
+//   * rrl::traj_decode (csrc/host/codec.cpp) -- this framework's own RRLT frames, which any peer
+//     of the trajectory PULL / the gRPC SendFrame route can send (seeds encoded here).
 //
 // usage: parser_fuzz ITERATIONS SEED_FILE...   (seeds: real reference frames and safetensors
 // files written by the test from transport/serde_pickle.reference_frame).  Each iteration takes
@@ -37,8 +39,57 @@ using rrl::pickle::Node;
 using rrl::pickle::NodeBuilder;
 
 struct Stats {
-  uint64_t runs = 0, accepted = 0, rejected = 0, tensors = 0, tensors_ok = 0, st_ok = 0, st_bad = 0, columns_ok = 0;
+  uint64_t runs = 0, accepted = 0, rejected = 0, tensors = 0, tensors_ok = 0, st_ok = 0, st_bad = 0, columns_ok = 0,
+           rrlt_ok = 0, rrlt_bad = 0;
 };
+
+// valid RRLT frames: episodes with obs / act / mask tensors of several dtypes, tensor and scalar
+// aux values, a terminal marker without tensors
+std::vector<std::string> rrlt_seeds() {
+  std::vector<std::string> out;
+  for (int variant = 0; variant < 3; ++variant) {
+    rrl::Trajectory t;
+    t.server = variant ? "tcp://127.0.0.1:7776" : "";
+    t.agent_id = "fuzz-" + std::to_string(variant);
+    t.seq = 7 + variant;
+    for (int i = 0; i < 3 + 4 * variant; ++i) {
+      rrl::Action a;
+      a.has_obs = a.has_act = true;
+      a.obs.dtype = variant == 2 ? rrl::DType::Double : rrl::DType::Float;
+      a.obs.shape = {4};
+      a.obs.raw.assign(4 * rrl::dtype_size(a.obs.dtype), (char)(i + 1));
+      a.act.dtype = variant == 1 ? rrl::DType::Long : rrl::DType::Int;
+      a.act.shape = {1};
+      a.act.raw.assign(rrl::dtype_size(a.act.dtype), (char)(i & 1));
+      a.has_mask = variant != 1;
+      if (a.has_mask) {
+        a.mask.dtype = rrl::DType::Float;
+        a.mask.shape = {2};
+        a.mask.raw.assign(8, '\0');
+      }
+      a.rew = 0.5f * i;
+      a.has_data = true;
+      rrl::AuxValue lp;
+      lp.kind = rrl::AuxValue::TENSOR;
+      lp.tensor.dtype = rrl::DType::Float;
+      lp.tensor.shape = {1};
+      lp.tensor.raw.assign(4, '\x3f');
+      a.data["logp_a"] = lp;
+      rrl::AuxValue sv;
+      sv.kind = variant == 0 ? rrl::AuxValue::STRING : rrl::AuxValue::DOUBLE;
+      sv.s = "note";
+      sv.d = 1.5;
+      a.data["extra"] = sv;
+      t.actions.push_back(a);
+    }
+    rrl::Action m;  // the terminal marker
+    m.done = true;
+    m.rew = 1.f;
+    t.actions.push_back(m);
+    out.push_back(rrl::traj_encode(t));
+  }
+  return out;
+}
 
 // every TensorData-like {.., "data": bytes} below the root goes through the column reader
 void walk(Node* n, rrl::StHeaderCache& hc, std::unordered_set<Node*>& seen, Stats& st, int depth) {
@@ -240,6 +291,20 @@ void run_all(const std::string& in, Stats& st) {
     rrl::st_tensor_f32(in.data(), in.size(), out, hc);
   } catch (const std::exception&) {
   }
+  // and as this framework's RRLT frame (traj_decode), touching every decoded byte
+  try {
+    const rrl::Trajectory t = rrl::traj_decode(in);
+    size_t sink = t.agent_id.size() + t.server.size();
+    for (const auto& a : t.actions) {
+      sink += a.obs.raw.size() + a.act.raw.size() + a.mask.raw.size();
+      for (const auto& kv : a.data) sink += kv.first.size() + kv.second.tensor.raw.size() + kv.second.s.size();
+    }
+    volatile size_t v = sink;
+    (void)v;
+    ++st.rrlt_ok;
+  } catch (const std::exception&) {
+    ++st.rrlt_bad;
+  }
 }
 
 }  // namespace
@@ -261,6 +326,9 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "no seeds\n");
     return 2;
   }
+  const std::vector<std::string> rrlt = rrlt_seeds();
+  seeds.insert(seeds.end(), rrlt.begin(), rrlt.end());
+  for (const auto& f : rrlt) rrl::traj_decode(f);  // the encoder's own frames must decode
   std::vector<std::string> st_seeds;  // safetensors files among the seeds (header length + '{')
   for (const auto& s : seeds)
     if (s.size() > 9 && s[8] == '{') st_seeds.push_back(s);
@@ -284,9 +352,11 @@ int main(int argc, char** argv) {
     run_all(cur, st);
   }
   std::printf("parser fuzz OK: %ld inputs, %llu VM runs (%llu accepted, %llu rejected), %llu tensors read "
-              "(%llu valid), st_decode %llu ok / %llu rejected, column frames %llu, seeds decoded %llu\n",
+              "(%llu valid), st_decode %llu ok / %llu rejected, column frames %llu, RRLT %llu ok / %llu rejected, "
+              "seeds decoded %llu\n",
               iters, (unsigned long long)st.runs, (unsigned long long)st.accepted, (unsigned long long)st.rejected,
               (unsigned long long)st.tensors, (unsigned long long)st.tensors_ok, (unsigned long long)st.st_ok,
-              (unsigned long long)st.st_bad, (unsigned long long)st.columns_ok, (unsigned long long)seed_ok);
+              (unsigned long long)st.st_bad, (unsigned long long)st.columns_ok, (unsigned long long)st.rrlt_ok,
+              (unsigned long long)st.rrlt_bad, (unsigned long long)seed_ok);
   return 0;
 }

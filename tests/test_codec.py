@@ -89,3 +89,40 @@ def test_rrlt_rejects_truncation():
     for cut in (3, len(b) // 2, len(b) - 1):
         with pytest.raises(Exception):
             _native.traj_decode(b[:cut])
+
+
+def _rrlt_header(n_actions):
+    import struct
+
+    return struct.pack("<II", 0x544C5252, 1) + struct.pack("<I", 0) + struct.pack("<I", 1000) + \
+        struct.pack("<I", 1) + b"a" + struct.pack("<Q", 0) + struct.pack("<I", n_actions)
+
+
+def test_rrlt_hostile_counts_and_shapes_are_refused_cheaply():
+    """Network-facing RRLT decoder (codec.cpp traj_decode; the fuzz harness found these): a tiny
+    frame claiming 2^28 actions is refused before anything is allocated for them (it used to
+    reserve ~100 GB), and tensor shapes whose element count overflows, or is negative, or whose
+    byte length field wraps, are refused instead of overflowing."""
+    import struct
+    import time
+
+    t0 = time.perf_counter()
+    with pytest.raises(Exception, match="action count"):
+        _native.traj_decode(_rrlt_header(1 << 28) + b"\0" * 16)
+    assert time.perf_counter() - t0 < 0.5
+
+    def one_tensor_frame(shape, nbytes_field, payload):
+        act = struct.pack("<Bf", 1, 0.0)  # has_obs, reward
+        act += struct.pack("<BB", 4, len(shape)) + b"".join(struct.pack("<q", d) for d in shape)
+        act += struct.pack("<Q", nbytes_field) + payload
+        return _rrlt_header(1) + act
+
+    good = one_tensor_frame([2, 2], 16, b"\0" * 16)
+    t = _native.traj_decode(good)
+    assert t["agent_id"] == "a" and t["actions"][0]["obs"] == ("Float", [2, 2], b"\0" * 16)
+    for shape, nb, payload in (([1 << 62, 8], 16, b"\0" * 16),           # count overflows int64
+                               ([-4, -1], 16, b"\0" * 16),                # negative dims
+                               ([2, 2], (1 << 64) - 1, b"\0" * 16),       # length field wraps
+                               ([3], 16, b"\0" * 16)):                    # plain mismatch
+        with pytest.raises(Exception):
+            _native.traj_decode(one_tensor_frame(shape, nb, payload))

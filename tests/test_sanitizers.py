@@ -41,6 +41,17 @@ def _fuzz_seeds(d):
             p = os.path.join(d, f"frame{k}_{j}.pkl")
             open(p, "wb").write(frame)
             paths.append(p)
+    from relayrl_prototype_amd.types import RelayRLTrajectory
+
+    for k, n in enumerate((0, 5)):  # this framework's own RRLT frames (traj_decode)
+        t = RelayRLTrajectory(1000, None, agent_id=f"fuzz-{k}")
+        t.actions = [RelayRLAction(rng.normal(size=4).astype(np.float32), np.array([i % 2], np.int32),
+                                   np.ones(2, np.float32), float(i), {"logp_a": np.array([-0.5], np.float32),
+                                                                      "note": "x", "k": 3}, False, True)
+                     for i in range(n)] + [RelayRLAction(None, None, None, 0.5, None, True, False)]
+        p = os.path.join(d, f"rrlt{k}.bin")
+        open(p, "wb").write(t.encode())
+        paths.append(p)
     for name, arr in (("Float", np.arange(6, dtype=np.float32)), ("Double", np.arange(3.0)),
                       ("Long", np.arange(4, dtype=np.int64)), ("Byte", np.arange(5, dtype=np.uint8)),
                       ("Int", np.arange(2, dtype=np.int32).reshape(1, 2)), ("Short", np.arange(3, dtype=np.int16))):
@@ -67,6 +78,8 @@ def test_network_parsers_survive_200k_mutants_under_asan_ubsan(tmp_path):
     m = re.search(r"\((\d+) accepted, (\d+) rejected\), (\d+) tensors read \((\d+) valid\)", out)
     acc, rej, tens, ok = map(int, m.groups())
     assert acc > 50_000 and rej > 50_000 and tens > 50_000 and ok > 1_000, out[-500:]  # both sides exercised
+    rok, rbad = map(int, re.search(r"RRLT (\d+) ok / (\d+) rejected", out).groups())
+    assert rok > 100 and rbad > 10_000, out[-500:]  # RRLT mutants reach the decoder
 
 
 @pytest.mark.skipif(shutil.which("g++") is None or not os.path.exists("/opt/conda/include/nghttp2/nghttp2.h"),
