@@ -218,6 +218,127 @@ static void test_policy() {
   for (int i = 0; i < 33; ++i) CHECK(act[i] >= 0 && act[i] < A);
 }
 
+// ---------------------------------------------------------------- ZMTP mutation fuzz (ASan + UBSan)
+// A PUSH peer's conversation as raw bytes: the NULL greeting, READY (Socket-Type PUSH), then
+// messages -- short and long frames, a multipart message -- the last one carrying ``marker``.
+static std::string zmtp_frame(uint8_t flags, const std::string& body) {
+  std::string f;
+  if (body.size() < 256 && !(flags & 0x02)) {
+    f.push_back((char)flags);
+    f.push_back((char)body.size());
+  } else {
+    f.push_back((char)(flags | 0x02));
+    for (int i = 7; i >= 0; --i) f.push_back((char)(((uint64_t)body.size() >> (8 * i)) & 0xFF));
+  }
+  return f + body;
+}
+static std::string zmtp_conversation(const std::string& marker) {
+  std::string g(64, '\0');
+  g[0] = (char)0xFF;
+  g[9] = 0x7F;
+  g[10] = 3;
+  std::memcpy(&g[12], "NULL", 4);
+  std::string ready = "\x05READY";
+  const std::string k = "Socket-Type", v = "PUSH";
+  ready.push_back((char)k.size());
+  ready += k;
+  for (int i = 3; i >= 0; --i) ready.push_back((char)((v.size() >> (8 * i)) & 0xFF));
+  ready += v;
+  std::string c = g + zmtp_frame(0x04, ready);
+  c += zmtp_frame(0x00, "short message");
+  c += zmtp_frame(0x02, std::string(300, 'L'));         // a long-form frame
+  c += zmtp_frame(0x01, "part one") + zmtp_frame(0x00, "part two");  // multipart
+  c += zmtp_frame(0x00, marker);
+  return c;
+}
+static void send_raw(int port, const std::string& bytes, bool linger) {
+  const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+  CHECK(fd >= 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)port);
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  if (::connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) == 0) {
+    size_t off = 0;
+    while (off < bytes.size()) {  // the server may drop us mid-way: errors are expected
+      const ssize_t w = ::send(fd, bytes.data() + off, bytes.size() - off, MSG_NOSIGNAL);
+      if (w <= 0) break;
+      off += (size_t)w;
+    }
+    if (linger) std::this_thread::sleep_for(std::chrono::milliseconds(2));
+  }
+  ::close(fd);
+}
+static int zmtp_fuzz(long iters, uint64_t seed) {
+  zmtp::Socket pull(zmtp::SockType::PULL);
+  const int port = pull.bind("tcp://127.0.0.1:0");
+  pull.set_inbox_limits(256, size_t(1) << 22);
+  pull.set_max_message_size(size_t(1) << 20);
+  uint64_t s = seed * 0x9E3779B97F4A7C15ull + 1;
+  auto rnd = [&]() {
+    s ^= s << 13;
+    s ^= s >> 7;
+    s ^= s << 17;
+    return s;
+  };
+  auto below = [&](size_t n) { return n ? (size_t)(rnd() % n) : 0; };
+  static const uint64_t kHuge[] = {0xFFFFFFFFFFFFFFFFull, 1ull << 63, 1ull << 40, 0xFFFFFFFFull, 1ull << 21, 255};
+  long delivered = 0, checks = 0;
+  zmtp::Message m;
+  for (long it = 0; it < iters; ++it) {
+    std::string b = zmtp_conversation("m" + std::to_string(it));
+    for (int k = 0, e = 1 + (int)below(4); k < e; ++k) {
+      switch (below(7)) {
+        case 0: b.resize(below(b.size() + 1)); break;                                      // truncate
+        case 1: for (int j = 0; j < 1 + (int)below(6); ++j) b[below(b.size())] ^= (char)(1 + below(255)); break;
+        case 2: {  // a long-frame size field to a huge value
+          const size_t at = below(b.size());
+          b.insert(at, zmtp_frame(0x02, ""));
+          const uint64_t v = kHuge[below(sizeof(kHuge) / sizeof(kHuge[0]))];
+          for (int i = 0; i < 8; ++i) b[at + 1 + i] = (char)((v >> (8 * (7 - i))) & 0xFF);
+          break;
+        }
+        case 3: b.insert(below(b.size() + 1), std::string(1 + below(64), (char)below(256))); break;  // junk
+        case 4: {  // a run of MORE frames (multipart pile-up)
+          std::string run;
+          for (int j = 0, n = 1 + (int)below(2000); j < n; ++j) run += zmtp_frame(0x01, std::string(1 + below(600), 'x'));
+          b.insert(below(b.size() + 1), run);
+          break;
+        }
+        case 5: {  // a command frame in the message phase, or a second READY
+          b.insert(below(b.size() + 1), zmtp_frame(0x04, std::string("\x05READY\x0bSocket-Type\x00\x00\x00\x04PULL", 26)));
+          break;
+        }
+        default: {  // duplicate a span
+          if (b.empty()) break;
+          const size_t a0 = below(b.size()), len = 1 + below(std::min<size_t>(256, b.size() - a0));
+          b.insert(below(b.size() + 1), b.substr(a0, len));
+        }
+      }
+    }
+    if (b.size() > (size_t(1) << 21)) b.resize(size_t(1) << 21);
+    send_raw(port, b, below(4) == 0);
+    while (pull.recv(m, 0)) ++delivered;
+    if (it % 200 == 199) {  // the endpoint still serves a well-formed peer, in order
+      const std::string mk = "alive-" + std::to_string(it);
+      send_raw(port, zmtp_conversation(mk), true);
+      bool seen = false;
+      const auto t0 = std::chrono::steady_clock::now();
+      while (!seen && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(10)) {
+        if (!pull.recv(m, 50)) continue;
+        ++delivered;
+        seen = !m.frames.empty() && m.frames[0] == mk;
+      }
+      CHECK(seen);
+      ++checks;
+    }
+  }
+  pull.close();
+  std::printf("zmtp fuzz OK: %ld mutated conversations, %ld messages delivered, %ld liveness checks\n", iters, delivered,
+              checks);
+  return 0;
+}
+
 // The ZMTP PULL endpoint's ingest ceiling (an -O2 build, tools/zmtp_rate.sh): CLIENTS PUSH sockets
 // send BYTES-byte messages back to back for SECONDS -- over one connection each, or (reconnect)
 // with a new connection and handshake per message, as reference agents upload -- while one thread
@@ -273,6 +394,8 @@ static int zmtp_rate(int clients, double seconds, int bytes, bool reconnect) {
 }
 
 int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "zmtp-fuzz")
+    return zmtp_fuzz(argc > 2 ? std::atol(argv[2]) : 2000, argc > 3 ? (uint64_t)std::atoll(argv[3]) : 1);
   if (argc > 1 && std::string(argv[1]) == "zmtp-rate")
     return zmtp_rate(argc > 2 ? std::atoi(argv[2]) : 8, argc > 3 ? std::atof(argv[3]) : 3.0,
                      argc > 4 ? std::atoi(argv[4]) : 4096, argc > 5 && std::string(argv[5]) == "reconnect");

@@ -1,6 +1,7 @@
 """Host C++ runtime under AddressSanitizer+UBSan and ThreadSanitizer (the
 reference has no race detection).  Builds csrc/host/selftest with tools/sanitize_host.sh
-and runs the concurrent ZMTP / VecEnv / codec / NativePolicy stress test under both."""
+and runs the concurrent ZMTP / VecEnv / codec / NativePolicy stress test under both, then the ZMTP
+endpoint against mutated peer conversations (host_selftest zmtp-fuzz)."""
 import os
 import shutil
 import subprocess
@@ -17,6 +18,8 @@ def test_host_runtime_clean_under_asan_ubsan_tsan():
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-4000:]
     assert out.count("host selftest OK") == 2
+    # the ZMTP endpoint against mutated peer conversations, still serving a well-formed peer after
+    assert "zmtp fuzz OK: 5000 mutated conversations" in out and "zmtp fuzz OK: 1000 mutated" in out, out[-2000:]
     assert "ThreadSanitizer" not in out and "AddressSanitizer" not in out and "runtime error" not in out
 
 

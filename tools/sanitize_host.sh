@@ -1,6 +1,6 @@
 #!/bin/bash
 # Sanitizer builds of the C++ host runtime (SURVEY §5.2 -- the reference has none).
-#   tools/sanitize_host.sh           # ASan+UBSan and TSan builds, then run both
+#   tools/sanitize_host.sh           # ASan+UBSan and TSan builds, then run both (+ the ZMTP fuzz)
 #   tools/sanitize_host.sh h2 [THREADS CALLS MUTANTS SEED]
 #                                    # the native gRPC server under ASan+UBSan / TSan: concurrent
 #                                    # nghttp2 clients, then mutated HTTP/2 client byte streams
@@ -53,3 +53,9 @@ echo "== ASan + UBSan"
 ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 "$OUT/host_selftest_asan"
 echo "== TSan"
 TSAN_OPTIONS=halt_on_error=1:second_deadlock_stack=1 "$OUT/host_selftest_tsan"
+# the ZMTP PULL endpoint (every reference agent's upload lands here) against mutated peer
+# conversations: truncations, flips, huge long-frame sizes, junk, multipart pile-ups, stray commands
+echo "== ZMTP fuzz (ASan + UBSan)"
+ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 "$OUT/host_selftest_asan" zmtp-fuzz "${RRL_ZMTP_FUZZ:-5000}" 1
+echo "== ZMTP fuzz (TSan)"
+TSAN_OPTIONS=halt_on_error=1:second_deadlock_stack=1 "$OUT/host_selftest_tsan" zmtp-fuzz 1000 2
