@@ -355,6 +355,66 @@ class RelayRLAgent:
         self._aux.append(data)
         return RelayRLAction(obs_a, a0, mask_a, 0.0, data, False, False)
 
+    def record_action(self, obs, act, mask=None, reward: float = 0.0, data=None, done: bool = False,
+                      reward_update_flag: bool = False) -> RelayRLAction:
+        """Record an action the agent's policy did not choose -- a scripted or human controller,
+        demonstrations, an exploration override -- as one step of the current episode
+        (agent_zmq.rs:585-596 declares this with these arguments and leaves it ``todo!()``).
+
+        ``reward`` is the reward this action received (a later ``request_for_action``, whose
+        ``reward`` argument is always the previous step's reward, sets it again); ``done=True``
+        ends the episode and uploads it, as ``flag_last_action`` does.  The log-probability stored for the learner is
+        ``data["logp_a"]`` when given, else the current policy's log-probability of ``act`` (so an
+        on-policy learner's ratios stay defined); ``data["v"]`` likewise, else V(obs) when the
+        policy has a value head.  ``reward_update_flag`` is accepted for signature parity (the
+        columnar wire carries no per-row flag)."""
+        del reward_update_flag
+        if not self.enabled:
+            raise RuntimeError("agent is disabled")
+        if self.policy is None:
+            raise RuntimeError("no model loaded")
+        rec = self._rec
+        obs_a = np.ascontiguousarray(obs, np.float32)
+        if rec.full():
+            self._ship(done=False, next_obs=obs_a)
+        p = self.policy
+        mask_a = np.ones(p.act_dim, np.float32) if mask is None else np.ascontiguousarray(mask, np.float32)
+        discrete = bool(getattr(p, "discrete", True))
+        a0 = np.asarray(act, np.int32).reshape(()) if discrete else np.ascontiguousarray(act, np.float32).reshape(-1)
+        data = dict(data or {})
+        logp, v = data.get("logp_a"), data.get("v")
+        if (logp is None or v is None) and not getattr(p, "is_torchscript", False):
+            with self._policy_lock:
+                x = obs_a.reshape(1, -1)
+                if logp is None:
+                    logp = self._log_prob(p, x, mask_a, a0)
+                if v is None:
+                    vv = p.value(x)
+                    v = None if vv is None else float(np.asarray(vv).reshape(-1)[0])
+        first = (lambda t: None if t is None else float(np.asarray(t, np.float32).reshape(-1)[0]))
+        if getattr(p, "is_torchscript", False):
+            self._aux.append(data)
+        rec.record(obs_a, a0, mask_a, first(logp), first(v))
+        rec.set_last_reward(float(reward))
+        aux = {k: np.asarray(x, np.float32) for k, x in data.items() if not isinstance(x, str)}
+        if logp is not None:
+            aux.setdefault("logp_a", np.asarray(first(logp), np.float32))
+        action = RelayRLAction(obs_a, a0, mask_a, float(reward), aux or None, bool(done), False)
+        if done:
+            self._ship(done=True)
+        return action
+
+    @staticmethod
+    def _log_prob(p, x, mask_a, a0) -> float:
+        """log pi(a0 | x) under the built-in policy (masked log-softmax, or the Gaussian head)."""
+        z = np.asarray(p.logits(x, mask_a.reshape(1, -1)), np.float64).reshape(-1)
+        if getattr(p, "discrete", True):
+            m = z.max()
+            return float(z[int(a0)] - m - np.log(np.exp(z - m).sum()))
+        ls = np.asarray(p.pi[6], np.float64)
+        zz = (np.asarray(a0, np.float64) - z) / np.exp(ls)
+        return float((-0.5 * zz * zz - ls - 0.9189385332046727).sum())
+
     def flag_last_action(self, reward: float = 0.0, done: bool = True, truncated: bool = False,
                          next_obs=None) -> None:
         """Close the episode with the final reward (agent_zmq.rs:605-610).  ``truncated=True``

@@ -263,3 +263,39 @@ def torch_tensor(a):
     import torch
 
     return torch.from_numpy(np.ascontiguousarray(a, np.float32))
+
+
+def test_record_action_steps_the_episode_with_external_actions(cfgdir):
+    """RelayRLAgent.record_action (agent_zmq.rs:585-596, ``todo!()`` there): externally chosen
+    actions join the episode with their rewards, the policy's log-probability of them and V(obs);
+    ``done=True`` uploads the episode like flag_last_action."""
+    tmp, cfgp = cfgdir
+    srv = TrainingServer("REINFORCE", 4, 2, 100000, env_dir=str(tmp / "env"), config_path=cfgp,
+                         server_type="local", device="cpu", hyperparams={"with_vf_baseline": "true"})
+    got = []
+    srv.service.submit = lambda traj: got.append(traj) or True
+    try:
+        agent = RelayRLAgent(config_path=cfgp, server_type="local", handshake_timeout_s=30)
+        p = agent.policy
+        obs = [np.full(4, 0.1 * (k + 1), np.float32) for k in range(4)]
+        agent.request_for_action(obs[0], None, 0.0)          # the policy's own step
+        a1 = agent.record_action(obs[1], 1, None, 2.0)         # a scripted one
+        assert a1.get_act().reshape(-1)[0] == 1 and a1.get_rew() == 2.0
+        agent.request_for_action(obs[2], np.array([1, 0], np.float32), 2.0)
+        agent.record_action(obs[3], 0, np.array([1, 1], np.float32), 5.0, done=True)
+        assert len(got) == 1
+        c = got[0]
+        np.testing.assert_array_equal(c.obs, np.stack(obs))
+        assert list(np.asarray(c.act).reshape(-1)[[1, 3]]) == [1, 0]
+        np.testing.assert_array_equal(np.asarray(c.rew)[1:], [2.0, 0.0, 5.0])  # row 2's reward never given
+        assert np.asarray(c.done)[-1] == 1
+        # the stored log-probability of the scripted action is the policy's
+        z = p.logits(obs[1].reshape(1, -1), np.ones((1, 2), np.float32))[0].astype(np.float64)
+        lp = z[1] - z.max() - np.log(np.exp(z - z.max()).sum())
+        assert abs(float(np.asarray(c.logp)[1]) - lp) < 1e-5
+        with pytest.raises(RuntimeError):
+            agent.disable_agent()
+            agent.record_action(obs[0], 0)
+        agent.close()
+    finally:
+        srv.close(save=False)

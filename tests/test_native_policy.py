@@ -133,3 +133,26 @@ def test_agent_fast_path_records_what_it_returns(tmp_path):
     assert r.n == 5
     np.testing.assert_array_equal(r.obs[:5], xs.astype(np.float32))
     np.testing.assert_array_equal(r.rew[:4], [1, 2, 3, 4])  # each reward lands on the previous action
+
+
+def test_record_action_gaussian_log_prob():
+    """record_action with a Gaussian policy: the stored log-probability is the policy's density of
+    the given action, the row's reward the one passed."""
+    import threading
+
+    from relayrl_prototype_amd.api.agent import RelayRLAgent
+    from relayrl_prototype_amd.types import EpisodeRecorder
+
+    p = _policy(False)
+    ag = RelayRLAgent.__new__(RelayRLAgent)
+    ag.enabled, ag.policy, ag._policy_lock, ag._rec, ag._aux = True, p, threading.Lock(), EpisodeRecorder(8), []
+    x = np.random.default_rng(7).standard_normal(6).astype(np.float32)
+    a = np.array([0.3, -0.2, 0.9], np.float32)
+    ag.record_action(x, a, None, 1.5)
+    mu, ls = p.logits(x.reshape(1, -1))[0].astype(np.float64), p.pi[6].astype(np.float64)
+    z = (a - mu) / np.exp(ls)
+    want = (-0.5 * z * z - ls - 0.9189385332046727).sum()
+    r = ag._rec
+    assert r.n == 1 and r.rew[0] == 1.5 and abs(r.logp[0] - want) < 1e-4
+    np.testing.assert_array_equal(r.act[0], a)
+    assert abs(r.val[0] - p.value(x.reshape(1, -1))[0]) < 1e-5
