@@ -676,4 +676,10 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
+    if os.environ.get("WORLD_SIZE"):
+        # under torchrun: a rank's exception lands in the launcher's failure summary (the root
+        # cause's traceback, not only "exitcode 1"), which is the tail a failed run shows
+        from torch.distributed.elastic.multiprocessing.errors import record
+
+        main = record(main)
     sys.exit(main())
