@@ -207,6 +207,10 @@ class Comm:
         else:
             ops.append(dist.P2POp(dist.isend, t, dst, self.group))
         if ops:
+            if t.is_cuda and self.backend != "nccl":
+                # gloo moves device bytes from host threads, outside stream order (RCCL P2P is
+                # stream-ordered): the kernels writing ``t`` / still reading ``out`` must be done
+                torch.cuda.current_stream(t.device).synchronize()
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
         return out

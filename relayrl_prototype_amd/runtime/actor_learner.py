@@ -273,6 +273,11 @@ class ActorLearner:
             self.front = self.actor.params
         self.back = torch.zeros_like(self.front) if (self.acts and not self.is_learner) else None
         self._pending_peers = []  # (peer rank, work) of the step's in-flight P2P transfers
+        # gloo P2P on device tensors (the one-GPU rehearsal of the multi-rank path) moves the bytes
+        # from host threads, outside stream order: the kernels that write a send buffer or still
+        # read a receive buffer must have finished before the transfer is posted (RCCL P2P is
+        # stream-ordered and needs no fence)
+        self._host_p2p = self.device.type == "cuda" and self.comm.backend != "nccl"
         self._seen_seq = {}       # actor rank -> last heartbeat sequence number received
         from ..utils.watchdog import StepWatchdog
 
@@ -360,6 +365,7 @@ class ActorLearner:
                 if d is not None:
                     ops.append(dist.P2POp(dist.irecv, d, a))
         if ops:
+            self._p2p_fence()  # the previous learn no longer reads the slots
             works = dist.batch_isend_irecv(ops)
             peers = [op.peer for op in ops] if len(works) == len(ops) else [op.peer for op in ops][:len(works)]
             self._pending_peers = list(zip(peers, works))
@@ -371,6 +377,7 @@ class ActorLearner:
         maybe_stall_at("send")
         dst = self.topo.learner_of(self.rank)
         ops = [dist.P2POp(dist.isend, p.contiguous(), dst) for p in parts if p is not None]
+        self._p2p_fence()  # the rollout kernels wrote the parts
         for w in dist.batch_isend_irecv(ops):
             w.wait()  # NCCL: stream order only; the next rollout kernel is queued after the send
 
@@ -386,6 +393,7 @@ class ActorLearner:
         if not remote:
             return
         self.wsend.copy_(self.learner.pi.params)
+        self._p2p_fence()
         self._send_works = dist.batch_isend_irecv([dist.P2POp(dist.isend, self.wsend, a) for a in remote])
 
     def _recv_weights(self):
@@ -394,11 +402,16 @@ class ActorLearner:
         src = self.topo.learner_of(self.rank)
         if self._recv_work is not None:  # (lag 1) v_k, posted last step
             self._finish_recv()
+        self._p2p_fence()  # front.copy_(back) has read the previous version
         works = dist.batch_isend_irecv([dist.P2POp(dist.irecv, self.back, src)])
         self._recv_work = (self.version + 1, works)
         self._pending_peers = [(src, w) for w in works]
         if self.cfg.max_lag == 0:
             self._finish_recv()
+
+    def _p2p_fence(self):
+        if self._host_p2p:
+            torch.cuda.current_stream(self.device).synchronize()
 
     def _finish_recv(self):
         ver, works = self._recv_work
