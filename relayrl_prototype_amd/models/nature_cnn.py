@@ -204,6 +204,9 @@ class DeviceNatureCNN:
         assert self.bwd2_variant in (0, 2, 3, 4, 5, 6, 7, 8), \
             "RRL_CNN_BWD2_VARIANT: 0, 2, 3 (16 waves), 4-7 (wave priority), 8 (16-byte da1 stores)"
         self.bwd3_variant = int(os.environ.get("RRL_CNN_BWD3_VARIANT", "0"))
+        # resident conv3-backward workgroups per CU (RRL_CNN_BWD3_WGS, A/B runs): its 74,880 B of
+        # LDS and 128 VGPRs leave room for a second one
+        self.bwd3_wgs = max(1, min(2, int(os.environ.get("RRL_CNN_BWD3_WGS", "1"))))
         assert self.bwd3_variant in (0, 1, 2, 3, 4, 5, 6), \
             "RRL_CNN_BWD3_VARIANT: 0 (s_setprio clusters), 1 (16 waves), 2 (no s_setprio), 3 (static), 4 / 5 (one cluster)"
         # conv2 backward + conv1 weight gradient in C row chunks, each chunk's da1 read back by
@@ -260,7 +263,7 @@ class DeviceNatureCNN:
             self._wplan[name] = s
             need = max(need, s * cout * K)
         self.cus = int(self.h.device_cus())
-        need = max(need, min(B, self.cus) * CONVS[2].cout * CONVS[2].K)  # fused conv3 backward partials
+        need = max(need, min(B, self.cus * self.bwd3_wgs) * CONVS[2].cout * CONVS[2].K)  # fused conv3 backward partials
         if self.fc_nt:
             need = max(need, self.FC_WGRAD_SPLITS * HIDDEN * FC_IN)
             self._ones8 = torch.ones(8, dtype=torch.bfloat16, device=dev)
@@ -274,11 +277,12 @@ class DeviceNatureCNN:
             nb = min(B, self.cus)
             C = self.bwd21_chunks
             L1_, L2_, L3_ = CONVS
-            self.cpart = {"c3": torch.empty(nb * L3_.cout * L3_.K, device=dev),
+            nb3 = min(B, self.cus * self.bwd3_wgs)
+            self.cpart = {"c3": torch.empty(nb3 * L3_.cout * L3_.K, device=dev),
                           "c2": torch.empty(C * nb * L2_.cout * L2_.K, device=dev),
                           "c1": torch.empty(C * 2 * nb * S2D.cout * S2D.K, device=dev)}  # 2 slabs per workgroup
             # bias partials: 64 per workgroup written, 512 per workgroup checked by the binding
-            self.cbias = {"c3": torch.empty(nb * 8 * L3_.cout, device=dev),
+            self.cbias = {"c3": torch.empty(nb3 * 8 * L3_.cout, device=dev),
                           "c2": torch.empty((C + 1) * nb * 8 * L2_.cout, device=dev),
                           "c1": torch.empty(C * 2 * nb * S2D.cout, device=dev)}
         self.sq_work = torch.empty(1024, device=dev)
@@ -625,7 +629,7 @@ class DeviceNatureCNN:
         if self.fused_convs:
             # dgrad + wgrad + bias in one pass over (da3, a2) per image (cnn_fused.hip); the
             # slab sums of all three conv layers run in one launch at the end
-            nblk = min(B, self.cus)
+            nblk = min(B, self.cus * self.bwd3_wgs)
             h.conv3_bwd(da3, sh[o["w3"]:o["b3"]], a2, da2, self.cpart["c3"], self.cbias["c3"], B, nblk,
                         variant=self.bwd3_variant)
             sums = [(self.cpart["c3"], nblk, L3.cout * L3.K, g[o["w3"]:o["b3"]]),
