@@ -439,20 +439,29 @@ fc_tn_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Y, flo
     }
 }
 
+// RRL_FC_TN_LDS_KB (A/B runs, read per call): launch the weight-gradient GEMM with this much
+// dynamic LDS (at least its own), e.g. 84 KB = one resident workgroup per CU, leaving a 75 KB
+// conv3-backward workgroup room beside it on the side stream
+static int fc_tn_lds(int own) {
+  const char* e = getenv("RRL_FC_TN_LDS_KB");
+  const int kb = (e && e[0]) ? atoi(e) : 0;
+  return kb * 1024 > own ? min(kb, 160) * 1024 : own;
+}
+
 template <int STAGES, bool SP>
 static int launch_fc_tn_sp(const uint16_t* X, const uint16_t* Y, float* part, int R, int I, int J, int splits,
                            const uint16_t* ones, float* bias_part, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)fc_tn_kernel<STAGES, SP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              fc_lds_bytes<STAGES>());
+                              160 * 1024);
     attr = true;
   }
   const int ti = (I + 127) / 128, tj = (J + 127) / 128, rt = R / 64;
   const int kps = (rt + splits - 1) / splits;
   splits = (rt + kps - 1) / kps;
-  hipLaunchKernelGGL((fc_tn_kernel<STAGES, SP>), dim3(ti * tj * splits), dim3(kFcThreads), fc_lds_bytes<STAGES>(), st,
-                     X, Y, part, R, I, J, ti, tj, kps, ones, bias_part);
+  hipLaunchKernelGGL((fc_tn_kernel<STAGES, SP>), dim3(ti * tj * splits), dim3(kFcThreads),
+                     fc_tn_lds(fc_lds_bytes<STAGES>()), st, X, Y, part, R, I, J, ti, tj, kps, ones, bias_part);
   return (int)hipGetLastError();
 }
 
@@ -1033,7 +1042,10 @@ int rrl_fc_tn_part(const uint16_t* x, const uint16_t* y, float* part, int R, int
   if (R % 64 || I % 8 || J % 8 || R < 64 || splits < 1) return -1;
   if ((ones == nullptr) != (bias_part == nullptr) || (bias_part && J % 128 == 0)) return -1;
   hipStream_t st = (hipStream_t)stream_;
-  if (fc_big(R >= 20480) && R / 64 >= 2 && I % 4 == 0) {  // 256 x 128 persistent tiles
+  // RRL_FC_TN_BIG (read per call) forces this site's choice alone; unset, RRL_FC_BIG / the size rule
+  const char* tb = getenv("RRL_FC_TN_BIG");
+  const bool big = (tb && tb[0]) ? tb[0] != '0' : fc_big(R >= 20480);
+  if (big && R / 64 >= 2 && I % 4 == 0) {  // 256 x 128 persistent tiles
     const int tiles = ((I + 255) / 256) * ((J + 127) / 128);
     int kps2, used2;
     fcp_splits(tiles, R / 64, splits, fcp_cus(), &kps2, &used2);
