@@ -1330,6 +1330,23 @@ extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16
     attr = true;
   }
   if (N < 1 || grid < 1) return 0;
+  // RRL_CNN_BWD3_LDS_KB (A/B runs, read per call): launch the 8-wave kernel with this much dynamic
+  // LDS (at least its own); 82 KB keeps it at one workgroup per CU, so a grid of 2 x CUs runs as
+  // two rounds of workgroups the dispatcher places where CUs are free (static image sets: the
+  // result does not depend on the placement)
+  int lds = c3b::kLds;
+  if (const char* e = getenv("RRL_CNN_BWD3_LDS_KB")) {
+    const int kb = atoi(e);
+    if (kb * 1024 > lds) {
+      lds = min(kb, 160) * 1024;
+      static bool attr_big = false;
+      if (!attr_big) {
+        (void)hipFuncSetAttribute((const void*)conv3_bwd_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+        attr_big = true;
+      }
+    }
+  }
   if (variant == 1 || variant == 6) {  // the 16-wave kernel (6: with s_setprio around its MFMA clusters)
     hipLaunchKernelGGL(variant == 6 ? conv3_bwd16_kernel<1> : conv3_bwd16_kernel<0>, dim3(grid), dim3(c3b16::kThreads),
                        c3b::kLds, (hipStream_t)stream, dy, w, xact, dx, part, bias_part, N);
@@ -1355,8 +1372,8 @@ extern "C" int rrl_conv3_bwd(const uint16_t* dy, const uint16_t* w, const uint16
                        c3b::kLds, (hipStream_t)stream, dy, w, xact, dx, part, bias_part, N);
   }
   else
-    hipLaunchKernelGGL(conv3_bwd_kernel<1>, dim3(grid), dim3(c3b::kThreads), c3b::kLds, (hipStream_t)stream, dy, w,
-                       xact, dx, part, bias_part, N);
+    hipLaunchKernelGGL(conv3_bwd_kernel<1>, dim3(grid), dim3(c3b::kThreads), lds, (hipStream_t)stream, dy, w, xact,
+                       dx, part, bias_part, N);
   return (int)hipGetLastError();
 }
 
