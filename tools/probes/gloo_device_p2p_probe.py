@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--fence", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=20)
     ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--op", choices=("p2p", "all_reduce", "broadcast"), default="p2p",
+                    help="all_reduce / broadcast: the gloo collective on the device buffer instead of send / recv")
     ap.add_argument("--via", choices=("dist", "comm"), default="dist",
                     help="comm: the transfer is Comm.gather_to (its own fence for non-RCCL backends)")
     a = ap.parse_args()
@@ -37,6 +39,26 @@ def main():
     torn = 0
     for r in range(1, a.rounds + 1):
         dist.barrier()
+        if a.op != "p2p":  # every rank writes its buffer late, then the collective runs at once
+            x = m
+            for _ in range(40):
+                x = torch.tanh(x @ m)
+            buf.fill_(float(r))
+            buf[:1].add_(x[:1, 0] * 0)
+            if a.fence:
+                torch.cuda.current_stream().synchronize()
+            if a.op == "all_reduce":
+                dist.all_reduce(buf)
+                want = 2.0 * r
+            else:
+                if rank == 1:
+                    buf.fill_(-1.0)
+                dist.broadcast(buf, 0)
+                want = float(r)
+            torch.cuda.synchronize()
+            if rank == 1 and not bool((buf == want).all()):
+                torn += 1
+            continue
         if rank == 0:
             x = m
             for _ in range(40):  # keep the stream busy so the fill below runs late
@@ -59,7 +81,7 @@ def main():
             if not bool((buf == float(r)).all()):
                 torn += 1
     if rank == 1:
-        print(json.dumps({"via": a.via, "fence": a.fence, "rounds": a.rounds, "stale_or_torn_rounds": torn,
+        print(json.dumps({"op": a.op, "via": a.via, "fence": a.fence, "rounds": a.rounds, "stale_or_torn_rounds": torn,
                           "backend": "gloo", "device": torch.cuda.get_device_name(0)}), flush=True)
     dist.destroy_process_group()
     os._exit(0)
